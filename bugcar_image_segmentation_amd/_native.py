@@ -1,0 +1,173 @@
+"""ctypes binding of libbugseg.so (include/bugseg.h).
+
+There is no fallback: if the library is missing or no HIP device is visible, every product call
+raises. torch is imported first so that the library binds to torch's already-loaded HIP runtime
+(same soname libamdhip64.so.7) and torch device pointers / streams are valid for it.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+import threading
+from pathlib import Path
+
+import torch  # noqa: F401  (must precede loading the library: shared HIP runtime)
+
+_PKG = Path(__file__).resolve().parent
+LIB_PATH = Path(os.environ.get("BUGSEG_LIB", _PKG / "libbugseg.so"))
+
+OK, EINVAL, ENOMEM, EHIP, EFORMAT, ESTATE = 0, -1, -2, -3, -4, -5
+FP32, BF16 = 0, 1
+OUT_LOGITS_F32, OUT_CLASS15_U8, OUT_CLASS3_U8, OUT_BINARY_U8 = 0, 1, 2, 3
+PRE_ENGINE, PRE_NCHW_F64, PRE_NCHW_F32 = 0, 1, 2
+
+EXPORTED = ("bugseg_version", "bugseg_create", "bugseg_destroy", "bugseg_load_weights", "bugseg_num_classes",
+            "bugseg_input_bytes", "bugseg_preprocess", "bugseg_nchw_to_input", "bugseg_enet_forward",
+            "bugseg_bev_occgrid", "bugseg_plan_info", "bugseg_last_error")
+
+
+class BevParams(ctypes.Structure):
+    _fields_ = [("M", ctypes.c_double * 9), ("in_rows", ctypes.c_int), ("in_cols", ctypes.c_int),
+                ("warp_w", ctypes.c_int), ("warp_h", ctypes.c_int), ("occ_w_px", ctypes.c_int),
+                ("occ_h_px", ctypes.c_int), ("occ_w", ctypes.c_int), ("occ_h", ctypes.c_int),
+                ("left_x", ctypes.c_int), ("top_y", ctypes.c_int), ("ros_layout", ctypes.c_int)]
+
+
+class BugsegError(RuntimeError):
+    def __init__(self, code: int, msg: str):
+        super().__init__(f"bugseg error {code}: {msg}")
+        self.code = code
+
+
+_lib = None
+_lock = threading.Lock()
+
+
+def load_library(path: Path | str | None = None) -> ctypes.CDLL:
+    """Load (once) and prototype libbugseg.so. Raises if it is missing."""
+    global _lib
+    with _lock:
+        if _lib is not None:
+            return _lib
+        p = Path(path) if path else LIB_PATH
+        if not p.exists():
+            raise FileNotFoundError(f"{p} not found: build it with `python -m bugcar_image_segmentation_amd.build` "
+                                    "(or __graft_entry__.build())")
+        lib = ctypes.CDLL(str(p))
+        vp, i, sz, cp = ctypes.c_void_p, ctypes.c_int, ctypes.c_size_t, ctypes.c_char_p
+        proto = {
+            "bugseg_version": (i, []),
+            "bugseg_create": (i, [i, i, ctypes.POINTER(vp)]),
+            "bugseg_destroy": (i, [vp]),
+            "bugseg_load_weights": (i, [vp, vp, sz]),
+            "bugseg_num_classes": (i, [vp]),
+            "bugseg_input_bytes": (sz, [vp, i, i, i]),
+            "bugseg_preprocess": (i, [vp, vp, i, i, i, i, i, i, vp, vp]),
+            "bugseg_nchw_to_input": (i, [vp, vp, i, i, i, i, vp, vp]),
+            "bugseg_enet_forward": (i, [vp, vp, i, i, i, i, vp, vp]),
+            "bugseg_bev_occgrid": (i, [vp, vp, i, ctypes.POINTER(BevParams), vp, vp]),
+            "bugseg_plan_info": (i, [vp, i, i, i, i, ctypes.POINTER(i), ctypes.POINTER(ctypes.c_double),
+                                     ctypes.POINTER(ctypes.c_double)]),
+            "bugseg_last_error": (cp, [vp]),
+        }
+        for name, (res, args) in proto.items():
+            f = getattr(lib, name)
+            f.restype = res
+            f.argtypes = args
+        _lib = lib
+        return lib
+
+
+def check(code: int, ctx=None) -> None:
+    if code != OK:
+        lib = load_library()
+        msg = lib.bugseg_last_error(ctx).decode(errors="replace")
+        if code == EINVAL:
+            raise ValueError(msg)
+        raise BugsegError(code, msg)
+
+
+def require_gpu() -> None:
+    if not torch.cuda.is_available():
+        raise RuntimeError("bugseg needs a HIP GPU (MI355X / gfx950); none is visible — there is no CPU fallback")
+
+
+def stream_handle(stream: torch.cuda.Stream | None = None) -> int:
+    s = stream if stream is not None else torch.cuda.current_stream()
+    return int(s.cuda_stream)
+
+
+class Context:
+    """Owns one bugseg_ctx (device + precision + weights + activation arena)."""
+
+    def __init__(self, device: int | None = None, precision: int = FP32):
+        require_gpu()
+        self.lib = load_library()
+        self.device = torch.cuda.current_device() if device is None else int(device)
+        self.precision = precision
+        h = ctypes.c_void_p()
+        check(self.lib.bugseg_create(self.device, precision, ctypes.byref(h)))
+        self.h = h
+
+    def close(self) -> None:
+        if getattr(self, "h", None) and self.h.value:
+            self.lib.bugseg_destroy(self.h)
+            self.h = ctypes.c_void_p()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def load_weights(self, blob: bytes) -> None:
+        buf = ctypes.create_string_buffer(blob, len(blob))
+        check(self.lib.bugseg_load_weights(self.h, buf, len(blob)), self.h)
+
+    @property
+    def num_classes(self) -> int:
+        return int(self.lib.bugseg_num_classes(self.h))
+
+    def input_bytes(self, B: int, H: int, W: int) -> int:
+        return int(self.lib.bugseg_input_bytes(self.h, B, H, W))
+
+    def preprocess(self, bgr, B, H0, W0, H, W, layout, out, stream=None):
+        check(self.lib.bugseg_preprocess(self.h, bgr.data_ptr(), B, H0, W0, H, W, layout, out.data_ptr(),
+                                         stream_handle(stream)), self.h)
+
+    def nchw_to_input(self, x, B, H, W, out, stream=None):
+        check(self.lib.bugseg_nchw_to_input(self.h, x.data_ptr(), int(x.dtype == torch.float64), B, H, W,
+                                            out.data_ptr(), stream_handle(stream)), self.h)
+
+    def forward(self, x, B, H, W, out_kind, out, stream=None):
+        check(self.lib.bugseg_enet_forward(self.h, x.data_ptr(), B, H, W, out_kind, out.data_ptr(),
+                                           stream_handle(stream)), self.h)
+
+    def bev(self, seg, B, params: BevParams, out, stream=None):
+        check(self.lib.bugseg_bev_occgrid(self.h, seg.data_ptr(), B, ctypes.byref(params), out.data_ptr(),
+                                          stream_handle(stream)), self.h)
+
+    def plan_info(self, B, H, W, out_kind):
+        n = ctypes.c_int()
+        by = ctypes.c_double()
+        fl = ctypes.c_double()
+        check(self.lib.bugseg_plan_info(self.h, B, H, W, out_kind, ctypes.byref(n), ctypes.byref(by),
+                                        ctypes.byref(fl)), self.h)
+        return n.value, by.value, fl.value
+
+
+_shared: dict[int, Context] = {}
+
+
+def shared_context(device: int | None = None) -> Context:
+    """Per-device context for the weight-free ops (preprocess classmethod, BEV rasteriser)."""
+    require_gpu()
+    d = torch.cuda.current_device() if device is None else int(device)
+    with _lock:
+        c = _shared.get(d)
+    if c is None:
+        c = Context(d, FP32)
+        with _lock:
+            _shared.setdefault(d, c)
+            c = _shared[d]
+    return c

@@ -1,0 +1,75 @@
+"""Build the native engine libbugseg.so in-tree for gfx950 (hipcc, no torch extension machinery).
+
+The shared library is plain HIP C++ behind the C ABI of include/bugseg.h; it links only the HIP
+runtime (libamdhip64.so.7). Loaded after `import torch`, it binds to the same HIP runtime torch
+uses, so torch device pointers and streams can be handed straight to it.
+"""
+from __future__ import annotations
+
+import os
+import subprocess
+import sys
+from concurrent.futures import ThreadPoolExecutor
+from pathlib import Path
+
+PKG = Path(__file__).resolve().parent
+ROOT = PKG.parent
+CSRC = PKG / "csrc"
+OBJ = PKG / "_build"
+LIB = PKG / "libbugseg.so"
+SOURCES = ["conv_kernels.hip", "prep_kernels.hip", "bev_kernels.hip", "bugseg_runtime.cpp"]
+HEADERS = [CSRC / "bugseg_internal.h", ROOT / "include" / "bugseg.h"]
+ARCH = os.environ.get("BUGSEG_OFFLOAD_ARCH", "gfx950")
+
+
+def _hipcc() -> str:
+    for c in (os.environ.get("HIPCC"), "/opt/rocm/bin/hipcc", "hipcc"):
+        if c and (os.path.sep not in c or os.path.exists(c)):
+            return c
+    raise RuntimeError("hipcc not found")
+
+
+def _stale(target: Path, deps) -> bool:
+    if not target.exists():
+        return True
+    t = target.stat().st_mtime
+    return any(Path(d).stat().st_mtime > t for d in deps)
+
+
+def build_native(force: bool = False, verbose: bool = False) -> Path:
+    OBJ.mkdir(exist_ok=True)
+    hipcc = _hipcc()
+    flags = [f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-Wall", "-Wno-unused-function",
+             f"-I{ROOT / 'include'}", f"-I{CSRC}"]
+    jobs = []
+    for s in SOURCES:
+        src = CSRC / s
+        obj = OBJ / (s + ".o")
+        if force or _stale(obj, [src, *HEADERS]):
+            lang = ["-x", "hip"] if s.endswith(".hip") else []
+            jobs.append((obj, [hipcc, *flags, *lang, "-c", str(src), "-o", str(obj)]))
+
+    def run(job):
+        obj, cmd = job
+        if verbose:
+            print(" ".join(cmd), file=sys.stderr)
+        r = subprocess.run(cmd, capture_output=True, text=True)
+        if r.returncode != 0:
+            raise RuntimeError(f"compile failed: {' '.join(cmd)}\n{r.stdout}\n{r.stderr}")
+        return obj
+
+    with ThreadPoolExecutor(max_workers=min(4, max(1, len(jobs)))) as ex:
+        list(ex.map(run, jobs))
+    objs = [OBJ / (s + ".o") for s in SOURCES]
+    if force or jobs or _stale(LIB, objs):
+        tmp = LIB.with_suffix(".so.tmp")
+        cmd = [hipcc, f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", str(tmp), *map(str, objs)]
+        r = subprocess.run(cmd, capture_output=True, text=True)
+        if r.returncode != 0:
+            raise RuntimeError(f"link failed: {' '.join(cmd)}\n{r.stdout}\n{r.stderr}")
+        os.replace(tmp, LIB)
+    return LIB
+
+
+if __name__ == "__main__":
+    print(build_native(force="--force" in sys.argv, verbose=True))

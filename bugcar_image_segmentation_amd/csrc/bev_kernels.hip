@@ -1,0 +1,127 @@
+// Fused BEV occupancy-grid rasteriser: bev_transform_tools.create_occupancy_grid, non-laserscan
+// branch (bev.py:301-381), for a batch of class maps in one launch.
+//
+// The reference materialises segmap+1 (bev.py:312), a full warped image (bev.py:317, e.g. 1000x1000),
+// a cropped/padded template (bev.py:318-330), an occupancy mask, its 3x3 opening (bev.py:331-340)
+// and the INTER_NEAREST-downsampled grid (bev.py:344). Here one thread produces one output cell:
+//   * the cell samples ONE template pixel p = (min(floor(cy*ify), h_px-1), min(floor(cx*ifx), w_px-1))
+//     (resizeNN), so only the template values that p depends on are ever computed;
+//   * template(t) = warp(t + (left_x, top_y)) when inside the warped image, else 0 — the crop/pad of
+//     bev.py:318-330 is exactly this shift;
+//   * warp() is cv2.warpPerspective INTER_LINEAR/BORDER_CONSTANT on segmap+1: double-precision
+//     inverse mapping with OpenCV's per-32x32-block split X0 + M0*x1 (FP contraction OFF so the
+//     IEEE order matches), cvRound to 1/32 pixel, Q15 bilinear weights, (sum + 2^14) >> 15;
+//   * if p is occupied ({1,3}) it is a speckle unless some 3x3-neighbour q of p has an all-occupied
+//     3x3 neighbourhood (erode then dilate, out-of-template taps ignored = OpenCV's default morphology
+//     border): the 5x5 occupancy window around p is evaluated lazily;
+//   * encode: speckle -> 2, 3 -> 1, then {0:-1, 1:100, 2:0} as int8 (bev.py:377-380), written in the
+//     reference (h, w) layout or directly in the ROS data order flip(0)+rot90ccw (occgrid_to_ros.py:18-25).
+// Algorithmic traffic per frame: the class map read once (in_rows*in_cols B, gathered; L2-resident)
+// + occ_h*occ_w B written — latency/gather-bound, far below the HBM roof.
+#include "bugseg_internal.h"
+
+namespace bugseg {
+
+__device__ __forceinline__ int warp_value(const BevArgs &a, const uint8_t *seg, int x, int y) {
+#pragma clang fp contract(off)
+    const double *M = a.Mi;
+    const int xb = (x / a.bw0) * a.bw0, x1 = x - xb;
+    const double X0 = M[0] * (double)xb + M[1] * (double)y + M[2];
+    const double Y0 = M[3] * (double)xb + M[4] * (double)y + M[5];
+    const double W0 = M[6] * (double)xb + M[7] * (double)y + M[8];
+    double W = W0 + M[6] * (double)x1;
+    W = W != 0.0 ? 32.0 / W : 0.0;
+    double fX = (X0 + M[0] * (double)x1) * W;
+    double fY = (Y0 + M[3] * (double)x1) * W;
+    fX = fmin(fmax(fX, -2147483648.0), 2147483647.0);
+    fY = fmin(fmax(fY, -2147483648.0), 2147483647.0);
+    const int X = (int)__builtin_rint(fX), Y = (int)__builtin_rint(fY);
+    int sx = X >> 5, sy = Y >> 5;
+    sx = sx < -32768 ? -32768 : (sx > 32767 ? 32767 : sx);
+    sy = sy < -32768 ? -32768 : (sy > 32767 ? 32767 : sy);
+    const int ax = X & 31, ay = Y & 31;
+    const int w = a.in_cols, h = a.in_rows;
+    // segmap + 1 (bev.py:312): taps inside the image read class+1, outside the border value 0
+    const bool x0 = (unsigned)sx < (unsigned)w, x1ok = (unsigned)(sx + 1) < (unsigned)w;
+    const bool y0 = (unsigned)sy < (unsigned)h, y1ok = (unsigned)(sy + 1) < (unsigned)h;
+    int v0 = 0, v1 = 0, v2 = 0, v3 = 0;
+    if (y0) {
+        const uint8_t *r = seg + (size_t)sy * w;
+        if (x0) v0 = r[sx] + 1;
+        if (x1ok) v1 = r[sx + 1] + 1;
+    }
+    if (y1ok) {
+        const uint8_t *r = seg + (size_t)(sy + 1) * w;
+        if (x0) v2 = r[sx] + 1;
+        if (x1ok) v3 = r[sx + 1] + 1;
+    }
+    const int acc = (v0 * (32 - ax) * (32 - ay) + v1 * ax * (32 - ay) + v2 * (32 - ax) * ay + v3 * ax * ay) * 32;
+    int v = (acc + (1 << 14)) >> 15;
+    return v > 255 ? 255 : v;
+}
+
+// template value at template pixel (tx, ty) (caller guarantees it lies inside the template)
+__device__ __forceinline__ int tmpl_value(const BevArgs &a, const uint8_t *seg, int tx, int ty) {
+    const int wx = tx + a.left_x, wy = ty + a.top_y;
+    if ((unsigned)wx >= (unsigned)a.warp_w || (unsigned)wy >= (unsigned)a.warp_h) return 0;
+    return warp_value(a, seg, wx, wy);
+}
+
+__device__ __forceinline__ bool occupied(const BevArgs &a, const uint8_t *seg, int tx, int ty) {
+    const int v = tmpl_value(a, seg, tx, ty);
+    return v == 1 || v == 3;
+}
+
+__global__ void __launch_bounds__(256) bev_occgrid_kernel(const BevArgs a) {
+    const long cells = (long)a.occ_h * a.occ_w, total = cells * a.B;
+    for (long i = blockIdx.x * 256L + threadIdx.x; i < total; i += (long)gridDim.x * 256) {
+        const int b = (int)(i / cells);
+        const int rem = (int)(i - (long)b * cells);
+        const int cy = rem / a.occ_w, cx = rem - cy * a.occ_w;
+        const uint8_t *seg = a.seg + (size_t)b * a.in_rows * a.in_cols;
+        int ty = (int)floor((double)cy * a.ify);
+        int tx = (int)floor((double)cx * a.ifx);
+        ty = ty < a.occ_h_px - 1 ? ty : a.occ_h_px - 1;
+        tx = tx < a.occ_w_px - 1 ? tx : a.occ_w_px - 1;
+        int v = tmpl_value(a, seg, tx, ty);
+        if (v == 1 || v == 3) {
+            // occ5[dy+2][dx+2]: occupancy of the 5x5 window around p; out-of-template taps are
+            // neutral for the erode (treated occupied) and never become dilate sources.
+            bool opened = false;
+            for (int qy = -1; qy <= 1 && !opened; ++qy)
+                for (int qx = -1; qx <= 1 && !opened; ++qx) {
+                    const int uy = ty + qy, ux = tx + qx;
+                    if ((unsigned)uy >= (unsigned)a.occ_h_px || (unsigned)ux >= (unsigned)a.occ_w_px) continue;
+                    bool all = true;
+                    for (int ry = -1; ry <= 1 && all; ++ry)
+                        for (int rx = -1; rx <= 1 && all; ++rx) {
+                            const int zy = uy + ry, zx = ux + rx;
+                            if ((unsigned)zy >= (unsigned)a.occ_h_px || (unsigned)zx >= (unsigned)a.occ_w_px) continue;
+                            if (zy == ty && zx == tx) continue;   // p itself is occupied
+                            all = occupied(a, seg, zx, zy);
+                        }
+                    opened = all;
+                }
+            if (!opened) v = 2;                  // isolated occupied pixel -> free (bev.py:339-340)
+        }
+        const int g = v == 3 ? 1 : v;            // bev.py:377
+        const int8_t o = (int8_t)(g == 0 ? -1 : 200 - 100 * g);   // bev.py:379-380
+        if (a.ros_layout) {
+            // occgrid_to_ros.py:18-21: flip(0) then rot90ccw == G[::-1, ::-1].T, shape (occ_w, occ_h)
+            a.out[(size_t)b * cells + (size_t)(a.occ_w - 1 - cx) * a.occ_h + (a.occ_h - 1 - cy)] = o;
+        } else {
+            a.out[i] = o;
+        }
+    }
+}
+
+hipError_t launch_bev(const BevArgs &a, hipStream_t s) {
+    const long total = (long)a.occ_h * a.occ_w * a.B;
+    long g = (total + 255) / 256;
+    if (g > 8192) g = 8192;
+    if (g < 1) g = 1;
+    hipLaunchKernelGGL(bev_occgrid_kernel, dim3((unsigned)g), dim3(256), 0, s, a);
+    return hipGetLastError();
+}
+
+}  // namespace bugseg

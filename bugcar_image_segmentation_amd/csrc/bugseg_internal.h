@@ -1,0 +1,93 @@
+// Internal interface between the host runtime (bugseg_runtime.cpp) and the gfx950 kernels.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+#include <stddef.h>
+
+namespace bugseg {
+
+// ---- implicit-GEMM convolution (conv_kernels.hip) -------------------------------------------
+// GEMM view: rows = output channels (MFMA A operand = packed weights [Npad][Kpad]),
+// columns = pixels of the GEMM grid (MFMA B operand gathered from the NHWC input), K = (tap, ci).
+// The k dimension is walked in 8-channel groups; gtab[g] = dy | dx<<8 | coff<<16 (0xffff = pad).
+enum Epi {
+    EPI_PLAIN = 0,     // out = act1(acc + bias)
+    EPI_RESADD = 1,    // out = act2(act1(acc + bias) + res)                       regular bottleneck
+    EPI_RESPOOL = 2,   // out = act2(act1(acc + bias) + pad(maxpool2x2(res)))     downsampling bottleneck
+    EPI_RESUNPOOL = 3, // out = act2(act1(acc + bias) + unpool(res, idx))         upsampling bottleneck
+    EPI_INIT = 4,      // out = act1(acc + bias + pscale * maxpool_k(in))          initial block concat
+    EPI_SHUFFLE = 5,   // 4 phases -> pixel (2y+a, 2x+b): transposed conv s2     upsampling ext tconv
+    EPI_CLASSES = 6,   // 4 phases x 16 classes -> argmax + LUT / f32 logits      final transposed conv
+    EPI_COUNT = 7
+};
+
+enum Prec { PREC_F32 = 0, PREC_BF16 = 1 };
+
+struct ConvArgs {
+    const void *in;      // NHWC input (B, Hin, Win, CinS)
+    int B, Hin, Win, CinS;
+    int Hg, Wg;          // GEMM pixel grid (output grid, or the input grid for phase convs)
+    int stride;
+    int M;               // B * Hg * Wg
+    int Ksteps, Kpad, Npad;
+    const void *w;       // packed weights [Npad][Kpad]
+    const int *gtab;     // [Ksteps * 4]
+    const float *bias, *slope1, *slope2, *pscale;   // [Npad]
+    int cconv, cpool, pool_k;                        // EPI_INIT
+    const void *res;     // residual source tensor
+    int resH, resW, resC, resCS;                     // its grid, valid channels, channel stride
+    const uint8_t *idx_in;                           // EPI_RESUNPOOL (low-res grid)
+    uint8_t *idx_out;                                // EPI_RESPOOL (output grid)
+    int idxCS;                                       // channel stride of the index tensors
+    void *out;           // NHWC output (B, Hout, Wout, outC)
+    int Hout, Wout, outC;
+    int coutP;           // per-phase padded channel count (EPI_SHUFFLE / EPI_CLASSES)
+    int ncls;            // EPI_CLASSES
+    const uint8_t *lut;  // EPI_CLASSES: 16-entry class remap (nullptr: raw class id)
+    uint8_t *cls_out;    // EPI_CLASSES: (B, Hout, Wout) u8, may be nullptr
+    float *logits_out;   // EPI_CLASSES: (B, ncls, Hout, Wout) f32 NCHW, may be nullptr
+    int ntiles;
+};
+
+// Launch one convolution. nr = Npad / 16 in {1, 2, 4, 8}. Returns hipSuccess or the launch error.
+hipError_t launch_conv(int prec, int nr, int epi, const ConvArgs &a, hipStream_t s);
+// pixels per tile for a given nr (sizes the grid)
+int conv_tile_pixels(int nr);
+size_t conv_lds_bytes(int prec, const ConvArgs &a);
+
+// ---- preprocess / layout (prep_kernels.hip) --------------------------------------------------
+struct PreArgs {
+    const uint8_t *bgr;  // (B, H0, W0, 3)
+    int B, H0, W0, H, W;
+    int mode;            // 0 copy, 1 area 2x, 2 linear fixed point
+    const int *xofs;     // [W]
+    const short *xa;     // [2W]
+    const int *yofs;     // [H]
+    const short *yb;     // [2H]
+    int vec_end;         // row elements < vec_end use the vectorised vertical rounding
+    const double *lut;   // [3][256] normalisation, RGB channel order
+    int out_layout;      // BUGSEG_PRE_*
+    int prec;            // engine precision (out_layout == ENGINE)
+    void *out;
+};
+hipError_t launch_preprocess(const PreArgs &a, hipStream_t s);
+
+struct NchwArgs {
+    const void *x; int is_f64; int B, H, W; int prec; void *out;
+};
+hipError_t launch_nchw_to_input(const NchwArgs &a, hipStream_t s);
+
+// ---- BEV rasteriser (bev_kernels.hip) --------------------------------------------------------
+struct BevArgs {
+    const uint8_t *seg;  // (B, in_rows, in_cols)
+    int B, in_rows, in_cols;
+    double Mi[9];        // inverse bev matrix (cv::invert closed form, computed on the host)
+    int bw0;             // warpPerspective x-block width
+    int warp_w, warp_h, occ_w_px, occ_h_px, occ_w, occ_h, left_x, top_y;
+    double ifx, ify;     // resizeNN inverse scales
+    int ros_layout;
+    int8_t *out;
+};
+hipError_t launch_bev(const BevArgs &a, hipStream_t s);
+
+}  // namespace bugseg

@@ -1,0 +1,883 @@
+// bugseg host runtime: the native engine behind include/bugseg.h.
+//
+// Replaces what the reference gets from the TensorFlow C++ runtime (GraphDef import + Session
+// executor, models.py:21-44) and from OpenCV (resize / warpPerspective / morphology / resize-NN,
+// models.py:87-89, bev.py:317-347):
+//   * parses the BSG1 weight blob (enet_spec.py), folds batch-norm into the convolutions in double,
+//     packs every convolution for the MFMA kernels ([Npad][Kpad] rows, 8-channel k groups, tap
+//     table) and uploads all of it in ONE device allocation;
+//   * expands the ENet block list into a launch plan per (B, H, W): one fused conv launch per
+//     convolution (89 for canonical ENet), ping-pong activation buffers + per-downsample pooling
+//     indices carved from ONE device arena, sized for the batch (HBM is 288 GB: the arena for
+//     B=64 at 640x480 is a few GB and stays resident between calls);
+//   * enqueues on the caller's stream; no host synchronisation, no allocation once a plan exists.
+#include <cmath>
+#include <cstring>
+#include <string>
+#include <vector>
+#include <algorithm>
+
+#include "bugseg_internal.h"
+#include "../../include/bugseg.h"
+
+using namespace bugseg;
+
+namespace {
+
+thread_local std::string g_thread_err;
+
+struct UnitDesc {
+    int kind = 0, cout = 0, cin = 0, kh = 0, kw = 0, stride = 1, pad_h = 0, pad_w = 0, dil_h = 1, dil_w = 1, out_pad = 0;
+    float eps = 0.f;
+    std::vector<float> w, b, gamma, beta, mean, var, slope;
+};
+
+struct BlockDesc {
+    int type = 0;
+    int attrs[8] = {0};
+    std::vector<UnitDesc> units;
+    std::vector<std::vector<float>> extra;
+};
+
+enum { BT_INITIAL = 1, BT_REGULAR = 2, BT_DOWN = 3, BT_UP = 4, BT_FULLCONV = 5 };
+
+// One packed convolution launch (weights resident on the device).
+struct Packed {
+    int Npad = 0, Kpad = 0, Ksteps = 0, nr = 0;
+    int CinS = 0;      // input storage channels
+    int stride = 1;    // on the GEMM grid
+    int cout = 0;      // valid output channels (per phase)
+    int coutP = 0;     // per-phase padded channels
+    int phases = 1;
+    double macs_per_px = 0;   // MACs per GEMM pixel (flop accounting)
+    size_t o_w = 0, o_gtab = 0, o_bias = 0, o_s1 = 0, o_s2 = 0, o_ps = 0;
+};
+
+struct Op {
+    ConvArgs a;
+    int nr = 0, epi = 0;
+    double bytes = 0, flops = 0;
+};
+
+struct Plan {
+    int B = 0, H = 0, W = 0;
+    std::vector<Op> ops;
+    void *arena = nullptr;
+    size_t arena_bytes = 0;
+};
+
+inline int round_up(int v, int m) { return (v + m - 1) / m * m; }
+inline int pow2_nr(int npad) {   // 16-row fragments, rounded up to 1, 2, 4 or 8
+    int nr = npad / 16;
+    int p = 1;
+    while (p < nr) p <<= 1;
+    return p;
+}
+
+}  // namespace
+
+struct bugseg_ctx {
+    int device = 0;
+    int prec = PREC_F32;
+    std::string err;
+    bool loaded = false;
+    int ncls = 0;
+    std::vector<BlockDesc> blocks;
+    // packed weights: host staging + one device allocation
+    std::vector<Packed> packed;
+    std::vector<std::vector<int>> block_convs;     // per block: indices into packed
+    std::vector<unsigned char> host_w;
+    void *dev_w = nullptr;
+    void *dev_luts = nullptr;                      // [0..15] lut3, [16..31] binary, then 3x256 f64 norm lut
+    Plan plan;
+    // preprocess resize tables
+    int pre_key[4] = {0, 0, 0, 0};
+    void *pre_tab = nullptr;
+    size_t pre_tab_bytes = 0;
+};
+
+namespace {
+
+int fail(bugseg_ctx *c, int code, const std::string &m) {
+    if (c) c->err = m;
+    else g_thread_err = m;
+    return code;
+}
+
+struct DeviceGuard {
+    int prev = -1;
+    explicit DeviceGuard(int dev) {
+        if (hipGetDevice(&prev) != hipSuccess) prev = -1;
+        if (prev != dev) (void)hipSetDevice(dev);
+    }
+    ~DeviceGuard() {
+        int cur = -1;
+        if (prev >= 0 && hipGetDevice(&cur) == hipSuccess && cur != prev) (void)hipSetDevice(prev);
+    }
+};
+
+// ---------------------------------------------------------------- blob parsing
+struct Reader {
+    const unsigned char *p, *end;
+    bool ok = true;
+    template <typename T> T get() {
+        T v{};
+        if (p + sizeof(T) > end) { ok = false; return v; }
+        std::memcpy(&v, p, sizeof(T));
+        p += sizeof(T);
+        return v;
+    }
+    std::vector<float> tensor() {
+        uint32_t n = get<uint32_t>();
+        std::vector<float> v;
+        if (!ok || p + (size_t)n * 4 > end) { ok = false; return v; }
+        v.resize(n);
+        std::memcpy(v.data(), p, (size_t)n * 4);
+        p += (size_t)n * 4;
+        return v;
+    }
+};
+
+bool parse_blob(const void *blob, size_t bytes, std::vector<BlockDesc> &out, int &ncls, std::string &why) {
+    Reader r{(const unsigned char *)blob, (const unsigned char *)blob + bytes};
+    char magic[4];
+    for (int i = 0; i < 4; ++i) magic[i] = r.get<char>();
+    if (!r.ok || std::memcmp(magic, "BSG1", 4) != 0) { why = "bad magic (expected BSG1)"; return false; }
+    uint32_t ver = r.get<uint32_t>(), nb = r.get<uint32_t>(), nc = r.get<uint32_t>();
+    if (!r.ok || ver != 1) { why = "unsupported blob version"; return false; }
+    if (nb == 0 || nb > 4096 || nc == 0 || nc > 16) { why = "bad block/class count"; return false; }
+    ncls = (int)nc;
+    for (uint32_t b = 0; b < nb; ++b) {
+        BlockDesc bd;
+        bd.type = (int)r.get<uint32_t>();
+        for (int i = 0; i < 8; ++i) bd.attrs[i] = r.get<int32_t>();
+        uint32_t nu = r.get<uint32_t>();
+        if (!r.ok || nu > 16) { why = "bad unit count"; return false; }
+        for (uint32_t u = 0; u < nu; ++u) {
+            UnitDesc ud;
+            int32_t iv[11];
+            for (int i = 0; i < 11; ++i) iv[i] = r.get<int32_t>();
+            ud.kind = iv[0]; ud.cout = iv[1]; ud.cin = iv[2]; ud.kh = iv[3]; ud.kw = iv[4]; ud.stride = iv[5];
+            ud.pad_h = iv[6]; ud.pad_w = iv[7]; ud.dil_h = iv[8]; ud.dil_w = iv[9]; ud.out_pad = iv[10];
+            ud.eps = r.get<float>();
+            ud.w = r.tensor(); ud.b = r.tensor(); ud.gamma = r.tensor(); ud.beta = r.tensor();
+            ud.mean = r.tensor(); ud.var = r.tensor(); ud.slope = r.tensor();
+            if (!r.ok) { why = "truncated unit"; return false; }
+            if (ud.cout <= 0 || ud.cin <= 0 || ud.kh <= 0 || ud.kw <= 0 || ud.cout > 128 || ud.cin > 128 || ud.kh > 7 || ud.kw > 7) {
+                why = "unit dims out of range"; return false;
+            }
+            const size_t nw = (size_t)ud.cout * ud.cin * ud.kh * ud.kw;
+            const size_t c = (size_t)ud.cout;
+            if (ud.w.size() != nw || ud.b.size() != c || ud.gamma.size() != c || ud.beta.size() != c ||
+                ud.mean.size() != c || ud.var.size() != c || ud.slope.size() != c) {
+                why = "unit tensor size mismatch"; return false;
+            }
+            bd.units.push_back(std::move(ud));
+        }
+        uint32_t ne = r.get<uint32_t>();
+        if (!r.ok || ne > 16) { why = "bad extra count"; return false; }
+        for (uint32_t e = 0; e < ne; ++e) bd.extra.push_back(r.tensor());
+        if (!r.ok) { why = "truncated extras"; return false; }
+        out.push_back(std::move(bd));
+    }
+    return true;
+}
+
+// ---------------------------------------------------------------- packing
+struct Packer {
+    int prec;
+    std::vector<unsigned char> &buf;
+    size_t push(const void *d, size_t n) {
+        size_t off = round_up((int)buf.size(), 256);
+        buf.resize(off + n);
+        std::memcpy(buf.data() + off, d, n);
+        return off;
+    }
+    size_t push_w(const std::vector<double> &w) {
+        if (prec == PREC_BF16) {
+            std::vector<uint16_t> h(w.size());
+            for (size_t i = 0; i < w.size(); ++i) {
+                float f = (float)w[i];
+                uint32_t u;
+                std::memcpy(&u, &f, 4);
+                u = u + 0x7fffu + ((u >> 16) & 1u);     // round to nearest even (weights are finite)
+                h[i] = (uint16_t)(u >> 16);
+            }
+            return push(h.data(), h.size() * 2);
+        }
+        std::vector<float> h(w.begin(), w.end());
+        return push(h.data(), h.size() * 4);
+    }
+    size_t push_f(const std::vector<float> &v) { return push(v.data(), v.size() * 4); }
+};
+
+void bn_fold(const UnitDesc &u, std::vector<double> &scale, std::vector<double> &shift) {
+    scale.resize(u.cout);
+    shift.resize(u.cout);
+    for (int c = 0; c < u.cout; ++c) {
+        const double s = (double)u.gamma[c] / std::sqrt((double)u.var[c] + (double)u.eps);
+        scale[c] = s;
+        shift[c] = ((double)u.b[c] - (double)u.mean[c]) * s + (double)u.beta[c];
+    }
+}
+
+int gentry(int dy, int dx, int coff) { return (dy & 0xff) | ((dx & 0xff) << 8) | (coff << 16); }
+
+// Ordinary convolution (OIHW weights) on an NHWC input with CinS storage channels.
+Packed pack_conv(Packer &pk, const UnitDesc &u, int CinS, const std::vector<float> *slope2) {
+    Packed p;
+    const int taps = u.kh * u.kw, CG = CinS / 8;
+    const int Kgroups = taps * CG;
+    p.Ksteps = (Kgroups + 3) / 4;
+    p.Kpad = p.Ksteps * 32;
+    p.cout = u.cout;
+    p.coutP = round_up(u.cout, 16);
+    p.nr = pow2_nr(p.coutP);
+    p.Npad = p.nr * 16;
+    p.CinS = CinS;
+    p.stride = u.stride;
+    p.macs_per_px = (double)u.cout * u.cin * taps;
+    std::vector<double> scale, shift;
+    bn_fold(u, scale, shift);
+    std::vector<double> w((size_t)p.Npad * p.Kpad, 0.0);
+    for (int co = 0; co < u.cout; ++co)
+        for (int ci = 0; ci < u.cin; ++ci)
+            for (int ky = 0; ky < u.kh; ++ky)
+                for (int kx = 0; kx < u.kw; ++kx) {
+                    const int tap = ky * u.kw + kx;
+                    w[(size_t)co * p.Kpad + tap * CinS + ci] =
+                        (double)u.w[(((size_t)co * u.cin + ci) * u.kh + ky) * u.kw + kx] * scale[co];
+                }
+    std::vector<int> gt(p.Ksteps * 4, gentry(0, 0, 0xffff));
+    for (int g = 0; g < Kgroups; ++g) {
+        const int tap = g / CG, ky = tap / u.kw, kx = tap % u.kw;
+        gt[g] = gentry(ky * u.dil_h - u.pad_h, kx * u.dil_w - u.pad_w, (g % CG) * 8);
+    }
+    std::vector<float> bias(p.Npad, 0.f), s1(p.Npad, 0.f), s2(p.Npad, 0.f), ps(p.Npad, 0.f);
+    for (int c = 0; c < u.cout; ++c) {
+        bias[c] = (float)shift[c];
+        s1[c] = u.slope[c];
+        if (slope2) s2[c] = (*slope2)[c];
+    }
+    p.o_w = pk.push_w(w);
+    p.o_gtab = pk.push(gt.data(), gt.size() * 4);
+    p.o_bias = pk.push_f(bias);
+    p.o_s1 = pk.push_f(s1);
+    p.o_s2 = pk.push_f(s2);
+    p.o_ps = pk.push_f(ps);
+    return p;
+}
+
+// Stride-2 transposed convolution (IOHW weights) as a 4-phase convolution over the INPUT grid:
+// output pixel (2i+a, 2j+b) = sum over taps (dy,dx) of in[i+dy][j+dx] . W[ky = a+pad-2dy][kx = b+pad-2dx]
+// (PyTorch/ONNX semantics y = 2i - pad + ky). GEMM row n = phase * coutP + co.
+Packed pack_tconv(Packer &pk, const UnitDesc &u, int CinS, std::string &why) {
+    Packed p;
+    if (u.stride != 2 || u.kh != u.kw || u.pad_h != u.pad_w) { why = "tconv: only square stride-2 kernels"; return p; }
+    const int k = u.kh, pad = u.pad_h;
+    if (-2 - 2 * pad + k + u.out_pad != 0) { why = "tconv: output must be exactly 2x the input"; return p; }
+    std::vector<int> D;
+    for (int d = -3; d <= 3; ++d) {
+        bool any = false;
+        for (int a = 0; a < 2; ++a) { const int kk = a + pad - 2 * d; any |= kk >= 0 && kk < k; }
+        if (any) D.push_back(d);
+    }
+    const int nd = (int)D.size(), taps = nd * nd, CG = CinS / 8;
+    const int Kgroups = taps * CG;
+    p.Ksteps = (Kgroups + 3) / 4;
+    p.Kpad = p.Ksteps * 32;
+    p.cout = u.cout;
+    p.coutP = round_up(u.cout, 16);
+    p.phases = 4;
+    p.nr = pow2_nr(4 * p.coutP);
+    p.Npad = p.nr * 16;
+    if (p.Npad != 4 * p.coutP || p.nr > 8) { why = "tconv: unsupported channel count"; return p; }
+    p.CinS = CinS;
+    p.stride = 1;
+    p.macs_per_px = (double)u.cout * u.cin * k * k;       // per INPUT pixel
+    std::vector<double> scale, shift;
+    bn_fold(u, scale, shift);
+    std::vector<double> w((size_t)p.Npad * p.Kpad, 0.0);
+    for (int a = 0; a < 2; ++a)
+        for (int b = 0; b < 2; ++b)
+            for (int ty = 0; ty < nd; ++ty)
+                for (int tx = 0; tx < nd; ++tx) {
+                    const int ky = a + pad - 2 * D[ty], kx = b + pad - 2 * D[tx];
+                    if (ky < 0 || ky >= k || kx < 0 || kx >= k) continue;
+                    const int tap = ty * nd + tx;
+                    for (int co = 0; co < u.cout; ++co)
+                        for (int ci = 0; ci < u.cin; ++ci)
+                            w[(size_t)((a * 2 + b) * p.coutP + co) * p.Kpad + tap * CinS + ci] =
+                                (double)u.w[(((size_t)ci * u.cout + co) * k + ky) * k + kx] * scale[co];
+                }
+    std::vector<int> gt(p.Ksteps * 4, gentry(0, 0, 0xffff));
+    for (int g = 0; g < Kgroups; ++g) {
+        const int tap = g / CG;
+        gt[g] = gentry(D[tap / nd], D[tap % nd], (g % CG) * 8);
+    }
+    std::vector<float> bias(p.Npad, 0.f), s1(p.Npad, 0.f), s2(p.Npad, 0.f), ps(p.Npad, 0.f);
+    for (int ph = 0; ph < 4; ++ph)
+        for (int c = 0; c < u.cout; ++c) {
+            bias[ph * p.coutP + c] = (float)shift[c];
+            s1[ph * p.coutP + c] = u.slope[c];
+        }
+    p.o_w = pk.push_w(w);
+    p.o_gtab = pk.push(gt.data(), gt.size() * 4);
+    p.o_bias = pk.push_f(bias);
+    p.o_s1 = pk.push_f(s1);
+    p.o_s2 = pk.push_f(s2);
+    p.o_ps = pk.push_f(ps);
+    return p;
+}
+
+int cstore(int c) { return round_up(c, 8); }
+
+bool pack_all(bugseg_ctx *ctx, std::string &why) {
+    ctx->packed.clear();
+    ctx->block_convs.clear();
+    ctx->host_w.clear();
+    Packer pk{ctx->prec, ctx->host_w};
+    int cur_c = 3;
+    std::vector<int> down_cin(ctx->blocks.size(), -1);
+    for (size_t bi = 0; bi < ctx->blocks.size(); ++bi) {
+        const BlockDesc &b = ctx->blocks[bi];
+        std::vector<int> ids;
+        auto add = [&](const Packed &p) { ctx->packed.push_back(p); ids.push_back((int)ctx->packed.size() - 1); };
+        auto expect_units = [&](size_t n) { return b.units.size() == n; };
+        switch (b.type) {
+        case BT_INITIAL: {
+            const int cin = b.attrs[0], cconv = b.attrs[1], pk_k = b.attrs[2];
+            if (bi != 0 || !expect_units(1) || cin != 3 || cconv + cin > 16 || (pk_k != 2 && pk_k != 3) ||
+                b.extra.size() != 6) { why = "initial block malformed"; return false; }
+            const UnitDesc &u = b.units[0];
+            if (u.cout != cconv || u.cin != cin || u.kh != 3 || u.kw != 3 || u.stride != 2 || u.pad_h != 1 || u.pad_w != 1) {
+                why = "initial conv must be 3x3 s2 p1"; return false;
+            }
+            Packed p = pack_conv(pk, u, 8, nullptr);
+            // pool channels [cconv, cconv+cin): BN of the concat as scale + shift, their own slope
+            std::vector<float> bias(p.Npad), s1(p.Npad), ps(p.Npad, 0.f);
+            std::memcpy(bias.data(), ctx->host_w.data() + p.o_bias, p.Npad * 4);
+            std::memcpy(s1.data(), ctx->host_w.data() + p.o_s1, p.Npad * 4);
+            const std::vector<float> &g = b.extra[0], &be = b.extra[1], &mu = b.extra[2], &va = b.extra[3],
+                                     &ep = b.extra[4], &sl = b.extra[5];
+            if ((int)g.size() != cin || ep.size() != 1 || (int)sl.size() != cin) { why = "initial extras malformed"; return false; }
+            for (int c = 0; c < cin; ++c) {
+                const double s = (double)g[c] / std::sqrt((double)va[c] + (double)ep[0]);
+                ps[cconv + c] = (float)s;
+                bias[cconv + c] = (float)((double)be[c] - (double)mu[c] * s);
+                s1[cconv + c] = sl[c];
+            }
+            std::memcpy(ctx->host_w.data() + p.o_bias, bias.data(), p.Npad * 4);
+            std::memcpy(ctx->host_w.data() + p.o_s1, s1.data(), p.Npad * 4);
+            std::memcpy(ctx->host_w.data() + p.o_ps, ps.data(), p.Npad * 4);
+            p.cout = cconv + cin;
+            add(p);
+            cur_c = cconv + cin;
+            break;
+        }
+        case BT_DOWN: {
+            const int cin = b.attrs[0], cout = b.attrs[1];
+            if (!expect_units(3) || b.extra.size() != 1 || cin != cur_c || cout < cin) { why = "down block malformed"; return false; }
+            const UnitDesc &u1 = b.units[0], &u2 = b.units[1], &u3 = b.units[2];
+            if (u1.kh != 2 || u1.kw != 2 || u1.stride != 2 || u1.cin != cin || u2.stride != 1 || u3.kh != 1 ||
+                u3.kw != 1 || u3.cout != cout || (int)b.extra[0].size() != cout) { why = "down block units malformed"; return false; }
+            add(pack_conv(pk, u1, cstore(cin), nullptr));
+            add(pack_conv(pk, u2, cstore(u1.cout), nullptr));
+            add(pack_conv(pk, u3, cstore(u2.cout), &b.extra[0]));
+            down_cin[bi] = cin;
+            cur_c = cout;
+            break;
+        }
+        case BT_REGULAR: {
+            const int ch = b.attrs[0];
+            if ((b.units.size() != 3 && b.units.size() != 4) || b.extra.size() != 1 || ch != cur_c) {
+                why = "regular block malformed"; return false;
+            }
+            int c = ch;
+            for (size_t i = 0; i < b.units.size(); ++i) {
+                const UnitDesc &u = b.units[i];
+                if (u.kind != 0 || u.cin != c || u.stride != 1) { why = "regular block unit chain malformed"; return false; }
+                const bool last = i + 1 == b.units.size();
+                add(pack_conv(pk, u, cstore(c), last ? &b.extra[0] : nullptr));
+                c = u.cout;
+            }
+            if (c != ch || (int)b.extra[0].size() != ch) { why = "regular block must preserve channels"; return false; }
+            break;
+        }
+        case BT_UP: {
+            const int cin = b.attrs[0], cout = b.attrs[1], ref = b.attrs[2];
+            if (!expect_units(4) || b.extra.size() != 1 || cin != cur_c || ref < 0 || ref >= (int)bi ||
+                ctx->blocks[ref].type != BT_DOWN || down_cin[ref] != cout) { why = "up block malformed"; return false; }
+            const UnitDesc &um = b.units[0], &u1 = b.units[1], &ut = b.units[2], &u2 = b.units[3];
+            if (um.kh != 1 || um.cout != cout || u1.kh != 1 || ut.kind != 1 || ut.kh != 2 || u2.kh != 1 || u2.cout != cout) {
+                why = "up block units malformed"; return false;
+            }
+            add(pack_conv(pk, um, cstore(cin), nullptr));
+            add(pack_conv(pk, u1, cstore(cin), nullptr));
+            Packed t = pack_tconv(pk, ut, cstore(u1.cout), why);
+            if (!why.empty()) return false;
+            add(t);
+            add(pack_conv(pk, u2, cstore(ut.cout), &b.extra[0]));
+            cur_c = cout;
+            break;
+        }
+        case BT_FULLCONV: {
+            if (!expect_units(1) || bi + 1 != ctx->blocks.size()) { why = "fullconv must be the last block"; return false; }
+            const UnitDesc &u = b.units[0];
+            if (u.kind != 1 || u.cin != cur_c || u.cout != ctx->ncls || u.cout > 16) { why = "fullconv malformed"; return false; }
+            Packed t = pack_tconv(pk, u, cstore(cur_c), why);
+            if (!why.empty()) return false;
+            if (t.coutP != 16) { why = "fullconv: classes must fit 16"; return false; }
+            add(t);
+            cur_c = u.cout;
+            break;
+        }
+        default:
+            why = "unknown block type";
+            return false;
+        }
+        ctx->block_convs.push_back(ids);
+    }
+    if (ctx->blocks.empty() || ctx->blocks.back().type != BT_FULLCONV) { why = "model must end in fullconv"; return false; }
+    return true;
+}
+
+// ---------------------------------------------------------------- plan
+struct Shape { int H, W, C; };   // C = storage channels
+
+ConvArgs base_args(const bugseg_ctx *ctx, const Packed &p) {
+    ConvArgs a;
+    std::memset(&a, 0, sizeof(a));
+    const unsigned char *d = (const unsigned char *)ctx->dev_w;
+    a.Ksteps = p.Ksteps;
+    a.Kpad = p.Kpad;
+    a.Npad = p.Npad;
+    a.w = d + p.o_w;
+    a.gtab = (const int *)(d + p.o_gtab);
+    a.bias = (const float *)(d + p.o_bias);
+    a.slope1 = (const float *)(d + p.o_s1);
+    a.slope2 = (const float *)(d + p.o_s2);
+    a.pscale = (const float *)(d + p.o_ps);
+    a.stride = p.stride;
+    a.CinS = p.CinS;
+    a.coutP = p.coutP;
+    return a;
+}
+
+// Walk the network for (B, H, W). With fill == false only the buffer sizes are computed.
+struct Walker {
+    bugseg_ctx *ctx;
+    int B, H, W;
+    size_t es;
+    // buffer sizes (bytes) and pointers
+    size_t szX = 0, szT = 0, szM = 0;
+    std::vector<size_t> szIdx;
+    unsigned char *X[2] = {nullptr, nullptr}, *T[3] = {nullptr, nullptr, nullptr}, *Mb = nullptr;
+    std::vector<unsigned char *> idx;
+    std::vector<Op> ops;
+
+    size_t tbytes(const Shape &s) const { return (size_t)B * s.H * s.W * s.C * es; }
+
+    void conv(const Packed &p, int epi, const void *in, Shape si, Shape sg, void *out, Shape so, Op &op) {
+        ConvArgs a = base_args(ctx, p);
+        a.in = in; a.B = B; a.Hin = si.H; a.Win = si.W;
+        a.Hg = sg.H; a.Wg = sg.W; a.M = B * sg.H * sg.W;
+        a.out = out; a.Hout = so.H; a.Wout = so.W; a.outC = so.C;
+        a.ntiles = (a.M + conv_tile_pixels(p.nr) - 1) / conv_tile_pixels(p.nr);
+        op.a = a; op.nr = p.nr; op.epi = epi;
+        op.flops = 2.0 * p.macs_per_px * a.M;
+        op.bytes = (double)B * si.H * si.W * si.C * es + (double)p.Npad * p.Kpad * es +
+                   (epi == EPI_CLASSES ? 0.0 : (double)B * so.H * so.W * so.C * es);
+    }
+
+    bool run(bool fill, std::string &why) {
+        es = ctx->prec == PREC_BF16 ? 2 : 4;
+        if (H % 8 || W % 8 || H <= 0 || W <= 0 || B <= 0) { why = "H and W must be positive multiples of 8"; return false; }
+        const size_t nb = ctx->blocks.size();
+        if (!fill) szIdx.assign(nb, 0);
+        Shape cur{H, W, 8};
+        const unsigned char *curp = nullptr;    // engine input, patched per call
+        int xi = 0;
+        ops.clear();
+        for (size_t bi = 0; bi < nb; ++bi) {
+            const BlockDesc &b = ctx->blocks[bi];
+            const std::vector<int> &ids = ctx->block_convs[bi];
+            auto P = [&](int i) -> const Packed & { return ctx->packed[ids[i]]; };
+            unsigned char *dst = X[xi];
+            switch (b.type) {
+            case BT_INITIAL: {
+                Shape so{H / 2, W / 2, cstore(P(0).cout)};
+                szX = std::max(szX, tbytes(so));
+                if (fill) {
+                    Op op;
+                    conv(P(0), EPI_INIT, curp, cur, so, dst, so, op);
+                    op.a.cconv = b.attrs[1]; op.a.cpool = b.attrs[0]; op.a.pool_k = b.attrs[2];
+                    op.a.CinS = 8;
+                    ops.push_back(op);
+                }
+                cur = so;
+                break;
+            }
+            case BT_DOWN: {
+                Shape s1{cur.H / 2, cur.W / 2, cstore(P(0).cout)}, s2{s1.H, s1.W, cstore(P(1).cout)};
+                Shape so{s1.H, s1.W, cstore(P(2).cout)};
+                const int idxCS = cstore(b.attrs[0]);
+                szT = std::max({szT, tbytes(s1), tbytes(s2)});
+                szX = std::max(szX, tbytes(so));
+                if (!fill) szIdx[bi] = (size_t)B * so.H * so.W * idxCS;
+                if (fill) {
+                    Op o1, o2, o3;
+                    conv(P(0), EPI_PLAIN, curp, cur, s1, T[0], s1, o1);
+                    conv(P(1), EPI_PLAIN, T[0], s1, s2, T[1], s2, o2);
+                    conv(P(2), EPI_RESPOOL, T[1], s2, so, dst, so, o3);
+                    o3.a.res = curp; o3.a.resH = cur.H; o3.a.resW = cur.W; o3.a.resC = b.attrs[0]; o3.a.resCS = cur.C;
+                    o3.a.idx_out = idx[bi]; o3.a.idxCS = idxCS;
+                    o3.bytes += (double)B * cur.H * cur.W * cur.C * es + (double)B * so.H * so.W * idxCS;
+                    ops.push_back(o1); ops.push_back(o2); ops.push_back(o3);
+                }
+                cur = so;
+                break;
+            }
+            case BT_REGULAR: {
+                const int nu = (int)b.units.size();
+                Shape s = cur;
+                const unsigned char *src = curp;
+                for (int i = 0; i < nu; ++i) {
+                    const UnitDesc &u = b.units[i];
+                    const bool last = i + 1 == nu;
+                    Shape so{s.H, s.W, cstore(u.cout)};
+                    unsigned char *o = last ? dst : T[i % 3];
+                    if (!last) szT = std::max(szT, tbytes(so));
+                    else szX = std::max(szX, tbytes(so));
+                    if (fill) {
+                        Op op;
+                        conv(P(i), last ? EPI_RESADD : EPI_PLAIN, src, s, so, o, so, op);
+                        if (last) {
+                            op.a.res = curp; op.a.resH = cur.H; op.a.resW = cur.W; op.a.resC = b.attrs[0]; op.a.resCS = cur.C;
+                            op.bytes += (double)B * cur.H * cur.W * cur.C * es;
+                        }
+                        ops.push_back(op);
+                    }
+                    s = so;
+                    src = o;
+                }
+                cur = s;
+                break;
+            }
+            case BT_UP: {
+                const int ref = b.attrs[2];
+                Shape sm{cur.H, cur.W, cstore(P(0).cout)}, s1{cur.H, cur.W, cstore(P(1).cout)};
+                Shape st{cur.H * 2, cur.W * 2, cstore(P(2).cout)}, so{cur.H * 2, cur.W * 2, cstore(P(3).cout)};
+                szM = std::max(szM, tbytes(sm));
+                szT = std::max({szT, tbytes(s1), tbytes(st)});
+                szX = std::max(szX, tbytes(so));
+                if (fill) {
+                    Op om, o1, ot, o2;
+                    conv(P(0), EPI_PLAIN, curp, cur, sm, Mb, sm, om);
+                    conv(P(1), EPI_PLAIN, curp, cur, s1, T[0], s1, o1);
+                    conv(P(2), EPI_SHUFFLE, T[0], s1, s1, T[1], st, ot);
+                    conv(P(3), EPI_RESUNPOOL, T[1], st, so, dst, so, o2);
+                    o2.a.res = Mb; o2.a.resH = sm.H; o2.a.resW = sm.W; o2.a.resC = b.attrs[1]; o2.a.resCS = sm.C;
+                    o2.a.idx_in = idx[ref]; o2.a.idxCS = cstore(ctx->blocks[ref].attrs[0]);
+                    o2.bytes += (double)B * sm.H * sm.W * sm.C * es + (double)B * sm.H * sm.W * o2.a.idxCS;
+                    ops.push_back(om); ops.push_back(o1); ops.push_back(ot); ops.push_back(o2);
+                }
+                cur = so;
+                break;
+            }
+            case BT_FULLCONV: {
+                Shape so{cur.H * 2, cur.W * 2, P(0).cout};
+                if (so.H != H || so.W != W) { why = "network does not return to the input resolution"; return false; }
+                if (fill) {
+                    Op op;
+                    conv(P(0), EPI_CLASSES, curp, cur, cur, nullptr, so, op);
+                    op.a.ncls = ctx->ncls;
+                    ops.push_back(op);
+                }
+                cur = so;
+                break;
+            }
+            }
+            if (b.type != BT_FULLCONV) {
+                curp = dst;
+                xi ^= 1;
+            }
+        }
+        return true;
+    }
+};
+
+bool build_plan(bugseg_ctx *ctx, int B, int H, int W, std::string &why) {
+    Plan &pl = ctx->plan;
+    if (pl.arena && pl.B == B && pl.H == H && pl.W == W) return true;
+    Walker w{ctx, B, H, W};
+    if (!w.run(false, why)) return false;
+    auto al = [](size_t v) { return (v + 4095) / 4096 * 4096; };
+    size_t total = 2 * al(w.szX) + 3 * al(w.szT) + al(w.szM);
+    for (size_t s : w.szIdx) total += al(s);
+    if (pl.arena) { (void)hipFree(pl.arena); pl.arena = nullptr; }
+    if (hipMalloc(&pl.arena, total) != hipSuccess) { why = "hipMalloc of the activation arena failed"; pl.arena = nullptr; return false; }
+    unsigned char *p = (unsigned char *)pl.arena;
+    w.X[0] = p; p += al(w.szX);
+    w.X[1] = p; p += al(w.szX);
+    for (int i = 0; i < 3; ++i) { w.T[i] = p; p += al(w.szT); }
+    w.Mb = p; p += al(w.szM);
+    w.idx.assign(w.szIdx.size(), nullptr);
+    for (size_t i = 0; i < w.szIdx.size(); ++i) if (w.szIdx[i]) { w.idx[i] = p; p += al(w.szIdx[i]); }
+    if (!w.run(true, why)) return false;
+    for (const Op &op : w.ops) {
+        const double elems = (double)op.a.M * 128.0;
+        if (elems > 2.0e9) { why = "batch too large for 32-bit pixel indexing"; return false; }
+    }
+    pl.ops = std::move(w.ops);
+    pl.B = B; pl.H = H; pl.W = W;
+    pl.arena_bytes = total;
+    return true;
+}
+
+// ---------------------------------------------------------------- preprocess tables
+void linear_coeffs(int dsize, int ssize, double scale, int *ofs, short *a01) {
+#pragma clang fp contract(off)
+    for (int d = 0; d < dsize; ++d) {
+        float f = (float)((d + 0.5) * scale - 0.5);
+        int s = (int)std::floor(f);
+        f -= (float)s;
+        if (s < 0) { f = 0.f; s = 0; }
+        if (s >= ssize - 1) { f = 0.f; s = ssize - 1; }
+        ofs[d] = s;
+        long v0 = std::lrintf((1.f - f) * 2048.f), v1 = std::lrintf(f * 2048.f);
+        a01[2 * d] = (short)std::min(32767L, std::max(-32768L, v0));
+        a01[2 * d + 1] = (short)std::min(32767L, std::max(-32768L, v1));
+    }
+}
+
+}  // namespace
+
+// =============================================================== C ABI
+extern "C" {
+
+int bugseg_version(void) { return 100; }
+
+const char *bugseg_last_error(const bugseg_ctx *ctx) { return ctx ? ctx->err.c_str() : g_thread_err.c_str(); }
+
+int bugseg_create(int device, int precision, bugseg_ctx **out) {
+    if (!out) return fail(nullptr, BUGSEG_EINVAL, "out is NULL");
+    *out = nullptr;
+    if (precision != BUGSEG_FP32 && precision != BUGSEG_BF16) return fail(nullptr, BUGSEG_EINVAL, "precision must be BUGSEG_FP32 or BUGSEG_BF16");
+    int n = 0;
+    if (hipGetDeviceCount(&n) != hipSuccess || device < 0 || device >= n)
+        return fail(nullptr, BUGSEG_EINVAL, "no such HIP device: " + std::to_string(device));
+    bugseg_ctx *c = new (std::nothrow) bugseg_ctx();
+    if (!c) return fail(nullptr, BUGSEG_ENOMEM, "out of host memory");
+    c->device = device;
+    c->prec = precision == BUGSEG_BF16 ? PREC_BF16 : PREC_F32;
+    DeviceGuard g(device);
+    // class remap tables (models.py:56-58 and :79-80) + the normalisation table (models.py:17-18, 91)
+    unsigned char tab[32 + 3 * 256 * 8];
+    const uint8_t lut3[16] = {1, 1, 0, 2, 2, 2, 2, 2, 2, 0, 2, 2, 2, 2, 2, 2};
+    const uint8_t lutb[16] = {1, 1, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
+    std::memcpy(tab, lut3, 16);
+    std::memcpy(tab + 16, lutb, 16);
+    const double mean[3] = {0.485, 0.456, 0.406}, stdv[3] = {0.229, 0.224, 0.225};
+    for (int ch = 0; ch < 3; ++ch)
+        for (int v = 0; v < 256; ++v) {
+            const double x = ((double)v / 256.0 - mean[ch]) / stdv[ch];
+            std::memcpy(tab + 32 + (ch * 256 + v) * 8, &x, 8);
+        }
+    if (hipMalloc(&c->dev_luts, sizeof(tab)) != hipSuccess || hipMemcpy(c->dev_luts, tab, sizeof(tab), hipMemcpyHostToDevice) != hipSuccess) {
+        delete c;
+        return fail(nullptr, BUGSEG_EHIP, "device allocation failed");
+    }
+    *out = c;
+    return BUGSEG_OK;
+}
+
+int bugseg_destroy(bugseg_ctx *ctx) {
+    if (!ctx) return BUGSEG_OK;
+    DeviceGuard g(ctx->device);
+    (void)hipDeviceSynchronize();
+    if (ctx->dev_w) (void)hipFree(ctx->dev_w);
+    if (ctx->dev_luts) (void)hipFree(ctx->dev_luts);
+    if (ctx->plan.arena) (void)hipFree(ctx->plan.arena);
+    if (ctx->pre_tab) (void)hipFree(ctx->pre_tab);
+    delete ctx;
+    return BUGSEG_OK;
+}
+
+int bugseg_load_weights(bugseg_ctx *ctx, const void *blob, size_t bytes) {
+    if (!ctx || !blob) return fail(ctx, BUGSEG_EINVAL, "NULL argument");
+    DeviceGuard g(ctx->device);
+    std::vector<BlockDesc> blocks;
+    int ncls = 0;
+    std::string why;
+    if (!parse_blob(blob, bytes, blocks, ncls, why)) return fail(ctx, BUGSEG_EFORMAT, "weight blob: " + why);
+    ctx->blocks = std::move(blocks);
+    ctx->ncls = ncls;
+    ctx->loaded = false;
+    if (!pack_all(ctx, why)) return fail(ctx, BUGSEG_EFORMAT, "weight blob: " + why);
+    (void)hipDeviceSynchronize();
+    if (ctx->dev_w) { (void)hipFree(ctx->dev_w); ctx->dev_w = nullptr; }
+    if (ctx->plan.arena) { (void)hipFree(ctx->plan.arena); ctx->plan = Plan(); }
+    if (hipMalloc(&ctx->dev_w, ctx->host_w.size()) != hipSuccess ||
+        hipMemcpy(ctx->dev_w, ctx->host_w.data(), ctx->host_w.size(), hipMemcpyHostToDevice) != hipSuccess)
+        return fail(ctx, BUGSEG_EHIP, "uploading weights failed");
+    ctx->loaded = true;
+    return BUGSEG_OK;
+}
+
+int bugseg_num_classes(const bugseg_ctx *ctx) { return ctx && ctx->loaded ? ctx->ncls : 0; }
+
+size_t bugseg_input_bytes(const bugseg_ctx *ctx, int B, int H, int W) {
+    if (!ctx || B <= 0 || H <= 0 || W <= 0) return 0;
+    return (size_t)B * H * W * 8 * (ctx->prec == PREC_BF16 ? 2 : 4);
+}
+
+int bugseg_preprocess(bugseg_ctx *ctx, const uint8_t *bgr, int B, int H0, int W0, int H, int W, int out_layout,
+                      void *out, void *stream) {
+    if (!ctx || !bgr || !out) return fail(ctx, BUGSEG_EINVAL, "NULL argument");
+    if (B <= 0 || H0 <= 0 || W0 <= 0 || H <= 0 || W <= 0) return fail(ctx, BUGSEG_EINVAL, "bad shape");
+    if (out_layout < BUGSEG_PRE_ENGINE || out_layout > BUGSEG_PRE_NCHW_F32) return fail(ctx, BUGSEG_EINVAL, "bad out_layout");
+    DeviceGuard g(ctx->device);
+    PreArgs a;
+    std::memset(&a, 0, sizeof(a));
+    a.bgr = bgr; a.B = B; a.H0 = H0; a.W0 = W0; a.H = H; a.W = W;
+    a.lut = (const double *)((const unsigned char *)ctx->dev_luts + 32);
+    a.out_layout = out_layout; a.prec = ctx->prec; a.out = out;
+    a.vec_end = W * 3 - (W * 3) % 8;
+    if (H0 == H && W0 == W) {
+        a.mode = 0;
+    } else {
+        const double sx = 1.0 / ((double)W / W0), sy = 1.0 / ((double)H / H0);
+        const int isx = (int)std::lrint(sx), isy = (int)std::lrint(sy);
+        const double eps = 2.220446049250313e-16;
+        if (std::fabs(sx - isx) < eps && std::fabs(sy - isy) < eps && isx == 2 && isy == 2) {
+            a.mode = 1;
+        } else {
+            a.mode = 2;
+            const int key[4] = {H0, W0, H, W};
+            const size_t need = (size_t)W * 4 + (size_t)W * 4 + (size_t)H * 4 + (size_t)H * 4;
+            if (!ctx->pre_tab || std::memcmp(key, ctx->pre_key, sizeof(key)) != 0) {
+                std::vector<unsigned char> h(need);
+                int *xo = (int *)h.data();
+                short *xa = (short *)(h.data() + (size_t)W * 4);
+                int *yo = (int *)(h.data() + (size_t)W * 8);
+                short *yb = (short *)(h.data() + (size_t)W * 8 + (size_t)H * 4);
+                linear_coeffs(W, W0, sx, xo, xa);
+                linear_coeffs(H, H0, sy, yo, yb);
+                if (hipStreamSynchronize((hipStream_t)stream) != hipSuccess) return fail(ctx, BUGSEG_EHIP, "stream sync failed");
+                if (ctx->pre_tab) (void)hipFree(ctx->pre_tab);
+                ctx->pre_tab = nullptr;
+                if (hipMalloc(&ctx->pre_tab, need) != hipSuccess ||
+                    hipMemcpy(ctx->pre_tab, h.data(), need, hipMemcpyHostToDevice) != hipSuccess) {
+                    ctx->pre_tab = nullptr;
+                    return fail(ctx, BUGSEG_EHIP, "resize table upload failed");
+                }
+                std::memcpy(ctx->pre_key, key, sizeof(key));
+                ctx->pre_tab_bytes = need;
+            }
+            unsigned char *t = (unsigned char *)ctx->pre_tab;
+            a.xofs = (const int *)t;
+            a.xa = (const short *)(t + (size_t)W * 4);
+            a.yofs = (const int *)(t + (size_t)W * 8);
+            a.yb = (const short *)(t + (size_t)W * 8 + (size_t)H * 4);
+        }
+    }
+    hipError_t e = launch_preprocess(a, (hipStream_t)stream);
+    if (e != hipSuccess) return fail(ctx, BUGSEG_EHIP, std::string("preprocess launch: ") + hipGetErrorString(e));
+    return BUGSEG_OK;
+}
+
+int bugseg_nchw_to_input(bugseg_ctx *ctx, const void *x, int is_f64, int B, int H, int W, void *out, void *stream) {
+    if (!ctx || !x || !out) return fail(ctx, BUGSEG_EINVAL, "NULL argument");
+    if (B <= 0 || H <= 0 || W <= 0) return fail(ctx, BUGSEG_EINVAL, "bad shape");
+    DeviceGuard g(ctx->device);
+    NchwArgs a{x, is_f64 ? 1 : 0, B, H, W, ctx->prec, out};
+    hipError_t e = launch_nchw_to_input(a, (hipStream_t)stream);
+    if (e != hipSuccess) return fail(ctx, BUGSEG_EHIP, std::string("layout launch: ") + hipGetErrorString(e));
+    return BUGSEG_OK;
+}
+
+int bugseg_enet_forward(bugseg_ctx *ctx, const void *in, int B, int H, int W, int out_kind, void *out, void *stream) {
+    if (!ctx || !in || !out) return fail(ctx, BUGSEG_EINVAL, "NULL argument");
+    if (!ctx->loaded) return fail(ctx, BUGSEG_ESTATE, "no weights loaded");
+    if (out_kind < BUGSEG_OUT_LOGITS_F32 || out_kind > BUGSEG_OUT_BINARY_U8) return fail(ctx, BUGSEG_EINVAL, "bad out_kind");
+    DeviceGuard g(ctx->device);
+    std::string why;
+    if (!build_plan(ctx, B, H, W, why)) return fail(ctx, BUGSEG_EINVAL, why);
+    Plan &pl = ctx->plan;
+    pl.ops.front().a.in = in;
+    ConvArgs &last = pl.ops.back().a;
+    last.cls_out = nullptr; last.logits_out = nullptr; last.lut = nullptr;
+    const uint8_t *luts = (const uint8_t *)ctx->dev_luts;
+    switch (out_kind) {
+    case BUGSEG_OUT_LOGITS_F32: last.logits_out = (float *)out; break;
+    case BUGSEG_OUT_CLASS15_U8: last.cls_out = (uint8_t *)out; break;
+    case BUGSEG_OUT_CLASS3_U8: last.cls_out = (uint8_t *)out; last.lut = luts; break;
+    case BUGSEG_OUT_BINARY_U8: last.cls_out = (uint8_t *)out; last.lut = luts + 16; break;
+    }
+    for (size_t i = 0; i < pl.ops.size(); ++i) {
+        const Op &op = pl.ops[i];
+        hipError_t e = launch_conv(ctx->prec, op.nr, op.epi, op.a, (hipStream_t)stream);
+        if (e != hipSuccess) return fail(ctx, BUGSEG_EHIP, "conv launch " + std::to_string(i) + ": " + hipGetErrorString(e));
+    }
+    return BUGSEG_OK;
+}
+
+int bugseg_bev_occgrid(bugseg_ctx *ctx, const uint8_t *seg, int B, const bugseg_bev_params *p, int8_t *out, void *stream) {
+    if (!ctx || !seg || !p || !out) return fail(ctx, BUGSEG_EINVAL, "NULL argument");
+    if (B <= 0 || p->in_rows <= 0 || p->in_cols <= 0 || p->warp_w <= 0 || p->warp_h <= 0 || p->occ_w <= 0 ||
+        p->occ_h <= 0 || p->occ_w_px <= 0 || p->occ_h_px <= 0)
+        return fail(ctx, BUGSEG_EINVAL, "bad BEV geometry");
+    DeviceGuard g(ctx->device);
+    BevArgs a;
+    std::memset(&a, 0, sizeof(a));
+    a.seg = seg; a.B = B; a.in_rows = p->in_rows; a.in_cols = p->in_cols;
+    {
+        // cv::invert(M) closed-form 3x3 branch (DECOMP_LU), as warpPerspective does without WARP_INVERSE_MAP
+#pragma clang fp contract(off)
+        const double *S = p->M;
+        double d = S[0] * (S[4] * S[8] - S[5] * S[7]) - S[1] * (S[3] * S[8] - S[5] * S[6]) + S[2] * (S[3] * S[7] - S[4] * S[6]);
+        if (d != 0.0) {
+            d = 1.0 / d;
+            a.Mi[0] = (S[4] * S[8] - S[5] * S[7]) * d;
+            a.Mi[1] = (S[2] * S[7] - S[1] * S[8]) * d;
+            a.Mi[2] = (S[1] * S[5] - S[2] * S[4]) * d;
+            a.Mi[3] = (S[5] * S[6] - S[3] * S[8]) * d;
+            a.Mi[4] = (S[0] * S[8] - S[2] * S[6]) * d;
+            a.Mi[5] = (S[2] * S[3] - S[0] * S[5]) * d;
+            a.Mi[6] = (S[3] * S[7] - S[4] * S[6]) * d;
+            a.Mi[7] = (S[1] * S[6] - S[0] * S[7]) * d;
+            a.Mi[8] = (S[0] * S[4] - S[1] * S[3]) * d;
+        }
+    }
+    const int bh0 = std::min(16, p->warp_h);
+    a.bw0 = std::min(1024 / bh0, p->warp_w);
+    a.warp_w = p->warp_w; a.warp_h = p->warp_h;
+    a.occ_w_px = p->occ_w_px; a.occ_h_px = p->occ_h_px; a.occ_w = p->occ_w; a.occ_h = p->occ_h;
+    a.left_x = p->left_x; a.top_y = p->top_y;
+    a.ifx = 1.0 / ((double)p->occ_w / p->occ_w_px);
+    a.ify = 1.0 / ((double)p->occ_h / p->occ_h_px);
+    a.ros_layout = p->ros_layout;
+    a.out = out;
+    hipError_t e = launch_bev(a, (hipStream_t)stream);
+    if (e != hipSuccess) return fail(ctx, BUGSEG_EHIP, std::string("bev launch: ") + hipGetErrorString(e));
+    return BUGSEG_OK;
+}
+
+int bugseg_plan_info(bugseg_ctx *ctx, int B, int H, int W, int out_kind, int *n_launches, double *alg_bytes, double *flops) {
+    if (!ctx) return fail(ctx, BUGSEG_EINVAL, "NULL ctx");
+    if (!ctx->loaded) return fail(ctx, BUGSEG_ESTATE, "no weights loaded");
+    DeviceGuard g(ctx->device);
+    std::string why;
+    if (!build_plan(ctx, B, H, W, why)) return fail(ctx, BUGSEG_EINVAL, why);
+    double by = 0, fl = 0;
+    for (const Op &op : ctx->plan.ops) { by += op.bytes; fl += op.flops; }
+    // final epilogue output
+    by += out_kind == BUGSEG_OUT_LOGITS_F32 ? (double)B * H * W * ctx->ncls * 4 : (double)B * H * W;
+    if (n_launches) *n_launches = (int)ctx->plan.ops.size();
+    if (alg_bytes) *alg_bytes = by;
+    if (flops) *flops = fl;
+    return BUGSEG_OK;
+}
+
+}  // extern "C"

@@ -1,0 +1,341 @@
+// Implicit-GEMM convolution for gfx950 with the ENet epilogues fused in.
+//
+// Replaces the TF Conv2D / BN / PReLU / MaxPoolWithArgmax / MaxUnpool / Conv2DBackpropInput /
+// ArgMax / SelectV2 kernels that run inside the reference's sess.run + tf.math.argmax
+// (models.py:43-58). One launch = one convolution of ENet with everything that consumes its
+// output element-wise (bias, activation, residual add, pooling / unpooling of the skip path,
+// pixel shuffle of a stride-2 transposed conv, class argmax + remap) done in registers.
+//
+// Tiling (CDNA4, wave64): a 256-thread workgroup owns 4 * MR * 16 consecutive pixels of the
+// GEMM grid; each wave owns MR 16-pixel column fragments and ALL output channels (NR 16-row
+// fragments). MFMA v_mfma_f32_16x16x32_bf16 (or 8 x v_mfma_f32_16x16x4_f32 in the fp32 parity
+// mode) takes A = weights (row = output channel) and B = pixels (column = pixel), so the
+// accumulator puts 4 consecutive channels of one pixel in each lane: NHWC stores and residual
+// loads are 8/16-byte vectors. The B fragment (8 consecutive k = 8 channels of one input pixel
+// at one tap) is one 16-byte (bf16) global load per lane straight into VGPRs — no LDS round
+// trip, since every loaded pixel fragment is reused by NR MFMAs in registers. The whole layer's
+// weights (<= 37 KB) are staged in LDS once per workgroup; workgroups stride over tiles with an
+// XCD-aware mapping (blocks sharing blockIdx%8 walk one contiguous range of tiles, so the 3x3 /
+// dilated halo re-reads of neighbouring tiles hit the same XCD's L2).
+#include "bugseg_internal.h"
+
+namespace bugseg {
+
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+
+struct RawB { uint4 v; };          // 8 bf16
+struct RawF { float4 a, b; };      // 8 f32
+
+template <typename T> struct Tr;
+template <> struct Tr<__bf16> { using Raw = RawB; };
+template <> struct Tr<float> { using Raw = RawF; };
+
+__device__ __forceinline__ void zero(RawB &r) { r.v = make_uint4(0, 0, 0, 0); }
+__device__ __forceinline__ void zero(RawF &r) { r.a = make_float4(0.f, 0.f, 0.f, 0.f); r.b = r.a; }
+__device__ __forceinline__ void ld8(RawB &r, const __bf16 *p) { r.v = *reinterpret_cast<const uint4 *>(p); }
+__device__ __forceinline__ void ld8(RawF &r, const float *p) {
+    r.a = reinterpret_cast<const float4 *>(p)[0];
+    r.b = reinterpret_cast<const float4 *>(p)[1];
+}
+
+__device__ __forceinline__ void mma(f32x4 &acc, const RawB &w, const RawB &x) {
+    acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, w.v), __builtin_bit_cast(bf16x8, x.v),
+                                                  acc, 0, 0, 0);
+}
+// fp32 parity mode: sub-MFMA j contracts element j of every lane's 8-group (lane>>4 = group),
+// so the 8 sub-MFMAs together cover the same 32 k as one bf16 MFMA (exact f32 products).
+__device__ __forceinline__ void mma(f32x4 &acc, const RawF &w, const RawF &x) {
+    acc = __builtin_amdgcn_mfma_f32_16x16x4f32(w.a.x, x.a.x, acc, 0, 0, 0);
+    acc = __builtin_amdgcn_mfma_f32_16x16x4f32(w.a.y, x.a.y, acc, 0, 0, 0);
+    acc = __builtin_amdgcn_mfma_f32_16x16x4f32(w.a.z, x.a.z, acc, 0, 0, 0);
+    acc = __builtin_amdgcn_mfma_f32_16x16x4f32(w.a.w, x.a.w, acc, 0, 0, 0);
+    acc = __builtin_amdgcn_mfma_f32_16x16x4f32(w.b.x, x.b.x, acc, 0, 0, 0);
+    acc = __builtin_amdgcn_mfma_f32_16x16x4f32(w.b.y, x.b.y, acc, 0, 0, 0);
+    acc = __builtin_amdgcn_mfma_f32_16x16x4f32(w.b.z, x.b.z, acc, 0, 0, 0);
+    acc = __builtin_amdgcn_mfma_f32_16x16x4f32(w.b.w, x.b.w, acc, 0, 0, 0);
+}
+
+__device__ __forceinline__ float4 ld4f(const float *p) { return *reinterpret_cast<const float4 *>(p); }
+__device__ __forceinline__ float4 ld4(const float *p) { return *reinterpret_cast<const float4 *>(p); }
+__device__ __forceinline__ float4 ld4(const __bf16 *p) {
+    uint2 u = *reinterpret_cast<const uint2 *>(p);
+    return make_float4(__uint_as_float(u.x << 16), __uint_as_float(u.x & 0xffff0000u),
+                       __uint_as_float(u.y << 16), __uint_as_float(u.y & 0xffff0000u));
+}
+__device__ __forceinline__ void st4(float *p, float4 v) { *reinterpret_cast<float4 *>(p) = v; }
+__device__ __forceinline__ void st4(__bf16 *p, float4 v) {
+    typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
+    bf16x4 b = {(__bf16)v.x, (__bf16)v.y, (__bf16)v.z, (__bf16)v.w};
+    *reinterpret_cast<bf16x4 *>(p) = b;
+}
+__device__ __forceinline__ float ld1(const float *p) { return *p; }
+__device__ __forceinline__ float ld1(const __bf16 *p) { return (float)*p; }
+
+__device__ __forceinline__ float prelu(float v, float s) { return v > 0.f ? v : v * s; }
+__device__ __forceinline__ float4 prelu4(float4 v, float4 s) {
+    return make_float4(prelu(v.x, s.x), prelu(v.y, s.y), prelu(v.z, s.z), prelu(v.w, s.w));
+}
+__device__ __forceinline__ float4 add4(float4 a, float4 b) { return make_float4(a.x + b.x, a.y + b.y, a.z + b.z, a.w + b.w); }
+__device__ __forceinline__ float4 f4(const f32x4 &v) { return make_float4(v[0], v[1], v[2], v[3]); }
+__device__ __forceinline__ float get(const float4 &v, int r) { return r == 0 ? v.x : r == 1 ? v.y : r == 2 ? v.z : v.w; }
+
+template <int NR> struct Cfg { static constexpr int MR = NR >= 4 ? 2 : 4; };
+
+template <typename T, int NR, int EPI>
+__global__ void __launch_bounds__(256) conv_kernel(const ConvArgs a) {
+    constexpr int MR = Cfg<NR>::MR;
+    constexpr int TILE = 4 * MR * 16;
+    using Raw = typename Tr<T>::Raw;
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+
+    const int tid = threadIdx.x;
+    const int lane = tid & 63, wave = tid >> 6, col = lane & 15, kq = lane >> 4;
+    const int KS = a.Kpad + 16 / (int)sizeof(T);                     // LDS row stride (elements)
+    T *wl = reinterpret_cast<T *>(smem);
+    int *gt = reinterpret_cast<int *>(smem + (size_t)a.Npad * KS * sizeof(T));
+    {
+        const int cpr = a.Kpad * (int)sizeof(T) / 16;
+        const int total = a.Npad * cpr;
+        const uint4 *src = reinterpret_cast<const uint4 *>(a.w);
+        for (int i = tid; i < total; i += 256) {
+            const int r = i / cpr, c = i - r * cpr;
+            *reinterpret_cast<uint4 *>(smem + (size_t)r * KS * sizeof(T) + c * 16) = src[i];
+        }
+        for (int i = tid; i < a.Ksteps * 4; i += 256) gt[i] = a.gtab[i];
+    }
+    __syncthreads();
+
+    const T *in = reinterpret_cast<const T *>(a.in);
+    const int HWg = a.Hg * a.Wg;
+    // XCD-aware tile walk: gridDim.x is a multiple of 8; group x = blockIdx%8 owns the contiguous
+    // chunk [x*C, (x+1)*C) of tiles (speed only; any placement is correct).
+    const int G = gridDim.x, grp = blockIdx.x & 7, slot = blockIdx.x >> 3, nslots = G >> 3;
+    const int C = (a.ntiles + 7) >> 3;
+
+    for (int i = slot; i < C; i += nslots) {
+        const int tile = grp * C + i;
+        if (tile >= a.ntiles) break;
+        int pn[MR], py[MR], px[MR];
+        bool pv[MR];
+#pragma unroll
+        for (int m = 0; m < MR; ++m) {
+            const int p = tile * TILE + wave * MR * 16 + m * 16 + col;
+            pv[m] = p < a.M;
+            const int pp = pv[m] ? p : 0;
+            pn[m] = pp / HWg;
+            const int r = pp - pn[m] * HWg;
+            py[m] = r / a.Wg;
+            px[m] = r - py[m] * a.Wg;
+        }
+        f32x4 acc[MR][NR];
+#pragma unroll
+        for (int m = 0; m < MR; ++m)
+#pragma unroll
+            for (int n = 0; n < NR; ++n) acc[m][n] = (f32x4){0.f, 0.f, 0.f, 0.f};
+
+        for (int s = 0; s < a.Ksteps; ++s) {
+            const int g = gt[s * 4 + kq];
+            const int dy = (int)(signed char)(g & 0xff), dx = (int)(signed char)((g >> 8) & 0xff);
+            const int coff = (g >> 16) & 0xffff;
+            Raw xf[MR];
+#pragma unroll
+            for (int m = 0; m < MR; ++m) {
+                const int iy = py[m] * a.stride + dy, ix = px[m] * a.stride + dx;
+                const bool ok = pv[m] && coff != 0xffff && (unsigned)iy < (unsigned)a.Hin && (unsigned)ix < (unsigned)a.Win;
+                if (ok)
+                    ld8(xf[m], in + ((size_t)(pn[m] * a.Hin + iy) * a.Win + ix) * a.CinS + coff);
+                else
+                    zero(xf[m]);
+            }
+#pragma unroll
+            for (int n = 0; n < NR; ++n) {
+                Raw wf;
+                ld8(wf, wl + (n * 16 + col) * KS + s * 32 + kq * 8);
+#pragma unroll
+                for (int m = 0; m < MR; ++m) mma(acc[m][n], wf, xf[m]);
+            }
+        }
+
+        // ------------------------------- epilogues -------------------------------------------
+        T *out = reinterpret_cast<T *>(a.out);
+        if constexpr (EPI == EPI_CLASSES) {
+            // n fragment = output phase (a,b); rows = 16 (padded) classes, 4 per lane.
+#pragma unroll
+            for (int m = 0; m < MR; ++m) {
+#pragma unroll
+                for (int n = 0; n < NR; ++n) {
+                    const int c = n * 16 + kq * 4;
+                    const float4 b4 = ld4f(a.bias + c);
+                    const float4 v = add4(f4(acc[m][n]), b4);
+                    float best = -INFINITY;
+                    int bi = 0x7fffffff;
+#pragma unroll
+                    for (int r = 0; r < 4; ++r) {
+                        const int cls = kq * 4 + r;
+                        const float x = get(v, r);
+                        if (cls < a.ncls && x > best) { best = x; bi = cls; }
+                    }
+                    // lowest class index wins ties (tf.math.argmax, models.py:55)
+#pragma unroll
+                    for (int off = 16; off <= 32; off <<= 1) {
+                        const float ob = __shfl_xor(best, off, 64);
+                        const int oi = __shfl_xor(bi, off, 64);
+                        if (ob > best || (ob == best && oi < bi)) { best = ob; bi = oi; }
+                    }
+                    if (pv[m]) {
+                        const int oy = 2 * py[m] + (n >> 1), ox = 2 * px[m] + (n & 1);
+                        const size_t opix = (size_t)(pn[m] * a.Hout + oy) * a.Wout + ox;
+                        if (a.cls_out && kq == 0) {
+                            const int k = bi < 16 ? bi : 0;
+                            a.cls_out[opix] = a.lut ? a.lut[k] : (uint8_t)k;
+                        }
+                        if (a.logits_out) {
+                            const size_t plane = (size_t)a.Hout * a.Wout;
+#pragma unroll
+                            for (int r = 0; r < 4; ++r) {
+                                const int cls = kq * 4 + r;
+                                if (cls < a.ncls)
+                                    a.logits_out[((size_t)pn[m] * a.ncls + cls) * plane + (size_t)oy * a.Wout + ox] = get(v, r);
+                            }
+                        }
+                    }
+                }
+            }
+        } else {
+#pragma unroll
+            for (int m = 0; m < MR; ++m) {
+                if (!pv[m]) continue;
+                const size_t gpix = (size_t)(pn[m] * a.Hg + py[m]) * a.Wg + px[m];
+#pragma unroll
+                for (int n = 0; n < NR; ++n) {
+                    const int c = n * 16 + kq * 4;
+                    float4 v = add4(f4(acc[m][n]), ld4f(a.bias + c));
+                    if constexpr (EPI == EPI_SHUFFLE) {
+                        const int ph = c / a.coutP, cl = c - ph * a.coutP;
+                        if (cl >= a.outC) continue;
+                        v = prelu4(v, ld4f(a.slope1 + c));
+                        const int oy = 2 * py[m] + (ph >> 1), ox = 2 * px[m] + (ph & 1);
+                        st4(out + ((size_t)(pn[m] * a.Hout + oy) * a.Wout + ox) * a.outC + cl, v);
+                        continue;
+                    }
+                    if (c >= a.outC) continue;
+                    if constexpr (EPI == EPI_INIT) {
+                        // concat(conv, maxpool(in)) -> BN -> act (InitialBlock); pool channels carry
+                        // their BN as pscale (x) + bias.
+                        const float4 ps = ld4f(a.pscale + c);
+                        float pv4[4] = {0.f, 0.f, 0.f, 0.f};
+                        const int k = a.pool_k, pad = (k - 1) >> 1;
+#pragma unroll
+                        for (int r = 0; r < 4; ++r) {
+                            const int ch = c + r - a.cconv;
+                            if (ch < 0 || ch >= a.cpool) continue;
+                            float mx = -INFINITY;
+                            for (int wy = 0; wy < k; ++wy) {
+                                const int iy = 2 * py[m] - pad + wy;
+                                if ((unsigned)iy >= (unsigned)a.Hin) continue;
+                                for (int wx = 0; wx < k; ++wx) {
+                                    const int ix = 2 * px[m] - pad + wx;
+                                    if ((unsigned)ix >= (unsigned)a.Win) continue;
+                                    const float x = ld1(in + ((size_t)(pn[m] * a.Hin + iy) * a.Win + ix) * a.CinS + ch);
+                                    mx = x > mx ? x : mx;
+                                }
+                            }
+                            pv4[r] = mx * get(ps, r);
+                        }
+                        v = add4(v, make_float4(pv4[0], pv4[1], pv4[2], pv4[3]));
+                        v = prelu4(v, ld4f(a.slope1 + c));
+                    } else {
+                        v = prelu4(v, ld4f(a.slope1 + c));
+                    }
+                    if constexpr (EPI == EPI_RESADD) {
+                        if (c < a.resC) v = add4(v, ld4(reinterpret_cast<const T *>(a.res) + gpix * a.resCS + c));
+                        v = prelu4(v, ld4f(a.slope2 + c));
+                    } else if constexpr (EPI == EPI_RESPOOL) {
+                        // main branch: MaxPool2d(2, 2, return_indices) of the block input, zero-padded
+                        // to cout channels; first maximum in window order wins (strict >).
+                        if (c < a.resC) {
+                            const T *rs = reinterpret_cast<const T *>(a.res);
+                            float4 best = make_float4(-INFINITY, -INFINITY, -INFINITY, -INFINITY);
+                            int bi[4] = {0, 0, 0, 0};
+#pragma unroll
+                            for (int pos = 0; pos < 4; ++pos) {
+                                const int ry = 2 * py[m] + (pos >> 1), rx = 2 * px[m] + (pos & 1);
+                                const float4 x = ld4(rs + ((size_t)(pn[m] * a.resH + ry) * a.resW + rx) * a.resCS + c);
+                                if (x.x > best.x) { best.x = x.x; bi[0] = pos; }
+                                if (x.y > best.y) { best.y = x.y; bi[1] = pos; }
+                                if (x.z > best.z) { best.z = x.z; bi[2] = pos; }
+                                if (x.w > best.w) { best.w = x.w; bi[3] = pos; }
+                            }
+                            v = add4(v, best);
+                            *reinterpret_cast<uint32_t *>(a.idx_out + gpix * a.idxCS + c) =
+                                (uint32_t)bi[0] | ((uint32_t)bi[1] << 8) | ((uint32_t)bi[2] << 16) | ((uint32_t)bi[3] << 24);
+                        }
+                        v = prelu4(v, ld4f(a.slope2 + c));
+                    } else if constexpr (EPI == EPI_RESUNPOOL) {
+                        // MaxUnpool2d(2): the low-res main value lands on the window position its
+                        // pooling index recorded; every other position of the window is 0.
+                        if (c < a.resC) {
+                            const int ly = py[m] >> 1, lx = px[m] >> 1;
+                            const size_t lpix = (size_t)(pn[m] * a.resH + ly) * a.resW + lx;
+                            const uint32_t id = *reinterpret_cast<const uint32_t *>(a.idx_in + lpix * a.idxCS + c);
+                            const uint32_t pos = (uint32_t)(((py[m] & 1) << 1) | (px[m] & 1));
+                            const float4 mv = ld4(reinterpret_cast<const T *>(a.res) + lpix * a.resCS + c);
+                            v.x += ((id & 0xff) == pos) ? mv.x : 0.f;
+                            v.y += (((id >> 8) & 0xff) == pos) ? mv.y : 0.f;
+                            v.z += (((id >> 16) & 0xff) == pos) ? mv.z : 0.f;
+                            v.w += (((id >> 24) & 0xff) == pos) ? mv.w : 0.f;
+                        }
+                        v = prelu4(v, ld4f(a.slope2 + c));
+                    }
+                    st4(out + gpix * a.outC + c, v);
+                }
+            }
+        }
+    }
+}
+
+int conv_tile_pixels(int nr) { return 4 * (nr >= 4 ? 2 : 4) * 16; }
+
+size_t conv_lds_bytes(int prec, const ConvArgs &a) {
+    const size_t es = prec == PREC_BF16 ? 2 : 4;
+    return (size_t)a.Npad * (a.Kpad + 16 / es) * es + (size_t)a.Ksteps * 4 * sizeof(int);
+}
+
+template <typename T, int NR>
+static hipError_t launch_nr(int epi, const ConvArgs &a, dim3 grid, size_t lds, hipStream_t s) {
+    switch (epi) {
+    case EPI_PLAIN: hipLaunchKernelGGL((conv_kernel<T, NR, EPI_PLAIN>), grid, dim3(256), lds, s, a); break;
+    case EPI_RESADD: hipLaunchKernelGGL((conv_kernel<T, NR, EPI_RESADD>), grid, dim3(256), lds, s, a); break;
+    case EPI_RESPOOL: hipLaunchKernelGGL((conv_kernel<T, NR, EPI_RESPOOL>), grid, dim3(256), lds, s, a); break;
+    case EPI_RESUNPOOL: hipLaunchKernelGGL((conv_kernel<T, NR, EPI_RESUNPOOL>), grid, dim3(256), lds, s, a); break;
+    case EPI_INIT: hipLaunchKernelGGL((conv_kernel<T, NR, EPI_INIT>), grid, dim3(256), lds, s, a); break;
+    case EPI_SHUFFLE: hipLaunchKernelGGL((conv_kernel<T, NR, EPI_SHUFFLE>), grid, dim3(256), lds, s, a); break;
+    case EPI_CLASSES: hipLaunchKernelGGL((conv_kernel<T, NR, EPI_CLASSES>), grid, dim3(256), lds, s, a); break;
+    default: return hipErrorInvalidValue;
+    }
+    return hipGetLastError();
+}
+
+template <typename T>
+static hipError_t launch_t(int nr, int epi, const ConvArgs &a, dim3 grid, size_t lds, hipStream_t s) {
+    switch (nr) {
+    case 1: return launch_nr<T, 1>(epi, a, grid, lds, s);
+    case 2: return launch_nr<T, 2>(epi, a, grid, lds, s);
+    case 4: return launch_nr<T, 4>(epi, a, grid, lds, s);
+    case 8: return launch_nr<T, 8>(epi, a, grid, lds, s);
+    default: return hipErrorInvalidValue;
+    }
+}
+
+hipError_t launch_conv(int prec, int nr, int epi, const ConvArgs &a, hipStream_t s) {
+    // one workgroup per tile up to 2048 workgroups (8 per CU), rounded to a multiple of 8 for the
+    // XCD-aware walk; larger grids stride.
+    int g = a.ntiles < 2048 ? a.ntiles : 2048;
+    g = (g + 7) & ~7;
+    const size_t lds = conv_lds_bytes(prec, a);
+    if (prec == PREC_BF16) return launch_t<__bf16>(nr, epi, a, dim3(g), lds, s);
+    return launch_t<float>(nr, epi, a, dim3(g), lds, s);
+}
+
+}  // namespace bugseg

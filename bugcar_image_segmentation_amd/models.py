@@ -1,0 +1,185 @@
+"""Model plugins with the reference's API (models.py), running on the native MI355X engine.
+
+Drop-in for `models.py` of the reference: same class names, class constants, method names,
+argument meaning and return dtypes/shapes. Underneath, `sess.run` on a frozen TF graph
+(models.py:43-44) and the TF-eager argmax/remap (models.py:55-58, 78-80) are replaced by one
+launch plan of hand-written gfx950 kernels (libbugseg.so) with the argmax + class remap fused into
+the final transposed-convolution epilogue. There is no CPU fallback: without the library or a GPU
+every call raises.
+
+Additions beyond the reference API (device fast paths for batching): `predict_device`,
+`logits`, `preprocess_device`.
+"""
+from __future__ import annotations
+
+import os
+from abc import ABC
+
+import numpy as np
+import torch
+
+from . import _native as N
+from . import enet_spec
+
+
+class InferenceModel(ABC):
+    """models.py:8-13. (The reference declares `preprocess(rgb_image)` under @classmethod, which
+    binds the image to `cls`; subclasses here take `(cls, bgr_frame)` as ENET does.)"""
+
+    def predict(self, preprocessed_image):
+        pass
+
+    @classmethod
+    def preprocess(cls, bgr_frame):
+        pass
+
+
+def _as_device_tensor(x, dtype=None) -> torch.Tensor:
+    if isinstance(x, torch.Tensor):
+        t = x
+    else:
+        t = torch.from_numpy(np.ascontiguousarray(x))
+    if dtype is not None and t.dtype != dtype:
+        t = t.to(dtype)
+    if not t.is_cuda:
+        t = t.to(torch.device("cuda", torch.cuda.current_device()), non_blocking=False)
+    return t.contiguous()
+
+
+def _load_blob(path: str) -> bytes:
+    if not os.path.exists(path):
+        # TF's GFile raises NotFoundError here (models.py:25); FileNotFoundError is its Python twin
+        raise FileNotFoundError(f"{path}: no such file")
+    with open(path, "rb") as f:
+        data = f.read()
+    if data[:4] == b"BSG1":
+        return data
+    raise NotImplementedError(
+        f"{path} is not a BSG1 weight blob. Frozen TF GraphDef import (enet.pb) is the next row of the "
+        "build (SURVEY.md §8(f) 1); convert the graph's Const tensors with enet_spec.serialize meanwhile.")
+
+
+class ENET(InferenceModel):
+    """models.py:14-95 on the MI355X engine."""
+    INPUT_TENSOR_NAME = "input0:0"
+    OUTPUT_TENSOR_NAME = "CATkrIDy/concat:0"
+    IMAGE_MEAN = np.array([0.485, 0.456, 0.406])
+    IMAGE_STD = np.array([0.229, 0.224, 0.225])
+    INPUT_WIDTH, INPUT_HEIGHT = (512, 256)
+
+    def __init__(self, GRAPH_PB_PATH=None, *, weights=None, precision: str = "fp32", device: int | None = None):
+        """GRAPH_PB_PATH: weight file (default "./pretrained_models/enet.pb", models.py:23-24).
+        weights: a BSG1 blob (bytes) or an enet_spec block list, instead of a file.
+        precision: "fp32" (parity mode) or "bf16" (throughput mode)."""
+        if precision not in ("fp32", "bf16"):
+            raise ValueError("precision must be 'fp32' or 'bf16'")
+        if weights is None:
+            if GRAPH_PB_PATH is None:
+                GRAPH_PB_PATH = "./pretrained_models/enet.pb"
+            blob = _load_blob(GRAPH_PB_PATH)
+        elif isinstance(weights, (bytes, bytearray)):
+            blob = bytes(weights)
+        else:
+            blob = enet_spec.serialize(weights)
+        self.precision = precision
+        self.ctx = N.Context(device, N.BF16 if precision == "bf16" else N.FP32)
+        self.ctx.load_weights(blob)
+        self.num_classes = self.ctx.num_classes
+        self._bufs: dict = {}
+        self.test = None
+
+    # -- device fast paths --------------------------------------------------------------------
+    def _buf(self, key, shape, dtype):
+        t = self._bufs.get(key)
+        if t is None or tuple(t.shape) != tuple(shape) or t.dtype != dtype or t.device.index != self.ctx.device:
+            t = torch.empty(shape, dtype=dtype, device=torch.device("cuda", self.ctx.device))
+            self._bufs[key] = t
+        return t
+
+    def engine_input(self, preprocessed) -> torch.Tensor:
+        """NCHW (B,3,H,W) float (numpy or torch) -> engine input tensor (B,H,W,8) on the device."""
+        x = _as_device_tensor(preprocessed)
+        if x.dtype not in (torch.float32, torch.float64):
+            x = x.to(torch.float32)
+        if x.dim() != 4 or x.shape[1] != 3:
+            raise ValueError(f"expected (B, 3, H, W) input, got {tuple(x.shape)}")
+        B, _, H, W = x.shape
+        es = 2 if self.precision == "bf16" else 4
+        out = self._buf("in", (B, H, W, 8 * es), torch.uint8)
+        self.ctx.nchw_to_input(x, B, H, W, out)
+        return out
+
+    def predict_device(self, engine_in: torch.Tensor, out_kind: int = N.OUT_CLASS3_U8, out: torch.Tensor | None = None):
+        """Forward on an engine-input tensor (B,H,W,8*elem bytes u8 view) -> device tensor."""
+        B, H, W = engine_in.shape[:3]
+        dev = torch.device("cuda", self.ctx.device)
+        if out is None:
+            if out_kind == N.OUT_LOGITS_F32:
+                out = torch.empty((B, self.num_classes, H, W), dtype=torch.float32, device=dev)
+            else:
+                out = torch.empty((B, H, W), dtype=torch.uint8, device=dev)
+        self.ctx.forward(engine_in, B, H, W, out_kind, out)
+        return out
+
+    def logits(self, preprocessed_imgs) -> np.ndarray:
+        """The TF output tensor OUTPUT_TENSOR_NAME: (B, classes, H, W) float32 NCHW (models.py:43-44,52)."""
+        return self.predict_device(self.engine_input(preprocessed_imgs), N.OUT_LOGITS_F32).cpu().numpy()
+
+    # -- reference API ------------------------------------------------------------------------
+    def predict(self, preprocessed_imgs) -> np.ndarray:
+        """models.py:42-69: uint8 (B,H,W); 1 road(+lane marking), 0 flat non-road (pavement,
+        vegetation), 2 everything else. Argmax ties go to the lowest class (tf.math.argmax)."""
+        return self.predict_device(self.engine_input(preprocessed_imgs), N.OUT_CLASS3_U8).cpu().numpy()
+
+    def predict_binary(self, preprocessed_imgs) -> np.ndarray:
+        """models.py:70-82: uint8 (B,H,W), 1 where the class is road or lane marking."""
+        return self.predict_device(self.engine_input(preprocessed_imgs), N.OUT_BINARY_U8).cpu().numpy()
+
+    @classmethod
+    def preprocess_device(cls, bgr, layout: int = N.PRE_NCHW_F64, ctx: "N.Context | None" = None,
+                          width: int | None = None, height: int | None = None) -> torch.Tensor:
+        """Batched models.py:84-95 on the device: bgr (B,H0,W0,3) or (H0,W0,3) uint8."""
+        x = _as_device_tensor(bgr, torch.uint8)
+        if x.dim() == 3:
+            x = x.unsqueeze(0)
+        if x.dim() != 4 or x.shape[3] != 3:
+            raise ValueError(f"expected a BGR uint8 frame (H, W, 3), got {tuple(x.shape)}")
+        W = cls.INPUT_WIDTH if width is None else width
+        H = cls.INPUT_HEIGHT if height is None else height
+        B, H0, W0 = x.shape[:3]
+        c = ctx if ctx is not None else N.shared_context(x.device.index)
+        dev = x.device
+        if layout == N.PRE_NCHW_F64:
+            out = torch.empty((B, 3, H, W), dtype=torch.float64, device=dev)
+        elif layout == N.PRE_NCHW_F32:
+            out = torch.empty((B, 3, H, W), dtype=torch.float32, device=dev)
+        else:
+            out = torch.empty((B, H, W, 8 * (2 if c.precision == N.BF16 else 4)), dtype=torch.uint8, device=dev)
+        c.preprocess(x, B, H0, W0, H, W, layout, out)
+        return out
+
+    @classmethod
+    def preprocess(cls, bgr_frame) -> np.ndarray:
+        """models.py:84-95: BGR uint8 frame -> (1, 3, INPUT_HEIGHT, INPUT_WIDTH) float64 RGB,
+        (x/256 - mean)/std. Bit-identical to the reference's NumPy float64 arithmetic given the
+        same resized image (cv2.resize INTER_LINEAR restated in fixed point on the device)."""
+        return cls.preprocess_device(bgr_frame, N.PRE_NCHW_F64).cpu().numpy()
+
+
+class DeepLabV3(InferenceModel):
+    """models.py:98-136. Not built this round: `deeplab.pb` is absent (.MISSING_LARGE_BLOBS:1), its
+    backbone is unknown and the reference wrapper is broken as written."""
+    INPUT_TENSOR_NAME = "import/ImageTensor:0"
+    OUTPUT_TENSOR_NAME = "import/SemanticPredictions:0"
+    INPUT_SIZE = 1024
+    FROZEN_GRAPH_NAME = "deeplab.pb"
+
+    def __init__(self, GRAPH_PB_PATH):
+        raise NotImplementedError("DeepLabV3 (ASPP) path is SURVEY.md §8(f) row 3: not built yet")
+
+    def predict(self, img):
+        raise NotImplementedError
+
+    @classmethod
+    def preprocess(cls, bgr_frame):
+        raise NotImplementedError

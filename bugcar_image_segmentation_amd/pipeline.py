@@ -1,0 +1,54 @@
+"""Batched, device-resident frame -> occupancy-grid path (BASELINE config 3):
+
+    BGR u8 frames (B,H0,W0,3)  --preprocess kernel-->  engine input (B,H,W,8)
+      --89 fused conv launches (ENet, argmax + 3-class remap in the last epilogue)-->  u8 (B,H,W)
+      --BEV rasteriser kernel-->  int8 grids (B,h,w)   [or ROS data order]
+
+Everything stays in HBM on one stream; there is no host round trip between stages. This is the
+loop the reference's (absent) ROS node runs per frame (README.md:19), batched.
+"""
+from __future__ import annotations
+
+import torch
+
+from . import _native as N
+from .bev import bev_transform_tools
+from .models import ENET
+
+
+class OccupancyPipeline:
+    def __init__(self, model: ENET, bev: bev_transform_tools, grid_w_m: float, grid_h_m: float, cell_m: float,
+                 model_hw: tuple[int, int] | None = None, ros_layout: bool = False):
+        self.model = model
+        self.bev = bev
+        self.grid = (grid_w_m, grid_h_m, cell_m)
+        self.H, self.W = model_hw if model_hw is not None else (ENET.INPUT_HEIGHT, ENET.INPUT_WIDTH)
+        self.ros_layout = ros_layout
+        if (self.H, self.W) != (bev.input_width, bev.input_height):
+            raise ValueError(f"model output {self.H}x{self.W} must equal the calibration's input image size "
+                             f"{bev.input_width}x{bev.input_height} (bev.py:304)")
+        self._x = None
+        self._seg = None
+        self._grid = None
+
+    def _bufs(self, B: int, dev: torch.device):
+        es = 2 if self.model.precision == "bf16" else 4
+        if self._x is None or self._x.shape[0] != B or self._x.device != dev:
+            self._x = torch.empty((B, self.H, self.W, 8 * es), dtype=torch.uint8, device=dev)
+            self._seg = torch.empty((B, self.H, self.W), dtype=torch.uint8, device=dev)
+            p = self.bev.occupancy_params(*self.grid, ros_layout=self.ros_layout)
+            shape = (B, p.occ_w, p.occ_h) if self.ros_layout else (B, p.occ_h, p.occ_w)
+            self._grid = torch.empty(shape, dtype=torch.int8, device=dev)
+        return self._x, self._seg, self._grid
+
+    def run(self, frames_bgr: torch.Tensor, out: torch.Tensor | None = None) -> torch.Tensor:
+        if frames_bgr.dim() != 4 or frames_bgr.shape[3] != 3 or frames_bgr.dtype != torch.uint8 or not frames_bgr.is_cuda:
+            raise ValueError("frames must be a (B, H0, W0, 3) uint8 device tensor")
+        B, H0, W0 = frames_bgr.shape[:3]
+        x, seg, grid = self._bufs(B, frames_bgr.device)
+        ctx = self.model.ctx
+        ctx.preprocess(frames_bgr.contiguous(), B, H0, W0, self.H, self.W, N.PRE_ENGINE, x)
+        ctx.forward(x, B, self.H, self.W, N.OUT_CLASS3_U8, seg)
+        out = grid if out is None else out
+        self.bev.create_occupancy_grid_device(seg, *self.grid, ros_layout=self.ros_layout, out=out)
+        return out

@@ -1,0 +1,130 @@
+/*
+ * bugseg — MI355X-native (gfx950) ENet segmentation -> BEV occupancy-grid path, C ABI.
+ *
+ * The reference exposes no FFI: its boundary is the Python plugin API of models.py / bev.py /
+ * occgrid_to_ros.py. These entry points are what that API's Python shims
+ * (bugcar_image_segmentation_amd/{models,bev,occgrid_to_ros}.py, bound with ctypes) call; each
+ * cites the reference interface it replaces. A ctypes binding a maintainer would add to the
+ * reference itself is shown in INTEGRATION.md.
+ *
+ * Conventions
+ *  - Every pointer argument named *_dev is a DEVICE pointer owned by the caller (e.g. a
+ *    torch tensor's data_ptr()). The library owns only its weights, tables and scratch.
+ *  - `stream` is a hipStream_t (NULL = the legacy default stream). All work of one call is
+ *    enqueued on it; calls return without synchronising.
+ *  - Return 0 on success or a negative BUGSEG_E* code; bugseg_last_error() explains it.
+ *  - One context per device. Calls on one context must be serialised by the caller.
+ *  - Tensor shapes: activations are NHWC. The "engine input" tensor is (B, H, W, 8): RGB plus 5
+ *    zero channels, in the context precision (f32 or bf16).
+ */
+#ifndef BUGSEG_H
+#define BUGSEG_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef struct bugseg_ctx bugseg_ctx;
+
+enum {
+    BUGSEG_OK = 0,
+    BUGSEG_EINVAL = -1,   /* bad argument / shape (reference: AssertionError, bev.py:304)     */
+    BUGSEG_ENOMEM = -2,
+    BUGSEG_EHIP = -3,     /* HIP runtime error                                                 */
+    BUGSEG_EFORMAT = -4,  /* malformed weight blob (reference: GraphDef ParseFromString error)  */
+    BUGSEG_ESTATE = -5    /* e.g. forward before load_weights                                  */
+};
+
+enum { BUGSEG_FP32 = 0, BUGSEG_BF16 = 1 };
+
+/* out_kind of bugseg_enet_forward */
+enum {
+    BUGSEG_OUT_LOGITS_F32 = 0,  /* (B, C, H, W) f32 NCHW — the TF output tensor "CATkrIDy/concat:0" (models.py:16,52) */
+    BUGSEG_OUT_CLASS15_U8 = 1,  /* (B, H, W) u8 raw argmax class id (models.py:55)                    */
+    BUGSEG_OUT_CLASS3_U8 = 2,   /* (B, H, W) u8 in {0,1,2}: ENET.predict (models.py:55-58,67)         */
+    BUGSEG_OUT_BINARY_U8 = 3    /* (B, H, W) u8 in {0,1}:   ENET.predict_binary (models.py:78-81)     */
+};
+
+/* out_layout of bugseg_preprocess */
+enum {
+    BUGSEG_PRE_ENGINE = 0,      /* (B, H, W, 8) engine input, context precision                      */
+    BUGSEG_PRE_NCHW_F64 = 1,    /* (B, 3, H, W) f64: exactly ENET.preprocess's array (models.py:84-95) */
+    BUGSEG_PRE_NCHW_F32 = 2     /* (B, 3, H, W) f32: what TF casts the feed to                         */
+};
+
+/* Geometry of bev_transform_tools.create_occupancy_grid (bev.py:301-330), computed on the host
+ * by the Python shim exactly as the reference computes it. */
+typedef struct {
+    double M[9];        /* forward bev matrix, row-major (bev.py:175 _bev_matrix)                */
+    int in_rows;        /* segmap rows  (== "input image size"[0], assert at bev.py:304)        */
+    int in_cols;        /* segmap cols  (== "input image size"[1])                               */
+    int warp_w;         /* after_warp_width  (bev.py:313; dsize of warpPerspective, bev.py:317)  */
+    int warp_h;         /* after_warp_height (bev.py:314)                                        */
+    int occ_w_px;       /* bev.py:309 */
+    int occ_h_px;       /* bev.py:311 */
+    int occ_w;          /* bev.py:308 grid cells across */
+    int occ_h;          /* bev.py:310 grid cells down   */
+    int left_x;         /* bev.py:318 */
+    int top_y;          /* bev.py:319 */
+    int ros_layout;     /* 0: reference (occ_h, occ_w) grid; 1: ROS data order = flip(0)+rot90ccw
+                           of it, (occ_w, occ_h) row-major (occgrid_to_ros.py:18-25)            */
+} bugseg_bev_params;
+
+/* Library version (major*10000 + minor*100 + patch). */
+int bugseg_version(void);
+
+/* Create / destroy a context on HIP device `device`, computing in `precision` (BUGSEG_FP32 is the
+ * parity mode: logits within 1e-3 of the fp32 oracle; BUGSEG_BF16 the throughput mode).
+ * Replaces ENET.__init__'s tf.compat.v1.Session() (models.py:21-22). */
+int bugseg_create(int device, int precision, bugseg_ctx **out);
+int bugseg_destroy(bugseg_ctx *ctx);
+
+/* Load a BSG1 weight blob (format: bugcar_image_segmentation_amd/enet_spec.py) from HOST memory;
+ * folds batch-norm, packs weights for the MFMA kernels and uploads them.
+ * Replaces GFile(...).read() + GraphDef.ParseFromString + import_graph_def (models.py:25-30). */
+int bugseg_load_weights(bugseg_ctx *ctx, const void *blob, size_t bytes);
+
+/* Number of classes of the loaded model (0 before load). */
+int bugseg_num_classes(const bugseg_ctx *ctx);
+
+/* Bytes of the engine-input tensor for (B, H, W) in the context precision. */
+size_t bugseg_input_bytes(const bugseg_ctx *ctx, int B, int H, int W);
+
+/* ENET.preprocess (models.py:84-95) on a batch: BGR u8 (B, H0, W0, 3) -> resize to (H, W)
+ * (cv2.resize INTER_LINEAR fixed point; identity when equal) -> BGR->RGB -> (x/256-mean)/std.
+ * out_layout: BUGSEG_PRE_*. */
+int bugseg_preprocess(bugseg_ctx *ctx, const uint8_t *bgr_dev, int B, int H0, int W0, int H, int W,
+                      int out_layout, void *out_dev, void *stream);
+
+/* (B, 3, H, W) NCHW float (is_f64 ? f64 : f32) -> engine input (B, H, W, 8). This is the feed of
+ * ENET.predict's sess.run (models.py:43-44), which receives ENET.preprocess's NCHW array. */
+int bugseg_nchw_to_input(bugseg_ctx *ctx, const void *x_dev, int is_f64, int B, int H, int W,
+                         void *out_dev, void *stream);
+
+/* ENet forward + fused argmax/remap epilogue. in_dev: engine input (B, H, W, 8); H and W must be
+ * multiples of 8. out_kind: BUGSEG_OUT_*. Replaces sess.run + tf.math.argmax + tf.where
+ * (models.py:43-58, 71-80). */
+int bugseg_enet_forward(bugseg_ctx *ctx, const void *in_dev, int B, int H, int W, int out_kind,
+                        void *out_dev, void *stream);
+
+/* Fused BEV rasteriser over a batch of class maps: seg_dev (B, in_rows, in_cols) u8 in {0,1,2}
+ * -> out_dev (B, occ_h, occ_w) int8 in {-1, 0, 100} (or the ROS layout, see ros_layout).
+ * Replaces bev_transform_tools.create_occupancy_grid, non-laserscan branch (bev.py:301-381). */
+int bugseg_bev_occgrid(bugseg_ctx *ctx, const uint8_t *seg_dev, int B, const bugseg_bev_params *p,
+                       int8_t *out_dev, void *stream);
+
+/* Plan introspection for the bench / roofline: number of kernel launches of one forward and the
+ * algorithmic bytes they move (activation reads + writes + weights, context precision). */
+int bugseg_plan_info(bugseg_ctx *ctx, int B, int H, int W, int out_kind, int *n_launches,
+                     double *alg_bytes, double *flops);
+
+/* Last error message of ctx (or of the calling thread when ctx is NULL). Never NULL. */
+const char *bugseg_last_error(const bugseg_ctx *ctx);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* BUGSEG_H */

@@ -1,0 +1,196 @@
+"""ORACLE — TEST INFRASTRUCTURE ONLY (never imported by the product package).
+
+NumPy restatement of the OpenCV 4.x primitives on the reference hot path, written
+independently of ``ocv_ref.c`` so the two restatements cross-check each other, and a
+restatement of ``bev_transform_tools.create_occupancy_grid`` that follows the reference's
+own array flow (full warped image, then the crop/pad slicing of bev.py:318-330) rather than
+the coordinate-shift form the C oracle and the HIP kernel use.
+
+Parity status: UNPINNED against OpenCV/TensorFlow (neither is installed, the reference holds
+no fixtures). Semantics pinned to the classic OpenCV 4.x fixed-point paths,
+see ocv_ref.c's header.
+"""
+from __future__ import annotations
+
+import numpy as np
+
+INTER_BITS = 5
+INTER_TAB_SIZE = 1 << INTER_BITS
+
+
+def invert3x3(M: np.ndarray) -> np.ndarray:
+    """cv::invert DECOMP_LU closed-form 3x3 branch (used by warpPerspective, bev.py:317)."""
+    S = np.asarray(M, dtype=np.float64).reshape(3, 3)
+    d = (S[0, 0] * (S[1, 1] * S[2, 2] - S[1, 2] * S[2, 1])
+         - S[0, 1] * (S[1, 0] * S[2, 2] - S[1, 2] * S[2, 0])
+         + S[0, 2] * (S[1, 0] * S[2, 1] - S[1, 1] * S[2, 0]))
+    if d == 0.0:
+        return np.zeros((3, 3))
+    d = 1.0 / d
+    t = np.empty(9)
+    t[0] = (S[1, 1] * S[2, 2] - S[1, 2] * S[2, 1]) * d
+    t[1] = (S[0, 2] * S[2, 1] - S[0, 1] * S[2, 2]) * d
+    t[2] = (S[0, 1] * S[1, 2] - S[0, 2] * S[1, 1]) * d
+    t[3] = (S[1, 2] * S[2, 0] - S[1, 0] * S[2, 2]) * d
+    t[4] = (S[0, 0] * S[2, 2] - S[0, 2] * S[2, 0]) * d
+    t[5] = (S[0, 2] * S[1, 0] - S[0, 0] * S[1, 2]) * d
+    t[6] = (S[1, 0] * S[2, 1] - S[1, 1] * S[2, 0]) * d
+    t[7] = (S[0, 1] * S[2, 0] - S[0, 0] * S[2, 1]) * d
+    t[8] = (S[0, 0] * S[1, 1] - S[0, 1] * S[1, 0]) * d
+    return t.reshape(3, 3)
+
+
+def warp_perspective(src: np.ndarray, M: np.ndarray, dsize: tuple[int, int]) -> np.ndarray:
+    """cv2.warpPerspective(src u8 1ch, M, dsize=(w, h)), INTER_LINEAR, BORDER_CONSTANT 0.
+
+    WarpPerspectiveInvoker forms X0/Y0/W0 at each block start xb (block width
+    bw0 = min(1024 // min(16, h), w)) and adds M0*x1 inside the block; remapBilinear
+    interpolates with the Q15 table indexed by the 5-bit fractions."""
+    dw, dh = dsize
+    sh, sw = src.shape
+    Mi = invert3x3(M).ravel()
+    bh0 = min(16, dh)
+    bw0 = min(1024 // bh0, dw)
+    ys, xs = np.meshgrid(np.arange(dh), np.arange(dw), indexing="ij")
+    xb = (xs // bw0) * bw0
+    x1 = (xs - xb).astype(np.float64)
+    xb = xb.astype(np.float64)
+    yd = ys.astype(np.float64)
+    X0 = Mi[0] * xb + Mi[1] * yd + Mi[2]
+    Y0 = Mi[3] * xb + Mi[4] * yd + Mi[5]
+    W0 = Mi[6] * xb + Mi[7] * yd + Mi[8]
+    W = W0 + Mi[6] * x1
+    with np.errstate(divide="ignore"):
+        W = np.where(W != 0.0, INTER_TAB_SIZE / np.where(W != 0.0, W, 1.0), 0.0)
+    fX = np.clip((X0 + Mi[0] * x1) * W, -2147483648.0, 2147483647.0)
+    fY = np.clip((Y0 + Mi[3] * x1) * W, -2147483648.0, 2147483647.0)
+    X = np.rint(fX).astype(np.int64)          # np.rint: round half to even == cvRound
+    Y = np.rint(fY).astype(np.int64)
+    sx = np.clip(X >> INTER_BITS, -32768, 32767)
+    sy = np.clip(Y >> INTER_BITS, -32768, 32767)
+    ax = X & (INTER_TAB_SIZE - 1)
+    ay = Y & (INTER_TAB_SIZE - 1)
+    src_i = src.astype(np.int64)
+
+    def tap(yy, xx):
+        ok = (yy >= 0) & (yy < sh) & (xx >= 0) & (xx < sw)
+        return np.where(ok, src_i[np.clip(yy, 0, sh - 1), np.clip(xx, 0, sw - 1)], 0)
+
+    acc = (tap(sy, sx) * (32 - ax) * (32 - ay) + tap(sy, sx + 1) * ax * (32 - ay)
+           + tap(sy + 1, sx) * (32 - ax) * ay + tap(sy + 1, sx + 1) * ax * ay) * 32
+    return np.clip((acc + (1 << 14)) >> 15, 0, 255).astype(np.uint8)
+
+
+def resize_nearest(src: np.ndarray, dsize: tuple[int, int]) -> np.ndarray:
+    """cv2.resize(..., INTER_NEAREST) (resizeNN): floor(d * (1/(dw/sw))), clamped."""
+    dw, dh = dsize
+    sh, sw = src.shape[:2]
+    ifx = 1.0 / (dw / sw)
+    ify = 1.0 / (dh / sh)
+    sx = np.minimum(np.floor(np.arange(dw) * ifx).astype(np.int64), sw - 1)
+    sy = np.minimum(np.floor(np.arange(dh) * ify).astype(np.int64), sh - 1)
+    return src[sy][:, sx]
+
+
+def morph_open3x3(src: np.ndarray) -> np.ndarray:
+    """cv2.morphologyEx(src, MORPH_OPEN, ones((3,3))) with the default border values."""
+    h, w = src.shape
+    big = np.full((h + 2, w + 2), 255, dtype=np.uint8)
+    big[1:-1, 1:-1] = src
+    er = np.full((h, w), 255, dtype=np.uint8)
+    for dy in range(3):
+        for dx in range(3):
+            er = np.minimum(er, big[dy:dy + h, dx:dx + w])
+    big = np.zeros((h + 2, w + 2), dtype=np.uint8)
+    big[1:-1, 1:-1] = er
+    di = np.zeros((h, w), dtype=np.uint8)
+    for dy in range(3):
+        for dx in range(3):
+            di = np.maximum(di, big[dy:dy + h, dx:dx + w])
+    return di
+
+
+def _linear_coeffs(dsize: int, ssize: int, scale: float):
+    d = np.arange(dsize)
+    f = ((d + 0.5) * scale - 0.5).astype(np.float32)
+    s = np.floor(f).astype(np.int64)
+    f = (f - s.astype(np.float32)).astype(np.float32)
+    lo = s < 0
+    f[lo] = 0.0
+    s[lo] = 0
+    hi = s >= ssize - 1
+    f[hi] = 0.0
+    s[hi] = ssize - 1
+    a0 = np.clip(np.rint((np.float32(1.0) - f) * np.float32(2048.0)), -32768, 32767).astype(np.int64)
+    a1 = np.clip(np.rint(f * np.float32(2048.0)), -32768, 32767).astype(np.int64)
+    return s, a0, a1
+
+
+def resize_linear(src: np.ndarray, dsize: tuple[int, int]) -> np.ndarray:
+    """cv2.resize(src u8 HxWxC, dsize) default INTER_LINEAR, classic fixed point (see ocv_ref.c)."""
+    dw, dh = dsize
+    sh, sw = src.shape[:2]
+    cn = 1 if src.ndim == 2 else src.shape[2]
+    if (sh, sw) == (dh, dw):
+        return src.copy()
+    s3 = src.reshape(sh, sw, cn).astype(np.int64)
+    scale_x = 1.0 / (dw / sw)
+    scale_y = 1.0 / (dh / sh)
+    isx, isy = int(np.rint(scale_x)), int(np.rint(scale_y))
+    eps = np.finfo(np.float64).eps
+    if abs(scale_x - isx) < eps and abs(scale_y - isy) < eps and isx == 2 and isy == 2:
+        v = s3[0:2 * dh:2, 0:2 * dw:2] + s3[0:2 * dh:2, 1:2 * dw:2] + s3[1:2 * dh:2, 0:2 * dw:2] + s3[1:2 * dh:2, 1:2 * dw:2]
+        out = ((v + 2) >> 2).astype(np.uint8)
+        return out[..., 0] if src.ndim == 2 else out
+    xo, xa0, xa1 = _linear_coeffs(dw, sw, scale_x)
+    yo, yb0, yb1 = _linear_coeffs(dh, sh, scale_y)
+    xo1 = np.minimum(xo + 1, sw - 1)
+    hrow = s3[:, xo, :] * xa0[None, :, None] + s3[:, xo1, :] * xa1[None, :, None]   # (sh, dw, cn)
+    r0 = hrow[yo].reshape(dh, dw * cn)
+    r1 = hrow[np.minimum(yo + 1, sh - 1)].reshape(dh, dw * cn)
+    b0 = yb0[:, None]
+    b1 = yb1[:, None]
+    width = dw * cn
+    vec_end = width - (width % 8)
+    s0 = np.clip(r0 >> 4, -32768, 32767)
+    s1 = np.clip(r1 >> 4, -32768, 32767)
+    vec = (((s0 * b0) >> 16) + ((s1 * b1) >> 16) + 2) >> 2
+    sca = (r0 * b0 + r1 * b1 + (1 << 21)) >> 22
+    out = np.where(np.arange(width)[None, :] < vec_end, vec, sca)
+    out = np.clip(out, 0, 255).astype(np.uint8).reshape(dh, dw, cn)
+    return out[..., 0] if src.ndim == 2 else out
+
+
+def create_occupancy_grid(segmap: np.ndarray, M: np.ndarray, after_warp_w: int, after_warp_h: int,
+                          cm_per_px: float, grid_w_m: float, grid_h_m: float, cell_m: float) -> np.ndarray:
+    """Restates bev.py:301-381 (non-laserscan branch) step by step on the arrays it builds."""
+    cell_px = cell_m * 100 / cm_per_px                                   # bev.py:307
+    occ_w = int(grid_w_m / cell_m)                                       # bev.py:308
+    occ_w_px = int(occ_w * cell_px)                                      # bev.py:309
+    occ_h = int(grid_h_m / cell_m)                                       # bev.py:310
+    occ_h_px = int(occ_h * cell_px)                                      # bev.py:311
+    lifted = np.add(segmap, 1).astype(np.uint8)                          # bev.py:312
+    warped = warp_perspective(lifted, M, (after_warp_w, after_warp_h))   # bev.py:317
+    left_x = int((after_warp_w - occ_w_px) / 2)                          # bev.py:318
+    top_y = after_warp_h - occ_h_px                                      # bev.py:319
+    wlx = int(np.clip(left_x, 0, np.inf))                                # bev.py:320
+    warped = warped[int(np.clip(top_y, 0, np.inf)):after_warp_h, wlx:wlx + occ_w_px]   # bev.py:321
+    glx = int(np.clip(-left_x, 0, np.inf))                               # bev.py:323
+    gty = int(np.clip(-top_y, 0, np.inf))                                # bev.py:324
+    tmpl = np.zeros((occ_h_px, occ_w_px))                                # bev.py:325
+    tmpl[gty:occ_h_px, glx:glx + warped.shape[1]] = warped               # bev.py:327
+    tmpl = tmpl.astype(np.uint8)                                         # bev.py:330
+    occ = np.logical_or(tmpl == 1, tmpl == 3).astype(np.uint8)           # bev.py:331
+    opened = morph_open3x3(occ)                                          # bev.py:333
+    mask1 = (opened > 0).astype(np.uint8)                                # bev.py:338
+    sub = np.clip(occ.astype(np.int16) - mask1, 0, 255)                  # bev.py:339 cv2.subtract saturates
+    tmpl = np.where(sub > 0, 2, tmpl).astype(np.uint8)                   # bev.py:340
+    tmpl = resize_nearest(tmpl, (occ_w, occ_h))                          # bev.py:344
+    new = np.where(tmpl == 3, 1, tmpl)                                   # bev.py:377
+    return np.where(new == 0, -1, 200 - new.astype(np.int64) * 100).astype(np.int8)   # bev.py:379
+
+
+def ros_layout(grid: np.ndarray) -> np.ndarray:
+    """cv2.flip(g, 0) then cv2.rotate(ROTATE_90_COUNTERCLOCKWISE) (occgrid_to_ros.py:18,21)."""
+    flipped = grid[::-1, :]
+    return np.ascontiguousarray(np.rot90(flipped, 1))

@@ -1,0 +1,279 @@
+/*
+ * ORACLE — TEST INFRASTRUCTURE ONLY.
+ *
+ * Plain-C restatement of the OpenCV 4.x primitives the reference's hot path calls, plus the
+ * reference's occupancy-grid rasteriser built on them. Only tests/, __graft_entry__.smoke()
+ * and bench.py's cpu_baseline leg may load this library, and only as the checker / CPU
+ * baseline. The product path (bugcar_image_segmentation_amd) never links or calls it.
+ *
+ * Parity status: UNPINNED against the real reference. OpenCV is absent from this image and
+ * the reference ships no golden vectors. The semantics restated here are
+ * the classic OpenCV 4.x fixed-point paths (imgwarp.cpp / resize.cpp / morph.cpp of the
+ * 4.2-4.10 series, the opencv-python wheels that accompanied TF 2.2; requirements.txt:1
+ * leaves opencv-python unpinned). OpenCV >= 4.11 replaced warpPerspective with a float
+ * implementation and is NOT what this pins.
+ *
+ * Build: cc -O2 -ffp-contract=off -fPIC -shared (x86-64 SSE2 doubles, no FMA contraction),
+ * so the double arithmetic is the IEEE evaluation order written below.
+ */
+#include <stdint.h>
+#include <string.h>
+#include <math.h>
+#include <limits.h>
+#include <stdlib.h>
+
+static inline int imin(int a, int b) { return a < b ? a : b; }
+static inline int imax(int a, int b) { return a > b ? a : b; }
+static inline int cv_round(double v) { return (int)lrint(v); }          /* round half to even */
+static inline int sat_short(int v) { return v < -32768 ? -32768 : (v > 32767 ? 32767 : v); }
+static inline uint8_t sat_u8(int v) { return (uint8_t)(v < 0 ? 0 : (v > 255 ? 255 : v)); }
+
+/* cv::invert(M, M) with the default DECOMP_LU: the closed-form 3x3 double branch of
+ * lapack.cpp (det3 + cofactors * 1/det). Used by warpPerspective without WARP_INVERSE_MAP
+ * (bev.py:317 passes the forward bev matrix). Returns 0 when det == 0 (OpenCV zeroes M). */
+int ocv_invert3x3(const double *S, double *t)
+{
+#define m(i, j) S[(i) * 3 + (j)]
+    double d = m(0, 0) * (m(1, 1) * m(2, 2) - m(1, 2) * m(2, 1)) -
+               m(0, 1) * (m(1, 0) * m(2, 2) - m(1, 2) * m(2, 0)) +
+               m(0, 2) * (m(1, 0) * m(2, 1) - m(1, 1) * m(2, 0));
+    if (d == 0.0) {
+        memset(t, 0, 9 * sizeof(double));
+        return 0;
+    }
+    d = 1.0 / d;
+    t[0] = (m(1, 1) * m(2, 2) - m(1, 2) * m(2, 1)) * d;
+    t[1] = (m(0, 2) * m(2, 1) - m(0, 1) * m(2, 2)) * d;
+    t[2] = (m(0, 1) * m(1, 2) - m(0, 2) * m(1, 1)) * d;
+    t[3] = (m(1, 2) * m(2, 0) - m(1, 0) * m(2, 2)) * d;
+    t[4] = (m(0, 0) * m(2, 2) - m(0, 2) * m(2, 0)) * d;
+    t[5] = (m(0, 2) * m(1, 0) - m(0, 0) * m(1, 2)) * d;
+    t[6] = (m(1, 0) * m(2, 1) - m(1, 1) * m(2, 0)) * d;
+    t[7] = (m(0, 1) * m(2, 0) - m(0, 0) * m(2, 1)) * d;
+    t[8] = (m(0, 0) * m(1, 1) - m(0, 1) * m(1, 0)) * d;
+#undef m
+    return 1;
+}
+
+/* One destination pixel of warpPerspective(INTER_LINEAR, BORDER_CONSTANT 0) on a 1-channel
+ * u8 image. Mi is the INVERSE map. The x coordinate is evaluated relative to the start of
+ * its 32x32-pixel-budget block (WarpPerspectiveInvoker: bh0 = min(16,H), bw0 = min(1024/bh0,W)),
+ * because OpenCV forms X0 = M0*xb + M1*y + M2 once per block row and then adds M0*x1; the
+ * rounding of that split is part of the result. Coordinates: saturate_cast<int>(fX*32/W)
+ * (cvRound, half-even), integer part X>>5 saturated to short, 5-bit fraction indexes the
+ * Q15 bilinear table; taps outside the source read the border value 0 (remapBilinear). */
+static inline uint8_t warp_px(const uint8_t *src, int sh, int sw, const double *Mi, int x, int y, int bw0)
+{
+    int xb = (x / bw0) * bw0, x1 = x - xb;
+    double X0 = Mi[0] * xb + Mi[1] * y + Mi[2];
+    double Y0 = Mi[3] * xb + Mi[4] * y + Mi[5];
+    double W0 = Mi[6] * xb + Mi[7] * y + Mi[8];
+    double W = W0 + Mi[6] * x1;
+    W = W != 0.0 ? 32.0 / W : 0.0;
+    double fX = (X0 + Mi[0] * x1) * W;
+    double fY = (Y0 + Mi[3] * x1) * W;
+    fX = fX < (double)INT_MIN ? (double)INT_MIN : (fX > (double)INT_MAX ? (double)INT_MAX : fX);
+    fY = fY < (double)INT_MIN ? (double)INT_MIN : (fY > (double)INT_MAX ? (double)INT_MAX : fY);
+    int X = cv_round(fX), Y = cv_round(fY);
+    int sx = sat_short(X >> 5), sy = sat_short(Y >> 5);
+    int ax = X & 31, ay = Y & 31;
+    int w0 = (32 - ax) * (32 - ay), w1 = ax * (32 - ay), w2 = (32 - ax) * ay, w3 = ax * ay;
+    int v0 = 0, v1 = 0, v2 = 0, v3 = 0;
+    int x0ok = (unsigned)sx < (unsigned)sw, x1ok = (unsigned)(sx + 1) < (unsigned)sw;
+    int y0ok = (unsigned)sy < (unsigned)sh, y1ok = (unsigned)(sy + 1) < (unsigned)sh;
+    if (y0ok) {
+        if (x0ok) v0 = src[(size_t)sy * sw + sx];
+        if (x1ok) v1 = src[(size_t)sy * sw + sx + 1];
+    }
+    if (y1ok) {
+        if (x0ok) v2 = src[(size_t)(sy + 1) * sw + sx];
+        if (x1ok) v3 = src[(size_t)(sy + 1) * sw + sx + 1];
+    }
+    int acc = (v0 * w0 + v1 * w1 + v2 * w2 + v3 * w3) * 32;   /* weights in Q15 sum to 32768 */
+    return sat_u8((acc + (1 << 14)) >> 15);
+}
+
+static inline int warp_bw0(int dh, int dw)
+{
+    int bh0 = imin(16, dh);
+    return imin(1024 / bh0, dw);
+}
+
+/* cv2.warpPerspective(src, M, (dw, dh)) with default flags; M is the FORWARD matrix. */
+int ocv_warp_perspective_u8(const uint8_t *src, int sh, int sw, uint8_t *dst, int dh, int dw, const double *M)
+{
+    double Mi[9];
+    ocv_invert3x3(M, Mi);
+    int bw0 = warp_bw0(dh, dw);
+    for (int y = 0; y < dh; y++)
+        for (int x = 0; x < dw; x++)
+            dst[(size_t)y * dw + x] = warp_px(src, sh, sw, Mi, x, y, bw0);
+    return 0;
+}
+
+/* cv2.resize(src, (dw, dh), interpolation=INTER_NEAREST) (resizeNN): sx = min(floor(x*ifx), sw-1)
+ * with ifx = 1/(dw/sw) in double. */
+int ocv_resize_nearest_u8(const uint8_t *src, int sh, int sw, int cn, uint8_t *dst, int dh, int dw)
+{
+    double ifx = 1.0 / ((double)dw / sw), ify = 1.0 / ((double)dh / sh);
+    for (int y = 0; y < dh; y++) {
+        int sy = imin((int)floor(y * ify), sh - 1);
+        for (int x = 0; x < dw; x++) {
+            int sx = imin((int)floor(x * ifx), sw - 1);
+            for (int c = 0; c < cn; c++)
+                dst[((size_t)y * dw + x) * cn + c] = src[((size_t)sy * sw + sx) * cn + c];
+        }
+    }
+    return 0;
+}
+
+/* cv2.morphologyEx(src, MORPH_OPEN, ones(3,3)): erode then dilate, each with the default
+ * morphology border (+inf for erode, -inf for dilate), i.e. out-of-image taps are ignored. */
+int ocv_morph_open3x3_u8(const uint8_t *src, int h, int w, uint8_t *dst)
+{
+    uint8_t *tmp = (uint8_t *)malloc((size_t)h * w);
+    if (!tmp) return -1;
+    for (int y = 0; y < h; y++)
+        for (int x = 0; x < w; x++) {
+            int v = 255;
+            for (int dy = -1; dy <= 1; dy++)
+                for (int dx = -1; dx <= 1; dx++) {
+                    int yy = y + dy, xx = x + dx;
+                    if (yy >= 0 && yy < h && xx >= 0 && xx < w) v = imin(v, src[(size_t)yy * w + xx]);
+                }
+            tmp[(size_t)y * w + x] = (uint8_t)v;
+        }
+    for (int y = 0; y < h; y++)
+        for (int x = 0; x < w; x++) {
+            int v = 0;
+            for (int dy = -1; dy <= 1; dy++)
+                for (int dx = -1; dx <= 1; dx++) {
+                    int yy = y + dy, xx = x + dx;
+                    if (yy >= 0 && yy < h && xx >= 0 && xx < w) v = imax(v, tmp[(size_t)yy * w + xx]);
+                }
+            dst[(size_t)y * w + x] = (uint8_t)v;
+        }
+    free(tmp);
+    return 0;
+}
+
+/* cv2.resize(src, (dw, dh)) with the default INTER_LINEAR on u8 (models.py:87), classic
+ * resizeGeneric_ fixed point: per-axis float coefficients fx = (float)((d+0.5)*scale-0.5),
+ * clamped at both edges, quantised to Q11 (saturate_cast<short>(c*2048)); horizontal pass
+ * exact in int; vertical pass as VResizeLinearVec_32s8u (128-bit universal intrinsics):
+ * ((S0>>4)*b0>>16) + ((S1>>4)*b1>>16), then (v+2)>>2 saturated — applied to every element
+ * of the row except a tail of fewer than 8 elements, which takes the scalar
+ * FixedPtCast<int,uchar,22> ((v + 2^21) >> 22). Exact 2x downscale is routed to INTER_AREA
+ * (resize.cpp: "INTER_AREA (fast) also is equal to INTER_LINEAR"), equal size is a copy. */
+static void linear_coeffs(int dsize, int ssize, double scale, int *ofs, short *a0, short *a1)
+{
+    for (int d = 0; d < dsize; d++) {
+        float f = (float)((d + 0.5) * scale - 0.5);
+        int s = (int)floorf(f);
+        f -= (float)s;
+        if (s < 0) { f = 0.f; s = 0; }
+        if (s >= ssize - 1) { f = 0.f; s = ssize - 1; }
+        ofs[d] = s;
+        a0[d] = (short)sat_short((int)lrintf((1.f - f) * 2048.f));
+        a1[d] = (short)sat_short((int)lrintf(f * 2048.f));
+    }
+}
+
+int ocv_resize_linear_u8(const uint8_t *src, int sh, int sw, int cn, uint8_t *dst, int dh, int dw)
+{
+    if (sh == dh && sw == dw) {
+        memcpy(dst, src, (size_t)sh * sw * cn);
+        return 0;
+    }
+    double inv_x = (double)dw / sw, inv_y = (double)dh / sh;
+    double scale_x = 1.0 / inv_x, scale_y = 1.0 / inv_y;
+    int isx = cv_round(scale_x), isy = cv_round(scale_y);
+    int area_fast = fabs(scale_x - isx) < 2.220446049250313e-16 && fabs(scale_y - isy) < 2.220446049250313e-16;
+    if (area_fast && isx == 2 && isy == 2) {
+        for (int y = 0; y < dh; y++)
+            for (int x = 0; x < dw; x++)
+                for (int c = 0; c < cn; c++) {
+                    const uint8_t *s = src + ((size_t)(2 * y) * sw + 2 * x) * cn + c;
+                    int v = s[0] + s[cn] + s[(size_t)sw * cn] + s[(size_t)sw * cn + cn];
+                    dst[((size_t)y * dw + x) * cn + c] = (uint8_t)((v + 2) >> 2);
+                }
+        return 0;
+    }
+    int *xo = (int *)malloc(sizeof(int) * dw), *yo = (int *)malloc(sizeof(int) * dh);
+    short *xa0 = (short *)malloc(sizeof(short) * dw), *xa1 = (short *)malloc(sizeof(short) * dw);
+    short *yb0 = (short *)malloc(sizeof(short) * dh), *yb1 = (short *)malloc(sizeof(short) * dh);
+    int *r0 = (int *)malloc(sizeof(int) * dw * cn), *r1 = (int *)malloc(sizeof(int) * dw * cn);
+    if (!xo || !yo || !xa0 || !xa1 || !yb0 || !yb1 || !r0 || !r1) return -1;
+    linear_coeffs(dw, sw, scale_x, xo, xa0, xa1);
+    linear_coeffs(dh, sh, scale_y, yo, yb0, yb1);
+    int width = dw * cn, vec_end = width - (width % 8);
+    for (int y = 0; y < dh; y++) {
+        int sy0 = yo[y], sy1 = imin(yo[y] + 1, sh - 1);
+        for (int k = 0; k < 2; k++) {
+            const uint8_t *row = src + (size_t)(k ? sy1 : sy0) * sw * cn;
+            int *r = k ? r1 : r0;
+            for (int x = 0; x < dw; x++)
+                for (int c = 0; c < cn; c++) {
+                    int sx = xo[x];
+                    int v = row[sx * cn + c] * xa0[x];
+                    if (xa1[x]) v += row[(sx + 1) * cn + c] * xa1[x];
+                    r[x * cn + c] = v;
+                }
+        }
+        int b0 = yb0[y], b1 = yb1[y];
+        uint8_t *d = dst + (size_t)y * width;
+        for (int x = 0; x < width; x++) {
+            if (x < vec_end) {
+                int s0 = sat_short(r0[x] >> 4), s1 = sat_short(r1[x] >> 4);
+                int v = ((s0 * b0) >> 16) + ((s1 * b1) >> 16);
+                d[x] = sat_u8((v + 2) >> 2);
+            } else {
+                d[x] = sat_u8((r0[x] * b0 + r1[x] * b1 + (1 << 21)) >> 22);
+            }
+        }
+    }
+    free(xo); free(yo); free(xa0); free(xa1); free(yb0); free(yb1); free(r0); free(r1);
+    return 0;
+}
+
+/* bev_transform_tools.create_occupancy_grid, non-laserscan branch (bev.py:301-381):
+ *   t  = warpPerspective(segmap + 1, M, (Wb, Hb))                     bev.py:312,317
+ *   template[ty][tx] = t[ty+top_y][tx+left_x] (0 outside)             bev.py:318-330
+ *   occ = (template==1)|(template==3); open 3x3; template[occ&!open]=2 bev.py:331-340
+ *   g = resize_nearest(template, (occ_w, occ_h))                      bev.py:344-347
+ *   g = where(g==3, 1, g); out = where(g==0, -1, 200-100*g) as int8    bev.py:377-380
+ * The crop/pad of bev.py:318-330 is restated as the equivalent coordinate shift.
+ * segmap is (hin, win) u8 class ids {0,1,2}; M is the forward bev matrix. */
+int bev_occgrid_ref(const uint8_t *segmap, int hin, int win, const double *M, int Wb, int Hb,
+                    int occ_w_px, int occ_h_px, int occ_w, int occ_h, int left_x, int top_y, int8_t *out)
+{
+    size_t n = (size_t)hin * win;
+    uint8_t *lifted = (uint8_t *)malloc(n);
+    uint8_t *tmpl = (uint8_t *)malloc((size_t)occ_h_px * occ_w_px);
+    uint8_t *occ = (uint8_t *)malloc((size_t)occ_h_px * occ_w_px);
+    uint8_t *opened = (uint8_t *)malloc((size_t)occ_h_px * occ_w_px);
+    uint8_t *cells = (uint8_t *)malloc((size_t)occ_h * occ_w);
+    if (!lifted || !tmpl || !occ || !opened || !cells) return -1;
+    for (size_t i = 0; i < n; i++) lifted[i] = (uint8_t)(segmap[i] + 1);
+    double Mi[9];
+    ocv_invert3x3(M, Mi);
+    int bw0 = warp_bw0(Hb, Wb);
+    for (int ty = 0; ty < occ_h_px; ty++)
+        for (int tx = 0; tx < occ_w_px; tx++) {
+            int wy = ty + top_y, wx = tx + left_x;
+            uint8_t v = 0;
+            if (wy >= 0 && wy < Hb && wx >= 0 && wx < Wb) v = warp_px(lifted, hin, win, Mi, wx, wy, bw0);
+            tmpl[(size_t)ty * occ_w_px + tx] = v;
+            occ[(size_t)ty * occ_w_px + tx] = (uint8_t)(v == 1 || v == 3);
+        }
+    ocv_morph_open3x3_u8(occ, occ_h_px, occ_w_px, opened);
+    for (size_t i = 0; i < (size_t)occ_h_px * occ_w_px; i++)
+        if (occ[i] && !opened[i]) tmpl[i] = 2;
+    ocv_resize_nearest_u8(tmpl, occ_h_px, occ_w_px, 1, cells, occ_h, occ_w);
+    for (size_t i = 0; i < (size_t)occ_h * occ_w; i++) {
+        int g = cells[i] == 3 ? 1 : cells[i];
+        out[i] = (int8_t)(g == 0 ? -1 : 200 - 100 * g);
+    }
+    free(lifted); free(tmpl); free(occ); free(opened); free(cells);
+    return 0;
+}

@@ -1,0 +1,177 @@
+"""The oracle itself (CPU only): the C and NumPy restatements of the OpenCV primitives agree, the
+known answers read off the reference hold, and the committed golden fixtures still reproduce.
+
+Parity of the oracle against the real reference is UNPINNED (no OpenCV, no TF, no enet.pb and no
+reference fixtures in this image — SURVEY.md §8(c)); what pins it here is (1) two independent
+restatements (ocv_ref.c follows OpenCV's code structure, ocv_np.py the reference's array flow) that
+must agree bit for bit, (2) known-answer tests derived from the reference source, and (3) the golden
+vectors in tests/golden (regression: they were produced by tests/golden/make_golden.py)."""
+from pathlib import Path
+
+import numpy as np
+import pytest
+import torch
+
+from bugcar_image_segmentation_amd import enet_spec, synthetic
+from oracle import enet_oracle as eo
+from oracle import ocv_c, ocv_np
+
+GOLDEN = Path(__file__).parent / "golden"
+
+
+# ---------------------------------------------------------------- known answers from the source
+def test_lut3_matches_models_py():
+    # models.py:56-58: {2, 9} -> 0; {0, 1} -> 1; everything else -> 2
+    expect = np.array([1 if c in (0, 1) else 0 if c in (2, 9) else 2 for c in range(15)], np.uint8)
+    assert np.array_equal(eo.LUT3, expect)
+    assert np.array_equal(eo.LUT_BINARY, np.array([1, 1] + [0] * 13, np.uint8))   # models.py:79-80
+
+
+def test_argmax_ties_lowest_index():
+    lo = np.zeros((1, 15, 1, 3), np.float32)
+    lo[0, [4, 7], 0, 0] = 5.0
+    lo[0, [0, 14], 0, 1] = 1.0
+    lo[0, :, 0, 2] = -1.0
+    assert eo.argmax_classes(lo).ravel().tolist() == [4, 0, 0]
+
+
+def test_encoding_non_laserscan():
+    # bev.py:377-380: template {0,1,2,3} -> where(t==3,1,t) -> {0:-1, 1:100, 2:0}
+    t = np.array([[0, 1, 2, 3]], np.uint8)
+    new = np.where(t == 3, 1, t)
+    out = np.where(new == 0, -1, 200 - new * 100).astype(np.int8)
+    assert out.tolist() == [[-1, 100, 0, 100]]
+
+
+def test_ros_layout_is_flip_rot90ccw():
+    g = np.arange(12, dtype=np.int8).reshape(3, 4)
+    assert np.array_equal(ocv_np.ros_layout(g), g[::-1, ::-1].T)
+    assert np.array_equal(ocv_np.ros_layout(g), np.rot90(np.flipud(g)))
+
+
+def test_normalize_uses_256_not_255():
+    lut = eo.normalize_lut()
+    assert lut[256 // 2, 0] == (128 / 256.0 - 0.485) / 0.229
+
+
+def test_invert3x3_closed_form():
+    M = synthetic.synthetic_bev()._bev_matrix
+    assert np.allclose(ocv_c.invert3x3(M), np.linalg.inv(M), rtol=1e-10, atol=1e-12)
+    assert np.array_equal(ocv_c.invert3x3(M), ocv_np.invert3x3(M))
+
+
+def test_warp_identity_is_copy():
+    src = np.random.default_rng(0).integers(0, 256, size=(40, 50), dtype=np.uint8)
+    out = ocv_c.warp_perspective(src, np.eye(3), (50, 40))
+    assert np.array_equal(out, src)
+
+
+def test_warp_half_pixel_shift_rounds():
+    # x' = x - 0.5: bilinear midpoint of columns (x-1, x); (a*16+b*16)*32 + 2^14 >> 15 = (a+b+1)//2
+    src = np.array([[0, 3, 1, 2]], np.uint8).repeat(3, 0)
+    M = np.array([[1, 0, 0.5], [0, 1, 0], [0, 0, 1]], np.float64)     # forward map: dst = src + 0.5
+    out = ocv_c.warp_perspective(src, M, (4, 3))
+    # dst x=0 samples src -0.5 -> taps (-1: border 0, 0: 0); x=1 -> (0,3) -> 2; x=2 -> (3,1) -> 2; x=3 -> (1,2) -> 2
+    assert out[1].tolist() == [0, 2, 2, 2]
+    assert np.array_equal(out, ocv_np.warp_perspective(src, M, (4, 3)))
+
+
+def test_morph_open_removes_specks_keeps_blocks():
+    a = np.zeros((10, 10), np.uint8)
+    a[1, 1] = 1            # isolated pixel
+    a[4:8, 4:8] = 1        # 4x4 block survives
+    a[0:3, 8] = 1          # 1-wide line
+    o = ocv_c.morph_open3x3(a)
+    assert o[1, 1] == 0 and o[4:8, 4:8].all() and not o[0:3, 8].any()
+    # image border does not erode (default border is +inf for erode)
+    b = np.ones((5, 5), np.uint8)
+    assert ocv_c.morph_open3x3(b).all()
+
+
+def test_resize_nearest_formula():
+    src = np.arange(1000 * 3, dtype=np.int64).reshape(1000, 3).astype(np.uint8)
+    out = ocv_c.resize_nearest(src, (3, 200))
+    assert np.array_equal(out, src[::5])
+
+
+# ---------------------------------------------------------------- C vs NumPy restatements
+@pytest.mark.parametrize("seed", range(4))
+def test_warp_c_vs_numpy(seed):
+    rng = np.random.default_rng(seed)
+    h, w = rng.integers(20, 90, size=2)
+    src = rng.integers(0, 4, size=(h, w)).astype(np.uint8)
+    bev = synthetic.synthetic_bev(h, w, 150, 120)
+    M = bev._bev_matrix @ np.array([[1, 0.01 * rng.normal(), 2 * rng.normal()], [0, 1, 2 * rng.normal()],
+                                    [1e-4 * rng.normal(), 0, 1]])
+    a = ocv_c.warp_perspective(src, M, (150, 120))
+    b = ocv_np.warp_perspective(src, M, (150, 120))
+    assert np.array_equal(a, b)
+
+
+@pytest.mark.parametrize("shape,dsize", [((512, 512), (512, 256)), ((480, 640), (512, 256)), ((100, 77), (51, 33)),
+                                         ((64, 64), (96, 128)), ((480, 640), (320, 240)), ((33, 35), (33, 35)),
+                                         ((20, 17), (13, 9))])
+def test_resize_linear_c_vs_numpy(shape, dsize):
+    src = np.random.default_rng(shape[0]).integers(0, 256, size=shape + (3,), dtype=np.uint8)
+    assert np.array_equal(ocv_c.resize_linear(src, dsize), ocv_np.resize_linear(src, dsize))
+
+
+@pytest.mark.parametrize("ww,wh,grid", [(1000, 1000, (10, 10, 0.05)), (900, 700, (10, 8, 0.05)),
+                                        (600, 1100, (7.3, 12.1, 0.07)), (400, 300, (12, 12, 0.05))])
+def test_occupancy_grid_c_vs_reference_flow(ww, wh, grid):
+    """ocv_ref.c's coordinate-shift form vs ocv_np's restatement of bev.py's crop/pad slicing."""
+    rng = np.random.default_rng(ww)
+    seg = np.kron(rng.integers(0, 3, size=(60, 80)), np.ones((8, 8), np.int64)).astype(np.uint8)
+    seg[rng.random(seg.shape) < 0.02] = 2
+    M = synthetic.synthetic_bev(480, 640, ww, wh)._bev_matrix
+    a = ocv_c.create_occupancy_grid(seg, M, ww, wh, 1.0, *grid)
+    b = ocv_np.create_occupancy_grid(seg, M, ww, wh, 1.0, *grid)
+    assert np.array_equal(a, b)
+    assert set(np.unique(a)) <= {-1, 0, 100}
+
+
+def test_oracle_fp32_vs_fp64(blocks):
+    x = np.random.default_rng(5).normal(size=(1, 3, 32, 48)).astype(np.float32)
+    a = eo.forward(blocks, x, torch.float32)
+    b = eo.forward(blocks, x, torch.float64)
+    assert np.abs(a - b).max() < 1e-4
+
+
+def test_synthetic_weights_deterministic():
+    a = enet_spec.serialize(enet_spec.build_enet())
+    b = enet_spec.serialize(enet_spec.build_enet())
+    assert a == b and a[:4] == b"BSG1"
+
+
+# ---------------------------------------------------------------- golden vectors (regression)
+def _golden(name):
+    p = GOLDEN / name
+    if not p.exists():
+        pytest.fail(f"missing golden fixture {p}: run tests/golden/make_golden.py")
+    return np.load(p, allow_pickle=False)
+
+
+def test_golden_warp_and_occgrid():
+    g = _golden("bev_cases.npz")
+    for i in range(int(g["n"])):
+        seg, M = g[f"seg{i}"], g[f"M{i}"]
+        ww, wh = (int(v) for v in g[f"warp{i}"])
+        grid = tuple(float(v) for v in g[f"grid{i}"])
+        assert np.array_equal(ocv_c.warp_perspective(seg + 1, M, (ww, wh)), g[f"warped{i}"])
+        assert np.array_equal(ocv_c.create_occupancy_grid(seg, M, ww, wh, 1.0, *grid), g[f"occ{i}"])
+
+
+def test_golden_resize():
+    g = _golden("resize_cases.npz")
+    for i in range(int(g["n"])):
+        src = g[f"src{i}"]
+        dh, dw = (int(v) for v in g[f"dsize{i}"])
+        assert np.array_equal(ocv_c.resize_linear(src, (dw, dh)), g[f"out{i}"])
+        assert np.array_equal(eo.preprocess(src, dw, dh), g[f"pre{i}"])
+
+
+def test_golden_enet(blocks):
+    g = _golden("enet_small.npz")
+    logits = eo.forward(blocks, g["x"], torch.float64)
+    assert np.abs(logits - g["logits"]).max() < 1e-9
+    assert np.array_equal(eo.LUT3[eo.argmax_classes(logits)], g["cls3"])
