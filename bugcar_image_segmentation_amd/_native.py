@@ -19,10 +19,11 @@ LIB_PATH = Path(os.environ.get("BUGSEG_LIB", _PKG / "libbugseg.so"))
 OK, EINVAL, ENOMEM, EHIP, EFORMAT, ESTATE = 0, -1, -2, -3, -4, -5
 FP32, BF16 = 0, 1
 OUT_LOGITS_F32, OUT_CLASS15_U8, OUT_CLASS3_U8, OUT_BINARY_U8 = 0, 1, 2, 3
-PRE_ENGINE, PRE_NCHW_F64, PRE_NCHW_F32 = 0, 1, 2
+PRE_ENGINE, PRE_NCHW_F64, PRE_NCHW_F32, PRE_BGR_U8 = 0, 1, 2, 3
 
 EXPORTED = ("bugseg_version", "bugseg_create", "bugseg_destroy", "bugseg_load_weights", "bugseg_num_classes",
             "bugseg_input_bytes", "bugseg_preprocess", "bugseg_nchw_to_input", "bugseg_enet_forward",
+            "bugseg_enet_forward_bgr",
             "bugseg_bev_occgrid", "bugseg_plan_info", "bugseg_last_error")
 
 
@@ -65,8 +66,9 @@ def load_library(path: Path | str | None = None) -> ctypes.CDLL:
             "bugseg_preprocess": (i, [vp, vp, i, i, i, i, i, i, vp, vp]),
             "bugseg_nchw_to_input": (i, [vp, vp, i, i, i, i, vp, vp]),
             "bugseg_enet_forward": (i, [vp, vp, i, i, i, i, vp, vp]),
+            "bugseg_enet_forward_bgr": (i, [vp, vp, i, i, i, i, vp, vp]),
             "bugseg_bev_occgrid": (i, [vp, vp, i, ctypes.POINTER(BevParams), vp, vp]),
-            "bugseg_plan_info": (i, [vp, i, i, i, i, ctypes.POINTER(i), ctypes.POINTER(ctypes.c_double),
+            "bugseg_plan_info": (i, [vp, i, i, i, i, i, ctypes.POINTER(i), ctypes.POINTER(ctypes.c_double),
                                      ctypes.POINTER(ctypes.c_double)]),
             "bugseg_last_error": (cp, [vp]),
         }
@@ -143,15 +145,19 @@ class Context:
         check(self.lib.bugseg_enet_forward(self.h, x.data_ptr(), B, H, W, out_kind, out.data_ptr(),
                                            stream_handle(stream)), self.h)
 
+    def forward_bgr(self, bgr, B, H, W, out_kind, out, stream=None):
+        check(self.lib.bugseg_enet_forward_bgr(self.h, bgr.data_ptr(), B, H, W, out_kind, out.data_ptr(),
+                                               stream_handle(stream)), self.h)
+
     def bev(self, seg, B, params: BevParams, out, stream=None):
         check(self.lib.bugseg_bev_occgrid(self.h, seg.data_ptr(), B, ctypes.byref(params), out.data_ptr(),
                                           stream_handle(stream)), self.h)
 
-    def plan_info(self, B, H, W, out_kind):
+    def plan_info(self, B, H, W, out_kind, bgr_input=False):
         n = ctypes.c_int()
         by = ctypes.c_double()
         fl = ctypes.c_double()
-        check(self.lib.bugseg_plan_info(self.h, B, H, W, out_kind, ctypes.byref(n), ctypes.byref(by),
+        check(self.lib.bugseg_plan_info(self.h, B, H, W, out_kind, int(bool(bgr_input)), ctypes.byref(n), ctypes.byref(by),
                                         ctypes.byref(fl)), self.h)
         return n.value, by.value, fl.value
 

@@ -67,10 +67,17 @@ __device__ __forceinline__ int tmpl_value(const BevArgs &a, const uint8_t *seg, 
     return warp_value(a, seg, wx, wy);
 }
 
-__device__ __forceinline__ bool occupied(const BevArgs &a, const uint8_t *seg, int tx, int ty) {
-    const int v = tmpl_value(a, seg, tx, ty);
-    return v == 1 || v == 3;
+// Occupancy bit of template pixel p + (dx, dy); pixels outside the template read 1 (neutral for the
+// erode: OpenCV's default erode border is +inf).
+__device__ __forceinline__ uint32_t occ_bit(const BevArgs &a, const uint8_t *seg, int tx, int ty, int dx, int dy) {
+    const int x = tx + dx, y = ty + dy;
+    if ((unsigned)x >= (unsigned)a.occ_w_px || (unsigned)y >= (unsigned)a.occ_h_px) return 1u;
+    const int v = tmpl_value(a, seg, x, y);
+    return (v == 1 || v == 3) ? 1u : 0u;
 }
+
+// bit index of offset (dx, dy) in the 5x5 window around p
+#define B5(dx, dy) (((dy) + 2) * 5 + ((dx) + 2))
 
 __global__ void __launch_bounds__(256) bev_occgrid_kernel(const BevArgs a) {
     const long cells = (long)a.occ_h * a.occ_w, total = cells * a.B;
@@ -85,23 +92,33 @@ __global__ void __launch_bounds__(256) bev_occgrid_kernel(const BevArgs a) {
         tx = tx < a.occ_w_px - 1 ? tx : a.occ_w_px - 1;
         int v = tmpl_value(a, seg, tx, ty);
         if (v == 1 || v == 3) {
-            // occ5[dy+2][dx+2]: occupancy of the 5x5 window around p; out-of-template taps are
-            // neutral for the erode (treated occupied) and never become dilate sources.
-            bool opened = false;
-            for (int qy = -1; qy <= 1 && !opened; ++qy)
-                for (int qx = -1; qx <= 1 && !opened; ++qx) {
-                    const int uy = ty + qy, ux = tx + qx;
-                    if ((unsigned)uy >= (unsigned)a.occ_h_px || (unsigned)ux >= (unsigned)a.occ_w_px) continue;
-                    bool all = true;
-                    for (int ry = -1; ry <= 1 && all; ++ry)
-                        for (int rx = -1; rx <= 1 && all; ++rx) {
-                            const int zy = uy + ry, zx = ux + rx;
-                            if ((unsigned)zy >= (unsigned)a.occ_h_px || (unsigned)zx >= (unsigned)a.occ_w_px) continue;
-                            if (zy == ty && zx == tx) continue;   // p itself is occupied
-                            all = occupied(a, seg, zx, zy);
-                        }
-                    opened = all;
-                }
+            // Opening at p = OR over q in N3(p) (inside the template) of AND over N3(q) of occupancy.
+            // Round 1: the 8 neighbours of p (independent gathers, issued together). If they are all
+            // occupied, q = p already survives the erode. Round 2 only for the rest: the 16-pixel ring.
+            uint32_t m = 1u << B5(0, 0);
+#pragma unroll
+            for (int dy = -1; dy <= 1; ++dy)
+#pragma unroll
+                for (int dx = -1; dx <= 1; ++dx)
+                    if (dx || dy) m |= occ_bit(a, seg, tx, ty, dx, dy) << B5(dx, dy);
+            const uint32_t inner = 0x739C0u;        // bits of the 3x3 around p: rows 1..3, cols 1..3
+            bool opened = (m & inner) == inner;
+            if (!opened) {
+#pragma unroll
+                for (int dy = -2; dy <= 2; ++dy)
+#pragma unroll
+                    for (int dx = -2; dx <= 2; ++dx)
+                        if (dx == -2 || dx == 2 || dy == -2 || dy == 2) m |= occ_bit(a, seg, tx, ty, dx, dy) << B5(dx, dy);
+#pragma unroll
+                for (int qy = -1; qy <= 1; ++qy)
+#pragma unroll
+                    for (int qx = -1; qx <= 1; ++qx) {
+                        const bool inside = (unsigned)(tx + qx) < (unsigned)a.occ_w_px && (unsigned)(ty + qy) < (unsigned)a.occ_h_px;
+                        const int sh = qy * 5 + qx;
+                        const uint32_t win = sh >= 0 ? inner << sh : inner >> -sh;   // 3x3 window centred at q
+                        opened |= inside && (m & win) == win;
+                    }
+            }
             if (!opened) v = 2;                  // isolated occupied pixel -> free (bev.py:339-340)
         }
         const int g = v == 3 ? 1 : v;            // bev.py:377

@@ -1,0 +1,327 @@
+// Fused ENet regular / dilated / asymmetric bottleneck in ONE launch.
+//
+//   t0  = act1(W1 . x + b1)            1x1 projection C -> I (= C/4)     over the tile + halo
+//   t1  = act2(W2 * t0 + b2)           3x3 (dilation d) or 5x1 then 1x5 over the tile
+//   out = act_out(act3(W3 . t1 + b3) + x)                                 1x1 expansion + residual
+//
+// Unfused, each 128-channel bottleneck moves ~1024 B/pixel through HBM (x read twice, three internal
+// tensors written and read); here x is read once (halo re-reads are L2 hits) and out written once:
+// 512 B/pixel in bf16. The internal tensors never leave LDS:
+//   * a 256-thread workgroup owns a TH x TW output tile of one frame; phase 1 computes t0 for the
+//     tile plus a halo of (ry, rx) pixels (zero outside the image: t0 is what the 3x3 zero-pads);
+//   * phase 2 accumulates its whole tile in registers, then (after a barrier) overwrites the t0
+//     region with t1, so one LDS region serves both (asymmetric: t0 -> t1a -> t1, same trick);
+//   * phase 3 streams 16-pixel fragments: MFMA with W3, residual from global (just read, L2/L1),
+//     activation, 8-byte NHWC stores.
+// MFMA operand mapping as conv_kernels.hip: A = weights (row = output channel) from LDS, B = 8
+// channels of one pixel (16-B LDS or global read per lane), accumulator = 4 consecutive channels of
+// one pixel per lane. All three weight matrices stay in LDS for the workgroup's lifetime.
+#include "bugseg_internal.h"
+#include "mfma_common.h"
+
+namespace bugseg {
+
+template <int C> struct BTile;
+template <> struct BTile<128> { static constexpr int TH = 16, TW = 16; };
+template <> struct BTile<64> { static constexpr int TH = 16, TW = 32; };
+template <> struct BTile<16> { static constexpr int TH = 16, TW = 32; };
+
+int bneck_tile_h(int C) { return C == 128 ? BTile<128>::TH : BTile<64>::TH; }
+int bneck_tile_w(int C) { return C == 128 ? BTile<128>::TW : BTile<64>::TW; }
+
+template <typename T, int C, bool ASYM>
+__global__ void __launch_bounds__(256) bneck_kernel(const BneckArgs a) {
+    using Raw = typename Tr<T>::Raw;
+    constexpr int I = C / 4;
+    constexpr int IS = I < 8 ? 8 : I;                 // stored internal channels (8-channel groups)
+    constexpr int NR1 = (I + 15) / 16;                // 16-row fragments of t0 / t1
+    constexpr int NR3 = C / 16;                       // 16-row fragments of out
+    constexpr int G1 = C / 8, KS1 = (G1 + 3) / 4;     // proj k groups / steps
+    constexpr int TAPS = ASYM ? 5 : 9;
+    constexpr int G2 = TAPS * IS / 8, KS2 = (G2 + 3) / 4;
+    constexpr int G3 = IS / 8;                        // expand k groups (<= 4: one step)
+    constexpr int TH = BTile<C>::TH, TW = BTile<C>::TW;
+    constexpr int PAD = 16 / (int)sizeof(T);
+    constexpr int PSTR = IS + PAD;                    // LDS pixel stride (elements)
+    constexpr int NF2 = TH * TW / 64;                 // phase-2/3 fragments per wave
+    constexpr int TWA = TW + 4;                       // asymmetric: width of t1a (1x5 halo 2+2)
+    constexpr int NF2A = TH * TWA / 64;
+    static_assert(TH * TW % 64 == 0 && TH * TWA % 64 == 0, "tile must split into 4 waves of fragments");
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+
+    const int tid = threadIdx.x;
+    const int lane = tid & 63, wave = tid >> 6, col = lane & 15, kq = lane >> 4;
+    const int K1S = KS1 * 32 + PAD, K2S = KS2 * 32 + PAD, K3S = 32 + PAD;
+    T *w1 = reinterpret_cast<T *>(smem);
+    T *w2 = w1 + NR1 * 16 * K1S;
+    T *w2b = w2 + NR1 * 16 * K2S;                     // asymmetric second conv (1x5)
+    T *w3 = w2b + (ASYM ? NR1 * 16 * K2S : 0);
+    T *ts = w3 + C * K3S;                             // t0 / t1a / t1 region
+    {
+        auto stage = [&](T *dst, const void *src, int rows, int kpad, int kstride) {
+            const int cpr = kpad * (int)sizeof(T) / 16;
+            const uint4 *s = reinterpret_cast<const uint4 *>(src);
+            for (int i = tid; i < rows * cpr; i += 256) {
+                const int r = i / cpr, c = i - r * cpr;
+                *reinterpret_cast<uint4 *>(reinterpret_cast<unsigned char *>(dst + (size_t)r * kstride) + c * 16) = s[i];
+            }
+        };
+        stage(w1, a.w1, NR1 * 16, KS1 * 32, K1S);
+        stage(w2, a.w2, NR1 * 16, KS2 * 32, K2S);
+        if constexpr (ASYM) stage(w2b, a.w2b, NR1 * 16, KS2 * 32, K2S);
+        stage(w3, a.w3, C, 32, K3S);
+    }
+    const T *x = reinterpret_cast<const T *>(a.x);
+    T *out = reinterpret_cast<T *>(a.out);
+    const int ry = a.ry, rx = a.rx, d = a.d;
+    const int HWW = TW + 2 * rx, HR = (TH + 2 * ry) * HWW;
+    const int nf1 = (HR + 15) >> 4;
+
+    // XCD-aware tile walk (see conv_kernels.hip)
+    const int G = gridDim.x, grp = blockIdx.x & 7, slot = blockIdx.x >> 3, nslots = G >> 3;
+    const int CH = (a.ntiles + 7) >> 3;
+    for (int it = slot; it < CH; it += nslots) {
+        const int tile = grp * CH + it;
+        if (tile >= a.ntiles) break;
+        const int n = tile / (a.tiles_y * a.tiles_x);
+        const int tr = tile - n * a.tiles_y * a.tiles_x;
+        const int ty0 = (tr / a.tiles_x) * TH, tx0 = (tr % a.tiles_x) * TW;
+        const T *xn = x + (size_t)n * a.H * a.W * C;
+        __syncthreads();   // weights staged (first tile) / previous tile done with ts
+
+        // ---- phase 1: t0 = act1(W1 x + b1) over tile + halo, 0 outside the image
+        for (int f = wave; f < nf1; f += 4) {
+            const int h = f * 16 + col;
+            const int hy = h / HWW, hx = h - hy * HWW;
+            const int iy = ty0 - ry + hy, ix = tx0 - rx + hx;
+            const bool ok = h < HR && (unsigned)iy < (unsigned)a.H && (unsigned)ix < (unsigned)a.W;
+            f32x4 acc[NR1];
+#pragma unroll
+            for (int r = 0; r < NR1; ++r) acc[r] = (f32x4){0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+            for (int s = 0; s < KS1; ++s) {
+                const int g = s * 4 + kq;
+                Raw xf;
+                if (ok && g < G1) ld8(xf, xn + ((size_t)iy * a.W + ix) * C + g * 8);
+                else zero(xf);
+#pragma unroll
+                for (int r = 0; r < NR1; ++r) {
+                    Raw wf;
+                    ld8(wf, w1 + (r * 16 + col) * K1S + s * 32 + kq * 8);
+                    mma(acc[r], wf, xf);
+                }
+            }
+            if (h < HR) {
+#pragma unroll
+                for (int r = 0; r < NR1; ++r) {
+                    const int c = r * 16 + kq * 4;
+                    if (c >= IS) continue;
+                    float4 v = prelu4(add4(f4(acc[r]), ld4f(a.b1 + c)), ld4f(a.s1 + c));
+                    if (!ok) v = make_float4(0.f, 0.f, 0.f, 0.f);
+                    st4(ts + h * PSTR + c, v);
+                }
+            }
+        }
+        __syncthreads();
+
+        // ---- phase 2: t1 = act2(W2 * t0 + b2) (asymmetric: t1a = 5x1 (t0); t1 = 1x5 (t1a))
+        if constexpr (!ASYM) {
+            f32x4 acc[NF2][NR1];
+#pragma unroll
+            for (int j = 0; j < NF2; ++j)
+#pragma unroll
+                for (int r = 0; r < NR1; ++r) acc[j][r] = (f32x4){0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+            for (int s = 0; s < KS2; ++s) {
+                const int g = s * 4 + kq;
+                const int tap = g / (IS / 8), coff = (g - tap * (IS / 8)) * 8;
+                const int dy = (tap / 3 - 1) * d, dx = (tap % 3 - 1) * d;
+                Raw wf[NR1];
+#pragma unroll
+                for (int r = 0; r < NR1; ++r) ld8(wf[r], w2 + (r * 16 + col) * K2S + s * 32 + kq * 8);
+#pragma unroll
+                for (int j = 0; j < NF2; ++j) {
+                    const int p = (wave + 4 * j) * 16 + col;
+                    const int oy = p / TW, ox = p - oy * TW;
+                    Raw xf;
+                    if (g < G2) ld8(xf, ts + ((oy + ry + dy) * HWW + (ox + rx + dx)) * PSTR + coff);
+                    else zero(xf);
+#pragma unroll
+                    for (int r = 0; r < NR1; ++r) mma(acc[j][r], wf[r], xf);
+                }
+            }
+            __syncthreads();   // every wave is done reading t0
+#pragma unroll
+            for (int j = 0; j < NF2; ++j) {
+                const int p = (wave + 4 * j) * 16 + col;
+#pragma unroll
+                for (int r = 0; r < NR1; ++r) {
+                    const int c = r * 16 + kq * 4;
+                    if (c >= IS) continue;
+                    st4(ts + p * PSTR + c, prelu4(add4(f4(acc[j][r]), ld4f(a.b2 + c)), ld4f(a.s2 + c)));
+                }
+            }
+        } else {
+            {   // 5x1 over rows (taps dy = -2..2), output width TW+4 (the 1x5's halo)
+                f32x4 acc[NF2A][NR1];
+#pragma unroll
+                for (int j = 0; j < NF2A; ++j)
+#pragma unroll
+                    for (int r = 0; r < NR1; ++r) acc[j][r] = (f32x4){0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+                for (int s = 0; s < KS2; ++s) {
+                    const int g = s * 4 + kq;
+                    const int tap = g / (IS / 8), coff = (g - tap * (IS / 8)) * 8;
+                    Raw wf[NR1];
+#pragma unroll
+                    for (int r = 0; r < NR1; ++r) ld8(wf[r], w2 + (r * 16 + col) * K2S + s * 32 + kq * 8);
+#pragma unroll
+                    for (int j = 0; j < NF2A; ++j) {
+                        const int p = (wave + 4 * j) * 16 + col;
+                        const int oy = p / TWA, ox = p - oy * TWA;
+                        Raw xf;
+                        if (g < G2) ld8(xf, ts + ((oy + ry + tap - 2) * HWW + ox) * PSTR + coff);
+                        else zero(xf);
+#pragma unroll
+                        for (int r = 0; r < NR1; ++r) mma(acc[j][r], wf[r], xf);
+                    }
+                }
+                __syncthreads();
+#pragma unroll
+                for (int j = 0; j < NF2A; ++j) {
+                    const int p = (wave + 4 * j) * 16 + col;
+                    const int ox = p - (p / TWA) * TWA;
+                    const bool inside = (unsigned)(tx0 - 2 + ox) < (unsigned)a.W;   // the 1x5 zero-pads t1a
+#pragma unroll
+                    for (int r = 0; r < NR1; ++r) {
+                        const int c = r * 16 + kq * 4;
+                        if (c >= IS) continue;
+                        float4 v = prelu4(add4(f4(acc[j][r]), ld4f(a.b2 + c)), ld4f(a.s2 + c));
+                        if (!inside) v = make_float4(0.f, 0.f, 0.f, 0.f);
+                        st4(ts + p * PSTR + c, v);
+                    }
+                }
+                __syncthreads();
+            }
+            {   // 1x5 over columns (taps dx = -2..2)
+                f32x4 acc[NF2][NR1];
+#pragma unroll
+                for (int j = 0; j < NF2; ++j)
+#pragma unroll
+                    for (int r = 0; r < NR1; ++r) acc[j][r] = (f32x4){0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+                for (int s = 0; s < KS2; ++s) {
+                    const int g = s * 4 + kq;
+                    const int tap = g / (IS / 8), coff = (g - tap * (IS / 8)) * 8;
+                    Raw wf[NR1];
+#pragma unroll
+                    for (int r = 0; r < NR1; ++r) ld8(wf[r], w2b + (r * 16 + col) * K2S + s * 32 + kq * 8);
+#pragma unroll
+                    for (int j = 0; j < NF2; ++j) {
+                        const int p = (wave + 4 * j) * 16 + col;
+                        const int oy = p / TW, ox = p - oy * TW;
+                        Raw xf;
+                        if (g < G2) ld8(xf, ts + (oy * TWA + ox + tap) * PSTR + coff);
+                        else zero(xf);
+#pragma unroll
+                        for (int r = 0; r < NR1; ++r) mma(acc[j][r], wf[r], xf);
+                    }
+                }
+                __syncthreads();
+#pragma unroll
+                for (int j = 0; j < NF2; ++j) {
+                    const int p = (wave + 4 * j) * 16 + col;
+#pragma unroll
+                    for (int r = 0; r < NR1; ++r) {
+                        const int c = r * 16 + kq * 4;
+                        if (c >= IS) continue;
+                        st4(ts + p * PSTR + c, prelu4(add4(f4(acc[j][r]), ld4f(a.b2b + c)), ld4f(a.s2b + c)));
+                    }
+                }
+            }
+        }
+        __syncthreads();
+
+        // ---- phase 3: out = act_out(act3(W3 t1 + b3) + x), fragment by fragment
+#pragma unroll 1
+        for (int j = 0; j < NF2; ++j) {
+            const int p = (wave + 4 * j) * 16 + col;
+            const int oy = p / TW, ox = p - oy * TW;
+            const int iy = ty0 + oy, ix = tx0 + ox;
+            const bool ok = (unsigned)iy < (unsigned)a.H && (unsigned)ix < (unsigned)a.W;
+            Raw tf;
+            if (kq < G3) ld8(tf, ts + p * PSTR + kq * 8);
+            else zero(tf);
+            f32x4 acc[NR3];
+#pragma unroll
+            for (int r = 0; r < NR3; ++r) {
+                acc[r] = (f32x4){0.f, 0.f, 0.f, 0.f};
+                Raw wf;
+                ld8(wf, w3 + (r * 16 + col) * K3S + kq * 8);
+                mma(acc[r], wf, tf);
+            }
+            if (ok) {
+                const size_t po = ((size_t)iy * a.W + ix) * C;
+#pragma unroll
+                for (int r = 0; r < NR3; ++r) {
+                    const int c = r * 16 + kq * 4;
+                    float4 v = prelu4(add4(f4(acc[r]), ld4f(a.b3 + c)), ld4f(a.s3 + c));
+                    v = prelu4(add4(v, ld4(xn + po + c)), ld4f(a.s_out + c));
+                    st4(out + (size_t)n * a.H * a.W * C + po + c, v);
+                }
+            }
+        }
+    }
+}
+
+size_t bneck_lds_bytes(int prec, int C, bool asym, int ry, int rx) {
+    const int es = prec == PREC_BF16 ? 2 : 4, pad = 16 / es;
+    const int I = C / 4, IS = I < 8 ? 8 : I, NR1 = (I + 15) / 16;
+    const int KS1 = (C / 8 + 3) / 4, KS2 = ((asym ? 5 : 9) * IS / 8 + 3) / 4;
+    const int TH = bneck_tile_h(C), TW = bneck_tile_w(C);
+    const size_t wts = (size_t)NR1 * 16 * (KS1 * 32 + pad) + (size_t)NR1 * 16 * (KS2 * 32 + pad) * (asym ? 2 : 1) +
+                       (size_t)C * (32 + pad);
+    const size_t halo = (size_t)(TH + 2 * ry) * (TW + 2 * rx);
+    return (wts + halo * (IS + pad)) * es;
+}
+
+template <typename T>
+static hipError_t launch_t(int C, bool asym, const BneckArgs &a, dim3 g, size_t lds, hipStream_t s) {
+#define BN_CASE(CC)                                                                                     \
+    if (C == CC) {                                                                                      \
+        if (asym) hipLaunchKernelGGL((bneck_kernel<T, CC, true>), g, dim3(256), lds, s, a);            \
+        else hipLaunchKernelGGL((bneck_kernel<T, CC, false>), g, dim3(256), lds, s, a);                \
+        return hipGetLastError();                                                                       \
+    }
+    BN_CASE(128)
+    BN_CASE(64)
+    BN_CASE(16)
+#undef BN_CASE
+    return hipErrorInvalidValue;
+}
+
+hipError_t launch_bneck(int prec, int C, bool asym, const BneckArgs &a, hipStream_t s) {
+    const size_t lds = bneck_lds_bytes(prec, C, asym, a.ry, a.rx);
+    static int attr_set[2][2][3] = {};
+    int g = a.ntiles < 2048 ? a.ntiles : 2048;
+    g = (g + 7) & ~7;
+    const int ci = C == 128 ? 0 : C == 64 ? 1 : 2;
+    if (lds > 64 * 1024 && !attr_set[prec][asym][ci]) {
+        // dynamic LDS above 64 KB must be allowed per kernel
+        hipError_t e;
+        if (prec == PREC_BF16)
+            e = C == 128 ? hipFuncSetAttribute(asym ? (const void *)bneck_kernel<__bf16, 128, true> : (const void *)bneck_kernel<__bf16, 128, false>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024)
+              : C == 64 ? hipFuncSetAttribute(asym ? (const void *)bneck_kernel<__bf16, 64, true> : (const void *)bneck_kernel<__bf16, 64, false>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024)
+                        : hipFuncSetAttribute(asym ? (const void *)bneck_kernel<__bf16, 16, true> : (const void *)bneck_kernel<__bf16, 16, false>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+        else
+            e = C == 128 ? hipFuncSetAttribute(asym ? (const void *)bneck_kernel<float, 128, true> : (const void *)bneck_kernel<float, 128, false>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024)
+              : C == 64 ? hipFuncSetAttribute(asym ? (const void *)bneck_kernel<float, 64, true> : (const void *)bneck_kernel<float, 64, false>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024)
+                        : hipFuncSetAttribute(asym ? (const void *)bneck_kernel<float, 16, true> : (const void *)bneck_kernel<float, 16, false>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+        if (e != hipSuccess) return e;
+        attr_set[prec][asym][ci] = 1;
+    }
+    if (prec == PREC_BF16) return launch_t<__bf16>(C, asym, a, dim3(g), lds, s);
+    return launch_t<float>(C, asym, a, dim3(g), lds, s);
+}
+
+}  // namespace bugseg

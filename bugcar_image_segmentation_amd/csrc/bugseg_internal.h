@@ -18,7 +18,8 @@ enum Epi {
     EPI_INIT = 4,      // out = act1(acc + bias + pscale * maxpool_k(in))          initial block concat
     EPI_SHUFFLE = 5,   // 4 phases -> pixel (2y+a, 2x+b): transposed conv s2     upsampling ext tconv
     EPI_CLASSES = 6,   // 4 phases x 16 classes -> argmax + LUT / f32 logits      final transposed conv
-    EPI_COUNT = 7
+    EPI_INIT_BGR = 7,  // EPI_INIT reading raw BGR u8 frames: normalise via LUT on load (preprocess fused)
+    EPI_COUNT = 8
 };
 
 enum Prec { PREC_F32 = 0, PREC_BF16 = 1 };
@@ -46,6 +47,7 @@ struct ConvArgs {
     const uint8_t *lut;  // EPI_CLASSES: 16-entry class remap (nullptr: raw class id)
     uint8_t *cls_out;    // EPI_CLASSES: (B, Hout, Wout) u8, may be nullptr
     float *logits_out;   // EPI_CLASSES: (B, ncls, Hout, Wout) f32 NCHW, may be nullptr
+    const double *nlut;  // EPI_INIT_BGR: [3][256] normalisation table, RGB order (models.py:91)
     int ntiles;
 };
 
@@ -54,6 +56,21 @@ hipError_t launch_conv(int prec, int nr, int epi, const ConvArgs &a, hipStream_t
 // pixels per tile for a given nr (sizes the grid)
 int conv_tile_pixels(int nr);
 size_t conv_lds_bytes(int prec, const ConvArgs &a);
+
+// ---- fused regular / dilated / asymmetric bottleneck (bneck_kernels.hip) ---------------------
+struct BneckArgs {
+    const void *x;       // block input (B, H, W, C) NHWC
+    void *out;           // block output, same shape
+    int B, H, W;
+    int ry, rx, d;       // halo of the middle conv (rows, cols) and its dilation
+    int tiles_x, tiles_y, ntiles;
+    const void *w1, *w2, *w2b, *w3;                   // packed [Npad][Kpad] (w2b: asymmetric 1x5)
+    const float *b1, *s1, *b2, *s2, *b2b, *s2b, *b3, *s3, *s_out;
+};
+hipError_t launch_bneck(int prec, int C, bool asym, const BneckArgs &a, hipStream_t s);
+size_t bneck_lds_bytes(int prec, int C, bool asym, int ry, int rx);
+int bneck_tile_h(int C);
+int bneck_tile_w(int C);
 
 // ---- preprocess / layout (prep_kernels.hip) --------------------------------------------------
 struct PreArgs {

@@ -16,6 +16,7 @@
 #include <string>
 #include <vector>
 #include <algorithm>
+#include <cstdlib>
 
 #include "bugseg_internal.h"
 #include "../../include/bugseg.h"
@@ -54,8 +55,12 @@ struct Packed {
 };
 
 struct Op {
+    int kind = 0;          // 0: conv_kernel launch, 1: fused bottleneck launch
     ConvArgs a;
     int nr = 0, epi = 0;
+    BneckArgs bn;
+    int bn_c = 0;
+    bool bn_asym = false;
     double bytes = 0, flops = 0;
 };
 
@@ -464,6 +469,36 @@ ConvArgs base_args(const bugseg_ctx *ctx, const Packed &p) {
     return a;
 }
 
+// A regular block runs as ONE fused launch (bneck_kernels.hip) when its shape is one the fused
+// kernel is built for and the halo of its middle conv stays small (recomputed projection <= 3x the
+// tile: dilation <= 4 on 16x16 tiles); otherwise as its 3-4 conv launches. BUGSEG_NO_FUSE=1 forces
+// the unfused plan (A/B testing; results are bit-identical).
+bool fusable_regular(const bugseg_ctx *ctx, const BlockDesc &b, int &ry, int &rx, int &d) {
+    const char *env = std::getenv("BUGSEG_NO_FUSE");     // read per plan build (plans are cached)
+    if (env && *env && *env != '0') return false;
+    const int C = b.attrs[0];
+    if (C != 128 && C != 64 && C != 16) return false;
+    const int nu = (int)b.units.size();
+    const UnitDesc &u1 = b.units[0], &u3 = b.units[nu - 1];
+    if (u1.kh != 1 || u1.kw != 1 || u1.cout != C / 4 || u3.kh != 1 || u3.kw != 1 || u3.cin != C / 4) return false;
+    if (nu == 4) {
+        const UnitDesc &a = b.units[1], &c = b.units[2];
+        if (a.kh != 5 || a.kw != 1 || a.pad_h != 2 || a.pad_w != 0 || a.dil_h != 1 ||
+            c.kh != 1 || c.kw != 5 || c.pad_h != 0 || c.pad_w != 2 || c.dil_w != 1 || a.cout != C / 4 || c.cout != C / 4)
+            return false;
+        ry = rx = 2; d = 1;
+    } else {
+        const UnitDesc &m = b.units[1];
+        if (m.kh != 3 || m.kw != 3 || m.dil_h != m.dil_w || m.pad_h != m.dil_h || m.pad_w != m.dil_w || m.cout != C / 4)
+            return false;
+        d = m.dil_h;
+        ry = rx = d;
+    }
+    const int th = bneck_tile_h(C), tw = bneck_tile_w(C);
+    if ((double)(th + 2 * ry) * (tw + 2 * rx) > 3.0 * th * tw) return false;
+    return bneck_lds_bytes(ctx->prec, C, nu == 4, ry, rx) <= 160 * 1024;
+}
+
 // Walk the network for (B, H, W). With fill == false only the buffer sizes are computed.
 struct Walker {
     bugseg_ctx *ctx;
@@ -542,6 +577,37 @@ struct Walker {
                 const int nu = (int)b.units.size();
                 Shape s = cur;
                 const unsigned char *src = curp;
+                int ry = 0, rx = 0, dd = 1;
+                if (fusable_regular(ctx, b, ry, rx, dd)) {
+                    // one launch: projection + middle conv + expansion + residual, internals in LDS
+                    szX = std::max(szX, tbytes(cur));
+                    if (fill) {
+                        Op op;
+                        op.kind = 1;
+                        op.bn_c = b.attrs[0];
+                        op.bn_asym = nu == 4;
+                        BneckArgs &q = op.bn;
+                        std::memset(&q, 0, sizeof(q));
+                        const unsigned char *dw = (const unsigned char *)ctx->dev_w;
+                        const Packed &p1 = P(0), &p2 = P(1), &p3 = P(nu - 1), &p2b = P(nu == 4 ? 2 : 1);
+                        q.x = curp; q.out = dst; q.B = B; q.H = cur.H; q.W = cur.W;
+                        q.ry = ry; q.rx = rx; q.d = dd;
+                        const int th = bneck_tile_h(op.bn_c), tw = bneck_tile_w(op.bn_c);
+                        q.tiles_y = (cur.H + th - 1) / th; q.tiles_x = (cur.W + tw - 1) / tw;
+                        q.ntiles = B * q.tiles_y * q.tiles_x;
+                        q.w1 = dw + p1.o_w; q.b1 = (const float *)(dw + p1.o_bias); q.s1 = (const float *)(dw + p1.o_s1);
+                        q.w2 = dw + p2.o_w; q.b2 = (const float *)(dw + p2.o_bias); q.s2 = (const float *)(dw + p2.o_s1);
+                        q.w2b = dw + p2b.o_w; q.b2b = (const float *)(dw + p2b.o_bias); q.s2b = (const float *)(dw + p2b.o_s1);
+                        q.w3 = dw + p3.o_w; q.b3 = (const float *)(dw + p3.o_bias); q.s3 = (const float *)(dw + p3.o_s1);
+                        q.s_out = (const float *)(dw + p3.o_s2);
+                        double fl = 0, wb = 0;
+                        for (int i = 0; i < nu; ++i) { fl += 2.0 * P(i).macs_per_px * B * cur.H * cur.W; wb += (double)P(i).Npad * P(i).Kpad * es; }
+                        op.flops = fl;
+                        op.bytes = 2.0 * B * cur.H * cur.W * cur.C * es + wb;
+                        ops.push_back(op);
+                    }
+                    break;
+                }
                 for (int i = 0; i < nu; ++i) {
                     const UnitDesc &u = b.units[i];
                     const bool last = i + 1 == nu;
@@ -736,7 +802,7 @@ int bugseg_preprocess(bugseg_ctx *ctx, const uint8_t *bgr, int B, int H0, int W0
                       void *out, void *stream) {
     if (!ctx || !bgr || !out) return fail(ctx, BUGSEG_EINVAL, "NULL argument");
     if (B <= 0 || H0 <= 0 || W0 <= 0 || H <= 0 || W <= 0) return fail(ctx, BUGSEG_EINVAL, "bad shape");
-    if (out_layout < BUGSEG_PRE_ENGINE || out_layout > BUGSEG_PRE_NCHW_F32) return fail(ctx, BUGSEG_EINVAL, "bad out_layout");
+    if (out_layout < BUGSEG_PRE_ENGINE || out_layout > BUGSEG_PRE_BGR_U8) return fail(ctx, BUGSEG_EINVAL, "bad out_layout");
     DeviceGuard g(ctx->device);
     PreArgs a;
     std::memset(&a, 0, sizeof(a));
@@ -797,7 +863,8 @@ int bugseg_nchw_to_input(bugseg_ctx *ctx, const void *x, int is_f64, int B, int 
     return BUGSEG_OK;
 }
 
-int bugseg_enet_forward(bugseg_ctx *ctx, const void *in, int B, int H, int W, int out_kind, void *out, void *stream) {
+static int enet_forward(bugseg_ctx *ctx, const void *in, bool bgr, int B, int H, int W, int out_kind, void *out,
+                        void *stream) {
     if (!ctx || !in || !out) return fail(ctx, BUGSEG_EINVAL, "NULL argument");
     if (!ctx->loaded) return fail(ctx, BUGSEG_ESTATE, "no weights loaded");
     if (out_kind < BUGSEG_OUT_LOGITS_F32 || out_kind > BUGSEG_OUT_BINARY_U8) return fail(ctx, BUGSEG_EINVAL, "bad out_kind");
@@ -805,7 +872,10 @@ int bugseg_enet_forward(bugseg_ctx *ctx, const void *in, int B, int H, int W, in
     std::string why;
     if (!build_plan(ctx, B, H, W, why)) return fail(ctx, BUGSEG_EINVAL, why);
     Plan &pl = ctx->plan;
-    pl.ops.front().a.in = in;
+    Op &first = pl.ops.front();
+    first.a.in = in;
+    first.epi = bgr ? EPI_INIT_BGR : EPI_INIT;
+    first.a.nlut = bgr ? (const double *)((const unsigned char *)ctx->dev_luts + 32) : nullptr;
     ConvArgs &last = pl.ops.back().a;
     last.cls_out = nullptr; last.logits_out = nullptr; last.lut = nullptr;
     const uint8_t *luts = (const uint8_t *)ctx->dev_luts;
@@ -817,10 +887,20 @@ int bugseg_enet_forward(bugseg_ctx *ctx, const void *in, int B, int H, int W, in
     }
     for (size_t i = 0; i < pl.ops.size(); ++i) {
         const Op &op = pl.ops[i];
-        hipError_t e = launch_conv(ctx->prec, op.nr, op.epi, op.a, (hipStream_t)stream);
+        hipError_t e = op.kind == 1 ? launch_bneck(ctx->prec, op.bn_c, op.bn_asym, op.bn, (hipStream_t)stream)
+                                    : launch_conv(ctx->prec, op.nr, op.epi, op.a, (hipStream_t)stream);
         if (e != hipSuccess) return fail(ctx, BUGSEG_EHIP, "conv launch " + std::to_string(i) + ": " + hipGetErrorString(e));
     }
     return BUGSEG_OK;
+}
+
+int bugseg_enet_forward(bugseg_ctx *ctx, const void *in, int B, int H, int W, int out_kind, void *out, void *stream) {
+    return enet_forward(ctx, in, false, B, H, W, out_kind, out, stream);
+}
+
+int bugseg_enet_forward_bgr(bugseg_ctx *ctx, const uint8_t *bgr, int B, int H, int W, int out_kind, void *out,
+                            void *stream) {
+    return enet_forward(ctx, bgr, true, B, H, W, out_kind, out, stream);
 }
 
 int bugseg_bev_occgrid(bugseg_ctx *ctx, const uint8_t *seg, int B, const bugseg_bev_params *p, int8_t *out, void *stream) {
@@ -864,7 +944,8 @@ int bugseg_bev_occgrid(bugseg_ctx *ctx, const uint8_t *seg, int B, const bugseg_
     return BUGSEG_OK;
 }
 
-int bugseg_plan_info(bugseg_ctx *ctx, int B, int H, int W, int out_kind, int *n_launches, double *alg_bytes, double *flops) {
+int bugseg_plan_info(bugseg_ctx *ctx, int B, int H, int W, int out_kind, int bgr_input, int *n_launches, double *alg_bytes,
+                     double *flops) {
     if (!ctx) return fail(ctx, BUGSEG_EINVAL, "NULL ctx");
     if (!ctx->loaded) return fail(ctx, BUGSEG_ESTATE, "no weights loaded");
     DeviceGuard g(ctx->device);
@@ -874,6 +955,8 @@ int bugseg_plan_info(bugseg_ctx *ctx, int B, int H, int W, int out_kind, int *n_
     for (const Op &op : ctx->plan.ops) { by += op.bytes; fl += op.flops; }
     // final epilogue output
     by += out_kind == BUGSEG_OUT_LOGITS_F32 ? (double)B * H * W * ctx->ncls * 4 : (double)B * H * W;
+    // raw BGR input (bugseg_enet_forward_bgr): 3 bytes per pixel instead of the 8-channel engine input
+    if (bgr_input) by -= (double)B * H * W * (8.0 * (ctx->prec == PREC_BF16 ? 2 : 4) - 3.0);
     if (n_launches) *n_launches = (int)ctx->plan.ops.size();
     if (alg_bytes) *alg_bytes = by;
     if (flops) *flops = fl;

@@ -18,67 +18,9 @@
 // XCD-aware mapping (blocks sharing blockIdx%8 walk one contiguous range of tiles, so the 3x3 /
 // dilated halo re-reads of neighbouring tiles hit the same XCD's L2).
 #include "bugseg_internal.h"
+#include "mfma_common.h"
 
 namespace bugseg {
-
-typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
-typedef float f32x4 __attribute__((ext_vector_type(4)));
-
-struct RawB { uint4 v; };          // 8 bf16
-struct RawF { float4 a, b; };      // 8 f32
-
-template <typename T> struct Tr;
-template <> struct Tr<__bf16> { using Raw = RawB; };
-template <> struct Tr<float> { using Raw = RawF; };
-
-__device__ __forceinline__ void zero(RawB &r) { r.v = make_uint4(0, 0, 0, 0); }
-__device__ __forceinline__ void zero(RawF &r) { r.a = make_float4(0.f, 0.f, 0.f, 0.f); r.b = r.a; }
-__device__ __forceinline__ void ld8(RawB &r, const __bf16 *p) { r.v = *reinterpret_cast<const uint4 *>(p); }
-__device__ __forceinline__ void ld8(RawF &r, const float *p) {
-    r.a = reinterpret_cast<const float4 *>(p)[0];
-    r.b = reinterpret_cast<const float4 *>(p)[1];
-}
-
-__device__ __forceinline__ void mma(f32x4 &acc, const RawB &w, const RawB &x) {
-    acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, w.v), __builtin_bit_cast(bf16x8, x.v),
-                                                  acc, 0, 0, 0);
-}
-// fp32 parity mode: sub-MFMA j contracts element j of every lane's 8-group (lane>>4 = group),
-// so the 8 sub-MFMAs together cover the same 32 k as one bf16 MFMA (exact f32 products).
-__device__ __forceinline__ void mma(f32x4 &acc, const RawF &w, const RawF &x) {
-    acc = __builtin_amdgcn_mfma_f32_16x16x4f32(w.a.x, x.a.x, acc, 0, 0, 0);
-    acc = __builtin_amdgcn_mfma_f32_16x16x4f32(w.a.y, x.a.y, acc, 0, 0, 0);
-    acc = __builtin_amdgcn_mfma_f32_16x16x4f32(w.a.z, x.a.z, acc, 0, 0, 0);
-    acc = __builtin_amdgcn_mfma_f32_16x16x4f32(w.a.w, x.a.w, acc, 0, 0, 0);
-    acc = __builtin_amdgcn_mfma_f32_16x16x4f32(w.b.x, x.b.x, acc, 0, 0, 0);
-    acc = __builtin_amdgcn_mfma_f32_16x16x4f32(w.b.y, x.b.y, acc, 0, 0, 0);
-    acc = __builtin_amdgcn_mfma_f32_16x16x4f32(w.b.z, x.b.z, acc, 0, 0, 0);
-    acc = __builtin_amdgcn_mfma_f32_16x16x4f32(w.b.w, x.b.w, acc, 0, 0, 0);
-}
-
-__device__ __forceinline__ float4 ld4f(const float *p) { return *reinterpret_cast<const float4 *>(p); }
-__device__ __forceinline__ float4 ld4(const float *p) { return *reinterpret_cast<const float4 *>(p); }
-__device__ __forceinline__ float4 ld4(const __bf16 *p) {
-    uint2 u = *reinterpret_cast<const uint2 *>(p);
-    return make_float4(__uint_as_float(u.x << 16), __uint_as_float(u.x & 0xffff0000u),
-                       __uint_as_float(u.y << 16), __uint_as_float(u.y & 0xffff0000u));
-}
-__device__ __forceinline__ void st4(float *p, float4 v) { *reinterpret_cast<float4 *>(p) = v; }
-__device__ __forceinline__ void st4(__bf16 *p, float4 v) {
-    typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
-    bf16x4 b = {(__bf16)v.x, (__bf16)v.y, (__bf16)v.z, (__bf16)v.w};
-    *reinterpret_cast<bf16x4 *>(p) = b;
-}
-__device__ __forceinline__ float ld1(const float *p) { return *p; }
-__device__ __forceinline__ float ld1(const __bf16 *p) { return (float)*p; }
-
-__device__ __forceinline__ float prelu(float v, float s) { return v > 0.f ? v : v * s; }
-__device__ __forceinline__ float4 prelu4(float4 v, float4 s) {
-    return make_float4(prelu(v.x, s.x), prelu(v.y, s.y), prelu(v.z, s.z), prelu(v.w, s.w));
-}
-__device__ __forceinline__ float4 add4(float4 a, float4 b) { return make_float4(a.x + b.x, a.y + b.y, a.z + b.z, a.w + b.w); }
-__device__ __forceinline__ float4 f4(const f32x4 &v) { return make_float4(v[0], v[1], v[2], v[3]); }
-__device__ __forceinline__ float get(const float4 &v, int r) { return r == 0 ? v.x : r == 1 ? v.y : r == 2 ? v.z : v.w; }
 
 template <int NR> struct Cfg { static constexpr int MR = NR >= 4 ? 2 : 4; };
 
@@ -103,8 +45,15 @@ __global__ void __launch_bounds__(256) conv_kernel(const ConvArgs a) {
             *reinterpret_cast<uint4 *>(smem + (size_t)r * KS * sizeof(T) + c * 16) = src[i];
         }
         for (int i = tid; i < a.Ksteps * 4; i += 256) gt[i] = a.gtab[i];
+        if constexpr (EPI == EPI_INIT_BGR) {
+            // normalisation table rounded exactly as the engine-input path rounds it (f64 -> f32 -> T)
+            float *lut = reinterpret_cast<float *>(gt + a.Ksteps * 4);
+            for (int i = tid; i < 3 * 256; i += 256) lut[i] = (float)(T)(float)a.nlut[i];
+        }
     }
     __syncthreads();
+    const float *nl = reinterpret_cast<const float *>(gt + a.Ksteps * 4);
+    const uint8_t *bgr = reinterpret_cast<const uint8_t *>(a.in);
 
     const T *in = reinterpret_cast<const T *>(a.in);
     const int HWg = a.Hg * a.Wg;
@@ -134,6 +83,9 @@ __global__ void __launch_bounds__(256) conv_kernel(const ConvArgs a) {
 #pragma unroll
             for (int n = 0; n < NR; ++n) acc[m][n] = (f32x4){0.f, 0.f, 0.f, 0.f};
 
+        int pmax[MR][3];      // EPI_INIT_BGR: running max of the raw bytes over this lane's pool taps
+#pragma unroll
+        for (int m = 0; m < MR; ++m) pmax[m][0] = pmax[m][1] = pmax[m][2] = -1;
         for (int s = 0; s < a.Ksteps; ++s) {
             const int g = gt[s * 4 + kq];
             const int dy = (int)(signed char)(g & 0xff), dx = (int)(signed char)((g >> 8) & 0xff);
@@ -143,10 +95,25 @@ __global__ void __launch_bounds__(256) conv_kernel(const ConvArgs a) {
             for (int m = 0; m < MR; ++m) {
                 const int iy = py[m] * a.stride + dy, ix = px[m] * a.stride + dx;
                 const bool ok = pv[m] && coff != 0xffff && (unsigned)iy < (unsigned)a.Hin && (unsigned)ix < (unsigned)a.Win;
-                if (ok)
-                    ld8(xf[m], in + ((size_t)(pn[m] * a.Hin + iy) * a.Win + ix) * a.CinS + coff);
-                else
+                if constexpr (EPI == EPI_INIT_BGR) {
+                    // one tap of the 3x3 s2 p1 window = 3 raw bytes; normalised RGB + 5 zero channels
                     zero(xf[m]);
+                    if (ok) {
+                        const uint8_t *q = bgr + ((size_t)(pn[m] * a.Hin + iy) * a.Win + ix) * 3;
+                        const int b0 = q[0], b1 = q[1], b2 = q[2];
+                        set3(xf[m], nl[b2], nl[256 + b1], nl[512 + b0]);
+                        if (a.pool_k == 3 || (dy >= 0 && dx >= 0)) {
+                            pmax[m][0] = max(pmax[m][0], b2);
+                            pmax[m][1] = max(pmax[m][1], b1);
+                            pmax[m][2] = max(pmax[m][2], b0);
+                        }
+                    }
+                } else {
+                    if (ok)
+                        ld8(xf[m], in + ((size_t)(pn[m] * a.Hin + iy) * a.Win + ix) * a.CinS + coff);
+                    else
+                        zero(xf[m]);
+                }
             }
 #pragma unroll
             for (int n = 0; n < NR; ++n) {
@@ -159,6 +126,18 @@ __global__ void __launch_bounds__(256) conv_kernel(const ConvArgs a) {
 
         // ------------------------------- epilogues -------------------------------------------
         T *out = reinterpret_cast<T *>(a.out);
+        int pmx[MR][3];
+#pragma unroll
+        for (int m = 0; m < MR; ++m)
+#pragma unroll
+            for (int c3 = 0; c3 < 3; ++c3) {
+                int v = pmax[m][c3];
+                if constexpr (EPI == EPI_INIT_BGR) {
+                    v = max(v, __shfl_xor(v, 16, 64));
+                    v = max(v, __shfl_xor(v, 32, 64));
+                }
+                pmx[m][c3] = v;
+            }
         if constexpr (EPI == EPI_CLASSES) {
             // n fragment = output phase (a,b); rows = 16 (padded) classes, 4 per lane.
 #pragma unroll
@@ -220,7 +199,21 @@ __global__ void __launch_bounds__(256) conv_kernel(const ConvArgs a) {
                         continue;
                     }
                     if (c >= a.outC) continue;
-                    if constexpr (EPI == EPI_INIT) {
+                    if constexpr (EPI == EPI_INIT_BGR) {
+                        // pool channels: max over the window of the raw bytes (the table is increasing, so
+                        // max(table(v)) == table(max(v))), reduced across the 4 lane groups above
+                        const float4 ps = ld4f(a.pscale + c);
+                        float pv4[4] = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+                        for (int r = 0; r < 4; ++r) {
+                            const int ch = c + r - a.cconv;
+                            if (ch < 0 || ch >= a.cpool) continue;
+                            const int mx = pmx[m][ch];
+                            pv4[r] = (mx >= 0 ? nl[ch * 256 + mx] : -INFINITY) * get(ps, r);
+                        }
+                        v = add4(v, make_float4(pv4[0], pv4[1], pv4[2], pv4[3]));
+                        v = prelu4(v, ld4f(a.slope1 + c));
+                    } else if constexpr (EPI == EPI_INIT) {
                         // concat(conv, maxpool(in)) -> BN -> act (InitialBlock); pool channels carry
                         // their BN as pscale (x) + bias.
                         const float4 ps = ld4f(a.pscale + c);
@@ -299,7 +292,7 @@ int conv_tile_pixels(int nr) { return 4 * (nr >= 4 ? 2 : 4) * 16; }
 
 size_t conv_lds_bytes(int prec, const ConvArgs &a) {
     const size_t es = prec == PREC_BF16 ? 2 : 4;
-    return (size_t)a.Npad * (a.Kpad + 16 / es) * es + (size_t)a.Ksteps * 4 * sizeof(int);
+    return (size_t)a.Npad * (a.Kpad + 16 / es) * es + (size_t)a.Ksteps * 4 * sizeof(int) + (a.nlut ? 3 * 256 * sizeof(float) : 0);
 }
 
 template <typename T, int NR>
@@ -312,6 +305,9 @@ static hipError_t launch_nr(int epi, const ConvArgs &a, dim3 grid, size_t lds, h
     case EPI_INIT: hipLaunchKernelGGL((conv_kernel<T, NR, EPI_INIT>), grid, dim3(256), lds, s, a); break;
     case EPI_SHUFFLE: hipLaunchKernelGGL((conv_kernel<T, NR, EPI_SHUFFLE>), grid, dim3(256), lds, s, a); break;
     case EPI_CLASSES: hipLaunchKernelGGL((conv_kernel<T, NR, EPI_CLASSES>), grid, dim3(256), lds, s, a); break;
+    case EPI_INIT_BGR:
+        if constexpr (NR == 1) { hipLaunchKernelGGL((conv_kernel<T, NR, EPI_INIT_BGR>), grid, dim3(256), lds, s, a); break; }
+        return hipErrorInvalidValue;
     default: return hipErrorInvalidValue;
     }
     return hipGetLastError();

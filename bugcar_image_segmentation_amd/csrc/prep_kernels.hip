@@ -49,6 +49,11 @@ __global__ void __launch_bounds__(256) preprocess_kernel(const PreArgs a) {
                 bgr[c] = v;
             }
         }
+        if (a.out_layout == BUGSEG_PRE_BGR_U8) {
+            uint8_t *o = reinterpret_cast<uint8_t *>(a.out) + i * 3;
+            o[0] = (uint8_t)bgr[0]; o[1] = (uint8_t)bgr[1]; o[2] = (uint8_t)bgr[2];
+            continue;
+        }
         // BGR -> RGB (models.py:89), then the normalisation table (models.py:91)
         const double r = a.lut[0 * 256 + bgr[2]], g = a.lut[1 * 256 + bgr[1]], bl = a.lut[2 * 256 + bgr[0]];
         if (a.out_layout == BUGSEG_PRE_ENGINE) {

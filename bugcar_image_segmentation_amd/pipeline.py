@@ -1,7 +1,8 @@
 """Batched, device-resident frame -> occupancy-grid path (BASELINE config 3):
 
-    BGR u8 frames (B,H0,W0,3)  --preprocess kernel-->  engine input (B,H,W,8)
-      --89 fused conv launches (ENet, argmax + 3-class remap in the last epilogue)-->  u8 (B,H,W)
+    BGR u8 frames (B,H0,W0,3)  --[resize kernel, only if H0xW0 != HxW]-->  BGR u8 (B,H,W,3)
+      --89 fused conv launches (ENet; the initial block normalises the raw bytes as it loads them,
+        argmax + 3-class remap in the last epilogue)-->  u8 (B,H,W)
       --BEV rasteriser kernel-->  int8 grids (B,h,w)   [or ROS data order]
 
 Everything stays in HBM on one stream; there is no host round trip between stages. This is the
@@ -32,9 +33,8 @@ class OccupancyPipeline:
         self._grid = None
 
     def _bufs(self, B: int, dev: torch.device):
-        es = 2 if self.model.precision == "bf16" else 4
         if self._x is None or self._x.shape[0] != B or self._x.device != dev:
-            self._x = torch.empty((B, self.H, self.W, 8 * es), dtype=torch.uint8, device=dev)
+            self._x = torch.empty((B, self.H, self.W, 3), dtype=torch.uint8, device=dev)   # resized BGR
             self._seg = torch.empty((B, self.H, self.W), dtype=torch.uint8, device=dev)
             p = self.bev.occupancy_params(*self.grid, ros_layout=self.ros_layout)
             shape = (B, p.occ_w, p.occ_h) if self.ros_layout else (B, p.occ_h, p.occ_w)
@@ -47,8 +47,12 @@ class OccupancyPipeline:
         B, H0, W0 = frames_bgr.shape[:3]
         x, seg, grid = self._bufs(B, frames_bgr.device)
         ctx = self.model.ctx
-        ctx.preprocess(frames_bgr.contiguous(), B, H0, W0, self.H, self.W, N.PRE_ENGINE, x)
-        ctx.forward(x, B, self.H, self.W, N.OUT_CLASS3_U8, seg)
+        frames = frames_bgr.contiguous()
+        if (H0, W0) != (self.H, self.W):
+            # resize only (models.py:87); colour swap + normalisation are fused into the initial block
+            ctx.preprocess(frames, B, H0, W0, self.H, self.W, N.PRE_BGR_U8, x)
+            frames = x
+        ctx.forward_bgr(frames, B, self.H, self.W, N.OUT_CLASS3_U8, seg)
         out = grid if out is None else out
         self.bev.create_occupancy_grid_device(seg, *self.grid, ros_layout=self.ros_layout, out=out)
         return out

@@ -52,7 +52,9 @@ enum {
 enum {
     BUGSEG_PRE_ENGINE = 0,      /* (B, H, W, 8) engine input, context precision                      */
     BUGSEG_PRE_NCHW_F64 = 1,    /* (B, 3, H, W) f64: exactly ENET.preprocess's array (models.py:84-95) */
-    BUGSEG_PRE_NCHW_F32 = 2     /* (B, 3, H, W) f32: what TF casts the feed to                         */
+    BUGSEG_PRE_NCHW_F32 = 2,    /* (B, 3, H, W) f32: what TF casts the feed to                         */
+    BUGSEG_PRE_BGR_U8 = 3       /* (B, H, W, 3) u8: the resized BGR frame only (models.py:87), for
+                                   bugseg_enet_forward_bgr, which fuses the rest of preprocess    */
 };
 
 /* Geometry of bev_transform_tools.create_occupancy_grid (bev.py:301-330), computed on the host
@@ -110,6 +112,13 @@ int bugseg_nchw_to_input(bugseg_ctx *ctx, const void *x_dev, int is_f64, int B, 
 int bugseg_enet_forward(bugseg_ctx *ctx, const void *in_dev, int B, int H, int W, int out_kind,
                         void *out_dev, void *stream);
 
+/* Same as bugseg_enet_forward, but reading raw BGR u8 frames (B, H, W, 3) already at the model
+ * resolution: BGR->RGB and (x/256-mean)/std (models.py:89-91) are applied while the initial block
+ * loads its input, so the normalised tensor never exists in HBM. Results are identical to
+ * bugseg_preprocess(ENGINE) followed by bugseg_enet_forward. */
+int bugseg_enet_forward_bgr(bugseg_ctx *ctx, const uint8_t *bgr_dev, int B, int H, int W, int out_kind,
+                            void *out_dev, void *stream);
+
 /* Fused BEV rasteriser over a batch of class maps: seg_dev (B, in_rows, in_cols) u8 in {0,1,2}
  * -> out_dev (B, occ_h, occ_w) int8 in {-1, 0, 100} (or the ROS layout, see ros_layout).
  * Replaces bev_transform_tools.create_occupancy_grid, non-laserscan branch (bev.py:301-381). */
@@ -117,8 +126,9 @@ int bugseg_bev_occgrid(bugseg_ctx *ctx, const uint8_t *seg_dev, int B, const bug
                        int8_t *out_dev, void *stream);
 
 /* Plan introspection for the bench / roofline: number of kernel launches of one forward and the
- * algorithmic bytes they move (activation reads + writes + weights, context precision). */
-int bugseg_plan_info(bugseg_ctx *ctx, int B, int H, int W, int out_kind, int *n_launches,
+ * algorithmic bytes they move (activation reads + writes + weights, context precision), for the
+ * engine-input entry (bgr_input = 0) or bugseg_enet_forward_bgr (bgr_input = 1). */
+int bugseg_plan_info(bugseg_ctx *ctx, int B, int H, int W, int out_kind, int bgr_input, int *n_launches,
                      double *alg_bytes, double *flops);
 
 /* Last error message of ctx (or of the calling thread when ctx is NULL). Never NULL. */

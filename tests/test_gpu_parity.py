@@ -148,6 +148,50 @@ def test_bev_occgrid_bit_exact(gpu, rows, cols, ww, wh, grid, seed):
     assert one.dtype == np.int8 and np.array_equal(one, ref[0])
 
 
+@pytest.mark.parametrize("prec", ["fp32", "bf16"])
+@pytest.mark.parametrize("pool_k", [3, 2])
+def test_forward_bgr_equals_preprocess_then_forward(gpu, prec, pool_k):
+    """The fused-preprocess entry (raw BGR into the initial block) is bit-identical to
+    preprocess(ENGINE) + forward, including the maxpool channels (pool over raw bytes)."""
+    bl = enet_spec.build_enet(seed=17, initial_pool_k=pool_k)
+    m = ENET(weights=bl, precision=prec)
+    B, H, W = 2, 64, 96
+    bgr = torch.from_numpy(synthetic.road_frames(B, H, W, seed=4)).cuda()
+    x = ENET.preprocess_device(bgr, N.PRE_ENGINE, ctx=m.ctx, width=W, height=H)
+    a = m.predict_device(x, N.OUT_LOGITS_F32)
+    b = torch.empty_like(a)
+    m.ctx.forward_bgr(bgr, B, H, W, N.OUT_LOGITS_F32, b)
+    assert torch.equal(a, b)
+    # resize-only preprocess + fused forward == full preprocess + forward
+    big = torch.from_numpy(synthetic.road_frames(B, 100, 150, seed=5)).cuda()
+    x2 = ENET.preprocess_device(big, N.PRE_ENGINE, ctx=m.ctx, width=W, height=H)
+    r = torch.empty((B, H, W, 3), dtype=torch.uint8, device=gpu)
+    m.ctx.preprocess(big, B, 100, 150, H, W, N.PRE_BGR_U8, r)
+    c = torch.empty_like(a)
+    m.ctx.forward_bgr(r, B, H, W, N.OUT_LOGITS_F32, c)
+    assert torch.equal(m.predict_device(x2, N.OUT_LOGITS_F32), c)
+
+
+@pytest.mark.parametrize("prec", ["fp32", "bf16"])
+@pytest.mark.parametrize("H,W", [(64, 96), (120, 160), (480, 640)])
+def test_fused_bottlenecks_equal_unfused(gpu, blocks, prec, H, W, monkeypatch):
+    """The fused bottleneck kernel (projection + middle conv + expansion + residual, internals in
+    LDS) rounds the internal tensors exactly as the unfused conv chain stores them: bit-identical."""
+    B = 2 if H < 480 else 1
+    bgr = torch.from_numpy(synthetic.road_frames(B, H, W, seed=H)).cuda()
+    fused = ENET(weights=blocks, precision=prec)
+    a = torch.empty((B, 15, H, W), dtype=torch.float32, device=gpu)
+    fused.ctx.forward_bgr(bgr, B, H, W, N.OUT_LOGITS_F32, a)
+    monkeypatch.setenv("BUGSEG_NO_FUSE", "1")
+    plain = ENET(weights=blocks, precision=prec)
+    b = torch.empty_like(a)
+    plain.ctx.forward_bgr(bgr, B, H, W, N.OUT_LOGITS_F32, b)
+    n_fused = fused.ctx.plan_info(B, H, W, N.OUT_LOGITS_F32)[0]
+    n_plain = plain.ctx.plan_info(B, H, W, N.OUT_LOGITS_F32)[0]
+    assert n_plain == 89 and n_fused < n_plain
+    assert torch.equal(a, b)
+
+
 def test_bev_shape_assert(gpu):
     bev = synthetic.synthetic_bev(120, 160, 300, 300)
     with pytest.raises(AssertionError):
