@@ -136,8 +136,9 @@ def main():
         t_fwd += ev[0].elapsed_time(ev[1])
         t_bev += ev[1].elapsed_time(ev[2])
     t_pre, t_fwd, t_bev = 0.0, t_fwd / reps, t_bev / reps
-    n_launch, alg_bytes, flops = model.ctx.plan_info(B, H, W, N.OUT_CLASS3_U8, bgr_input=True)
+    n_launch, alg_bytes, plan_bytes, flops = model.ctx.plan_info(B, H, W, N.OUT_CLASS3_U8, bgr_input=True)
     achieved = alg_bytes / (t_fwd * 1e-3) / 1e9
+    moved = plan_bytes / (t_fwd * 1e-3) / 1e9
     tflops = flops / (t_fwd * 1e-3) / 1e12
 
     if rank == 0:
@@ -155,8 +156,11 @@ def main():
                        "parallelism": f"frame-sharded dp{world}" + (" + RCCL all-gather of grids" if world > 1 else "")},
             "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": None,
-                         "kernel": f"ENet forward: {n_launch} conv_kernel launches (one plan), "
-                                   f"{alg_bytes / B / 1e6:.1f} MB algorithmic bytes/frame",
+                         "kernel": f"ENet forward: {n_launch} launches (conv_kernel + fused bneck_kernel, one plan); "
+                                   f"{alg_bytes / B / 1e6:.1f} MB/frame per-layer algorithmic bytes (SURVEY 8(d) "
+                                   f"definition); the fused plan must move {plan_bytes / B / 1e6:.1f} MB/frame",
+                         "plan_bytes_per_frame": round(plan_bytes / B),
+                         "plan_achieved_gbs": round(moved, 1), "plan_frac": round(moved / HBM_PEAK_GBS, 4),
                          "mfma_tflops": round(tflops, 2),
                          "mfma_frac": round(tflops / (MFMA_BF16_PEAK_TFLOPS if a.precision == "bf16" else MFMA_F32_PEAK_TFLOPS), 4)},
             "stages_ms": {"preprocess": round(t_pre, 4), "enet_forward": round(t_fwd, 4), "bev_occgrid": round(t_bev, 4)},

@@ -69,7 +69,7 @@ def load_library(path: Path | str | None = None) -> ctypes.CDLL:
             "bugseg_enet_forward_bgr": (i, [vp, vp, i, i, i, i, vp, vp]),
             "bugseg_bev_occgrid": (i, [vp, vp, i, ctypes.POINTER(BevParams), vp, vp]),
             "bugseg_plan_info": (i, [vp, i, i, i, i, i, ctypes.POINTER(i), ctypes.POINTER(ctypes.c_double),
-                                     ctypes.POINTER(ctypes.c_double)]),
+                                     ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_double)]),
             "bugseg_last_error": (cp, [vp]),
         }
         for name, (res, args) in proto.items():
@@ -154,12 +154,14 @@ class Context:
                                           stream_handle(stream)), self.h)
 
     def plan_info(self, B, H, W, out_kind, bgr_input=False):
+        """-> (launches, per-layer algorithmic bytes, plan compulsory bytes, flops) of one forward."""
         n = ctypes.c_int()
-        by = ctypes.c_double()
+        lb = ctypes.c_double()
+        pb = ctypes.c_double()
         fl = ctypes.c_double()
-        check(self.lib.bugseg_plan_info(self.h, B, H, W, out_kind, int(bool(bgr_input)), ctypes.byref(n), ctypes.byref(by),
-                                        ctypes.byref(fl)), self.h)
-        return n.value, by.value, fl.value
+        check(self.lib.bugseg_plan_info(self.h, B, H, W, out_kind, int(bool(bgr_input)), ctypes.byref(n),
+                                        ctypes.byref(lb), ctypes.byref(pb), ctypes.byref(fl)), self.h)
+        return n.value, lb.value, pb.value, fl.value
 
 
 _shared: dict[int, Context] = {}

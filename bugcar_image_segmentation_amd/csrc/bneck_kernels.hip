@@ -29,9 +29,24 @@ template <> struct BTile<16> { static constexpr int TH = 16, TW = 32; };
 int bneck_tile_h(int C) { return C == 128 ? BTile<128>::TH : BTile<64>::TH; }
 int bneck_tile_w(int C) { return C == 128 ? BTile<128>::TW : BTile<64>::TW; }
 
+// Raw 4-channel vector of T (the residual of one lane: 4 consecutive channels of one pixel)
+template <typename T> struct R4;
+template <> struct R4<__bf16> { uint2 v; };
+template <> struct R4<float> { float4 v; };
+__device__ __forceinline__ void ldr4(R4<__bf16> &r, const __bf16 *p) { r.v = *reinterpret_cast<const uint2 *>(p); }
+__device__ __forceinline__ void ldr4(R4<float> &r, const float *p) { r.v = *reinterpret_cast<const float4 *>(p); }
+__device__ __forceinline__ float4 cvt4(const R4<__bf16> &r) {
+    return make_float4(__uint_as_float(r.v.x << 16), __uint_as_float(r.v.x & 0xffff0000u),
+                       __uint_as_float(r.v.y << 16), __uint_as_float(r.v.y & 0xffff0000u));
+}
+__device__ __forceinline__ float4 cvt4(const R4<float> &r) { return r.v; }
+
+constexpr int BN_WAVES = 8;   // 512-thread workgroups: two waves per SIMD share one LDS footprint
+
 template <typename T, int C, bool ASYM>
-__global__ void __launch_bounds__(256) bneck_kernel(const BneckArgs a) {
+__global__ void __launch_bounds__(512, sizeof(T) == 2 ? 4 : 1) bneck_kernel(const BneckArgs a) {
     using Raw = typename Tr<T>::Raw;
+    constexpr int NW = BN_WAVES, NT = NW * 64;
     constexpr int I = C / 4;
     constexpr int IS = I < 8 ? 8 : I;                 // stored internal channels (8-channel groups)
     constexpr int NR1 = (I + 15) / 16;                // 16-row fragments of t0 / t1
@@ -43,10 +58,13 @@ __global__ void __launch_bounds__(256) bneck_kernel(const BneckArgs a) {
     constexpr int TH = BTile<C>::TH, TW = BTile<C>::TW;
     constexpr int PAD = 16 / (int)sizeof(T);
     constexpr int PSTR = IS + PAD;                    // LDS pixel stride (elements)
-    constexpr int NF2 = TH * TW / 64;                 // phase-2/3 fragments per wave
-    constexpr int TWA = TW + 4;                       // asymmetric: width of t1a (1x5 halo 2+2)
-    constexpr int NF2A = TH * TWA / 64;
-    static_assert(TH * TW % 64 == 0 && TH * TWA % 64 == 0, "tile must split into 4 waves of fragments");
+    constexpr int NFT = TH * TW / 16;                 // 16-pixel fragments of the tile
+    constexpr int NF2 = (NFT + NW - 1) / NW;          // ... per wave
+    constexpr int TWA = TW + 4;                       // asymmetric: width of t1a (the 1x5's halo)
+    constexpr int NFA = TH * TWA / 16;
+    constexpr int NF2A = (NFA + NW - 1) / NW;
+    constexpr int CH1 = KS1 >= 4 ? 3 : KS1 == 2 ? 6 : 8;   // phase-1 fragments whose loads fly together
+    static_assert(NFT % NW == 0, "tile fragments must split evenly over the waves");
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
 
     const int tid = threadIdx.x;
@@ -61,7 +79,7 @@ __global__ void __launch_bounds__(256) bneck_kernel(const BneckArgs a) {
         auto stage = [&](T *dst, const void *src, int rows, int kpad, int kstride) {
             const int cpr = kpad * (int)sizeof(T) / 16;
             const uint4 *s = reinterpret_cast<const uint4 *>(src);
-            for (int i = tid; i < rows * cpr; i += 256) {
+            for (int i = tid; i < rows * cpr; i += NT) {
                 const int r = i / cpr, c = i - r * cpr;
                 *reinterpret_cast<uint4 *>(reinterpret_cast<unsigned char *>(dst + (size_t)r * kstride) + c * 16) = s[i];
             }
@@ -89,40 +107,68 @@ __global__ void __launch_bounds__(256) bneck_kernel(const BneckArgs a) {
         const T *xn = x + (size_t)n * a.H * a.W * C;
         __syncthreads();   // weights staged (first tile) / previous tile done with ts
 
-        // ---- phase 1: t0 = act1(W1 x + b1) over tile + halo, 0 outside the image
-        for (int f = wave; f < nf1; f += 4) {
-            const int h = f * 16 + col;
-            const int hy = h / HWW, hx = h - hy * HWW;
-            const int iy = ty0 - ry + hy, ix = tx0 - rx + hx;
-            const bool ok = h < HR && (unsigned)iy < (unsigned)a.H && (unsigned)ix < (unsigned)a.W;
-            f32x4 acc[NR1];
+        // ---- phase 1: t0 = act1(W1 x + b1) over tile + halo, 0 outside the image. The loads of CH1
+        // fragments are issued together before any of them is consumed (memory-level parallelism).
+        for (int f0 = wave; f0 < nf1; f0 += NW * CH1) {
+            Raw xf[CH1][KS1];
+            bool okc[CH1];
 #pragma unroll
-            for (int r = 0; r < NR1; ++r) acc[r] = (f32x4){0.f, 0.f, 0.f, 0.f};
+            for (int c = 0; c < CH1; ++c) {
+                const int h = (f0 + c * NW) * 16 + col;
+                const int hy = h / HWW, hx = h - hy * HWW;
+                const int iy = ty0 - ry + hy, ix = tx0 - rx + hx;
+                okc[c] = h < HR && (unsigned)iy < (unsigned)a.H && (unsigned)ix < (unsigned)a.W;
 #pragma unroll
-            for (int s = 0; s < KS1; ++s) {
-                const int g = s * 4 + kq;
-                Raw xf;
-                if (ok && g < G1) ld8(xf, xn + ((size_t)iy * a.W + ix) * C + g * 8);
-                else zero(xf);
-#pragma unroll
-                for (int r = 0; r < NR1; ++r) {
-                    Raw wf;
-                    ld8(wf, w1 + (r * 16 + col) * K1S + s * 32 + kq * 8);
-                    mma(acc[r], wf, xf);
+                for (int s = 0; s < KS1; ++s) {
+                    const int g = s * 4 + kq;
+                    if (okc[c] && g < G1) ld8(xf[c][s], xn + ((size_t)iy * a.W + ix) * C + g * 8);
+                    else zero(xf[c][s]);
                 }
             }
-            if (h < HR) {
 #pragma unroll
-                for (int r = 0; r < NR1; ++r) {
-                    const int c = r * 16 + kq * 4;
-                    if (c >= IS) continue;
-                    float4 v = prelu4(add4(f4(acc[r]), ld4f(a.b1 + c)), ld4f(a.s1 + c));
-                    if (!ok) v = make_float4(0.f, 0.f, 0.f, 0.f);
-                    st4(ts + h * PSTR + c, v);
+            for (int c = 0; c < CH1; ++c) {
+                const int h = (f0 + c * NW) * 16 + col;
+                f32x4 acc[NR1];
+#pragma unroll
+                for (int r = 0; r < NR1; ++r) acc[r] = (f32x4){0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+                for (int s = 0; s < KS1; ++s)
+#pragma unroll
+                    for (int r = 0; r < NR1; ++r) {
+                        Raw wf;
+                        ld8(wf, w1 + (r * 16 + col) * K1S + s * 32 + kq * 8);
+                        mma(acc[r], wf, xf[c][s]);
+                    }
+                if (h < HR) {
+#pragma unroll
+                    for (int r = 0; r < NR1; ++r) {
+                        const int ch = r * 16 + kq * 4;
+                        if (ch >= IS) continue;
+                        float4 v = prelu4(add4(f4(acc[r]), ld4f(a.b1 + ch)), ld4f(a.s1 + ch));
+                        if (!okc[c]) v = make_float4(0.f, 0.f, 0.f, 0.f);
+                        st4(ts + h * PSTR + ch, v);
+                    }
                 }
             }
         }
         __syncthreads();
+
+        // residual of phase 3, prefetched early so its latency hides behind phase 2 (asymmetric:
+        // after its 5x1 pass, to keep the two passes' live ranges apart)
+        R4<T> res[NF2][NR3];
+        auto prefetch_res = [&]() {
+#pragma unroll
+            for (int j = 0; j < NF2; ++j) {
+                const int p = (wave + NW * j) * 16 + col;
+                const int oy = p / TW, ox = p - oy * TW;
+                const int iy = ty0 + oy, ix = tx0 + ox;
+                const bool ok = (unsigned)iy < (unsigned)a.H && (unsigned)ix < (unsigned)a.W;
+                const size_t po = ((size_t)(ok ? iy : 0) * a.W + (ok ? ix : 0)) * C;
+#pragma unroll
+                for (int r = 0; r < NR3; ++r) ldr4(res[j][r], xn + po + r * 16 + kq * 4);
+            }
+        };
+        if constexpr (!ASYM) prefetch_res();
 
         // ---- phase 2: t1 = act2(W2 * t0 + b2) (asymmetric: t1a = 5x1 (t0); t1 = 1x5 (t1a))
         if constexpr (!ASYM) {
@@ -131,7 +177,7 @@ __global__ void __launch_bounds__(256) bneck_kernel(const BneckArgs a) {
             for (int j = 0; j < NF2; ++j)
 #pragma unroll
                 for (int r = 0; r < NR1; ++r) acc[j][r] = (f32x4){0.f, 0.f, 0.f, 0.f};
-#pragma unroll
+#pragma unroll 1
             for (int s = 0; s < KS2; ++s) {
                 const int g = s * 4 + kq;
                 const int tap = g / (IS / 8), coff = (g - tap * (IS / 8)) * 8;
@@ -141,7 +187,7 @@ __global__ void __launch_bounds__(256) bneck_kernel(const BneckArgs a) {
                 for (int r = 0; r < NR1; ++r) ld8(wf[r], w2 + (r * 16 + col) * K2S + s * 32 + kq * 8);
 #pragma unroll
                 for (int j = 0; j < NF2; ++j) {
-                    const int p = (wave + 4 * j) * 16 + col;
+                    const int p = (wave + NW * j) * 16 + col;
                     const int oy = p / TW, ox = p - oy * TW;
                     Raw xf;
                     if (g < G2) ld8(xf, ts + ((oy + ry + dy) * HWW + (ox + rx + dx)) * PSTR + coff);
@@ -153,12 +199,12 @@ __global__ void __launch_bounds__(256) bneck_kernel(const BneckArgs a) {
             __syncthreads();   // every wave is done reading t0
 #pragma unroll
             for (int j = 0; j < NF2; ++j) {
-                const int p = (wave + 4 * j) * 16 + col;
+                const int p = (wave + NW * j) * 16 + col;
 #pragma unroll
                 for (int r = 0; r < NR1; ++r) {
-                    const int c = r * 16 + kq * 4;
-                    if (c >= IS) continue;
-                    st4(ts + p * PSTR + c, prelu4(add4(f4(acc[j][r]), ld4f(a.b2 + c)), ld4f(a.s2 + c)));
+                    const int ch = r * 16 + kq * 4;
+                    if (ch >= IS) continue;
+                    st4(ts + p * PSTR + ch, prelu4(add4(f4(acc[j][r]), ld4f(a.b2 + ch)), ld4f(a.s2 + ch)));
                 }
             }
         } else {
@@ -168,7 +214,7 @@ __global__ void __launch_bounds__(256) bneck_kernel(const BneckArgs a) {
                 for (int j = 0; j < NF2A; ++j)
 #pragma unroll
                     for (int r = 0; r < NR1; ++r) acc[j][r] = (f32x4){0.f, 0.f, 0.f, 0.f};
-#pragma unroll
+#pragma unroll 1
                 for (int s = 0; s < KS2; ++s) {
                     const int g = s * 4 + kq;
                     const int tap = g / (IS / 8), coff = (g - tap * (IS / 8)) * 8;
@@ -177,10 +223,11 @@ __global__ void __launch_bounds__(256) bneck_kernel(const BneckArgs a) {
                     for (int r = 0; r < NR1; ++r) ld8(wf[r], w2 + (r * 16 + col) * K2S + s * 32 + kq * 8);
 #pragma unroll
                     for (int j = 0; j < NF2A; ++j) {
-                        const int p = (wave + 4 * j) * 16 + col;
+                        const int f = wave + NW * j;
+                        const int p = f * 16 + col;
                         const int oy = p / TWA, ox = p - oy * TWA;
                         Raw xf;
-                        if (g < G2) ld8(xf, ts + ((oy + ry + tap - 2) * HWW + ox) * PSTR + coff);
+                        if (g < G2 && f < NFA) ld8(xf, ts + ((oy + ry + tap - 2) * HWW + ox) * PSTR + coff);
                         else zero(xf);
 #pragma unroll
                         for (int r = 0; r < NR1; ++r) mma(acc[j][r], wf[r], xf);
@@ -189,27 +236,30 @@ __global__ void __launch_bounds__(256) bneck_kernel(const BneckArgs a) {
                 __syncthreads();
 #pragma unroll
                 for (int j = 0; j < NF2A; ++j) {
-                    const int p = (wave + 4 * j) * 16 + col;
+                    const int f = wave + NW * j;
+                    if (f >= NFA) continue;
+                    const int p = f * 16 + col;
                     const int ox = p - (p / TWA) * TWA;
                     const bool inside = (unsigned)(tx0 - 2 + ox) < (unsigned)a.W;   // the 1x5 zero-pads t1a
 #pragma unroll
                     for (int r = 0; r < NR1; ++r) {
-                        const int c = r * 16 + kq * 4;
-                        if (c >= IS) continue;
-                        float4 v = prelu4(add4(f4(acc[j][r]), ld4f(a.b2 + c)), ld4f(a.s2 + c));
+                        const int ch = r * 16 + kq * 4;
+                        if (ch >= IS) continue;
+                        float4 v = prelu4(add4(f4(acc[j][r]), ld4f(a.b2 + ch)), ld4f(a.s2 + ch));
                         if (!inside) v = make_float4(0.f, 0.f, 0.f, 0.f);
-                        st4(ts + p * PSTR + c, v);
+                        st4(ts + p * PSTR + ch, v);
                     }
                 }
                 __syncthreads();
             }
+            prefetch_res();
             {   // 1x5 over columns (taps dx = -2..2)
                 f32x4 acc[NF2][NR1];
 #pragma unroll
                 for (int j = 0; j < NF2; ++j)
 #pragma unroll
                     for (int r = 0; r < NR1; ++r) acc[j][r] = (f32x4){0.f, 0.f, 0.f, 0.f};
-#pragma unroll
+#pragma unroll 1
                 for (int s = 0; s < KS2; ++s) {
                     const int g = s * 4 + kq;
                     const int tap = g / (IS / 8), coff = (g - tap * (IS / 8)) * 8;
@@ -218,7 +268,7 @@ __global__ void __launch_bounds__(256) bneck_kernel(const BneckArgs a) {
                     for (int r = 0; r < NR1; ++r) ld8(wf[r], w2b + (r * 16 + col) * K2S + s * 32 + kq * 8);
 #pragma unroll
                     for (int j = 0; j < NF2; ++j) {
-                        const int p = (wave + 4 * j) * 16 + col;
+                        const int p = (wave + NW * j) * 16 + col;
                         const int oy = p / TW, ox = p - oy * TW;
                         Raw xf;
                         if (g < G2) ld8(xf, ts + (oy * TWA + ox + tap) * PSTR + coff);
@@ -230,45 +280,39 @@ __global__ void __launch_bounds__(256) bneck_kernel(const BneckArgs a) {
                 __syncthreads();
 #pragma unroll
                 for (int j = 0; j < NF2; ++j) {
-                    const int p = (wave + 4 * j) * 16 + col;
+                    const int p = (wave + NW * j) * 16 + col;
 #pragma unroll
                     for (int r = 0; r < NR1; ++r) {
-                        const int c = r * 16 + kq * 4;
-                        if (c >= IS) continue;
-                        st4(ts + p * PSTR + c, prelu4(add4(f4(acc[j][r]), ld4f(a.b2b + c)), ld4f(a.s2b + c)));
+                        const int ch = r * 16 + kq * 4;
+                        if (ch >= IS) continue;
+                        st4(ts + p * PSTR + ch, prelu4(add4(f4(acc[j][r]), ld4f(a.b2b + ch)), ld4f(a.s2b + ch)));
                     }
                 }
             }
         }
         __syncthreads();
 
-        // ---- phase 3: out = act_out(act3(W3 t1 + b3) + x), fragment by fragment
-#pragma unroll 1
+        // ---- phase 3: out = act_out(act3(W3 t1 + b3) + x)
+#pragma unroll
         for (int j = 0; j < NF2; ++j) {
-            const int p = (wave + 4 * j) * 16 + col;
+            const int p = (wave + NW * j) * 16 + col;
             const int oy = p / TW, ox = p - oy * TW;
             const int iy = ty0 + oy, ix = tx0 + ox;
             const bool ok = (unsigned)iy < (unsigned)a.H && (unsigned)ix < (unsigned)a.W;
             Raw tf;
             if (kq < G3) ld8(tf, ts + p * PSTR + kq * 8);
             else zero(tf);
-            f32x4 acc[NR3];
+            const size_t po = ((size_t)n * a.H * a.W + (size_t)iy * a.W + ix) * C;
 #pragma unroll
             for (int r = 0; r < NR3; ++r) {
-                acc[r] = (f32x4){0.f, 0.f, 0.f, 0.f};
+                f32x4 acc = (f32x4){0.f, 0.f, 0.f, 0.f};
                 Raw wf;
                 ld8(wf, w3 + (r * 16 + col) * K3S + kq * 8);
-                mma(acc[r], wf, tf);
-            }
-            if (ok) {
-                const size_t po = ((size_t)iy * a.W + ix) * C;
-#pragma unroll
-                for (int r = 0; r < NR3; ++r) {
-                    const int c = r * 16 + kq * 4;
-                    float4 v = prelu4(add4(f4(acc[r]), ld4f(a.b3 + c)), ld4f(a.s3 + c));
-                    v = prelu4(add4(v, ld4(xn + po + c)), ld4f(a.s_out + c));
-                    st4(out + (size_t)n * a.H * a.W * C + po + c, v);
-                }
+                mma(acc, wf, tf);
+                const int ch = r * 16 + kq * 4;
+                float4 v = prelu4(add4(f4(acc), ld4f(a.b3 + ch)), ld4f(a.s3 + ch));
+                v = prelu4(add4(v, cvt4(res[j][r])), ld4f(a.s_out + ch));
+                if (ok) st4(out + po + ch, v);
             }
         }
     }
@@ -289,8 +333,8 @@ template <typename T>
 static hipError_t launch_t(int C, bool asym, const BneckArgs &a, dim3 g, size_t lds, hipStream_t s) {
 #define BN_CASE(CC)                                                                                     \
     if (C == CC) {                                                                                      \
-        if (asym) hipLaunchKernelGGL((bneck_kernel<T, CC, true>), g, dim3(256), lds, s, a);            \
-        else hipLaunchKernelGGL((bneck_kernel<T, CC, false>), g, dim3(256), lds, s, a);                \
+        if (asym) hipLaunchKernelGGL((bneck_kernel<T, CC, true>), g, dim3(BN_WAVES * 64), lds, s, a);            \
+        else hipLaunchKernelGGL((bneck_kernel<T, CC, false>), g, dim3(BN_WAVES * 64), lds, s, a);                \
         return hipGetLastError();                                                                       \
     }
     BN_CASE(128)

@@ -62,6 +62,11 @@ struct Op {
     int bn_c = 0;
     bool bn_asym = false;
     double bytes = 0, flops = 0;
+    double layer_bytes = -1;   // per-layer (unfused) algorithmic bytes of the work; -1: same as bytes
+    Op() {
+        std::memset(&a, 0, sizeof(a));
+        std::memset(&bn, 0, sizeof(bn));
+    }
 };
 
 struct Plan {
@@ -600,10 +605,16 @@ struct Walker {
                         q.w2b = dw + p2b.o_w; q.b2b = (const float *)(dw + p2b.o_bias); q.s2b = (const float *)(dw + p2b.o_s1);
                         q.w3 = dw + p3.o_w; q.b3 = (const float *)(dw + p3.o_bias); q.s3 = (const float *)(dw + p3.o_s1);
                         q.s_out = (const float *)(dw + p3.o_s2);
-                        double fl = 0, wb = 0;
-                        for (int i = 0; i < nu; ++i) { fl += 2.0 * P(i).macs_per_px * B * cur.H * cur.W; wb += (double)P(i).Npad * P(i).Kpad * es; }
+                        double fl = 0, wb = 0, lb = 0;
+                        const double px = (double)B * cur.H * cur.W;
+                        for (int i = 0; i < nu; ++i) {
+                            fl += 2.0 * P(i).macs_per_px * px;
+                            wb += (double)P(i).Npad * P(i).Kpad * es;
+                            lb += px * (cstore(b.units[i].cin) + cstore(b.units[i].cout)) * es;   // layer by layer
+                        }
                         op.flops = fl;
-                        op.bytes = 2.0 * B * cur.H * cur.W * cur.C * es + wb;
+                        op.bytes = 2.0 * px * cur.C * es + wb;             // what this launch must move
+                        op.layer_bytes = lb + px * cur.C * es + wb;        // + the residual re-read
                         ops.push_back(op);
                     }
                     break;
@@ -692,7 +703,7 @@ bool build_plan(bugseg_ctx *ctx, int B, int H, int W, std::string &why) {
     for (size_t i = 0; i < w.szIdx.size(); ++i) if (w.szIdx[i]) { w.idx[i] = p; p += al(w.szIdx[i]); }
     if (!w.run(true, why)) return false;
     for (const Op &op : w.ops) {
-        const double elems = (double)op.a.M * 128.0;
+        const double elems = op.kind == 1 ? (double)op.bn.B * op.bn.H * op.bn.W * op.bn_c : (double)op.a.M * 128.0;
         if (elems > 2.0e9) { why = "batch too large for 32-bit pixel indexing"; return false; }
     }
     pl.ops = std::move(w.ops);
@@ -945,20 +956,25 @@ int bugseg_bev_occgrid(bugseg_ctx *ctx, const uint8_t *seg, int B, const bugseg_
 }
 
 int bugseg_plan_info(bugseg_ctx *ctx, int B, int H, int W, int out_kind, int bgr_input, int *n_launches, double *alg_bytes,
-                     double *flops) {
+                     double *plan_bytes, double *flops) {
     if (!ctx) return fail(ctx, BUGSEG_EINVAL, "NULL ctx");
     if (!ctx->loaded) return fail(ctx, BUGSEG_ESTATE, "no weights loaded");
     DeviceGuard g(ctx->device);
     std::string why;
     if (!build_plan(ctx, B, H, W, why)) return fail(ctx, BUGSEG_EINVAL, why);
-    double by = 0, fl = 0;
-    for (const Op &op : ctx->plan.ops) { by += op.bytes; fl += op.flops; }
+    double lb = 0, pb = 0, fl = 0;
+    for (const Op &op : ctx->plan.ops) {
+        pb += op.bytes;
+        lb += op.layer_bytes >= 0 ? op.layer_bytes : op.bytes;
+        fl += op.flops;
+    }
     // final epilogue output
-    by += out_kind == BUGSEG_OUT_LOGITS_F32 ? (double)B * H * W * ctx->ncls * 4 : (double)B * H * W;
+    const double fin = out_kind == BUGSEG_OUT_LOGITS_F32 ? (double)B * H * W * ctx->ncls * 4 : (double)B * H * W;
     // raw BGR input (bugseg_enet_forward_bgr): 3 bytes per pixel instead of the 8-channel engine input
-    if (bgr_input) by -= (double)B * H * W * (8.0 * (ctx->prec == PREC_BF16 ? 2 : 4) - 3.0);
+    const double adj = bgr_input ? (double)B * H * W * (8.0 * (ctx->prec == PREC_BF16 ? 2 : 4) - 3.0) : 0.0;
     if (n_launches) *n_launches = (int)ctx->plan.ops.size();
-    if (alg_bytes) *alg_bytes = by;
+    if (alg_bytes) *alg_bytes = lb + fin - adj;
+    if (plan_bytes) *plan_bytes = pb + fin - adj;
     if (flops) *flops = fl;
     return BUGSEG_OK;
 }

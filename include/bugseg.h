@@ -125,11 +125,16 @@ int bugseg_enet_forward_bgr(bugseg_ctx *ctx, const uint8_t *bgr_dev, int B, int 
 int bugseg_bev_occgrid(bugseg_ctx *ctx, const uint8_t *seg_dev, int B, const bugseg_bev_params *p,
                        int8_t *out_dev, void *stream);
 
-/* Plan introspection for the bench / roofline: number of kernel launches of one forward and the
- * algorithmic bytes they move (activation reads + writes + weights, context precision), for the
- * engine-input entry (bgr_input = 0) or bugseg_enet_forward_bgr (bgr_input = 1). */
+/* Plan introspection for the bench / roofline, for the engine-input entry (bgr_input = 0) or
+ * bugseg_enet_forward_bgr (bgr_input = 1), context precision:
+ *   n_launches  kernel launches of one forward;
+ *   alg_bytes   the network's per-layer algorithmic traffic (every convolution reads its input and
+ *               writes its output once, residual branches re-read the block input, weights once per
+ *               layer) — a property of the model and shape, the SURVEY.md §8(d) definition;
+ *   plan_bytes  the compulsory traffic of this plan (fused launches keep internals on chip);
+ *   flops       2 x MACs. */
 int bugseg_plan_info(bugseg_ctx *ctx, int B, int H, int W, int out_kind, int bgr_input, int *n_launches,
-                     double *alg_bytes, double *flops);
+                     double *alg_bytes, double *plan_bytes, double *flops);
 
 /* Last error message of ctx (or of the calling thread when ctx is NULL). Never NULL. */
 const char *bugseg_last_error(const bugseg_ctx *ctx);

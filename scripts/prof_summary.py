@@ -19,12 +19,12 @@ def main(prof_dir, bench_json, out_md):
     if bench_json:
         js = [ln for ln in Path(bench_json).read_text().splitlines() if ln.startswith('{"metric"')]
         bench = json.loads(js[-1]) if js else None
-    n_fwd = sum(1 for r in trace if "preprocess_kernel" in r["Kernel_Name"])
-    conv = [r for r in trace if "conv_kernel" in r["Kernel_Name"]]
+    n_fwd = sum(1 for r in trace if "bev_occgrid_kernel" in r["Kernel_Name"])   # one per pipeline step
+    conv = [r for r in trace if "conv_kernel" in r["Kernel_Name"] or "bneck_kernel" in r["Kernel_Name"]]
     per_fwd_launches = len(conv) / max(1, n_fwd)
     conv_ns = sum(int(r["End_Timestamp"]) - int(r["Start_Timestamp"]) for r in conv)
     lines = [f"# rocprofv3 kernel summary: {prof_dir.name}", "",
-             f"forwards in trace: {n_fwd}; conv launches per forward: {per_fwd_launches:.1f}", "",
+             f"forwards in trace: {n_fwd}; ENet launches (conv_kernel + bneck_kernel) per forward: {per_fwd_launches:.1f}", "",
              "| kernel | calls | avg us | total ms | per forward us | % |", "|---|---|---|---|---|---|"]
     for r in stats:
         name = r["Name"]
@@ -33,7 +33,7 @@ def main(prof_dir, bench_json, out_md):
                      f"{int(r['TotalDurationNs']) / 1e6:.3f} | {int(r['TotalDurationNs']) / 1e3 / max(1, n_fwd):.1f} | "
                      f"{float(r['Percentage']):.2f} |")
     fwd_ms = conv_ns / 1e6 / max(1, n_fwd)
-    lines += ["", f"**ENet forward, sum of conv_kernel durations per forward: {fwd_ms:.4f} ms**"]
+    lines += ["", f"**ENet forward, sum of conv_kernel + bneck_kernel durations per forward: {fwd_ms:.4f} ms**"]
     if bench:
         lines += [f"bench.py event-timed enet_forward: {bench['stages_ms']['enet_forward']:.4f} ms "
                   f"(profiled run; the profiler clocks differ slightly, MI355X_MICROARCH.md 'DVFS give-back' (2))",
