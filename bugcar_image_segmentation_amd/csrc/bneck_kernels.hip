@@ -29,17 +29,6 @@ template <> struct BTile<16> { static constexpr int TH = 16, TW = 32; };
 int bneck_tile_h(int C) { return C == 128 ? BTile<128>::TH : BTile<64>::TH; }
 int bneck_tile_w(int C) { return C == 128 ? BTile<128>::TW : BTile<64>::TW; }
 
-// Raw 4-channel vector of T (the residual of one lane: 4 consecutive channels of one pixel)
-template <typename T> struct R4;
-template <> struct R4<__bf16> { uint2 v; };
-template <> struct R4<float> { float4 v; };
-__device__ __forceinline__ void ldr4(R4<__bf16> &r, const __bf16 *p) { r.v = *reinterpret_cast<const uint2 *>(p); }
-__device__ __forceinline__ void ldr4(R4<float> &r, const float *p) { r.v = *reinterpret_cast<const float4 *>(p); }
-__device__ __forceinline__ float4 cvt4(const R4<__bf16> &r) {
-    return make_float4(__uint_as_float(r.v.x << 16), __uint_as_float(r.v.x & 0xffff0000u),
-                       __uint_as_float(r.v.y << 16), __uint_as_float(r.v.y & 0xffff0000u));
-}
-__device__ __forceinline__ float4 cvt4(const R4<float> &r) { return r.v; }
 
 constexpr int BN_WAVES = 8;   // 512-thread workgroups: two waves per SIMD share one LDS footprint
 
@@ -63,7 +52,11 @@ __global__ void __launch_bounds__(512, sizeof(T) == 2 ? 4 : 1) bneck_kernel(cons
     constexpr int TWA = TW + 4;                       // asymmetric: width of t1a (the 1x5's halo)
     constexpr int NFA = TH * TWA / 16;
     constexpr int NF2A = (NFA + NW - 1) / NW;
-    constexpr int CH1 = KS1 >= 4 ? 3 : KS1 == 2 ? 6 : 8;   // phase-1 fragments whose loads fly together
+    constexpr int CH1 = KS1 >= 4 ? 3 : KS1 == 2 ? 4 : 8;   // phase-1 fragments whose loads fly together
+    constexpr int EPC = 16 / (int)sizeof(T);          // elements per 16-B chunk
+    constexpr int CPF = 16 * C / EPC;                 // 16-B chunks of one 16-pixel output fragment
+    constexpr int CPL = (CPF + 63) / 64;              // ... per lane
+    constexpr int OSTR = C + EPC;                     // phase-3 staging row stride (16-B padded)
     static_assert(NFT % NW == 0, "tile fragments must split evenly over the waves");
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
 
@@ -121,7 +114,7 @@ __global__ void __launch_bounds__(512, sizeof(T) == 2 ? 4 : 1) bneck_kernel(cons
 #pragma unroll
                 for (int s = 0; s < KS1; ++s) {
                     const int g = s * 4 + kq;
-                    if (okc[c] && g < G1) ld8(xf[c][s], xn + ((size_t)iy * a.W + ix) * C + g * 8);
+                    if (okc[c] && g < G1 && !(a.ablate & 1)) ld8(xf[c][s], xn + ((size_t)iy * a.W + ix) * C + g * 8);
                     else zero(xf[c][s]);
                 }
             }
@@ -153,19 +146,23 @@ __global__ void __launch_bounds__(512, sizeof(T) == 2 ? 4 : 1) bneck_kernel(cons
         }
         __syncthreads();
 
-        // residual of phase 3, prefetched early so its latency hides behind phase 2 (asymmetric:
-        // after its 5x1 pass, to keep the two passes' live ranges apart)
-        R4<T> res[NF2][NR3];
+        // residual of phase 3 (x at the tile pixels), prefetched early (asymmetric: after its 5x1 pass,
+        // to keep the two passes' live ranges apart) with coalesced 16-B loads: a fragment is 16
+        // consecutive pixels of one tile row, i.e. one contiguous run of 16*C elements of x.
+        uint4 res[NF2][CPL];
         auto prefetch_res = [&]() {
 #pragma unroll
             for (int j = 0; j < NF2; ++j) {
-                const int p = (wave + NW * j) * 16 + col;
-                const int oy = p / TW, ox = p - oy * TW;
-                const int iy = ty0 + oy, ix = tx0 + ox;
-                const bool ok = (unsigned)iy < (unsigned)a.H && (unsigned)ix < (unsigned)a.W;
-                const size_t po = ((size_t)(ok ? iy : 0) * a.W + (ok ? ix : 0)) * C;
+                const int p0 = (wave + NW * j) * 16;
+                const int oy = p0 / TW, ox0 = p0 - oy * TW, iy = ty0 + oy;
 #pragma unroll
-                for (int r = 0; r < NR3; ++r) ldr4(res[j][r], xn + po + r * 16 + kq * 4);
+                for (int k = 0; k < CPL; ++k) {
+                    const int q = lane + 64 * k;
+                    const int ix = tx0 + ox0 + q * EPC / C;
+                    const bool ok = q < CPF && (unsigned)iy < (unsigned)a.H && (unsigned)ix < (unsigned)a.W;
+                    res[j][k] = ok ? *reinterpret_cast<const uint4 *>(xn + ((size_t)iy * a.W + tx0 + ox0) * C + q * EPC)
+                                   : make_uint4(0, 0, 0, 0);
+                }
             }
         };
         if constexpr (!ASYM) prefetch_res();
@@ -192,6 +189,7 @@ __global__ void __launch_bounds__(512, sizeof(T) == 2 ? 4 : 1) bneck_kernel(cons
                     Raw xf;
                     if (g < G2) ld8(xf, ts + ((oy + ry + dy) * HWW + (ox + rx + dx)) * PSTR + coff);
                     else zero(xf);
+                    if (a.ablate & 2) continue;
 #pragma unroll
                     for (int r = 0; r < NR1; ++r) mma(acc[j][r], wf[r], xf);
                 }
@@ -252,7 +250,6 @@ __global__ void __launch_bounds__(512, sizeof(T) == 2 ? 4 : 1) bneck_kernel(cons
                 }
                 __syncthreads();
             }
-            prefetch_res();
             {   // 1x5 over columns (taps dx = -2..2)
                 f32x4 acc[NF2][NR1];
 #pragma unroll
@@ -277,6 +274,7 @@ __global__ void __launch_bounds__(512, sizeof(T) == 2 ? 4 : 1) bneck_kernel(cons
                         for (int r = 0; r < NR1; ++r) mma(acc[j][r], wf[r], xf);
                     }
                 }
+                prefetch_res();
                 __syncthreads();
 #pragma unroll
                 for (int j = 0; j < NF2; ++j) {
@@ -292,28 +290,52 @@ __global__ void __launch_bounds__(512, sizeof(T) == 2 ? 4 : 1) bneck_kernel(cons
         }
         __syncthreads();
 
-        // ---- phase 3: out = act_out(act3(W3 t1 + b3) + x)
+        // ---- phase 3: out = act_out(act3(W3 t1 + b3) + x). The t1 fragments go to registers, then
+        // the t1 region becomes per-wave staging: residual chunks in, results over them, and the
+        // fragment leaves as contiguous 16-B-per-lane stores (a per-lane NHWC store would write
+        // 16 partial lines per instruction: the ablation showed stores dominating this kernel).
+        Raw tf[NF2];
 #pragma unroll
         for (int j = 0; j < NF2; ++j) {
             const int p = (wave + NW * j) * 16 + col;
-            const int oy = p / TW, ox = p - oy * TW;
-            const int iy = ty0 + oy, ix = tx0 + ox;
-            const bool ok = (unsigned)iy < (unsigned)a.H && (unsigned)ix < (unsigned)a.W;
-            Raw tf;
-            if (kq < G3) ld8(tf, ts + p * PSTR + kq * 8);
-            else zero(tf);
-            const size_t po = ((size_t)n * a.H * a.W + (size_t)iy * a.W + ix) * C;
+            if (kq < G3) ld8(tf[j], ts + p * PSTR + kq * 8);
+            else zero(tf[j]);
+        }
+        __syncthreads();
+        T *stg = ts + wave * 16 * OSTR;
+        T *outn = out + (size_t)n * a.H * a.W * C;
+#pragma unroll
+        for (int j = 0; j < NF2; ++j) {
+            const int p0 = (wave + NW * j) * 16;
+            const int oy = p0 / TW, ox0 = p0 - oy * TW, iy = ty0 + oy;
+#pragma unroll
+            for (int k = 0; k < CPL; ++k) {
+                const int q = lane + 64 * k;
+                if (q < CPF) *reinterpret_cast<uint4 *>(stg + (q * EPC / C) * OSTR + (q * EPC) % C) = res[j][k];
+            }
+            wave_lds_sync();
 #pragma unroll
             for (int r = 0; r < NR3; ++r) {
                 f32x4 acc = (f32x4){0.f, 0.f, 0.f, 0.f};
                 Raw wf;
                 ld8(wf, w3 + (r * 16 + col) * K3S + kq * 8);
-                mma(acc, wf, tf);
+                mma(acc, wf, tf[j]);
                 const int ch = r * 16 + kq * 4;
+                T *sp = stg + col * OSTR + ch;
                 float4 v = prelu4(add4(f4(acc), ld4f(a.b3 + ch)), ld4f(a.s3 + ch));
-                v = prelu4(add4(v, cvt4(res[j][r])), ld4f(a.s_out + ch));
-                if (ok) st4(out + po + ch, v);
+                v = prelu4(add4(v, ld4(sp)), ld4f(a.s_out + ch));
+                st4(sp, v);
             }
+            wave_lds_sync();
+#pragma unroll
+            for (int k = 0; k < CPL; ++k) {
+                const int q = lane + 64 * k;
+                const int ix = tx0 + ox0 + q * EPC / C;
+                if (q < CPF && (unsigned)iy < (unsigned)a.H && (unsigned)ix < (unsigned)a.W && !(a.ablate & 4))
+                    *reinterpret_cast<uint4 *>(outn + ((size_t)iy * a.W + tx0 + ox0) * C + q * EPC) =
+                        *reinterpret_cast<const uint4 *>(stg + (q * EPC / C) * OSTR + (q * EPC) % C);
+            }
+            wave_lds_sync();
         }
     }
 }
@@ -325,8 +347,9 @@ size_t bneck_lds_bytes(int prec, int C, bool asym, int ry, int rx) {
     const int TH = bneck_tile_h(C), TW = bneck_tile_w(C);
     const size_t wts = (size_t)NR1 * 16 * (KS1 * 32 + pad) + (size_t)NR1 * 16 * (KS2 * 32 + pad) * (asym ? 2 : 1) +
                        (size_t)C * (32 + pad);
-    const size_t halo = (size_t)(TH + 2 * ry) * (TW + 2 * rx);
-    return (wts + halo * (IS + pad)) * es;
+    const size_t halo = (size_t)(TH + 2 * ry) * (TW + 2 * rx) * (IS + pad);
+    const size_t stage = (size_t)BN_WAVES * 16 * (C + pad);            // phase-3 output staging
+    return (wts + (halo > stage ? halo : stage)) * es;
 }
 
 template <typename T>

@@ -49,6 +49,8 @@ struct ConvArgs {
     float *logits_out;   // EPI_CLASSES: (B, ncls, Hout, Wout) f32 NCHW, may be nullptr
     const double *nlut;  // EPI_INIT_BGR: [3][256] normalisation table, RGB order (models.py:91)
     int ntiles;
+    int stg_elems;       // per-wave output staging (elements); 0 for EPI_CLASSES
+    int stage_ok;        // EPI_SHUFFLE: fragments never straddle an input row (Wg % 16 == 0, M % 16 == 0)
 };
 
 // Launch one convolution. nr = Npad / 16 in {1, 2, 4, 8}. Returns hipSuccess or the launch error.
@@ -64,6 +66,7 @@ struct BneckArgs {
     int B, H, W;
     int ry, rx, d;       // halo of the middle conv (rows, cols) and its dilation
     int tiles_x, tiles_y, ntiles;
+    int ablate;          // debug only (BUGSEG_BNECK_ABLATE): 1 skip x loads, 2 skip middle conv, 4 skip stores
     const void *w1, *w2, *w2b, *w3;                   // packed [Npad][Kpad] (w2b: asymmetric 1x5)
     const float *b1, *s1, *b2, *s2, *b2b, *s2b, *b3, *s3, *s_out;
 };

@@ -524,6 +524,9 @@ struct Walker {
         a.Hg = sg.H; a.Wg = sg.W; a.M = B * sg.H * sg.W;
         a.out = out; a.Hout = so.H; a.Wout = so.W; a.outC = so.C;
         a.ntiles = (a.M + conv_tile_pixels(p.nr) - 1) / conv_tile_pixels(p.nr);
+        const int epc = 16 / (int)es;
+        a.stg_elems = epi == EPI_CLASSES ? 0 : epi == EPI_SHUFFLE ? 64 * (so.C + epc) : 16 * (so.C + epc);
+        a.stage_ok = sg.W % 16 == 0 && a.M % 16 == 0;
         op.a = a; op.nr = p.nr; op.epi = epi;
         op.flops = 2.0 * p.macs_per_px * a.M;
         op.bytes = (double)B * si.H * si.W * si.C * es + (double)p.Npad * p.Kpad * es +
@@ -597,6 +600,7 @@ struct Walker {
                         const Packed &p1 = P(0), &p2 = P(1), &p3 = P(nu - 1), &p2b = P(nu == 4 ? 2 : 1);
                         q.x = curp; q.out = dst; q.B = B; q.H = cur.H; q.W = cur.W;
                         q.ry = ry; q.rx = rx; q.d = dd;
+                        if (const char *ab = std::getenv("BUGSEG_BNECK_ABLATE")) q.ablate = std::atoi(ab);
                         const int th = bneck_tile_h(op.bn_c), tw = bneck_tile_w(op.bn_c);
                         q.tiles_y = (cur.H + th - 1) / th; q.tiles_x = (cur.W + tw - 1) / tw;
                         q.ntiles = B * q.tiles_y * q.tiles_x;

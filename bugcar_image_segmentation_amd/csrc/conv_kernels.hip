@@ -24,6 +24,13 @@ namespace bugseg {
 
 template <int NR> struct Cfg { static constexpr int MR = NR >= 4 ? 2 : 4; };
 
+// LDS carve: [weights Npad x (Kpad+pad)] [tap table] [normalisation table (EPI_INIT_BGR)] [4 x staging]
+__host__ __device__ inline size_t conv_stage_offset(int es, const ConvArgs &a) {
+    const size_t o = (size_t)a.Npad * (a.Kpad + 16 / es) * es + (size_t)a.Ksteps * 4 * sizeof(int) +
+                     (a.nlut ? 3 * 256 * sizeof(float) : 0);
+    return (o + 15) & ~(size_t)15;
+}
+
 template <typename T, int NR, int EPI>
 __global__ void __launch_bounds__(256) conv_kernel(const ConvArgs a) {
     constexpr int MR = Cfg<NR>::MR;
@@ -54,6 +61,7 @@ __global__ void __launch_bounds__(256) conv_kernel(const ConvArgs a) {
     __syncthreads();
     const float *nl = reinterpret_cast<const float *>(gt + a.Ksteps * 4);
     const uint8_t *bgr = reinterpret_cast<const uint8_t *>(a.in);
+    T *stage_base = reinterpret_cast<T *>(smem + conv_stage_offset((int)sizeof(T), a));
 
     const T *in = reinterpret_cast<const T *>(a.in);
     const int HWg = a.Hg * a.Wg;
@@ -182,10 +190,32 @@ __global__ void __launch_bounds__(256) conv_kernel(const ConvArgs a) {
                 }
             }
         } else {
+            // Output staging: each wave owns an LDS region; a 16-pixel fragment's results are written
+            // there and leave as contiguous 16-B-per-lane stores (a per-lane NHWC store writes 16
+            // partial lines per instruction). EPI_SHUFFLE stages the fragment's two output rows of 32
+            // pixels. The RESADD residual comes in the same coalesced way.
+            constexpr int EPC = 16 / (int)sizeof(T);
+            const bool staged = EPI != EPI_SHUFFLE || a.stage_ok;
+            T *stg = stage_base + wave * a.stg_elems;
+            const int OSTR = a.outC + EPC;
+            const T *res = reinterpret_cast<const T *>(a.res);
 #pragma unroll
             for (int m = 0; m < MR; ++m) {
-                if (!pv[m]) continue;
+                const int p0 = tile * TILE + wave * MR * 16 + m * 16;     // first GEMM pixel of the fragment
                 const size_t gpix = (size_t)(pn[m] * a.Hg + py[m]) * a.Wg + px[m];
+                bool res_staged = false;
+                if constexpr (EPI == EPI_RESADD) {
+                    if (a.resCS == a.outC) {
+                        for (int q = lane; q < 16 * a.outC / EPC; q += 64) {
+                            const int pp = p0 + q * EPC / a.outC;
+                            uint4 v4 = make_uint4(0, 0, 0, 0);
+                            if (pp < a.M) v4 = *reinterpret_cast<const uint4 *>(res + (size_t)p0 * a.outC + q * EPC);
+                            *reinterpret_cast<uint4 *>(stg + (q * EPC / a.outC) * OSTR + (q * EPC) % a.outC) = v4;
+                        }
+                        wave_lds_sync();
+                        res_staged = true;
+                    }
+                }
 #pragma unroll
                 for (int n = 0; n < NR; ++n) {
                     const int c = n * 16 + kq * 4;
@@ -194,11 +224,15 @@ __global__ void __launch_bounds__(256) conv_kernel(const ConvArgs a) {
                         const int ph = c / a.coutP, cl = c - ph * a.coutP;
                         if (cl >= a.outC) continue;
                         v = prelu4(v, ld4f(a.slope1 + c));
-                        const int oy = 2 * py[m] + (ph >> 1), ox = 2 * px[m] + (ph & 1);
-                        st4(out + ((size_t)(pn[m] * a.Hout + oy) * a.Wout + ox) * a.outC + cl, v);
+                        if (staged) {
+                            st4(stg + ((ph >> 1) * 32 + 2 * col + (ph & 1)) * OSTR + cl, v);
+                        } else if (pv[m]) {
+                            const int oy = 2 * py[m] + (ph >> 1), ox = 2 * px[m] + (ph & 1);
+                            st4(out + ((size_t)(pn[m] * a.Hout + oy) * a.Wout + ox) * a.outC + cl, v);
+                        }
                         continue;
                     }
-                    if (c >= a.outC) continue;
+                    if (c >= a.outC || !pv[m]) continue;
                     if constexpr (EPI == EPI_INIT_BGR) {
                         // pool channels: max over the window of the raw bytes (the table is increasing, so
                         // max(table(v)) == table(max(v))), reduced across the 4 lane groups above
@@ -242,7 +276,8 @@ __global__ void __launch_bounds__(256) conv_kernel(const ConvArgs a) {
                         v = prelu4(v, ld4f(a.slope1 + c));
                     }
                     if constexpr (EPI == EPI_RESADD) {
-                        if (c < a.resC) v = add4(v, ld4(reinterpret_cast<const T *>(a.res) + gpix * a.resCS + c));
+                        if (res_staged) v = add4(v, ld4(stg + col * OSTR + c));
+                        else if (c < a.resC) v = add4(v, ld4(res + gpix * a.resCS + c));
                         v = prelu4(v, ld4f(a.slope2 + c));
                     } else if constexpr (EPI == EPI_RESPOOL) {
                         // main branch: MaxPool2d(2, 2, return_indices) of the block input, zero-padded
@@ -281,8 +316,28 @@ __global__ void __launch_bounds__(256) conv_kernel(const ConvArgs a) {
                         }
                         v = prelu4(v, ld4f(a.slope2 + c));
                     }
-                    st4(out + gpix * a.outC + c, v);
+                    st4(stg + col * OSTR + c, v);
                 }
+                if (!staged) continue;
+                wave_lds_sync();
+                if constexpr (EPI == EPI_SHUFFLE) {
+                    // two output rows 2y, 2y+1, each 32 pixels from x = 2*px of the fragment's first lane
+                    const int nq = 32 * a.outC / EPC;
+                    const int n0 = __shfl(pn[m], 0, 64), y0 = __shfl(py[m], 0, 64), x0 = __shfl(px[m], 0, 64);
+                    for (int q = lane; q < 2 * nq; q += 64) {
+                        const int row = q >= nq, qq = q - row * nq;
+                        if (p0 < a.M)
+                            *reinterpret_cast<uint4 *>(out + ((size_t)(n0 * a.Hout + 2 * y0 + row) * a.Wout + 2 * x0) * a.outC + qq * EPC) =
+                                *reinterpret_cast<const uint4 *>(stg + (row * 32 + qq * EPC / a.outC) * OSTR + (qq * EPC) % a.outC);
+                    }
+                } else {
+                    for (int q = lane; q < 16 * a.outC / EPC; q += 64) {
+                        if (p0 + q * EPC / a.outC < a.M)
+                            *reinterpret_cast<uint4 *>(out + (size_t)p0 * a.outC + q * EPC) =
+                                *reinterpret_cast<const uint4 *>(stg + (q * EPC / a.outC) * OSTR + (q * EPC) % a.outC);
+                    }
+                }
+                wave_lds_sync();
             }
         }
     }
@@ -291,8 +346,8 @@ __global__ void __launch_bounds__(256) conv_kernel(const ConvArgs a) {
 int conv_tile_pixels(int nr) { return 4 * (nr >= 4 ? 2 : 4) * 16; }
 
 size_t conv_lds_bytes(int prec, const ConvArgs &a) {
-    const size_t es = prec == PREC_BF16 ? 2 : 4;
-    return (size_t)a.Npad * (a.Kpad + 16 / es) * es + (size_t)a.Ksteps * 4 * sizeof(int) + (a.nlut ? 3 * 256 * sizeof(float) : 0);
+    const int es = prec == PREC_BF16 ? 2 : 4;
+    return conv_stage_offset(es, a) + (size_t)4 * a.stg_elems * es;
 }
 
 template <typename T, int NR>

@@ -4,6 +4,13 @@
 
 namespace bugseg {
 
+// LDS hand-off between lanes of ONE wave: wait for the wave's LDS operations, keep the compiler
+// from moving memory operations across (no s_barrier needed inside a wave).
+__device__ __forceinline__ void wave_lds_sync() {
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_wave_barrier();
+}
+
 typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 typedef float f32x4 __attribute__((ext_vector_type(4)));
 

@@ -1,0 +1,31 @@
+"""Debug: time each fused-bottleneck ablation variant (BUGSEG_BNECK_ABLATE bits: 1 no x loads,
+2 no middle-conv MFMAs, 4 no output stores) on the bench workload. Run under rocprofv3 --kernel-trace;
+each variant is its own context (the flag is read when the plan is built), run `reps` times."""
+import os
+import sys
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+import torch  # noqa: E402
+
+from bugcar_image_segmentation_amd import _native as N  # noqa: E402
+from bugcar_image_segmentation_amd import enet_spec, synthetic  # noqa: E402
+from bugcar_image_segmentation_amd.models import ENET  # noqa: E402
+
+B, H, W = 64, 480, 640
+blocks = enet_spec.build_enet()
+frames = torch.from_numpy(synthetic.uniform_frames(B, H, W)).cuda()
+seg = torch.empty((B, H, W), dtype=torch.uint8, device="cuda")
+for flags in [int(v) for v in (sys.argv[1:] or ["0", "1", "2", "4", "7"])]:
+    os.environ["BUGSEG_BNECK_ABLATE"] = str(flags)
+    m = ENET(weights=blocks, precision="bf16")
+    for _ in range(4):
+        m.ctx.forward_bgr(frames, B, H, W, N.OUT_CLASS3_U8, seg)
+    torch.cuda.synchronize()
+    ev = [torch.cuda.Event(enable_timing=True) for _ in range(2)]
+    ev[0].record()
+    for _ in range(5):
+        m.ctx.forward_bgr(frames, B, H, W, N.OUT_CLASS3_U8, seg)
+    ev[1].record()
+    ev[1].synchronize()
+    print(f"ablate={flags}: forward {ev[0].elapsed_time(ev[1]) / 5:.3f} ms", flush=True)
+    del m
