@@ -42,6 +42,7 @@ def parse():
     p.add_argument("--height", type=int, default=480)
     p.add_argument("--width", type=int, default=640)
     p.add_argument("--precision", default="bf16", choices=["bf16", "fp32"])
+    p.add_argument("--streams", type=int, default=1, help="frame shards run concurrently on this many HIP streams")
     p.add_argument("--cpu-baseline-seconds", type=float, default=12.0)
     p.add_argument("--no-cpu-baseline", action="store_true")
     return p.parse_args()
@@ -92,7 +93,7 @@ def main():
     model = ENET(weights=blocks, precision=a.precision)
     bev = synthetic.synthetic_bev(H, W)
     grid = (synthetic.GRID_W_M, synthetic.GRID_H_M, synthetic.CELL_M)
-    pipe = OccupancyPipeline(model, bev, *grid, model_hw=(H, W))
+    pipe = OccupancyPipeline(model, bev, *grid, model_hw=(H, W), streams=a.streams)
     frames = torch.from_numpy(synthetic.uniform_frames(B, H, W, seed=rank)).to(dev)
 
     def step():
@@ -153,7 +154,8 @@ def main():
             "config": {"workload": f"config3/5: ENet {W}x{H} batch {B} per GPU, preprocess + forward + argmax/LUT + "
                                    f"fused BEV warp/occgrid (1000x1000 BEV -> 200x200 cells)",
                        "global_batch": B * world, "per_gpu_batch": B, "height": H, "width": W,
-                       "parallelism": f"frame-sharded dp{world}" + (" + RCCL all-gather of grids" if world > 1 else "")},
+                       "parallelism": f"frame-sharded dp{world}" + (" + RCCL all-gather of grids" if world > 1 else ""),
+                       "streams_per_gpu": a.streams},
             "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": None,
                          "kernel": f"ENet forward: {n_launch} launches (conv_kernel + fused bneck_kernel, one plan); "

@@ -84,6 +84,7 @@ class ENET(InferenceModel):
         self.precision = precision
         self.ctx = N.Context(device, N.BF16 if precision == "bf16" else N.FP32)
         self.ctx.load_weights(blob)
+        self.blob = blob
         self.num_classes = self.ctx.num_classes
         self._bufs: dict = {}
         self.test = None

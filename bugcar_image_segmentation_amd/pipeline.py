@@ -18,8 +18,12 @@ from .models import ENET
 
 
 class OccupancyPipeline:
+    """streams > 1 splits the batch into that many frame shards, each run by its own engine context
+    (own activation arena) on its own HIP stream, so the launches of different shards overlap on the
+    device (one shard's compute phases beside another's memory phases). Results are identical."""
+
     def __init__(self, model: ENET, bev: bev_transform_tools, grid_w_m: float, grid_h_m: float, cell_m: float,
-                 model_hw: tuple[int, int] | None = None, ros_layout: bool = False):
+                 model_hw: tuple[int, int] | None = None, ros_layout: bool = False, streams: int = 1):
         self.model = model
         self.bev = bev
         self.grid = (grid_w_m, grid_h_m, cell_m)
@@ -28,9 +32,22 @@ class OccupancyPipeline:
         if (self.H, self.W) != (bev.input_width, bev.input_height):
             raise ValueError(f"model output {self.H}x{self.W} must equal the calibration's input image size "
                              f"{bev.input_width}x{bev.input_height} (bev.py:304)")
+        if streams < 1:
+            raise ValueError("streams must be >= 1")
+        self.streams = streams
+        self._ctxs = [model.ctx]
+        self._streams = []
         self._x = None
         self._seg = None
         self._grid = None
+
+    def _shard_ctxs(self, dev: torch.device):
+        while len(self._ctxs) < self.streams:
+            c = N.Context(dev.index, self.model.ctx.precision)
+            c.load_weights(self.model.blob)
+            self._ctxs.append(c)
+            self._streams.append(torch.cuda.Stream(device=dev))
+        return self._ctxs, self._streams
 
     def _bufs(self, B: int, dev: torch.device):
         if self._x is None or self._x.shape[0] != B or self._x.device != dev:
@@ -46,13 +63,32 @@ class OccupancyPipeline:
             raise ValueError("frames must be a (B, H0, W0, 3) uint8 device tensor")
         B, H0, W0 = frames_bgr.shape[:3]
         x, seg, grid = self._bufs(B, frames_bgr.device)
-        ctx = self.model.ctx
         frames = frames_bgr.contiguous()
+        out = grid if out is None else out
+        if self.streams == 1 or B < self.streams:
+            self._run_shard(self.model.ctx, frames, x, seg, out, None)
+            return out
+        ctxs, streams = self._shard_ctxs(frames.device)
+        main = torch.cuda.current_stream(frames.device)
+        ready = main.record_event()
+        bounds = [B * i // self.streams for i in range(self.streams + 1)]
+        for i in range(self.streams):
+            s, e = bounds[i], bounds[i + 1]
+            st = main if i == 0 else streams[i - 1]
+            if i:
+                st.wait_event(ready)
+            with torch.cuda.stream(st):
+                self._run_shard(ctxs[i], frames[s:e], x[s:e], seg[s:e], out[s:e], st)
+        for st in streams[: self.streams - 1]:
+            main.wait_stream(st)
+        return out
+
+    def _run_shard(self, ctx, frames, x, seg, out, stream):
+        B, H0, W0 = frames.shape[:3]
         if (H0, W0) != (self.H, self.W):
             # resize only (models.py:87); colour swap + normalisation are fused into the initial block
-            ctx.preprocess(frames, B, H0, W0, self.H, self.W, N.PRE_BGR_U8, x)
+            ctx.preprocess(frames, B, H0, W0, self.H, self.W, N.PRE_BGR_U8, x, stream)
             frames = x
-        ctx.forward_bgr(frames, B, self.H, self.W, N.OUT_CLASS3_U8, seg)
-        out = grid if out is None else out
-        self.bev.create_occupancy_grid_device(seg, *self.grid, ros_layout=self.ros_layout, out=out)
-        return out
+        ctx.forward_bgr(frames, B, self.H, self.W, N.OUT_CLASS3_U8, seg, stream)
+        p = self.bev.occupancy_params(*self.grid, ros_layout=self.ros_layout)
+        N.shared_context(frames.device.index).bev(seg, B, p, out, stream)

@@ -216,6 +216,17 @@ def test_pipeline_end_to_end_fp32(fp32_model, blocks):
     print(f"end-to-end grid agreement vs oracle {(out == grids_ref).mean():.6f}")
 
 
+def test_multistream_pipeline_identical(bf16_model):
+    H, W, B = 96, 128, 10
+    frames = torch.from_numpy(synthetic.road_frames(B, H, W, seed=8)).cuda()
+    bev = synthetic.synthetic_bev(H, W, 300, 300)
+    one = OccupancyPipeline(bf16_model, bev, 3.0, 3.0, 0.05, model_hw=(H, W)).run(frames).clone()
+    for s in (2, 3):
+        many = OccupancyPipeline(bf16_model, bev, 3.0, 3.0, 0.05, model_hw=(H, W), streams=s).run(frames)
+        torch.cuda.synchronize()
+        assert torch.equal(one, many)
+
+
 def test_full_size_batch_properties(bf16_model):
     """Full configs[2] shape (B=32, 480x640): value sets, determinism, batch independence."""
     H, W, B = 480, 640, 32
