@@ -42,7 +42,7 @@ def parse():
     p.add_argument("--height", type=int, default=480)
     p.add_argument("--width", type=int, default=640)
     p.add_argument("--precision", default="bf16", choices=["bf16", "fp32"])
-    p.add_argument("--streams", type=int, default=1, help="frame shards run concurrently on this many HIP streams")
+    p.add_argument("--streams", type=int, default=2, help="frame shards run concurrently on this many HIP streams")
     p.add_argument("--cpu-baseline-seconds", type=float, default=12.0)
     p.add_argument("--no-cpu-baseline", action="store_true")
     return p.parse_args()

@@ -21,21 +21,23 @@
 
 namespace bugseg {
 
+// Tile and workgroup shape per channel count. 128 channels: the LDS footprint (weights + halo or
+// output staging, ~64-73 KB) allows two workgroups per CU, so they are 8-wave (512-thread) to put
+// 16 waves on a CU; 64 / 16 channels (~28 KB): four 4-wave workgroups per CU — more independent
+// tile pipelines (memory phase of one beside compute phase of another) for the same waves.
 template <int C> struct BTile;
-template <> struct BTile<128> { static constexpr int TH = 16, TW = 16; };
-template <> struct BTile<64> { static constexpr int TH = 16, TW = 32; };
-template <> struct BTile<16> { static constexpr int TH = 16, TW = 32; };
+template <> struct BTile<128> { static constexpr int TH = 16, TW = 16, NW = 8; };
+template <> struct BTile<64> { static constexpr int TH = 16, TW = 16, NW = 4; };
+template <> struct BTile<16> { static constexpr int TH = 16, TW = 16, NW = 4; };
 
-int bneck_tile_h(int C) { return C == 128 ? BTile<128>::TH : BTile<64>::TH; }
-int bneck_tile_w(int C) { return C == 128 ? BTile<128>::TW : BTile<64>::TW; }
-
-
-constexpr int BN_WAVES = 8;   // 512-thread workgroups: two waves per SIMD share one LDS footprint
+int bneck_tile_h(int C) { return C == 128 ? BTile<128>::TH : C == 64 ? BTile<64>::TH : BTile<16>::TH; }
+int bneck_tile_w(int C) { return C == 128 ? BTile<128>::TW : C == 64 ? BTile<64>::TW : BTile<16>::TW; }
+static int bneck_waves(int C) { return C == 128 ? BTile<128>::NW : C == 64 ? BTile<64>::NW : BTile<16>::NW; }
 
 template <typename T, int C, bool ASYM>
-__global__ void __launch_bounds__(512, sizeof(T) == 2 ? 4 : 1) bneck_kernel(const BneckArgs a) {
+__global__ void __launch_bounds__(BTile<C>::NW * 64, sizeof(T) == 2 ? 4 : 1) bneck_kernel(const BneckArgs a) {
     using Raw = typename Tr<T>::Raw;
-    constexpr int NW = BN_WAVES, NT = NW * 64;
+    constexpr int NW = BTile<C>::NW, NT = NW * 64;
     constexpr int I = C / 4;
     constexpr int IS = I < 8 ? 8 : I;                 // stored internal channels (8-channel groups)
     constexpr int NR1 = (I + 15) / 16;                // 16-row fragments of t0 / t1
@@ -67,7 +69,12 @@ __global__ void __launch_bounds__(512, sizeof(T) == 2 ? 4 : 1) bneck_kernel(cons
     T *w2 = w1 + NR1 * 16 * K1S;
     T *w2b = w2 + NR1 * 16 * K2S;                     // asymmetric second conv (1x5)
     T *w3 = w2b + (ASYM ? NR1 * 16 * K2S : 0);
-    T *ts = w3 + C * K3S;                             // t0 / t1a / t1 region
+    // per-channel epilogue constants live in LDS too: a global load per use was most of this
+    // kernel's vector-memory instructions and a latency the epilogues waited on
+    constexpr int NP1 = NR1 * 16;
+    float *cb1 = reinterpret_cast<float *>(w3 + C * K3S), *cs1 = cb1 + NP1, *cb2 = cs1 + NP1, *cs2 = cb2 + NP1;
+    float *cb2b = cs2 + NP1, *cs2b = cb2b + NP1, *cb3 = cs2b + NP1, *cs3 = cb3 + C, *cso = cs3 + C;
+    T *ts = reinterpret_cast<T *>(cso + C);           // t0 / t1a / t1 region
     {
         auto stage = [&](T *dst, const void *src, int rows, int kpad, int kstride) {
             const int cpr = kpad * (int)sizeof(T) / 16;
@@ -81,6 +88,11 @@ __global__ void __launch_bounds__(512, sizeof(T) == 2 ? 4 : 1) bneck_kernel(cons
         stage(w2, a.w2, NR1 * 16, KS2 * 32, K2S);
         if constexpr (ASYM) stage(w2b, a.w2b, NR1 * 16, KS2 * 32, K2S);
         stage(w3, a.w3, C, 32, K3S);
+        for (int i = tid; i < NP1; i += NT) {
+            cb1[i] = a.b1[i]; cs1[i] = a.s1[i]; cb2[i] = a.b2[i]; cs2[i] = a.s2[i];
+            cb2b[i] = ASYM ? a.b2b[i] : 0.f; cs2b[i] = ASYM ? a.s2b[i] : 0.f;
+        }
+        for (int i = tid; i < C; i += NT) { cb3[i] = a.b3[i]; cs3[i] = a.s3[i]; cso[i] = a.s_out[i]; }
     }
     const T *x = reinterpret_cast<const T *>(a.x);
     T *out = reinterpret_cast<T *>(a.out);
@@ -137,7 +149,7 @@ __global__ void __launch_bounds__(512, sizeof(T) == 2 ? 4 : 1) bneck_kernel(cons
                     for (int r = 0; r < NR1; ++r) {
                         const int ch = r * 16 + kq * 4;
                         if (ch >= IS) continue;
-                        float4 v = prelu4(add4(f4(acc[r]), ld4f(a.b1 + ch)), ld4f(a.s1 + ch));
+                        float4 v = prelu4(add4(f4(acc[r]), ld4f(cb1 + ch)), ld4f(cs1 + ch));
                         if (!okc[c]) v = make_float4(0.f, 0.f, 0.f, 0.f);
                         st4(ts + h * PSTR + ch, v);
                     }
@@ -202,7 +214,7 @@ __global__ void __launch_bounds__(512, sizeof(T) == 2 ? 4 : 1) bneck_kernel(cons
                 for (int r = 0; r < NR1; ++r) {
                     const int ch = r * 16 + kq * 4;
                     if (ch >= IS) continue;
-                    st4(ts + p * PSTR + ch, prelu4(add4(f4(acc[j][r]), ld4f(a.b2 + ch)), ld4f(a.s2 + ch)));
+                    st4(ts + p * PSTR + ch, prelu4(add4(f4(acc[j][r]), ld4f(cb2 + ch)), ld4f(cs2 + ch)));
                 }
             }
         } else {
@@ -243,7 +255,7 @@ __global__ void __launch_bounds__(512, sizeof(T) == 2 ? 4 : 1) bneck_kernel(cons
                     for (int r = 0; r < NR1; ++r) {
                         const int ch = r * 16 + kq * 4;
                         if (ch >= IS) continue;
-                        float4 v = prelu4(add4(f4(acc[j][r]), ld4f(a.b2 + ch)), ld4f(a.s2 + ch));
+                        float4 v = prelu4(add4(f4(acc[j][r]), ld4f(cb2 + ch)), ld4f(cs2 + ch));
                         if (!inside) v = make_float4(0.f, 0.f, 0.f, 0.f);
                         st4(ts + p * PSTR + ch, v);
                     }
@@ -283,7 +295,7 @@ __global__ void __launch_bounds__(512, sizeof(T) == 2 ? 4 : 1) bneck_kernel(cons
                     for (int r = 0; r < NR1; ++r) {
                         const int ch = r * 16 + kq * 4;
                         if (ch >= IS) continue;
-                        st4(ts + p * PSTR + ch, prelu4(add4(f4(acc[j][r]), ld4f(a.b2b + ch)), ld4f(a.s2b + ch)));
+                        st4(ts + p * PSTR + ch, prelu4(add4(f4(acc[j][r]), ld4f(cb2b + ch)), ld4f(cs2b + ch)));
                     }
                 }
             }
@@ -322,8 +334,8 @@ __global__ void __launch_bounds__(512, sizeof(T) == 2 ? 4 : 1) bneck_kernel(cons
                 mma(acc, wf, tf[j]);
                 const int ch = r * 16 + kq * 4;
                 T *sp = stg + col * OSTR + ch;
-                float4 v = prelu4(add4(f4(acc), ld4f(a.b3 + ch)), ld4f(a.s3 + ch));
-                v = prelu4(add4(v, ld4(sp)), ld4f(a.s_out + ch));
+                float4 v = prelu4(add4(f4(acc), ld4f(cb3 + ch)), ld4f(cs3 + ch));
+                v = prelu4(add4(v, ld4(sp)), ld4f(cso + ch));
                 st4(sp, v);
             }
             wave_lds_sync();
@@ -348,16 +360,17 @@ size_t bneck_lds_bytes(int prec, int C, bool asym, int ry, int rx) {
     const size_t wts = (size_t)NR1 * 16 * (KS1 * 32 + pad) + (size_t)NR1 * 16 * (KS2 * 32 + pad) * (asym ? 2 : 1) +
                        (size_t)C * (32 + pad);
     const size_t halo = (size_t)(TH + 2 * ry) * (TW + 2 * rx) * (IS + pad);
-    const size_t stage = (size_t)BN_WAVES * 16 * (C + pad);            // phase-3 output staging
-    return (wts + (halo > stage ? halo : stage)) * es;
+    const size_t stage = (size_t)bneck_waves(C) * 16 * (C + pad);      // phase-3 output staging
+    const size_t consts = ((size_t)6 * NR1 * 16 + 3 * (size_t)C) * sizeof(float);
+    return (wts + (halo > stage ? halo : stage)) * es + consts;
 }
 
 template <typename T>
 static hipError_t launch_t(int C, bool asym, const BneckArgs &a, dim3 g, size_t lds, hipStream_t s) {
 #define BN_CASE(CC)                                                                                     \
     if (C == CC) {                                                                                      \
-        if (asym) hipLaunchKernelGGL((bneck_kernel<T, CC, true>), g, dim3(BN_WAVES * 64), lds, s, a);            \
-        else hipLaunchKernelGGL((bneck_kernel<T, CC, false>), g, dim3(BN_WAVES * 64), lds, s, a);                \
+        if (asym) hipLaunchKernelGGL((bneck_kernel<T, CC, true>), g, dim3(BTile<CC>::NW * 64), lds, s, a);            \
+        else hipLaunchKernelGGL((bneck_kernel<T, CC, false>), g, dim3(BTile<CC>::NW * 64), lds, s, a);                \
         return hipGetLastError();                                                                       \
     }
     BN_CASE(128)

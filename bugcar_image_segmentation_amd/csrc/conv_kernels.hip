@@ -24,11 +24,15 @@ namespace bugseg {
 
 template <int NR> struct Cfg { static constexpr int MR = NR >= 4 ? 2 : 4; };
 
-// LDS carve: [weights Npad x (Kpad+pad)] [tap table] [normalisation table (EPI_INIT_BGR)] [4 x staging]
-__host__ __device__ inline size_t conv_stage_offset(int es, const ConvArgs &a) {
+// LDS carve: [weights Npad x (Kpad+pad)] [tap table] [normalisation table (EPI_INIT_BGR)]
+//            [bias, slope1, slope2, pscale: Npad floats each] [4 x output staging]
+__host__ __device__ inline size_t conv_const_offset(int es, const ConvArgs &a) {
     const size_t o = (size_t)a.Npad * (a.Kpad + 16 / es) * es + (size_t)a.Ksteps * 4 * sizeof(int) +
                      (a.nlut ? 3 * 256 * sizeof(float) : 0);
     return (o + 15) & ~(size_t)15;
+}
+__host__ __device__ inline size_t conv_stage_offset(int es, const ConvArgs &a) {
+    return conv_const_offset(es, a) + (size_t)4 * a.Npad * sizeof(float);
 }
 
 template <typename T, int NR, int EPI>
@@ -57,8 +61,19 @@ __global__ void __launch_bounds__(256) conv_kernel(const ConvArgs a) {
             float *lut = reinterpret_cast<float *>(gt + a.Ksteps * 4);
             for (int i = tid; i < 3 * 256; i += 256) lut[i] = (float)(T)(float)a.nlut[i];
         }
+        // per-channel epilogue constants (a global load per use would be a long-latency VMEM op
+        // in every epilogue)
+        float *cst = reinterpret_cast<float *>(smem + conv_const_offset((int)sizeof(T), a));
+        for (int i = tid; i < a.Npad; i += 256) {
+            cst[i] = a.bias[i];
+            cst[a.Npad + i] = a.slope1[i];
+            cst[2 * a.Npad + i] = a.slope2[i];
+            cst[3 * a.Npad + i] = a.pscale[i];
+        }
     }
     __syncthreads();
+    const float *cbias = reinterpret_cast<const float *>(smem + conv_const_offset((int)sizeof(T), a));
+    const float *cs1 = cbias + a.Npad, *cs2 = cbias + 2 * a.Npad, *cps = cbias + 3 * a.Npad;
     const float *nl = reinterpret_cast<const float *>(gt + a.Ksteps * 4);
     const uint8_t *bgr = reinterpret_cast<const uint8_t *>(a.in);
     T *stage_base = reinterpret_cast<T *>(smem + conv_stage_offset((int)sizeof(T), a));
@@ -153,7 +168,7 @@ __global__ void __launch_bounds__(256) conv_kernel(const ConvArgs a) {
 #pragma unroll
                 for (int n = 0; n < NR; ++n) {
                     const int c = n * 16 + kq * 4;
-                    const float4 b4 = ld4f(a.bias + c);
+                    const float4 b4 = ld4f(cbias + c);
                     const float4 v = add4(f4(acc[m][n]), b4);
                     float best = -INFINITY;
                     int bi = 0x7fffffff;
@@ -219,11 +234,11 @@ __global__ void __launch_bounds__(256) conv_kernel(const ConvArgs a) {
 #pragma unroll
                 for (int n = 0; n < NR; ++n) {
                     const int c = n * 16 + kq * 4;
-                    float4 v = add4(f4(acc[m][n]), ld4f(a.bias + c));
+                    float4 v = add4(f4(acc[m][n]), ld4f(cbias + c));
                     if constexpr (EPI == EPI_SHUFFLE) {
                         const int ph = c / a.coutP, cl = c - ph * a.coutP;
                         if (cl >= a.outC) continue;
-                        v = prelu4(v, ld4f(a.slope1 + c));
+                        v = prelu4(v, ld4f(cs1 + c));
                         if (staged) {
                             st4(stg + ((ph >> 1) * 32 + 2 * col + (ph & 1)) * OSTR + cl, v);
                         } else if (pv[m]) {
@@ -236,7 +251,7 @@ __global__ void __launch_bounds__(256) conv_kernel(const ConvArgs a) {
                     if constexpr (EPI == EPI_INIT_BGR) {
                         // pool channels: max over the window of the raw bytes (the table is increasing, so
                         // max(table(v)) == table(max(v))), reduced across the 4 lane groups above
-                        const float4 ps = ld4f(a.pscale + c);
+                        const float4 ps = ld4f(cps + c);
                         float pv4[4] = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
                         for (int r = 0; r < 4; ++r) {
@@ -246,11 +261,11 @@ __global__ void __launch_bounds__(256) conv_kernel(const ConvArgs a) {
                             pv4[r] = (mx >= 0 ? nl[ch * 256 + mx] : -INFINITY) * get(ps, r);
                         }
                         v = add4(v, make_float4(pv4[0], pv4[1], pv4[2], pv4[3]));
-                        v = prelu4(v, ld4f(a.slope1 + c));
+                        v = prelu4(v, ld4f(cs1 + c));
                     } else if constexpr (EPI == EPI_INIT) {
                         // concat(conv, maxpool(in)) -> BN -> act (InitialBlock); pool channels carry
                         // their BN as pscale (x) + bias.
-                        const float4 ps = ld4f(a.pscale + c);
+                        const float4 ps = ld4f(cps + c);
                         float pv4[4] = {0.f, 0.f, 0.f, 0.f};
                         const int k = a.pool_k, pad = (k - 1) >> 1;
 #pragma unroll
@@ -271,14 +286,14 @@ __global__ void __launch_bounds__(256) conv_kernel(const ConvArgs a) {
                             pv4[r] = mx * get(ps, r);
                         }
                         v = add4(v, make_float4(pv4[0], pv4[1], pv4[2], pv4[3]));
-                        v = prelu4(v, ld4f(a.slope1 + c));
+                        v = prelu4(v, ld4f(cs1 + c));
                     } else {
-                        v = prelu4(v, ld4f(a.slope1 + c));
+                        v = prelu4(v, ld4f(cs1 + c));
                     }
                     if constexpr (EPI == EPI_RESADD) {
                         if (res_staged) v = add4(v, ld4(stg + col * OSTR + c));
                         else if (c < a.resC) v = add4(v, ld4(res + gpix * a.resCS + c));
-                        v = prelu4(v, ld4f(a.slope2 + c));
+                        v = prelu4(v, ld4f(cs2 + c));
                     } else if constexpr (EPI == EPI_RESPOOL) {
                         // main branch: MaxPool2d(2, 2, return_indices) of the block input, zero-padded
                         // to cout channels; first maximum in window order wins (strict >).
@@ -299,7 +314,7 @@ __global__ void __launch_bounds__(256) conv_kernel(const ConvArgs a) {
                             *reinterpret_cast<uint32_t *>(a.idx_out + gpix * a.idxCS + c) =
                                 (uint32_t)bi[0] | ((uint32_t)bi[1] << 8) | ((uint32_t)bi[2] << 16) | ((uint32_t)bi[3] << 24);
                         }
-                        v = prelu4(v, ld4f(a.slope2 + c));
+                        v = prelu4(v, ld4f(cs2 + c));
                     } else if constexpr (EPI == EPI_RESUNPOOL) {
                         // MaxUnpool2d(2): the low-res main value lands on the window position its
                         // pooling index recorded; every other position of the window is 0.
@@ -314,7 +329,7 @@ __global__ void __launch_bounds__(256) conv_kernel(const ConvArgs a) {
                             v.z += (((id >> 16) & 0xff) == pos) ? mv.z : 0.f;
                             v.w += (((id >> 24) & 0xff) == pos) ? mv.w : 0.f;
                         }
-                        v = prelu4(v, ld4f(a.slope2 + c));
+                        v = prelu4(v, ld4f(cs2 + c));
                     }
                     st4(stg + col * OSTR + c, v);
                 }
