@@ -49,15 +49,27 @@ struct ConvArgs {
     float *logits_out;   // EPI_CLASSES: (B, ncls, Hout, Wout) f32 NCHW, may be nullptr
     const double *nlut;  // EPI_INIT_BGR: [3][256] normalisation table, RGB order (models.py:91)
     int ntiles;
-    int stg_elems;       // per-wave output staging (elements); 0 for EPI_CLASSES
+    int stg_elems;       // per-wave output staging (elements)
     int stage_ok;        // EPI_SHUFFLE: fragments never straddle an input row (Wg % 16 == 0, M % 16 == 0)
+    // derived on the host (finish_conv_args): magic divisors, buffer sizes, staging shifts
+    uint32_t mHWg, mWg; int sHWg, sWg;               // fdiv by Hg*Wg and by Wg
+    uint32_t in_bytes, out_bytes, res_bytes, idx_bytes;
+    int cpr_sh;          // log2(outC / (16 B / elem)): 16-B chunks per output pixel (power of two)
+    int slopes_le1;      // every slope1 / slope2 <= 1: PReLU as max(v, s*v)
 };
+
+// magic number for fdiv (mfma_common.h): divisor d >= 1
+void fastdiv(uint32_t d, uint32_t &m, int &s);
 
 // Launch one convolution. nr = Npad / 16 in {1, 2, 4, 8}. Returns hipSuccess or the launch error.
 hipError_t launch_conv(int prec, int nr, int epi, const ConvArgs &a, hipStream_t s);
 // pixels per tile for a given nr (sizes the grid)
 int conv_tile_pixels(int nr);
 size_t conv_lds_bytes(int prec, const ConvArgs &a);
+
+// ---- initial block (init_kernels.hip): EPI_INIT / EPI_INIT_BGR launches of launch_conv land here.
+// Requires the initial block's shape (3x3 s2 p1 conv of 3 channels packed as tap*8 + c, pool_k 2|3).
+hipError_t launch_init(int prec, bool bgr, const ConvArgs &a, hipStream_t s);
 
 // ---- fused regular / dilated / asymmetric bottleneck (bneck_kernels.hip) ---------------------
 struct BneckArgs {

@@ -525,8 +525,13 @@ struct Walker {
         a.out = out; a.Hout = so.H; a.Wout = so.W; a.outC = so.C;
         a.ntiles = (a.M + conv_tile_pixels(p.nr) - 1) / conv_tile_pixels(p.nr);
         const int epc = 16 / (int)es;
-        a.stg_elems = epi == EPI_CLASSES ? 0 : epi == EPI_SHUFFLE ? 64 * (so.C + epc) : 16 * (so.C + epc);
-        a.stage_ok = sg.W % 16 == 0 && a.M % 16 == 0;
+        a.stg_elems = epi == EPI_CLASSES ? 64 * 20 * 4 / (int)es      // 64 pixels x 20 floats (conv_kernels.hip CLS_STR)
+                    : epi == EPI_SHUFFLE ? 64 * (so.C + epc) : 16 * (so.C + epc);
+        // PReLU as max(v, s*v) is exact when every slope of the launch is <= 1
+        const float *s1 = (const float *)(ctx->host_w.data() + p.o_s1), *s2 = (const float *)(ctx->host_w.data() + p.o_s2);
+        a.slopes_le1 = 1;
+        for (int c = 0; c < p.Npad; ++c)
+            if (!(s1[c] <= 1.f) || !(s2[c] <= 1.f)) a.slopes_le1 = 0;
         op.a = a; op.nr = p.nr; op.epi = epi;
         op.flops = 2.0 * p.macs_per_px * a.M;
         op.bytes = (double)B * si.H * si.W * si.C * es + (double)p.Npad * p.Kpad * es +
@@ -688,6 +693,29 @@ struct Walker {
     }
 };
 
+// Derived launch fields (conv_kernels.hip): magic divisors, buffer-descriptor sizes (every tensor
+// must be addressable with 31-bit byte offsets), the staging shift. false: a tensor is too large.
+bool finish_conv_args(ConvArgs &a, int epi, size_t es) {
+    fastdiv((uint32_t)(a.Hg * a.Wg), a.mHWg, a.sHWg);
+    fastdiv((uint32_t)a.Wg, a.mWg, a.sWg);
+    const double in_b = (double)a.B * a.Hin * a.Win * a.CinS * es;
+    const double out_b = epi == EPI_CLASSES ? 0.0 : (double)a.B * a.Hout * a.Wout * a.outC * es;
+    const double res_b = a.res ? (double)a.B * a.resH * a.resW * a.resCS * es : 0.0;
+    const double idx_b = a.idx_out ? (double)a.M * a.idxCS : a.idx_in ? (double)a.B * a.resH * a.resW * a.idxCS : 0.0;
+    const double lim = 2147483648.0;
+    if (in_b >= lim || out_b >= lim || res_b >= lim || idx_b >= lim ||
+        (epi == EPI_CLASSES && (double)a.B * a.Hout * a.Wout * a.ncls * 4.0 >= 4.0 * lim))
+        return false;
+    a.in_bytes = (uint32_t)in_b; a.out_bytes = (uint32_t)out_b;
+    a.res_bytes = (uint32_t)res_b; a.idx_bytes = (uint32_t)idx_b;
+    const int epc = 16 / (int)es, cpr = a.outC / epc;
+    a.cpr_sh = -1;
+    if (a.outC % epc == 0 && cpr > 0 && (cpr & (cpr - 1)) == 0)
+        for (a.cpr_sh = 0; (1 << a.cpr_sh) < cpr; ++a.cpr_sh) {}
+    a.stage_ok = a.cpr_sh >= 0 && (epi != EPI_SHUFFLE || (a.Wg % 16 == 0 && a.M % 16 == 0));
+    return true;
+}
+
 bool build_plan(bugseg_ctx *ctx, int B, int H, int W, std::string &why) {
     Plan &pl = ctx->plan;
     if (pl.arena && pl.B == B && pl.H == H && pl.W == W) return true;
@@ -706,9 +734,13 @@ bool build_plan(bugseg_ctx *ctx, int B, int H, int W, std::string &why) {
     w.idx.assign(w.szIdx.size(), nullptr);
     for (size_t i = 0; i < w.szIdx.size(); ++i) if (w.szIdx[i]) { w.idx[i] = p; p += al(w.szIdx[i]); }
     if (!w.run(true, why)) return false;
-    for (const Op &op : w.ops) {
-        const double elems = op.kind == 1 ? (double)op.bn.B * op.bn.H * op.bn.W * op.bn_c : (double)op.a.M * 128.0;
-        if (elems > 2.0e9) { why = "batch too large for 32-bit pixel indexing"; return false; }
+    for (Op &op : w.ops) {
+        if (op.kind == 1) {
+            const double bytes = (double)op.bn.B * op.bn.H * op.bn.W * op.bn_c * w.es;
+            if (bytes >= 2147483648.0) { why = "batch too large for 32-bit tensor offsets"; return false; }
+            continue;
+        }
+        if (!finish_conv_args(op.a, op.epi, w.es)) { why = "batch too large for 32-bit tensor offsets"; return false; }
     }
     pl.ops = std::move(w.ops);
     pl.B = B; pl.H = H; pl.W = W;

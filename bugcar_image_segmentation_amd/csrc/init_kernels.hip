@@ -1,0 +1,212 @@
+// ENet initial block, both input forms, as one tiled kernel:
+//
+//   out = act(BN(concat(conv3x3_s2(x) [cconv ch], maxpool_k_s2(x) [3 ch])))
+//
+// x is either the raw BGR u8 frame (EPI_INIT_BGR: ENET.preprocess fused, models.py:84-95 — the
+// (v/256 - mean)/std table is applied as the bytes enter LDS) or the engine input (EPI_INIT:
+// NHWC, 8 storage channels, 3 used). A 256-thread workgroup owns an 8 x 32 output tile:
+//   * the 17 x 65 x 3 input patch is read once — thread q < 195 owns byte column q of all 17 rows,
+//     each row one contiguous run, addressed as (column voffset, row soffset) so the loads cost
+//     no VALU — and stored normalised in LDS (zero outside the frame = the conv's zero padding);
+//   * K = 27 dense, ordered so that lanes of k group kq < 3 read the 8 consecutive patch elements
+//     (3 pixels x 3 channels, minus the last) of window row kq with four 4-byte LDS reads, and group 3
+//     the three leftovers: one v_mfma_f32_16x16x32 per 16 output pixels;
+//   * the pool channels: lane (col, kq) computes the 3 window maxima of pixel col of fragment kq
+//     (the table is increasing, so this is the table of the max byte; taps outside the frame are
+//     excluded as MaxPool2d's -inf padding is), then every lane fetches its fragment's maxima with
+//     ds_bpermute — the max work is spread over all 64 lanes instead of the 16 that hold pool
+//     channels;
+//   * the accumulator layout (4 consecutive channels of one pixel per lane) makes the 16-channel
+//     NHWC row of a 16-pixel fragment one contiguous 512-B (bf16) store across the wave.
+// The generic implicit-GEMM path this replaces was VALU-bound (per-lane 3-byte gathers, integer
+// divisions, a 16-lane pool loop the whole wave executed). Both input forms go through the same
+// arithmetic, so forward_bgr == preprocess + forward bit for bit.
+#include "bugseg_internal.h"
+#include "mfma_common.h"
+
+namespace bugseg {
+
+constexpr int IT_H = 8, IT_W = 32;                        // output tile
+constexpr int IP_H = 2 * IT_H + 1, IP_W = 2 * IT_W + 1;   // input patch (pixels)
+constexpr int IP_RS = IP_W * 3 + 1;                       // LDS patch row stride (elements, even)
+
+// k -> (window row, element of the row's 9-run), the B/A fragment K order described above
+__device__ __forceinline__ void init_k(int kq, int j, int &dy, int &e) {
+    if (kq < 3) { dy = kq; e = j; }
+    else { dy = j; e = j < 3 ? 8 : -1; }
+}
+
+template <typename T, bool BGR>
+__global__ void __launch_bounds__(256) init_kernel(const ConvArgs a) {
+    __shared__ __attribute__((aligned(16))) T patch[IP_H * IP_RS];
+    __shared__ float lut[BGR ? 3 * 256 : 1];
+    using Raw = typename Tr<T>::Raw;
+    const int tid = threadIdx.x;
+    const int lane = tid & 63, col = lane & 15, kq = lane >> 4;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    if constexpr (BGR) {
+        // rounded exactly as the engine-input path rounds it (f64 -> f32 -> T)
+        for (int i = tid; i < 3 * 256; i += 256) lut[i] = (float)(T)(float)a.nlut[i];
+    }
+    // A operand (weights), loop-invariant: row = output channel `col`, k = 8*kq + j in the order of
+    // init_k, from the generic packing [Npad][Kpad] with k' = tap * 8 + c.
+    Raw wf;
+    {
+        const T *wp = reinterpret_cast<const T *>(a.w);
+        T wv[8];
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+            int dy, e;
+            init_k(kq, j, dy, e);
+            wv[j] = e >= 0 ? wp[col * a.Kpad + (dy * 3 + e / 3) * 8 + e % 3] : (T)0.f;
+        }
+        set8(wf, wv);
+    }
+    const int c0 = kq * 4;
+    const float4 b4 = ld4f(a.bias + c0), s4 = ld4f(a.slope1 + c0), p4 = ld4f(a.pscale + c0);
+    const int po = a.pool_k == 3 ? 0 : 1;                  // pool window: patch offsets po .. 2
+    const uint32_t in_bytes = BGR ? (uint32_t)((size_t)a.B * a.Hin * a.Win * 3)
+                                  : (uint32_t)((size_t)a.B * a.Hin * a.Win * a.CinS * sizeof(T));
+    const auto rin = mkbuf(a.in, in_bytes);
+    const auto rout = mkbuf(a.out, (uint32_t)((size_t)a.B * a.Hg * a.Wg * a.outC * sizeof(T)));
+
+    // patch column owned by this thread (constant over tiles)
+    const int q = tid, px = q / 3, cb = q - px * 3;
+    const bool qok = q < IP_W * 3;
+    const int dpatch = BGR ? px * 3 + (2 - cb) : q;        // BGR byte cb is RGB channel 2 - cb (models.py:87)
+    const int lbase = (2 - cb) * 256;
+
+    const int tiles_x = (a.Wg + IT_W - 1) / IT_W, tiles_y = (a.Hg + IT_H - 1) / IT_H;
+    const int per = tiles_x * tiles_y, ntiles = a.B * per;
+    // XCD-aware tile walk (see conv_kernels.hip)
+    const int G = gridDim.x, grp = blockIdx.x & 7, slot = blockIdx.x >> 3, nslots = G >> 3;
+    const int CH = (ntiles + 7) >> 3;
+    for (int it = slot; it < CH; it += nslots) {
+        const int tile = grp * CH + it;
+        if (tile >= ntiles) break;
+        const int n = tile / per, tr = tile - n * per;
+        const int ty0 = (tr / tiles_x) * IT_H, tx0 = (tr % tiles_x) * IT_W;
+        const int iy0 = 2 * ty0 - 1, ix0 = 2 * tx0 - 1;
+        // ---- patch: all 17 loads issued before any is consumed
+        // (the whole offset goes in voffset: the descriptor's range check does not cover soffset)
+        const int ix = ix0 + px;
+        const bool colok = qok && (unsigned)ix < (unsigned)a.Win;
+        constexpr uint32_t PB = BGR ? 3u : 8u * (uint32_t)sizeof(T);       // bytes per input pixel (CinS = 8)
+        const uint32_t qoff = BGR ? (uint32_t)q : (uint32_t)(px * PB + cb * sizeof(T));
+        const uint32_t rowpix = (uint32_t)((n * a.Hin + iy0) * a.Win + ix0);   // wraps for iy0 = -1: row unused
+        uint32_t raw[IP_H];
+#pragma unroll
+        for (int r = 0; r < IP_H; ++r) {
+            const bool ok = colok && (unsigned)(iy0 + r) < (unsigned)a.Hin;
+            const uint32_t off = ok ? (rowpix + (uint32_t)(r * a.Win)) * PB + qoff : OOB;
+            if constexpr (BGR) raw[r] = __builtin_amdgcn_raw_buffer_load_b8(rin, (int)off, 0, 0);
+            else if constexpr (sizeof(T) == 2) raw[r] = __builtin_amdgcn_raw_buffer_load_b16(rin, (int)off, 0, 0);
+            else raw[r] = __builtin_amdgcn_raw_buffer_load_b32(rin, (int)off, 0, 0);
+        }
+        __syncthreads();   // lut staged / previous tile done with the patch
+        if (qok) {
+#pragma unroll
+            for (int r = 0; r < IP_H; ++r) {
+                const bool ok = colok && (unsigned)(iy0 + r) < (unsigned)a.Hin;
+                T v;
+                if constexpr (BGR) v = (T)lut[lbase + (int)(raw[r] & 0xff)];
+                else if constexpr (sizeof(T) == 2) v = __builtin_bit_cast(T, (unsigned short)raw[r]);
+                else v = __builtin_bit_cast(T, raw[r]);
+                patch[r * IP_RS + dpatch] = ok ? v : (T)0.f;
+            }
+        }
+        __syncthreads();
+
+        // ---- pool maxima: lane (col, kq) -> pixel col of fragment f = kq (row 2*wave + (f>>1))
+        float pm[3];
+        {
+            const int lr = 2 * wave + (kq >> 1), lc = (kq & 1) * 16 + col;
+            const T *pp = patch + 2 * lr * IP_RS + 6 * lc;
+            const bool top = iy0 + 2 * lr < 0, left = ix0 + 2 * lc < 0;   // window row/col 0 outside the frame
+#pragma unroll
+            for (int ch = 0; ch < 3; ++ch) {
+                float mx = -INFINITY;
+#pragma unroll
+                for (int dy = 0; dy < 3; ++dy) {
+                    if (dy < po || (dy == 0 && top)) continue;
+#pragma unroll
+                    for (int dx = 0; dx < 3; ++dx) {
+                        if (dx < po || (dx == 0 && left)) continue;
+                        mx = fmaxf(mx, (float)pp[dy * IP_RS + dx * 3 + ch]);
+                    }
+                }
+                pm[ch] = mx;
+            }
+        }
+
+#pragma unroll
+        for (int f = 0; f < 4; ++f) {
+            const int lr = 2 * wave + (f >> 1), lc = (f & 1) * 16 + col;
+            const T *pp = patch + 2 * lr * IP_RS + 6 * lc;   // window origin (tap dy = dx = 0)
+            Raw xf;
+            if (kq < 3) {
+                const T *src = pp + kq * IP_RS;
+                if constexpr (sizeof(T) == 2) {
+                    const uint32_t *s32 = reinterpret_cast<const uint32_t *>(src);
+                    xf.v = make_uint4(s32[0], s32[1], s32[2], s32[3]);
+                } else {
+                    const float2 *s2 = reinterpret_cast<const float2 *>(src);
+                    const float2 u0 = s2[0], u1 = s2[1], u2 = s2[2], u3 = s2[3];
+                    xf.a = make_float4(u0.x, u0.y, u1.x, u1.y);
+                    xf.b = make_float4(u2.x, u2.y, u3.x, u3.y);
+                }
+            } else {
+                T xv[8];
+#pragma unroll
+                for (int j = 0; j < 8; ++j) xv[j] = j < 3 ? pp[j * IP_RS + 8] : (T)0.f;
+                set8(xf, xv);
+            }
+            f32x4 acc = (f32x4){0.f, 0.f, 0.f, 0.f};
+            mma(acc, wf, xf);
+            float4 v = add4(f4(acc), b4);
+            // this fragment's pool maxima for pixel col live in lane col + 16 f
+            float pv[4] = {0.f, 0.f, 0.f, 0.f};
+            const int src = (col + 16 * f) << 2;
+            float pf[3];
+#pragma unroll
+            for (int ch = 0; ch < 3; ++ch)
+                pf[ch] = __int_as_float(__builtin_amdgcn_ds_bpermute(src, __float_as_int(pm[ch])));
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                const int ch = c0 + r - a.cconv;
+                if (ch >= 0 && ch < a.cpool) pv[r] = (ch == 0 ? pf[0] : ch == 1 ? pf[1] : pf[2]) * get(p4, r);
+            }
+            v = prelu4(add4(v, make_float4(pv[0], pv[1], pv[2], pv[3])), s4);
+            const int oy = ty0 + lr, ox = tx0 + lc;
+            const bool ok = oy < a.Hg && ox < a.Wg && c0 < a.outC;
+            const uint32_t off = ok ? (uint32_t)(((n * a.Hg + oy) * a.Wg + ox) * a.outC + c0) * (uint32_t)sizeof(T) : OOB;
+            if constexpr (sizeof(T) == 2) {
+                typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
+                bf16x4 b = {(__bf16)v.x, (__bf16)v.y, (__bf16)v.z, (__bf16)v.w};
+                __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u32x2, b), rout, (int)off, 0, 0);
+            } else {
+                bst16(rout, off, __builtin_bit_cast(uint4, v));
+            }
+        }
+    }
+}
+
+int init_tiles(const ConvArgs &a) {
+    return a.B * ((a.Hg + IT_H - 1) / IT_H) * ((a.Wg + IT_W - 1) / IT_W);
+}
+
+hipError_t launch_init(int prec, bool bgr, const ConvArgs &a, hipStream_t s) {
+    int g = init_tiles(a);
+    g = g < 2048 ? g : 2048;
+    g = (g + 7) & ~7;
+    if (prec == PREC_BF16) {
+        if (bgr) hipLaunchKernelGGL((init_kernel<__bf16, true>), dim3(g), dim3(256), 0, s, a);
+        else hipLaunchKernelGGL((init_kernel<__bf16, false>), dim3(g), dim3(256), 0, s, a);
+    } else {
+        if (bgr) hipLaunchKernelGGL((init_kernel<float, true>), dim3(g), dim3(256), 0, s, a);
+        else hipLaunchKernelGGL((init_kernel<float, false>), dim3(g), dim3(256), 0, s, a);
+    }
+    return hipGetLastError();
+}
+
+}  // namespace bugseg

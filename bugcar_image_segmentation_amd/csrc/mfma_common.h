@@ -39,6 +39,15 @@ __device__ __forceinline__ void set3(RawF &r, float a, float b, float c) {
     r.b = make_float4(0.f, 0.f, 0.f, 0.f);
 }
 
+__device__ __forceinline__ void set8(RawB &r, const __bf16 (&v)[8]) {
+    bf16x8 b = {v[0], v[1], v[2], v[3], v[4], v[5], v[6], v[7]};
+    r.v = __builtin_bit_cast(uint4, b);
+}
+__device__ __forceinline__ void set8(RawF &r, const float (&v)[8]) {
+    r.a = make_float4(v[0], v[1], v[2], v[3]);
+    r.b = make_float4(v[4], v[5], v[6], v[7]);
+}
+
 __device__ __forceinline__ void mma(f32x4 &acc, const RawB &w, const RawB &x) {
     acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, w.v), __builtin_bit_cast(bf16x8, x.v),
                                                   acc, 0, 0, 0);
@@ -72,7 +81,47 @@ __device__ __forceinline__ void st4(__bf16 *p, float4 v) {
 __device__ __forceinline__ float ld1(const float *p) { return *p; }
 __device__ __forceinline__ float ld1(const __bf16 *p) { return (float)*p; }
 
+// ---- buffer (SRSRC) memory ops: 32-bit byte offsets against a wave-uniform descriptor built from
+// kernel arguments; an offset past the descriptor's size reads 0 and drops a store, which is how
+// padding taps and masked lanes are handled without branches (OOB = any offset >= 2^31 here).
+typedef unsigned int u32x2 __attribute__((ext_vector_type(2)));
+typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+constexpr uint32_t OOB = 0x80000000u;
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t mkbuf(const void *p, uint32_t bytes) {
+    return __builtin_amdgcn_make_buffer_rsrc(const_cast<void *>(p), (short)0, (int)bytes, 0x00020000);
+}
+__device__ __forceinline__ uint4 bld16(__amdgpu_buffer_rsrc_t r, uint32_t off) {
+    return __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(r, (int)off, 0, 0));
+}
+__device__ __forceinline__ void bst16(__amdgpu_buffer_rsrc_t r, uint32_t off, uint4 v) {
+    __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, v), r, (int)off, 0, 0);
+}
+__device__ __forceinline__ void bld8(RawB &x, __amdgpu_buffer_rsrc_t r, uint32_t off) { x.v = bld16(r, off); }
+__device__ __forceinline__ void bld8(RawF &x, __amdgpu_buffer_rsrc_t r, uint32_t off) {
+    x.a = __builtin_bit_cast(float4, bld16(r, off));
+    x.b = __builtin_bit_cast(float4, bld16(r, off + 16));
+}
+// 4 consecutive elements -> float4
+__device__ __forceinline__ float4 bld4(__amdgpu_buffer_rsrc_t r, uint32_t off, const float *) {
+    return __builtin_bit_cast(float4, bld16(r, off));
+}
+__device__ __forceinline__ float4 bld4(__amdgpu_buffer_rsrc_t r, uint32_t off, const __bf16 *) {
+    const u32x2 u = __builtin_amdgcn_raw_buffer_load_b64(r, (int)off, 0, 0);
+    return make_float4(__uint_as_float(u.x << 16), __uint_as_float(u.x & 0xffff0000u),
+                       __uint_as_float(u.y << 16), __uint_as_float(u.y & 0xffff0000u));
+}
+
+// Division by a runtime-invariant divisor d via a host-computed magic number (bugseg_runtime.cpp
+// fastdiv()): q = umulhi(n, m) >> s for d >= 2, s < 0 encodes d == 1. Exact for 0 <= n < 2^31.
+__device__ __forceinline__ uint32_t fdiv(uint32_t n, uint32_t m, int s) {
+    return s < 0 ? n : (__umulhi(n, m) >> s);
+}
+
 __device__ __forceinline__ float prelu(float v, float s) { return v > 0.f ? v : v * s; }
+// == prelu when s <= 1 (v > 0: v*s <= v; v < 0: v*s >= v): 2 VALU instead of 3
+__device__ __forceinline__ float4 prelu4m(float4 v, float4 s) {
+    return make_float4(fmaxf(v.x, v.x * s.x), fmaxf(v.y, v.y * s.y), fmaxf(v.z, v.z * s.z), fmaxf(v.w, v.w * s.w));
+}
 __device__ __forceinline__ float4 prelu4(float4 v, float4 s) {
     return make_float4(prelu(v.x, s.x), prelu(v.y, s.y), prelu(v.z, s.z), prelu(v.w, s.w));
 }

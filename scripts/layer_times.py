@@ -1,0 +1,65 @@
+"""Per-layer kernel durations from a rocprofv3 kernel trace of repeated single-stream forwards.
+
+The trace is cut into forwards at each launch of the initial-block kernel (EPI 7 / EPI 4); every
+forward of one variant has the same launch sequence, so durations are averaged per position.
+Variants (e.g. the ablation script's contexts) are split every `--per-variant` forwards.
+
+usage: python scripts/layer_times.py gpurun_out/ablate/run_kernel_trace.csv [--per-variant 9] [--labels 0,1,2]
+"""
+import argparse
+import csv
+import re
+from collections import defaultdict
+
+
+def short(name):
+    m = re.search(r"bneck_kernelI(DF16b|f)Li(\d+)ELb(\d)E", name)
+    if m:
+        return f"bneck C{m.group(2)}{' asym' if m.group(3) == '1' else ''}"
+    m = re.search(r"conv_kernelI(DF16b|f)Li(\d+)ELi(\d+)E", name)
+    if m:
+        return f"conv NR{m.group(2)} E{m.group(3)}"
+    m = re.search(r"conv_kernel<.*, (\d+)>", name)
+    if m:
+        return f"conv NR1 E{m.group(1)}"
+    if "init_kernel" in name:
+        return "init"
+    return name.split("(")[0][-40:]
+
+
+def main():
+    p = argparse.ArgumentParser()
+    p.add_argument("trace")
+    p.add_argument("--per-variant", type=int, default=0)
+    p.add_argument("--labels", default="")
+    a = p.parse_args()
+    rows = sorted(csv.DictReader(open(a.trace)), key=lambda r: int(r["Start_Timestamp"]))
+    rows = [r for r in rows if any(k in r["Kernel_Name"] for k in ("conv_kernel", "bneck_kernel", "init_kernel"))]
+    fwds, cur = [], None
+    for r in rows:
+        s = short(r["Kernel_Name"])
+        if s.endswith("E7") or s.endswith("E4") or s.startswith("init"):
+            cur = []
+            fwds.append(cur)
+        if cur is not None:
+            cur.append((s, (int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e3, int(r["Grid_Size_X"])))
+    per = a.per_variant or len(fwds)
+    variants = [fwds[i:i + per] for i in range(0, len(fwds), per)]
+    labels = a.labels.split(",") if a.labels else [str(i) for i in range(len(variants))]
+    tables = []
+    for v in variants:
+        n = len(v[0])
+        avg = defaultdict(float)
+        for f in v:
+            for i, (s, d, g) in enumerate(f[:n]):
+                avg[i] += d / len(v)
+        tables.append((v[0], avg))
+    base = tables[0][0]
+    print("pos  kernel             grid  " + "  ".join(f"{lab:>8}" for lab in labels[:len(tables)]))
+    for i, (s, _, g) in enumerate(base):
+        print(f"{i:3d}  {s:16s} {g // 64:6d}  " + "  ".join(f"{t[1][i]:8.1f}" for t in tables))
+    print("sum                       " + "  ".join(f"{sum(t[1].values()):8.1f}" for t in tables))
+
+
+if __name__ == "__main__":
+    main()
