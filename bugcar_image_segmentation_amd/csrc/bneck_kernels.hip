@@ -26,16 +26,17 @@ namespace bugseg {
 // 16 waves on a CU; 64 / 16 channels (~28 KB): four 4-wave workgroups per CU — more independent
 // tile pipelines (memory phase of one beside compute phase of another) for the same waves.
 template <int C> struct BTile;
-template <> struct BTile<128> { static constexpr int TH = 16, TW = 16, NW = 8; };
-template <> struct BTile<64> { static constexpr int TH = 16, TW = 16, NW = 4; };
-template <> struct BTile<16> { static constexpr int TH = 16, TW = 16, NW = 4; };
+// OCC: waves per SIMD the bf16 build is held to (registers), matching what LDS allows.
+template <> struct BTile<128> { static constexpr int TH = 16, TW = 16, NW = 8, OCC = 4; };
+template <> struct BTile<64> { static constexpr int TH = 16, TW = 16, NW = 4, OCC = 5; };
+template <> struct BTile<16> { static constexpr int TH = 16, TW = 16, NW = 4, OCC = 6; };
 
 int bneck_tile_h(int C) { return C == 128 ? BTile<128>::TH : C == 64 ? BTile<64>::TH : BTile<16>::TH; }
 int bneck_tile_w(int C) { return C == 128 ? BTile<128>::TW : C == 64 ? BTile<64>::TW : BTile<16>::TW; }
 static int bneck_waves(int C) { return C == 128 ? BTile<128>::NW : C == 64 ? BTile<64>::NW : BTile<16>::NW; }
 
 template <typename T, int C, bool ASYM>
-__global__ void __launch_bounds__(BTile<C>::NW * 64, sizeof(T) == 2 ? 4 : 1) bneck_kernel(const BneckArgs a) {
+__global__ void __launch_bounds__(BTile<C>::NW * 64, sizeof(T) == 2 ? BTile<C>::OCC : 1) bneck_kernel(const BneckArgs a) {
     using Raw = typename Tr<T>::Raw;
     constexpr int NW = BTile<C>::NW, NT = NW * 64;
     constexpr int I = C / 4;
@@ -63,7 +64,8 @@ __global__ void __launch_bounds__(BTile<C>::NW * 64, sizeof(T) == 2 ? 4 : 1) bne
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
 
     const int tid = threadIdx.x;
-    const int lane = tid & 63, wave = tid >> 6, col = lane & 15, kq = lane >> 4;
+    const int lane = tid & 63, col = lane & 15, kq = lane >> 4;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);   // provably uniform: scalar fragment math
     const int K1S = KS1 * 32 + PAD, K2S = KS2 * 32 + PAD, K3S = 32 + PAD;
     T *w1 = reinterpret_cast<T *>(smem);
     T *w2 = w1 + NR1 * 16 * K1S;
@@ -94,8 +96,12 @@ __global__ void __launch_bounds__(BTile<C>::NW * 64, sizeof(T) == 2 ? 4 : 1) bne
         }
         for (int i = tid; i < C; i += NT) { cb3[i] = a.b3[i]; cs3[i] = a.s3[i]; cso[i] = a.s_out[i]; }
     }
-    const T *x = reinterpret_cast<const T *>(a.x);
-    T *out = reinterpret_cast<T *>(a.out);
+    // x / out through buffer descriptors: 32-bit offsets, and an out-of-range offset reads 0 / drops
+    // the store (mfma_common.h), so image-border masking costs one select per access
+    const auto rxb = mkbuf(a.x, a.x_bytes);
+    const auto rob = mkbuf(a.out, a.x_bytes);
+    const bool fast = a.slopes_le1;
+    auto act = [&](float4 v, const float *s) { return fast ? prelu4m(v, ld4f(s)) : prelu4(v, ld4f(s)); };
     const int ry = a.ry, rx = a.rx, d = a.d;
     const int HWW = TW + 2 * rx, HR = (TH + 2 * ry) * HWW;
     const int nf1 = (HR + 15) >> 4;
@@ -109,7 +115,7 @@ __global__ void __launch_bounds__(BTile<C>::NW * 64, sizeof(T) == 2 ? 4 : 1) bne
         const int n = tile / (a.tiles_y * a.tiles_x);
         const int tr = tile - n * a.tiles_y * a.tiles_x;
         const int ty0 = (tr / a.tiles_x) * TH, tx0 = (tr % a.tiles_x) * TW;
-        const T *xn = x + (size_t)n * a.H * a.W * C;
+        const uint32_t xn = (uint32_t)(n * a.H * a.W) * (uint32_t)(C * sizeof(T));   // frame byte offset
         __syncthreads();   // weights staged (first tile) / previous tile done with ts
 
         // ---- phase 1: t0 = act1(W1 x + b1) over tile + halo, 0 outside the image. The loads of CH1
@@ -120,14 +126,14 @@ __global__ void __launch_bounds__(BTile<C>::NW * 64, sizeof(T) == 2 ? 4 : 1) bne
 #pragma unroll
             for (int c = 0; c < CH1; ++c) {
                 const int h = (f0 + c * NW) * 16 + col;
-                const int hy = h / HWW, hx = h - hy * HWW;
+                const int hy = (int)fdiv((uint32_t)h, a.mHWW, a.sHWW), hx = h - hy * HWW;
                 const int iy = ty0 - ry + hy, ix = tx0 - rx + hx;
                 okc[c] = h < HR && (unsigned)iy < (unsigned)a.H && (unsigned)ix < (unsigned)a.W;
 #pragma unroll
                 for (int s = 0; s < KS1; ++s) {
                     const int g = s * 4 + kq;
-                    if (okc[c] && g < G1 && !(a.ablate & 1)) ld8(xf[c][s], xn + ((size_t)iy * a.W + ix) * C + g * 8);
-                    else zero(xf[c][s]);
+                    const bool ld = okc[c] && g < G1 && !(a.ablate & 1);
+                    bld8(xf[c][s], rxb, ld ? xn + (uint32_t)((iy * a.W + ix) * C + g * 8) * (uint32_t)sizeof(T) : OOB);
                 }
             }
 #pragma unroll
@@ -149,7 +155,7 @@ __global__ void __launch_bounds__(BTile<C>::NW * 64, sizeof(T) == 2 ? 4 : 1) bne
                     for (int r = 0; r < NR1; ++r) {
                         const int ch = r * 16 + kq * 4;
                         if (ch >= IS) continue;
-                        float4 v = prelu4(add4(f4(acc[r]), ld4f(cb1 + ch)), ld4f(cs1 + ch));
+                        float4 v = act(add4(f4(acc[r]), ld4f(cb1 + ch)), cs1 + ch);
                         if (!okc[c]) v = make_float4(0.f, 0.f, 0.f, 0.f);
                         st4(ts + h * PSTR + ch, v);
                     }
@@ -172,8 +178,7 @@ __global__ void __launch_bounds__(BTile<C>::NW * 64, sizeof(T) == 2 ? 4 : 1) bne
                     const int q = lane + 64 * k;
                     const int ix = tx0 + ox0 + q * EPC / C;
                     const bool ok = q < CPF && (unsigned)iy < (unsigned)a.H && (unsigned)ix < (unsigned)a.W;
-                    res[j][k] = ok ? *reinterpret_cast<const uint4 *>(xn + ((size_t)iy * a.W + tx0 + ox0) * C + q * EPC)
-                                   : make_uint4(0, 0, 0, 0);
+                    res[j][k] = bld16(rxb, ok ? xn + (uint32_t)((iy * a.W + tx0 + ox0) * C + q * EPC) * (uint32_t)sizeof(T) : OOB);
                 }
             }
         };
@@ -214,7 +219,7 @@ __global__ void __launch_bounds__(BTile<C>::NW * 64, sizeof(T) == 2 ? 4 : 1) bne
                 for (int r = 0; r < NR1; ++r) {
                     const int ch = r * 16 + kq * 4;
                     if (ch >= IS) continue;
-                    st4(ts + p * PSTR + ch, prelu4(add4(f4(acc[j][r]), ld4f(cb2 + ch)), ld4f(cs2 + ch)));
+                    st4(ts + p * PSTR + ch, act(add4(f4(acc[j][r]), ld4f(cb2 + ch)), cs2 + ch));
                 }
             }
         } else {
@@ -255,7 +260,7 @@ __global__ void __launch_bounds__(BTile<C>::NW * 64, sizeof(T) == 2 ? 4 : 1) bne
                     for (int r = 0; r < NR1; ++r) {
                         const int ch = r * 16 + kq * 4;
                         if (ch >= IS) continue;
-                        float4 v = prelu4(add4(f4(acc[j][r]), ld4f(cb2 + ch)), ld4f(cs2 + ch));
+                        float4 v = act(add4(f4(acc[j][r]), ld4f(cb2 + ch)), cs2 + ch);
                         if (!inside) v = make_float4(0.f, 0.f, 0.f, 0.f);
                         st4(ts + p * PSTR + ch, v);
                     }
@@ -295,7 +300,7 @@ __global__ void __launch_bounds__(BTile<C>::NW * 64, sizeof(T) == 2 ? 4 : 1) bne
                     for (int r = 0; r < NR1; ++r) {
                         const int ch = r * 16 + kq * 4;
                         if (ch >= IS) continue;
-                        st4(ts + p * PSTR + ch, prelu4(add4(f4(acc[j][r]), ld4f(cb2b + ch)), ld4f(cs2b + ch)));
+                        st4(ts + p * PSTR + ch, act(add4(f4(acc[j][r]), ld4f(cb2b + ch)), cs2b + ch));
                     }
                 }
             }
@@ -315,7 +320,6 @@ __global__ void __launch_bounds__(BTile<C>::NW * 64, sizeof(T) == 2 ? 4 : 1) bne
         }
         __syncthreads();
         T *stg = ts + wave * 16 * OSTR;
-        T *outn = out + (size_t)n * a.H * a.W * C;
 #pragma unroll
         for (int j = 0; j < NF2; ++j) {
             const int p0 = (wave + NW * j) * 16;
@@ -334,8 +338,8 @@ __global__ void __launch_bounds__(BTile<C>::NW * 64, sizeof(T) == 2 ? 4 : 1) bne
                 mma(acc, wf, tf[j]);
                 const int ch = r * 16 + kq * 4;
                 T *sp = stg + col * OSTR + ch;
-                float4 v = prelu4(add4(f4(acc), ld4f(cb3 + ch)), ld4f(cs3 + ch));
-                v = prelu4(add4(v, ld4(sp)), ld4f(cso + ch));
+                float4 v = act(add4(f4(acc), ld4f(cb3 + ch)), cs3 + ch);
+                v = act(add4(v, ld4(sp)), cso + ch);
                 st4(sp, v);
             }
             wave_lds_sync();
@@ -343,9 +347,10 @@ __global__ void __launch_bounds__(BTile<C>::NW * 64, sizeof(T) == 2 ? 4 : 1) bne
             for (int k = 0; k < CPL; ++k) {
                 const int q = lane + 64 * k;
                 const int ix = tx0 + ox0 + q * EPC / C;
-                if (q < CPF && (unsigned)iy < (unsigned)a.H && (unsigned)ix < (unsigned)a.W && !(a.ablate & 4))
-                    *reinterpret_cast<uint4 *>(outn + ((size_t)iy * a.W + tx0 + ox0) * C + q * EPC) =
-                        *reinterpret_cast<const uint4 *>(stg + (q * EPC / C) * OSTR + (q * EPC) % C);
+                const bool ok = q < CPF && (unsigned)iy < (unsigned)a.H && (unsigned)ix < (unsigned)a.W && !(a.ablate & 4);
+                if (q < CPF)
+                    bst16(rob, ok ? xn + (uint32_t)((iy * a.W + tx0 + ox0) * C + q * EPC) * (uint32_t)sizeof(T) : OOB,
+                          *reinterpret_cast<const uint4 *>(stg + (q * EPC / C) * OSTR + (q * EPC) % C));
             }
             wave_lds_sync();
         }

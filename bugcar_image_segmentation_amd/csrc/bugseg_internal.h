@@ -81,6 +81,9 @@ struct BneckArgs {
     int ablate;          // debug only (BUGSEG_BNECK_ABLATE): 1 skip x loads, 2 skip middle conv, 4 skip stores
     const void *w1, *w2, *w2b, *w3;                   // packed [Npad][Kpad] (w2b: asymmetric 1x5)
     const float *b1, *s1, *b2, *s2, *b2b, *s2b, *b3, *s3, *s_out;
+    uint32_t mHWW; int sHWW;                          // fdiv by the halo-tile width TW + 2*rx
+    uint32_t x_bytes;                                 // bytes of x (== out)
+    int slopes_le1;                                   // every PReLU slope <= 1: max(v, s*v)
 };
 hipError_t launch_bneck(int prec, int C, bool asym, const BneckArgs &a, hipStream_t s);
 size_t bneck_lds_bytes(int prec, int C, bool asym, int ry, int rx);

@@ -614,6 +614,15 @@ struct Walker {
                         q.w2b = dw + p2b.o_w; q.b2b = (const float *)(dw + p2b.o_bias); q.s2b = (const float *)(dw + p2b.o_s1);
                         q.w3 = dw + p3.o_w; q.b3 = (const float *)(dw + p3.o_bias); q.s3 = (const float *)(dw + p3.o_s1);
                         q.s_out = (const float *)(dw + p3.o_s2);
+                        fastdiv((uint32_t)(tw + 2 * rx), q.mHWW, q.sHWW);
+                        q.slopes_le1 = 1;
+                        const std::pair<size_t, int> slopes[] = {{p1.o_s1, p1.Npad}, {p2.o_s1, p2.Npad}, {p2b.o_s1, p2b.Npad},
+                                                                 {p3.o_s1, p3.Npad}, {p3.o_s2, p3.Npad}};
+                        for (const auto &sv : slopes) {
+                            const float *sl = (const float *)(ctx->host_w.data() + sv.first);
+                            for (int c = 0; c < sv.second; ++c)
+                                if (!(sl[c] <= 1.f)) q.slopes_le1 = 0;
+                        }
                         double fl = 0, wb = 0, lb = 0;
                         const double px = (double)B * cur.H * cur.W;
                         for (int i = 0; i < nu; ++i) {
@@ -738,6 +747,7 @@ bool build_plan(bugseg_ctx *ctx, int B, int H, int W, std::string &why) {
         if (op.kind == 1) {
             const double bytes = (double)op.bn.B * op.bn.H * op.bn.W * op.bn_c * w.es;
             if (bytes >= 2147483648.0) { why = "batch too large for 32-bit tensor offsets"; return false; }
+            op.bn.x_bytes = (uint32_t)bytes;
             continue;
         }
         if (!finish_conv_args(op.a, op.epi, w.es)) { why = "batch too large for 32-bit tensor offsets"; return false; }

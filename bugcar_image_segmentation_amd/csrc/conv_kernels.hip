@@ -38,7 +38,7 @@ __host__ __device__ inline size_t conv_tap_offset(int es, const ConvArgs &a) {
     return ((size_t)a.Npad * (a.Kpad + 16 / es) * es + 15) & ~(size_t)15;
 }
 __host__ __device__ inline size_t conv_const_offset(int es, const ConvArgs &a) {
-    return conv_tap_offset(es, a) + (size_t)a.Ksteps * 4 * 16;
+    return conv_tap_offset(es, a) + (size_t)((a.Ksteps + 3) & ~3) * 4 * 16;   // padded to whole load chunks
 }
 __host__ __device__ inline size_t conv_stage_offset(int es, const ConvArgs &a) {
     return conv_const_offset(es, a) + (size_t)3 * a.Npad * sizeof(float) + 16 * sizeof(int);
@@ -53,6 +53,8 @@ __global__ void __launch_bounds__(256, sizeof(T) == 2 ? (NR == 8 ? 3 : 4) : 1) c
     constexpr int MR = Cfg<NR>::MR;
     constexpr int TILE = 4 * MR * 16;
     constexpr int ES = (int)sizeof(T), EPC = 16 / ES;
+    // k-steps per load chunk: 32 VGPRs of B fragments in flight (bf16); fp32 (parity mode) keeps 2 / 1
+    constexpr int KC = ES == 2 ? (MR >= 4 ? 2 : 4) : (MR >= 4 ? 1 : 2);
     using Raw = typename Tr<T>::Raw;
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
 
@@ -71,8 +73,8 @@ __global__ void __launch_bounds__(256, sizeof(T) == 2 ? (NR == 8 ? 3 : 4) : 1) c
             const int r = i / cpr, c = i - r * cpr;
             *reinterpret_cast<uint4 *>(smem + (size_t)r * KS * ES + c * 16) = src[i];
         }
-        for (int i = tid; i < a.Ksteps * 4; i += 256) {
-            const int g = a.gtab[i];
+        for (int i = tid; i < ((a.Ksteps + 3) & ~3) * 4; i += 256) {
+            const int g = i < a.Ksteps * 4 ? a.gtab[i] : (int)0xffff0000u;
             const int dy = (int)(signed char)(g & 0xff), dx = (int)(signed char)((g >> 8) & 0xff);
             const int coff = (g >> 16) & 0xffff;
             gt[i] = coff == 0xffff ? make_int4(TAP_PAD, 0, 0, 0)
@@ -124,26 +126,73 @@ __global__ void __launch_bounds__(256, sizeof(T) == 2 ? (NR == 8 ? 3 : 4) : 1) c
             x0[m] = px[m] * a.stride;
             boff[m] = (uint32_t)(((pn[m] * a.Hin + py[m] * a.stride) * a.Win + x0[m]) * a.CinS) * ES;
         }
+        // Epilogue operands that do not depend on the accumulators are requested before the k loop, so
+        // their latency hides under it: the staged residual chunks (EPI_RESADD) and the unpooling
+        // indices + low-res main values (EPI_RESUNPOOL). Kept raw; converted where used.
+        constexpr int RQ = (NR * 4 / EPC) > 0 ? NR * 4 / EPC : 1;      // >= 16*CPR/64 chunks per lane
+        uint4 rpre[EPI == EPI_RESADD ? MR : 1][RQ];
+        uint32_t upid[EPI == EPI_RESUNPOOL ? MR : 1][NR];
+        MvRaw<T> upmv[EPI == EPI_RESUNPOOL ? MR : 1][NR];
+        const int CPR = 1 << a.cpr_sh;
+        if constexpr (EPI == EPI_RESADD) {
+            if (a.stage_ok && a.resCS == a.outC) {
+#pragma unroll
+                for (int m = 0; m < MR; ++m) {
+                    const int p0 = tile * TILE + wave * MR * 16 + m * 16;
+#pragma unroll
+                    for (int k = 0; k < RQ; ++k) {
+                        const int q = lane + 64 * k;
+                        const bool ok = q < 16 * CPR && p0 + (q >> a.cpr_sh) < a.M;
+                        rpre[m][k] = bld16(rres, ok ? (uint32_t)(p0 * a.outC + q * EPC) * ES : OOB);
+                    }
+                }
+            }
+        }
+        if constexpr (EPI == EPI_RESUNPOOL) {
+            const auto ridx = mkbuf(a.idx_in, a.idx_bytes);
+#pragma unroll
+            for (int m = 0; m < MR; ++m) {
+                const uint32_t lpix = (uint32_t)((pn[m] * a.resH + (py[m] >> 1)) * a.resW + (px[m] >> 1));
+#pragma unroll
+                for (int n = 0; n < NR; ++n) {
+                    const int c = n * 16 + kq * 4;
+                    const bool ok = pv[m] && c < a.resC;
+                    upid[m][n] = __builtin_amdgcn_raw_buffer_load_b32(ridx, ok ? (int)(lpix * a.idxCS + c) : (int)OOB, 0, 0);
+                    upmv[m][n] = mvload<T>(rres, ok ? (lpix * a.resCS + c) * ES : OOB);
+                }
+            }
+        }
+
         f32x4 acc[MR][NR];
 #pragma unroll
         for (int m = 0; m < MR; ++m)
 #pragma unroll
             for (int n = 0; n < NR; ++n) acc[m][n] = (f32x4){0.f, 0.f, 0.f, 0.f};
 
-        for (int s = 0; s < a.Ksteps; ++s) {
-            const int4 g = gt[s * 4 + kq];
-            Raw xf[MR];
+        // KC k-steps per chunk: all their B-fragment loads are issued before the first MFMA, so a
+        // tile waits on memory ceil(Ksteps / KC) times instead of Ksteps times (the tap table is padded
+        // with always-out-of-range entries to whole chunks; MFMAs past Ksteps are skipped)
+        for (int s0 = 0; s0 < a.Ksteps; s0 += KC) {
+            Raw xf[KC][MR];
 #pragma unroll
-            for (int m = 0; m < MR; ++m) {
-                const bool ok = (unsigned)(y0[m] + g.x) < (unsigned)a.Hin && (unsigned)(x0[m] + g.y) < (unsigned)a.Win;
-                bld8(xf[m], rin, ok ? boff[m] + (uint32_t)g.z : OOB);
+            for (int kc = 0; kc < KC; ++kc) {
+                const int4 g = gt[(s0 + kc) * 4 + kq];
+#pragma unroll
+                for (int m = 0; m < MR; ++m) {
+                    const bool ok = (unsigned)(y0[m] + g.x) < (unsigned)a.Hin && (unsigned)(x0[m] + g.y) < (unsigned)a.Win;
+                    bld8(xf[kc][m], rin, ok ? boff[m] + (uint32_t)g.z : OOB);
+                }
             }
 #pragma unroll
-            for (int n = 0; n < NR; ++n) {
-                Raw wf;
-                ld8(wf, wl + (n * 16 + col) * KS + s * 32 + kq * 8);
+            for (int kc = 0; kc < KC; ++kc) {
+                if (s0 + kc >= a.Ksteps) break;
 #pragma unroll
-                for (int m = 0; m < MR; ++m) mma(acc[m][n], wf, xf[m]);
+                for (int n = 0; n < NR; ++n) {
+                    Raw wf;
+                    ld8(wf, wl + (n * 16 + col) * KS + (s0 + kc) * 32 + kq * 8);
+#pragma unroll
+                    for (int m = 0; m < MR; ++m) mma(acc[m][n], wf, xf[kc][m]);
+                }
             }
         }
 
@@ -203,7 +252,7 @@ __global__ void __launch_bounds__(256, sizeof(T) == 2 ? (NR == 8 ? 3 : 4) : 1) c
             const bool staged = a.stage_ok;
             T *stg = stage_base + wave * a.stg_elems;
             const int OSTR = a.outC + EPC;
-            const int csh = a.cpr_sh, CPR = 1 << csh;
+            const int csh = a.cpr_sh;
             // EPI_SHUFFLE: output phase and channel of accumulator fragment n (coutP is a multiple of 16)
             int phn[NR], cln[NR];
 #pragma unroll
@@ -215,10 +264,11 @@ __global__ void __launch_bounds__(256, sizeof(T) == 2 ? (NR == 8 ? 3 : 4) : 1) c
                 bool res_staged = false;
                 if constexpr (EPI == EPI_RESADD) {
                     if (staged && a.resCS == a.outC) {
-                        for (int q = lane; q < 16 * CPR; q += 64) {
-                            const int pix = q >> csh;
-                            const uint32_t off = p0 + pix < a.M ? (uint32_t)(p0 * a.outC + q * EPC) * ES : OOB;
-                            *reinterpret_cast<uint4 *>(stg + pix * OSTR + (q & (CPR - 1)) * EPC) = bld16(rres, off);
+#pragma unroll
+                        for (int k = 0; k < RQ; ++k) {
+                            const int q = lane + 64 * k;
+                            if (q < 16 * CPR)
+                                *reinterpret_cast<uint4 *>(stg + (q >> csh) * OSTR + (q & (CPR - 1)) * EPC) = rpre[m][k];
                         }
                         wave_lds_sync();
                         res_staged = true;
@@ -272,10 +322,9 @@ __global__ void __launch_bounds__(256, sizeof(T) == 2 ? (NR == 8 ? 3 : 4) : 1) c
                         // MaxUnpool2d(2): the low-res main value lands on the window position its
                         // pooling index recorded; every other position of the window is 0.
                         if (c < a.resC) {
-                            const uint32_t lpix = (uint32_t)((pn[m] * a.resH + (py[m] >> 1)) * a.resW + (px[m] >> 1));
-                            const uint32_t id = *reinterpret_cast<const uint32_t *>(a.idx_in + lpix * a.idxCS + c);
+                            const uint32_t id = upid[m][n];
                             const uint32_t pos = (uint32_t)(((py[m] & 1) << 1) | (px[m] & 1));
-                            const float4 mv = bld4(rres, (lpix * a.resCS + c) * ES, (const T *)nullptr);
+                            const float4 mv = mvcvt(upmv[m][n]);
                             v.x += ((id & 0xff) == pos) ? mv.x : 0.f;
                             v.y += (((id >> 8) & 0xff) == pos) ? mv.y : 0.f;
                             v.z += (((id >> 16) & 0xff) == pos) ? mv.z : 0.f;

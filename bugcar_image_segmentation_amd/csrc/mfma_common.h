@@ -111,6 +111,26 @@ __device__ __forceinline__ float4 bld4(__amdgpu_buffer_rsrc_t r, uint32_t off, c
                        __uint_as_float(u.y << 16), __uint_as_float(u.y & 0xffff0000u));
 }
 
+// 4 consecutive elements kept raw (prefetched early, converted where used)
+template <typename T> struct MvRawT;
+template <> struct MvRawT<__bf16> { using type = u32x2; };
+template <> struct MvRawT<float> { using type = u32x4; };
+template <typename T> using MvRaw = typename MvRawT<T>::type;
+template <typename T> __device__ __forceinline__ MvRaw<T> mvload(__amdgpu_buffer_rsrc_t r, uint32_t off);
+template <> __device__ __forceinline__ u32x2 mvload<__bf16>(__amdgpu_buffer_rsrc_t r, uint32_t off) {
+    return __builtin_amdgcn_raw_buffer_load_b64(r, (int)off, 0, 0);
+}
+template <> __device__ __forceinline__ u32x4 mvload<float>(__amdgpu_buffer_rsrc_t r, uint32_t off) {
+    return __builtin_amdgcn_raw_buffer_load_b128(r, (int)off, 0, 0);
+}
+__device__ __forceinline__ float4 mvcvt(u32x2 u) {
+    return make_float4(__uint_as_float(u.x << 16), __uint_as_float(u.x & 0xffff0000u),
+                       __uint_as_float(u.y << 16), __uint_as_float(u.y & 0xffff0000u));
+}
+__device__ __forceinline__ float4 mvcvt(u32x4 u) {
+    return make_float4(__uint_as_float(u.x), __uint_as_float(u.y), __uint_as_float(u.z), __uint_as_float(u.w));
+}
+
 // Division by a runtime-invariant divisor d via a host-computed magic number (bugseg_runtime.cpp
 // fastdiv()): q = umulhi(n, m) >> s for d >= 2, s < 0 encodes d == 1. Exact for 0 <= n < 2^31.
 __device__ __forceinline__ uint32_t fdiv(uint32_t n, uint32_t m, int s) {
