@@ -100,8 +100,9 @@ __global__ void __launch_bounds__(BTile<C>::NW * 64, sizeof(T) == 2 ? BTile<C>::
     // the store (mfma_common.h), so image-border masking costs one select per access
     const auto rxb = mkbuf(a.x, a.x_bytes);
     const auto rob = mkbuf(a.out, a.x_bytes);
-    const bool fast = a.slopes_le1;
-    auto act = [&](float4 v, const float *s) { return fast ? prelu4m(v, ld4f(s)) : prelu4(v, ld4f(s)); };
+    // the fused path is planned only when every slope is <= 1 (bugseg_runtime.cpp fusable_regular),
+    // so PReLU is max(v, s*v); accumulators start at the bias
+    auto act = [&](float4 v, const float *s) { return prelu4m(v, ld4f(s)); };
     const int ry = a.ry, rx = a.rx, d = a.d;
     const int HWW = TW + 2 * rx, HR = (TH + 2 * ry) * HWW;
     const int nf1 = (HR + 15) >> 4;
@@ -141,7 +142,7 @@ __global__ void __launch_bounds__(BTile<C>::NW * 64, sizeof(T) == 2 ? BTile<C>::
                 const int h = (f0 + c * NW) * 16 + col;
                 f32x4 acc[NR1];
 #pragma unroll
-                for (int r = 0; r < NR1; ++r) acc[r] = (f32x4){0.f, 0.f, 0.f, 0.f};
+                for (int r = 0; r < NR1; ++r) acc[r] = bias4(cb1 + r * 16 + kq * 4);
 #pragma unroll
                 for (int s = 0; s < KS1; ++s)
 #pragma unroll
@@ -155,7 +156,7 @@ __global__ void __launch_bounds__(BTile<C>::NW * 64, sizeof(T) == 2 ? BTile<C>::
                     for (int r = 0; r < NR1; ++r) {
                         const int ch = r * 16 + kq * 4;
                         if (ch >= IS) continue;
-                        float4 v = act(add4(f4(acc[r]), ld4f(cb1 + ch)), cs1 + ch);
+                        float4 v = act(f4(acc[r]), cs1 + ch);
                         if (!okc[c]) v = make_float4(0.f, 0.f, 0.f, 0.f);
                         st4(ts + h * PSTR + ch, v);
                     }
@@ -190,7 +191,7 @@ __global__ void __launch_bounds__(BTile<C>::NW * 64, sizeof(T) == 2 ? BTile<C>::
 #pragma unroll
             for (int j = 0; j < NF2; ++j)
 #pragma unroll
-                for (int r = 0; r < NR1; ++r) acc[j][r] = (f32x4){0.f, 0.f, 0.f, 0.f};
+                for (int r = 0; r < NR1; ++r) acc[j][r] = bias4(cb2 + r * 16 + kq * 4);
 #pragma unroll 1
             for (int s = 0; s < KS2; ++s) {
                 const int g = s * 4 + kq;
@@ -219,7 +220,7 @@ __global__ void __launch_bounds__(BTile<C>::NW * 64, sizeof(T) == 2 ? BTile<C>::
                 for (int r = 0; r < NR1; ++r) {
                     const int ch = r * 16 + kq * 4;
                     if (ch >= IS) continue;
-                    st4(ts + p * PSTR + ch, act(add4(f4(acc[j][r]), ld4f(cb2 + ch)), cs2 + ch));
+                    st4(ts + p * PSTR + ch, act(f4(acc[j][r]), cs2 + ch));
                 }
             }
         } else {
@@ -228,7 +229,7 @@ __global__ void __launch_bounds__(BTile<C>::NW * 64, sizeof(T) == 2 ? BTile<C>::
 #pragma unroll
                 for (int j = 0; j < NF2A; ++j)
 #pragma unroll
-                    for (int r = 0; r < NR1; ++r) acc[j][r] = (f32x4){0.f, 0.f, 0.f, 0.f};
+                    for (int r = 0; r < NR1; ++r) acc[j][r] = bias4(cb2 + r * 16 + kq * 4);
 #pragma unroll 1
                 for (int s = 0; s < KS2; ++s) {
                     const int g = s * 4 + kq;
@@ -260,7 +261,7 @@ __global__ void __launch_bounds__(BTile<C>::NW * 64, sizeof(T) == 2 ? BTile<C>::
                     for (int r = 0; r < NR1; ++r) {
                         const int ch = r * 16 + kq * 4;
                         if (ch >= IS) continue;
-                        float4 v = act(add4(f4(acc[j][r]), ld4f(cb2 + ch)), cs2 + ch);
+                        float4 v = act(f4(acc[j][r]), cs2 + ch);
                         if (!inside) v = make_float4(0.f, 0.f, 0.f, 0.f);
                         st4(ts + p * PSTR + ch, v);
                     }
@@ -272,7 +273,7 @@ __global__ void __launch_bounds__(BTile<C>::NW * 64, sizeof(T) == 2 ? BTile<C>::
 #pragma unroll
                 for (int j = 0; j < NF2; ++j)
 #pragma unroll
-                    for (int r = 0; r < NR1; ++r) acc[j][r] = (f32x4){0.f, 0.f, 0.f, 0.f};
+                    for (int r = 0; r < NR1; ++r) acc[j][r] = bias4(cb2b + r * 16 + kq * 4);
 #pragma unroll 1
                 for (int s = 0; s < KS2; ++s) {
                     const int g = s * 4 + kq;
@@ -300,7 +301,7 @@ __global__ void __launch_bounds__(BTile<C>::NW * 64, sizeof(T) == 2 ? BTile<C>::
                     for (int r = 0; r < NR1; ++r) {
                         const int ch = r * 16 + kq * 4;
                         if (ch >= IS) continue;
-                        st4(ts + p * PSTR + ch, act(add4(f4(acc[j][r]), ld4f(cb2b + ch)), cs2b + ch));
+                        st4(ts + p * PSTR + ch, act(f4(acc[j][r]), cs2b + ch));
                     }
                 }
             }
@@ -332,13 +333,13 @@ __global__ void __launch_bounds__(BTile<C>::NW * 64, sizeof(T) == 2 ? BTile<C>::
             wave_lds_sync();
 #pragma unroll
             for (int r = 0; r < NR3; ++r) {
-                f32x4 acc = (f32x4){0.f, 0.f, 0.f, 0.f};
+                const int ch = r * 16 + kq * 4;
+                f32x4 acc = bias_in_acc(NR3) ? bias4(cb3 + ch) : (f32x4){0.f, 0.f, 0.f, 0.f};
                 Raw wf;
                 ld8(wf, w3 + (r * 16 + col) * K3S + kq * 8);
                 mma(acc, wf, tf[j]);
-                const int ch = r * 16 + kq * 4;
                 T *sp = stg + col * OSTR + ch;
-                float4 v = act(add4(f4(acc), ld4f(cb3 + ch)), cs3 + ch);
+                float4 v = act(bias_in_acc(NR3) ? f4(acc) : add4(f4(acc), ld4f(cb3 + ch)), cs3 + ch);
                 v = act(add4(v, ld4(sp)), cso + ch);
                 st4(sp, v);
             }

@@ -478,9 +478,16 @@ ConvArgs base_args(const bugseg_ctx *ctx, const Packed &p) {
 // kernel is built for and the halo of its middle conv stays small (recomputed projection <= 3x the
 // tile: dilation <= 4 on 16x16 tiles); otherwise as its 3-4 conv launches. BUGSEG_NO_FUSE=1 forces
 // the unfused plan (A/B testing; results are bit-identical).
-bool fusable_regular(const bugseg_ctx *ctx, const BlockDesc &b, int &ry, int &rx, int &d) {
+bool fusable_regular(const bugseg_ctx *ctx, const BlockDesc &b, const std::vector<int> &ids, int &ry, int &rx, int &d) {
     const char *env = std::getenv("BUGSEG_NO_FUSE");     // read per plan build (plans are cached)
     if (env && *env && *env != '0') return false;
+    // the fused kernel computes PReLU as max(v, s*v), exact only for slopes <= 1
+    for (const int id : ids) {
+        const Packed &p = ctx->packed[id];
+        const float *s1 = (const float *)(ctx->host_w.data() + p.o_s1), *s2 = (const float *)(ctx->host_w.data() + p.o_s2);
+        for (int c = 0; c < p.Npad; ++c)
+            if (!(s1[c] <= 1.f) || !(s2[c] <= 1.f)) return false;
+    }
     const int C = b.attrs[0];
     if (C != 128 && C != 64 && C != 16) return false;
     const int nu = (int)b.units.size();
@@ -591,7 +598,7 @@ struct Walker {
                 Shape s = cur;
                 const unsigned char *src = curp;
                 int ry = 0, rx = 0, dd = 1;
-                if (fusable_regular(ctx, b, ry, rx, dd)) {
+                if (fusable_regular(ctx, b, ids, ry, rx, dd)) {
                     // one launch: projection + middle conv + expansion + residual, internals in LDS
                     szX = std::max(szX, tbytes(cur));
                     if (fill) {

@@ -53,8 +53,9 @@ __global__ void __launch_bounds__(256, sizeof(T) == 2 ? (NR == 8 ? 3 : 4) : 1) c
     constexpr int MR = Cfg<NR>::MR;
     constexpr int TILE = 4 * MR * 16;
     constexpr int ES = (int)sizeof(T), EPC = 16 / ES;
-    // k-steps per load chunk: 32 VGPRs of B fragments in flight (bf16); fp32 (parity mode) keeps 2 / 1
-    constexpr int KC = ES == 2 ? (MR >= 4 ? 2 : 4) : (MR >= 4 ? 1 : 2);
+    // k-steps per load chunk: 32 VGPRs of B fragments in flight (bf16; 16 beside NR 8's 64 accumulator
+    // VGPRs); fp32 (parity mode) keeps half
+    constexpr int KC = ES == 2 ? (MR >= 4 || NR >= 8 ? 2 : 4) : (MR >= 4 || NR >= 8 ? 1 : 2);
     using Raw = typename Tr<T>::Raw;
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
 
@@ -167,7 +168,8 @@ __global__ void __launch_bounds__(256, sizeof(T) == 2 ? (NR == 8 ? 3 : 4) : 1) c
 #pragma unroll
         for (int m = 0; m < MR; ++m)
 #pragma unroll
-            for (int n = 0; n < NR; ++n) acc[m][n] = (f32x4){0.f, 0.f, 0.f, 0.f};
+            for (int n = 0; n < NR; ++n)
+                acc[m][n] = bias_in_acc(NR) ? bias4(cbias + n * 16 + kq * 4) : (f32x4){0.f, 0.f, 0.f, 0.f};
 
         // KC k-steps per chunk: all their B-fragment loads are issued before the first MFMA, so a
         // tile waits on memory ceil(Ksteps / KC) times instead of Ksteps times (the tap table is padded
@@ -213,8 +215,8 @@ __global__ void __launch_bounds__(256, sizeof(T) == 2 ? (NR == 8 ? 3 : 4) : 1) c
 #pragma unroll
                 for (int n = 0; n < NR; ++n) {
                     const int c = n * 16 + kq * 4;
-                    *reinterpret_cast<float4 *>(cstg + (n * 16 + col) * CLS_STR + kq * 4) =
-                        add4(f4(acc[m][n]), ld4f(cbias + c));
+                    static_assert(bias_in_acc(NR), "EPI_CLASSES: bias in the accumulator");
+                    *reinterpret_cast<float4 *>(cstg + (n * 16 + col) * CLS_STR + kq * 4) = f4(acc[m][n]);
                 }
                 wave_lds_sync();
                 const int p = tile * TILE + wave * MR * 16 + m * 16 + rc;
@@ -277,7 +279,7 @@ __global__ void __launch_bounds__(256, sizeof(T) == 2 ? (NR == 8 ? 3 : 4) : 1) c
 #pragma unroll
                 for (int n = 0; n < NR; ++n) {
                     const int c = n * 16 + kq * 4;
-                    float4 v = add4(f4(acc[m][n]), ld4f(cbias + c));
+                    float4 v = bias_in_acc(NR) ? f4(acc[m][n]) : add4(f4(acc[m][n]), ld4f(cbias + c));
                     if constexpr (EPI == EPI_SHUFFLE) {
                         const int ph = phn[n], cl = cln[n] + kq * 4;
                         if (cl >= a.outC) continue;

@@ -6,8 +6,9 @@
 // (v/256 - mean)/std table is applied as the bytes enter LDS) or the engine input (EPI_INIT:
 // NHWC, 8 storage channels, 3 used). A 256-thread workgroup owns an 8 x 32 output tile:
 //   * the 17 x 65 x 3 input patch is read once — thread q < 195 owns byte column q of all 17 rows,
-//     each row one contiguous run, addressed as (column voffset, row soffset) so the loads cost
-//     no VALU — and stored normalised in LDS (zero outside the frame = the conv's zero padding);
+//     each row one contiguous run, 17 buffer loads in flight per thread, out-of-frame ones masked by
+//     an out-of-range offset — and stored normalised in LDS (zero outside the frame = the conv's
+//     zero padding);
 //   * K = 27 dense, ordered so that lanes of k group kq < 3 read the 8 consecutive patch elements
 //     (3 pixels x 3 channels, minus the last) of window row kq with four 4-byte LDS reads, and group 3
 //     the three leftovers: one v_mfma_f32_16x16x32 per 16 output pixels;
@@ -161,9 +162,9 @@ __global__ void __launch_bounds__(256) init_kernel(const ConvArgs a) {
                 for (int j = 0; j < 8; ++j) xv[j] = j < 3 ? pp[j * IP_RS + 8] : (T)0.f;
                 set8(xf, xv);
             }
-            f32x4 acc = (f32x4){0.f, 0.f, 0.f, 0.f};
+            f32x4 acc = (f32x4){b4.x, b4.y, b4.z, b4.w};   // the MFMA adds the bias
             mma(acc, wf, xf);
-            float4 v = add4(f4(acc), b4);
+            float4 v = f4(acc);
             // this fragment's pool maxima for pixel col live in lane col + 16 f
             float pv[4] = {0.f, 0.f, 0.f, 0.f};
             const int src = (col + 16 * f) << 2;

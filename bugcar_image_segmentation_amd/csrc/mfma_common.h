@@ -139,8 +139,23 @@ __device__ __forceinline__ uint32_t fdiv(uint32_t n, uint32_t m, int s) {
 
 __device__ __forceinline__ float prelu(float v, float s) { return v > 0.f ? v : v * s; }
 // == prelu when s <= 1 (v > 0: v*s <= v; v < 0: v*s >= v): 2 VALU instead of 3
+// (a bare v_max_f32: fmaxf would add a NaN-quieting v_max per operand in IEEE mode)
+__device__ __forceinline__ float vmax(float a, float b) {
+    float r;
+    asm("v_max_f32 %0, %1, %2" : "=v"(r) : "v"(a), "v"(b));
+    return r;
+}
 __device__ __forceinline__ float4 prelu4m(float4 v, float4 s) {
-    return make_float4(fmaxf(v.x, v.x * s.x), fmaxf(v.y, v.y * s.y), fmaxf(v.z, v.z * s.z), fmaxf(v.w, v.w * s.w));
+    return make_float4(vmax(v.x, v.x * s.x), vmax(v.y, v.y * s.y), vmax(v.z, v.z * s.z), vmax(v.w, v.w * s.w));
+}
+// Accumulators start at the bias (the MFMA adds it for free) for outputs of fewer than 8 16-row
+// fragments; with 8 (128 channels) the bias comes after, since bias-initialised accumulators are live
+// across the k loop's loads and would spill. Both kernels follow this rule, so a fused bottleneck and
+// its unfused launches stay bit-identical.
+__host__ __device__ constexpr bool bias_in_acc(int nr) { return nr < 8; }
+__device__ __forceinline__ f32x4 bias4(const float *p) {
+    const float4 b = *reinterpret_cast<const float4 *>(p);
+    return (f32x4){b.x, b.y, b.z, b.w};
 }
 __device__ __forceinline__ float4 prelu4(float4 v, float4 s) {
     return make_float4(prelu(v.x, s.x), prelu(v.y, s.y), prelu(v.z, s.z), prelu(v.w, s.w));
