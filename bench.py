@@ -1,17 +1,23 @@
 """Benchmark: frames/sec of the ENet 640x480 segmentation -> BEV occupancy-grid path on MI355X.
 
 One "step" = one pass of the hot path over one batch of synthetic 640x480x3 BGR frames already
-resident in HBM: preprocess kernel -> ENet forward (89 fused conv launches, argmax + 3-class remap
-in the last epilogue) -> fused BEV rasteriser -> (N > 1) RCCL all-gather of the int8 grids.
-Per-GPU batch is fixed (weak scaling): rank r of N owns `--batch` frames of the N*batch global batch
-(BASELINE configs 3 and 5: 64 frames per GPU = config 5's share at N=8).
+resident in HBM: ENet forward (47 launches: the initial block normalises the raw bytes as it loads
+them, regular bottlenecks run fused, argmax + 3-class remap in the last epilogue) -> fused BEV
+rasteriser -> (N > 1) RCCL all-gather of the int8 grids. The batch is split into `--streams` frame
+shards run concurrently on their own HIP streams. Per-GPU batch is fixed (weak scaling): rank r of N
+owns `--batch` frames of the N*batch global batch (BASELINE configs 3 and 5: 64 frames per GPU =
+config 5's share at N=8).
 
 Run:  python bench.py [--gpus N --steps K --warmup W]
       python -m torch.distributed.run --nproc-per-node N --master-addr 127.0.0.1 ... bench.py --gpus N
-Rank 0 prints ONE JSON line. Roofline: the ENet forward's algorithmic bytes (per-layer activation
-reads + writes + weights, from the engine's launch plan) / its measured duration (HIP events on the
-stream the kernels run on), against the 8 TB/s HBM peak; the CPU oracle (PyTorch-CPU ENet + C BEV
-restatement) is timed on a bounded sample on rank 0 as the reported CPU baseline.
+Rank 0 prints ONE JSON line. `roofline` describes the dominant kernel of the forward (largest total
+time): the bytes one launch must move (block input read once, output written once) / its average
+launch duration, measured here with HIP events around every launch of one forward on the stream the
+kernels run on, against the 8 TB/s HBM peak; `traffic` is the PMC-measured HBM bytes per launch of
+that kernel from the committed profile (profiles/pmc_traffic.json). `roofline.forward` adds the
+whole-forward figures (SURVEY.md 8(d)'s 180.2 MB/frame per-layer definition and the plan's own byte
+counts). The CPU oracle (PyTorch-CPU ENet + C BEV restatement) is timed on a bounded sample on rank 0
+as the reported CPU baseline.
 """
 from __future__ import annotations
 
@@ -31,6 +37,52 @@ import torch.distributed as dist  # noqa: E402
 HBM_PEAK_GBS = 8000.0          # MI355X_MICROARCH.md chip table (spec)
 MFMA_BF16_PEAK_TFLOPS = 2500.0  # dense bf16 (spec)
 MFMA_F32_PEAK_TFLOPS = 157.3
+
+
+SURVEY_BYTES_PER_FRAME = 180.2e6   # bf16 per-layer activation bytes per 480x640 frame
+# rocprofv3 kernel names of the plan's kernel tags (scripts/layer_times.py maps them back)
+KERNEL_NAMES = {"bneck C128": "bneck_kernel<bf16,128,sym>", "bneck C128 asym": "bneck_kernel<bf16,128,asym>",
+                "bneck C64": "bneck_kernel<bf16,64,sym>", "bneck C16": "bneck_kernel<bf16,16,sym>",
+                "init": "init_kernel<bf16,bgr>"}
+
+
+def kernel_table(ctx, B, H, W, reps, stream):
+    """Per-launch durations of the forward the context last ran, measured with HIP events recorded
+    around every launch on the stream the kernels run on, in forward order (so each kernel sees the
+    cache state it has in the pipeline). Grouped by kernel tag."""
+    n = ctx.plan_info(B, H, W, 2)[0]
+    info = [ctx.plan_op(B, H, W, i) for i in range(n)]
+    evs = [[torch.cuda.Event(enable_timing=True) for _ in range(n + 1)] for _ in range(reps)]
+    for r in range(reps):
+        for i in range(n):
+            evs[r][i].record(stream)
+            ctx.launch_op(B, H, W, i, stream)
+        evs[r][n].record(stream)
+    torch.cuda.synchronize()
+    groups = {}
+    for i, (tag, _lb, pb, _fl) in enumerate(info):
+        us = sum(evs[r][i].elapsed_time(evs[r][i + 1]) for r in range(reps)) / reps * 1e3
+        gr = groups.setdefault(tag, {"launches": 0, "total_us": 0.0, "bytes": 0.0})
+        gr["launches"] += 1
+        gr["total_us"] += us
+        gr["bytes"] += pb
+    for gr in groups.values():
+        gr["us_per_launch"] = gr["total_us"] / gr["launches"]
+        gr["bytes_per_launch"] = gr["bytes"] / gr["launches"]
+    return groups
+
+
+def pmc_traffic(tag):
+    """HBM bytes per launch of `tag` from the committed PMC summary (profiles/pmc_traffic.json, written
+    by scripts/pmc_summary.py from rocprofv3 FETCH_SIZE / WRITE_SIZE passes of this bench), or None."""
+    p = os.path.join(ROOT, "profiles", "pmc_traffic.json")
+    try:
+        with open(p) as f:
+            t = json.load(f)
+        v = t.get("per_launch_bytes", {}).get(tag)
+        return None if v is None else round(float(v))
+    except (OSError, ValueError):
+        return None
 
 
 def parse():
@@ -120,31 +172,36 @@ def main():
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         el = float(t.item())
 
-    # ---- per-stage timing with HIP events on the stream the kernels are launched on (untimed region)
+    # ---- per-stage and per-kernel timing with HIP events on the stream the kernels are launched on
+    # (untimed region), at the shard size the timed region launched (shard 0 runs on model.ctx), so every
+    # launch of this command has one shape and rocprof's per-kernel averages describe the same launches
     stream = torch.cuda.current_stream()
+    Bs = B // a.streams if a.streams > 1 and B >= a.streams else B
     x, seg, g = pipe._bufs(B, dev)
+    fs, ss, gs = frames[:Bs], seg[:Bs], g[:Bs]
     reps = max(3, min(20, a.steps))
     ev = [torch.cuda.Event(enable_timing=True) for _ in range(3)]
     t_fwd = t_bev = 0.0
     for _ in range(reps):
         # frames are already at the model resolution: preprocess is fused into the initial block
         ev[0].record(stream)
-        model.ctx.forward_bgr(frames, B, H, W, N.OUT_CLASS3_U8, seg)
+        model.ctx.forward_bgr(fs, Bs, H, W, N.OUT_CLASS3_U8, ss)
         ev[1].record(stream)
-        bev.create_occupancy_grid_device(seg, *grid, out=g)
+        bev.create_occupancy_grid_device(ss, *grid, out=gs)
         ev[2].record(stream)
         ev[2].synchronize()
         t_fwd += ev[0].elapsed_time(ev[1])
         t_bev += ev[1].elapsed_time(ev[2])
-    t_pre, t_fwd, t_bev = 0.0, t_fwd / reps, t_bev / reps
-    n_launch, alg_bytes, plan_bytes, flops = model.ctx.plan_info(B, H, W, N.OUT_CLASS3_U8, bgr_input=True)
-    achieved = alg_bytes / (t_fwd * 1e-3) / 1e9
-    moved = plan_bytes / (t_fwd * 1e-3) / 1e9
-    tflops = flops / (t_fwd * 1e-3) / 1e12
+    t_fwd, t_bev = t_fwd / reps, t_bev / reps
+    n_launch, alg_bytes, plan_bytes, flops = model.ctx.plan_info(Bs, H, W, N.OUT_CLASS3_U8, bgr_input=True)
+    kernels = kernel_table(model.ctx, Bs, H, W, reps, stream)
 
     if rank == 0:
         frames_total = B * world * a.steps
         value = frames_total / el
+        tag, k = max(kernels.items(), key=lambda kv: kv[1]["total_us"])
+        k_achieved = k["bytes_per_launch"] / (k["us_per_launch"] * 1e-6) / 1e9
+        traffic = pmc_traffic(tag)
         res = {
             "metric": "frames/sec ENet 640x480 segmentation -> BEV occupancy grid (synthetic), whole job",
             "value": round(value, 2), "unit": "frames/s", "n_gpus": world, "steps": a.steps, "warmup": a.warmup,
@@ -156,16 +213,31 @@ def main():
                        "global_batch": B * world, "per_gpu_batch": B, "height": H, "width": W,
                        "parallelism": f"frame-sharded dp{world}" + (" + RCCL all-gather of grids" if world > 1 else ""),
                        "streams_per_gpu": a.streams},
-            "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                         "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": None,
-                         "kernel": f"ENet forward: {n_launch} launches (conv_kernel + fused bneck_kernel, one plan); "
-                                   f"{alg_bytes / B / 1e6:.1f} MB/frame per-layer algorithmic bytes (SURVEY 8(d) "
-                                   f"definition); the fused plan must move {plan_bytes / B / 1e6:.1f} MB/frame",
-                         "plan_bytes_per_frame": round(plan_bytes / B),
-                         "plan_achieved_gbs": round(moved, 1), "plan_frac": round(moved / HBM_PEAK_GBS, 4),
-                         "mfma_tflops": round(tflops, 2),
-                         "mfma_frac": round(tflops / (MFMA_BF16_PEAK_TFLOPS if a.precision == "bf16" else MFMA_F32_PEAK_TFLOPS), 4)},
-            "stages_ms": {"preprocess": round(t_pre, 4), "enet_forward": round(t_fwd, 4), "bev_occgrid": round(t_bev, 4)},
+            "roofline": {
+                "bound": "hbm", "achieved": round(k_achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                "frac": round(k_achieved / HBM_PEAK_GBS, 4),
+                "traffic": traffic,
+                "kernel": f"{KERNEL_NAMES.get(tag, tag)} [{tag}]: the dominant kernel of the forward "
+                          f"({k['launches']} launches, {k['total_us']:.0f} us of {t_fwd * 1e3:.0f} us); "
+                          f"{k['bytes_per_launch'] / 1e6:.1f} MB per launch = the bytes the launch must move "
+                          f"(block input read once + output written once); {k['us_per_launch']:.2f} us per launch "
+                          f"(HIP events around each launch, in forward order)",
+                "forward": {
+                    "launches": n_launch, "ms": round(t_fwd, 4),
+                    "survey_bytes_per_frame": SURVEY_BYTES_PER_FRAME,
+                    "frames": Bs,
+                    "survey_achieved_gbs": round(SURVEY_BYTES_PER_FRAME * Bs / (t_fwd * 1e-3) / 1e9, 1),
+                    "plan_layer_bytes_per_frame": round(alg_bytes / Bs),
+                    "plan_bytes_per_frame": round(plan_bytes / Bs),
+                    "plan_achieved_gbs": round(plan_bytes / (t_fwd * 1e-3) / 1e9, 1),
+                    "mfma_tflops": round(flops / (t_fwd * 1e-3) / 1e12, 2),
+                    "mfma_frac": round(flops / (t_fwd * 1e-3) / 1e12 /
+                                       (MFMA_BF16_PEAK_TFLOPS if a.precision == "bf16" else MFMA_F32_PEAK_TFLOPS), 4)},
+            },
+            "kernels": {t: {"launches": v["launches"], "us_per_launch": round(v["us_per_launch"], 2),
+                            "GBps": round(v["bytes_per_launch"] / (v["us_per_launch"] * 1e-6) / 1e9, 1)}
+                        for t, v in sorted(kernels.items(), key=lambda kv: -kv[1]["total_us"])},
+            "stages_ms": {"frames": Bs, "enet_forward": round(t_fwd, 4), "bev_occgrid": round(t_bev, 4)},
         }
         if not a.no_cpu_baseline:
             res["cpu_baseline"] = cpu_baseline(blocks, bev, grid, H, W, a.cpu_baseline_seconds)

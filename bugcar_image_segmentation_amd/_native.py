@@ -24,7 +24,8 @@ PRE_ENGINE, PRE_NCHW_F64, PRE_NCHW_F32, PRE_BGR_U8 = 0, 1, 2, 3
 EXPORTED = ("bugseg_version", "bugseg_create", "bugseg_destroy", "bugseg_load_weights", "bugseg_num_classes",
             "bugseg_input_bytes", "bugseg_preprocess", "bugseg_nchw_to_input", "bugseg_enet_forward",
             "bugseg_enet_forward_bgr",
-            "bugseg_bev_occgrid", "bugseg_plan_info", "bugseg_last_error")
+            "bugseg_bev_occgrid", "bugseg_plan_info", "bugseg_plan_op", "bugseg_plan_launch_op",
+            "bugseg_last_error")
 
 
 class BevParams(ctypes.Structure):
@@ -70,6 +71,9 @@ def load_library(path: Path | str | None = None) -> ctypes.CDLL:
             "bugseg_bev_occgrid": (i, [vp, vp, i, ctypes.POINTER(BevParams), vp, vp]),
             "bugseg_plan_info": (i, [vp, i, i, i, i, i, ctypes.POINTER(i), ctypes.POINTER(ctypes.c_double),
                                      ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_double)]),
+            "bugseg_plan_op": (i, [vp, i, i, i, i, cp, i, ctypes.POINTER(ctypes.c_double),
+                                   ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_double)]),
+            "bugseg_plan_launch_op": (i, [vp, i, i, i, i, vp]),
             "bugseg_last_error": (cp, [vp]),
         }
         for name, (res, args) in proto.items():
@@ -162,6 +166,19 @@ class Context:
         check(self.lib.bugseg_plan_info(self.h, B, H, W, out_kind, int(bool(bgr_input)), ctypes.byref(n),
                                         ctypes.byref(lb), ctypes.byref(pb), ctypes.byref(fl)), self.h)
         return n.value, lb.value, pb.value, fl.value
+
+    def plan_op(self, B, H, W, op):
+        """Profiling hook: -> (kernel tag, per-layer algorithmic bytes, bytes the launch moves, flops)
+        of launch `op` of the plan the last forward at (B, H, W) ran."""
+        buf = ctypes.create_string_buffer(64)
+        lb, pb, fl = ctypes.c_double(), ctypes.c_double(), ctypes.c_double()
+        check(self.lib.bugseg_plan_op(self.h, B, H, W, op, buf, 64, ctypes.byref(lb), ctypes.byref(pb),
+                                      ctypes.byref(fl)), self.h)
+        return buf.value.decode(), lb.value, pb.value, fl.value
+
+    def launch_op(self, B, H, W, op, stream=None):
+        """Profiling hook: enqueue launch `op` of that plan alone (its buffers must still be alive)."""
+        check(self.lib.bugseg_plan_launch_op(self.h, B, H, W, op, ctypes.c_void_p(stream_handle(stream))), self.h)
 
 
 _shared: dict[int, Context] = {}

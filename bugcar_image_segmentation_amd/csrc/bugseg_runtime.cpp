@@ -1032,4 +1032,51 @@ int bugseg_plan_info(bugseg_ctx *ctx, int B, int H, int W, int out_kind, int bgr
     return BUGSEG_OK;
 }
 
+int bugseg_plan_op(bugseg_ctx *ctx, int B, int H, int W, int op, char *kernel, int kernel_len, double *alg_bytes,
+                   double *plan_bytes, double *flops) {
+    if (!ctx) return fail(ctx, BUGSEG_EINVAL, "NULL ctx");
+    if (!ctx->loaded) return fail(ctx, BUGSEG_ESTATE, "no weights loaded");
+    Plan &pl = ctx->plan;
+    if (!pl.arena || pl.B != B || pl.H != H || pl.W != W) return fail(ctx, BUGSEG_ESTATE, "no forward has run at these dimensions");
+    if (op < 0 || op >= (int)pl.ops.size()) return fail(ctx, BUGSEG_EINVAL, "op index out of range");
+    const Op &o = pl.ops[op];
+    std::string tag;
+    if (o.kind == 1) tag = "bneck C" + std::to_string(o.bn_c) + (o.bn_asym ? " asym" : "");
+    else if (o.epi == EPI_INIT || o.epi == EPI_INIT_BGR) tag = "init";
+    else tag = "conv NR" + std::to_string(o.nr) + " E" + std::to_string(o.epi);
+    if (kernel && kernel_len > 0) {
+        std::strncpy(kernel, tag.c_str(), (size_t)kernel_len - 1);
+        kernel[kernel_len - 1] = 0;
+    }
+    double lb = o.layer_bytes >= 0 ? o.layer_bytes : o.bytes, pb = o.bytes;
+    const int es = ctx->prec == PREC_BF16 ? 2 : 4;
+    if (o.kind == 0 && o.epi == EPI_INIT_BGR) {           // raw BGR input: 3 B/px, not the 8-channel engine input
+        const double adj = (double)B * H * W * (8.0 * es - 3.0);
+        lb -= adj; pb -= adj;
+    }
+    if (o.kind == 0 && o.epi == EPI_CLASSES) {            // the output the last forward asked for
+        const double fin = o.a.logits_out ? (double)B * H * W * ctx->ncls * 4 : (double)B * H * W;
+        lb += fin; pb += fin;
+    }
+    if (alg_bytes) *alg_bytes = lb;
+    if (plan_bytes) *plan_bytes = pb;
+    if (flops) *flops = o.flops;
+    return BUGSEG_OK;
+}
+
+int bugseg_plan_launch_op(bugseg_ctx *ctx, int B, int H, int W, int op, void *stream) {
+    if (!ctx) return fail(ctx, BUGSEG_EINVAL, "NULL ctx");
+    if (!ctx->loaded) return fail(ctx, BUGSEG_ESTATE, "no weights loaded");
+    Plan &pl = ctx->plan;
+    if (!pl.arena || pl.B != B || pl.H != H || pl.W != W || !pl.ops.front().a.in)
+        return fail(ctx, BUGSEG_ESTATE, "no forward has run at these dimensions");
+    if (op < 0 || op >= (int)pl.ops.size()) return fail(ctx, BUGSEG_EINVAL, "op index out of range");
+    DeviceGuard g(ctx->device);
+    const Op &o = pl.ops[op];
+    hipError_t e = o.kind == 1 ? launch_bneck(ctx->prec, o.bn_c, o.bn_asym, o.bn, (hipStream_t)stream)
+                               : launch_conv(ctx->prec, o.nr, o.epi, o.a, (hipStream_t)stream);
+    if (e != hipSuccess) return fail(ctx, BUGSEG_EHIP, "launch of op " + std::to_string(op) + ": " + hipGetErrorString(e));
+    return BUGSEG_OK;
+}
+
 }  // extern "C"

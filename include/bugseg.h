@@ -136,6 +136,15 @@ int bugseg_bev_occgrid(bugseg_ctx *ctx, const uint8_t *seg_dev, int B, const bug
 int bugseg_plan_info(bugseg_ctx *ctx, int B, int H, int W, int out_kind, int bgr_input, int *n_launches,
                      double *alg_bytes, double *plan_bytes, double *flops);
 
+/* Profiling hooks (no reference counterpart): one launch of the cached plan for (B, H, W), as the
+ * last forward call at those dimensions left it (its input / output buffers must still be alive).
+ * bugseg_plan_op: kernel tag ("init", "conv NR<n> E<epilogue>", "bneck C<c>[ asym]") and the
+ * launch's per-layer algorithmic bytes, the bytes it must move, and its flops.
+ * bugseg_plan_launch_op: enqueue that one launch on `stream` (bench.py times kernels with it). */
+int bugseg_plan_op(bugseg_ctx *ctx, int B, int H, int W, int op, char *kernel, int kernel_len, double *alg_bytes,
+                   double *plan_bytes, double *flops);
+int bugseg_plan_launch_op(bugseg_ctx *ctx, int B, int H, int W, int op, void *stream);
+
 /* Last error message of ctx (or of the calling thread when ctx is NULL). Never NULL. */
 const char *bugseg_last_error(const bugseg_ctx *ctx);
 

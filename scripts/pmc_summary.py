@@ -1,49 +1,59 @@
-"""HBM traffic per forward from rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes of bench.py.
+"""HBM traffic per kernel launch from rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes of bench.py.
 
 FETCH_SIZE / WRITE_SIZE are in KiB. On gfx950 FETCH_SIZE reads exactly half the bytes of a wide
 coalesced streaming read (MI355X_MICROARCH.md §HBM), so reads are doubled here; the initial
-block's raw-frame read (64 x 480x640x3 B = 59 MB) checks the factor: it reports 29.1 MB.
-Infinity-Cache hits are counted too (same section), so this is traffic at the L2's memory side.
+block's raw-frame read checks the factor. Infinity-Cache hits are counted too (same section), so this
+is traffic at the L2's memory side. Every launch of bench.py's command has one shape (bench.py times
+stages and kernels at the timed region's shard size), so per-launch averages per kernel tag are
+well defined.
 
-usage: python scripts/pmc_summary.py gpurun_out/<tag> [out.md]
+Writes a markdown table and profiles/pmc_traffic.json ({"per_launch_bytes": {tag: bytes}}), which
+bench.py reports as roofline.traffic for its dominant kernel.
+
+usage: python scripts/pmc_summary.py gpurun_out/<tag> [out.md] [out.json]
 """
 import csv
+import json
 import sys
 from collections import defaultdict
 from pathlib import Path
+
+sys.path.insert(0, str(Path(__file__).resolve().parent))
+from layer_times import short  # noqa: E402
 
 
 def per_kernel(path, counter):
     vals = defaultdict(list)
     for r in csv.DictReader(open(path)):
         if r["Counter_Name"] == counter:
-            vals[r["Kernel_Name"]].append(float(r["Counter_Value"]) * 1024.0)
+            vals[short(r["Kernel_Name"])].append(float(r["Counter_Value"]) * 1024.0)
     return vals
 
 
-def main(tag_dir, out_md=None):
+def main(tag_dir, out_md=None, out_json=None):
     d = Path(tag_dir)
     fetch = per_kernel(next((d / "fetch").glob("*counter_collection.csv")), "FETCH_SIZE")
     write = per_kernel(next((d / "write").glob("*counter_collection.csv")), "WRITE_SIZE")
-    n_fwd = len(fetch.get("bugseg::bev_occgrid_kernel(bugseg::BevArgs)", [])) or 1
-    lines = ["| kernel | dispatches/fwd | read MB/fwd (x2 corrected) | write MB/fwd |", "|---|---|---|---|"]
-    tot_r = tot_w = 0.0
+    lines = ["| kernel | launches | read MB/launch (FETCH x2) | write MB/launch | total MB/launch |",
+             "|---|---|---|---|---|"]
+    per = {}
     for k in sorted(fetch, key=lambda k: -sum(fetch[k])):
-        if "conv_kernel" not in k and "bneck_kernel" not in k:
+        if not any(t in k for t in ("conv", "bneck", "init", "bev")):
             continue
-        r = 2 * sum(fetch[k]) / n_fwd / 1e6
-        w = sum(write.get(k, [0])) / n_fwd / 1e6
-        tot_r += r
-        tot_w += w
-        lines.append(f"| `{k[:80]}` | {len(fetch[k]) / n_fwd:.0f} | {r:.1f} | {w:.1f} |")
-    lines += ["", f"ENet forward HBM traffic (memory side of L2): read {tot_r:.1f} MB + write {tot_w:.1f} MB = "
-                  f"{tot_r + tot_w:.1f} MB per forward ({n_fwd} forwards in the trace)"]
+        n = len(fetch[k])
+        r = 2 * sum(fetch[k]) / n
+        w = sum(write.get(k, [0.0])) / max(1, len(write.get(k, [])))
+        per[k] = r + w
+        lines.append(f"| `{k}` | {n} | {r / 1e6:.1f} | {w / 1e6:.1f} | {(r + w) / 1e6:.1f} |")
     text = "\n".join(lines)
     print(text)
     if out_md:
         Path(out_md).write_text(text + "\n")
-    return tot_r + tot_w
+    if out_json:
+        Path(out_json).write_text(json.dumps({"source": str(d), "correction": "FETCH_SIZE x2 (gfx950)",
+                                              "per_launch_bytes": per}, indent=1) + "\n")
+    return per
 
 
 if __name__ == "__main__":
-    main(*sys.argv[1:3])
+    main(*sys.argv[1:4])
