@@ -32,7 +32,8 @@ class BevParams(ctypes.Structure):
     _fields_ = [("M", ctypes.c_double * 9), ("in_rows", ctypes.c_int), ("in_cols", ctypes.c_int),
                 ("warp_w", ctypes.c_int), ("warp_h", ctypes.c_int), ("occ_w_px", ctypes.c_int),
                 ("occ_h_px", ctypes.c_int), ("occ_w", ctypes.c_int), ("occ_h", ctypes.c_int),
-                ("left_x", ctypes.c_int), ("top_y", ctypes.c_int), ("ros_layout", ctypes.c_int)]
+                ("left_x", ctypes.c_int), ("top_y", ctypes.c_int), ("ros_layout", ctypes.c_int),
+                ("variant", ctypes.c_int)]
 
 
 class BugsegError(RuntimeError):

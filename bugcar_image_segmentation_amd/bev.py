@@ -126,8 +126,9 @@ class bev_transform_tools:
 
     # -- geometry ----------------------------------------------------------------------------
     def occupancy_params(self, occupancy_grid_width_in_m, occupancy_grid_height_in_m, cell_size_in_m,
-                         ros_layout: bool = False) -> N.BevParams:
-        """bev.py:307-319, with the reference's float arithmetic and int() truncations."""
+                         ros_layout: bool = False, binary: bool = False) -> N.BevParams:
+        """bev.py:307-319 (bev.py:101-114 for the binary variant: the same arithmetic), with the
+        reference's float arithmetic and int() truncations."""
         cell_size_in_px = (cell_size_in_m * 100 / self.cm_per_px)
         occ_grid_width = int(occupancy_grid_width_in_m / cell_size_in_m)
         occ_width_pixel = int(occ_grid_width * cell_size_in_px)
@@ -147,6 +148,7 @@ class bev_transform_tools:
         p.occ_w, p.occ_h = occ_grid_width, occ_grid_height
         p.left_x, p.top_y = left_x, top_y
         p.ros_layout = int(bool(ros_layout))
+        p.variant = int(bool(binary))
         return p
 
     def _check_shape(self, shape):
@@ -157,9 +159,10 @@ class bev_transform_tools:
     # -- the hot path --------------------------------------------------------------------------
     def create_occupancy_grid_device(self, segmaps: torch.Tensor, occupancy_grid_width_in_m,
                                      occupancy_grid_height_in_m, cell_size_in_m, ros_layout: bool = False,
-                                     out: torch.Tensor | None = None) -> torch.Tensor:
+                                     out: torch.Tensor | None = None, binary: bool = False) -> torch.Tensor:
         """Batched create_occupancy_grid on device tensors: segmaps (B, rows, cols) uint8 class maps
-        -> (B, h, w) int8 (or (B, w, h) in ROS data order when ros_layout)."""
+        -> (B, h, w) int8 (or (B, w, h) in ROS data order when ros_layout). binary=True is
+        create_occupancy_grid_binary (bev.py:97-165)."""
         if self.laserscan_like_occupancy_grid:
             raise NotImplementedError("laserscan-like occupancy mode (bev.py:351-375) is SURVEY.md §8(f) row 2: "
                                       "not built yet")
@@ -170,7 +173,8 @@ class bev_transform_tools:
         if not seg.is_cuda:
             seg = seg.to(torch.device("cuda", torch.cuda.current_device()))
         seg = seg.contiguous()
-        p = self.occupancy_params(occupancy_grid_width_in_m, occupancy_grid_height_in_m, cell_size_in_m, ros_layout)
+        p = self.occupancy_params(occupancy_grid_width_in_m, occupancy_grid_height_in_m, cell_size_in_m, ros_layout,
+                                  binary)
         B = seg.shape[0]
         shape = (B, p.occ_w, p.occ_h) if ros_layout else (B, p.occ_h, p.occ_w)
         if out is None:
@@ -186,5 +190,11 @@ class bev_transform_tools:
                                                  cell_size_in_m)[0].cpu().numpy()
 
     def create_occupancy_grid_binary(self, segmap, occupancy_grid_width_in_m, occupancy_grid_height_in_m, cell_size_in_m):
-        """bev.py:97-165 (legacy, for predict_binary maps) — SURVEY.md §8(f) row 4: not built yet."""
-        raise NotImplementedError("create_occupancy_grid_binary is SURVEY.md §8(f) row 4: not built yet")
+        """bev.py:97-165 (legacy variant for ENET.predict_binary maps) -> np.int8 (h, w).
+        Occupied = template value 1 only (bev.py:126); the reference's uint8 encoding gives
+        {0: -1, 1: 100, 2: 0} and, for a 3-class map's class 2, -100 (bev.py:137-141 under NumPy 1.x
+        casting). For {0,1} maps it equals create_occupancy_grid."""
+        self._check_shape(np.shape(segmap))
+        seg = segmap if isinstance(segmap, torch.Tensor) else torch.from_numpy(np.ascontiguousarray(segmap, dtype=np.uint8))
+        return self.create_occupancy_grid_device(seg, occupancy_grid_width_in_m, occupancy_grid_height_in_m,
+                                                 cell_size_in_m, binary=True)[0].cpu().numpy()

@@ -67,13 +67,15 @@ __device__ __forceinline__ int tmpl_value(const BevArgs &a, const uint8_t *seg, 
     return warp_value(a, seg, wx, wy);
 }
 
+// occupied template values: {1, 3} (bev.py:331), or {1} in the binary variant (bev.py:126)
+__device__ __forceinline__ bool occupied(const BevArgs &a, int v) { return v == 1 || (v == 3 && !a.variant); }
+
 // Occupancy bit of template pixel p + (dx, dy); pixels outside the template read 1 (neutral for the
 // erode: OpenCV's default erode border is +inf).
 __device__ __forceinline__ uint32_t occ_bit(const BevArgs &a, const uint8_t *seg, int tx, int ty, int dx, int dy) {
     const int x = tx + dx, y = ty + dy;
     if ((unsigned)x >= (unsigned)a.occ_w_px || (unsigned)y >= (unsigned)a.occ_h_px) return 1u;
-    const int v = tmpl_value(a, seg, x, y);
-    return (v == 1 || v == 3) ? 1u : 0u;
+    return occupied(a, tmpl_value(a, seg, x, y)) ? 1u : 0u;
 }
 
 // bit index of offset (dx, dy) in the 5x5 window around p
@@ -91,7 +93,7 @@ __global__ void __launch_bounds__(256) bev_occgrid_kernel(const BevArgs a) {
         ty = ty < a.occ_h_px - 1 ? ty : a.occ_h_px - 1;
         tx = tx < a.occ_w_px - 1 ? tx : a.occ_w_px - 1;
         int v = tmpl_value(a, seg, tx, ty);
-        if (v == 1 || v == 3) {
+        if (occupied(a, v)) {
             // Opening at p = OR over q in N3(p) (inside the template) of AND over N3(q) of occupancy.
             // Round 1: the 8 neighbours of p (independent gathers, issued together). If they are all
             // occupied, q = p already survives the erode. Round 2 only for the rest: the 16-pixel ring.
@@ -121,8 +123,15 @@ __global__ void __launch_bounds__(256) bev_occgrid_kernel(const BevArgs a) {
             }
             if (!opened) v = 2;                  // isolated occupied pixel -> free (bev.py:339-340)
         }
-        const int g = v == 3 ? 1 : v;            // bev.py:377
-        const int8_t o = (int8_t)(g == 0 ? -1 : 200 - 100 * g);   // bev.py:379-380
+        int8_t o;
+        if (!a.variant) {
+            const int g = v == 3 ? 1 : v;        // bev.py:377
+            o = (int8_t)(g == 0 ? -1 : 200 - 100 * g);   // bev.py:379-380
+        } else {
+            // bev.py:137-141, :165 in uint8 arithmetic: {0:-1, 1:100, 2:0, 3:-100}
+            const uint8_t g = (uint8_t)(v * 100);
+            o = (int8_t)(uint8_t)(g == 0 ? 0xff : (uint8_t)(200 - g));
+        }
         if (a.ros_layout) {
             // occgrid_to_ros.py:18-21: flip(0) then rot90ccw == G[::-1, ::-1].T, shape (occ_w, occ_h)
             a.out[(size_t)b * cells + (size_t)(a.occ_w - 1 - cx) * a.occ_h + (a.occ_h - 1 - cy)] = o;

@@ -121,6 +121,7 @@ struct BevArgs {
     int warp_w, warp_h, occ_w_px, occ_h_px, occ_w, occ_h, left_x, top_y;
     double ifx, ify;     // resizeNN inverse scales
     int ros_layout;
+    int variant;         // 0 create_occupancy_grid, 1 create_occupancy_grid_binary
     int8_t *out;
 };
 hipError_t launch_bev(const BevArgs &a, hipStream_t s);

@@ -972,6 +972,7 @@ int bugseg_bev_occgrid(bugseg_ctx *ctx, const uint8_t *seg, int B, const bugseg_
     if (B <= 0 || p->in_rows <= 0 || p->in_cols <= 0 || p->warp_w <= 0 || p->warp_h <= 0 || p->occ_w <= 0 ||
         p->occ_h <= 0 || p->occ_w_px <= 0 || p->occ_h_px <= 0)
         return fail(ctx, BUGSEG_EINVAL, "bad BEV geometry");
+    if (p->variant != 0 && p->variant != 1) return fail(ctx, BUGSEG_EINVAL, "variant must be 0 or 1");
     DeviceGuard g(ctx->device);
     BevArgs a;
     std::memset(&a, 0, sizeof(a));
@@ -1002,6 +1003,7 @@ int bugseg_bev_occgrid(bugseg_ctx *ctx, const uint8_t *seg, int B, const bugseg_
     a.ifx = 1.0 / ((double)p->occ_w / p->occ_w_px);
     a.ify = 1.0 / ((double)p->occ_h / p->occ_h_px);
     a.ros_layout = p->ros_layout;
+    a.variant = p->variant;
     a.out = out;
     hipError_t e = launch_bev(a, (hipStream_t)stream);
     if (e != hipSuccess) return fail(ctx, BUGSEG_EHIP, std::string("bev launch: ") + hipGetErrorString(e));

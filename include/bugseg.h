@@ -73,6 +73,10 @@ typedef struct {
     int top_y;          /* bev.py:319 */
     int ros_layout;     /* 0: reference (occ_h, occ_w) grid; 1: ROS data order = flip(0)+rot90ccw
                            of it, (occ_w, occ_h) row-major (occgrid_to_ros.py:18-25)            */
+    int variant;        /* 0: create_occupancy_grid (bev.py:301-381): occupied = template {1,3},
+                              encoding {0:-1, 1:100, 2:0, 3:100};
+                           1: create_occupancy_grid_binary (bev.py:97-165): occupied = {1}, the
+                              reference's uint8 encoding {0:-1, 1:100, 2:0, 3:-100}               */
 } bugseg_bev_params;
 
 /* Library version (major*10000 + minor*100 + patch). */
@@ -119,9 +123,10 @@ int bugseg_enet_forward(bugseg_ctx *ctx, const void *in_dev, int B, int H, int W
 int bugseg_enet_forward_bgr(bugseg_ctx *ctx, const uint8_t *bgr_dev, int B, int H, int W, int out_kind,
                             void *out_dev, void *stream);
 
-/* Fused BEV rasteriser over a batch of class maps: seg_dev (B, in_rows, in_cols) u8 in {0,1,2}
- * -> out_dev (B, occ_h, occ_w) int8 in {-1, 0, 100} (or the ROS layout, see ros_layout).
- * Replaces bev_transform_tools.create_occupancy_grid, non-laserscan branch (bev.py:301-381). */
+/* Fused BEV rasteriser over a batch of class maps: seg_dev (B, in_rows, in_cols) u8
+ * -> out_dev (B, occ_h, occ_w) int8 (or the ROS layout, see ros_layout).
+ * Replaces bev_transform_tools.create_occupancy_grid (bev.py:301-381) or, with variant = 1,
+ * create_occupancy_grid_binary (bev.py:97-165); non-laserscan branches. */
 int bugseg_bev_occgrid(bugseg_ctx *ctx, const uint8_t *seg_dev, int B, const bugseg_bev_params *p,
                        int8_t *out_dev, void *stream);
 

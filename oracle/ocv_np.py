@@ -190,6 +190,36 @@ def create_occupancy_grid(segmap: np.ndarray, M: np.ndarray, after_warp_w: int, 
     return np.where(new == 0, -1, 200 - new.astype(np.int64) * 100).astype(np.int8)   # bev.py:379
 
 
+def create_occupancy_grid_binary(segmap: np.ndarray, M: np.ndarray, after_warp_w: int, after_warp_h: int,
+                                 cm_per_px: float, grid_w_m: float, grid_h_m: float, cell_m: float) -> np.ndarray:
+    """Restates bev.py:97-165 (legacy binary variant, non-laserscan branch) on the arrays it builds.
+    Its uint8 arithmetic is NumPy 1.x's (value-based casting, wrap-around), emulated explicitly."""
+    cell_px = cell_m * 100 / cm_per_px                                   # bev.py:101
+    occ_w = int(grid_w_m / cell_m)                                       # bev.py:102
+    occ_w_px = int(occ_w * cell_px)                                      # bev.py:103
+    occ_h = int(grid_h_m / cell_m)                                       # bev.py:104
+    occ_h_px = int(occ_h * cell_px)                                      # bev.py:105
+    lifted = np.add(segmap, 1).astype(np.uint8)                          # bev.py:106
+    warped = warp_perspective(lifted, M, (after_warp_w, after_warp_h))   # bev.py:112
+    left_x = int((after_warp_w - occ_w_px) / 2)                          # bev.py:113
+    top_y = after_warp_h - occ_h_px                                      # bev.py:114
+    wlx = int(np.clip(left_x, 0, np.inf))                                # bev.py:115
+    warped = warped[int(np.clip(top_y, 0, np.inf)):after_warp_h, wlx:wlx + occ_w_px]   # bev.py:116
+    glx = int(np.clip(-left_x, 0, np.inf))                               # bev.py:118
+    gty = int(np.clip(-top_y, 0, np.inf))                                # bev.py:119
+    tmpl = np.zeros((occ_h_px, occ_w_px))                                # bev.py:120
+    tmpl[gty:occ_h_px, glx:glx + warped.shape[1]] = warped               # bev.py:122-124
+    tmpl = tmpl.astype(np.uint8)                                         # bev.py:125
+    occ = (tmpl == 1).astype(np.uint8)                                   # bev.py:126
+    opened = morph_open3x3(occ)                                          # bev.py:128-129
+    mask1 = (opened > 0).astype(np.uint8)                                # bev.py:131
+    sub = np.clip(occ.astype(np.int16) - mask1, 0, 255)                  # bev.py:132 cv2.subtract saturates
+    tmpl = np.where(sub > 0, 2, tmpl).astype(np.uint8)                   # bev.py:133
+    og = (resize_nearest(tmpl, (occ_w, occ_h)).astype(np.int64) * 100) % 256   # bev.py:137-139: uint8 * 100 wraps
+    r = np.where(og == 0, -1, (200 - og) % 256)                          # bev.py:140 (uint8 200 - og)
+    return (r % 256).astype(np.uint8).astype(np.int8)                    # bev.py:141, :165
+
+
 def ros_layout(grid: np.ndarray) -> np.ndarray:
     """cv2.flip(g, 0) then cv2.rotate(ROTATE_90_COUNTERCLOCKWISE) (occgrid_to_ros.py:18,21)."""
     flipped = grid[::-1, :]

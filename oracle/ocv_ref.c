@@ -277,3 +277,43 @@ int bev_occgrid_ref(const uint8_t *segmap, int hin, int win, const double *M, in
     free(lifted); free(tmpl); free(occ); free(opened); free(cells);
     return 0;
 }
+
+/* bev_transform_tools.create_occupancy_grid_binary (bev.py:97-165, non-laserscan branch; the legacy
+ * variant for predict_binary maps). Same warp / crop-pad / opening / NN resize as above, but the
+ * occupied set is {1} only (bev.py:126) and the encoding is the reference's uint8 arithmetic under
+ * NumPy 1.x casting: g = uint8(cell * 100) (bev.py:135-138), r = g == 0 ? -1 : uint8(200 - g)
+ * (bev.py:139-140), out = int8(uint8(r)) (bev.py:140, :165) -> {0:-1, 1:100, 2:0, 3:-100}. */
+int bev_occgrid_binary_ref(const uint8_t *segmap, int hin, int win, const double *M, int Wb, int Hb,
+                           int occ_w_px, int occ_h_px, int occ_w, int occ_h, int left_x, int top_y, int8_t *out)
+{
+    size_t n = (size_t)hin * win;
+    uint8_t *lifted = (uint8_t *)malloc(n);
+    uint8_t *tmpl = (uint8_t *)malloc((size_t)occ_h_px * occ_w_px);
+    uint8_t *occ = (uint8_t *)malloc((size_t)occ_h_px * occ_w_px);
+    uint8_t *opened = (uint8_t *)malloc((size_t)occ_h_px * occ_w_px);
+    uint8_t *cells = (uint8_t *)malloc((size_t)occ_h * occ_w);
+    if (!lifted || !tmpl || !occ || !opened || !cells) return -1;
+    for (size_t i = 0; i < n; i++) lifted[i] = (uint8_t)(segmap[i] + 1);                      /* bev.py:107 */
+    double Mi[9];
+    ocv_invert3x3(M, Mi);
+    int bw0 = warp_bw0(Hb, Wb);
+    for (int ty = 0; ty < occ_h_px; ty++)
+        for (int tx = 0; tx < occ_w_px; tx++) {
+            int wy = ty + top_y, wx = tx + left_x;                                                /* bev.py:114-125 */
+            uint8_t v = 0;
+            if (wy >= 0 && wy < Hb && wx >= 0 && wx < Wb) v = warp_px(lifted, hin, win, Mi, wx, wy, bw0);
+            tmpl[(size_t)ty * occ_w_px + tx] = v;
+            occ[(size_t)ty * occ_w_px + tx] = (uint8_t)(v == 1);                                  /* bev.py:126 */
+        }
+    ocv_morph_open3x3_u8(occ, occ_h_px, occ_w_px, opened);                                        /* bev.py:128-129 */
+    for (size_t i = 0; i < (size_t)occ_h_px * occ_w_px; i++)
+        if (occ[i] && !opened[i]) tmpl[i] = 2;                                                    /* bev.py:131-133 */
+    ocv_resize_nearest_u8(tmpl, occ_h_px, occ_w_px, 1, cells, occ_h, occ_w);                      /* bev.py:135-138 */
+    for (size_t i = 0; i < (size_t)occ_h * occ_w; i++) {
+        uint8_t g = (uint8_t)(cells[i] * 100);
+        int r = g == 0 ? -1 : (int)(uint8_t)(200 - g);
+        out[i] = (int8_t)(uint8_t)r;
+    }
+    free(lifted); free(tmpl); free(occ); free(opened); free(cells);
+    return 0;
+}

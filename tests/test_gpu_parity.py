@@ -148,6 +148,24 @@ def test_bev_occgrid_bit_exact(gpu, rows, cols, ww, wh, grid, seed):
     assert one.dtype == np.int8 and np.array_equal(one, ref[0])
 
 
+@pytest.mark.parametrize("rows,cols,ww,wh,grid,seed", [
+    (480, 640, 1000, 1000, (10.0, 10.0, 0.05), 4),
+    (96, 128, 250, 180, (3.1, 2.7, 0.07), 5),
+])
+def test_bev_occgrid_binary_bit_exact(gpu, rows, cols, ww, wh, grid, seed):
+    """create_occupancy_grid_binary (bev.py:97-165) vs its C restatement: predict_binary maps ({0,1})
+    and 3-class maps (the reference's uint8 encoding turns class 2 into -100)."""
+    bev = _bev_case(rows, cols, ww, wh, seed)
+    rng = np.random.default_rng(seed)
+    segs = np.stack([np.kron(rng.integers(0, k, size=(rows // 8, cols // 8)), np.ones((8, 8), np.int64)).astype(np.uint8)
+                     for k in (2, 3)] + [rng.integers(0, 2, size=(rows, cols)).astype(np.uint8)])
+    ref = np.stack([ocv_c.create_occupancy_grid_binary(s, bev._bev_matrix, ww, wh, 1.0, *grid) for s in segs])
+    got = bev.create_occupancy_grid_device(torch.from_numpy(segs).cuda(), *grid, binary=True).cpu().numpy()
+    assert np.array_equal(got, ref)
+    one = bev.create_occupancy_grid_binary(segs[0], *grid)
+    assert one.dtype == np.int8 and np.array_equal(one, ref[0])
+
+
 @pytest.mark.parametrize("prec", ["fp32", "bf16"])
 @pytest.mark.parametrize("pool_k", [3, 2])
 def test_forward_bgr_equals_preprocess_then_forward(gpu, prec, pool_k):

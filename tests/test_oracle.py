@@ -130,6 +130,26 @@ def test_occupancy_grid_c_vs_reference_flow(ww, wh, grid):
     assert set(np.unique(a)) <= {-1, 0, 100}
 
 
+@pytest.mark.parametrize("ww,wh,grid", [(1000, 1000, (10, 10, 0.05)), (600, 1100, (7.3, 12.1, 0.07))])
+@pytest.mark.parametrize("classes", [2, 3])
+def test_occupancy_grid_binary_c_vs_reference_flow(ww, wh, grid, classes):
+    """bev.py:97-165: C restatement vs the NumPy restatement of the reference's array flow, for
+    predict_binary maps ({0,1}) and for 3-class maps (class 2 -> template 3 -> the uint8 wrap -100)."""
+    rng = np.random.default_rng(ww + classes)
+    seg = np.kron(rng.integers(0, classes, size=(60, 80)), np.ones((8, 8), np.int64)).astype(np.uint8)
+    seg[rng.random(seg.shape) < 0.02] = 0
+    M = synthetic.synthetic_bev(480, 640, ww, wh)._bev_matrix
+    a = ocv_c.create_occupancy_grid_binary(seg, M, ww, wh, 1.0, *grid)
+    b = ocv_np.create_occupancy_grid_binary(seg, M, ww, wh, 1.0, *grid)
+    assert np.array_equal(a, b)
+    assert set(np.unique(a)) <= ({-1, 0, 100} if classes == 2 else {-1, 0, 100, -100})
+    if classes == 2:
+        # for {0,1} maps the binary variant and create_occupancy_grid coincide ({1} == {1,3} on them)
+        assert np.array_equal(a, ocv_c.create_occupancy_grid(seg, M, ww, wh, 1.0, *grid))
+    else:
+        assert (a == -100).any()
+
+
 def test_oracle_fp32_vs_fp64(blocks):
     x = np.random.default_rng(5).normal(size=(1, 3, 32, 48)).astype(np.float32)
     a = eo.forward(blocks, x, torch.float32)
