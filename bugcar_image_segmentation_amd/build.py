@@ -36,15 +36,19 @@ def _stale(target: Path, deps) -> bool:
     return any(Path(d).stat().st_mtime > t for d in deps)
 
 
-def build_native(force: bool = False, verbose: bool = False) -> Path:
-    OBJ.mkdir(exist_ok=True)
+def build_native(force: bool = False, verbose: bool = False, stamps: bool = False) -> Path:
+    """stamps=True: the debug variant libbugseg_stamps.so (-DBUGSEG_STAMPS: in-kernel phase clocks,
+    scripts/stamp_probe.py); never loaded by the product path."""
+    obj_dir = OBJ / "stamps" if stamps else OBJ
+    lib = PKG / "libbugseg_stamps.so" if stamps else LIB
+    obj_dir.mkdir(parents=True, exist_ok=True)
     hipcc = _hipcc()
     flags = [f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-Wall", "-Wno-unused-function",
-             f"-I{ROOT / 'include'}", f"-I{CSRC}"]
+             f"-I{ROOT / 'include'}", f"-I{CSRC}"] + (["-DBUGSEG_STAMPS"] if stamps else [])
     jobs = []
     for s in SOURCES:
         src = CSRC / s
-        obj = OBJ / (s + ".o")
+        obj = obj_dir / (s + ".o")
         if force or _stale(obj, [src, *HEADERS]):
             lang = ["-x", "hip"] if s.endswith(".hip") else []
             jobs.append((obj, [hipcc, *flags, *lang, "-c", str(src), "-o", str(obj)]))
@@ -60,16 +64,16 @@ def build_native(force: bool = False, verbose: bool = False) -> Path:
 
     with ThreadPoolExecutor(max_workers=min(4, max(1, len(jobs)))) as ex:
         list(ex.map(run, jobs))
-    objs = [OBJ / (s + ".o") for s in SOURCES]
-    if force or jobs or _stale(LIB, objs):
-        tmp = LIB.with_suffix(".so.tmp")
+    objs = [obj_dir / (s + ".o") for s in SOURCES]
+    if force or jobs or _stale(lib, objs):
+        tmp = lib.with_suffix(".so.tmp")
         cmd = [hipcc, f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", str(tmp), *map(str, objs)]
         r = subprocess.run(cmd, capture_output=True, text=True)
         if r.returncode != 0:
             raise RuntimeError(f"link failed: {' '.join(cmd)}\n{r.stdout}\n{r.stderr}")
-        os.replace(tmp, LIB)
-    return LIB
+        os.replace(tmp, lib)
+    return lib
 
 
 if __name__ == "__main__":
-    print(build_native(force="--force" in sys.argv, verbose=True))
+    print(build_native(force="--force" in sys.argv, verbose=True, stamps="--stamps" in sys.argv))

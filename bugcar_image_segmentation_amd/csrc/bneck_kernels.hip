@@ -7,12 +7,26 @@
 // Unfused, each 128-channel bottleneck moves ~1024 B/pixel through HBM (x read twice, three internal
 // tensors written and read); here x is read once (halo re-reads are L2 hits) and out written once:
 // 512 B/pixel in bf16. The internal tensors never leave LDS:
-//   * a 256-thread workgroup owns a TH x TW output tile of one frame; phase 1 computes t0 for the
-//     tile plus a halo of (ry, rx) pixels (zero outside the image: t0 is what the 3x3 zero-pads);
+//   * a workgroup owns a TH x TW tile of one frame; phase 1 computes t0 for the tile plus a halo ring
+//     of R pixels (zero outside the image: t0 is what the middle conv zero-pads);
 //   * phase 2 accumulates its whole tile in registers, then (after a barrier) overwrites the t0
 //     region with t1, so one LDS region serves both (asymmetric: t0 -> t1a -> t1, same trick);
-//   * phase 3 streams 16-pixel fragments: MFMA with W3, residual from global (just read, L2/L1),
-//     activation, 8-byte NHWC stores.
+//   * phase 3 streams 16-pixel fragments: MFMA with W3, residual staged in LDS, activation,
+//     16-B-per-lane stores.
+//
+// Dilated tiling. A 3x3 conv of dilation d only couples pixels whose coordinates agree mod d, so a
+// tile is a TH x TW block of ONE such phase: tile pixel (i, j) is image pixel (oy0 + d*i, ox0 + d*j),
+// and the dilated conv is a plain 3x3 over tile coordinates with a one-pixel halo ring whatever d is
+// (the d-pixel halo of a contiguous tile recomputes (16+2d)^2 / 16^2 of the projection: 2.25x at
+// d = 4). NHWC keeps every pixel a contiguous C-element run, so strided pixels cost no extra lines.
+//
+// Tile shapes are template variants (BShape) picked per layer by the runtime (bugseg_runtime.cpp
+// pick_bneck_variant) so that the tile count fills the resident workgroup slots in whole rounds. A
+// tile may be transposed (a.tr: tile rows run along image columns; the middle conv's taps swap
+// axes with it), so one 20 x 16 shape covers 60 x 80 at d = 1 (20 rows x 16 columns), d = 2 and
+// d = 4 (20 columns x 16 rows of a 30 x 40 / 15 x 20 phase) in 15-16 tiles per frame. Fragments
+// are 16-pixel runs of one tile row (TW is a multiple of 16), so a fragment's row is wave-uniform.
+//
 // MFMA operand mapping as conv_kernels.hip: A = weights (row = output channel) from LDS, B = 8
 // channels of one pixel (16-B LDS or global read per lane), accumulator = 4 consecutive channels of
 // one pixel per lane. All three weight matrices stay in LDS for the workgroup's lifetime.
@@ -21,24 +35,43 @@
 
 namespace bugseg {
 
-// Tile and workgroup shape per channel count. 128 channels: the LDS footprint (weights + halo or
-// output staging, ~64-73 KB) allows two workgroups per CU, so they are 8-wave (512-thread) to put
-// 16 waves on a CU; 64 / 16 channels (~28 KB): four 4-wave workgroups per CU — more independent
-// tile pipelines (memory phase of one beside compute phase of another) for the same waves.
-template <int C> struct BTile;
-// OCC: waves per SIMD the bf16 build is held to (registers), matching what LDS allows.
-template <> struct BTile<128> { static constexpr int TH = 16, TW = 16, NW = 8, OCC = 4; };
-template <> struct BTile<64> { static constexpr int TH = 16, TW = 16, NW = 4, OCC = 5; };
-template <> struct BTile<16> { static constexpr int TH = 16, TW = 16, NW = 4, OCC = 6; };
+// Debug build only (-DBUGSEG_STAMPS, scripts/stamp_probe.py): thread 0 of each workgroup records the
+// shader clock at phase boundaries of every tile, stamps[tile * 8 + k]; slot 7 = workgroup index.
+#ifdef BUGSEG_STAMPS
+__device__ unsigned long long *bugseg_stamps;
+#define STAMP(k) do { if (tid == 0 && bugseg_stamps) bugseg_stamps[(size_t)tile * 8 + (k)] = __builtin_amdgcn_s_memtime(); } while (0)
+#define STAMP_WG() do { if (tid == 0 && bugseg_stamps) bugseg_stamps[(size_t)tile * 8 + 7] = blockIdx.x; } while (0)
+#else
+#define STAMP(k) do {} while (0)
+#define STAMP_WG() do {} while (0)
+#endif
 
-int bneck_tile_h(int C) { return C == 128 ? BTile<128>::TH : C == 64 ? BTile<64>::TH : BTile<16>::TH; }
-int bneck_tile_w(int C) { return C == 128 ? BTile<128>::TW : C == 64 ? BTile<64>::TW : BTile<16>::TW; }
-static int bneck_waves(int C) { return C == 128 ? BTile<128>::NW : C == 64 ? BTile<64>::NW : BTile<16>::NW; }
+// Tile shape variants per channel count: TH x TW tile pixels, NW waves per workgroup, OCC = waves
+// per SIMD the bf16 build is held to (registers), matching what LDS allows. 128 channels: the LDS
+// footprint (weights + halo or output staging, ~75 KB) allows two workgroups per CU, so they are
+// 8-wave; 64 / 16 channels (~28-33 KB): four 4-wave workgroups per CU.
+template <int C, int V> struct BShape;
+// RP = residual fragments each wave prefetches before the middle conv (a ring refilled in phase 3
+// when a wave has more fragments than that: an L2 round trip then sits on the phase-3 path).
+template <> struct BShape<128, 0> { static constexpr int TH = 16, TW = 16, NW = 8, OCC = 4, RP = 2; };
+template <> struct BShape<128, 1> { static constexpr int TH = 20, TW = 16, NW = 8, OCC = 4, RP = 2; };
+template <> struct BShape<64, 0> { static constexpr int TH = 16, TW = 16, NW = 4, OCC = 5, RP = 4; };
+template <> struct BShape<64, 1> { static constexpr int TH = 20, TW = 16, NW = 4, OCC = 5, RP = 3; };
+template <> struct BShape<16, 0> { static constexpr int TH = 16, TW = 16, NW = 4, OCC = 6, RP = 4; };
 
-template <typename T, int C, bool ASYM>
-__global__ void __launch_bounds__(BTile<C>::NW * 64, sizeof(T) == 2 ? BTile<C>::OCC : 1) bneck_kernel(const BneckArgs a) {
+int bneck_variants(int C) { return C == 16 ? 1 : 2; }
+
+void bneck_shape(int C, int v, int &th, int &tw, int &nw) {
+#define BS_CASE(CC, VV) if (C == CC && v == VV) { th = BShape<CC, VV>::TH; tw = BShape<CC, VV>::TW; nw = BShape<CC, VV>::NW; return; }
+    BS_CASE(128, 0) BS_CASE(128, 1) BS_CASE(64, 0) BS_CASE(64, 1) BS_CASE(16, 0)
+#undef BS_CASE
+    th = tw = nw = 0;
+}
+
+template <typename T, int C, bool ASYM, int V, bool TR>
+__global__ void __launch_bounds__((BShape<C, V>::NW * 64), (sizeof(T) == 2 ? BShape<C, V>::OCC : 1)) bneck_kernel(const BneckArgs a) {
     using Raw = typename Tr<T>::Raw;
-    constexpr int NW = BTile<C>::NW, NT = NW * 64;
+    constexpr int TH = BShape<C, V>::TH, TW = BShape<C, V>::TW, NW = BShape<C, V>::NW, NT = NW * 64;
     constexpr int I = C / 4;
     constexpr int IS = I < 8 ? 8 : I;                 // stored internal channels (8-channel groups)
     constexpr int NR1 = (I + 15) / 16;                // 16-row fragments of t0 / t1
@@ -47,20 +80,25 @@ __global__ void __launch_bounds__(BTile<C>::NW * 64, sizeof(T) == 2 ? BTile<C>::
     constexpr int TAPS = ASYM ? 5 : 9;
     constexpr int G2 = TAPS * IS / 8, KS2 = (G2 + 3) / 4;
     constexpr int G3 = IS / 8;                        // expand k groups (<= 4: one step)
-    constexpr int TH = BTile<C>::TH, TW = BTile<C>::TW;
+    constexpr int R = ASYM ? 2 : 1;                   // halo ring of the middle conv (tile coordinates)
+    constexpr int HWW = TW + 2 * R, HR = (TH + 2 * R) * HWW;
+    constexpr int NF1 = (HR + 15) / 16;               // 16-pixel fragments of tile + halo
     constexpr int PAD = 16 / (int)sizeof(T);
     constexpr int PSTR = IS + PAD;                    // LDS pixel stride (elements)
-    constexpr int NFT = TH * TW / 16;                 // 16-pixel fragments of the tile
-    constexpr int NF2 = (NFT + NW - 1) / NW;          // ... per wave
+    constexpr int NPX = TH * TW;
+    constexpr int NFT = (NPX + 15) / 16;              // 16-pixel fragments of the tile
+    constexpr int NF2 = (NFT + NW - 1) / NW;          // ... per wave (the last may be partial / absent)
     constexpr int TWA = TW + 4;                       // asymmetric: width of t1a (the 1x5's halo)
-    constexpr int NFA = TH * TWA / 16;
+    constexpr int NPA = TH * TWA;
+    constexpr int NFA = (NPA + 15) / 16;
     constexpr int NF2A = (NFA + NW - 1) / NW;
     constexpr int CH1 = KS1 >= 4 ? 3 : KS1 == 2 ? 4 : 8;   // phase-1 fragments whose loads fly together
     constexpr int EPC = 16 / (int)sizeof(T);          // elements per 16-B chunk
-    constexpr int CPF = 16 * C / EPC;                 // 16-B chunks of one 16-pixel output fragment
+    constexpr int CPP = C / EPC;                      // 16-B chunks per pixel
+    constexpr int CPF = 16 * CPP;                     // 16-B chunks of one 16-pixel output fragment
     constexpr int CPL = (CPF + 63) / 64;              // ... per lane
     constexpr int OSTR = C + EPC;                     // phase-3 staging row stride (16-B padded)
-    static_assert(NFT % NW == 0, "tile fragments must split evenly over the waves");
+    static_assert(TW % 16 == 0, "a fragment is a run of one tile row");
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
 
     const int tid = threadIdx.x;
@@ -103,32 +141,49 @@ __global__ void __launch_bounds__(BTile<C>::NW * 64, sizeof(T) == 2 ? BTile<C>::
     // the fused path is planned only when every slope is <= 1 (bugseg_runtime.cpp fusable_regular),
     // so PReLU is max(v, s*v); accumulators start at the bias
     auto act = [&](float4 v, const float *s) { return prelu4m(v, ld4f(s)); };
-    const int ry = a.ry, rx = a.rx, d = a.d;
-    const int HWW = TW + 2 * rx, HR = (TH + 2 * ry) * HWW;
-    const int nf1 = (HR + 15) >> 4;
+    const int dt = a.dt;                              // tiling dilation (1 for asymmetric blocks)
+    constexpr bool tr = TR && !ASYM;                  // transposed tile
 
-    // XCD-aware tile walk (see conv_kernels.hip)
+    // XCD-aware tile walk (see conv_kernels.hip): each XCD takes a contiguous run of tiles, so the
+    // halo re-reads of neighbouring tiles hit the same L2
     const int G = gridDim.x, grp = blockIdx.x & 7, slot = blockIdx.x >> 3, nslots = G >> 3;
     const int CH = (a.ntiles + 7) >> 3;
     for (int it = slot; it < CH; it += nslots) {
         const int tile = grp * CH + it;
         if (tile >= a.ntiles) break;
-        const int n = tile / (a.tiles_y * a.tiles_x);
-        const int tr = tile - n * a.tiles_y * a.tiles_x;
-        const int ty0 = (tr / a.tiles_x) * TH, tx0 = (tr % a.tiles_x) * TW;
+        // tile -> frame n, phase (py, px), tile row / column of that phase's sub-image (scalar math)
+        int t = tile;
+        const int txi = t % a.tiles_x; t /= a.tiles_x;
+        const int tyi = t % a.tiles_y; t /= a.tiles_y;
+        const int ph = t % a.phases, n = t / a.phases;
+        const int py = ph / dt, px = ph - py * dt;
+        // image pixel of tile pixel (0, 0); tile pixel (i, j) is image (oy0 + dt i, ox0 + dt j), or
+        // (oy0 + dt j, ox0 + dt i) transposed
+        const int oy0 = py + dt * tyi * (tr ? TW : TH), ox0 = px + dt * txi * (tr ? TH : TW);
         const uint32_t xn = (uint32_t)(n * a.H * a.W) * (uint32_t)(C * sizeof(T));   // frame byte offset
+        // byte offset of channel chunk `choff` of pixel pi (per lane, 0..15) of tile fragment f (wave
+        // uniform), or OOB outside the image. A fragment is a run of one tile row: its row i is a
+        // scalar and only the column j is per lane.
+        auto pix_off = [&](int f, int pi, int choff) -> uint32_t {
+            const int i = (f * 16) / TW, j = (f * 16) % TW + pi;
+            const int y = oy0 + dt * (tr ? j : i), x = ox0 + dt * (tr ? i : j);
+            const bool ok = y < a.H && x < a.W;
+            return ok ? xn + (uint32_t)((y * a.W + x) * C + choff) * (uint32_t)sizeof(T) : OOB;
+        };
+        STAMP(0); STAMP_WG();
         __syncthreads();   // weights staged (first tile) / previous tile done with ts
+        STAMP(1);
 
         // ---- phase 1: t0 = act1(W1 x + b1) over tile + halo, 0 outside the image. The loads of CH1
         // fragments are issued together before any of them is consumed (memory-level parallelism).
-        for (int f0 = wave; f0 < nf1; f0 += NW * CH1) {
+        for (int f0 = wave; f0 < NF1; f0 += NW * CH1) {
             Raw xf[CH1][KS1];
             bool okc[CH1];
 #pragma unroll
             for (int c = 0; c < CH1; ++c) {
                 const int h = (f0 + c * NW) * 16 + col;
-                const int hy = (int)fdiv((uint32_t)h, a.mHWW, a.sHWW), hx = h - hy * HWW;
-                const int iy = ty0 - ry + hy, ix = tx0 - rx + hx;
+                const int hy = h / HWW, hx = h - hy * HWW;
+                const int iy = oy0 + dt * ((tr ? hx : hy) - R), ix = ox0 + dt * ((tr ? hy : hx) - R);
                 okc[c] = h < HR && (unsigned)iy < (unsigned)a.H && (unsigned)ix < (unsigned)a.W;
 #pragma unroll
                 for (int s = 0; s < KS1; ++s) {
@@ -163,25 +218,28 @@ __global__ void __launch_bounds__(BTile<C>::NW * 64, sizeof(T) == 2 ? BTile<C>::
                 }
             }
         }
+        STAMP(2);
         __syncthreads();
+        STAMP(3);
 
-        // residual of phase 3 (x at the tile pixels), prefetched early (asymmetric: after its 5x1 pass,
-        // to keep the two passes' live ranges apart) with coalesced 16-B loads: a fragment is 16
-        // consecutive pixels of one tile row, i.e. one contiguous run of 16*C elements of x.
-        uint4 res[NF2][CPL];
+        // residual of phase 3 (x at the tile pixels) with coalesced 16-B loads: lane chunk q of
+        // fragment f is channel chunk q % CPP of tile pixel 16 f + q / CPP. RP fragments are
+        // prefetched before the middle conv (asymmetric: after its 5x1 pass, to keep the two passes'
+        // live ranges apart); phase 3 refills the ring as it consumes it.
+        constexpr int RP = BShape<C, V>::RP < NF2 ? BShape<C, V>::RP : NF2;
+        uint4 res[RP][CPL];
+        auto load_res = [&](int j, uint4 (&r)[CPL]) {
+            const int f = wave + NW * j;
+#pragma unroll
+            for (int k = 0; k < CPL; ++k) {
+                const int q = lane + 64 * k;
+                const uint32_t off = pix_off(f, q / CPP, (q % CPP) * EPC);
+                r[k] = bld16(rxb, q < CPF ? off : OOB);
+            }
+        };
         auto prefetch_res = [&]() {
 #pragma unroll
-            for (int j = 0; j < NF2; ++j) {
-                const int p0 = (wave + NW * j) * 16;
-                const int oy = p0 / TW, ox0 = p0 - oy * TW, iy = ty0 + oy;
-#pragma unroll
-                for (int k = 0; k < CPL; ++k) {
-                    const int q = lane + 64 * k;
-                    const int ix = tx0 + ox0 + q * EPC / C;
-                    const bool ok = q < CPF && (unsigned)iy < (unsigned)a.H && (unsigned)ix < (unsigned)a.W;
-                    res[j][k] = bld16(rxb, ok ? xn + (uint32_t)((iy * a.W + tx0 + ox0) * C + q * EPC) * (uint32_t)sizeof(T) : OOB);
-                }
-            }
+            for (int j = 0; j < RP; ++j) load_res(j, res[j]);
         };
         if constexpr (!ASYM) prefetch_res();
 
@@ -196,26 +254,32 @@ __global__ void __launch_bounds__(BTile<C>::NW * 64, sizeof(T) == 2 ? BTile<C>::
             for (int s = 0; s < KS2; ++s) {
                 const int g = s * 4 + kq;
                 const int tap = g / (IS / 8), coff = (g - tap * (IS / 8)) * 8;
-                const int dy = (tap / 3 - 1) * d, dx = (tap % 3 - 1) * d;
+                const int ky = tap / 3, kx = tap - ky * 3;
+                const int ti = tr ? kx : ky, tj = tr ? ky : kx;   // tap offset in tile axes
                 Raw wf[NR1];
 #pragma unroll
                 for (int r = 0; r < NR1; ++r) ld8(wf[r], w2 + (r * 16 + col) * K2S + s * 32 + kq * 8);
 #pragma unroll
                 for (int j = 0; j < NF2; ++j) {
-                    const int p = (wave + NW * j) * 16 + col;
+                    if (wave + NW * j >= NFT) continue;       // wave-uniform
+                    int p = (wave + NW * j) * 16 + col;
+                    if constexpr (NPX % 16 != 0) p = p < NPX ? p : 0;   // partial fragment: read anything, discarded
                     const int oy = p / TW, ox = p - oy * TW;
                     Raw xf;
-                    if (g < G2) ld8(xf, ts + ((oy + ry + dy) * HWW + (ox + rx + dx)) * PSTR + coff);
+                    if (g < G2) ld8(xf, ts + ((oy + ti) * HWW + (ox + tj)) * PSTR + coff);
                     else zero(xf);
                     if (a.ablate & 2) continue;
 #pragma unroll
                     for (int r = 0; r < NR1; ++r) mma(acc[j][r], wf[r], xf);
                 }
             }
+            STAMP(4);
             __syncthreads();   // every wave is done reading t0
 #pragma unroll
             for (int j = 0; j < NF2; ++j) {
+                if (wave + NW * j >= NFT) continue;
                 const int p = (wave + NW * j) * 16 + col;
+                if (p >= NPX) continue;
 #pragma unroll
                 for (int r = 0; r < NR1; ++r) {
                     const int ch = r * 16 + kq * 4;
@@ -240,10 +304,12 @@ __global__ void __launch_bounds__(BTile<C>::NW * 64, sizeof(T) == 2 ? BTile<C>::
 #pragma unroll
                     for (int j = 0; j < NF2A; ++j) {
                         const int f = wave + NW * j;
-                        const int p = f * 16 + col;
+                        if (f >= NFA) continue;
+                        int p = f * 16 + col;
+                        if constexpr (NPA % 16 != 0) p = p < NPA ? p : 0;
                         const int oy = p / TWA, ox = p - oy * TWA;
                         Raw xf;
-                        if (g < G2 && f < NFA) ld8(xf, ts + ((oy + ry + tap - 2) * HWW + ox) * PSTR + coff);
+                        if (g < G2) ld8(xf, ts + ((oy + tap) * HWW + ox) * PSTR + coff);
                         else zero(xf);
 #pragma unroll
                         for (int r = 0; r < NR1; ++r) mma(acc[j][r], wf[r], xf);
@@ -255,8 +321,9 @@ __global__ void __launch_bounds__(BTile<C>::NW * 64, sizeof(T) == 2 ? BTile<C>::
                     const int f = wave + NW * j;
                     if (f >= NFA) continue;
                     const int p = f * 16 + col;
+                    if (p >= NPA) continue;
                     const int ox = p - (p / TWA) * TWA;
-                    const bool inside = (unsigned)(tx0 - 2 + ox) < (unsigned)a.W;   // the 1x5 zero-pads t1a
+                    const bool inside = (unsigned)(ox0 - 2 + ox) < (unsigned)a.W;   // the 1x5 zero-pads t1a
 #pragma unroll
                     for (int r = 0; r < NR1; ++r) {
                         const int ch = r * 16 + kq * 4;
@@ -283,7 +350,9 @@ __global__ void __launch_bounds__(BTile<C>::NW * 64, sizeof(T) == 2 ? BTile<C>::
                     for (int r = 0; r < NR1; ++r) ld8(wf[r], w2b + (r * 16 + col) * K2S + s * 32 + kq * 8);
 #pragma unroll
                     for (int j = 0; j < NF2; ++j) {
-                        const int p = (wave + NW * j) * 16 + col;
+                        if (wave + NW * j >= NFT) continue;
+                        int p = (wave + NW * j) * 16 + col;
+                        if constexpr (NPX % 16 != 0) p = p < NPX ? p : 0;
                         const int oy = p / TW, ox = p - oy * TW;
                         Raw xf;
                         if (g < G2) ld8(xf, ts + (oy * TWA + ox + tap) * PSTR + coff);
@@ -296,7 +365,9 @@ __global__ void __launch_bounds__(BTile<C>::NW * 64, sizeof(T) == 2 ? BTile<C>::
                 __syncthreads();
 #pragma unroll
                 for (int j = 0; j < NF2; ++j) {
+                    if (wave + NW * j >= NFT) continue;
                     const int p = (wave + NW * j) * 16 + col;
+                    if (p >= NPX) continue;
 #pragma unroll
                     for (int r = 0; r < NR1; ++r) {
                         const int ch = r * 16 + kq * 4;
@@ -310,26 +381,28 @@ __global__ void __launch_bounds__(BTile<C>::NW * 64, sizeof(T) == 2 ? BTile<C>::
 
         // ---- phase 3: out = act_out(act3(W3 t1 + b3) + x). The t1 fragments go to registers, then
         // the t1 region becomes per-wave staging: residual chunks in, results over them, and the
-        // fragment leaves as contiguous 16-B-per-lane stores (a per-lane NHWC store would write
-        // 16 partial lines per instruction: the ablation showed stores dominating this kernel).
+        // fragment leaves as 16-B-per-lane stores (a per-lane NHWC store would write 16 partial
+        // lines per instruction: the ablation showed stores dominating this kernel).
         Raw tf[NF2];
 #pragma unroll
         for (int j = 0; j < NF2; ++j) {
             const int p = (wave + NW * j) * 16 + col;
-            if (kq < G3) ld8(tf[j], ts + p * PSTR + kq * 8);
+            if (kq < G3 && p < NPX) ld8(tf[j], ts + p * PSTR + kq * 8);
             else zero(tf[j]);
         }
         __syncthreads();
+        STAMP(5);
         T *stg = ts + wave * 16 * OSTR;
 #pragma unroll
         for (int j = 0; j < NF2; ++j) {
+            if (wave + NW * j >= NFT) break;              // wave-uniform
             const int p0 = (wave + NW * j) * 16;
-            const int oy = p0 / TW, ox0 = p0 - oy * TW, iy = ty0 + oy;
 #pragma unroll
             for (int k = 0; k < CPL; ++k) {
                 const int q = lane + 64 * k;
-                if (q < CPF) *reinterpret_cast<uint4 *>(stg + (q * EPC / C) * OSTR + (q * EPC) % C) = res[j][k];
+                if (q < CPF) *reinterpret_cast<uint4 *>(stg + (q / CPP) * OSTR + (q % CPP) * EPC) = res[j % RP][k];
             }
+            if (j + RP < NF2 && wave + NW * (j + RP) < NFT) load_res(j + RP, res[j % RP]);
             wave_lds_sync();
 #pragma unroll
             for (int r = 0; r < NR3; ++r) {
@@ -347,67 +420,89 @@ __global__ void __launch_bounds__(BTile<C>::NW * 64, sizeof(T) == 2 ? BTile<C>::
 #pragma unroll
             for (int k = 0; k < CPL; ++k) {
                 const int q = lane + 64 * k;
-                const int ix = tx0 + ox0 + q * EPC / C;
-                const bool ok = q < CPF && (unsigned)iy < (unsigned)a.H && (unsigned)ix < (unsigned)a.W && !(a.ablate & 4);
-                if (q < CPF)
-                    bst16(rob, ok ? xn + (uint32_t)((iy * a.W + tx0 + ox0) * C + q * EPC) * (uint32_t)sizeof(T) : OOB,
-                          *reinterpret_cast<const uint4 *>(stg + (q * EPC / C) * OSTR + (q * EPC) % C));
+                if (q < CPF) {
+                    const uint32_t off = (a.ablate & 4) ? OOB : pix_off(wave + NW * j, q / CPP, (q % CPP) * EPC);
+                    bst16(rob, off, *reinterpret_cast<const uint4 *>(stg + (q / CPP) * OSTR + (q % CPP) * EPC));
+                }
             }
             wave_lds_sync();
         }
+        STAMP(6);
     }
 }
 
-size_t bneck_lds_bytes(int prec, int C, bool asym, int ry, int rx) {
+#ifdef BUGSEG_STAMPS
+extern "C" int bugseg_debug_set_stamps(void *p) {
+    return hipMemcpyToSymbol(HIP_SYMBOL(bugseg_stamps), &p, sizeof(p)) == hipSuccess ? 0 : -3;
+}
+#endif
+
+size_t bneck_lds_bytes(int prec, int C, bool asym, int v) {
+    int TH, TW, NW;
+    bneck_shape(C, v, TH, TW, NW);
     const int es = prec == PREC_BF16 ? 2 : 4, pad = 16 / es;
     const int I = C / 4, IS = I < 8 ? 8 : I, NR1 = (I + 15) / 16;
     const int KS1 = (C / 8 + 3) / 4, KS2 = ((asym ? 5 : 9) * IS / 8 + 3) / 4;
-    const int TH = bneck_tile_h(C), TW = bneck_tile_w(C);
+    const int R = asym ? 2 : 1;
     const size_t wts = (size_t)NR1 * 16 * (KS1 * 32 + pad) + (size_t)NR1 * 16 * (KS2 * 32 + pad) * (asym ? 2 : 1) +
                        (size_t)C * (32 + pad);
-    const size_t halo = (size_t)(TH + 2 * ry) * (TW + 2 * rx) * (IS + pad);
-    const size_t stage = (size_t)bneck_waves(C) * 16 * (C + pad);      // phase-3 output staging
+    const size_t halo = (size_t)(TH + 2 * R) * (TW + 2 * R) * (IS + pad);
+    const size_t stage = (size_t)NW * 16 * (C + pad);      // phase-3 output staging
     const size_t consts = ((size_t)6 * NR1 * 16 + 3 * (size_t)C) * sizeof(float);
     return (wts + (halo > stage ? halo : stage)) * es + consts;
 }
 
+// kernel symbol of (precision, C, asym, variant, transposed); nullptr if not built
 template <typename T>
-static hipError_t launch_t(int C, bool asym, const BneckArgs &a, dim3 g, size_t lds, hipStream_t s) {
-#define BN_CASE(CC)                                                                                     \
-    if (C == CC) {                                                                                      \
-        if (asym) hipLaunchKernelGGL((bneck_kernel<T, CC, true>), g, dim3(BTile<CC>::NW * 64), lds, s, a);            \
-        else hipLaunchKernelGGL((bneck_kernel<T, CC, false>), g, dim3(BTile<CC>::NW * 64), lds, s, a);                \
-        return hipGetLastError();                                                                       \
-    }
-    BN_CASE(128)
-    BN_CASE(64)
-    BN_CASE(16)
-#undef BN_CASE
-    return hipErrorInvalidValue;
+static const void *kfun(int C, bool asym, int v, bool tr) {
+#define BK_CASE(CC, VV) \
+    if (C == CC && v == VV && !tr) return asym ? (const void *)bneck_kernel<T, CC, true, VV, false> : (const void *)bneck_kernel<T, CC, false, VV, false>;
+    BK_CASE(128, 0) BK_CASE(128, 1) BK_CASE(64, 0) BK_CASE(64, 1) BK_CASE(16, 0)
+#undef BK_CASE
+    if (C == 128 && v == 1 && tr && !asym) return (const void *)bneck_kernel<T, 128, false, 1, true>;
+    return nullptr;
 }
 
-hipError_t launch_bneck(int prec, int C, bool asym, const BneckArgs &a, hipStream_t s) {
-    const size_t lds = bneck_lds_bytes(prec, C, asym, a.ry, a.rx);
-    static int attr_set[2][2][3] = {};
+static const void *bneck_fun(int prec, int C, bool asym, int v, bool tr) {
+    return prec == PREC_BF16 ? kfun<__bf16>(C, asym, v, tr) : kfun<float>(C, asym, v, tr);
+}
+
+// dynamic LDS above 64 KB must be allowed per kernel (once)
+static hipError_t allow_lds(const void *f) {
+    static const void *done[64] = {};
+    for (const void *d : done)
+        if (d == f) return hipSuccess;
+    hipError_t e = hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+    if (e != hipSuccess) return e;
+    for (const void *&d : done)
+        if (!d) { d = f; break; }
+    return hipSuccess;
+}
+
+int bneck_slots_per_cu(int prec, int C, bool asym, int v, bool tr) {
+    const void *f = bneck_fun(prec, C, asym, v, tr);
+    int th, tw, nw;
+    bneck_shape(C, v, th, tw, nw);
+    if (!f || allow_lds(f) != hipSuccess) return 0;
+    int n = 0;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, f, nw * 64, bneck_lds_bytes(prec, C, asym, v)) != hipSuccess) return 0;
+    return n;
+}
+
+hipError_t launch_bneck(int prec, int C, bool asym, int v, const BneckArgs &a, hipStream_t s) {
+    const void *f = bneck_fun(prec, C, asym, v, a.tr != 0);
+    if (!f) return hipErrorInvalidValue;
+    int th, tw, nw;
+    bneck_shape(C, v, th, tw, nw);
+    const size_t lds = bneck_lds_bytes(prec, C, asym, v);
+    if (lds > 64 * 1024) {
+        hipError_t e = allow_lds(f);
+        if (e != hipSuccess) return e;
+    }
     int g = a.ntiles < 2048 ? a.ntiles : 2048;
     g = (g + 7) & ~7;
-    const int ci = C == 128 ? 0 : C == 64 ? 1 : 2;
-    if (lds > 64 * 1024 && !attr_set[prec][asym][ci]) {
-        // dynamic LDS above 64 KB must be allowed per kernel
-        hipError_t e;
-        if (prec == PREC_BF16)
-            e = C == 128 ? hipFuncSetAttribute(asym ? (const void *)bneck_kernel<__bf16, 128, true> : (const void *)bneck_kernel<__bf16, 128, false>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024)
-              : C == 64 ? hipFuncSetAttribute(asym ? (const void *)bneck_kernel<__bf16, 64, true> : (const void *)bneck_kernel<__bf16, 64, false>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024)
-                        : hipFuncSetAttribute(asym ? (const void *)bneck_kernel<__bf16, 16, true> : (const void *)bneck_kernel<__bf16, 16, false>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
-        else
-            e = C == 128 ? hipFuncSetAttribute(asym ? (const void *)bneck_kernel<float, 128, true> : (const void *)bneck_kernel<float, 128, false>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024)
-              : C == 64 ? hipFuncSetAttribute(asym ? (const void *)bneck_kernel<float, 64, true> : (const void *)bneck_kernel<float, 64, false>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024)
-                        : hipFuncSetAttribute(asym ? (const void *)bneck_kernel<float, 16, true> : (const void *)bneck_kernel<float, 16, false>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
-        if (e != hipSuccess) return e;
-        attr_set[prec][asym][ci] = 1;
-    }
-    if (prec == PREC_BF16) return launch_t<__bf16>(C, asym, a, dim3(g), lds, s);
-    return launch_t<float>(C, asym, a, dim3(g), lds, s);
+    void *args[] = {const_cast<BneckArgs *>(&a)};
+    return hipLaunchKernel(f, dim3(g), dim3(nw * 64), args, lds, s);
 }
 
 }  // namespace bugseg

@@ -76,19 +76,22 @@ struct BneckArgs {
     const void *x;       // block input (B, H, W, C) NHWC
     void *out;           // block output, same shape
     int B, H, W;
-    int ry, rx, d;       // halo of the middle conv (rows, cols) and its dilation
-    int tiles_x, tiles_y, ntiles;
+    int dt, phases;      // tiling dilation (the middle conv's dilation; 1 for asymmetric) and dt^2
+    int tr;              // transposed tiles: tile rows run along image columns (symmetric blocks only)
+    int tiles_x, tiles_y, ntiles;   // tiles per phase sub-image row / column; B * phases * tiles_y * tiles_x
     int ablate;          // debug only (BUGSEG_BNECK_ABLATE): 1 skip x loads, 2 skip middle conv, 4 skip stores
     const void *w1, *w2, *w2b, *w3;                   // packed [Npad][Kpad] (w2b: asymmetric 1x5)
     const float *b1, *s1, *b2, *s2, *b2b, *s2b, *b3, *s3, *s_out;
-    uint32_t mHWW; int sHWW;                          // fdiv by the halo-tile width TW + 2*rx
     uint32_t x_bytes;                                 // bytes of x (== out)
     int slopes_le1;                                   // every PReLU slope <= 1: max(v, s*v)
 };
-hipError_t launch_bneck(int prec, int C, bool asym, const BneckArgs &a, hipStream_t s);
-size_t bneck_lds_bytes(int prec, int C, bool asym, int ry, int rx);
-int bneck_tile_h(int C);
-int bneck_tile_w(int C);
+// tile-shape variants of the fused kernel for C channels: 0 .. bneck_variants(C) - 1
+int bneck_variants(int C);
+void bneck_shape(int C, int v, int &th, int &tw, int &nw);
+size_t bneck_lds_bytes(int prec, int C, bool asym, int v);
+// resident workgroups per CU (occupancy API); 0 if (C, asym, v, tr) is not built
+int bneck_slots_per_cu(int prec, int C, bool asym, int v, bool tr);
+hipError_t launch_bneck(int prec, int C, bool asym, int v, const BneckArgs &a, hipStream_t s);
 
 // ---- preprocess / layout (prep_kernels.hip) --------------------------------------------------
 struct PreArgs {

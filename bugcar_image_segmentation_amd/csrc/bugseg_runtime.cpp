@@ -59,7 +59,7 @@ struct Op {
     ConvArgs a;
     int nr = 0, epi = 0;
     BneckArgs bn;
-    int bn_c = 0;
+    int bn_c = 0, bn_var = 0;
     bool bn_asym = false;
     double bytes = 0, flops = 0;
     double layer_bytes = -1;   // per-layer (unfused) algorithmic bytes of the work; -1: same as bytes
@@ -475,10 +475,10 @@ ConvArgs base_args(const bugseg_ctx *ctx, const Packed &p) {
 }
 
 // A regular block runs as ONE fused launch (bneck_kernels.hip) when its shape is one the fused
-// kernel is built for and the halo of its middle conv stays small (recomputed projection <= 3x the
-// tile: dilation <= 4 on 16x16 tiles); otherwise as its 3-4 conv launches. BUGSEG_NO_FUSE=1 forces
-// the unfused plan (A/B testing; results are bit-identical).
-bool fusable_regular(const bugseg_ctx *ctx, const BlockDesc &b, const std::vector<int> &ids, int &ry, int &rx, int &d) {
+// kernel is built for and a tile variant covers the layer efficiently (pick_bneck_variant);
+// otherwise as its 3-4 conv launches. BUGSEG_NO_FUSE=1 forces the unfused plan (A/B testing;
+// results are bit-identical).
+bool fusable_regular(const bugseg_ctx *ctx, const BlockDesc &b, const std::vector<int> &ids, int &r, int &d) {
     const char *env = std::getenv("BUGSEG_NO_FUSE");     // read per plan build (plans are cached)
     if (env && *env && *env != '0') return false;
     // the fused kernel computes PReLU as max(v, s*v), exact only for slopes <= 1
@@ -498,17 +498,56 @@ bool fusable_regular(const bugseg_ctx *ctx, const BlockDesc &b, const std::vecto
         if (a.kh != 5 || a.kw != 1 || a.pad_h != 2 || a.pad_w != 0 || a.dil_h != 1 ||
             c.kh != 1 || c.kw != 5 || c.pad_h != 0 || c.pad_w != 2 || c.dil_w != 1 || a.cout != C / 4 || c.cout != C / 4)
             return false;
-        ry = rx = 2; d = 1;
+        r = 2; d = 1;
     } else {
         const UnitDesc &m = b.units[1];
         if (m.kh != 3 || m.kw != 3 || m.dil_h != m.dil_w || m.pad_h != m.dil_h || m.pad_w != m.dil_w || m.cout != C / 4)
             return false;
         d = m.dil_h;
-        ry = rx = d;
+        r = 1;
     }
-    const int th = bneck_tile_h(C), tw = bneck_tile_w(C);
-    if ((double)(th + 2 * ry) * (tw + 2 * rx) > 3.0 * th * tw) return false;
-    return bneck_lds_bytes(ctx->prec, C, nu == 4, ry, rx) <= 160 * 1024;
+    return true;
+}
+
+// Tile variant of a fused bottleneck layer: the variant whose estimated time is least, where a
+// launch costs (rounds of resident workgroups) x (per-tile cost) and the per-tile cost is the
+// per-wave fragment count of the two tile phases (weights from in-kernel phase clocks of the 16x16
+// C128 tile, scripts/stamp_probe.py: ~3.8k cycles per halo fragment per wave in the projection,
+// ~7.5k per tile fragment per wave in the middle conv + expansion, ~4.5k fixed). Returns -1 when no
+// variant keeps at least 60 % of the computed tile pixels inside the image (large dilations on small
+// feature maps: the unfused launches are cheaper). BUGSEG_BNECK_VARIANT forces a variant.
+int pick_bneck_variant(const bugseg_ctx *ctx, int C, bool asym, int d, int B, int H, int W, int &tiles_y, int &tiles_x,
+                       int &tr) {
+    int cus = 0;
+    if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, ctx->device) != hipSuccess || cus <= 0) cus = 256;
+    const char *force = std::getenv("BUGSEG_BNECK_VARIANT");
+    const int R = asym ? 2 : 1;
+    const int hs = (H + d - 1) / d, ws = (W + d - 1) / d;    // phase sub-image (largest phase)
+    int best = -1;
+    double best_cost = 0;
+    for (int v = 0; v < bneck_variants(C); ++v) {
+        int th, tw, nw;
+        bneck_shape(C, v, th, tw, nw);
+        if (bneck_lds_bytes(ctx->prec, C, asym, v) > 160 * 1024) continue;
+        const bool forced = force && *force && std::atoi(force) == v;
+        for (int t = 0; t < (asym ? 1 : 2); ++t) {
+            const int spc = bneck_slots_per_cu(ctx->prec, C, asym, v, t != 0);
+            if (spc <= 0) continue;                           // this orientation is not built
+            const int slots = spc * cus;
+            const int ty = t ? (hs + tw - 1) / tw : (hs + th - 1) / th, tx = t ? (ws + th - 1) / th : (ws + tw - 1) / tw;
+            const double ntiles = (double)B * d * d * ty * tx;
+            const double eff = (double)H * W / (ntiles / B * th * tw);
+            const double nf1 = std::ceil((th + 2.0 * R) * (tw + 2.0 * R) / 16.0), nft = std::ceil(th * tw / 16.0);
+            const double tile = 3.8 * std::ceil(nf1 / nw) + 7.5 * std::ceil(nft / nw) + 4.5;
+            const double cost = std::ceil(ntiles / slots) * tile;
+            if (!forced && eff < 0.6) continue;
+            if (best < 0 || (forced && best != v) || cost < best_cost) {
+                best = v; best_cost = cost; tiles_y = ty; tiles_x = tx; tr = t;
+            }
+        }
+        if (forced && best == v) break;
+    }
+    return best;
 }
 
 // Walk the network for (B, H, W). With fill == false only the buffer sizes are computed.
@@ -597,8 +636,10 @@ struct Walker {
                 const int nu = (int)b.units.size();
                 Shape s = cur;
                 const unsigned char *src = curp;
-                int ry = 0, rx = 0, dd = 1;
-                if (fusable_regular(ctx, b, ids, ry, rx, dd)) {
+                int rr = 0, dd = 1, ty = 0, tx = 0, ttr = 0, var = -1;
+                if (fusable_regular(ctx, b, ids, rr, dd))
+                    var = pick_bneck_variant(ctx, b.attrs[0], nu == 4, dd, B, cur.H, cur.W, ty, tx, ttr);
+                if (var >= 0) {
                     // one launch: projection + middle conv + expansion + residual, internals in LDS
                     szX = std::max(szX, tbytes(cur));
                     if (fill) {
@@ -606,22 +647,21 @@ struct Walker {
                         op.kind = 1;
                         op.bn_c = b.attrs[0];
                         op.bn_asym = nu == 4;
+                        op.bn_var = var;
                         BneckArgs &q = op.bn;
                         std::memset(&q, 0, sizeof(q));
                         const unsigned char *dw = (const unsigned char *)ctx->dev_w;
                         const Packed &p1 = P(0), &p2 = P(1), &p3 = P(nu - 1), &p2b = P(nu == 4 ? 2 : 1);
                         q.x = curp; q.out = dst; q.B = B; q.H = cur.H; q.W = cur.W;
-                        q.ry = ry; q.rx = rx; q.d = dd;
+                        q.dt = dd; q.phases = dd * dd; q.tr = ttr;
                         if (const char *ab = std::getenv("BUGSEG_BNECK_ABLATE")) q.ablate = std::atoi(ab);
-                        const int th = bneck_tile_h(op.bn_c), tw = bneck_tile_w(op.bn_c);
-                        q.tiles_y = (cur.H + th - 1) / th; q.tiles_x = (cur.W + tw - 1) / tw;
-                        q.ntiles = B * q.tiles_y * q.tiles_x;
+                        q.tiles_y = ty; q.tiles_x = tx;
+                        q.ntiles = B * q.phases * ty * tx;
                         q.w1 = dw + p1.o_w; q.b1 = (const float *)(dw + p1.o_bias); q.s1 = (const float *)(dw + p1.o_s1);
                         q.w2 = dw + p2.o_w; q.b2 = (const float *)(dw + p2.o_bias); q.s2 = (const float *)(dw + p2.o_s1);
                         q.w2b = dw + p2b.o_w; q.b2b = (const float *)(dw + p2b.o_bias); q.s2b = (const float *)(dw + p2b.o_s1);
                         q.w3 = dw + p3.o_w; q.b3 = (const float *)(dw + p3.o_bias); q.s3 = (const float *)(dw + p3.o_s1);
                         q.s_out = (const float *)(dw + p3.o_s2);
-                        fastdiv((uint32_t)(tw + 2 * rx), q.mHWW, q.sHWW);
                         q.slopes_le1 = 1;
                         const std::pair<size_t, int> slopes[] = {{p1.o_s1, p1.Npad}, {p2.o_s1, p2.Npad}, {p2b.o_s1, p2b.Npad},
                                                                  {p3.o_s1, p3.Npad}, {p3.o_s2, p3.Npad}};
@@ -951,7 +991,7 @@ static int enet_forward(bugseg_ctx *ctx, const void *in, bool bgr, int B, int H,
     }
     for (size_t i = 0; i < pl.ops.size(); ++i) {
         const Op &op = pl.ops[i];
-        hipError_t e = op.kind == 1 ? launch_bneck(ctx->prec, op.bn_c, op.bn_asym, op.bn, (hipStream_t)stream)
+        hipError_t e = op.kind == 1 ? launch_bneck(ctx->prec, op.bn_c, op.bn_asym, op.bn_var, op.bn, (hipStream_t)stream)
                                     : launch_conv(ctx->prec, op.nr, op.epi, op.a, (hipStream_t)stream);
         if (e != hipSuccess) return fail(ctx, BUGSEG_EHIP, "conv launch " + std::to_string(i) + ": " + hipGetErrorString(e));
     }
@@ -1043,7 +1083,13 @@ int bugseg_plan_op(bugseg_ctx *ctx, int B, int H, int W, int op, char *kernel, i
     if (op < 0 || op >= (int)pl.ops.size()) return fail(ctx, BUGSEG_EINVAL, "op index out of range");
     const Op &o = pl.ops[op];
     std::string tag;
-    if (o.kind == 1) tag = "bneck C" + std::to_string(o.bn_c) + (o.bn_asym ? " asym" : "");
+    if (o.kind == 1) {
+        int th, tw, nw;
+        bneck_shape(o.bn_c, o.bn_var, th, tw, nw);
+        tag = "bneck C" + std::to_string(o.bn_c) + (o.bn_asym ? " asym" : "") + " " + std::to_string(th) + "x" +
+              std::to_string(tw);
+        (void)nw;
+    }
     else if (o.epi == EPI_INIT || o.epi == EPI_INIT_BGR) tag = "init";
     else tag = "conv NR" + std::to_string(o.nr) + " E" + std::to_string(o.epi);
     if (kernel && kernel_len > 0) {
@@ -1075,7 +1121,7 @@ int bugseg_plan_launch_op(bugseg_ctx *ctx, int B, int H, int W, int op, void *st
     if (op < 0 || op >= (int)pl.ops.size()) return fail(ctx, BUGSEG_EINVAL, "op index out of range");
     DeviceGuard g(ctx->device);
     const Op &o = pl.ops[op];
-    hipError_t e = o.kind == 1 ? launch_bneck(ctx->prec, o.bn_c, o.bn_asym, o.bn, (hipStream_t)stream)
+    hipError_t e = o.kind == 1 ? launch_bneck(ctx->prec, o.bn_c, o.bn_asym, o.bn_var, o.bn, (hipStream_t)stream)
                                : launch_conv(ctx->prec, o.nr, o.epi, o.a, (hipStream_t)stream);
     if (e != hipSuccess) return fail(ctx, BUGSEG_EHIP, "launch of op " + std::to_string(op) + ": " + hipGetErrorString(e));
     return BUGSEG_OK;

@@ -1,10 +1,9 @@
+# Stream / batch sweep of the bench (no CPU baseline).
 set -o pipefail
 cd $GRAFT_REPO_ROOT
-mkdir -p gpurun_out
-timeout -k 10 600 python -m pytest tests -m gpu -q -x --timeout 500 > gpurun_out/pytest_gpu.log 2>&1
-echo "pytest exit $?" >> gpurun_out/pytest_gpu.log
-for s in 1 2 4; do
-  timeout -k 10 300 python bench.py --steps 20 --warmup 5 --no-cpu-baseline --streams $s > gpurun_out/bench_s$s.json 2> gpurun_out/bench_s$s.err || exit 1
+mkdir -p gpurun_out/streams
+for cfg in "64 1" "64 2" "64 4" "96 3" "128 4" "128 2"; do
+  set -- $cfg
+  timeout -k 10 120 python bench.py --batch $1 --streams $2 --steps 20 --warmup 5 --no-cpu-baseline > gpurun_out/streams/b$1_s$2.json 2>/dev/null || exit 1
 done
-timeout -k 10 300 python bench.py --steps 10 --warmup 3 --no-cpu-baseline --streams 2 --batch 128 > gpurun_out/bench_s2_b128.json 2> gpurun_out/bench_s2_b128.err || exit 1
 echo done

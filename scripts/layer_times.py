@@ -12,10 +12,17 @@ import re
 from collections import defaultdict
 
 
+# tile shape of each fused-bottleneck variant (bneck_kernels.hip BShape)
+BNECK_SHAPES = {(128, 0): "16x16", (128, 1): "20x16", (64, 0): "16x16", (64, 1): "20x16", (16, 0): "16x16"}
+
+
 def short(name):
-    m = re.search(r"bneck_kernelI(DF16b|f)Li(\d+)ELb(\d)E", name)
+    m = re.search(r"bneck_kernelI(DF16b|f)Li(\d+)ELb(\d)ELi(\d+)E", name)
+    if not m:
+        m = re.search(r"bneck_kernel<(__bf16|float), (\d+), (false|true), (\d+)>", name)
     if m:
-        return f"bneck C{m.group(2)}{' asym' if m.group(3) == '1' else ''}"
+        asym = m.group(3) in ("1", "true")
+        return f"bneck C{m.group(2)}{' asym' if asym else ''} {BNECK_SHAPES.get((int(m.group(2)), int(m.group(4))), '?')}"
     m = re.search(r"conv_kernelI(DF16b|f)Li(\d+)ELi(\d+)E", name)
     if m:
         return f"conv NR{m.group(2)} E{m.group(3)}"

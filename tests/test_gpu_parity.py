@@ -190,16 +190,22 @@ def test_forward_bgr_equals_preprocess_then_forward(gpu, prec, pool_k):
     assert torch.equal(m.predict_device(x2, N.OUT_LOGITS_F32), c)
 
 
+@pytest.mark.parametrize("variant", [None, "0", "1"])
 @pytest.mark.parametrize("prec", ["fp32", "bf16"])
 @pytest.mark.parametrize("H,W", [(64, 96), (120, 160), (480, 640)])
-def test_fused_bottlenecks_equal_unfused(gpu, blocks, prec, H, W, monkeypatch):
+def test_fused_bottlenecks_equal_unfused(gpu, blocks, prec, H, W, variant, monkeypatch):
     """The fused bottleneck kernel (projection + middle conv + expansion + residual, internals in
-    LDS) rounds the internal tensors exactly as the unfused conv chain stores them: bit-identical."""
+    LDS) rounds the internal tensors exactly as the unfused conv chain stores them: bit-identical.
+    `variant` forces one tile shape for every fused layer (bypassing the efficiency rule, so the
+    d = 8 / 16 blocks run fused through the dilated tiling too); None = the runtime's choice."""
     B = 2 if H < 480 else 1
     bgr = torch.from_numpy(synthetic.road_frames(B, H, W, seed=H)).cuda()
+    if variant is not None:
+        monkeypatch.setenv("BUGSEG_BNECK_VARIANT", variant)
     fused = ENET(weights=blocks, precision=prec)
     a = torch.empty((B, 15, H, W), dtype=torch.float32, device=gpu)
     fused.ctx.forward_bgr(bgr, B, H, W, N.OUT_LOGITS_F32, a)
+    monkeypatch.delenv("BUGSEG_BNECK_VARIANT", raising=False)
     monkeypatch.setenv("BUGSEG_NO_FUSE", "1")
     plain = ENET(weights=blocks, precision=prec)
     b = torch.empty_like(a)
