@@ -193,6 +193,16 @@ def main():
         t_fwd += ev[0].elapsed_time(ev[1])
         t_bev += ev[1].elapsed_time(ev[2])
     t_fwd, t_bev = t_fwd / reps, t_bev / reps
+    # the laserscan-like occupancy mode (bev.py:351-375) on the same class maps (not in the timed step)
+    bev.laserscan_like_occupancy_grid = True
+    bev.create_occupancy_grid_device(ss, *grid, out=gs)
+    ev[0].record(stream)
+    for _ in range(reps):
+        bev.create_occupancy_grid_device(ss, *grid, out=gs)
+    ev[1].record(stream)
+    ev[1].synchronize()
+    t_ls = ev[0].elapsed_time(ev[1]) / reps
+    bev.laserscan_like_occupancy_grid = False
     n_launch, alg_bytes, plan_bytes, flops = model.ctx.plan_info(Bs, H, W, N.OUT_CLASS3_U8, bgr_input=True)
     kernels = kernel_table(model.ctx, Bs, H, W, reps, stream)
 
@@ -237,7 +247,8 @@ def main():
             "kernels": {t: {"launches": v["launches"], "us_per_launch": round(v["us_per_launch"], 2),
                             "GBps": round(v["bytes_per_launch"] / (v["us_per_launch"] * 1e-6) / 1e9, 1)}
                         for t, v in sorted(kernels.items(), key=lambda kv: -kv[1]["total_us"])},
-            "stages_ms": {"frames": Bs, "enet_forward": round(t_fwd, 4), "bev_occgrid": round(t_bev, 4)},
+            "stages_ms": {"frames": Bs, "enet_forward": round(t_fwd, 4), "bev_occgrid": round(t_bev, 4),
+                          "bev_occgrid_laserscan": round(t_ls, 4)},
         }
         if not a.no_cpu_baseline:
             res["cpu_baseline"] = cpu_baseline(blocks, bev, grid, H, W, a.cpu_baseline_seconds)

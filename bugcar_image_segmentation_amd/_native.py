@@ -33,7 +33,7 @@ class BevParams(ctypes.Structure):
                 ("warp_w", ctypes.c_int), ("warp_h", ctypes.c_int), ("occ_w_px", ctypes.c_int),
                 ("occ_h_px", ctypes.c_int), ("occ_w", ctypes.c_int), ("occ_h", ctypes.c_int),
                 ("left_x", ctypes.c_int), ("top_y", ctypes.c_int), ("ros_layout", ctypes.c_int),
-                ("variant", ctypes.c_int)]
+                ("variant", ctypes.c_int), ("laserscan", ctypes.c_int)]
 
 
 class BugsegError(RuntimeError):

@@ -8,6 +8,10 @@ kernel (csrc/bev_kernels.hip). The geometry below (cell sizes, template offsets)
 written exactly as the reference writes it, because its float-to-int truncations are part of the
 result.
 
+The laserscan-like mode ("is_laserscan", bev.py:351-375 and the binary variant's bev.py:143-164) runs
+on the engine too: the rasteriser, a per-ray nearest-obstacle kernel and a re-projection kernel over
+polar tables the library builds once per geometry (csrc/bev_kernels.hip).
+
 Additions: `create_occupancy_grid_device` (batched, device tensors in and out, optional ROS data
 layout) and `occupancy_params`.
 """
@@ -126,7 +130,7 @@ class bev_transform_tools:
 
     # -- geometry ----------------------------------------------------------------------------
     def occupancy_params(self, occupancy_grid_width_in_m, occupancy_grid_height_in_m, cell_size_in_m,
-                         ros_layout: bool = False, binary: bool = False) -> N.BevParams:
+                         ros_layout: bool = False, binary: bool = False, laserscan: bool | None = None) -> N.BevParams:
         """bev.py:307-319 (bev.py:101-114 for the binary variant: the same arithmetic), with the
         reference's float arithmetic and int() truncations."""
         cell_size_in_px = (cell_size_in_m * 100 / self.cm_per_px)
@@ -149,6 +153,7 @@ class bev_transform_tools:
         p.left_x, p.top_y = left_x, top_y
         p.ros_layout = int(bool(ros_layout))
         p.variant = int(bool(binary))
+        p.laserscan = int(bool(self.laserscan_like_occupancy_grid if laserscan is None else laserscan))
         return p
 
     def _check_shape(self, shape):
@@ -162,10 +167,9 @@ class bev_transform_tools:
                                      out: torch.Tensor | None = None, binary: bool = False) -> torch.Tensor:
         """Batched create_occupancy_grid on device tensors: segmaps (B, rows, cols) uint8 class maps
         -> (B, h, w) int8 (or (B, w, h) in ROS data order when ros_layout). binary=True is
-        create_occupancy_grid_binary (bev.py:97-165)."""
-        if self.laserscan_like_occupancy_grid:
-            raise NotImplementedError("laserscan-like occupancy mode (bev.py:351-375) is SURVEY.md §8(f) row 2: "
-                                      "not built yet")
+        create_occupancy_grid_binary (bev.py:97-165). The laserscan-like mode follows the object's
+        is_laserscan flag; binary + laserscan returns (2, B, ...): the grid, then the polar
+        re-projection of its nearest obstacles (the reference's returned pair, bev.py:162)."""
         if segmaps.dim() == 2:
             segmaps = segmaps.unsqueeze(0)
         self._check_shape(segmaps.shape[1:])
@@ -177,13 +181,19 @@ class bev_transform_tools:
                                   binary)
         B = seg.shape[0]
         shape = (B, p.occ_w, p.occ_h) if ros_layout else (B, p.occ_h, p.occ_w)
+        if binary and p.laserscan:
+            shape = (2,) + shape
+        if out is not None and tuple(out.shape) != shape:
+            raise ValueError(f"out has shape {tuple(out.shape)}, expected {shape}")
         if out is None:
             out = torch.empty(shape, dtype=torch.int8, device=seg.device)
         N.shared_context(seg.device.index).bev(seg, B, p, out)
         return out
 
     def create_occupancy_grid(self, segmap, occupancy_grid_width_in_m, occupancy_grid_height_in_m, cell_size_in_m):
-        """bev.py:301-381 -> np.int8 (h, w) in {-1 unknown, 0 free, 100 occupied}."""
+        """bev.py:301-381 -> np.int8 (h, w) in {-1 unknown, 0 free, 100 occupied}. In laserscan-like mode
+        (bev.py:351-375) only the obstacle cells nearest the vehicle along each polar ray stay
+        occupied; obstacle cells behind them become unknown."""
         self._check_shape(np.shape(segmap))
         seg = segmap if isinstance(segmap, torch.Tensor) else torch.from_numpy(np.ascontiguousarray(segmap, dtype=np.uint8))
         return self.create_occupancy_grid_device(seg, occupancy_grid_width_in_m, occupancy_grid_height_in_m,
@@ -193,8 +203,13 @@ class bev_transform_tools:
         """bev.py:97-165 (legacy variant for ENET.predict_binary maps) -> np.int8 (h, w).
         Occupied = template value 1 only (bev.py:126); the reference's uint8 encoding gives
         {0: -1, 1: 100, 2: 0} and, for a 3-class map's class 2, -100 (bev.py:137-141 under NumPy 1.x
-        casting). For {0,1} maps it equals create_occupancy_grid."""
+        casting). For {0,1} maps it equals create_occupancy_grid. In laserscan-like mode it returns the
+        reference's pair (grid, re-projected nearest obstacles) (bev.py:143-162)."""
         self._check_shape(np.shape(segmap))
         seg = segmap if isinstance(segmap, torch.Tensor) else torch.from_numpy(np.ascontiguousarray(segmap, dtype=np.uint8))
-        return self.create_occupancy_grid_device(seg, occupancy_grid_width_in_m, occupancy_grid_height_in_m,
-                                                 cell_size_in_m, binary=True)[0].cpu().numpy()
+        g = self.create_occupancy_grid_device(seg, occupancy_grid_width_in_m, occupancy_grid_height_in_m,
+                                              cell_size_in_m, binary=True)
+        if self.laserscan_like_occupancy_grid:
+            g = g.cpu().numpy()
+            return g[0, 0], g[1, 0]
+        return g[0].cpu().numpy()

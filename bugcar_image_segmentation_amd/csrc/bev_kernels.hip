@@ -132,6 +132,11 @@ __global__ void __launch_bounds__(256) bev_occgrid_kernel(const BevArgs a) {
             const uint8_t g = (uint8_t)(v * 100);
             o = (int8_t)(uint8_t)(g == 0 ? 0xff : (uint8_t)(200 - g));
         }
+        if (a.laserscan) {
+            // the polar warp's source: the cells (bev.py:353) or the encoded grid (bev.py:146)
+            a.cells[i] = a.variant ? (uint8_t)o : (uint8_t)v;
+            if (!a.variant) continue;            // the final laserscan kernel writes out
+        }
         if (a.ros_layout) {
             // occgrid_to_ros.py:18-21: flip(0) then rot90ccw == G[::-1, ::-1].T, shape (occ_w, occ_h)
             a.out[(size_t)b * cells + (size_t)(a.occ_w - 1 - cx) * a.occ_h + (a.occ_h - 1 - cy)] = o;
@@ -141,12 +146,87 @@ __global__ void __launch_bounds__(256) bev_occgrid_kernel(const BevArgs a) {
     }
 }
 
+// ---- laserscan-like occupancy (bev.py:351-375; binary variant bev.py:143-164) ----------------------
+// The reference polar-warps the grid (cv2.warpPolar, nearest), finds per polar row (ray angle) the
+// nearest obstacle (np.where + npi.group_by(...).min — a Python loop over rays follows), stamps a
+// radius-1 cv2.circle there and warps the stamps back. Here:
+//   polar_min_kernel   one wave per (frame, ray): the ray's cells are gathered through the host-built
+//                      forward table (fmap) and the nearest hit is a ballot + find-first-set per 64
+//                      radii — the polar image is never materialised;
+//   laserscan_kernel   one thread per output cell: the inverse table (imap) gives its (rho, ray); it is
+//                      stamped iff some circle covers it — Circle() radius 1 is the plus
+//                      {(r-1..r+1, ray), (r, ray-1), (r, ray+1)} — i.e. |rho - rmin[ray]| <= 1 or
+//                      rmin[ray -/+ 1] == rho; then the reference's merge and encoding.
+// The tables hold the float -> short rounding of remap(INTER_NEAREST) exactly as OpenCV builds them
+// (cos/sin and fastAtan32f on the host, once per geometry). Traffic per frame: the grid read a few
+// times (L2) + the tables (L2-resident, shared by the batch) + the grid written once.
+
+__global__ void __launch_bounds__(256) polar_min_kernel(const BevArgs a) {
+    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const long rays = (long)a.B * a.ph;
+    const long cells = (long)a.occ_h * a.occ_w;
+    for (long r = blockIdx.x * 4L + wave; r < rays; r += (long)gridDim.x * 4) {
+        const int b = (int)(r / a.ph), phi = (int)(r - (long)b * a.ph);
+        const uint8_t *g = a.cells + (size_t)b * cells;
+        const int32_t *fm = a.fmap + (size_t)phi * a.pw;
+        int found = -1;
+        for (int r0 = 0; r0 < a.pw; r0 += 64) {
+            const int rho = r0 + lane;
+            bool hit = false;
+            if (rho < a.pw) {
+                const int32_t m = fm[rho];
+                hit = m >= 0 && g[(size_t)(m >> 16) * a.occ_w + (m & 0xffff)] == a.hit;
+            }
+            const unsigned long long bal = __ballot(hit);
+            if (bal) { found = r0 + __ffsll((long long)bal) - 1; break; }
+        }
+        if (lane == 0) a.rmin[r] = found;
+    }
+}
+
+__global__ void __launch_bounds__(256) laserscan_kernel(const BevArgs a) {
+    const long cells = (long)a.occ_h * a.occ_w, total = cells * a.B;
+    for (long i = blockIdx.x * 256L + threadIdx.x; i < total; i += (long)gridDim.x * 256) {
+        const int b = (int)(i / cells);
+        const int rem = (int)(i - (long)b * cells);
+        const int cy = rem / a.occ_w, cx = rem - cy * a.occ_w;
+        const int v = a.cells[i];
+        int s = 0;
+        if (a.variant || v == 3) {
+            const int32_t m = a.imap[rem];
+            if (m >= 0) {
+                const int rho = m & 0xffff, row = m >> 16;
+                const int32_t *rm = a.rmin + (size_t)b * a.ph;
+                const int r0 = rm[row];
+                s = (r0 >= 0 && abs(rho - r0) <= 1) || (row > 0 && rm[row - 1] == rho) ||
+                    (row + 1 < a.ph && rm[row + 1] == rho);
+            }
+        }
+        int8_t o;
+        if (!a.variant) {
+            const int g = v != 3 ? v : s;        // bev.py:372
+            o = (int8_t)(g == 0 ? -1 : 200 - 100 * g);   // bev.py:379
+        } else {
+            o = v == 255 ? (int8_t)-1 : (int8_t)(s * 100);  // bev.py:159-161
+        }
+        int8_t *out = a.variant ? a.out + (size_t)a.B * cells : a.out;   // binary: the second grid
+        if (a.ros_layout) out[(size_t)b * cells + (size_t)(a.occ_w - 1 - cx) * a.occ_h + (a.occ_h - 1 - cy)] = o;
+        else out[i] = o;
+    }
+}
+
 hipError_t launch_bev(const BevArgs &a, hipStream_t s) {
     const long total = (long)a.occ_h * a.occ_w * a.B;
     long g = (total + 255) / 256;
     if (g > 8192) g = 8192;
     if (g < 1) g = 1;
     hipLaunchKernelGGL(bev_occgrid_kernel, dim3((unsigned)g), dim3(256), 0, s, a);
+    if (!a.laserscan) return hipGetLastError();
+    const long rays = (long)a.B * a.ph;
+    long gr = (rays + 3) / 4;
+    if (gr > 8192) gr = 8192;
+    hipLaunchKernelGGL(polar_min_kernel, dim3((unsigned)gr), dim3(256), 0, s, a);
+    hipLaunchKernelGGL(laserscan_kernel, dim3((unsigned)g), dim3(256), 0, s, a);
     return hipGetLastError();
 }
 

@@ -126,6 +126,17 @@ struct BevArgs {
     int ros_layout;
     int variant;         // 0 create_occupancy_grid, 1 create_occupancy_grid_binary
     int8_t *out;
+    // laserscan-like mode (bev.py:351-375 / :143-164): the rasteriser also writes the polar warp's
+    // source grid (variant 0: the template cells; 1: the encoded grid as uint8) to `cells`, and for
+    // variant 0 leaves `out` to the final laserscan kernel
+    int laserscan;
+    uint8_t *cells;      // (B, occ_h, occ_w)
+    // polar tables (host-built, bugseg_runtime.cpp polar_tables) and per-row minima
+    const int32_t *fmap; // (ph, pw): source cell x | y << 16, or -1
+    const int32_t *imap; // (occ_h, occ_w): polar rho | row << 16, or -1
+    int pw, ph;
+    int32_t *rmin;       // (B, ph)
+    int hit;             // polar value that is an obstacle: 3 (variant 0) or 100 (variant 1)
 };
 hipError_t launch_bev(const BevArgs &a, hipStream_t s);
 

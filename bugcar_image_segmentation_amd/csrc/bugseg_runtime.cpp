@@ -104,6 +104,12 @@ struct bugseg_ctx {
     int pre_key[4] = {0, 0, 0, 0};
     void *pre_tab = nullptr;
     size_t pre_tab_bytes = 0;
+    // laserscan mode: polar tables of the last geometry (occ_w, occ_h, variant) and batch scratch
+    int polar_key[3] = {0, 0, -1};
+    int polar_pw = 0, polar_ph = 0;
+    void *polar_tab = nullptr;       // fmap (ph*pw int32) then imap (occ_h*occ_w int32)
+    void *ls_scratch = nullptr;      // cells (B*occ_h*occ_w u8, 256-B aligned) then rmin (B*ph int32)
+    size_t ls_scratch_bytes = 0;
 };
 
 namespace {
@@ -870,6 +876,8 @@ int bugseg_destroy(bugseg_ctx *ctx) {
     if (ctx->dev_luts) (void)hipFree(ctx->dev_luts);
     if (ctx->plan.arena) (void)hipFree(ctx->plan.arena);
     if (ctx->pre_tab) (void)hipFree(ctx->pre_tab);
+    if (ctx->polar_tab) (void)hipFree(ctx->polar_tab);
+    if (ctx->ls_scratch) (void)hipFree(ctx->ls_scratch);
     delete ctx;
     return BUGSEG_OK;
 }
@@ -1007,12 +1015,125 @@ int bugseg_enet_forward_bgr(bugseg_ctx *ctx, const uint8_t *bgr, int B, int H, i
     return enet_forward(ctx, bgr, true, B, H, W, out_kind, out, stream);
 }
 
+}  // extern "C"
+
+namespace {
+
+// ---- laserscan-like mode: cv::warpPolar's remap tables (imgwarp.cpp 4.x), built on the host once
+// per geometry. Forward: polar (rho, phi) -> grid cell, phi the row of a ph x pw polar image,
+// x = (float)(rho*Kmag) * cos(Kangle*phi) + cx in double, rounded to float, then half-to-even to a
+// short (remap INTER_NEAREST). Inverse: grid cell -> (rho, polar row) through hal::magnitude32f /
+// fastAtan32f (the AVX2 dispatch: fused polynomial) on float offsets, the BORDER_WRAP row of
+// copyMakeBorder folded into the row index. -1 = outside (BORDER_TRANSPARENT).
+#pragma clang fp contract(off)
+const float kAtanP1 = 0.9997878412794807f * (float)(180 / 3.1415926535897932384626433832795);
+const float kAtanP3 = -0.3258083974640975f * (float)(180 / 3.1415926535897932384626433832795);
+const float kAtanP5 = 0.1555786518463281f * (float)(180 / 3.1415926535897932384626433832795);
+const float kAtanP7 = -0.04432655554792128f * (float)(180 / 3.1415926535897932384626433832795);
+
+float fast_atan_rad(float y, float x) {
+    const float ax = std::fabs(x), ay = std::fabs(y);
+    const float c = std::min(ax, ay) / (std::max(ax, ay) + (float)2.220446049250313e-16);
+    const float cc = c * c;
+    float a = std::fma(std::fma(std::fma(cc, kAtanP7, kAtanP5), cc, kAtanP3), cc, kAtanP1) * c;
+    if (!(ax >= ay)) a = 90.f - a;
+    if (x < 0) a = 180.f - a;
+    if (y < 0) a = 360.f - a;
+    return a * (float)(3.1415926535897932384626433832795 / 180);
+}
+
+int round_short(float v) {
+    const long r = std::lrint(v);
+    return (int)(r < -32768 ? -32768 : r > 32767 ? 32767 : r);
+}
+
+void polar_tables(int pw, int ph, double max_radius, float cx, float cy, int w, int h, std::vector<int32_t> &fmap,
+                  std::vector<int32_t> &imap) {
+    const double CV_2PI = 6.283185307179586476925286766559;
+    const double Kangle = CV_2PI / ph, Kmag = max_radius / pw;
+    fmap.resize((size_t)pw * ph);
+    for (int phi = 0; phi < ph; ++phi) {
+        const double KKy = Kangle * phi, cp = std::cos(KKy), sp = std::sin(KKy);
+        for (int rho = 0; rho < pw; ++rho) {
+            const float r = (float)(rho * Kmag);
+            const float mx = (float)(r * cp + (double)cx), my = (float)(r * sp + (double)cy);
+            const int sx = round_short(mx), sy = round_short(my);
+            fmap[(size_t)phi * pw + rho] = ((unsigned)sx < (unsigned)w && (unsigned)sy < (unsigned)h) ? (sx | (sy << 16)) : -1;
+        }
+    }
+    imap.resize((size_t)w * h);
+    for (int y = 0; y < h; ++y)
+        for (int x = 0; x < w; ++x) {
+            const float bx = (float)x - cx, by = (float)y - cy;
+            const float mag = std::sqrt(std::fma(bx, bx, by * by));
+            const float ang = fast_atan_rad(by, bx);
+            const double rho = mag / Kmag, phi = ang / Kangle;
+            const float mx = (float)rho, my = (float)phi + 1;
+            const int X = round_short(mx), Y = round_short(my);
+            int32_t v = -1;
+            if ((unsigned)X < (unsigned)pw && (unsigned)Y < (unsigned)(ph + 2)) {
+                const int row = Y == 0 ? ph - 1 : (Y == ph + 1 ? 0 : Y - 1);
+                v = X | (row << 16);
+            }
+            imap[(size_t)y * w + x] = v;
+        }
+}
+#pragma clang fp contract(on)
+
+// Polar tables and scratch for a laserscan call; fills a.fmap / imap / pw / ph / cells / rmin / hit.
+int prepare_laserscan(bugseg_ctx *ctx, const bugseg_bev_params *p, int B, BevArgs &a, void *stream) {
+    const int w = p->occ_w, h = p->occ_h, L = std::max(w, h);
+    // warpPolar dsize: (-1, -1) -> (round(L), round(L*pi)) for create_occupancy_grid (bev.py:355);
+    // the explicit (w, h) of create_occupancy_grid_binary (bev.py:146)
+    const int pw = p->variant ? w : (int)std::lrint((double)L);
+    const int ph = p->variant ? h : (int)std::lrint((double)L * 3.1415926535897932384626433832795);
+    if (pw <= 0 || ph <= 0 || pw > 32767 || ph > 32767 || w > 32767 || h > 32767)
+        return fail(ctx, BUGSEG_EINVAL, "laserscan grid too large for the polar tables");
+    if (ctx->polar_key[0] != w || ctx->polar_key[1] != h || ctx->polar_key[2] != p->variant || !ctx->polar_tab) {
+        std::vector<int32_t> fmap, imap;
+        polar_tables(pw, ph, (double)L, (float)(w / 2.0 - 1), (float)h, w, h, fmap, imap);
+        if (hipStreamSynchronize((hipStream_t)stream) != hipSuccess) return fail(ctx, BUGSEG_EHIP, "stream sync failed");
+        if (ctx->polar_tab) (void)hipFree(ctx->polar_tab);
+        ctx->polar_tab = nullptr;
+        const size_t bytes = (fmap.size() + imap.size()) * sizeof(int32_t);
+        if (hipMalloc(&ctx->polar_tab, bytes) != hipSuccess) return fail(ctx, BUGSEG_ENOMEM, "polar table allocation failed");
+        if (hipMemcpy(ctx->polar_tab, fmap.data(), fmap.size() * 4, hipMemcpyHostToDevice) != hipSuccess ||
+            hipMemcpy((int32_t *)ctx->polar_tab + fmap.size(), imap.data(), imap.size() * 4, hipMemcpyHostToDevice) != hipSuccess)
+            return fail(ctx, BUGSEG_EHIP, "polar table upload failed");
+        ctx->polar_key[0] = w; ctx->polar_key[1] = h; ctx->polar_key[2] = p->variant;
+        ctx->polar_pw = pw; ctx->polar_ph = ph;
+    }
+    const size_t cells_bytes = ((size_t)B * w * h + 255) & ~(size_t)255;
+    const size_t need = cells_bytes + (size_t)B * ph * sizeof(int32_t);
+    if (need > ctx->ls_scratch_bytes) {
+        if (hipStreamSynchronize((hipStream_t)stream) != hipSuccess) return fail(ctx, BUGSEG_EHIP, "stream sync failed");
+        if (ctx->ls_scratch) (void)hipFree(ctx->ls_scratch);
+        ctx->ls_scratch = nullptr;
+        ctx->ls_scratch_bytes = 0;
+        if (hipMalloc(&ctx->ls_scratch, need) != hipSuccess) return fail(ctx, BUGSEG_ENOMEM, "laserscan scratch allocation failed");
+        ctx->ls_scratch_bytes = need;
+    }
+    a.laserscan = 1;
+    a.fmap = (const int32_t *)ctx->polar_tab;
+    a.imap = (const int32_t *)ctx->polar_tab + (size_t)pw * ph;
+    a.pw = pw; a.ph = ph;
+    a.cells = (uint8_t *)ctx->ls_scratch;
+    a.rmin = (int32_t *)((unsigned char *)ctx->ls_scratch + cells_bytes);
+    a.hit = p->variant ? 100 : 3;
+    return BUGSEG_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
 int bugseg_bev_occgrid(bugseg_ctx *ctx, const uint8_t *seg, int B, const bugseg_bev_params *p, int8_t *out, void *stream) {
     if (!ctx || !seg || !p || !out) return fail(ctx, BUGSEG_EINVAL, "NULL argument");
     if (B <= 0 || p->in_rows <= 0 || p->in_cols <= 0 || p->warp_w <= 0 || p->warp_h <= 0 || p->occ_w <= 0 ||
         p->occ_h <= 0 || p->occ_w_px <= 0 || p->occ_h_px <= 0)
         return fail(ctx, BUGSEG_EINVAL, "bad BEV geometry");
     if (p->variant != 0 && p->variant != 1) return fail(ctx, BUGSEG_EINVAL, "variant must be 0 or 1");
+    if (p->laserscan != 0 && p->laserscan != 1) return fail(ctx, BUGSEG_EINVAL, "laserscan must be 0 or 1");
     DeviceGuard g(ctx->device);
     BevArgs a;
     std::memset(&a, 0, sizeof(a));
@@ -1045,6 +1166,10 @@ int bugseg_bev_occgrid(bugseg_ctx *ctx, const uint8_t *seg, int B, const bugseg_
     a.ros_layout = p->ros_layout;
     a.variant = p->variant;
     a.out = out;
+    if (p->laserscan) {
+        const int rc = prepare_laserscan(ctx, p, B, a, stream);
+        if (rc != BUGSEG_OK) return rc;
+    }
     hipError_t e = launch_bev(a, (hipStream_t)stream);
     if (e != hipSuccess) return fail(ctx, BUGSEG_EHIP, std::string("bev launch: ") + hipGetErrorString(e));
     return BUGSEG_OK;

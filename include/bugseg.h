@@ -77,6 +77,11 @@ typedef struct {
                               encoding {0:-1, 1:100, 2:0, 3:100};
                            1: create_occupancy_grid_binary (bev.py:97-165): occupied = {1}, the
                               reference's uint8 encoding {0:-1, 1:100, 2:0, 3:-100}               */
+    int laserscan;      /* 1: laserscan-like mode ("is_laserscan", bev.py:37): variant 0 keeps only the
+                              obstacle cells nearest the vehicle along each polar ray, the rest of
+                              the obstacles become unknown (bev.py:351-375); variant 1 returns TWO
+                              grids per frame, out_dev = (2, B, ...): the encoded grid, then the
+                              polar re-projection of its nearest obstacles (bev.py:143-164)        */
 } bugseg_bev_params;
 
 /* Library version (major*10000 + minor*100 + patch). */
@@ -126,7 +131,8 @@ int bugseg_enet_forward_bgr(bugseg_ctx *ctx, const uint8_t *bgr_dev, int B, int 
 /* Fused BEV rasteriser over a batch of class maps: seg_dev (B, in_rows, in_cols) u8
  * -> out_dev (B, occ_h, occ_w) int8 (or the ROS layout, see ros_layout).
  * Replaces bev_transform_tools.create_occupancy_grid (bev.py:301-381) or, with variant = 1,
- * create_occupancy_grid_binary (bev.py:97-165); non-laserscan branches. */
+ * create_occupancy_grid_binary (bev.py:97-165), either branch (p->laserscan). The laserscan mode
+ * keeps polar tables per geometry and scratch per batch in the context. */
 int bugseg_bev_occgrid(bugseg_ctx *ctx, const uint8_t *seg_dev, int B, const bugseg_bev_params *p,
                        int8_t *out_dev, void *stream);
 

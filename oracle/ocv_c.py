@@ -29,8 +29,13 @@ def lib():
         L.ocv_resize_linear_u8.argtypes = [u8p, i, i, i, u8p, i, i]
         L.bev_occgrid_ref.argtypes = [u8p, i, i, dp, i, i, i, i, i, i, i, i, i8p]
         L.bev_occgrid_binary_ref.argtypes = [u8p, i, i, dp, i, i, i, i, i, i, i, i, i8p]
+        L.bev_occgrid_laserscan_ref.argtypes = [u8p, i, i, dp, i, i, i, i, i, i, i, i, i8p]
+        L.bev_occgrid_binary_laserscan_ref.argtypes = [u8p, i, i, dp, i, i, i, i, i, i, i, i, i8p, i8p]
+        L.ocv_fast_atan_rad.argtypes = [ctypes.c_float, ctypes.c_float]
+        L.ocv_fast_atan_rad.restype = ctypes.c_float
         for f in (L.ocv_invert3x3, L.ocv_warp_perspective_u8, L.ocv_resize_nearest_u8, L.ocv_morph_open3x3_u8,
-                  L.ocv_resize_linear_u8, L.bev_occgrid_ref, L.bev_occgrid_binary_ref):
+                  L.ocv_resize_linear_u8, L.bev_occgrid_ref, L.bev_occgrid_binary_ref, L.bev_occgrid_laserscan_ref,
+                  L.bev_occgrid_binary_laserscan_ref):
             f.restype = ctypes.c_int
         _lib = L
     return _lib
@@ -112,6 +117,35 @@ def create_occupancy_grid_binary(segmap, M, after_warp_w, after_warp_h, cm_per_p
     if rc != 0:
         raise MemoryError("bev_occgrid_binary_ref failed")
     return out
+
+
+def create_occupancy_grid_laserscan(segmap, M, after_warp_w, after_warp_h, cm_per_px, grid_w_m, grid_h_m, cell_m):
+    """bev.py:301-381 with is_laserscan (polar branch bev.py:351-375) via the C restatement."""
+    seg = np.ascontiguousarray(segmap, np.uint8)
+    g = occgrid_geometry(after_warp_w, after_warp_h, cm_per_px, grid_w_m, grid_h_m, cell_m)
+    out = np.empty((g["occ_h"], g["occ_w"]), np.int8)
+    rc = lib().bev_occgrid_laserscan_ref(seg, seg.shape[0], seg.shape[1], np.ascontiguousarray(M, np.float64).reshape(9),
+                                         after_warp_w, after_warp_h, g["occ_w_px"], g["occ_h_px"], g["occ_w"], g["occ_h"],
+                                         g["left_x"], g["top_y"], out)
+    if rc != 0:
+        raise MemoryError("bev_occgrid_laserscan_ref failed")
+    return out
+
+
+def create_occupancy_grid_binary_laserscan(segmap, M, after_warp_w, after_warp_h, cm_per_px, grid_w_m, grid_h_m,
+                                           cell_m):
+    """bev.py:97-165 with is_laserscan (bev.py:143-164) via the C restatement -> (grid, new) int8."""
+    seg = np.ascontiguousarray(segmap, np.uint8)
+    g = occgrid_geometry(after_warp_w, after_warp_h, cm_per_px, grid_w_m, grid_h_m, cell_m)
+    out = np.empty((g["occ_h"], g["occ_w"]), np.int8)
+    out2 = np.empty_like(out)
+    rc = lib().bev_occgrid_binary_laserscan_ref(seg, seg.shape[0], seg.shape[1],
+                                                np.ascontiguousarray(M, np.float64).reshape(9), after_warp_w,
+                                                after_warp_h, g["occ_w_px"], g["occ_h_px"], g["occ_w"], g["occ_h"],
+                                                g["left_x"], g["top_y"], out, out2)
+    if rc != 0:
+        raise MemoryError("bev_occgrid_binary_laserscan_ref failed")
+    return out, out2
 
 
 def pipeline(frames_bgr, blocks, M, after_warp_w, after_warp_h, cm_per_px, grid, model_hw, dtype=None):

@@ -224,3 +224,160 @@ def ros_layout(grid: np.ndarray) -> np.ndarray:
     """cv2.flip(g, 0) then cv2.rotate(ROTATE_90_COUNTERCLOCKWISE) (occgrid_to_ros.py:18,21)."""
     flipped = grid[::-1, :]
     return np.ascontiguousarray(np.rot90(flipped, 1))
+
+
+# ---- laserscan-like occupancy (bev.py:351-375, binary variant bev.py:143-164) -----------------------
+
+CV_PI = 3.1415926535897932384626433832795
+_F = np.float32
+_ATAN_P = [_F(c) * _F(180 / CV_PI) for c in (0.9997878412794807, -0.3258083974640975, 0.1555786518463281,
+                                              -0.04432655554792128)]   # p1, p3, p5, p7 (float products)
+
+
+def _fma32(a, b, c):
+    """float32 fused multiply-add (one rounding) via 80-bit long double: a*b of two floats is exact
+    there and the sum rounds once before the float32 rounding."""
+    ld = np.longdouble
+    return (np.asarray(a, ld) * np.asarray(b, ld) + np.asarray(c, ld)).astype(_F)
+
+
+def fast_atan_rad(y: np.ndarray, x: np.ndarray) -> np.ndarray:
+    """cv::hal::fastAtan32f (AVX2 dispatch, v_fma polynomial), angle in radians, float32."""
+    x = np.asarray(x, _F)
+    y = np.asarray(y, _F)
+    ax, ay = np.abs(x), np.abs(y)
+    c = np.minimum(ax, ay) / (np.maximum(ax, ay) + _F(2.220446049250313e-16))
+    cc = c * c
+    p1, p3, p5, p7 = _ATAN_P
+    a = _fma32(_fma32(_fma32(cc, p7, p5), cc, p3), cc, p1) * c
+    a = np.where(ax >= ay, a, _F(90) - a)
+    a = np.where(x < 0, _F(180) - a, a)
+    a = np.where(y < 0, _F(360) - a, a)
+    return (a * _F(CV_PI / 180)).astype(_F)
+
+
+def _remap_nearest(src: np.ndarray, mx: np.ndarray, my: np.ndarray, dst: np.ndarray) -> np.ndarray:
+    """remap(INTER_NEAREST, BORDER_TRANSPARENT) with float maps: coordinates round half-to-even to
+    short; pixels mapping outside src keep dst's value."""
+    sx = np.clip(np.rint(mx), -32768, 32767).astype(np.int64)
+    sy = np.clip(np.rint(my), -32768, 32767).astype(np.int64)
+    ok = (sx >= 0) & (sx < src.shape[1]) & (sy >= 0) & (sy < src.shape[0])
+    dst[ok] = src[sy[ok], sx[ok]]
+    return dst
+
+
+def warp_polar(src: np.ndarray, dsize, center, max_radius: float, inverse: bool = False) -> np.ndarray:
+    """cv2.warpPolar(src, dsize, center, maxRadius, WARP_POLAR_LINEAR [| WARP_INVERSE_MAP]) with
+    INTER_NEAREST and BORDER_TRANSPARENT (imgwarp.cpp 4.x). The destination starts zeroed (the
+    reference's is an uninitialised array: pixels mapping outside the source are unspecified there)."""
+    dw, dh = dsize
+    cx, cy = _F(center[0]), _F(center[1])
+    if not inverse:
+        if dw <= 0 and dh <= 0:
+            dw, dh = int(np.rint(max_radius)), int(np.rint(max_radius * CV_PI))
+        elif dh <= 0:
+            dh = int(np.rint(dw * CV_PI))
+        Kangle = 2 * CV_PI / dh
+        Kmag = max_radius / dw
+        rhos = (np.arange(dw) * Kmag).astype(_F).astype(np.float64)
+        kky = Kangle * np.arange(dh)
+        cp, sp = np.cos(kky)[:, None], np.sin(kky)[:, None]
+        mx = (rhos[None, :] * cp + np.float64(cx)).astype(_F)
+        my = (rhos[None, :] * sp + np.float64(cy)).astype(_F)
+        return _remap_nearest(src, mx, my, np.zeros((dh, dw), src.dtype))
+    ph, pw = src.shape[:2]
+    bordered = np.concatenate([src[-1:], src, src[:1]], 0)      # copyMakeBorder(1, 1, 0, 0, BORDER_WRAP)
+    Kangle = 2 * CV_PI / ph
+    Kmag = max_radius / pw
+    bx = (np.arange(dw, dtype=_F) - cx)[None, :].repeat(dh, 0)
+    by = (np.arange(dh, dtype=_F) - cy)[:, None].repeat(dw, 1)
+    mag = np.sqrt(_fma32(bx, bx, by * by)).astype(_F)           # hal::magnitude32f (v_muladd)
+    ang = fast_atan_rad(by, bx)
+    mx = (mag.astype(np.float64) / Kmag).astype(_F)
+    my = ((ang.astype(np.float64) / Kangle).astype(_F) + _F(1)).astype(_F)
+    return _remap_nearest(bordered, mx, my, np.zeros((dh, dw), src.dtype))
+
+
+def circle_filled_r1(img: np.ndarray, center, color) -> np.ndarray:
+    """cv2.circle(img, center, 1, color, -1): drawing.cpp Circle() with radius 1 fills the plus
+    {(x-1..x+1, y), (x, y-1), (x, y+1)}, clipped to the image."""
+    x, y = int(center[0]), int(center[1])
+    h, w = img.shape[:2]
+    if 0 <= y < h:
+        img[y, max(x - 1, 0):min(x + 1, w - 1) + 1] = color
+    for yy in (y - 1, y + 1):
+        if 0 <= yy < h and 0 <= x < w:
+            img[yy, x] = color
+    return img
+
+
+def _group_min(rows: np.ndarray, cols: np.ndarray):
+    """npi.group_by(rows).min(cols) -> (sorted unique rows, min col per row)."""
+    if rows.size == 0:
+        return rows, cols
+    keys = np.unique(rows)
+    mins = np.full(keys.size, np.iinfo(np.int64).max)
+    np.minimum.at(mins, np.searchsorted(keys, rows), cols)
+    return keys, mins
+
+
+def _template_cells(segmap, M, after_warp_w, after_warp_h, cm_per_px, grid_w_m, grid_h_m, cell_m, binary):
+    """The array flow of bev.py:301-347 (or :97-138 binary) up to the NN resize."""
+    cell_px = cell_m * 100 / cm_per_px
+    occ_w = int(grid_w_m / cell_m)
+    occ_w_px = int(occ_w * cell_px)
+    occ_h = int(grid_h_m / cell_m)
+    occ_h_px = int(occ_h * cell_px)
+    lifted = np.add(segmap, 1).astype(np.uint8)
+    warped = warp_perspective(lifted, M, (after_warp_w, after_warp_h))
+    left_x = int((after_warp_w - occ_w_px) / 2)
+    top_y = after_warp_h - occ_h_px
+    wlx = int(np.clip(left_x, 0, np.inf))
+    warped = warped[int(np.clip(top_y, 0, np.inf)):after_warp_h, wlx:wlx + occ_w_px]
+    glx = int(np.clip(-left_x, 0, np.inf))
+    gty = int(np.clip(-top_y, 0, np.inf))
+    tmpl = np.zeros((occ_h_px, occ_w_px))
+    tmpl[gty:occ_h_px, glx:glx + warped.shape[1]] = warped
+    tmpl = tmpl.astype(np.uint8)
+    occ = ((tmpl == 1) if binary else np.logical_or(tmpl == 1, tmpl == 3)).astype(np.uint8)
+    mask1 = (morph_open3x3(occ) > 0).astype(np.uint8)
+    sub = np.clip(occ.astype(np.int16) - mask1, 0, 255)
+    tmpl = np.where(sub > 0, 2, tmpl).astype(np.uint8)
+    return resize_nearest(tmpl, (occ_w, occ_h))
+
+
+def create_occupancy_grid_laserscan(segmap, M, after_warp_w, after_warp_h, cm_per_px, grid_w_m, grid_h_m, cell_m):
+    """Restates bev.py:301-381 with is_laserscan (the polar branch, bev.py:351-375)."""
+    t = _template_cells(segmap, M, after_warp_w, after_warp_h, cm_per_px, grid_w_m, grid_h_m, cell_m, False)
+    shape = (t.shape[1], t.shape[0])                                                # bev.py:353
+    longer = max(shape[0], shape[1])                                                # bev.py:354
+    center = (shape[0] / 2 - 1, shape[1])
+    polar = warp_polar(t, (-1, -1), center, longer)                                 # bev.py:355
+    empty = np.zeros(polar.shape)                                                   # bev.py:360
+    pts = np.where(polar == 3)                                                      # bev.py:363
+    keys, mins = _group_min(pts[0], pts[1])                                         # bev.py:364-365
+    for i, mx in enumerate(mins):                                                   # bev.py:368-369
+        empty = circle_filled_r1(empty, (mx, keys[i]), 1)
+    new = warp_polar(empty, shape, center, longer, inverse=True)                    # bev.py:371
+    new = np.where(t != 3, t, new)                                                  # bev.py:372
+    return np.where(new == 0, -1, 200 - new * 100).astype(np.int8)                  # bev.py:379
+
+
+def create_occupancy_grid_binary_laserscan(segmap, M, after_warp_w, after_warp_h, cm_per_px, grid_w_m, grid_h_m,
+                                           cell_m):
+    """Restates bev.py:97-165 with is_laserscan (bev.py:143-164) -> (grid int8, new int8)."""
+    t = _template_cells(segmap, M, after_warp_w, after_warp_h, cm_per_px, grid_w_m, grid_h_m, cell_m, True)
+    og = (t.astype(np.int64) * 100) % 256                                           # bev.py:135-138 (uint8)
+    og = ((np.where(og == 0, -1, (200 - og) % 256)) % 256).astype(np.uint8)          # bev.py:139-140
+    shape = (og.shape[1], og.shape[0])                                              # bev.py:144
+    longer = max(shape[0], shape[1])                                                # bev.py:145
+    center = (og.shape[1] / 2 - 1, og.shape[0])
+    polar = warp_polar(og, shape, center, longer)                                   # bev.py:146
+    empty = np.zeros(polar.shape)                                                   # bev.py:150
+    vc = np.where(polar == 100)                                                     # bev.py:152
+    keys, mins = _group_min(vc[0], vc[1])                                           # bev.py:153-154
+    for i, mx in enumerate(mins):                                                   # bev.py:155-156
+        empty = circle_filled_r1(empty, (mx, keys[i]), 100)
+    new = warp_polar(empty, shape, center, longer, inverse=True).astype(np.int8)   # bev.py:158-159
+    new[og == 255] = -1                                                             # bev.py:161
+    return og.astype(np.int8), new                                                  # bev.py:162

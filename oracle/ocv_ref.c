@@ -244,37 +244,50 @@ int ocv_resize_linear_u8(const uint8_t *src, int sh, int sw, int cn, uint8_t *ds
  *   g = where(g==3, 1, g); out = where(g==0, -1, 200-100*g) as int8    bev.py:377-380
  * The crop/pad of bev.py:318-330 is restated as the equivalent coordinate shift.
  * segmap is (hin, win) u8 class ids {0,1,2}; M is the forward bev matrix. */
-int bev_occgrid_ref(const uint8_t *segmap, int hin, int win, const double *M, int Wb, int Hb,
-                    int occ_w_px, int occ_h_px, int occ_w, int occ_h, int left_x, int top_y, int8_t *out)
+/* The template cells both rasterisers share: warp + crop/pad + opening + NN resize, before the
+ * encoding. binary = 0: occupied set {1, 3} (bev.py:331-340); 1: {1} (bev.py:126). */
+int bev_template_cells_ref(const uint8_t *segmap, int hin, int win, const double *M, int Wb, int Hb,
+                           int occ_w_px, int occ_h_px, int occ_w, int occ_h, int left_x, int top_y, int binary,
+                           uint8_t *cells)
 {
     size_t n = (size_t)hin * win;
     uint8_t *lifted = (uint8_t *)malloc(n);
     uint8_t *tmpl = (uint8_t *)malloc((size_t)occ_h_px * occ_w_px);
     uint8_t *occ = (uint8_t *)malloc((size_t)occ_h_px * occ_w_px);
     uint8_t *opened = (uint8_t *)malloc((size_t)occ_h_px * occ_w_px);
-    uint8_t *cells = (uint8_t *)malloc((size_t)occ_h * occ_w);
-    if (!lifted || !tmpl || !occ || !opened || !cells) return -1;
-    for (size_t i = 0; i < n; i++) lifted[i] = (uint8_t)(segmap[i] + 1);
+    if (!lifted || !tmpl || !occ || !opened) return -1;
+    for (size_t i = 0; i < n; i++) lifted[i] = (uint8_t)(segmap[i] + 1);                      /* bev.py:312 / :107 */
     double Mi[9];
     ocv_invert3x3(M, Mi);
     int bw0 = warp_bw0(Hb, Wb);
     for (int ty = 0; ty < occ_h_px; ty++)
         for (int tx = 0; tx < occ_w_px; tx++) {
-            int wy = ty + top_y, wx = tx + left_x;
+            int wy = ty + top_y, wx = tx + left_x;                                                /* bev.py:318-330 */
             uint8_t v = 0;
             if (wy >= 0 && wy < Hb && wx >= 0 && wx < Wb) v = warp_px(lifted, hin, win, Mi, wx, wy, bw0);
             tmpl[(size_t)ty * occ_w_px + tx] = v;
-            occ[(size_t)ty * occ_w_px + tx] = (uint8_t)(v == 1 || v == 3);
+            occ[(size_t)ty * occ_w_px + tx] = (uint8_t)(binary ? v == 1 : (v == 1 || v == 3));
         }
-    ocv_morph_open3x3_u8(occ, occ_h_px, occ_w_px, opened);
+    ocv_morph_open3x3_u8(occ, occ_h_px, occ_w_px, opened);                                        /* bev.py:335 / :128 */
     for (size_t i = 0; i < (size_t)occ_h_px * occ_w_px; i++)
         if (occ[i] && !opened[i]) tmpl[i] = 2;
-    ocv_resize_nearest_u8(tmpl, occ_h_px, occ_w_px, 1, cells, occ_h, occ_w);
+    ocv_resize_nearest_u8(tmpl, occ_h_px, occ_w_px, 1, cells, occ_h, occ_w);                      /* bev.py:344 / :135 */
+    free(lifted); free(tmpl); free(occ); free(opened);
+    return 0;
+}
+
+int bev_occgrid_ref(const uint8_t *segmap, int hin, int win, const double *M, int Wb, int Hb,
+                    int occ_w_px, int occ_h_px, int occ_w, int occ_h, int left_x, int top_y, int8_t *out)
+{
+    uint8_t *cells = (uint8_t *)malloc((size_t)occ_h * occ_w);
+    if (!cells) return -1;
+    if (bev_template_cells_ref(segmap, hin, win, M, Wb, Hb, occ_w_px, occ_h_px, occ_w, occ_h, left_x, top_y, 0, cells))
+        return -1;
     for (size_t i = 0; i < (size_t)occ_h * occ_w; i++) {
-        int g = cells[i] == 3 ? 1 : cells[i];
+        int g = cells[i] == 3 ? 1 : cells[i];                                                     /* bev.py:377-380 */
         out[i] = (int8_t)(g == 0 ? -1 : 200 - 100 * g);
     }
-    free(lifted); free(tmpl); free(occ); free(opened); free(cells);
+    free(cells);
     return 0;
 }
 
@@ -286,34 +299,167 @@ int bev_occgrid_ref(const uint8_t *segmap, int hin, int win, const double *M, in
 int bev_occgrid_binary_ref(const uint8_t *segmap, int hin, int win, const double *M, int Wb, int Hb,
                            int occ_w_px, int occ_h_px, int occ_w, int occ_h, int left_x, int top_y, int8_t *out)
 {
-    size_t n = (size_t)hin * win;
-    uint8_t *lifted = (uint8_t *)malloc(n);
-    uint8_t *tmpl = (uint8_t *)malloc((size_t)occ_h_px * occ_w_px);
-    uint8_t *occ = (uint8_t *)malloc((size_t)occ_h_px * occ_w_px);
-    uint8_t *opened = (uint8_t *)malloc((size_t)occ_h_px * occ_w_px);
     uint8_t *cells = (uint8_t *)malloc((size_t)occ_h * occ_w);
-    if (!lifted || !tmpl || !occ || !opened || !cells) return -1;
-    for (size_t i = 0; i < n; i++) lifted[i] = (uint8_t)(segmap[i] + 1);                      /* bev.py:107 */
-    double Mi[9];
-    ocv_invert3x3(M, Mi);
-    int bw0 = warp_bw0(Hb, Wb);
-    for (int ty = 0; ty < occ_h_px; ty++)
-        for (int tx = 0; tx < occ_w_px; tx++) {
-            int wy = ty + top_y, wx = tx + left_x;                                                /* bev.py:114-125 */
-            uint8_t v = 0;
-            if (wy >= 0 && wy < Hb && wx >= 0 && wx < Wb) v = warp_px(lifted, hin, win, Mi, wx, wy, bw0);
-            tmpl[(size_t)ty * occ_w_px + tx] = v;
-            occ[(size_t)ty * occ_w_px + tx] = (uint8_t)(v == 1);                                  /* bev.py:126 */
-        }
-    ocv_morph_open3x3_u8(occ, occ_h_px, occ_w_px, opened);                                        /* bev.py:128-129 */
-    for (size_t i = 0; i < (size_t)occ_h_px * occ_w_px; i++)
-        if (occ[i] && !opened[i]) tmpl[i] = 2;                                                    /* bev.py:131-133 */
-    ocv_resize_nearest_u8(tmpl, occ_h_px, occ_w_px, 1, cells, occ_h, occ_w);                      /* bev.py:135-138 */
+    if (!cells) return -1;
+    if (bev_template_cells_ref(segmap, hin, win, M, Wb, Hb, occ_w_px, occ_h_px, occ_w, occ_h, left_x, top_y, 1, cells))
+        return -1;
     for (size_t i = 0; i < (size_t)occ_h * occ_w; i++) {
         uint8_t g = (uint8_t)(cells[i] * 100);
         int r = g == 0 ? -1 : (int)(uint8_t)(200 - g);
         out[i] = (int8_t)(uint8_t)r;
     }
-    free(lifted); free(tmpl); free(occ); free(opened); free(cells);
+    free(cells);
+    return 0;
+}
+
+/* ---- laserscan-like occupancy (bev.py:351-375; binary variant bev.py:143-164) -------------------
+ *
+ * cv::warpPolar(WARP_POLAR_LINEAR, INTER_NEAREST, no WARP_FILL_OUTLIERS -> BORDER_TRANSPARENT) as
+ * imgwarp.cpp (4.x) builds it: float remap tables, then remap() with INTER_NEAREST, which rounds
+ * each float coordinate half-to-even to a short (v_round / saturate_cast<short>) and leaves a
+ * destination pixel UNTOUCHED when it maps outside the source. The reference's destinations are
+ * fresh, uninitialised NumPy arrays, so those pixels are unspecified there; this restatement (and
+ * the kernel) writes 0 — what fresh zeroed pages give. */
+
+#define CV_PI 3.1415926535897932384626433832795
+
+/* cv::hal::fastAtan32f (mathfuncs_core.simd.hpp, the AVX2 dispatch: v_fma polynomial), radians */
+static const float ATAN_P1 = 0.9997878412794807f * (float)(180 / CV_PI);
+static const float ATAN_P3 = -0.3258083974640975f * (float)(180 / CV_PI);
+static const float ATAN_P5 = 0.1555786518463281f * (float)(180 / CV_PI);
+static const float ATAN_P7 = -0.04432655554792128f * (float)(180 / CV_PI);
+
+float ocv_fast_atan_rad(float y, float x)
+{
+    float ax = fabsf(x), ay = fabsf(y);
+    float c = (ax < ay ? ax : ay) / ((ax > ay ? ax : ay) + (float)2.220446049250313e-16);
+    float cc = c * c;
+    float a = fmaf(fmaf(fmaf(cc, ATAN_P7, ATAN_P5), cc, ATAN_P3), cc, ATAN_P1) * c;
+    if (!(ax >= ay)) a = 90.f - a;
+    if (x < 0) a = 180.f - a;
+    if (y < 0) a = 360.f - a;
+    return a * (float)(CV_PI / 180);
+}
+
+static inline int round_short(float v) { return sat_short((int)lrintf(v)); }
+
+/* Forward polar table of warpPolar(src (sw x sh), dsize (pw x ph), center, maxRadius):
+ * fmap[phi*pw + rho] = sx | sy << 16 (source pixel), or -1 outside the source. */
+void ocv_polar_forward_map(int pw, int ph, double max_radius, float cx, float cy, int sw, int sh, int32_t *fmap)
+{
+    double Kangle = 2 * CV_PI / ph, Kmag = max_radius / pw;
+    for (int phi = 0; phi < ph; phi++) {
+        double KKy = Kangle * phi, cp = cos(KKy), sp = sin(KKy);
+        for (int rho = 0; rho < pw; rho++) {
+            float r = (float)(rho * Kmag);
+            float mx = (float)(r * cp + cx), my = (float)(r * sp + cy);
+            int sx = round_short(mx), sy = round_short(my);
+            fmap[(size_t)phi * pw + rho] = ((unsigned)sx < (unsigned)sw && (unsigned)sy < (unsigned)sh) ? (sx | (sy << 16)) : -1;
+        }
+    }
+}
+
+/* Inverse table of warpPolar(polar (pw x ph), dsize (dw x dh), center, maxRadius, WARP_INVERSE_MAP):
+ * the source is the polar image with one BORDER_WRAP row above and below; imap[y*dw + x] =
+ * rho | row << 16 (row already unwrapped into 0..ph-1), or -1 when rho falls outside. */
+void ocv_polar_inverse_map(int pw, int ph, double max_radius, float cx, float cy, int dw, int dh, int32_t *imap)
+{
+    double Kangle = 2 * CV_PI / ph, Kmag = max_radius / pw;
+    for (int y = 0; y < dh; y++)
+        for (int x = 0; x < dw; x++) {
+            float bx = (float)x - cx, by = (float)y - cy;
+            float mag = sqrtf(fmaf(bx, bx, by * by));        /* hal::magnitude32f (v_muladd) */
+            float ang = ocv_fast_atan_rad(by, bx);
+            double rho = mag / Kmag, phi = ang / Kangle;
+            float mx = (float)rho, my = (float)phi + 1;       /* ANGLE_BORDER = 1 */
+            int X = round_short(mx), Y = round_short(my);
+            int32_t v = -1;
+            if ((unsigned)X < (unsigned)pw && (unsigned)Y < (unsigned)(ph + 2)) {
+                int row = Y == 0 ? ph - 1 : (Y == ph + 1 ? 0 : Y - 1);
+                v = X | (row << 16);
+            }
+            imap[(size_t)y * dw + x] = v;
+        }
+}
+
+/* The laserscan step on a (h x w) grid `g`: polar-warp it (fmap), take per polar row the smallest
+ * rho whose value is `hit` (npi.group_by(rows).min(cols)), stamp a radius-1 filled cv2.circle there
+ * (Circle(): the plus {(r-1..r+1, phi), (r, phi-1), (r, phi+1)}, clipped, no angular wrap), and
+ * sample the stamps back per grid pixel (imap) -> s[y*w+x] in {0, 1}. */
+static int polar_stamps(const uint8_t *g, int w, int h, int pw, int ph, const int32_t *fmap, const int32_t *imap,
+                        uint8_t hit, uint8_t *s)
+{
+    int *rmin = (int *)malloc(sizeof(int) * ph);
+    uint8_t *stamp = (uint8_t *)calloc((size_t)ph * pw, 1);
+    if (!rmin || !stamp) return -1;
+    for (int phi = 0; phi < ph; phi++) {
+        rmin[phi] = -1;
+        for (int rho = 0; rho < pw; rho++) {
+            int32_t m = fmap[(size_t)phi * pw + rho];
+            uint8_t v = m < 0 ? 0 : g[(size_t)(m >> 16) * w + (m & 0xffff)];
+            if (v == hit) { rmin[phi] = rho; break; }
+        }
+    }
+    for (int phi = 0; phi < ph; phi++) {
+        int r = rmin[phi];
+        if (r < 0) continue;
+        for (int c = imax(r - 1, 0); c <= imin(r + 1, pw - 1); c++) stamp[(size_t)phi * pw + c] = 1;
+        if (phi > 0) stamp[(size_t)(phi - 1) * pw + r] = 1;
+        if (phi + 1 < ph) stamp[(size_t)(phi + 1) * pw + r] = 1;
+    }
+    for (size_t i = 0; i < (size_t)w * h; i++) {
+        int32_t m = imap[i];
+        s[i] = m < 0 ? 0 : stamp[(size_t)(m >> 16) * pw + (m & 0xffff)];
+    }
+    free(rmin); free(stamp);
+    return 0;
+}
+
+/* create_occupancy_grid with is_laserscan (bev.py:301-381): the template cells of bev_occgrid_ref,
+ * then warpPolar(cells, (-1,-1), (w/2-1, h), L = max(w, h)) -> (round(L), round(L*pi)) polar image;
+ * obstacle value 3; new = cells != 3 ? cells : stamp; out = new == 0 ? -1 : 200 - 100*new. */
+int bev_occgrid_laserscan_ref(const uint8_t *segmap, int hin, int win, const double *M, int Wb, int Hb,
+                              int occ_w_px, int occ_h_px, int occ_w, int occ_h, int left_x, int top_y, int8_t *out)
+{
+    size_t n = (size_t)occ_h * occ_w;
+    uint8_t *cells = (uint8_t *)malloc(n), *s = (uint8_t *)malloc(n);
+    int L = occ_w > occ_h ? occ_w : occ_h;
+    int pw = cv_round((double)L), ph = cv_round((double)L * CV_PI);
+    int32_t *fmap = (int32_t *)malloc(sizeof(int32_t) * (size_t)pw * ph), *imap = (int32_t *)malloc(sizeof(int32_t) * n);
+    if (!cells || !s || !fmap || !imap) return -1;
+    bev_template_cells_ref(segmap, hin, win, M, Wb, Hb, occ_w_px, occ_h_px, occ_w, occ_h, left_x, top_y, 0, cells);
+    float cx = (float)(occ_w / 2.0 - 1), cy = (float)occ_h;
+    ocv_polar_forward_map(pw, ph, (double)L, cx, cy, occ_w, occ_h, fmap);
+    ocv_polar_inverse_map(pw, ph, (double)L, cx, cy, occ_w, occ_h, imap);
+    if (polar_stamps(cells, occ_w, occ_h, pw, ph, fmap, imap, 3, s)) return -1;
+    for (size_t i = 0; i < n; i++) {
+        int g = cells[i] != 3 ? cells[i] : s[i];
+        out[i] = (int8_t)(g == 0 ? -1 : 200 - 100 * g);
+    }
+    free(cells); free(s); free(fmap); free(imap);
+    return 0;
+}
+
+/* create_occupancy_grid_binary with is_laserscan (bev.py:143-164): the encoded binary grid G (as
+ * bev_occgrid_binary_ref, kept as uint8: 255 = -1), warpPolar(G, (w, h), (w/2-1, h), L) — an
+ * explicit dsize, so the polar image is w x h; obstacle value 100; stamps of 100 sampled back;
+ * new = int8(stamp * 100), -1 where G == 255. Returns G in out and new in out2. */
+int bev_occgrid_binary_laserscan_ref(const uint8_t *segmap, int hin, int win, const double *M, int Wb, int Hb,
+                                     int occ_w_px, int occ_h_px, int occ_w, int occ_h, int left_x, int top_y,
+                                     int8_t *out, int8_t *out2)
+{
+    size_t n = (size_t)occ_h * occ_w;
+    uint8_t *s = (uint8_t *)malloc(n);
+    int L = occ_w > occ_h ? occ_w : occ_h;
+    int pw = occ_w, ph = occ_h;
+    int32_t *fmap = (int32_t *)malloc(sizeof(int32_t) * (size_t)pw * ph), *imap = (int32_t *)malloc(sizeof(int32_t) * n);
+    if (!s || !fmap || !imap) return -1;
+    if (bev_occgrid_binary_ref(segmap, hin, win, M, Wb, Hb, occ_w_px, occ_h_px, occ_w, occ_h, left_x, top_y, out)) return -1;
+    float cx = (float)(occ_w / 2.0 - 1), cy = (float)occ_h;
+    ocv_polar_forward_map(pw, ph, (double)L, cx, cy, occ_w, occ_h, fmap);
+    ocv_polar_inverse_map(pw, ph, (double)L, cx, cy, occ_w, occ_h, imap);
+    if (polar_stamps((const uint8_t *)out, occ_w, occ_h, pw, ph, fmap, imap, 100, s)) return -1;
+    for (size_t i = 0; i < n; i++) out2[i] = (uint8_t)out[i] == 255 ? -1 : (int8_t)(s[i] * 100);
+    free(s); free(fmap); free(imap);
     return 0;
 }

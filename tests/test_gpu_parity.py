@@ -166,6 +166,45 @@ def test_bev_occgrid_binary_bit_exact(gpu, rows, cols, ww, wh, grid, seed):
     assert one.dtype == np.int8 and np.array_equal(one, ref[0])
 
 
+@pytest.mark.parametrize("rows,cols,ww,wh,grid,seed", [
+    (480, 640, 1000, 1000, (10.0, 10.0, 0.05), 6),
+    (120, 160, 300, 260, (3.0, 2.0, 0.05), 7),       # wide grid: the polar radius follows the width
+    (96, 128, 250, 180, (3.1, 2.7, 0.07), 8),        # odd grid width: half-pixel polar centre
+    (64, 80, 200, 150, (1.0, 1.6, 0.1), 9),          # tall grid
+])
+def test_bev_laserscan_bit_exact(gpu, rows, cols, ww, wh, grid, seed):
+    """Laserscan-like mode (bev.py:351-375; binary variant bev.py:143-164) vs the C restatement: the
+    per-ray nearest obstacle, the stamped pluses and the re-projection, batched, in both layouts."""
+    bev = _bev_case(rows, cols, ww, wh, seed)
+    bev.laserscan_like_occupancy_grid = True
+    rng = np.random.default_rng(seed)
+    blocky = np.kron(rng.integers(0, 3, size=(rows // 8, cols // 8)), np.ones((8, 8), np.int64)).astype(np.uint8)
+    sparse = np.ones((rows, cols), np.uint8)
+    sparse[rng.random((rows, cols)) < 0.05] = 2
+    none = np.ones((rows, cols), np.uint8)           # no obstacle on any ray
+    segs = np.stack([blocky, sparse, none, rng.integers(0, 3, size=(rows, cols)).astype(np.uint8)])
+    M = bev._bev_matrix
+    ref = np.stack([ocv_c.create_occupancy_grid_laserscan(s, M, ww, wh, 1.0, *grid) for s in segs])
+    dev = torch.from_numpy(segs).cuda()
+    got = bev.create_occupancy_grid_device(dev, *grid).cpu().numpy()
+    assert np.array_equal(got, ref)
+    ros = bev.create_occupancy_grid_device(dev, *grid, ros_layout=True).cpu().numpy()
+    assert np.array_equal(ros, np.stack([ocv_np.ros_layout(r) for r in ref]))
+    assert np.array_equal(bev.create_occupancy_grid(blocky, *grid), ref[0])
+    # binary variant: the reference's returned pair
+    bref = [ocv_c.create_occupancy_grid_binary_laserscan(s, M, ww, wh, 1.0, *grid) for s in segs]
+    bgot = bev.create_occupancy_grid_device(dev, *grid, binary=True).cpu().numpy()
+    assert bgot.shape[0] == 2
+    assert np.array_equal(bgot[0], np.stack([r[0] for r in bref]))
+    assert np.array_equal(bgot[1], np.stack([r[1] for r in bref]))
+    g, n = bev.create_occupancy_grid_binary(segs[1], *grid)
+    assert np.array_equal(g, bref[1][0]) and np.array_equal(n, bref[1][1])
+    # a non-laserscan call on the same context after the laserscan ones is unaffected
+    bev.laserscan_like_occupancy_grid = False
+    assert np.array_equal(bev.create_occupancy_grid(blocky, *grid),
+                          ocv_c.create_occupancy_grid(blocky, M, ww, wh, 1.0, *grid))
+
+
 @pytest.mark.parametrize("prec", ["fp32", "bf16"])
 @pytest.mark.parametrize("pool_k", [3, 2])
 def test_forward_bgr_equals_preprocess_then_forward(gpu, prec, pool_k):

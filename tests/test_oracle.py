@@ -150,6 +150,82 @@ def test_occupancy_grid_binary_c_vs_reference_flow(ww, wh, grid, classes):
         assert (a == -100).any()
 
 
+# ---------------------------------------------------------------- laserscan-like mode (bev.py:351-375)
+def test_fast_atan_matches_opencv_accuracy_and_quadrants():
+    """fastAtan32f: within OpenCV's documented ~0.3 degree of atan2, angles in [0, 2pi), C == NumPy."""
+    rng = np.random.default_rng(5)
+    x = (rng.integers(-400, 400, 20000) + rng.choice([0.0, 0.5], 20000)).astype(np.float32)
+    y = rng.integers(-400, 400, 20000).astype(np.float32)
+    a = ocv_np.fast_atan_rad(y, x)
+    ref = np.mod(np.arctan2(y.astype(np.float64), x), 2 * np.pi)
+    d = np.abs(a - ref)
+    d = np.minimum(d, 2 * np.pi - d)
+    assert d.max() < np.deg2rad(0.3) and (a >= 0).all() and (a <= np.float32(2 * np.pi)).all()
+    lib = ocv_c.lib()
+    c = np.array([lib.ocv_fast_atan_rad(float(yy), float(xx)) for xx, yy in zip(x[:3000], y[:3000])], np.float32)
+    assert np.array_equal(c, a[:3000])
+    assert ocv_np.fast_atan_rad(np.float32(0), np.float32(0)) == 0
+
+
+def test_warp_polar_sizes_and_inverse_round_trip():
+    """warpPolar(-1,-1) sizes (round(R), round(R*pi)); an inverse warp of a forward warp returns the
+    source on the pixels both maps reach (nearest sampling)."""
+    g = np.zeros((40, 50), np.uint8)
+    g[5:35, 10:40] = np.arange(30)[:, None].astype(np.uint8) + 1
+    p = ocv_np.warp_polar(g, (-1, -1), (50 / 2 - 1, 40), 50)
+    assert p.shape == (int(np.rint(50 * np.pi)), 50)
+    back = ocv_np.warp_polar(p, (50, 40), (50 / 2 - 1, 40), 50, inverse=True)
+    near = (back == g)
+    assert near[30:, 15:35].mean() > 0.9      # close to the pole the polar grid oversamples
+
+
+def test_laserscan_known_answer_shadow():
+    """A wall of obstacles straight ahead: the cells of the wall nearest the vehicle stay occupied,
+    obstacle cells behind them (farther along the same rays) become unknown (-1), free cells stay 0."""
+    H, W = 120, 160
+    bev = synthetic.synthetic_bev(H, W, 300, 300)
+    seg = np.ones((H, W), np.uint8)              # class 1 -> lifted 2 -> free
+    seg[80:110, 50:110] = 2                      # class 2 -> lifted 3 -> non-flat obstacle (in the grid)
+    grid = (3.0, 3.0, 0.05)
+    std = ocv_c.create_occupancy_grid(seg, bev._bev_matrix, 300, 300, 1.0, *grid)
+    ls = ocv_c.create_occupancy_grid_laserscan(seg, bev._bev_matrix, 300, 300, 1.0, *grid)
+    assert np.array_equal(ls, ocv_np.create_occupancy_grid_laserscan(seg, bev._bev_matrix, 300, 300, 1.0, *grid))
+    occ = std == 100
+    assert occ.any()
+    assert ((ls == 100) <= occ).all()                      # only obstacles can stay occupied
+    assert (ls[std == 0] == 0).all()                       # free cells untouched
+    hidden = occ & (ls == -1)
+    assert hidden.any() and (ls[occ] == 100).any()
+    # along each grid column through the wall, occupied cells are nearer (larger row) than hidden ones
+    for c in np.nonzero(occ.any(0) & hidden.any(0))[0]:
+        rows_occ, rows_hid = np.nonzero(ls[:, c] == 100)[0], np.nonzero(hidden[:, c])[0]
+        if rows_occ.size and rows_hid.size:
+            assert rows_occ.max() > rows_hid.min()
+
+
+@pytest.mark.parametrize("ww,wh,grid", [(1000, 1000, (10, 10, 0.05)), (900, 700, (10, 8, 0.05)),
+                                        (600, 1100, (7.3, 12.1, 0.07)), (400, 300, (12, 12, 0.05))])
+def test_laserscan_c_vs_reference_flow(ww, wh, grid):
+    """bev.py:351-375 (and the binary variant bev.py:143-164): the C restatement (precomputed polar
+    tables, per-row minimum, stamped pluses) vs the NumPy restatement of the reference's array flow
+    (warpPolar images, np.where, group-by-min, cv2.circle, inverse warpPolar)."""
+    rng = np.random.default_rng(ww + wh)
+    seg = np.kron(rng.integers(0, 3, size=(60, 80)), np.ones((8, 8), np.int64)).astype(np.uint8)
+    seg[rng.random(seg.shape) < 0.02] = 2
+    M = synthetic.synthetic_bev(480, 640, ww, wh)._bev_matrix
+    a = ocv_c.create_occupancy_grid_laserscan(seg, M, ww, wh, 1.0, *grid)
+    b = ocv_np.create_occupancy_grid_laserscan(seg, M, ww, wh, 1.0, *grid)
+    assert np.array_equal(a, b)
+    assert set(np.unique(a)) <= {-1, 0, 100}
+    std = ocv_c.create_occupancy_grid(seg, M, ww, wh, 1.0, *grid)
+    assert (a[std == 0] == 0).all() and (a[std == -1] == -1).all()
+    g1, n1 = ocv_c.create_occupancy_grid_binary_laserscan(seg, M, ww, wh, 1.0, *grid)
+    g2, n2 = ocv_np.create_occupancy_grid_binary_laserscan(seg, M, ww, wh, 1.0, *grid)
+    assert np.array_equal(g1, g2) and np.array_equal(n1, n2)
+    assert np.array_equal(g1, ocv_c.create_occupancy_grid_binary(seg, M, ww, wh, 1.0, *grid))
+    assert set(np.unique(n1)) <= {-1, 0, 100}
+
+
 def test_oracle_fp32_vs_fp64(blocks):
     x = np.random.default_rng(5).normal(size=(1, 3, 32, 48)).astype(np.float32)
     a = eo.forward(blocks, x, torch.float32)
