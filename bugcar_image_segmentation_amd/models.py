@@ -47,6 +47,8 @@ def _as_device_tensor(x, dtype=None) -> torch.Tensor:
 
 
 def _load_blob(path: str) -> bytes:
+    """Weight file -> BSG1 blob: a BSG1 file as is, or a frozen TF GraphDef (the reference's enet.pb,
+    models.py:25-30) through the importer (graphdef.py), which checks it is the canonical ENet."""
     if not os.path.exists(path):
         # TF's GFile raises NotFoundError here (models.py:25); FileNotFoundError is its Python twin
         raise FileNotFoundError(f"{path}: no such file")
@@ -54,9 +56,8 @@ def _load_blob(path: str) -> bytes:
         data = f.read()
     if data[:4] == b"BSG1":
         return data
-    raise NotImplementedError(
-        f"{path} is not a BSG1 weight blob. Frozen TF GraphDef import (enet.pb) is the next row of the "
-        "build (SURVEY.md §8(f) 1); convert the graph's Const tensors with enet_spec.serialize meanwhile.")
+    from . import graphdef
+    return graphdef.graphdef_to_blob(data, input_name=ENET.INPUT_TENSOR_NAME.split(":")[0])
 
 
 class ENET(InferenceModel):

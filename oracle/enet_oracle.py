@@ -34,6 +34,21 @@ def _t(a, dtype):
     return torch.as_tensor(np.asarray(a), dtype=dtype)
 
 
+def _bn(y, mean, var, gamma, beta, eps, dtype):
+    """Inference batch norm; eps == 0 (units imported with BN already reduced to an affine, or
+    without BN) is evaluated directly (F.batch_norm requires eps > 0)."""
+    if float(eps) > 0:
+        return F.batch_norm(y, _t(mean, dtype), _t(var, dtype), _t(gamma, dtype), _t(beta, dtype),
+                            training=False, eps=float(eps))
+    v = lambda a: _t(a, dtype).view(1, -1, 1, 1)  # noqa: E731
+    return (y - v(mean)) / torch.sqrt(v(var)) * v(gamma) + v(beta)
+
+
+def _identity_bn(u) -> bool:
+    return (np.all(np.asarray(u.gamma) == 1) and not np.any(u.beta) and not np.any(u.mean)
+            and np.all(np.asarray(u.var) == 1))
+
+
 def _unit(x, u, dtype, act=True):
     w = _t(u.w, dtype)
     if u.kind == 0:
@@ -42,8 +57,7 @@ def _unit(x, u, dtype, act=True):
     else:
         y = F.conv_transpose2d(x, w, _t(u.b, dtype), stride=u.stride, padding=(u.pad_h, u.pad_w),
                                output_padding=u.out_pad)
-    y = F.batch_norm(y, _t(u.mean, dtype), _t(u.var, dtype), _t(u.gamma, dtype), _t(u.beta, dtype),
-                     training=False, eps=float(u.eps))
+    y = _bn(y, u.mean, u.var, u.gamma, u.beta, u.eps, dtype)
     if act:
         y = _prelu(y, u.slope, dtype)
     return y
@@ -67,11 +81,15 @@ def forward(blocks, x: np.ndarray, dtype=torch.float32) -> np.ndarray:
                 ext = F.max_pool2d(h, k, stride=2, padding=(k - 1) // 2)
                 y = torch.cat([main, ext], 1)
                 e = b.extra
-                mean = torch.cat([_t(u.mean, dtype), _t(e["pool_mean"], dtype)])
-                var = torch.cat([_t(u.var, dtype), _t(e["pool_var"], dtype)])
-                gamma = torch.cat([_t(u.gamma, dtype), _t(e["pool_gamma"], dtype)])
-                beta = torch.cat([_t(u.beta, dtype), _t(e["pool_beta"], dtype)])
-                y = F.batch_norm(y, mean, var, gamma, beta, training=False, eps=float(u.eps))
+                if float(u.eps) == float(e["pool_eps"][0]):
+                    y = _bn(y, np.concatenate([u.mean, e["pool_mean"]]), np.concatenate([u.var, e["pool_var"]]),
+                            np.concatenate([u.gamma, e["pool_gamma"]]), np.concatenate([u.beta, e["pool_beta"]]),
+                            u.eps, dtype)
+                else:
+                    c = u.cout
+                    y = torch.cat([_bn(y[:, :c], u.mean, u.var, u.gamma, u.beta, u.eps, dtype),
+                                   _bn(y[:, c:], e["pool_mean"], e["pool_var"], e["pool_gamma"], e["pool_beta"],
+                                       e["pool_eps"][0], dtype)], 1)
                 h = _prelu(y, np.concatenate([u.slope, e["pool_slope"]]), dtype)
             elif b.type == "down":
                 main, idx = F.max_pool2d(h, 2, stride=2, return_indices=True)
@@ -99,6 +117,8 @@ def forward(blocks, x: np.ndarray, dtype=torch.float32) -> np.ndarray:
                 u = b.units[0]
                 h = F.conv_transpose2d(h, _t(u.w, dtype), _t(u.b, dtype), stride=2,
                                        padding=(u.pad_h, u.pad_w), output_padding=u.out_pad)
+                if not _identity_bn(u):       # the engine folds a classifier BN like any other
+                    h = _bn(h, u.mean, u.var, u.gamma, u.beta, u.eps, dtype)
         return h.numpy()
 
 

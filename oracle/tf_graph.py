@@ -1,0 +1,172 @@
+"""ORACLE — TEST INFRASTRUCTURE ONLY. A NumPy / PyTorch-CPU interpreter of frozen TensorFlow
+GraphDefs: the stand-in for the reference's ``sess.run(OUTPUT_TENSOR_NAME, feed_dict=...)``
+(models.py:43-44) where TensorFlow is absent.
+
+It evaluates the ops an ENet export uses (convolutions, transposed convolutions, pooling with
+argmax, scatter, padding, slicing, concatenation, batch norm and the elementwise ops) with TF's
+semantics — NHWC / NCHW data formats, SAME / VALID / EXPLICIT padding (SAME splits the padding
+total as floor before / ceil after), Conv2DBackpropInput cropping its full output at the forward
+convolution's leading pad, MaxPoolWithArgmax flat indices ((y * W + x) * C + c) — in float64.
+
+Parity status: UNPINNED (no TensorFlow here to check the op semantics against; they are restated
+from the TF op definitions). Used to check that the GraphDef importer
+(bugcar_image_segmentation_amd/graphdef.py) plus the engine reproduce the graph: on the real
+enet.pb, `run(pb, x)` vs the engine's logits is the TF-parity check of the north star.
+"""
+from __future__ import annotations
+
+import numpy as np
+import torch
+import torch.nn.functional as F
+
+from bugcar_image_segmentation_amd.graphdef import (ELEMENTWISE, Graph, GraphImportError, _s, _src, eval_op,
+                                                    parse_graphdef)
+
+
+def _nchw(node):
+    return _s(node.attr.get("data_format", b"NHWC")) == "NCHW"
+
+
+def _hw(v, nchw):
+    v = [int(x) for x in v]
+    return (v[2], v[3]) if nchw else (v[1], v[2])
+
+
+def _same(inp, k, s, d=1):
+    ke = (k - 1) * d + 1
+    out = -(-inp // s)
+    tot = max((out - 1) * s + ke - inp, 0)
+    return tot // 2, tot - tot // 2
+
+
+def _to_nchw(x, nchw):
+    return x if nchw else np.transpose(x, (0, 3, 1, 2))
+
+
+def _from_nchw(x, nchw):
+    return x if nchw else np.transpose(x, (0, 2, 3, 1))
+
+
+def _t(a):
+    return torch.from_numpy(np.ascontiguousarray(a, np.float64))
+
+
+def conv2d(node, x, w):
+    nchw = _nchw(node)
+    s = _hw(node.attr.get("strides", [1, 1, 1, 1]), nchw)
+    d = _hw(node.attr.get("dilations", [1, 1, 1, 1]), nchw)
+    xc = _to_nchw(x, nchw)
+    kh, kw = w.shape[:2]
+    padding = _s(node.attr.get("padding"))
+    if padding == "SAME":
+        ph, pw = _same(xc.shape[2], kh, s[0], d[0]), _same(xc.shape[3], kw, s[1], d[1])
+    elif padding == "EXPLICIT":
+        ep = [int(v) for v in node.attr["explicit_paddings"]]
+        ph, pw = ((ep[4], ep[5]), (ep[6], ep[7])) if nchw else ((ep[2], ep[3]), (ep[4], ep[5]))
+    else:
+        ph = pw = (0, 0)
+    xt = F.pad(_t(xc), (pw[0], pw[1], ph[0], ph[1]))
+    y = F.conv2d(xt, _t(np.transpose(w, (3, 2, 0, 1))), stride=s, dilation=d).numpy()
+    return _from_nchw(y, nchw)
+
+
+def conv2d_backprop_input(node, sizes, w, x):
+    """TF conv2d_transpose: full = sum over i*s + k of x[i] w[k]; out = full[pad_before : ...]
+    where pad_before is the forward convolution's leading pad for an input of `sizes`."""
+    nchw = _nchw(node)
+    s = _hw(node.attr.get("strides", [1, 1, 1, 1]), nchw)
+    sizes = [int(v) for v in sizes]
+    oh, ow = (sizes[2], sizes[3]) if nchw else (sizes[1], sizes[2])
+    kh, kw = w.shape[:2]
+    xc = _to_nchw(x, nchw)
+    full = F.conv_transpose2d(_t(xc), _t(np.transpose(w, (3, 2, 0, 1))), stride=s).numpy()
+    if _s(node.attr.get("padding")) == "SAME":
+        th, tw = _same(oh, kh, s[0])[0], _same(ow, kw, s[1])[0]
+    else:
+        th = tw = 0
+    need_h, need_w = th + oh, tw + ow
+    if full.shape[2] < need_h or full.shape[3] < need_w:
+        full = np.pad(full, ((0, 0), (0, 0), (0, max(0, need_h - full.shape[2])), (0, max(0, need_w - full.shape[3]))))
+    return _from_nchw(full[:, :, th:th + oh, tw:tw + ow], nchw)
+
+
+def max_pool(node, x, with_argmax=False):
+    nchw = _nchw(node)
+    k = _hw(node.attr["ksize"], nchw)
+    s = _hw(node.attr["strides"], nchw)
+    xc = _to_nchw(x, nchw)
+    if _s(node.attr.get("padding")) == "SAME":
+        ph, pw = _same(xc.shape[2], k[0], s[0]), _same(xc.shape[3], k[1], s[1])
+        xc = np.pad(xc, ((0, 0), (0, 0), ph, pw), constant_values=-np.inf)
+    y, idx = F.max_pool2d(_t(xc), k, stride=s, return_indices=True)
+    y = _from_nchw(y.numpy(), nchw)
+    if not with_argmax:
+        return y
+    if nchw:
+        raise GraphImportError("MaxPoolWithArgmax is NHWC-only in TensorFlow")
+    C = xc.shape[1]
+    flat = idx.numpy().astype(np.int64) * C + np.arange(C).reshape(1, C, 1, 1)   # (y*W + x)*C + c
+    return y, _from_nchw(flat, False)
+
+
+def run(pb: bytes, feed: dict, fetch: str):
+    """Evaluate tensor `fetch` of a frozen GraphDef given {placeholder name: array}."""
+    g = Graph(parse_graphdef(pb))
+    vals: dict = {}
+    for k, v in feed.items():
+        vals[_src(k)[0] + ":0"] = np.asarray(v, np.float64)
+
+    def get(name):
+        nm, idx = _src(name)
+        key = f"{nm}:{idx}"
+        if key not in vals:
+            ev(g.node(nm))
+        return vals[key]
+
+    def ev(n):
+        if f"{n.name}:0" in vals:
+            return
+        op = n.op
+        if op == "Const":
+            v = n.attr["value"]
+            vals[n.name + ":0"] = v.astype(np.float64) if v.dtype.kind == "f" else v
+            return
+        if op == "Placeholder":
+            raise GraphImportError(f"placeholder {n.name} not fed")
+        args = [get(s) for s in n.inputs]
+        if op == "Conv2D":
+            out = conv2d(n, *args)
+        elif op == "Conv2DBackpropInput":
+            out = conv2d_backprop_input(n, *args)
+        elif op == "MaxPool":
+            out = max_pool(n, args[0])
+        elif op == "MaxPoolWithArgmax":
+            y, am = max_pool(n, args[0], True)
+            vals[n.name + ":1"] = am
+            out = y
+        elif op in ("Pad", "PadV2"):
+            cv = float(args[2]) if len(args) > 2 else 0.0
+            out = np.pad(args[0], [tuple(int(v) for v in p) for p in args[1]], constant_values=cv)
+        elif op == "ScatterNd":
+            idx, upd, shape = args
+            out = np.zeros([int(v) for v in shape], np.float64)
+            np.add.at(out, tuple(np.asarray(idx, np.int64).reshape(-1, idx.shape[-1]).T), upd.reshape(-1))
+        elif op == "Slice":
+            b = [int(v) for v in args[1]]
+            sz = [int(v) for v in args[2]]
+            out = args[0][tuple(slice(bi, None if si == -1 else bi + si) for bi, si in zip(b, sz))]
+        elif op == "StridedSlice":
+            b, e, st = ([int(v) for v in a] for a in args[1:4])
+            out = args[0][tuple(slice(bi, ei if ei != 0 else None, si) for bi, ei, si in zip(b, e, st))]
+        elif op == "ArgMax":
+            out = np.argmax(args[0], axis=int(args[1]))
+        elif op in ELEMENTWISE or op in ("Transpose", "Reshape", "ExpandDims", "Squeeze", "ConcatV2", "Pack",
+                                         "Shape", "Fill", "Range", "FloorDiv", "FloorMod"):
+            if op.startswith("FusedBatchNorm"):
+                args = args[:5]
+            out = eval_op(n, args)
+        else:
+            raise GraphImportError(f"op {op} ({n.name}) not supported by the interpreter")
+        vals[n.name + ":0"] = out
+
+    return get(fetch)

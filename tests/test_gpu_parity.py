@@ -5,6 +5,9 @@ the fp32 oracle, class maps exact wherever the oracle's top-2 logit margin excee
 whose two best classes are closer than the tolerance is undecided by that tolerance); bf16 mode —
 agreement rate reported and bounded. Integer / byte paths (preprocess, BEV rasteriser) bit-exact.
 """
+import os
+from pathlib import Path
+
 import numpy as np
 import pytest
 import torch
@@ -312,3 +315,54 @@ def test_errors_are_loud(gpu, blocks):
         m.predict(np.zeros((1, 3, 30, 44), np.float32))      # not a multiple of 8
     with pytest.raises(N.BugsegError):
         ENET(weights=b"BSG1" + b"\0" * 12)
+
+
+@pytest.mark.parametrize("style", ["nhwc", "nchw"])
+def test_enet_from_graphdef_matches_graph_interpreter(gpu, tmp_path, style):
+    """The north star's TF-parity check, on a frozen GraphDef written from the synthetic weights
+    (tests/graph_writer.py; the real enet.pb is absent): ENET("x.pb") — the reference's constructor
+    (models.py:21-31) through the GraphDef importer — against the NumPy interpreter of the same
+    graph (oracle/tf_graph.py, the sess.run stand-in): logits within 1e-3 (fp32), classes equal
+    wherever the interpreter's top-2 margin exceeds 2e-3."""
+    import sys
+    sys.path.insert(0, str(Path(__file__).parent))
+    from graph_writer import with_biases, write_enet_graphdef
+    from oracle import tf_graph
+    H, W = 120, 160
+    blocks = with_biases(enet_spec.build_enet(), seed=3)
+    pb = write_enet_graphdef(blocks, H, W, style)
+    path = tmp_path / "enet.pb"
+    path.write_bytes(pb)
+    x = np.concatenate([ENET.preprocess_device(f, width=W, height=H).cpu().numpy()
+                        for f in synthetic.road_frames(1, H, W, seed=11)]).astype(np.float32)
+    want = tf_graph.run(pb, {"input0": x}, ENET.OUTPUT_TENSOR_NAME)
+    model = ENET(str(path), precision="fp32")
+    got = model.logits(x)
+    assert got.shape == want.shape
+    err = float(np.abs(got - want).max())
+    assert err < 1e-3, err
+    s = np.sort(want, axis=1)
+    decided = (s[:, -1] - s[:, -2]) > 2e-3
+    cls = np.argmax(want, axis=1)
+    assert (model.predict(x)[decided] == eo.LUT3[cls][decided]).all()
+
+
+@pytest.mark.skipif(not os.environ.get("BUGSEG_ENET_PB"), reason="set BUGSEG_ENET_PB=path/to/enet.pb (absent here)")
+def test_real_enet_pb_tf_parity(gpu):
+    """The one-command TF-parity check for when the reference's pretrained_models/enet.pb is
+    supplied: BUGSEG_ENET_PB=.../enet.pb pytest tests/test_gpu_parity.py -m gpu -k real_enet_pb.
+    Same bar as the synthetic-graph test: logits within 1e-3 of the graph (interpreted), classes
+    equal wherever the top-2 margin exceeds 2e-3, at the reference's 256 x 512 input."""
+    from oracle import tf_graph
+    path = os.environ["BUGSEG_ENET_PB"]
+    pb = Path(path).read_bytes()
+    H, W = ENET.INPUT_HEIGHT, ENET.INPUT_WIDTH
+    x = np.concatenate([ENET.preprocess_device(f, width=W, height=H).cpu().numpy()
+                        for f in synthetic.road_frames(1, 512, 512, seed=5)]).astype(np.float32)
+    want = tf_graph.run(pb, {ENET.INPUT_TENSOR_NAME.split(":")[0]: x}, ENET.OUTPUT_TENSOR_NAME)
+    model = ENET(path, precision="fp32")
+    got = model.logits(x)
+    assert np.abs(got - want).max() < 1e-3
+    s = np.sort(want, axis=1)
+    decided = (s[:, -1] - s[:, -2]) > 2e-3
+    assert (model.predict(x)[decided] == eo.LUT3[np.argmax(want, axis=1)][decided]).all()
