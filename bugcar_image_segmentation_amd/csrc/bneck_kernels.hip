@@ -53,19 +53,27 @@ __device__ unsigned long long *bugseg_stamps;
 template <int C, int V> struct BShape;
 // RP = residual fragments each wave prefetches before the middle conv (a ring refilled in phase 3
 // when a wave has more fragments than that: an L2 round trip then sits on the phase-3 path).
-template <> struct BShape<128, 0> { static constexpr int TH = 16, TW = 16, NW = 8, OCC = 4, RP = 2; };
-template <> struct BShape<128, 1> { static constexpr int TH = 20, TW = 16, NW = 8, OCC = 4, RP = 2; };
-template <> struct BShape<64, 0> { static constexpr int TH = 16, TW = 16, NW = 4, OCC = 5, RP = 4; };
-template <> struct BShape<64, 1> { static constexpr int TH = 20, TW = 16, NW = 4, OCC = 5, RP = 3; };
-template <> struct BShape<16, 0> { static constexpr int TH = 16, TW = 16, NW = 4, OCC = 6, RP = 4; };
+// RD = row-dilated full-width tiles (symmetric blocks, large dilation d on narrow maps): a tile is
+// TH rows d apart (one row phase) spanning all columns (W <= TW), so the middle conv's vertical taps
+// are the tile's one-row halo and its horizontal taps stay inside the tile — masked at the image
+// edge, no horizontal halo stored. 4 x 80 tiles cover 60 x 80 at d = 8 and d = 16 in 16 tiles per
+// frame (the phase sub-images, 8 x 10 and 4 x 5, are far too small for square tiles).
+template <> struct BShape<128, 0> { static constexpr int TH = 16, TW = 16, NW = 8, OCC = 4, RP = 2, RD = 0; };
+template <> struct BShape<128, 1> { static constexpr int TH = 20, TW = 16, NW = 8, OCC = 4, RP = 2, RD = 0; };
+template <> struct BShape<128, 2> { static constexpr int TH = 4, TW = 80, NW = 8, OCC = 4, RP = 2, RD = 1; };
+template <> struct BShape<128, 3> { static constexpr int TH = 4, TW = 64, NW = 8, OCC = 4, RP = 2, RD = 1; };
+template <> struct BShape<64, 0> { static constexpr int TH = 16, TW = 16, NW = 4, OCC = 5, RP = 4, RD = 0; };
+template <> struct BShape<64, 1> { static constexpr int TH = 20, TW = 16, NW = 4, OCC = 5, RP = 3, RD = 0; };
+template <> struct BShape<16, 0> { static constexpr int TH = 16, TW = 16, NW = 4, OCC = 6, RP = 4, RD = 0; };
 
-int bneck_variants(int C) { return C == 16 ? 1 : 2; }
+int bneck_variants(int C) { return C == 128 ? 4 : C == 64 ? 2 : 1; }
 
-void bneck_shape(int C, int v, int &th, int &tw, int &nw) {
-#define BS_CASE(CC, VV) if (C == CC && v == VV) { th = BShape<CC, VV>::TH; tw = BShape<CC, VV>::TW; nw = BShape<CC, VV>::NW; return; }
-    BS_CASE(128, 0) BS_CASE(128, 1) BS_CASE(64, 0) BS_CASE(64, 1) BS_CASE(16, 0)
+void bneck_shape(int C, int v, int &th, int &tw, int &nw, int *rd) {
+#define BS_CASE(CC, VV) if (C == CC && v == VV) { th = BShape<CC, VV>::TH; tw = BShape<CC, VV>::TW; nw = BShape<CC, VV>::NW; if (rd) *rd = BShape<CC, VV>::RD; return; }
+    BS_CASE(128, 0) BS_CASE(128, 1) BS_CASE(128, 2) BS_CASE(128, 3) BS_CASE(64, 0) BS_CASE(64, 1) BS_CASE(16, 0)
 #undef BS_CASE
     th = tw = nw = 0;
+    if (rd) *rd = 0;
 }
 
 template <typename T, int C, bool ASYM, int V, bool TR>
@@ -80,8 +88,11 @@ __global__ void __launch_bounds__((BShape<C, V>::NW * 64), (sizeof(T) == 2 ? BSh
     constexpr int TAPS = ASYM ? 5 : 9;
     constexpr int G2 = TAPS * IS / 8, KS2 = (G2 + 3) / 4;
     constexpr int G3 = IS / 8;                        // expand k groups (<= 4: one step)
-    constexpr int R = ASYM ? 2 : 1;                   // halo ring of the middle conv (tile coordinates)
-    constexpr int HWW = TW + 2 * R, HR = (TH + 2 * R) * HWW;
+    constexpr bool RD = BShape<C, V>::RD;
+    static_assert(!(RD && ASYM), "row-dilated tiles are for 3x3 blocks");
+    constexpr int RY = ASYM ? 2 : 1;                  // halo rows / columns of the middle conv (tile coordinates)
+    constexpr int RX = RD ? 0 : RY;                   // row-dilated tiles span the width: no column halo
+    constexpr int HWW = TW + 2 * RX, HR = (TH + 2 * RY) * HWW;
     constexpr int NF1 = (HR + 15) / 16;               // 16-pixel fragments of tile + halo
     constexpr int PAD = 16 / (int)sizeof(T);
     constexpr int PSTR = IS + PAD;                    // LDS pixel stride (elements)
@@ -156,17 +167,18 @@ __global__ void __launch_bounds__((BShape<C, V>::NW * 64), (sizeof(T) == 2 ? BSh
         const int txi = t % a.tiles_x; t /= a.tiles_x;
         const int tyi = t % a.tiles_y; t /= a.tiles_y;
         const int ph = t % a.phases, n = t / a.phases;
-        const int py = ph / dt, px = ph - py * dt;
+        const int py = RD ? ph : ph / dt, px = RD ? 0 : ph - py * dt;   // RD: phases = row phases
         // image pixel of tile pixel (0, 0); tile pixel (i, j) is image (oy0 + dt i, ox0 + dt j), or
         // (oy0 + dt j, ox0 + dt i) transposed
-        const int oy0 = py + dt * tyi * (tr ? TW : TH), ox0 = px + dt * txi * (tr ? TH : TW);
+        const int oy0 = py + dt * tyi * (tr ? TW : TH), ox0 = RD ? 0 : px + dt * txi * (tr ? TH : TW);
+        const int dtx = RD ? 1 : dt;                  // column step of the tile
         const uint32_t xn = (uint32_t)(n * a.H * a.W) * (uint32_t)(C * sizeof(T));   // frame byte offset
         // byte offset of channel chunk `choff` of pixel pi (per lane, 0..15) of tile fragment f (wave
         // uniform), or OOB outside the image. A fragment is a run of one tile row: its row i is a
         // scalar and only the column j is per lane.
         auto pix_off = [&](int f, int pi, int choff) -> uint32_t {
             const int i = (f * 16) / TW, j = (f * 16) % TW + pi;
-            const int y = oy0 + dt * (tr ? j : i), x = ox0 + dt * (tr ? i : j);
+            const int y = oy0 + dt * (tr ? j : i), x = ox0 + dtx * (tr ? i : j);
             const bool ok = y < a.H && x < a.W;
             return ok ? xn + (uint32_t)((y * a.W + x) * C + choff) * (uint32_t)sizeof(T) : OOB;
         };
@@ -183,7 +195,7 @@ __global__ void __launch_bounds__((BShape<C, V>::NW * 64), (sizeof(T) == 2 ? BSh
             for (int c = 0; c < CH1; ++c) {
                 const int h = (f0 + c * NW) * 16 + col;
                 const int hy = h / HWW, hx = h - hy * HWW;
-                const int iy = oy0 + dt * ((tr ? hx : hy) - R), ix = ox0 + dt * ((tr ? hy : hx) - R);
+                const int iy = oy0 + dt * ((tr ? hx : hy) - RY), ix = ox0 + dtx * ((tr ? hy : hx) - RX);
                 okc[c] = h < HR && (unsigned)iy < (unsigned)a.H && (unsigned)ix < (unsigned)a.W;
 #pragma unroll
                 for (int s = 0; s < KS1; ++s) {
@@ -255,7 +267,8 @@ __global__ void __launch_bounds__((BShape<C, V>::NW * 64), (sizeof(T) == 2 ? BSh
                 const int g = s * 4 + kq;
                 const int tap = g / (IS / 8), coff = (g - tap * (IS / 8)) * 8;
                 const int ky = tap / 3, kx = tap - ky * 3;
-                const int ti = tr ? kx : ky, tj = tr ? ky : kx;   // tap offset in tile axes
+                // tap offset in tile axes (RD: the column offset is (kx - 1) d inside the tile)
+                const int ti = tr ? kx : ky, tj = RD ? (kx - 1) * dt : tr ? ky : kx;
                 Raw wf[NR1];
 #pragma unroll
                 for (int r = 0; r < NR1; ++r) ld8(wf[r], w2 + (r * 16 + col) * K2S + s * 32 + kq * 8);
@@ -266,7 +279,8 @@ __global__ void __launch_bounds__((BShape<C, V>::NW * 64), (sizeof(T) == 2 ? BSh
                     if constexpr (NPX % 16 != 0) p = p < NPX ? p : 0;   // partial fragment: read anything, discarded
                     const int oy = p / TW, ox = p - oy * TW;
                     Raw xf;
-                    if (g < G2) ld8(xf, ts + ((oy + ti) * HWW + (ox + tj)) * PSTR + coff);
+                    const bool in = g < G2 && (!RD || (unsigned)(ox + tj) < (unsigned)TW);
+                    if (in) ld8(xf, ts + ((oy + ti) * HWW + (ox + tj)) * PSTR + coff);
                     else zero(xf);
                     if (a.ablate & 2) continue;
 #pragma unroll
@@ -438,15 +452,15 @@ extern "C" int bugseg_debug_set_stamps(void *p) {
 #endif
 
 size_t bneck_lds_bytes(int prec, int C, bool asym, int v) {
-    int TH, TW, NW;
-    bneck_shape(C, v, TH, TW, NW);
+    int TH, TW, NW, RD;
+    bneck_shape(C, v, TH, TW, NW, &RD);
     const int es = prec == PREC_BF16 ? 2 : 4, pad = 16 / es;
     const int I = C / 4, IS = I < 8 ? 8 : I, NR1 = (I + 15) / 16;
     const int KS1 = (C / 8 + 3) / 4, KS2 = ((asym ? 5 : 9) * IS / 8 + 3) / 4;
-    const int R = asym ? 2 : 1;
+    const int R = asym ? 2 : 1, RX = RD ? 0 : R;
     const size_t wts = (size_t)NR1 * 16 * (KS1 * 32 + pad) + (size_t)NR1 * 16 * (KS2 * 32 + pad) * (asym ? 2 : 1) +
                        (size_t)C * (32 + pad);
-    const size_t halo = (size_t)(TH + 2 * R) * (TW + 2 * R) * (IS + pad);
+    const size_t halo = (size_t)(TH + 2 * R) * (TW + 2 * RX) * (IS + pad);
     const size_t stage = (size_t)NW * 16 * (C + pad);      // phase-3 output staging
     const size_t consts = ((size_t)6 * NR1 * 16 + 3 * (size_t)C) * sizeof(float);
     return (wts + (halo > stage ? halo : stage)) * es + consts;
@@ -460,6 +474,8 @@ static const void *kfun(int C, bool asym, int v, bool tr) {
     BK_CASE(128, 0) BK_CASE(128, 1) BK_CASE(64, 0) BK_CASE(64, 1) BK_CASE(16, 0)
 #undef BK_CASE
     if (C == 128 && v == 1 && tr && !asym) return (const void *)bneck_kernel<T, 128, false, 1, true>;
+    if (C == 128 && v == 2 && !tr && !asym) return (const void *)bneck_kernel<T, 128, false, 2, false>;
+    if (C == 128 && v == 3 && !tr && !asym) return (const void *)bneck_kernel<T, 128, false, 3, false>;
     return nullptr;
 }
 
@@ -482,7 +498,7 @@ static hipError_t allow_lds(const void *f) {
 int bneck_slots_per_cu(int prec, int C, bool asym, int v, bool tr) {
     const void *f = bneck_fun(prec, C, asym, v, tr);
     int th, tw, nw;
-    bneck_shape(C, v, th, tw, nw);
+    bneck_shape(C, v, th, tw, nw, nullptr);
     if (!f || allow_lds(f) != hipSuccess) return 0;
     int n = 0;
     if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, f, nw * 64, bneck_lds_bytes(prec, C, asym, v)) != hipSuccess) return 0;
@@ -493,7 +509,7 @@ hipError_t launch_bneck(int prec, int C, bool asym, int v, const BneckArgs &a, h
     const void *f = bneck_fun(prec, C, asym, v, a.tr != 0);
     if (!f) return hipErrorInvalidValue;
     int th, tw, nw;
-    bneck_shape(C, v, th, tw, nw);
+    bneck_shape(C, v, th, tw, nw, nullptr);
     const size_t lds = bneck_lds_bytes(prec, C, asym, v);
     if (lds > 64 * 1024) {
         hipError_t e = allow_lds(f);

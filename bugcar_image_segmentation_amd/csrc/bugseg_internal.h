@@ -76,7 +76,8 @@ struct BneckArgs {
     const void *x;       // block input (B, H, W, C) NHWC
     void *out;           // block output, same shape
     int B, H, W;
-    int dt, phases;      // tiling dilation (the middle conv's dilation; 1 for asymmetric) and dt^2
+    int dt, phases;      // tiling dilation (the middle conv's dilation; 1 for asymmetric) and the phase
+                         // count: dt^2, or dt for row-dilated full-width variants
     int tr;              // transposed tiles: tile rows run along image columns (symmetric blocks only)
     int tiles_x, tiles_y, ntiles;   // tiles per phase sub-image row / column; B * phases * tiles_y * tiles_x
     int ablate;          // debug only (BUGSEG_BNECK_ABLATE): 1 skip x loads, 2 skip middle conv, 4 skip stores
@@ -87,7 +88,8 @@ struct BneckArgs {
 };
 // tile-shape variants of the fused kernel for C channels: 0 .. bneck_variants(C) - 1
 int bneck_variants(int C);
-void bneck_shape(int C, int v, int &th, int &tw, int &nw);
+// rd (optional): 1 for a row-dilated full-width variant (tiles_x = 1, phases = d, needs W <= tw)
+void bneck_shape(int C, int v, int &th, int &tw, int &nw, int *rd = nullptr);
 size_t bneck_lds_bytes(int prec, int C, bool asym, int v);
 // resident workgroups per CU (occupancy API); 0 if (C, asym, v, tr) is not built
 int bneck_slots_per_cu(int prec, int C, bool asym, int v, bool tr);

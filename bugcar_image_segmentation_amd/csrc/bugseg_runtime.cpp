@@ -523,7 +523,7 @@ bool fusable_regular(const bugseg_ctx *ctx, const BlockDesc &b, const std::vecto
 // variant keeps at least 60 % of the computed tile pixels inside the image (large dilations on small
 // feature maps: the unfused launches are cheaper). BUGSEG_BNECK_VARIANT forces a variant.
 int pick_bneck_variant(const bugseg_ctx *ctx, int C, bool asym, int d, int B, int H, int W, int &tiles_y, int &tiles_x,
-                       int &tr) {
+                       int &tr, int &rdv) {
     int cus = 0;
     if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, ctx->device) != hipSuccess || cus <= 0) cus = 256;
     const char *force = std::getenv("BUGSEG_BNECK_VARIANT");
@@ -532,23 +532,25 @@ int pick_bneck_variant(const bugseg_ctx *ctx, int C, bool asym, int d, int B, in
     int best = -1;
     double best_cost = 0;
     for (int v = 0; v < bneck_variants(C); ++v) {
-        int th, tw, nw;
-        bneck_shape(C, v, th, tw, nw);
+        int th, tw, nw, rd;
+        bneck_shape(C, v, th, tw, nw, &rd);
         if (bneck_lds_bytes(ctx->prec, C, asym, v) > 160 * 1024) continue;
+        if (rd && (asym || W > tw || d < 2)) continue;        // row-dilated tiles span the width
         const bool forced = force && *force && std::atoi(force) == v;
-        for (int t = 0; t < (asym ? 1 : 2); ++t) {
+        for (int t = 0; t < (asym || rd ? 1 : 2); ++t) {
             const int spc = bneck_slots_per_cu(ctx->prec, C, asym, v, t != 0);
             if (spc <= 0) continue;                           // this orientation is not built
             const int slots = spc * cus;
-            const int ty = t ? (hs + tw - 1) / tw : (hs + th - 1) / th, tx = t ? (ws + th - 1) / th : (ws + tw - 1) / tw;
-            const double ntiles = (double)B * d * d * ty * tx;
+            const int ty = rd ? (hs + th - 1) / th : t ? (hs + tw - 1) / tw : (hs + th - 1) / th;
+            const int tx = rd ? 1 : t ? (ws + th - 1) / th : (ws + tw - 1) / tw;
+            const double ntiles = (double)B * (rd ? d : d * d) * ty * tx;
             const double eff = (double)H * W / (ntiles / B * th * tw);
-            const double nf1 = std::ceil((th + 2.0 * R) * (tw + 2.0 * R) / 16.0), nft = std::ceil(th * tw / 16.0);
+            const double nf1 = std::ceil((th + 2.0 * R) * (tw + (rd ? 0.0 : 2.0 * R)) / 16.0), nft = std::ceil(th * tw / 16.0);
             const double tile = 3.8 * std::ceil(nf1 / nw) + 7.5 * std::ceil(nft / nw) + 4.5;
             const double cost = std::ceil(ntiles / slots) * tile;
             if (!forced && eff < 0.6) continue;
             if (best < 0 || (forced && best != v) || cost < best_cost) {
-                best = v; best_cost = cost; tiles_y = ty; tiles_x = tx; tr = t;
+                best = v; best_cost = cost; tiles_y = ty; tiles_x = tx; tr = t; rdv = rd;
             }
         }
         if (forced && best == v) break;
@@ -642,9 +644,9 @@ struct Walker {
                 const int nu = (int)b.units.size();
                 Shape s = cur;
                 const unsigned char *src = curp;
-                int rr = 0, dd = 1, ty = 0, tx = 0, ttr = 0, var = -1;
+                int rr = 0, dd = 1, ty = 0, tx = 0, ttr = 0, trd = 0, var = -1;
                 if (fusable_regular(ctx, b, ids, rr, dd))
-                    var = pick_bneck_variant(ctx, b.attrs[0], nu == 4, dd, B, cur.H, cur.W, ty, tx, ttr);
+                    var = pick_bneck_variant(ctx, b.attrs[0], nu == 4, dd, B, cur.H, cur.W, ty, tx, ttr, trd);
                 if (var >= 0) {
                     // one launch: projection + middle conv + expansion + residual, internals in LDS
                     szX = std::max(szX, tbytes(cur));
@@ -659,7 +661,7 @@ struct Walker {
                         const unsigned char *dw = (const unsigned char *)ctx->dev_w;
                         const Packed &p1 = P(0), &p2 = P(1), &p3 = P(nu - 1), &p2b = P(nu == 4 ? 2 : 1);
                         q.x = curp; q.out = dst; q.B = B; q.H = cur.H; q.W = cur.W;
-                        q.dt = dd; q.phases = dd * dd; q.tr = ttr;
+                        q.dt = dd; q.phases = trd ? dd : dd * dd; q.tr = ttr;
                         if (const char *ab = std::getenv("BUGSEG_BNECK_ABLATE")) q.ablate = std::atoi(ab);
                         q.tiles_y = ty; q.tiles_x = tx;
                         q.ntiles = B * q.phases * ty * tx;
@@ -1210,7 +1212,7 @@ int bugseg_plan_op(bugseg_ctx *ctx, int B, int H, int W, int op, char *kernel, i
     std::string tag;
     if (o.kind == 1) {
         int th, tw, nw;
-        bneck_shape(o.bn_c, o.bn_var, th, tw, nw);
+        bneck_shape(o.bn_c, o.bn_var, th, tw, nw, nullptr);
         tag = "bneck C" + std::to_string(o.bn_c) + (o.bn_asym ? " asym" : "") + " " + std::to_string(th) + "x" +
               std::to_string(tw);
         (void)nw;

@@ -13,7 +13,8 @@ from collections import defaultdict
 
 
 # tile shape of each fused-bottleneck variant (bneck_kernels.hip BShape)
-BNECK_SHAPES = {(128, 0): "16x16", (128, 1): "20x16", (64, 0): "16x16", (64, 1): "20x16", (16, 0): "16x16"}
+BNECK_SHAPES = {(128, 0): "16x16", (128, 1): "20x16", (128, 2): "4x80", (128, 3): "4x64", (64, 0): "16x16", (64, 1): "20x16",
+                (16, 0): "16x16"}
 
 
 def short(name):
