@@ -11,8 +11,8 @@
 //     of R pixels (zero outside the image: t0 is what the middle conv zero-pads);
 //   * phase 2 accumulates its whole tile in registers, then (after a barrier) overwrites the t0
 //     region with t1, so one LDS region serves both (asymmetric: t0 -> t1a -> t1, same trick);
-//   * phase 3 streams 16-pixel fragments: MFMA with W3, residual staged in LDS, activation,
-//     16-B-per-lane stores.
+//   * phase 3 streams 16-pixel fragments: MFMA with W3, residual, activation and 16-B-per-lane
+//     stores, all in registers (lane-pair transposes with v_permlane16_swap).
 //
 // Dilated tiling. A 3x3 conv of dilation d only couples pixels whose coordinates agree mod d, so a
 // tile is a TH x TW block of ONE such phase: tile pixel (i, j) is image pixel (oy0 + d*i, ox0 + d*j),
@@ -104,17 +104,27 @@ __global__ void __launch_bounds__((BShape<C, V>::NW * 64), (sizeof(T) == 2 ? BSh
     constexpr int NFA = (NPA + 15) / 16;
     constexpr int NF2A = (NFA + NW - 1) / NW;
     constexpr int CH1 = KS1 >= 4 ? 3 : KS1 == 2 ? 4 : 8;   // phase-1 fragments whose loads fly together
+    // phase-3 chunking (see phase 3): bf16 with an even number of 16-row blocks swaps row pairs
+    // into 16-B chunks; bf16 C = 16 stores 8-B quads (HALF); fp32 quads are 16-B chunks
+    // REG3: the register epilogue (C = 128 and 16). C = 64 keeps the LDS-staged epilogue: its 128-B
+    // pixels would be written as half lines by the register layout, which measured slower there.
+    constexpr bool REG3 = C != 64;
+    constexpr bool SWAP = REG3 && sizeof(T) == 2 && NR3 % 2 == 0;
+    constexpr bool HALF = REG3 && sizeof(T) == 2 && NR3 % 2 != 0;
     constexpr int EPC = 16 / (int)sizeof(T);          // elements per 16-B chunk
     constexpr int CPP = C / EPC;                      // 16-B chunks per pixel
-    constexpr int CPF = 16 * CPP;                     // 16-B chunks of one 16-pixel output fragment
+    constexpr int CPF = 16 * CPP;                     // (staged) 16-B chunks of one 16-pixel fragment
     constexpr int CPL = (CPF + 63) / 64;              // ... per lane
-    constexpr int OSTR = C + EPC;                     // phase-3 staging row stride (16-B padded)
+    constexpr int OSTR = C + EPC;                     // staged epilogue: row stride (16-B padded)
+    constexpr int RQ3 = !REG3 ? CPL : SWAP ? NR3 / 2 : NR3;   // residual chunks per lane per fragment
     static_assert(TW % 16 == 0, "a fragment is a run of one tile row");
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
 
     const int tid = threadIdx.x;
     const int lane = tid & 63, col = lane & 15, kq = lane >> 4;
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);   // provably uniform: scalar fragment math
+    // first channel of this lane's phase-3 chunk t
+    auto chunk_ch = [&](int t) -> int { return SWAP ? (2 * t + (kq & 1)) * 16 + 8 * (kq >> 1) : t * 16 + kq * 4; };
     const int K1S = KS1 * 32 + PAD, K2S = KS2 * 32 + PAD, K3S = 32 + PAD;
     T *w1 = reinterpret_cast<T *>(smem);
     T *w2 = w1 + NR1 * 16 * K1S;
@@ -182,6 +192,8 @@ __global__ void __launch_bounds__((BShape<C, V>::NW * 64), (sizeof(T) == 2 ? BSh
             const bool ok = y < a.H && x < a.W;
             return ok ? xn + (uint32_t)((y * a.W + x) * C + choff) * (uint32_t)sizeof(T) : OOB;
         };
+        // byte offset of pixel pi of fragment f (channel 0), or OOB outside the image
+        auto pix_base = [&](int f, int pi) -> uint32_t { return pix_off(f, pi, 0); };
         STAMP(0); STAMP_WG();
         __syncthreads();   // weights staged (first tile) / previous tile done with ts
         STAMP(1);
@@ -234,19 +246,35 @@ __global__ void __launch_bounds__((BShape<C, V>::NW * 64), (sizeof(T) == 2 ? BSh
         __syncthreads();
         STAMP(3);
 
-        // residual of phase 3 (x at the tile pixels) with coalesced 16-B loads: lane chunk q of
-        // fragment f is channel chunk q % CPP of tile pixel 16 f + q / CPP. RP fragments are
-        // prefetched before the middle conv (asymmetric: after its 5x1 pass, to keep the two passes'
-        // live ranges apart); phase 3 refills the ring as it consumes it.
+        // residual of phase 3 (x at the tile pixels), loaded in the layout phase 3 stores in (see
+        // there): per lane and row pair t of the expansion, one 16-B chunk of its pixel. RP fragments
+        // are prefetched before the middle conv (asymmetric: after its 5x1 pass, to keep the two
+        // passes' live ranges apart); phase 3 refills the ring as it consumes it.
         constexpr int RP = BShape<C, V>::RP < NF2 ? BShape<C, V>::RP : NF2;
-        uint4 res[RP][CPL];
-        auto load_res = [&](int j, uint4 (&r)[CPL]) {
-            const int f = wave + NW * j;
+        uint4 res[RP][RQ3];
+        auto load_res = [&](int j, uint4 (&r)[RQ3]) {
+            if constexpr (!REG3) {
+                // staged epilogue: lane chunk q of fragment f is channel chunk q % CPP of its pixel
+                // q / CPP (coalesced 16-B loads)
+                const int f = wave + NW * j;
 #pragma unroll
-            for (int k = 0; k < CPL; ++k) {
-                const int q = lane + 64 * k;
-                const uint32_t off = pix_off(f, q / CPP, (q % CPP) * EPC);
-                r[k] = bld16(rxb, q < CPF ? off : OOB);
+                for (int k = 0; k < CPL; ++k) {
+                    const int q = lane + 64 * k;
+                    const uint32_t off = pix_off(f, q / CPP, (q % CPP) * EPC);
+                    r[k] = bld16(rxb, q < CPF ? off : OOB);
+                }
+                return;
+            }
+            const uint32_t po = pix_base(wave + NW * j, col);
+#pragma unroll
+            for (int t = 0; t < RQ3; ++t) {
+                const uint32_t off = po == OOB ? OOB : po + (uint32_t)chunk_ch(t) * (uint32_t)sizeof(T);
+                if constexpr (HALF) {
+                    const u32x2_t v = __builtin_amdgcn_raw_buffer_load_b64(rxb, (int)off, 0, 0);
+                    r[t] = make_uint4(v.x, v.y, 0u, 0u);
+                } else {
+                    r[t] = bld16(rxb, off);
+                }
             }
         };
         auto prefetch_res = [&]() {
@@ -393,10 +421,14 @@ __global__ void __launch_bounds__((BShape<C, V>::NW * 64), (sizeof(T) == 2 ? BSh
         }
         __syncthreads();
 
-        // ---- phase 3: out = act_out(act3(W3 t1 + b3) + x). The t1 fragments go to registers, then
-        // the t1 region becomes per-wave staging: residual chunks in, results over them, and the
-        // fragment leaves as 16-B-per-lane stores (a per-lane NHWC store would write 16 partial
-        // lines per instruction: the ablation showed stores dominating this kernel).
+        // ---- phase 3: out = act_out(act3(W3 t1 + b3) + x), entirely in registers. An accumulator
+        // quad is 4 consecutive channels of one pixel (lane = (pixel col, quad kq)); in bf16 two
+        // rows' quads of lanes kq and kq^1 are traded with v_permlane16_swap so that each lane holds
+        // 8 consecutive channels (16 B) of its pixel: row 2t + (kq & 1), channels 8 (kq >> 1) ...
+        // +7 — one wave store then writes 16 pixels x 64 contiguous bytes. The residual arrives in
+        // that chunk layout and the same (involutive) swap returns it to accumulator quads. fp32
+        // quads are already 16-B chunks; C = 16 (one row) stores its 8-B quads (a 16-pixel
+        // fragment of 32-B pixels is one 512-B run). No LDS staging, no wave syncs.
         Raw tf[NF2];
 #pragma unroll
         for (int j = 0; j < NF2; ++j) {
@@ -404,42 +436,97 @@ __global__ void __launch_bounds__((BShape<C, V>::NW * 64), (sizeof(T) == 2 ? BSh
             if (kq < G3 && p < NPX) ld8(tf[j], ts + p * PSTR + kq * 8);
             else zero(tf[j]);
         }
-        __syncthreads();
+        if constexpr (!REG3) {
+            // staged epilogue: the t1 region becomes per-wave staging — residual chunks in, results
+            // over them, and the fragment leaves as contiguous 16-B-per-lane stores
+            __syncthreads();
+            STAMP(5);
+            T *stg = ts + wave * 16 * OSTR;
+#pragma unroll
+            for (int j = 0; j < NF2; ++j) {
+                if (wave + NW * j >= NFT) break;          // wave-uniform
+#pragma unroll
+                for (int k = 0; k < CPL; ++k) {
+                    const int q = lane + 64 * k;
+                    if (q < CPF) *reinterpret_cast<uint4 *>(stg + (q / CPP) * OSTR + (q % CPP) * EPC) = res[j % RP][k];
+                }
+                if (j + RP < NF2 && wave + NW * (j + RP) < NFT) load_res(j + RP, res[j % RP]);
+                wave_lds_sync();
+#pragma unroll
+                for (int r = 0; r < NR3; ++r) {
+                    const int ch = r * 16 + kq * 4;
+                    f32x4 acc = bias_in_acc(NR3) ? bias4(cb3 + ch) : (f32x4){0.f, 0.f, 0.f, 0.f};
+                    Raw wf;
+                    ld8(wf, w3 + (r * 16 + col) * K3S + kq * 8);
+                    mma(acc, wf, tf[j]);
+                    T *sp = stg + col * OSTR + ch;
+                    float4 v = act(bias_in_acc(NR3) ? f4(acc) : add4(f4(acc), ld4f(cb3 + ch)), cs3 + ch);
+                    v = act(add4(v, ld4(sp)), cso + ch);
+                    st4(sp, v);
+                }
+                wave_lds_sync();
+#pragma unroll
+                for (int k = 0; k < CPL; ++k) {
+                    const int q = lane + 64 * k;
+                    if (q < CPF) {
+                        const uint32_t off = (a.ablate & 4) ? OOB : pix_off(wave + NW * j, q / CPP, (q % CPP) * EPC);
+                        bst16(rob, off, *reinterpret_cast<const uint4 *>(stg + (q / CPP) * OSTR + (q % CPP) * EPC));
+                    }
+                }
+                wave_lds_sync();
+            }
+            STAMP(6);
+            continue;
+        }
         STAMP(5);
-        T *stg = ts + wave * 16 * OSTR;
 #pragma unroll
         for (int j = 0; j < NF2; ++j) {
             if (wave + NW * j >= NFT) break;              // wave-uniform
-            const int p0 = (wave + NW * j) * 16;
-#pragma unroll
-            for (int k = 0; k < CPL; ++k) {
-                const int q = lane + 64 * k;
-                if (q < CPF) *reinterpret_cast<uint4 *>(stg + (q / CPP) * OSTR + (q % CPP) * EPC) = res[j % RP][k];
-            }
-            if (j + RP < NF2 && wave + NW * (j + RP) < NFT) load_res(j + RP, res[j % RP]);
-            wave_lds_sync();
-#pragma unroll
-            for (int r = 0; r < NR3; ++r) {
+            const uint32_t po = (a.ablate & 4) ? OOB : pix_base(wave + NW * j, col);
+            auto out3 = [&](int r, const f32x4 &acc) {
                 const int ch = r * 16 + kq * 4;
-                f32x4 acc = bias_in_acc(NR3) ? bias4(cb3 + ch) : (f32x4){0.f, 0.f, 0.f, 0.f};
-                Raw wf;
-                ld8(wf, w3 + (r * 16 + col) * K3S + kq * 8);
-                mma(acc, wf, tf[j]);
-                T *sp = stg + col * OSTR + ch;
-                float4 v = act(bias_in_acc(NR3) ? f4(acc) : add4(f4(acc), ld4f(cb3 + ch)), cs3 + ch);
-                v = act(add4(v, ld4(sp)), cso + ch);
-                st4(sp, v);
-            }
-            wave_lds_sync();
+                return act(bias_in_acc(NR3) ? f4(acc) : add4(f4(acc), ld4f(cb3 + ch)), cs3 + ch);
+            };
 #pragma unroll
-            for (int k = 0; k < CPL; ++k) {
-                const int q = lane + 64 * k;
-                if (q < CPF) {
-                    const uint32_t off = (a.ablate & 4) ? OOB : pix_off(wave + NW * j, q / CPP, (q % CPP) * EPC);
-                    bst16(rob, off, *reinterpret_cast<const uint4 *>(stg + (q / CPP) * OSTR + (q % CPP) * EPC));
+            for (int t = 0; t < RQ3; ++t) {
+                const uint32_t off = po == OOB ? OOB : po + (uint32_t)chunk_ch(t) * (uint32_t)sizeof(T);
+                const uint4 rc = res[j % RP][t];
+                if constexpr (SWAP) {
+                    const int r0 = 2 * t, r1 = 2 * t + 1;
+                    f32x4 acc0 = bias_in_acc(NR3) ? bias4(cb3 + r0 * 16 + kq * 4) : (f32x4){0.f, 0.f, 0.f, 0.f};
+                    f32x4 acc1 = bias_in_acc(NR3) ? bias4(cb3 + r1 * 16 + kq * 4) : (f32x4){0.f, 0.f, 0.f, 0.f};
+                    Raw w0, w1;
+                    ld8(w0, w3 + (r0 * 16 + col) * K3S + kq * 8);
+                    ld8(w1, w3 + (r1 * 16 + col) * K3S + kq * 8);
+                    mma(acc0, w0, tf[j]);
+                    mma(acc1, w1, tf[j]);
+                    // residual chunk -> quads of rows r0 / r1
+                    uint32_t a0 = rc.x, a1 = rc.y, b0 = rc.z, b1 = rc.w;
+                    pl16swap(a0, b0);
+                    pl16swap(a1, b1);
+                    float4 v0 = act(add4(out3(r0, acc0), unpack_bf16x4((u32x2_t){a0, a1})), cso + r0 * 16 + kq * 4);
+                    float4 v1 = act(add4(out3(r1, acc1), unpack_bf16x4((u32x2_t){b0, b1})), cso + r1 * 16 + kq * 4);
+                    u32x2_t p0 = pack_bf16x4(v0), p1 = pack_bf16x4(v1);
+                    uint32_t x0 = p0.x, x1 = p0.y, y0 = p1.x, y1 = p1.y;
+                    pl16swap(x0, y0);
+                    pl16swap(x1, y1);
+                    bst16(rob, off, make_uint4(x0, x1, y0, y1));
+                } else {
+                    const int r = t;
+                    f32x4 acc = bias_in_acc(NR3) ? bias4(cb3 + r * 16 + kq * 4) : (f32x4){0.f, 0.f, 0.f, 0.f};
+                    Raw wf;
+                    ld8(wf, w3 + (r * 16 + col) * K3S + kq * 8);
+                    mma(acc, wf, tf[j]);
+                    if constexpr (HALF) {
+                        float4 v = act(add4(out3(r, acc), unpack_bf16x4((u32x2_t){rc.x, rc.y})), cso + r * 16 + kq * 4);
+                        __builtin_amdgcn_raw_buffer_store_b64(pack_bf16x4(v), rob, (int)off, 0, 0);
+                    } else {
+                        float4 v = act(add4(out3(r, acc), __builtin_bit_cast(float4, rc)), cso + r * 16 + kq * 4);
+                        bst16(rob, off, __builtin_bit_cast(uint4, v));
+                    }
                 }
             }
-            wave_lds_sync();
+            if (j + RP < NF2 && wave + NW * (j + RP) < NFT) load_res(j + RP, res[j % RP]);
         }
         STAMP(6);
     }
@@ -461,7 +548,7 @@ size_t bneck_lds_bytes(int prec, int C, bool asym, int v) {
     const size_t wts = (size_t)NR1 * 16 * (KS1 * 32 + pad) + (size_t)NR1 * 16 * (KS2 * 32 + pad) * (asym ? 2 : 1) +
                        (size_t)C * (32 + pad);
     const size_t halo = (size_t)(TH + 2 * R) * (TW + 2 * RX) * (IS + pad);
-    const size_t stage = (size_t)NW * 16 * (C + pad);      // phase-3 output staging
+    const size_t stage = C == 64 ? (size_t)NW * 16 * (C + pad) : 0;    // staged epilogue (REG3 off)
     const size_t consts = ((size_t)6 * NR1 * 16 + 3 * (size_t)C) * sizeof(float);
     return (wts + (halo > stage ? halo : stage)) * es + consts;
 }

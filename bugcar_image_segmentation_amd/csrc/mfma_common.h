@@ -13,6 +13,7 @@ __device__ __forceinline__ void wave_lds_sync() {
 
 typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 typedef float f32x4 __attribute__((ext_vector_type(4)));
+typedef unsigned int u32x2_t __attribute__((ext_vector_type(2)));
 
 struct RawB { uint4 v; };          // 8 bf16
 struct RawF { float4 a, b; };      // 8 f32
@@ -78,6 +79,25 @@ __device__ __forceinline__ void st4(__bf16 *p, float4 v) {
     bf16x4 b = {(__bf16)v.x, (__bf16)v.y, (__bf16)v.z, (__bf16)v.w};
     *reinterpret_cast<bf16x4 *>(p) = b;
 }
+// 4 floats <-> 4 bf16 packed in two dwords (round to nearest even, as the (__bf16) casts of st4)
+__device__ __forceinline__ u32x2_t pack_bf16x4(float4 v) {
+    typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
+    bf16x4 b = {(__bf16)v.x, (__bf16)v.y, (__bf16)v.z, (__bf16)v.w};
+    return __builtin_bit_cast(u32x2_t, b);
+}
+__device__ __forceinline__ float4 unpack_bf16x4(u32x2_t u) {
+    return make_float4(__uint_as_float(u.x << 16), __uint_as_float(u.x & 0xffff0000u),
+                       __uint_as_float(u.y << 16), __uint_as_float(u.y & 0xffff0000u));
+}
+// v_permlane16_swap_b32 (gfx950): lanes of the odd 16-lane rows of `a` trade places with the lanes
+// of the even rows of `b` one row below (lane l of row 2i+1 of a <-> lane l-16 of row 2i of b).
+// An involution; measured on MI355X with scripts/permlane_probe.hip.
+__device__ __forceinline__ void pl16swap(uint32_t &a, uint32_t &b) {
+    const u32x2_t r = __builtin_amdgcn_permlane16_swap(a, b, false, false);
+    a = r.x;
+    b = r.y;
+}
+
 __device__ __forceinline__ float ld1(const float *p) { return *p; }
 __device__ __forceinline__ float ld1(const __bf16 *p) { return (float)*p; }
 
