@@ -284,10 +284,29 @@ Packed pack_conv(Packer &pk, const UnitDesc &u, int CinS, const std::vector<floa
     return p;
 }
 
+// Two 1x1 convolutions over the same input as ONE launch (the upsampling block's main 1x1 and its
+// extension branch's first 1x1, which both read the block input): rows [0, m.cout) are m's,
+// rows [m.cout, m.cout + e.cout) e's, each with its own folded BN and slope. Bit-identical per output
+// channel to the two separate launches when both pack to the same bias placement.
+Packed pack_conv_pair(Packer &pk, const UnitDesc &m, const UnitDesc &e, int CinS) {
+    UnitDesc u = m;
+    u.cout = m.cout + e.cout;
+    u.w.insert(u.w.end(), e.w.begin(), e.w.end());
+    u.b.insert(u.b.end(), e.b.begin(), e.b.end());
+    auto cat = [](std::vector<float> a, const std::vector<float> &b) { a.insert(a.end(), b.begin(), b.end()); return a; };
+    // BN folds per channel (the caller requires m.eps == e.eps)
+    u.gamma = cat(m.gamma, e.gamma);
+    u.beta = cat(m.beta, e.beta);
+    u.mean = cat(m.mean, e.mean);
+    u.var = cat(m.var, e.var);
+    u.slope = cat(m.slope, e.slope);
+    return pack_conv(pk, u, CinS, nullptr);
+}
+
 // Stride-2 transposed convolution (IOHW weights) as a 4-phase convolution over the INPUT grid:
 // output pixel (2i+a, 2j+b) = sum over taps (dy,dx) of in[i+dy][j+dx] . W[ky = a+pad-2dy][kx = b+pad-2dx]
 // (PyTorch/ONNX semantics y = 2i - pad + ky). GEMM row n = phase * coutP + co.
-Packed pack_tconv(Packer &pk, const UnitDesc &u, int CinS, std::string &why) {
+Packed pack_tconv(Packer &pk, const UnitDesc &u, int CinS, std::string &why, int choff = 0) {
     Packed p;
     if (u.stride != 2 || u.kh != u.kw || u.pad_h != u.pad_w) { why = "tconv: only square stride-2 kernels"; return p; }
     const int k = u.kh, pad = u.pad_h;
@@ -298,7 +317,8 @@ Packed pack_tconv(Packer &pk, const UnitDesc &u, int CinS, std::string &why) {
         for (int a = 0; a < 2; ++a) { const int kk = a + pad - 2 * d; any |= kk >= 0 && kk < k; }
         if (any) D.push_back(d);
     }
-    const int nd = (int)D.size(), taps = nd * nd, CG = CinS / 8;
+    // input groups: cstore(u.cin) channels starting at channel `choff` of a CinS-channel tensor
+    const int nd = (int)D.size(), taps = nd * nd, CG = round_up(u.cin, 8) / 8;
     const int Kgroups = taps * CG;
     p.Ksteps = (Kgroups + 3) / 4;
     p.Kpad = p.Ksteps * 32;
@@ -323,13 +343,13 @@ Packed pack_tconv(Packer &pk, const UnitDesc &u, int CinS, std::string &why) {
                     const int tap = ty * nd + tx;
                     for (int co = 0; co < u.cout; ++co)
                         for (int ci = 0; ci < u.cin; ++ci)
-                            w[(size_t)((a * 2 + b) * p.coutP + co) * p.Kpad + tap * CinS + ci] =
+                            w[(size_t)((a * 2 + b) * p.coutP + co) * p.Kpad + tap * CG * 8 + ci] =
                                 (double)u.w[(((size_t)ci * u.cout + co) * k + ky) * k + kx] * scale[co];
                 }
     std::vector<int> gt(p.Ksteps * 4, gentry(0, 0, 0xffff));
     for (int g = 0; g < Kgroups; ++g) {
         const int tap = g / CG;
-        gt[g] = gentry(D[tap / nd], D[tap % nd], (g % CG) * 8);
+        gt[g] = gentry(D[tap / nd], D[tap % nd], choff + (g % CG) * 8);
     }
     std::vector<float> bias(p.Npad, 0.f), s1(p.Npad, 0.f), s2(p.Npad, 0.f), ps(p.Npad, 0.f);
     for (int ph = 0; ph < 4; ++ph)
@@ -434,6 +454,22 @@ bool pack_all(bugseg_ctx *ctx, std::string &why) {
             if (!why.empty()) return false;
             add(t);
             add(pack_conv(pk, u2, cstore(ut.cout), &b.extra[0]));
+            // main 1x1 + extension 1x1 merged into one launch over the block input (ids 4, 5: the pair
+            // and the tconv reading the extension half of its output) when the pair's output keeps a
+            // power-of-two count of 16-B chunks per pixel (the conv epilogue's staged stores) and
+            // both halves fold their bias the same way (bias_in_acc); bit-identical per channel
+            const int es = ctx->prec == PREC_BF16 ? 2 : 4, mc = cstore(um.cout) + cstore(u1.cout);
+            const int chunks = mc * es / 16;
+            const int nr_pair = pow2_nr(round_up(um.cout, 16) + round_up(u1.cout, 16));
+            auto bias_acc = [](int nr) { return nr < 8; };     // mfma_common.h bias_in_acc
+            if (um.cout % 16 == 0 && (chunks & (chunks - 1)) == 0 && nr_pair <= 8 && um.eps == u1.eps &&
+                bias_acc(nr_pair) == bias_acc(pow2_nr(round_up(um.cout, 16))) &&
+                bias_acc(nr_pair) == bias_acc(pow2_nr(round_up(u1.cout, 16))) && !std::getenv("BUGSEG_NO_PAIR")) {
+                add(pack_conv_pair(pk, um, u1, cstore(cin)));
+                Packed t2 = pack_tconv(pk, ut, mc, why, cstore(um.cout));
+                if (!why.empty()) return false;
+                add(t2);
+            }
             cur_c = cout;
             break;
         }
@@ -721,7 +757,21 @@ struct Walker {
                 szM = std::max(szM, tbytes(sm));
                 szT = std::max({szT, tbytes(s1), tbytes(st)});
                 szX = std::max(szX, tbytes(so));
-                if (fill) {
+                const bool pair = ids.size() == 6;
+                // paired: the main and extension 1x1 outputs share one tensor (main channels first)
+                Shape sp{cur.H, cur.W, pair ? sm.C + s1.C : sm.C};
+                szM = std::max(szM, tbytes(sp));
+                if (fill && pair) {
+                    Op om1, ot, o2;
+                    conv(P(4), EPI_PLAIN, curp, cur, sp, Mb, sp, om1);
+                    conv(P(5), EPI_SHUFFLE, Mb, sp, sp, T[1], st, ot);
+                    ot.bytes -= (double)B * sp.H * sp.W * sm.C * es;    // reads only the extension half
+                    conv(P(3), EPI_RESUNPOOL, T[1], st, so, dst, so, o2);
+                    o2.a.res = Mb; o2.a.resH = sp.H; o2.a.resW = sp.W; o2.a.resC = b.attrs[1]; o2.a.resCS = sp.C;
+                    o2.a.idx_in = idx[ref]; o2.a.idxCS = cstore(ctx->blocks[ref].attrs[0]);
+                    o2.bytes += (double)B * sm.H * sm.W * sm.C * es + (double)B * sm.H * sm.W * o2.a.idxCS;
+                    ops.push_back(om1); ops.push_back(ot); ops.push_back(o2);
+                } else if (fill) {
                     Op om, o1, ot, o2;
                     conv(P(0), EPI_PLAIN, curp, cur, sm, Mb, sm, om);
                     conv(P(1), EPI_PLAIN, curp, cur, s1, T[0], s1, o1);

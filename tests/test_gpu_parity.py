@@ -254,7 +254,25 @@ def test_fused_bottlenecks_equal_unfused(gpu, blocks, prec, H, W, variant, monke
     plain.ctx.forward_bgr(bgr, B, H, W, N.OUT_LOGITS_F32, b)
     n_fused = fused.ctx.plan_info(B, H, W, N.OUT_LOGITS_F32)[0]
     n_plain = plain.ctx.plan_info(B, H, W, N.OUT_LOGITS_F32)[0]
-    assert n_plain == 89 and n_fused < n_plain
+    assert n_plain == 88 and n_fused < n_plain      # 89 convolutions; the up5 main + extension 1x1 pair is one launch
+    assert torch.equal(a, b)
+
+
+@pytest.mark.parametrize("prec", ["fp32", "bf16"])
+def test_up_block_pair_equals_separate(gpu, blocks, prec, monkeypatch):
+    """The upsampling blocks' main and extension 1x1 convolutions merged into one launch (one read
+    of the block input, the tconv reading the extension half) are bit-identical to the separate
+    launches (BUGSEG_NO_PAIR=1)."""
+    H, W = 120, 160
+    bgr = torch.from_numpy(synthetic.road_frames(2, H, W, seed=4)).cuda()
+    paired = ENET(weights=blocks, precision=prec)
+    a = torch.empty((2, 15, H, W), dtype=torch.float32, device=gpu)
+    paired.ctx.forward_bgr(bgr, 2, H, W, N.OUT_LOGITS_F32, a)
+    monkeypatch.setenv("BUGSEG_NO_PAIR", "1")
+    sep = ENET(weights=blocks, precision=prec)
+    b = torch.empty_like(a)
+    sep.ctx.forward_bgr(bgr, 2, H, W, N.OUT_LOGITS_F32, b)
+    assert paired.ctx.plan_info(2, H, W, N.OUT_LOGITS_F32)[0] < sep.ctx.plan_info(2, H, W, N.OUT_LOGITS_F32)[0]
     assert torch.equal(a, b)
 
 
