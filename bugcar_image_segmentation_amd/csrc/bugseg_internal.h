@@ -95,6 +95,21 @@ size_t bneck_lds_bytes(int prec, int C, bool asym, int v);
 int bneck_slots_per_cu(int prec, int C, bool asym, int v, bool tr);
 hipError_t launch_bneck(int prec, int C, bool asym, int v, const BneckArgs &a, hipStream_t s);
 
+// ---- fused upsampling bottleneck (up_kernels.hip) ----------------------------------------------
+struct UpArgs {
+    const void *x;            // block input (B, h, w, Cin) NHWC
+    const uint8_t *idx;       // pooling indices of the paired down block (B, h, w, idxCS), byte = window position
+    void *out;                // (B, 2h, 2w, Cout)
+    int M, h, w, idxCS;       // M = B * h * w input pixels
+    uint32_t mHW, mW; int sHW, sW;                    // fdiv by h * w and by w
+    const void *w1, *w2, *w3;                         // [main; e1] pair, tconv (4 phases), expansion
+    const float *b1, *s1, *b2, *s2, *b3, *s3, *s_out;
+    uint32_t x_bytes, idx_bytes, out_bytes;
+    int slopes_le1;
+};
+bool up_supported(int cin, int it, int cout);
+hipError_t launch_up(int prec, int cin, int it, int cout, const UpArgs &a, hipStream_t s);
+
 // ---- preprocess / layout (prep_kernels.hip) --------------------------------------------------
 struct PreArgs {
     const uint8_t *bgr;  // (B, H0, W0, 3)

@@ -55,10 +55,12 @@ struct Packed {
 };
 
 struct Op {
-    int kind = 0;          // 0: conv_kernel launch, 1: fused bottleneck launch
+    int kind = 0;          // 0: conv_kernel launch, 1: fused bottleneck launch, 2: fused upsampling block
     ConvArgs a;
     int nr = 0, epi = 0;
     BneckArgs bn;
+    UpArgs up;
+    int up_cin = 0, up_it = 0, up_cout = 0;
     int bn_c = 0, bn_var = 0;
     bool bn_asym = false;
     double bytes = 0, flops = 0;
@@ -66,6 +68,7 @@ struct Op {
     Op() {
         std::memset(&a, 0, sizeof(a));
         std::memset(&bn, 0, sizeof(bn));
+        std::memset(&up, 0, sizeof(up));
     }
 };
 
@@ -454,21 +457,24 @@ bool pack_all(bugseg_ctx *ctx, std::string &why) {
             if (!why.empty()) return false;
             add(t);
             add(pack_conv(pk, u2, cstore(ut.cout), &b.extra[0]));
-            // main 1x1 + extension 1x1 merged into one launch over the block input (ids 4, 5: the pair
-            // and the tconv reading the extension half of its output) when the pair's output keeps a
-            // power-of-two count of 16-B chunks per pixel (the conv epilogue's staged stores) and
-            // both halves fold their bias the same way (bias_in_acc); bit-identical per channel
+            // ids 4 (and 5): the main 1x1 and the extension 1x1 packed as ONE matrix over the block
+            // input (rows: main then extension, each with its own folded BN and slope). Used by the
+            // fused upsampling kernel (up_kernels.hip), or, where that kernel is not built for the
+            // shape, as one conv launch whose output the tconv reads from channel cout on (id 5) —
+            // that needs a power-of-two count of 16-B chunks per pixel (the conv epilogue's staged
+            // stores). Both require the two halves to fold their bias the same way (bias_in_acc).
             const int es = ctx->prec == PREC_BF16 ? 2 : 4, mc = cstore(um.cout) + cstore(u1.cout);
             const int chunks = mc * es / 16;
             const int nr_pair = pow2_nr(round_up(um.cout, 16) + round_up(u1.cout, 16));
             auto bias_acc = [](int nr) { return nr < 8; };     // mfma_common.h bias_in_acc
-            if (um.cout % 16 == 0 && (chunks & (chunks - 1)) == 0 && nr_pair <= 8 && um.eps == u1.eps &&
-                bias_acc(nr_pair) == bias_acc(pow2_nr(round_up(um.cout, 16))) &&
-                bias_acc(nr_pair) == bias_acc(pow2_nr(round_up(u1.cout, 16))) && !std::getenv("BUGSEG_NO_PAIR")) {
+            const bool same_bias = bias_acc(pow2_nr(round_up(um.cout, 16))) && bias_acc(pow2_nr(round_up(u1.cout, 16)));
+            if (um.cout % 16 == 0 && u1.cout % 16 == 0 && um.eps == u1.eps && same_bias) {
                 add(pack_conv_pair(pk, um, u1, cstore(cin)));
-                Packed t2 = pack_tconv(pk, ut, mc, why, cstore(um.cout));
-                if (!why.empty()) return false;
-                add(t2);
+                if ((chunks & (chunks - 1)) == 0 && nr_pair <= 8 && bias_acc(nr_pair) && !std::getenv("BUGSEG_NO_PAIR")) {
+                    Packed t2 = pack_tconv(pk, ut, mc, why, cstore(um.cout));
+                    if (!why.empty()) return false;
+                    add(t2);
+                }
             }
             cur_c = cout;
             break;
@@ -757,6 +763,51 @@ struct Walker {
                 szM = std::max(szM, tbytes(sm));
                 szT = std::max({szT, tbytes(s1), tbytes(st)});
                 szX = std::max(szX, tbytes(so));
+                const int cin_b = b.attrs[0], cout_b = b.attrs[1], it_b = P(1).cout;
+                const char *nf = std::getenv("BUGSEG_NO_FUSE");
+                const bool fuse_up = ids.size() >= 5 && up_supported(cin_b, it_b, cout_b) && cur.C == cin_b &&
+                                     so.C == cout_b && !(nf && *nf && *nf != '0');
+                if (fuse_up) {
+                    // one launch: x read once, out written once, everything else in registers
+                    if (fill) {
+                        Op op;
+                        op.kind = 2;
+                        op.up_cin = cin_b; op.up_it = it_b; op.up_cout = cout_b;
+                        UpArgs &q = op.up;
+                        const unsigned char *dw = (const unsigned char *)ctx->dev_w;
+                        const Packed &p1 = P(4), &p2 = P(2), &p3 = P(3);
+                        q.x = curp; q.idx = idx[ref]; q.out = dst;
+                        q.M = B * cur.H * cur.W; q.h = cur.H; q.w = cur.W;
+                        q.idxCS = cstore(ctx->blocks[ref].attrs[0]);
+                        fastdiv((uint32_t)(cur.H * cur.W), q.mHW, q.sHW);
+                        fastdiv((uint32_t)cur.W, q.mW, q.sW);
+                        q.w1 = dw + p1.o_w; q.b1 = (const float *)(dw + p1.o_bias); q.s1 = (const float *)(dw + p1.o_s1);
+                        q.w2 = dw + p2.o_w; q.b2 = (const float *)(dw + p2.o_bias); q.s2 = (const float *)(dw + p2.o_s1);
+                        q.w3 = dw + p3.o_w; q.b3 = (const float *)(dw + p3.o_bias); q.s3 = (const float *)(dw + p3.o_s1);
+                        q.s_out = (const float *)(dw + p3.o_s2);
+                        q.x_bytes = (uint32_t)std::min<size_t>((size_t)B * cur.H * cur.W * cur.C * es, 0x7fffffff);
+                        q.idx_bytes = (uint32_t)std::min<size_t>((size_t)B * cur.H * cur.W * q.idxCS, 0x7fffffff);
+                        q.out_bytes = (uint32_t)std::min<size_t>((size_t)B * so.H * so.W * so.C * es, 0x7fffffff);
+                        q.slopes_le1 = 1;
+                        const std::pair<size_t, int> sl[] = {{p1.o_s1, p1.Npad}, {p2.o_s1, p2.Npad}, {p3.o_s1, p3.Npad},
+                                                             {p3.o_s2, p3.Npad}};
+                        for (const auto &v : sl) {
+                            const float *f = (const float *)(ctx->host_w.data() + v.first);
+                            for (int c = 0; c < v.second; ++c)
+                                if (!(f[c] <= 1.f)) q.slopes_le1 = 0;
+                        }
+                        const double px = (double)B * cur.H * cur.W;
+                        double wb = 0, fl = 0;
+                        for (int i = 0; i < 4; ++i) { wb += (double)P(i).Npad * P(i).Kpad * es; fl += 2.0 * P(i).macs_per_px * px; }
+                        op.flops = fl;
+                        op.bytes = px * cur.C * es + px * q.idxCS + 4.0 * px * so.C * es + wb;   // x + idx in, out
+                        op.layer_bytes = px * cur.C * es * 2 + px * (sm.C + s1.C) * es + px * s1.C * es + 4.0 * px * st.C * es * 2 +
+                                         px * sm.C * es + px * q.idxCS + 4.0 * px * so.C * es + wb;
+                        ops.push_back(op);
+                    }
+                    cur = so;
+                    break;
+                }
                 const bool pair = ids.size() == 6;
                 // paired: the main and extension 1x1 outputs share one tensor (main channels first)
                 Shape sp{cur.H, cur.W, pair ? sm.C + s1.C : sm.C};
@@ -1052,6 +1103,7 @@ static int enet_forward(bugseg_ctx *ctx, const void *in, bool bgr, int B, int H,
     for (size_t i = 0; i < pl.ops.size(); ++i) {
         const Op &op = pl.ops[i];
         hipError_t e = op.kind == 1 ? launch_bneck(ctx->prec, op.bn_c, op.bn_asym, op.bn_var, op.bn, (hipStream_t)stream)
+                     : op.kind == 2 ? launch_up(ctx->prec, op.up_cin, op.up_it, op.up_cout, op.up, (hipStream_t)stream)
                                     : launch_conv(ctx->prec, op.nr, op.epi, op.a, (hipStream_t)stream);
         if (e != hipSuccess) return fail(ctx, BUGSEG_EHIP, "conv launch " + std::to_string(i) + ": " + hipGetErrorString(e));
     }
@@ -1260,7 +1312,9 @@ int bugseg_plan_op(bugseg_ctx *ctx, int B, int H, int W, int op, char *kernel, i
     if (op < 0 || op >= (int)pl.ops.size()) return fail(ctx, BUGSEG_EINVAL, "op index out of range");
     const Op &o = pl.ops[op];
     std::string tag;
-    if (o.kind == 1) {
+    if (o.kind == 2) {
+        tag = "up C" + std::to_string(o.up_cout);
+    } else if (o.kind == 1) {
         int th, tw, nw;
         bneck_shape(o.bn_c, o.bn_var, th, tw, nw, nullptr);
         tag = "bneck C" + std::to_string(o.bn_c) + (o.bn_asym ? " asym" : "") + " " + std::to_string(th) + "x" +
@@ -1299,6 +1353,7 @@ int bugseg_plan_launch_op(bugseg_ctx *ctx, int B, int H, int W, int op, void *st
     DeviceGuard g(ctx->device);
     const Op &o = pl.ops[op];
     hipError_t e = o.kind == 1 ? launch_bneck(ctx->prec, o.bn_c, o.bn_asym, o.bn_var, o.bn, (hipStream_t)stream)
+                 : o.kind == 2 ? launch_up(ctx->prec, o.up_cin, o.up_it, o.up_cout, o.up, (hipStream_t)stream)
                                : launch_conv(ctx->prec, o.nr, o.epi, o.a, (hipStream_t)stream);
     if (e != hipSuccess) return fail(ctx, BUGSEG_EHIP, "launch of op " + std::to_string(op) + ": " + hipGetErrorString(e));
     return BUGSEG_OK;

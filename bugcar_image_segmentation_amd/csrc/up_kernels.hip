@@ -1,0 +1,254 @@
+// Fused ENet upsampling bottleneck in ONE launch, entirely in registers.
+//
+//   main = BN(W_m . x)                       1x1 Cin -> Cout         (no activation)
+//   e1   = act(W_e1 . x + b)                  1x1 Cin -> I            (I = Cin / 4)
+//   t    = act(tconv2x2_s2(e1))               I -> I, 4 output phases (a, b)
+//   out  = act_out(act(W_e2 . t + b) + unpool(main, idx))
+//
+// A 2x2 stride-2 transposed convolution maps each input pixel to exactly one 2x2 output block, and
+// every other op here is per pixel, so the block is pointwise in the INPUT grid: a wave takes 16
+// input pixels and produces their 64 output pixels with no halo and no LDS traffic beyond the
+// weights. Unfused it is 3-4 launches that write and re-read the main tensor, e1 and the 4x larger
+// t (up5 at 640x480: 12.5 MB/frame); fused it reads x and the pooling indices once and writes out
+// once (5.2 MB/frame).
+//
+// MFMA mapping as conv_kernels.hip (A = weights, rows = output channels; B = 8 channels of one pixel
+// per lane; accumulator quad = 4 channels of one pixel). An intermediate goes from accumulator
+// quads to the next GEMM's B operand with two lane permutations: v_permlane32_swap then
+// v_permlane16_swap turn the quads of two 16-channel row fragments into each lane's 8 consecutive
+// channels (see to_bop). Every intermediate is rounded to the storage type exactly where the unfused
+// launches store it, and each GEMM adds its bias where the unfused launch with that row count does
+// (bias_in_acc), so the fused block is bit-identical to the unfused plan.
+#include "bugseg_internal.h"
+#include "mfma_common.h"
+
+namespace bugseg {
+
+__device__ __forceinline__ void pl32swap(uint32_t &a, uint32_t &b) {
+    const u32x2_t r = __builtin_amdgcn_permlane32_swap(a, b, false, false);
+    a = r.x;
+    b = r.y;
+}
+
+// storage rounding of an activation (the unfused plan stores it as T and reads it back)
+__device__ __forceinline__ float4 round_t(float4 v, const __bf16 *) { return unpack_bf16x4(pack_bf16x4(v)); }
+__device__ __forceinline__ float4 round_t(float4 v, const float *) { return v; }
+
+// Two 16-channel row fragments (quads qa, qb: lane kq holds channels 4kq..4kq+3 of each) -> the B
+// operand of one 32-channel k-step (lane kq holds channels 8kq..8kq+7):
+//   permlane32_swap: lanes kq 2,3 of qa <- lanes kq 0,1 of qb, lanes kq 0,1 of qb <- kq 2,3 of qa;
+//   permlane16_swap: odd rows of qa' <-> even rows of qb'.
+// Afterwards lane kq holds (qa'', qb'') = channels 8kq..8kq+3 and 8kq+4..8kq+7 (measured semantics:
+// scripts/permlane_probe.hip). qb == 0 for a single fragment (k groups 2, 3 zero).
+__device__ __forceinline__ void to_bop(RawB &r, float4 qa, float4 qb) {
+    const u32x2_t a = pack_bf16x4(qa), b = pack_bf16x4(qb);
+    uint32_t a0 = a.x, a1 = a.y, b0 = b.x, b1 = b.y;
+    pl32swap(a0, b0);
+    pl32swap(a1, b1);
+    pl16swap(a0, b0);
+    pl16swap(a1, b1);
+    r.v = make_uint4(a0, a1, b0, b1);
+}
+__device__ __forceinline__ void to_bop(RawF &r, float4 qa, float4 qb) {
+    uint32_t a[4] = {__float_as_uint(qa.x), __float_as_uint(qa.y), __float_as_uint(qa.z), __float_as_uint(qa.w)};
+    uint32_t b[4] = {__float_as_uint(qb.x), __float_as_uint(qb.y), __float_as_uint(qb.z), __float_as_uint(qb.w)};
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+        pl32swap(a[i], b[i]);
+        pl16swap(a[i], b[i]);
+    }
+    r.a = make_float4(__uint_as_float(a[0]), __uint_as_float(a[1]), __uint_as_float(a[2]), __uint_as_float(a[3]));
+    r.b = make_float4(__uint_as_float(b[0]), __uint_as_float(b[1]), __uint_as_float(b[2]), __uint_as_float(b[3]));
+}
+
+template <typename T, int CIN, int I, int COUT>
+__global__ void __launch_bounds__(256, (sizeof(T) == 2 ? (CIN >= 128 ? 2 : 3) : 1)) up_kernel(const UpArgs a) {
+    using Raw = typename Tr<T>::Raw;
+    constexpr int ES = (int)sizeof(T);
+    constexpr int NR1 = (COUT + I) / 16;              // GEMM 1 rows: main then e1
+    constexpr int NM = COUT / 16, NE = I / 16;        // row fragments of main / e1 (per tconv phase)
+    constexpr int KS1 = CIN / 32;                     // GEMM 1 k-steps
+    constexpr int NR2 = 4 * I / 16;                   // tconv rows (4 phases)
+    constexpr int NR3 = COUT / 16;                    // expansion rows
+    static_assert(COUT % 16 == 0 && I % 16 == 0 && CIN % 32 == 0 && I <= 32, "up_kernel shape");
+    constexpr bool SWAP = ES == 2 && NR3 % 2 == 0;    // 16-B output chunks by lane-pair swaps (bneck phase 3)
+    // bias placement of the unfused launches (bias_in_acc of their row counts): the main and e1
+    // 1x1s both accumulate from the bias (the host plans this kernel only then), the tconv and the
+    // expansion as their own row counts say
+    static_assert(NM <= 4 && NE <= 4, "main / e1 launches must carry their bias in the accumulator");
+    constexpr bool B1ACC = true;
+    constexpr bool B2ACC = bias_in_acc(NR2), B3ACC = bias_in_acc(NR3);
+    // LDS: weights of the three GEMMs (+16 B row pad) and their per-row constants
+    constexpr int K1S = CIN + 16 / ES, K2S = 32 + 16 / ES, K3S = 32 + 16 / ES;
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+    T *w1 = reinterpret_cast<T *>(smem);
+    T *w2 = w1 + NR1 * 16 * K1S;
+    T *w3 = w2 + NR2 * 16 * K2S;
+    float *cb1 = reinterpret_cast<float *>(w3 + NR3 * 16 * K3S), *cs1 = cb1 + NR1 * 16;
+    float *cb2 = cs1 + NR1 * 16, *cs2 = cb2 + NR2 * 16;
+    float *cb3 = cs2 + NR2 * 16, *cs3 = cb3 + NR3 * 16, *cso = cs3 + NR3 * 16;
+    const int tid = threadIdx.x;
+    {
+        auto stage = [&](T *dst, const void *src, int rows, int kpad, int kstride) {
+            const int cpr = kpad * ES / 16;
+            const uint4 *s = reinterpret_cast<const uint4 *>(src);
+            for (int i = tid; i < rows * cpr; i += 256) {
+                const int r = i / cpr, c = i - r * cpr;
+                *reinterpret_cast<uint4 *>(reinterpret_cast<unsigned char *>(dst + (size_t)r * kstride) + c * 16) = s[i];
+            }
+        };
+        stage(w1, a.w1, NR1 * 16, CIN, K1S);           // pair pack: K = CIN exactly (1x1, CinS = CIN)
+        stage(w2, a.w2, NR2 * 16, 32, K2S);
+        stage(w3, a.w3, NR3 * 16, 32, K3S);
+        for (int i = tid; i < NR1 * 16; i += 256) { cb1[i] = a.b1[i]; cs1[i] = a.s1[i]; }
+        for (int i = tid; i < NR2 * 16; i += 256) { cb2[i] = a.b2[i]; cs2[i] = a.s2[i]; }
+        for (int i = tid; i < NR3 * 16; i += 256) { cb3[i] = a.b3[i]; cs3[i] = a.s3[i]; cso[i] = a.s_out[i]; }
+    }
+    __syncthreads();
+    const int lane = tid & 63, col = lane & 15, kq = lane >> 4;
+    const bool fast = a.slopes_le1;
+    auto act = [&](float4 v, const float *s) { return fast ? prelu4m(v, ld4f(s)) : prelu4(v, ld4f(s)); };
+    const auto rx = mkbuf(a.x, a.x_bytes);
+    const auto ri = mkbuf(a.idx, a.idx_bytes);
+    const auto ro = mkbuf(a.out, a.out_bytes);
+    const int hw = a.h * a.w;
+    const int nfrag = (a.M + 15) >> 4;
+    const int gw = blockIdx.x * 4 + __builtin_amdgcn_readfirstlane(tid >> 6), nw = gridDim.x * 4;
+
+    for (int f = gw; f < nfrag; f += nw) {
+        const int p = f * 16 + col;
+        const bool pv = p < a.M;
+        const uint32_t pp = pv ? (uint32_t)p : 0u;
+        const int n = (int)fdiv(pp, a.mHW, a.sHW), rr = (int)pp - n * hw;
+        const int y = (int)fdiv((uint32_t)rr, a.mW, a.sW), x = rr - y * a.w;
+
+        // ---- GEMM 1: [main; e1] = W1 . x  (the block input read once, 16 B per lane per k-step)
+        Raw xf[KS1];
+#pragma unroll
+        for (int s = 0; s < KS1; ++s) bld8(xf[s], rx, pv ? (uint32_t)(p * CIN + s * 32 + kq * 8) * ES : OOB);
+        // pooling indices of this pixel's main channels (one byte per channel: window position)
+        uint32_t id[NM];
+#pragma unroll
+        for (int r = 0; r < NM; ++r)
+            id[r] = __builtin_amdgcn_raw_buffer_load_b32(ri, pv ? (int)(p * a.idxCS + r * 16 + kq * 4) : (int)OOB, 0, 0);
+        f32x4 acc1[NR1];
+#pragma unroll
+        for (int r = 0; r < NR1; ++r) acc1[r] = B1ACC ? bias4(cb1 + r * 16 + kq * 4) : (f32x4){0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int s = 0; s < KS1; ++s)
+#pragma unroll
+            for (int r = 0; r < NR1; ++r) {
+                Raw wf;
+                ld8(wf, w1 + (r * 16 + col) * K1S + s * 32 + kq * 8);
+                mma(acc1[r], wf, xf[s]);
+            }
+        auto ep1 = [&](int r) {
+            const int c = r * 16 + kq * 4;
+            return round_t(act(B1ACC ? f4(acc1[r]) : add4(f4(acc1[r]), ld4f(cb1 + c)), cs1 + c), (const T *)nullptr);
+        };
+        float4 mv[NM];
+#pragma unroll
+        for (int r = 0; r < NM; ++r) mv[r] = ep1(r);
+        Raw bop2;
+        to_bop(bop2, ep1(NM), NE > 1 ? ep1(NM + 1) : make_float4(0.f, 0.f, 0.f, 0.f));
+
+        // ---- per output phase (a, b): t = act(tconv) -> expansion -> + unpooled main -> act -> store
+        const uint32_t obase = pv ? (uint32_t)((n * 2 * a.h + 2 * y) * (2 * a.w) + 2 * x) : 0u;   // output pixel (2y, 2x)
+        // (not unrolled: one phase's weight fragments live at a time)
+#pragma unroll 1
+        for (int ph = 0; ph < 4; ++ph) {
+            f32x4 acc2[NE];
+#pragma unroll
+            for (int e = 0; e < NE; ++e) {
+                const int r2 = ph * NE + e;
+                acc2[e] = B2ACC ? bias4(cb2 + r2 * 16 + kq * 4) : (f32x4){0.f, 0.f, 0.f, 0.f};
+                Raw wf;
+                ld8(wf, w2 + (r2 * 16 + col) * K2S + kq * 8);
+                mma(acc2[e], wf, bop2);
+            }
+            auto ep2 = [&](int e) {
+                const int c = (ph * NE + e) * 16 + kq * 4;
+                return round_t(act(B2ACC ? f4(acc2[e]) : add4(f4(acc2[e]), ld4f(cb2 + c)), cs2 + c), (const T *)nullptr);
+            };
+            Raw bop3;
+            to_bop(bop3, ep2(0), NE > 1 ? ep2(1) : make_float4(0.f, 0.f, 0.f, 0.f));
+            const uint32_t opix = obase + (uint32_t)((ph >> 1) * 2 * a.w + (ph & 1));
+            auto ep3 = [&](int r) {
+                const int c = r * 16 + kq * 4;
+                f32x4 acc = B3ACC ? bias4(cb3 + c) : (f32x4){0.f, 0.f, 0.f, 0.f};
+                Raw wf;
+                ld8(wf, w3 + (r * 16 + col) * K3S + kq * 8);
+                mma(acc, wf, bop3);
+                float4 v = act(B3ACC ? f4(acc) : add4(f4(acc), ld4f(cb3 + c)), cs3 + c);
+                // MaxUnpool2d(2): the main value lands where its pooling index points
+                const uint32_t w = id[r];
+                const uint32_t pos = (uint32_t)ph;
+                v.x += ((w & 0xff) == pos) ? mv[r].x : 0.f;
+                v.y += (((w >> 8) & 0xff) == pos) ? mv[r].y : 0.f;
+                v.z += (((w >> 16) & 0xff) == pos) ? mv[r].z : 0.f;
+                v.w += (((w >> 24) & 0xff) == pos) ? mv[r].w : 0.f;
+                return act(v, cso + c);
+            };
+            if constexpr (SWAP) {
+#pragma unroll
+                for (int t = 0; t < NR3 / 2; ++t) {
+                    const u32x2_t p0 = pack_bf16x4(ep3(2 * t)), p1 = pack_bf16x4(ep3(2 * t + 1));
+                    uint32_t x0 = p0.x, x1 = p0.y, y0 = p1.x, y1 = p1.y;
+                    pl16swap(x0, y0);
+                    pl16swap(x1, y1);
+                    const int ch = (2 * t + (kq & 1)) * 16 + 8 * (kq >> 1);
+                    bst16(ro, pv ? (opix * COUT + ch) * ES : OOB, make_uint4(x0, x1, y0, y1));
+                }
+            } else {
+#pragma unroll
+                for (int r = 0; r < NR3; ++r) {
+                    const float4 v = ep3(r);
+                    const uint32_t off = pv ? (opix * COUT + r * 16 + kq * 4) * ES : OOB;
+                    if constexpr (ES == 2) __builtin_amdgcn_raw_buffer_store_b64(pack_bf16x4(v), ro, (int)off, 0, 0);
+                    else bst16(ro, off, __builtin_bit_cast(uint4, v));
+                }
+            }
+        }
+    }
+}
+
+template <typename T, int CIN, int I, int COUT>
+static size_t up_lds() {
+    constexpr int ES = (int)sizeof(T);
+    constexpr int NR1 = (COUT + I) / 16, NR2 = 4 * I / 16, NR3 = COUT / 16;
+    return (size_t)(NR1 * 16 * (CIN + 16 / ES) + NR2 * 16 * (32 + 16 / ES) + NR3 * 16 * (32 + 16 / ES)) * ES +
+           (size_t)(2 * NR1 * 16 + 2 * NR2 * 16 + 3 * NR3 * 16) * sizeof(float);
+}
+
+bool up_supported(int cin, int it, int cout) {
+    return (cin == 128 && it == 32 && cout == 64) || (cin == 64 && it == 16 && cout == 16);
+}
+
+template <int CI, int II, int CO>
+static hipError_t launch_shape(int prec, const UpArgs &a, dim3 g, hipStream_t s) {
+    if (prec == PREC_BF16) {
+        const size_t lds = up_lds<__bf16, CI, II, CO>();
+        hipLaunchKernelGGL((up_kernel<__bf16, CI, II, CO>), g, dim3(256), lds, s, a);
+    } else {
+        const size_t lds = up_lds<float, CI, II, CO>();
+        if (lds > 64 * 1024) {
+            hipError_t e = hipFuncSetAttribute((const void *)up_kernel<float, CI, II, CO>,
+                                               hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+            if (e != hipSuccess) return e;
+        }
+        hipLaunchKernelGGL((up_kernel<float, CI, II, CO>), g, dim3(256), lds, s, a);
+    }
+    return hipGetLastError();
+}
+
+hipError_t launch_up(int prec, int cin, int it, int cout, const UpArgs &a, hipStream_t s) {
+    const int nfrag = (a.M + 15) / 16;
+    int g = (nfrag + 3) / 4;
+    if (g > 2048) g = 2048;
+    if (g < 1) g = 1;
+    if (cin == 128 && it == 32 && cout == 64) return launch_shape<128, 32, 64>(prec, a, dim3(g), s);
+    if (cin == 64 && it == 16 && cout == 16) return launch_shape<64, 16, 16>(prec, a, dim3(g), s);
+    return hipErrorInvalidValue;
+}
+
+}  // namespace bugseg

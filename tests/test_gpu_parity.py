@@ -255,6 +255,7 @@ def test_fused_bottlenecks_equal_unfused(gpu, blocks, prec, H, W, variant, monke
     n_fused = fused.ctx.plan_info(B, H, W, N.OUT_LOGITS_F32)[0]
     n_plain = plain.ctx.plan_info(B, H, W, N.OUT_LOGITS_F32)[0]
     assert n_plain == 88 and n_fused < n_plain      # 89 convolutions; the up5 main + extension 1x1 pair is one launch
+    # (BUGSEG_NO_FUSE also turns off the fused upsampling blocks: this compares them too)
     assert torch.equal(a, b)
 
 
@@ -265,10 +266,12 @@ def test_up_block_pair_equals_separate(gpu, blocks, prec, monkeypatch):
     launches (BUGSEG_NO_PAIR=1)."""
     H, W = 120, 160
     bgr = torch.from_numpy(synthetic.road_frames(2, H, W, seed=4)).cuda()
+    monkeypatch.setenv("BUGSEG_NO_FUSE", "1")
     paired = ENET(weights=blocks, precision=prec)
     a = torch.empty((2, 15, H, W), dtype=torch.float32, device=gpu)
     paired.ctx.forward_bgr(bgr, 2, H, W, N.OUT_LOGITS_F32, a)
     monkeypatch.setenv("BUGSEG_NO_PAIR", "1")
+    monkeypatch.setenv("BUGSEG_NO_FUSE", "1")        # (the fused upsampling kernel would take both)
     sep = ENET(weights=blocks, precision=prec)
     b = torch.empty_like(a)
     sep.ctx.forward_bgr(bgr, 2, H, W, N.OUT_LOGITS_F32, b)
