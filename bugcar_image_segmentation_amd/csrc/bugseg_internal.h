@@ -67,6 +67,10 @@ hipError_t launch_conv(int prec, int nr, int epi, const ConvArgs &a, hipStream_t
 int conv_tile_pixels(int nr);
 size_t conv_lds_bytes(int prec, const ConvArgs &a);
 
+// ---- class layer (cls_kernels.hip): EPI_CLASSES launches with 16 input channels land here.
+bool cls_supported(const ConvArgs &a);
+hipError_t launch_cls(int prec, const ConvArgs &a, hipStream_t s);
+
 // ---- initial block (init_kernels.hip): EPI_INIT / EPI_INIT_BGR launches of launch_conv land here.
 // Requires the initial block's shape (3x3 s2 p1 conv of 3 channels packed as tap*8 + c, pool_k 2|3).
 hipError_t launch_init(int prec, bool bgr, const ConvArgs &a, hipStream_t s);

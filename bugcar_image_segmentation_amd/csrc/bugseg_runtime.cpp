@@ -1322,6 +1322,7 @@ int bugseg_plan_op(bugseg_ctx *ctx, int B, int H, int W, int op, char *kernel, i
         (void)nw;
     }
     else if (o.epi == EPI_INIT || o.epi == EPI_INIT_BGR) tag = "init";
+    else if (o.epi == EPI_CLASSES && cls_supported(o.a) && !std::getenv("BUGSEG_CLS_CONV")) tag = "classes";
     else tag = "conv NR" + std::to_string(o.nr) + " E" + std::to_string(o.epi);
     if (kernel && kernel_len > 0) {
         std::strncpy(kernel, tag.c_str(), (size_t)kernel_len - 1);

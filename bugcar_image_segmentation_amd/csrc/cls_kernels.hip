@@ -1,0 +1,232 @@
+// The class layer: ENet's final transposed convolution (16 -> ncls, stride 2) + argmax + class LUT,
+// i.e. the tail of the reference's sess.run + tf.math.argmax (models.py:43-58), in one streaming
+// kernel (EPI_CLASSES launches of launch_conv land here when the layer has 16 input channels).
+//
+// GEMM view as conv_kernels.hip: a column is one input pixel, K = (tap of the 2x2 input
+// neighbourhood, channel), rows = (output phase, class). The MFMA is v_mfma_f32_32x32x16_bf16
+// (fp32 parity mode: 8 x v_mfma_f32_32x32x2_f32 per tap, one per channel pair): its accumulator gives
+// lane (col, h) the 16 rows {8j + 4h + i}. Rows are permuted (the weights are gathered with the
+// permutation, nothing is repacked) so that those 16 rows are the 16 classes of ONE output phase:
+//   block b (two per column), lane half h  ->  phase 2b + h = output pixel (2y + b, 2x + h),
+//   accumulator register c                 ->  class c.
+// The argmax is therefore a scan of one lane's own registers — no staging, no cross-lane traffic — and
+// one v_permlane32_swap pairs each lane with the horizontally adjacent output pixel for 2-byte stores.
+//
+// The whole layer's weights (64 rows x 4 taps x 16 channels) live in 32 VGPRs per lane for the
+// kernel's lifetime; the only per-pixel traffic is the B fragments (one 16-B load per lane and tap,
+// the next group's loads in flight while the current group computes) and the class bytes.
+#include "bugseg_internal.h"
+#include "mfma_common.h"
+
+namespace bugseg {
+
+typedef float f32x16 __attribute__((ext_vector_type(16)));
+
+__device__ __forceinline__ void mma32(f32x16 &acc, const RawB &w, const RawB &x) {
+    acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(bf16x8, w.v), __builtin_bit_cast(bf16x8, x.v),
+                                                  acc, 0, 0, 0);
+}
+// fp32: sub-MFMA j contracts element j of both lane halves (channels j and 8 + j of the tap)
+__device__ __forceinline__ void mma32(f32x16 &acc, const RawF &w, const RawF &x) {
+    acc = __builtin_amdgcn_mfma_f32_32x32x2f32(w.a.x, x.a.x, acc, 0, 0, 0);
+    acc = __builtin_amdgcn_mfma_f32_32x32x2f32(w.a.y, x.a.y, acc, 0, 0, 0);
+    acc = __builtin_amdgcn_mfma_f32_32x32x2f32(w.a.z, x.a.z, acc, 0, 0, 0);
+    acc = __builtin_amdgcn_mfma_f32_32x32x2f32(w.a.w, x.a.w, acc, 0, 0, 0);
+    acc = __builtin_amdgcn_mfma_f32_32x32x2f32(w.b.x, x.b.x, acc, 0, 0, 0);
+    acc = __builtin_amdgcn_mfma_f32_32x32x2f32(w.b.y, x.b.y, acc, 0, 0, 0);
+    acc = __builtin_amdgcn_mfma_f32_32x32x2f32(w.b.z, x.b.z, acc, 0, 0, 0);
+    acc = __builtin_amdgcn_mfma_f32_32x32x2f32(w.b.w, x.b.w, acc, 0, 0, 0);
+}
+
+__device__ __forceinline__ bool nonzero(const RawB &r) { return (r.v.x | r.v.y | r.v.z | r.v.w) != 0u; }
+__device__ __forceinline__ bool nonzero(const RawF &r) {
+    const uint4 u = __builtin_bit_cast(uint4, r.a), v = __builtin_bit_cast(uint4, r.b);
+    return (u.x | u.y | u.z | u.w | v.x | v.y | v.z | v.w) != 0u;
+}
+
+// Taps: the 2x2 input neighbourhood (dy, dx) = (s >> 1, s & 1) of the k = 3 layer in pack_tconv's
+// order (D = {0, 1}, tap = ty * 2 + tx). LOGITS: the fp32 logits are written too (parity runs).
+template <typename T, bool LOGITS>
+__global__ void __launch_bounds__(256, sizeof(T) == 2 ? 4 : 1) cls_kernel(const ConvArgs a) {
+    constexpr int CLS_TAPS = 4;
+    using Raw = typename Tr<T>::Raw;
+    constexpr int ES = (int)sizeof(T);
+    __shared__ float sbias[64];
+    __shared__ int slut[16];
+    const int tid = threadIdx.x, lane = tid & 63, col = lane & 31, h = lane >> 5;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    if (tid < 64) sbias[tid] = a.bias[tid];
+    if (tid < 16) slut[tid] = a.lut ? (int)a.lut[tid] : tid;
+
+    // weights: block b, row r = lane's col -> packed row (phase 2b + ((r >> 2) & 1), class 4 (r >> 3) + (r & 3));
+    // this lane's k half = channels 8h .. 8h + 7 of each tap
+    Raw wr[2][CLS_TAPS];
+    {
+        const T *w = reinterpret_cast<const T *>(a.w);
+#pragma unroll
+        for (int b = 0; b < 2; ++b) {
+            const int prow = (2 * b + ((col >> 2) & 1)) * 16 + 4 * (col >> 3) + (col & 3);
+#pragma unroll
+            for (int s = 0; s < CLS_TAPS; ++s) {
+                ld8(wr[b][s], w + (size_t)prow * a.Kpad + s * 16 + 8 * h);
+            }
+        }
+    }
+    // A block whose dy = 1 taps (s = 2, 3) have all-zero weights skips them: output row 2y of the 3x3
+    // transposed kernel never sees input row y + 1 (a wave-uniform choice, made once)
+    bool short_blk[2];
+#pragma unroll
+    for (int b = 0; b < 2; ++b) short_blk[b] = __ballot(nonzero(wr[b][2]) || nonzero(wr[b][3])) == 0;
+    __syncthreads();
+
+    float cmask[16];                                  // 0 for a class of the model, -inf for padding
+#pragma unroll
+    for (int c = 0; c < 16; ++c) cmask[c] = c < a.ncls ? 0.f : -INFINITY;
+    const auto rin = mkbuf(a.in, a.in_bytes);
+    const int HWg = a.Hg * a.Wg;
+    const size_t plane = (size_t)a.Hout * a.Wout;
+    const int groups = (a.M + 31) >> 5;
+    // XCD-aware: XCD x = blockIdx % 8 walks the contiguous run [x*C, (x+1)*C) of 32-pixel groups, its
+    // waves interleaved over it
+    const int xcd = blockIdx.x & 7, nw = (gridDim.x >> 3) * 4, wi = (blockIdx.x >> 3) * 4 + wave;
+    const int C = (groups + 7) >> 3, g0 = xcd * C, g1 = g0 + C < groups ? g0 + C : groups;
+    // tap s is a wave-uniform byte delta (the buffer load's scalar offset) from the lane's pixel,
+    // valid where x + dx < Win and y + dy < Hin
+    const uint32_t pixB = (uint32_t)(a.CinS * ES), rowB = (uint32_t)a.Win * pixB;
+
+    // lane pixel of group g: the group's first pixel is divided out on the scalar unit (g is
+    // wave-uniform; Hg * Wg, Wg >= 32 > 1), each lane then steps at most one row on
+    struct Px { int n, y, x; bool ok; };
+    auto pixel = [&](int g) -> Px {
+        const uint32_t p0 = (uint32_t)g * 32u;
+        const int n0 = (int)(__umulhi(p0, a.mHWg) >> a.sHWg);
+        const uint32_t r = p0 - (uint32_t)(n0 * HWg);
+        const int y0 = (int)(__umulhi(r, a.mWg) >> a.sWg), x0 = (int)r - y0 * a.Wg;
+        Px q;
+        q.ok = (int)p0 + col < a.M;
+        q.x = x0 + col;
+        const bool wrap = q.x >= a.Wg;
+        q.x = wrap ? q.x - a.Wg : q.x;
+        q.y = y0 + (wrap ? 1 : 0);
+        const bool wrapn = q.y >= a.Hg;
+        q.y = wrapn ? 0 : q.y;
+        q.n = n0 + (wrapn ? 1 : 0);
+        return q;
+    };
+    auto load = [&](int g, Raw (&xf)[CLS_TAPS]) {
+        const Px q = pixel(g);
+        const uint32_t base = (uint32_t)((q.n * a.Hin + q.y) * a.Win + q.x) * pixB + (uint32_t)(8 * h * ES);
+        const bool okx = q.x + 1 < a.Win, oky = q.y + 1 < a.Hin;
+        const int v00 = (int)(q.ok ? base : OOB), v01 = (int)(q.ok && okx ? base : OOB);
+        const int v10 = (int)(q.ok && oky ? base : OOB), v11 = (int)(q.ok && okx && oky ? base : OOB);
+        const int vo[CLS_TAPS] = {v00, v01, v10, v11};
+#pragma unroll
+        for (int s = 0; s < CLS_TAPS; ++s) {
+            const int d = (int)((uint32_t)(s >> 1) * rowB + (uint32_t)(s & 1) * pixB);
+            if constexpr (sizeof(T) == 2) {
+                xf[s].v = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(rin, vo[s], d, 0));
+            } else {
+                reinterpret_cast<RawF &>(xf[s]).a =
+                    __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(rin, vo[s], d, 0));
+                reinterpret_cast<RawF &>(xf[s]).b =
+                    __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(rin, vo[s], d + 16, 0));
+            }
+        }
+    };
+
+    // one group: MFMAs, argmax, stores; `nxt` first receives the next group's loads (they fly during
+    // this one; the two buffers alternate by unrolling, never by a runtime index)
+    auto step = [&](int g, const Raw (&cur)[CLS_TAPS], Raw (&nxt)[CLS_TAPS]) {
+        if (g + nw < g1) load(g + nw, nxt);
+        const Px q = pixel(g);
+        int cls[2];
+        // one 32-row block at a time (16 accumulator VGPRs live)
+#pragma unroll
+        for (int b = 0; b < 2; ++b) {
+            f32x16 acc;
+            // (the opaque offset keeps the compiler from hoisting these reads out of the group loop
+            // into 32 loop-long VGPRs)
+            int boff = (2 * b + h) * 16;
+            asm volatile("" : "+v"(boff));
+            const float4 *bb = reinterpret_cast<const float4 *>(sbias + boff);
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                const float4 v = bb[j];
+                acc[4 * j] = v.x; acc[4 * j + 1] = v.y; acc[4 * j + 2] = v.z; acc[4 * j + 3] = v.w;
+            }
+            mma32(acc, wr[b][0], cur[0]);
+            mma32(acc, wr[b][1], cur[1]);
+            if (!short_blk[b]) {
+                mma32(acc, wr[b][2], cur[2]);
+                mma32(acc, wr[b][3], cur[3]);
+            }
+            if (LOGITS && q.ok) {
+                float *lo = a.logits_out + (size_t)q.n * a.ncls * plane + (size_t)(2 * q.y + b) * a.Wout + 2 * q.x + h;
+#pragma unroll
+                for (int c = 0; c < 16; ++c)
+                    if (c < a.ncls) lo[(size_t)c * plane] = acc[c];
+            }
+            // argmax over this lane's classes = the sequential strict > scan from -inf of
+            // tf.math.argmax (models.py:55): the maximum (v_max ignores NaN), then its first index;
+            // nothing above -inf -> 0. Padding classes are masked by adding -inf (in place).
+#pragma unroll
+            for (int c = 0; c < 16; ++c) acc[c] += cmask[c];
+            float best = acc[0];
+#pragma unroll
+            for (int c = 1; c < 16; ++c) best = __builtin_fmaxf(best, acc[c]);
+            int bi = 15;
+#pragma unroll
+            for (int c = 14; c >= 0; --c) bi = acc[c] == best ? c : bi;
+            bi = best > -INFINITY ? bi : 0;
+            cls[b] = slut[bi];
+        }
+        if (a.cls_out) {
+            // lanes < 32 take output row 2y (their phase-(0,0) byte + the (0,1) byte of lane + 32), lanes
+            // >= 32 row 2y + 1: one 2-byte store of pixels (2x, 2x + 1) each
+            uint32_t c0 = (uint32_t)cls[0], c1 = (uint32_t)cls[1];
+            pl32swap(c0, c1);
+            if (q.ok) {
+                const size_t o = ((size_t)q.n * a.Hout + 2 * q.y + h) * a.Wout + 2 * q.x;
+                *reinterpret_cast<uint16_t *>(a.cls_out + o) = (uint16_t)(c0 | (c1 << 8));
+            }
+        }
+    };
+    Raw xa[CLS_TAPS], xb[CLS_TAPS];
+    int g = g0 + wi;
+    if (g < g1) load(g, xa);
+    while (g < g1) {
+        step(g, xa, xb);
+        g += nw;
+        if (g >= g1) break;
+        step(g, xb, xa);
+        g += nw;
+    }
+}
+
+// 16 input channels in two 8-channel groups per tap, the 4 taps of the k = 3 layer (Kpad = 4 x 16: a
+// 3x3 stride-2 transposed conv with output exactly 2x has pad 1, so pack_tconv's D = {0, 1}), grids
+// at least 32 wide; other class layers (k = 2, narrow grids) keep the generic conv path
+bool cls_supported(const ConvArgs &a) {
+    return a.CinS == 16 && a.Npad == 64 && a.Kpad == 64 && a.ncls >= 1 && a.ncls <= 16 && a.Wg >= 32 &&
+           a.Hout == 2 * a.Hg && a.Wout == 2 * a.Wg && a.Hg == a.Hin && a.Wg == a.Win;
+}
+
+hipError_t launch_cls(int prec, const ConvArgs &a, hipStream_t s) {
+    // waves stream over 32-pixel groups: enough workgroups to fill every CU at 4 waves per SIMD,
+    // a multiple of 8 for the XCD split
+    const int groups = (a.M + 31) / 32;
+    int g = (groups + 3) / 4;
+    g = g < 1024 ? g : 1024;
+    g = (g + 7) & ~7;
+    const bool lg = a.logits_out != nullptr;
+    if (prec == PREC_BF16) {
+        if (lg) hipLaunchKernelGGL((cls_kernel<__bf16, true>), dim3(g), dim3(256), 0, s, a);
+        else hipLaunchKernelGGL((cls_kernel<__bf16, false>), dim3(g), dim3(256), 0, s, a);
+    } else {
+        if (lg) hipLaunchKernelGGL((cls_kernel<float, true>), dim3(g), dim3(256), 0, s, a);
+        else hipLaunchKernelGGL((cls_kernel<float, false>), dim3(g), dim3(256), 0, s, a);
+    }
+    return hipGetLastError();
+}
+
+}  // namespace bugseg

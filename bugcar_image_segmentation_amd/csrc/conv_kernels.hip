@@ -28,6 +28,8 @@
 #include "bugseg_internal.h"
 #include "mfma_common.h"
 
+#include <cstdlib>
+
 namespace bugseg {
 
 template <int NR> struct Cfg { static constexpr int MR = NR >= 4 ? 2 : 4; };
@@ -400,6 +402,8 @@ static hipError_t launch_t(int nr, int epi, const ConvArgs &a, dim3 grid, size_t
 hipError_t launch_conv(int prec, int nr, int epi, const ConvArgs &a, hipStream_t s) {
     // the initial block has its own tiled kernel (init_kernels.hip)
     if (epi == EPI_INIT || epi == EPI_INIT_BGR) return launch_init(prec, epi == EPI_INIT_BGR, a, s);
+    // so has the class layer (cls_kernels.hip), when it has ENet's 16 input channels
+    if (epi == EPI_CLASSES && cls_supported(a) && !std::getenv("BUGSEG_CLS_CONV")) return launch_cls(prec, a, s);
     // one workgroup per tile up to 2048 workgroups (8 per CU), rounded to a multiple of 8 for the
     // XCD-aware walk; larger grids stride.
     int g = a.ntiles < 2048 ? a.ntiles : 2048;

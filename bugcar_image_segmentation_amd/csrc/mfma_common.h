@@ -97,6 +97,13 @@ __device__ __forceinline__ void pl16swap(uint32_t &a, uint32_t &b) {
     a = r.x;
     b = r.y;
 }
+// v_permlane32_swap: lanes 32-63 of a <-> lanes 0-31 of b
+__device__ __forceinline__ void pl32swap(uint32_t &a, uint32_t &b) {
+    const u32x2_t r = __builtin_amdgcn_permlane32_swap(a, b, false, false);
+    a = r.x;
+    b = r.y;
+}
+
 
 __device__ __forceinline__ float ld1(const float *p) { return *p; }
 __device__ __forceinline__ float ld1(const __bf16 *p) { return (float)*p; }

@@ -24,11 +24,6 @@
 
 namespace bugseg {
 
-__device__ __forceinline__ void pl32swap(uint32_t &a, uint32_t &b) {
-    const u32x2_t r = __builtin_amdgcn_permlane32_swap(a, b, false, false);
-    a = r.x;
-    b = r.y;
-}
 
 // storage rounding of an activation (the unfused plan stores it as T and reads it back)
 __device__ __forceinline__ float4 round_t(float4 v, const __bf16 *) { return unpack_bf16x4(pack_bf16x4(v)); }

@@ -30,6 +30,11 @@ def short(name):
     m = re.search(r"conv_kernel<.*, (\d+)>", name)
     if m:
         return f"conv NR1 E{m.group(1)}"
+    m = re.search(r"up_kernelI(DF16b|f)Li(\d+)ELi(\d+)ELi(\d+)E", name)
+    if m:
+        return f"up C{m.group(4)}"
+    if "cls_kernel" in name:
+        return "classes"
     if "init_kernel" in name:
         return "init"
     return name.split("(")[0][-40:]
@@ -42,7 +47,7 @@ def main():
     p.add_argument("--labels", default="")
     a = p.parse_args()
     rows = sorted(csv.DictReader(open(a.trace)), key=lambda r: int(r["Start_Timestamp"]))
-    rows = [r for r in rows if any(k in r["Kernel_Name"] for k in ("conv_kernel", "bneck_kernel", "init_kernel"))]
+    rows = [r for r in rows if any(k in r["Kernel_Name"] for k in ("conv_kernel", "bneck_kernel", "init_kernel", "up_kernel", "cls_kernel"))]
     fwds, cur = [], None
     for r in rows:
         s = short(r["Kernel_Name"])

@@ -28,7 +28,7 @@ def forwards(disp, meta):
     fw, cur = [], None
     for k in sorted(disp):
         name = short(meta[k][0])
-        if not any(t in meta[k][0] for t in ("conv_kernel", "bneck_kernel", "init_kernel")):
+        if not any(t in meta[k][0] for t in ("conv_kernel", "bneck_kernel", "init_kernel", "up_kernel", "cls_kernel")):
             continue
         if name.startswith("init") or name.endswith("E7") or name.endswith("E4"):
             cur = []

@@ -279,6 +279,35 @@ def test_up_block_pair_equals_separate(gpu, blocks, prec, monkeypatch):
     assert torch.equal(a, b)
 
 
+@pytest.mark.parametrize("prec", ["fp32", "bf16"])
+def test_class_layer_kernel_matches_conv_path(gpu, blocks, prec, monkeypatch):
+    """The class-layer kernel (cls_kernels.hip: 32x32 MFMA, all 16 logits of an output pixel in one
+    lane, in-register argmax) against the generic implicit-GEMM path (BUGSEG_CLS_CONV=1) on the same
+    network: the two sum the 64 products in different orders, so logits agree to rounding and class
+    maps wherever the top-2 margin is not a near-tie; the argmax itself is checked exactly against the
+    kernel's own logits."""
+    H, W = 120, 160
+    bgr = torch.from_numpy(synthetic.road_frames(2, H, W, seed=6)).cuda()
+    model = ENET(weights=blocks, precision=prec)
+    a = torch.empty((2, 15, H, W), dtype=torch.float32, device=gpu)
+    model.ctx.forward_bgr(bgr, 2, H, W, N.OUT_LOGITS_F32, a)
+    raw = torch.empty((2, H, W), dtype=torch.uint8, device=gpu)
+    model.ctx.forward_bgr(bgr, 2, H, W, N.OUT_CLASS15_U8, raw)
+    tags = [model.ctx.plan_op(2, H, W, i)[0] for i in range(model.ctx.plan_info(2, H, W, N.OUT_CLASS15_U8)[0])]
+    assert tags[-1] == "classes"
+    monkeypatch.setenv("BUGSEG_CLS_CONV", "1")
+    ref = ENET(weights=blocks, precision=prec)
+    b = torch.empty_like(a)
+    ref.ctx.forward_bgr(bgr, 2, H, W, N.OUT_LOGITS_F32, b)
+    la, lb = a.cpu().numpy(), b.cpu().numpy()
+    tol = 1e-4 if prec == "fp32" else 2e-2
+    np.testing.assert_allclose(la, lb, rtol=0, atol=tol * max(1.0, float(np.abs(lb).max())))
+    # the kernel's class map is exactly tf.math.argmax of its own logits (lowest index on ties)
+    assert np.array_equal(raw.cpu().numpy(), la.argmax(axis=1))
+    decided = _margin(lb) > (MARGIN if prec == "fp32" else 0.1)
+    assert (la.argmax(axis=1)[decided] == lb.argmax(axis=1)[decided]).all()
+
+
 def test_bev_shape_assert(gpu):
     bev = synthetic.synthetic_bev(120, 160, 300, 300)
     with pytest.raises(AssertionError):
