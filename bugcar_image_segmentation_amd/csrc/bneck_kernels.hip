@@ -135,7 +135,9 @@ __global__ void __launch_bounds__((BShape<C, V>::NW * 64), (sizeof(T) == 2 ? BSh
     constexpr int NP1 = NR1 * 16;
     float *cb1 = reinterpret_cast<float *>(w3 + C * K3S), *cs1 = cb1 + NP1, *cb2 = cs1 + NP1, *cs2 = cb2 + NP1;
     float *cb2b = cs2 + NP1, *cs2b = cb2b + NP1, *cb3 = cs2b + NP1, *cs3 = cb3 + C, *cso = cs3 + C;
-    T *ts = reinterpret_cast<T *>(cso + C);           // t0 / t1a / t1 region
+    // 16 zero elements: masked-off B fragments read them (an address select, not a divergent branch)
+    T *zpad = reinterpret_cast<T *>(cso + C);
+    T *ts = zpad + 16;                                // t0 / t1a / t1 region
     {
         auto stage = [&](T *dst, const void *src, int rows, int kpad, int kstride) {
             const int cpr = kpad * (int)sizeof(T) / 16;
@@ -154,6 +156,7 @@ __global__ void __launch_bounds__((BShape<C, V>::NW * 64), (sizeof(T) == 2 ? BSh
             cb2b[i] = ASYM ? a.b2b[i] : 0.f; cs2b[i] = ASYM ? a.s2b[i] : 0.f;
         }
         for (int i = tid; i < C; i += NT) { cb3[i] = a.b3[i]; cs3[i] = a.s3[i]; cso[i] = a.s_out[i]; }
+        if (tid < 16) zpad[tid] = (T)0.f;
     }
     // x / out through buffer descriptors: 32-bit offsets, and an out-of-range offset reads 0 / drops
     // the store (mfma_common.h), so image-border masking costs one select per access
@@ -308,8 +311,7 @@ __global__ void __launch_bounds__((BShape<C, V>::NW * 64), (sizeof(T) == 2 ? BSh
                     const int oy = p / TW, ox = p - oy * TW;
                     Raw xf;
                     const bool in = g < G2 && (!RD || (unsigned)(ox + tj) < (unsigned)TW);
-                    if (in) ld8(xf, ts + ((oy + ti) * HWW + (ox + tj)) * PSTR + coff);
-                    else zero(xf);
+                    ld8(xf, in ? ts + ((oy + ti) * HWW + (ox + tj)) * PSTR + coff : zpad);
                     if (a.ablate & 2) continue;
 #pragma unroll
                     for (int r = 0; r < NR1; ++r) mma(acc[j][r], wf[r], xf);
@@ -351,8 +353,7 @@ __global__ void __launch_bounds__((BShape<C, V>::NW * 64), (sizeof(T) == 2 ? BSh
                         if constexpr (NPA % 16 != 0) p = p < NPA ? p : 0;
                         const int oy = p / TWA, ox = p - oy * TWA;
                         Raw xf;
-                        if (g < G2) ld8(xf, ts + ((oy + tap) * HWW + ox) * PSTR + coff);
-                        else zero(xf);
+                        ld8(xf, g < G2 ? ts + ((oy + tap) * HWW + ox) * PSTR + coff : zpad);
 #pragma unroll
                         for (int r = 0; r < NR1; ++r) mma(acc[j][r], wf[r], xf);
                     }
@@ -397,8 +398,7 @@ __global__ void __launch_bounds__((BShape<C, V>::NW * 64), (sizeof(T) == 2 ? BSh
                         if constexpr (NPX % 16 != 0) p = p < NPX ? p : 0;
                         const int oy = p / TW, ox = p - oy * TW;
                         Raw xf;
-                        if (g < G2) ld8(xf, ts + (oy * TWA + ox + tap) * PSTR + coff);
-                        else zero(xf);
+                        ld8(xf, g < G2 ? ts + (oy * TWA + ox + tap) * PSTR + coff : zpad);
 #pragma unroll
                         for (int r = 0; r < NR1; ++r) mma(acc[j][r], wf[r], xf);
                     }
@@ -433,8 +433,7 @@ __global__ void __launch_bounds__((BShape<C, V>::NW * 64), (sizeof(T) == 2 ? BSh
 #pragma unroll
         for (int j = 0; j < NF2; ++j) {
             const int p = (wave + NW * j) * 16 + col;
-            if (kq < G3 && p < NPX) ld8(tf[j], ts + p * PSTR + kq * 8);
-            else zero(tf[j]);
+            ld8(tf[j], kq < G3 && p < NPX ? ts + p * PSTR + kq * 8 : zpad);
         }
         if constexpr (!REG3) {
             // staged epilogue: the t1 region becomes per-wave staging — residual chunks in, results
@@ -550,7 +549,7 @@ size_t bneck_lds_bytes(int prec, int C, bool asym, int v) {
     const size_t halo = (size_t)(TH + 2 * R) * (TW + 2 * RX) * (IS + pad);
     const size_t stage = C == 64 ? (size_t)NW * 16 * (C + pad) : 0;    // staged epilogue (REG3 off)
     const size_t consts = ((size_t)6 * NR1 * 16 + 3 * (size_t)C) * sizeof(float);
-    return (wts + (halo > stage ? halo : stage)) * es + consts;
+    return (wts + 16 + (halo > stage ? halo : stage)) * es + consts;   // + the zero pad
 }
 
 // kernel symbol of (precision, C, asym, variant, transposed); nullptr if not built
