@@ -193,7 +193,12 @@ __global__ void __launch_bounds__((BShape<C, V>::NW * 64), (sizeof(T) == 2 ? BSh
             const int i = (f * 16) / TW, j = (f * 16) % TW + pi;
             const int y = oy0 + dt * (tr ? j : i), x = ox0 + dtx * (tr ? i : j);
             const bool ok = y < a.H && x < a.W;
-            return ok ? xn + (uint32_t)((y * a.W + x) * C + choff) * (uint32_t)sizeof(T) : OOB;
+            // 24-bit multiplies (full rate; v_mul_lo_u32 is quarter rate): coordinates < 2^24. The
+            // offset is computed for every lane and pinned, so the mask is a select, not a divergent
+            // branch around the arithmetic
+            uint32_t v = xn + ((__umul24((uint32_t)y, (uint32_t)a.W) + (uint32_t)x) * C + choff) * (uint32_t)sizeof(T);
+            asm volatile("" : "+v"(v));
+            return ok ? v : OOB;
         };
         // byte offset of pixel pi of fragment f (channel 0), or OOB outside the image
         auto pix_base = [&](int f, int pi) -> uint32_t { return pix_off(f, pi, 0); };
@@ -215,8 +220,8 @@ __global__ void __launch_bounds__((BShape<C, V>::NW * 64), (sizeof(T) == 2 ? BSh
 #pragma unroll
                 for (int s = 0; s < KS1; ++s) {
                     const int g = s * 4 + kq;
-                    const bool ld = okc[c] && g < G1 && !(a.ablate & 1);
-                    bld8(xf[c][s], rxb, ld ? xn + (uint32_t)((iy * a.W + ix) * C + g * 8) * (uint32_t)sizeof(T) : OOB);
+                    const bool ld = okc[c] && g < G1;
+                    bld8(xf[c][s], rxb, ld ? xn + ((__umul24((uint32_t)iy, (uint32_t)a.W) + (uint32_t)ix) * C + g * 8) * (uint32_t)sizeof(T) : OOB);
                 }
             }
 #pragma unroll
@@ -311,8 +316,9 @@ __global__ void __launch_bounds__((BShape<C, V>::NW * 64), (sizeof(T) == 2 ? BSh
                     const int oy = p / TW, ox = p - oy * TW;
                     Raw xf;
                     const bool in = g < G2 && (!RD || (unsigned)(ox + tj) < (unsigned)TW);
-                    ld8(xf, in ? ts + ((oy + ti) * HWW + (ox + tj)) * PSTR + coff : zpad);
-                    if (a.ablate & 2) continue;
+                    int off = ((oy + ti) * HWW + (ox + tj)) * PSTR + coff;
+                    asm volatile("" : "+v"(off));
+                    ld8(xf, ts + (in ? off : -16));           // masked: the zero pad just below ts
 #pragma unroll
                     for (int r = 0; r < NR1; ++r) mma(acc[j][r], wf[r], xf);
                 }
@@ -468,7 +474,7 @@ __global__ void __launch_bounds__((BShape<C, V>::NW * 64), (sizeof(T) == 2 ? BSh
                 for (int k = 0; k < CPL; ++k) {
                     const int q = lane + 64 * k;
                     if (q < CPF) {
-                        const uint32_t off = (a.ablate & 4) ? OOB : pix_off(wave + NW * j, q / CPP, (q % CPP) * EPC);
+                        const uint32_t off = pix_off(wave + NW * j, q / CPP, (q % CPP) * EPC);
                         bst16(rob, off, *reinterpret_cast<const uint4 *>(stg + (q / CPP) * OSTR + (q % CPP) * EPC));
                     }
                 }
@@ -481,7 +487,7 @@ __global__ void __launch_bounds__((BShape<C, V>::NW * 64), (sizeof(T) == 2 ? BSh
 #pragma unroll
         for (int j = 0; j < NF2; ++j) {
             if (wave + NW * j >= NFT) break;              // wave-uniform
-            const uint32_t po = (a.ablate & 4) ? OOB : pix_base(wave + NW * j, col);
+            const uint32_t po = pix_base(wave + NW * j, col);
             auto out3 = [&](int r, const f32x4 &acc) {
                 const int ch = r * 16 + kq * 4;
                 return act(bias_in_acc(NR3) ? f4(acc) : add4(f4(acc), ld4f(cb3 + ch)), cs3 + ch);

@@ -84,7 +84,6 @@ struct BneckArgs {
                          // count: dt^2, or dt for row-dilated full-width variants
     int tr;              // transposed tiles: tile rows run along image columns (symmetric blocks only)
     int tiles_x, tiles_y, ntiles;   // tiles per phase sub-image row / column; B * phases * tiles_y * tiles_x
-    int ablate;          // debug only (BUGSEG_BNECK_ABLATE): 1 skip x loads, 2 skip middle conv, 4 skip stores
     const void *w1, *w2, *w2b, *w3;                   // packed [Npad][Kpad] (w2b: asymmetric 1x5)
     const float *b1, *s1, *b2, *s2, *b2b, *s2b, *b3, *s3, *s_out;
     uint32_t x_bytes;                                 // bytes of x (== out)

@@ -705,7 +705,6 @@ struct Walker {
                         const Packed &p1 = P(0), &p2 = P(1), &p3 = P(nu - 1), &p2b = P(nu == 4 ? 2 : 1);
                         q.x = curp; q.out = dst; q.B = B; q.H = cur.H; q.W = cur.W;
                         q.dt = dd; q.phases = trd ? dd : dd * dd; q.tr = ttr;
-                        if (const char *ab = std::getenv("BUGSEG_BNECK_ABLATE")) q.ablate = std::atoi(ab);
                         q.tiles_y = ty; q.tiles_x = tx;
                         q.ntiles = B * q.phases * ty * tx;
                         q.w1 = dw + p1.o_w; q.b1 = (const float *)(dw + p1.o_bias); q.s1 = (const float *)(dw + p1.o_s1);

@@ -1,6 +1,7 @@
-"""Debug: time each fused-bottleneck ablation variant (BUGSEG_BNECK_ABLATE bits: 1 no x loads,
-2 no middle-conv MFMAs, 4 no output stores) on the bench workload. Run under rocprofv3 --kernel-trace;
-each variant is its own context (the flag is read when the plan is built), run `reps` times."""
+"""Debug: a few single-stream bench-workload forwards (B = 32) to run under rocprofv3 (--kernel-trace
+or --pmc; scripts/gpu_sqpmc.sh, scripts/gpu_layers.sh). The argument list is kept for the earlier
+in-kernel ablation runs (round-1 record in DESIGN.md); the ablation hooks are gone from the kernel,
+so every argument now runs the same baseline."""
 import os
 import sys
 
