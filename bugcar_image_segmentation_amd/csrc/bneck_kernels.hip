@@ -76,15 +76,25 @@ void bneck_shape(int C, int v, int &th, int &tw, int &nw, int *rd) {
     if (rd) *rd = 0;
 }
 
-template <typename T, int C, bool ASYM, int V, bool TR>
+// CI > 0: the DOWNSAMPLING bottleneck with a CI-channel input at twice the
+// output resolution: the projection is the 2x2 stride-2 conv (K = 4 CI), the middle conv the block's
+// 3x3, and the residual is the main branch — maxpool 2x2 of the input, zero-padded from CI to C
+// channels, its argmax indices written for the paired upsampling block. The pooling uses the
+// projection's own B fragments (lane kq holds taps of one 8-channel group: the 4 taps in-lane for
+// CI >= 32, two taps in-lane + one v_permlane32_swap for CI = 16) and leaves the pooled values in a
+// small global scratch (a.pool) that phase 3 reads back as its residual (L2 hits).
+template <typename T, int C, bool ASYM, int V, bool TR, int CI = 0>
 __global__ void __launch_bounds__((BShape<C, V>::NW * 64), (sizeof(T) == 2 ? BShape<C, V>::OCC : 1)) bneck_kernel(const BneckArgs a) {
     using Raw = typename Tr<T>::Raw;
     constexpr int TH = BShape<C, V>::TH, TW = BShape<C, V>::TW, NW = BShape<C, V>::NW, NT = NW * 64;
-    constexpr int I = C / 4;
+    constexpr int I = CI > 0 ? CI / 4 : C / 4;      // internal channels (ENet: input / 4)
     constexpr int IS = I < 8 ? 8 : I;                 // stored internal channels (8-channel groups)
     constexpr int NR1 = (I + 15) / 16;                // 16-row fragments of t0 / t1
     constexpr int NR3 = C / 16;                       // 16-row fragments of out
-    constexpr int G1 = C / 8, KS1 = (G1 + 3) / 4;     // proj k groups / steps
+    constexpr bool DN = CI > 0;                       // (I above already depends on it)
+    static_assert(!DN || (!ASYM && !TR && !BShape<C, V>::RD && (CI == 16 || CI % 32 == 0)), "down mode: plain tiles");
+    constexpr int G1 = DN ? CI / 2 : C / 8, KS1 = (G1 + 3) / 4;   // proj k groups / steps (down: 4 taps x CI)
+    constexpr int CG1 = CI / 8;                       // down: 8-channel groups per tap
     constexpr int TAPS = ASYM ? 5 : 9;
     constexpr int G2 = TAPS * IS / 8, KS2 = (G2 + 3) / 4;
     constexpr int G3 = IS / 8;                        // expand k groups (<= 4: one step)
@@ -103,7 +113,7 @@ __global__ void __launch_bounds__((BShape<C, V>::NW * 64), (sizeof(T) == 2 ? BSh
     constexpr int NPA = TH * TWA;
     constexpr int NFA = (NPA + 15) / 16;
     constexpr int NF2A = (NFA + NW - 1) / NW;
-    constexpr int CH1 = KS1 >= 4 ? 3 : KS1 == 2 ? 4 : 8;   // phase-1 fragments whose loads fly together
+    constexpr int CH1 = KS1 >= 8 ? 1 : KS1 >= 4 ? 3 : KS1 == 2 ? 4 : 8;   // phase-1 fragments whose loads fly together
     // phase-3 chunking (see phase 3): bf16 with an even number of 16-row blocks swaps row pairs
     // into 16-B chunks; bf16 C = 16 stores 8-B quads (HALF); fp32 quads are 16-B chunks
     // REG3: the register epilogue (C = 128 and 16). C = 64 keeps the LDS-staged epilogue: its 128-B
@@ -160,8 +170,11 @@ __global__ void __launch_bounds__((BShape<C, V>::NW * 64), (sizeof(T) == 2 ? BSh
     }
     // x / out through buffer descriptors: 32-bit offsets, and an out-of-range offset reads 0 / drops
     // the store (mfma_common.h), so image-border masking costs one select per access
-    const auto rxb = mkbuf(a.x, a.x_bytes);
+    // down mode: x is the (2H, 2W, CI) block input; the residual comes from the pooled scratch
+    const auto rxb = mkbuf(DN ? a.xin : a.x, DN ? a.xin_bytes : a.x_bytes);
     const auto rob = mkbuf(a.out, a.x_bytes);
+    const auto rpb = mkbuf(a.pool, a.pool_bytes);
+    const auto rib = mkbuf(a.idx_out, a.idx_bytes);
     // the fused path is planned only when every slope is <= 1 (bugseg_runtime.cpp fusable_regular),
     // so PReLU is max(v, s*v); accumulators start at the bias
     auto act = [&](float4 v, const float *s) { return prelu4m(v, ld4f(s)); };
@@ -186,6 +199,7 @@ __global__ void __launch_bounds__((BShape<C, V>::NW * 64), (sizeof(T) == 2 ? BSh
         const int oy0 = py + dt * tyi * (tr ? TW : TH), ox0 = RD ? 0 : px + dt * txi * (tr ? TH : TW);
         const int dtx = RD ? 1 : dt;                  // column step of the tile
         const uint32_t xn = (uint32_t)(n * a.H * a.W) * (uint32_t)(C * sizeof(T));   // frame byte offset
+        const uint32_t xin_n = (uint32_t)(n * 4 * a.H * a.W) * (uint32_t)(CI * sizeof(T));   // down: input frame
         // byte offset of channel chunk `choff` of pixel pi (per lane, 0..15) of tile fragment f (wave
         // uniform), or OOB outside the image. A fragment is a run of one tile row: its row i is a
         // scalar and only the column j is per lane.
@@ -202,6 +216,115 @@ __global__ void __launch_bounds__((BShape<C, V>::NW * 64), (sizeof(T) == 2 ? BSh
         };
         // byte offset of pixel pi of fragment f (channel 0), or OOB outside the image
         auto pix_base = [&](int f, int pi) -> uint32_t { return pix_off(f, pi, 0); };
+        // residual source: x itself, or (down) the pooled scratch (CI channels; channels >= CI read 0)
+        const auto rrb = DN ? rpb : rxb;
+        const uint32_t pn = (uint32_t)(n * a.H * a.W) * (uint32_t)(CI * sizeof(T));
+        auto res_off = [&](int f, int pi, int ch) -> uint32_t {
+            if constexpr (!DN) {
+                return pix_off(f, pi, ch);
+            } else {
+                const int i = (f * 16) / TW, j = (f * 16) % TW + pi;
+                const int y = oy0 + dt * i, x = ox0 + dtx * j;
+                const bool ok = y < a.H && x < a.W && ch < CI;
+                uint32_t v = pn + ((__umul24((uint32_t)y, (uint32_t)a.W) + (uint32_t)x) * CI + ch) * (uint32_t)sizeof(T);
+                asm volatile("" : "+v"(v));
+                return ok ? v : OOB;
+            }
+        };
+        // down: main-branch maxpool of output pixel (y, x) from the projection's B fragments (see the
+        // kernel comment); the first maximum in window order wins (strict >, NaN / -inf never chosen:
+        // as a key, larger value first, then lower window position; position 4 = no candidate -> 0)
+        auto pool_store = [&](const Raw (&xs)[KS1], bool interior, int y, int x) {
+            if constexpr (DN) {
+                if (__ballot(interior) == 0) return;          // halo-only fragment (wave-uniform)
+                auto elems = [&](const Raw &r, float (&e)[8]) {
+                    if constexpr (sizeof(T) == 2) {
+                        const uint32_t w[4] = {r.v.x, r.v.y, r.v.z, r.v.w};
+#pragma unroll
+                        for (int i = 0; i < 4; ++i) { e[2 * i] = __uint_as_float(w[i] << 16); e[2 * i + 1] = __uint_as_float(w[i] & 0xffff0000u); }
+                    } else {
+                        const RawF &f = reinterpret_cast<const RawF &>(r);
+                        e[0] = f.a.x; e[1] = f.a.y; e[2] = f.a.z; e[3] = f.a.w; e[4] = f.b.x; e[5] = f.b.y; e[6] = f.b.z; e[7] = f.b.w;
+                    }
+                };
+                const uint32_t pix = (uint32_t)((n * a.H + y) * a.W + x);
+                auto emit = [&](int cc, const float (&bv)[8], const int (&bp)[8], bool wr) {
+                    // 8 pooled channels (exact input values) + their window positions (4 = none -> 0)
+                    uint32_t pw[8 * sizeof(T) / 4];
+                    if constexpr (sizeof(T) == 2) {
+#pragma unroll
+                        for (int i = 0; i < 4; ++i)
+                            pw[i] = (__float_as_uint(bv[2 * i]) >> 16) | (__float_as_uint(bv[2 * i + 1]) & 0xffff0000u);
+                    } else {
+#pragma unroll
+                        for (int i = 0; i < 8; ++i) pw[i] = __float_as_uint(bv[i]);
+                    }
+                    uint32_t lo = 0, hi = 0;
+#pragma unroll
+                    for (int i = 0; i < 4; ++i) {
+                        lo |= (uint32_t)(bp[i] & 3) << (8 * i);
+                        hi |= (uint32_t)(bp[4 + i] & 3) << (8 * i);
+                    }
+                    const uint32_t po = wr ? (pix * CI + cc * 8) * (uint32_t)sizeof(T) : OOB;
+#pragma unroll
+                    for (int i = 0; i < (int)(8 * sizeof(T) / 16); ++i)
+                        bst16(rpb, po == OOB ? OOB : po + 16 * i, make_uint4(pw[4 * i], pw[4 * i + 1], pw[4 * i + 2], pw[4 * i + 3]));
+                    __builtin_amdgcn_raw_buffer_store_b64((u32x2_t){lo, hi}, rib, wr ? (int)(pix * a.idxCS + cc * 8) : (int)OOB, 0, 0);
+                };
+                // in window order: strict > from -inf (NaN and -inf never taken), position 4 = none
+                auto seq = [](float &bv, int &bp, float v, int p) {
+                    const bool t = v > bv;
+                    bv = t ? v : bv;
+                    bp = t ? p : bp;
+                };
+                if constexpr (CG1 >= 4) {
+                    // k step s holds tap s / (CG1 / 4) of channel group (s % (CG1 / 4)) * 4 + kq
+#pragma unroll
+                    for (int hgrp = 0; hgrp < CG1 / 4; ++hgrp) {
+                        float bv[8], e[8];
+                        int bp[8];
+#pragma unroll
+                        for (int i = 0; i < 8; ++i) { bv[i] = -INFINITY; bp[i] = 4; }
+#pragma unroll
+                        for (int tap = 0; tap < 4; ++tap) {
+                            elems(xs[tap * (CG1 / 4) + hgrp], e);
+#pragma unroll
+                            for (int i = 0; i < 8; ++i) seq(bv[i], bp[i], e[i], tap);
+                        }
+                        emit(hgrp * 4 + kq, bv, bp, interior);
+                    }
+                } else {
+                    // CI = 16: step s holds dy = s, dx = kq >> 1, group kq & 1; the dx = 1 half of the
+                    // wave (lanes 32-63) is traded in with v_permlane32_swap and merged as a key
+                    // (larger value, then lower position)
+                    float bv[8], e[8];
+                    int bp[8];
+#pragma unroll
+                    for (int i = 0; i < 8; ++i) { bv[i] = -INFINITY; bp[i] = 4; }
+                    const int dx = kq >> 1;
+#pragma unroll
+                    for (int dy = 0; dy < 2; ++dy) {
+                        elems(xs[dy], e);
+#pragma unroll
+                        for (int i = 0; i < 8; ++i) seq(bv[i], bp[i], e[i], dy * 2 + dx);
+                    }
+                    const bool lo_half = kq < 2;
+#pragma unroll
+                    for (int i = 0; i < 8; ++i) {
+                        uint32_t v0 = __float_as_uint(bv[i]), v1 = v0, p0 = (uint32_t)bp[i], p1 = p0;
+                        pl32swap(v0, v1);
+                        pl32swap(p0, p1);
+                        const float pv = __uint_as_float(lo_half ? v1 : v0);
+                        const int pp = (int)(lo_half ? p1 : p0);
+                        const bool t = pv > bv[i] || (pv == bv[i] && pp < bp[i]);
+                        bv[i] = t ? pv : bv[i];
+                        bp[i] = t ? pp : bp[i];
+                    }
+                    // both halves now agree; lanes 0-31 (groups kq = 0, 1) write
+                    emit(kq & 1, bv, bp, interior && lo_half);
+                }
+            }
+        };
         STAMP(0); STAMP_WG();
         __syncthreads();   // weights staged (first tile) / previous tile done with ts
         STAMP(1);
@@ -221,7 +344,16 @@ __global__ void __launch_bounds__((BShape<C, V>::NW * 64), (sizeof(T) == 2 ? BSh
                 for (int s = 0; s < KS1; ++s) {
                     const int g = s * 4 + kq;
                     const bool ld = okc[c] && g < G1;
-                    bld8(xf[c][s], rxb, ld ? xn + ((__umul24((uint32_t)iy, (uint32_t)a.W) + (uint32_t)ix) * C + g * 8) * (uint32_t)sizeof(T) : OOB);
+                    if constexpr (DN) {
+                        // 2x2 stride-2 tap (tap = g / CG1: dy = tap >> 1, dx = tap & 1), pack_conv's K order
+                        const int tap = g / CG1, cc = g - tap * CG1;
+                        const uint32_t sy = (uint32_t)(2 * iy + (tap >> 1)), sx = (uint32_t)(2 * ix + (tap & 1));
+                        uint32_t v = xin_n + ((__umul24(sy, (uint32_t)(2 * a.W)) + sx) * CI + cc * 8) * (uint32_t)sizeof(T);
+                        asm volatile("" : "+v"(v));
+                        bld8(xf[c][s], rxb, ld ? v : OOB);
+                    } else {
+                        bld8(xf[c][s], rxb, ld ? xn + ((__umul24((uint32_t)iy, (uint32_t)a.W) + (uint32_t)ix) * C + g * 8) * (uint32_t)sizeof(T) : OOB);
+                    }
                 }
             }
 #pragma unroll
@@ -248,6 +380,11 @@ __global__ void __launch_bounds__((BShape<C, V>::NW * 64), (sizeof(T) == 2 ? BSh
                         st4(ts + h * PSTR + ch, v);
                     }
                 }
+                if constexpr (DN) {
+                    const int hy = h / HWW, hx = h - hy * HWW;
+                    const bool interior = okc[c] && hy >= 1 && hy <= TH && hx >= 1 && hx <= TW;
+                    pool_store(xf[c], interior, oy0 + (hy - 1), ox0 + (hx - 1));
+                }
             }
         }
         STAMP(2);
@@ -268,20 +405,21 @@ __global__ void __launch_bounds__((BShape<C, V>::NW * 64), (sizeof(T) == 2 ? BSh
 #pragma unroll
                 for (int k = 0; k < CPL; ++k) {
                     const int q = lane + 64 * k;
-                    const uint32_t off = pix_off(f, q / CPP, (q % CPP) * EPC);
-                    r[k] = bld16(rxb, q < CPF ? off : OOB);
+                    const uint32_t off = res_off(f, q / CPP, (q % CPP) * EPC);
+                    r[k] = bld16(rrb, q < CPF ? off : OOB);
                 }
                 return;
             }
-            const uint32_t po = pix_base(wave + NW * j, col);
+            const uint32_t po = DN ? 0u : pix_base(wave + NW * j, col);
 #pragma unroll
             for (int t = 0; t < RQ3; ++t) {
-                const uint32_t off = po == OOB ? OOB : po + (uint32_t)chunk_ch(t) * (uint32_t)sizeof(T);
+                const uint32_t off = DN ? res_off(wave + NW * j, col, chunk_ch(t))
+                                        : po == OOB ? OOB : po + (uint32_t)chunk_ch(t) * (uint32_t)sizeof(T);
                 if constexpr (HALF) {
-                    const u32x2_t v = __builtin_amdgcn_raw_buffer_load_b64(rxb, (int)off, 0, 0);
+                    const u32x2_t v = __builtin_amdgcn_raw_buffer_load_b64(rrb, (int)off, 0, 0);
                     r[t] = make_uint4(v.x, v.y, 0u, 0u);
                 } else {
-                    r[t] = bld16(rxb, off);
+                    r[t] = bld16(rrb, off);
                 }
             }
         };
@@ -543,12 +681,12 @@ extern "C" int bugseg_debug_set_stamps(void *p) {
 }
 #endif
 
-size_t bneck_lds_bytes(int prec, int C, bool asym, int v) {
+size_t bneck_lds_bytes(int prec, int C, bool asym, int v, int cin) {
     int TH, TW, NW, RD;
     bneck_shape(C, v, TH, TW, NW, &RD);
     const int es = prec == PREC_BF16 ? 2 : 4, pad = 16 / es;
-    const int I = C / 4, IS = I < 8 ? 8 : I, NR1 = (I + 15) / 16;
-    const int KS1 = (C / 8 + 3) / 4, KS2 = ((asym ? 5 : 9) * IS / 8 + 3) / 4;
+    const int I = cin > 0 ? cin / 4 : C / 4, IS = I < 8 ? 8 : I, NR1 = (I + 15) / 16;
+    const int KS1 = ((cin > 0 ? cin / 2 : C / 8) + 3) / 4, KS2 = ((asym ? 5 : 9) * IS / 8 + 3) / 4;
     const int R = asym ? 2 : 1, RX = RD ? 0 : R;
     const size_t wts = (size_t)NR1 * 16 * (KS1 * 32 + pad) + (size_t)NR1 * 16 * (KS2 * 32 + pad) * (asym ? 2 : 1) +
                        (size_t)C * (32 + pad);
@@ -570,8 +708,16 @@ static const void *kfun(int C, bool asym, int v, bool tr) {
     if (C == 128 && v == 3 && !tr && !asym) return (const void *)bneck_kernel<T, 128, false, 3, false>;
     return nullptr;
 }
+// downsampling forms: ENet's down1 (16 -> 64 at 120x160) and down2 (64 -> 128 at 60x80)
+template <typename T>
+static const void *kfun_down(int C, int v, int cin) {
+    if (C == 64 && v == 0 && cin == 16) return (const void *)bneck_kernel<T, 64, false, 0, false, 16>;
+    if (C == 128 && v == 1 && cin == 64) return (const void *)bneck_kernel<T, 128, false, 1, false, 64>;
+    return nullptr;
+}
 
-static const void *bneck_fun(int prec, int C, bool asym, int v, bool tr) {
+static const void *bneck_fun(int prec, int C, bool asym, int v, bool tr, int cin) {
+    if (cin > 0) return asym || tr ? nullptr : prec == PREC_BF16 ? kfun_down<__bf16>(C, v, cin) : kfun_down<float>(C, v, cin);
     return prec == PREC_BF16 ? kfun<__bf16>(C, asym, v, tr) : kfun<float>(C, asym, v, tr);
 }
 
@@ -587,22 +733,23 @@ static hipError_t allow_lds(const void *f) {
     return hipSuccess;
 }
 
-int bneck_slots_per_cu(int prec, int C, bool asym, int v, bool tr) {
-    const void *f = bneck_fun(prec, C, asym, v, tr);
+int bneck_slots_per_cu(int prec, int C, bool asym, int v, bool tr, int cin) {
+    const void *f = bneck_fun(prec, C, asym, v, tr, cin);
     int th, tw, nw;
     bneck_shape(C, v, th, tw, nw, nullptr);
     if (!f || allow_lds(f) != hipSuccess) return 0;
     int n = 0;
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, f, nw * 64, bneck_lds_bytes(prec, C, asym, v)) != hipSuccess) return 0;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, f, nw * 64, bneck_lds_bytes(prec, C, asym, v, cin)) != hipSuccess)
+        return 0;
     return n;
 }
 
-hipError_t launch_bneck(int prec, int C, bool asym, int v, const BneckArgs &a, hipStream_t s) {
-    const void *f = bneck_fun(prec, C, asym, v, a.tr != 0);
+hipError_t launch_bneck(int prec, int C, bool asym, int v, const BneckArgs &a, hipStream_t s, int cin) {
+    const void *f = bneck_fun(prec, C, asym, v, a.tr != 0, cin);
     if (!f) return hipErrorInvalidValue;
     int th, tw, nw;
     bneck_shape(C, v, th, tw, nw, nullptr);
-    const size_t lds = bneck_lds_bytes(prec, C, asym, v);
+    const size_t lds = bneck_lds_bytes(prec, C, asym, v, cin);
     if (lds > 64 * 1024) {
         hipError_t e = allow_lds(f);
         if (e != hipSuccess) return e;

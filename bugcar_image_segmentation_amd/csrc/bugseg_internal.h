@@ -88,15 +88,24 @@ struct BneckArgs {
     const float *b1, *s1, *b2, *s2, *b2b, *s2b, *b3, *s3, *s_out;
     uint32_t x_bytes;                                 // bytes of x (== out)
     int slopes_le1;                                   // every PReLU slope <= 1: max(v, s*v)
+    // downsampling blocks (cin > 0 in launch_bneck): x is unused; xin = block input (B, 2H, 2W, cin),
+    // pool = scratch for the pooled main branch (B, H, W, cin), idx_out = its window positions
+    const void *xin;
+    void *pool;
+    uint8_t *idx_out;
+    int idxCS;
+    uint32_t xin_bytes, pool_bytes, idx_bytes;
 };
 // tile-shape variants of the fused kernel for C channels: 0 .. bneck_variants(C) - 1
 int bneck_variants(int C);
 // rd (optional): 1 for a row-dilated full-width variant (tiles_x = 1, phases = d, needs W <= tw)
 void bneck_shape(int C, int v, int &th, int &tw, int &nw, int *rd = nullptr);
-size_t bneck_lds_bytes(int prec, int C, bool asym, int v);
-// resident workgroups per CU (occupancy API); 0 if (C, asym, v, tr) is not built
-int bneck_slots_per_cu(int prec, int C, bool asym, int v, bool tr);
-hipError_t launch_bneck(int prec, int C, bool asym, int v, const BneckArgs &a, hipStream_t s);
+// cin > 0: the downsampling form (bneck_kernels.hip) with a cin-channel input; built for (64, v0,
+// cin 16) and (128, v1, cin 64)
+size_t bneck_lds_bytes(int prec, int C, bool asym, int v, int cin = 0);
+// resident workgroups per CU (occupancy API); 0 if (C, asym, v, tr, cin) is not built
+int bneck_slots_per_cu(int prec, int C, bool asym, int v, bool tr, int cin = 0);
+hipError_t launch_bneck(int prec, int C, bool asym, int v, const BneckArgs &a, hipStream_t s, int cin = 0);
 
 // ---- fused upsampling bottleneck (up_kernels.hip) ----------------------------------------------
 struct UpArgs {

@@ -12,6 +12,7 @@
 //     B=64 at 640x480 is a few GB and stays resident between calls);
 //   * enqueues on the caller's stream; no host synchronisation, no allocation once a plan exists.
 #include <cmath>
+#include <cstdio>
 #include <cstring>
 #include <string>
 #include <vector>
@@ -61,7 +62,7 @@ struct Op {
     BneckArgs bn;
     UpArgs up;
     int up_cin = 0, up_it = 0, up_cout = 0;
-    int bn_c = 0, bn_var = 0;
+    int bn_c = 0, bn_var = 0, bn_cin = 0;   // bn_cin > 0: a downsampling block (cin input channels)
     bool bn_asym = false;
     double bytes = 0, flops = 0;
     double layer_bytes = -1;   // per-layer (unfused) algorithmic bytes of the work; -1: same as bytes
@@ -557,6 +558,33 @@ bool fusable_regular(const bugseg_ctx *ctx, const BlockDesc &b, const std::vecto
     return true;
 }
 
+// The downsampling block in one fused launch (bneck_kernels.hip, cin > 0): ENet's two shapes
+// (16 -> 64, 64 -> 128, internal cin / 4), 2x2 stride-2 projection, 3x3 middle conv, PReLU slopes
+// <= 1. -> the tile variant (C64: 16x16, C128: 20x16, untransposed) or -1.
+int fusable_down(const bugseg_ctx *ctx, const BlockDesc &b, const std::vector<int> &ids) {
+    const char *env = std::getenv("BUGSEG_NO_FUSE");
+    if (env && *env && *env != '0') return -1;
+    const int cin = b.attrs[0], C = b.attrs[1];
+    const int v = C == 64 && cin == 16 ? 0 : C == 128 && cin == 64 ? 1 : -1;
+    if (v < 0 || b.units.size() != 3) return -1;
+    for (const int id : ids) {
+        const Packed &p = ctx->packed[id];
+        const float *s1 = (const float *)(ctx->host_w.data() + p.o_s1), *s2 = (const float *)(ctx->host_w.data() + p.o_s2);
+        for (int c = 0; c < p.Npad; ++c)
+            if (!(s1[c] <= 1.f) || !(s2[c] <= 1.f)) return -1;
+    }
+    const UnitDesc &u1 = b.units[0], &u2 = b.units[1], &u3 = b.units[2];
+    const int I = cin / 4;                              // ENet: internal = input channels / 4
+    if (u1.kh != 2 || u1.kw != 2 || u1.stride != 2 || u1.pad_h != 0 || u1.pad_w != 0 || u1.cin != cin || u1.cout != I)
+        return -1;
+    if (u2.kh != 3 || u2.kw != 3 || u2.stride != 1 || u2.pad_h != 1 || u2.pad_w != 1 || u2.dil_h != 1 || u2.dil_w != 1 ||
+        u2.cin != I || u2.cout != I)
+        return -1;
+    if (u3.kh != 1 || u3.kw != 1 || u3.cin != I || u3.cout != C) return -1;
+    if (bneck_slots_per_cu(ctx->prec, C, false, v, false, cin) <= 0) return -1;
+    return v;
+}
+
 // Tile variant of a fused bottleneck layer: the variant whose estimated time is least, where a
 // launch costs (rounds of resident workgroups) x (per-tile cost) and the per-tile cost is the
 // per-wave fragment count of the two tile phases (weights from in-kernel phase clocks of the 16x16
@@ -670,6 +698,54 @@ struct Walker {
                 szT = std::max({szT, tbytes(s1), tbytes(s2)});
                 szX = std::max(szX, tbytes(so));
                 if (!fill) szIdx[bi] = (size_t)B * so.H * so.W * idxCS;
+                const int dv = cur.C == b.attrs[0] ? fusable_down(ctx, b, ids) : -1;
+                if (dv >= 0) {
+                    // one launch: 2x2 projection + 3x3 + expansion + pooled main branch (pooled values
+                    // through the T[0] scratch, read back as the residual)
+                    const Shape sp{so.H, so.W, idxCS};
+                    szT = std::max(szT, tbytes(sp));
+                    if (fill) {
+                        Op op;
+                        op.kind = 1;
+                        op.bn_c = b.attrs[1];
+                        op.bn_var = dv;
+                        op.bn_cin = b.attrs[0];
+                        BneckArgs &q = op.bn;
+                        std::memset(&q, 0, sizeof(q));
+                        const unsigned char *dw = (const unsigned char *)ctx->dev_w;
+                        const Packed &p1 = P(0), &p2 = P(1), &p3 = P(2);
+                        int th, tw, nw;
+                        bneck_shape(op.bn_c, dv, th, tw, nw, nullptr);
+                        q.x = nullptr; q.out = dst; q.B = B; q.H = so.H; q.W = so.W;
+                        q.dt = 1; q.phases = 1; q.tr = 0;
+                        q.tiles_y = (so.H + th - 1) / th; q.tiles_x = (so.W + tw - 1) / tw;
+                        q.ntiles = B * q.tiles_y * q.tiles_x;
+                        q.w1 = dw + p1.o_w; q.b1 = (const float *)(dw + p1.o_bias); q.s1 = (const float *)(dw + p1.o_s1);
+                        q.w2 = dw + p2.o_w; q.b2 = (const float *)(dw + p2.o_bias); q.s2 = (const float *)(dw + p2.o_s1);
+                        q.w2b = q.w2; q.b2b = q.b2; q.s2b = q.s2;
+                        q.w3 = dw + p3.o_w; q.b3 = (const float *)(dw + p3.o_bias); q.s3 = (const float *)(dw + p3.o_s1);
+                        q.s_out = (const float *)(dw + p3.o_s2);
+                        q.slopes_le1 = 1;
+                        q.x_bytes = (uint32_t)std::min<size_t>(tbytes(so), 0x7fffffff);
+                        q.xin = curp;
+                        q.xin_bytes = (uint32_t)std::min<size_t>(tbytes(cur), 0x7fffffff);
+                        q.pool = T[0];
+                        q.pool_bytes = (uint32_t)std::min<size_t>(tbytes(sp), 0x7fffffff);
+                        q.idx_out = idx[bi]; q.idxCS = idxCS;
+                        q.idx_bytes = (uint32_t)std::min<size_t>((size_t)B * so.H * so.W * idxCS, 0x7fffffff);
+                        const double px = (double)B * so.H * so.W;
+                        double wb = 0, fl = 0;
+                        for (int i = 0; i < 3; ++i) { wb += (double)P(i).Npad * P(i).Kpad * es; fl += 2.0 * P(i).macs_per_px * px; }
+                        op.flops = fl;
+                        // x read once, out + indices written once (the pooled scratch round trip is L2)
+                        op.bytes = (double)tbytes(cur) + (double)tbytes(so) + px * idxCS + wb;
+                        op.layer_bytes = (double)tbytes(cur) * 2 + 2.0 * (tbytes(s1) + tbytes(s2)) + (double)tbytes(so) +
+                                         px * idxCS + wb;
+                        ops.push_back(op);
+                    }
+                    cur = so;
+                    break;
+                }
                 if (fill) {
                     Op o1, o2, o3;
                     conv(P(0), EPI_PLAIN, curp, cur, s1, T[0], s1, o1);
@@ -902,7 +978,8 @@ bool build_plan(bugseg_ctx *ctx, int B, int H, int W, std::string &why) {
     for (Op &op : w.ops) {
         if (op.kind == 1) {
             const double bytes = (double)op.bn.B * op.bn.H * op.bn.W * op.bn_c * w.es;
-            if (bytes >= 2147483648.0) { why = "batch too large for 32-bit tensor offsets"; return false; }
+            const double in_bytes = op.bn_cin ? 4.0 * op.bn.B * op.bn.H * op.bn.W * op.bn_cin * w.es : 0.0;
+            if (bytes >= 2147483648.0 || in_bytes >= 2147483648.0) { why = "batch too large for 32-bit tensor offsets"; return false; }
             op.bn.x_bytes = (uint32_t)bytes;
             continue;
         }
@@ -1102,7 +1179,7 @@ static int enet_forward(bugseg_ctx *ctx, const void *in, bool bgr, int B, int H,
     }
     for (size_t i = 0; i < pl.ops.size(); ++i) {
         const Op &op = pl.ops[i];
-        hipError_t e = op.kind == 1 ? launch_bneck(ctx->prec, op.bn_c, op.bn_asym, op.bn_var, op.bn, (hipStream_t)stream)
+        hipError_t e = op.kind == 1 ? launch_bneck(ctx->prec, op.bn_c, op.bn_asym, op.bn_var, op.bn, (hipStream_t)stream, op.bn_cin)
                      : op.kind == 2 ? launch_up(ctx->prec, op.up_cin, op.up_it, op.up_cout, op.up, (hipStream_t)stream)
                                     : launch_conv(ctx->prec, op.nr, op.epi, op.a, (hipStream_t)stream);
         if (e != hipSuccess) return fail(ctx, BUGSEG_EHIP, "conv launch " + std::to_string(i) + ": " + hipGetErrorString(e));
@@ -1317,8 +1394,8 @@ int bugseg_plan_op(bugseg_ctx *ctx, int B, int H, int W, int op, char *kernel, i
     } else if (o.kind == 1) {
         int th, tw, nw;
         bneck_shape(o.bn_c, o.bn_var, th, tw, nw, nullptr);
-        tag = "bneck C" + std::to_string(o.bn_c) + (o.bn_asym ? " asym" : "") + " " + std::to_string(th) + "x" +
-              std::to_string(tw);
+        tag = std::string(o.bn_cin ? "down C" : "bneck C") + std::to_string(o.bn_c) + (o.bn_asym ? " asym" : "") + " " +
+              std::to_string(th) + "x" + std::to_string(tw);
         (void)nw;
     }
     else if (o.epi == EPI_INIT || o.epi == EPI_INIT_BGR) tag = "init";
@@ -1353,7 +1430,7 @@ int bugseg_plan_launch_op(bugseg_ctx *ctx, int B, int H, int W, int op, void *st
     if (op < 0 || op >= (int)pl.ops.size()) return fail(ctx, BUGSEG_EINVAL, "op index out of range");
     DeviceGuard g(ctx->device);
     const Op &o = pl.ops[op];
-    hipError_t e = o.kind == 1 ? launch_bneck(ctx->prec, o.bn_c, o.bn_asym, o.bn_var, o.bn, (hipStream_t)stream)
+    hipError_t e = o.kind == 1 ? launch_bneck(ctx->prec, o.bn_c, o.bn_asym, o.bn_var, o.bn, (hipStream_t)stream, o.bn_cin)
                  : o.kind == 2 ? launch_up(ctx->prec, o.up_cin, o.up_it, o.up_cout, o.up, (hipStream_t)stream)
                                : launch_conv(ctx->prec, o.nr, o.epi, o.a, (hipStream_t)stream);
     if (e != hipSuccess) return fail(ctx, BUGSEG_EHIP, "launch of op " + std::to_string(op) + ": " + hipGetErrorString(e));
