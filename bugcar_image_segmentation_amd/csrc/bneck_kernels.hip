@@ -429,6 +429,21 @@ __global__ void __launch_bounds__((BShape<C, V>::NW * 64), (sizeof(T) == 2 ? BSh
         };
         if constexpr (!ASYM) prefetch_res();
 
+        // t1 never goes through LDS: each wave's middle-conv accumulators (quads: lane kq holds channels
+        // 4kq..4kq+3 of a pixel) are rounded as the unfused plan stores them and turned into the
+        // expansion's B operand (lane kq: channels 8kq..8kq+7) with two lane swaps (to_bop) — the
+        // expansion of a fragment runs on the wave that computed it, so no barrier is needed either
+        Raw tf[NF2];
+        auto to_tf = [&](const f32x4 (&acc)[NF2][NR1], const float *cs) {
+#pragma unroll
+            for (int j = 0; j < NF2; ++j) {
+                const float4 q0 = act(f4(acc[j][0]), cs + kq * 4);
+                const float4 q1 = NR1 > 1 ? act(f4(acc[j][NR1 > 1 ? 1 : 0]), cs + 16 + kq * 4) : make_float4(0.f, 0.f, 0.f, 0.f);
+                to_bop(tf[j], q0, q1);
+            }
+        };
+        static_assert(NR1 <= 2, "t1 in registers: at most 32 internal channels");
+
         // ---- phase 2: t1 = act2(W2 * t0 + b2) (asymmetric: t1a = 5x1 (t0); t1 = 1x5 (t1a))
         if constexpr (!ASYM) {
             f32x4 acc[NF2][NR1];
@@ -462,19 +477,7 @@ __global__ void __launch_bounds__((BShape<C, V>::NW * 64), (sizeof(T) == 2 ? BSh
                 }
             }
             STAMP(4);
-            __syncthreads();   // every wave is done reading t0
-#pragma unroll
-            for (int j = 0; j < NF2; ++j) {
-                if (wave + NW * j >= NFT) continue;
-                const int p = (wave + NW * j) * 16 + col;
-                if (p >= NPX) continue;
-#pragma unroll
-                for (int r = 0; r < NR1; ++r) {
-                    const int ch = r * 16 + kq * 4;
-                    if (ch >= IS) continue;
-                    st4(ts + p * PSTR + ch, act(f4(acc[j][r]), cs2 + ch));
-                }
-            }
+            to_tf(acc, cs2);
         } else {
             {   // 5x1 over rows (taps dy = -2..2), output width TW+4 (the 1x5's halo)
                 f32x4 acc[NF2A][NR1];
@@ -548,22 +551,9 @@ __global__ void __launch_bounds__((BShape<C, V>::NW * 64), (sizeof(T) == 2 ? BSh
                     }
                 }
                 prefetch_res();
-                __syncthreads();
-#pragma unroll
-                for (int j = 0; j < NF2; ++j) {
-                    if (wave + NW * j >= NFT) continue;
-                    const int p = (wave + NW * j) * 16 + col;
-                    if (p >= NPX) continue;
-#pragma unroll
-                    for (int r = 0; r < NR1; ++r) {
-                        const int ch = r * 16 + kq * 4;
-                        if (ch >= IS) continue;
-                        st4(ts + p * PSTR + ch, act(f4(acc[j][r]), cs2b + ch));
-                    }
-                }
+                to_tf(acc, cs2b);
             }
         }
-        __syncthreads();
 
         // ---- phase 3: out = act_out(act3(W3 t1 + b3) + x), entirely in registers. An accumulator
         // quad is 4 consecutive channels of one pixel (lane = (pixel col, quad kq)); in bf16 two
@@ -573,15 +563,10 @@ __global__ void __launch_bounds__((BShape<C, V>::NW * 64), (sizeof(T) == 2 ? BSh
         // that chunk layout and the same (involutive) swap returns it to accumulator quads. fp32
         // quads are already 16-B chunks; C = 16 (one row) stores its 8-B quads (a 16-pixel
         // fragment of 32-B pixels is one 512-B run). No LDS staging, no wave syncs.
-        Raw tf[NF2];
-#pragma unroll
-        for (int j = 0; j < NF2; ++j) {
-            const int p = (wave + NW * j) * 16 + col;
-            ld8(tf[j], kq < G3 && p < NPX ? ts + p * PSTR + kq * 8 : zpad);
-        }
         if constexpr (!REG3) {
-            // staged epilogue: the t1 region becomes per-wave staging — residual chunks in, results
-            // over them, and the fragment leaves as contiguous 16-B-per-lane stores
+            // staged epilogue: the t0 region becomes per-wave staging (once every wave is done
+            // reading t0) — residual chunks in, results over them, and the fragment leaves as
+            // contiguous 16-B-per-lane stores
             __syncthreads();
             STAMP(5);
             T *stg = ts + wave * 16 * OSTR;

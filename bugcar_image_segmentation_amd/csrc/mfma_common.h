@@ -172,6 +172,37 @@ __device__ __forceinline__ float vmax(float a, float b) {
     asm("v_max_f32 %0, %1, %2" : "=v"(r) : "v"(a), "v"(b));
     return r;
 }
+// storage rounding of an activation (the unfused plan stores it as T and reads it back)
+__device__ __forceinline__ float4 round_t(float4 v, const __bf16 *) { return unpack_bf16x4(pack_bf16x4(v)); }
+__device__ __forceinline__ float4 round_t(float4 v, const float *) { return v; }
+
+// Two 16-channel row fragments (quads qa, qb: lane kq holds channels 4kq..4kq+3 of each) -> the B
+// operand of one 32-channel k-step (lane kq holds channels 8kq..8kq+7):
+//   permlane32_swap: lanes kq 2,3 of qa <- lanes kq 0,1 of qb, lanes kq 0,1 of qb <- kq 2,3 of qa;
+//   permlane16_swap: odd rows of qa' <-> even rows of qb'.
+// Afterwards lane kq holds (qa'', qb'') = channels 8kq..8kq+3 and 8kq+4..8kq+7 (measured semantics:
+// scripts/permlane_probe.hip). qb == 0 for a single fragment (k groups 2, 3 zero).
+__device__ __forceinline__ void to_bop(RawB &r, float4 qa, float4 qb) {
+    const u32x2_t a = pack_bf16x4(qa), b = pack_bf16x4(qb);
+    uint32_t a0 = a.x, a1 = a.y, b0 = b.x, b1 = b.y;
+    pl32swap(a0, b0);
+    pl32swap(a1, b1);
+    pl16swap(a0, b0);
+    pl16swap(a1, b1);
+    r.v = make_uint4(a0, a1, b0, b1);
+}
+__device__ __forceinline__ void to_bop(RawF &r, float4 qa, float4 qb) {
+    uint32_t a[4] = {__float_as_uint(qa.x), __float_as_uint(qa.y), __float_as_uint(qa.z), __float_as_uint(qa.w)};
+    uint32_t b[4] = {__float_as_uint(qb.x), __float_as_uint(qb.y), __float_as_uint(qb.z), __float_as_uint(qb.w)};
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+        pl32swap(a[i], b[i]);
+        pl16swap(a[i], b[i]);
+    }
+    r.a = make_float4(__uint_as_float(a[0]), __uint_as_float(a[1]), __uint_as_float(a[2]), __uint_as_float(a[3]));
+    r.b = make_float4(__uint_as_float(b[0]), __uint_as_float(b[1]), __uint_as_float(b[2]), __uint_as_float(b[3]));
+}
+
 __device__ __forceinline__ float4 prelu4m(float4 v, float4 s) {
     return make_float4(vmax(v.x, v.x * s.x), vmax(v.y, v.y * s.y), vmax(v.z, v.z * s.z), vmax(v.w, v.w * s.w));
 }
