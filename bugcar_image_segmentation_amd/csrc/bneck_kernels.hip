@@ -117,8 +117,10 @@ __global__ void __launch_bounds__((BShape<C, V>::NW * 64), (sizeof(T) == 2 ? BSh
     // phase-3 chunking (see phase 3): bf16 with an even number of 16-row blocks swaps row pairs
     // into 16-B chunks; bf16 C = 16 stores 8-B quads (HALF); fp32 quads are 16-B chunks
     // REG3: the register epilogue (C = 128 and 16). C = 64 keeps the LDS-staged epilogue: its 128-B
-    // pixels would be written as half lines by the register layout, which measured slower there.
-    constexpr bool REG3 = C != 64;
+    // pixels would be written as half lines by the register layout, which measured slower there
+    // (44.7 vs 43.0 us per launch with t1 in registers).
+    // (the down form's C = 64 launch measured faster with the register epilogue: 53 vs 55 us)
+    constexpr bool REG3 = C != 64 || DN;
     constexpr bool SWAP = REG3 && sizeof(T) == 2 && NR3 % 2 == 0;
     constexpr bool HALF = REG3 && sizeof(T) == 2 && NR3 % 2 != 0;
     constexpr int EPC = 16 / (int)sizeof(T);          // elements per 16-B chunk
