@@ -79,6 +79,21 @@ __global__ void __launch_bounds__(256, (sizeof(T) == 2 ? (CIN >= 128 ? 2 : 3) : 
     const int nfrag = (a.M + 15) >> 4;
     const int gw = blockIdx.x * 4 + __builtin_amdgcn_readfirstlane(tid >> 6), nw = gridDim.x * 4;
 
+    // The grid is sized to the resident waves (launch_up) and each wave streams over fragments: the
+    // next fragment's block input and pooling indices are in flight while this one computes.
+    Raw xn[KS1];
+    uint32_t idn[NM];
+    auto load = [&](int f) {
+        const int p = f * 16 + col;
+        const bool pv = p < a.M;
+#pragma unroll
+        for (int s = 0; s < KS1; ++s) bld8(xn[s], rx, pv ? (uint32_t)(p * CIN + s * 32 + kq * 8) * ES : OOB);
+        // pooling indices of this pixel's main channels (one byte per channel: window position)
+#pragma unroll
+        for (int r = 0; r < NM; ++r)
+            idn[r] = __builtin_amdgcn_raw_buffer_load_b32(ri, pv ? (int)(p * a.idxCS + r * 16 + kq * 4) : (int)OOB, 0, 0);
+    };
+    if (gw < nfrag) load(gw);
     for (int f = gw; f < nfrag; f += nw) {
         const int p = f * 16 + col;
         const bool pv = p < a.M;
@@ -88,13 +103,12 @@ __global__ void __launch_bounds__(256, (sizeof(T) == 2 ? (CIN >= 128 ? 2 : 3) : 
 
         // ---- GEMM 1: [main; e1] = W1 . x  (the block input read once, 16 B per lane per k-step)
         Raw xf[KS1];
-#pragma unroll
-        for (int s = 0; s < KS1; ++s) bld8(xf[s], rx, pv ? (uint32_t)(p * CIN + s * 32 + kq * 8) * ES : OOB);
-        // pooling indices of this pixel's main channels (one byte per channel: window position)
         uint32_t id[NM];
 #pragma unroll
-        for (int r = 0; r < NM; ++r)
-            id[r] = __builtin_amdgcn_raw_buffer_load_b32(ri, pv ? (int)(p * a.idxCS + r * 16 + kq * 4) : (int)OOB, 0, 0);
+        for (int s = 0; s < KS1; ++s) xf[s] = xn[s];
+#pragma unroll
+        for (int r = 0; r < NM; ++r) id[r] = idn[r];
+        if (f + nw < nfrag) load(f + nw);
         f32x4 acc1[NR1];
 #pragma unroll
         for (int r = 0; r < NR1; ++r) acc1[r] = B1ACC ? bias4(cb1 + r * 16 + kq * 4) : (f32x4){0.f, 0.f, 0.f, 0.f};
@@ -205,10 +219,29 @@ static hipError_t launch_shape(int prec, const UpArgs &a, dim3 g, hipStream_t s)
     return hipGetLastError();
 }
 
+// workgroups resident at once (occupancy API, per kernel instance), cached
+template <typename T, int CI, int II, int CO>
+static int up_resident() {
+    static int n = 0;
+    if (n == 0) {
+        int dev = 0, cus = 0, per = 0;
+        if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
+            cus = 256;
+        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, (const void *)up_kernel<T, CI, II, CO>, 256, up_lds<T, CI, II, CO>()) !=
+                hipSuccess || per <= 0)
+            per = 2;
+        n = cus * per;
+    }
+    return n;
+}
+
 hipError_t launch_up(int prec, int cin, int it, int cout, const UpArgs &a, hipStream_t s) {
     const int nfrag = (a.M + 15) / 16;
     int g = (nfrag + 3) / 4;
-    if (g > 2048) g = 2048;
+    // one resident round of workgroups, each streaming over its fragments (prefetch in the kernel)
+    const int res = cin == 128 ? (prec == PREC_BF16 ? up_resident<__bf16, 128, 32, 64>() : up_resident<float, 128, 32, 64>())
+                               : (prec == PREC_BF16 ? up_resident<__bf16, 64, 16, 16>() : up_resident<float, 64, 16, 16>());
+    if (g > res) g = res;
     if (g < 1) g = 1;
     if (cin == 128 && it == 32 && cout == 64) return launch_shape<128, 32, 64>(prec, a, dim3(g), s);
     if (cin == 64 && it == 16 && cout == 16) return launch_shape<64, 16, 16>(prec, a, dim3(g), s);
