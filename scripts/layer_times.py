@@ -18,6 +18,9 @@ BNECK_SHAPES = {(128, 0): "16x16", (128, 1): "20x16", (128, 2): "4x80", (128, 3)
 
 
 def short(name):
+    m = re.search(r"bneck_kernelI(DF16b|f)Li(\d+)ELb(\d)ELi(\d+)ELb\dELi([1-9]\d*)E", name)
+    if m:   # the downsampling form (non-zero input-channel template argument)
+        return f"down C{m.group(2)} {BNECK_SHAPES.get((int(m.group(2)), int(m.group(4))), '?')}"
     m = re.search(r"bneck_kernelI(DF16b|f)Li(\d+)ELb(\d)ELi(\d+)E", name)
     if not m:
         m = re.search(r"bneck_kernel<(__bf16|float), (\d+), (false|true), (\d+)>", name)
