@@ -41,7 +41,7 @@ stream = torch.cuda.current_stream()
 seen = set()
 for i in range(n):
     tag = m.ctx.plan_op(B, H, W, i)[0]
-    if not tag.startswith("bneck") or tag in seen:
+    if not (tag.startswith("bneck") or tag.startswith("down")) or tag in seen:
         continue
     seen.add(tag)
     for _ in range(3):
