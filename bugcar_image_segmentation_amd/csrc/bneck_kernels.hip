@@ -614,12 +614,12 @@ __global__ void __launch_bounds__((BShape<C, V>::NW * 64), (sizeof(T) == 2 ? BSh
 #pragma unroll
                 for (int r = 0; r < NR3; ++r) {
                     const int ch = r * 16 + kq * 4;
-                    f32x4 acc = bias_in_acc(NR3) ? bias4(cb3 + ch) : (f32x4){0.f, 0.f, 0.f, 0.f};
+                    f32x4 acc = bias_in_acc(NR3, 1) ? bias4(cb3 + ch) : (f32x4){0.f, 0.f, 0.f, 0.f};
                     Raw wf;
                     ld8(wf, w3 + (r * 16 + col) * K3S + kq * 8);
                     mma(acc, wf, tf[j]);
                     T *sp = stg + col * OSTR + ch;
-                    float4 v = act(bias_in_acc(NR3) ? f4(acc) : add4(f4(acc), ld4f(cb3 + ch)), cs3 + ch);
+                    float4 v = act(bias_in_acc(NR3, 1) ? f4(acc) : add4(f4(acc), ld4f(cb3 + ch)), cs3 + ch);
                     v = act(add4(v, ld4(sp)), cso + ch);
                     st4(sp, v);
                 }
@@ -644,7 +644,7 @@ __global__ void __launch_bounds__((BShape<C, V>::NW * 64), (sizeof(T) == 2 ? BSh
             const uint32_t po = pix_base(wave + NW * j, col);
             auto out3 = [&](int r, const f32x4 &acc) {
                 const int ch = r * 16 + kq * 4;
-                return act(bias_in_acc(NR3) ? f4(acc) : add4(f4(acc), ld4f(cb3 + ch)), cs3 + ch);
+                return act(bias_in_acc(NR3, 1) ? f4(acc) : add4(f4(acc), ld4f(cb3 + ch)), cs3 + ch);
             };
 #pragma unroll
             for (int t = 0; t < RQ3; ++t) {
@@ -652,8 +652,8 @@ __global__ void __launch_bounds__((BShape<C, V>::NW * 64), (sizeof(T) == 2 ? BSh
                 const uint4 rc = res[j % RP][t];
                 if constexpr (SWAP) {
                     const int r0 = 2 * t, r1 = 2 * t + 1;
-                    f32x4 acc0 = bias_in_acc(NR3) ? bias4(cb3 + r0 * 16 + kq * 4) : (f32x4){0.f, 0.f, 0.f, 0.f};
-                    f32x4 acc1 = bias_in_acc(NR3) ? bias4(cb3 + r1 * 16 + kq * 4) : (f32x4){0.f, 0.f, 0.f, 0.f};
+                    f32x4 acc0 = bias_in_acc(NR3, 1) ? bias4(cb3 + r0 * 16 + kq * 4) : (f32x4){0.f, 0.f, 0.f, 0.f};
+                    f32x4 acc1 = bias_in_acc(NR3, 1) ? bias4(cb3 + r1 * 16 + kq * 4) : (f32x4){0.f, 0.f, 0.f, 0.f};
                     Raw w0, w1;
                     ld8(w0, w3 + (r0 * 16 + col) * K3S + kq * 8);
                     ld8(w1, w3 + (r1 * 16 + col) * K3S + kq * 8);
@@ -672,7 +672,7 @@ __global__ void __launch_bounds__((BShape<C, V>::NW * 64), (sizeof(T) == 2 ? BSh
                     bst16(rob, off, make_uint4(x0, x1, y0, y1));
                 } else {
                     const int r = t;
-                    f32x4 acc = bias_in_acc(NR3) ? bias4(cb3 + r * 16 + kq * 4) : (f32x4){0.f, 0.f, 0.f, 0.f};
+                    f32x4 acc = bias_in_acc(NR3, 1) ? bias4(cb3 + r * 16 + kq * 4) : (f32x4){0.f, 0.f, 0.f, 0.f};
                     Raw wf;
                     ld8(wf, w3 + (r * 16 + col) * K3S + kq * 8);
                     mma(acc, wf, tf[j]);

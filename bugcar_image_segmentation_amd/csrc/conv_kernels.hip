@@ -100,6 +100,7 @@ __global__ void __launch_bounds__(256, sizeof(T) == 2 ? (NR == 8 ? 3 : 4) : 1) c
     const auto rout = mkbuf(a.out, a.out_bytes);
     const auto rres = mkbuf(a.res, a.res_bytes);
     const bool fast = a.slopes_le1;
+    const bool bia = bias_in_acc(NR, a.Ksteps);            // bias placement (mfma_common.h), wave-uniform
     auto act1 = [&](float4 v, int c) { return fast ? prelu4m(v, ld4f(cs1 + c)) : prelu4(v, ld4f(cs1 + c)); };
     auto act2 = [&](float4 v, int c) { return fast ? prelu4m(v, ld4f(cs2 + c)) : prelu4(v, ld4f(cs2 + c)); };
 
@@ -171,7 +172,7 @@ __global__ void __launch_bounds__(256, sizeof(T) == 2 ? (NR == 8 ? 3 : 4) : 1) c
         for (int m = 0; m < MR; ++m)
 #pragma unroll
             for (int n = 0; n < NR; ++n)
-                acc[m][n] = bias_in_acc(NR) ? bias4(cbias + n * 16 + kq * 4) : (f32x4){0.f, 0.f, 0.f, 0.f};
+                acc[m][n] = bia ? bias4(cbias + n * 16 + kq * 4) : (f32x4){0.f, 0.f, 0.f, 0.f};
 
         // KC k-steps per chunk: all their B-fragment loads are issued before the first MFMA, so a
         // tile waits on memory ceil(Ksteps / KC) times instead of Ksteps times (the tap table is padded
@@ -281,7 +282,7 @@ __global__ void __launch_bounds__(256, sizeof(T) == 2 ? (NR == 8 ? 3 : 4) : 1) c
 #pragma unroll
                 for (int n = 0; n < NR; ++n) {
                     const int c = n * 16 + kq * 4;
-                    float4 v = bias_in_acc(NR) ? f4(acc[m][n]) : add4(f4(acc[m][n]), ld4f(cbias + c));
+                    float4 v = bia ? f4(acc[m][n]) : add4(f4(acc[m][n]), ld4f(cbias + c));
                     if constexpr (EPI == EPI_SHUFFLE) {
                         const int ph = phn[n], cl = cln[n] + kq * 4;
                         if (cl >= a.outC) continue;

@@ -210,7 +210,9 @@ __device__ __forceinline__ float4 prelu4m(float4 v, float4 s) {
 // fragments; with 8 (128 channels) the bias comes after, since bias-initialised accumulators are live
 // across the k loop's loads and would spill. Both kernels follow this rule, so a fused bottleneck and
 // its unfused launches stay bit-identical.
-__host__ __device__ constexpr bool bias_in_acc(int nr) { return nr < 8; }
+// A single-k-step launch (K <= 32: the 1x1 expansions, the up-block transposed conv) has no k loop
+// for the bias-initialised accumulators to live across, so it always starts from the bias.
+__host__ __device__ constexpr bool bias_in_acc(int nr, int ksteps = 2) { return nr < 8 || ksteps == 1; }
 __device__ __forceinline__ f32x4 bias4(const float *p) {
     const float4 b = *reinterpret_cast<const float4 *>(p);
     return (f32x4){b.x, b.y, b.z, b.w};

@@ -41,7 +41,7 @@ __global__ void __launch_bounds__(256, (sizeof(T) == 2 ? (CIN >= 128 ? 2 : 3) : 
     // expansion as their own row counts say
     static_assert(NM <= 4 && NE <= 4, "main / e1 launches must carry their bias in the accumulator");
     constexpr bool B1ACC = true;
-    constexpr bool B2ACC = bias_in_acc(NR2), B3ACC = bias_in_acc(NR3);
+    constexpr bool B2ACC = bias_in_acc(NR2, 1), B3ACC = bias_in_acc(NR3, 1);   // one k step each (K = I <= 32)
     // LDS: weights of the three GEMMs (+16 B row pad) and their per-row constants
     constexpr int K1S = CIN + 16 / ES, K2S = 32 + 16 / ES, K3S = 32 + 16 / ES;
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];

@@ -308,6 +308,24 @@ def test_class_layer_kernel_matches_conv_path(gpu, blocks, prec, monkeypatch):
     assert (la.argmax(axis=1)[decided] == lb.argmax(axis=1)[decided]).all()
 
 
+def test_canonical_plan_is_one_launch_per_block(gpu, blocks):
+    """At the bench shape every ENet block of the canonical graph runs as ONE fused launch: initial
+    block, 2 downsampling, 23 regular / dilated / asymmetric bottlenecks, 2 upsampling blocks and
+    the class layer (29 launches); the unfused reference plan has one launch per convolution."""
+    B, H, W = 2, 480, 640
+    m = ENET(weights=blocks, precision="bf16")
+    bgr = torch.from_numpy(synthetic.uniform_frames(B, H, W)).cuda()
+    seg = torch.empty((B, H, W), dtype=torch.uint8, device=gpu)
+    m.ctx.forward_bgr(bgr, B, H, W, N.OUT_CLASS3_U8, seg)
+    n = m.ctx.plan_info(B, H, W, N.OUT_CLASS3_U8, bgr_input=True)[0]
+    tags = [m.ctx.plan_op(B, H, W, i)[0] for i in range(n)]
+    assert n == 29
+    assert tags[0] == "init" and tags[-1] == "classes"
+    assert [t.split(" ")[0] + " " + t.split(" ")[1] for t in tags if t.startswith(("down", "up"))] == \
+        ["down C64", "down C128", "up C64", "up C16"]
+    assert sum(t.startswith("bneck") for t in tags) == 23
+
+
 def test_bev_shape_assert(gpu):
     bev = synthetic.synthetic_bev(120, 160, 300, 300)
     with pytest.raises(AssertionError):
