@@ -58,13 +58,29 @@ template <int C, int V> struct BShape;
 // are the tile's one-row halo and its horizontal taps stay inside the tile — masked at the image
 // edge, no horizontal halo stored. 4 x 80 tiles cover 60 x 80 at d = 8 and d = 16 in 16 tiles per
 // frame (the phase sub-images, 8 x 10 and 4 x 5, are far too small for square tiles).
-template <> struct BShape<128, 0> { static constexpr int TH = 16, TW = 16, NW = 8, OCC = 4, RP = 2, RD = 0; };
-template <> struct BShape<128, 1> { static constexpr int TH = 20, TW = 16, NW = 8, OCC = 4, RP = 2, RD = 0; };
-template <> struct BShape<128, 2> { static constexpr int TH = 4, TW = 80, NW = 8, OCC = 4, RP = 2, RD = 1; };
-template <> struct BShape<128, 3> { static constexpr int TH = 4, TW = 64, NW = 8, OCC = 4, RP = 2, RD = 1; };
-template <> struct BShape<64, 0> { static constexpr int TH = 16, TW = 16, NW = 4, OCC = 5, RP = 4, RD = 0; };
-template <> struct BShape<64, 1> { static constexpr int TH = 20, TW = 16, NW = 4, OCC = 5, RP = 3, RD = 0; };
-template <> struct BShape<16, 0> { static constexpr int TH = 16, TW = 16, NW = 4, OCC = 6, RP = 4, RD = 0; };
+template <> struct BShape<128, 0> { static constexpr int TH = 16, TW = 16, NW = 8, OCC = 4, RP = 2, RD = 0, WIDE = 1; };
+template <> struct BShape<128, 1> { static constexpr int TH = 20, TW = 16, NW = 8, OCC = 4, RP = 2, RD = 0, WIDE = 1; };
+template <> struct BShape<128, 2> { static constexpr int TH = 4, TW = 80, NW = 8, OCC = 4, RP = 2, RD = 1, WIDE = 0; };
+template <> struct BShape<128, 3> { static constexpr int TH = 4, TW = 64, NW = 8, OCC = 4, RP = 2, RD = 1, WIDE = 1; };
+template <> struct BShape<64, 0> { static constexpr int TH = 16, TW = 16, NW = 4, OCC = 5, RP = 4, RD = 0, WIDE = 1; };
+template <> struct BShape<64, 1> { static constexpr int TH = 20, TW = 16, NW = 4, OCC = 5, RP = 3, RD = 0, WIDE = 1; };
+template <> struct BShape<16, 0> { static constexpr int TH = 16, TW = 16, NW = 4, OCC = 6, RP = 4, RD = 0, WIDE = 1; };
+
+// LDS strides (elements). bf16: a 16-lane group of ds_read_b128 (one 16-B k group of 16 pixels or
+// weight rows) is conflict-free when the row stride is 8, 24, 40 or 56 dwords mod 64 (the SQ counters
+// had 35% of LDS cycles in bank conflicts with the 16-B pads): weight rows pad 16 elements; t0
+// pixels unpadded for 8 / 16 internal channels and 48 elements for 32 where the workgroup still fits
+// twice per CU (WIDE; asymmetric and 4x80 tiles keep 40); fp32 (parity mode) keeps 16-B pads.
+__host__ __device__ constexpr int bneck_padw(int es, int C, bool wide) { return es == 2 && (C != 128 || wide) ? 16 : 16 / es; }
+__host__ __device__ constexpr int bneck_pstr(int es, int IS, bool wide) {
+    return es != 2 ? IS + 16 / es : IS == 32 ? (wide ? 48 : 40) : IS;
+}
+static bool bneck_wide(int C, int v, bool asym) {
+#define BW_CASE(CC, VV) if (C == CC && v == VV) return BShape<CC, VV>::WIDE && !asym;
+    BW_CASE(128, 0) BW_CASE(128, 1) BW_CASE(128, 2) BW_CASE(128, 3) BW_CASE(64, 0) BW_CASE(64, 1) BW_CASE(16, 0)
+#undef BW_CASE
+    return false;
+}
 
 int bneck_variants(int C) { return C == 128 ? 4 : C == 64 ? 2 : 1; }
 
@@ -104,8 +120,9 @@ __global__ void __launch_bounds__((BShape<C, V>::NW * 64), (sizeof(T) == 2 ? BSh
     constexpr int RX = RD ? 0 : RY;                   // row-dilated tiles span the width: no column halo
     constexpr int HWW = TW + 2 * RX, HR = (TH + 2 * RY) * HWW;
     constexpr int NF1 = (HR + 15) / 16;               // 16-pixel fragments of tile + halo
-    constexpr int PAD = 16 / (int)sizeof(T);
-    constexpr int PSTR = IS + PAD;                    // LDS pixel stride (elements)
+    constexpr bool WIDE = BShape<C, V>::WIDE && !ASYM;
+    constexpr int PADW = bneck_padw((int)sizeof(T), C, WIDE);   // weight-row pad (elements)
+    constexpr int PSTR = bneck_pstr((int)sizeof(T), IS, WIDE);  // LDS pixel stride (elements)
     constexpr int NPX = TH * TW;
     constexpr int NFT = (NPX + 15) / 16;              // 16-pixel fragments of the tile
     constexpr int NF2 = (NFT + NW - 1) / NW;          // ... per wave (the last may be partial / absent)
@@ -137,7 +154,7 @@ __global__ void __launch_bounds__((BShape<C, V>::NW * 64), (sizeof(T) == 2 ? BSh
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);   // provably uniform: scalar fragment math
     // first channel of this lane's phase-3 chunk t
     auto chunk_ch = [&](int t) -> int { return SWAP ? (2 * t + (kq & 1)) * 16 + 8 * (kq >> 1) : t * 16 + kq * 4; };
-    const int K1S = KS1 * 32 + PAD, K2S = KS2 * 32 + PAD, K3S = 32 + PAD;
+    const int K1S = KS1 * 32 + PADW, K2S = KS2 * 32 + PADW, K3S = 32 + PADW;
     T *w1 = reinterpret_cast<T *>(smem);
     T *w2 = w1 + NR1 * 16 * K1S;
     T *w2b = w2 + NR1 * 16 * K2S;                     // asymmetric second conv (1x5)
@@ -704,9 +721,11 @@ size_t bneck_lds_bytes(int prec, int C, bool asym, int v, int cin) {
     const int I = cin > 0 ? cin / 4 : C / 4, IS = I < 8 ? 8 : I, NR1 = (I + 15) / 16;
     const int KS1 = ((cin > 0 ? cin / 2 : C / 8) + 3) / 4, KS2 = ((asym ? 5 : 9) * IS / 8 + 3) / 4;
     const int R = asym ? 2 : 1, RX = RD ? 0 : R;
-    const size_t wts = (size_t)NR1 * 16 * (KS1 * 32 + pad) + (size_t)NR1 * 16 * (KS2 * 32 + pad) * (asym ? 2 : 1) +
-                       (size_t)C * (32 + pad);
-    const size_t halo = (size_t)(TH + 2 * R) * (TW + 2 * RX) * (IS + pad);
+    const bool wide = bneck_wide(C, v, asym);
+    const int padw = bneck_padw(es, C, wide);
+    const size_t wts = (size_t)NR1 * 16 * (KS1 * 32 + padw) + (size_t)NR1 * 16 * (KS2 * 32 + padw) * (asym ? 2 : 1) +
+                       (size_t)C * (32 + padw);
+    const size_t halo = (size_t)(TH + 2 * R) * (TW + 2 * RX) * bneck_pstr(es, IS, wide);
     const size_t stage = C == 64 ? (size_t)NW * 16 * (C + pad) : 0;    // staged epilogue (REG3 off)
     const size_t consts = ((size_t)6 * NR1 * 16 + 3 * (size_t)C) * sizeof(float);
     return (wts + 16 + (halo > stage ? halo : stage)) * es + consts;   // + the zero pad
