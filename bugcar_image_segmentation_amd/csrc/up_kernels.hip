@@ -43,7 +43,10 @@ __global__ void __launch_bounds__(256, (sizeof(T) == 2 ? (CIN >= 128 ? 2 : 3) : 
     constexpr bool B1ACC = true;
     constexpr bool B2ACC = bias_in_acc(NR2, 1), B3ACC = bias_in_acc(NR3, 1);   // one k step each (K = I <= 32)
     // LDS: weights of the three GEMMs (+16 B row pad) and their per-row constants
-    constexpr int K1S = CIN + 16 / ES, K2S = 32 + 16 / ES, K3S = 32 + 16 / ES;
+    // row pads: bf16 16 elements (row strides 8 / 24 / 40 dwords mod 64: conflict-free ds_read_b128
+    // groups, bneck_kernels.hip bneck_padw), fp32 16 B
+    constexpr int UPAD = ES == 2 ? 16 : 16 / ES;
+    constexpr int K1S = CIN + UPAD, K2S = 32 + UPAD, K3S = 32 + UPAD;
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     T *w1 = reinterpret_cast<T *>(smem);
     T *w2 = w1 + NR1 * 16 * K1S;
@@ -194,7 +197,8 @@ template <typename T, int CIN, int I, int COUT>
 static size_t up_lds() {
     constexpr int ES = (int)sizeof(T);
     constexpr int NR1 = (COUT + I) / 16, NR2 = 4 * I / 16, NR3 = COUT / 16;
-    return (size_t)(NR1 * 16 * (CIN + 16 / ES) + NR2 * 16 * (32 + 16 / ES) + NR3 * 16 * (32 + 16 / ES)) * ES +
+    constexpr int UPAD = ES == 2 ? 16 : 16 / ES;      // = up_kernel's
+    return (size_t)(NR1 * 16 * (CIN + UPAD) + NR2 * 16 * (32 + UPAD) + NR3 * 16 * (32 + UPAD)) * ES +
            (size_t)(2 * NR1 * 16 + 2 * NR2 * 16 + 3 * NR3 * 16) * sizeof(float);
 }
 
