@@ -234,7 +234,7 @@ def test_forward_bgr_equals_preprocess_then_forward(gpu, prec, pool_k):
 
 @pytest.mark.parametrize("variant", [None, "0", "1", "2", "3"])
 @pytest.mark.parametrize("prec", ["fp32", "bf16"])
-@pytest.mark.parametrize("H,W", [(64, 96), (120, 160), (480, 640)])
+@pytest.mark.parametrize("H,W", [(64, 96), (72, 104), (120, 160), (480, 640)])
 def test_fused_bottlenecks_equal_unfused(gpu, blocks, prec, H, W, variant, monkeypatch):
     """The fused bottleneck kernel (projection + middle conv + expansion + residual, internals in
     LDS) rounds the internal tensors exactly as the unfused conv chain stores them: bit-identical.
