@@ -205,8 +205,12 @@ def _tensor(buf: list, a) -> None:
     buf.append(a.tobytes())
 
 
-def serialize(blocks, num_classes: int = NUM_CLASSES) -> bytes:
-    """Block list -> BSG1 weight blob (format in the module docstring)."""
+def serialize(blocks, num_classes: int | None = None) -> bytes:
+    """Block list -> BSG1 weight blob (format in the module docstring). num_classes defaults to the
+    final transposed conv's class count."""
+    if num_classes is None:
+        fc = [b for b in blocks if b.type == "fullconv"]
+        num_classes = int(fc[-1].attrs["classes"]) if fc else NUM_CLASSES
     out = [b"BSG1", struct.pack("<III", 1, len(blocks), num_classes)]
     for b in blocks:
         attrs = [int(b.attrs[k]) for k in _ATTR_ORDER[b.type]]

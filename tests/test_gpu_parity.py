@@ -97,6 +97,23 @@ def test_fullconv_k2_and_pool2_variants(gpu):
     assert np.abs(m.logits(x) - ref).max() < LOGIT_TOL
 
 
+@pytest.mark.parametrize("ncls", [3, 16])
+def test_class_counts(gpu, ncls):
+    """The class layer at other class counts (the kernel masks padding classes): 3 (the reference's
+    road / obstacle / background head) and 16 (no padding), fp32 against the oracle."""
+    bl = enet_spec.build_enet(seed=20 + ncls, num_classes=ncls)
+    m = ENET(weights=bl, precision="fp32")
+    assert m.num_classes == ncls
+    x = np.random.default_rng(ncls).normal(size=(1, 3, 64, 96)).astype(np.float32)
+    ref = eo.forward(bl, x)
+    got = m.logits(x)
+    assert got.shape == ref.shape == (1, ncls, 64, 96)
+    assert np.abs(got - ref).max() < LOGIT_TOL
+    decided = _margin(ref) > MARGIN
+    raw = m.predict_device(m.engine_input(x), N.OUT_CLASS15_U8).cpu().numpy()
+    assert (raw[decided] == eo.argmax_classes(ref)[decided]).all()
+
+
 @pytest.mark.parametrize("shape,dsize", [((512, 512), (512, 256)), ((480, 640), (512, 256)),
                                          ((256, 512), (512, 256)), ((100, 130), (64, 48)),
                                          ((512, 1024), (512, 256)), ((37, 41), (96, 80))])
