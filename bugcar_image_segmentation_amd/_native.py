@@ -25,7 +25,10 @@ EXPORTED = ("bugseg_version", "bugseg_create", "bugseg_destroy", "bugseg_load_we
             "bugseg_input_bytes", "bugseg_preprocess", "bugseg_nchw_to_input", "bugseg_enet_forward",
             "bugseg_enet_forward_bgr",
             "bugseg_bev_occgrid", "bugseg_plan_info", "bugseg_plan_op", "bugseg_plan_launch_op",
-            "bugseg_last_error")
+            "bugseg_last_error",
+            "bugseg_dl_create", "bugseg_dl_destroy", "bugseg_dl_load_weights", "bugseg_dl_set_plan",
+            "bugseg_dl_forward", "bugseg_dl_launch_op", "bugseg_dl_read_buffer", "bugseg_dl_last_error")
+DL_OP_FIELDS = 32
 
 
 class BevParams(ctypes.Structure):
@@ -76,6 +79,14 @@ def load_library(path: Path | str | None = None) -> ctypes.CDLL:
                                    ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_double)]),
             "bugseg_plan_launch_op": (i, [vp, i, i, i, i, vp]),
             "bugseg_last_error": (cp, [vp]),
+            "bugseg_dl_create": (i, [i, i, ctypes.POINTER(vp)]),
+            "bugseg_dl_destroy": (i, [vp]),
+            "bugseg_dl_load_weights": (i, [vp, vp, sz]),
+            "bugseg_dl_set_plan": (i, [vp, vp, i, vp, i, i, i, i]),
+            "bugseg_dl_forward": (i, [vp, vp, i, i, i, vp, vp]),
+            "bugseg_dl_launch_op": (i, [vp, i, vp]),
+            "bugseg_dl_read_buffer": (i, [vp, i, vp, sz, vp]),
+            "bugseg_dl_last_error": (cp, [vp]),
         }
         for name, (res, args) in proto.items():
             f = getattr(lib, name)
@@ -197,3 +208,57 @@ def shared_context(device: int | None = None) -> Context:
             _shared.setdefault(d, c)
             c = _shared[d]
     return c
+
+
+class DeepLabContext:
+    """Owns one bugseg_dl (DeepLabV3 executor: weights + op list + activation arena), include/bugseg.h."""
+
+    def __init__(self, device: int | None = None, precision: int = BF16):
+        require_gpu()
+        self.lib = load_library()
+        self.device = torch.cuda.current_device() if device is None else int(device)
+        self.precision = precision
+        h = ctypes.c_void_p()
+        self._check(self.lib.bugseg_dl_create(self.device, precision, ctypes.byref(h)), None)
+        self.h = h
+
+    def _check(self, code, h):
+        if code != OK:
+            msg = self.lib.bugseg_dl_last_error(h).decode(errors="replace")
+            if code == EINVAL:
+                raise ValueError(msg)
+            raise BugsegError(code, msg)
+
+    def close(self) -> None:
+        if getattr(self, "h", None) and self.h.value:
+            self.lib.bugseg_dl_destroy(self.h)
+            self.h = ctypes.c_void_p()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def load_weights(self, blob: bytes) -> None:
+        buf = ctypes.create_string_buffer(blob, len(blob))
+        self._check(self.lib.bugseg_dl_load_weights(self.h, buf, len(blob)), self.h)
+
+    def set_plan(self, ops, buf_bytes, B: int, Hc: int, Wc: int) -> None:
+        import numpy as np
+        o = np.ascontiguousarray(ops, dtype=np.int32)
+        assert o.ndim == 2 and o.shape[1] == DL_OP_FIELDS
+        b = np.ascontiguousarray(buf_bytes, dtype=np.uint64)
+        self._check(self.lib.bugseg_dl_set_plan(self.h, o.ctypes.data, o.shape[0], b.ctypes.data, b.shape[0], B, Hc, Wc),
+                    self.h)
+
+    def forward(self, rgb, B, H, W, out, stream=None):
+        self._check(self.lib.bugseg_dl_forward(self.h, rgb.data_ptr(), B, H, W, out.data_ptr(), stream_handle(stream)),
+                    self.h)
+
+    def launch_op(self, op, stream=None):
+        self._check(self.lib.bugseg_dl_launch_op(self.h, op, ctypes.c_void_p(stream_handle(stream))), self.h)
+
+    def read_buffer(self, buf, out, stream=None):
+        self._check(self.lib.bugseg_dl_read_buffer(self.h, buf, out.data_ptr(), out.numel() * out.element_size(),
+                                                   ctypes.c_void_p(stream_handle(stream))), self.h)

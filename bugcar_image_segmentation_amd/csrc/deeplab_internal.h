@@ -1,0 +1,73 @@
+// Internal interface between the DeepLab executor (deeplab_runtime.cpp) and its gfx950 kernels
+// (deeplab_kernels.hip). SURVEY.md §8(f) row 3 / BASELINE config 4.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace bugseg {
+
+struct DlPrepArgs {
+    const uint8_t *rgb;  // (B, H, W, 3) u8, the ImageTensor feed (models.py:123-124)
+    int B, H, W;         // H <= Hc, W <= Wc
+    int Hc, Wc;          // crop size (513): the padded engine input
+    void *out;           // (B, Hc, Wc, 8) T
+};
+
+struct DlConvArgs {
+    const void *in;      // NHWC (B, Hin, Win, CS) T
+    int B, Hin, Win, CS;
+    int Hout, Wout, M;   // M = B * Hout * Wout
+    int kh, kw, taps, stride, dil, pad_t, pad_l;
+    int cinP;            // input channels padded to 32 (packing of w)
+    int NP;              // output channels padded to 64 (rows of w)
+    const void *w;       // [NP][taps][cinP] T
+    const float *bias;   // [NP]
+    const float *bias_img;  // optional per-image bias (B, bias_img_stride) f32
+    int bias_img_stride;
+    int act;             // 0 none, 1 ReLU, 2 ReLU6
+    const void *res;     // optional residual NHWC T, (B, Hout, Wout, res_cs)
+    int res_cs;
+    void *out;           // NHWC (B, Hout, Wout, out_cs), channels [out_off, out_off + cout)
+    int out_cs, out_off, cout;
+    uint32_t in_bytes;
+    uint32_t mHW, mW; int sHW, sW;   // fdiv by Hout * Wout and by Wout
+};
+
+struct DlDwArgs {
+    const void *in;      // (B, Hin, Win, C) T
+    int B, Hin, Win, C;
+    int Hout, Wout, M, stride, dil, pad_t, pad_l;
+    const float *w;      // [9][C]
+    const float *bias;   // [C]
+    void *out;           // (B, Hout, Wout, C) T
+    uint32_t mHW, mW; int sHW, sW;
+};
+
+struct DlPoolArgs {
+    const void *x;       // (B, H, W, CS) T: the ASPP input
+    int B, H, W, C, CS;
+    int chunk_px, nchunks;
+    float *part;         // (B, nchunks, C) scratch
+    int cmid, cout;
+    const float *wp, *bp;    // image-pooling 1x1: [cmid][C], [cmid]
+    const float *wq, *bq;    // its columns of the concat projection: [cout][cmid], projection bias [cout]
+    float *z;            // (B, z_stride) per-image projection bias
+    int z_stride;
+};
+
+struct DlArgmaxArgs {
+    const float *logits; // (B, h, w, LCS) f32
+    int B, h, w, LCS, ncls;
+    float sy, sx;        // (h - 1) / (Hc - 1), (w - 1) / (Wc - 1) in f32
+    int Ho, Wo;          // output rows / cols (the un-padded image)
+    int Hout, Wout;      // output tensor dims (== Ho, Wo)
+    int64_t *out;        // (B, Hout, Wout)
+};
+
+hipError_t dl_launch_prep(int prec, const DlPrepArgs &a, hipStream_t s);
+hipError_t dl_launch_conv(int prec, bool out_f32, const DlConvArgs &a, hipStream_t s);
+hipError_t dl_launch_dw(int prec, const DlDwArgs &a, hipStream_t s);
+hipError_t dl_launch_pool(int prec, const DlPoolArgs &a, hipStream_t s);
+hipError_t dl_launch_argmax(const DlArgmaxArgs &a, hipStream_t s);
+
+}  // namespace bugseg

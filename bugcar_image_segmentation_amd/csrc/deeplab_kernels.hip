@@ -1,0 +1,308 @@
+// DeepLabV3 (MobileNetV2 backbone + ASPP) kernels for gfx950 — SURVEY.md §8(f) row 3, config 4.
+//
+// The reference runs the frozen DeepLab export through TF sess.run (models.py:115-125:
+// ImageTensor u8 -> SemanticPredictions int64). The graph is the standard TF DeepLab export
+// (deeplab/export_model.py): pad to the crop size with the mean pixel, (2/255)x - 1, MobileNetV2
+// (inverted residuals: 1x1 expand + ReLU6, 3x3 depthwise (strided / atrous) + ReLU6, linear 1x1
+// projection, residual), ASPP (image pooling, 1x1, optional atrous 3x3 branches), concat
+// projection, 1x1 logits, bilinear resize (align_corners) to the crop, argmax.
+//
+// Kernels (NHWC activations, channel stride a multiple of 8, T = float | __bf16):
+//   dl_prep_kernel        u8 RGB -> padded, normalised (B, Hc, Wc, 8) engine input
+//   dl_conv_kernel        implicit-GEMM dense conv (1x1, 3x3 strided / atrous) on MFMA 16x16x32 bf16
+//                         (or 8x 16x16x4 f32): rows = output channels, columns = pixels, k = (tap, ci);
+//                         epilogue bias (+ per-image bias) + ReLU / ReLU6 + residual, written at a
+//                         channel offset of the destination (ASPP concat without a copy)
+//   dl_dw_kernel          depthwise 3x3 (stride, dilation, SAME pad) + bias + ReLU6, 8 channels/thread
+//   dl_gap_kernel         image-pooling partial sums (deterministic: fixed chunking, no atomics)
+//   dl_pool_kernel        image-pooling branch: mean -> 1x1 + ReLU -> its share of the concat
+//                         projection, folded into a per-image bias of the projection conv (the
+//                         branch is a broadcast 1x1 image, so it never has to exist at 65x65)
+//   dl_resize_argmax_kernel  logits (h, w) -> bilinear (align_corners, TF's legacy lerp order) at the
+//                         crop resolution -> argmax (lowest index on ties) -> int64 class map
+#include "bugseg_internal.h"
+#include "deeplab_internal.h"
+#include "mfma_common.h"
+
+namespace bugseg {
+
+// ------------------------------------------------------------------ preprocess
+// TF: pad_to_bounding_box(x - 127.5) + 127.5 (exact for integer x), then (2/255) * x - 1 in f32.
+template <typename T>
+__global__ void __launch_bounds__(256) dl_prep_kernel(const DlPrepArgs a) {
+#pragma clang fp contract(off)
+    const int i = blockIdx.x * 256 + threadIdx.x;
+    const int n = a.B * a.Hc * a.Wc;
+    if (i >= n) return;
+    const int x = i % a.Wc, t = i / a.Wc, y = t % a.Hc, b = t / a.Hc;
+    const float scale = 2.0f / 255.0f;   // f32(2/255), as TF's constant
+    float v[3];
+    if (y < a.H && x < a.W) {
+        const uint8_t *p = a.rgb + ((size_t)(b * a.H + y) * a.W + x) * 3;
+        for (int c = 0; c < 3; ++c) v[c] = scale * (float)p[c] - 1.0f;
+    } else {
+        for (int c = 0; c < 3; ++c) v[c] = scale * 127.5f - 1.0f;
+    }
+    T *o = reinterpret_cast<T *>(a.out) + (size_t)i * 8;
+    typename Tr<T>::Raw r;
+    set3(r, v[0], v[1], v[2]);
+    if constexpr (sizeof(T) == 2) *reinterpret_cast<uint4 *>(o) = r.v;
+    else {
+        reinterpret_cast<float4 *>(o)[0] = r.a;
+        reinterpret_cast<float4 *>(o)[1] = r.b;
+    }
+}
+
+// ------------------------------------------------------------------ dense conv (implicit GEMM)
+// Workgroup = 4 waves = 128 pixels x 64 output channels; a wave owns 32 pixels (2 B fragments)
+// x 64 channels (4 A fragments): 8 MFMAs per k-step of 32 (one tap, 32 input channels).
+// A fragment (weights, packed [NP][taps][cinP], k contiguous): lane row = col, k = 8*kq .. +7.
+// B fragment (pixels): lane column = col, channels 8*kq .. +7 of that pixel at that tap; taps
+// outside the image and channels past the input's stride read 0 through the buffer descriptor.
+template <typename T, bool OUTF32>
+__global__ void __launch_bounds__(256) dl_conv_kernel(const DlConvArgs a) {
+    using Raw = typename Tr<T>::Raw;
+    const int lane = threadIdx.x & 63, col = lane & 15, kq = lane >> 4;
+    const int wave = threadIdx.x >> 6;
+    const int n0 = blockIdx.y * 64;
+    const __amdgpu_buffer_rsrc_t rin = mkbuf(a.in, a.in_bytes);
+    const int esz = (int)sizeof(T);
+
+    int pb[2], piy[2], pix[2];
+    bool pv[2];
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+        const int p = blockIdx.x * 128 + wave * 32 + j * 16 + col;
+        pv[j] = p < a.M;
+        const int pp = pv[j] ? p : 0;
+        const int b = (int)fdiv((uint32_t)pp, a.mHW, a.sHW);
+        const int r = pp - b * a.Hout * a.Wout;
+        const int oy = (int)fdiv((uint32_t)r, a.mW, a.sW);
+        const int ox = r - oy * a.Wout;
+        pb[j] = b;
+        piy[j] = oy * a.stride - a.pad_t;
+        pix[j] = ox * a.stride - a.pad_l;
+    }
+    f32x4 acc[2][4];
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) acc[j][r] = (f32x4){0.f, 0.f, 0.f, 0.f};
+
+    const int K = a.taps * a.cinP;
+    const T *wrow[4];
+#pragma unroll
+    for (int r = 0; r < 4; ++r) wrow[r] = reinterpret_cast<const T *>(a.w) + (size_t)(n0 + r * 16 + col) * K + kq * 8;
+    const int chunks = a.cinP >> 5;
+
+    for (int t = 0; t < a.taps; ++t) {
+        const int ky = t / a.kw, kx = t - (t / a.kw) * a.kw;
+        uint32_t base[2];
+#pragma unroll
+        for (int j = 0; j < 2; ++j) {
+            const int iy = piy[j] + ky * a.dil, ix = pix[j] + kx * a.dil;
+            const bool ok = pv[j] && (unsigned)iy < (unsigned)a.Hin && (unsigned)ix < (unsigned)a.Win;
+            base[j] = ok ? (uint32_t)(((pb[j] * a.Hin + iy) * a.Win + ix) * a.CS) : OOB;
+        }
+        for (int ch = 0; ch < chunks; ++ch) {
+            const int c = ch * 32 + kq * 8;
+            Raw bx[2], wa[4];
+#pragma unroll
+            for (int j = 0; j < 2; ++j) {
+                const uint32_t off = (base[j] != OOB && c < a.CS) ? (base[j] + c) * esz : OOB;
+                bld8(bx[j], rin, off);
+            }
+#pragma unroll
+            for (int r = 0; r < 4; ++r) ld8(wa[r], wrow[r] + t * a.cinP + ch * 32);
+#pragma unroll
+            for (int j = 0; j < 2; ++j)
+#pragma unroll
+                for (int r = 0; r < 4; ++r) mma(acc[j][r], wa[r], bx[j]);
+        }
+    }
+
+    // epilogue: lane holds channels n0 + 16r + 4kq .. +3 of pixel column `col` of fragment j
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+        if (!pv[j]) continue;
+        const int p = blockIdx.x * 128 + wave * 32 + j * 16 + col;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+            const int n = n0 + r * 16 + kq * 4;
+            if (n >= a.cout) continue;
+            float4 v = add4(f4(acc[j][r]), ld4f(a.bias + n));
+            if (a.bias_img) v = add4(v, ld4f(a.bias_img + (size_t)pb[j] * a.bias_img_stride + n));
+            if (a.act >= 1) v = make_float4(fmaxf(v.x, 0.f), fmaxf(v.y, 0.f), fmaxf(v.z, 0.f), fmaxf(v.w, 0.f));
+            if (a.act == 2) v = make_float4(fminf(v.x, 6.f), fminf(v.y, 6.f), fminf(v.z, 6.f), fminf(v.w, 6.f));
+            if (a.res) v = add4(v, ld4(reinterpret_cast<const T *>(a.res) + (size_t)p * a.res_cs + n));
+            if constexpr (OUTF32) st4(reinterpret_cast<float *>(a.out) + (size_t)p * a.out_cs + a.out_off + n, v);
+            else st4(reinterpret_cast<T *>(a.out) + (size_t)p * a.out_cs + a.out_off + n, v);
+        }
+    }
+}
+
+// ------------------------------------------------------------------ depthwise 3x3
+// One thread = one output pixel x 8 channels; weights [9][C] f32 (already rounded to T's precision
+// on the host), bias [C]. Sum in tap order (ky, kx), then bias, ReLU6.
+template <typename T>
+__global__ void __launch_bounds__(256) dl_dw_kernel(const DlDwArgs a) {
+    const int i = blockIdx.x * 256 + threadIdx.x;
+    const int groups = a.C >> 3;
+    if (i >= a.M * groups) return;
+    const int g = i % groups, p = i / groups;
+    const int b = (int)fdiv((uint32_t)p, a.mHW, a.sHW);
+    const int r = p - b * a.Hout * a.Wout;
+    const int oy = (int)fdiv((uint32_t)r, a.mW, a.sW);
+    const int ox = r - oy * a.Wout;
+    const int iy0 = oy * a.stride - a.pad_t, ix0 = ox * a.stride - a.pad_l;
+    const T *in = reinterpret_cast<const T *>(a.in);
+    float acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int ky = 0; ky < 3; ++ky) {
+        const int iy = iy0 + ky * a.dil;
+        if ((unsigned)iy >= (unsigned)a.Hin) continue;
+#pragma unroll
+        for (int kx = 0; kx < 3; ++kx) {
+            const int ix = ix0 + kx * a.dil;
+            if ((unsigned)ix >= (unsigned)a.Win) continue;
+            const T *px = in + ((size_t)(b * a.Hin + iy) * a.Win + ix) * a.C + g * 8;
+            const float4 x0 = ld4(px), x1 = ld4(px + 4);
+            const float *w = a.w + (ky * 3 + kx) * a.C + g * 8;
+            const float4 w0 = ld4f(w), w1 = ld4f(w + 4);
+            acc[0] = fmaf(x0.x, w0.x, acc[0]); acc[1] = fmaf(x0.y, w0.y, acc[1]);
+            acc[2] = fmaf(x0.z, w0.z, acc[2]); acc[3] = fmaf(x0.w, w0.w, acc[3]);
+            acc[4] = fmaf(x1.x, w1.x, acc[4]); acc[5] = fmaf(x1.y, w1.y, acc[5]);
+            acc[6] = fmaf(x1.z, w1.z, acc[6]); acc[7] = fmaf(x1.w, w1.w, acc[7]);
+        }
+    }
+    const float4 b0 = ld4f(a.bias + g * 8), b1 = ld4f(a.bias + g * 8 + 4);
+    auto r6 = [](float v) { return fminf(fmaxf(v, 0.f), 6.f); };
+    const float4 v0 = make_float4(r6(acc[0] + b0.x), r6(acc[1] + b0.y), r6(acc[2] + b0.z), r6(acc[3] + b0.w));
+    const float4 v1 = make_float4(r6(acc[4] + b1.x), r6(acc[5] + b1.y), r6(acc[6] + b1.z), r6(acc[7] + b1.w));
+    T *o = reinterpret_cast<T *>(a.out) + (size_t)p * a.C + g * 8;
+    st4(o, v0);
+    st4(o + 4, v1);
+}
+
+// ------------------------------------------------------------------ image pooling
+// Partial channel sums over a fixed pixel chunk per workgroup: part[b][chunk][c] (f32).
+template <typename T>
+__global__ void __launch_bounds__(256) dl_gap_kernel(const DlPoolArgs a) {
+    const int b = blockIdx.y, chunk = blockIdx.x;
+    const int HW = a.H * a.W;
+    const int p0 = chunk * a.chunk_px, p1 = min(HW, p0 + a.chunk_px);
+    const T *x = reinterpret_cast<const T *>(a.x) + (size_t)b * HW * a.CS;
+    for (int c = threadIdx.x; c < a.C; c += 256) {
+        float s = 0.f;
+        for (int p = p0; p < p1; ++p) s += ld1(x + (size_t)p * a.CS + c);
+        a.part[((size_t)b * a.nchunks + chunk) * a.C + c] = s;
+    }
+}
+
+// One workgroup per image: mean (partials summed in chunk order) -> y = relu(Wp . mean + bp),
+// rounded to T as the stored branch output would be -> z = Wq . y + bq (f32) = the per-image bias
+// of the concat projection. Wp [cmid][C], Wq [cout][cmid] in f32 (rounded to T's precision).
+template <typename T>
+__global__ void __launch_bounds__(256) dl_pool_kernel(const DlPoolArgs a) {
+    __shared__ float mean[1024];
+    __shared__ float y[1024];
+    const int b = blockIdx.x;
+    const float inv = 1.0f / (float)(a.H * a.W);
+    for (int c = threadIdx.x; c < a.C; c += 256) {
+        float s = 0.f;
+        for (int k = 0; k < a.nchunks; ++k) s += a.part[((size_t)b * a.nchunks + k) * a.C + c];
+        mean[c] = (float)(T)(s * inv);
+    }
+    __syncthreads();
+    for (int m = threadIdx.x; m < a.cmid; m += 256) {
+        float s = 0.f;
+        const float *w = a.wp + (size_t)m * a.C;
+        for (int c = 0; c < a.C; ++c) s = fmaf(w[c], mean[c], s);
+        s = fmaxf(s + a.bp[m], 0.f);
+        y[m] = (float)(T)s;
+    }
+    __syncthreads();
+    for (int n = threadIdx.x; n < a.cout; n += 256) {
+        float s = 0.f;
+        const float *w = a.wq + (size_t)n * a.cmid;
+        for (int m = 0; m < a.cmid; ++m) s = fmaf(w[m], y[m], s);
+        a.z[(size_t)b * a.z_stride + n] = s + a.bq[n];
+    }
+}
+
+// ------------------------------------------------------------------ logits -> class map
+// TF resize_bilinear (align_corners = True, legacy scaler): in = out * ((in_size - 1) / (out_size - 1))
+// in f32; top = floor(in), bottom = min(top + 1, in_size - 1), lerp = in - top;
+// value = top_row + (bottom_row - top_row) * y_lerp with row = left + (right - left) * x_lerp.
+// Then argmax over classes (first maximum).
+__global__ void __launch_bounds__(256) dl_resize_argmax_kernel(const DlArgmaxArgs a) {
+#pragma clang fp contract(off)
+    const int i = blockIdx.x * 256 + threadIdx.x;
+    if (i >= a.B * a.Ho * a.Wo) return;
+    const int x = i % a.Wo, t = i / a.Wo, y = t % a.Ho, b = t / a.Ho;
+    const float in_y = (float)y * a.sy, in_x = (float)x * a.sx;
+    const int y0 = (int)floorf(in_y), x0 = (int)floorf(in_x);
+    const int y1 = min(y0 + 1, a.h - 1), x1 = min(x0 + 1, a.w - 1);
+    const float ly = in_y - (float)y0, lx = in_x - (float)x0;
+    const float *base = a.logits + (size_t)b * a.h * a.w * a.LCS;
+    const float *tl = base + ((size_t)y0 * a.w + x0) * a.LCS, *tr = base + ((size_t)y0 * a.w + x1) * a.LCS;
+    const float *bl = base + ((size_t)y1 * a.w + x0) * a.LCS, *br = base + ((size_t)y1 * a.w + x1) * a.LCS;
+    float best = 0.f;
+    int bi = 0;
+    for (int c = 0; c < a.ncls; ++c) {
+        const float top = tl[c] + (tr[c] - tl[c]) * lx;
+        const float bot = bl[c] + (br[c] - bl[c]) * lx;
+        const float v = top + (bot - top) * ly;
+        if (c == 0 || v > best) { best = v; bi = c; }
+    }
+    a.out[((size_t)b * a.Hout + y) * a.Wout + x] = (int64_t)bi;
+}
+
+// ------------------------------------------------------------------ launchers
+hipError_t dl_launch_prep(int prec, const DlPrepArgs &a, hipStream_t s) {
+    const int n = a.B * a.Hc * a.Wc;
+    const dim3 g((n + 255) / 256);
+    if (prec == PREC_BF16) hipLaunchKernelGGL(dl_prep_kernel<__bf16>, g, dim3(256), 0, s, a);
+    else hipLaunchKernelGGL(dl_prep_kernel<float>, g, dim3(256), 0, s, a);
+    return hipGetLastError();
+}
+
+hipError_t dl_launch_conv(int prec, bool out_f32, const DlConvArgs &a, hipStream_t s) {
+    const dim3 g((a.M + 127) / 128, a.NP / 64);
+    if (prec == PREC_BF16) {
+        if (out_f32) hipLaunchKernelGGL((dl_conv_kernel<__bf16, true>), g, dim3(256), 0, s, a);
+        else hipLaunchKernelGGL((dl_conv_kernel<__bf16, false>), g, dim3(256), 0, s, a);
+    } else {
+        if (out_f32) hipLaunchKernelGGL((dl_conv_kernel<float, true>), g, dim3(256), 0, s, a);
+        else hipLaunchKernelGGL((dl_conv_kernel<float, false>), g, dim3(256), 0, s, a);
+    }
+    return hipGetLastError();
+}
+
+hipError_t dl_launch_dw(int prec, const DlDwArgs &a, hipStream_t s) {
+    const int n = a.M * (a.C >> 3);
+    const dim3 g((n + 255) / 256);
+    if (prec == PREC_BF16) hipLaunchKernelGGL(dl_dw_kernel<__bf16>, g, dim3(256), 0, s, a);
+    else hipLaunchKernelGGL(dl_dw_kernel<float>, g, dim3(256), 0, s, a);
+    return hipGetLastError();
+}
+
+hipError_t dl_launch_pool(int prec, const DlPoolArgs &a, hipStream_t s) {
+    const dim3 g1(a.nchunks, a.B);
+    if (prec == PREC_BF16) {
+        hipLaunchKernelGGL(dl_gap_kernel<__bf16>, g1, dim3(256), 0, s, a);
+        hipLaunchKernelGGL(dl_pool_kernel<__bf16>, dim3(a.B), dim3(256), 0, s, a);
+    } else {
+        hipLaunchKernelGGL(dl_gap_kernel<float>, g1, dim3(256), 0, s, a);
+        hipLaunchKernelGGL(dl_pool_kernel<float>, dim3(a.B), dim3(256), 0, s, a);
+    }
+    return hipGetLastError();
+}
+
+hipError_t dl_launch_argmax(const DlArgmaxArgs &a, hipStream_t s) {
+    const int n = a.B * a.Ho * a.Wo;
+    hipLaunchKernelGGL(dl_resize_argmax_kernel, dim3((n + 255) / 256), dim3(256), 0, s, a);
+    return hipGetLastError();
+}
+
+}  // namespace bugseg

@@ -1,0 +1,392 @@
+"""DeepLabV3 graph builder: topology, synthetic weights, batch-norm folding, weight packing and
+lowering to the executor's op list (libbugseg.so, bugseg_dl_*). SURVEY.md §8(f) row 3 / config 4.
+
+What the reference runs (models.py:98-136) is a frozen TF DeepLab export fed through
+``import/ImageTensor:0`` (u8 RGB, batch of images) and read from ``import/SemanticPredictions:0``
+(int64 class ids). ``deeplab.pb`` is absent (.MISSING_LARGE_BLOBS:1), so the network here is the
+standard export that name denotes — deeplab/export_model.py over the MobileNetV2 feature extractor
+of the TF DeepLab model zoo (``mobilenet_v2``, depth multiplier 1, output stride 8, crop 513):
+
+* preprocessing: pad to the crop with the mean pixel 127.5, then ``(2/255) x - 1``;
+* MobileNetV2 ``V2_DEF`` (slim): 3x3 s2 conv 32 + ReLU6, then inverted residuals
+  (t, c, n, s) = (1,16,1,1) (6,24,2,2) (6,32,3,2) (6,64,4,2) (6,96,3,1) (6,160,3,2) (6,320,1,1):
+  1x1 expand + ReLU6 (absent for t = 1), 3x3 depthwise + ReLU6, linear 1x1 projection, residual when
+  stride 1 and channels match; once the output stride is reached, strides become atrous rates the
+  way slim's ``mobilenet_base`` does it (layer stride 1, layer rate = running rate, rate *= stride);
+  every convolution SAME-padded, batch norm (eps 1e-3) after each;
+* ASPP (deeplab/model.py ``extract_features``): image pooling (global mean, 1x1 256 + BN + ReLU,
+  broadcast back), 1x1 256 + BN + ReLU, optional atrous 3x3 branches (``atrous_rates``: none for the
+  MobileNetV2 zoo models; 6/12/18 at output stride 16 for the ResNet / Xception ones, here dense
+  convs), concat [pool, 1x1, atrous...], 1x1 projection 256 + BN + ReLU (dropout: identity);
+* logits: 1x1 conv with bias; bilinear resize (align_corners=True) to the crop; argmax.
+
+Parity is UNPINNED against TF on the real deeplab.pb (neither exists here); the oracle is
+``oracle/deeplab_oracle.py`` on the same synthetic weights.
+
+Op list (``lower``): int32 records of ``OP_FIELDS`` fields, interpreted by deeplab_runtime.cpp:
+  PREP   [1, dst]
+  CONV   [2, src, dst, res, Hin, Win, CS, Hout, Wout, kh, kw, stride, dil, pad_t, pad_l, cinP, NP,
+          w_off, b_off, act, res_cs, out_cs, out_off, cout, out_f32, bias_img_buf, bias_img_stride]
+  DW     [3, src, dst, Hin, Win, C, Hout, Wout, stride, dil, pad_t, pad_l, w_off, b_off]
+  POOL   [4, src, part, z, H, W, C, CS, chunk_px, nchunks, cmid, cout, wp_off, bp_off, wq_off, bq_off, z_stride]
+  ARGMAX [5, logits, h, w, LCS, ncls]
+"""
+from __future__ import annotations
+
+from dataclasses import dataclass, field
+
+import numpy as np
+import torch
+
+OP_FIELDS = 32
+OP_PREP, OP_CONV, OP_DW, OP_POOL, OP_ARGMAX = 1, 2, 3, 4, 5
+ACT_NONE, ACT_RELU, ACT_RELU6 = 0, 1, 2
+BN_EPS = 1e-3
+CROP = 513
+NUM_CLASSES = 21
+ASPP_DEPTH = 256
+# slim mobilenet_v2 V2_DEF: (expansion t, output channels c, repeats n, first stride s)
+MNV2_BLOCKS = [(1, 16, 1, 1), (6, 24, 2, 2), (6, 32, 3, 2), (6, 64, 4, 2), (6, 96, 3, 1), (6, 160, 3, 2), (6, 320, 1, 1)]
+
+
+@dataclass
+class Conv:
+    """One convolution + (optional) inference batch norm + activation. w: (cout, cin/groups, kh, kw)."""
+    w: np.ndarray
+    b: np.ndarray | None = None        # conv bias (logits only)
+    gamma: np.ndarray | None = None    # batch norm (None: no BN)
+    beta: np.ndarray | None = None
+    mean: np.ndarray | None = None
+    var: np.ndarray | None = None
+    eps: float = BN_EPS
+    act: int = ACT_NONE
+    stride: int = 1
+    dil: int = 1
+    depthwise: bool = False
+
+    @property
+    def cout(self):
+        return self.w.shape[0]
+
+    @property
+    def k(self):
+        return self.w.shape[2]
+
+    def folded(self):
+        """(w, b) with the batch norm folded in, float64."""
+        w = self.w.astype(np.float64)
+        b = np.zeros(self.cout) if self.b is None else self.b.astype(np.float64)
+        if self.gamma is not None:
+            s = self.gamma.astype(np.float64) / np.sqrt(self.var.astype(np.float64) + self.eps)
+            w = w * s.reshape(-1, 1, 1, 1)
+            b = (b - self.mean) * s + self.beta
+        return w, b
+
+
+@dataclass
+class Block:
+    """MobileNetV2 inverted residual (slim expanded_conv)."""
+    expand: Conv | None
+    dw: Conv
+    project: Conv
+    residual: bool
+
+
+@dataclass
+class DeepLab:
+    stem: Conv
+    blocks: list
+    pool: Conv                   # image pooling 1x1
+    aspp0: Conv
+    atrous: list                 # 3x3 dense atrous branches
+    project: Conv                # concat projection over [pool, aspp0, atrous...]
+    logits: Conv
+    num_classes: int = NUM_CLASSES
+    output_stride: int = 8
+    crop: int = CROP
+    meta: dict = field(default_factory=dict)
+
+
+def same_pad(n_in: int, k: int, s: int, d: int):
+    """TF 'SAME': out = ceil(in / s), pad_total = max((out - 1) s + (k - 1) d + 1 - in, 0),
+    pad_before = pad_total // 2."""
+    out = -(-n_in // s)
+    tot = max((out - 1) * s + (k - 1) * d + 1 - n_in, 0)
+    return out, tot // 2
+
+
+class _Init:
+    def __init__(self, seed: int):
+        self.r = np.random.default_rng(seed)
+
+    def conv(self, cout, cin, k, act, *, stride=1, dil=1, depthwise=False, bn=True, gamma=(0.5, 1.5), bias=False):
+        r = self.r
+        fan_in = (1 if depthwise else cin) * k * k
+        w = (r.standard_normal((cout, 1 if depthwise else cin, k, k)) * np.sqrt(2.0 / fan_in)).astype(np.float32)
+        c = Conv(w=w, act=act, stride=stride, dil=dil, depthwise=depthwise)
+        if bn:
+            c.gamma = r.uniform(*gamma, cout).astype(np.float32)
+            c.beta = (r.standard_normal(cout) * 0.1).astype(np.float32)
+            c.mean = (r.standard_normal(cout) * 0.1).astype(np.float32)
+            c.var = r.uniform(0.5, 1.5, cout).astype(np.float32)
+        if bias:
+            c.b = (r.standard_normal(cout) * 0.1).astype(np.float32)
+        return c
+
+
+def build_deeplab(seed: int = 4321, num_classes: int = NUM_CLASSES, output_stride: int = 8,
+                  atrous_rates=(), crop: int = CROP, width: float = 1.0) -> DeepLab:
+    """Synthetic-weight DeepLabV3-MobileNetV2 (He-normal convs, BN gamma~U(0.5,1.5), beta~N(0,0.1),
+    mean~N(0,0.1), var~U(0.5,1.5); the linear projections of residual blocks draw gamma from
+    U(0.1,0.3) so the residual stream stays O(1) without trained statistics). `width` scales the
+    channel counts (tests use small widths; multiples of 8 are kept)."""
+    ini = _Init(seed)
+    ch = lambda c: max(8, int(round(c * width / 8)) * 8)  # noqa: E731
+    stem = ini.conv(ch(32), 3, 3, ACT_RELU6, stride=2)
+    blocks = []
+    cin = ch(32)
+    cur_stride, rate = 2, 1
+    for t, c, n, s in MNV2_BLOCKS:
+        cout = ch(c) if c != 16 else ch(16)
+        for i in range(n):
+            st = s if i == 0 else 1
+            if output_stride is not None and cur_stride == output_stride:
+                lstride, lrate = 1, rate
+                rate *= st
+            else:
+                lstride, lrate = st, 1
+                cur_stride *= st
+            inner = cin * t
+            expand = ini.conv(inner, cin, 1, ACT_RELU6) if t != 1 else None
+            dw = ini.conv(inner, inner, 3, ACT_RELU6, stride=lstride, dil=lrate, depthwise=True)
+            res = lstride == 1 and cin == cout
+            proj = ini.conv(cout, inner, 1, ACT_NONE, gamma=(0.1, 0.3) if res else (0.5, 1.5))
+            blocks.append(Block(expand, dw, proj, res))
+            cin = cout
+    D = ASPP_DEPTH if width >= 1.0 else ch(ASPP_DEPTH)
+    pool = ini.conv(D, cin, 1, ACT_RELU)
+    aspp0 = ini.conv(D, cin, 1, ACT_RELU)
+    atrous = [ini.conv(D, cin, 3, ACT_RELU, dil=int(r)) for r in atrous_rates]
+    project = ini.conv(D, D * (2 + len(atrous)), 1, ACT_RELU)
+    logits = ini.conv(num_classes, D, 1, ACT_NONE, bn=False, bias=True)
+    logits.w = (ini.r.standard_normal(logits.w.shape) * np.sqrt(1.0 / D)).astype(np.float32)
+    return DeepLab(stem, blocks, pool, aspp0, atrous, project, logits, num_classes, output_stride, crop,
+                   meta=dict(seed=seed, atrous_rates=tuple(int(r) for r in atrous_rates), width=width))
+
+
+def feature_size(net: DeepLab, n: int) -> int:
+    """Spatial size of the backbone output for an n-pixel crop side."""
+    n, _ = same_pad(n, 3, 2, 1)
+    for b in net.blocks:
+        n, _ = same_pad(n, 3, b.dw.stride, b.dw.dil)
+    return n
+
+
+def _r8(c):
+    return (c + 7) // 8 * 8
+
+
+def _r(c, m):
+    return (c + m - 1) // m * m
+
+
+def _round(a: np.ndarray, bf16: bool) -> np.ndarray:
+    """f64/f32 -> f32 holding values representable in the compute type."""
+    t = torch.from_numpy(np.ascontiguousarray(a, dtype=np.float32))
+    if bf16:
+        t = t.to(torch.bfloat16).to(torch.float32)
+    return t.numpy()
+
+
+class _Blob:
+    def __init__(self, bf16: bool):
+        self.bf16 = bf16
+        self.parts: list[bytes] = []
+        self.size = 0
+
+    def add(self, a: np.ndarray, as_compute_type: bool) -> int:
+        off = self.size
+        t = torch.from_numpy(np.ascontiguousarray(a, dtype=np.float32))
+        if as_compute_type and self.bf16:
+            raw = t.to(torch.bfloat16).view(torch.int16).numpy().tobytes()
+        else:
+            raw = t.numpy().tobytes()
+        pad = (-len(raw)) % 256
+        self.parts.append(raw + b"\0" * pad)
+        self.size += len(raw) + pad
+        return off
+
+    def bytes(self) -> bytes:
+        return b"".join(self.parts)
+
+
+def pack_conv(c: Conv, cinS: int, bf16: bool):
+    """-> (packed [NP][taps][cinP] f32 array (values rounded to the compute type), bias [NP], cinP, NP).
+    Input channel c of tap (ky, kx) sits at k = (ky * kw + kx) * cinP + c."""
+    w, b = c.folded()
+    cout, cin, kh, kw = w.shape
+    cinP, NP = _r(max(cinS, cin), 32), _r(cout, 64)
+    p = np.zeros((NP, kh * kw, cinP), np.float64)
+    p[:cout, :, :cin] = w.transpose(0, 2, 3, 1).reshape(cout, kh * kw, cin)
+    bb = np.zeros(NP, np.float64)
+    bb[:cout] = b
+    return _round(p, bf16), bb.astype(np.float32), cinP, NP
+
+
+def lower(net: DeepLab, B: int, bf16: bool):
+    """-> (weight blob bytes, ops int32 (nops, OP_FIELDS), buffer bytes uint64 (nbufs,), info dict).
+    Buffers: 0 input, 1/2 block ping-pong, 3 expanded, 4 depthwise out, 5 ASPP concat, 6 projection,
+    7 logits (f32), 8 pooling partials (f32), 9 per-image projection bias (f32)."""
+    es = 2 if bf16 else 4
+    blob = _Blob(bf16)
+    ops = []
+    nb = 10
+    need = [0] * nb
+    info = dict(flops=0.0, bytes=0.0, per_op=[])
+
+    def use(buf, nbytes):
+        need[buf] = max(need[buf], int(nbytes))
+
+    def op(rec, tag, flops, nbytes):
+        r = list(rec) + [0] * (OP_FIELDS - len(rec))
+        ops.append(r)
+        info["per_op"].append((tag, float(flops), float(nbytes)))
+        info["flops"] += flops
+        info["bytes"] += nbytes
+
+    Hc = Wc = net.crop
+    use(0, B * Hc * Wc * 8 * es)
+    op([OP_PREP, 0], "prep", 0, B * Hc * Wc * (3 + 8 * es))
+
+    def conv(c: Conv, src, H, W, CS, dst, out_cs, out_off=0, res=-1, out_f32=False, bias_img=-1, bias_img_stride=0,
+             zero_bias=False, cout=None, tag="conv"):
+        k = c.k
+        Ho, pt = same_pad(H, k, c.stride, c.dil)
+        Wo, pl = same_pad(W, k, c.stride, c.dil)
+        wp, bias, cinP, NP = pack_conv(c, CS, bf16)
+        if zero_bias:
+            bias = np.zeros_like(bias)
+        w_off = blob.add(wp, True)
+        b_off = blob.add(bias, False)
+        cw = c.cout if cout is None else cout
+        oes = 4 if out_f32 else es
+        use(dst, B * Ho * Wo * out_cs * oes)
+        cin = c.w.shape[1]
+        flops = 2.0 * B * Ho * Wo * c.cout * cin * k * k
+        nbytes = B * H * W * CS * es + B * Ho * Wo * cw * oes + (B * Ho * Wo * cw * es if res >= 0 else 0) + wp.size * es
+        op([OP_CONV, src, dst, res, H, W, CS, Ho, Wo, k, k, c.stride, c.dil, pt, pl, cinP, NP, w_off, b_off, c.act,
+            out_cs if res >= 0 else 0, out_cs, out_off, cw, int(out_f32), bias_img, bias_img_stride], tag, flops, nbytes)
+        return Ho, Wo
+
+    # stem
+    H, W = conv(net.stem, 0, Hc, Wc, 8, 1, _r8(net.stem.cout), tag="conv stem")
+    C = net.stem.cout
+    cur = 1
+    for bi, blk in enumerate(net.blocks):
+        nxt = 2 if cur == 1 else 1
+        x_in, Cin = cur, C
+        if blk.expand is not None:
+            conv(blk.expand, x_in, H, W, Cin, 3, blk.expand.cout, tag="conv expand")
+            src, Cm = 3, blk.expand.cout
+        else:
+            src, Cm = x_in, Cin
+        d = blk.dw
+        Ho, pt = same_pad(H, 3, d.stride, d.dil)
+        Wo, pl = same_pad(W, 3, d.stride, d.dil)
+        wd, bd = d.folded()
+        w_off = blob.add(_round(wd.reshape(Cm, 9).T, bf16), False)
+        b_off = blob.add(bd.astype(np.float32), False)
+        use(4, B * Ho * Wo * Cm * es)
+        op([OP_DW, src, 4, H, W, Cm, Ho, Wo, d.stride, d.dil, pt, pl, w_off, b_off], "dw",
+           2.0 * B * Ho * Wo * Cm * 9, B * (H * W + Ho * Wo) * Cm * es)
+        H, W = Ho, Wo
+        Cout = blk.project.cout
+        conv(blk.project, 4, H, W, Cm, nxt, Cout, res=x_in if blk.residual else -1, tag="conv project")
+        cur, C = nxt, Cout
+
+    # ASPP
+    D = net.aspp0.cout
+    nbr = 1 + len(net.atrous)
+    cat_cs = D * nbr
+    h, w = H, W
+    chunk = 64
+    nch = -(-(h * w) // chunk)
+    use(8, B * nch * C * 4)
+    zs = _r(D, 64)
+    use(9, B * zs * 4)
+    wpool, bpool = net.pool.folded()
+    wproj, bproj = net.project.folded()
+    wp_off = blob.add(_round(wpool.reshape(D, C), bf16), False)
+    bp_off = blob.add(bpool.astype(np.float32), False)
+    wq_off = blob.add(_round(wproj.reshape(D, -1)[:, :D], bf16), False)
+    bq_off = blob.add(bproj.astype(np.float32), False)
+    op([OP_POOL, cur, 8, 9, h, w, C, C, chunk, nch, D, D, wp_off, bp_off, wq_off, bq_off, zs], "pool",
+       2.0 * B * (D * C + D * D) + B * h * w * C, B * h * w * C * es)
+    conv(net.aspp0, cur, h, w, C, 5, cat_cs, out_off=0, tag="conv aspp")
+    for i, a in enumerate(net.atrous):
+        conv(a, cur, h, w, C, 5, cat_cs, out_off=D * (i + 1), tag="conv atrous")
+    # the projection over the concat minus its pooled part (that part arrives as the per-image bias)
+    pj = Conv(w=net.project.w[:, D:], gamma=net.project.gamma, beta=net.project.beta, mean=net.project.mean,
+              var=net.project.var, eps=net.project.eps, act=net.project.act)
+    conv(pj, 5, h, w, cat_cs, 6, D, bias_img=9, bias_img_stride=zs, zero_bias=True, tag="conv project")
+    LCS = _r(net.num_classes, 4)
+    conv(net.logits, 6, h, w, D, 7, LCS, out_f32=True, cout=LCS, tag="conv logits")
+    op([OP_ARGMAX, 7, h, w, LCS, net.num_classes], "argmax", 0, B * (h * w * LCS * 4 + Hc * Wc * 8))
+    info.update(feature=(h, w), lcs=LCS, nops=len(ops))
+    return blob.bytes(), np.asarray(ops, np.int32), np.asarray(need, np.uint64), info
+
+
+# ---------------------------------------------------------------- weight file (.npz, no pickle)
+_CONV_FIELDS = ("w", "b", "gamma", "beta", "mean", "var")
+
+
+def _convs(net: DeepLab):
+    yield "stem", net.stem
+    for i, b in enumerate(net.blocks):
+        if b.expand is not None:
+            yield f"b{i}.expand", b.expand
+        yield f"b{i}.dw", b.dw
+        yield f"b{i}.project", b.project
+    yield "pool", net.pool
+    yield "aspp0", net.aspp0
+    for i, a in enumerate(net.atrous):
+        yield f"atrous{i}", a
+    yield "project", net.project
+    yield "logits", net.logits
+
+
+def save(net: DeepLab, path) -> None:
+    """Weights + topology attributes as a plain .npz (loadable with allow_pickle=False)."""
+    arrs = {}
+    for name, c in _convs(net):
+        for f in _CONV_FIELDS:
+            v = getattr(c, f)
+            if v is not None:
+                arrs[f"{name}.{f}"] = np.asarray(v, np.float32)
+        arrs[f"{name}.attrs"] = np.array([c.act, c.stride, c.dil, int(c.depthwise)], np.int32)
+        arrs[f"{name}.eps"] = np.array([c.eps], np.float64)
+    arrs["net.residual"] = np.array([int(b.residual) for b in net.blocks], np.int32)
+    arrs["net.expand"] = np.array([int(b.expand is not None) for b in net.blocks], np.int32)
+    arrs["net.attrs"] = np.array([net.num_classes, net.output_stride or 0, net.crop, len(net.atrous)], np.int32)
+    np.savez(path, **arrs)
+
+
+def load(path) -> DeepLab:
+    z = np.load(path, allow_pickle=False)
+
+    def conv(name):
+        if f"{name}.w" not in z:
+            raise KeyError(f"{path}: missing {name}.w")
+        act, stride, dil, dw = (int(v) for v in z[f"{name}.attrs"])
+        c = Conv(w=z[f"{name}.w"], act=act, stride=stride, dil=dil, depthwise=bool(dw), eps=float(z[f"{name}.eps"][0]))
+        for f in _CONV_FIELDS[1:]:
+            if f"{name}.{f}" in z:
+                setattr(c, f, z[f"{name}.{f}"])
+        return c
+
+    ncls, os_, crop, natr = (int(v) for v in z["net.attrs"])
+    blocks = []
+    for i, (res, ex) in enumerate(zip(z["net.residual"], z["net.expand"])):
+        blocks.append(Block(conv(f"b{i}.expand") if ex else None, conv(f"b{i}.dw"), conv(f"b{i}.project"), bool(res)))
+    return DeepLab(conv("stem"), blocks, conv("pool"), conv("aspp0"), [conv(f"atrous{i}") for i in range(natr)],
+                   conv("project"), conv("logits"), ncls, os_ or None, crop)

@@ -169,19 +169,107 @@ class ENET(InferenceModel):
 
 
 class DeepLabV3(InferenceModel):
-    """models.py:98-136. Not built this round: `deeplab.pb` is absent (.MISSING_LARGE_BLOBS:1), its
-    backbone is unknown and the reference wrapper is broken as written (SURVEY.md §2 #7, §8(f) 3)."""
+    """models.py:98-136 on the MI355X engine (BASELINE config 4).
+
+    The reference feeds ``[img]`` to ``import/ImageTensor:0`` and returns
+    ``import/SemanticPredictions:0`` (models.py:115-125): u8 RGB images in, int64 class ids out,
+    with padding to the 513 crop, normalisation, MobileNetV2 + ASPP, logits, bilinear resize and
+    argmax all inside the frozen graph. Here the same graph (deeplab_spec.py) runs as one op list of
+    gfx950 kernels (libbugseg.so, bugseg_dl_*).
+
+    Deviations, because the reference wrapper is broken as written:
+    ``predict`` takes the ImageTensor layout itself — (H, W, 3) or (B, H, W, 3) u8 RGB, H, W <= 513 —
+    instead of unpacking a 4-D NCHW shape and wrapping it in a list (models.py:116,124);
+    ``preprocess`` (whose reference body uses undefined ``cls.input_size`` / ``IMAGE_MEAN``,
+    models.py:129,132) returns the RGB u8 frame resized so the longer side is at most the crop — the
+    resize the DeepLab demo applies before feeding the graph. The node-name printing
+    (models.py:112-113, 116, 121) is dropped.
+
+    Weights: ``deeplab.pb`` is absent (.MISSING_LARGE_BLOBS:1) and a TF GraphDef of DeepLab is not
+    imported (the GraphDef importer covers ENet); GRAPH_PB_PATH may be a ``deeplab_spec.save`` .npz,
+    or None for the seeded synthetic network (``deeplab_spec.build_deeplab``)."""
     INPUT_TENSOR_NAME = "import/ImageTensor:0"
     OUTPUT_TENSOR_NAME = "import/SemanticPredictions:0"
     INPUT_SIZE = 1024
     FROZEN_GRAPH_NAME = "deeplab.pb"
+    CROP_SIZE = 513
 
-    def __init__(self, GRAPH_PB_PATH):
-        raise NotImplementedError("DeepLabV3 (ASPP) path is SURVEY.md §8(f) row 3: not built yet")
+    def __init__(self, GRAPH_PB_PATH=None, *, net=None, precision: str = "bf16", device: int | None = None):
+        from . import deeplab_spec
+        if precision not in ("fp32", "bf16"):
+            raise ValueError("precision must be 'fp32' or 'bf16'")
+        if net is None:
+            if GRAPH_PB_PATH is None:
+                net = deeplab_spec.build_deeplab()
+            else:
+                if not os.path.exists(GRAPH_PB_PATH):
+                    raise FileNotFoundError(f"{GRAPH_PB_PATH}: no such file")
+                with open(GRAPH_PB_PATH, "rb") as f:
+                    magic = f.read(4)
+                if magic[:2] != b"PK":
+                    raise NotImplementedError(f"{GRAPH_PB_PATH}: only deeplab_spec .npz weight files are supported "
+                                              "(TF GraphDef import covers ENet only)")
+                net = deeplab_spec.load(GRAPH_PB_PATH)
+        self.net = net
+        self.precision = precision
+        self.ctx = N.DeepLabContext(device, N.BF16 if precision == "bf16" else N.FP32)
+        self._spec = deeplab_spec
+        self._blob = None
+        self._plan_B = None
+        self.plan_info = None
 
-    def predict(self, img):
-        raise NotImplementedError
+    def _ensure_plan(self, B: int) -> None:
+        if self._plan_B == B:
+            return
+        blob, ops, bufs, info = self._spec.lower(self.net, B, self.precision == "bf16")
+        if self._blob is None:
+            self.ctx.load_weights(blob)
+            self._blob = blob
+        self.ctx.set_plan(ops, bufs, B, self.net.crop, self.net.crop)
+        self._plan_B = B
+        self.plan_info = info
+
+    def predict_device(self, rgb, out: torch.Tensor | None = None) -> torch.Tensor:
+        """(B, H, W, 3) u8 RGB (device or host) -> (B, H, W) int64 device tensor."""
+        x = _as_device_tensor(rgb, torch.uint8)
+        if x.dim() == 3:
+            x = x.unsqueeze(0)
+        if x.dim() != 4 or x.shape[3] != 3:
+            raise ValueError(f"expected u8 RGB images (B, H, W, 3), got {tuple(x.shape)}")
+        B, H, W = x.shape[:3]
+        if H > self.net.crop or W > self.net.crop:
+            raise ValueError(f"image {H}x{W} exceeds the {self.net.crop} crop: resize it first (DeepLabV3.preprocess)")
+        self._ensure_plan(B)
+        if out is None:
+            out = torch.empty((B, H, W), dtype=torch.int64, device=x.device)
+        self.ctx.forward(x, B, H, W, out)
+        return out
+
+    def logits_device(self) -> torch.Tensor:
+        """The last forward's logits (B, h, w, classes padded to 4) f32 at the backbone resolution."""
+        h, w = self.plan_info["feature"]
+        t = torch.empty((self._plan_B, h, w, self.plan_info["lcs"]), dtype=torch.float32,
+                        device=torch.device("cuda", self.ctx.device))
+        self.ctx.read_buffer(7, t)
+        return t
+
+    def predict(self, img) -> np.ndarray:
+        """models.py:115-125: SemanticPredictions, (B, H, W) int64."""
+        return self.predict_device(img).cpu().numpy()
 
     @classmethod
-    def preprocess(cls, bgr_frame):
-        raise NotImplementedError
+    def preprocess(cls, bgr_frame) -> np.ndarray:
+        """BGR u8 frame -> RGB u8 frame whose longer side is at most CROP_SIZE (nearest-pixel
+        downscale when larger; the reference body is broken, see the class docstring)."""
+        f = np.asarray(bgr_frame)
+        if f.ndim != 3 or f.shape[2] != 3 or f.dtype != np.uint8:
+            raise ValueError("expected a BGR uint8 frame (H, W, 3)")
+        rgb = f[:, :, ::-1]
+        H, W = rgb.shape[:2]
+        r = cls.CROP_SIZE / max(H, W)
+        if r < 1.0:
+            h, w = max(1, int(r * H)), max(1, int(r * W))
+            ys = np.minimum((np.arange(h) * (H / h)).astype(np.int64), H - 1)
+            xs = np.minimum((np.arange(w) * (W / w)).astype(np.int64), W - 1)
+            rgb = rgb[ys][:, xs]
+        return np.ascontiguousarray(rgb)

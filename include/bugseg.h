@@ -159,6 +159,35 @@ int bugseg_plan_launch_op(bugseg_ctx *ctx, int B, int H, int W, int op, void *st
 /* Last error message of ctx (or of the calling thread when ctx is NULL). Never NULL. */
 const char *bugseg_last_error(const bugseg_ctx *ctx);
 
+/* ---- DeepLabV3 (BASELINE config 4) -------------------------------------
+ * Replaces DeepLabV3 (models.py:98-136): tf.compat.v1.Session + GraphDef import (models.py:105-113)
+ * and sess.run("ImageTensor:0" u8 -> "SemanticPredictions:0" int64) (models.py:115-125).
+ * The graph builder is host code (deeplab_spec.py): it folds batch-norm, packs the weights into
+ * one blob (bugseg_dl_load_weights) and lowers the network to a flat op list over numbered
+ * activation buffers for one batch size and crop (bugseg_dl_set_plan). Op records are
+ * BUGSEG_DL_OP_FIELDS int32 each; kinds and field meanings are documented in deeplab_spec.py
+ * (lower()) and validated here against the buffers and the blob before the plan is accepted. */
+#define BUGSEG_DL_OP_FIELDS 32
+typedef struct bugseg_dl bugseg_dl;
+
+int bugseg_dl_create(int device, int precision, bugseg_dl **out);
+int bugseg_dl_destroy(bugseg_dl *dl);
+/* weight blob in HOST memory (bf16 / f32 per the precision, as packed by deeplab_spec.pack) */
+int bugseg_dl_load_weights(bugseg_dl *dl, const void *blob, size_t bytes);
+/* ops: nops * BUGSEG_DL_OP_FIELDS int32; buf_bytes[nbufs]: arena layout; B frames of at most
+ * Hc x Wc (the crop size: 513 for the standard export) */
+int bugseg_dl_set_plan(bugseg_dl *dl, const int32_t *ops, int nops, const uint64_t *buf_bytes, int nbufs,
+                       int B, int Hc, int Wc);
+/* rgb_dev: (B, H, W, 3) u8 RGB, H <= Hc, W <= Wc (padded with the mean pixel to the crop, as the
+ * export's preprocessing does); out_dev: (B, H, W) int64 class ids. */
+int bugseg_dl_forward(bugseg_dl *dl, const uint8_t *rgb_dev, int B, int H, int W, int64_t *out_dev, void *stream);
+/* Profiling hook: enqueue op `op` of the plan alone, on the last forward's I/O buffers. */
+int bugseg_dl_launch_op(bugseg_dl *dl, int op, void *stream);
+/* Test hook: copy `bytes` of activation buffer `buf` (deeplab_spec.lower's numbering; 7 = the f32
+ * logits at the backbone resolution) to a device pointer, on `stream`. */
+int bugseg_dl_read_buffer(bugseg_dl *dl, int buf, void *dst_dev, size_t bytes, void *stream);
+const char *bugseg_dl_last_error(const bugseg_dl *dl);
+
 #ifdef __cplusplus
 }
 #endif

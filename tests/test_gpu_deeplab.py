@@ -1,0 +1,93 @@
+"""GPU parity of the DeepLabV3 path (BASELINE config 4) through the C ABI
+(bugseg_dl_*) against the CPU oracle (oracle/deeplab_oracle.py) on the same synthetic weights.
+
+Tolerances: fp32 mode — logits within 1e-3 absolute of the oracle (fp64 at reduced width, fp32 at
+full size), class maps exact wherever the oracle's top-2 margin of the upsampled logits exceeds 2e-3;
+the resize + argmax stage is checked bit-exactly against the oracle's TF-formula restatement applied
+to the GPU's own logits. bf16 mode — against the oracle's bf16-storage emulation: mean |dlogit|
+< 2e-2, class agreement > 98%.
+"""
+import numpy as np
+import pytest
+import torch
+
+from bugcar_image_segmentation_amd import deeplab_spec as S
+from bugcar_image_segmentation_amd.models import DeepLabV3
+from oracle import deeplab_oracle as O
+
+pytestmark = pytest.mark.gpu
+
+LOGIT_TOL = 1e-3
+MARGIN = 2e-3
+
+
+def _frames(B, H, W, seed):
+    return np.random.default_rng(seed).integers(0, 256, (B, H, W, 3), dtype=np.uint8)
+
+
+def _gpu_logits(model):
+    L = model.logits_device().cpu().numpy()[..., :model.net.num_classes]   # (B, h, w, C)
+    return L.transpose(0, 3, 1, 2)
+
+
+def _check_fp32(model, net, x, ref_dtype):
+    got_cls = model.predict(x)
+    got = _gpu_logits(model)
+    ref = O.forward(net, x, dtype=ref_dtype).numpy()
+    assert got.shape == ref.shape
+    assert np.abs(got - ref).max() < LOGIT_TOL, np.abs(got - ref).max()
+    # resize + argmax kernel: bit-exact on the GPU's own logits
+    assert np.array_equal(got_cls, O.predict(net, x, logits=got))
+    # class maps vs the oracle wherever its margin decides them
+    up = O.resize_bilinear_tf(ref, net.crop, net.crop)[:, :, :x.shape[1], :x.shape[2]]
+    s = np.sort(up, axis=1)
+    decided = (s[:, -1] - s[:, -2]) > MARGIN
+    ref_cls = O.predict(net, x, logits=ref)
+    assert got_cls.dtype == np.int64 and got_cls.shape == x.shape[:3]
+    assert np.array_equal(got_cls[decided], ref_cls[decided])
+    assert decided.mean() > 0.98
+
+
+@pytest.mark.parametrize("B,H,W,os_,rates", [(2, 90, 97, 8, ()), (1, 97, 97, 16, (6, 12, 18)), (3, 64, 40, 8, ())])
+def test_deeplab_fp32_small(gpu, B, H, W, os_, rates):
+    net = S.build_deeplab(width=0.25, crop=97, output_stride=os_, atrous_rates=rates)
+    model = DeepLabV3(net=net, precision="fp32")
+    _check_fp32(model, net, _frames(B, H, W, B * 7 + H), torch.float64)
+
+
+def test_deeplab_fp32_full_513(gpu):
+    net = S.build_deeplab()
+    model = DeepLabV3(net=net, precision="fp32")
+    _check_fp32(model, net, _frames(1, 513, 513, 3), torch.float32)
+
+
+def test_deeplab_bf16_vs_storage_emulation(gpu):
+    net = S.build_deeplab(width=0.5, crop=129)
+    model = DeepLabV3(net=net, precision="bf16")
+    x = _frames(2, 129, 120, 11)
+    got_cls = model.predict(x)
+    got = _gpu_logits(model)
+    ref = O.forward(net, x, bf16_storage=True).numpy()
+    assert np.abs(got - ref).mean() < 2e-2
+    assert (got_cls == O.predict(net, x, logits=ref)).mean() > 0.98
+    assert np.array_equal(got_cls, O.predict(net, x, logits=got))
+
+
+def test_deeplab_bf16_full_batch_properties(gpu):
+    """Config 4 shape in the throughput mode: batch independence and run-to-run determinism."""
+    model = DeepLabV3(precision="bf16")
+    x = _frames(4, 513, 513, 5)
+    a = model.predict_device(x).clone()
+    b = model.predict_device(x)
+    assert torch.equal(a, b)
+    one = DeepLabV3(net=model.net, precision="bf16").predict(x[2:3])
+    assert np.array_equal(a[2:3].cpu().numpy(), one)
+    assert a.min() >= 0 and a.max() < model.net.num_classes
+
+
+def test_deeplab_errors(gpu):
+    model = DeepLabV3(net=S.build_deeplab(width=0.25, crop=65), precision="fp32")
+    with pytest.raises(ValueError):
+        model.predict(_frames(1, 66, 40, 0))
+    with pytest.raises(ValueError):
+        model.predict(np.zeros((1, 10, 10, 4), np.uint8))
