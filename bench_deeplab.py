@@ -1,0 +1,167 @@
+"""Benchmark of BASELINE config 4: DeepLabV3 (MobileNetV2, output stride 8, ASPP) at 513x513 on MI355X.
+
+One "step" = the DeepLab plugin's forward (models.DeepLabV3.predict_device: pad + normalise,
+backbone, ASPP, logits, bilinear resize to 513x513, argmax -> int64) over one batch of synthetic
+513x513 RGB frames already resident in HBM. bench.py stays the headline (ENet -> BEV occupancy
+grid); this prints ONE JSON line of the same shape for config 4. With WORLD_SIZE > 1 (torchrun)
+frames shard across ranks with no collective (weak scaling).
+
+`roofline` describes the dominant kernel tag (largest total time per forward), timed per launch
+with HIP events on the stream the kernels run on (bugseg_dl_launch_op): achieved = the launch's
+algorithmic bytes (input read once, output written once, residual read, weights once;
+deeplab_spec.lower) / its average duration, against 8 TB/s; `forward` adds whole-forward bytes,
+flops and the MFMA fraction. The CPU baseline is the oracle (PyTorch-CPU fp32, TF semantics) on a
+bounded sample.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+from collections import defaultdict
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+import torch.distributed as dist  # noqa: E402
+
+HBM_PEAK_GBS = 8000.0
+MFMA_PEAK_TFLOPS = {"bf16": 2500.0, "fp32": 157.3}
+
+
+def parse():
+    p = argparse.ArgumentParser(description=__doc__)
+    p.add_argument("--gpus", type=int, default=1)
+    p.add_argument("--steps", type=int, default=20)
+    p.add_argument("--warmup", type=int, default=5)
+    p.add_argument("--batch", type=int, default=16, help="frames per GPU")
+    p.add_argument("--precision", default="bf16", choices=["bf16", "fp32"])
+    p.add_argument("--cpu-baseline-seconds", type=float, default=12.0)
+    p.add_argument("--no-cpu-baseline", action="store_true")
+    return p.parse_args()
+
+
+def cpu_baseline(net, budget_s):
+    from oracle import deeplab_oracle as O
+    threads = min(16, len(os.sched_getaffinity(0)))
+    torch.set_num_threads(threads)
+    x = np.random.default_rng(7).integers(0, 256, (1, net.crop, net.crop, 3), dtype=np.uint8)
+    O.predict(net, x, dtype=torch.float32)   # warm-up
+    n, t0 = 0, time.perf_counter()
+    while True:
+        O.predict(net, x, dtype=torch.float32)
+        n += 1
+        el = time.perf_counter() - t0
+        if el >= budget_s and n >= 2:
+            break
+    return {"value": round(n / el, 3), "unit": "frames/s", "cores": threads, "kind": "port",
+            "sample": f"{n} frames of the same workload ({net.crop}x{net.crop}, fp32 PyTorch-CPU oracle with TF "
+                      f"semantics), {el:.1f} s, one frame per call"}
+
+
+def main():
+    a = parse()
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+    from bugcar_image_segmentation_amd.models import DeepLabV3
+
+    model = DeepLabV3(precision=a.precision)
+    net, B, C = model.net, a.batch, model.net.crop
+    frames = torch.from_numpy(np.random.default_rng(rank).integers(0, 256, (B, C, C, 3), dtype=np.uint8)).to(dev)
+    out = torch.empty((B, C, C), dtype=torch.int64, device=dev)
+
+    for _ in range(a.warmup):
+        model.predict_device(frames, out=out)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(a.steps):
+        model.predict_device(frames, out=out)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    el = time.perf_counter() - t0
+    if world > 1:
+        t = torch.tensor([el], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        el = float(t.item())
+
+    # per-launch HIP-event timing of the plan the timed region ran (untimed region)
+    stream = torch.cuda.current_stream()
+    info = model.plan_info
+    reps = max(3, min(10, a.steps))
+    per = defaultdict(lambda: {"launches": 0, "us": 0.0, "bytes": 0.0, "flops": 0.0})
+    evs = [torch.cuda.Event(enable_timing=True) for _ in range(2)]
+    fwd_us = 0.0
+    per_op = []
+    for i, (tag, flops, nbytes) in enumerate(info["per_op"]):
+        model.ctx.launch_op(i, stream)
+        evs[0].record(stream)
+        for _ in range(reps):
+            model.ctx.launch_op(i, stream)
+        evs[1].record(stream)
+        evs[1].synchronize()
+        us = evs[0].elapsed_time(evs[1]) * 1e3 / reps
+        fwd_us += us
+        per_op.append([tag, round(us, 2), round(nbytes / (us * 1e-6) / 1e9, 1)])
+        d = per[tag]
+        d["launches"] += 1
+        d["us"] += us
+        d["bytes"] += nbytes
+        d["flops"] += flops
+
+    if rank == 0:
+        value = B * world * a.steps / el
+        tag, k = max(per.items(), key=lambda kv: kv[1]["us"])
+        achieved = k["bytes"] / (k["us"] * 1e-6) / 1e9
+        peak_tf = MFMA_PEAK_TFLOPS[a.precision]
+        res = {
+            "metric": "frames/sec DeepLabV3 513x513 -> SemanticPredictions (synthetic), whole job",
+            "value": round(value, 2), "unit": "frames/s", "n_gpus": world, "steps": a.steps, "warmup": a.warmup,
+            "ms_per_step": round(el / a.steps * 1e3, 4), "higher_is_better": True, "scaling": "weak",
+            "vs_baseline": None, "dtype": a.precision,
+            "data": "synthetic (uniform u8 RGB frames, seed=rank; random-init DeepLabV3-MobileNetV2 weights seed 4321)",
+            "config": {"workload": f"config4: DeepLabV3 MobileNetV2 OS8 + ASPP (image pooling + 1x1), {C}x{C}, "
+                                   f"batch {B} per GPU, pad/normalise + forward + bilinear resize + argmax int64",
+                       "global_batch": B * world, "per_gpu_batch": B, "crop": C,
+                       "parallelism": f"frame-sharded dp{world}"},
+            "roofline": {
+                "bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": None,
+                "kernel": f"{tag}: dominant kernel tag ({k['launches']} launches, {k['us']:.0f} us of {fwd_us:.0f} us "
+                          f"per forward); {k['bytes'] / k['launches'] / 1e6:.1f} MB per launch (input once + output "
+                          f"once + residual + weights); {k['flops'] / (k['us'] * 1e-6) / 1e12:.1f} TFLOP/s "
+                          f"({k['flops'] / (k['us'] * 1e-6) / 1e12 / peak_tf:.3f} of the dense {a.precision} MFMA peak)",
+                "forward": {"launches": len(info["per_op"]), "us": round(fwd_us, 1), "frames": B,
+                            "bytes_per_frame": round(info["bytes"] / B), "flops_per_frame": round(info["flops"] / B),
+                            "achieved_gbs": round(info["bytes"] / (fwd_us * 1e-6) / 1e9, 1),
+                            "mfma_tflops": round(info["flops"] / (fwd_us * 1e-6) / 1e12, 2),
+                            "mfma_frac": round(info["flops"] / (fwd_us * 1e-6) / 1e12 / peak_tf, 4)},
+            },
+            "kernels": {t: {"launches": v["launches"], "us": round(v["us"], 1),
+                            "GBps": round(v["bytes"] / (v["us"] * 1e-6) / 1e9, 1),
+                            "TFLOPs": round(v["flops"] / (v["us"] * 1e-6) / 1e12, 2)}
+                        for t, v in sorted(per.items(), key=lambda kv: -kv[1]["us"])},
+            "per_op": per_op,
+        }
+        if not a.no_cpu_baseline:
+            res["cpu_baseline"] = cpu_baseline(net, a.cpu_baseline_seconds)
+        print(json.dumps(res), flush=True)
+    if world > 1:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

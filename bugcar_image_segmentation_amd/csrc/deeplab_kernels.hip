@@ -59,6 +59,7 @@ __global__ void __launch_bounds__(256) dl_prep_kernel(const DlPrepArgs a) {
 // A fragment (weights, packed [NP][taps][cinP], k contiguous): lane row = col, k = 8*kq .. +7.
 // B fragment (pixels): lane column = col, channels 8*kq .. +7 of that pixel at that tap; taps
 // outside the image and channels past the input's stride read 0 through the buffer descriptor.
+constexpr int DL_STG_RS = 68;   // staging row stride (floats): 64 channels + 4 (bank spread)
 template <typename T, bool OUTF32>
 __global__ void __launch_bounds__(256) dl_conv_kernel(const DlConvArgs a) {
     using Raw = typename Tr<T>::Raw;
@@ -121,67 +122,108 @@ __global__ void __launch_bounds__(256) dl_conv_kernel(const DlConvArgs a) {
         }
     }
 
-    // epilogue: lane holds channels n0 + 16r + 4kq .. +3 of pixel column `col` of fragment j
+    // epilogue: lane holds channels n0 + 16r + 4kq .. +3 of pixel column `col` of fragment j.
+    // bias (+ per-image bias) and the activation in registers, then the wave's 32 px x 64 ch tile goes
+    // through LDS (f32, so a residual add still rounds once) and comes back as 8 consecutive channels
+    // per lane: each store / residual load instruction covers 8 pixels' contiguous 128-B channel runs.
+    __shared__ __attribute__((aligned(16))) float stg[4][32 * DL_STG_RS];
+    float *st = stg[wave];
 #pragma unroll
     for (int j = 0; j < 2; ++j) {
-        if (!pv[j]) continue;
-        const int p = blockIdx.x * 128 + wave * 32 + j * 16 + col;
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
-            const int n = n0 + r * 16 + kq * 4;
-            if (n >= a.cout) continue;
+            const int nl = r * 16 + kq * 4, n = n0 + nl;
             float4 v = add4(f4(acc[j][r]), ld4f(a.bias + n));
             if (a.bias_img) v = add4(v, ld4f(a.bias_img + (size_t)pb[j] * a.bias_img_stride + n));
             if (a.act >= 1) v = make_float4(fmaxf(v.x, 0.f), fmaxf(v.y, 0.f), fmaxf(v.z, 0.f), fmaxf(v.w, 0.f));
             if (a.act == 2) v = make_float4(fminf(v.x, 6.f), fminf(v.y, 6.f), fminf(v.z, 6.f), fminf(v.w, 6.f));
-            if (a.res) v = add4(v, ld4(reinterpret_cast<const T *>(a.res) + (size_t)p * a.res_cs + n));
-            if constexpr (OUTF32) st4(reinterpret_cast<float *>(a.out) + (size_t)p * a.out_cs + a.out_off + n, v);
-            else st4(reinterpret_cast<T *>(a.out) + (size_t)p * a.out_cs + a.out_off + n, v);
+            *reinterpret_cast<float4 *>(st + (j * 16 + col) * DL_STG_RS + nl) = v;
+        }
+    }
+    wave_lds_sync();
+    const int c8 = (lane & 7) * 8;
+    const bool cok = n0 + c8 < a.cout;          // cout is a multiple of 8
+#pragma unroll
+    for (int it = 0; it < 4; ++it) {
+        const int pl = it * 8 + (lane >> 3);
+        const int p = blockIdx.x * 128 + wave * 32 + pl;
+        if (p >= a.M || !cok) continue;
+        float4 v0 = *reinterpret_cast<const float4 *>(st + pl * DL_STG_RS + c8);
+        float4 v1 = *reinterpret_cast<const float4 *>(st + pl * DL_STG_RS + c8 + 4);
+        const int n = n0 + c8;
+        if (a.res) {
+            const T *rp = reinterpret_cast<const T *>(a.res) + (size_t)p * a.res_cs + n;
+            v0 = add4(v0, ld4(rp));
+            v1 = add4(v1, ld4(rp + 4));
+        }
+        if constexpr (OUTF32) {
+            float *o = reinterpret_cast<float *>(a.out) + (size_t)p * a.out_cs + a.out_off + n;
+            st4(o, v0);
+            st4(o + 4, v1);
+        } else {
+            T *o = reinterpret_cast<T *>(a.out) + (size_t)p * a.out_cs + a.out_off + n;
+            st4(o, v0);
+            st4(o + 4, v1);
         }
     }
 }
 
 // ------------------------------------------------------------------ depthwise 3x3
-// One thread = one output pixel x 8 channels; weights [9][C] f32 (already rounded to T's precision
-// on the host), bias [C]. Sum in tap order (ky, kx), then bias, ReLU6.
+// One thread = DW_PX consecutive output pixels of one row x 8 channels, the 9 x 8 weights loaded once
+// into registers for all of them. Threads with consecutive ids take consecutive channel groups of the
+// same pixels (coalesced 16-B loads). DW_PX = 4 measured slower than 1 (1.36 vs 1.09 ms per
+// 16-frame forward): the kernel is latency-bound and wants the extra waves.
+// Weights [9][C] f32 (already rounded to T's precision on the host), bias [C]. Per pixel the taps are
+// summed in (ky, kx) order, then bias, ReLU6.
+constexpr int DW_PX = 1;
 template <typename T>
 __global__ void __launch_bounds__(256) dl_dw_kernel(const DlDwArgs a) {
     const int i = blockIdx.x * 256 + threadIdx.x;
     const int groups = a.C >> 3;
-    if (i >= a.M * groups) return;
-    const int g = i % groups, p = i / groups;
-    const int b = (int)fdiv((uint32_t)p, a.mHW, a.sHW);
-    const int r = p - b * a.Hout * a.Wout;
-    const int oy = (int)fdiv((uint32_t)r, a.mW, a.sW);
-    const int ox = r - oy * a.Wout;
-    const int iy0 = oy * a.stride - a.pad_t, ix0 = ox * a.stride - a.pad_l;
+    const int qx = (a.Wout + DW_PX - 1) / DW_PX;
+    if (i >= a.B * a.Hout * qx * groups) return;
+    const int g = i % groups, q = i / groups;
+    const int oxq = q % qx, t = q / qx;
+    const int oy = t % a.Hout, b = t / a.Hout;
+    const int iy0 = oy * a.stride - a.pad_t;
     const T *in = reinterpret_cast<const T *>(a.in);
-    float acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+    float4 w[9][2];
 #pragma unroll
-    for (int ky = 0; ky < 3; ++ky) {
-        const int iy = iy0 + ky * a.dil;
-        if ((unsigned)iy >= (unsigned)a.Hin) continue;
-#pragma unroll
-        for (int kx = 0; kx < 3; ++kx) {
-            const int ix = ix0 + kx * a.dil;
-            if ((unsigned)ix >= (unsigned)a.Win) continue;
-            const T *px = in + ((size_t)(b * a.Hin + iy) * a.Win + ix) * a.C + g * 8;
-            const float4 x0 = ld4(px), x1 = ld4(px + 4);
-            const float *w = a.w + (ky * 3 + kx) * a.C + g * 8;
-            const float4 w0 = ld4f(w), w1 = ld4f(w + 4);
-            acc[0] = fmaf(x0.x, w0.x, acc[0]); acc[1] = fmaf(x0.y, w0.y, acc[1]);
-            acc[2] = fmaf(x0.z, w0.z, acc[2]); acc[3] = fmaf(x0.w, w0.w, acc[3]);
-            acc[4] = fmaf(x1.x, w1.x, acc[4]); acc[5] = fmaf(x1.y, w1.y, acc[5]);
-            acc[6] = fmaf(x1.z, w1.z, acc[6]); acc[7] = fmaf(x1.w, w1.w, acc[7]);
-        }
+    for (int k = 0; k < 9; ++k) {
+        w[k][0] = ld4f(a.w + k * a.C + g * 8);
+        w[k][1] = ld4f(a.w + k * a.C + g * 8 + 4);
     }
     const float4 b0 = ld4f(a.bias + g * 8), b1 = ld4f(a.bias + g * 8 + 4);
     auto r6 = [](float v) { return fminf(fmaxf(v, 0.f), 6.f); };
-    const float4 v0 = make_float4(r6(acc[0] + b0.x), r6(acc[1] + b0.y), r6(acc[2] + b0.z), r6(acc[3] + b0.w));
-    const float4 v1 = make_float4(r6(acc[4] + b1.x), r6(acc[5] + b1.y), r6(acc[6] + b1.z), r6(acc[7] + b1.w));
-    T *o = reinterpret_cast<T *>(a.out) + (size_t)p * a.C + g * 8;
-    st4(o, v0);
-    st4(o + 4, v1);
+#pragma unroll
+    for (int j = 0; j < DW_PX; ++j) {
+        const int ox = oxq * DW_PX + j;
+        if (ox >= a.Wout) break;
+        const int ix0 = ox * a.stride - a.pad_l;
+        float acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int ky = 0; ky < 3; ++ky) {
+            const int iy = iy0 + ky * a.dil;
+            if ((unsigned)iy >= (unsigned)a.Hin) continue;
+#pragma unroll
+            for (int kx = 0; kx < 3; ++kx) {
+                const int ix = ix0 + kx * a.dil;
+                if ((unsigned)ix >= (unsigned)a.Win) continue;
+                const T *px = in + ((size_t)(b * a.Hin + iy) * a.Win + ix) * a.C + g * 8;
+                const float4 x0 = ld4(px), x1 = ld4(px + 4);
+                const float4 w0 = w[ky * 3 + kx][0], w1 = w[ky * 3 + kx][1];
+                acc[0] = fmaf(x0.x, w0.x, acc[0]); acc[1] = fmaf(x0.y, w0.y, acc[1]);
+                acc[2] = fmaf(x0.z, w0.z, acc[2]); acc[3] = fmaf(x0.w, w0.w, acc[3]);
+                acc[4] = fmaf(x1.x, w1.x, acc[4]); acc[5] = fmaf(x1.y, w1.y, acc[5]);
+                acc[6] = fmaf(x1.z, w1.z, acc[6]); acc[7] = fmaf(x1.w, w1.w, acc[7]);
+            }
+        }
+        const float4 v0 = make_float4(r6(acc[0] + b0.x), r6(acc[1] + b0.y), r6(acc[2] + b0.z), r6(acc[3] + b0.w));
+        const float4 v1 = make_float4(r6(acc[4] + b1.x), r6(acc[5] + b1.y), r6(acc[6] + b1.z), r6(acc[7] + b1.w));
+        T *o = reinterpret_cast<T *>(a.out) + ((size_t)(b * a.Hout + oy) * a.Wout + ox) * a.C + g * 8;
+        st4(o, v0);
+        st4(o + 4, v1);
+    }
 }
 
 // ------------------------------------------------------------------ image pooling
@@ -201,7 +243,8 @@ __global__ void __launch_bounds__(256) dl_gap_kernel(const DlPoolArgs a) {
 
 // One workgroup per image: mean (partials summed in chunk order) -> y = relu(Wp . mean + bp),
 // rounded to T as the stored branch output would be -> z = Wq . y + bq (f32) = the per-image bias
-// of the concat projection. Wp [cmid][C], Wq [cout][cmid] in f32 (rounded to T's precision).
+// of the concat projection. Wp [C][cmid], Wq [cmid][cout] in f32 (rounded to T's precision),
+// transposed so the threads of a workgroup (one output each) read consecutive addresses.
 template <typename T>
 __global__ void __launch_bounds__(256) dl_pool_kernel(const DlPoolArgs a) {
     __shared__ float mean[1024];
@@ -216,16 +259,14 @@ __global__ void __launch_bounds__(256) dl_pool_kernel(const DlPoolArgs a) {
     __syncthreads();
     for (int m = threadIdx.x; m < a.cmid; m += 256) {
         float s = 0.f;
-        const float *w = a.wp + (size_t)m * a.C;
-        for (int c = 0; c < a.C; ++c) s = fmaf(w[c], mean[c], s);
+        for (int c = 0; c < a.C; ++c) s = fmaf(a.wp[(size_t)c * a.cmid + m], mean[c], s);
         s = fmaxf(s + a.bp[m], 0.f);
         y[m] = (float)(T)s;
     }
     __syncthreads();
     for (int n = threadIdx.x; n < a.cout; n += 256) {
         float s = 0.f;
-        const float *w = a.wq + (size_t)n * a.cmid;
-        for (int m = 0; m < a.cmid; ++m) s = fmaf(w[m], y[m], s);
+        for (int m = 0; m < a.cmid; ++m) s = fmaf(a.wq[(size_t)m * a.cout + n], y[m], s);
         a.z[(size_t)b * a.z_stride + n] = s + a.bq[n];
     }
 }
@@ -249,11 +290,19 @@ __global__ void __launch_bounds__(256) dl_resize_argmax_kernel(const DlArgmaxArg
     const float *bl = base + ((size_t)y1 * a.w + x0) * a.LCS, *br = base + ((size_t)y1 * a.w + x1) * a.LCS;
     float best = 0.f;
     int bi = 0;
-    for (int c = 0; c < a.ncls; ++c) {
-        const float top = tl[c] + (tr[c] - tl[c]) * lx;
-        const float bot = bl[c] + (br[c] - bl[c]) * lx;
-        const float v = top + (bot - top) * ly;
-        if (c == 0 || v > best) { best = v; bi = c; }
+    // LCS is a multiple of 4 and every row 16-B aligned: 4 classes per corner load
+    for (int c0 = 0; c0 < a.ncls; c0 += 4) {
+        const float4 q[4] = {ld4f(tl + c0), ld4f(tr + c0), ld4f(bl + c0), ld4f(br + c0)};
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            const int c = c0 + j;
+            if (c >= a.ncls) break;
+            const float vtl = get(q[0], j), vtr = get(q[1], j), vbl = get(q[2], j), vbr = get(q[3], j);
+            const float top = vtl + (vtr - vtl) * lx;
+            const float bot = vbl + (vbr - vbl) * lx;
+            const float v = top + (bot - top) * ly;
+            if (c == 0 || v > best) { best = v; bi = c; }
+        }
     }
     a.out[((size_t)b * a.Hout + y) * a.Wout + x] = (int64_t)bi;
 }
@@ -280,7 +329,7 @@ hipError_t dl_launch_conv(int prec, bool out_f32, const DlConvArgs &a, hipStream
 }
 
 hipError_t dl_launch_dw(int prec, const DlDwArgs &a, hipStream_t s) {
-    const int n = a.M * (a.C >> 3);
+    const int n = a.B * a.Hout * ((a.Wout + DW_PX - 1) / DW_PX) * (a.C >> 3);
     const dim3 g((n + 255) / 256);
     if (prec == PREC_BF16) hipLaunchKernelGGL(dl_dw_kernel<__bf16>, g, dim3(256), 0, s, a);
     else hipLaunchKernelGGL(dl_dw_kernel<float>, g, dim3(256), 0, s, a);

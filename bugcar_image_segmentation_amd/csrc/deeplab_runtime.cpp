@@ -87,8 +87,8 @@ bool check_op(const bugseg_dl *c, const DlOp &o, std::string &why) {
         const int act = f[19], res_cs = f[20], out_cs = f[21], out_off = f[22], cout = f[23], out_f32 = f[24];
         const int bimg = f[25], bimg_stride = f[26];
         if (Hin < 1 || Win < 1 || Hout < 1 || Wout < 1 || kh < 1 || kw < 1 || stride < 1 || dil < 1 || CS < 8 ||
-            CS % 8 || cinP % 32 || cinP < 32 || NP % 64 || NP < 64 || act < 0 || act > 2 || cout < 4 || cout % 4 ||
-            cout > NP || out_off % 4 || out_off + cout > out_cs) { why = "conv: bad shape"; return false; }
+            CS % 8 || cinP % 32 || cinP < 32 || NP % 64 || NP < 64 || act < 0 || act > 2 || cout < 8 || cout % 8 ||
+            cout > NP || out_off % 8 || out_off + cout > out_cs) { why = "conv: bad shape"; return false; }
         if (!buf_ok(c, src, (double)B * Hin * Win * CS * es)) { why = "conv: source buffer too small"; return false; }
         if (!buf_ok(c, dst, (double)B * Hout * Wout * out_cs * (out_f32 ? 4.0 : es))) { why = "conv: destination too small"; return false; }
         if (res >= 0 && (res_cs < cout || !buf_ok(c, res, (double)B * Hout * Wout * res_cs * es))) { why = "conv: residual too small"; return false; }

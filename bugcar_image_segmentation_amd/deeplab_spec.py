@@ -316,9 +316,9 @@ def lower(net: DeepLab, B: int, bf16: bool):
     use(9, B * zs * 4)
     wpool, bpool = net.pool.folded()
     wproj, bproj = net.project.folded()
-    wp_off = blob.add(_round(wpool.reshape(D, C), bf16), False)
+    wp_off = blob.add(_round(wpool.reshape(D, C).T, bf16), False)           # [C][D]
     bp_off = blob.add(bpool.astype(np.float32), False)
-    wq_off = blob.add(_round(wproj.reshape(D, -1)[:, :D], bf16), False)
+    wq_off = blob.add(_round(wproj.reshape(D, -1)[:, :D].T, bf16), False)   # [D (pooled ch)][D (out)]
     bq_off = blob.add(bproj.astype(np.float32), False)
     op([OP_POOL, cur, 8, 9, h, w, C, C, chunk, nch, D, D, wp_off, bp_off, wq_off, bq_off, zs], "pool",
        2.0 * B * (D * C + D * D) + B * h * w * C, B * h * w * C * es)
@@ -329,7 +329,7 @@ def lower(net: DeepLab, B: int, bf16: bool):
     pj = Conv(w=net.project.w[:, D:], gamma=net.project.gamma, beta=net.project.beta, mean=net.project.mean,
               var=net.project.var, eps=net.project.eps, act=net.project.act)
     conv(pj, 5, h, w, cat_cs, 6, D, bias_img=9, bias_img_stride=zs, zero_bias=True, tag="conv project")
-    LCS = _r(net.num_classes, 4)
+    LCS = _r(net.num_classes, 8)
     conv(net.logits, 6, h, w, D, 7, LCS, out_f32=True, cout=LCS, tag="conv logits")
     op([OP_ARGMAX, 7, h, w, LCS, net.num_classes], "argmax", 0, B * (h * w * LCS * 4 + Hc * Wc * 8))
     info.update(feature=(h, w), lcs=LCS, nops=len(ops))
