@@ -31,6 +31,12 @@ struct DlConvArgs {
     int out_cs, out_off, cout;
     uint32_t in_bytes;
     uint32_t mHW, mW; int sHW, sW;   // fdiv by Hout * Wout and by Wout
+    // depthwise-fused projection (dw_w != nullptr): `in` is the depthwise conv's INPUT (B, Hin, Win, CS)
+    // and the 1x1 conv's B operand is computed on load: relu6(sum_taps in * dw_w + dw_b), rounded to T
+    const float *dw_w;   // [9][CS]
+    const float *dw_b;   // [CS]
+    int dw_stride, dw_dil, dw_pt, dw_pl;
+    int nb;              // pixel fragments per wave: 2 (128-px workgroup tile) or 4 (256 px)
 };
 
 struct DlDwArgs {

@@ -60,20 +60,50 @@ __global__ void __launch_bounds__(256) dl_prep_kernel(const DlPrepArgs a) {
 // B fragment (pixels): lane column = col, channels 8*kq .. +7 of that pixel at that tap; taps
 // outside the image and channels past the input's stride read 0 through the buffer descriptor.
 constexpr int DL_STG_RS = 68;   // staging row stride (floats): 64 channels + 4 (bank spread)
-template <typename T, bool OUTF32>
+
+// Depthwise 3x3 of 8 channels [c, c+8) at one pixel from its 9 tap offsets (OOB = padding), in the
+// dw kernel's exact order (taps (ky, kx), fmaf per channel, then bias, ReLU6), rounded to T.
+template <typename T>
+__device__ __forceinline__ void dw8(typename Tr<T>::Raw &out, __amdgpu_buffer_rsrc_t rin, const uint32_t (&tb)[9], int c,
+                                    const float *dw_w, const float *dw_b, int C) {
+    float acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int t = 0; t < 9; ++t) {
+        if (tb[t] == OOB) continue;
+        const uint32_t off = (tb[t] + c) * (uint32_t)sizeof(T);
+        const float4 x0 = bld4(rin, off, (const T *)nullptr), x1 = bld4(rin, off + 4 * sizeof(T), (const T *)nullptr);
+        const float4 w0 = ld4f(dw_w + t * C + c), w1 = ld4f(dw_w + t * C + c + 4);
+        acc[0] = fmaf(x0.x, w0.x, acc[0]); acc[1] = fmaf(x0.y, w0.y, acc[1]);
+        acc[2] = fmaf(x0.z, w0.z, acc[2]); acc[3] = fmaf(x0.w, w0.w, acc[3]);
+        acc[4] = fmaf(x1.x, w1.x, acc[4]); acc[5] = fmaf(x1.y, w1.y, acc[5]);
+        acc[6] = fmaf(x1.z, w1.z, acc[6]); acc[7] = fmaf(x1.w, w1.w, acc[7]);
+    }
+    const float4 b0 = ld4f(dw_b + c), b1 = ld4f(dw_b + c + 4);
+    auto r6 = [](float v) { return fminf(fmaxf(v, 0.f), 6.f); };
+    const T v[8] = {(T)r6(acc[0] + b0.x), (T)r6(acc[1] + b0.y), (T)r6(acc[2] + b0.z), (T)r6(acc[3] + b0.w),
+                    (T)r6(acc[4] + b1.x), (T)r6(acc[5] + b1.y), (T)r6(acc[6] + b1.z), (T)r6(acc[7] + b1.w)};
+    set8(out, v);
+}
+
+// Grid: 1-D, the N tiles of one pixel tile adjacent in launch order (they share the input tile).
+// NB = pixel fragments per wave (2: 128-px workgroup tiles, 4: 256-px tiles, twice the MFMAs per weight load).
+template <typename T, bool OUTF32, bool DWF, int NB>
 __global__ void __launch_bounds__(256) dl_conv_kernel(const DlConvArgs a) {
+    constexpr int WPX = NB * 16, TPX = 4 * WPX;   // pixels per wave / per workgroup
     using Raw = typename Tr<T>::Raw;
     const int lane = threadIdx.x & 63, col = lane & 15, kq = lane >> 4;
     const int wave = threadIdx.x >> 6;
-    const int n0 = blockIdx.y * 64;
+    const int ntn = a.NP >> 6;
+    const int n0 = (blockIdx.x % ntn) * 64;
+    const int mtile = blockIdx.x / ntn;
     const __amdgpu_buffer_rsrc_t rin = mkbuf(a.in, a.in_bytes);
     const int esz = (int)sizeof(T);
 
-    int pb[2], piy[2], pix[2];
-    bool pv[2];
+    int pb[NB], piy[NB], pix[NB];
+    bool pv[NB];
 #pragma unroll
-    for (int j = 0; j < 2; ++j) {
-        const int p = blockIdx.x * 128 + wave * 32 + j * 16 + col;
+    for (int j = 0; j < NB; ++j) {
+        const int p = mtile * TPX + wave * WPX + j * 16 + col;
         pv[j] = p < a.M;
         const int pp = pv[j] ? p : 0;
         const int b = (int)fdiv((uint32_t)pp, a.mHW, a.sHW);
@@ -84,9 +114,9 @@ __global__ void __launch_bounds__(256) dl_conv_kernel(const DlConvArgs a) {
         piy[j] = oy * a.stride - a.pad_t;
         pix[j] = ox * a.stride - a.pad_l;
     }
-    f32x4 acc[2][4];
+    f32x4 acc[NB][4];
 #pragma unroll
-    for (int j = 0; j < 2; ++j)
+    for (int j = 0; j < NB; ++j)
 #pragma unroll
         for (int r = 0; r < 4; ++r) acc[j][r] = (f32x4){0.f, 0.f, 0.f, 0.f};
 
@@ -96,29 +126,79 @@ __global__ void __launch_bounds__(256) dl_conv_kernel(const DlConvArgs a) {
     for (int r = 0; r < 4; ++r) wrow[r] = reinterpret_cast<const T *>(a.w) + (size_t)(n0 + r * 16 + col) * K + kq * 8;
     const int chunks = a.cinP >> 5;
 
-    for (int t = 0; t < a.taps; ++t) {
-        const int ky = t / a.kw, kx = t - (t / a.kw) * a.kw;
-        uint32_t base[2];
+    if constexpr (DWF) {
+        // 1x1 projection of the depthwise output computed on load; pixel (oy, ox) of the dw output grid
+        uint32_t tb[NB][9];
 #pragma unroll
-        for (int j = 0; j < 2; ++j) {
-            const int iy = piy[j] + ky * a.dil, ix = pix[j] + kx * a.dil;
-            const bool ok = pv[j] && (unsigned)iy < (unsigned)a.Hin && (unsigned)ix < (unsigned)a.Win;
-            base[j] = ok ? (uint32_t)(((pb[j] * a.Hin + iy) * a.Win + ix) * a.CS) : OOB;
+        for (int j = 0; j < NB; ++j) {
+            const int iy0 = piy[j] * a.dw_stride - a.dw_pt, ix0 = pix[j] * a.dw_stride - a.dw_pl;
+#pragma unroll
+            for (int t = 0; t < 9; ++t) {
+                const int iy = iy0 + (t / 3) * a.dw_dil, ix = ix0 + (t % 3) * a.dw_dil;
+                const bool ok = pv[j] && (unsigned)iy < (unsigned)a.Hin && (unsigned)ix < (unsigned)a.Win;
+                tb[j][t] = ok ? (uint32_t)(((pb[j] * a.Hin + iy) * a.Win + ix) * a.CS) : OOB;
+            }
         }
         for (int ch = 0; ch < chunks; ++ch) {
             const int c = ch * 32 + kq * 8;
-            Raw bx[2], wa[4];
+            Raw bx[NB], wa[4];
 #pragma unroll
-            for (int j = 0; j < 2; ++j) {
+            for (int j = 0; j < NB; ++j) {
+                if (c < a.CS) dw8<T>(bx[j], rin, tb[j], c, a.dw_w, a.dw_b, a.CS);
+                else zero(bx[j]);
+            }
+#pragma unroll
+            for (int r = 0; r < 4; ++r) ld8(wa[r], wrow[r] + ch * 32);
+#pragma unroll
+            for (int j = 0; j < NB; ++j)
+#pragma unroll
+                for (int r = 0; r < 4; ++r) mma(acc[j][r], wa[r], bx[j]);
+        }
+    } else {
+        // k-steps (tap, 32-channel chunk) flattened; the next step's fragments are in flight while
+        // the current step's MFMAs run
+        const int nks = a.taps * chunks;
+        auto bases = [&](int t, uint32_t (&base)[NB]) {
+            const int ky = t / a.kw, kx = t - (t / a.kw) * a.kw;
+#pragma unroll
+            for (int j = 0; j < NB; ++j) {
+                const int iy = piy[j] + ky * a.dil, ix = pix[j] + kx * a.dil;
+                const bool ok = pv[j] && (unsigned)iy < (unsigned)a.Hin && (unsigned)ix < (unsigned)a.Win;
+                base[j] = ok ? (uint32_t)(((pb[j] * a.Hin + iy) * a.Win + ix) * a.CS) : OOB;
+            }
+        };
+        auto load = [&](int t, int ch, const uint32_t (&base)[NB], Raw (&bx)[NB], Raw (&wa)[4]) {
+            const int c = ch * 32 + kq * 8;
+#pragma unroll
+            for (int j = 0; j < NB; ++j) {
                 const uint32_t off = (base[j] != OOB && c < a.CS) ? (base[j] + c) * esz : OOB;
                 bld8(bx[j], rin, off);
             }
 #pragma unroll
             for (int r = 0; r < 4; ++r) ld8(wa[r], wrow[r] + t * a.cinP + ch * 32);
+        };
+        uint32_t base[NB];
+        int t = 0, ch = 0;
+        bases(0, base);
+        Raw bx[NB], wa[4];
+        load(0, 0, base, bx, wa);
+        for (int ks = 0; ks < nks; ++ks) {
+            Raw bn[NB], wn[4];
+            if (ks + 1 < nks) {
+                if (++ch == chunks) {
+                    ch = 0;
+                    bases(++t, base);
+                }
+                load(t, ch, base, bn, wn);
+            }
 #pragma unroll
-            for (int j = 0; j < 2; ++j)
+            for (int j = 0; j < NB; ++j)
 #pragma unroll
                 for (int r = 0; r < 4; ++r) mma(acc[j][r], wa[r], bx[j]);
+#pragma unroll
+            for (int j = 0; j < NB; ++j) bx[j] = bn[j];
+#pragma unroll
+            for (int r = 0; r < 4; ++r) wa[r] = wn[r];
         }
     }
 
@@ -126,104 +206,111 @@ __global__ void __launch_bounds__(256) dl_conv_kernel(const DlConvArgs a) {
     // bias (+ per-image bias) and the activation in registers, then the wave's 32 px x 64 ch tile goes
     // through LDS (f32, so a residual add still rounds once) and comes back as 8 consecutive channels
     // per lane: each store / residual load instruction covers 8 pixels' contiguous 128-B channel runs.
+    // staged 32 pixels (two fragments) at a time: 34 KB of LDS per workgroup at any NB
     __shared__ __attribute__((aligned(16))) float stg[4][32 * DL_STG_RS];
     float *st = stg[wave];
-#pragma unroll
-    for (int j = 0; j < 2; ++j) {
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-            const int nl = r * 16 + kq * 4, n = n0 + nl;
-            float4 v = add4(f4(acc[j][r]), ld4f(a.bias + n));
-            if (a.bias_img) v = add4(v, ld4f(a.bias_img + (size_t)pb[j] * a.bias_img_stride + n));
-            if (a.act >= 1) v = make_float4(fmaxf(v.x, 0.f), fmaxf(v.y, 0.f), fmaxf(v.z, 0.f), fmaxf(v.w, 0.f));
-            if (a.act == 2) v = make_float4(fminf(v.x, 6.f), fminf(v.y, 6.f), fminf(v.z, 6.f), fminf(v.w, 6.f));
-            *reinterpret_cast<float4 *>(st + (j * 16 + col) * DL_STG_RS + nl) = v;
-        }
-    }
-    wave_lds_sync();
     const int c8 = (lane & 7) * 8;
     const bool cok = n0 + c8 < a.cout;          // cout is a multiple of 8
 #pragma unroll
-    for (int it = 0; it < 4; ++it) {
-        const int pl = it * 8 + (lane >> 3);
-        const int p = blockIdx.x * 128 + wave * 32 + pl;
-        if (p >= a.M || !cok) continue;
-        float4 v0 = *reinterpret_cast<const float4 *>(st + pl * DL_STG_RS + c8);
-        float4 v1 = *reinterpret_cast<const float4 *>(st + pl * DL_STG_RS + c8 + 4);
-        const int n = n0 + c8;
-        if (a.res) {
-            const T *rp = reinterpret_cast<const T *>(a.res) + (size_t)p * a.res_cs + n;
-            v0 = add4(v0, ld4(rp));
-            v1 = add4(v1, ld4(rp + 4));
+    for (int h = 0; h < NB / 2; ++h) {
+        if (h) wave_lds_sync();                 // the previous half's reads are done
+#pragma unroll
+        for (int jj = 0; jj < 2; ++jj) {
+            const int j = 2 * h + jj;
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                const int nl = r * 16 + kq * 4, n = n0 + nl;
+                float4 v = add4(f4(acc[j][r]), ld4f(a.bias + n));
+                if (a.bias_img) v = add4(v, ld4f(a.bias_img + (size_t)pb[j] * a.bias_img_stride + n));
+                if (a.act >= 1) v = make_float4(fmaxf(v.x, 0.f), fmaxf(v.y, 0.f), fmaxf(v.z, 0.f), fmaxf(v.w, 0.f));
+                if (a.act == 2) v = make_float4(fminf(v.x, 6.f), fminf(v.y, 6.f), fminf(v.z, 6.f), fminf(v.w, 6.f));
+                *reinterpret_cast<float4 *>(st + (jj * 16 + col) * DL_STG_RS + nl) = v;
+            }
         }
-        if constexpr (OUTF32) {
-            float *o = reinterpret_cast<float *>(a.out) + (size_t)p * a.out_cs + a.out_off + n;
-            st4(o, v0);
-            st4(o + 4, v1);
-        } else {
-            T *o = reinterpret_cast<T *>(a.out) + (size_t)p * a.out_cs + a.out_off + n;
-            st4(o, v0);
-            st4(o + 4, v1);
+        wave_lds_sync();
+#pragma unroll
+        for (int it = 0; it < 4; ++it) {
+            const int pl = it * 8 + (lane >> 3);
+            const int p = mtile * TPX + wave * WPX + h * 32 + pl;
+            if (p >= a.M || !cok) continue;
+            float4 v0 = *reinterpret_cast<const float4 *>(st + pl * DL_STG_RS + c8);
+            float4 v1 = *reinterpret_cast<const float4 *>(st + pl * DL_STG_RS + c8 + 4);
+            const int n = n0 + c8;
+            if (a.res) {
+                const T *rp = reinterpret_cast<const T *>(a.res) + (size_t)p * a.res_cs + n;
+                v0 = add4(v0, ld4(rp));
+                v1 = add4(v1, ld4(rp + 4));
+            }
+            if constexpr (OUTF32) {
+                float *o = reinterpret_cast<float *>(a.out) + (size_t)p * a.out_cs + a.out_off + n;
+                st4(o, v0);
+                st4(o + 4, v1);
+            } else {
+                T *o = reinterpret_cast<T *>(a.out) + (size_t)p * a.out_cs + a.out_off + n;
+                st4(o, v0);
+                st4(o + 4, v1);
+            }
         }
     }
 }
 
 // ------------------------------------------------------------------ depthwise 3x3
-// One thread = DW_PX consecutive output pixels of one row x 8 channels, the 9 x 8 weights loaded once
-// into registers for all of them. Threads with consecutive ids take consecutive channel groups of the
-// same pixels (coalesced 16-B loads). DW_PX = 4 measured slower than 1 (1.36 vs 1.09 ms per
-// 16-frame forward): the kernel is latency-bound and wants the extra waves.
-// Weights [9][C] f32 (already rounded to T's precision on the host), bias [C]. Per pixel the taps are
-// summed in (ky, kx) order, then bias, ReLU6.
-constexpr int DW_PX = 1;
+// One thread = one output pixel x 8 channels; threads with consecutive ids take consecutive channel
+// groups of the same pixel (coalesced 16-B loads). Weights [9][C] f32 (already rounded to T's
+// precision on the host), loaded per in-range tap; bias [C]. Sum in tap order (ky, kx), then bias,
+// ReLU6. Measured variants (per 16-frame 513x513 forward, 17 launches): this form 1.09 ms; all 72
+// weights hoisted into registers 1.41 ms; 4 output pixels per thread sharing them 1.36 ms — the
+// kernel is latency-bound and wants the waves.
+// 8 consecutive elements -> two float4, one 16-B load for bf16
+__device__ __forceinline__ void ld8f(const __bf16 *p, float4 &a, float4 &b) {
+    const uint4 u = *reinterpret_cast<const uint4 *>(p);
+    a = unpack_bf16x4((u32x2_t){u.x, u.y});
+    b = unpack_bf16x4((u32x2_t){u.z, u.w});
+}
+__device__ __forceinline__ void ld8f(const float *p, float4 &a, float4 &b) {
+    a = ld4f(p);
+    b = ld4f(p + 4);
+}
+
 template <typename T>
 __global__ void __launch_bounds__(256) dl_dw_kernel(const DlDwArgs a) {
     const int i = blockIdx.x * 256 + threadIdx.x;
     const int groups = a.C >> 3;
-    const int qx = (a.Wout + DW_PX - 1) / DW_PX;
-    if (i >= a.B * a.Hout * qx * groups) return;
-    const int g = i % groups, q = i / groups;
-    const int oxq = q % qx, t = q / qx;
-    const int oy = t % a.Hout, b = t / a.Hout;
-    const int iy0 = oy * a.stride - a.pad_t;
+    if (i >= a.M * groups) return;
+    const int g = i % groups, p = i / groups;
+    const int b = (int)fdiv((uint32_t)p, a.mHW, a.sHW);
+    const int r = p - b * a.Hout * a.Wout;
+    const int oy = (int)fdiv((uint32_t)r, a.mW, a.sW);
+    const int ox = r - oy * a.Wout;
+    const int iy0 = oy * a.stride - a.pad_t, ix0 = ox * a.stride - a.pad_l;
     const T *in = reinterpret_cast<const T *>(a.in);
-    float4 w[9][2];
+    float acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-    for (int k = 0; k < 9; ++k) {
-        w[k][0] = ld4f(a.w + k * a.C + g * 8);
-        w[k][1] = ld4f(a.w + k * a.C + g * 8 + 4);
+    for (int ky = 0; ky < 3; ++ky) {
+        const int iy = iy0 + ky * a.dil;
+        if ((unsigned)iy >= (unsigned)a.Hin) continue;
+#pragma unroll
+        for (int kx = 0; kx < 3; ++kx) {
+            const int ix = ix0 + kx * a.dil;
+            if ((unsigned)ix >= (unsigned)a.Win) continue;
+            const T *px = in + ((size_t)(b * a.Hin + iy) * a.Win + ix) * a.C + g * 8;
+            float4 x0, x1;
+            ld8f(px, x0, x1);
+            const float *w = a.w + (ky * 3 + kx) * a.C + g * 8;
+            const float4 w0 = ld4f(w), w1 = ld4f(w + 4);
+            acc[0] = fmaf(x0.x, w0.x, acc[0]); acc[1] = fmaf(x0.y, w0.y, acc[1]);
+            acc[2] = fmaf(x0.z, w0.z, acc[2]); acc[3] = fmaf(x0.w, w0.w, acc[3]);
+            acc[4] = fmaf(x1.x, w1.x, acc[4]); acc[5] = fmaf(x1.y, w1.y, acc[5]);
+            acc[6] = fmaf(x1.z, w1.z, acc[6]); acc[7] = fmaf(x1.w, w1.w, acc[7]);
+        }
     }
     const float4 b0 = ld4f(a.bias + g * 8), b1 = ld4f(a.bias + g * 8 + 4);
     auto r6 = [](float v) { return fminf(fmaxf(v, 0.f), 6.f); };
-#pragma unroll
-    for (int j = 0; j < DW_PX; ++j) {
-        const int ox = oxq * DW_PX + j;
-        if (ox >= a.Wout) break;
-        const int ix0 = ox * a.stride - a.pad_l;
-        float acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-        for (int ky = 0; ky < 3; ++ky) {
-            const int iy = iy0 + ky * a.dil;
-            if ((unsigned)iy >= (unsigned)a.Hin) continue;
-#pragma unroll
-            for (int kx = 0; kx < 3; ++kx) {
-                const int ix = ix0 + kx * a.dil;
-                if ((unsigned)ix >= (unsigned)a.Win) continue;
-                const T *px = in + ((size_t)(b * a.Hin + iy) * a.Win + ix) * a.C + g * 8;
-                const float4 x0 = ld4(px), x1 = ld4(px + 4);
-                const float4 w0 = w[ky * 3 + kx][0], w1 = w[ky * 3 + kx][1];
-                acc[0] = fmaf(x0.x, w0.x, acc[0]); acc[1] = fmaf(x0.y, w0.y, acc[1]);
-                acc[2] = fmaf(x0.z, w0.z, acc[2]); acc[3] = fmaf(x0.w, w0.w, acc[3]);
-                acc[4] = fmaf(x1.x, w1.x, acc[4]); acc[5] = fmaf(x1.y, w1.y, acc[5]);
-                acc[6] = fmaf(x1.z, w1.z, acc[6]); acc[7] = fmaf(x1.w, w1.w, acc[7]);
-            }
-        }
-        const float4 v0 = make_float4(r6(acc[0] + b0.x), r6(acc[1] + b0.y), r6(acc[2] + b0.z), r6(acc[3] + b0.w));
-        const float4 v1 = make_float4(r6(acc[4] + b1.x), r6(acc[5] + b1.y), r6(acc[6] + b1.z), r6(acc[7] + b1.w));
-        T *o = reinterpret_cast<T *>(a.out) + ((size_t)(b * a.Hout + oy) * a.Wout + ox) * a.C + g * 8;
-        st4(o, v0);
-        st4(o + 4, v1);
-    }
+    const float4 v0 = make_float4(r6(acc[0] + b0.x), r6(acc[1] + b0.y), r6(acc[2] + b0.z), r6(acc[3] + b0.w));
+    const float4 v1 = make_float4(r6(acc[4] + b1.x), r6(acc[5] + b1.y), r6(acc[6] + b1.z), r6(acc[7] + b1.w));
+    T *o = reinterpret_cast<T *>(a.out) + (size_t)p * a.C + g * 8;
+    st4(o, v0);
+    st4(o + 4, v1);
 }
 
 // ------------------------------------------------------------------ image pooling
@@ -316,20 +403,29 @@ hipError_t dl_launch_prep(int prec, const DlPrepArgs &a, hipStream_t s) {
     return hipGetLastError();
 }
 
-hipError_t dl_launch_conv(int prec, bool out_f32, const DlConvArgs &a, hipStream_t s) {
-    const dim3 g((a.M + 127) / 128, a.NP / 64);
+template <int NB>
+static void conv_nb(int prec, bool out_f32, bool dwf, const DlConvArgs &a, hipStream_t s) {
+    const dim3 g(((a.M + NB * 64 - 1) / (NB * 64)) * (a.NP / 64));
     if (prec == PREC_BF16) {
-        if (out_f32) hipLaunchKernelGGL((dl_conv_kernel<__bf16, true>), g, dim3(256), 0, s, a);
-        else hipLaunchKernelGGL((dl_conv_kernel<__bf16, false>), g, dim3(256), 0, s, a);
+        if (dwf) hipLaunchKernelGGL((dl_conv_kernel<__bf16, false, true, NB>), g, dim3(256), 0, s, a);
+        else if (out_f32) hipLaunchKernelGGL((dl_conv_kernel<__bf16, true, false, NB>), g, dim3(256), 0, s, a);
+        else hipLaunchKernelGGL((dl_conv_kernel<__bf16, false, false, NB>), g, dim3(256), 0, s, a);
     } else {
-        if (out_f32) hipLaunchKernelGGL((dl_conv_kernel<float, true>), g, dim3(256), 0, s, a);
-        else hipLaunchKernelGGL((dl_conv_kernel<float, false>), g, dim3(256), 0, s, a);
+        if (dwf) hipLaunchKernelGGL((dl_conv_kernel<float, false, true, NB>), g, dim3(256), 0, s, a);
+        else if (out_f32) hipLaunchKernelGGL((dl_conv_kernel<float, true, false, NB>), g, dim3(256), 0, s, a);
+        else hipLaunchKernelGGL((dl_conv_kernel<float, false, false, NB>), g, dim3(256), 0, s, a);
     }
+}
+
+hipError_t dl_launch_conv(int prec, bool out_f32, const DlConvArgs &a, hipStream_t s) {
+    const bool dwf = a.dw_w != nullptr;
+    if (a.nb == 4) conv_nb<4>(prec, out_f32, dwf, a, s);
+    else conv_nb<2>(prec, out_f32, dwf, a, s);
     return hipGetLastError();
 }
 
 hipError_t dl_launch_dw(int prec, const DlDwArgs &a, hipStream_t s) {
-    const int n = a.B * a.Hout * ((a.Wout + DW_PX - 1) / DW_PX) * (a.C >> 3);
+    const int n = a.M * (a.C >> 3);
     const dim3 g((n + 255) / 256);
     if (prec == PREC_BF16) hipLaunchKernelGGL(dl_dw_kernel<__bf16>, g, dim3(256), 0, s, a);
     else hipLaunchKernelGGL(dl_dw_kernel<float>, g, dim3(256), 0, s, a);

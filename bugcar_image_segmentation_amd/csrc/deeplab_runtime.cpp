@@ -97,6 +97,17 @@ bool check_op(const bugseg_dl *c, const DlOp &o, std::string &why) {
             why = "conv: weights out of the blob"; return false;
         }
         if ((double)B * Hin * Win * CS * es >= 2147483648.0) { why = "conv: input exceeds 31-bit offsets"; return false; }
+        if (f[30] != 0 && f[30] != 2 && f[30] != 4) { why = "conv: pixel fragments per wave must be 2 or 4"; return false; }
+        if (f[27] >= 0) {   // depthwise-fused projection: 1x1 over the dw output grid (Hout, Wout)
+            const int dws = f[29] & 0xff, dwd = (f[29] >> 8) & 0xff, pt = (f[29] >> 16) & 0xff, pl = (f[29] >> 24) & 0xff;
+            if (kh != 1 || kw != 1 || stride != 1 || f[13] || f[14] || dws < 1 || dwd < 1 ||
+                (Hout - 1) * dws - pt > Hin - 1 + 2 * dwd || (Wout - 1) * dws - pl > Win - 1 + 2 * dwd) {
+                why = "conv: bad depthwise-fused geometry"; return false;
+            }
+            if (!in_w(c, f[27], 9L * CS * 4) || !in_w(c, f[28], (long)CS * 4) || f[27] % 16 || f[28] % 16) {
+                why = "conv: depthwise weights out of the blob"; return false;
+            }
+        }
         return true;
     }
     case OP_DW: {
@@ -155,6 +166,13 @@ hipError_t run_op(bugseg_dl *c, const DlOp &o, const uint8_t *rgb, int H, int W,
         a.bias_img = f[25] >= 0 ? static_cast<const float *>(bufp(c, f[25])) : nullptr;
         a.bias_img_stride = f[26];
         a.in_bytes = (uint32_t)((size_t)B * a.Hin * a.Win * a.CS * (c->prec == PREC_BF16 ? 2 : 4));
+        a.nb = f[30] == 4 ? 4 : 2;
+        if (f[27] >= 0) {
+            a.dw_w = reinterpret_cast<const float *>(wb + f[27]);
+            a.dw_b = reinterpret_cast<const float *>(wb + f[28]);
+            a.dw_stride = f[29] & 0xff; a.dw_dil = (f[29] >> 8) & 0xff;
+            a.dw_pt = (f[29] >> 16) & 0xff; a.dw_pl = (f[29] >> 24) & 0xff;
+        }
         fastdiv((uint32_t)(a.Hout * a.Wout), a.mHW, a.sHW);
         fastdiv((uint32_t)a.Wout, a.mW, a.sW);
         return dl_launch_conv(c->prec, f[24] != 0, a, s);

@@ -33,6 +33,7 @@ Op list (``lower``): int32 records of ``OP_FIELDS`` fields, interpreted by deepl
 """
 from __future__ import annotations
 
+import os
 from dataclasses import dataclass, field
 
 import numpy as np
@@ -233,15 +234,31 @@ def pack_conv(c: Conv, cinS: int, bf16: bool):
     return _round(p, bf16), bb.astype(np.float32), cinP, NP
 
 
-def lower(net: DeepLab, B: int, bf16: bool):
+def _pick_nb(tag: str, hw: int, K: int, cout: int) -> int:
+    """Measured on MI355X (bench_deeplab.py per-op times, 16 frames): 4 pixel fragments per wave pay
+    for wide, deep 1x1s (960 -> 320: 219 -> 169 us, 576 -> 160: 87 -> 72 us); 2 win for shallow K
+    (expansions, 24 -> 144: 30 -> 34 us with 4). BUGSEG_DL_NB=2|4 forces one for A/B runs."""
+    env = os.environ.get("BUGSEG_DL_NB")
+    if env:
+        return int(env)
+    return 4 if K >= 192 and cout >= 64 else 2
+
+
+def lower(net: DeepLab, B: int, bf16: bool, fuse_dw: bool = False, nb=None):
     """-> (weight blob bytes, ops int32 (nops, OP_FIELDS), buffer bytes uint64 (nbufs,), info dict).
     Buffers: 0 input, 1/2 block ping-pong, 3 expanded, 4 depthwise out, 5 ASPP concat, 6 projection,
-    7 logits (f32), 8 pooling partials (f32), 9 per-image projection bias (f32)."""
+    7 logits (f32), 8 pooling partials (f32), 9 per-image projection bias (f32).
+    nb: pixel fragments per wave of the conv kernel (CONV field 30): 2 or 4, a callable
+    (tag, Hout * Wout, K, cout) -> 2 | 4, or None for the measured default (_pick_nb).
+    fuse_dw: each block's depthwise conv runs inside its projection's operand loads (CONV fields
+    27-29: dw weight / bias offsets, stride | dil << 8 | pad_t << 16 | pad_l << 24); bit-identical to
+    the default plan (separate DW ops through buffer 4) but measured 2.4x slower (5.1 vs 2.2 ms per
+    16-frame forward for the pair): the 9 tap loads of every operand chunk serialise ahead of the
+    MFMAs and are recomputed for every 64-channel output tile."""
     es = 2 if bf16 else 4
     blob = _Blob(bf16)
     ops = []
-    nb = 10
-    need = [0] * nb
+    need = [256] * 10
     info = dict(flops=0.0, bytes=0.0, per_op=[])
 
     def use(buf, nbytes):
@@ -259,10 +276,19 @@ def lower(net: DeepLab, B: int, bf16: bool):
     op([OP_PREP, 0], "prep", 0, B * Hc * Wc * (3 + 8 * es))
 
     def conv(c: Conv, src, H, W, CS, dst, out_cs, out_off=0, res=-1, out_f32=False, bias_img=-1, bias_img_stride=0,
-             zero_bias=False, cout=None, tag="conv"):
+             zero_bias=False, cout=None, tag="conv", dwf=None):
         k = c.k
         Ho, pt = same_pad(H, k, c.stride, c.dil)
         Wo, pl = same_pad(W, k, c.stride, c.dil)
+        extra = [-1, -1, 0]
+        Hin, Win = H, W
+        if dwf is not None:   # (dw conv, its input H, W): this 1x1 runs over the dw output grid
+            d, Hin, Win = dwf
+            Ho, dpt = same_pad(Hin, 3, d.stride, d.dil)
+            Wo, dpl = same_pad(Win, 3, d.stride, d.dil)
+            wd, bd = d.folded()
+            extra = [blob.add(_round(wd.reshape(CS, 9).T, bf16), False), blob.add(bd.astype(np.float32), False),
+                     d.stride | d.dil << 8 | dpt << 16 | dpl << 24]
         wp, bias, cinP, NP = pack_conv(c, CS, bf16)
         if zero_bias:
             bias = np.zeros_like(bias)
@@ -272,10 +298,13 @@ def lower(net: DeepLab, B: int, bf16: bool):
         oes = 4 if out_f32 else es
         use(dst, B * Ho * Wo * out_cs * oes)
         cin = c.w.shape[1]
-        flops = 2.0 * B * Ho * Wo * c.cout * cin * k * k
-        nbytes = B * H * W * CS * es + B * Ho * Wo * cw * oes + (B * Ho * Wo * cw * es if res >= 0 else 0) + wp.size * es
-        op([OP_CONV, src, dst, res, H, W, CS, Ho, Wo, k, k, c.stride, c.dil, pt, pl, cinP, NP, w_off, b_off, c.act,
-            out_cs if res >= 0 else 0, out_cs, out_off, cw, int(out_f32), bias_img, bias_img_stride], tag, flops, nbytes)
+        flops = 2.0 * B * Ho * Wo * c.cout * cin * k * k + (2.0 * B * Ho * Wo * CS * 9 if dwf else 0)
+        nbytes = B * Hin * Win * CS * es + B * Ho * Wo * cw * oes + (B * Ho * Wo * cw * es if res >= 0 else 0) + wp.size * es
+        t = tag if dwf is None else "conv dw+project"
+        f30 = nb(t, Ho * Wo, cinP * k * k, cw) if callable(nb) else (nb or _pick_nb(t, Ho * Wo, cinP * k * k, cw))
+        op([OP_CONV, src, dst, res, Hin, Win, CS, Ho, Wo, k, k, c.stride, c.dil, pt, pl, cinP, NP, w_off, b_off, c.act,
+            out_cs if res >= 0 else 0, out_cs, out_off, cw, int(out_f32), bias_img, bias_img_stride] + extra + [f30],
+           tag if dwf is None else "conv dw+project", flops, nbytes)
         return Ho, Wo
 
     # stem
@@ -293,6 +322,12 @@ def lower(net: DeepLab, B: int, bf16: bool):
         d = blk.dw
         Ho, pt = same_pad(H, 3, d.stride, d.dil)
         Wo, pl = same_pad(W, 3, d.stride, d.dil)
+        Cout = blk.project.cout
+        if fuse_dw:
+            conv(blk.project, src, H, W, Cm, nxt, Cout, res=x_in if blk.residual else -1, dwf=(d, H, W))
+            H, W = Ho, Wo
+            cur, C = nxt, Cout
+            continue
         wd, bd = d.folded()
         w_off = blob.add(_round(wd.reshape(Cm, 9).T, bf16), False)
         b_off = blob.add(bd.astype(np.float32), False)
@@ -300,7 +335,6 @@ def lower(net: DeepLab, B: int, bf16: bool):
         op([OP_DW, src, 4, H, W, Cm, Ho, Wo, d.stride, d.dil, pt, pl, w_off, b_off], "dw",
            2.0 * B * Ho * Wo * Cm * 9, B * (H * W + Ho * Wo) * Cm * es)
         H, W = Ho, Wo
-        Cout = blk.project.cout
         conv(blk.project, 4, H, W, Cm, nxt, Cout, res=x_in if blk.residual else -1, tag="conv project")
         cur, C = nxt, Cout
 

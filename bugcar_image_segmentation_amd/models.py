@@ -194,7 +194,10 @@ class DeepLabV3(InferenceModel):
     FROZEN_GRAPH_NAME = "deeplab.pb"
     CROP_SIZE = 513
 
-    def __init__(self, GRAPH_PB_PATH=None, *, net=None, precision: str = "bf16", device: int | None = None):
+    def __init__(self, GRAPH_PB_PATH=None, *, net=None, precision: str = "bf16", device: int | None = None,
+                 fuse_dw: bool = False):
+        """fuse_dw=True computes each depthwise conv inside its projection's operand loads
+        (bit-identical, measured slower; deeplab_spec.lower)."""
         from . import deeplab_spec
         if precision not in ("fp32", "bf16"):
             raise ValueError("precision must be 'fp32' or 'bf16'")
@@ -217,11 +220,12 @@ class DeepLabV3(InferenceModel):
         self._blob = None
         self._plan_B = None
         self.plan_info = None
+        self.fuse_dw = fuse_dw
 
     def _ensure_plan(self, B: int) -> None:
         if self._plan_B == B:
             return
-        blob, ops, bufs, info = self._spec.lower(self.net, B, self.precision == "bf16")
+        blob, ops, bufs, info = self._spec.lower(self.net, B, self.precision == "bf16", fuse_dw=self.fuse_dw)
         if self._blob is None:
             self.ctx.load_weights(blob)
             self._blob = blob

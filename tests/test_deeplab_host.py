@@ -37,6 +37,10 @@ def test_lowering_is_consistent():
     kinds = list(ops[:, 0])
     assert kinds[0] == S.OP_PREP and kinds[-1] == S.OP_ARGMAX and kinds.count(S.OP_POOL) == 1
     assert kinds.count(S.OP_DW) == 17
+    _, ops_f, _, info_f = S.lower(net, 2, bf16=True, fuse_dw=True)
+    assert list(ops_f[:, 0]).count(S.OP_DW) == 0 and info["nops"] == info_f["nops"] + 17
+    assert [t for t, _, _ in info_f["per_op"]].count("conv dw+project") == 17
+    assert info["bytes"] > info_f["bytes"] and info["flops"] == info["flops"]
     conv = ops[ops[:, 0] == S.OP_CONV]
     assert np.all(conv[:, 17] % 256 == 0) and np.all(conv[:, 17] < len(blob))   # weight offsets aligned, inside
     assert np.all(conv[:, 15] % 32 == 0) and np.all(conv[:, 16] % 64 == 0)

@@ -91,3 +91,18 @@ def test_deeplab_errors(gpu):
         model.predict(_frames(1, 66, 40, 0))
     with pytest.raises(ValueError):
         model.predict(np.zeros((1, 10, 10, 4), np.uint8))
+
+
+@pytest.mark.parametrize("precision", ["fp32", "bf16"])
+def test_deeplab_fused_dw_bit_identical(gpu, precision):
+    """The depthwise-fused projection against the default plan (separate depthwise launches)."""
+    net = S.build_deeplab(width=0.5, crop=129, atrous_rates=(6,))
+    x = _frames(2, 129, 129, 21)
+    fused = DeepLabV3(net=net, precision=precision, fuse_dw=True)
+    plain = DeepLabV3(net=net, precision=precision)
+    a = fused.predict(x)
+    la = fused.logits_device().cpu()
+    b = plain.predict(x)
+    lb = plain.logits_device().cpu()
+    assert torch.equal(la, lb)
+    assert np.array_equal(a, b)
