@@ -33,7 +33,7 @@ struct DlConvArgs {
     uint32_t mHW, mW; int sHW, sW;   // fdiv by Hout * Wout and by Wout
     // depthwise-fused projection (dw_w != nullptr): `in` is the depthwise conv's INPUT (B, Hin, Win, CS)
     // and the 1x1 conv's B operand is computed on load: relu6(sum_taps in * dw_w + dw_b), rounded to T
-    const float *dw_w;   // [9][CS]
+    const void *dw_w;    // [9][CS] T
     const float *dw_b;   // [CS]
     int dw_stride, dw_dil, dw_pt, dw_pl;
     int nb;              // pixel fragments per wave: 2 (128-px workgroup tile) or 4 (256 px)
@@ -43,7 +43,7 @@ struct DlDwArgs {
     const void *in;      // (B, Hin, Win, C) T
     int B, Hin, Win, C;
     int Hout, Wout, M, stride, dil, pad_t, pad_l;
-    const float *w;      // [9][C]
+    const void *w;       // [9][C] T
     const float *bias;   // [C]
     void *out;           // (B, Hout, Wout, C) T
     uint32_t mHW, mW; int sHW, sW;

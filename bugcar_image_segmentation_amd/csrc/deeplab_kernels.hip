@@ -65,14 +65,14 @@ constexpr int DL_STG_RS = 68;   // staging row stride (floats): 64 channels + 4 
 // dw kernel's exact order (taps (ky, kx), fmaf per channel, then bias, ReLU6), rounded to T.
 template <typename T>
 __device__ __forceinline__ void dw8(typename Tr<T>::Raw &out, __amdgpu_buffer_rsrc_t rin, const uint32_t (&tb)[9], int c,
-                                    const float *dw_w, const float *dw_b, int C) {
+                                    const T *dw_w, const float *dw_b, int C) {
     float acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
 #pragma unroll
     for (int t = 0; t < 9; ++t) {
         if (tb[t] == OOB) continue;
         const uint32_t off = (tb[t] + c) * (uint32_t)sizeof(T);
         const float4 x0 = bld4(rin, off, (const T *)nullptr), x1 = bld4(rin, off + 4 * sizeof(T), (const T *)nullptr);
-        const float4 w0 = ld4f(dw_w + t * C + c), w1 = ld4f(dw_w + t * C + c + 4);
+        const float4 w0 = ld4(dw_w + t * C + c), w1 = ld4(dw_w + t * C + c + 4);
         acc[0] = fmaf(x0.x, w0.x, acc[0]); acc[1] = fmaf(x0.y, w0.y, acc[1]);
         acc[2] = fmaf(x0.z, w0.z, acc[2]); acc[3] = fmaf(x0.w, w0.w, acc[3]);
         acc[4] = fmaf(x1.x, w1.x, acc[4]); acc[5] = fmaf(x1.y, w1.y, acc[5]);
@@ -144,7 +144,7 @@ __global__ void __launch_bounds__(256) dl_conv_kernel(const DlConvArgs a) {
             Raw bx[NB], wa[4];
 #pragma unroll
             for (int j = 0; j < NB; ++j) {
-                if (c < a.CS) dw8<T>(bx[j], rin, tb[j], c, a.dw_w, a.dw_b, a.CS);
+                if (c < a.CS) dw8<T>(bx[j], rin, tb[j], c, reinterpret_cast<const T *>(a.dw_w), a.dw_b, a.CS);
                 else zero(bx[j]);
             }
 #pragma unroll
@@ -258,9 +258,9 @@ __global__ void __launch_bounds__(256) dl_conv_kernel(const DlConvArgs a) {
 // One thread = one output pixel x 8 channels; threads with consecutive ids take consecutive channel
 // groups of the same pixel (coalesced 16-B loads). Weights [9][C] f32 (already rounded to T's
 // precision on the host), loaded per in-range tap; bias [C]. Sum in tap order (ky, kx), then bias,
-// ReLU6. Measured variants (per 16-frame 513x513 forward, 17 launches): this form 1.09 ms; all 72
-// weights hoisted into registers 1.41 ms; 4 output pixels per thread sharing them 1.36 ms — the
-// kernel is latency-bound and wants the waves.
+// ReLU6. Measured variants (per 16-frame 513x513 forward, 17 launches): one pixel per thread with f32
+// weights 1.09 ms (L1-bound: 48 B of loads per tap and lane, two thirds of them weights); all 72
+// weights hoisted into registers 1.41 ms; 4 output pixels per thread sharing them 1.36 ms.
 // 8 consecutive elements -> two float4, one 16-B load for bf16
 __device__ __forceinline__ void ld8f(const __bf16 *p, float4 &a, float4 &b) {
     const uint4 u = *reinterpret_cast<const uint4 *>(p);
@@ -272,45 +272,68 @@ __device__ __forceinline__ void ld8f(const float *p, float4 &a, float4 &b) {
     b = ld4f(p + 4);
 }
 
+// Two output rows per thread: rows r1 and r1 + ph where ph = the dilation for stride 1 (their taps
+// share two of three input rows) and 1 for stride 2; each 16-B weight load (T, per tap) serves both.
+// Row slots: slot yq -> block yq / ph, phase yq % ph, r1 = block * 2ph + phase; every row exactly once.
 template <typename T>
 __global__ void __launch_bounds__(256) dl_dw_kernel(const DlDwArgs a) {
     const int i = blockIdx.x * 256 + threadIdx.x;
     const int groups = a.C >> 3;
-    if (i >= a.M * groups) return;
-    const int g = i % groups, p = i / groups;
-    const int b = (int)fdiv((uint32_t)p, a.mHW, a.sHW);
-    const int r = p - b * a.Hout * a.Wout;
-    const int oy = (int)fdiv((uint32_t)r, a.mW, a.sW);
-    const int ox = r - oy * a.Wout;
-    const int iy0 = oy * a.stride - a.pad_t, ix0 = ox * a.stride - a.pad_l;
-    const T *in = reinterpret_cast<const T *>(a.in);
-    float acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+    const int ph = a.stride == 1 ? a.dil : 1;
+    const int slots = (a.Hout + 2 * ph - 1) / (2 * ph) * ph;
+    if (i >= a.B * slots * a.Wout * groups) return;
+    const int g = i % groups, q = i / groups;
+    const int ox = q % a.Wout, t = q / a.Wout;
+    const int yq = t % slots, b = t / slots;
+    const int r1 = (yq / ph) * 2 * ph + yq % ph, r2 = r1 + ph;
+    if (r1 >= a.Hout) return;
+    const bool v2 = r2 < a.Hout;
+    const int ix0 = ox * a.stride - a.pad_l;
+    const int iy1 = r1 * a.stride - a.pad_t, iy2 = r2 * a.stride - a.pad_t;
+    const T *in = reinterpret_cast<const T *>(a.in) + (size_t)b * a.Hin * a.Win * a.C + g * 8;
+    const T *wt = reinterpret_cast<const T *>(a.w) + g * 8;
+    float acc1[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f}, acc2[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+    auto fma8 = [](float (&acc)[8], float4 x0, float4 x1, float4 w0, float4 w1) {
+        acc[0] = fmaf(x0.x, w0.x, acc[0]); acc[1] = fmaf(x0.y, w0.y, acc[1]);
+        acc[2] = fmaf(x0.z, w0.z, acc[2]); acc[3] = fmaf(x0.w, w0.w, acc[3]);
+        acc[4] = fmaf(x1.x, w1.x, acc[4]); acc[5] = fmaf(x1.y, w1.y, acc[5]);
+        acc[6] = fmaf(x1.z, w1.z, acc[6]); acc[7] = fmaf(x1.w, w1.w, acc[7]);
+    };
 #pragma unroll
     for (int ky = 0; ky < 3; ++ky) {
-        const int iy = iy0 + ky * a.dil;
-        if ((unsigned)iy >= (unsigned)a.Hin) continue;
+        const int ya = iy1 + ky * a.dil, yb = iy2 + ky * a.dil;
+        const bool oka = (unsigned)ya < (unsigned)a.Hin, okb = v2 && (unsigned)yb < (unsigned)a.Hin;
+        if (!oka && !okb) continue;
 #pragma unroll
         for (int kx = 0; kx < 3; ++kx) {
             const int ix = ix0 + kx * a.dil;
             if ((unsigned)ix >= (unsigned)a.Win) continue;
-            const T *px = in + ((size_t)(b * a.Hin + iy) * a.Win + ix) * a.C + g * 8;
-            float4 x0, x1;
-            ld8f(px, x0, x1);
-            const float *w = a.w + (ky * 3 + kx) * a.C + g * 8;
-            const float4 w0 = ld4f(w), w1 = ld4f(w + 4);
-            acc[0] = fmaf(x0.x, w0.x, acc[0]); acc[1] = fmaf(x0.y, w0.y, acc[1]);
-            acc[2] = fmaf(x0.z, w0.z, acc[2]); acc[3] = fmaf(x0.w, w0.w, acc[3]);
-            acc[4] = fmaf(x1.x, w1.x, acc[4]); acc[5] = fmaf(x1.y, w1.y, acc[5]);
-            acc[6] = fmaf(x1.z, w1.z, acc[6]); acc[7] = fmaf(x1.w, w1.w, acc[7]);
+            float4 w0, w1, x0, x1;
+            ld8f(wt + (ky * 3 + kx) * a.C, w0, w1);
+            if (oka) {
+                ld8f(in + ((size_t)ya * a.Win + ix) * a.C, x0, x1);
+                fma8(acc1, x0, x1, w0, w1);
+            }
+            if (okb) {
+                ld8f(in + ((size_t)yb * a.Win + ix) * a.C, x0, x1);
+                fma8(acc2, x0, x1, w0, w1);
+            }
         }
     }
-    const float4 b0 = ld4f(a.bias + g * 8), b1 = ld4f(a.bias + g * 8 + 4);
+    float4 b0, b1;
+    ld8f(reinterpret_cast<const float *>(a.bias) + g * 8, b0, b1);
     auto r6 = [](float v) { return fminf(fmaxf(v, 0.f), 6.f); };
-    const float4 v0 = make_float4(r6(acc[0] + b0.x), r6(acc[1] + b0.y), r6(acc[2] + b0.z), r6(acc[3] + b0.w));
-    const float4 v1 = make_float4(r6(acc[4] + b1.x), r6(acc[5] + b1.y), r6(acc[6] + b1.z), r6(acc[7] + b1.w));
-    T *o = reinterpret_cast<T *>(a.out) + (size_t)p * a.C + g * 8;
-    st4(o, v0);
-    st4(o + 4, v1);
+    T *o = reinterpret_cast<T *>(a.out) + (size_t)b * a.Hout * a.Wout * a.C + g * 8;
+    {
+        T *o1 = o + ((size_t)r1 * a.Wout + ox) * a.C;
+        st4(o1, make_float4(r6(acc1[0] + b0.x), r6(acc1[1] + b0.y), r6(acc1[2] + b0.z), r6(acc1[3] + b0.w)));
+        st4(o1 + 4, make_float4(r6(acc1[4] + b1.x), r6(acc1[5] + b1.y), r6(acc1[6] + b1.z), r6(acc1[7] + b1.w)));
+    }
+    if (v2) {
+        T *o2 = o + ((size_t)r2 * a.Wout + ox) * a.C;
+        st4(o2, make_float4(r6(acc2[0] + b0.x), r6(acc2[1] + b0.y), r6(acc2[2] + b0.z), r6(acc2[3] + b0.w)));
+        st4(o2 + 4, make_float4(r6(acc2[4] + b1.x), r6(acc2[5] + b1.y), r6(acc2[6] + b1.z), r6(acc2[7] + b1.w)));
+    }
 }
 
 // ------------------------------------------------------------------ image pooling
@@ -425,7 +448,8 @@ hipError_t dl_launch_conv(int prec, bool out_f32, const DlConvArgs &a, hipStream
 }
 
 hipError_t dl_launch_dw(int prec, const DlDwArgs &a, hipStream_t s) {
-    const int n = a.M * (a.C >> 3);
+    const int ph = a.stride == 1 ? a.dil : 1;
+    const int n = a.B * ((a.Hout + 2 * ph - 1) / (2 * ph) * ph) * a.Wout * (a.C >> 3);
     const dim3 g((n + 255) / 256);
     if (prec == PREC_BF16) hipLaunchKernelGGL(dl_dw_kernel<__bf16>, g, dim3(256), 0, s, a);
     else hipLaunchKernelGGL(dl_dw_kernel<float>, g, dim3(256), 0, s, a);

@@ -104,7 +104,7 @@ bool check_op(const bugseg_dl *c, const DlOp &o, std::string &why) {
                 (Hout - 1) * dws - pt > Hin - 1 + 2 * dwd || (Wout - 1) * dws - pl > Win - 1 + 2 * dwd) {
                 why = "conv: bad depthwise-fused geometry"; return false;
             }
-            if (!in_w(c, f[27], 9L * CS * 4) || !in_w(c, f[28], (long)CS * 4) || f[27] % 16 || f[28] % 16) {
+            if (!in_w(c, f[27], 9L * CS * (long)es) || !in_w(c, f[28], (long)CS * 4) || f[27] % 16 || f[28] % 16) {
                 why = "conv: depthwise weights out of the blob"; return false;
             }
         }
@@ -115,7 +115,7 @@ bool check_op(const bugseg_dl *c, const DlOp &o, std::string &why) {
         const long w_off = f[12], b_off = f[13];
         if (C < 8 || C % 8 || Hin < 1 || Win < 1 || Hout < 1 || Wout < 1 || f[8] < 1 || f[9] < 1) { why = "dw: bad shape"; return false; }
         if (!buf_ok(c, src, (double)B * Hin * Win * C * es) || !buf_ok(c, dst, (double)B * Hout * Wout * C * es)) { why = "dw: buffer too small"; return false; }
-        if (!in_w(c, w_off, 9L * C * 4) || !in_w(c, b_off, (long)C * 4) || w_off % 16 || b_off % 16) { why = "dw: weights out of the blob"; return false; }
+        if (!in_w(c, w_off, 9L * C * (long)es) || !in_w(c, b_off, (long)C * 4) || w_off % 16 || b_off % 16) { why = "dw: weights out of the blob"; return false; }
         return true;
     }
     case OP_POOL: {
@@ -168,7 +168,7 @@ hipError_t run_op(bugseg_dl *c, const DlOp &o, const uint8_t *rgb, int H, int W,
         a.in_bytes = (uint32_t)((size_t)B * a.Hin * a.Win * a.CS * (c->prec == PREC_BF16 ? 2 : 4));
         a.nb = f[30] == 4 ? 4 : 2;
         if (f[27] >= 0) {
-            a.dw_w = reinterpret_cast<const float *>(wb + f[27]);
+            a.dw_w = wb + f[27];
             a.dw_b = reinterpret_cast<const float *>(wb + f[28]);
             a.dw_stride = f[29] & 0xff; a.dw_dil = (f[29] >> 8) & 0xff;
             a.dw_pt = (f[29] >> 16) & 0xff; a.dw_pl = (f[29] >> 24) & 0xff;
@@ -182,7 +182,7 @@ hipError_t run_op(bugseg_dl *c, const DlOp &o, const uint8_t *rgb, int H, int W,
         a.in = bufp(c, f[1]); a.out = bufp(c, f[2]);
         a.B = B; a.Hin = f[3]; a.Win = f[4]; a.C = f[5]; a.Hout = f[6]; a.Wout = f[7];
         a.M = B * a.Hout * a.Wout; a.stride = f[8]; a.dil = f[9]; a.pad_t = f[10]; a.pad_l = f[11];
-        a.w = reinterpret_cast<const float *>(wb + f[12]);
+        a.w = wb + f[12];
         a.bias = reinterpret_cast<const float *>(wb + f[13]);
         fastdiv((uint32_t)(a.Hout * a.Wout), a.mHW, a.sHW);
         fastdiv((uint32_t)a.Wout, a.mW, a.sW);

@@ -287,7 +287,7 @@ def lower(net: DeepLab, B: int, bf16: bool, fuse_dw: bool = False, nb=None):
             Ho, dpt = same_pad(Hin, 3, d.stride, d.dil)
             Wo, dpl = same_pad(Win, 3, d.stride, d.dil)
             wd, bd = d.folded()
-            extra = [blob.add(_round(wd.reshape(CS, 9).T, bf16), False), blob.add(bd.astype(np.float32), False),
+            extra = [blob.add(wd.reshape(CS, 9).T, True), blob.add(bd.astype(np.float32), False),
                      d.stride | d.dil << 8 | dpt << 16 | dpl << 24]
         wp, bias, cinP, NP = pack_conv(c, CS, bf16)
         if zero_bias:
@@ -329,7 +329,7 @@ def lower(net: DeepLab, B: int, bf16: bool, fuse_dw: bool = False, nb=None):
             cur, C = nxt, Cout
             continue
         wd, bd = d.folded()
-        w_off = blob.add(_round(wd.reshape(Cm, 9).T, bf16), False)
+        w_off = blob.add(wd.reshape(Cm, 9).T, True)   # [9][C] in the compute type
         b_off = blob.add(bd.astype(np.float32), False)
         use(4, B * Ho * Wo * Cm * es)
         op([OP_DW, src, 4, H, W, Cm, Ho, Wo, d.stride, d.dil, pt, pl, w_off, b_off], "dw",
