@@ -47,6 +47,7 @@ struct DlDwArgs {
     const float *bias;   // [C]
     void *out;           // (B, Hout, Wout, C) T
     uint32_t mHW, mW; int sHW, sW;
+    uint32_t in_bytes;
 };
 
 struct DlPoolArgs {

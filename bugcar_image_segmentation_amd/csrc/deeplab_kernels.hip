@@ -275,6 +275,12 @@ __device__ __forceinline__ void ld8f(const float *p, float4 &a, float4 &b) {
 // Two output rows per thread: rows r1 and r1 + ph where ph = the dilation for stride 1 (their taps
 // share two of three input rows) and 1 for stride 2; each 16-B weight load (T, per tap) serves both.
 // Row slots: slot yq -> block yq / ph, phase yq % ph, r1 = block * 2ph + phase; every row exactly once.
+__device__ __forceinline__ void raw4(const RawB &r, float4 &a, float4 &b) {
+    a = unpack_bf16x4((u32x2_t){r.v.x, r.v.y});
+    b = unpack_bf16x4((u32x2_t){r.v.z, r.v.w});
+}
+__device__ __forceinline__ void raw4(const RawF &r, float4 &a, float4 &b) { a = r.a; b = r.b; }
+
 template <typename T>
 __global__ void __launch_bounds__(256) dl_dw_kernel(const DlDwArgs a) {
     const int i = blockIdx.x * 256 + threadIdx.x;
@@ -290,7 +296,6 @@ __global__ void __launch_bounds__(256) dl_dw_kernel(const DlDwArgs a) {
     const bool v2 = r2 < a.Hout;
     const int ix0 = ox * a.stride - a.pad_l;
     const int iy1 = r1 * a.stride - a.pad_t, iy2 = r2 * a.stride - a.pad_t;
-    const T *in = reinterpret_cast<const T *>(a.in) + (size_t)b * a.Hin * a.Win * a.C + g * 8;
     const T *wt = reinterpret_cast<const T *>(a.w) + g * 8;
     float acc1[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f}, acc2[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
     auto fma8 = [](float (&acc)[8], float4 x0, float4 x1, float4 w0, float4 w1) {
@@ -299,26 +304,39 @@ __global__ void __launch_bounds__(256) dl_dw_kernel(const DlDwArgs a) {
         acc[4] = fmaf(x1.x, w1.x, acc[4]); acc[5] = fmaf(x1.y, w1.y, acc[5]);
         acc[6] = fmaf(x1.z, w1.z, acc[6]); acc[7] = fmaf(x1.w, w1.w, acc[7]);
     };
+    // branch-free: a padding tap's offset is out of the descriptor's range and reads 0; adding the
+    // zero product leaves the sum unchanged (+0 + -0 = +0), so this matches the skipping form bit for
+    // bit, and all 27 loads can be in flight together
+    const __amdgpu_buffer_rsrc_t rin = mkbuf(a.in, a.in_bytes);
+    const uint32_t cb = (uint32_t)((size_t)b * a.Hin * a.Win * a.C + g * 8);
+    uint32_t oa[9], ob[9];
 #pragma unroll
     for (int ky = 0; ky < 3; ++ky) {
         const int ya = iy1 + ky * a.dil, yb = iy2 + ky * a.dil;
         const bool oka = (unsigned)ya < (unsigned)a.Hin, okb = v2 && (unsigned)yb < (unsigned)a.Hin;
-        if (!oka && !okb) continue;
 #pragma unroll
         for (int kx = 0; kx < 3; ++kx) {
             const int ix = ix0 + kx * a.dil;
-            if ((unsigned)ix >= (unsigned)a.Win) continue;
-            float4 w0, w1, x0, x1;
-            ld8f(wt + (ky * 3 + kx) * a.C, w0, w1);
-            if (oka) {
-                ld8f(in + ((size_t)ya * a.Win + ix) * a.C, x0, x1);
-                fma8(acc1, x0, x1, w0, w1);
-            }
-            if (okb) {
-                ld8f(in + ((size_t)yb * a.Win + ix) * a.C, x0, x1);
-                fma8(acc2, x0, x1, w0, w1);
-            }
+            const bool okx = (unsigned)ix < (unsigned)a.Win;
+            oa[ky * 3 + kx] = oka && okx ? (cb + (uint32_t)((ya * a.Win + ix) * a.C)) * (uint32_t)sizeof(T) : OOB;
+            ob[ky * 3 + kx] = okb && okx ? (cb + (uint32_t)((yb * a.Win + ix) * a.C)) * (uint32_t)sizeof(T) : OOB;
         }
+    }
+    typename Tr<T>::Raw xa[9], xb[9], wr[9];
+#pragma unroll
+    for (int t = 0; t < 9; ++t) {
+        bld8(xa[t], rin, oa[t]);
+        bld8(xb[t], rin, ob[t]);
+        ld8(wr[t], wt + t * a.C);
+    }
+#pragma unroll
+    for (int t = 0; t < 9; ++t) {
+        float4 w0, w1, x0, x1;
+        raw4(wr[t], w0, w1);
+        raw4(xa[t], x0, x1);
+        fma8(acc1, x0, x1, w0, w1);
+        raw4(xb[t], x0, x1);
+        fma8(acc2, x0, x1, w0, w1);
     }
     float4 b0, b1;
     ld8f(reinterpret_cast<const float *>(a.bias) + g * 8, b0, b1);

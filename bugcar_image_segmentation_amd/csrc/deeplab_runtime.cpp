@@ -115,6 +115,7 @@ bool check_op(const bugseg_dl *c, const DlOp &o, std::string &why) {
         const long w_off = f[12], b_off = f[13];
         if (C < 8 || C % 8 || Hin < 1 || Win < 1 || Hout < 1 || Wout < 1 || f[8] < 1 || f[9] < 1) { why = "dw: bad shape"; return false; }
         if (!buf_ok(c, src, (double)B * Hin * Win * C * es) || !buf_ok(c, dst, (double)B * Hout * Wout * C * es)) { why = "dw: buffer too small"; return false; }
+        if ((double)B * Hin * Win * C * es >= 2147483648.0) { why = "dw: input exceeds 31-bit offsets"; return false; }
         if (!in_w(c, w_off, 9L * C * (long)es) || !in_w(c, b_off, (long)C * 4) || w_off % 16 || b_off % 16) { why = "dw: weights out of the blob"; return false; }
         return true;
     }
@@ -183,6 +184,7 @@ hipError_t run_op(bugseg_dl *c, const DlOp &o, const uint8_t *rgb, int H, int W,
         a.B = B; a.Hin = f[3]; a.Win = f[4]; a.C = f[5]; a.Hout = f[6]; a.Wout = f[7];
         a.M = B * a.Hout * a.Wout; a.stride = f[8]; a.dil = f[9]; a.pad_t = f[10]; a.pad_l = f[11];
         a.w = wb + f[12];
+        a.in_bytes = (uint32_t)((size_t)B * a.Hin * a.Win * a.C * (c->prec == PREC_BF16 ? 2 : 4));
         a.bias = reinterpret_cast<const float *>(wb + f[13]);
         fastdiv((uint32_t)(a.Hout * a.Wout), a.mHW, a.sHW);
         fastdiv((uint32_t)a.Wout, a.mW, a.sW);
