@@ -56,6 +56,7 @@ struct DlPoolArgs {
     int chunk_px, nchunks;
     float *part;         // (B, nchunks, C) scratch
     int cmid, cout;
+    float *y;            // (B, cmid) scratch: the image-pooling branch output
     const float *wp, *bp;    // image-pooling 1x1: [cmid][C], [cmid]
     const float *wq, *bq;    // its columns of the concat projection: [cout][cmid], projection bias [cout]
     float *z;            // (B, z_stride) per-image projection bias

@@ -15,7 +15,7 @@
 //                         channel offset of the destination (ASPP concat without a copy)
 //   dl_dw_kernel          depthwise 3x3 (stride, dilation, SAME pad) + bias + ReLU6, 8 channels/thread
 //   dl_gap_kernel         image-pooling partial sums (deterministic: fixed chunking, no atomics)
-//   dl_pool_kernel        image-pooling branch: mean -> 1x1 + ReLU -> its share of the concat
+//   dl_pool_mean/gemv     image-pooling branch: mean -> 1x1 + ReLU -> its share of the concat
 //                         projection, folded into a per-image bias of the projection conv (the
 //                         branch is a broadcast 1x1 image, so it never has to exist at 65x65)
 //   dl_resize_argmax_kernel  logits (h, w) -> bilinear (align_corners, TF's legacy lerp order) at the
@@ -86,7 +86,8 @@ __device__ __forceinline__ void dw8(typename Tr<T>::Raw &out, __amdgpu_buffer_rs
 }
 
 // Grid: 1-D, the N tiles of one pixel tile adjacent in launch order (they share the input tile).
-// NB = pixel fragments per wave (2: 128-px workgroup tiles, 4: 256-px tiles, twice the MFMAs per weight load).
+// NB = pixel fragments per wave (2: 128-px workgroup tiles, 4: 256 px, 8: 512 px (bf16 only); NB MFMAs per
+// weight-fragment load).
 template <typename T, bool OUTF32, bool DWF, int NB>
 __global__ void __launch_bounds__(256) dl_conv_kernel(const DlConvArgs a) {
     constexpr int WPX = NB * 16, TPX = 4 * WPX;   // pixels per wave / per workgroup
@@ -369,33 +370,37 @@ __global__ void __launch_bounds__(256) dl_gap_kernel(const DlPoolArgs a) {
     }
 }
 
-// One workgroup per image: mean (partials summed in chunk order) -> y = relu(Wp . mean + bp),
-// rounded to T as the stored branch output would be -> z = Wq . y + bq (f32) = the per-image bias
-// of the concat projection. Wp [C][cmid], Wq [cmid][cout] in f32 (rounded to T's precision),
-// transposed so the threads of a workgroup (one output each) read consecutive addresses.
+// Mean per (image, channel): partials summed in chunk order, rounded to T as a stored tensor would
+// be; written over chunk 0 of the partials (each thread reads its own channel's column first).
 template <typename T>
-__global__ void __launch_bounds__(256) dl_pool_kernel(const DlPoolArgs a) {
-    __shared__ float mean[1024];
-    __shared__ float y[1024];
-    const int b = blockIdx.x;
+__global__ void __launch_bounds__(256) dl_pool_mean_kernel(const DlPoolArgs a) {
+    const int i = blockIdx.x * 256 + threadIdx.x;
+    if (i >= a.B * a.C) return;
+    const int b = i / a.C, c = i - b * a.C;
     const float inv = 1.0f / (float)(a.H * a.W);
-    for (int c = threadIdx.x; c < a.C; c += 256) {
-        float s = 0.f;
-        for (int k = 0; k < a.nchunks; ++k) s += a.part[((size_t)b * a.nchunks + k) * a.C + c];
-        mean[c] = (float)(T)(s * inv);
-    }
-    __syncthreads();
-    for (int m = threadIdx.x; m < a.cmid; m += 256) {
-        float s = 0.f;
-        for (int c = 0; c < a.C; ++c) s = fmaf(a.wp[(size_t)c * a.cmid + m], mean[c], s);
-        s = fmaxf(s + a.bp[m], 0.f);
-        y[m] = (float)(T)s;
-    }
-    __syncthreads();
-    for (int n = threadIdx.x; n < a.cout; n += 256) {
-        float s = 0.f;
-        for (int m = 0; m < a.cmid; ++m) s = fmaf(a.wq[(size_t)m * a.cout + n], y[m], s);
-        a.z[(size_t)b * a.z_stride + n] = s + a.bq[n];
+    float s = 0.f;
+    for (int k = 0; k < a.nchunks; ++k) s += a.part[((size_t)b * a.nchunks + k) * a.C + c];
+    a.part[(size_t)b * a.nchunks * a.C + c] = (float)(T)(s * inv);
+}
+
+// One wave per output (image b, row m): out[b][m] = W[m] . in[b] + bias[m] (lanes stride the input,
+// butterfly reduction); stage 0: the image-pooling 1x1 (ReLU, rounded to T) into y; stage 1: its
+// columns of the concat projection plus the projection bias -> the per-image bias z.
+template <typename T, int STAGE>
+__global__ void __launch_bounds__(256) dl_pool_gemv_kernel(const DlPoolArgs a) {
+    const int wv = blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
+    const int rows = STAGE == 0 ? a.cmid : a.cout, cols = STAGE == 0 ? a.C : a.cmid;
+    if (wv >= a.B * rows) return;
+    const int b = wv / rows, m = wv - b * rows;
+    const float *w = (STAGE == 0 ? a.wp : a.wq) + (size_t)m * cols;
+    const float *in = STAGE == 0 ? a.part + (size_t)b * a.nchunks * a.C : a.y + (size_t)b * a.cmid;
+    float s = 0.f;
+    for (int c = lane; c < cols; c += 64) s = fmaf(w[c], in[c], s);
+#pragma unroll
+    for (int o = 32; o >= 1; o >>= 1) s += __shfl_xor(s, o);
+    if (lane == 0) {
+        if (STAGE == 0) a.y[(size_t)b * a.cmid + m] = (float)(T)fmaxf(s + a.bp[m], 0.f);
+        else a.z[(size_t)b * a.z_stride + m] = s + a.bq[m];
     }
 }
 
@@ -404,7 +409,58 @@ __global__ void __launch_bounds__(256) dl_pool_kernel(const DlPoolArgs a) {
 // in f32; top = floor(in), bottom = min(top + 1, in_size - 1), lerp = in - top;
 // value = top_row + (bottom_row - top_row) * y_lerp with row = left + (right - left) * x_lerp.
 // Then argmax over classes (first maximum).
+// One thread = AM_PX consecutive output pixels of a row; the 4 corner logit vectors are (re)loaded
+// only when x0 changes along the run (with the 65 -> 513 scale of 1/8, once per 8 pixels).
+constexpr int AM_PX = 8, AM_C = 24;   // classes held in registers (LCS <= AM_C uses this kernel)
 __global__ void __launch_bounds__(256) dl_resize_argmax_kernel(const DlArgmaxArgs a) {
+#pragma clang fp contract(off)
+    const int qx = (a.Wo + AM_PX - 1) / AM_PX;
+    const int i = blockIdx.x * 256 + threadIdx.x;
+    if (i >= a.B * a.Ho * qx) return;
+    const int xq = i % qx, t = i / qx, y = t % a.Ho, b = t / a.Ho;
+    const float in_y = (float)y * a.sy;
+    const int y0 = (int)floorf(in_y), y1 = min(y0 + 1, a.h - 1);
+    const float ly = in_y - (float)y0;
+    const float *base = a.logits + (size_t)b * a.h * a.w * a.LCS;
+    const float *row0 = base + (size_t)y0 * a.w * a.LCS, *row1 = base + (size_t)y1 * a.w * a.LCS;
+    float tl[AM_C], tr[AM_C], bl[AM_C], br[AM_C];
+    int cur = -1;
+    int64_t *orow = a.out + ((size_t)b * a.Hout + y) * a.Wout;
+    for (int j = 0; j < AM_PX; ++j) {
+        const int x = xq * AM_PX + j;
+        if (x >= a.Wo) break;
+        const float in_x = (float)x * a.sx;
+        const int x0 = (int)floorf(in_x), x1 = min(x0 + 1, a.w - 1);
+        const float lx = in_x - (float)x0;
+        if (x0 != cur) {
+            cur = x0;
+#pragma unroll
+            for (int c0 = 0; c0 < AM_C; c0 += 4) {
+                if (c0 >= a.LCS) break;
+                const float4 q0 = ld4f(row0 + x0 * a.LCS + c0), q1 = ld4f(row0 + x1 * a.LCS + c0);
+                const float4 q2 = ld4f(row1 + x0 * a.LCS + c0), q3 = ld4f(row1 + x1 * a.LCS + c0);
+                tl[c0] = q0.x; tl[c0 + 1] = q0.y; tl[c0 + 2] = q0.z; tl[c0 + 3] = q0.w;
+                tr[c0] = q1.x; tr[c0 + 1] = q1.y; tr[c0 + 2] = q1.z; tr[c0 + 3] = q1.w;
+                bl[c0] = q2.x; bl[c0 + 1] = q2.y; bl[c0 + 2] = q2.z; bl[c0 + 3] = q2.w;
+                br[c0] = q3.x; br[c0 + 1] = q3.y; br[c0 + 2] = q3.z; br[c0 + 3] = q3.w;
+            }
+        }
+        float best = 0.f;
+        int bi = 0;
+#pragma unroll
+        for (int c = 0; c < AM_C; ++c) {
+            if (c >= a.ncls) break;
+            const float top = tl[c] + (tr[c] - tl[c]) * lx;
+            const float bot = bl[c] + (br[c] - bl[c]) * lx;
+            const float v = top + (bot - top) * ly;
+            if (c == 0 || v > best) { best = v; bi = c; }
+        }
+        orow[x] = (int64_t)bi;
+    }
+}
+
+// Any class count: one thread per output pixel, float4 corner loads.
+__global__ void __launch_bounds__(256) dl_resize_argmax_generic(const DlArgmaxArgs a) {
 #pragma clang fp contract(off)
     const int i = blockIdx.x * 256 + threadIdx.x;
     if (i >= a.B * a.Ho * a.Wo) return;
@@ -435,6 +491,7 @@ __global__ void __launch_bounds__(256) dl_resize_argmax_kernel(const DlArgmaxArg
     a.out[((size_t)b * a.Hout + y) * a.Wout + x] = (int64_t)bi;
 }
 
+
 // ------------------------------------------------------------------ launchers
 hipError_t dl_launch_prep(int prec, const DlPrepArgs &a, hipStream_t s) {
     const int n = a.B * a.Hc * a.Wc;
@@ -447,7 +504,10 @@ hipError_t dl_launch_prep(int prec, const DlPrepArgs &a, hipStream_t s) {
 template <int NB>
 static void conv_nb(int prec, bool out_f32, bool dwf, const DlConvArgs &a, hipStream_t s) {
     const dim3 g(((a.M + NB * 64 - 1) / (NB * 64)) * (a.NP / 64));
-    if (prec == PREC_BF16) {
+    if constexpr (NB == 8) {   // bf16, no depthwise fusion (register budget)
+        if (out_f32) hipLaunchKernelGGL((dl_conv_kernel<__bf16, true, false, 8>), g, dim3(256), 0, s, a);
+        else hipLaunchKernelGGL((dl_conv_kernel<__bf16, false, false, 8>), g, dim3(256), 0, s, a);
+    } else if (prec == PREC_BF16) {
         if (dwf) hipLaunchKernelGGL((dl_conv_kernel<__bf16, false, true, NB>), g, dim3(256), 0, s, a);
         else if (out_f32) hipLaunchKernelGGL((dl_conv_kernel<__bf16, true, false, NB>), g, dim3(256), 0, s, a);
         else hipLaunchKernelGGL((dl_conv_kernel<__bf16, false, false, NB>), g, dim3(256), 0, s, a);
@@ -460,7 +520,8 @@ static void conv_nb(int prec, bool out_f32, bool dwf, const DlConvArgs &a, hipSt
 
 hipError_t dl_launch_conv(int prec, bool out_f32, const DlConvArgs &a, hipStream_t s) {
     const bool dwf = a.dw_w != nullptr;
-    if (a.nb == 4) conv_nb<4>(prec, out_f32, dwf, a, s);
+    if (a.nb == 8 && prec == PREC_BF16 && !dwf) conv_nb<8>(prec, out_f32, false, a, s);
+    else if (a.nb >= 4) conv_nb<4>(prec, out_f32, dwf, a, s);
     else conv_nb<2>(prec, out_f32, dwf, a, s);
     return hipGetLastError();
 }
@@ -478,16 +539,25 @@ hipError_t dl_launch_pool(int prec, const DlPoolArgs &a, hipStream_t s) {
     const dim3 g1(a.nchunks, a.B);
     if (prec == PREC_BF16) {
         hipLaunchKernelGGL(dl_gap_kernel<__bf16>, g1, dim3(256), 0, s, a);
-        hipLaunchKernelGGL(dl_pool_kernel<__bf16>, dim3(a.B), dim3(256), 0, s, a);
+        hipLaunchKernelGGL(dl_pool_mean_kernel<__bf16>, dim3((a.B * a.C + 255) / 256), dim3(256), 0, s, a);
+        hipLaunchKernelGGL((dl_pool_gemv_kernel<__bf16, 0>), dim3((a.B * a.cmid + 3) / 4), dim3(256), 0, s, a);
+        hipLaunchKernelGGL((dl_pool_gemv_kernel<__bf16, 1>), dim3((a.B * a.cout + 3) / 4), dim3(256), 0, s, a);
     } else {
         hipLaunchKernelGGL(dl_gap_kernel<float>, g1, dim3(256), 0, s, a);
-        hipLaunchKernelGGL(dl_pool_kernel<float>, dim3(a.B), dim3(256), 0, s, a);
+        hipLaunchKernelGGL(dl_pool_mean_kernel<float>, dim3((a.B * a.C + 255) / 256), dim3(256), 0, s, a);
+        hipLaunchKernelGGL((dl_pool_gemv_kernel<float, 0>), dim3((a.B * a.cmid + 3) / 4), dim3(256), 0, s, a);
+        hipLaunchKernelGGL((dl_pool_gemv_kernel<float, 1>), dim3((a.B * a.cout + 3) / 4), dim3(256), 0, s, a);
     }
     return hipGetLastError();
 }
 
 hipError_t dl_launch_argmax(const DlArgmaxArgs &a, hipStream_t s) {
-    const int n = a.B * a.Ho * a.Wo;
+    if (a.LCS > AM_C) {
+        const int n = a.B * a.Ho * a.Wo;
+        hipLaunchKernelGGL(dl_resize_argmax_generic, dim3((n + 255) / 256), dim3(256), 0, s, a);
+        return hipGetLastError();
+    }
+    const int n = a.B * a.Ho * ((a.Wo + AM_PX - 1) / AM_PX);
     hipLaunchKernelGGL(dl_resize_argmax_kernel, dim3((n + 255) / 256), dim3(256), 0, s, a);
     return hipGetLastError();
 }

@@ -97,7 +97,7 @@ bool check_op(const bugseg_dl *c, const DlOp &o, std::string &why) {
             why = "conv: weights out of the blob"; return false;
         }
         if ((double)B * Hin * Win * CS * es >= 2147483648.0) { why = "conv: input exceeds 31-bit offsets"; return false; }
-        if (f[30] != 0 && f[30] != 2 && f[30] != 4) { why = "conv: pixel fragments per wave must be 2 or 4"; return false; }
+        if (f[30] != 0 && f[30] != 2 && f[30] != 4 && f[30] != 8) { why = "conv: pixel fragments per wave must be 2, 4 or 8"; return false; }
         if (f[27] >= 0) {   // depthwise-fused projection: 1x1 over the dw output grid (Hout, Wout)
             const int dws = f[29] & 0xff, dwd = (f[29] >> 8) & 0xff, pt = (f[29] >> 16) & 0xff, pl = (f[29] >> 24) & 0xff;
             if (kh != 1 || kw != 1 || stride != 1 || f[13] || f[14] || dws < 1 || dwd < 1 ||
@@ -125,14 +125,14 @@ bool check_op(const bugseg_dl *c, const DlOp &o, std::string &why) {
         if (C < 1 || C > 1024 || CS < C || cmid < 1 || cmid > 1024 || cout < 1 || zs < cout || chunk < 1 || nch < 1 ||
             (long)chunk * nch < (long)H * W) { why = "pool: bad shape"; return false; }
         if (!buf_ok(c, src, (double)B * H * W * CS * es) || !buf_ok(c, part, (double)B * nch * C * 4.0) ||
-            !buf_ok(c, z, (double)B * zs * 4.0)) { why = "pool: buffer too small"; return false; }
+            !buf_ok(c, z, (double)B * zs * 4.0) || !buf_ok(c, f[17], (double)B * cmid * 4.0)) { why = "pool: buffer too small"; return false; }
         if (!in_w(c, f[12], (long)cmid * C * 4) || !in_w(c, f[13], (long)cmid * 4) || !in_w(c, f[14], (long)cout * cmid * 4) ||
             !in_w(c, f[15], (long)cout * 4)) { why = "pool: weights out of the blob"; return false; }
         return true;
     }
     case OP_ARGMAX: {
         const int lg = f[1], h = f[2], w = f[3], LCS = f[4], ncls = f[5];
-        if (h < 1 || w < 1 || ncls < 1 || LCS < ncls) { why = "argmax: bad shape"; return false; }
+        if (h < 1 || w < 1 || ncls < 1 || LCS < ncls || LCS % 4) { why = "argmax: bad shape"; return false; }
         if (!buf_ok(c, lg, (double)B * h * w * LCS * 4.0)) { why = "argmax: logits buffer too small"; return false; }
         return true;
     }
@@ -167,7 +167,7 @@ hipError_t run_op(bugseg_dl *c, const DlOp &o, const uint8_t *rgb, int H, int W,
         a.bias_img = f[25] >= 0 ? static_cast<const float *>(bufp(c, f[25])) : nullptr;
         a.bias_img_stride = f[26];
         a.in_bytes = (uint32_t)((size_t)B * a.Hin * a.Win * a.CS * (c->prec == PREC_BF16 ? 2 : 4));
-        a.nb = f[30] == 4 ? 4 : 2;
+        a.nb = f[30] == 8 ? 8 : f[30] == 4 ? 4 : 2;
         if (f[27] >= 0) {
             a.dw_w = wb + f[27];
             a.dw_b = reinterpret_cast<const float *>(wb + f[28]);
@@ -198,6 +198,7 @@ hipError_t run_op(bugseg_dl *c, const DlOp &o, const uint8_t *rgb, int H, int W,
         a.wp = reinterpret_cast<const float *>(wb + f[12]); a.bp = reinterpret_cast<const float *>(wb + f[13]);
         a.wq = reinterpret_cast<const float *>(wb + f[14]); a.bq = reinterpret_cast<const float *>(wb + f[15]);
         a.z_stride = f[16];
+        a.y = static_cast<float *>(bufp(c, f[17]));
         return dl_launch_pool(c->prec, a, s);
     }
     case OP_ARGMAX: {

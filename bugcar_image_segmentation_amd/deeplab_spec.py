@@ -28,7 +28,7 @@ Op list (``lower``): int32 records of ``OP_FIELDS`` fields, interpreted by deepl
   CONV   [2, src, dst, res, Hin, Win, CS, Hout, Wout, kh, kw, stride, dil, pad_t, pad_l, cinP, NP,
           w_off, b_off, act, res_cs, out_cs, out_off, cout, out_f32, bias_img_buf, bias_img_stride]
   DW     [3, src, dst, Hin, Win, C, Hout, Wout, stride, dil, pad_t, pad_l, w_off, b_off]
-  POOL   [4, src, part, z, H, W, C, CS, chunk_px, nchunks, cmid, cout, wp_off, bp_off, wq_off, bq_off, z_stride]
+  POOL   [4, src, part, z, H, W, C, CS, chunk_px, nchunks, cmid, cout, wp_off, bp_off, wq_off, bq_off, z_stride, y]
   ARGMAX [5, logits, h, w, LCS, ncls]
 """
 from __future__ import annotations
@@ -241,13 +241,16 @@ def _pick_nb(tag: str, hw: int, K: int, cout: int) -> int:
     env = os.environ.get("BUGSEG_DL_NB")
     if env:
         return int(env)
+    if K >= 576 and cout >= 160:
+        return 8    # bf16 only (the launcher uses 4 in fp32): 960 -> 320 165 -> 149 us, elsewhere slower
     return 4 if K >= 192 and cout >= 64 else 2
 
 
 def lower(net: DeepLab, B: int, bf16: bool, fuse_dw: bool = False, nb=None):
     """-> (weight blob bytes, ops int32 (nops, OP_FIELDS), buffer bytes uint64 (nbufs,), info dict).
     Buffers: 0 input, 1/2 block ping-pong, 3 expanded, 4 depthwise out, 5 ASPP concat, 6 projection,
-    7 logits (f32), 8 pooling partials (f32), 9 per-image projection bias (f32).
+    7 logits (f32), 8 pooling partials (f32), 9 per-image projection bias (f32), 10 image-pooling
+    branch output (f32).
     nb: pixel fragments per wave of the conv kernel (CONV field 30): 2 or 4, a callable
     (tag, Hout * Wout, K, cout) -> 2 | 4, or None for the measured default (_pick_nb).
     fuse_dw: each block's depthwise conv runs inside its projection's operand loads (CONV fields
@@ -258,7 +261,7 @@ def lower(net: DeepLab, B: int, bf16: bool, fuse_dw: bool = False, nb=None):
     es = 2 if bf16 else 4
     blob = _Blob(bf16)
     ops = []
-    need = [256] * 10
+    need = [256] * 11
     info = dict(flops=0.0, bytes=0.0, per_op=[])
 
     def use(buf, nbytes):
@@ -350,11 +353,12 @@ def lower(net: DeepLab, B: int, bf16: bool, fuse_dw: bool = False, nb=None):
     use(9, B * zs * 4)
     wpool, bpool = net.pool.folded()
     wproj, bproj = net.project.folded()
-    wp_off = blob.add(_round(wpool.reshape(D, C).T, bf16), False)           # [C][D]
+    use(10, B * D * 4)
+    wp_off = blob.add(_round(wpool.reshape(D, C), bf16), False)             # [D][C]
     bp_off = blob.add(bpool.astype(np.float32), False)
-    wq_off = blob.add(_round(wproj.reshape(D, -1)[:, :D].T, bf16), False)   # [D (pooled ch)][D (out)]
+    wq_off = blob.add(_round(wproj.reshape(D, -1)[:, :D], bf16), False)     # [D (out)][D (pooled ch)]
     bq_off = blob.add(bproj.astype(np.float32), False)
-    op([OP_POOL, cur, 8, 9, h, w, C, C, chunk, nch, D, D, wp_off, bp_off, wq_off, bq_off, zs], "pool",
+    op([OP_POOL, cur, 8, 9, h, w, C, C, chunk, nch, D, D, wp_off, bp_off, wq_off, bq_off, zs, 10], "pool",
        2.0 * B * (D * C + D * D) + B * h * w * C, B * h * w * C * es)
     conv(net.aspp0, cur, h, w, C, 5, cat_cs, out_off=0, tag="conv aspp")
     for i, a in enumerate(net.atrous):

@@ -55,6 +55,13 @@ def test_deeplab_fp32_small(gpu, B, H, W, os_, rates):
     _check_fp32(model, net, _frames(B, H, W, B * 7 + H), torch.float64)
 
 
+def test_deeplab_fp32_many_classes(gpu):
+    """More than 24 (padded) classes: the per-pixel resize + argmax kernel."""
+    net = S.build_deeplab(width=0.25, crop=65, num_classes=30)
+    model = DeepLabV3(net=net, precision="fp32")
+    _check_fp32(model, net, _frames(2, 65, 50, 9), torch.float64)
+
+
 def test_deeplab_fp32_full_513(gpu):
     net = S.build_deeplab()
     model = DeepLabV3(net=net, precision="fp32")
