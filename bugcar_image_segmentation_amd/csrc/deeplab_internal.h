@@ -36,7 +36,8 @@ struct DlConvArgs {
     const void *dw_w;    // [9][CS] T
     const float *dw_b;   // [CS]
     int dw_stride, dw_dil, dw_pt, dw_pl;
-    int nb;              // pixel fragments per wave: 2 (128-px workgroup tile) or 4 (256 px)
+    int nb;              // pixel fragments per wave: 2 (128-px workgroup tile), 4 (256 px) or 8 (bf16, 512 px)
+    int tap_packed;      // CS == 8: w is [NP][ceil(taps / 4) * 32], k = tap * 8 + c
 };
 
 struct DlDwArgs {

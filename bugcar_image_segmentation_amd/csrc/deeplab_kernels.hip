@@ -121,7 +121,7 @@ __global__ void __launch_bounds__(256) dl_conv_kernel(const DlConvArgs a) {
 #pragma unroll
         for (int r = 0; r < 4; ++r) acc[j][r] = (f32x4){0.f, 0.f, 0.f, 0.f};
 
-    const int K = a.taps * a.cinP;
+    const int K = a.tap_packed ? ((a.taps + 3) >> 2) * 32 : a.taps * a.cinP;
     const T *wrow[4];
 #pragma unroll
     for (int r = 0; r < 4; ++r) wrow[r] = reinterpret_cast<const T *>(a.w) + (size_t)(n0 + r * 16 + col) * K + kq * 8;
@@ -150,6 +150,27 @@ __global__ void __launch_bounds__(256) dl_conv_kernel(const DlConvArgs a) {
             }
 #pragma unroll
             for (int r = 0; r < 4; ++r) ld8(wa[r], wrow[r] + ch * 32);
+#pragma unroll
+            for (int j = 0; j < NB; ++j)
+#pragma unroll
+                for (int r = 0; r < 4; ++r) mma(acc[j][r], wa[r], bx[j]);
+        }
+    } else if (a.tap_packed) {
+        // input of at most 8 channels (the stem): a k-step is 4 taps x 8 channels, lane group kq
+        // takes tap 4 ks + kq (weights packed k = tap * 8 + c): 3 k-steps for a 3x3 instead of 9
+        const int nks = (a.taps + 3) >> 2;
+        for (int ks = 0; ks < nks; ++ks) {
+            const int t = ks * 4 + kq;
+            const int ky = t / a.kw, kx = t - (t / a.kw) * a.kw;
+            Raw bx[NB], wa[4];
+#pragma unroll
+            for (int j = 0; j < NB; ++j) {
+                const int iy = piy[j] + ky * a.dil, ix = pix[j] + kx * a.dil;
+                const bool ok = t < a.taps && pv[j] && (unsigned)iy < (unsigned)a.Hin && (unsigned)ix < (unsigned)a.Win;
+                bld8(bx[j], rin, ok ? (uint32_t)(((pb[j] * a.Hin + iy) * a.Win + ix) * a.CS) * esz : OOB);
+            }
+#pragma unroll
+            for (int r = 0; r < 4; ++r) ld8(wa[r], wrow[r] + ks * 32);
 #pragma unroll
             for (int j = 0; j < NB; ++j)
 #pragma unroll

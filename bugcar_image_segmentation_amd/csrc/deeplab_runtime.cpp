@@ -93,7 +93,9 @@ bool check_op(const bugseg_dl *c, const DlOp &o, std::string &why) {
         if (!buf_ok(c, dst, (double)B * Hout * Wout * out_cs * (out_f32 ? 4.0 : es))) { why = "conv: destination too small"; return false; }
         if (res >= 0 && (res_cs < cout || !buf_ok(c, res, (double)B * Hout * Wout * res_cs * es))) { why = "conv: residual too small"; return false; }
         if (bimg >= 0 && (bimg_stride < NP || !buf_ok(c, bimg, (double)B * bimg_stride * 4.0))) { why = "conv: per-image bias too small"; return false; }
-        if (!in_w(c, w_off, (long)NP * kh * kw * cinP * (long)es) || !in_w(c, b_off, (long)NP * 4) || w_off % 16 || b_off % 16) {
+        const long wk = f[31] ? (long)((kh * kw + 3) / 4) * 32 : (long)kh * kw * cinP;
+        if (f[31] && (CS != 8 || f[27] >= 0)) { why = "conv: tap packing needs an 8-channel input"; return false; }
+        if (!in_w(c, w_off, (long)NP * wk * (long)es) || !in_w(c, b_off, (long)NP * 4) || w_off % 16 || b_off % 16) {
             why = "conv: weights out of the blob"; return false;
         }
         if ((double)B * Hin * Win * CS * es >= 2147483648.0) { why = "conv: input exceeds 31-bit offsets"; return false; }
@@ -168,6 +170,7 @@ hipError_t run_op(bugseg_dl *c, const DlOp &o, const uint8_t *rgb, int H, int W,
         a.bias_img_stride = f[26];
         a.in_bytes = (uint32_t)((size_t)B * a.Hin * a.Win * a.CS * (c->prec == PREC_BF16 ? 2 : 4));
         a.nb = f[30] == 8 ? 8 : f[30] == 4 ? 4 : 2;
+        a.tap_packed = f[31];
         if (f[27] >= 0) {
             a.dw_w = wb + f[27];
             a.dw_b = reinterpret_cast<const float *>(wb + f[28]);

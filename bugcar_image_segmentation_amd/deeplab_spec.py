@@ -221,14 +221,23 @@ class _Blob:
         return b"".join(self.parts)
 
 
-def pack_conv(c: Conv, cinS: int, bf16: bool):
+def pack_conv(c: Conv, cinS: int, bf16: bool, tap_packed: bool = False):
     """-> (packed [NP][taps][cinP] f32 array (values rounded to the compute type), bias [NP], cinP, NP).
-    Input channel c of tap (ky, kx) sits at k = (ky * kw + kx) * cinP + c."""
+    Input channel c of tap (ky, kx) sits at k = (ky * kw + kx) * cinP + c; tap_packed (inputs of at
+    most 8 channels): [NP][ceil(taps / 4) * 32] with k = tap * 8 + c."""
     w, b = c.folded()
     cout, cin, kh, kw = w.shape
     cinP, NP = _r(max(cinS, cin), 32), _r(cout, 64)
-    p = np.zeros((NP, kh * kw, cinP), np.float64)
-    p[:cout, :, :cin] = w.transpose(0, 2, 3, 1).reshape(cout, kh * kw, cin)
+    if tap_packed:
+        assert cinS == 8 and cin <= 8
+        taps = kh * kw
+        p = np.zeros((NP, (taps + 3) // 4 * 32), np.float64)
+        q = np.zeros((cout, taps, 8))
+        q[:, :, :cin] = w.transpose(0, 2, 3, 1).reshape(cout, taps, cin)
+        p[:cout, :taps * 8] = q.reshape(cout, taps * 8)
+    else:
+        p = np.zeros((NP, kh * kw, cinP), np.float64)
+        p[:cout, :, :cin] = w.transpose(0, 2, 3, 1).reshape(cout, kh * kw, cin)
     bb = np.zeros(NP, np.float64)
     bb[:cout] = b
     return _round(p, bf16), bb.astype(np.float32), cinP, NP
@@ -254,7 +263,8 @@ def lower(net: DeepLab, B: int, bf16: bool, fuse_dw: bool = False, nb=None):
     nb: pixel fragments per wave of the conv kernel (CONV field 30): 2 or 4, a callable
     (tag, Hout * Wout, K, cout) -> 2 | 4, or None for the measured default (_pick_nb).
     fuse_dw: each block's depthwise conv runs inside its projection's operand loads (CONV fields
-    27-29: dw weight / bias offsets, stride | dil << 8 | pad_t << 16 | pad_l << 24); bit-identical to
+    27-29: dw weight / bias offsets, stride | dil << 8 | pad_t << 16 | pad_l << 24; field 31: the
+    stem's tap packing, 4 taps x 8 channels per k-step); bit-identical to
     the default plan (separate DW ops through buffer 4) but measured 2.4x slower (5.1 vs 2.2 ms per
     16-frame forward for the pair): the 9 tap loads of every operand chunk serialise ahead of the
     MFMAs and are recomputed for every 64-channel output tile."""
@@ -292,7 +302,8 @@ def lower(net: DeepLab, B: int, bf16: bool, fuse_dw: bool = False, nb=None):
             wd, bd = d.folded()
             extra = [blob.add(wd.reshape(CS, 9).T, True), blob.add(bd.astype(np.float32), False),
                      d.stride | d.dil << 8 | dpt << 16 | dpl << 24]
-        wp, bias, cinP, NP = pack_conv(c, CS, bf16)
+        tp = CS == 8 and dwf is None and k > 1
+        wp, bias, cinP, NP = pack_conv(c, CS, bf16, tap_packed=tp)
         if zero_bias:
             bias = np.zeros_like(bias)
         w_off = blob.add(wp, True)
@@ -306,7 +317,7 @@ def lower(net: DeepLab, B: int, bf16: bool, fuse_dw: bool = False, nb=None):
         t = tag if dwf is None else "conv dw+project"
         f30 = nb(t, Ho * Wo, cinP * k * k, cw) if callable(nb) else (nb or _pick_nb(t, Ho * Wo, cinP * k * k, cw))
         op([OP_CONV, src, dst, res, Hin, Win, CS, Ho, Wo, k, k, c.stride, c.dil, pt, pl, cinP, NP, w_off, b_off, c.act,
-            out_cs if res >= 0 else 0, out_cs, out_off, cw, int(out_f32), bias_img, bias_img_stride] + extra + [f30],
+            out_cs if res >= 0 else 0, out_cs, out_off, cw, int(out_f32), bias_img, bias_img_stride] + extra + [f30, int(tp)],
            tag if dwf is None else "conv dw+project", flops, nbytes)
         return Ho, Wo
 
