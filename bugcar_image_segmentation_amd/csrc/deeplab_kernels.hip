@@ -61,18 +61,30 @@ __global__ void __launch_bounds__(256) dl_prep_kernel(const DlPrepArgs a) {
 // outside the image and channels past the input's stride read 0 through the buffer descriptor.
 constexpr int DL_STG_RS = 68;   // staging row stride (floats): 64 channels + 4 (bank spread)
 
+__device__ __forceinline__ void raw4(const RawB &r, float4 &a, float4 &b) {
+    a = unpack_bf16x4((u32x2_t){r.v.x, r.v.y});
+    b = unpack_bf16x4((u32x2_t){r.v.z, r.v.w});
+}
+__device__ __forceinline__ void raw4(const RawF &r, float4 &a, float4 &b) { a = r.a; b = r.b; }
+
 // Depthwise 3x3 of 8 channels [c, c+8) at one pixel from its 9 tap offsets (OOB = padding), in the
 // dw kernel's exact order (taps (ky, kx), fmaf per channel, then bias, ReLU6), rounded to T.
 template <typename T>
 __device__ __forceinline__ void dw8(typename Tr<T>::Raw &out, __amdgpu_buffer_rsrc_t rin, const uint32_t (&tb)[9], int c,
                                     const T *dw_w, const float *dw_b, int C) {
+    // branch-free (padding taps read 0 through the descriptor, as in dl_dw_kernel): 18 loads in flight
     float acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+    typename Tr<T>::Raw xr[9], wr[9];
 #pragma unroll
     for (int t = 0; t < 9; ++t) {
-        if (tb[t] == OOB) continue;
-        const uint32_t off = (tb[t] + c) * (uint32_t)sizeof(T);
-        const float4 x0 = bld4(rin, off, (const T *)nullptr), x1 = bld4(rin, off + 4 * sizeof(T), (const T *)nullptr);
-        const float4 w0 = ld4(dw_w + t * C + c), w1 = ld4(dw_w + t * C + c + 4);
+        bld8(xr[t], rin, tb[t] == OOB ? OOB : (tb[t] + c) * (uint32_t)sizeof(T));
+        ld8(wr[t], dw_w + t * C + c);
+    }
+#pragma unroll
+    for (int t = 0; t < 9; ++t) {
+        float4 x0, x1, w0, w1;
+        raw4(xr[t], x0, x1);
+        raw4(wr[t], w0, w1);
         acc[0] = fmaf(x0.x, w0.x, acc[0]); acc[1] = fmaf(x0.y, w0.y, acc[1]);
         acc[2] = fmaf(x0.z, w0.z, acc[2]); acc[3] = fmaf(x0.w, w0.w, acc[3]);
         acc[4] = fmaf(x1.x, w1.x, acc[4]); acc[5] = fmaf(x1.y, w1.y, acc[5]);
@@ -297,12 +309,6 @@ __device__ __forceinline__ void ld8f(const float *p, float4 &a, float4 &b) {
 // Two output rows per thread: rows r1 and r1 + ph where ph = the dilation for stride 1 (their taps
 // share two of three input rows) and 1 for stride 2; each 16-B weight load (T, per tap) serves both.
 // Row slots: slot yq -> block yq / ph, phase yq % ph, r1 = block * 2ph + phase; every row exactly once.
-__device__ __forceinline__ void raw4(const RawB &r, float4 &a, float4 &b) {
-    a = unpack_bf16x4((u32x2_t){r.v.x, r.v.y});
-    b = unpack_bf16x4((u32x2_t){r.v.z, r.v.w});
-}
-__device__ __forceinline__ void raw4(const RawF &r, float4 &a, float4 &b) { a = r.a; b = r.b; }
-
 template <typename T>
 __global__ void __launch_bounds__(256) dl_dw_kernel(const DlDwArgs a) {
     const int i = blockIdx.x * 256 + threadIdx.x;

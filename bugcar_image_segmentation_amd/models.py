@@ -195,7 +195,7 @@ class DeepLabV3(InferenceModel):
     CROP_SIZE = 513
 
     def __init__(self, GRAPH_PB_PATH=None, *, net=None, precision: str = "bf16", device: int | None = None,
-                 fuse_dw: bool = False):
+                 fuse_dw: bool | None = None):
         """fuse_dw=True computes each depthwise conv inside its projection's operand loads
         (bit-identical, measured slower; deeplab_spec.lower)."""
         from . import deeplab_spec
@@ -220,7 +220,7 @@ class DeepLabV3(InferenceModel):
         self._blob = None
         self._plan_B = None
         self.plan_info = None
-        self.fuse_dw = fuse_dw
+        self.fuse_dw = bool(int(os.environ.get("BUGSEG_DL_FUSE_DW", "0"))) if fuse_dw is None else fuse_dw
 
     def _ensure_plan(self, B: int) -> None:
         if self._plan_B == B:

@@ -1,11 +1,12 @@
-# One GPU session: parity tests, bench (bf16 + fp32), rocprofv3 kernel-trace stats of the bench.
+# One GPU session: every GPU test, smoke(), the headline bench (ENet -> BEV) and the config-4 bench (DeepLab).
 set -o pipefail
 cd $GRAFT_REPO_ROOT
-mkdir -p gpurun_out
+mkdir -p gpurun_out/round
 export TMPDIR=/tmp
-timeout -k 10 600 python -m pytest tests -m gpu -q -rA --timeout 500 > gpurun_out/pytest_gpu.log 2>&1
-echo "pytest exit $?" >> gpurun_out/pytest_gpu.log
-timeout -k 10 300 python bench.py --steps 20 --warmup 5 > gpurun_out/bench_bf16.json 2> gpurun_out/bench_bf16.err || exit 1
-timeout -k 10 300 python bench.py --steps 10 --warmup 3 --precision fp32 --no-cpu-baseline > gpurun_out/bench_fp32.json 2> gpurun_out/bench_fp32.err || exit 1
-timeout -k 10 400 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_bf16 -o run --output-format csv -- python bench.py --steps 10 --warmup 3 --no-cpu-baseline > gpurun_out/prof_bf16.log 2>&1 || exit 1
+timeout -k 10 600 python -u -m pytest tests -m gpu -x -q -rA --timeout 120 --timeout-method thread > gpurun_out/round/pytest_gpu.log 2>&1 || { tail -40 gpurun_out/round/pytest_gpu.log; exit 1; }
+tail -2 gpurun_out/round/pytest_gpu.log
+timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/round/smoke.txt 2>&1 || { cat gpurun_out/round/smoke.txt; exit 1; }
+cat gpurun_out/round/smoke.txt
+timeout -k 10 300 python bench.py > gpurun_out/round/bench.json 2> gpurun_out/round/bench.err || exit 1
+timeout -k 10 300 python bench_deeplab.py > gpurun_out/round/bench_deeplab.json 2> gpurun_out/round/bench_deeplab.err || exit 1
 echo done
