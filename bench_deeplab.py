@@ -63,6 +63,22 @@ def cpu_baseline(net, budget_s):
                       f"semantics), {el:.1f} s, one frame per call"}
 
 
+def pmc_traffic(tag, batch):
+    """HBM bytes per launch of op tag `tag` from the committed PMC summary
+    (profiles/dl_pmc_traffic.json, written by scripts/dl_pmc_summary.py from rocprofv3 FETCH_SIZE /
+    WRITE_SIZE passes of this script at the same batch), or None."""
+    p = os.path.join(ROOT, "profiles", "dl_pmc_traffic.json")
+    try:
+        with open(p) as f:
+            d = json.load(f)
+    except (OSError, ValueError):
+        return None
+    if int(d.get("batch", -1)) != batch:
+        return None
+    v = d.get("per_launch_bytes", {}).get(tag)
+    return None if v is None else round(float(v))
+
+
 def main():
     a = parse()
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -138,7 +154,7 @@ def main():
                        "parallelism": f"frame-sharded dp{world}"},
             "roofline": {
                 "bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": None,
+                "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": pmc_traffic(tag, B),
                 "kernel": f"{tag}: dominant kernel tag ({k['launches']} launches, {k['us']:.0f} us of {fwd_us:.0f} us "
                           f"per forward); {k['bytes'] / k['launches'] / 1e6:.1f} MB per launch (input once + output "
                           f"once + residual + weights); {k['flops'] / (k['us'] * 1e-6) / 1e12:.1f} TFLOP/s "

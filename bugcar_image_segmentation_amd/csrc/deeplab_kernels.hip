@@ -26,6 +26,15 @@
 
 namespace bugseg {
 
+// XCD-aware block order: workgroup h goes to XCD h % 8 (round-robin dispatch), so neighbouring
+// blockIdx values land on different XCDs and each of them pulls the tiles they share into its own L2.
+// Remapped, XCD x walks the contiguous run of logical blocks [x q', (x + 1) q') (q' = G / 8, the first
+// G % 8 XCDs one more): the N tiles of one pixel tile, and row-neighbouring pixel tiles, share an L2.
+__device__ __forceinline__ int xcd_block(int h, int G) {
+    const int q = G >> 3, r = G & 7, x = h & 7, s = h >> 3;
+    return x < r ? x * (q + 1) + s : r * (q + 1) + (x - r) * q + s;
+}
+
 // ------------------------------------------------------------------ preprocess
 // TF: pad_to_bounding_box(x - 127.5) + 127.5 (exact for integer x), then (2/255) * x - 1 in f32.
 template <typename T>
@@ -97,7 +106,8 @@ __device__ __forceinline__ void dw8(typename Tr<T>::Raw &out, __amdgpu_buffer_rs
     set8(out, v);
 }
 
-// Grid: 1-D, the N tiles of one pixel tile adjacent in launch order (they share the input tile).
+// Grid: 1-D, the N tiles of one pixel tile adjacent in logical order (they share the input tile), the
+// logical order XCD-aware (xcd_block).
 // NB = pixel fragments per wave (2: 128-px workgroup tiles, 4: 256 px, 8: 512 px (bf16 only); NB MFMAs per
 // weight-fragment load).
 template <typename T, bool OUTF32, bool DWF, int NB>
@@ -107,8 +117,9 @@ __global__ void __launch_bounds__(256) dl_conv_kernel(const DlConvArgs a) {
     const int lane = threadIdx.x & 63, col = lane & 15, kq = lane >> 4;
     const int wave = threadIdx.x >> 6;
     const int ntn = a.NP >> 6;
-    const int n0 = (blockIdx.x % ntn) * 64;
-    const int mtile = blockIdx.x / ntn;
+    const int bid = xcd_block(blockIdx.x, gridDim.x);
+    const int n0 = (bid % ntn) * 64;
+    const int mtile = bid / ntn;
     const __amdgpu_buffer_rsrc_t rin = mkbuf(a.in, a.in_bytes);
     const int esz = (int)sizeof(T);
 
@@ -311,7 +322,7 @@ __device__ __forceinline__ void ld8f(const float *p, float4 &a, float4 &b) {
 // Row slots: slot yq -> block yq / ph, phase yq % ph, r1 = block * 2ph + phase; every row exactly once.
 template <typename T>
 __global__ void __launch_bounds__(256) dl_dw_kernel(const DlDwArgs a) {
-    const int i = blockIdx.x * 256 + threadIdx.x;
+    const int i = xcd_block(blockIdx.x, gridDim.x) * 256 + threadIdx.x;
     const int groups = a.C >> 3;
     const int ph = a.stride == 1 ? a.dil : 1;
     const int slots = (a.Hout + 2 * ph - 1) / (2 * ph) * ph;
