@@ -185,9 +185,9 @@ class DeepLabV3(InferenceModel):
     resize the DeepLab demo applies before feeding the graph. The node-name printing
     (models.py:112-113, 116, 121) is dropped.
 
-    Weights: ``deeplab.pb`` is absent (.MISSING_LARGE_BLOBS:1) and a TF GraphDef of DeepLab is not
-    imported (the GraphDef importer covers ENet); GRAPH_PB_PATH may be a ``deeplab_spec.save`` .npz,
-    or None for the seeded synthetic network (``deeplab_spec.build_deeplab``)."""
+    Weights: GRAPH_PB_PATH may be a frozen TF DeepLab-MobileNetV2 GraphDef (``deeplab.pb``, read by
+    deeplab_graphdef.import_deeplab; the file itself is absent, .MISSING_LARGE_BLOBS:1), a
+    ``deeplab_spec.save`` .npz, or None for the seeded synthetic network (``deeplab_spec.build_deeplab``)."""
     INPUT_TENSOR_NAME = "import/ImageTensor:0"
     OUTPUT_TENSOR_NAME = "import/SemanticPredictions:0"
     INPUT_SIZE = 1024
@@ -209,10 +209,13 @@ class DeepLabV3(InferenceModel):
                     raise FileNotFoundError(f"{GRAPH_PB_PATH}: no such file")
                 with open(GRAPH_PB_PATH, "rb") as f:
                     magic = f.read(4)
-                if magic[:2] != b"PK":
-                    raise NotImplementedError(f"{GRAPH_PB_PATH}: only deeplab_spec .npz weight files are supported "
-                                              "(TF GraphDef import covers ENet only)")
-                net = deeplab_spec.load(GRAPH_PB_PATH)
+                if magic[:2] == b"PK":
+                    net = deeplab_spec.load(GRAPH_PB_PATH)
+                else:
+                    # a frozen TF DeepLab export (models.py:104-110 reads it as a GraphDef)
+                    from .deeplab_graphdef import import_deeplab
+                    with open(GRAPH_PB_PATH, "rb") as f:
+                        net = import_deeplab(f.read(), crop=self.CROP_SIZE)
         self.net = net
         self.precision = precision
         self.ctx = N.DeepLabContext(device, N.BF16 if precision == "bf16" else N.FP32)

@@ -3,7 +3,9 @@ GraphDefs: the stand-in for the reference's ``sess.run(OUTPUT_TENSOR_NAME, feed_
 (models.py:43-44) where TensorFlow is absent.
 
 It evaluates the ops an ENet export uses (convolutions, transposed convolutions, pooling with
-argmax, scatter, padding, slicing, concatenation, batch norm and the elementwise ops) with TF's
+argmax, scatter, padding, slicing, concatenation, batch norm and the elementwise ops) and those of a
+DeepLab export (depthwise convolutions, SpaceToBatchND / BatchToSpaceND around atrous layers, spatial
+Mean, AvgPool, align_corners ResizeBilinear) with TF's
 semantics — NHWC / NCHW data formats, SAME / VALID / EXPLICIT padding (SAME splits the padding
 total as floor before / ceil after), Conv2DBackpropInput cropping its full output at the forward
 convolution's leading pad, MaxPoolWithArgmax flat indices ((y * W + x) * C + c) — in float64.
@@ -68,6 +70,65 @@ def conv2d(node, x, w):
     xt = F.pad(_t(xc), (pw[0], pw[1], ph[0], ph[1]))
     y = F.conv2d(xt, _t(np.transpose(w, (3, 2, 0, 1))), stride=s, dilation=d).numpy()
     return _from_nchw(y, nchw)
+
+
+def depthwise_conv2d(node, x, w):
+    """DepthwiseConv2dNative, channel multiplier 1: filter (kh, kw, C, 1)."""
+    nchw = _nchw(node)
+    s = _hw(node.attr.get("strides", [1, 1, 1, 1]), nchw)
+    d = _hw(node.attr.get("dilations", [1, 1, 1, 1]), nchw)
+    if w.shape[3] != 1:
+        raise GraphImportError(f"{node.name}: channel multiplier {w.shape[3]}")
+    xc = _to_nchw(x, nchw)
+    kh, kw, C = w.shape[:3]
+    padding = _s(node.attr.get("padding"))
+    ph, pw = (_same(xc.shape[2], kh, s[0], d[0]), _same(xc.shape[3], kw, s[1], d[1])) if padding == "SAME" \
+        else ((0, 0), (0, 0))
+    xt = F.pad(_t(xc), (pw[0], pw[1], ph[0], ph[1]))
+    y = F.conv2d(xt, _t(np.transpose(w, (2, 3, 0, 1))), stride=s, dilation=d, groups=C).numpy()
+    return _from_nchw(y, nchw)
+
+
+def space_to_batch_nd(x, block, pads):
+    """NHWC: pad the spatial dims, then (B, H, W, C) -> (bh * bw * B, H / bh, W / bw, C), batch index
+    (i * bw + j) * B + b for the block offset (i, j) — TF's SpaceToBatchND."""
+    bh, bw = (int(v) for v in block)
+    x = np.pad(x, ((0, 0), tuple(int(v) for v in pads[0]), tuple(int(v) for v in pads[1]), (0, 0)))
+    B, H, W, C = x.shape
+    if H % bh or W % bw:
+        raise GraphImportError("SpaceToBatchND: padded size not a multiple of the block")
+    y = x.reshape(B, H // bh, bh, W // bw, bw, C).transpose(2, 4, 0, 1, 3, 5)
+    return y.reshape(bh * bw * B, H // bh, W // bw, C)
+
+
+def batch_to_space_nd(x, block, crops):
+    bh, bw = (int(v) for v in block)
+    N, h, w, C = x.shape
+    B = N // (bh * bw)
+    y = x.reshape(bh, bw, B, h, w, C).transpose(2, 3, 0, 4, 1, 5).reshape(B, h * bh, w * bw, C)
+    (c0, c1), (c2, c3) = ((int(a), int(b)) for a, b in crops)
+    return y[:, c0:h * bh - c1, c2:w * bw - c3]
+
+
+def avg_pool(node, x):
+    if _s(node.attr.get("padding")) != "VALID":
+        raise GraphImportError(f"{node.name}: only VALID average pooling is interpreted")
+    nchw = _nchw(node)
+    k = _hw(node.attr["ksize"], nchw)
+    s = _hw(node.attr["strides"], nchw)
+    y = F.avg_pool2d(_t(_to_nchw(x, nchw)), k, stride=s).numpy()
+    return _from_nchw(y, nchw)
+
+
+def resize_bilinear(node, x, size):
+    """TF1 ResizeBilinear (NHWC), align_corners=True: the f32 computation of
+    oracle/deeplab_oracle.resize_bilinear_tf (TF's op computes in f32)."""
+    from oracle.deeplab_oracle import resize_bilinear_tf
+    if not node.attr.get("align_corners") or node.attr.get("half_pixel_centers"):
+        raise GraphImportError(f"{node.name}: only align_corners=True bilinear resizing is interpreted")
+    oh, ow = (int(v) for v in size)
+    y = resize_bilinear_tf(np.transpose(np.asarray(x, np.float32), (0, 3, 1, 2)), oh, ow)
+    return np.transpose(y, (0, 2, 3, 1)).astype(np.float64)
 
 
 def conv2d_backprop_input(node, sizes, w, x):
@@ -138,6 +199,19 @@ def run(pb: bytes, feed: dict, fetch: str):
             out = conv2d(n, *args)
         elif op == "Conv2DBackpropInput":
             out = conv2d_backprop_input(n, *args)
+        elif op == "DepthwiseConv2dNative":
+            out = depthwise_conv2d(n, *args)
+        elif op == "SpaceToBatchND":
+            out = space_to_batch_nd(*args)
+        elif op == "BatchToSpaceND":
+            out = batch_to_space_nd(*args)
+        elif op == "AvgPool":
+            out = avg_pool(n, args[0])
+        elif op in ("ResizeBilinear", "ResizeBilinearV2"):
+            out = resize_bilinear(n, *args)
+        elif op == "Mean":
+            ax = tuple(int(v) for v in np.atleast_1d(args[1]))
+            out = np.mean(args[0], axis=ax, keepdims=bool(n.attr.get("keep_dims")))
         elif op == "MaxPool":
             out = max_pool(n, args[0])
         elif op == "MaxPoolWithArgmax":

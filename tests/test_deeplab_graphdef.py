@@ -1,0 +1,94 @@
+"""DeepLab GraphDef importer (bugcar_image_segmentation_amd/deeplab_graphdef.py, SURVEY.md §8(f) rows 1 + 3)
+against graphs written by tests/deeplab_graph_writer.py in two encodings, and the NumPy GraphDef
+interpreter (oracle/tf_graph.py, the sess.run stand-in) on the same graphs.
+
+Bars: imported weights equal the written network's after batch-norm folding (rtol 1e-5, fp32
+storage); the oracle forward of the imported network equals the written network's within 1e-4
+(fp64); the interpreter's pre-resize logits equal the oracle's within 1e-4 and its
+SemanticPredictions equal the oracle's class map wherever the top-2 margin exceeds 1e-4.
+Parity against TF on the real deeplab.pb is unpinned (neither exists here).
+"""
+import numpy as np
+import pytest
+import torch
+
+from bugcar_image_segmentation_amd import deeplab_spec as S
+from bugcar_image_segmentation_amd.deeplab_graphdef import graphdef_to_npz, import_deeplab
+from bugcar_image_segmentation_amd.graphdef import GraphImportError
+from deeplab_graph_writer import write_deeplab_graph
+from oracle import deeplab_oracle as O
+from oracle import tf_graph
+
+CROP = 65
+
+
+def _net(rates=(2, 4), os_=8, ncls=S.NUM_CLASSES):
+    return S.build_deeplab(width=0.25, crop=CROP, output_stride=os_, atrous_rates=rates, num_classes=ncls)
+
+
+def _same_weights(a: S.DeepLab, b: S.DeepLab):
+    ca, cb = list(S._convs(a)), list(S._convs(b))
+    assert [n for n, _ in ca] == [n for n, _ in cb]
+    for (name, x), (_, y) in zip(ca, cb):
+        assert (x.act, x.stride, x.dil, x.depthwise) == (y.act, y.stride, y.dil, y.depthwise), name
+        wx, bx = x.folded()
+        wy, by = y.folded()
+        assert wx.shape == wy.shape, name
+        np.testing.assert_allclose(wy, wx, rtol=1e-5, atol=1e-6, err_msg=name)
+        np.testing.assert_allclose(by, bx, rtol=1e-5, atol=1e-6, err_msg=name)
+    assert [blk.residual for blk in a.blocks] == [blk.residual for blk in b.blocks]
+    assert (a.num_classes, a.crop) == (b.num_classes, b.crop)
+
+
+@pytest.mark.parametrize("style", ["slim", "folded"])
+@pytest.mark.parametrize("rates,os_", [((2, 4), 8), ((), 16)])
+def test_import_recovers_the_network(style, rates, os_):
+    net = _net(rates, os_)
+    got = import_deeplab(write_deeplab_graph(net, style, 60, 65), crop=CROP)
+    _same_weights(net, got)
+    assert got.output_stride == os_
+    if style == "slim":     # unfolded batch norm keeps its own statistics
+        assert got.stem.gamma is not None and got.stem.eps == pytest.approx(net.stem.eps)
+    x = np.random.default_rng(3).integers(0, 256, (2, 60, 65, 3), dtype=np.uint8)
+    np.testing.assert_allclose(O.forward(got, x).numpy(), O.forward(net, x).numpy(), atol=1e-4)
+
+
+@pytest.mark.parametrize("style", ["slim", "folded"])
+def test_interpreter_runs_the_written_graph_like_the_oracle(style):
+    net = _net((2,), 8, ncls=5)
+    H, W = 57, 64
+    pb = write_deeplab_graph(net, style, H, W, B=1)
+    x = np.random.default_rng(4).integers(0, 256, (1, H, W, 3), dtype=np.uint8)
+    ref = O.forward(net, x, dtype=torch.float64).numpy()
+    lg = tf_graph.run(pb, {"ImageTensor": x}, "logits")
+    np.testing.assert_allclose(np.transpose(lg, (0, 3, 1, 2)), ref, atol=1e-4)
+    cls = tf_graph.run(pb, {"ImageTensor": x}, "SemanticPredictions")
+    want = O.predict(net, x, logits=ref.astype(np.float32))
+    up = O.resize_bilinear_tf(ref.astype(np.float32), CROP, CROP)[:, :, :H, :W]
+    s = np.sort(up, axis=1)
+    decided = (s[:, -1] - s[:, -2]) > 1e-4
+    assert cls.shape == (1, H, W)
+    assert np.array_equal(np.asarray(cls, np.int64)[decided], want[decided])
+    assert decided.mean() > 0.99
+
+
+def test_npz_round_trip(tmp_path):
+    net = _net()
+    p = tmp_path / "dl.npz"
+    got = graphdef_to_npz(write_deeplab_graph(net, "slim", 65, 65), p, crop=CROP)
+    _same_weights(got, S.load(p))
+
+
+def test_rejects_graphs_that_are_not_deeplab():
+    from graph_writer import GraphBuilder, F32
+    g = GraphBuilder()
+    x = g.node("Placeholder", [], name="ImageTensor", dtype=F32)
+    for _ in range(6):
+        x = g.node("Conv2D", [x, g.const(np.ones((1, 1, 4, 4), np.float32))], T=F32, strides=[1, 1, 1, 1],
+                   padding="SAME", data_format="NHWC")
+    with pytest.raises(GraphImportError, match="stem"):
+        import_deeplab(g.bytes())
+    net = _net()
+    net.blocks[2].dw.act = S.ACT_RELU        # wrong activation after a depthwise conv
+    with pytest.raises(GraphImportError, match="depthwise"):
+        import_deeplab(write_deeplab_graph(net, "slim", 65, 65), crop=CROP)

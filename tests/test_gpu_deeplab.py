@@ -113,3 +113,21 @@ def test_deeplab_fused_dw_bit_identical(gpu, precision):
     lb = plain.logits_device().cpu()
     assert torch.equal(la, lb)
     assert np.array_equal(a, b)
+
+
+@pytest.mark.parametrize("style", ["slim", "folded"])
+def test_deeplab_from_frozen_graphdef(gpu, tmp_path, style):
+    """DeepLabV3(GRAPH_PB_PATH=<frozen GraphDef>) (models.py:104-110): the imported network on the GPU
+    against the NumPy GraphDef interpreter's logits (the sess.run stand-in) and the oracle."""
+    from deeplab_graph_writer import write_deeplab_graph
+    from oracle import tf_graph
+    net = S.build_deeplab(width=0.25, crop=S.CROP, atrous_rates=(2, 4))
+    H, W = 120, 97
+    pb = tmp_path / "deeplab.pb"
+    pb.write_bytes(write_deeplab_graph(net, style, H, W))
+    model = DeepLabV3(str(pb), precision="fp32")
+    assert model.net.crop == S.CROP and len(model.net.atrous) == 2
+    x = _frames(1, H, W, 11)
+    _check_fp32(model, model.net, x, torch.float32)
+    lg = np.transpose(tf_graph.run(pb.read_bytes(), {"ImageTensor": x}, "logits"), (0, 3, 1, 2))
+    assert np.abs(_gpu_logits(model) - lg).max() < LOGIT_TOL
