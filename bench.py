@@ -95,6 +95,7 @@ def parse():
     p.add_argument("--width", type=int, default=640)
     p.add_argument("--precision", default="bf16", choices=["bf16", "fp32"])
     p.add_argument("--streams", type=int, default=2, help="frame shards run concurrently on this many HIP streams")
+    p.add_argument("--graph", type=int, default=0, help="1: replay the step as one captured HIP graph")
     p.add_argument("--cpu-baseline-seconds", type=float, default=12.0)
     p.add_argument("--no-cpu-baseline", action="store_true")
     return p.parse_args()
@@ -148,8 +149,13 @@ def main():
     pipe = OccupancyPipeline(model, bev, *grid, model_hw=(H, W), streams=a.streams)
     frames = torch.from_numpy(synthetic.uniform_frames(B, H, W, seed=rank)).to(dev)
 
+    run = lambda: pipe.run(frames)  # noqa: E731
+    if a.graph:
+        replay, grids = pipe.capture(frames)
+        run = lambda: (replay(), grids)[1]  # noqa: E731
+
     def step():
-        g = pipe.run(frames)
+        g = run()
         if world > 1:
             gather_grids(g, B * world)
         return g
@@ -222,7 +228,7 @@ def main():
                                    f"fused BEV warp/occgrid (1000x1000 BEV -> 200x200 cells)",
                        "global_batch": B * world, "per_gpu_batch": B, "height": H, "width": W,
                        "parallelism": f"frame-sharded dp{world}" + (" + RCCL all-gather of grids" if world > 1 else ""),
-                       "streams_per_gpu": a.streams},
+                       "streams_per_gpu": a.streams, "hip_graph": bool(a.graph)},
             "roofline": {
                 "bound": "hbm", "achieved": round(k_achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                 "frac": round(k_achieved / HBM_PEAK_GBS, 4),

@@ -83,6 +83,19 @@ class OccupancyPipeline:
             main.wait_stream(st)
         return out
 
+    def capture(self, frames_bgr: torch.Tensor, out: torch.Tensor | None = None):
+        """Record one ``run`` over these frame / output buffers as a HIP graph (every shard's launches
+        and the stream fork / join between them) and return (replay, out): ``replay()`` re-launches the
+        whole step with one call, reading whatever the frame buffer holds at that time. The buffers
+        must stay alive and keep their addresses. One eager ``run`` first sizes every arena and table
+        (allocations are not allowed while capturing)."""
+        self.run(frames_bgr, out)
+        torch.cuda.synchronize(frames_bgr.device)
+        graph = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(graph):
+            res = self.run(frames_bgr, out)
+        return graph.replay, res
+
     def _run_shard(self, ctx, frames, x, seg, out, stream):
         B, H0, W0 = frames.shape[:3]
         if (H0, W0) != (self.H, self.W):

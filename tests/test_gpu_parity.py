@@ -378,6 +378,29 @@ def test_multistream_pipeline_identical(bf16_model):
         assert torch.equal(one, many)
 
 
+@pytest.mark.parametrize("streams", [1, 2])
+def test_captured_pipeline_identical(bf16_model, streams):
+    """OccupancyPipeline.capture: the HIP-graph replay of a step equals the eager step, and re-reads
+    the frame buffer at every replay."""
+    H, W, B = 96, 128, 8
+    bev = synthetic.synthetic_bev(H, W, 300, 300)
+    a = torch.from_numpy(synthetic.road_frames(B, H, W, seed=8)).cuda()
+    b = torch.from_numpy(synthetic.road_frames(B, H, W, seed=9)).cuda()
+    eager = OccupancyPipeline(bf16_model, bev, 3.0, 3.0, 0.05, model_hw=(H, W))
+    ref_a, ref_b = eager.run(a).clone(), eager.run(b).clone()
+    pipe = OccupancyPipeline(bf16_model, bev, 3.0, 3.0, 0.05, model_hw=(H, W), streams=streams)
+    buf = a.clone()
+    replay, grids = pipe.capture(buf)
+    buf.copy_(b)
+    replay()
+    torch.cuda.synchronize()
+    assert torch.equal(grids, ref_b)
+    buf.copy_(a)
+    replay()
+    torch.cuda.synchronize()
+    assert torch.equal(grids, ref_a)
+
+
 def test_full_size_batch_properties(bf16_model):
     """Full configs[2] shape (B=32, 480x640): value sets, determinism, batch independence."""
     H, W, B = 480, 640, 32
