@@ -24,6 +24,8 @@
 #include "deeplab_internal.h"
 #include "mfma_common.h"
 
+#include <cstdlib>
+
 namespace bugseg {
 
 // XCD-aware block order: workgroup h goes to XCD h % 8 (round-robin dispatch), so neighbouring
@@ -110,7 +112,7 @@ __device__ __forceinline__ void dw8(typename Tr<T>::Raw &out, __amdgpu_buffer_rs
 // logical order XCD-aware (xcd_block).
 // NB = pixel fragments per wave (2: 128-px workgroup tiles, 4: 256 px, 8: 512 px (bf16 only); NB MFMAs per
 // weight-fragment load).
-template <typename T, bool OUTF32, bool DWF, int NB>
+template <typename T, bool OUTF32, bool DWF, int NB, int PD = 1>
 __global__ void __launch_bounds__(256) dl_conv_kernel(const DlConvArgs a) {
     constexpr int WPX = NB * 16, TPX = 4 * WPX;   // pixels per wave / per workgroup
     using Raw = typename Tr<T>::Raw;
@@ -200,10 +202,13 @@ __global__ void __launch_bounds__(256) dl_conv_kernel(const DlConvArgs a) {
                 for (int r = 0; r < 4; ++r) mma(acc[j][r], wa[r], bx[j]);
         }
     } else {
-        // k-steps (tap, 32-channel chunk) flattened; the next step's fragments are in flight while
-        // the current step's MFMAs run
+        // k-steps (tap, 32-channel chunk) flattened; the fragments of the next PD steps are in flight
+        // while the current step's MFMAs run (a ring of PD + 1 register slots, unrolled so every slot
+        // index is a compile-time constant; loads are issued in step order by one cursor)
         const int nks = a.taps * chunks;
-        auto bases = [&](int t, uint32_t (&base)[NB]) {
+        int lt = 0, lch = 0;                    // load cursor: tap, chunk
+        uint32_t base[NB];
+        auto bases = [&](int t) {
             const int ky = t / a.kw, kx = t - (t / a.kw) * a.kw;
 #pragma unroll
             for (int j = 0; j < NB; ++j) {
@@ -212,38 +217,36 @@ __global__ void __launch_bounds__(256) dl_conv_kernel(const DlConvArgs a) {
                 base[j] = ok ? (uint32_t)(((pb[j] * a.Hin + iy) * a.Win + ix) * a.CS) : OOB;
             }
         };
-        auto load = [&](int t, int ch, const uint32_t (&base)[NB], Raw (&bx)[NB], Raw (&wa)[4]) {
-            const int c = ch * 32 + kq * 8;
+        auto load = [&](Raw (&bx)[NB], Raw (&wa)[4]) {
+            const int c = lch * 32 + kq * 8;
 #pragma unroll
             for (int j = 0; j < NB; ++j) {
                 const uint32_t off = (base[j] != OOB && c < a.CS) ? (base[j] + c) * esz : OOB;
                 bld8(bx[j], rin, off);
             }
 #pragma unroll
-            for (int r = 0; r < 4; ++r) ld8(wa[r], wrow[r] + t * a.cinP + ch * 32);
-        };
-        uint32_t base[NB];
-        int t = 0, ch = 0;
-        bases(0, base);
-        Raw bx[NB], wa[4];
-        load(0, 0, base, bx, wa);
-        for (int ks = 0; ks < nks; ++ks) {
-            Raw bn[NB], wn[4];
-            if (ks + 1 < nks) {
-                if (++ch == chunks) {
-                    ch = 0;
-                    bases(++t, base);
-                }
-                load(t, ch, base, bn, wn);
+            for (int r = 0; r < 4; ++r) ld8(wa[r], wrow[r] + lt * a.cinP + lch * 32);
+            if (++lch == chunks) {
+                lch = 0;
+                if (++lt < a.taps) bases(lt);
             }
+        };
+        bases(0);
+        Raw bx[PD + 1][NB], wa[PD + 1][4];
 #pragma unroll
-            for (int j = 0; j < NB; ++j)
+        for (int u = 0; u < PD; ++u)
+            if (u < nks) load(bx[u], wa[u]);
+        for (int ks = 0; ks < nks; ks += PD + 1) {
 #pragma unroll
-                for (int r = 0; r < 4; ++r) mma(acc[j][r], wa[r], bx[j]);
+            for (int u = 0; u <= PD; ++u) {
+                if (ks + u < nks) {
+                    if (ks + u + PD < nks) load(bx[(u + PD) % (PD + 1)], wa[(u + PD) % (PD + 1)]);
 #pragma unroll
-            for (int j = 0; j < NB; ++j) bx[j] = bn[j];
+                    for (int j = 0; j < NB; ++j)
 #pragma unroll
-            for (int r = 0; r < 4; ++r) wa[r] = wn[r];
+                        for (int r = 0; r < 4; ++r) mma(acc[j][r], wa[u][r], bx[u][j]);
+                }
+            }
         }
     }
 
@@ -539,16 +542,34 @@ hipError_t dl_launch_prep(int prec, const DlPrepArgs &a, hipStream_t s) {
     return hipGetLastError();
 }
 
+// k-step prefetch depth of the bf16 conv (template PD): BUGSEG_DL_PD=1|2|3 forces one for A/B runs
+static int conv_pd(const DlConvArgs &a, int nb) {
+    static const int env = [] { const char *e = std::getenv("BUGSEG_DL_PD"); return e ? std::atoi(e) : 0; }();
+    if (env >= 1 && env <= 3) return env;
+    (void)a; (void)nb;
+    // measured (16 frames, 513x513, per-op HIP events): two steps ahead is 1.3% faster over the 38
+    // conv launches than one (1609 vs 1631 us); three is between (1620 us); no op gains more than 3%
+    return 2;
+}
+
+template <int NB, int PD>
+static void conv_bf16(bool out_f32, const DlConvArgs &a, const dim3 g, hipStream_t s) {
+    if (out_f32) hipLaunchKernelGGL((dl_conv_kernel<__bf16, true, false, NB, PD>), g, dim3(256), 0, s, a);
+    else hipLaunchKernelGGL((dl_conv_kernel<__bf16, false, false, NB, PD>), g, dim3(256), 0, s, a);
+}
+
 template <int NB>
 static void conv_nb(int prec, bool out_f32, bool dwf, const DlConvArgs &a, hipStream_t s) {
     const dim3 g(((a.M + NB * 64 - 1) / (NB * 64)) * (a.NP / 64));
-    if constexpr (NB == 8) {   // bf16, no depthwise fusion (register budget)
-        if (out_f32) hipLaunchKernelGGL((dl_conv_kernel<__bf16, true, false, 8>), g, dim3(256), 0, s, a);
-        else hipLaunchKernelGGL((dl_conv_kernel<__bf16, false, false, 8>), g, dim3(256), 0, s, a);
+    if (prec == PREC_BF16 && !dwf) {   // NB = 8: bf16 only, no depthwise fusion (register budget)
+        const int pd = a.tap_packed ? 1 : conv_pd(a, NB);
+        if (pd == 3) conv_bf16<NB, 3>(out_f32, a, g, s);
+        else if (pd == 2) conv_bf16<NB, 2>(out_f32, a, g, s);
+        else conv_bf16<NB, 1>(out_f32, a, g, s);
+    } else if constexpr (NB == 8) {
+        return;
     } else if (prec == PREC_BF16) {
-        if (dwf) hipLaunchKernelGGL((dl_conv_kernel<__bf16, false, true, NB>), g, dim3(256), 0, s, a);
-        else if (out_f32) hipLaunchKernelGGL((dl_conv_kernel<__bf16, true, false, NB>), g, dim3(256), 0, s, a);
-        else hipLaunchKernelGGL((dl_conv_kernel<__bf16, false, false, NB>), g, dim3(256), 0, s, a);
+        hipLaunchKernelGGL((dl_conv_kernel<__bf16, false, true, NB>), g, dim3(256), 0, s, a);
     } else {
         if (dwf) hipLaunchKernelGGL((dl_conv_kernel<float, false, true, NB>), g, dim3(256), 0, s, a);
         else if (out_f32) hipLaunchKernelGGL((dl_conv_kernel<float, true, false, NB>), g, dim3(256), 0, s, a);

@@ -76,7 +76,25 @@ def per_op(disp, kinds):
     return out
 
 
+def sq_table(d, B=16):
+    """Per-op SQ counter values (wave-cycle breakdown) of a --pmc pass over SQ counters in `d`."""
+    path = next(Path(d).glob("*counter_collection.csv"))
+    names = sorted({r["Counter_Name"] for r in csv.DictReader(open(path))})
+    kinds, tags = op_kinds(B)
+    cols = {}
+    for c in names:
+        f = per_op([(i, k, v / 1024.0) for i, k, v in dispatches(path, c)], kinds)
+        cols[c] = [sum(x[i] for x in f) / max(1, len(f)) for i in range(len(kinds))]
+    lines = ["| op | tag | " + " | ".join(names) + " |", "|---" * (len(names) + 2) + "|"]
+    for i, t in enumerate(tags):
+        lines.append(f"| {i} | {t} | " + " | ".join(f"{cols[c][i]:.4g}" for c in names) + " |")
+    return "\n".join(lines)
+
+
 def main(argv):
+    if argv and argv[0] == "--sq":
+        print(sq_table(argv[1]))
+        return None
     B = 16
     if "--batch" in argv:
         i = argv.index("--batch")
