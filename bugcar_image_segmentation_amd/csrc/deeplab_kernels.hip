@@ -323,11 +323,19 @@ __device__ __forceinline__ void ld8f(const float *p, float4 &a, float4 &b) {
 // Two output rows per thread: rows r1 and r1 + ph where ph = the dilation for stride 1 (their taps
 // share two of three input rows) and 1 for stride 2; each 16-B weight load (T, per tap) serves both.
 // Row slots: slot yq -> block yq / ph, phase yq % ph, r1 = block * 2ph + phase; every row exactly once.
-template <typename T>
+// The two rows' taps overlap in input rows (stride 1: rows r1 + {0,1,2} d and r1 + {1,2,3} d, two
+// shared; stride 2: 2 r1 + {0,1,2} and 2 r1 + {2,3,4}, one shared), so each distinct input row-tap is
+// loaded (and unpacked) once: 12 or 15 activation loads instead of 18. FMAs go two channels per
+// v_pk_fma_f32 (each lane an IEEE fma, so the sums equal the scalar fmaf chain bit for bit).
+typedef float f32x2_t __attribute__((ext_vector_type(2)));
+
+template <typename T, bool S1>
 __global__ void __launch_bounds__(256) dl_dw_kernel(const DlDwArgs a) {
+    constexpr int NR = S1 ? 4 : 5;          // distinct input rows of the two output rows
+    constexpr int RB = S1 ? 1 : 2;          // row index offset of the second output row's taps
     const int i = xcd_block(blockIdx.x, gridDim.x) * 256 + threadIdx.x;
     const int groups = a.C >> 3;
-    const int ph = a.stride == 1 ? a.dil : 1;
+    const int ph = S1 ? a.dil : 1;
     const int slots = (a.Hout + 2 * ph - 1) / (2 * ph) * ph;
     if (i >= a.B * slots * a.Wout * groups) return;
     const int g = i % groups, q = i / groups;
@@ -337,47 +345,46 @@ __global__ void __launch_bounds__(256) dl_dw_kernel(const DlDwArgs a) {
     if (r1 >= a.Hout) return;
     const bool v2 = r2 < a.Hout;
     const int ix0 = ox * a.stride - a.pad_l;
-    const int iy1 = r1 * a.stride - a.pad_t, iy2 = r2 * a.stride - a.pad_t;
+    const int iy1 = r1 * a.stride - a.pad_t;
+    const int rstep = S1 ? a.dil : 1;       // input-row distance between consecutive distinct rows
     const T *wt = reinterpret_cast<const T *>(a.w) + g * 8;
-    float acc1[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f}, acc2[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
-    auto fma8 = [](float (&acc)[8], float4 x0, float4 x1, float4 w0, float4 w1) {
-        acc[0] = fmaf(x0.x, w0.x, acc[0]); acc[1] = fmaf(x0.y, w0.y, acc[1]);
-        acc[2] = fmaf(x0.z, w0.z, acc[2]); acc[3] = fmaf(x0.w, w0.w, acc[3]);
-        acc[4] = fmaf(x1.x, w1.x, acc[4]); acc[5] = fmaf(x1.y, w1.y, acc[5]);
-        acc[6] = fmaf(x1.z, w1.z, acc[6]); acc[7] = fmaf(x1.w, w1.w, acc[7]);
+    f32x2_t acc1[4], acc2[4];
+#pragma unroll
+    for (int c = 0; c < 4; ++c) acc1[c] = acc2[c] = (f32x2_t){0.f, 0.f};
+    auto fma8 = [](f32x2_t (&acc)[4], float4 x0, float4 x1, float4 w0, float4 w1) {
+        acc[0] = __builtin_elementwise_fma((f32x2_t){x0.x, x0.y}, (f32x2_t){w0.x, w0.y}, acc[0]);
+        acc[1] = __builtin_elementwise_fma((f32x2_t){x0.z, x0.w}, (f32x2_t){w0.z, w0.w}, acc[1]);
+        acc[2] = __builtin_elementwise_fma((f32x2_t){x1.x, x1.y}, (f32x2_t){w1.x, w1.y}, acc[2]);
+        acc[3] = __builtin_elementwise_fma((f32x2_t){x1.z, x1.w}, (f32x2_t){w1.z, w1.w}, acc[3]);
     };
     // branch-free: a padding tap's offset is out of the descriptor's range and reads 0; adding the
     // zero product leaves the sum unchanged (+0 + -0 = +0), so this matches the skipping form bit for
-    // bit, and all 27 loads can be in flight together
+    // bit, and every load can be in flight together
     const __amdgpu_buffer_rsrc_t rin = mkbuf(a.in, a.in_bytes);
     const uint32_t cb = (uint32_t)((size_t)b * a.Hin * a.Win * a.C + g * 8);
-    uint32_t oa[9], ob[9];
+    typename Tr<T>::Raw xr[NR][3], wr[9];
 #pragma unroll
-    for (int ky = 0; ky < 3; ++ky) {
-        const int ya = iy1 + ky * a.dil, yb = iy2 + ky * a.dil;
-        const bool oka = (unsigned)ya < (unsigned)a.Hin, okb = v2 && (unsigned)yb < (unsigned)a.Hin;
+    for (int k = 0; k < NR; ++k) {
+        const int y = iy1 + k * rstep;
+        // rows only the second output row reads are skipped when it is past the edge
+        const bool oky = (k < 3 || v2) && (unsigned)y < (unsigned)a.Hin;
 #pragma unroll
         for (int kx = 0; kx < 3; ++kx) {
             const int ix = ix0 + kx * a.dil;
-            const bool okx = (unsigned)ix < (unsigned)a.Win;
-            oa[ky * 3 + kx] = oka && okx ? (cb + (uint32_t)((ya * a.Win + ix) * a.C)) * (uint32_t)sizeof(T) : OOB;
-            ob[ky * 3 + kx] = okb && okx ? (cb + (uint32_t)((yb * a.Win + ix) * a.C)) * (uint32_t)sizeof(T) : OOB;
+            const bool ok = oky && (unsigned)ix < (unsigned)a.Win;
+            bld8(xr[k][kx], rin, ok ? (cb + (uint32_t)((y * a.Win + ix) * a.C)) * (uint32_t)sizeof(T) : OOB);
         }
     }
-    typename Tr<T>::Raw xa[9], xb[9], wr[9];
+#pragma unroll
+    for (int t = 0; t < 9; ++t) ld8(wr[t], wt + t * a.C);
 #pragma unroll
     for (int t = 0; t < 9; ++t) {
-        bld8(xa[t], rin, oa[t]);
-        bld8(xb[t], rin, ob[t]);
-        ld8(wr[t], wt + t * a.C);
-    }
-#pragma unroll
-    for (int t = 0; t < 9; ++t) {
+        const int ky = t / 3, kx = t % 3;
         float4 w0, w1, x0, x1;
         raw4(wr[t], w0, w1);
-        raw4(xa[t], x0, x1);
+        raw4(xr[ky][kx], x0, x1);
         fma8(acc1, x0, x1, w0, w1);
-        raw4(xb[t], x0, x1);
+        raw4(xr[ky + RB][kx], x0, x1);
         fma8(acc2, x0, x1, w0, w1);
     }
     float4 b0, b1;
@@ -386,13 +393,13 @@ __global__ void __launch_bounds__(256) dl_dw_kernel(const DlDwArgs a) {
     T *o = reinterpret_cast<T *>(a.out) + (size_t)b * a.Hout * a.Wout * a.C + g * 8;
     {
         T *o1 = o + ((size_t)r1 * a.Wout + ox) * a.C;
-        st4(o1, make_float4(r6(acc1[0] + b0.x), r6(acc1[1] + b0.y), r6(acc1[2] + b0.z), r6(acc1[3] + b0.w)));
-        st4(o1 + 4, make_float4(r6(acc1[4] + b1.x), r6(acc1[5] + b1.y), r6(acc1[6] + b1.z), r6(acc1[7] + b1.w)));
+        st4(o1, make_float4(r6(acc1[0].x + b0.x), r6(acc1[0].y + b0.y), r6(acc1[1].x + b0.z), r6(acc1[1].y + b0.w)));
+        st4(o1 + 4, make_float4(r6(acc1[2].x + b1.x), r6(acc1[2].y + b1.y), r6(acc1[3].x + b1.z), r6(acc1[3].y + b1.w)));
     }
     if (v2) {
         T *o2 = o + ((size_t)r2 * a.Wout + ox) * a.C;
-        st4(o2, make_float4(r6(acc2[0] + b0.x), r6(acc2[1] + b0.y), r6(acc2[2] + b0.z), r6(acc2[3] + b0.w)));
-        st4(o2 + 4, make_float4(r6(acc2[4] + b1.x), r6(acc2[5] + b1.y), r6(acc2[6] + b1.z), r6(acc2[7] + b1.w)));
+        st4(o2, make_float4(r6(acc2[0].x + b0.x), r6(acc2[0].y + b0.y), r6(acc2[1].x + b0.z), r6(acc2[1].y + b0.w)));
+        st4(o2 + 4, make_float4(r6(acc2[2].x + b1.x), r6(acc2[2].y + b1.y), r6(acc2[3].x + b1.z), r6(acc2[3].y + b1.w)));
     }
 }
 
@@ -589,8 +596,14 @@ hipError_t dl_launch_dw(int prec, const DlDwArgs &a, hipStream_t s) {
     const int ph = a.stride == 1 ? a.dil : 1;
     const int n = a.B * ((a.Hout + 2 * ph - 1) / (2 * ph) * ph) * a.Wout * (a.C >> 3);
     const dim3 g((n + 255) / 256);
-    if (prec == PREC_BF16) hipLaunchKernelGGL(dl_dw_kernel<__bf16>, g, dim3(256), 0, s, a);
-    else hipLaunchKernelGGL(dl_dw_kernel<float>, g, dim3(256), 0, s, a);
+    if (a.stride != 1 && (a.stride != 2 || a.dil != 1)) return hipErrorInvalidValue;   // TF: no strided atrous
+    if (prec == PREC_BF16) {
+        if (a.stride == 1) hipLaunchKernelGGL((dl_dw_kernel<__bf16, true>), g, dim3(256), 0, s, a);
+        else hipLaunchKernelGGL((dl_dw_kernel<__bf16, false>), g, dim3(256), 0, s, a);
+    } else {
+        if (a.stride == 1) hipLaunchKernelGGL((dl_dw_kernel<float, true>), g, dim3(256), 0, s, a);
+        else hipLaunchKernelGGL((dl_dw_kernel<float, false>), g, dim3(256), 0, s, a);
+    }
     return hipGetLastError();
 }
 
