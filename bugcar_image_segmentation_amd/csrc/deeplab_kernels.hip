@@ -329,33 +329,35 @@ __device__ __forceinline__ void ld8f(const float *p, float4 &a, float4 &b) {
 // v_pk_fma_f32 (each lane an IEEE fma, so the sums equal the scalar fmaf chain bit for bit).
 typedef float f32x2_t __attribute__((ext_vector_type(2)));
 
-template <typename T, bool S1>
+template <typename T, bool S1, int R>
 __global__ void __launch_bounds__(256) dl_dw_kernel(const DlDwArgs a) {
-    constexpr int NR = S1 ? 4 : 5;          // distinct input rows of the two output rows
-    constexpr int RB = S1 ? 1 : 2;          // row index offset of the second output row's taps
+    constexpr int NR = S1 ? R + 2 : 2 * R + 1;   // distinct input rows of the R output rows
+    constexpr int RB = S1 ? 1 : 2;               // row index offset between consecutive output rows
     const int i = xcd_block(blockIdx.x, gridDim.x) * 256 + threadIdx.x;
     const int groups = a.C >> 3;
     const int ph = S1 ? a.dil : 1;
-    const int slots = (a.Hout + 2 * ph - 1) / (2 * ph) * ph;
+    const int slots = (a.Hout + R * ph - 1) / (R * ph) * ph;
     if (i >= a.B * slots * a.Wout * groups) return;
     const int g = i % groups, q = i / groups;
     const int ox = q % a.Wout, t = q / a.Wout;
     const int yq = t % slots, b = t / slots;
-    const int r1 = (yq / ph) * 2 * ph + yq % ph, r2 = r1 + ph;
+    const int r1 = (yq / ph) * R * ph + yq % ph;  // output rows r1 + j ph, j < R
     if (r1 >= a.Hout) return;
-    const bool v2 = r2 < a.Hout;
     const int ix0 = ox * a.stride - a.pad_l;
     const int iy1 = r1 * a.stride - a.pad_t;
-    const int rstep = S1 ? a.dil : 1;       // input-row distance between consecutive distinct rows
+    const int rstep = S1 ? a.dil : 1;            // input-row distance between consecutive distinct rows
+    const int rows_in = min(NR, S1 ? (a.Hout - r1 + ph - 1) / ph + 2 : 2 * ((a.Hout - r1 + ph - 1) / ph) + 1);
     const T *wt = reinterpret_cast<const T *>(a.w) + g * 8;
-    f32x2_t acc1[4], acc2[4];
+    f32x2_t acc[R][4];
 #pragma unroll
-    for (int c = 0; c < 4; ++c) acc1[c] = acc2[c] = (f32x2_t){0.f, 0.f};
-    auto fma8 = [](f32x2_t (&acc)[4], float4 x0, float4 x1, float4 w0, float4 w1) {
-        acc[0] = __builtin_elementwise_fma((f32x2_t){x0.x, x0.y}, (f32x2_t){w0.x, w0.y}, acc[0]);
-        acc[1] = __builtin_elementwise_fma((f32x2_t){x0.z, x0.w}, (f32x2_t){w0.z, w0.w}, acc[1]);
-        acc[2] = __builtin_elementwise_fma((f32x2_t){x1.x, x1.y}, (f32x2_t){w1.x, w1.y}, acc[2]);
-        acc[3] = __builtin_elementwise_fma((f32x2_t){x1.z, x1.w}, (f32x2_t){w1.z, w1.w}, acc[3]);
+    for (int j = 0; j < R; ++j)
+#pragma unroll
+        for (int c = 0; c < 4; ++c) acc[j][c] = (f32x2_t){0.f, 0.f};
+    auto fma8 = [](f32x2_t (&ac)[4], float4 x0, float4 x1, float4 w0, float4 w1) {
+        ac[0] = __builtin_elementwise_fma((f32x2_t){x0.x, x0.y}, (f32x2_t){w0.x, w0.y}, ac[0]);
+        ac[1] = __builtin_elementwise_fma((f32x2_t){x0.z, x0.w}, (f32x2_t){w0.z, w0.w}, ac[1]);
+        ac[2] = __builtin_elementwise_fma((f32x2_t){x1.x, x1.y}, (f32x2_t){w1.x, w1.y}, ac[2]);
+        ac[3] = __builtin_elementwise_fma((f32x2_t){x1.z, x1.w}, (f32x2_t){w1.z, w1.w}, ac[3]);
     };
     // branch-free: a padding tap's offset is out of the descriptor's range and reads 0; adding the
     // zero product leaves the sum unchanged (+0 + -0 = +0), so this matches the skipping form bit for
@@ -366,8 +368,8 @@ __global__ void __launch_bounds__(256) dl_dw_kernel(const DlDwArgs a) {
 #pragma unroll
     for (int k = 0; k < NR; ++k) {
         const int y = iy1 + k * rstep;
-        // rows only the second output row reads are skipped when it is past the edge
-        const bool oky = (k < 3 || v2) && (unsigned)y < (unsigned)a.Hin;
+        // rows only output rows past the bottom edge would read are skipped
+        const bool oky = k < rows_in && (unsigned)y < (unsigned)a.Hin;
 #pragma unroll
         for (int kx = 0; kx < 3; ++kx) {
             const int ix = ix0 + kx * a.dil;
@@ -382,24 +384,24 @@ __global__ void __launch_bounds__(256) dl_dw_kernel(const DlDwArgs a) {
         const int ky = t / 3, kx = t % 3;
         float4 w0, w1, x0, x1;
         raw4(wr[t], w0, w1);
-        raw4(xr[ky][kx], x0, x1);
-        fma8(acc1, x0, x1, w0, w1);
-        raw4(xr[ky + RB][kx], x0, x1);
-        fma8(acc2, x0, x1, w0, w1);
+#pragma unroll
+        for (int j = 0; j < R; ++j) {
+            raw4(xr[ky + j * RB][kx], x0, x1);
+            fma8(acc[j], x0, x1, w0, w1);
+        }
     }
     float4 b0, b1;
     ld8f(reinterpret_cast<const float *>(a.bias) + g * 8, b0, b1);
     auto r6 = [](float v) { return fminf(fmaxf(v, 0.f), 6.f); };
     T *o = reinterpret_cast<T *>(a.out) + (size_t)b * a.Hout * a.Wout * a.C + g * 8;
-    {
-        T *o1 = o + ((size_t)r1 * a.Wout + ox) * a.C;
-        st4(o1, make_float4(r6(acc1[0].x + b0.x), r6(acc1[0].y + b0.y), r6(acc1[1].x + b0.z), r6(acc1[1].y + b0.w)));
-        st4(o1 + 4, make_float4(r6(acc1[2].x + b1.x), r6(acc1[2].y + b1.y), r6(acc1[3].x + b1.z), r6(acc1[3].y + b1.w)));
-    }
-    if (v2) {
-        T *o2 = o + ((size_t)r2 * a.Wout + ox) * a.C;
-        st4(o2, make_float4(r6(acc2[0].x + b0.x), r6(acc2[0].y + b0.y), r6(acc2[1].x + b0.z), r6(acc2[1].y + b0.w)));
-        st4(o2 + 4, make_float4(r6(acc2[2].x + b1.x), r6(acc2[2].y + b1.y), r6(acc2[3].x + b1.z), r6(acc2[3].y + b1.w)));
+#pragma unroll
+    for (int j = 0; j < R; ++j) {
+        const int r = r1 + j * ph;
+        if (r < a.Hout) {
+            T *oj = o + ((size_t)r * a.Wout + ox) * a.C;
+            st4(oj, make_float4(r6(acc[j][0].x + b0.x), r6(acc[j][0].y + b0.y), r6(acc[j][1].x + b0.z), r6(acc[j][1].y + b0.w)));
+            st4(oj + 4, make_float4(r6(acc[j][2].x + b1.x), r6(acc[j][2].y + b1.y), r6(acc[j][3].x + b1.z), r6(acc[j][3].y + b1.w)));
+        }
     }
 }
 
@@ -592,19 +594,31 @@ hipError_t dl_launch_conv(int prec, bool out_f32, const DlConvArgs &a, hipStream
     return hipGetLastError();
 }
 
-hipError_t dl_launch_dw(int prec, const DlDwArgs &a, hipStream_t s) {
+template <int R>
+static hipError_t launch_dw_r(int prec, const DlDwArgs &a, hipStream_t s) {
     const int ph = a.stride == 1 ? a.dil : 1;
-    const int n = a.B * ((a.Hout + 2 * ph - 1) / (2 * ph) * ph) * a.Wout * (a.C >> 3);
+    const int n = a.B * ((a.Hout + R * ph - 1) / (R * ph) * ph) * a.Wout * (a.C >> 3);
     const dim3 g((n + 255) / 256);
-    if (a.stride != 1 && (a.stride != 2 || a.dil != 1)) return hipErrorInvalidValue;   // TF: no strided atrous
     if (prec == PREC_BF16) {
-        if (a.stride == 1) hipLaunchKernelGGL((dl_dw_kernel<__bf16, true>), g, dim3(256), 0, s, a);
-        else hipLaunchKernelGGL((dl_dw_kernel<__bf16, false>), g, dim3(256), 0, s, a);
+        if (a.stride == 1) hipLaunchKernelGGL((dl_dw_kernel<__bf16, true, R>), g, dim3(256), 0, s, a);
+        else hipLaunchKernelGGL((dl_dw_kernel<__bf16, false, R>), g, dim3(256), 0, s, a);
     } else {
-        if (a.stride == 1) hipLaunchKernelGGL((dl_dw_kernel<float, true>), g, dim3(256), 0, s, a);
-        else hipLaunchKernelGGL((dl_dw_kernel<float, false>), g, dim3(256), 0, s, a);
+        if (a.stride == 1) hipLaunchKernelGGL((dl_dw_kernel<float, true, R>), g, dim3(256), 0, s, a);
+        else hipLaunchKernelGGL((dl_dw_kernel<float, false, R>), g, dim3(256), 0, s, a);
     }
     return hipGetLastError();
+}
+
+// Output rows per thread (R). Measured (16 frames, 513x513, per-op HIP events, 17 launches): stride-1
+// layers R = 2 / 4 / 8: 680 / 576 / 534 us in total, R = 8 fastest in every layer (246 VGPRs, two waves
+// per SIMD); stride 2 keeps R = 2 (R = 4 / 8 within 1%). BUGSEG_DL_DWR=2|4|8 forces R for stride 1.
+hipError_t dl_launch_dw(int prec, const DlDwArgs &a, hipStream_t s) {
+    if (a.stride != 1 && (a.stride != 2 || a.dil != 1)) return hipErrorInvalidValue;   // TF: no strided atrous
+    static const int env = [] { const char *e = std::getenv("BUGSEG_DL_DWR"); return e ? std::atoi(e) : 0; }();
+    if (a.stride == 2) return launch_dw_r<2>(prec, a, s);
+    if (env == 2) return launch_dw_r<2>(prec, a, s);
+    if (env == 4) return launch_dw_r<4>(prec, a, s);
+    return launch_dw_r<8>(prec, a, s);
 }
 
 hipError_t dl_launch_pool(int prec, const DlPoolArgs &a, hipStream_t s) {
