@@ -406,21 +406,41 @@ __global__ void __launch_bounds__(256) dl_dw_kernel(const DlDwArgs a) {
 }
 
 // ------------------------------------------------------------------ image pooling
-// Partial channel sums over a fixed pixel chunk per workgroup: part[b][chunk][c] (f32).
+// Partial channel sums over a fixed pixel chunk per workgroup: part[b][chunk][c] (f32). Thread =
+// 8 channels (one 16-B load per pixel) x one of `lanes` pixel lanes striding the chunk; the lanes'
+// sums are added in lane order through LDS (deterministic, no atomics). Needs C % 8 == 0, C <= 2048.
 template <typename T>
 __global__ void __launch_bounds__(256) dl_gap_kernel(const DlPoolArgs a) {
+    __shared__ float red[256 * 8];
     const int b = blockIdx.y, chunk = blockIdx.x;
     const int HW = a.H * a.W;
     const int p0 = chunk * a.chunk_px, p1 = min(HW, p0 + a.chunk_px);
-    const T *x = reinterpret_cast<const T *>(a.x) + (size_t)b * HW * a.CS;
+    const int groups = a.C >> 3, lanes = 256 / groups;
+    const int g = threadIdx.x % groups, l = threadIdx.x / groups;
+    if (l < lanes) {
+        const T *x = reinterpret_cast<const T *>(a.x) + (size_t)b * HW * a.CS + g * 8;
+        float s[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+#pragma unroll 4
+        for (int p = p0 + l; p < p1; p += lanes) {
+            typename Tr<T>::Raw r;
+            ld8(r, x + (size_t)p * a.CS);
+            float4 u, v;
+            raw4(r, u, v);
+            s[0] += u.x; s[1] += u.y; s[2] += u.z; s[3] += u.w;
+            s[4] += v.x; s[5] += v.y; s[6] += v.z; s[7] += v.w;
+        }
+#pragma unroll
+        for (int c = 0; c < 8; ++c) red[(l * groups + g) * 8 + c] = s[c];
+    }
+    __syncthreads();
     for (int c = threadIdx.x; c < a.C; c += 256) {
-        float s = 0.f;
-        for (int p = p0; p < p1; ++p) s += ld1(x + (size_t)p * a.CS + c);
-        a.part[((size_t)b * a.nchunks + chunk) * a.C + c] = s;
+        float acc = 0.f;
+        for (int k = 0; k < lanes; ++k) acc += red[(k * groups + (c >> 3)) * 8 + (c & 7)];
+        a.part[((size_t)b * a.nchunks + chunk) * a.C + c] = acc;
     }
 }
 
-// Mean per (image, channel): partials summed in chunk order, rounded to T as a stored tensor would
+// Mean per (image, channel): partials summed in a fixed order, rounded to T as a stored tensor would
 // be; written over chunk 0 of the partials (each thread reads its own channel's column first).
 template <typename T>
 __global__ void __launch_bounds__(256) dl_pool_mean_kernel(const DlPoolArgs a) {
@@ -428,8 +448,19 @@ __global__ void __launch_bounds__(256) dl_pool_mean_kernel(const DlPoolArgs a) {
     if (i >= a.B * a.C) return;
     const int b = i / a.C, c = i - b * a.C;
     const float inv = 1.0f / (float)(a.H * a.W);
+    // eight interleaved partial sums (chunk k into lane k % 8), then added in lane order: eight loads
+    // in flight instead of a chain of nchunks dependent ones (18 -> 5.5 us at 67 chunks x 16 x 320)
+    float q[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+    const float *pp = a.part + (size_t)b * a.nchunks * a.C + c;
+    int k = 0;
+    for (; k + 8 <= a.nchunks; k += 8) {
+#pragma unroll
+        for (int u = 0; u < 8; ++u) q[u] += pp[(size_t)(k + u) * a.C];
+    }
+    for (int u = 0; k < a.nchunks; ++k, ++u) q[u] += pp[(size_t)k * a.C];
     float s = 0.f;
-    for (int k = 0; k < a.nchunks; ++k) s += a.part[((size_t)b * a.nchunks + k) * a.C + c];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) s += q[u];
     a.part[(size_t)b * a.nchunks * a.C + c] = (float)(T)(s * inv);
 }
 
@@ -622,6 +653,7 @@ hipError_t dl_launch_dw(int prec, const DlDwArgs &a, hipStream_t s) {
 }
 
 hipError_t dl_launch_pool(int prec, const DlPoolArgs &a, hipStream_t s) {
+    if ((a.C & 7) || a.C > 2048) return hipErrorInvalidValue;
     const dim3 g1(a.nchunks, a.B);
     if (prec == PREC_BF16) {
         hipLaunchKernelGGL(dl_gap_kernel<__bf16>, g1, dim3(256), 0, s, a);
