@@ -490,53 +490,86 @@ __global__ void __launch_bounds__(256) dl_pool_gemv_kernel(const DlPoolArgs a) {
 // in f32; top = floor(in), bottom = min(top + 1, in_size - 1), lerp = in - top;
 // value = top_row + (bottom_row - top_row) * y_lerp with row = left + (right - left) * x_lerp.
 // Then argmax over classes (first maximum).
-// One thread = AM_PX consecutive output pixels of a row; the 4 corner logit vectors are (re)loaded
-// only when x0 changes along the run (with the 65 -> 513 scale of 1/8, once per 8 pixels).
-constexpr int AM_PX = 8, AM_C = 24;   // classes held in registers (LCS <= AM_C uses this kernel)
+constexpr int AM_PX = 8, AM_PY = 1, AM_C = 24;   // classes held in registers (LCS <= AM_C uses this kernel)
+// One thread = AM_PX consecutive output pixels in each of AM_PY consecutive rows; the 4 corner logit
+// vectors are reloaded only when the corner cell (x0, y0) changes (at the 65 -> 513 scale of 1/8, once
+// per 8 pixels of a row). Class ids of a run go out as 16-B stores (two int64) where the address
+// allows (46 -> 44 us). Measured: AM_PY = 4 (corner loads shared by 4 rows) 66 us — fewer threads
+// cost more than the L2 corner reads they save.
 __global__ void __launch_bounds__(256) dl_resize_argmax_kernel(const DlArgmaxArgs a) {
 #pragma clang fp contract(off)
-    const int qx = (a.Wo + AM_PX - 1) / AM_PX;
+    const int qx = (a.Wo + AM_PX - 1) / AM_PX, qy = (a.Ho + AM_PY - 1) / AM_PY;
     const int i = blockIdx.x * 256 + threadIdx.x;
-    if (i >= a.B * a.Ho * qx) return;
-    const int xq = i % qx, t = i / qx, y = t % a.Ho, b = t / a.Ho;
-    const float in_y = (float)y * a.sy;
-    const int y0 = (int)floorf(in_y), y1 = min(y0 + 1, a.h - 1);
-    const float ly = in_y - (float)y0;
+    if (i >= a.B * qy * qx) return;
+    const int xq = i % qx, t = i / qx, yq = t % qy, b = t / qy;
     const float *base = a.logits + (size_t)b * a.h * a.w * a.LCS;
-    const float *row0 = base + (size_t)y0 * a.w * a.LCS, *row1 = base + (size_t)y1 * a.w * a.LCS;
     float tl[AM_C], tr[AM_C], bl[AM_C], br[AM_C];
-    int cur = -1;
-    int64_t *orow = a.out + ((size_t)b * a.Hout + y) * a.Wout;
-    for (int j = 0; j < AM_PX; ++j) {
-        const int x = xq * AM_PX + j;
-        if (x >= a.Wo) break;
-        const float in_x = (float)x * a.sx;
-        const int x0 = (int)floorf(in_x), x1 = min(x0 + 1, a.w - 1);
-        const float lx = in_x - (float)x0;
-        if (x0 != cur) {
-            cur = x0;
+    int curx = -1, cury = -1;
+    const int xb = xq * AM_PX, nx = min(AM_PX, a.Wo - xb);
+    for (int r = 0; r < AM_PY; ++r) {
+        const int y = yq * AM_PY + r;
+        if (y >= a.Ho) break;
+        const float in_y = (float)y * a.sy;
+        const int y0 = (int)floorf(in_y), y1 = min(y0 + 1, a.h - 1);
+        const float ly = in_y - (float)y0;
+        const float *row0 = base + (size_t)y0 * a.w * a.LCS, *row1 = base + (size_t)y1 * a.w * a.LCS;
+        uint32_t packed[2] = {0u, 0u};      // the run's class ids, one byte each (ncls <= AM_C < 256)
+        for (int j = 0; j < nx; ++j) {
+            const int x = xb + j;
+            const float in_x = (float)x * a.sx;
+            const int x0 = (int)floorf(in_x), x1 = min(x0 + 1, a.w - 1);
+            const float lx = in_x - (float)x0;
+            if (x0 != curx || y0 != cury) {
+                curx = x0;
+                cury = y0;
 #pragma unroll
-            for (int c0 = 0; c0 < AM_C; c0 += 4) {
-                if (c0 >= a.LCS) break;
-                const float4 q0 = ld4f(row0 + x0 * a.LCS + c0), q1 = ld4f(row0 + x1 * a.LCS + c0);
-                const float4 q2 = ld4f(row1 + x0 * a.LCS + c0), q3 = ld4f(row1 + x1 * a.LCS + c0);
-                tl[c0] = q0.x; tl[c0 + 1] = q0.y; tl[c0 + 2] = q0.z; tl[c0 + 3] = q0.w;
-                tr[c0] = q1.x; tr[c0 + 1] = q1.y; tr[c0 + 2] = q1.z; tr[c0 + 3] = q1.w;
-                bl[c0] = q2.x; bl[c0 + 1] = q2.y; bl[c0 + 2] = q2.z; bl[c0 + 3] = q2.w;
-                br[c0] = q3.x; br[c0 + 1] = q3.y; br[c0 + 2] = q3.z; br[c0 + 3] = q3.w;
+                for (int c0 = 0; c0 < AM_C; c0 += 4) {
+                    if (c0 >= a.LCS) break;
+                    const float4 q0 = ld4f(row0 + x0 * a.LCS + c0), q1 = ld4f(row0 + x1 * a.LCS + c0);
+                    const float4 q2 = ld4f(row1 + x0 * a.LCS + c0), q3 = ld4f(row1 + x1 * a.LCS + c0);
+                    tl[c0] = q0.x; tl[c0 + 1] = q0.y; tl[c0 + 2] = q0.z; tl[c0 + 3] = q0.w;
+                    tr[c0] = q1.x; tr[c0 + 1] = q1.y; tr[c0 + 2] = q1.z; tr[c0 + 3] = q1.w;
+                    bl[c0] = q2.x; bl[c0 + 1] = q2.y; bl[c0 + 2] = q2.z; bl[c0 + 3] = q2.w;
+                    br[c0] = q3.x; br[c0 + 1] = q3.y; br[c0 + 2] = q3.z; br[c0 + 3] = q3.w;
+                }
             }
-        }
-        float best = 0.f;
-        int bi = 0;
+            float best = 0.f;
+            int bi = 0;
 #pragma unroll
-        for (int c = 0; c < AM_C; ++c) {
-            if (c >= a.ncls) break;
-            const float top = tl[c] + (tr[c] - tl[c]) * lx;
-            const float bot = bl[c] + (br[c] - bl[c]) * lx;
-            const float v = top + (bot - top) * ly;
-            if (c == 0 || v > best) { best = v; bi = c; }
+            for (int c = 0; c < AM_C; ++c) {
+                if (c >= a.ncls) break;
+                const float top = tl[c] + (tr[c] - tl[c]) * lx;
+                const float bot = bl[c] + (br[c] - bl[c]) * lx;
+                const float v = top + (bot - top) * ly;
+                if (c == 0 || v > best) { best = v; bi = c; }
+            }
+            if (j < 4) packed[0] |= (uint32_t)bi << (8 * j);
+            else packed[1] |= (uint32_t)bi << (8 * (j - 4));
         }
-        orow[x] = (int64_t)bi;
+        int res[AM_PX];
+#pragma unroll
+        for (int j = 0; j < AM_PX; ++j) res[j] = (int)((packed[j >> 2] >> (8 * (j & 3))) & 0xffu);
+        // rows of odd width start 8-B aligned: a misaligned run writes its first and last pixel alone
+        // and the six between in pairs
+        int64_t *o = a.out + ((size_t)b * a.Hout + y) * a.Wout + xb;
+        auto st2 = [](int64_t *p, int u, int v) {
+            *reinterpret_cast<longlong2 *>(p) = make_longlong2((long long)u, (long long)v);
+        };
+        if (nx == AM_PX) {
+            if ((reinterpret_cast<uintptr_t>(o) & 15) == 0) {
+#pragma unroll
+                for (int j = 0; j < AM_PX; j += 2) st2(o + j, res[j], res[j + 1]);
+            } else {
+                o[0] = res[0];
+#pragma unroll
+                for (int j = 1; j < AM_PX - 1; j += 2) st2(o + j, res[j], res[j + 1]);
+                o[AM_PX - 1] = res[AM_PX - 1];
+            }
+        } else {
+#pragma unroll
+            for (int j = 0; j < AM_PX; ++j)
+                if (j < nx) o[j] = res[j];
+        }
     }
 }
 
@@ -675,7 +708,7 @@ hipError_t dl_launch_argmax(const DlArgmaxArgs &a, hipStream_t s) {
         hipLaunchKernelGGL(dl_resize_argmax_generic, dim3((n + 255) / 256), dim3(256), 0, s, a);
         return hipGetLastError();
     }
-    const int n = a.B * a.Ho * ((a.Wo + AM_PX - 1) / AM_PX);
+    const int n = a.B * ((a.Ho + AM_PY - 1) / AM_PY) * ((a.Wo + AM_PX - 1) / AM_PX);
     hipLaunchKernelGGL(dl_resize_argmax_kernel, dim3((n + 255) / 256), dim3(256), 0, s, a);
     return hipGetLastError();
 }
