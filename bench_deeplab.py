@@ -10,8 +10,10 @@ frames shard across ranks with no collective (weak scaling).
 with HIP events on the stream the kernels run on (bugseg_dl_launch_op): achieved = the launch's
 algorithmic bytes (input read once, output written once, residual read, weights once;
 deeplab_spec.lower) / its average duration, against 8 TB/s; `forward` adds whole-forward bytes,
-flops and the MFMA fraction. The CPU baseline is the oracle (PyTorch-CPU fp32, TF semantics) on a
-bounded sample.
+flops and the MFMA fraction; `traffic` is the PMC-measured HBM bytes per launch of that op tag from
+the committed profile (profiles/dl_pmc_traffic.json, scripts/dl_pmc_summary.py), when it was taken
+at the same batch. The CPU baseline is the oracle (PyTorch-CPU fp32, TF semantics) on a bounded
+sample.
 """
 from __future__ import annotations
 
