@@ -494,8 +494,8 @@ constexpr int AM_PX = 8, AM_PY = 1, AM_C = 24;   // classes held in registers (L
 // One thread = AM_PX consecutive output pixels in each of AM_PY consecutive rows; the 4 corner logit
 // vectors are reloaded only when the corner cell (x0, y0) changes (at the 65 -> 513 scale of 1/8, once
 // per 8 pixels of a row). Class ids of a run go out as 16-B stores (two int64) where the address
-// allows (46 -> 44 us). Measured: AM_PY = 4 (corner loads shared by 4 rows) 66 us — fewer threads
-// cost more than the L2 corner reads they save.
+// allows (46 -> 44 us). Measured at B = 64: AM_PY = 2 167 us, AM_PY = 4 (B = 16) 66 vs 44 us, AM_PX = 4
+// 149 vs 148 us — fewer threads cost more than the L2 corner reads they save.
 __global__ void __launch_bounds__(256) dl_resize_argmax_kernel(const DlArgmaxArgs a) {
 #pragma clang fp contract(off)
     const int qx = (a.Wo + AM_PX - 1) / AM_PX, qy = (a.Ho + AM_PY - 1) / AM_PY;
