@@ -38,6 +38,10 @@ struct DlConvArgs {
     int dw_stride, dw_dil, dw_pt, dw_pl;
     int nb;              // pixel fragments per wave: 2 (128-px workgroup tile), 4 (256 px) or 8 (bf16, 512 px)
     int tap_packed;      // CS == 8: w is [NP][ceil(taps / 4) * 32], k = tap * 8 + c
+    // tap-packed only: when rgb != nullptr the input is the raw (B, img_h, img_w, 3) u8 RGB batch and
+    // the (B, Hin, Win, 8) operand is formed on load (dl_prep_kernel's padding and normalisation)
+    const uint8_t *rgb;
+    int img_h, img_w;
 };
 
 struct DlDwArgs {

@@ -64,6 +64,23 @@ __global__ void __launch_bounds__(256) dl_prep_kernel(const DlPrepArgs a) {
     }
 }
 
+// The engine input at crop pixel (iy, ix) of image b, formed from the raw RGB bytes exactly as
+// dl_prep_kernel stores it (inside the image: f32(2/255) x - 1; padding: the mean pixel 127.5
+// normalised), for the stem's fused-preprocessing operand loads. Caller: (iy, ix) inside the crop.
+template <typename T>
+__device__ __forceinline__ void prep_px(typename Tr<T>::Raw &r, const uint8_t *rgb, int b, int H, int W, int iy, int ix) {
+#pragma clang fp contract(off)
+    const float scale = 2.0f / 255.0f;
+    float v[3];
+    if (iy < H && ix < W) {
+        const uint8_t *p = rgb + ((size_t)(b * H + iy) * W + ix) * 3;
+        for (int c = 0; c < 3; ++c) v[c] = scale * (float)p[c] - 1.0f;
+    } else {
+        for (int c = 0; c < 3; ++c) v[c] = scale * 127.5f - 1.0f;
+    }
+    set3(r, v[0], v[1], v[2]);
+}
+
 // ------------------------------------------------------------------ dense conv (implicit GEMM)
 // Workgroup = 4 waves = 128 pixels x 64 output channels; a wave owns 32 pixels (2 B fragments)
 // x 64 channels (4 A fragments): 8 MFMAs per k-step of 32 (one tap, 32 input channels).
@@ -192,7 +209,12 @@ __global__ void __launch_bounds__(256) dl_conv_kernel(const DlConvArgs a) {
             for (int j = 0; j < NB; ++j) {
                 const int iy = piy[j] + ky * a.dil, ix = pix[j] + kx * a.dil;
                 const bool ok = t < a.taps && pv[j] && (unsigned)iy < (unsigned)a.Hin && (unsigned)ix < (unsigned)a.Win;
-                bld8(bx[j], rin, ok ? (uint32_t)(((pb[j] * a.Hin + iy) * a.Win + ix) * a.CS) * esz : OOB);
+                if (a.rgb) {
+                    if (ok) prep_px<T>(bx[j], a.rgb, pb[j], a.img_h, a.img_w, iy, ix);
+                    else zero(bx[j]);
+                } else {
+                    bld8(bx[j], rin, ok ? (uint32_t)(((pb[j] * a.Hin + iy) * a.Win + ix) * a.CS) * esz : OOB);
+                }
             }
 #pragma unroll
             for (int r = 0; r < 4; ++r) ld8(wa[r], wrow[r] + ks * 32);

@@ -170,7 +170,8 @@ hipError_t run_op(bugseg_dl *c, const DlOp &o, const uint8_t *rgb, int H, int W,
         a.bias_img_stride = f[26];
         a.in_bytes = (uint32_t)((size_t)B * a.Hin * a.Win * a.CS * (c->prec == PREC_BF16 ? 2 : 4));
         a.nb = f[30] == 8 ? 8 : f[30] == 4 ? 4 : 2;
-        a.tap_packed = f[31];
+        a.tap_packed = f[31] != 0;
+        if (f[31] == 2) { a.rgb = rgb; a.img_h = H; a.img_w = W; }   // stem with the preprocessing fused
         if (f[27] >= 0) {
             a.dw_w = wb + f[27];
             a.dw_b = reinterpret_cast<const float *>(wb + f[28]);

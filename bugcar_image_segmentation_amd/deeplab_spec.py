@@ -255,7 +255,7 @@ def _pick_nb(tag: str, hw: int, K: int, cout: int) -> int:
     return 4 if K >= 192 and cout >= 64 else 2
 
 
-def lower(net: DeepLab, B: int, bf16: bool, fuse_dw: bool = False, nb=None):
+def lower(net: DeepLab, B: int, bf16: bool, fuse_dw: bool = False, nb=None, fuse_prep: bool = True):
     """-> (weight blob bytes, ops int32 (nops, OP_FIELDS), buffer bytes uint64 (nbufs,), info dict).
     Buffers: 0 input, 1/2 block ping-pong, 3 expanded, 4 depthwise out, 5 ASPP concat, 6 projection,
     7 logits (f32), 8 pooling partials (f32), 9 per-image projection bias (f32), 10 image-pooling
@@ -286,10 +286,13 @@ def lower(net: DeepLab, B: int, bf16: bool, fuse_dw: bool = False, nb=None):
 
     Hc = Wc = net.crop
     use(0, B * Hc * Wc * 8 * es)
-    op([OP_PREP, 0], "prep", 0, B * Hc * Wc * (3 + 8 * es))
+    if not fuse_prep:
+        op([OP_PREP, 0], "prep", 0, B * Hc * Wc * (3 + 8 * es))
 
     def conv(c: Conv, src, H, W, CS, dst, out_cs, out_off=0, res=-1, out_f32=False, bias_img=-1, bias_img_stride=0,
-             zero_bias=False, cout=None, tag="conv", dwf=None):
+             zero_bias=False, cout=None, tag="conv", dwf=None, rgb=False):
+        """rgb: the input is the raw u8 RGB frame batch, padded and normalised on load (the stem with
+        fuse_prep; tap field 2)."""
         k = c.k
         Ho, pt = same_pad(H, k, c.stride, c.dil)
         Wo, pl = same_pad(W, k, c.stride, c.dil)
@@ -313,16 +316,20 @@ def lower(net: DeepLab, B: int, bf16: bool, fuse_dw: bool = False, nb=None):
         use(dst, B * Ho * Wo * out_cs * oes)
         cin = c.w.shape[1]
         flops = 2.0 * B * Ho * Wo * c.cout * cin * k * k + (2.0 * B * Ho * Wo * CS * 9 if dwf else 0)
-        nbytes = B * Hin * Win * CS * es + B * Ho * Wo * cw * oes + (B * Ho * Wo * cw * es if res >= 0 else 0) + wp.size * es
+        nbytes = (B * Hin * Win * 3 if rgb else B * Hin * Win * CS * es) + B * Ho * Wo * cw * oes + \
+            (B * Ho * Wo * cw * es if res >= 0 else 0) + wp.size * es
         t = tag if dwf is None else "conv dw+project"
         f30 = nb(t, Ho * Wo, cinP * k * k, cw) if callable(nb) else (nb or _pick_nb(t, Ho * Wo, cinP * k * k, cw))
         op([OP_CONV, src, dst, res, Hin, Win, CS, Ho, Wo, k, k, c.stride, c.dil, pt, pl, cinP, NP, w_off, b_off, c.act,
-            out_cs if res >= 0 else 0, out_cs, out_off, cw, int(out_f32), bias_img, bias_img_stride] + extra + [f30, int(tp)],
+            out_cs if res >= 0 else 0, out_cs, out_off, cw, int(out_f32), bias_img, bias_img_stride] + extra +
+           [f30, 2 if (rgb and tp) else int(tp)],
            tag if dwf is None else "conv dw+project", flops, nbytes)
         return Ho, Wo
 
     # stem
-    H, W = conv(net.stem, 0, Hc, Wc, 8, 1, _r8(net.stem.cout), tag="conv stem")
+    H, W = conv(net.stem, 0, Hc, Wc, 8, 1, _r8(net.stem.cout), tag="conv stem", rgb=fuse_prep)
+    if fuse_prep and int(ops[-1][31]) != 2:
+        raise ValueError("fuse_prep needs the tap-packed stem (3x3 over the 8-channel input)")
     C = net.stem.cout
     cur = 1
     for bi, blk in enumerate(net.blocks):

@@ -195,9 +195,10 @@ class DeepLabV3(InferenceModel):
     CROP_SIZE = 513
 
     def __init__(self, GRAPH_PB_PATH=None, *, net=None, precision: str = "bf16", device: int | None = None,
-                 fuse_dw: bool | None = None):
+                 fuse_dw: bool | None = None, fuse_prep: bool = True):
         """fuse_dw=True computes each depthwise conv inside its projection's operand loads
-        (bit-identical, measured slower; deeplab_spec.lower)."""
+        (bit-identical, measured slower; deeplab_spec.lower). fuse_prep=False runs the padding +
+        normalisation as its own launch instead of inside the stem's operand loads (bit-identical)."""
         from . import deeplab_spec
         if precision not in ("fp32", "bf16"):
             raise ValueError("precision must be 'fp32' or 'bf16'")
@@ -224,11 +225,13 @@ class DeepLabV3(InferenceModel):
         self._plan_B = None
         self.plan_info = None
         self.fuse_dw = bool(int(os.environ.get("BUGSEG_DL_FUSE_DW", "0"))) if fuse_dw is None else fuse_dw
+        self.fuse_prep = fuse_prep
 
     def _ensure_plan(self, B: int) -> None:
         if self._plan_B == B:
             return
-        blob, ops, bufs, info = self._spec.lower(self.net, B, self.precision == "bf16", fuse_dw=self.fuse_dw)
+        blob, ops, bufs, info = self._spec.lower(self.net, B, self.precision == "bf16", fuse_dw=self.fuse_dw,
+                                                 fuse_prep=self.fuse_prep)
         if self._blob is None:
             self.ctx.load_weights(blob)
             self._blob = blob

@@ -2,7 +2,7 @@
 
 Several ops share one kernel template (the 1x1 expansions, projections and ASPP convs are all
 dl_conv_kernel), so the counters are attributed per op, not per kernel name: the dispatches of
-each full forward (the 57-op plan, starting at its dl_prep_kernel) are walked in plan order, conv /
+each full forward (wherever the plan's whole kernel sequence matches) are walked in plan order, conv /
 dw / argmax ops take one dispatch each, the pooling op takes the gap / mean / GEMV dispatches that
 follow it. Only complete forwards (warmup + timed steps) are used; the per-op timing loop after
 them repeats single ops and is skipped.
@@ -49,7 +49,7 @@ def op_kinds(B):
 def per_op(disp, kinds):
     """Per-op byte totals of every complete forward in `disp`."""
     from bugcar_image_segmentation_amd import deeplab_spec as D
-    starts = [i for i, (_, k, _) in enumerate(disp) if "dl_prep_kernel" in k]
+    starts = range(len(disp))          # a forward starts wherever the whole plan's kernel sequence matches
     out = []
     for s in starts:
         j, vals, ok = s, [], True
@@ -60,10 +60,13 @@ def per_op(disp, kinds):
             name = disp[j][1]
             want = {D.OP_PREP: "dl_prep", D.OP_CONV: "dl_conv", D.OP_DW: "dl_dw", D.OP_ARGMAX: "argmax"}.get(kind)
             if kind == D.OP_POOL:
-                v = 0.0
+                v, j0 = 0.0, j
                 while j < len(disp) and ("gap" in disp[j][1] or "pool" in disp[j][1]):
                     v += disp[j][2]
                     j += 1
+                if j == j0:
+                    ok = False
+                    break
                 vals.append(v)
                 continue
             if want not in name:

@@ -35,7 +35,10 @@ def test_lowering_is_consistent():
     blob, ops, bufs, info = S.lower(net, 2, bf16=True)
     assert ops.shape == (info["nops"], S.OP_FIELDS) and ops.dtype == np.int32
     kinds = list(ops[:, 0])
-    assert kinds[0] == S.OP_PREP and kinds[-1] == S.OP_ARGMAX and kinds.count(S.OP_POOL) == 1
+    assert kinds[0] == S.OP_CONV and kinds[-1] == S.OP_ARGMAX and kinds.count(S.OP_POOL) == 1
+    assert ops[0, 31] == 2 and S.OP_PREP not in kinds          # preprocessing fused into the stem's loads
+    _, ops_p, _, info_p = S.lower(net, 2, bf16=True, fuse_prep=False)
+    assert ops_p[0, 0] == S.OP_PREP and ops_p[1, 31] == 1 and info_p["nops"] == info["nops"] + 1
     assert kinds.count(S.OP_DW) == 17
     _, ops_f, _, info_f = S.lower(net, 2, bf16=True, fuse_dw=True)
     assert list(ops_f[:, 0]).count(S.OP_DW) == 0 and info["nops"] == info_f["nops"] + 17

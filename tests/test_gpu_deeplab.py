@@ -115,6 +115,24 @@ def test_deeplab_fused_dw_bit_identical(gpu, precision):
     assert np.array_equal(a, b)
 
 
+@pytest.mark.parametrize("precision", ["fp32", "bf16"])
+def test_deeplab_fused_prep_bit_identical(gpu, precision):
+    """The stem forming its operand from the raw RGB bytes (default) against the separate
+    dl_prep_kernel launch: the same padded, normalised values, so identical logits and classes;
+    images smaller than the crop in both dimensions exercise the mean-pixel padding."""
+    net = S.build_deeplab(width=0.5, crop=129, atrous_rates=(6,))
+    for B, H, W in ((2, 129, 129), (3, 100, 77)):
+        x = _frames(B, H, W, 31 + H)
+        fused = DeepLabV3(net=net, precision=precision)
+        plain = DeepLabV3(net=net, precision=precision, fuse_prep=False)
+        a = fused.predict(x)
+        la = fused.logits_device().cpu()
+        b = plain.predict(x)
+        lb = plain.logits_device().cpu()
+        assert torch.equal(la, lb)
+        assert np.array_equal(a, b)
+
+
 @pytest.mark.parametrize("style", ["slim", "folded"])
 def test_deeplab_from_frozen_graphdef(gpu, tmp_path, style):
     """DeepLabV3(GRAPH_PB_PATH=<frozen GraphDef>) (models.py:104-110): the imported network on the GPU
