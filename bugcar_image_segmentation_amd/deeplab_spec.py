@@ -243,13 +243,20 @@ def pack_conv(c: Conv, cinS: int, bf16: bool, tap_packed: bool = False):
     return _round(p, bf16), bb.astype(np.float32), cinP, NP
 
 
-def _pick_nb(tag: str, hw: int, K: int, cout: int) -> int:
+def _pick_nb(tag: str, hw: int, K: int, cout: int, B: int = 16) -> int:
     """Measured on MI355X (bench_deeplab.py per-op times, 16 frames): 4 pixel fragments per wave pay
     for wide, deep 1x1s (960 -> 320: 219 -> 169 us, 576 -> 160: 87 -> 72 us); 2 win for shallow K
     (expansions, 24 -> 144: 30 -> 34 us with 4). BUGSEG_DL_NB=2|4 forces one for A/B runs."""
     env = os.environ.get("BUGSEG_DL_NB")
     if env:
         return int(env)
+    if hw <= 4225 and B * hw >= 131072:
+        # the output-stride-8 layers at B >= 32 (per-op sweep at B = 64, all 31 convs at 65x65): 4 fragments
+        # win from K = 64 / cout = 64 up (960 -> 160: 434 -> 408 us, 160 -> 960: 367 -> 331 us), 8 only
+        # for 960 -> 320 (603 -> 548 us); 2 stays best for the 32-channel blocks
+        if K >= 576 and cout >= 320:
+            return 8
+        return 4 if (K >= 64 and cout >= 64) or K >= 256 else 2
     if K >= 576 and cout >= 160:
         return 8    # bf16 only (the launcher uses 4 in fp32): 960 -> 320 165 -> 149 us, elsewhere slower
     return 4 if K >= 192 and cout >= 64 else 2
@@ -319,7 +326,7 @@ def lower(net: DeepLab, B: int, bf16: bool, fuse_dw: bool = False, nb=None, fuse
         nbytes = (B * Hin * Win * 3 if rgb else B * Hin * Win * CS * es) + B * Ho * Wo * cw * oes + \
             (B * Ho * Wo * cw * es if res >= 0 else 0) + wp.size * es
         t = tag if dwf is None else "conv dw+project"
-        f30 = nb(t, Ho * Wo, cinP * k * k, cw) if callable(nb) else (nb or _pick_nb(t, Ho * Wo, cinP * k * k, cw))
+        f30 = nb(t, Ho * Wo, cinP * k * k, cw) if callable(nb) else (nb or _pick_nb(t, Ho * Wo, cinP * k * k, cw, B))
         op([OP_CONV, src, dst, res, Hin, Win, CS, Ho, Wo, k, k, c.stride, c.dil, pt, pl, cinP, NP, w_off, b_off, c.act,
             out_cs if res >= 0 else 0, out_cs, out_off, cw, int(out_f32), bias_img, bias_img_stride] + extra +
            [f30, 2 if (rgb and tp) else int(tp)],
