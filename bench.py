@@ -1,8 +1,8 @@
 """Benchmark: frames/sec of the ENet 640x480 segmentation -> BEV occupancy-grid path on MI355X.
 
 One "step" = one pass of the hot path over one batch of synthetic 640x480x3 BGR frames already
-resident in HBM: ENet forward (47 launches: the initial block normalises the raw bytes as it loads
-them, regular bottlenecks run fused, argmax + 3-class remap in the last epilogue) -> fused BEV
+resident in HBM: ENet forward (29 launches, one per block: the initial block normalises the raw
+bytes as it loads them, argmax + 3-class remap in the class layer's epilogue) -> fused BEV
 rasteriser -> (N > 1) RCCL all-gather of the int8 grids. The batch is split into `--streams` frame
 shards run concurrently on their own HIP streams. Per-GPU batch is fixed (weak scaling): rank r of N
 owns `--batch` frames of the N*batch global batch (BASELINE configs 3 and 5: 64 frames per GPU =
@@ -98,31 +98,171 @@ def parse():
     p.add_argument("--graph", type=int, default=0, help="1: replay the step as one captured HIP graph")
     p.add_argument("--cpu-baseline-seconds", type=float, default=12.0)
     p.add_argument("--no-cpu-baseline", action="store_true")
+    p.add_argument("--extras", type=int, default=-1,
+                   help="1: add the fp32 / batch-1 latency / bf16-agreement / DeepLab sub-records (measured "
+                        "outside the timed loop); default: on at N = 1, off for N > 1")
+    p.add_argument("--deeplab-batch", type=int, default=64)
     return p.parse_args()
+
+
+_T0 = time.perf_counter()
+
+
+def log(msg):
+    """Progress on stderr (the JSON line stays the only stdout output)."""
+    print(f"[bench {time.perf_counter() - _T0:7.1f}s] {msg}", file=sys.stderr, flush=True)
+
+
+def _cpu_rate(fn, threads, budget_s):
+    torch.set_num_threads(threads)
+    fn(0)                                                 # warm-up (also sizes the thread pool)
+    n = 0
+    t0 = time.perf_counter()
+    while True:
+        fn(n)
+        n += 1
+        el = time.perf_counter() - t0
+        if el >= budget_s and n >= 2:
+            return n, el
+
+
+def cgroup_cpu_quota():
+    """CPUs granted by the cgroup CPU quota (cgroup v2 cpu.max or v1 cfs quota / period), or None."""
+    try:
+        with open("/sys/fs/cgroup/cpu.max") as f:
+            q, per = f.read().split()[:2]
+        if q != "max":
+            return float(q) / float(per)
+    except (OSError, ValueError):
+        pass
+    try:
+        with open("/sys/fs/cgroup/cpu/cpu.cfs_quota_us") as f:
+            q = float(f.read())
+        with open("/sys/fs/cgroup/cpu/cpu.cfs_period_us") as f:
+            per = float(f.read())
+        if q > 0:
+            return q / per
+    except (OSError, ValueError):
+        pass
+    return None
+
+
+def cpu_cores():
+    """(threads, description) of the CPU cores this process really gets: the affinity mask, capped by
+    the cgroup CPU quota and by OMP_NUM_THREADS when the runtime sets it (the GPU box grants a 16-CPU
+    share per GPU while its affinity mask lists the whole host; 256 threads on a 16-CPU quota run
+    ~50x slower than 16, measured). Returns the host facts alongside, so the record states them."""
+    aff = len(os.sched_getaffinity(0))
+    quota = cgroup_cpu_quota()
+    n = aff
+    if quota is not None:
+        n = min(n, max(1, int(quota)))
+    omp = os.environ.get("OMP_NUM_THREADS")
+    if omp and omp.isdigit() and int(omp) > 0:
+        n = min(n, int(omp))
+    return n, {"host_cpus": os.cpu_count(), "affinity_cpus": aff,
+               "cgroup_cpu_quota": None if quota is None else round(quota, 2), "omp_num_threads": omp}
 
 
 def cpu_baseline(blocks, bev, grid, H, W, budget_s):
     """The CPU oracle on a bounded sample of the same workload (frames processed one at a time as
-    the reference's loop does)."""
+    the reference's loop does), on every CPU the process is granted (cpu_cores)."""
     from bugcar_image_segmentation_amd import synthetic
     from oracle import ocv_c
-    threads = min(16, len(os.sched_getaffinity(0)))
-    torch.set_num_threads(threads)
     frames = synthetic.uniform_frames(8, H, W, seed=123)
-    ocv_c.pipeline(frames[:1], blocks, bev._bev_matrix, bev.after_warp_width, bev.after_warp_height,
-                   bev.cm_per_px, grid, (H, W))          # warm-up
-    n = 0
-    t0 = time.perf_counter()
-    while True:
+
+    def one(n):
         ocv_c.pipeline(frames[n % 8: n % 8 + 1], blocks, bev._bev_matrix, bev.after_warp_width,
                        bev.after_warp_height, bev.cm_per_px, grid, (H, W))
-        n += 1
-        el = time.perf_counter() - t0
-        if el >= budget_s and n >= 2:
-            break
-    return {"value": n / el, "unit": "frames/s", "cores": threads, "kind": "port",
+    t, facts = cpu_cores()
+    log(f"cpu baseline at {t} threads")
+    n, el = _cpu_rate(one, t, budget_s)
+    return {"value": round(n / el, 3), "unit": "frames/s", "cores": t, "kind": "port", **facts,
             "sample": f"{n} frames of the same workload ({H}x{W}, fp32 PyTorch-CPU ENet + C BEV/occgrid), "
-                      f"{el:.1f} s, one frame per call"}
+                      f"{el:.1f} s at {t} threads (every CPU the process is granted), one frame per call"}
+
+
+def fp32_record(blocks, bev, grid, H, W, frames, streams, steps):
+    """The fp32 parity mode (logits within 1e-3 of the oracle) on the same step, same batch."""
+    from bugcar_image_segmentation_amd.models import ENET
+    from bugcar_image_segmentation_amd.pipeline import OccupancyPipeline
+    B = frames.shape[0]
+    model = ENET(weights=blocks, precision="fp32")
+    pipe = OccupancyPipeline(model, bev, *grid, model_hw=(H, W), streams=streams)
+    for _ in range(3):
+        pipe.run(frames)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        pipe.run(frames)
+    torch.cuda.synchronize()
+    el = time.perf_counter() - t0
+    del pipe, model
+    return {"value": round(B * steps / el, 2), "unit": "frames/s", "ms_per_step": round(el / steps * 1e3, 4),
+            "per_gpu_batch": B, "steps": steps, "streams_per_gpu": streams}
+
+
+def latency_b1(blocks, precision, bev, grid, H, W, frame, iters):
+    """BASELINE config 2 / the reference's loop shape (one camera frame per call, models.py:94):
+    frame -> class map -> occupancy grid, host-synchronised after every frame, eager and as one
+    replayed HIP graph. ms per frame = the latency a ROS node would see (README.md:23: 60 fps)."""
+    from bugcar_image_segmentation_amd.models import ENET
+    from bugcar_image_segmentation_amd.pipeline import OccupancyPipeline
+    model = ENET(weights=blocks, precision=precision)
+    pipe = OccupancyPipeline(model, bev, *grid, model_hw=(H, W))
+    f = frame.clone()
+
+    def timed(fn):
+        for _ in range(5):
+            fn()
+        torch.cuda.synchronize()
+        ts = []
+        for _ in range(iters):
+            t0 = time.perf_counter()
+            fn()
+            torch.cuda.synchronize()
+            ts.append(time.perf_counter() - t0)
+        ts.sort()
+        return round(sum(ts) / len(ts) * 1e3, 4), round(ts[len(ts) // 2] * 1e3, 4), round(ts[int(len(ts) * 0.99)] * 1e3, 4)
+    e_mean, e_med, e_p99 = timed(lambda: pipe.run(f))
+    replay, _ = pipe.capture(f)
+    g_mean, g_med, g_p99 = timed(replay)
+    del pipe, model
+    return {"dtype": precision, "frame": f"{H}x{W}", "iters": iters,
+            "eager_ms": e_mean, "eager_median_ms": e_med, "eager_p99_ms": e_p99,
+            "graph_ms": g_mean, "graph_median_ms": g_med, "graph_p99_ms": g_p99,
+            "graph_fps": round(1e3 / g_mean, 1)}
+
+
+def bf16_agreement(blocks, H, W, nframes, dev):
+    """Per-pixel class agreement of the bf16 throughput mode with the fp32 parity mode on a fixed
+    frame set (structured road scenes, seed 77), over the 15 raw classes and the 3-class remap
+    (models.py:55-58); of the disagreeing pixels, the share whose fp32 top-2 margin exceeds 1e-2
+    (i.e. not a near-tie). Torch ops here only compare the two engine outputs."""
+    from bugcar_image_segmentation_amd import _native as N
+    from bugcar_image_segmentation_amd import synthetic
+    from bugcar_image_segmentation_amd.models import ENET
+    bgr = torch.from_numpy(synthetic.road_frames(nframes, H, W, seed=77)).to(dev)
+    lg = {}
+    for prec in ("fp32", "bf16"):
+        m = ENET(weights=blocks, precision=prec)
+        out = torch.empty((nframes, m.num_classes, H, W), dtype=torch.float32, device=dev)
+        m.ctx.forward_bgr(bgr, nframes, H, W, N.OUT_LOGITS_F32, out)
+        torch.cuda.synchronize()
+        lg[prec] = out
+        del m
+    a32, a16 = lg["fp32"].argmax(1), lg["bf16"].argmax(1)
+    lut3 = torch.tensor([1, 1, 0, 2, 2, 2, 2, 2, 2, 0, 2, 2, 2, 2, 2, 2], device=dev)
+    top2 = lg["fp32"].topk(2, dim=1).values
+    margin = top2[:, 0] - top2[:, 1]
+    dis = a32 != a16
+    nd = int(dis.sum())
+    return {"frames": nframes, "pixels": int(a32.numel()),
+            "class15_agreement": round(float((~dis).float().mean()), 6),
+            "class3_agreement": round(float((lut3[a32] == lut3[a16]).float().mean()), 6),
+            "disagreeing_pixels": nd,
+            "disagreeing_with_fp32_margin_gt_1e-2": round(int((dis & (margin > 1e-2)).sum()) / max(nd, 1), 4),
+            "max_abs_logit_diff": round(float((lg["fp32"] - lg["bf16"]).abs().max()), 4)}
 
 
 def main():
@@ -160,6 +300,7 @@ def main():
             gather_grids(g, B * world)
         return g
 
+    log("warmup")
     for _ in range(a.warmup):
         step()
     torch.cuda.synchronize()
@@ -178,6 +319,7 @@ def main():
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         el = float(t.item())
 
+    log(f"timed loop done: {el:.3f} s")
     # ---- per-stage and per-kernel timing with HIP events on the stream the kernels are launched on
     # (untimed region), at the shard size the timed region launched (shard 0 runs on model.ctx), so every
     # launch of this command has one shape and rocprof's per-kernel averages describe the same launches
@@ -199,7 +341,7 @@ def main():
         t_fwd += ev[0].elapsed_time(ev[1])
         t_bev += ev[1].elapsed_time(ev[2])
     t_fwd, t_bev = t_fwd / reps, t_bev / reps
-    # the laserscan-like occupancy mode (bev.py:351-375) on the same class maps (not in the timed step)
+    # the laserscan-like occupancy mode (bev.py:216-240) on the same class maps (not in the timed step)
     bev.laserscan_like_occupancy_grid = True
     bev.create_occupancy_grid_device(ss, *grid, out=gs)
     ev[0].record(stream)
@@ -256,6 +398,18 @@ def main():
             "stages_ms": {"frames": Bs, "enet_forward": round(t_fwd, 4), "bev_occgrid": round(t_bev, 4),
                           "bev_occgrid_laserscan": round(t_ls, 4)},
         }
+        extras = a.extras if a.extras >= 0 else int(world == 1)
+        if extras:
+            log("fp32 sub-record")
+            res["fp32"] = fp32_record(blocks, bev, grid, H, W, frames, a.streams, max(5, a.steps // 2))
+            log("batch-1 latency sub-record")
+            res["latency_b1_ms"] = latency_b1(blocks, a.precision, bev, grid, H, W, frames[:1], 100)
+            log("bf16 agreement sub-record")
+            res["bf16_class_agreement_vs_fp32"] = bf16_agreement(blocks, H, W, 4, dev)
+            import bench_deeplab
+            log("deeplab sub-record")
+            res["deeplab"] = bench_deeplab.record(dev, a.deeplab_batch, max(5, a.steps // 2), 3, "bf16",
+                                                  cpu_seconds=0 if a.no_cpu_baseline else 6.0)
         if not a.no_cpu_baseline:
             res["cpu_baseline"] = cpu_baseline(blocks, bev, grid, H, W, a.cpu_baseline_seconds)
         print(json.dumps(res), flush=True)

@@ -48,10 +48,12 @@ def parse():
 
 
 def cpu_baseline(net, budget_s):
+    """The oracle on a bounded sample, on every CPU the process is granted (bench.cpu_cores)."""
+    from bench import cpu_cores
     from oracle import deeplab_oracle as O
-    threads = min(16, len(os.sched_getaffinity(0)))
-    torch.set_num_threads(threads)
     x = np.random.default_rng(7).integers(0, 256, (1, net.crop, net.crop, 3), dtype=np.uint8)
+    threads, facts = cpu_cores()
+    torch.set_num_threads(threads)
     O.predict(net, x, dtype=torch.float32)   # warm-up
     n, t0 = 0, time.perf_counter()
     while True:
@@ -60,9 +62,9 @@ def cpu_baseline(net, budget_s):
         el = time.perf_counter() - t0
         if el >= budget_s and n >= 2:
             break
-    return {"value": round(n / el, 3), "unit": "frames/s", "cores": threads, "kind": "port",
+    return {"value": round(n / el, 3), "unit": "frames/s", "cores": threads, "kind": "port", **facts,
             "sample": f"{n} frames of the same workload ({net.crop}x{net.crop}, fp32 PyTorch-CPU oracle with TF "
-                      f"semantics), {el:.1f} s, one frame per call"}
+                      f"semantics), {el:.1f} s at {threads} threads, one frame per call"}
 
 
 def pmc_traffic(tag, batch):
@@ -81,30 +83,25 @@ def pmc_traffic(tag, batch):
     return None if v is None else round(float(v))
 
 
-def main():
-    a = parse()
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
-    if world > 1:
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
-    torch.cuda.set_device(local)
-    dev = torch.device("cuda", local)
+def measure(dev, B, steps, warmup, precision, world=1, rank=0):
+    """Time `steps` DeepLab forwards of B frames (barrier + sync on both sides, max over ranks), then
+    every launch of the plan with HIP events (untimed). Returns (el seconds, model, per-tag table,
+    per-op list, forward us)."""
     from bugcar_image_segmentation_amd.models import DeepLabV3
 
-    model = DeepLabV3(precision=a.precision)
-    net, B, C = model.net, a.batch, model.net.crop
+    model = DeepLabV3(precision=precision)
+    C = model.net.crop
     frames = torch.from_numpy(np.random.default_rng(rank).integers(0, 256, (B, C, C, 3), dtype=np.uint8)).to(dev)
     out = torch.empty((B, C, C), dtype=torch.int64, device=dev)
 
-    for _ in range(a.warmup):
+    for _ in range(warmup):
         model.predict_device(frames, out=out)
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    for _ in range(a.steps):
+    for _ in range(steps):
         model.predict_device(frames, out=out)
     torch.cuda.synchronize()
     if world > 1:
@@ -118,7 +115,7 @@ def main():
     # per-launch HIP-event timing of the plan the timed region ran (untimed region)
     stream = torch.cuda.current_stream()
     info = model.plan_info
-    reps = max(3, min(10, a.steps))
+    reps = max(3, min(10, steps))
     per = defaultdict(lambda: {"launches": 0, "us": 0.0, "bytes": 0.0, "flops": 0.0})
     evs = [torch.cuda.Event(enable_timing=True) for _ in range(2)]
     fwd_us = 0.0
@@ -138,12 +135,64 @@ def main():
         d["us"] += us
         d["bytes"] += nbytes
         d["flops"] += flops
+    return el, model, per, per_op, fwd_us
+
+
+def roofline(model, per, fwd_us, B, precision):
+    info = model.plan_info
+    tag, k = max(per.items(), key=lambda kv: kv[1]["us"])
+    achieved = k["bytes"] / (k["us"] * 1e-6) / 1e9
+    peak_tf = MFMA_PEAK_TFLOPS[precision]
+    return {
+        "bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+        "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": pmc_traffic(tag, B),
+        "kernel": f"{tag}: dominant kernel tag ({k['launches']} launches, {k['us']:.0f} us of {fwd_us:.0f} us "
+                  f"per forward); {k['bytes'] / k['launches'] / 1e6:.1f} MB per launch (input once + output "
+                  f"once + residual + weights); {k['flops'] / (k['us'] * 1e-6) / 1e12:.1f} TFLOP/s "
+                  f"({k['flops'] / (k['us'] * 1e-6) / 1e12 / peak_tf:.3f} of the dense {precision} MFMA peak)",
+        "forward": {"launches": len(info["per_op"]), "us": round(fwd_us, 1), "frames": B,
+                    "bytes_per_frame": round(info["bytes"] / B), "flops_per_frame": round(info["flops"] / B),
+                    "achieved_gbs": round(info["bytes"] / (fwd_us * 1e-6) / 1e9, 1),
+                    "mfma_tflops": round(info["flops"] / (fwd_us * 1e-6) / 1e12, 2),
+                    "mfma_frac": round(info["flops"] / (fwd_us * 1e-6) / 1e12 / peak_tf, 4)},
+    }
+
+
+def kernel_summary(per):
+    return {t: {"launches": v["launches"], "us": round(v["us"], 1),
+                "GBps": round(v["bytes"] / (v["us"] * 1e-6) / 1e9, 1),
+                "TFLOPs": round(v["flops"] / (v["us"] * 1e-6) / 1e12, 2)}
+            for t, v in sorted(per.items(), key=lambda kv: -kv[1]["us"])}
+
+
+def record(dev, B, steps, warmup, precision, cpu_seconds=0.0):
+    """The config-4 sub-record bench.py adds to its line (one GPU, measured after its timed loop)."""
+    el, model, per, _per_op, fwd_us = measure(dev, B, steps, warmup, precision)
+    res = {"value": round(B * steps / el, 2), "unit": "frames/s", "ms_per_step": round(el / steps * 1e3, 4),
+           "steps": steps, "dtype": precision, "per_gpu_batch": B, "crop": model.net.crop,
+           "workload": "config4: DeepLabV3 MobileNetV2 OS8 + ASPP, 513x513 u8 RGB -> SemanticPredictions int64",
+           "roofline": roofline(model, per, fwd_us, B, precision)}
+    if cpu_seconds > 0:
+        res["cpu_baseline"] = cpu_baseline(model.net, cpu_seconds)
+    del model
+    return res
+
+
+def main():
+    a = parse()
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+    B = a.batch
+    el, model, per, per_op, fwd_us = measure(dev, B, a.steps, a.warmup, a.precision, world, rank)
+    C = model.net.crop
 
     if rank == 0:
         value = B * world * a.steps / el
-        tag, k = max(per.items(), key=lambda kv: kv[1]["us"])
-        achieved = k["bytes"] / (k["us"] * 1e-6) / 1e9
-        peak_tf = MFMA_PEAK_TFLOPS[a.precision]
         res = {
             "metric": "frames/sec DeepLabV3 513x513 -> SemanticPredictions (synthetic), whole job",
             "value": round(value, 2), "unit": "frames/s", "n_gpus": world, "steps": a.steps, "warmup": a.warmup,
@@ -154,27 +203,12 @@ def main():
                                    f"batch {B} per GPU, pad/normalise + forward + bilinear resize + argmax int64",
                        "global_batch": B * world, "per_gpu_batch": B, "crop": C,
                        "parallelism": f"frame-sharded dp{world}"},
-            "roofline": {
-                "bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": pmc_traffic(tag, B),
-                "kernel": f"{tag}: dominant kernel tag ({k['launches']} launches, {k['us']:.0f} us of {fwd_us:.0f} us "
-                          f"per forward); {k['bytes'] / k['launches'] / 1e6:.1f} MB per launch (input once + output "
-                          f"once + residual + weights); {k['flops'] / (k['us'] * 1e-6) / 1e12:.1f} TFLOP/s "
-                          f"({k['flops'] / (k['us'] * 1e-6) / 1e12 / peak_tf:.3f} of the dense {a.precision} MFMA peak)",
-                "forward": {"launches": len(info["per_op"]), "us": round(fwd_us, 1), "frames": B,
-                            "bytes_per_frame": round(info["bytes"] / B), "flops_per_frame": round(info["flops"] / B),
-                            "achieved_gbs": round(info["bytes"] / (fwd_us * 1e-6) / 1e9, 1),
-                            "mfma_tflops": round(info["flops"] / (fwd_us * 1e-6) / 1e12, 2),
-                            "mfma_frac": round(info["flops"] / (fwd_us * 1e-6) / 1e12 / peak_tf, 4)},
-            },
-            "kernels": {t: {"launches": v["launches"], "us": round(v["us"], 1),
-                            "GBps": round(v["bytes"] / (v["us"] * 1e-6) / 1e9, 1),
-                            "TFLOPs": round(v["flops"] / (v["us"] * 1e-6) / 1e12, 2)}
-                        for t, v in sorted(per.items(), key=lambda kv: -kv[1]["us"])},
+            "roofline": roofline(model, per, fwd_us, B, a.precision),
+            "kernels": kernel_summary(per),
             "per_op": per_op,
         }
         if not a.no_cpu_baseline:
-            res["cpu_baseline"] = cpu_baseline(net, a.cpu_baseline_seconds)
+            res["cpu_baseline"] = cpu_baseline(model.net, a.cpu_baseline_seconds)
         print(json.dumps(res), flush=True)
     if world > 1:
         dist.barrier()

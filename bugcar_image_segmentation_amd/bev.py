@@ -3,12 +3,12 @@
 `fromJSON`, the constructor, `save_to_JSON` and `create_occupancy_grid` keep the reference's
 names, argument meaning, shape assert and return dtype. The per-frame work — warpPerspective of the
 lifted class map, the crop/pad into the grid template, the 3x3 opening that frees isolated occupied
-pixels, the INTER_NEAREST downsample and the int8 encoding (bev.py:301-381) — is ONE fused gfx950
+pixels, the INTER_NEAREST downsample and the int8 encoding (bev.py:166-246) — is ONE fused gfx950
 kernel (csrc/bev_kernels.hip). The geometry below (cell sizes, template offsets) is host arithmetic
 written exactly as the reference writes it, because its float-to-int truncations are part of the
 result.
 
-The laserscan-like mode ("is_laserscan", bev.py:351-375 and the binary variant's bev.py:143-164) runs
+The laserscan-like mode ("is_laserscan", bev.py:216-240 and the binary variant's bev.py:143-164) runs
 on the engine too: the rasteriser, a per-ray nearest-obstacle kernel and a re-projection kernel over
 polar tables the library builds once per geometry (csrc/bev_kernels.hip).
 
@@ -131,7 +131,7 @@ class bev_transform_tools:
     # -- geometry ----------------------------------------------------------------------------
     def occupancy_params(self, occupancy_grid_width_in_m, occupancy_grid_height_in_m, cell_size_in_m,
                          ros_layout: bool = False, binary: bool = False, laserscan: bool | None = None) -> N.BevParams:
-        """bev.py:307-319 (bev.py:101-114 for the binary variant: the same arithmetic), with the
+        """bev.py:172-184 (bev.py:101-114 for the binary variant: the same arithmetic), with the
         reference's float arithmetic and int() truncations."""
         cell_size_in_px = (cell_size_in_m * 100 / self.cm_per_px)
         occ_grid_width = int(occupancy_grid_width_in_m / cell_size_in_m)
@@ -187,12 +187,12 @@ class bev_transform_tools:
             raise ValueError(f"out has shape {tuple(out.shape)}, expected {shape}")
         if out is None:
             out = torch.empty(shape, dtype=torch.int8, device=seg.device)
-        N.shared_context(seg.device.index).bev(seg, B, p, out)
+        N.shared_context(seg.device.index).bev(seg, B, p, out, torch.cuda.current_stream(seg.device))
         return out
 
     def create_occupancy_grid(self, segmap, occupancy_grid_width_in_m, occupancy_grid_height_in_m, cell_size_in_m):
-        """bev.py:301-381 -> np.int8 (h, w) in {-1 unknown, 0 free, 100 occupied}. In laserscan-like mode
-        (bev.py:351-375) only the obstacle cells nearest the vehicle along each polar ray stay
+        """bev.py:166-246 -> np.int8 (h, w) in {-1 unknown, 0 free, 100 occupied}. In laserscan-like mode
+        (bev.py:216-240) only the obstacle cells nearest the vehicle along each polar ray stay
         occupied; obstacle cells behind them become unknown."""
         self._check_shape(np.shape(segmap))
         seg = segmap if isinstance(segmap, torch.Tensor) else torch.from_numpy(np.ascontiguousarray(segmap, dtype=np.uint8))

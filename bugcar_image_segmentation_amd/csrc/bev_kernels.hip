@@ -1,20 +1,20 @@
 // Fused BEV occupancy-grid rasteriser: bev_transform_tools.create_occupancy_grid, non-laserscan
-// branch (bev.py:301-381), for a batch of class maps in one launch.
+// branch (bev.py:166-246), for a batch of class maps in one launch.
 //
-// The reference materialises segmap+1 (bev.py:312), a full warped image (bev.py:317, e.g. 1000x1000),
-// a cropped/padded template (bev.py:318-330), an occupancy mask, its 3x3 opening (bev.py:331-340)
-// and the INTER_NEAREST-downsampled grid (bev.py:344). Here one thread produces one output cell:
+// The reference materialises segmap+1 (bev.py:177), a full warped image (bev.py:182, e.g. 1000x1000),
+// a cropped/padded template (bev.py:183-195), an occupancy mask, its 3x3 opening (bev.py:196-205)
+// and the INTER_NEAREST-downsampled grid (bev.py:209). Here one thread produces one output cell:
 //   * the cell samples ONE template pixel p = (min(floor(cy*ify), h_px-1), min(floor(cx*ifx), w_px-1))
 //     (resizeNN), so only the template values that p depends on are ever computed;
 //   * template(t) = warp(t + (left_x, top_y)) when inside the warped image, else 0 — the crop/pad of
-//     bev.py:318-330 is exactly this shift;
+//     bev.py:183-195 is exactly this shift;
 //   * warp() is cv2.warpPerspective INTER_LINEAR/BORDER_CONSTANT on segmap+1: double-precision
 //     inverse mapping with OpenCV's per-32x32-block split X0 + M0*x1 (FP contraction OFF so the
 //     IEEE order matches), cvRound to 1/32 pixel, Q15 bilinear weights, (sum + 2^14) >> 15;
 //   * if p is occupied ({1,3}) it is a speckle unless some 3x3-neighbour q of p has an all-occupied
 //     3x3 neighbourhood (erode then dilate, out-of-template taps ignored = OpenCV's default morphology
 //     border): the 5x5 occupancy window around p is evaluated lazily;
-//   * encode: speckle -> 2, 3 -> 1, then {0:-1, 1:100, 2:0} as int8 (bev.py:377-380), written in the
+//   * encode: speckle -> 2, 3 -> 1, then {0:-1, 1:100, 2:0} as int8 (bev.py:242-245), written in the
 //     reference (h, w) layout or directly in the ROS data order flip(0)+rot90ccw (occgrid_to_ros.py:18-25).
 // Algorithmic traffic per frame: the class map read once (in_rows*in_cols B, gathered; L2-resident)
 // + occ_h*occ_w B written — latency/gather-bound, far below the HBM roof.
@@ -41,7 +41,7 @@ __device__ __forceinline__ int warp_value(const BevArgs &a, const uint8_t *seg, 
     sy = sy < -32768 ? -32768 : (sy > 32767 ? 32767 : sy);
     const int ax = X & 31, ay = Y & 31;
     const int w = a.in_cols, h = a.in_rows;
-    // segmap + 1 (bev.py:312): taps inside the image read class+1, outside the border value 0
+    // segmap + 1 (bev.py:177): taps inside the image read class+1, outside the border value 0
     const bool x0 = (unsigned)sx < (unsigned)w, x1ok = (unsigned)(sx + 1) < (unsigned)w;
     const bool y0 = (unsigned)sy < (unsigned)h, y1ok = (unsigned)(sy + 1) < (unsigned)h;
     int v0 = 0, v1 = 0, v2 = 0, v3 = 0;
@@ -67,7 +67,7 @@ __device__ __forceinline__ int tmpl_value(const BevArgs &a, const uint8_t *seg, 
     return warp_value(a, seg, wx, wy);
 }
 
-// occupied template values: {1, 3} (bev.py:331), or {1} in the binary variant (bev.py:126)
+// occupied template values: {1, 3} (bev.py:196), or {1} in the binary variant (bev.py:128)
 __device__ __forceinline__ bool occupied(const BevArgs &a, int v) { return v == 1 || (v == 3 && !a.variant); }
 
 // Occupancy bit of template pixel p + (dx, dy); pixels outside the template read 1 (neutral for the
@@ -121,19 +121,19 @@ __global__ void __launch_bounds__(256) bev_occgrid_kernel(const BevArgs a) {
                         opened |= inside && (m & win) == win;
                     }
             }
-            if (!opened) v = 2;                  // isolated occupied pixel -> free (bev.py:339-340)
+            if (!opened) v = 2;                  // isolated occupied pixel -> free (bev.py:204-205)
         }
         int8_t o;
         if (!a.variant) {
-            const int g = v == 3 ? 1 : v;        // bev.py:377
-            o = (int8_t)(g == 0 ? -1 : 200 - 100 * g);   // bev.py:379-380
+            const int g = v == 3 ? 1 : v;        // bev.py:242
+            o = (int8_t)(g == 0 ? -1 : 200 - 100 * g);   // bev.py:244-245
         } else {
-            // bev.py:137-141, :165 in uint8 arithmetic: {0:-1, 1:100, 2:0, 3:-100}
+            // bev.py:139-144, :165 in uint8 arithmetic: {0:-1, 1:100, 2:0, 3:-100}
             const uint8_t g = (uint8_t)(v * 100);
             o = (int8_t)(uint8_t)(g == 0 ? 0xff : (uint8_t)(200 - g));
         }
         if (a.laserscan) {
-            // the polar warp's source: the cells (bev.py:353) or the encoded grid (bev.py:146)
+            // the polar warp's source: the cells (bev.py:219) or the encoded grid (bev.py:146)
             a.cells[i] = a.variant ? (uint8_t)o : (uint8_t)v;
             if (!a.variant) continue;            // the final laserscan kernel writes out
         }
@@ -146,7 +146,7 @@ __global__ void __launch_bounds__(256) bev_occgrid_kernel(const BevArgs a) {
     }
 }
 
-// ---- laserscan-like occupancy (bev.py:351-375; binary variant bev.py:143-164) ----------------------
+// ---- laserscan-like occupancy (bev.py:216-240; binary variant bev.py:143-164) ----------------------
 // The reference polar-warps the grid (cv2.warpPolar, nearest), finds per polar row (ray angle) the
 // nearest obstacle (np.where + npi.group_by(...).min — a Python loop over rays follows), stamps a
 // radius-1 cv2.circle there and warps the stamps back. Here:
@@ -204,10 +204,10 @@ __global__ void __launch_bounds__(256) laserscan_kernel(const BevArgs a) {
         }
         int8_t o;
         if (!a.variant) {
-            const int g = v != 3 ? v : s;        // bev.py:372
-            o = (int8_t)(g == 0 ? -1 : 200 - 100 * g);   // bev.py:379
+            const int g = v != 3 ? v : s;        // bev.py:236
+            o = (int8_t)(g == 0 ? -1 : 200 - 100 * g);   // bev.py:244
         } else {
-            o = v == 255 ? (int8_t)-1 : (int8_t)(s * 100);  // bev.py:159-161
+            o = v == 255 ? (int8_t)-1 : (int8_t)(s * 100);  // bev.py:160-163
         }
         int8_t *out = a.variant ? a.out + (size_t)a.B * cells : a.out;   // binary: the second grid
         if (a.ros_layout) out[(size_t)b * cells + (size_t)(a.occ_w - 1 - cx) * a.occ_h + (a.occ_h - 1 - cy)] = o;

@@ -155,7 +155,7 @@ struct BevArgs {
     int ros_layout;
     int variant;         // 0 create_occupancy_grid, 1 create_occupancy_grid_binary
     int8_t *out;
-    // laserscan-like mode (bev.py:351-375 / :143-164): the rasteriser also writes the polar warp's
+    // laserscan-like mode (bev.py:216-240 / :143-164): the rasteriser also writes the polar warp's
     // source grid (variant 0: the template cells; 1: the encoded grid as uint8) to `cells`, and for
     // variant 0 leaves `out` to the final laserscan kernel
     int laserscan;

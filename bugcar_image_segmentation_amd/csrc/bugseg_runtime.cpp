@@ -2,7 +2,7 @@
 //
 // Replaces what the reference gets from the TensorFlow C++ runtime (GraphDef import + Session
 // executor, models.py:21-44) and from OpenCV (resize / warpPerspective / morphology / resize-NN,
-// models.py:87-89, bev.py:317-347):
+// models.py:87-89, bev.py:182-212):
 //   * parses the BSG1 weight blob (enet_spec.py), folds batch-norm into the convolutions in double,
 //     packs every convolution for the MFMA kernels ([Npad][Kpad] rows, 8-channel k groups, tap
 //     table) and uploads all of it in ONE device allocation;
@@ -112,8 +112,11 @@ struct bugseg_ctx {
     int polar_key[3] = {0, 0, -1};
     int polar_pw = 0, polar_ph = 0;
     void *polar_tab = nullptr;       // fmap (ph*pw int32) then imap (occ_h*occ_w int32)
-    void *ls_scratch = nullptr;      // cells (B*occ_h*occ_w u8, 256-B aligned) then rmin (B*ph int32)
-    size_t ls_scratch_bytes = 0;
+    // per-stream batch scratch: cells (B*occ_h*occ_w u8, 256-B aligned) then rmin (B*ph int32). Keyed
+    // by stream so that calls enqueued on different streams of one context never share intermediate
+    // buffers (the polar tables are read-only once built and are shared).
+    struct LsScratch { void *stream = nullptr; void *p = nullptr; size_t bytes = 0; };
+    std::vector<LsScratch> ls_scratch;
 };
 
 namespace {
@@ -965,7 +968,11 @@ bool build_plan(bugseg_ctx *ctx, int B, int H, int W, std::string &why) {
     auto al = [](size_t v) { return (v + 4095) / 4096 * 4096; };
     size_t total = 2 * al(w.szX) + 3 * al(w.szT) + al(w.szM);
     for (size_t s : w.szIdx) total += al(s);
-    if (pl.arena) { (void)hipFree(pl.arena); pl.arena = nullptr; }
+    if (pl.arena) {
+        (void)hipDeviceSynchronize();   // a forward of the old shape may still be running on any stream
+        (void)hipFree(pl.arena);
+        pl.arena = nullptr;
+    }
     if (hipMalloc(&pl.arena, total) != hipSuccess) { why = "hipMalloc of the activation arena failed"; pl.arena = nullptr; return false; }
     unsigned char *p = (unsigned char *)pl.arena;
     w.X[0] = p; p += al(w.szX);
@@ -1057,7 +1064,7 @@ int bugseg_destroy(bugseg_ctx *ctx) {
     if (ctx->plan.arena) (void)hipFree(ctx->plan.arena);
     if (ctx->pre_tab) (void)hipFree(ctx->pre_tab);
     if (ctx->polar_tab) (void)hipFree(ctx->polar_tab);
-    if (ctx->ls_scratch) (void)hipFree(ctx->ls_scratch);
+    for (auto &s : ctx->ls_scratch) if (s.p) (void)hipFree(s.p);
     delete ctx;
     return BUGSEG_OK;
 }
@@ -1122,7 +1129,8 @@ int bugseg_preprocess(bugseg_ctx *ctx, const uint8_t *bgr, int B, int H0, int W0
                 short *yb = (short *)(h.data() + (size_t)W * 8 + (size_t)H * 4);
                 linear_coeffs(W, W0, sx, xo, xa);
                 linear_coeffs(H, H0, sy, yo, yb);
-                if (hipStreamSynchronize((hipStream_t)stream) != hipSuccess) return fail(ctx, BUGSEG_EHIP, "stream sync failed");
+                // the old table may still be read by work enqueued on any stream of this context
+                if (hipDeviceSynchronize() != hipSuccess) return fail(ctx, BUGSEG_EHIP, "device sync failed");
                 if (ctx->pre_tab) (void)hipFree(ctx->pre_tab);
                 ctx->pre_tab = nullptr;
                 if (hipMalloc(&ctx->pre_tab, need) != hipSuccess ||
@@ -1264,7 +1272,7 @@ void polar_tables(int pw, int ph, double max_radius, float cx, float cy, int w, 
 // Polar tables and scratch for a laserscan call; fills a.fmap / imap / pw / ph / cells / rmin / hit.
 int prepare_laserscan(bugseg_ctx *ctx, const bugseg_bev_params *p, int B, BevArgs &a, void *stream) {
     const int w = p->occ_w, h = p->occ_h, L = std::max(w, h);
-    // warpPolar dsize: (-1, -1) -> (round(L), round(L*pi)) for create_occupancy_grid (bev.py:355);
+    // warpPolar dsize: (-1, -1) -> (round(L), round(L*pi)) for create_occupancy_grid (bev.py:219);
     // the explicit (w, h) of create_occupancy_grid_binary (bev.py:146)
     const int pw = p->variant ? w : (int)std::lrint((double)L);
     const int ph = p->variant ? h : (int)std::lrint((double)L * 3.1415926535897932384626433832795);
@@ -1273,7 +1281,8 @@ int prepare_laserscan(bugseg_ctx *ctx, const bugseg_bev_params *p, int B, BevArg
     if (ctx->polar_key[0] != w || ctx->polar_key[1] != h || ctx->polar_key[2] != p->variant || !ctx->polar_tab) {
         std::vector<int32_t> fmap, imap;
         polar_tables(pw, ph, (double)L, (float)(w / 2.0 - 1), (float)h, w, h, fmap, imap);
-        if (hipStreamSynchronize((hipStream_t)stream) != hipSuccess) return fail(ctx, BUGSEG_EHIP, "stream sync failed");
+        // the old tables may still be read by work enqueued on ANY stream of this context
+        if (hipDeviceSynchronize() != hipSuccess) return fail(ctx, BUGSEG_EHIP, "device sync failed");
         if (ctx->polar_tab) (void)hipFree(ctx->polar_tab);
         ctx->polar_tab = nullptr;
         const size_t bytes = (fmap.size() + imap.size()) * sizeof(int32_t);
@@ -1286,20 +1295,29 @@ int prepare_laserscan(bugseg_ctx *ctx, const bugseg_bev_params *p, int B, BevArg
     }
     const size_t cells_bytes = ((size_t)B * w * h + 255) & ~(size_t)255;
     const size_t need = cells_bytes + (size_t)B * ph * sizeof(int32_t);
-    if (need > ctx->ls_scratch_bytes) {
-        if (hipStreamSynchronize((hipStream_t)stream) != hipSuccess) return fail(ctx, BUGSEG_EHIP, "stream sync failed");
-        if (ctx->ls_scratch) (void)hipFree(ctx->ls_scratch);
-        ctx->ls_scratch = nullptr;
-        ctx->ls_scratch_bytes = 0;
-        if (hipMalloc(&ctx->ls_scratch, need) != hipSuccess) return fail(ctx, BUGSEG_ENOMEM, "laserscan scratch allocation failed");
-        ctx->ls_scratch_bytes = need;
+    bugseg_ctx::LsScratch *sc = nullptr;
+    for (auto &x : ctx->ls_scratch) if (x.stream == stream) sc = &x;
+    if (!sc) {
+        ctx->ls_scratch.push_back(bugseg_ctx::LsScratch());
+        sc = &ctx->ls_scratch.back();
+        sc->stream = stream;
+    }
+    if (need > sc->bytes) {
+        // this stream's scratch is only used by this stream's work; a device-wide sync also covers a
+        // caller that reuses a stream handle value after destroying the stream
+        if (hipDeviceSynchronize() != hipSuccess) return fail(ctx, BUGSEG_EHIP, "device sync failed");
+        if (sc->p) (void)hipFree(sc->p);
+        sc->p = nullptr;
+        sc->bytes = 0;
+        if (hipMalloc(&sc->p, need) != hipSuccess) return fail(ctx, BUGSEG_ENOMEM, "laserscan scratch allocation failed");
+        sc->bytes = need;
     }
     a.laserscan = 1;
     a.fmap = (const int32_t *)ctx->polar_tab;
     a.imap = (const int32_t *)ctx->polar_tab + (size_t)pw * ph;
     a.pw = pw; a.ph = ph;
-    a.cells = (uint8_t *)ctx->ls_scratch;
-    a.rmin = (int32_t *)((unsigned char *)ctx->ls_scratch + cells_bytes);
+    a.cells = (uint8_t *)sc->p;
+    a.rmin = (int32_t *)((unsigned char *)sc->p + cells_bytes);
     a.hit = p->variant ? 100 : 3;
     return BUGSEG_OK;
 }

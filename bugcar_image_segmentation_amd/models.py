@@ -34,7 +34,11 @@ class InferenceModel(ABC):
         pass
 
 
-def _as_device_tensor(x, dtype=None) -> torch.Tensor:
+def _as_device_tensor(x, dtype=None, device: int | None = None) -> torch.Tensor:
+    """Host array / tensor -> contiguous tensor on HIP device `device` (default: the current one).
+    A tensor already on another device is refused rather than silently used with this context's
+    stream (the kernels would run on the context's device with a foreign pointer)."""
+    dev = torch.device("cuda", torch.cuda.current_device() if device is None else device)
     if isinstance(x, torch.Tensor):
         t = x
     else:
@@ -42,7 +46,9 @@ def _as_device_tensor(x, dtype=None) -> torch.Tensor:
     if dtype is not None and t.dtype != dtype:
         t = t.to(dtype)
     if not t.is_cuda:
-        t = t.to(torch.device("cuda", torch.cuda.current_device()), non_blocking=False)
+        t = t.to(dev, non_blocking=False)
+    elif t.device != dev:
+        raise ValueError(f"input is on {t.device}, but the model runs on {dev}")
     return t.contiguous()
 
 
@@ -100,7 +106,7 @@ class ENET(InferenceModel):
 
     def engine_input(self, preprocessed) -> torch.Tensor:
         """NCHW (B,3,H,W) float (numpy or torch) -> engine input tensor (B,H,W,8) on the device."""
-        x = _as_device_tensor(preprocessed)
+        x = _as_device_tensor(preprocessed, device=self.ctx.device)
         if x.dtype not in (torch.float32, torch.float64):
             x = x.to(torch.float32)
         if x.dim() != 4 or x.shape[1] != 3:
@@ -108,19 +114,24 @@ class ENET(InferenceModel):
         B, _, H, W = x.shape
         es = 2 if self.precision == "bf16" else 4
         out = self._buf("in", (B, H, W, 8 * es), torch.uint8)
-        self.ctx.nchw_to_input(x, B, H, W, out)
+        self.ctx.nchw_to_input(x, B, H, W, out, self._stream())
         return out
+
+    def _stream(self):
+        return torch.cuda.current_stream(torch.device("cuda", self.ctx.device))
 
     def predict_device(self, engine_in: torch.Tensor, out_kind: int = N.OUT_CLASS3_U8, out: torch.Tensor | None = None):
         """Forward on an engine-input tensor (B,H,W,8*elem bytes u8 view) -> device tensor."""
         B, H, W = engine_in.shape[:3]
         dev = torch.device("cuda", self.ctx.device)
+        if engine_in.device != dev:
+            raise ValueError(f"input is on {engine_in.device}, but the model runs on {dev}")
         if out is None:
             if out_kind == N.OUT_LOGITS_F32:
                 out = torch.empty((B, self.num_classes, H, W), dtype=torch.float32, device=dev)
             else:
                 out = torch.empty((B, H, W), dtype=torch.uint8, device=dev)
-        self.ctx.forward(engine_in, B, H, W, out_kind, out)
+        self.ctx.forward(engine_in, B, H, W, out_kind, out, self._stream())
         return out
 
     def logits(self, preprocessed_imgs) -> np.ndarray:
@@ -141,7 +152,7 @@ class ENET(InferenceModel):
     def preprocess_device(cls, bgr, layout: int = N.PRE_NCHW_F64, ctx: "N.Context | None" = None,
                           width: int | None = None, height: int | None = None) -> torch.Tensor:
         """Batched models.py:84-95 on the device: bgr (B,H0,W0,3) or (H0,W0,3) uint8."""
-        x = _as_device_tensor(bgr, torch.uint8)
+        x = _as_device_tensor(bgr, torch.uint8, None if ctx is None else ctx.device)
         if x.dim() == 3:
             x = x.unsqueeze(0)
         if x.dim() != 4 or x.shape[3] != 3:
@@ -157,7 +168,7 @@ class ENET(InferenceModel):
             out = torch.empty((B, 3, H, W), dtype=torch.float32, device=dev)
         else:
             out = torch.empty((B, H, W, 8 * (2 if c.precision == N.BF16 else 4)), dtype=torch.uint8, device=dev)
-        c.preprocess(x, B, H0, W0, H, W, layout, out)
+        c.preprocess(x, B, H0, W0, H, W, layout, out, torch.cuda.current_stream(dev))
         return out
 
     @classmethod
@@ -194,9 +205,12 @@ class DeepLabV3(InferenceModel):
     FROZEN_GRAPH_NAME = "deeplab.pb"
     CROP_SIZE = 513
 
-    def __init__(self, GRAPH_PB_PATH=None, *, net=None, precision: str = "bf16", device: int | None = None,
+    def __init__(self, GRAPH_PB_PATH=None, *, net=None, precision: str = "fp32", device: int | None = None,
                  fuse_dw: bool | None = None, fuse_prep: bool = True):
-        """fuse_dw=True computes each depthwise conv inside its projection's operand loads
+        """precision: "fp32" (default: the parity mode, logits within 1e-3 of the fp32 graph, as a
+        drop-in for the reference's TF fp32 sess.run) or "bf16" (the throughput mode the bench uses;
+        class ids can differ from fp32 where two logits are close).
+        fuse_dw=True computes each depthwise conv inside its projection's operand loads
         (bit-identical, measured slower; deeplab_spec.lower). fuse_prep=False runs the padding +
         normalisation as its own launch instead of inside the stem's operand loads (bit-identical)."""
         from . import deeplab_spec
@@ -241,7 +255,7 @@ class DeepLabV3(InferenceModel):
 
     def predict_device(self, rgb, out: torch.Tensor | None = None) -> torch.Tensor:
         """(B, H, W, 3) u8 RGB (device or host) -> (B, H, W) int64 device tensor."""
-        x = _as_device_tensor(rgb, torch.uint8)
+        x = _as_device_tensor(rgb, torch.uint8, self.ctx.device)
         if x.dim() == 3:
             x = x.unsqueeze(0)
         if x.dim() != 4 or x.shape[3] != 3:
@@ -252,7 +266,7 @@ class DeepLabV3(InferenceModel):
         self._ensure_plan(B)
         if out is None:
             out = torch.empty((B, H, W), dtype=torch.int64, device=x.device)
-        self.ctx.forward(x, B, H, W, out)
+        self.ctx.forward(x, B, H, W, out, torch.cuda.current_stream(x.device))
         return out
 
     def logits_device(self) -> torch.Tensor:
@@ -260,7 +274,7 @@ class DeepLabV3(InferenceModel):
         h, w = self.plan_info["feature"]
         t = torch.empty((self._plan_B, h, w, self.plan_info["lcs"]), dtype=torch.float32,
                         device=torch.device("cuda", self.ctx.device))
-        self.ctx.read_buffer(7, t)
+        self.ctx.read_buffer(7, t, torch.cuda.current_stream(t.device))
         return t
 
     def predict(self, img) -> np.ndarray:

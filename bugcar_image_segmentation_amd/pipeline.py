@@ -1,11 +1,12 @@
 """Batched, device-resident frame -> occupancy-grid path (BASELINE config 3):
 
     BGR u8 frames (B,H0,W0,3)  --[resize kernel, only if H0xW0 != HxW]-->  BGR u8 (B,H,W,3)
-      --89 fused conv launches (ENet; the initial block normalises the raw bytes as it loads them,
-        argmax + 3-class remap in the last epilogue)-->  u8 (B,H,W)
+      --29 launches, one per ENet block (the initial block normalises the raw bytes as it loads
+        them, argmax + 3-class remap in the class layer's epilogue)-->  u8 (B,H,W)
       --BEV rasteriser kernel-->  int8 grids (B,h,w)   [or ROS data order]
 
-Everything stays in HBM on one stream; there is no host round trip between stages. This is the
+Everything stays in HBM; there is no host round trip between stages. With streams > 1 every frame
+shard runs all three stages on its own context and stream. This is the
 loop the reference's (absent) ROS node runs per frame (README.md:19), batched.
 """
 from __future__ import annotations
@@ -23,15 +24,20 @@ class OccupancyPipeline:
     device (one shard's compute phases beside another's memory phases). Results are identical."""
 
     def __init__(self, model: ENET, bev: bev_transform_tools, grid_w_m: float, grid_h_m: float, cell_m: float,
-                 model_hw: tuple[int, int] | None = None, ros_layout: bool = False, streams: int = 1):
+                 model_hw: tuple[int, int] | None = None, ros_layout: bool = False, streams: int = 1,
+                 binary: bool = False):
+        """binary=True is the predict_binary + create_occupancy_grid_binary pairing (models.py:70-82,
+        bev.py:97-165): class maps through the binary LUT, the binary rasteriser; in the laserscan-like
+        mode its output is the reference's pair, (2, B, ...) (bev.py:164)."""
         self.model = model
+        self.binary = binary
         self.bev = bev
         self.grid = (grid_w_m, grid_h_m, cell_m)
         self.H, self.W = model_hw if model_hw is not None else (ENET.INPUT_HEIGHT, ENET.INPUT_WIDTH)
         self.ros_layout = ros_layout
         if (self.H, self.W) != (bev.input_width, bev.input_height):
             raise ValueError(f"model output {self.H}x{self.W} must equal the calibration's input image size "
-                             f"{bev.input_width}x{bev.input_height} (bev.py:304)")
+                             f"{bev.input_width}x{bev.input_height} (bev.py:169)")
         if streams < 1:
             raise ValueError("streams must be >= 1")
         self.streams = streams
@@ -53,21 +59,33 @@ class OccupancyPipeline:
         if self._x is None or self._x.shape[0] != B or self._x.device != dev:
             self._x = torch.empty((B, self.H, self.W, 3), dtype=torch.uint8, device=dev)   # resized BGR
             self._seg = torch.empty((B, self.H, self.W), dtype=torch.uint8, device=dev)
-            p = self.bev.occupancy_params(*self.grid, ros_layout=self.ros_layout)
-            shape = (B, p.occ_w, p.occ_h) if self.ros_layout else (B, p.occ_h, p.occ_w)
-            self._grid = torch.empty(shape, dtype=torch.int8, device=dev)
+            self._grid = torch.empty(self._grid_shape(B), dtype=torch.int8, device=dev)
         return self._x, self._seg, self._grid
+
+    def _params(self):
+        return self.bev.occupancy_params(*self.grid, ros_layout=self.ros_layout, binary=self.binary)
+
+    def _grid_shape(self, B):
+        p = self._params()
+        shape = (B, p.occ_w, p.occ_h) if self.ros_layout else (B, p.occ_h, p.occ_w)
+        return ((2,) + shape) if self.binary and p.laserscan else shape
 
     def run(self, frames_bgr: torch.Tensor, out: torch.Tensor | None = None) -> torch.Tensor:
         if frames_bgr.dim() != 4 or frames_bgr.shape[3] != 3 or frames_bgr.dtype != torch.uint8 or not frames_bgr.is_cuda:
             raise ValueError("frames must be a (B, H0, W0, 3) uint8 device tensor")
         B, H0, W0 = frames_bgr.shape[:3]
         x, seg, grid = self._bufs(B, frames_bgr.device)
+        if grid.shape != self._grid_shape(B):       # the calibration's laserscan flag changed
+            self._grid = grid = torch.empty(self._grid_shape(B), dtype=torch.int8, device=frames_bgr.device)
         frames = frames_bgr.contiguous()
         out = grid if out is None else out
+        if tuple(out.shape) != tuple(grid.shape) or out.dtype != torch.int8 or not out.is_contiguous():
+            raise ValueError(f"out must be a contiguous int8 tensor of shape {tuple(grid.shape)}")
+        p = self._params()
         if self.streams == 1 or B < self.streams:
-            self._run_shard(self.model.ctx, frames, x, seg, out, None)
+            self._run_shard(self.model.ctx, frames, x, seg, out, p, None)
             return out
+        pair = self.binary and bool(p.laserscan)
         ctxs, streams = self._shard_ctxs(frames.device)
         main = torch.cuda.current_stream(frames.device)
         ready = main.record_event()
@@ -78,10 +96,25 @@ class OccupancyPipeline:
             if i:
                 st.wait_event(ready)
             with torch.cuda.stream(st):
-                self._run_shard(ctxs[i], frames[s:e], x[s:e], seg[s:e], out[s:e], st)
+                if pair:
+                    # the kernel writes a shard's pair as one contiguous (2, e - s, ...) block; the
+                    # batch's pair (2, B, ...) holds it as two slabs, so stage it and copy
+                    tmp = self._pair_buf(i, (2, e - s) + tuple(out.shape[2:]), out.device)
+                    self._run_shard(ctxs[i], frames[s:e], x[s:e], seg[s:e], tmp, p, st)
+                    out[:, s:e].copy_(tmp)
+                else:
+                    self._run_shard(ctxs[i], frames[s:e], x[s:e], seg[s:e], out[s:e], p, st)
         for st in streams[: self.streams - 1]:
             main.wait_stream(st)
         return out
+
+    def _pair_buf(self, i, shape, dev):
+        if not hasattr(self, "_pairs"):
+            self._pairs = {}
+        t = self._pairs.get(i)
+        if t is None or tuple(t.shape) != shape or t.device != dev:
+            t = self._pairs[i] = torch.empty(shape, dtype=torch.int8, device=dev)
+        return t
 
     def capture(self, frames_bgr: torch.Tensor, out: torch.Tensor | None = None):
         """Record one ``run`` over these frame / output buffers as a HIP graph (every shard's launches
@@ -96,12 +129,12 @@ class OccupancyPipeline:
             res = self.run(frames_bgr, out)
         return graph.replay, res
 
-    def _run_shard(self, ctx, frames, x, seg, out, stream):
+    def _run_shard(self, ctx, frames, x, seg, out, p, stream):
         B, H0, W0 = frames.shape[:3]
         if (H0, W0) != (self.H, self.W):
             # resize only (models.py:87); colour swap + normalisation are fused into the initial block
             ctx.preprocess(frames, B, H0, W0, self.H, self.W, N.PRE_BGR_U8, x, stream)
             frames = x
-        ctx.forward_bgr(frames, B, self.H, self.W, N.OUT_CLASS3_U8, seg, stream)
-        p = self.bev.occupancy_params(*self.grid, ros_layout=self.ros_layout)
-        N.shared_context(frames.device.index).bev(seg, B, p, out, stream)
+        ctx.forward_bgr(frames, B, self.H, self.W, N.OUT_BINARY_U8 if self.binary else N.OUT_CLASS3_U8, seg, stream)
+        # the shard's own context: its laserscan scratch is never shared with another shard's stream
+        ctx.bev(seg, B, p, out, stream)

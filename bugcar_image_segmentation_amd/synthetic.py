@@ -5,7 +5,7 @@ the workload is synthetic with fixed seeds:
   * frames: uniform u8 (default_rng(0)) or a structured "road scene" (horizontal bands with
     gradients and noise) so the class maps are not degenerate;
   * calibration: input image size [480, 640] (rows, cols — the reference's assert convention,
-    bev.py:304), output size [1000, 1000], cm_per_px 1.0, homography from a 4-point solve mapping a
+    bev.py:169), output size [1000, 1000], cm_per_px 1.0, homography from a 4-point solve mapping a
     road trapezoid of the camera image onto the BEV image.
 """
 from __future__ import annotations

@@ -13,7 +13,12 @@
  *  - `stream` is a hipStream_t (NULL = the legacy default stream). All work of one call is
  *    enqueued on it; calls return without synchronising.
  *  - Return 0 on success or a negative BUGSEG_E* code; bugseg_last_error() explains it.
- *  - One context per device. Calls on one context must be serialised by the caller.
+ *  - Calls on one context must not overlap in time from several host threads.
+ *  - A context's forward activation arena is ONE set of buffers: ENet forwards of one context must
+ *    all be enqueued on one stream (run concurrent frame shards on one context each, as
+ *    pipeline.py does). bugseg_bev_occgrid keeps its laserscan scratch per stream, so BEV calls of
+ *    one context may be enqueued on several streams at once. Any reallocation of a table, scratch
+ *    or arena first synchronises the device, so nothing in flight on any stream reads freed memory.
  *  - Tensor shapes: activations are NHWC. The "engine input" tensor is (B, H, W, 8): RGB plus 5
  *    zero channels, in the context precision (f32 or bf16).
  */
@@ -31,7 +36,7 @@ typedef struct bugseg_ctx bugseg_ctx;
 
 enum {
     BUGSEG_OK = 0,
-    BUGSEG_EINVAL = -1,   /* bad argument / shape (reference: AssertionError, bev.py:304)     */
+    BUGSEG_EINVAL = -1,   /* bad argument / shape (reference: AssertionError, bev.py:169)     */
     BUGSEG_ENOMEM = -2,
     BUGSEG_EHIP = -3,     /* HIP runtime error                                                 */
     BUGSEG_EFORMAT = -4,  /* malformed weight blob (reference: GraphDef ParseFromString error)  */
@@ -57,29 +62,29 @@ enum {
                                    bugseg_enet_forward_bgr, which fuses the rest of preprocess    */
 };
 
-/* Geometry of bev_transform_tools.create_occupancy_grid (bev.py:301-330), computed on the host
+/* Geometry of bev_transform_tools.create_occupancy_grid (bev.py:166-195), computed on the host
  * by the Python shim exactly as the reference computes it. */
 typedef struct {
-    double M[9];        /* forward bev matrix, row-major (bev.py:175 _bev_matrix)                */
-    int in_rows;        /* segmap rows  (== "input image size"[0], assert at bev.py:304)        */
+    double M[9];        /* forward bev matrix, row-major (bev.py:182 _bev_matrix)                */
+    int in_rows;        /* segmap rows  (== "input image size"[0], assert at bev.py:169)        */
     int in_cols;        /* segmap cols  (== "input image size"[1])                               */
-    int warp_w;         /* after_warp_width  (bev.py:313; dsize of warpPerspective, bev.py:317)  */
-    int warp_h;         /* after_warp_height (bev.py:314)                                        */
-    int occ_w_px;       /* bev.py:309 */
-    int occ_h_px;       /* bev.py:311 */
-    int occ_w;          /* bev.py:308 grid cells across */
-    int occ_h;          /* bev.py:310 grid cells down   */
-    int left_x;         /* bev.py:318 */
-    int top_y;          /* bev.py:319 */
+    int warp_w;         /* after_warp_width  (bev.py:178; dsize of warpPerspective, bev.py:182)  */
+    int warp_h;         /* after_warp_height (bev.py:179)                                        */
+    int occ_w_px;       /* bev.py:174 */
+    int occ_h_px;       /* bev.py:176 */
+    int occ_w;          /* bev.py:173 grid cells across */
+    int occ_h;          /* bev.py:175 grid cells down   */
+    int left_x;         /* bev.py:183 */
+    int top_y;          /* bev.py:184 */
     int ros_layout;     /* 0: reference (occ_h, occ_w) grid; 1: ROS data order = flip(0)+rot90ccw
                            of it, (occ_w, occ_h) row-major (occgrid_to_ros.py:18-25)            */
-    int variant;        /* 0: create_occupancy_grid (bev.py:301-381): occupied = template {1,3},
+    int variant;        /* 0: create_occupancy_grid (bev.py:166-246): occupied = template {1,3},
                               encoding {0:-1, 1:100, 2:0, 3:100};
                            1: create_occupancy_grid_binary (bev.py:97-165): occupied = {1}, the
                               reference's uint8 encoding {0:-1, 1:100, 2:0, 3:-100}               */
     int laserscan;      /* 1: laserscan-like mode ("is_laserscan", bev.py:37): variant 0 keeps only the
                               obstacle cells nearest the vehicle along each polar ray, the rest of
-                              the obstacles become unknown (bev.py:351-375); variant 1 returns TWO
+                              the obstacles become unknown (bev.py:216-240); variant 1 returns TWO
                               grids per frame, out_dev = (2, B, ...): the encoded grid, then the
                               polar re-projection of its nearest obstacles (bev.py:143-164)        */
 } bugseg_bev_params;
@@ -130,9 +135,9 @@ int bugseg_enet_forward_bgr(bugseg_ctx *ctx, const uint8_t *bgr_dev, int B, int 
 
 /* Fused BEV rasteriser over a batch of class maps: seg_dev (B, in_rows, in_cols) u8
  * -> out_dev (B, occ_h, occ_w) int8 (or the ROS layout, see ros_layout).
- * Replaces bev_transform_tools.create_occupancy_grid (bev.py:301-381) or, with variant = 1,
+ * Replaces bev_transform_tools.create_occupancy_grid (bev.py:166-246) or, with variant = 1,
  * create_occupancy_grid_binary (bev.py:97-165), either branch (p->laserscan). The laserscan mode
- * keeps polar tables per geometry and scratch per batch in the context. */
+ * keeps polar tables per geometry in the context and its batch scratch per (context, stream). */
 int bugseg_bev_occgrid(bugseg_ctx *ctx, const uint8_t *seg_dev, int B, const bugseg_bev_params *p,
                        int8_t *out_dev, void *stream);
 

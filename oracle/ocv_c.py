@@ -82,7 +82,7 @@ def resize_linear(src, dsize):
 
 
 def occgrid_geometry(after_warp_w, after_warp_h, cm_per_px, grid_w_m, grid_h_m, cell_m):
-    """bev.py:307-319 restated (host float arithmetic + int() truncation)."""
+    """bev.py:172-184 restated (host float arithmetic + int() truncation)."""
     cell_px = cell_m * 100 / cm_per_px
     occ_w = int(grid_w_m / cell_m)
     occ_w_px = int(occ_w * cell_px)
@@ -94,7 +94,7 @@ def occgrid_geometry(after_warp_w, after_warp_h, cm_per_px, grid_w_m, grid_h_m, 
 
 
 def create_occupancy_grid(segmap, M, after_warp_w, after_warp_h, cm_per_px, grid_w_m, grid_h_m, cell_m):
-    """bev.py:301-381 (non-laserscan) via the C restatement -> int8 (occ_h, occ_w)."""
+    """bev.py:166-246 (non-laserscan) via the C restatement -> int8 (occ_h, occ_w)."""
     seg = np.ascontiguousarray(segmap, np.uint8)
     g = occgrid_geometry(after_warp_w, after_warp_h, cm_per_px, grid_w_m, grid_h_m, cell_m)
     out = np.empty((g["occ_h"], g["occ_w"]), np.int8)
@@ -120,7 +120,7 @@ def create_occupancy_grid_binary(segmap, M, after_warp_w, after_warp_h, cm_per_p
 
 
 def create_occupancy_grid_laserscan(segmap, M, after_warp_w, after_warp_h, cm_per_px, grid_w_m, grid_h_m, cell_m):
-    """bev.py:301-381 with is_laserscan (polar branch bev.py:351-375) via the C restatement."""
+    """bev.py:166-246 with is_laserscan (polar branch bev.py:216-240) via the C restatement."""
     seg = np.ascontiguousarray(segmap, np.uint8)
     g = occgrid_geometry(after_warp_w, after_warp_h, cm_per_px, grid_w_m, grid_h_m, cell_m)
     out = np.empty((g["occ_h"], g["occ_w"]), np.int8)

@@ -3,7 +3,7 @@
 NumPy restatement of the OpenCV 4.x primitives on the reference hot path, written
 independently of ``ocv_ref.c`` so the two restatements cross-check each other, and a
 restatement of ``bev_transform_tools.create_occupancy_grid`` that follows the reference's
-own array flow (full warped image, then the crop/pad slicing of bev.py:318-330) rather than
+own array flow (full warped image, then the crop/pad slicing of bev.py:183-195) rather than
 the coordinate-shift form the C oracle and the HIP kernel use.
 
 Parity status: UNPINNED against OpenCV/TensorFlow (neither is installed, the reference holds
@@ -19,7 +19,7 @@ INTER_TAB_SIZE = 1 << INTER_BITS
 
 
 def invert3x3(M: np.ndarray) -> np.ndarray:
-    """cv::invert DECOMP_LU closed-form 3x3 branch (used by warpPerspective, bev.py:317)."""
+    """cv::invert DECOMP_LU closed-form 3x3 branch (used by warpPerspective, bev.py:182)."""
     S = np.asarray(M, dtype=np.float64).reshape(3, 3)
     d = (S[0, 0] * (S[1, 1] * S[2, 2] - S[1, 2] * S[2, 1])
          - S[0, 1] * (S[1, 0] * S[2, 2] - S[1, 2] * S[2, 0])
@@ -163,61 +163,61 @@ def resize_linear(src: np.ndarray, dsize: tuple[int, int]) -> np.ndarray:
 
 def create_occupancy_grid(segmap: np.ndarray, M: np.ndarray, after_warp_w: int, after_warp_h: int,
                           cm_per_px: float, grid_w_m: float, grid_h_m: float, cell_m: float) -> np.ndarray:
-    """Restates bev.py:301-381 (non-laserscan branch) step by step on the arrays it builds."""
-    cell_px = cell_m * 100 / cm_per_px                                   # bev.py:307
-    occ_w = int(grid_w_m / cell_m)                                       # bev.py:308
-    occ_w_px = int(occ_w * cell_px)                                      # bev.py:309
-    occ_h = int(grid_h_m / cell_m)                                       # bev.py:310
-    occ_h_px = int(occ_h * cell_px)                                      # bev.py:311
-    lifted = np.add(segmap, 1).astype(np.uint8)                          # bev.py:312
-    warped = warp_perspective(lifted, M, (after_warp_w, after_warp_h))   # bev.py:317
-    left_x = int((after_warp_w - occ_w_px) / 2)                          # bev.py:318
-    top_y = after_warp_h - occ_h_px                                      # bev.py:319
-    wlx = int(np.clip(left_x, 0, np.inf))                                # bev.py:320
-    warped = warped[int(np.clip(top_y, 0, np.inf)):after_warp_h, wlx:wlx + occ_w_px]   # bev.py:321
-    glx = int(np.clip(-left_x, 0, np.inf))                               # bev.py:323
-    gty = int(np.clip(-top_y, 0, np.inf))                                # bev.py:324
-    tmpl = np.zeros((occ_h_px, occ_w_px))                                # bev.py:325
-    tmpl[gty:occ_h_px, glx:glx + warped.shape[1]] = warped               # bev.py:327
-    tmpl = tmpl.astype(np.uint8)                                         # bev.py:330
-    occ = np.logical_or(tmpl == 1, tmpl == 3).astype(np.uint8)           # bev.py:331
-    opened = morph_open3x3(occ)                                          # bev.py:333
-    mask1 = (opened > 0).astype(np.uint8)                                # bev.py:338
-    sub = np.clip(occ.astype(np.int16) - mask1, 0, 255)                  # bev.py:339 cv2.subtract saturates
-    tmpl = np.where(sub > 0, 2, tmpl).astype(np.uint8)                   # bev.py:340
-    tmpl = resize_nearest(tmpl, (occ_w, occ_h))                          # bev.py:344
-    new = np.where(tmpl == 3, 1, tmpl)                                   # bev.py:377
-    return np.where(new == 0, -1, 200 - new.astype(np.int64) * 100).astype(np.int8)   # bev.py:379
+    """Restates bev.py:166-246 (non-laserscan branch) step by step on the arrays it builds."""
+    cell_px = cell_m * 100 / cm_per_px                                   # bev.py:172
+    occ_w = int(grid_w_m / cell_m)                                       # bev.py:173
+    occ_w_px = int(occ_w * cell_px)                                      # bev.py:174
+    occ_h = int(grid_h_m / cell_m)                                       # bev.py:175
+    occ_h_px = int(occ_h * cell_px)                                      # bev.py:176
+    lifted = np.add(segmap, 1).astype(np.uint8)                          # bev.py:177
+    warped = warp_perspective(lifted, M, (after_warp_w, after_warp_h))   # bev.py:182
+    left_x = int((after_warp_w - occ_w_px) / 2)                          # bev.py:183
+    top_y = after_warp_h - occ_h_px                                      # bev.py:184
+    wlx = int(np.clip(left_x, 0, np.inf))                                # bev.py:185
+    warped = warped[int(np.clip(top_y, 0, np.inf)):after_warp_h, wlx:wlx + occ_w_px]   # bev.py:186
+    glx = int(np.clip(-left_x, 0, np.inf))                               # bev.py:188
+    gty = int(np.clip(-top_y, 0, np.inf))                                # bev.py:189
+    tmpl = np.zeros((occ_h_px, occ_w_px))                                # bev.py:190
+    tmpl[gty:occ_h_px, glx:glx + warped.shape[1]] = warped               # bev.py:192
+    tmpl = tmpl.astype(np.uint8)                                         # bev.py:195
+    occ = np.logical_or(tmpl == 1, tmpl == 3).astype(np.uint8)           # bev.py:196
+    opened = morph_open3x3(occ)                                          # bev.py:198
+    mask1 = (opened > 0).astype(np.uint8)                                # bev.py:203
+    sub = np.clip(occ.astype(np.int16) - mask1, 0, 255)                  # bev.py:204 cv2.subtract saturates
+    tmpl = np.where(sub > 0, 2, tmpl).astype(np.uint8)                   # bev.py:205
+    tmpl = resize_nearest(tmpl, (occ_w, occ_h))                          # bev.py:209
+    new = np.where(tmpl == 3, 1, tmpl)                                   # bev.py:242
+    return np.where(new == 0, -1, 200 - new.astype(np.int64) * 100).astype(np.int8)   # bev.py:244
 
 
 def create_occupancy_grid_binary(segmap: np.ndarray, M: np.ndarray, after_warp_w: int, after_warp_h: int,
                                  cm_per_px: float, grid_w_m: float, grid_h_m: float, cell_m: float) -> np.ndarray:
     """Restates bev.py:97-165 (legacy binary variant, non-laserscan branch) on the arrays it builds.
     Its uint8 arithmetic is NumPy 1.x's (value-based casting, wrap-around), emulated explicitly."""
-    cell_px = cell_m * 100 / cm_per_px                                   # bev.py:101
-    occ_w = int(grid_w_m / cell_m)                                       # bev.py:102
-    occ_w_px = int(occ_w * cell_px)                                      # bev.py:103
-    occ_h = int(grid_h_m / cell_m)                                       # bev.py:104
-    occ_h_px = int(occ_h * cell_px)                                      # bev.py:105
-    lifted = np.add(segmap, 1).astype(np.uint8)                          # bev.py:106
-    warped = warp_perspective(lifted, M, (after_warp_w, after_warp_h))   # bev.py:112
-    left_x = int((after_warp_w - occ_w_px) / 2)                          # bev.py:113
-    top_y = after_warp_h - occ_h_px                                      # bev.py:114
-    wlx = int(np.clip(left_x, 0, np.inf))                                # bev.py:115
-    warped = warped[int(np.clip(top_y, 0, np.inf)):after_warp_h, wlx:wlx + occ_w_px]   # bev.py:116
-    glx = int(np.clip(-left_x, 0, np.inf))                               # bev.py:118
-    gty = int(np.clip(-top_y, 0, np.inf))                                # bev.py:119
-    tmpl = np.zeros((occ_h_px, occ_w_px))                                # bev.py:120
-    tmpl[gty:occ_h_px, glx:glx + warped.shape[1]] = warped               # bev.py:122-124
-    tmpl = tmpl.astype(np.uint8)                                         # bev.py:125
-    occ = (tmpl == 1).astype(np.uint8)                                   # bev.py:126
-    opened = morph_open3x3(occ)                                          # bev.py:128-129
-    mask1 = (opened > 0).astype(np.uint8)                                # bev.py:131
-    sub = np.clip(occ.astype(np.int16) - mask1, 0, 255)                  # bev.py:132 cv2.subtract saturates
-    tmpl = np.where(sub > 0, 2, tmpl).astype(np.uint8)                   # bev.py:133
-    og = (resize_nearest(tmpl, (occ_w, occ_h)).astype(np.int64) * 100) % 256   # bev.py:137-139: uint8 * 100 wraps
-    r = np.where(og == 0, -1, (200 - og) % 256)                          # bev.py:140 (uint8 200 - og)
-    return (r % 256).astype(np.uint8).astype(np.int8)                    # bev.py:141, :165
+    cell_px = cell_m * 100 / cm_per_px                                   # bev.py:103
+    occ_w = int(grid_w_m / cell_m)                                       # bev.py:104
+    occ_w_px = int(occ_w * cell_px)                                      # bev.py:105
+    occ_h = int(grid_h_m / cell_m)                                       # bev.py:106
+    occ_h_px = int(occ_h * cell_px)                                      # bev.py:107
+    lifted = np.add(segmap, 1).astype(np.uint8)                          # bev.py:108
+    warped = warp_perspective(lifted, M, (after_warp_w, after_warp_h))   # bev.py:114
+    left_x = int((after_warp_w - occ_w_px) / 2)                          # bev.py:115
+    top_y = after_warp_h - occ_h_px                                      # bev.py:116
+    wlx = int(np.clip(left_x, 0, np.inf))                                # bev.py:117
+    warped = warped[int(np.clip(top_y, 0, np.inf)):after_warp_h, wlx:wlx + occ_w_px]   # bev.py:118-119
+    glx = int(np.clip(-left_x, 0, np.inf))                               # bev.py:120
+    gty = int(np.clip(-top_y, 0, np.inf))                                # bev.py:121
+    tmpl = np.zeros((occ_h_px, occ_w_px))                                # bev.py:122
+    tmpl[gty:occ_h_px, glx:glx + warped.shape[1]] = warped               # bev.py:124-126
+    tmpl = tmpl.astype(np.uint8)                                         # bev.py:127
+    occ = (tmpl == 1).astype(np.uint8)                                   # bev.py:128
+    opened = morph_open3x3(occ)                                          # bev.py:130-131
+    mask1 = (opened > 0).astype(np.uint8)                                # bev.py:133
+    sub = np.clip(occ.astype(np.int16) - mask1, 0, 255)                  # bev.py:134 cv2.subtract saturates
+    tmpl = np.where(sub > 0, 2, tmpl).astype(np.uint8)                   # bev.py:135
+    og = (resize_nearest(tmpl, (occ_w, occ_h)).astype(np.int64) * 100) % 256   # bev.py:139-142: uint8 * 100 wraps
+    r = np.where(og == 0, -1, (200 - og) % 256)                          # bev.py:143-144 (uint8 200 - og)
+    return (r % 256).astype(np.uint8).astype(np.int8)                    # bev.py:144, :165
 
 
 def ros_layout(grid: np.ndarray) -> np.ndarray:
@@ -226,7 +226,7 @@ def ros_layout(grid: np.ndarray) -> np.ndarray:
     return np.ascontiguousarray(np.rot90(flipped, 1))
 
 
-# ---- laserscan-like occupancy (bev.py:351-375, binary variant bev.py:143-164) -----------------------
+# ---- laserscan-like occupancy (bev.py:216-240, binary variant bev.py:143-164) -----------------------
 
 CV_PI = 3.1415926535897932384626433832795
 _F = np.float32
@@ -322,7 +322,7 @@ def _group_min(rows: np.ndarray, cols: np.ndarray):
 
 
 def _template_cells(segmap, M, after_warp_w, after_warp_h, cm_per_px, grid_w_m, grid_h_m, cell_m, binary):
-    """The array flow of bev.py:301-347 (or :97-138 binary) up to the NN resize."""
+    """The array flow of bev.py:166-212 (or :97-138 binary) up to the NN resize."""
     cell_px = cell_m * 100 / cm_per_px
     occ_w = int(grid_w_m / cell_m)
     occ_w_px = int(occ_w * cell_px)
@@ -347,37 +347,37 @@ def _template_cells(segmap, M, after_warp_w, after_warp_h, cm_per_px, grid_w_m, 
 
 
 def create_occupancy_grid_laserscan(segmap, M, after_warp_w, after_warp_h, cm_per_px, grid_w_m, grid_h_m, cell_m):
-    """Restates bev.py:301-381 with is_laserscan (the polar branch, bev.py:351-375)."""
+    """Restates bev.py:166-246 with is_laserscan (the polar branch, bev.py:216-240)."""
     t = _template_cells(segmap, M, after_warp_w, after_warp_h, cm_per_px, grid_w_m, grid_h_m, cell_m, False)
-    shape = (t.shape[1], t.shape[0])                                                # bev.py:353
-    longer = max(shape[0], shape[1])                                                # bev.py:354
+    shape = (t.shape[1], t.shape[0])                                                # bev.py:217
+    longer = max(shape[0], shape[1])                                                # bev.py:218
     center = (shape[0] / 2 - 1, shape[1])
-    polar = warp_polar(t, (-1, -1), center, longer)                                 # bev.py:355
-    empty = np.zeros(polar.shape)                                                   # bev.py:360
-    pts = np.where(polar == 3)                                                      # bev.py:363
-    keys, mins = _group_min(pts[0], pts[1])                                         # bev.py:364-365
-    for i, mx in enumerate(mins):                                                   # bev.py:368-369
+    polar = warp_polar(t, (-1, -1), center, longer)                                 # bev.py:219
+    empty = np.zeros(polar.shape)                                                   # bev.py:224
+    pts = np.where(polar == 3)                                                      # bev.py:227
+    keys, mins = _group_min(pts[0], pts[1])                                         # bev.py:229
+    for i, mx in enumerate(mins):                                                   # bev.py:232-233
         empty = circle_filled_r1(empty, (mx, keys[i]), 1)
-    new = warp_polar(empty, shape, center, longer, inverse=True)                    # bev.py:371
-    new = np.where(t != 3, t, new)                                                  # bev.py:372
-    return np.where(new == 0, -1, 200 - new * 100).astype(np.int8)                  # bev.py:379
+    new = warp_polar(empty, shape, center, longer, inverse=True)                    # bev.py:235
+    new = np.where(t != 3, t, new)                                                  # bev.py:236
+    return np.where(new == 0, -1, 200 - new * 100).astype(np.int8)                  # bev.py:244
 
 
 def create_occupancy_grid_binary_laserscan(segmap, M, after_warp_w, after_warp_h, cm_per_px, grid_w_m, grid_h_m,
                                            cell_m):
     """Restates bev.py:97-165 with is_laserscan (bev.py:143-164) -> (grid int8, new int8)."""
     t = _template_cells(segmap, M, after_warp_w, after_warp_h, cm_per_px, grid_w_m, grid_h_m, cell_m, True)
-    og = (t.astype(np.int64) * 100) % 256                                           # bev.py:135-138 (uint8)
-    og = ((np.where(og == 0, -1, (200 - og) % 256)) % 256).astype(np.uint8)          # bev.py:139-140
-    shape = (og.shape[1], og.shape[0])                                              # bev.py:144
-    longer = max(shape[0], shape[1])                                                # bev.py:145
+    og = (t.astype(np.int64) * 100) % 256                                           # bev.py:139-142 (uint8)
+    og = ((np.where(og == 0, -1, (200 - og) % 256)) % 256).astype(np.uint8)          # bev.py:143-144
+    shape = (og.shape[1], og.shape[0])                                              # bev.py:146
+    longer = max(shape[0], shape[1])                                                # bev.py:147
     center = (og.shape[1] / 2 - 1, og.shape[0])
-    polar = warp_polar(og, shape, center, longer)                                   # bev.py:146
-    empty = np.zeros(polar.shape)                                                   # bev.py:150
-    vc = np.where(polar == 100)                                                     # bev.py:152
-    keys, mins = _group_min(vc[0], vc[1])                                           # bev.py:153-154
-    for i, mx in enumerate(mins):                                                   # bev.py:155-156
+    polar = warp_polar(og, shape, center, longer)                                   # bev.py:148
+    empty = np.zeros(polar.shape)                                                   # bev.py:152
+    vc = np.where(polar == 100)                                                     # bev.py:154
+    keys, mins = _group_min(vc[0], vc[1])                                           # bev.py:155-156
+    for i, mx in enumerate(mins):                                                   # bev.py:157-158
         empty = circle_filled_r1(empty, (mx, keys[i]), 100)
-    new = warp_polar(empty, shape, center, longer, inverse=True).astype(np.int8)   # bev.py:158-159
-    new[og == 255] = -1                                                             # bev.py:161
-    return og.astype(np.int8), new                                                  # bev.py:162
+    new = warp_polar(empty, shape, center, longer, inverse=True).astype(np.int8)   # bev.py:160-161
+    new[og == 255] = -1                                                             # bev.py:163
+    return og.astype(np.int8), new                                                  # bev.py:164

@@ -30,7 +30,7 @@ static inline uint8_t sat_u8(int v) { return (uint8_t)(v < 0 ? 0 : (v > 255 ? 25
 
 /* cv::invert(M, M) with the default DECOMP_LU: the closed-form 3x3 double branch of
  * lapack.cpp (det3 + cofactors * 1/det). Used by warpPerspective without WARP_INVERSE_MAP
- * (bev.py:317 passes the forward bev matrix). Returns 0 when det == 0 (OpenCV zeroes M). */
+ * (bev.py:182 passes the forward bev matrix). Returns 0 when det == 0 (OpenCV zeroes M). */
 int ocv_invert3x3(const double *S, double *t)
 {
 #define m(i, j) S[(i) * 3 + (j)]
@@ -236,16 +236,16 @@ int ocv_resize_linear_u8(const uint8_t *src, int sh, int sw, int cn, uint8_t *ds
     return 0;
 }
 
-/* bev_transform_tools.create_occupancy_grid, non-laserscan branch (bev.py:301-381):
- *   t  = warpPerspective(segmap + 1, M, (Wb, Hb))                     bev.py:312,317
- *   template[ty][tx] = t[ty+top_y][tx+left_x] (0 outside)             bev.py:318-330
- *   occ = (template==1)|(template==3); open 3x3; template[occ&!open]=2 bev.py:331-340
- *   g = resize_nearest(template, (occ_w, occ_h))                      bev.py:344-347
- *   g = where(g==3, 1, g); out = where(g==0, -1, 200-100*g) as int8    bev.py:377-380
- * The crop/pad of bev.py:318-330 is restated as the equivalent coordinate shift.
+/* bev_transform_tools.create_occupancy_grid, non-laserscan branch (bev.py:166-246):
+ *   t  = warpPerspective(segmap + 1, M, (Wb, Hb))                     bev.py:177,182
+ *   template[ty][tx] = t[ty+top_y][tx+left_x] (0 outside)             bev.py:183-195
+ *   occ = (template==1)|(template==3); open 3x3; template[occ&!open]=2 bev.py:196-205
+ *   g = resize_nearest(template, (occ_w, occ_h))                      bev.py:209-212
+ *   g = where(g==3, 1, g); out = where(g==0, -1, 200-100*g) as int8    bev.py:242-245
+ * The crop/pad of bev.py:183-195 is restated as the equivalent coordinate shift.
  * segmap is (hin, win) u8 class ids {0,1,2}; M is the forward bev matrix. */
 /* The template cells both rasterisers share: warp + crop/pad + opening + NN resize, before the
- * encoding. binary = 0: occupied set {1, 3} (bev.py:331-340); 1: {1} (bev.py:126). */
+ * encoding. binary = 0: occupied set {1, 3} (bev.py:196-205); 1: {1} (bev.py:128). */
 int bev_template_cells_ref(const uint8_t *segmap, int hin, int win, const double *M, int Wb, int Hb,
                            int occ_w_px, int occ_h_px, int occ_w, int occ_h, int left_x, int top_y, int binary,
                            uint8_t *cells)
@@ -256,22 +256,22 @@ int bev_template_cells_ref(const uint8_t *segmap, int hin, int win, const double
     uint8_t *occ = (uint8_t *)malloc((size_t)occ_h_px * occ_w_px);
     uint8_t *opened = (uint8_t *)malloc((size_t)occ_h_px * occ_w_px);
     if (!lifted || !tmpl || !occ || !opened) return -1;
-    for (size_t i = 0; i < n; i++) lifted[i] = (uint8_t)(segmap[i] + 1);                      /* bev.py:312 / :107 */
+    for (size_t i = 0; i < n; i++) lifted[i] = (uint8_t)(segmap[i] + 1);                      /* bev.py:177 / :108 */
     double Mi[9];
     ocv_invert3x3(M, Mi);
     int bw0 = warp_bw0(Hb, Wb);
     for (int ty = 0; ty < occ_h_px; ty++)
         for (int tx = 0; tx < occ_w_px; tx++) {
-            int wy = ty + top_y, wx = tx + left_x;                                                /* bev.py:318-330 */
+            int wy = ty + top_y, wx = tx + left_x;                                                /* bev.py:183-195 */
             uint8_t v = 0;
             if (wy >= 0 && wy < Hb && wx >= 0 && wx < Wb) v = warp_px(lifted, hin, win, Mi, wx, wy, bw0);
             tmpl[(size_t)ty * occ_w_px + tx] = v;
             occ[(size_t)ty * occ_w_px + tx] = (uint8_t)(binary ? v == 1 : (v == 1 || v == 3));
         }
-    ocv_morph_open3x3_u8(occ, occ_h_px, occ_w_px, opened);                                        /* bev.py:335 / :128 */
+    ocv_morph_open3x3_u8(occ, occ_h_px, occ_w_px, opened);                                        /* bev.py:198 / :130 */
     for (size_t i = 0; i < (size_t)occ_h_px * occ_w_px; i++)
         if (occ[i] && !opened[i]) tmpl[i] = 2;
-    ocv_resize_nearest_u8(tmpl, occ_h_px, occ_w_px, 1, cells, occ_h, occ_w);                      /* bev.py:344 / :135 */
+    ocv_resize_nearest_u8(tmpl, occ_h_px, occ_w_px, 1, cells, occ_h, occ_w);                      /* bev.py:209 / :139 */
     free(lifted); free(tmpl); free(occ); free(opened);
     return 0;
 }
@@ -284,7 +284,7 @@ int bev_occgrid_ref(const uint8_t *segmap, int hin, int win, const double *M, in
     if (bev_template_cells_ref(segmap, hin, win, M, Wb, Hb, occ_w_px, occ_h_px, occ_w, occ_h, left_x, top_y, 0, cells))
         return -1;
     for (size_t i = 0; i < (size_t)occ_h * occ_w; i++) {
-        int g = cells[i] == 3 ? 1 : cells[i];                                                     /* bev.py:377-380 */
+        int g = cells[i] == 3 ? 1 : cells[i];                                                     /* bev.py:242-245 */
         out[i] = (int8_t)(g == 0 ? -1 : 200 - 100 * g);
     }
     free(cells);
@@ -293,9 +293,9 @@ int bev_occgrid_ref(const uint8_t *segmap, int hin, int win, const double *M, in
 
 /* bev_transform_tools.create_occupancy_grid_binary (bev.py:97-165, non-laserscan branch; the legacy
  * variant for predict_binary maps). Same warp / crop-pad / opening / NN resize as above, but the
- * occupied set is {1} only (bev.py:126) and the encoding is the reference's uint8 arithmetic under
- * NumPy 1.x casting: g = uint8(cell * 100) (bev.py:135-138), r = g == 0 ? -1 : uint8(200 - g)
- * (bev.py:139-140), out = int8(uint8(r)) (bev.py:140, :165) -> {0:-1, 1:100, 2:0, 3:-100}. */
+ * occupied set is {1} only (bev.py:128) and the encoding is the reference's uint8 arithmetic under
+ * NumPy 1.x casting: g = uint8(cell * 100) (bev.py:139-142), r = g == 0 ? -1 : uint8(200 - g)
+ * (bev.py:143-144), out = int8(uint8(r)) (bev.py:144, :165) -> {0:-1, 1:100, 2:0, 3:-100}. */
 int bev_occgrid_binary_ref(const uint8_t *segmap, int hin, int win, const double *M, int Wb, int Hb,
                            int occ_w_px, int occ_h_px, int occ_w, int occ_h, int left_x, int top_y, int8_t *out)
 {
@@ -312,7 +312,7 @@ int bev_occgrid_binary_ref(const uint8_t *segmap, int hin, int win, const double
     return 0;
 }
 
-/* ---- laserscan-like occupancy (bev.py:351-375; binary variant bev.py:143-164) -------------------
+/* ---- laserscan-like occupancy (bev.py:216-240; binary variant bev.py:143-164) -------------------
  *
  * cv::warpPolar(WARP_POLAR_LINEAR, INTER_NEAREST, no WARP_FILL_OUTLIERS -> BORDER_TRANSPARENT) as
  * imgwarp.cpp (4.x) builds it: float remap tables, then remap() with INTER_NEAREST, which rounds
@@ -415,7 +415,7 @@ static int polar_stamps(const uint8_t *g, int w, int h, int pw, int ph, const in
     return 0;
 }
 
-/* create_occupancy_grid with is_laserscan (bev.py:301-381): the template cells of bev_occgrid_ref,
+/* create_occupancy_grid with is_laserscan (bev.py:166-246): the template cells of bev_occgrid_ref,
  * then warpPolar(cells, (-1,-1), (w/2-1, h), L = max(w, h)) -> (round(L), round(L*pi)) polar image;
  * obstacle value 3; new = cells != 3 ? cells : stamp; out = new == 0 ? -1 : 200 - 100*new. */
 int bev_occgrid_laserscan_ref(const uint8_t *segmap, int hin, int win, const double *M, int Wb, int Hb,

@@ -1,4 +1,4 @@
-# One GPU session: every GPU test, smoke(), the headline bench (ENet -> BEV) and the config-4 bench (DeepLab).
+# One GPU session: every GPU test, smoke(), the headline bench (ENet -> BEV) (with its config-4 DeepLab sub-record).
 set -o pipefail
 cd $GRAFT_REPO_ROOT
 mkdir -p gpurun_out/round
@@ -8,5 +8,4 @@ tail -2 gpurun_out/round/pytest_gpu.log
 timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/round/smoke.txt 2>&1 || { cat gpurun_out/round/smoke.txt; exit 1; }
 cat gpurun_out/round/smoke.txt
 timeout -k 10 300 python bench.py > gpurun_out/round/bench.json 2> gpurun_out/round/bench.err || exit 1
-timeout -k 10 300 python bench_deeplab.py > gpurun_out/round/bench_deeplab.json 2> gpurun_out/round/bench_deeplab.err || exit 1
 echo done

@@ -193,7 +193,7 @@ def test_bev_occgrid_binary_bit_exact(gpu, rows, cols, ww, wh, grid, seed):
     (64, 80, 200, 150, (1.0, 1.6, 0.1), 9),          # tall grid
 ])
 def test_bev_laserscan_bit_exact(gpu, rows, cols, ww, wh, grid, seed):
-    """Laserscan-like mode (bev.py:351-375; binary variant bev.py:143-164) vs the C restatement: the
+    """Laserscan-like mode (bev.py:216-240; binary variant bev.py:143-164) vs the C restatement: the
     per-ray nearest obstacle, the stamped pluses and the re-projection, batched, in both layouts."""
     bev = _bev_case(rows, cols, ww, wh, seed)
     bev.laserscan_like_occupancy_grid = True
@@ -376,6 +376,87 @@ def test_multistream_pipeline_identical(bf16_model):
         many = OccupancyPipeline(bf16_model, bev, 3.0, 3.0, 0.05, model_hw=(H, W), streams=s).run(frames)
         torch.cuda.synchronize()
         assert torch.equal(one, many)
+
+
+@pytest.mark.parametrize("binary", [False, True])
+def test_multistream_pipeline_laserscan(bf16_model, binary):
+    """Laserscan-like mode through OccupancyPipeline with 2 and 3 frame shards on their own streams
+    (B = 10: the uneven 3/3/4 split included), several steps back to back so the shards' kernels
+    overlap each other and the previous step: identical to streams = 1, which is itself equal to the
+    C restatement recomputed from the GPU's own class maps (bev.py:216-240; the binary pairing
+    predict_binary + create_occupancy_grid_binary returns the reference's pair, bev.py:143-164)."""
+    H, W, B = 240, 320, 10
+    ww = wh = 600
+    grid = (6.0, 6.0, 0.05)
+    frames = torch.from_numpy(synthetic.road_frames(B, H, W, seed=12)).cuda()
+    bev = synthetic.synthetic_bev(H, W, ww, wh)
+    bev.laserscan_like_occupancy_grid = True
+    one_pipe = OccupancyPipeline(bf16_model, bev, *grid, model_hw=(H, W), binary=binary)
+    one = one_pipe.run(frames).clone()
+    seg = one_pipe._seg.cpu().numpy()
+    M = bev._bev_matrix
+    if binary:
+        assert set(np.unique(seg).tolist()) <= {0, 1}
+        ref = [ocv_c.create_occupancy_grid_binary_laserscan(c, M, ww, wh, 1.0, *grid) for c in seg]
+        want = np.stack([np.stack([r[0] for r in ref]), np.stack([r[1] for r in ref])])
+    else:
+        want = np.stack([ocv_c.create_occupancy_grid_laserscan(c, M, ww, wh, 1.0, *grid) for c in seg])
+    assert one.shape == want.shape
+    assert np.array_equal(one.cpu().numpy(), want)
+    for s in (2, 3):
+        many = OccupancyPipeline(bf16_model, bev, *grid, model_hw=(H, W), streams=s, binary=binary)
+        outs = [many.run(frames).clone() for _ in range(3)]
+        torch.cuda.synchronize()
+        for o in outs:
+            assert torch.equal(one, o)
+
+
+def test_shared_context_bev_on_two_streams(gpu):
+    """bugseg_bev_occgrid keeps its laserscan scratch per (context, stream): the per-device shared
+    context, driven from two streams at once with batches of different sizes (a larger batch grows
+    its stream's scratch while the other stream's kernels are in flight), gives the single-stream
+    results."""
+    rows, cols, ww, wh, grid = 240, 320, 600, 600, (6.0, 6.0, 0.05)
+    bev = _bev_case(rows, cols, ww, wh, 13)
+    bev.laserscan_like_occupancy_grid = True
+    rng = np.random.default_rng(13)
+    segs = [torch.from_numpy(np.kron(rng.integers(0, 3, size=(b, rows // 4, cols // 4)),
+                                     np.ones((1, 4, 4), np.int64)).astype(np.uint8)).cuda() for b in (6, 16, 4, 24)]
+    want = [bev.create_occupancy_grid_device(s, *grid).clone() for s in segs]
+    torch.cuda.synchronize()
+    sts = [torch.cuda.Stream(), torch.cuda.Stream()]
+    got = []
+    for rep in range(2):
+        for i, s in enumerate(segs):
+            st = sts[i % 2]
+            st.wait_stream(torch.cuda.current_stream())
+            with torch.cuda.stream(st):
+                got.append((i, bev.create_occupancy_grid_device(s, *grid)))
+    torch.cuda.synchronize()
+    for i, g in got:
+        assert torch.equal(g, want[i])
+
+
+def test_config1_reference_resolution_fp32(fp32_model, blocks):
+    """BASELINE config 1: a 512x512 BGR frame -> ENET.preprocess (cv2.resize INTER_LINEAR to
+    512x256, BGR->RGB, (x/256 - mean)/std; models.py:84-95) -> the fp32 forward at the reference's
+    native 256x512 (models.py:19, 42-44) -> logits within 1e-3 of the oracle, class maps (predict and
+    predict_binary, models.py:55-58, 78-80) equal on every pixel whose top-2 margin exceeds 2e-3."""
+    frame = synthetic.road_frames(1, 512, 512, seed=21)[0]
+    x = ENET.preprocess(frame)
+    assert x.shape == (1, 3, 256, 512) and x.dtype == np.float64
+    assert np.array_equal(x, eo.preprocess(frame))
+    ref = eo.forward(blocks, x.astype(np.float32))
+    got = fp32_model.logits(x)
+    assert got.shape == ref.shape == (1, 15, 256, 512)
+    assert np.abs(got - ref).max() < LOGIT_TOL
+    decided = _margin(ref) > MARGIN
+    assert decided.mean() > 0.98
+    cls = eo.argmax_classes(ref)
+    p3 = fp32_model.predict(x)
+    assert p3.shape == (1, 256, 512) and p3.dtype == np.uint8
+    assert (p3[decided] == eo.LUT3[cls][decided]).all()
+    assert (fp32_model.predict_binary(x)[decided] == eo.LUT_BINARY[cls][decided]).all()
 
 
 @pytest.mark.parametrize("streams", [1, 2])

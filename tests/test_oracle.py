@@ -36,7 +36,7 @@ def test_argmax_ties_lowest_index():
 
 
 def test_encoding_non_laserscan():
-    # bev.py:377-380: template {0,1,2,3} -> where(t==3,1,t) -> {0:-1, 1:100, 2:0}
+    # bev.py:242-245: template {0,1,2,3} -> where(t==3,1,t) -> {0:-1, 1:100, 2:0}
     t = np.array([[0, 1, 2, 3]], np.uint8)
     new = np.where(t == 3, 1, t)
     out = np.where(new == 0, -1, 200 - new * 100).astype(np.int8)
@@ -150,7 +150,7 @@ def test_occupancy_grid_binary_c_vs_reference_flow(ww, wh, grid, classes):
         assert (a == -100).any()
 
 
-# ---------------------------------------------------------------- laserscan-like mode (bev.py:351-375)
+# ---------------------------------------------------------------- laserscan-like mode (bev.py:216-240)
 def test_fast_atan_matches_opencv_accuracy_and_quadrants():
     """fastAtan32f: within OpenCV's documented ~0.3 degree of atan2, angles in [0, 2pi), C == NumPy."""
     rng = np.random.default_rng(5)
@@ -206,7 +206,7 @@ def test_laserscan_known_answer_shadow():
 @pytest.mark.parametrize("ww,wh,grid", [(1000, 1000, (10, 10, 0.05)), (900, 700, (10, 8, 0.05)),
                                         (600, 1100, (7.3, 12.1, 0.07)), (400, 300, (12, 12, 0.05))])
 def test_laserscan_c_vs_reference_flow(ww, wh, grid):
-    """bev.py:351-375 (and the binary variant bev.py:143-164): the C restatement (precomputed polar
+    """bev.py:216-240 (and the binary variant bev.py:143-164): the C restatement (precomputed polar
     tables, per-row minimum, stamped pluses) vs the NumPy restatement of the reference's array flow
     (warpPolar images, np.where, group-by-min, cv2.circle, inverse warpPolar)."""
     rng = np.random.default_rng(ww + wh)
