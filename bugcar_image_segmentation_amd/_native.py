@@ -27,7 +27,8 @@ EXPORTED = ("bugseg_version", "bugseg_create", "bugseg_destroy", "bugseg_load_we
             "bugseg_bev_occgrid", "bugseg_plan_info", "bugseg_plan_op", "bugseg_plan_launch_op",
             "bugseg_last_error",
             "bugseg_dl_create", "bugseg_dl_destroy", "bugseg_dl_load_weights", "bugseg_dl_set_plan",
-            "bugseg_dl_forward", "bugseg_dl_launch_op", "bugseg_dl_read_buffer", "bugseg_dl_last_error")
+            "bugseg_dl_forward", "bugseg_dl_launch_op", "bugseg_dl_read_buffer", "bugseg_dl_last_error",
+            "bugseg_debug_parse_pack", "bugseg_debug_polar_tables", "bugseg_dl_debug_check_plan")
 DL_OP_FIELDS = 32
 
 
@@ -87,6 +88,9 @@ def load_library(path: Path | str | None = None) -> ctypes.CDLL:
             "bugseg_dl_launch_op": (i, [vp, i, vp]),
             "bugseg_dl_read_buffer": (i, [vp, i, vp, sz, vp]),
             "bugseg_dl_last_error": (cp, [vp]),
+            "bugseg_debug_parse_pack": (i, [vp, sz, i, ctypes.POINTER(i)]),
+            "bugseg_debug_polar_tables": (i, [i, i, i, vp, sz, vp, sz, ctypes.POINTER(i), ctypes.POINTER(i)]),
+            "bugseg_dl_debug_check_plan": (i, [vp, i, vp, i, i, i, i, i, sz]),
         }
         for name, (res, args) in proto.items():
             f = getattr(lib, name)

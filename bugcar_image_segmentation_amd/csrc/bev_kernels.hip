@@ -3,7 +3,12 @@
 //
 // The reference materialises segmap+1 (bev.py:177), a full warped image (bev.py:182, e.g. 1000x1000),
 // a cropped/padded template (bev.py:183-195), an occupancy mask, its 3x3 opening (bev.py:196-205)
-// and the INTER_NEAREST-downsampled grid (bev.py:209). Here one thread produces one output cell:
+// and the INTER_NEAREST-downsampled grid (bev.py:209). Here one thread produces one output cell.
+// The geometry (which class-map taps, with which Q15 fractions, each template pixel blends) does not
+// depend on the frame: bev_table_kernel evaluates the double-precision inverse mapping ONCE per
+// calibration for the 5x5 window of template pixels around every cell's sample (a [25][cells] table,
+// 8 B per entry, resident across calls), and bev_occgrid_kernel does per frame only byte gathers and
+// integer arithmetic:
 //   * the cell samples ONE template pixel p = (min(floor(cy*ify), h_px-1), min(floor(cx*ifx), w_px-1))
 //     (resizeNN), so only the template values that p depends on are ever computed;
 //   * template(t) = warp(t + (left_x, top_y)) when inside the warped image, else 0 — the crop/pad of
@@ -17,12 +22,20 @@
 //   * encode: speckle -> 2, 3 -> 1, then {0:-1, 1:100, 2:0} as int8 (bev.py:242-245), written in the
 //     reference (h, w) layout or directly in the ROS data order flip(0)+rot90ccw (occgrid_to_ros.py:18-25).
 // Algorithmic traffic per frame: the class map read once (in_rows*in_cols B, gathered; L2-resident)
-// + occ_h*occ_w B written — latency/gather-bound, far below the HBM roof.
+// + occ_h*occ_w B written, plus the table entries a cell reads (1, 9 or 25 x 8 B, shared by every
+// frame: L2 / Infinity-Cache hits) — gather-bound, far below the HBM roof.
+#include <cstdlib>
+
 #include "bugseg_internal.h"
 
 namespace bugseg {
 
-__device__ __forceinline__ int warp_value(const BevArgs &a, const uint8_t *seg, int x, int y) {
+// warpPerspective's source taps of warped pixel (x, y): (sy, sx) of the top-left tap, the 1/32-pixel
+// fractions (ax, ay) and which of the 4 taps lie inside the image — OpenCV's arithmetic exactly:
+// double-precision inverse mapping with the per-block split X0 + M0*x1 (FP contraction OFF so the IEEE
+// order matches), cvRound to 1/32 pixel.
+struct WarpTap { int sx, sy, ax, ay; bool x0, x1, y0, y1; };
+__device__ __forceinline__ WarpTap warp_tap(const BevArgs &a, int x, int y) {
 #pragma clang fp contract(off)
     const double *M = a.Mi;
     const int xb = (x / a.bw0) * a.bw0, x1 = x - xb;
@@ -39,78 +52,144 @@ __device__ __forceinline__ int warp_value(const BevArgs &a, const uint8_t *seg, 
     int sx = X >> 5, sy = Y >> 5;
     sx = sx < -32768 ? -32768 : (sx > 32767 ? 32767 : sx);
     sy = sy < -32768 ? -32768 : (sy > 32767 ? 32767 : sy);
-    const int ax = X & 31, ay = Y & 31;
+    WarpTap t;
+    t.sx = sx; t.sy = sy; t.ax = X & 31; t.ay = Y & 31;
     const int w = a.in_cols, h = a.in_rows;
-    // segmap + 1 (bev.py:177): taps inside the image read class+1, outside the border value 0
-    const bool x0 = (unsigned)sx < (unsigned)w, x1ok = (unsigned)(sx + 1) < (unsigned)w;
-    const bool y0 = (unsigned)sy < (unsigned)h, y1ok = (unsigned)(sy + 1) < (unsigned)h;
-    int v0 = 0, v1 = 0, v2 = 0, v3 = 0;
-    if (y0) {
-        const uint8_t *r = seg + (size_t)sy * w;
-        if (x0) v0 = r[sx] + 1;
-        if (x1ok) v1 = r[sx + 1] + 1;
-    }
-    if (y1ok) {
-        const uint8_t *r = seg + (size_t)(sy + 1) * w;
-        if (x0) v2 = r[sx] + 1;
-        if (x1ok) v3 = r[sx + 1] + 1;
-    }
-    const int acc = (v0 * (32 - ax) * (32 - ay) + v1 * ax * (32 - ay) + v2 * (32 - ax) * ay + v3 * ax * ay) * 32;
-    int v = (acc + (1 << 14)) >> 15;
-    return v > 255 ? 255 : v;
+    t.x0 = (unsigned)sx < (unsigned)w; t.x1 = (unsigned)(sx + 1) < (unsigned)w;
+    t.y0 = (unsigned)sy < (unsigned)h; t.y1 = (unsigned)(sy + 1) < (unsigned)h;
+    return t;
 }
 
-// template value at template pixel (tx, ty) (caller guarantees it lies inside the template)
-__device__ __forceinline__ int tmpl_value(const BevArgs &a, const uint8_t *seg, int tx, int ty) {
-    const int wx = tx + a.left_x, wy = ty + a.top_y;
-    if ((unsigned)wx >= (unsigned)a.warp_w || (unsigned)wy >= (unsigned)a.warp_h) return 0;
-    return warp_value(a, seg, wx, wy);
+// Table entry of a template pixel (bits of .y): 0-4 ax, 5-9 ay, 10-13 which taps (top-left,
+// top-right, bottom-left, bottom-right) are inside the class map, 14 = the pixel lies outside the
+// template (a neutral 1 for the erode: OpenCV's default erode border is +inf). .x = the byte offset of
+// the top-left tap in the frame (sy * in_cols + sx). A pixel inside the template but outside the warped
+// image has no valid tap: value 0 (the crop/pad of bev.py:183-195).
+constexpr uint32_t TAB_OUT = 1u << 14;
+__device__ __forceinline__ uint2 tab_entry(const BevArgs &a, int tx, int ty) {
+    if ((unsigned)tx >= (unsigned)a.occ_w_px || (unsigned)ty >= (unsigned)a.occ_h_px) return make_uint2(0u, TAB_OUT);
+    const int wx = tx + a.left_x, wy = ty + a.top_y;   // template(t) = warp(t + (left_x, top_y))
+    if ((unsigned)wx >= (unsigned)a.warp_w || (unsigned)wy >= (unsigned)a.warp_h) return make_uint2(0u, 0u);
+    const WarpTap t = warp_tap(a, wx, wy);
+    const uint32_t valid = (uint32_t)(t.y0 && t.x0) | (uint32_t)(t.y0 && t.x1) << 1 | (uint32_t)(t.y1 && t.x0) << 2 |
+                           (uint32_t)(t.y1 && t.x1) << 3;
+    return make_uint2((uint32_t)(t.sy * a.in_cols + t.sx), (uint32_t)t.ax | (uint32_t)t.ay << 5 | valid << 10);
 }
 
-// occupied template values: {1, 3} (bev.py:196), or {1} in the binary variant (bev.py:128)
-__device__ __forceinline__ bool occupied(const BevArgs &a, int v) { return v == 1 || (v == 3 && !a.variant); }
-
-// Occupancy bit of template pixel p + (dx, dy); pixels outside the template read 1 (neutral for the
-// erode: OpenCV's default erode border is +inf).
-__device__ __forceinline__ uint32_t occ_bit(const BevArgs &a, const uint8_t *seg, int tx, int ty, int dx, int dy) {
-    const int x = tx + dx, y = ty + dy;
-    if ((unsigned)x >= (unsigned)a.occ_w_px || (unsigned)y >= (unsigned)a.occ_h_px) return 1u;
-    return occupied(a, tmpl_value(a, seg, x, y)) ? 1u : 0u;
+// template pixel sampled by cell (cx, cy): resizeNN (bev.py:209), src = min(floor(d * inv_scale), size - 1)
+__device__ __forceinline__ void cell_pixel(const BevArgs &a, int cx, int cy, int &tx, int &ty) {
+    ty = (int)floor((double)cy * a.ify);
+    tx = (int)floor((double)cx * a.ifx);
+    ty = ty < a.occ_h_px - 1 ? ty : a.occ_h_px - 1;
+    tx = tx < a.occ_w_px - 1 ? tx : a.occ_w_px - 1;
 }
 
 // bit index of offset (dx, dy) in the 5x5 window around p
 #define B5(dx, dy) (((dy) + 2) * 5 + ((dx) + 2))
 
-__global__ void __launch_bounds__(256) bev_occgrid_kernel(const BevArgs a) {
-    const long cells = (long)a.occ_h * a.occ_w, total = cells * a.B;
+// One thread per (cell, window position): the geometry-only half of the rasteriser, run once per
+// calibration. Everything per frame (bev_occgrid_kernel) is then integer gathers and Q15 arithmetic.
+__global__ void __launch_bounds__(256) bev_table_kernel(const BevArgs a) {
+    const long cells = (long)a.occ_h * a.occ_w, total = cells * BEV_WIN;
     for (long i = blockIdx.x * 256L + threadIdx.x; i < total; i += (long)gridDim.x * 256) {
-        const int b = (int)(i / cells);
-        const int rem = (int)(i - (long)b * cells);
+        const int k = (int)(i / cells), c = (int)(i - (long)k * cells);
+        const int cy = c / a.occ_w, cx = c - cy * a.occ_w;
+        int tx, ty;
+        cell_pixel(a, cx, cy, tx, ty);
+        a.wtab[i] = tab_entry(a, tx + k % 5 - 2, ty + k / 5 - 2);
+    }
+}
+
+// value of a template pixel from its table entry: the bilinear Q15 blend of segmap + 1 (bev.py:177;
+// taps outside the class map read the border value 0), (sum + 2^14) >> 15
+__device__ __forceinline__ int tab_value(__amdgpu_buffer_rsrc_t seg, int w, uint2 e) {
+    const uint32_t m = e.y;
+    const int ax = m & 31, ay = (m >> 5) & 31;
+    const uint32_t b = e.x;
+    const int v0 = __builtin_amdgcn_raw_buffer_load_b8(seg, (int)((m & (1u << 10)) ? b : 0x80000000u), 0, 0);
+    const int v1 = __builtin_amdgcn_raw_buffer_load_b8(seg, (int)((m & (1u << 11)) ? b + 1 : 0x80000000u), 0, 0);
+    const int v2 = __builtin_amdgcn_raw_buffer_load_b8(seg, (int)((m & (1u << 12)) ? b + w : 0x80000000u), 0, 0);
+    const int v3 = __builtin_amdgcn_raw_buffer_load_b8(seg, (int)((m & (1u << 13)) ? b + w + 1 : 0x80000000u), 0, 0);
+    const int c0 = (m >> 10) & 1, c1 = (m >> 11) & 1, c2 = (m >> 12) & 1, c3 = (m >> 13) & 1;   // + 1 inside
+    const int acc = ((v0 + c0) * (32 - ax) * (32 - ay) + (v1 + c1) * ax * (32 - ay) + (v2 + c2) * (32 - ax) * ay +
+                     (v3 + c3) * ax * ay) * 32;
+    const int v = (acc + (1 << 14)) >> 15;
+    return v > 255 ? 255 : v;
+}
+
+// occupied template values: {1, 3} (bev.py:196), or {1} in the binary variant (bev.py:128)
+__device__ __forceinline__ bool occupied(const BevArgs &a, int v) { return v == 1 || (v == 3 && !a.variant); }
+
+// F frames per thread (the cell's table entries are loaded once and serve all F), the 3x3 around the
+// sample evaluated eagerly (one round of 36 gathers per frame instead of a dependent centre-then-
+// neighbours chain); the 16-pixel ring only for the frames whose 3x3 does not settle the opening.
+template <int F>
+__global__ void __launch_bounds__(256) bev_occgrid_kernel(const BevArgs a) {
+    const long cells = (long)a.occ_h * a.occ_w;
+    const int groups = (a.B + F - 1) / F;
+    const long total = cells * groups;
+    const uint32_t frame_bytes = (uint32_t)a.in_rows * (uint32_t)a.in_cols;
+    // the 3x3 around p: window positions B5(dx, dy), dx, dy in -1..1, in row order
+    constexpr int K3[9] = {6, 7, 8, 11, 12, 13, 16, 17, 18};
+    for (long i = blockIdx.x * 256L + threadIdx.x; i < total; i += (long)gridDim.x * 256) {
+        const int g = (int)(i / cells);
+        const int rem = (int)(i - (long)g * cells);
         const int cy = rem / a.occ_w, cx = rem - cy * a.occ_w;
-        const uint8_t *seg = a.seg + (size_t)b * a.in_rows * a.in_cols;
-        int ty = (int)floor((double)cy * a.ify);
-        int tx = (int)floor((double)cx * a.ifx);
-        ty = ty < a.occ_h_px - 1 ? ty : a.occ_h_px - 1;
-        tx = tx < a.occ_w_px - 1 ? tx : a.occ_w_px - 1;
-        int v = tmpl_value(a, seg, tx, ty);
-        if (occupied(a, v)) {
-            // Opening at p = OR over q in N3(p) (inside the template) of AND over N3(q) of occupancy.
-            // Round 1: the 8 neighbours of p (independent gathers, issued together). If they are all
-            // occupied, q = p already survives the erode. Round 2 only for the rest: the 16-pixel ring.
-            uint32_t m = 1u << B5(0, 0);
+        const uint2 *tab = a.wtab + rem;
+        uint2 e3[9];
 #pragma unroll
-            for (int dy = -1; dy <= 1; ++dy)
+        for (int k = 0; k < 9; ++k) e3[k] = tab[(long)K3[k] * cells];
+        __amdgpu_buffer_rsrc_t seg[F];
 #pragma unroll
-                for (int dx = -1; dx <= 1; ++dx)
-                    if (dx || dy) m |= occ_bit(a, seg, tx, ty, dx, dy) << B5(dx, dy);
-            const uint32_t inner = 0x739C0u;        // bits of the 3x3 around p: rows 1..3, cols 1..3
-            bool opened = (m & inner) == inner;
-            if (!opened) {
+        for (int f = 0; f < F; ++f) {
+            // a frame past the batch gets an empty descriptor: its loads read 0, its result is dropped
+            const int b = g * F + f;
+            seg[f] = __builtin_amdgcn_make_buffer_rsrc(const_cast<uint8_t *>(a.seg) + (size_t)(b < a.B ? b : 0) * frame_bytes,
+                                                       (short)0, b < a.B ? (int)frame_bytes : 0, 0x00020000);
+        }
+        uint32_t m[F];
+        int v[F];
 #pragma unroll
-                for (int dy = -2; dy <= 2; ++dy)
+        for (int f = 0; f < F; ++f) {
+            m[f] = 0;
 #pragma unroll
-                    for (int dx = -2; dx <= 2; ++dx)
-                        if (dx == -2 || dx == 2 || dy == -2 || dy == 2) m |= occ_bit(a, seg, tx, ty, dx, dy) << B5(dx, dy);
+            for (int k = 0; k < 9; ++k) {
+                const int t = tab_value(seg[f], a.in_cols, e3[k]);
+                if (k == 4) v[f] = t;
+                // outside the template: 1 (neutral for the erode: OpenCV's default erode border is +inf)
+                const bool o = (e3[k].y & TAB_OUT) || occupied(a, t);
+                m[f] |= (uint32_t)o << K3[k];
+            }
+        }
+        const uint32_t inner = 0x739C0u;            // bits of the 3x3 around p: rows 1..3, cols 1..3
+        bool need_ring = false;
+#pragma unroll
+        for (int f = 0; f < F; ++f) need_ring |= occupied(a, v[f]) && (m[f] & inner) != inner;
+        if (need_ring) {
+            // Opening at p = OR over q in N3(p) (inside the template) of AND over N3(q) of occupancy:
+            // the ring completes the 5x5 window for the frames whose centre is occupied but whose 3x3
+            // is not (if it is, q = p already survives the erode)
+            int tx, ty;
+            cell_pixel(a, cx, cy, tx, ty);
+            uint2 er[16];
+            {
+                int n = 0;
+#pragma unroll
+                for (int k = 0; k < 25; ++k)
+                    if (k % 5 == 0 || k % 5 == 4 || k / 5 == 0 || k / 5 == 4) er[n++] = tab[(long)k * cells];
+            }
+#pragma unroll
+            for (int f = 0; f < F; ++f) {
+                if (!(occupied(a, v[f]) && (m[f] & inner) != inner)) continue;
+                int n = 0;
+#pragma unroll
+                for (int k = 0; k < 25; ++k) {
+                    if (!(k % 5 == 0 || k % 5 == 4 || k / 5 == 0 || k / 5 == 4)) continue;
+                    const uint2 e = er[n++];
+                    const bool o = (e.y & TAB_OUT) || occupied(a, tab_value(seg[f], a.in_cols, e));
+                    m[f] |= (uint32_t)o << k;
+                }
+                bool opened = false;
 #pragma unroll
                 for (int qy = -1; qy <= 1; ++qy)
 #pragma unroll
@@ -118,30 +197,36 @@ __global__ void __launch_bounds__(256) bev_occgrid_kernel(const BevArgs a) {
                         const bool inside = (unsigned)(tx + qx) < (unsigned)a.occ_w_px && (unsigned)(ty + qy) < (unsigned)a.occ_h_px;
                         const int sh = qy * 5 + qx;
                         const uint32_t win = sh >= 0 ? inner << sh : inner >> -sh;   // 3x3 window centred at q
-                        opened |= inside && (m & win) == win;
+                        opened |= inside && (m[f] & win) == win;
                     }
+                if (!opened) v[f] = 2;           // isolated occupied pixel -> free (bev.py:204-205)
             }
-            if (!opened) v = 2;                  // isolated occupied pixel -> free (bev.py:204-205)
         }
-        int8_t o;
-        if (!a.variant) {
-            const int g = v == 3 ? 1 : v;        // bev.py:242
-            o = (int8_t)(g == 0 ? -1 : 200 - 100 * g);   // bev.py:244-245
-        } else {
-            // bev.py:139-144, :165 in uint8 arithmetic: {0:-1, 1:100, 2:0, 3:-100}
-            const uint8_t g = (uint8_t)(v * 100);
-            o = (int8_t)(uint8_t)(g == 0 ? 0xff : (uint8_t)(200 - g));
-        }
-        if (a.laserscan) {
-            // the polar warp's source: the cells (bev.py:219) or the encoded grid (bev.py:146)
-            a.cells[i] = a.variant ? (uint8_t)o : (uint8_t)v;
-            if (!a.variant) continue;            // the final laserscan kernel writes out
-        }
-        if (a.ros_layout) {
-            // occgrid_to_ros.py:18-21: flip(0) then rot90ccw == G[::-1, ::-1].T, shape (occ_w, occ_h)
-            a.out[(size_t)b * cells + (size_t)(a.occ_w - 1 - cx) * a.occ_h + (a.occ_h - 1 - cy)] = o;
-        } else {
-            a.out[i] = o;
+#pragma unroll
+        for (int f = 0; f < F; ++f) {
+            const int b = g * F + f;
+            if (b >= a.B) break;
+            const long o_i = (long)b * cells + rem;
+            int8_t o;
+            if (!a.variant) {
+                const int gg = v[f] == 3 ? 1 : v[f];     // bev.py:242
+                o = (int8_t)(gg == 0 ? -1 : 200 - 100 * gg);   // bev.py:244-245
+            } else {
+                // bev.py:139-144, :165 in uint8 arithmetic: {0:-1, 1:100, 2:0, 3:-100}
+                const uint8_t gg = (uint8_t)(v[f] * 100);
+                o = (int8_t)(uint8_t)(gg == 0 ? 0xff : (uint8_t)(200 - gg));
+            }
+            if (a.laserscan) {
+                // the polar warp's source: the cells (bev.py:219) or the encoded grid (bev.py:146)
+                a.cells[o_i] = a.variant ? (uint8_t)o : (uint8_t)v[f];
+                if (!a.variant) continue;        // the final laserscan kernel writes out
+            }
+            if (a.ros_layout) {
+                // occgrid_to_ros.py:18-21: flip(0) then rot90ccw == G[::-1, ::-1].T, shape (occ_w, occ_h)
+                a.out[(size_t)b * cells + (size_t)(a.occ_w - 1 - cx) * a.occ_h + (a.occ_h - 1 - cy)] = o;
+            } else {
+                a.out[o_i] = o;
+            }
         }
     }
 }
@@ -215,12 +300,28 @@ __global__ void __launch_bounds__(256) laserscan_kernel(const BevArgs a) {
     }
 }
 
-hipError_t launch_bev(const BevArgs &a, hipStream_t s) {
-    const long total = (long)a.occ_h * a.occ_w * a.B;
+hipError_t launch_bev_table(const BevArgs &a, hipStream_t s) {
+    const long total = (long)a.occ_h * a.occ_w * BEV_WIN;
     long g = (total + 255) / 256;
     if (g > 8192) g = 8192;
     if (g < 1) g = 1;
-    hipLaunchKernelGGL(bev_occgrid_kernel, dim3((unsigned)g), dim3(256), 0, s, a);
+    hipLaunchKernelGGL(bev_table_kernel, dim3((unsigned)g), dim3(256), 0, s, a);
+    return hipGetLastError();
+}
+
+hipError_t launch_bev(const BevArgs &a, hipStream_t s) {
+    static const int F = [] { const char *e = std::getenv("BUGSEG_BEV_F"); return e ? std::atoi(e) : 2; }();
+    const long total = (long)a.occ_h * a.occ_w * a.B;
+    const int f = F == 4 ? 4 : F == 1 ? 1 : 2;
+    long gf = ((long)a.occ_h * a.occ_w * ((a.B + f - 1) / f) + 255) / 256;
+    if (gf > 8192) gf = 8192;
+    if (gf < 1) gf = 1;
+    if (f == 1) hipLaunchKernelGGL(bev_occgrid_kernel<1>, dim3((unsigned)gf), dim3(256), 0, s, a);
+    else if (f == 2) hipLaunchKernelGGL(bev_occgrid_kernel<2>, dim3((unsigned)gf), dim3(256), 0, s, a);
+    else hipLaunchKernelGGL(bev_occgrid_kernel<4>, dim3((unsigned)gf), dim3(256), 0, s, a);
+    long g = (total + 255) / 256;
+    if (g > 8192) g = 8192;
+    if (g < 1) g = 1;
     if (!a.laserscan) return hipGetLastError();
     const long rays = (long)a.B * a.ph;
     long gr = (rays + 3) / 4;

@@ -130,14 +130,20 @@ __global__ void __launch_bounds__((BShape<C, V>::NW * 64), (sizeof(T) == 2 ? BSh
     constexpr int NPA = TH * TWA;
     constexpr int NFA = (NPA + 15) / 16;
     constexpr int NF2A = (NFA + NW - 1) / NW;
-    constexpr int CH1 = KS1 >= 8 ? 1 : KS1 >= 4 ? (NF1 + NW - 1) / NW : KS1 == 2 ? 4 : 8;   // phase-1 fragments whose loads fly together
+#ifndef BNECK_CH1_K2
+#define BNECK_CH1_K2 4
+#endif
+#ifndef BNECK_REG3_C64
+#define BNECK_REG3_C64 0
+#endif
+    constexpr int CH1 = KS1 >= 8 ? 1 : KS1 >= 4 ? (NF1 + NW - 1) / NW : KS1 == 2 ? BNECK_CH1_K2 : 8;   // phase-1 fragments whose loads fly together
     // phase-3 chunking (see phase 3): bf16 with an even number of 16-row blocks swaps row pairs
     // into 16-B chunks; bf16 C = 16 stores 8-B quads (HALF); fp32 quads are 16-B chunks
     // REG3: the register epilogue (C = 128 and 16). C = 64 keeps the LDS-staged epilogue: its 128-B
     // pixels would be written as half lines by the register layout, which measured slower there
     // (44.7 vs 43.0 us per launch with t1 in registers).
     // (the down form's C = 64 launch measured faster with the register epilogue: 53 vs 55 us)
-    constexpr bool REG3 = C != 64 || DN;
+    constexpr bool REG3 = C != 64 || DN || BNECK_REG3_C64;
     constexpr bool SWAP = REG3 && sizeof(T) == 2 && NR3 % 2 == 0;
     constexpr bool HALF = REG3 && sizeof(T) == 2 && NR3 % 2 != 0;
     constexpr int EPC = 16 / (int)sizeof(T);          // elements per 16-B chunk
@@ -646,7 +652,7 @@ __global__ void __launch_bounds__((BShape<C, V>::NW * 64), (sizeof(T) == 2 ? BSh
                     const int q = lane + 64 * k;
                     if (q < CPF) {
                         const uint32_t off = pix_off(wave + NW * j, q / CPP, (q % CPP) * EPC);
-                        bst16(rob, off, *reinterpret_cast<const uint4 *>(stg + (q / CPP) * OSTR + (q % CPP) * EPC));
+                        bst16o(rob, off, *reinterpret_cast<const uint4 *>(stg + (q / CPP) * OSTR + (q % CPP) * EPC));
                     }
                 }
                 wave_lds_sync();
@@ -686,7 +692,7 @@ __global__ void __launch_bounds__((BShape<C, V>::NW * 64), (sizeof(T) == 2 ? BSh
                     uint32_t x0 = p0.x, x1 = p0.y, y0 = p1.x, y1 = p1.y;
                     pl16swap(x0, y0);
                     pl16swap(x1, y1);
-                    bst16(rob, off, make_uint4(x0, x1, y0, y1));
+                    bst16o(rob, off, make_uint4(x0, x1, y0, y1));
                 } else {
                     const int r = t;
                     f32x4 acc = bias_in_acc(NR3, 1) ? bias4(cb3 + r * 16 + kq * 4) : (f32x4){0.f, 0.f, 0.f, 0.f};
@@ -695,10 +701,10 @@ __global__ void __launch_bounds__((BShape<C, V>::NW * 64), (sizeof(T) == 2 ? BSh
                     mma(acc, wf, tf[j]);
                     if constexpr (HALF) {
                         float4 v = act(add4(out3(r, acc), unpack_bf16x4((u32x2_t){rc.x, rc.y})), cso + r * 16 + kq * 4);
-                        __builtin_amdgcn_raw_buffer_store_b64(pack_bf16x4(v), rob, (int)off, 0, 0);
+                        bst8o(rob, off, pack_bf16x4(v));
                     } else {
                         float4 v = act(add4(out3(r, acc), __builtin_bit_cast(float4, rc)), cso + r * 16 + kq * 4);
-                        bst16(rob, off, __builtin_bit_cast(uint4, v));
+                        bst16o(rob, off, __builtin_bit_cast(uint4, v));
                     }
                 }
             }
@@ -726,7 +732,7 @@ size_t bneck_lds_bytes(int prec, int C, bool asym, int v, int cin) {
     const size_t wts = (size_t)NR1 * 16 * (KS1 * 32 + padw) + (size_t)NR1 * 16 * (KS2 * 32 + padw) * (asym ? 2 : 1) +
                        (size_t)C * (32 + padw);
     const size_t halo = (size_t)(TH + 2 * R) * (TW + 2 * RX) * bneck_pstr(es, IS, wide);
-    const size_t stage = C == 64 ? (size_t)NW * 16 * (C + pad) : 0;    // staged epilogue (REG3 off)
+    const size_t stage = C == 64 && !BNECK_REG3_C64 ? (size_t)NW * 16 * (C + pad) : 0;    // staged epilogue (REG3 off)
     const size_t consts = ((size_t)6 * NR1 * 16 + 3 * (size_t)C) * sizeof(float);
     return (wts + 16 + (halo > stage ? halo : stage)) * es + consts;   // + the zero pad
 }

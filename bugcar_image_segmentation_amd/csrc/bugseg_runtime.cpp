@@ -117,6 +117,10 @@ struct bugseg_ctx {
     // buffers (the polar tables are read-only once built and are shared).
     struct LsScratch { void *stream = nullptr; void *p = nullptr; size_t bytes = 0; };
     std::vector<LsScratch> ls_scratch;
+    // BEV warp-tap tables (bev_kernels.hip bev_table_kernel), one per recent geometry (read-only
+    // once built, shared by every stream); key = the geometry fields of BevArgs
+    struct BevTab { std::vector<unsigned char> key; uint2 *tab = nullptr; };
+    std::vector<BevTab> bev_tabs;
 };
 
 namespace {
@@ -153,9 +157,9 @@ struct Reader {
     std::vector<float> tensor() {
         uint32_t n = get<uint32_t>();
         std::vector<float> v;
-        if (!ok || p + (size_t)n * 4 > end) { ok = false; return v; }
+        if (!ok || (size_t)(end - p) / 4 < (size_t)n) { ok = false; return v; }   // (no pointer past the end)
         v.resize(n);
-        std::memcpy(v.data(), p, (size_t)n * 4);
+        if (n) std::memcpy(v.data(), p, (size_t)n * 4);   // (memcpy from / to NULL is UB even for 0 bytes)
         p += (size_t)n * 4;
         return v;
     }
@@ -1065,6 +1069,7 @@ int bugseg_destroy(bugseg_ctx *ctx) {
     if (ctx->pre_tab) (void)hipFree(ctx->pre_tab);
     if (ctx->polar_tab) (void)hipFree(ctx->polar_tab);
     for (auto &s : ctx->ls_scratch) if (s.p) (void)hipFree(s.p);
+    for (auto &t : ctx->bev_tabs) if (t.tab) (void)hipFree(t.tab);
     delete ctx;
     return BUGSEG_OK;
 }
@@ -1365,12 +1370,75 @@ int bugseg_bev_occgrid(bugseg_ctx *ctx, const uint8_t *seg, int B, const bugseg_
     a.ros_layout = p->ros_layout;
     a.variant = p->variant;
     a.out = out;
+    {
+        // the geometry's warp-tap table: built once (on this stream), then shared by every call
+        std::vector<unsigned char> key(sizeof(double) * 11 + sizeof(int) * 12);
+        unsigned char *kp = key.data();
+        auto put = [&](const void *v, size_t n) { std::memcpy(kp, v, n); kp += n; };
+        put(a.Mi, sizeof(a.Mi)); put(&a.ifx, sizeof(double)); put(&a.ify, sizeof(double));
+        const int ik[12] = {a.in_rows, a.in_cols, a.bw0, a.warp_w, a.warp_h, a.occ_w_px, a.occ_h_px, a.occ_w, a.occ_h,
+                            a.left_x, a.top_y, 0};
+        put(ik, sizeof(ik));
+        bugseg_ctx::BevTab *hit = nullptr;
+        for (auto &t : ctx->bev_tabs) if (t.key == key) hit = &t;
+        if (!hit) {
+            const size_t cells = (size_t)a.occ_h * a.occ_w;
+            if (cells * BEV_WIN > (size_t)1 << 31) return fail(ctx, BUGSEG_EINVAL, "occupancy grid too large");
+            if (ctx->bev_tabs.size() >= 4) {            // keep the 4 most recent geometries
+                if (hipDeviceSynchronize() != hipSuccess) return fail(ctx, BUGSEG_EHIP, "device sync failed");
+                (void)hipFree(ctx->bev_tabs.front().tab);
+                ctx->bev_tabs.erase(ctx->bev_tabs.begin());
+            }
+            bugseg_ctx::BevTab t;
+            t.key = key;
+            if (hipMalloc(&t.tab, cells * BEV_WIN * sizeof(uint2)) != hipSuccess)
+                return fail(ctx, BUGSEG_ENOMEM, "BEV table allocation failed");
+            a.wtab = t.tab;
+            hipError_t e = launch_bev_table(a, (hipStream_t)stream);
+            if (e == hipSuccess) e = hipStreamSynchronize((hipStream_t)stream);   // other streams may use it next
+            if (e != hipSuccess) {
+                (void)hipFree(t.tab);
+                return fail(ctx, BUGSEG_EHIP, std::string("BEV table: ") + hipGetErrorString(e));
+            }
+            ctx->bev_tabs.push_back(std::move(t));
+            hit = &ctx->bev_tabs.back();
+        }
+        a.wtab = hit->tab;
+    }
     if (p->laserscan) {
         const int rc = prepare_laserscan(ctx, p, B, a, stream);
         if (rc != BUGSEG_OK) return rc;
     }
     hipError_t e = launch_bev(a, (hipStream_t)stream);
     if (e != hipSuccess) return fail(ctx, BUGSEG_EHIP, std::string("bev launch: ") + hipGetErrorString(e));
+    return BUGSEG_OK;
+}
+
+// ---- test hooks (host only: no device, no HIP call) — tests/asan drives them under ASan + UBSan
+int bugseg_debug_parse_pack(const void *blob, size_t bytes, int precision, int *ncls) {
+    if (!blob) return fail(nullptr, BUGSEG_EINVAL, "NULL blob");
+    bugseg_ctx c;                                     // host state only; nothing to free on the device
+    c.prec = precision == BUGSEG_BF16 ? PREC_BF16 : PREC_F32;
+    std::string why;
+    if (!parse_blob(blob, bytes, c.blocks, c.ncls, why)) return fail(nullptr, BUGSEG_EFORMAT, "weight blob: " + why);
+    if (!pack_all(&c, why)) return fail(nullptr, BUGSEG_EFORMAT, "weight blob: " + why);
+    if (ncls) *ncls = c.ncls;
+    return BUGSEG_OK;
+}
+
+int bugseg_debug_polar_tables(int w, int h, int variant, int32_t *fmap, size_t fmap_n, int32_t *imap, size_t imap_n,
+                              int *pw_out, int *ph_out) {
+    if (w <= 0 || h <= 0 || w > 32767 || h > 32767) return fail(nullptr, BUGSEG_EINVAL, "bad grid");
+    const int L = std::max(w, h);
+    const int pw = variant ? w : (int)std::lrint((double)L);
+    const int ph = variant ? h : (int)std::lrint((double)L * 3.1415926535897932384626433832795);
+    if (ph > 32767) return fail(nullptr, BUGSEG_EINVAL, "grid too large for the polar tables");
+    std::vector<int32_t> f, im;
+    polar_tables(pw, ph, (double)L, (float)(w / 2.0 - 1), (float)h, w, h, f, im);
+    if (pw_out) *pw_out = pw;
+    if (ph_out) *ph_out = ph;
+    if (fmap) std::memcpy(fmap, f.data(), std::min(fmap_n, f.size()) * sizeof(int32_t));
+    if (imap) std::memcpy(imap, im.data(), std::min(imap_n, im.size()) * sizeof(int32_t));
     return BUGSEG_OK;
 }
 

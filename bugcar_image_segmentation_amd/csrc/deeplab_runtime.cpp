@@ -72,10 +72,15 @@ bool buf_ok(const bugseg_dl *c, int id, double bytes) {
 }
 
 // Shape / bounds validation of one op against the plan's buffers and the weight blob.
+bool in_range(int v, int lo, int hi) { return v >= lo && v <= hi; }
+
 bool check_op(const bugseg_dl *c, const DlOp &o, std::string &why) {
     const int *f = o.f;
     const double es = c->prec == PREC_BF16 ? 2.0 : 4.0;
     const int B = c->B;
+    // every field that enters integer arithmetic here or in run_op is bounded first (no overflow):
+    // spatial sizes <= 16384, channels <= 8192, kernel extents <= 15, strides / dilations <= 255
+    constexpr int SP = 16384, CH = 8192;
     switch (f[0]) {
     case OP_PREP:
         if (!buf_ok(c, f[1], (double)B * c->Hc * c->Wc * 8 * es)) { why = "prep: destination buffer too small"; return false; }
@@ -86,6 +91,12 @@ bool check_op(const bugseg_dl *c, const DlOp &o, std::string &why) {
         const long w_off = f[17], b_off = f[18];
         const int act = f[19], res_cs = f[20], out_cs = f[21], out_off = f[22], cout = f[23], out_f32 = f[24];
         const int bimg = f[25], bimg_stride = f[26];
+        if (!in_range(Hin, 1, SP) || !in_range(Win, 1, SP) || !in_range(Hout, 1, SP) || !in_range(Wout, 1, SP) ||
+            !in_range(kh, 1, 15) || !in_range(kw, 1, 15) || !in_range(stride, 1, 255) || !in_range(dil, 1, 255) ||
+            !in_range(f[13], 0, 255) || !in_range(f[14], 0, 255) || !in_range(CS, 8, CH) || !in_range(cinP, 32, CH) ||
+            !in_range(NP, 64, CH) || !in_range(res_cs, 0, CH) || !in_range(out_cs, 8, CH) || !in_range(out_off, 0, CH) ||
+            !in_range(cout, 8, CH) || !in_range(bimg_stride, 0, 1 << 20) || (f[31] != 0 && f[31] != 1 && f[31] != 2) ||
+            (double)B * Hout * Wout >= 2147483648.0) { why = "conv: field out of range"; return false; }
         if (Hin < 1 || Win < 1 || Hout < 1 || Wout < 1 || kh < 1 || kw < 1 || stride < 1 || dil < 1 || CS < 8 ||
             CS % 8 || cinP % 32 || cinP < 32 || NP % 64 || NP < 64 || act < 0 || act > 2 || cout < 8 || cout % 8 ||
             cout > NP || out_off % 8 || out_off + cout > out_cs) { why = "conv: bad shape"; return false; }
@@ -115,6 +126,9 @@ bool check_op(const bugseg_dl *c, const DlOp &o, std::string &why) {
     case OP_DW: {
         const int src = f[1], dst = f[2], Hin = f[3], Win = f[4], C = f[5], Hout = f[6], Wout = f[7];
         const long w_off = f[12], b_off = f[13];
+        if (!in_range(Hin, 1, SP) || !in_range(Win, 1, SP) || !in_range(Hout, 1, SP) || !in_range(Wout, 1, SP) ||
+            !in_range(C, 8, CH) || !in_range(f[8], 1, 255) || !in_range(f[9], 1, 255) || !in_range(f[10], 0, 255) ||
+            !in_range(f[11], 0, 255) || (double)B * Hout * Wout >= 2147483648.0) { why = "dw: field out of range"; return false; }
         if (C < 8 || C % 8 || Hin < 1 || Win < 1 || Hout < 1 || Wout < 1 || f[8] < 1 || f[9] < 1) { why = "dw: bad shape"; return false; }
         if (!buf_ok(c, src, (double)B * Hin * Win * C * es) || !buf_ok(c, dst, (double)B * Hout * Wout * C * es)) { why = "dw: buffer too small"; return false; }
         if ((double)B * Hin * Win * C * es >= 2147483648.0) { why = "dw: input exceeds 31-bit offsets"; return false; }
@@ -124,6 +138,7 @@ bool check_op(const bugseg_dl *c, const DlOp &o, std::string &why) {
     case OP_POOL: {
         const int src = f[1], part = f[2], z = f[3], H = f[4], W = f[5], C = f[6], CS = f[7], chunk = f[8], nch = f[9];
         const int cmid = f[10], cout = f[11], zs = f[16];
+        if (!in_range(H, 1, SP) || !in_range(W, 1, SP) || !in_range(CS, 1, CH)) { why = "pool: field out of range"; return false; }
         if (C < 1 || C > 1024 || CS < C || cmid < 1 || cmid > 1024 || cout < 1 || zs < cout || chunk < 1 || nch < 1 ||
             (long)chunk * nch < (long)H * W) { why = "pool: bad shape"; return false; }
         if (!buf_ok(c, src, (double)B * H * W * CS * es) || !buf_ok(c, part, (double)B * nch * C * 4.0) ||
@@ -134,6 +149,7 @@ bool check_op(const bugseg_dl *c, const DlOp &o, std::string &why) {
     }
     case OP_ARGMAX: {
         const int lg = f[1], h = f[2], w = f[3], LCS = f[4], ncls = f[5];
+        if (!in_range(h, 1, SP) || !in_range(w, 1, SP) || !in_range(LCS, 1, CH)) { why = "argmax: field out of range"; return false; }
         if (h < 1 || w < 1 || ncls < 1 || LCS < ncls || LCS % 4) { why = "argmax: bad shape"; return false; }
         if (!buf_ok(c, lg, (double)B * h * w * LCS * 4.0)) { why = "argmax: logits buffer too small"; return false; }
         return true;
@@ -246,7 +262,7 @@ int bugseg_dl_destroy(bugseg_dl *c) {
 int bugseg_dl_load_weights(bugseg_dl *c, const void *blob, size_t bytes) {
     if (!c || !blob || bytes == 0 || bytes >= (size_t)1 << 31) return dl_fail(c, BUGSEG_EINVAL, "bad weight blob");
     DevGuard g(c->device);
-    if (c->dev_w) { (void)hipFree(c->dev_w); c->dev_w = nullptr; }
+    if (c->dev_w) { (void)hipDeviceSynchronize(); (void)hipFree(c->dev_w); c->dev_w = nullptr; }
     if (hipMalloc(&c->dev_w, bytes) != hipSuccess) return dl_fail(c, BUGSEG_ENOMEM, "weight allocation failed");
     if (hipMemcpy(c->dev_w, blob, bytes, hipMemcpyHostToDevice) != hipSuccess) return dl_fail(c, BUGSEG_EHIP, "weight upload failed");
     c->w_bytes = bytes;
@@ -254,26 +270,64 @@ int bugseg_dl_load_weights(bugseg_dl *c, const void *blob, size_t bytes) {
     return BUGSEG_OK;
 }
 
-int bugseg_dl_set_plan(bugseg_dl *c, const int32_t *ops, int nops, const uint64_t *buf_bytes, int nbufs, int B, int Hc, int Wc) {
-    if (!c || !ops || nops < 1 || nbufs < 1 || !buf_bytes || B < 1 || Hc < 2 || Wc < 2) return dl_fail(c, BUGSEG_EINVAL, "bad plan");
-    if (!c->dev_w) return dl_fail(c, BUGSEG_ESTATE, "plan before weights");
-    DevGuard g(c->device);
-    std::vector<DlOp> v(nops);
+}  // extern "C"
+
+namespace {
+// Host-only validation of a whole plan (bugseg_dl_set_plan, and the ASan test hook below): every op
+// against the new buffers and a weight blob of w_bytes. -> arena layout in off / total.
+int validate_plan(bugseg_dl *c, int prec, size_t w_bytes, const int32_t *ops, int nops, const uint64_t *buf_bytes, int nbufs,
+                  int B, int Hc, int Wc, std::vector<DlOp> &v, std::vector<size_t> &bb, std::vector<size_t> &off,
+                  size_t &total) {
+    if (!ops || nops < 1 || nops > 4096 || nbufs < 1 || nbufs > 64 || !buf_bytes || B < 1 || Hc < 2 || Wc < 2 ||
+        Hc > 8192 || Wc > 8192)
+        return dl_fail(c, BUGSEG_EINVAL, "bad plan");
+    v.resize(nops);
     std::memcpy(v.data(), ops, sizeof(DlOp) * (size_t)nops);
-    std::vector<size_t> bb(buf_bytes, buf_bytes + nbufs), off(nbufs);
-    size_t total = 0;
+    bb.assign(buf_bytes, buf_bytes + nbufs);
+    off.resize(nbufs);
+    total = 0;
     for (int i = 0; i < nbufs; ++i) {
+        if (bb[i] > ((uint64_t)1 << 40)) return dl_fail(c, BUGSEG_EINVAL, "buffer " + std::to_string(i) + " too large");
         off[i] = total;
         total += (bb[i] + 255) & ~(size_t)255;
     }
-    // validate against the new plan before touching the old one
     bugseg_dl probe;
-    probe.prec = c->prec; probe.w_bytes = c->w_bytes; probe.buf_bytes = bb; probe.B = B; probe.Hc = Hc; probe.Wc = Wc;
+    probe.prec = prec; probe.w_bytes = w_bytes; probe.buf_bytes = bb; probe.B = B; probe.Hc = Hc; probe.Wc = Wc;
     for (int i = 0; i < nops; ++i) {
         std::string why;
         if (!check_op(&probe, v[i], why)) return dl_fail(c, BUGSEG_EINVAL, "op " + std::to_string(i) + ": " + why);
     }
-    if (c->arena) { (void)hipFree(c->arena); c->arena = nullptr; }
+    return BUGSEG_OK;
+}
+}  // namespace
+
+extern "C" {
+
+// Test hook (host only, no device): the validation bugseg_dl_set_plan runs, for a blob of w_bytes.
+int bugseg_dl_debug_check_plan(const int32_t *ops, int nops, const uint64_t *buf_bytes, int nbufs, int B, int Hc, int Wc,
+                               int precision, size_t w_bytes) {
+    std::vector<DlOp> v;
+    std::vector<size_t> bb, off;
+    size_t total = 0;
+    return validate_plan(nullptr, precision == BUGSEG_BF16 ? PREC_BF16 : PREC_F32, w_bytes, ops, nops, buf_bytes, nbufs, B,
+                         Hc, Wc, v, bb, off, total);
+}
+
+int bugseg_dl_set_plan(bugseg_dl *c, const int32_t *ops, int nops, const uint64_t *buf_bytes, int nbufs, int B, int Hc, int Wc) {
+    if (!c) return dl_fail(c, BUGSEG_EINVAL, "bad plan");
+    if (!c->dev_w) return dl_fail(c, BUGSEG_ESTATE, "plan before weights");
+    std::vector<DlOp> v;
+    std::vector<size_t> bb, off;
+    size_t total = 0;
+    // validate against the new plan before touching the old one
+    const int rc = validate_plan(c, c->prec, c->w_bytes, ops, nops, buf_bytes, nbufs, B, Hc, Wc, v, bb, off, total);
+    if (rc != BUGSEG_OK) return rc;
+    DevGuard g(c->device);
+    if (c->arena) {
+        (void)hipDeviceSynchronize();   // a forward of the old plan may still be running on any stream
+        (void)hipFree(c->arena);
+        c->arena = nullptr;
+    }
     if (hipMalloc(&c->arena, total) != hipSuccess) return dl_fail(c, BUGSEG_ENOMEM, "activation arena allocation failed");
     c->ops = std::move(v);
     c->buf_bytes = std::move(bb);

@@ -184,9 +184,9 @@ __global__ void __launch_bounds__(256) init_kernel(const ConvArgs a) {
             if constexpr (sizeof(T) == 2) {
                 typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
                 bf16x4 b = {(__bf16)v.x, (__bf16)v.y, (__bf16)v.z, (__bf16)v.w};
-                __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u32x2, b), rout, (int)off, 0, 0);
+                bst8o(rout, off, __builtin_bit_cast(u32x2, b));
             } else {
-                bst16(rout, off, __builtin_bit_cast(uint4, v));
+                bst16o(rout, off, __builtin_bit_cast(uint4, v));
             }
         }
     }

@@ -123,6 +123,18 @@ __device__ __forceinline__ uint4 bld16(__amdgpu_buffer_rsrc_t r, uint32_t off) {
 __device__ __forceinline__ void bst16(__amdgpu_buffer_rsrc_t r, uint32_t off, uint4 v) {
     __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, v), r, (int)off, 0, 0);
 }
+// Stores of a launch's output, which the launch itself never reads back: cache policy OUT_AUX (0 =
+// default; 16 = sc1 write-through, the line leaves the XCD's L2; 2 = nt), so a kernel's output
+// stream does not evict the input lines its neighbouring tiles still re-read from L2.
+#ifndef BUGSEG_OUT_AUX
+#define BUGSEG_OUT_AUX 0
+#endif
+__device__ __forceinline__ void bst16o(__amdgpu_buffer_rsrc_t r, uint32_t off, uint4 v) {
+    __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, v), r, (int)off, 0, BUGSEG_OUT_AUX);
+}
+__device__ __forceinline__ void bst8o(__amdgpu_buffer_rsrc_t r, uint32_t off, u32x2 v) {
+    __builtin_amdgcn_raw_buffer_store_b64(v, r, (int)off, 0, BUGSEG_OUT_AUX);
+}
 __device__ __forceinline__ void bld8(RawB &x, __amdgpu_buffer_rsrc_t r, uint32_t off) { x.v = bld16(r, off); }
 __device__ __forceinline__ void bld8(RawF &x, __amdgpu_buffer_rsrc_t r, uint32_t off) {
     x.a = __builtin_bit_cast(float4, bld16(r, off));

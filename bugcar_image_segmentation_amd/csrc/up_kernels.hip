@@ -178,15 +178,15 @@ __global__ void __launch_bounds__(256, (sizeof(T) == 2 ? (CIN >= 128 ? 2 : 3) : 
                     pl16swap(x0, y0);
                     pl16swap(x1, y1);
                     const int ch = (2 * t + (kq & 1)) * 16 + 8 * (kq >> 1);
-                    bst16(ro, pv ? (opix * COUT + ch) * ES : OOB, make_uint4(x0, x1, y0, y1));
+                    bst16o(ro, pv ? (opix * COUT + ch) * ES : OOB, make_uint4(x0, x1, y0, y1));
                 }
             } else {
 #pragma unroll
                 for (int r = 0; r < NR3; ++r) {
                     const float4 v = ep3(r);
                     const uint32_t off = pv ? (opix * COUT + r * 16 + kq * 4) * ES : OOB;
-                    if constexpr (ES == 2) __builtin_amdgcn_raw_buffer_store_b64(pack_bf16x4(v), ro, (int)off, 0, 0);
-                    else bst16(ro, off, __builtin_bit_cast(uint4, v));
+                    if constexpr (ES == 2) bst8o(ro, off, pack_bf16x4(v));
+                    else bst16o(ro, off, __builtin_bit_cast(uint4, v));
                 }
             }
         }

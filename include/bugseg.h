@@ -164,6 +164,14 @@ int bugseg_plan_launch_op(bugseg_ctx *ctx, int B, int H, int W, int op, void *st
 /* Last error message of ctx (or of the calling thread when ctx is NULL). Never NULL. */
 const char *bugseg_last_error(const bugseg_ctx *ctx);
 
+/* Test hooks (no reference counterpart; host only: no device is touched). The weight-blob parser
+ * and packer of bugseg_load_weights, and the polar-table builder of the laserscan mode, for the
+ * host-sanitizer tests (tests/asan: truncated / corrupted blobs under ASan + UBSan). Errors go to
+ * bugseg_last_error(NULL). */
+int bugseg_debug_parse_pack(const void *blob, size_t bytes, int precision, int *ncls);
+int bugseg_debug_polar_tables(int w, int h, int variant, int32_t *fmap, size_t fmap_n, int32_t *imap, size_t imap_n,
+                              int *pw, int *ph);
+
 /* ---- DeepLabV3 (BASELINE config 4) -------------------------------------
  * Replaces DeepLabV3 (models.py:98-136): tf.compat.v1.Session + GraphDef import (models.py:105-113)
  * and sess.run("ImageTensor:0" u8 -> "SemanticPredictions:0" int64) (models.py:115-125).
@@ -192,6 +200,10 @@ int bugseg_dl_launch_op(bugseg_dl *dl, int op, void *stream);
  * logits at the backbone resolution) to a device pointer, on `stream`. */
 int bugseg_dl_read_buffer(bugseg_dl *dl, int buf, void *dst_dev, size_t bytes, void *stream);
 const char *bugseg_dl_last_error(const bugseg_dl *dl);
+/* Test hook (host only): the plan validation of bugseg_dl_set_plan against a weight blob of w_bytes;
+ * errors go to bugseg_dl_last_error(NULL). */
+int bugseg_dl_debug_check_plan(const int32_t *ops, int nops, const uint64_t *buf_bytes, int nbufs, int B, int Hc, int Wc,
+                               int precision, size_t w_bytes);
 
 #ifdef __cplusplus
 }
