@@ -62,8 +62,8 @@ __device__ __forceinline__ WarpTap warp_tap(const BevArgs &a, int x, int y) {
 
 // Table entry of a template pixel (bits of .y): 0-4 ax, 5-9 ay, 10-13 which taps (top-left,
 // top-right, bottom-left, bottom-right) are inside the class map, 14 = the pixel lies outside the
-// template (a neutral 1 for the erode: OpenCV's default erode border is +inf). .x = the byte offset of
-// the top-left tap in the frame (sy * in_cols + sx). A pixel inside the template but outside the warped
+// template (a neutral 1 for the erode: OpenCV's default erode border is +inf). .x = the top-left tap
+// (sy << 16 | sx & 0xffff, both 16-bit signed). A pixel inside the template but outside the warped
 // image has no valid tap: value 0 (the crop/pad of bev.py:183-195).
 constexpr uint32_t TAB_OUT = 1u << 14;
 __device__ __forceinline__ uint2 tab_entry(const BevArgs &a, int tx, int ty) {
@@ -73,7 +73,7 @@ __device__ __forceinline__ uint2 tab_entry(const BevArgs &a, int tx, int ty) {
     const WarpTap t = warp_tap(a, wx, wy);
     const uint32_t valid = (uint32_t)(t.y0 && t.x0) | (uint32_t)(t.y0 && t.x1) << 1 | (uint32_t)(t.y1 && t.x0) << 2 |
                            (uint32_t)(t.y1 && t.x1) << 3;
-    return make_uint2((uint32_t)(t.sy * a.in_cols + t.sx), (uint32_t)t.ax | (uint32_t)t.ay << 5 | valid << 10);
+    return make_uint2((uint32_t)t.sy << 16 | ((uint32_t)t.sx & 0xffffu), (uint32_t)t.ax | (uint32_t)t.ay << 5 | valid << 10);
 }
 
 // template pixel sampled by cell (cx, cy): resizeNN (bev.py:209), src = min(floor(d * inv_scale), size - 1)
@@ -102,38 +102,87 @@ __global__ void __launch_bounds__(256) bev_table_kernel(const BevArgs a) {
 
 // value of a template pixel from its table entry: the bilinear Q15 blend of segmap + 1 (bev.py:177;
 // taps outside the class map read the border value 0), (sum + 2^14) >> 15
+__device__ __forceinline__ int tap_sy(uint2 e) { return (int)e.x >> 16; }
+__device__ __forceinline__ int tap_sx(uint2 e) { return (int)(short)(e.x & 0xffffu); }
+typedef unsigned short bev_u16x2 __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ uint32_t dot2(uint32_t a, uint32_t b, uint32_t c) {
+    return __builtin_amdgcn_udot2(__builtin_bit_cast(bev_u16x2, a), __builtin_bit_cast(bev_u16x2, b), c, false);
+}
+// labels (segmap + 1, uint8 wrap-around as np.add on uint8) of the 4 taps, 0 outside the class map,
+// blended in Q15 with three v_dot2_u32_u16: (32 - ax) | ax << 16 weights each row pair, then the rows.
+// Each tap row is ONE 2-byte load (byte-aligned: gfx950 buffer loads need no alignment) of the pair
+// (sx, sx + 1), shifted by one byte where one of the two lies outside the class map, so the load never
+// leaves the tap's image row.
+__device__ __forceinline__ uint32_t tap_pair(__amdgpu_buffer_rsrc_t seg, uint32_t b, bool v0, bool v1) {
+    const uint32_t off = v0 ? (v1 ? b : b - 1) : (v1 ? b + 1 : 0x80000000u);
+    const uint32_t r = __builtin_amdgcn_raw_buffer_load_b16(seg, (int)off, 0, 0);
+    const uint32_t lo = v0 ? (((v1 ? r : r >> 8) + 1) & 255u) : 0u;              // byte sx  (+1)
+    const uint32_t hi = v1 ? ((((v0 ? r >> 8 : r) & 255u) + 1) & 255u) : 0u;     // byte sx+1 (+1)
+    return lo | hi << 16;
+}
 __device__ __forceinline__ int tab_value(__amdgpu_buffer_rsrc_t seg, int w, uint2 e) {
     const uint32_t m = e.y;
-    const int ax = m & 31, ay = (m >> 5) & 31;
-    const uint32_t b = e.x;
-    const int v0 = __builtin_amdgcn_raw_buffer_load_b8(seg, (int)((m & (1u << 10)) ? b : 0x80000000u), 0, 0);
-    const int v1 = __builtin_amdgcn_raw_buffer_load_b8(seg, (int)((m & (1u << 11)) ? b + 1 : 0x80000000u), 0, 0);
-    const int v2 = __builtin_amdgcn_raw_buffer_load_b8(seg, (int)((m & (1u << 12)) ? b + w : 0x80000000u), 0, 0);
-    const int v3 = __builtin_amdgcn_raw_buffer_load_b8(seg, (int)((m & (1u << 13)) ? b + w + 1 : 0x80000000u), 0, 0);
-    const int c0 = (m >> 10) & 1, c1 = (m >> 11) & 1, c2 = (m >> 12) & 1, c3 = (m >> 13) & 1;   // + 1 inside
-    const int acc = ((v0 + c0) * (32 - ax) * (32 - ay) + (v1 + c1) * ax * (32 - ay) + (v2 + c2) * (32 - ax) * ay +
-                     (v3 + c3) * ax * ay) * 32;
-    const int v = (acc + (1 << 14)) >> 15;
-    return v > 255 ? 255 : v;
+    const uint32_t b = (uint32_t)(__mul24(tap_sy(e), w) + tap_sx(e));
+    const uint32_t t0 = tap_pair(seg, b, m & (1u << 10), m & (1u << 11));
+    const uint32_t t1 = tap_pair(seg, b + w, m & (1u << 12), m & (1u << 13));
+    const uint32_t ax = m & 31u, ay = (m >> 5) & 31u;
+    const uint32_t wx = 32u + ax * 65535u, wy = 32u + ay * 65535u;
+    const uint32_t top = dot2(t0, wx, 0u), bot = dot2(t1, wx, 0u);
+    return (int)(dot2(top | bot << 16, wy, 512u) >> 10);
 }
 
 // occupied template values: {1, 3} (bev.py:196), or {1} in the binary variant (bev.py:128)
-__device__ __forceinline__ bool occupied(const BevArgs &a, int v) { return v == 1 || (v == 3 && !a.variant); }
+__device__ __forceinline__ bool occupied(const BevArgs &a, int v) {
+    return (v == 1) | ((v == 3) & !a.variant);      // bitwise: no divergent branch per tap
+}
 
 // F frames per thread (the cell's table entries are loaded once and serve all F), the 3x3 around the
 // sample evaluated eagerly (one round of 36 gathers per frame instead of a dependent centre-then-
 // neighbours chain); the 16-pixel ring only for the frames whose 3x3 does not settle the opening.
+// encode template value v of cell (cx, cy) of frame b and store it (or, in the laserscan mode, the
+// polar warp's source)
+__device__ __forceinline__ void bev_emit(const BevArgs &a, int b, int rem, int cx, int cy, long cells, int v) {
+    const long o_i = (long)b * cells + rem;
+    int8_t o;
+    if (!a.variant) {
+        const int gg = v == 3 ? 1 : v;               // bev.py:242
+        o = (int8_t)(gg == 0 ? -1 : 200 - 100 * gg);   // bev.py:244-245
+    } else {
+        // bev.py:139-144, :165 in uint8 arithmetic: {0:-1, 1:100, 2:0, 3:-100}
+        const uint8_t gg = (uint8_t)(v * 100);
+        o = (int8_t)(uint8_t)(gg == 0 ? 0xff : (uint8_t)(200 - gg));
+    }
+    if (a.laserscan) {
+        // the polar warp's source: the cells (bev.py:219) or the encoded grid (bev.py:146)
+        a.cells[o_i] = a.variant ? (uint8_t)o : (uint8_t)v;
+        if (!a.variant) return;                      // the final laserscan kernel writes out
+    }
+    if (a.ros_layout) {
+        // occgrid_to_ros.py:18-21: flip(0) then rot90ccw == G[::-1, ::-1].T, shape (occ_w, occ_h)
+        a.out[(size_t)b * cells + (size_t)(a.occ_w - 1 - cx) * a.occ_h + (a.occ_h - 1 - cy)] = o;
+    } else {
+        a.out[o_i] = o;
+    }
+}
+
+// XCD-aware work split: the grid is a multiple of 8 and the blocks b with b % 8 == x (one XCD under
+// round-robin dispatch; speed only, never correctness) take grid rows [x*rows, (x+1)*rows) of every
+// frame. A band of grid rows is a band of distances, i.e. a band of class-map rows, so each XCD's L2
+// holds 1/8 of the tap table and 1/8 of every class map instead of all of both.
 template <int F>
 __global__ void __launch_bounds__(256) bev_occgrid_kernel(const BevArgs a) {
     const long cells = (long)a.occ_h * a.occ_w;
     const int groups = (a.B + F - 1) / F;
-    const long total = cells * groups;
+    const int xcd = blockIdx.x & 7, slot = blockIdx.x >> 3, nslot = gridDim.x >> 3;
+    const int rows = (a.occ_h + 7) >> 3, r0 = min(a.occ_h, xcd * rows), r1 = min(a.occ_h, r0 + rows);
+    const long band = (long)(r1 - r0) * a.occ_w;
+    const long total = band * groups;
     const uint32_t frame_bytes = (uint32_t)a.in_rows * (uint32_t)a.in_cols;
     // the 3x3 around p: window positions B5(dx, dy), dx, dy in -1..1, in row order
     constexpr int K3[9] = {6, 7, 8, 11, 12, 13, 16, 17, 18};
-    for (long i = blockIdx.x * 256L + threadIdx.x; i < total; i += (long)gridDim.x * 256) {
-        const int g = (int)(i / cells);
-        const int rem = (int)(i - (long)g * cells);
+    for (long j = slot * 256L + threadIdx.x; j < total; j += (long)nslot * 256) {
+        const int g = (int)(j / band);
+        const int rem = (int)((long)r0 * a.occ_w + (j - (long)g * band));
         const int cy = rem / a.occ_w, cx = rem - cy * a.occ_w;
         const uint2 *tab = a.wtab + rem;
         uint2 e3[9];
@@ -206,28 +255,163 @@ __global__ void __launch_bounds__(256) bev_occgrid_kernel(const BevArgs a) {
         for (int f = 0; f < F; ++f) {
             const int b = g * F + f;
             if (b >= a.B) break;
-            const long o_i = (long)b * cells + rem;
-            int8_t o;
-            if (!a.variant) {
-                const int gg = v[f] == 3 ? 1 : v[f];     // bev.py:242
-                o = (int8_t)(gg == 0 ? -1 : 200 - 100 * gg);   // bev.py:244-245
-            } else {
-                // bev.py:139-144, :165 in uint8 arithmetic: {0:-1, 1:100, 2:0, 3:-100}
-                const uint8_t gg = (uint8_t)(v[f] * 100);
-                o = (int8_t)(uint8_t)(gg == 0 ? 0xff : (uint8_t)(200 - gg));
+            bev_emit(a, b, rem, cx, cy, cells, v[f]);
+        }
+    }
+}
+
+// ---- LDS-staged form (the default when in_cols % 16 == 0): a workgroup owns a 16 x 16 block of
+// cells and a group of frames. The taps of every template pixel its cells need fall in one box of the
+// class map (fixed by the geometry; found once per workgroup from the table). Each frame's box is read
+// once with coalesced 16-B loads into LDS as segmap + 1 (bev.py:177, uint8 wrap-around), with a
+// border of zeros where the box leaves the image — exactly warpPerspective's BORDER_CONSTANT taps — so
+// every one of a cell's 25 x 4 taps is an unmasked LDS byte read and the Q15 blend is three
+// v_dot2_u32_u16; the next frame's box is in flight in registers while the current one is evaluated.
+// A block whose box exceeds BEV_BOX_CAP (or has no valid tap) gathers from global memory instead, with
+// the same arithmetic.
+constexpr int BEV_CB = 16, BEV_BOX_CAP = 32768, BEV_PF = BEV_BOX_CAP / 16 / 256;   // 16-B chunks per thread
+// per-byte x + 1 mod 256 of 4 packed bytes (no carry between bytes)
+__device__ __forceinline__ uint32_t inc4(uint32_t v) { return ((v & 0x7f7f7f7fu) + 0x01010101u) ^ (v & 0x80808080u); }
+
+__global__ void __launch_bounds__(256, 4) bev_occgrid_lds_kernel(const BevArgs a, int fg) {
+    __shared__ __attribute__((aligned(16))) uint8_t box[BEV_BOX_CAP];
+    __shared__ int red[4];
+    const int tid = threadIdx.x;
+    const long cells = (long)a.occ_h * a.occ_w;
+    const int nbx = (a.occ_w + BEV_CB - 1) / BEV_CB, nby = (a.occ_h + BEV_CB - 1) / BEV_CB, nblk = nbx * nby;
+    const int blk = blockIdx.x % nblk, grp = blockIdx.x / nblk;
+    const int cx = (blk % nbx) * BEV_CB + (tid & 15), cy = (blk / nbx) * BEV_CB + (tid >> 4);
+    const bool cell_ok = cx < a.occ_w && cy < a.occ_h;
+    const int rem = cell_ok ? cy * a.occ_w + cx : 0;
+    const uint2 *tab = a.wtab + rem;
+    // the class-map box of every valid tap of the block: rows [ylo, yhi], columns [xlo, xhi]
+    int ylo = 1 << 30, yhi = -(1 << 30), xlo = 1 << 30, xhi = -(1 << 30);
+    uint32_t outm = 0;                              // window positions outside the template
+    if (cell_ok) {
+#pragma unroll
+        for (int k = 0; k < BEV_WIN; ++k) {
+            const uint2 e = tab[(long)k * cells];
+            const uint32_t v = (e.y >> 10) & 15;
+            const int sy = tap_sy(e), sx = tap_sx(e);
+            if (v & 3) { ylo = min(ylo, sy); yhi = max(yhi, sy); }
+            if (v & 12) { ylo = min(ylo, sy + 1); yhi = max(yhi, sy + 1); }
+            if (v & 5) { xlo = min(xlo, sx); xhi = max(xhi, sx); }
+            if (v & 10) { xlo = min(xlo, sx + 1); xhi = max(xhi, sx + 1); }
+            outm |= (uint32_t)((e.y & TAB_OUT) != 0) << k;
+        }
+    } else {
+        outm = (1u << BEV_WIN) - 1;
+    }
+    if (tid < 4) red[tid] = tid & 1 ? -(1 << 30) : (1 << 30);
+    __syncthreads();
+    atomicMin(&red[0], ylo); atomicMax(&red[1], yhi); atomicMin(&red[2], xlo); atomicMax(&red[3], xhi);
+    __syncthreads();
+    // the box with a one-pixel border: rows [ylo - 1, yhi + 1], columns [xa, xb) in whole 16-B chunks,
+    // then a 16-B-aligned zero pad that tap-less template pixels read
+    const int y0 = red[0] - 1, bh = red[1] - red[0] + 3;
+    const int xa = (red[2] - 1) & ~15, bw = ((red[3] + 17) & ~15) - xa;
+    const int zpad = bh * bw;
+    const bool lds = red[1] >= red[0] && (long)bh * bw + 2 * bw + 16 <= BEV_BOX_CAP;   // workgroup-uniform
+    const int cpr = lds ? bw >> 4 : 1, nch = lds ? bh * cpr : 0;          // 16-B chunks per row / in all
+    const uint32_t frame_bytes = (uint32_t)a.in_rows * (uint32_t)a.in_cols;
+    // this thread's chunks q = tid + 256 i of the box: LDS offset 16 q (rows of bw bytes), global
+    // offset, or OOB where the chunk lies outside the image (whole chunks: in_cols % 16 == 0)
+    uint32_t goff[BEV_PF];
+#pragma unroll
+    for (int i = 0; i < BEV_PF; ++i) {
+        const int q = tid + 256 * i;
+        const int r = q / cpr, c = q - r * cpr;
+        const int gy = y0 + r, gx = xa + c * 16;
+        const bool in = q < nch && (unsigned)gy < (unsigned)a.in_rows && (unsigned)gx < (unsigned)a.in_cols;
+        goff[i] = in ? (uint32_t)(gy * a.in_cols + gx) : 0x80000000u;
+    }
+    // per window position ONE register: the top-left tap's offset in the box (16 bits) | ax << 16 |
+    // ay << 21; a template pixel with no tap inside the class map reads the zero pad
+    uint32_t ek[BEV_WIN];
+    if (lds) {
+#pragma unroll
+        for (int k = 0; k < BEV_WIN; ++k) {
+            const uint2 e = cell_ok ? tab[(long)k * cells] : make_uint2(0u, TAB_OUT);
+            const bool any = ((e.y >> 10) & 15) != 0;
+            const int o = any ? (tap_sy(e) - y0) * bw + (tap_sx(e) - xa) : zpad;
+            ek[k] = (uint32_t)o | (e.y & 1023u) << 16;
+        }
+    }
+    auto frame_rsrc = [&](int b) {
+        return __builtin_amdgcn_make_buffer_rsrc(const_cast<uint8_t *>(a.seg) + (size_t)(b < a.B ? b : 0) * frame_bytes,
+                                                 (short)0, b < a.B ? (int)frame_bytes : 0, 0x00020000);
+    };
+    uint4 pf[BEV_PF];
+    auto fetch = [&](int b) {
+        const auto r = frame_rsrc(b);
+#pragma unroll
+        for (int i = 0; i < BEV_PF; ++i) pf[i] = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(r, (int)goff[i], 0, 0));
+    };
+    const int b0 = grp * fg;
+    if (lds) {
+        fetch(b0);
+        for (int i = tid; i < 2 * bw + 16; i += 256) box[zpad + i] = 0;
+    }
+    const uint32_t inner = 0x739C0u;                // bits of the 3x3 around p: rows 1..3, cols 1..3
+    int tx = 0, ty = 0;
+    cell_pixel(a, cx, cy, tx, ty);
+    // windows of the 9 q in N3(p) that lie inside the template
+    uint32_t wins[9];
+#pragma unroll
+    for (int qy = -1; qy <= 1; ++qy)
+#pragma unroll
+        for (int qx = -1; qx <= 1; ++qx) {
+            const bool inside = (unsigned)(tx + qx) < (unsigned)a.occ_w_px && (unsigned)(ty + qy) < (unsigned)a.occ_h_px;
+            const int sh = qy * 5 + qx;
+            wins[(qy + 1) * 3 + qx + 1] = inside ? (sh >= 0 ? inner << sh : inner >> -sh) : 0xffffffffu;
+        }
+    for (int fi = 0; fi < fg; ++fi) {
+        const int b = b0 + fi;
+        if (b >= a.B) break;                        // workgroup-uniform
+        uint32_t msk = 0;
+        int v = 0;
+        if (lds) {
+            __syncthreads();                        // the previous frame's reads of the box are done
+#pragma unroll
+            for (int i = 0; i < BEV_PF; ++i)
+                if (tid + 256 * i < nch)
+                    *reinterpret_cast<uint4 *>(box + 16 * (tid + 256 * i)) =
+                        goff[i] == 0x80000000u ? make_uint4(0u, 0u, 0u, 0u)
+                                               : make_uint4(inc4(pf[i].x), inc4(pf[i].y), inc4(pf[i].z), inc4(pf[i].w));
+            __syncthreads();
+            if (fi + 1 < fg && b + 1 < a.B) fetch(b + 1);   // next frame's box flies during this frame
+#pragma unroll 5
+            for (int k = 0; k < BEV_WIN; ++k) {
+                const uint32_t e = ek[k];
+                const uint8_t *p = box + (e & 0xffffu);
+                const uint32_t l0 = p[0], l1 = p[1], l2 = p[bw], l3 = p[bw + 1];
+                const uint32_t ax = (e >> 16) & 31u, ay = (e >> 21) & 31u;
+                const uint32_t wx = 32u + ax * 65535u, wy = 32u + ay * 65535u;   // (32 - a) | a << 16
+                const uint32_t top = dot2(l0 | l1 << 16, wx, 0u), bot = dot2(l2 | l3 << 16, wx, 0u);
+                const int t = (int)(dot2(top | bot << 16, wy, 512u) >> 10);      // (sum + 2^14) >> 15 of OpenCV
+                if (k == B5(0, 0)) v = t;
+                msk |= (uint32_t)occupied(a, t) << k;
             }
-            if (a.laserscan) {
-                // the polar warp's source: the cells (bev.py:219) or the encoded grid (bev.py:146)
-                a.cells[o_i] = a.variant ? (uint8_t)o : (uint8_t)v[f];
-                if (!a.variant) continue;        // the final laserscan kernel writes out
-            }
-            if (a.ros_layout) {
-                // occgrid_to_ros.py:18-21: flip(0) then rot90ccw == G[::-1, ::-1].T, shape (occ_w, occ_h)
-                a.out[(size_t)b * cells + (size_t)(a.occ_w - 1 - cx) * a.occ_h + (a.occ_h - 1 - cy)] = o;
-            } else {
-                a.out[o_i] = o;
+        } else {
+            const auto seg = frame_rsrc(b);
+#pragma unroll 1
+            for (int k = 0; k < BEV_WIN; ++k) {
+                const uint2 e = cell_ok ? tab[(long)k * cells] : make_uint2(0u, TAB_OUT);
+                const int t = tab_value(seg, a.in_cols, e);
+                if (k == B5(0, 0)) v = t;
+                msk |= (uint32_t)occupied(a, t) << k;
             }
         }
+        if (!cell_ok) continue;
+        msk |= outm;                                // outside the template: the erode's +inf border
+        if (occupied(a, v)) {
+            // opening at p = OR over q in N3(p) (inside the template) of AND over N3(q) of occupancy
+            bool opened = false;
+#pragma unroll
+            for (int q = 0; q < 9; ++q) opened |= (msk & wins[q]) == wins[q];
+            if (!opened) v = 2;                     // isolated occupied pixel -> free (bev.py:204-205)
+        }
+        bev_emit(a, b, rem, cx, cy, cells, v);
     }
 }
 
@@ -310,13 +494,24 @@ hipError_t launch_bev_table(const BevArgs &a, hipStream_t s) {
 }
 
 hipError_t launch_bev(const BevArgs &a, hipStream_t s) {
-    static const int F = [] { const char *e = std::getenv("BUGSEG_BEV_F"); return e ? std::atoi(e) : 2; }();
+    // form (measured, scripts/bev_probe.py): the gather kernel, 1 frame per thread (BUGSEG_BEV_F = 2 / 4:
+    // frames per thread; BUGSEG_BEV_FG = n > 0: the LDS-staged kernel with n frames per workgroup);
+    // read per call so tests can exercise every form
+    const char *fe = std::getenv("BUGSEG_BEV_F");
+    const int F = fe ? std::atoi(fe) : 1;
     const long total = (long)a.occ_h * a.occ_w * a.B;
     const int f = F == 4 ? 4 : F == 1 ? 1 : 2;
-    long gf = ((long)a.occ_h * a.occ_w * ((a.B + f - 1) / f) + 255) / 256;
+    const long band = (long)((a.occ_h + 7) / 8) * a.occ_w * ((a.B + f - 1) / f);   // items of one XCD
+    long gf = 8 * ((band + 255) / 256);
     if (gf > 8192) gf = 8192;
-    if (gf < 1) gf = 1;
-    if (f == 1) hipLaunchKernelGGL(bev_occgrid_kernel<1>, dim3((unsigned)gf), dim3(256), 0, s, a);
+    if (gf < 8) gf = 8;
+    const char *fge = std::getenv("BUGSEG_BEV_FG");
+    const int FG = fge ? std::atoi(fge) : 0;
+    if (F != 0 && a.in_cols % 16 == 0 && FG > 0) {
+        const long nblk = (long)((a.occ_w + BEV_CB - 1) / BEV_CB) * ((a.occ_h + BEV_CB - 1) / BEV_CB);
+        const long grid = nblk * ((a.B + FG - 1) / FG);
+        if (grid < (1L << 31)) hipLaunchKernelGGL(bev_occgrid_lds_kernel, dim3((unsigned)grid), dim3(256), 0, s, a, FG);
+    } else if (f == 1) hipLaunchKernelGGL(bev_occgrid_kernel<1>, dim3((unsigned)gf), dim3(256), 0, s, a);
     else if (f == 2) hipLaunchKernelGGL(bev_occgrid_kernel<2>, dim3((unsigned)gf), dim3(256), 0, s, a);
     else hipLaunchKernelGGL(bev_occgrid_kernel<4>, dim3((unsigned)gf), dim3(256), 0, s, a);
     long g = (total + 255) / 256;

@@ -144,19 +144,28 @@ def _bev_case(rows, cols, ww, wh, seed):
     return bev
 
 
+@pytest.mark.parametrize("form", [None, "FG4", "F2"])
 @pytest.mark.parametrize("rows,cols,ww,wh,grid,seed", [
     (480, 640, 1000, 1000, (10.0, 10.0, 0.05), 0),
     (120, 160, 300, 260, (3.0, 2.0, 0.05), 1),
     (96, 128, 250, 180, (3.1, 2.7, 0.07), 2),     # template wider than the warp (negative left_x/top_y)
     (64, 80, 200, 150, (1.0, 1.0, 0.1), 3),
 ])
-def test_bev_occgrid_bit_exact(gpu, rows, cols, ww, wh, grid, seed):
+def test_bev_occgrid_bit_exact(gpu, rows, cols, ww, wh, grid, seed, form, monkeypatch):
+    """Every form of the rasteriser (bev_kernels.hip: the default gather kernel, the LDS-staged one,
+    2 frames per thread) is bit-exact against the C restatement; class maps with labels past the
+    3-class range (up to 255: segmap + 1 wraps in uint8 as np.add does, bev.py:177) included."""
+    if form == "FG4":
+        monkeypatch.setenv("BUGSEG_BEV_FG", "4")
+    elif form == "F2":
+        monkeypatch.setenv("BUGSEG_BEV_F", "2")
     bev = _bev_case(rows, cols, ww, wh, seed)
     rng = np.random.default_rng(seed)
     # blocky class maps (realistic regions + speckles) and pure noise
     blocky = np.kron(rng.integers(0, 3, size=(rows // 8, cols // 8)), np.ones((8, 8), np.int64)).astype(np.uint8)
     noise = rng.integers(0, 3, size=(rows, cols)).astype(np.uint8)
-    segs = np.stack([blocky, noise])
+    wide = rng.integers(0, 256, size=(rows, cols)).astype(np.uint8)
+    segs = np.stack([blocky, noise, wide])
     ref = np.stack([ocv_c.create_occupancy_grid(s, bev._bev_matrix, ww, wh, 1.0, *grid) for s in segs])
     got = bev.create_occupancy_grid_device(torch.from_numpy(segs).cuda(), *grid).cpu().numpy()
     assert got.dtype == np.int8 and got.shape == ref.shape
