@@ -87,23 +87,37 @@ __device__ __forceinline__ void cell_pixel(const BevArgs &a, int cx, int cy, int
 // bit index of offset (dx, dy) in the 5x5 window around p
 #define B5(dx, dy) (((dy) + 2) * 5 + ((dx) + 2))
 
-// One thread per (cell, window position): the geometry-only half of the rasteriser, run once per
+// Table order of the window positions B5(dx, dy): the sample itself and its 3x3 first (one round of
+// 5 slots serves every cell), then the 16-pixel ring (8 more slots, read only when the 3x3 does not
+// settle the opening); entry i lives in slot i / 2, half i % 2.
+__device__ constexpr int BEV_ORDER[BEV_WIN] = {12, 6, 7, 8, 11, 13, 16, 17, 18,
+                                               0, 1, 2, 3, 4, 5, 9, 10, 14, 15, 19, 20, 21, 22, 23, 24};
+__device__ __forceinline__ uint2 slot_half(const uint4 &s, int h) { return h ? make_uint2(s.z, s.w) : make_uint2(s.x, s.y); }
+
+// One thread per (cell, table slot): the geometry-only half of the rasteriser, run once per
 // calibration. Everything per frame (bev_occgrid_kernel) is then integer gathers and Q15 arithmetic.
 __global__ void __launch_bounds__(256) bev_table_kernel(const BevArgs a) {
-    const long cells = (long)a.occ_h * a.occ_w, total = cells * BEV_WIN;
+    const long cells = (long)a.occ_h * a.occ_w, total = cells * BEV_SLOTS;
     for (long i = blockIdx.x * 256L + threadIdx.x; i < total; i += (long)gridDim.x * 256) {
-        const int k = (int)(i / cells), c = (int)(i - (long)k * cells);
+        const int j = (int)(i / cells), c = (int)(i - (long)j * cells);
         const int cy = c / a.occ_w, cx = c - cy * a.occ_w;
         int tx, ty;
         cell_pixel(a, cx, cy, tx, ty);
-        a.wtab[i] = tab_entry(a, tx + k % 5 - 2, ty + k / 5 - 2);
+        const int k0 = BEV_ORDER[2 * j];
+        const uint2 e0 = tab_entry(a, tx + k0 % 5 - 2, ty + k0 / 5 - 2);
+        uint2 e1 = make_uint2(0u, TAB_OUT);
+        if (2 * j + 1 < BEV_WIN) {
+            const int k1 = BEV_ORDER[2 * j + 1];
+            e1 = tab_entry(a, tx + k1 % 5 - 2, ty + k1 / 5 - 2);
+        }
+        a.wtab[i] = make_uint4(e0.x, e0.y, e1.x, e1.y);
     }
 }
 
-// value of a template pixel from its table entry: the bilinear Q15 blend of segmap + 1 (bev.py:177;
-// taps outside the class map read the border value 0), (sum + 2^14) >> 15
+// the top-left tap of a table entry (.x = sy << 16 | sx & 0xffff)
 __device__ __forceinline__ int tap_sy(uint2 e) { return (int)e.x >> 16; }
 __device__ __forceinline__ int tap_sx(uint2 e) { return (int)(short)(e.x & 0xffffu); }
+
 typedef unsigned short bev_u16x2 __attribute__((ext_vector_type(2)));
 __device__ __forceinline__ uint32_t dot2(uint32_t a, uint32_t b, uint32_t c) {
     return __builtin_amdgcn_udot2(__builtin_bit_cast(bev_u16x2, a), __builtin_bit_cast(bev_u16x2, b), c, false);
@@ -178,16 +192,15 @@ __global__ void __launch_bounds__(256) bev_occgrid_kernel(const BevArgs a) {
     const long band = (long)(r1 - r0) * a.occ_w;
     const long total = band * groups;
     const uint32_t frame_bytes = (uint32_t)a.in_rows * (uint32_t)a.in_cols;
-    // the 3x3 around p: window positions B5(dx, dy), dx, dy in -1..1, in row order
-    constexpr int K3[9] = {6, 7, 8, 11, 12, 13, 16, 17, 18};
     for (long j = slot * 256L + threadIdx.x; j < total; j += (long)nslot * 256) {
         const int g = (int)(j / band);
         const int rem = (int)((long)r0 * a.occ_w + (j - (long)g * band));
         const int cy = rem / a.occ_w, cx = rem - cy * a.occ_w;
-        const uint2 *tab = a.wtab + rem;
-        uint2 e3[9];
+        const uint4 *tab = a.wtab + rem;
+        // table entries 0..8: the sample and its 3x3 (slots 0..4; slot 4's second half is ring entry 9)
+        uint4 s3[5];
 #pragma unroll
-        for (int k = 0; k < 9; ++k) e3[k] = tab[(long)K3[k] * cells];
+        for (int q = 0; q < 5; ++q) s3[q] = tab[(long)q * cells];
         __amdgpu_buffer_rsrc_t seg[F];
 #pragma unroll
         for (int f = 0; f < F; ++f) {
@@ -202,12 +215,13 @@ __global__ void __launch_bounds__(256) bev_occgrid_kernel(const BevArgs a) {
         for (int f = 0; f < F; ++f) {
             m[f] = 0;
 #pragma unroll
-            for (int k = 0; k < 9; ++k) {
-                const int t = tab_value(seg[f], a.in_cols, e3[k]);
-                if (k == 4) v[f] = t;
+            for (int i = 0; i < 9; ++i) {
+                const uint2 e = slot_half(s3[i >> 1], i & 1);
+                const int t = tab_value(seg[f], a.in_cols, e);
+                if (i == 0) v[f] = t;
                 // outside the template: 1 (neutral for the erode: OpenCV's default erode border is +inf)
-                const bool o = (e3[k].y & TAB_OUT) || occupied(a, t);
-                m[f] |= (uint32_t)o << K3[k];
+                const bool o = (e.y & TAB_OUT) || occupied(a, t);
+                m[f] |= (uint32_t)o << BEV_ORDER[i];
             }
         }
         const uint32_t inner = 0x739C0u;            // bits of the 3x3 around p: rows 1..3, cols 1..3
@@ -220,23 +234,17 @@ __global__ void __launch_bounds__(256) bev_occgrid_kernel(const BevArgs a) {
             // is not (if it is, q = p already survives the erode)
             int tx, ty;
             cell_pixel(a, cx, cy, tx, ty);
-            uint2 er[16];
-            {
-                int n = 0;
+            uint4 sr[8];
 #pragma unroll
-                for (int k = 0; k < 25; ++k)
-                    if (k % 5 == 0 || k % 5 == 4 || k / 5 == 0 || k / 5 == 4) er[n++] = tab[(long)k * cells];
-            }
+            for (int q = 0; q < 8; ++q) sr[q] = tab[(long)(q + 5) * cells];
 #pragma unroll
             for (int f = 0; f < F; ++f) {
                 if (!(occupied(a, v[f]) && (m[f] & inner) != inner)) continue;
-                int n = 0;
 #pragma unroll
-                for (int k = 0; k < 25; ++k) {
-                    if (!(k % 5 == 0 || k % 5 == 4 || k / 5 == 0 || k / 5 == 4)) continue;
-                    const uint2 e = er[n++];
+                for (int i = 9; i < BEV_WIN; ++i) {
+                    const uint2 e = i == 9 ? slot_half(s3[4], 1) : slot_half(sr[(i >> 1) - 5], i & 1);
                     const bool o = (e.y & TAB_OUT) || occupied(a, tab_value(seg[f], a.in_cols, e));
-                    m[f] |= (uint32_t)o << k;
+                    m[f] |= (uint32_t)o << BEV_ORDER[i];
                 }
                 bool opened = false;
 #pragma unroll
@@ -283,21 +291,22 @@ __global__ void __launch_bounds__(256, 4) bev_occgrid_lds_kernel(const BevArgs a
     const int cx = (blk % nbx) * BEV_CB + (tid & 15), cy = (blk / nbx) * BEV_CB + (tid >> 4);
     const bool cell_ok = cx < a.occ_w && cy < a.occ_h;
     const int rem = cell_ok ? cy * a.occ_w + cx : 0;
-    const uint2 *tab = a.wtab + rem;
+    const uint4 *tab = a.wtab + rem;
+    auto ent = [&](int i) { return slot_half(tab[(long)(i >> 1) * cells], i & 1); };   // table entry i
     // the class-map box of every valid tap of the block: rows [ylo, yhi], columns [xlo, xhi]
     int ylo = 1 << 30, yhi = -(1 << 30), xlo = 1 << 30, xhi = -(1 << 30);
     uint32_t outm = 0;                              // window positions outside the template
     if (cell_ok) {
 #pragma unroll
         for (int k = 0; k < BEV_WIN; ++k) {
-            const uint2 e = tab[(long)k * cells];
+            const uint2 e = ent(k);
             const uint32_t v = (e.y >> 10) & 15;
             const int sy = tap_sy(e), sx = tap_sx(e);
             if (v & 3) { ylo = min(ylo, sy); yhi = max(yhi, sy); }
             if (v & 12) { ylo = min(ylo, sy + 1); yhi = max(yhi, sy + 1); }
             if (v & 5) { xlo = min(xlo, sx); xhi = max(xhi, sx); }
             if (v & 10) { xlo = min(xlo, sx + 1); xhi = max(xhi, sx + 1); }
-            outm |= (uint32_t)((e.y & TAB_OUT) != 0) << k;
+            outm |= (uint32_t)((e.y & TAB_OUT) != 0) << BEV_ORDER[k];
         }
     } else {
         outm = (1u << BEV_WIN) - 1;
@@ -331,7 +340,7 @@ __global__ void __launch_bounds__(256, 4) bev_occgrid_lds_kernel(const BevArgs a
     if (lds) {
 #pragma unroll
         for (int k = 0; k < BEV_WIN; ++k) {
-            const uint2 e = cell_ok ? tab[(long)k * cells] : make_uint2(0u, TAB_OUT);
+            const uint2 e = cell_ok ? ent(k) : make_uint2(0u, TAB_OUT);
             const bool any = ((e.y >> 10) & 15) != 0;
             const int o = any ? (tap_sy(e) - y0) * bw + (tap_sx(e) - xa) : zpad;
             ek[k] = (uint32_t)o | (e.y & 1023u) << 16;
@@ -389,17 +398,17 @@ __global__ void __launch_bounds__(256, 4) bev_occgrid_lds_kernel(const BevArgs a
                 const uint32_t wx = 32u + ax * 65535u, wy = 32u + ay * 65535u;   // (32 - a) | a << 16
                 const uint32_t top = dot2(l0 | l1 << 16, wx, 0u), bot = dot2(l2 | l3 << 16, wx, 0u);
                 const int t = (int)(dot2(top | bot << 16, wy, 512u) >> 10);      // (sum + 2^14) >> 15 of OpenCV
-                if (k == B5(0, 0)) v = t;
-                msk |= (uint32_t)occupied(a, t) << k;
+                if (k == 0) v = t;
+                msk |= (uint32_t)occupied(a, t) << BEV_ORDER[k];
             }
         } else {
             const auto seg = frame_rsrc(b);
 #pragma unroll 1
             for (int k = 0; k < BEV_WIN; ++k) {
-                const uint2 e = cell_ok ? tab[(long)k * cells] : make_uint2(0u, TAB_OUT);
+                const uint2 e = cell_ok ? ent(k) : make_uint2(0u, TAB_OUT);
                 const int t = tab_value(seg, a.in_cols, e);
-                if (k == B5(0, 0)) v = t;
-                msk |= (uint32_t)occupied(a, t) << k;
+                if (k == 0) v = t;
+                msk |= (uint32_t)occupied(a, t) << BEV_ORDER[k];
             }
         }
         if (!cell_ok) continue;
@@ -485,7 +494,7 @@ __global__ void __launch_bounds__(256) laserscan_kernel(const BevArgs a) {
 }
 
 hipError_t launch_bev_table(const BevArgs &a, hipStream_t s) {
-    const long total = (long)a.occ_h * a.occ_w * BEV_WIN;
+    const long total = (long)a.occ_h * a.occ_w * BEV_SLOTS;
     long g = (total + 255) / 256;
     if (g > 8192) g = 8192;
     if (g < 1) g = 1;

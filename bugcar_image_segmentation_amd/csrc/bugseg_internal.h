@@ -167,12 +167,13 @@ struct BevArgs {
     int32_t *rmin;       // (B, ph)
     int hit;             // polar value that is an obstacle: 3 (variant 0) or 100 (variant 1)
     // warp-tap table (bev_kernels.hip): per grid cell, the warpPerspective taps of the 25 template
-    // pixels of the 5x5 window around the pixel the cell samples, SoA [25][occ_h*occ_w]; a property
-    // of the geometry only, built once per calibration by launch_bev_table and shared by every frame
-    uint2 *wtab;
+    // pixels of the 5x5 window around the pixel the cell samples, two 8-B entries per 16-B slot, SoA
+    // [BEV_SLOTS][occ_h*occ_w] (the 3x3 around the sample first); a property of the geometry only,
+    // built once per calibration by launch_bev_table and shared by every frame
+    uint4 *wtab;
 };
 hipError_t launch_bev(const BevArgs &a, hipStream_t s);
 hipError_t launch_bev_table(const BevArgs &a, hipStream_t s);
-constexpr int BEV_WIN = 25;
+constexpr int BEV_WIN = 25, BEV_SLOTS = 13;
 
 }  // namespace bugseg

@@ -119,7 +119,7 @@ struct bugseg_ctx {
     std::vector<LsScratch> ls_scratch;
     // BEV warp-tap tables (bev_kernels.hip bev_table_kernel), one per recent geometry (read-only
     // once built, shared by every stream); key = the geometry fields of BevArgs
-    struct BevTab { std::vector<unsigned char> key; uint2 *tab = nullptr; };
+    struct BevTab { std::vector<unsigned char> key; uint4 *tab = nullptr; };
     std::vector<BevTab> bev_tabs;
 };
 
@@ -1383,7 +1383,7 @@ int bugseg_bev_occgrid(bugseg_ctx *ctx, const uint8_t *seg, int B, const bugseg_
         for (auto &t : ctx->bev_tabs) if (t.key == key) hit = &t;
         if (!hit) {
             const size_t cells = (size_t)a.occ_h * a.occ_w;
-            if (cells * BEV_WIN > (size_t)1 << 31) return fail(ctx, BUGSEG_EINVAL, "occupancy grid too large");
+            if (cells * BEV_SLOTS > (size_t)1 << 31) return fail(ctx, BUGSEG_EINVAL, "occupancy grid too large");
             if (ctx->bev_tabs.size() >= 4) {            // keep the 4 most recent geometries
                 if (hipDeviceSynchronize() != hipSuccess) return fail(ctx, BUGSEG_EHIP, "device sync failed");
                 (void)hipFree(ctx->bev_tabs.front().tab);
@@ -1391,7 +1391,7 @@ int bugseg_bev_occgrid(bugseg_ctx *ctx, const uint8_t *seg, int B, const bugseg_
             }
             bugseg_ctx::BevTab t;
             t.key = key;
-            if (hipMalloc(&t.tab, cells * BEV_WIN * sizeof(uint2)) != hipSuccess)
+            if (hipMalloc(&t.tab, cells * BEV_SLOTS * sizeof(uint4)) != hipSuccess)
                 return fail(ctx, BUGSEG_ENOMEM, "BEV table allocation failed");
             a.wtab = t.tab;
             hipError_t e = launch_bev_table(a, (hipStream_t)stream);
