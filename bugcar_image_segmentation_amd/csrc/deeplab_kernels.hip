@@ -324,6 +324,136 @@ __global__ void __launch_bounds__(256) dl_conv_kernel(const DlConvArgs a) {
     }
 }
 
+// ------------------------------------------------------------------ 1x1 conv as an LDS-staged GEMM
+// The expansions, projections and the ASPP / logits 1x1s (bf16): out[p][n] = act(sum_k in[p][k] w[n][k]
+// + bias (+ per-image bias)) (+ residual). dl_conv_kernel feeds its MFMAs straight from global memory,
+// every wave issuing 16-B loads that touch half-used lines and re-load the weights its neighbours
+// load (the measured limit: vector-memory issue); here a workgroup tile of TM = 256 pixels
+// x 64 output channels is staged through LDS in k-stages of 64 channels: the pixels' 128-B channel
+// runs and the weight rows arrive as whole lines (8 lanes per line), once per workgroup, the next
+// stage's loads are in flight in registers while the current stage's 32 MFMAs per wave run, and every
+// wave reads its 16 x 16 fragments from LDS. The k-steps (32 channels) go through the MFMAs in the
+// same order and with the same epilogue as dl_conv_kernel, so the results are bit-identical.
+constexpr int GM_TM = 256, GM_TN = 64, GM_KT = 64, GM_RS = GM_KT + 16;   // LDS row: 80 elements (40 dwords)
+
+template <bool OUTF32>
+__global__ void __launch_bounds__(256, 2) dl_gemm_kernel(const DlConvArgs a) {
+    __shared__ __attribute__((aligned(16))) __bf16 sm[(GM_TN + GM_TM) * GM_RS];
+    __bf16 *sA = sm, *sB = sm + GM_TN * GM_RS;
+    const int tid = threadIdx.x, lane = tid & 63, col = lane & 15, kq = lane >> 4, wave = tid >> 6;
+    const int ntn = a.NP >> 6;
+    const int bid = xcd_block(blockIdx.x, gridDim.x);
+    const int n0 = (bid % ntn) * GM_TN, p0 = (bid / ntn) * GM_TM;
+    const int K = a.cinP;
+    const __amdgpu_buffer_rsrc_t rin = mkbuf(a.in, a.in_bytes);
+    const __amdgpu_buffer_rsrc_t rw = mkbuf(a.w, (uint32_t)((size_t)a.NP * K * 2));
+    // this thread's 16-B chunks of a stage: pixel rows q >> 3 (8 per thread), weight rows (2 per thread)
+    uint32_t boff[8], woff[2];
+    int bk[8], wk[2];
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+        const int q = tid + 256 * i, px = q >> 3;
+        bk[i] = (q & 7) * 8;
+        boff[i] = p0 + px < a.M ? (uint32_t)((p0 + px) * a.CS + bk[i]) * 2u : OOB;
+    }
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+        const int q = tid + 256 * i, row = q >> 3;
+        wk[i] = (q & 7) * 8;
+        woff[i] = (uint32_t)((n0 + row) * K + wk[i]) * 2u;
+    }
+    uint4 pb[8], pw[2];
+    auto fetch = [&](int k0) {
+#pragma unroll
+        for (int i = 0; i < 8; ++i) pb[i] = bld16(rin, boff[i] != OOB && k0 + bk[i] < a.CS ? boff[i] + k0 * 2 : OOB);
+#pragma unroll
+        for (int i = 0; i < 2; ++i) pw[i] = bld16(rw, k0 + wk[i] < K ? woff[i] + k0 * 2 : OOB);
+    };
+    f32x4 acc[4][4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) acc[j][r] = (f32x4){0.f, 0.f, 0.f, 0.f};
+    const int nst = (K + GM_KT - 1) / GM_KT;
+    fetch(0);
+    for (int st = 0; st < nst; ++st) {
+        __syncthreads();                          // every wave is done reading the previous stage
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {
+            const int q = tid + 256 * i;
+            *reinterpret_cast<uint4 *>(sB + (q >> 3) * GM_RS + (q & 7) * 8) = pb[i];
+        }
+#pragma unroll
+        for (int i = 0; i < 2; ++i) {
+            const int q = tid + 256 * i;
+            *reinterpret_cast<uint4 *>(sA + (q >> 3) * GM_RS + (q & 7) * 8) = pw[i];
+        }
+        __syncthreads();
+        if (st + 1 < nst) fetch((st + 1) * GM_KT);
+#pragma unroll
+        for (int s2 = 0; s2 < GM_KT / 32; ++s2) {
+            if (st * GM_KT + s2 * 32 >= K) break;  // (uniform) a 32-channel tail stage: no empty k-step
+            RawB wa[4], bx[4];
+#pragma unroll
+            for (int r = 0; r < 4; ++r) ld8(wa[r], sA + (r * 16 + col) * GM_RS + s2 * 32 + kq * 8);
+#pragma unroll
+            for (int j = 0; j < 4; ++j) ld8(bx[j], sB + (wave * 64 + j * 16 + col) * GM_RS + s2 * 32 + kq * 8);
+#pragma unroll
+            for (int j = 0; j < 4; ++j)
+#pragma unroll
+                for (int r = 0; r < 4; ++r) mma(acc[j][r], wa[r], bx[j]);
+        }
+    }
+    // epilogue (dl_conv_kernel's, 32 pixels at a time through the wave's share of the staging LDS)
+    __syncthreads();
+    float *st = reinterpret_cast<float *>(sm) + wave * 32 * DL_STG_RS;
+    const int c8 = (lane & 7) * 8;
+    const bool cok = n0 + c8 < a.cout;
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+        if (h) wave_lds_sync();
+#pragma unroll
+        for (int jj = 0; jj < 2; ++jj) {
+            const int j = 2 * h + jj;
+            const int p = p0 + wave * 64 + j * 16 + col;
+            const int pimg = a.bias_img ? (int)fdiv((uint32_t)(p < a.M ? p : 0), a.mHW, a.sHW) : 0;
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                const int nl = r * 16 + kq * 4, n = n0 + nl;
+                float4 v = add4(f4(acc[j][r]), ld4f(a.bias + n));
+                if (a.bias_img) v = add4(v, ld4f(a.bias_img + (size_t)pimg * a.bias_img_stride + n));
+                if (a.act >= 1) v = make_float4(fmaxf(v.x, 0.f), fmaxf(v.y, 0.f), fmaxf(v.z, 0.f), fmaxf(v.w, 0.f));
+                if (a.act == 2) v = make_float4(fminf(v.x, 6.f), fminf(v.y, 6.f), fminf(v.z, 6.f), fminf(v.w, 6.f));
+                *reinterpret_cast<float4 *>(st + (jj * 16 + col) * DL_STG_RS + nl) = v;
+            }
+        }
+        wave_lds_sync();
+#pragma unroll
+        for (int it = 0; it < 4; ++it) {
+            const int pl = it * 8 + (lane >> 3);
+            const int p = p0 + wave * 64 + h * 32 + pl;
+            if (p >= a.M || !cok) continue;
+            float4 v0 = *reinterpret_cast<const float4 *>(st + pl * DL_STG_RS + c8);
+            float4 v1 = *reinterpret_cast<const float4 *>(st + pl * DL_STG_RS + c8 + 4);
+            const int n = n0 + c8;
+            if (a.res) {
+                const __bf16 *rp = reinterpret_cast<const __bf16 *>(a.res) + (size_t)p * a.res_cs + n;
+                v0 = add4(v0, ld4(rp));
+                v1 = add4(v1, ld4(rp + 4));
+            }
+            if constexpr (OUTF32) {
+                float *o = reinterpret_cast<float *>(a.out) + (size_t)p * a.out_cs + a.out_off + n;
+                st4(o, v0);
+                st4(o + 4, v1);
+            } else {
+                __bf16 *o = reinterpret_cast<__bf16 *>(a.out) + (size_t)p * a.out_cs + a.out_off + n;
+                st4(o, v0);
+                st4(o + 4, v1);
+            }
+        }
+    }
+}
+
 // ------------------------------------------------------------------ depthwise 3x3
 // One thread = one output pixel x 8 channels; threads with consecutive ids take consecutive channel
 // groups of the same pixel (coalesced 16-B loads). Weights [9][C] f32 (already rounded to T's
@@ -672,8 +802,23 @@ static void conv_nb(int prec, bool out_f32, bool dwf, const DlConvArgs &a, hipSt
     }
 }
 
+// the LDS-staged GEMM form applies to plain 1x1 convolutions (bf16; BUGSEG_DL_GEMM=0 turns it off)
+static bool gemm_ok(int prec, const DlConvArgs &a) {
+    const char *e = std::getenv("BUGSEG_DL_GEMM");
+    if (e && *e == '0') return false;
+    return prec == PREC_BF16 && !a.dw_w && !a.tap_packed && a.kh == 1 && a.kw == 1 && a.stride == 1 && a.pad_t == 0 &&
+           a.pad_l == 0 && a.Hin == a.Hout && a.Win == a.Wout && a.cinP % 32 == 0 && a.NP % 64 == 0 &&
+           (size_t)a.NP * a.cinP * 2 < ((size_t)1 << 31);
+}
+
 hipError_t dl_launch_conv(int prec, bool out_f32, const DlConvArgs &a, hipStream_t s) {
     const bool dwf = a.dw_w != nullptr;
+    if (gemm_ok(prec, a)) {
+        const dim3 g(((a.M + GM_TM - 1) / GM_TM) * (a.NP / GM_TN));
+        if (out_f32) hipLaunchKernelGGL(dl_gemm_kernel<true>, g, dim3(256), 0, s, a);
+        else hipLaunchKernelGGL(dl_gemm_kernel<false>, g, dim3(256), 0, s, a);
+        return hipGetLastError();
+    }
     if (a.nb == 8 && prec == PREC_BF16 && !dwf) conv_nb<8>(prec, out_f32, false, a, s);
     else if (a.nb >= 4) conv_nb<4>(prec, out_f32, dwf, a, s);
     else conv_nb<2>(prec, out_f32, dwf, a, s);

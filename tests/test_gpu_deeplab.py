@@ -149,3 +149,22 @@ def test_deeplab_from_frozen_graphdef(gpu, tmp_path, style):
     _check_fp32(model, model.net, x, torch.float32)
     lg = np.transpose(tf_graph.run(pb.read_bytes(), {"ImageTensor": x}, "logits"), (0, 3, 1, 2))
     assert np.abs(_gpu_logits(model) - lg).max() < LOGIT_TOL
+
+
+@pytest.mark.parametrize("width,crop,B", [(0.5, 129, 2), (1.0, 97, 3)])
+def test_deeplab_gemm_1x1_bit_identical(gpu, monkeypatch, width, crop, B):
+    """The LDS-staged GEMM kernel of the 1x1 convolutions (default in bf16) against dl_conv_kernel
+    (BUGSEG_DL_GEMM=0): the same k-steps through the same MFMA in the same order and the same
+    epilogue, so identical logits and class maps — over tile tails (pixel counts not a multiple of
+    256), 32-channel k tails, the residual projections and the per-image-bias projection."""
+    net = S.build_deeplab(width=width, crop=crop, atrous_rates=(6,))
+    x = _frames(B, crop, crop - 5, 41)
+    gemm = DeepLabV3(net=net, precision="bf16")
+    a = gemm.predict(x)
+    la = gemm.logits_device().cpu()
+    monkeypatch.setenv("BUGSEG_DL_GEMM", "0")
+    plain = DeepLabV3(net=net, precision="bf16")
+    b = plain.predict(x)
+    lb = plain.logits_device().cpu()
+    assert torch.equal(la, lb)
+    assert np.array_equal(a, b)
