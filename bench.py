@@ -93,13 +93,14 @@ def parse():
     p.add_argument("--batch", type=int, default=64, help="frames per GPU")
     p.add_argument("--height", type=int, default=480)
     p.add_argument("--width", type=int, default=640)
-    p.add_argument("--precision", default="bf16", choices=["bf16", "fp32"])
+    p.add_argument("--precision", default="fp16", choices=["bf16", "fp16", "fp32"],
+                   help="storage precision of the timed step (fp16: bf16's bytes and MFMA rate, 3 more mantissa bits)")
     p.add_argument("--streams", type=int, default=2, help="frame shards run concurrently on this many HIP streams")
     p.add_argument("--graph", type=int, default=0, help="1: replay the step as one captured HIP graph")
     p.add_argument("--cpu-baseline-seconds", type=float, default=12.0)
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--extras", type=int, default=-1,
-                   help="1: add the fp32 / batch-1 latency / bf16-agreement / DeepLab sub-records (measured "
+                   help="1: add the other precision modes / batch-1 latency / class-agreement / DeepLab sub-records (measured "
                         "outside the timed loop); default: on at N = 1, off for N > 1")
     p.add_argument("--deeplab-batch", type=int, default=64)
     return p.parse_args()
@@ -182,12 +183,13 @@ def cpu_baseline(blocks, bev, grid, H, W, budget_s):
                       f"{el:.1f} s at {t} threads (every CPU the process is granted), one frame per call"}
 
 
-def fp32_record(blocks, bev, grid, H, W, frames, streams, steps):
-    """The fp32 parity mode (logits within 1e-3 of the oracle) on the same step, same batch."""
+def mode_record(blocks, bev, grid, H, W, frames, streams, steps, precision):
+    """Another precision mode (fp32: the parity mode, logits within 1e-3 of the oracle; fp16 / bf16)
+    on the same step, same batch."""
     from bugcar_image_segmentation_amd.models import ENET
     from bugcar_image_segmentation_amd.pipeline import OccupancyPipeline
     B = frames.shape[0]
-    model = ENET(weights=blocks, precision="fp32")
+    model = ENET(weights=blocks, precision=precision)
     pipe = OccupancyPipeline(model, bev, *grid, model_hw=(H, W), streams=streams)
     for _ in range(3):
         pipe.run(frames)
@@ -199,7 +201,7 @@ def fp32_record(blocks, bev, grid, H, W, frames, streams, steps):
     el = time.perf_counter() - t0
     del pipe, model
     return {"value": round(B * steps / el, 2), "unit": "frames/s", "ms_per_step": round(el / steps * 1e3, 4),
-            "per_gpu_batch": B, "steps": steps, "streams_per_gpu": streams}
+            "per_gpu_batch": B, "steps": steps, "streams_per_gpu": streams, "dtype": precision}
 
 
 def latency_b1(blocks, precision, bev, grid, H, W, frame, iters):
@@ -234,35 +236,39 @@ def latency_b1(blocks, precision, bev, grid, H, W, frame, iters):
             "graph_fps": round(1e3 / g_mean, 1)}
 
 
-def bf16_agreement(blocks, H, W, nframes, dev):
-    """Per-pixel class agreement of the bf16 throughput mode with the fp32 parity mode on a fixed
+def class_agreement(blocks, H, W, nframes, dev, precs=("bf16", "fp16")):
+    """Per-pixel class agreement of the 2-byte throughput modes with the fp32 parity mode on a fixed
     frame set (structured road scenes, seed 77), over the 15 raw classes and the 3-class remap
     (models.py:55-58); of the disagreeing pixels, the share whose fp32 top-2 margin exceeds 1e-2
-    (i.e. not a near-tie). Torch ops here only compare the two engine outputs."""
+    (i.e. not a near-tie). Torch ops here only compare the engine outputs."""
     from bugcar_image_segmentation_amd import _native as N
     from bugcar_image_segmentation_amd import synthetic
     from bugcar_image_segmentation_amd.models import ENET
     bgr = torch.from_numpy(synthetic.road_frames(nframes, H, W, seed=77)).to(dev)
     lg = {}
-    for prec in ("fp32", "bf16"):
+    for prec in ("fp32",) + tuple(precs):
         m = ENET(weights=blocks, precision=prec)
         out = torch.empty((nframes, m.num_classes, H, W), dtype=torch.float32, device=dev)
         m.ctx.forward_bgr(bgr, nframes, H, W, N.OUT_LOGITS_F32, out)
         torch.cuda.synchronize()
         lg[prec] = out
         del m
-    a32, a16 = lg["fp32"].argmax(1), lg["bf16"].argmax(1)
+    a32 = lg["fp32"].argmax(1)
     lut3 = torch.tensor([1, 1, 0, 2, 2, 2, 2, 2, 2, 0, 2, 2, 2, 2, 2, 2], device=dev)
     top2 = lg["fp32"].topk(2, dim=1).values
     margin = top2[:, 0] - top2[:, 1]
-    dis = a32 != a16
-    nd = int(dis.sum())
-    return {"frames": nframes, "pixels": int(a32.numel()),
-            "class15_agreement": round(float((~dis).float().mean()), 6),
-            "class3_agreement": round(float((lut3[a32] == lut3[a16]).float().mean()), 6),
-            "disagreeing_pixels": nd,
-            "disagreeing_with_fp32_margin_gt_1e-2": round(int((dis & (margin > 1e-2)).sum()) / max(nd, 1), 4),
-            "max_abs_logit_diff": round(float((lg["fp32"] - lg["bf16"]).abs().max()), 4)}
+    res = {}
+    for prec in precs:
+        a = lg[prec].argmax(1)
+        dis = a32 != a
+        nd = int(dis.sum())
+        res[prec] = {"frames": nframes, "pixels": int(a32.numel()),
+                     "class15_agreement": round(float((~dis).float().mean()), 6),
+                     "class3_agreement": round(float((lut3[a32] == lut3[a]).float().mean()), 6),
+                     "disagreeing_pixels": nd,
+                     "disagreeing_with_fp32_margin_gt_1e-2": round(int((dis & (margin > 1e-2)).sum()) / max(nd, 1), 4),
+                     "max_abs_logit_diff": round(float((lg["fp32"] - lg[prec]).abs().max()), 4)}
+    return res
 
 
 def main():
@@ -390,7 +396,7 @@ def main():
                     "plan_achieved_gbs": round(plan_bytes / (t_fwd * 1e-3) / 1e9, 1),
                     "mfma_tflops": round(flops / (t_fwd * 1e-3) / 1e12, 2),
                     "mfma_frac": round(flops / (t_fwd * 1e-3) / 1e12 /
-                                       (MFMA_BF16_PEAK_TFLOPS if a.precision == "bf16" else MFMA_F32_PEAK_TFLOPS), 4)},
+                                       (MFMA_F32_PEAK_TFLOPS if a.precision == "fp32" else MFMA_BF16_PEAK_TFLOPS), 4)},
             },
             "kernels": {t: {"launches": v["launches"], "us_per_launch": round(v["us_per_launch"], 2),
                             "GBps": round(v["bytes_per_launch"] / (v["us_per_launch"] * 1e-6) / 1e9, 1)}
@@ -400,12 +406,16 @@ def main():
         }
         extras = a.extras if a.extras >= 0 else int(world == 1)
         if extras:
-            log("fp32 sub-record")
-            res["fp32"] = fp32_record(blocks, bev, grid, H, W, frames, a.streams, max(5, a.steps // 2))
+            for prec in ("fp32", "fp16", "bf16"):
+                if prec != a.precision:
+                    log(f"{prec} sub-record")
+                    res[prec] = mode_record(blocks, bev, grid, H, W, frames, a.streams, max(5, a.steps // 2), prec)
             log("batch-1 latency sub-record")
             res["latency_b1_ms"] = latency_b1(blocks, a.precision, bev, grid, H, W, frames[:1], 100)
-            log("bf16 agreement sub-record")
-            res["bf16_class_agreement_vs_fp32"] = bf16_agreement(blocks, H, W, 4, dev)
+            log("class agreement sub-records")
+            agree = class_agreement(blocks, H, W, 4, dev)
+            res["bf16_class_agreement_vs_fp32"] = agree["bf16"]
+            res["fp16_class_agreement_vs_fp32"] = agree["fp16"]
             import bench_deeplab
             log("deeplab sub-record")
             res["deeplab"] = bench_deeplab.record(dev, a.deeplab_batch, max(5, a.steps // 2), 3, "bf16",

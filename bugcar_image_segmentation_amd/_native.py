@@ -17,7 +17,7 @@ _PKG = Path(__file__).resolve().parent
 LIB_PATH = Path(os.environ.get("BUGSEG_LIB", _PKG / "libbugseg.so"))
 
 OK, EINVAL, ENOMEM, EHIP, EFORMAT, ESTATE = 0, -1, -2, -3, -4, -5
-FP32, BF16 = 0, 1
+FP32, BF16, F16 = 0, 1, 2
 OUT_LOGITS_F32, OUT_CLASS15_U8, OUT_CLASS3_U8, OUT_BINARY_U8 = 0, 1, 2, 3
 PRE_ENGINE, PRE_NCHW_F64, PRE_NCHW_F32, PRE_BGR_U8 = 0, 1, 2, 3
 

@@ -293,9 +293,8 @@ __global__ void __launch_bounds__((BShape<C, V>::NW * 64), (sizeof(T) == 2 ? BSh
                 if (__ballot(interior) == 0) return;          // halo-only fragment (wave-uniform)
                 auto elems = [&](const Raw &r, float (&e)[8]) {
                     if constexpr (sizeof(T) == 2) {
-                        const uint32_t w[4] = {r.v.x, r.v.y, r.v.z, r.v.w};
-#pragma unroll
-                        for (int i = 0; i < 4; ++i) { e[2 * i] = __uint_as_float(w[i] << 16); e[2 * i + 1] = __uint_as_float(w[i] & 0xffff0000u); }
+                        const float4 lo = unpack4<T>((u32x2_t){r.v.x, r.v.y}), hi = unpack4<T>((u32x2_t){r.v.z, r.v.w});
+                        e[0] = lo.x; e[1] = lo.y; e[2] = lo.z; e[3] = lo.w; e[4] = hi.x; e[5] = hi.y; e[6] = hi.z; e[7] = hi.w;
                     } else {
                         const RawF &f = reinterpret_cast<const RawF &>(r);
                         e[0] = f.a.x; e[1] = f.a.y; e[2] = f.a.z; e[3] = f.a.w; e[4] = f.b.x; e[5] = f.b.y; e[6] = f.b.z; e[7] = f.b.w;
@@ -306,9 +305,10 @@ __global__ void __launch_bounds__((BShape<C, V>::NW * 64), (sizeof(T) == 2 ? BSh
                     // 8 pooled channels (exact input values) + their window positions (4 = none -> 0)
                     uint32_t pw[8 * sizeof(T) / 4];
                     if constexpr (sizeof(T) == 2) {
-#pragma unroll
-                        for (int i = 0; i < 4; ++i)
-                            pw[i] = (__float_as_uint(bv[2 * i]) >> 16) | (__float_as_uint(bv[2 * i + 1]) & 0xffff0000u);
+                        // exact input values (the pool selects, it does not round): re-packing is lossless
+                        const u32x2_t lo = pack4<T>(make_float4(bv[0], bv[1], bv[2], bv[3]));
+                        const u32x2_t hi = pack4<T>(make_float4(bv[4], bv[5], bv[6], bv[7]));
+                        pw[0] = lo.x; pw[1] = lo.y; pw[2] = hi.x; pw[3] = hi.y;
                     } else {
 #pragma unroll
                         for (int i = 0; i < 8; ++i) pw[i] = __float_as_uint(bv[i]);
@@ -686,9 +686,9 @@ __global__ void __launch_bounds__((BShape<C, V>::NW * 64), (sizeof(T) == 2 ? BSh
                     uint32_t a0 = rc.x, a1 = rc.y, b0 = rc.z, b1 = rc.w;
                     pl16swap(a0, b0);
                     pl16swap(a1, b1);
-                    float4 v0 = act(add4(out3(r0, acc0), unpack_bf16x4((u32x2_t){a0, a1})), cso + r0 * 16 + kq * 4);
-                    float4 v1 = act(add4(out3(r1, acc1), unpack_bf16x4((u32x2_t){b0, b1})), cso + r1 * 16 + kq * 4);
-                    u32x2_t p0 = pack_bf16x4(v0), p1 = pack_bf16x4(v1);
+                    float4 v0 = act(add4(out3(r0, acc0), unpack4<T>((u32x2_t){a0, a1})), cso + r0 * 16 + kq * 4);
+                    float4 v1 = act(add4(out3(r1, acc1), unpack4<T>((u32x2_t){b0, b1})), cso + r1 * 16 + kq * 4);
+                    u32x2_t p0 = pack4<T>(v0), p1 = pack4<T>(v1);
                     uint32_t x0 = p0.x, x1 = p0.y, y0 = p1.x, y1 = p1.y;
                     pl16swap(x0, y0);
                     pl16swap(x1, y1);
@@ -700,8 +700,8 @@ __global__ void __launch_bounds__((BShape<C, V>::NW * 64), (sizeof(T) == 2 ? BSh
                     ld8(wf, w3 + (r * 16 + col) * K3S + kq * 8);
                     mma(acc, wf, tf[j]);
                     if constexpr (HALF) {
-                        float4 v = act(add4(out3(r, acc), unpack_bf16x4((u32x2_t){rc.x, rc.y})), cso + r * 16 + kq * 4);
-                        bst8o(rob, off, pack_bf16x4(v));
+                        float4 v = act(add4(out3(r, acc), unpack4<T>((u32x2_t){rc.x, rc.y})), cso + r * 16 + kq * 4);
+                        bst8o(rob, off, pack4<T>(v));
                     } else {
                         float4 v = act(add4(out3(r, acc), __builtin_bit_cast(float4, rc)), cso + r * 16 + kq * 4);
                         bst16o(rob, off, __builtin_bit_cast(uint4, v));
@@ -723,7 +723,7 @@ extern "C" int bugseg_debug_set_stamps(void *p) {
 size_t bneck_lds_bytes(int prec, int C, bool asym, int v, int cin) {
     int TH, TW, NW, RD;
     bneck_shape(C, v, TH, TW, NW, &RD);
-    const int es = prec == PREC_BF16 ? 2 : 4, pad = 16 / es;
+    const int es = prec_es(prec), pad = 16 / es;
     const int I = cin > 0 ? cin / 4 : C / 4, IS = I < 8 ? 8 : I, NR1 = (I + 15) / 16;
     const int KS1 = ((cin > 0 ? cin / 2 : C / 8) + 3) / 4, KS2 = ((asym ? 5 : 9) * IS / 8 + 3) / 4;
     const int R = asym ? 2 : 1, RX = RD ? 0 : R;
@@ -758,8 +758,13 @@ static const void *kfun_down(int C, int v, int cin) {
 }
 
 static const void *bneck_fun(int prec, int C, bool asym, int v, bool tr, int cin) {
-    if (cin > 0) return asym || tr ? nullptr : prec == PREC_BF16 ? kfun_down<__bf16>(C, v, cin) : kfun_down<float>(C, v, cin);
-    return prec == PREC_BF16 ? kfun<__bf16>(C, asym, v, tr) : kfun<float>(C, asym, v, tr);
+    if (cin > 0)
+        return asym || tr ? nullptr
+               : prec == PREC_BF16 ? kfun_down<__bf16>(C, v, cin)
+               : prec == PREC_F16  ? kfun_down<_Float16>(C, v, cin)
+                                   : kfun_down<float>(C, v, cin);
+    return prec == PREC_BF16 ? kfun<__bf16>(C, asym, v, tr) : prec == PREC_F16 ? kfun<_Float16>(C, asym, v, tr)
+                                                            : kfun<float>(C, asym, v, tr);
 }
 
 // dynamic LDS above 64 KB must be allowed per kernel (once)

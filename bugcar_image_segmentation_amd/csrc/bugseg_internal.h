@@ -22,7 +22,9 @@ enum Epi {
     EPI_COUNT = 8
 };
 
-enum Prec { PREC_F32 = 0, PREC_BF16 = 1 };
+enum Prec { PREC_F32 = 0, PREC_BF16 = 1, PREC_F16 = 2 };
+// bytes per stored element: fp32 parity mode 4; bf16 / f16 storage modes 2
+inline constexpr int prec_es(int prec) { return prec == PREC_F32 ? 4 : 2; }
 
 struct ConvArgs {
     const void *in;      // NHWC input (B, Hin, Win, CinS)

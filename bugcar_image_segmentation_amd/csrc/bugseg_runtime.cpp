@@ -211,6 +211,31 @@ bool parse_blob(const void *blob, size_t bytes, std::vector<BlockDesc> &out, int
 }
 
 // ---------------------------------------------------------------- packing
+// IEEE binary16 bits of a finite float, round to nearest even (the fp16-storage mode's weights);
+// overflow to +-inf, underflow through the subnormals to +-0 — as a (_Float16) cast does
+uint16_t f32_to_f16(float f) {
+    uint32_t u;
+    std::memcpy(&u, &f, 4);
+    const uint32_t sign = (u >> 16) & 0x8000u;
+    const int32_t exp = (int32_t)((u >> 23) & 0xff) - 127 + 15;
+    uint32_t man = u & 0x7fffffu;
+    if (((u >> 23) & 0xff) == 0xff) return (uint16_t)(sign | 0x7c00u | (man ? 0x200u : 0u));   // inf / nan
+    if (exp >= 31) return (uint16_t)(sign | 0x7c00u);
+    if (exp <= 0) {                                  // subnormal half (or zero)
+        if (exp < -10) return (uint16_t)sign;
+        man |= 0x800000u;
+        const int shift = 14 - exp;                  // 24-bit significand -> 10 + exp bits
+        uint32_t h = man >> shift;
+        const uint32_t rem = man & ((1u << shift) - 1), half = 1u << (shift - 1);
+        if (rem > half || (rem == half && (h & 1u))) ++h;
+        return (uint16_t)(sign | h);
+    }
+    uint32_t h = ((uint32_t)exp << 10) | (man >> 13);
+    const uint32_t rem = man & 0x1fffu;
+    if (rem > 0x1000u || (rem == 0x1000u && (h & 1u))) ++h;   // may carry into the exponent (-> inf): correct
+    return (uint16_t)(sign | h);
+}
+
 struct Packer {
     int prec;
     std::vector<unsigned char> &buf;
@@ -221,6 +246,11 @@ struct Packer {
         return off;
     }
     size_t push_w(const std::vector<double> &w) {
+        if (prec == PREC_F16) {
+            std::vector<uint16_t> h(w.size());
+            for (size_t i = 0; i < w.size(); ++i) h[i] = f32_to_f16((float)w[i]);
+            return push(h.data(), h.size() * 2);
+        }
         if (prec == PREC_BF16) {
             std::vector<uint16_t> h(w.size());
             for (size_t i = 0; i < w.size(); ++i) {
@@ -471,7 +501,7 @@ bool pack_all(bugseg_ctx *ctx, std::string &why) {
             // shape, as one conv launch whose output the tconv reads from channel cout on (id 5) —
             // that needs a power-of-two count of 16-B chunks per pixel (the conv epilogue's staged
             // stores). Both require the two halves to fold their bias the same way (bias_in_acc).
-            const int es = ctx->prec == PREC_BF16 ? 2 : 4, mc = cstore(um.cout) + cstore(u1.cout);
+            const int es = prec_es(ctx->prec), mc = cstore(um.cout) + cstore(u1.cout);
             const int chunks = mc * es / 16;
             const int nr_pair = pow2_nr(round_up(um.cout, 16) + round_up(u1.cout, 16));
             auto bias_acc = [](int nr) { return nr < 8; };     // mfma_common.h bias_in_acc
@@ -671,7 +701,7 @@ struct Walker {
     }
 
     bool run(bool fill, std::string &why) {
-        es = ctx->prec == PREC_BF16 ? 2 : 4;
+        es = prec_es(ctx->prec);
         if (H % 8 || W % 8 || H <= 0 || W <= 0 || B <= 0) { why = "H and W must be positive multiples of 8"; return false; }
         const size_t nb = ctx->blocks.size();
         if (!fill) szIdx.assign(nb, 0);
@@ -1030,14 +1060,15 @@ const char *bugseg_last_error(const bugseg_ctx *ctx) { return ctx ? ctx->err.c_s
 int bugseg_create(int device, int precision, bugseg_ctx **out) {
     if (!out) return fail(nullptr, BUGSEG_EINVAL, "out is NULL");
     *out = nullptr;
-    if (precision != BUGSEG_FP32 && precision != BUGSEG_BF16) return fail(nullptr, BUGSEG_EINVAL, "precision must be BUGSEG_FP32 or BUGSEG_BF16");
+    if (precision != BUGSEG_FP32 && precision != BUGSEG_BF16 && precision != BUGSEG_F16)
+        return fail(nullptr, BUGSEG_EINVAL, "precision must be BUGSEG_FP32, BUGSEG_BF16 or BUGSEG_F16");
     int n = 0;
     if (hipGetDeviceCount(&n) != hipSuccess || device < 0 || device >= n)
         return fail(nullptr, BUGSEG_EINVAL, "no such HIP device: " + std::to_string(device));
     bugseg_ctx *c = new (std::nothrow) bugseg_ctx();
     if (!c) return fail(nullptr, BUGSEG_ENOMEM, "out of host memory");
     c->device = device;
-    c->prec = precision == BUGSEG_BF16 ? PREC_BF16 : PREC_F32;
+    c->prec = precision == BUGSEG_BF16 ? PREC_BF16 : precision == BUGSEG_F16 ? PREC_F16 : PREC_F32;
     DeviceGuard g(device);
     // class remap tables (models.py:56-58 and :79-80) + the normalisation table (models.py:17-18, 91)
     unsigned char tab[32 + 3 * 256 * 8];
@@ -1099,7 +1130,7 @@ int bugseg_num_classes(const bugseg_ctx *ctx) { return ctx && ctx->loaded ? ctx-
 
 size_t bugseg_input_bytes(const bugseg_ctx *ctx, int B, int H, int W) {
     if (!ctx || B <= 0 || H <= 0 || W <= 0) return 0;
-    return (size_t)B * H * W * 8 * (ctx->prec == PREC_BF16 ? 2 : 4);
+    return (size_t)B * H * W * 8 * prec_es(ctx->prec);
 }
 
 int bugseg_preprocess(bugseg_ctx *ctx, const uint8_t *bgr, int B, int H0, int W0, int H, int W, int out_layout,
@@ -1418,7 +1449,7 @@ int bugseg_bev_occgrid(bugseg_ctx *ctx, const uint8_t *seg, int B, const bugseg_
 int bugseg_debug_parse_pack(const void *blob, size_t bytes, int precision, int *ncls) {
     if (!blob) return fail(nullptr, BUGSEG_EINVAL, "NULL blob");
     bugseg_ctx c;                                     // host state only; nothing to free on the device
-    c.prec = precision == BUGSEG_BF16 ? PREC_BF16 : PREC_F32;
+    c.prec = precision == BUGSEG_BF16 ? PREC_BF16 : precision == BUGSEG_F16 ? PREC_F16 : PREC_F32;
     std::string why;
     if (!parse_blob(blob, bytes, c.blocks, c.ncls, why)) return fail(nullptr, BUGSEG_EFORMAT, "weight blob: " + why);
     if (!pack_all(&c, why)) return fail(nullptr, BUGSEG_EFORMAT, "weight blob: " + why);
@@ -1458,7 +1489,7 @@ int bugseg_plan_info(bugseg_ctx *ctx, int B, int H, int W, int out_kind, int bgr
     // final epilogue output
     const double fin = out_kind == BUGSEG_OUT_LOGITS_F32 ? (double)B * H * W * ctx->ncls * 4 : (double)B * H * W;
     // raw BGR input (bugseg_enet_forward_bgr): 3 bytes per pixel instead of the 8-channel engine input
-    const double adj = bgr_input ? (double)B * H * W * (8.0 * (ctx->prec == PREC_BF16 ? 2 : 4) - 3.0) : 0.0;
+    const double adj = bgr_input ? (double)B * H * W * (8.0 * prec_es(ctx->prec) - 3.0) : 0.0;
     if (n_launches) *n_launches = (int)ctx->plan.ops.size();
     if (alg_bytes) *alg_bytes = lb + fin - adj;
     if (plan_bytes) *plan_bytes = pb + fin - adj;
@@ -1492,7 +1523,7 @@ int bugseg_plan_op(bugseg_ctx *ctx, int B, int H, int W, int op, char *kernel, i
         kernel[kernel_len - 1] = 0;
     }
     double lb = o.layer_bytes >= 0 ? o.layer_bytes : o.bytes, pb = o.bytes;
-    const int es = ctx->prec == PREC_BF16 ? 2 : 4;
+    const int es = prec_es(ctx->prec);
     if (o.kind == 0 && o.epi == EPI_INIT_BGR) {           // raw BGR input: 3 B/px, not the 8-channel engine input
         const double adj = (double)B * H * W * (8.0 * es - 3.0);
         lb -= adj; pb -= adj;

@@ -26,6 +26,10 @@ __device__ __forceinline__ void mma32(f32x16 &acc, const RawB &w, const RawB &x)
     acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(bf16x8, w.v), __builtin_bit_cast(bf16x8, x.v),
                                                   acc, 0, 0, 0);
 }
+__device__ __forceinline__ void mma32(f32x16 &acc, const RawH &w, const RawH &x) {
+    acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(__builtin_bit_cast(f16x8, w.v), __builtin_bit_cast(f16x8, x.v),
+                                                 acc, 0, 0, 0);
+}
 // fp32: sub-MFMA j contracts element j of both lane halves (channels j and 8 + j of the tap)
 __device__ __forceinline__ void mma32(f32x16 &acc, const RawF &w, const RawF &x) {
     acc = __builtin_amdgcn_mfma_f32_32x32x2f32(w.a.x, x.a.x, acc, 0, 0, 0);
@@ -39,6 +43,7 @@ __device__ __forceinline__ void mma32(f32x16 &acc, const RawF &w, const RawF &x)
 }
 
 __device__ __forceinline__ bool nonzero(const RawB &r) { return (r.v.x | r.v.y | r.v.z | r.v.w) != 0u; }
+__device__ __forceinline__ bool nonzero(const RawH &r) { return (r.v.x | r.v.y | r.v.z | r.v.w) != 0u; }
 __device__ __forceinline__ bool nonzero(const RawF &r) {
     const uint4 u = __builtin_bit_cast(uint4, r.a), v = __builtin_bit_cast(uint4, r.b);
     return (u.x | u.y | u.z | u.w | v.x | v.y | v.z | v.w) != 0u;
@@ -222,6 +227,9 @@ hipError_t launch_cls(int prec, const ConvArgs &a, hipStream_t s) {
     if (prec == PREC_BF16) {
         if (lg) hipLaunchKernelGGL((cls_kernel<__bf16, true>), dim3(g), dim3(256), 0, s, a);
         else hipLaunchKernelGGL((cls_kernel<__bf16, false>), dim3(g), dim3(256), 0, s, a);
+    } else if (prec == PREC_F16) {
+        if (lg) hipLaunchKernelGGL((cls_kernel<_Float16, true>), dim3(g), dim3(256), 0, s, a);
+        else hipLaunchKernelGGL((cls_kernel<_Float16, false>), dim3(g), dim3(256), 0, s, a);
     } else {
         if (lg) hipLaunchKernelGGL((cls_kernel<float, true>), dim3(g), dim3(256), 0, s, a);
         else hipLaunchKernelGGL((cls_kernel<float, false>), dim3(g), dim3(256), 0, s, a);

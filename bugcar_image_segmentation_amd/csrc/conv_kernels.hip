@@ -329,7 +329,7 @@ __global__ void __launch_bounds__(256, sizeof(T) == 2 ? (NR == 8 ? 3 : 4) : 1) c
                         if (c < a.resC) {
                             const uint32_t id = upid[m][n];
                             const uint32_t pos = (uint32_t)(((py[m] & 1) << 1) | (px[m] & 1));
-                            const float4 mv = mvcvt(upmv[m][n]);
+                            const float4 mv = mvcvt<T>(upmv[m][n]);
                             v.x += ((id & 0xff) == pos) ? mv.x : 0.f;
                             v.y += (((id >> 8) & 0xff) == pos) ? mv.y : 0.f;
                             v.z += (((id >> 16) & 0xff) == pos) ? mv.z : 0.f;
@@ -369,7 +369,7 @@ __global__ void __launch_bounds__(256, sizeof(T) == 2 ? (NR == 8 ? 3 : 4) : 1) c
 int conv_tile_pixels(int nr) { return 4 * (nr >= 4 ? 2 : 4) * 16; }
 
 size_t conv_lds_bytes(int prec, const ConvArgs &a) {
-    const int es = prec == PREC_BF16 ? 2 : 4;
+    const int es = prec_es(prec);
     return conv_stage_offset(es, a) + (size_t)4 * a.stg_elems * es;
 }
 
@@ -411,6 +411,7 @@ hipError_t launch_conv(int prec, int nr, int epi, const ConvArgs &a, hipStream_t
     g = (g + 7) & ~7;
     const size_t lds = conv_lds_bytes(prec, a);
     if (prec == PREC_BF16) return launch_t<__bf16>(nr, epi, a, dim3(g), lds, s);
+    if (prec == PREC_F16) return launch_t<_Float16>(nr, epi, a, dim3(g), lds, s);
     return launch_t<float>(nr, epi, a, dim3(g), lds, s);
 }
 

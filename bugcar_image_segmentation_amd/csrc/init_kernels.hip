@@ -110,7 +110,11 @@ __global__ void __launch_bounds__(256) init_kernel(const ConvArgs a) {
             for (int r = 0; r < IP_H; ++r) {
                 const bool ok = colok && (unsigned)(iy0 + r) < (unsigned)a.Hin;
                 T v;
-                if constexpr (BGR) v = (T)lut[lbase + (int)(raw[r] & 0xff)];
+                if constexpr (BGR) {
+                    // f16: through f32, as the separate preprocess stores the engine input (prep_kernels.hip)
+                    if constexpr (__is_same(T, _Float16)) v = (T)(float)lut[lbase + (int)(raw[r] & 0xff)];
+                    else v = (T)lut[lbase + (int)(raw[r] & 0xff)];
+                }
                 else if constexpr (sizeof(T) == 2) v = __builtin_bit_cast(T, (unsigned short)raw[r]);
                 else v = __builtin_bit_cast(T, raw[r]);
                 patch[r * IP_RS + dpatch] = ok ? v : (T)0.f;
@@ -182,9 +186,7 @@ __global__ void __launch_bounds__(256) init_kernel(const ConvArgs a) {
             const bool ok = oy < a.Hg && ox < a.Wg && c0 < a.outC;
             const uint32_t off = ok ? (uint32_t)(((n * a.Hg + oy) * a.Wg + ox) * a.outC + c0) * (uint32_t)sizeof(T) : OOB;
             if constexpr (sizeof(T) == 2) {
-                typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
-                bf16x4 b = {(__bf16)v.x, (__bf16)v.y, (__bf16)v.z, (__bf16)v.w};
-                bst8o(rout, off, __builtin_bit_cast(u32x2, b));
+                bst8o(rout, off, pack4<T>(v));
             } else {
                 bst16o(rout, off, __builtin_bit_cast(uint4, v));
             }
@@ -203,6 +205,9 @@ hipError_t launch_init(int prec, bool bgr, const ConvArgs &a, hipStream_t s) {
     if (prec == PREC_BF16) {
         if (bgr) hipLaunchKernelGGL((init_kernel<__bf16, true>), dim3(g), dim3(256), 0, s, a);
         else hipLaunchKernelGGL((init_kernel<__bf16, false>), dim3(g), dim3(256), 0, s, a);
+    } else if (prec == PREC_F16) {
+        if (bgr) hipLaunchKernelGGL((init_kernel<_Float16, true>), dim3(g), dim3(256), 0, s, a);
+        else hipLaunchKernelGGL((init_kernel<_Float16, false>), dim3(g), dim3(256), 0, s, a);
     } else {
         if (bgr) hipLaunchKernelGGL((init_kernel<float, true>), dim3(g), dim3(256), 0, s, a);
         else hipLaunchKernelGGL((init_kernel<float, false>), dim3(g), dim3(256), 0, s, a);

@@ -15,14 +15,32 @@ typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 typedef float f32x4 __attribute__((ext_vector_type(4)));
 typedef unsigned int u32x2_t __attribute__((ext_vector_type(2)));
 
+typedef _Float16 f16x8 __attribute__((ext_vector_type(8)));
+typedef _Float16 f16x4 __attribute__((ext_vector_type(4)));
+
 struct RawB { uint4 v; };          // 8 bf16
+struct RawH { uint4 v; };          // 8 f16 (the fp16-storage mode: 3 more mantissa bits than bf16)
 struct RawF { float4 a, b; };      // 8 f32
 
 template <typename T> struct Tr;
 template <> struct Tr<__bf16> { using Raw = RawB; };
+template <> struct Tr<_Float16> { using Raw = RawH; };
 template <> struct Tr<float> { using Raw = RawF; };
 
 __device__ __forceinline__ void zero(RawB &r) { r.v = make_uint4(0, 0, 0, 0); }
+__device__ __forceinline__ void zero(RawH &r) { r.v = make_uint4(0, 0, 0, 0); }
+__device__ __forceinline__ void ld8(RawH &r, const _Float16 *p) { r.v = *reinterpret_cast<const uint4 *>(p); }
+__device__ __forceinline__ void set3(RawH &r, float a, float b, float c) {
+    f16x8 v = {(_Float16)a, (_Float16)b, (_Float16)c, (_Float16)0.f, (_Float16)0.f, (_Float16)0.f, (_Float16)0.f, (_Float16)0.f};
+    r.v = __builtin_bit_cast(uint4, v);
+}
+__device__ __forceinline__ void set8(RawH &r, const _Float16 (&v)[8]) {
+    f16x8 b = {v[0], v[1], v[2], v[3], v[4], v[5], v[6], v[7]};
+    r.v = __builtin_bit_cast(uint4, b);
+}
+__device__ __forceinline__ void mma(f32x4 &acc, const RawH &w, const RawH &x) {
+    acc = __builtin_amdgcn_mfma_f32_16x16x32_f16(__builtin_bit_cast(f16x8, w.v), __builtin_bit_cast(f16x8, x.v), acc, 0, 0, 0);
+}
 __device__ __forceinline__ void zero(RawF &r) { r.a = make_float4(0.f, 0.f, 0.f, 0.f); r.b = r.a; }
 __device__ __forceinline__ void ld8(RawB &r, const __bf16 *p) { r.v = *reinterpret_cast<const uint4 *>(p); }
 __device__ __forceinline__ void ld8(RawF &r, const float *p) {
@@ -89,6 +107,25 @@ __device__ __forceinline__ float4 unpack_bf16x4(u32x2_t u) {
     return make_float4(__uint_as_float(u.x << 16), __uint_as_float(u.x & 0xffff0000u),
                        __uint_as_float(u.y << 16), __uint_as_float(u.y & 0xffff0000u));
 }
+// 4 floats <-> 4 f16 in two dwords (round to nearest even, as the (_Float16) casts)
+__device__ __forceinline__ u32x2_t pack_f16x4(float4 v) {
+    f16x4 b = {(_Float16)v.x, (_Float16)v.y, (_Float16)v.z, (_Float16)v.w};
+    return __builtin_bit_cast(u32x2_t, b);
+}
+__device__ __forceinline__ float4 unpack_f16x4(u32x2_t u) {
+    const f16x4 h = __builtin_bit_cast(f16x4, u);
+    return make_float4((float)h.x, (float)h.y, (float)h.z, (float)h.w);
+}
+// the storage format of a 2-byte element type T (bf16 or f16)
+template <typename T> __device__ __forceinline__ u32x2_t pack4(float4 v);
+template <> __device__ __forceinline__ u32x2_t pack4<__bf16>(float4 v) { return pack_bf16x4(v); }
+template <> __device__ __forceinline__ u32x2_t pack4<_Float16>(float4 v) { return pack_f16x4(v); }
+template <typename T> __device__ __forceinline__ float4 unpack4(u32x2_t u);
+template <> __device__ __forceinline__ float4 unpack4<__bf16>(u32x2_t u) { return unpack_bf16x4(u); }
+template <> __device__ __forceinline__ float4 unpack4<_Float16>(u32x2_t u) { return unpack_f16x4(u); }
+__device__ __forceinline__ float4 ld4(const _Float16 *p) { return unpack_f16x4(*reinterpret_cast<const u32x2_t *>(p)); }
+__device__ __forceinline__ void st4(_Float16 *p, float4 v) { *reinterpret_cast<u32x2_t *>(p) = pack_f16x4(v); }
+
 // v_permlane16_swap_b32 (gfx950): lanes of the odd 16-lane rows of `a` trade places with the lanes
 // of the even rows of `b` one row below (lane l of row 2i+1 of a <-> lane l-16 of row 2i of b).
 // An involution; measured on MI355X with scripts/permlane_probe.hip.
@@ -107,6 +144,7 @@ __device__ __forceinline__ void pl32swap(uint32_t &a, uint32_t &b) {
 
 __device__ __forceinline__ float ld1(const float *p) { return *p; }
 __device__ __forceinline__ float ld1(const __bf16 *p) { return (float)*p; }
+__device__ __forceinline__ float ld1(const _Float16 *p) { return (float)*p; }
 
 // ---- buffer (SRSRC) memory ops: 32-bit byte offsets against a wave-uniform descriptor built from
 // kernel arguments; an offset past the descriptor's size reads 0 and drops a store, which is how
@@ -136,6 +174,7 @@ __device__ __forceinline__ void bst8o(__amdgpu_buffer_rsrc_t r, uint32_t off, u3
     __builtin_amdgcn_raw_buffer_store_b64(v, r, (int)off, 0, BUGSEG_OUT_AUX);
 }
 __device__ __forceinline__ void bld8(RawB &x, __amdgpu_buffer_rsrc_t r, uint32_t off) { x.v = bld16(r, off); }
+__device__ __forceinline__ void bld8(RawH &x, __amdgpu_buffer_rsrc_t r, uint32_t off) { x.v = bld16(r, off); }
 __device__ __forceinline__ void bld8(RawF &x, __amdgpu_buffer_rsrc_t r, uint32_t off) {
     x.a = __builtin_bit_cast(float4, bld16(r, off));
     x.b = __builtin_bit_cast(float4, bld16(r, off + 16));
@@ -149,24 +188,33 @@ __device__ __forceinline__ float4 bld4(__amdgpu_buffer_rsrc_t r, uint32_t off, c
     return make_float4(__uint_as_float(u.x << 16), __uint_as_float(u.x & 0xffff0000u),
                        __uint_as_float(u.y << 16), __uint_as_float(u.y & 0xffff0000u));
 }
+__device__ __forceinline__ float4 bld4(__amdgpu_buffer_rsrc_t r, uint32_t off, const _Float16 *) {
+    return unpack_f16x4(__builtin_amdgcn_raw_buffer_load_b64(r, (int)off, 0, 0));
+}
 
 // 4 consecutive elements kept raw (prefetched early, converted where used)
 template <typename T> struct MvRawT;
 template <> struct MvRawT<__bf16> { using type = u32x2; };
+template <> struct MvRawT<_Float16> { using type = u32x2; };
 template <> struct MvRawT<float> { using type = u32x4; };
 template <typename T> using MvRaw = typename MvRawT<T>::type;
 template <typename T> __device__ __forceinline__ MvRaw<T> mvload(__amdgpu_buffer_rsrc_t r, uint32_t off);
 template <> __device__ __forceinline__ u32x2 mvload<__bf16>(__amdgpu_buffer_rsrc_t r, uint32_t off) {
     return __builtin_amdgcn_raw_buffer_load_b64(r, (int)off, 0, 0);
 }
+template <> __device__ __forceinline__ u32x2 mvload<_Float16>(__amdgpu_buffer_rsrc_t r, uint32_t off) {
+    return __builtin_amdgcn_raw_buffer_load_b64(r, (int)off, 0, 0);
+}
 template <> __device__ __forceinline__ u32x4 mvload<float>(__amdgpu_buffer_rsrc_t r, uint32_t off) {
     return __builtin_amdgcn_raw_buffer_load_b128(r, (int)off, 0, 0);
 }
-__device__ __forceinline__ float4 mvcvt(u32x2 u) {
+template <typename T> __device__ __forceinline__ float4 mvcvt(MvRaw<T> u);
+template <> __device__ __forceinline__ float4 mvcvt<__bf16>(u32x2 u) {
     return make_float4(__uint_as_float(u.x << 16), __uint_as_float(u.x & 0xffff0000u),
                        __uint_as_float(u.y << 16), __uint_as_float(u.y & 0xffff0000u));
 }
-__device__ __forceinline__ float4 mvcvt(u32x4 u) {
+template <> __device__ __forceinline__ float4 mvcvt<_Float16>(u32x2 u) { return unpack_f16x4(u); }
+template <> __device__ __forceinline__ float4 mvcvt<float>(u32x4 u) {
     return make_float4(__uint_as_float(u.x), __uint_as_float(u.y), __uint_as_float(u.z), __uint_as_float(u.w));
 }
 
@@ -186,6 +234,7 @@ __device__ __forceinline__ float vmax(float a, float b) {
 }
 // storage rounding of an activation (the unfused plan stores it as T and reads it back)
 __device__ __forceinline__ float4 round_t(float4 v, const __bf16 *) { return unpack_bf16x4(pack_bf16x4(v)); }
+__device__ __forceinline__ float4 round_t(float4 v, const _Float16 *) { return unpack_f16x4(pack_f16x4(v)); }
 __device__ __forceinline__ float4 round_t(float4 v, const float *) { return v; }
 
 // Two 16-channel row fragments (quads qa, qb: lane kq holds channels 4kq..4kq+3 of each) -> the B
@@ -196,6 +245,15 @@ __device__ __forceinline__ float4 round_t(float4 v, const float *) { return v; }
 // scripts/permlane_probe.hip). qb == 0 for a single fragment (k groups 2, 3 zero).
 __device__ __forceinline__ void to_bop(RawB &r, float4 qa, float4 qb) {
     const u32x2_t a = pack_bf16x4(qa), b = pack_bf16x4(qb);
+    uint32_t a0 = a.x, a1 = a.y, b0 = b.x, b1 = b.y;
+    pl32swap(a0, b0);
+    pl32swap(a1, b1);
+    pl16swap(a0, b0);
+    pl16swap(a1, b1);
+    r.v = make_uint4(a0, a1, b0, b1);
+}
+__device__ __forceinline__ void to_bop(RawH &r, float4 qa, float4 qb) {
+    const u32x2_t a = pack_f16x4(qa), b = pack_f16x4(qb);
     uint32_t a0 = a.x, a1 = a.y, b0 = b.x, b1 = b.y;
     pl32swap(a0, b0);
     pl32swap(a1, b1);

@@ -8,6 +8,7 @@
 // so the f64 output equals NumPy's bit for bit and the f32 / bf16 outputs are its roundings.
 // HBM-bound: 3 B read (x up to 4 taps, L1/L2-served) + 16 B (bf16 engine layout) written per pixel.
 #include "bugseg_internal.h"
+#include "mfma_common.h"
 #include "../../include/bugseg.h"
 
 namespace bugseg {
@@ -62,6 +63,10 @@ __global__ void __launch_bounds__(256) preprocess_kernel(const PreArgs a) {
                 bf16x8 v = {(__bf16)(float)r, (__bf16)(float)g, (__bf16)(float)bl, (__bf16)0.f,
                             (__bf16)0.f, (__bf16)0.f, (__bf16)0.f, (__bf16)0.f};
                 reinterpret_cast<bf16x8 *>(a.out)[i] = v;
+            } else if (a.prec == PREC_F16) {
+                f16x8 v = {(_Float16)(float)r, (_Float16)(float)g, (_Float16)(float)bl, (_Float16)0.f,
+                           (_Float16)0.f, (_Float16)0.f, (_Float16)0.f, (_Float16)0.f};
+                reinterpret_cast<f16x8 *>(a.out)[i] = v;
             } else {
                 float4 *o = reinterpret_cast<float4 *>(a.out) + 2 * i;
                 o[0] = make_float4((float)r, (float)g, (float)bl, 0.f);
@@ -104,6 +109,10 @@ __global__ void __launch_bounds__(256) nchw_to_input_kernel(const NchwArgs a) {
             bf16x8 o = {(__bf16)v[0], (__bf16)v[1], (__bf16)v[2], (__bf16)0.f,
                         (__bf16)0.f, (__bf16)0.f, (__bf16)0.f, (__bf16)0.f};
             reinterpret_cast<bf16x8 *>(a.out)[i] = o;
+        } else if (a.prec == PREC_F16) {
+            f16x8 o = {(_Float16)v[0], (_Float16)v[1], (_Float16)v[2], (_Float16)0.f,
+                       (_Float16)0.f, (_Float16)0.f, (_Float16)0.f, (_Float16)0.f};
+            reinterpret_cast<f16x8 *>(a.out)[i] = o;
         } else {
             float4 *o = reinterpret_cast<float4 *>(a.out) + 2 * i;
             o[0] = make_float4(v[0], v[1], v[2], 0.f);

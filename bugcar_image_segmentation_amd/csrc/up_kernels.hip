@@ -173,7 +173,7 @@ __global__ void __launch_bounds__(256, (sizeof(T) == 2 ? (CIN >= 128 ? 2 : 3) : 
             if constexpr (SWAP) {
 #pragma unroll
                 for (int t = 0; t < NR3 / 2; ++t) {
-                    const u32x2_t p0 = pack_bf16x4(ep3(2 * t)), p1 = pack_bf16x4(ep3(2 * t + 1));
+                    const u32x2_t p0 = pack4<T>(ep3(2 * t)), p1 = pack4<T>(ep3(2 * t + 1));
                     uint32_t x0 = p0.x, x1 = p0.y, y0 = p1.x, y1 = p1.y;
                     pl16swap(x0, y0);
                     pl16swap(x1, y1);
@@ -185,7 +185,7 @@ __global__ void __launch_bounds__(256, (sizeof(T) == 2 ? (CIN >= 128 ? 2 : 3) : 
                 for (int r = 0; r < NR3; ++r) {
                     const float4 v = ep3(r);
                     const uint32_t off = pv ? (opix * COUT + r * 16 + kq * 4) * ES : OOB;
-                    if constexpr (ES == 2) bst8o(ro, off, pack_bf16x4(v));
+                    if constexpr (ES == 2) bst8o(ro, off, pack4<T>(v));
                     else bst16o(ro, off, __builtin_bit_cast(uint4, v));
                 }
             }
@@ -211,6 +211,9 @@ static hipError_t launch_shape(int prec, const UpArgs &a, dim3 g, hipStream_t s)
     if (prec == PREC_BF16) {
         const size_t lds = up_lds<__bf16, CI, II, CO>();
         hipLaunchKernelGGL((up_kernel<__bf16, CI, II, CO>), g, dim3(256), lds, s, a);
+    } else if (prec == PREC_F16) {
+        const size_t lds = up_lds<_Float16, CI, II, CO>();
+        hipLaunchKernelGGL((up_kernel<_Float16, CI, II, CO>), g, dim3(256), lds, s, a);
     } else {
         const size_t lds = up_lds<float, CI, II, CO>();
         if (lds > 64 * 1024) {
@@ -243,8 +246,12 @@ hipError_t launch_up(int prec, int cin, int it, int cout, const UpArgs &a, hipSt
     const int nfrag = (a.M + 15) / 16;
     int g = (nfrag + 3) / 4;
     // one resident round of workgroups, each streaming over its fragments (prefetch in the kernel)
-    const int res = cin == 128 ? (prec == PREC_BF16 ? up_resident<__bf16, 128, 32, 64>() : up_resident<float, 128, 32, 64>())
-                               : (prec == PREC_BF16 ? up_resident<__bf16, 64, 16, 16>() : up_resident<float, 64, 16, 16>());
+    const int res = cin == 128 ? (prec == PREC_BF16  ? up_resident<__bf16, 128, 32, 64>()
+                                  : prec == PREC_F16 ? up_resident<_Float16, 128, 32, 64>()
+                                                     : up_resident<float, 128, 32, 64>())
+                               : (prec == PREC_BF16  ? up_resident<__bf16, 64, 16, 16>()
+                                  : prec == PREC_F16 ? up_resident<_Float16, 64, 16, 16>()
+                                                     : up_resident<float, 64, 16, 16>());
     if (g > res) g = res;
     if (g < 1) g = 1;
     if (cin == 128 && it == 32 && cout == 64) return launch_shape<128, 32, 64>(prec, a, dim3(g), s);

@@ -77,9 +77,11 @@ class ENET(InferenceModel):
     def __init__(self, GRAPH_PB_PATH=None, *, weights=None, precision: str = "fp32", device: int | None = None):
         """GRAPH_PB_PATH: weight file (default "./pretrained_models/enet.pb", models.py:23-24).
         weights: a BSG1 blob (bytes) or an enet_spec block list, instead of a file.
-        precision: "fp32" (parity mode) or "bf16" (throughput mode)."""
-        if precision not in ("fp32", "bf16"):
-            raise ValueError("precision must be 'fp32' or 'bf16'")
+        precision: "fp32" (parity mode), "bf16" or "fp16" (throughput modes: 2-byte activations and
+        weights, f32 accumulation; fp16 keeps 3 more mantissa bits than bf16, so its class maps agree
+        more closely with fp32, within fp16's +-65504 range)."""
+        if precision not in ("fp32", "bf16", "fp16"):
+            raise ValueError("precision must be 'fp32', 'bf16' or 'fp16'")
         if weights is None:
             if GRAPH_PB_PATH is None:
                 GRAPH_PB_PATH = "./pretrained_models/enet.pb"
@@ -89,7 +91,7 @@ class ENET(InferenceModel):
         else:
             blob = enet_spec.serialize(weights)
         self.precision = precision
-        self.ctx = N.Context(device, N.BF16 if precision == "bf16" else N.FP32)
+        self.ctx = N.Context(device, {"fp32": N.FP32, "bf16": N.BF16, "fp16": N.F16}[precision])
         self.ctx.load_weights(blob)
         self.blob = blob
         self.num_classes = self.ctx.num_classes
@@ -112,7 +114,7 @@ class ENET(InferenceModel):
         if x.dim() != 4 or x.shape[1] != 3:
             raise ValueError(f"expected (B, 3, H, W) input, got {tuple(x.shape)}")
         B, _, H, W = x.shape
-        es = 2 if self.precision == "bf16" else 4
+        es = 4 if self.precision == "fp32" else 2
         out = self._buf("in", (B, H, W, 8 * es), torch.uint8)
         self.ctx.nchw_to_input(x, B, H, W, out, self._stream())
         return out
@@ -167,7 +169,7 @@ class ENET(InferenceModel):
         elif layout == N.PRE_NCHW_F32:
             out = torch.empty((B, 3, H, W), dtype=torch.float32, device=dev)
         else:
-            out = torch.empty((B, H, W, 8 * (2 if c.precision == N.BF16 else 4)), dtype=torch.uint8, device=dev)
+            out = torch.empty((B, H, W, 8 * (4 if c.precision == N.FP32 else 2)), dtype=torch.uint8, device=dev)
         c.preprocess(x, B, H0, W0, H, W, layout, out, torch.cuda.current_stream(dev))
         return out
 

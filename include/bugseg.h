@@ -43,7 +43,10 @@ enum {
     BUGSEG_ESTATE = -5    /* e.g. forward before load_weights                                  */
 };
 
-enum { BUGSEG_FP32 = 0, BUGSEG_BF16 = 1 };
+/* Precisions: activations and weights stored as f32 (the parity mode), bf16 (the throughput mode) or
+ * f16 (the same bytes and MFMA rate as bf16 with 3 more mantissa bits: closer class agreement with
+ * fp32; range +-65504). Products accumulate in f32 in every mode. */
+enum { BUGSEG_FP32 = 0, BUGSEG_BF16 = 1, BUGSEG_F16 = 2 };
 
 /* out_kind of bugseg_enet_forward */
 enum {
@@ -93,7 +96,7 @@ typedef struct {
 int bugseg_version(void);
 
 /* Create / destroy a context on HIP device `device`, computing in `precision` (BUGSEG_FP32 is the
- * parity mode: logits within 1e-3 of the fp32 oracle; BUGSEG_BF16 the throughput mode).
+ * parity mode: logits within 1e-3 of the fp32 oracle; BUGSEG_BF16 / BUGSEG_F16 the throughput modes).
  * Replaces ENET.__init__'s tf.compat.v1.Session() (models.py:21-22). */
 int bugseg_create(int device, int precision, bugseg_ctx **out);
 int bugseg_destroy(bugseg_ctx *ctx);

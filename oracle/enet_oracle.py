@@ -153,8 +153,12 @@ def preprocess(bgr: np.ndarray, width: int = 512, height: int = 256) -> np.ndarr
 
 
 # ---------------------------------------------------------------- bf16-storage emulation
+_STORE = torch.bfloat16      # the storage type forward_bf16_storage rounds to (forward_storage sets it)
+
+
 def _bf16(t):
-    return t.to(torch.bfloat16).to(torch.float32)
+    """Round to the emulated storage type (bf16 unless forward_storage selected f16) and back."""
+    return t.to(_STORE).to(torch.float32)
 
 
 def _fold(u):
@@ -229,3 +233,14 @@ def forward_bf16_storage(blocks, x: np.ndarray) -> np.ndarray:
             elif b.type == "fullconv":
                 h = _unit_bf16(h, b.units[0], act=False)
         return h.numpy()
+
+
+def forward_storage(blocks, x: np.ndarray, dtype=torch.bfloat16) -> np.ndarray:
+    """forward_bf16_storage with the stored activations and folded weights rounded to `dtype`
+    (torch.bfloat16: the bf16 mode; torch.float16: the fp16 mode), f32 products and accumulation."""
+    global _STORE
+    prev, _STORE = _STORE, dtype
+    try:
+        return forward_bf16_storage(blocks, x)
+    finally:
+        _STORE = prev
