@@ -41,9 +41,9 @@ MFMA_F32_PEAK_TFLOPS = 157.3
 
 SURVEY_BYTES_PER_FRAME = 180.2e6   # bf16 per-layer activation bytes per 480x640 frame
 # rocprofv3 kernel names of the plan's kernel tags (scripts/layer_times.py maps them back)
-KERNEL_NAMES = {"bneck C128": "bneck_kernel<bf16,128,sym>", "bneck C128 asym": "bneck_kernel<bf16,128,asym>",
-                "bneck C64": "bneck_kernel<bf16,64,sym>", "bneck C16": "bneck_kernel<bf16,16,sym>",
-                "init": "init_kernel<bf16,bgr>"}
+KERNEL_NAMES = {"bneck C128": "bneck_kernel<{t},128,sym>", "bneck C128 asym": "bneck_kernel<{t},128,asym>",
+                "bneck C64": "bneck_kernel<{t},64,sym>", "bneck C16": "bneck_kernel<{t},16,sym>",
+                "init": "init_kernel<{t},bgr>"}
 
 
 def kernel_table(ctx, B, H, W, reps, stream):
@@ -381,7 +381,7 @@ def main():
                 "bound": "hbm", "achieved": round(k_achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                 "frac": round(k_achieved / HBM_PEAK_GBS, 4),
                 "traffic": traffic,
-                "kernel": f"{KERNEL_NAMES.get(tag, tag)} [{tag}]: the dominant kernel of the forward "
+                "kernel": f"{KERNEL_NAMES.get(tag.rsplit(' ', 1)[0], tag).format(t=a.precision)} [{tag}]: the dominant kernel of the forward "
                           f"({k['launches']} launches, {k['total_us']:.0f} us of {t_fwd * 1e3:.0f} us); "
                           f"{k['bytes_per_launch'] / 1e6:.1f} MB per launch = the bytes the launch must move "
                           f"(block input read once + output written once); {k['us_per_launch']:.2f} us per launch "
