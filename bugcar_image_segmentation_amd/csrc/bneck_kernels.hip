@@ -108,6 +108,7 @@ __global__ void __launch_bounds__((BShape<C, V>::NW * 64), (sizeof(T) == 2 ? BSh
     constexpr int NR1 = (I + 15) / 16;                // 16-row fragments of t0 / t1
     constexpr int NR3 = C / 16;                       // 16-row fragments of out
     constexpr bool DN = CI > 0;                       // (I above already depends on it)
+    constexpr int OAUX = OUT_AUX_SEL((C >= 64 && CI != 16) ? 16 : 0);   // sc1 output stores (mfma_common.h)
     static_assert(!DN || (!ASYM && !TR && !BShape<C, V>::RD && (CI == 16 || CI % 32 == 0)), "down mode: plain tiles");
     constexpr int G1 = DN ? CI / 2 : C / 8, KS1 = (G1 + 3) / 4;   // proj k groups / steps (down: 4 taps x CI)
     constexpr int CG1 = CI / 8;                       // down: 8-channel groups per tap
@@ -652,7 +653,7 @@ __global__ void __launch_bounds__((BShape<C, V>::NW * 64), (sizeof(T) == 2 ? BSh
                     const int q = lane + 64 * k;
                     if (q < CPF) {
                         const uint32_t off = pix_off(wave + NW * j, q / CPP, (q % CPP) * EPC);
-                        bst16o(rob, off, *reinterpret_cast<const uint4 *>(stg + (q / CPP) * OSTR + (q % CPP) * EPC));
+                        bst16o<OAUX>(rob, off, *reinterpret_cast<const uint4 *>(stg + (q / CPP) * OSTR + (q % CPP) * EPC));
                     }
                 }
                 wave_lds_sync();
@@ -692,7 +693,7 @@ __global__ void __launch_bounds__((BShape<C, V>::NW * 64), (sizeof(T) == 2 ? BSh
                     uint32_t x0 = p0.x, x1 = p0.y, y0 = p1.x, y1 = p1.y;
                     pl16swap(x0, y0);
                     pl16swap(x1, y1);
-                    bst16o(rob, off, make_uint4(x0, x1, y0, y1));
+                    bst16o<OAUX>(rob, off, make_uint4(x0, x1, y0, y1));
                 } else {
                     const int r = t;
                     f32x4 acc = bias_in_acc(NR3, 1) ? bias4(cb3 + r * 16 + kq * 4) : (f32x4){0.f, 0.f, 0.f, 0.f};
@@ -701,10 +702,10 @@ __global__ void __launch_bounds__((BShape<C, V>::NW * 64), (sizeof(T) == 2 ? BSh
                     mma(acc, wf, tf[j]);
                     if constexpr (HALF) {
                         float4 v = act(add4(out3(r, acc), unpack4<T>((u32x2_t){rc.x, rc.y})), cso + r * 16 + kq * 4);
-                        bst8o(rob, off, pack4<T>(v));
+                        bst8o<OAUX>(rob, off, pack4<T>(v));
                     } else {
                         float4 v = act(add4(out3(r, acc), __builtin_bit_cast(float4, rc)), cso + r * 16 + kq * 4);
-                        bst16o(rob, off, __builtin_bit_cast(uint4, v));
+                        bst16o<OAUX>(rob, off, __builtin_bit_cast(uint4, v));
                     }
                 }
             }

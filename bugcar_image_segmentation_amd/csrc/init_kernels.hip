@@ -186,9 +186,9 @@ __global__ void __launch_bounds__(256) init_kernel(const ConvArgs a) {
             const bool ok = oy < a.Hg && ox < a.Wg && c0 < a.outC;
             const uint32_t off = ok ? (uint32_t)(((n * a.Hg + oy) * a.Wg + ox) * a.outC + c0) * (uint32_t)sizeof(T) : OOB;
             if constexpr (sizeof(T) == 2) {
-                bst8o(rout, off, pack4<T>(v));
+                bst8o<OUT_AUX_SEL(16)>(rout, off, pack4<T>(v));
             } else {
-                bst16o(rout, off, __builtin_bit_cast(uint4, v));
+                bst16o<OUT_AUX_SEL(16)>(rout, off, __builtin_bit_cast(uint4, v));
             }
         }
     }

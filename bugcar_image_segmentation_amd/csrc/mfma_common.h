@@ -161,17 +161,26 @@ __device__ __forceinline__ uint4 bld16(__amdgpu_buffer_rsrc_t r, uint32_t off) {
 __device__ __forceinline__ void bst16(__amdgpu_buffer_rsrc_t r, uint32_t off, uint4 v) {
     __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, v), r, (int)off, 0, 0);
 }
-// Stores of a launch's output, which the launch itself never reads back: cache policy OUT_AUX (0 =
+// Stores of a launch's output, which the launch itself never reads back: cache policy AUX (0 =
 // default; 16 = sc1 write-through, the line leaves the XCD's L2; 2 = nt), so a kernel's output
-// stream does not evict the input lines its neighbouring tiles still re-read from L2.
+// stream does not evict the input lines its neighbouring tiles still re-read from L2 (the phase-3
+// residual, the halo rows of the next tile band). OUT_AUX_SEL(sel) names the per-kernel choice
+// (sc1 for the C >= 64 bottleneck / C128 up / initial kernels), built with -DBUGSEG_OUT_AUX=-1.
+// Measured (round 2, same box, alternating A/B twice): it makes those kernels 3-6% faster one stream
+// at a time (C128 26.8 -> 25.4 us, PMC reads 66 -> 62 MB per launch) but the 2-stream bench 2.4%
+// slower (37.1k -> 36.2k frames/s; why is not pinned down: with two shards interleaved, write-back
+// lines still in L2 evidently serve more reads than they evict). So the default is 0 (off).
 #ifndef BUGSEG_OUT_AUX
 #define BUGSEG_OUT_AUX 0
 #endif
+#define OUT_AUX_SEL(sel) (BUGSEG_OUT_AUX >= 0 ? BUGSEG_OUT_AUX : (sel))
+template <int AUX>
 __device__ __forceinline__ void bst16o(__amdgpu_buffer_rsrc_t r, uint32_t off, uint4 v) {
-    __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, v), r, (int)off, 0, BUGSEG_OUT_AUX);
+    __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, v), r, (int)off, 0, AUX);
 }
+template <int AUX>
 __device__ __forceinline__ void bst8o(__amdgpu_buffer_rsrc_t r, uint32_t off, u32x2 v) {
-    __builtin_amdgcn_raw_buffer_store_b64(v, r, (int)off, 0, BUGSEG_OUT_AUX);
+    __builtin_amdgcn_raw_buffer_store_b64(v, r, (int)off, 0, AUX);
 }
 __device__ __forceinline__ void bld8(RawB &x, __amdgpu_buffer_rsrc_t r, uint32_t off) { x.v = bld16(r, off); }
 __device__ __forceinline__ void bld8(RawH &x, __amdgpu_buffer_rsrc_t r, uint32_t off) { x.v = bld16(r, off); }

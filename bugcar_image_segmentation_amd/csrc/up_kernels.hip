@@ -29,6 +29,7 @@ template <typename T, int CIN, int I, int COUT>
 __global__ void __launch_bounds__(256, (sizeof(T) == 2 ? (CIN >= 128 ? 2 : 3) : 1)) up_kernel(const UpArgs a) {
     using Raw = typename Tr<T>::Raw;
     constexpr int ES = (int)sizeof(T);
+    constexpr int OAUX = OUT_AUX_SEL(CIN >= 128 ? 16 : 0);   // sc1 output stores (mfma_common.h)
     constexpr int NR1 = (COUT + I) / 16;              // GEMM 1 rows: main then e1
     constexpr int NM = COUT / 16, NE = I / 16;        // row fragments of main / e1 (per tconv phase)
     constexpr int KS1 = CIN / 32;                     // GEMM 1 k-steps
@@ -178,15 +179,15 @@ __global__ void __launch_bounds__(256, (sizeof(T) == 2 ? (CIN >= 128 ? 2 : 3) : 
                     pl16swap(x0, y0);
                     pl16swap(x1, y1);
                     const int ch = (2 * t + (kq & 1)) * 16 + 8 * (kq >> 1);
-                    bst16o(ro, pv ? (opix * COUT + ch) * ES : OOB, make_uint4(x0, x1, y0, y1));
+                    bst16o<OAUX>(ro, pv ? (opix * COUT + ch) * ES : OOB, make_uint4(x0, x1, y0, y1));
                 }
             } else {
 #pragma unroll
                 for (int r = 0; r < NR3; ++r) {
                     const float4 v = ep3(r);
                     const uint32_t off = pv ? (opix * COUT + r * 16 + kq * 4) * ES : OOB;
-                    if constexpr (ES == 2) bst8o(ro, off, pack4<T>(v));
-                    else bst16o(ro, off, __builtin_bit_cast(uint4, v));
+                    if constexpr (ES == 2) bst8o<OAUX>(ro, off, pack4<T>(v));
+                    else bst16o<OAUX>(ro, off, __builtin_bit_cast(uint4, v));
                 }
             }
         }
