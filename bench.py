@@ -96,6 +96,7 @@ def parse():
     p.add_argument("--precision", default="fp16", choices=["bf16", "fp16", "fp32"],
                    help="storage precision of the timed step (fp16: bf16's bytes and MFMA rate, 3 more mantissa bits)")
     p.add_argument("--streams", type=int, default=2, help="frame shards run concurrently on this many HIP streams")
+    p.add_argument("--stream-priority", type=int, default=0, help="HIP priority of the side shards' streams")
     p.add_argument("--graph", type=int, default=0, help="1: replay the step as one captured HIP graph")
     p.add_argument("--cpu-baseline-seconds", type=float, default=12.0)
     p.add_argument("--no-cpu-baseline", action="store_true")
@@ -292,7 +293,8 @@ def main():
     model = ENET(weights=blocks, precision=a.precision)
     bev = synthetic.synthetic_bev(H, W)
     grid = (synthetic.GRID_W_M, synthetic.GRID_H_M, synthetic.CELL_M)
-    pipe = OccupancyPipeline(model, bev, *grid, model_hw=(H, W), streams=a.streams)
+    pipe = OccupancyPipeline(model, bev, *grid, model_hw=(H, W), streams=a.streams,
+                             stream_priority=a.stream_priority)
     frames = torch.from_numpy(synthetic.uniform_frames(B, H, W, seed=rank)).to(dev)
 
     run = lambda: pipe.run(frames)  # noqa: E731

@@ -25,10 +25,11 @@ class OccupancyPipeline:
 
     def __init__(self, model: ENET, bev: bev_transform_tools, grid_w_m: float, grid_h_m: float, cell_m: float,
                  model_hw: tuple[int, int] | None = None, ros_layout: bool = False, streams: int = 1,
-                 binary: bool = False):
+                 binary: bool = False, stream_priority: int = 0):
         """binary=True is the predict_binary + create_occupancy_grid_binary pairing (models.py:70-82,
         bev.py:97-165): class maps through the binary LUT, the binary rasteriser; in the laserscan-like
-        mode its output is the reference's pair, (2, B, ...) (bev.py:164)."""
+        mode its output is the reference's pair, (2, B, ...) (bev.py:164). stream_priority is the HIP
+        priority of the side shards' streams (shard 0 runs on the caller's stream; lower = higher)."""
         self.model = model
         self.binary = binary
         self.bev = bev
@@ -41,6 +42,7 @@ class OccupancyPipeline:
         if streams < 1:
             raise ValueError("streams must be >= 1")
         self.streams = streams
+        self.stream_priority = stream_priority
         self._ctxs = [model.ctx]
         self._streams = []
         self._x = None
@@ -52,7 +54,7 @@ class OccupancyPipeline:
             c = N.Context(dev.index, self.model.ctx.precision)
             c.load_weights(self.model.blob)
             self._ctxs.append(c)
-            self._streams.append(torch.cuda.Stream(device=dev))
+            self._streams.append(torch.cuda.Stream(device=dev, priority=self.stream_priority))
         return self._ctxs, self._streams
 
     def _bufs(self, B: int, dev: torch.device):
