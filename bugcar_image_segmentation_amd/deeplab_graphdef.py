@@ -24,9 +24,12 @@ folding of graphdef.py, and returns the network the engine runs:
 * the projection's input channels are permuted from the graph's concat order to the engine's
   [image pooling, 1x1, atrous...] order.
 
-Not read from the graph: the preprocessing (pad to the crop with 127.5, ``(2/255) x - 1``) and the
-final bilinear resize + argmax are the export's fixed semantics and the engine's own (deeplab_spec.py);
-``crop`` is a parameter (default 513, the export's crop size).
+The crop size IS read from the graph: deeplab/input_preprocess.py pads every image to
+``image_size + max(crop - image_size, 0)`` per axis, which a frozen export holds as
+``Maximum(Sub(Const crop, StridedSlice(Shape(image), [axis])), 0)`` — the two ``Const`` operands give
+(crop height, crop width), the lower axis being the height (read_crop). Not read from the graph: the
+pad value 127.5, ``(2/255) x - 1`` and the final bilinear resize + argmax, the export's fixed
+semantics and the engine's own (deeplab_spec.py).
 
 Parity: pinned against graphs written by tests/deeplab_graph_writer.py (run by the NumPy GraphDef
 interpreter oracle/tf_graph.py as the sess.run stand-in); UNPINNED against TF on the real deeplab.pb.
@@ -141,9 +144,36 @@ def _expect(cond, msg):
         raise GraphImportError(msg)
 
 
-def import_deeplab(data: bytes, crop: int = D.CROP) -> D.DeepLab:
-    """Frozen DeepLab-MobileNetV2 GraphDef bytes -> deeplab_spec.DeepLab (weights + topology)."""
+def read_crop(g: Graph):
+    """(crop height, crop width) from the export's pad-to-crop arithmetic, or None when the graph has
+    none (see the module docstring)."""
+    found = {}
+    for n in g.nodes:
+        if n.op != "Sub" or len(n.inputs) != 2 or not g.is_const(n.inputs[0]) or g.is_const(n.inputs[1]):
+            continue
+        v = np.asarray(g.const(n.inputs[0]))
+        if v.size != 1 or v.dtype.kind not in "iu" or not any(c.op == "Maximum" for c in g.consumers[n.name]):
+            continue
+        ss = g.producer_chain(n.inputs[1], PASS)
+        if ss.op != "StridedSlice" or len(ss.inputs) < 2 or g.producer_chain(ss.inputs[0], PASS).op != "Shape" \
+                or not g.is_const(ss.inputs[1]):
+            continue
+        found[int(np.atleast_1d(g.const(ss.inputs[1]))[0])] = int(v.reshape(()))
+    if len(found) != 2:
+        return None
+    (_, h), (_, w) = sorted(found.items())
+    _expect(h >= 2 and w >= 2, f"graph pads to a {h}x{w} crop")
+    return h, w
+
+
+def import_deeplab(data: bytes, crop=None, default_crop: int = D.CROP) -> D.DeepLab:
+    """Frozen DeepLab-MobileNetV2 GraphDef bytes -> deeplab_spec.DeepLab (weights + topology).
+    crop: None reads the export's crop from the graph (read_crop; ``default_crop`` when the graph
+    holds none), an int or (height, width) overrides it."""
     g = Graph(parse_graphdef(data))
+    if crop is None:
+        crop = read_crop(g) or default_crop
+    crop_h, crop_w = (int(crop), int(crop)) if np.ndim(crop) == 0 else (int(crop[0]), int(crop[1]))
     convs = [_Conv(g, n) for n in g.nodes if n.op in CONV_OPS]
     _expect(len(convs) >= 6, f"graph has {len(convs)} convolutions; not a DeepLab export")
     closures = [_affine_act(g, c) for c in convs]
@@ -272,12 +302,13 @@ def import_deeplab(data: bytes, crop: int = D.CROP) -> D.DeepLab:
     os_ = stem.stride
     for b in blocks:
         os_ *= b.dw.stride
-    net = D.DeepLab(stem, blocks, pool, aspp0, atrous_convs, project, logits, logits.cout, os_, crop,
-                    meta=dict(source="graphdef", atrous_rates=tuple(a.dil for a in atrous_convs)))
+    net = D.DeepLab(stem, blocks, pool, aspp0, atrous_convs, project, logits, logits.cout, os_, crop_h,
+                    meta=dict(source="graphdef", atrous_rates=tuple(a.dil for a in atrous_convs)),
+                    crop_w=crop_w if crop_w != crop_h else 0)
     return net
 
 
-def graphdef_to_npz(data: bytes, path, crop: int = D.CROP) -> D.DeepLab:
+def graphdef_to_npz(data: bytes, path, crop=None) -> D.DeepLab:
     net = import_deeplab(data, crop=crop)
     D.save(net, path)
     return net
@@ -290,4 +321,5 @@ if __name__ == "__main__":
         sys.exit(2)
     with open(sys.argv[1], "rb") as f:
         net = graphdef_to_npz(f.read(), sys.argv[2])
-    print(f"{sys.argv[2]}: {len(net.blocks)} blocks, {net.num_classes} classes, output stride {net.output_stride}")
+    print(f"{sys.argv[2]}: {len(net.blocks)} blocks, {net.num_classes} classes, output stride {net.output_stride}, "
+          f"crop {D.crop_hw(net)}")

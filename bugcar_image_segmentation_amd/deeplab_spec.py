@@ -104,8 +104,14 @@ class DeepLab:
     logits: Conv
     num_classes: int = NUM_CLASSES
     output_stride: int = 8
-    crop: int = CROP
+    crop: int = CROP             # crop height (the export's crop_size[0])
     meta: dict = field(default_factory=dict)
+    crop_w: int = 0              # crop width when the export's crop is not square (0: = crop)
+
+
+def crop_hw(net: "DeepLab") -> tuple:
+    """(crop height, crop width): the padded size every image runs at (pad_to_bounding_box)."""
+    return int(net.crop), int(net.crop_w or net.crop)
 
 
 def same_pad(n_in: int, k: int, s: int, d: int):
@@ -136,11 +142,13 @@ class _Init:
 
 
 def build_deeplab(seed: int = 4321, num_classes: int = NUM_CLASSES, output_stride: int = 8,
-                  atrous_rates=(), crop: int = CROP, width: float = 1.0) -> DeepLab:
+                  atrous_rates=(), crop=CROP, width: float = 1.0) -> DeepLab:
     """Synthetic-weight DeepLabV3-MobileNetV2 (He-normal convs, BN gamma~U(0.5,1.5), beta~N(0,0.1),
     mean~N(0,0.1), var~U(0.5,1.5); the linear projections of residual blocks draw gamma from
     U(0.1,0.3) so the residual stream stays O(1) without trained statistics). `width` scales the
-    channel counts (tests use small widths; multiples of 8 are kept)."""
+    channel counts (tests use small widths; multiples of 8 are kept). `crop`: an int or (height,
+    width)."""
+    crop_h, crop_w = (int(crop), 0) if np.ndim(crop) == 0 else (int(crop[0]), int(crop[1]))
     ini = _Init(seed)
     ch = lambda c: max(8, int(round(c * width / 8)) * 8)  # noqa: E731
     stem = ini.conv(ch(32), 3, 3, ACT_RELU6, stride=2)
@@ -171,8 +179,9 @@ def build_deeplab(seed: int = 4321, num_classes: int = NUM_CLASSES, output_strid
     project = ini.conv(D, D * (2 + len(atrous)), 1, ACT_RELU)
     logits = ini.conv(num_classes, D, 1, ACT_NONE, bn=False, bias=True)
     logits.w = (ini.r.standard_normal(logits.w.shape) * np.sqrt(1.0 / D)).astype(np.float32)
-    return DeepLab(stem, blocks, pool, aspp0, atrous, project, logits, num_classes, output_stride, crop,
-                   meta=dict(seed=seed, atrous_rates=tuple(int(r) for r in atrous_rates), width=width))
+    return DeepLab(stem, blocks, pool, aspp0, atrous, project, logits, num_classes, output_stride, crop_h,
+                   meta=dict(seed=seed, atrous_rates=tuple(int(r) for r in atrous_rates), width=width),
+                   crop_w=crop_w if crop_w != crop_h else 0)
 
 
 def feature_size(net: DeepLab, n: int) -> int:
@@ -291,7 +300,7 @@ def lower(net: DeepLab, B: int, bf16: bool, fuse_dw: bool = False, nb=None, fuse
         info["flops"] += flops
         info["bytes"] += nbytes
 
-    Hc = Wc = net.crop
+    Hc, Wc = crop_hw(net)
     use(0, B * Hc * Wc * 8 * es)
     if not fuse_prep:
         op([OP_PREP, 0], "prep", 0, B * Hc * Wc * (3 + 8 * es))
@@ -431,6 +440,7 @@ def save(net: DeepLab, path) -> None:
     arrs["net.residual"] = np.array([int(b.residual) for b in net.blocks], np.int32)
     arrs["net.expand"] = np.array([int(b.expand is not None) for b in net.blocks], np.int32)
     arrs["net.attrs"] = np.array([net.num_classes, net.output_stride or 0, net.crop, len(net.atrous)], np.int32)
+    arrs["net.crop_w"] = np.array([net.crop_w or 0], np.int32)
     np.savez(path, **arrs)
 
 
@@ -452,4 +462,5 @@ def load(path) -> DeepLab:
     for i, (res, ex) in enumerate(zip(z["net.residual"], z["net.expand"])):
         blocks.append(Block(conv(f"b{i}.expand") if ex else None, conv(f"b{i}.dw"), conv(f"b{i}.project"), bool(res)))
     return DeepLab(conv("stem"), blocks, conv("pool"), conv("aspp0"), [conv(f"atrous{i}") for i in range(natr)],
-                   conv("project"), conv("logits"), ncls, os_ or None, crop)
+                   conv("project"), conv("logits"), ncls, os_ or None, crop,
+                   crop_w=int(z["net.crop_w"][0]) if "net.crop_w" in z else 0)

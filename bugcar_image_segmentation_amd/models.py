@@ -186,17 +186,22 @@ class DeepLabV3(InferenceModel):
 
     The reference feeds ``[img]`` to ``import/ImageTensor:0`` and returns
     ``import/SemanticPredictions:0`` (models.py:115-125): u8 RGB images in, int64 class ids out,
-    with padding to the 513 crop, normalisation, MobileNetV2 + ASPP, logits, bilinear resize and
+    with padding to the export's crop (513 in the model zoo), normalisation, MobileNetV2 + ASPP, logits, bilinear resize and
     argmax all inside the frozen graph. Here the same graph (deeplab_spec.py) runs as one op list of
     gfx950 kernels (libbugseg.so, bugseg_dl_*).
 
     Deviations, because the reference wrapper is broken as written:
-    ``predict`` takes the ImageTensor layout itself — (H, W, 3) or (B, H, W, 3) u8 RGB, H, W <= 513 —
-    instead of unpacking a 4-D NCHW shape and wrapping it in a list (models.py:116,124);
+    ``predict`` takes the ImageTensor layout itself — (H, W, 3) or (B, H, W, 3) u8 RGB, H, W at most
+    the crop — instead of unpacking a 4-D NCHW shape and wrapping it in a list (models.py:116,124);
     ``preprocess`` (whose reference body uses undefined ``cls.input_size`` / ``IMAGE_MEAN``,
     models.py:129,132) returns the RGB u8 frame resized so the longer side is at most the crop — the
     resize the DeepLab demo applies before feeding the graph. The node-name printing
     (models.py:112-113, 116, 121) is dropped.
+
+    The crop (height, width) is the export's own: read from the graph's pad-to-crop arithmetic by
+    deeplab_graphdef.import_deeplab (``CROP_SIZE`` only when a graph does not hold it). Images larger
+    than the crop are refused: the export sizes its image-pooling window and resize from the crop
+    (deeplab/model.py, ``crop_size`` given at export), so the graph itself cannot run them.
 
     Weights: GRAPH_PB_PATH may be a frozen TF DeepLab-MobileNetV2 GraphDef (``deeplab.pb``, read by
     deeplab_graphdef.import_deeplab; the file itself is absent, .MISSING_LARGE_BLOBS:1), a
@@ -232,7 +237,7 @@ class DeepLabV3(InferenceModel):
                     # a frozen TF DeepLab export (models.py:104-110 reads it as a GraphDef)
                     from .deeplab_graphdef import import_deeplab
                     with open(GRAPH_PB_PATH, "rb") as f:
-                        net = import_deeplab(f.read(), crop=self.CROP_SIZE)
+                        net = import_deeplab(f.read(), crop=None, default_crop=self.CROP_SIZE)
         self.net = net
         self.precision = precision
         self.ctx = N.DeepLabContext(device, N.BF16 if precision == "bf16" else N.FP32)
@@ -251,7 +256,7 @@ class DeepLabV3(InferenceModel):
         if self._blob is None:
             self.ctx.load_weights(blob)
             self._blob = blob
-        self.ctx.set_plan(ops, bufs, B, self.net.crop, self.net.crop)
+        self.ctx.set_plan(ops, bufs, B, *self._spec.crop_hw(self.net))
         self._plan_B = B
         self.plan_info = info
 
@@ -263,8 +268,10 @@ class DeepLabV3(InferenceModel):
         if x.dim() != 4 or x.shape[3] != 3:
             raise ValueError(f"expected u8 RGB images (B, H, W, 3), got {tuple(x.shape)}")
         B, H, W = x.shape[:3]
-        if H > self.net.crop or W > self.net.crop:
-            raise ValueError(f"image {H}x{W} exceeds the {self.net.crop} crop: resize it first (DeepLabV3.preprocess)")
+        Hc, Wc = self._spec.crop_hw(self.net)
+        if H > Hc or W > Wc:
+            raise ValueError(f"image {H}x{W} exceeds the export's {Hc}x{Wc} crop: resize it first "
+                             "(DeepLabV3.preprocess)")
         self._ensure_plan(B)
         if out is None:
             out = torch.empty((B, H, W), dtype=torch.int64, device=x.device)
@@ -286,7 +293,8 @@ class DeepLabV3(InferenceModel):
     @classmethod
     def preprocess(cls, bgr_frame) -> np.ndarray:
         """BGR u8 frame -> RGB u8 frame whose longer side is at most CROP_SIZE (nearest-pixel
-        downscale when larger; the reference body is broken, see the class docstring)."""
+        downscale when larger; the reference body is broken, see the class docstring). For an export
+        with another crop, set CROP_SIZE on the class (or resize to the model's net.crop)."""
         f = np.asarray(bgr_frame)
         if f.ndim != 3 or f.shape[2] != 3 or f.dtype != np.uint8:
             raise ValueError("expected a BGR uint8 frame (H, W, 3)")

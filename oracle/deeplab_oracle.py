@@ -27,11 +27,17 @@ import torch
 import torch.nn.functional as F
 
 
-def preprocess(rgb: np.ndarray, crop: int) -> np.ndarray:
-    """(B, H, W, 3) u8 -> (B, crop, crop, 3) f32."""
+def crop_hw(net):
+    """(crop height, crop width) of the export (a square crop stores only ``crop``)."""
+    return int(net.crop), int(getattr(net, "crop_w", 0) or net.crop)
+
+
+def preprocess(rgb: np.ndarray, crop) -> np.ndarray:
+    """(B, H, W, 3) u8 -> (B, crop_h, crop_w, 3) f32; ``crop`` an int or (height, width)."""
+    ch, cw = (crop, crop) if np.ndim(crop) == 0 else crop
     B, H, W, _ = rgb.shape
-    assert H <= crop and W <= crop
-    x = np.full((B, crop, crop, 3), 127.5, np.float32)
+    assert H <= ch and W <= cw
+    x = np.full((B, ch, cw, 3), 127.5, np.float32)
     x[:, :H, :W] = rgb.astype(np.float32)
     return (np.float32(2.0 / 255.0) * x - np.float32(1.0)).astype(np.float32)
 
@@ -89,7 +95,7 @@ def _conv(n: _Num, x, c, groups=1):
 def forward(net, rgb: np.ndarray, dtype=torch.float64, bf16_storage: bool = False) -> torch.Tensor:
     """(B, H, W, 3) u8 RGB -> logits (B, classes, h, w) at the backbone resolution, f32."""
     n = _Num(torch.float32 if bf16_storage else dtype, bf16_storage)
-    x = torch.from_numpy(preprocess(rgb, net.crop)).permute(0, 3, 1, 2).to(n.dtype)
+    x = torch.from_numpy(preprocess(rgb, crop_hw(net))).permute(0, 3, 1, 2).to(n.dtype)
     x = n.store(x)
     x = n.store(_conv(n, x, net.stem))
     for blk in net.blocks:
@@ -141,5 +147,5 @@ def predict(net, rgb: np.ndarray, logits: torch.Tensor | np.ndarray | None = Non
     if logits is None:
         logits = forward(net, rgb, **kw)
     L = np.asarray(logits.numpy() if isinstance(logits, torch.Tensor) else logits, np.float32)
-    up = resize_bilinear_tf(L, net.crop, net.crop)
+    up = resize_bilinear_tf(L, *crop_hw(net))
     return np.argmax(up, axis=1)[:, :H, :W].astype(np.int64)

@@ -231,7 +231,9 @@ def run(pb: bytes, feed: dict, fetch: str):
             out = args[0][tuple(slice(bi, None if si == -1 else bi + si) for bi, si in zip(b, sz))]
         elif op == "StridedSlice":
             b, e, st = ([int(v) for v in a] for a in args[1:4])
-            out = args[0][tuple(slice(bi, ei if ei != 0 else None, si) for bi, ei, si in zip(b, e, st))]
+            shrink = int(n.attr.get("shrink_axis_mask", 0) or 0)
+            out = args[0][tuple(bi if shrink >> i & 1 else slice(bi, ei if ei != 0 else None, si)
+                                for i, (bi, ei, si) in enumerate(zip(b, e, st)))]
         elif op == "ArgMax":
             out = np.argmax(args[0], axis=int(args[1]))
         elif op in ELEMENTWISE or op in ("Transpose", "Reshape", "ExpandDims", "Squeeze", "ConcatV2", "Pack",

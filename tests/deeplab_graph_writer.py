@@ -13,8 +13,11 @@ and to run the graph through the NumPy GraphDef interpreter (oracle/tf_graph.py)
 
 Both take ``ImageTensor`` (B, H, W, 3) u8 and end in ``SemanticPredictions`` (int64, (B, H, W)),
 the reference's tensor names without the ``import/`` scope (models.py:102-103,115-125), with the
-export's preprocessing (pad to the crop with 127.5, (2/255) x - 1) and bilinear resize
-(align_corners) + argmax written as graph ops. ``logits`` names the pre-resize logits tensor.
+export's preprocessing and bilinear resize (align_corners) + argmax written as graph ops. The pad is
+the export's dynamic form (deeplab/input_preprocess.py): per axis ``size + Maximum(Sub(crop, size), 0)``
+from ``Shape`` / ``StridedSlice`` of the image, pad value 127.5, then (2/255) x - 1; the final resize
+goes to that padded size. ``crop_in_graph=False`` writes the older static ``PadV2`` instead (no crop
+constants in the graph). ``logits`` names the pre-resize logits tensor.
 """
 from __future__ import annotations
 
@@ -27,16 +30,17 @@ I32 = ("type", 3)
 
 
 class DeepLabWriter:
-    def __init__(self, net: D.DeepLab, style: str, H: int, W: int, B: int = 1):
+    def __init__(self, net: D.DeepLab, style: str, H: int, W: int, B: int = 1, crop_in_graph: bool = True):
         assert style in ("slim", "folded")
         self.net, self.style, self.g = net, style, GraphBuilder()
         self.B, self.H, self.W = B, H, W
+        self.crop_in_graph = crop_in_graph
 
     def i32(self, v):
         return self.g.const(np.asarray(v, np.int32), np.int32)
 
-    def conv(self, x, c: D.Conv, n: int):
-        """-> (output tensor, spatial size)."""
+    def conv(self, x, c: D.Conv, n):
+        """n: input (height, width) -> (output tensor, output (height, width))."""
         g = self.g
         k, s, d = c.k, c.stride, c.dil
         w = np.asarray(c.w, np.float64)
@@ -51,17 +55,17 @@ class DeepLabWriter:
             filt = g.const(np.transpose(w, (2, 3, 1, 0)).astype(np.float32))      # HWIO
             op = "Conv2D"
         filt = g.node("Identity", [filt], T=F32)                                    # the frozen 'read' node
-        n_out = -(-n // s)
+        n_out = tuple(-(-v // s) for v in n)
         if self.style == "slim" and d > 1:
             # tf.nn.atrous_conv2d / with_space_to_batch: SAME base paddings + the extra making the padded
             # size a multiple of the rate, cropped again after the convolution
             tot = (k - 1) * d
             p0, p1 = tot // 2, tot - tot // 2
-            extra = (-(n + p0 + p1)) % d
-            x = g.node("SpaceToBatchND", [x, self.i32([d, d]), self.i32([[p0, p1 + extra], [p0, p1 + extra]])],
+            ex = [(-(v + p0 + p1)) % d for v in n]
+            x = g.node("SpaceToBatchND", [x, self.i32([d, d]), self.i32([[p0, p1 + ex[0]], [p0, p1 + ex[1]]])],
                        T=F32, Tblock_shape=I32, Tpaddings=I32)
             y = g.node(op, [x, filt], T=F32, strides=[1, 1, 1, 1], padding="VALID", data_format="NHWC")
-            y = g.node("BatchToSpaceND", [y, self.i32([d, d]), self.i32([[0, extra], [0, extra]])], T=F32,
+            y = g.node("BatchToSpaceND", [y, self.i32([d, d]), self.i32([[0, ex[0]], [0, ex[1]]])], T=F32,
                        Tblock_shape=I32, Tcrops=I32)
         else:
             y = g.node(op, [x, filt], T=F32, strides=[1, s, s, 1], padding="SAME", data_format="NHWC",
@@ -80,13 +84,38 @@ class DeepLabWriter:
             y = g.node("Relu", [y], T=F32)
         return y, n_out
 
+    def pad_to_crop(self, x):
+        """-> (padded image, padded (height, width) tensors): input_preprocess.py's dynamic pad."""
+        g = self.g
+        Ch, Cw = D.crop_hw(self.net)
+        shp = g.node("Shape", [x], T=F32, out_type=I32)
+        sizes = []
+        for axis, crop in ((1, Ch), (2, Cw)):
+            v = g.node("StridedSlice", [shp, self.i32([axis]), self.i32([axis + 1]), self.i32([1])], T=I32, Index=I32,
+                       shrink_axis_mask=1)
+            extra = g.node("Maximum", [g.node("Sub", [self.i32(crop), v], T=I32), self.i32(0)], T=I32)
+            sizes.append((v, extra, g.node("AddV2", [v, extra], T=I32)))
+        zero = self.i32(0)
+        pads = g.node("Pack", [g.node("Pack", [zero, zero], T=I32, N=2, axis=0),
+                               g.node("Pack", [zero, sizes[0][1]], T=I32, N=2, axis=0),
+                               g.node("Pack", [zero, sizes[1][1]], T=I32, N=2, axis=0),
+                               g.node("Pack", [zero, zero], T=I32, N=2, axis=0)], T=I32, N=4, axis=0)
+        x = g.node("PadV2", [x, pads, g.const(np.float32(127.5))], T=F32, Tpaddings=I32)
+        return x, g.node("Pack", [sizes[0][2], sizes[1][2]], T=I32, N=2, axis=0)
+
     def build(self) -> bytes:
         g, net = self.g, self.net
-        B, H, W, C = self.B, self.H, self.W, net.crop
+        B, H, W = self.B, self.H, self.W
+        C = D.crop_hw(net)
+        assert H <= C[0] and W <= C[1]
         x = g.node("Placeholder", [], name="ImageTensor", dtype=("type", 4), shape=("shape", [B, H, W, 3]))
         x = g.node("Cast", [x], SrcT=("type", 4), DstT=F32)
-        x = g.node("PadV2", [x, self.i32([[0, 0], [0, C - H], [0, C - W], [0, 0]]), g.const(np.float32(127.5))],
-                   T=F32, Tpaddings=I32)
+        if self.crop_in_graph:
+            x, out_size = self.pad_to_crop(x)
+        else:
+            x = g.node("PadV2", [x, self.i32([[0, 0], [0, C[0] - H], [0, C[1] - W], [0, 0]]),
+                                 g.const(np.float32(127.5))], T=F32, Tpaddings=I32)
+            out_size = self.i32(list(C))
         x = g.node("Mul", [x, g.const(np.float32(2.0 / 255.0))], T=F32)
         x = g.node("Sub", [x, g.const(np.float32(1.0))], T=F32)
         x, n = self.conv(x, net.stem, C)
@@ -102,10 +131,10 @@ class DeepLabWriter:
         if self.style == "slim":
             p = g.node("Mean", [feat, self.i32([1, 2])], T=F32, Tidx=I32, keep_dims=True)
         else:
-            p = g.node("AvgPool", [feat], T=F32, ksize=[1, n, n, 1], strides=[1, n, n, 1], padding="VALID",
-                       data_format="NHWC")
-        p, _ = self.conv(p, net.pool, 1)
-        p = g.node("ResizeBilinear", [p, self.i32([n, n])], T=F32, align_corners=True)
+            p = g.node("AvgPool", [feat], T=F32, ksize=[1, n[0], n[1], 1], strides=[1, n[0], n[1], 1],
+                       padding="VALID", data_format="NHWC")
+        p, _ = self.conv(p, net.pool, (1, 1))
+        p = g.node("ResizeBilinear", [p, self.i32(list(n))], T=F32, align_corners=True)
         a0, _ = self.conv(feat, net.aspp0, n)
         atr = [self.conv(feat, a, n)[0] for a in net.atrous]
         parts = [p, a0] + atr if self.style == "slim" else [a0] + atr + [p]
@@ -121,12 +150,12 @@ class DeepLabWriter:
         y, _ = self.conv(cat, proj, n)
         lg, _ = self.conv(y, net.logits, n)
         lg = g.node("Identity", [lg], name="logits", T=F32)
-        up = g.node("ResizeBilinear", [lg, self.i32([C, C])], T=F32, align_corners=True)
+        up = g.node("ResizeBilinear", [lg, out_size], T=F32, align_corners=True)
         am = g.node("ArgMax", [up, self.i32(3)], T=F32, Tidx=I32, output_type=("type", 9))
         sl = g.node("Slice", [am, self.i32([0, 0, 0]), self.i32([-1, H, W])], T=("type", 9), Index=I32)
         g.node("Identity", [sl], name="SemanticPredictions", T=("type", 9))
         return g.bytes()
 
 
-def write_deeplab_graph(net: D.DeepLab, style: str, H: int, W: int, B: int = 1) -> bytes:
-    return DeepLabWriter(net, style, H, W, B).build()
+def write_deeplab_graph(net: D.DeepLab, style: str, H: int, W: int, B: int = 1, crop_in_graph: bool = True) -> bytes:
+    return DeepLabWriter(net, style, H, W, B, crop_in_graph).build()

@@ -22,8 +22,8 @@ from oracle import tf_graph
 CROP = 65
 
 
-def _net(rates=(2, 4), os_=8, ncls=S.NUM_CLASSES):
-    return S.build_deeplab(width=0.25, crop=CROP, output_stride=os_, atrous_rates=rates, num_classes=ncls)
+def _net(rates=(2, 4), os_=8, ncls=S.NUM_CLASSES, crop=CROP):
+    return S.build_deeplab(width=0.25, crop=crop, output_stride=os_, atrous_rates=rates, num_classes=ncls)
 
 
 def _same_weights(a: S.DeepLab, b: S.DeepLab):
@@ -37,7 +37,7 @@ def _same_weights(a: S.DeepLab, b: S.DeepLab):
         np.testing.assert_allclose(wy, wx, rtol=1e-5, atol=1e-6, err_msg=name)
         np.testing.assert_allclose(by, bx, rtol=1e-5, atol=1e-6, err_msg=name)
     assert [blk.residual for blk in a.blocks] == [blk.residual for blk in b.blocks]
-    assert (a.num_classes, a.crop) == (b.num_classes, b.crop)
+    assert (a.num_classes, S.crop_hw(a)) == (b.num_classes, S.crop_hw(b))
 
 
 @pytest.mark.parametrize("style", ["slim", "folded"])
@@ -53,9 +53,9 @@ def test_import_recovers_the_network(style, rates, os_):
     np.testing.assert_allclose(O.forward(got, x).numpy(), O.forward(net, x).numpy(), atol=1e-4)
 
 
-@pytest.mark.parametrize("style", ["slim", "folded"])
-def test_interpreter_runs_the_written_graph_like_the_oracle(style):
-    net = _net((2,), 8, ncls=5)
+@pytest.mark.parametrize("style,crop", [("slim", CROP), ("folded", CROP), ("slim", (57, 81))])
+def test_interpreter_runs_the_written_graph_like_the_oracle(style, crop):
+    net = _net((2,), 8, ncls=5, crop=crop)
     H, W = 57, 64
     pb = write_deeplab_graph(net, style, H, W, B=1)
     x = np.random.default_rng(4).integers(0, 256, (1, H, W, 3), dtype=np.uint8)
@@ -64,7 +64,7 @@ def test_interpreter_runs_the_written_graph_like_the_oracle(style):
     np.testing.assert_allclose(np.transpose(lg, (0, 3, 1, 2)), ref, atol=1e-4)
     cls = tf_graph.run(pb, {"ImageTensor": x}, "SemanticPredictions")
     want = O.predict(net, x, logits=ref.astype(np.float32))
-    up = O.resize_bilinear_tf(ref.astype(np.float32), CROP, CROP)[:, :, :H, :W]
+    up = O.resize_bilinear_tf(ref.astype(np.float32), *S.crop_hw(net))[:, :, :H, :W]
     s = np.sort(up, axis=1)
     decided = (s[:, -1] - s[:, -2]) > 1e-4
     assert cls.shape == (1, H, W)
@@ -72,10 +72,29 @@ def test_interpreter_runs_the_written_graph_like_the_oracle(style):
     assert decided.mean() > 0.99
 
 
+@pytest.mark.parametrize("crop", [CROP, (57, 81), (97, 41)])
+def test_crop_is_read_from_the_graph(crop):
+    """The export's pad-to-crop arithmetic (Maximum(Sub(crop, size), 0) per axis) gives the crop; an
+    explicit crop overrides it; a graph without it (static PadV2) falls back to default_crop."""
+    net = _net((2,), 8, crop=crop)
+    pb = write_deeplab_graph(net, "slim", 33, 40)
+    got = import_deeplab(pb)
+    assert S.crop_hw(got) == S.crop_hw(net)
+    _same_weights(net, got)
+    assert S.crop_hw(import_deeplab(pb, crop=(129, 161))) == (129, 161)
+    static = write_deeplab_graph(net, "folded", 33, 40, crop_in_graph=False)
+    assert S.crop_hw(import_deeplab(static, default_crop=77)) == (77, 77)
+    assert S.crop_hw(import_deeplab(static)) == (S.CROP, S.CROP)
+
+
 def test_npz_round_trip(tmp_path):
     net = _net()
     p = tmp_path / "dl.npz"
     got = graphdef_to_npz(write_deeplab_graph(net, "slim", 65, 65), p, crop=CROP)
+    _same_weights(got, S.load(p))
+    net = _net(crop=(65, 97))
+    got = graphdef_to_npz(write_deeplab_graph(net, "slim", 65, 65), p)
+    assert S.crop_hw(S.load(p)) == (65, 97)
     _same_weights(got, S.load(p))
 
 

@@ -114,3 +114,25 @@ def test_plugin_preprocess_rgb_and_resize():
     assert np.array_equal(DeepLabV3.preprocess(small), small[:, :, ::-1])
     with pytest.raises(ValueError):
         DeepLabV3.preprocess(f[:, :, :2])
+
+
+def test_non_square_crop_lowering_and_weight_file(tmp_path):
+    """An export with crop_size (h, w), h != w: the plan pads to h x w (stem input and the final
+    resize), feature size per axis; the .npz keeps the width; the oracle pads and resizes to it."""
+    net = S.build_deeplab(width=0.25, crop=(65, 97))
+    assert S.crop_hw(net) == (65, 97)
+    _, ops, bufs, info = S.lower(net, 2, bf16=False)
+    assert tuple(ops[0, 4:6]) == (65, 97)                  # stem input H, W = the crop
+    assert info["feature"] == (S.feature_size(net, 65), S.feature_size(net, 97))
+    p = tmp_path / "dl.npz"
+    S.save(net, p)
+    assert S.crop_hw(S.load(p)) == (65, 97)
+    sq = S.build_deeplab(width=0.25, crop=65)
+    S.save(sq, p)
+    assert S.crop_hw(S.load(p)) == (65, 65) and S.load(p).crop_w == 0
+    x = np.random.default_rng(4).integers(0, 256, (1, 50, 90, 3), dtype=np.uint8)
+    pre = O.preprocess(x, S.crop_hw(net))
+    assert pre.shape == (1, 65, 97, 3) and np.all(pre[:, 50:] == np.float32(2 / 255) * np.float32(127.5) - 1)
+    lg = O.forward(net, x)
+    assert tuple(lg.shape[2:]) == info["feature"]
+    assert O.predict(net, x, logits=lg).shape == (1, 50, 90)

@@ -39,7 +39,7 @@ def _check_fp32(model, net, x, ref_dtype):
     # resize + argmax kernel: bit-exact on the GPU's own logits
     assert np.array_equal(got_cls, O.predict(net, x, logits=got))
     # class maps vs the oracle wherever its margin decides them
-    up = O.resize_bilinear_tf(ref, net.crop, net.crop)[:, :, :x.shape[1], :x.shape[2]]
+    up = O.resize_bilinear_tf(ref, *S.crop_hw(net))[:, :, :x.shape[1], :x.shape[2]]
     s = np.sort(up, axis=1)
     decided = (s[:, -1] - s[:, -2]) > MARGIN
     ref_cls = O.predict(net, x, logits=ref)
@@ -53,6 +53,18 @@ def test_deeplab_fp32_small(gpu, B, H, W, os_, rates):
     net = S.build_deeplab(width=0.25, crop=97, output_stride=os_, atrous_rates=rates)
     model = DeepLabV3(net=net, precision="fp32")
     _check_fp32(model, net, _frames(B, H, W, B * 7 + H), torch.float64)
+
+
+@pytest.mark.parametrize("crop,B,H,W", [((65, 113), 2, 60, 113), ((121, 49), 1, 100, 49)])
+def test_deeplab_fp32_non_square_crop(gpu, crop, B, H, W):
+    """An export whose crop_size is not square (pad to crop_h x crop_w, resize back to it)."""
+    net = S.build_deeplab(width=0.25, crop=crop, atrous_rates=(2,))
+    model = DeepLabV3(net=net, precision="fp32")
+    _check_fp32(model, net, _frames(B, H, W, 5 + H), torch.float64)
+    with pytest.raises(ValueError):
+        model.predict(_frames(1, crop[0] + 1, 8, 0))
+    with pytest.raises(ValueError):
+        model.predict(_frames(1, 8, crop[1] + 1, 0))
 
 
 def test_deeplab_fp32_many_classes(gpu):
@@ -133,18 +145,19 @@ def test_deeplab_fused_prep_bit_identical(gpu, precision):
         assert np.array_equal(a, b)
 
 
-@pytest.mark.parametrize("style", ["slim", "folded"])
-def test_deeplab_from_frozen_graphdef(gpu, tmp_path, style):
+@pytest.mark.parametrize("style,crop", [("slim", S.CROP), ("folded", S.CROP), ("slim", (129, 193))])
+def test_deeplab_from_frozen_graphdef(gpu, tmp_path, style, crop):
     """DeepLabV3(GRAPH_PB_PATH=<frozen GraphDef>) (models.py:104-110): the imported network on the GPU
-    against the NumPy GraphDef interpreter's logits (the sess.run stand-in) and the oracle."""
+    against the NumPy GraphDef interpreter's logits (the sess.run stand-in) and the oracle; the crop
+    comes from the graph (an export at another crop than 513 runs at its own)."""
     from deeplab_graph_writer import write_deeplab_graph
     from oracle import tf_graph
-    net = S.build_deeplab(width=0.25, crop=S.CROP, atrous_rates=(2, 4))
+    net = S.build_deeplab(width=0.25, crop=crop, atrous_rates=(2, 4))
     H, W = 120, 97
     pb = tmp_path / "deeplab.pb"
     pb.write_bytes(write_deeplab_graph(net, style, H, W))
     model = DeepLabV3(str(pb), precision="fp32")
-    assert model.net.crop == S.CROP and len(model.net.atrous) == 2
+    assert S.crop_hw(model.net) == S.crop_hw(net) and len(model.net.atrous) == 2
     x = _frames(1, H, W, 11)
     _check_fp32(model, model.net, x, torch.float32)
     lg = np.transpose(tf_graph.run(pb.read_bytes(), {"ImageTensor": x}, "logits"), (0, 3, 1, 2))
