@@ -53,6 +53,21 @@ struct DlDwArgs {
     void *out;           // (B, Hout, Wout, C) T
     uint32_t mHW, mW; int sHW, sW;
     uint32_t in_bytes;
+    int act;             // 0 none, 1 ReLU, 2 ReLU6 (MobileNetV2: 2; Xception's pre-activation modules: 0)
+    int in_relu;         // ReLU applied to the input as it is loaded (Xception: activation before the
+                         // separable conv, the un-rectified tensor still feeding the module's skip)
+};
+
+// Bilinear resize, align_corners (TF1 ResizeBilinear, the formula of the argmax stage) of a T tensor
+// into channels [out_off, out_off + C) of another: the DeepLabV3+ decoder's upsampling of the ASPP
+// output to the low-level feature size before the concat.
+struct DlResizeArgs {
+    const void *in;      // (B, h, w, in_cs) T, channels [0, C) used
+    int B, h, w, in_cs, C;
+    float sy, sx;        // (h - 1) / (Ho - 1), (w - 1) / (Wo - 1) in f32
+    int Ho, Wo;
+    void *out;           // (B, Ho, Wo, out_cs) T
+    int out_cs, out_off;
 };
 
 struct DlPoolArgs {
@@ -82,5 +97,6 @@ hipError_t dl_launch_conv(int prec, bool out_f32, const DlConvArgs &a, hipStream
 hipError_t dl_launch_dw(int prec, const DlDwArgs &a, hipStream_t s);
 hipError_t dl_launch_pool(int prec, const DlPoolArgs &a, hipStream_t s);
 hipError_t dl_launch_argmax(const DlArgmaxArgs &a, hipStream_t s);
+hipError_t dl_launch_resize(int prec, const DlResizeArgs &a, hipStream_t s);
 
 }  // namespace bugseg

@@ -480,6 +480,9 @@ __device__ __forceinline__ void ld8f(const float *p, float4 &a, float4 &b) {
 // loaded (and unpacked) once: 12 or 15 activation loads instead of 18. FMAs go two channels per
 // v_pk_fma_f32 (each lane an IEEE fma, so the sums equal the scalar fmaf chain bit for bit).
 typedef float f32x2_t __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ float4 relu4(float4 v) {
+    return make_float4(fmaxf(v.x, 0.f), fmaxf(v.y, 0.f), fmaxf(v.z, 0.f), fmaxf(v.w, 0.f));
+}
 
 template <typename T, bool S1, int R>
 __global__ void __launch_bounds__(256) dl_dw_kernel(const DlDwArgs a) {
@@ -539,12 +542,14 @@ __global__ void __launch_bounds__(256) dl_dw_kernel(const DlDwArgs a) {
 #pragma unroll
         for (int j = 0; j < R; ++j) {
             raw4(xr[ky + j * RB][kx], x0, x1);
+            if (a.in_relu) { x0 = relu4(x0); x1 = relu4(x1); }   // padding taps are 0 either way
             fma8(acc[j], x0, x1, w0, w1);
         }
     }
     float4 b0, b1;
     ld8f(reinterpret_cast<const float *>(a.bias) + g * 8, b0, b1);
-    auto r6 = [](float v) { return fminf(fmaxf(v, 0.f), 6.f); };
+    const int act = a.act;
+    auto r6 = [act](float v) { return act == 2 ? fminf(fmaxf(v, 0.f), 6.f) : act == 1 ? fmaxf(v, 0.f) : v; };
     T *o = reinterpret_cast<T *>(a.out) + (size_t)b * a.Hout * a.Wout * a.C + g * 8;
 #pragma unroll
     for (int j = 0; j < R; ++j) {
@@ -757,6 +762,43 @@ __global__ void __launch_bounds__(256) dl_resize_argmax_generic(const DlArgmaxAr
     a.out[((size_t)b * a.Hout + y) * a.Wout + x] = (int64_t)bi;
 }
 
+// Feature resize for the decoder: one thread = 8 channels of one output pixel; the four corner
+// vectors are 16-B (bf16) / 2 x 16-B (f32) loads; contraction off so the lerps round as TF's do.
+template <typename T>
+__global__ void __launch_bounds__(256) dl_resize_kernel(const DlResizeArgs a) {
+#pragma clang fp contract(off)
+    const int groups = a.C >> 3;
+    const int i = blockIdx.x * 256 + threadIdx.x;
+    if (i >= a.B * a.Ho * a.Wo * groups) return;
+    const int g = i % groups, q = i / groups;
+    const int x = q % a.Wo, t = q / a.Wo, y = t % a.Ho, b = t / a.Ho;
+    const float in_y = (float)y * a.sy, in_x = (float)x * a.sx;
+    const int y0 = (int)floorf(in_y), x0 = (int)floorf(in_x);
+    const int y1 = min(y0 + 1, a.h - 1), x1 = min(x0 + 1, a.w - 1);
+    const float ly = in_y - (float)y0, lx = in_x - (float)x0;
+    const T *base = reinterpret_cast<const T *>(a.in) + (size_t)b * a.h * a.w * a.in_cs + g * 8;
+    using Raw = typename Tr<T>::Raw;
+    Raw r[4];
+    ld8(r[0], base + ((size_t)y0 * a.w + x0) * a.in_cs);
+    ld8(r[1], base + ((size_t)y0 * a.w + x1) * a.in_cs);
+    ld8(r[2], base + ((size_t)y1 * a.w + x0) * a.in_cs);
+    ld8(r[3], base + ((size_t)y1 * a.w + x1) * a.in_cs);
+    float4 v[4][2];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) raw4(r[k], v[k][0], v[k][1]);
+    float o[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+        const float tl = get(v[0][j >> 2], j & 3), tr = get(v[1][j >> 2], j & 3);
+        const float bl = get(v[2][j >> 2], j & 3), br = get(v[3][j >> 2], j & 3);
+        const float top = tl + (tr - tl) * lx;
+        const float bot = bl + (br - bl) * lx;
+        o[j] = top + (bot - top) * ly;
+    }
+    T *op = reinterpret_cast<T *>(a.out) + (((size_t)b * a.Ho + y) * a.Wo + x) * a.out_cs + a.out_off + g * 8;
+    st4(op, make_float4(o[0], o[1], o[2], o[3]));
+    st4(op + 4, make_float4(o[4], o[5], o[6], o[7]));
+}
 
 // ------------------------------------------------------------------ launchers
 hipError_t dl_launch_prep(int prec, const DlPrepArgs &a, hipStream_t s) {
@@ -866,6 +908,14 @@ hipError_t dl_launch_pool(int prec, const DlPoolArgs &a, hipStream_t s) {
         hipLaunchKernelGGL((dl_pool_gemv_kernel<float, 0>), dim3((a.B * a.cmid + 3) / 4), dim3(256), 0, s, a);
         hipLaunchKernelGGL((dl_pool_gemv_kernel<float, 1>), dim3((a.B * a.cout + 3) / 4), dim3(256), 0, s, a);
     }
+    return hipGetLastError();
+}
+
+hipError_t dl_launch_resize(int prec, const DlResizeArgs &a, hipStream_t s) {
+    if ((a.C & 7) || (a.in_cs & 7) || (a.out_cs & 7) || (a.out_off & 7)) return hipErrorInvalidValue;
+    const int n = a.B * a.Ho * a.Wo * (a.C >> 3);
+    if (prec == PREC_BF16) hipLaunchKernelGGL(dl_resize_kernel<__bf16>, dim3((n + 255) / 256), dim3(256), 0, s, a);
+    else hipLaunchKernelGGL(dl_resize_kernel<float>, dim3((n + 255) / 256), dim3(256), 0, s, a);
     return hipGetLastError();
 }
 

@@ -4,7 +4,7 @@
 // the kernels into one blob, and lowers the network to a flat op list with buffer ids for a batch
 // size. This executor owns the device copies (weights, one activation arena per plan), validates
 // every op's shapes against its buffers before anything is launched, and enqueues the launches on
-// the caller's stream. It knows nothing about MobileNetV2 or ASPP beyond the op kinds.
+// the caller's stream. It knows nothing about MobileNetV2, Xception or ASPP beyond the op kinds.
 #include <hip/hip_runtime.h>
 
 #include <cstring>
@@ -21,7 +21,7 @@ namespace {
 
 thread_local std::string g_dl_err;
 
-enum { OP_PREP = 1, OP_CONV = 2, OP_DW = 3, OP_POOL = 4, OP_ARGMAX = 5 };
+enum { OP_PREP = 1, OP_CONV = 2, OP_DW = 3, OP_POOL = 4, OP_ARGMAX = 5, OP_RESIZE = 6 };
 
 struct DlOp {
     int f[BUGSEG_DL_OP_FIELDS];
@@ -130,6 +130,8 @@ bool check_op(const bugseg_dl *c, const DlOp &o, std::string &why) {
             !in_range(C, 8, CH) || !in_range(f[8], 1, 255) || !in_range(f[9], 1, 255) || !in_range(f[10], 0, 255) ||
             !in_range(f[11], 0, 255) || (double)B * Hout * Wout >= 2147483648.0) { why = "dw: field out of range"; return false; }
         if (C < 8 || C % 8 || Hin < 1 || Win < 1 || Hout < 1 || Wout < 1 || f[8] < 1 || f[9] < 1) { why = "dw: bad shape"; return false; }
+        if (!in_range(f[14], 0, 2) || !in_range(f[15], 0, 1)) { why = "dw: bad activation flags"; return false; }
+        if (f[8] != 1 && (f[8] != 2 || f[9] != 1)) { why = "dw: stride 2 with dilation (TF has no strided atrous)"; return false; }
         if (!buf_ok(c, src, (double)B * Hin * Win * C * es) || !buf_ok(c, dst, (double)B * Hout * Wout * C * es)) { why = "dw: buffer too small"; return false; }
         if ((double)B * Hin * Win * C * es >= 2147483648.0) { why = "dw: input exceeds 31-bit offsets"; return false; }
         if (!in_w(c, w_off, 9L * C * (long)es) || !in_w(c, b_off, (long)C * 4) || w_off % 16 || b_off % 16) { why = "dw: weights out of the blob"; return false; }
@@ -139,7 +141,7 @@ bool check_op(const bugseg_dl *c, const DlOp &o, std::string &why) {
         const int src = f[1], part = f[2], z = f[3], H = f[4], W = f[5], C = f[6], CS = f[7], chunk = f[8], nch = f[9];
         const int cmid = f[10], cout = f[11], zs = f[16];
         if (!in_range(H, 1, SP) || !in_range(W, 1, SP) || !in_range(CS, 1, CH)) { why = "pool: field out of range"; return false; }
-        if (C < 1 || C > 1024 || CS < C || cmid < 1 || cmid > 1024 || cout < 1 || zs < cout || chunk < 1 || nch < 1 ||
+        if (C < 1 || C > 2048 || C % 8 || CS < C || cmid < 1 || cmid > 1024 || cout < 1 || zs < cout || chunk < 1 || nch < 1 ||
             (long)chunk * nch < (long)H * W) { why = "pool: bad shape"; return false; }
         if (!buf_ok(c, src, (double)B * H * W * CS * es) || !buf_ok(c, part, (double)B * nch * C * 4.0) ||
             !buf_ok(c, z, (double)B * zs * 4.0) || !buf_ok(c, f[17], (double)B * cmid * 4.0)) { why = "pool: buffer too small"; return false; }
@@ -152,6 +154,18 @@ bool check_op(const bugseg_dl *c, const DlOp &o, std::string &why) {
         if (!in_range(h, 1, SP) || !in_range(w, 1, SP) || !in_range(LCS, 1, CH)) { why = "argmax: field out of range"; return false; }
         if (h < 1 || w < 1 || ncls < 1 || LCS < ncls || LCS % 4) { why = "argmax: bad shape"; return false; }
         if (!buf_ok(c, lg, (double)B * h * w * LCS * 4.0)) { why = "argmax: logits buffer too small"; return false; }
+        return true;
+    }
+    case OP_RESIZE: {
+        const int src = f[1], dst = f[2], h = f[3], w = f[4], in_cs = f[5], C = f[6], Ho = f[7], Wo = f[8];
+        const int out_cs = f[9], out_off = f[10];
+        if (!in_range(h, 1, SP) || !in_range(w, 1, SP) || !in_range(Ho, 1, SP) || !in_range(Wo, 1, SP) ||
+            !in_range(in_cs, 8, CH) || !in_range(C, 8, CH) || !in_range(out_cs, 8, CH) || !in_range(out_off, 0, CH) ||
+            (double)B * Ho * Wo * out_cs >= 2147483648.0) { why = "resize: field out of range"; return false; }
+        if (C % 8 || in_cs % 8 || out_cs % 8 || out_off % 8 || C > in_cs || out_off + C > out_cs) { why = "resize: bad shape"; return false; }
+        if (!buf_ok(c, src, (double)B * h * w * in_cs * es) || !buf_ok(c, dst, (double)B * Ho * Wo * out_cs * es)) {
+            why = "resize: buffer too small"; return false;
+        }
         return true;
     }
     default:
@@ -206,9 +220,19 @@ hipError_t run_op(bugseg_dl *c, const DlOp &o, const uint8_t *rgb, int H, int W,
         a.w = wb + f[12];
         a.in_bytes = (uint32_t)((size_t)B * a.Hin * a.Win * a.C * (c->prec == PREC_BF16 ? 2 : 4));
         a.bias = reinterpret_cast<const float *>(wb + f[13]);
+        a.act = f[14]; a.in_relu = f[15];
         fastdiv((uint32_t)(a.Hout * a.Wout), a.mHW, a.sHW);
         fastdiv((uint32_t)a.Wout, a.mW, a.sW);
         return dl_launch_dw(c->prec, a, s);
+    }
+    case OP_RESIZE: {
+        DlResizeArgs a{};
+        a.in = bufp(c, f[1]); a.out = bufp(c, f[2]);
+        a.B = B; a.h = f[3]; a.w = f[4]; a.in_cs = f[5]; a.C = f[6]; a.Ho = f[7]; a.Wo = f[8];
+        a.out_cs = f[9]; a.out_off = f[10];
+        a.sy = a.Ho > 1 ? (float)(a.h - 1) / (float)(a.Ho - 1) : 0.f;
+        a.sx = a.Wo > 1 ? (float)(a.w - 1) / (float)(a.Wo - 1) : 0.f;
+        return dl_launch_resize(c->prec, a, s);
     }
     case OP_POOL: {
         DlPoolArgs a{};

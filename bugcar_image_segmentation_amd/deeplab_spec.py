@@ -27,9 +27,10 @@ Op list (``lower``): int32 records of ``OP_FIELDS`` fields, interpreted by deepl
   PREP   [1, dst]
   CONV   [2, src, dst, res, Hin, Win, CS, Hout, Wout, kh, kw, stride, dil, pad_t, pad_l, cinP, NP,
           w_off, b_off, act, res_cs, out_cs, out_off, cout, out_f32, bias_img_buf, bias_img_stride]
-  DW     [3, src, dst, Hin, Win, C, Hout, Wout, stride, dil, pad_t, pad_l, w_off, b_off]
+  DW     [3, src, dst, Hin, Win, C, Hout, Wout, stride, dil, pad_t, pad_l, w_off, b_off, act, in_relu]
   POOL   [4, src, part, z, H, W, C, CS, chunk_px, nchunks, cmid, cout, wp_off, bp_off, wq_off, bq_off, z_stride, y]
   ARGMAX [5, logits, h, w, LCS, ncls]
+  RESIZE [6, src, dst, h, w, in_cs, C, Hout, Wout, out_cs, out_off]   (bilinear, align_corners; DeepLabV3+ decoder)
 """
 from __future__ import annotations
 
@@ -40,7 +41,7 @@ import numpy as np
 import torch
 
 OP_FIELDS = 32
-OP_PREP, OP_CONV, OP_DW, OP_POOL, OP_ARGMAX = 1, 2, 3, 4, 5
+OP_PREP, OP_CONV, OP_DW, OP_POOL, OP_ARGMAX, OP_RESIZE = 1, 2, 3, 4, 5, 6
 ACT_NONE, ACT_RELU, ACT_RELU6 = 0, 1, 2
 BN_EPS = 1e-3
 CROP = 513
@@ -271,7 +272,124 @@ def _pick_nb(tag: str, hw: int, K: int, cout: int, B: int = 16) -> int:
     return 4 if K >= 192 and cout >= 64 else 2
 
 
-def lower(net: DeepLab, B: int, bf16: bool, fuse_dw: bool = False, nb=None, fuse_prep: bool = True):
+class Lowering:
+    """Op-list builder shared by the backbones (lower, deeplab_xception.lower_xception): the weight
+    blob, the op records, each buffer's size and the per-op (tag, flops, bytes) accounting."""
+
+    def __init__(self, B: int, bf16: bool, nbufs: int, nb=None):
+        self.B, self.bf16, self.es, self.nb = B, bf16, (2 if bf16 else 4), nb
+        self.blob = _Blob(bf16)
+        self.ops = []
+        self.need = [256] * nbufs
+        self.info = dict(flops=0.0, bytes=0.0, per_op=[])
+
+    def use(self, buf, nbytes):
+        self.need[buf] = max(self.need[buf], int(nbytes))
+
+    def op(self, rec, tag, flops, nbytes):
+        self.ops.append(list(rec) + [0] * (OP_FIELDS - len(rec)))
+        self.info["per_op"].append((tag, float(flops), float(nbytes)))
+        self.info["flops"] += flops
+        self.info["bytes"] += nbytes
+
+    def conv(self, c: Conv, src, H, W, CS, dst, out_cs, out_off=0, res=-1, out_f32=False, bias_img=-1,
+             bias_img_stride=0, zero_bias=False, cout=None, tag="conv", dwf=None, rgb=False, geom=None):
+        """-> (Hout, Wout). rgb: the input is the raw u8 RGB frame batch, padded and normalised on load
+        (the stem with fuse_prep; tap field 2). geom: (Hout, pad_t, Wout, pad_l) instead of SAME."""
+        B, es, blob = self.B, self.es, self.blob
+        k = c.k
+        if geom is None:
+            Ho, pt = same_pad(H, k, c.stride, c.dil)
+            Wo, pl = same_pad(W, k, c.stride, c.dil)
+        else:
+            Ho, pt, Wo, pl = geom
+        extra = [-1, -1, 0]
+        Hin, Win = H, W
+        if dwf is not None:   # (dw conv, its input H, W): this 1x1 runs over the dw output grid
+            d, Hin, Win = dwf
+            Ho, dpt = same_pad(Hin, 3, d.stride, d.dil)
+            Wo, dpl = same_pad(Win, 3, d.stride, d.dil)
+            wd, bd = d.folded()
+            extra = [blob.add(wd.reshape(CS, 9).T, True), blob.add(bd.astype(np.float32), False),
+                     d.stride | d.dil << 8 | dpt << 16 | dpl << 24]
+        tp = CS == 8 and dwf is None and k > 1
+        wp, bias, cinP, NP = pack_conv(c, CS, self.bf16, tap_packed=tp)
+        if zero_bias:
+            bias = np.zeros_like(bias)
+        w_off = blob.add(wp, True)
+        b_off = blob.add(bias, False)
+        cw = c.cout if cout is None else cout
+        oes = 4 if out_f32 else es
+        self.use(dst, B * Ho * Wo * out_cs * oes)
+        cin = c.w.shape[1]
+        flops = 2.0 * B * Ho * Wo * c.cout * cin * k * k + (2.0 * B * Ho * Wo * CS * 9 if dwf else 0)
+        nbytes = (B * Hin * Win * 3 if rgb else B * Hin * Win * CS * es) + B * Ho * Wo * cw * oes + \
+            (B * Ho * Wo * cw * es if res >= 0 else 0) + wp.size * es
+        t = tag if dwf is None else "conv dw+project"
+        nb = self.nb
+        f30 = nb(t, Ho * Wo, cinP * k * k, cw) if callable(nb) else (nb or _pick_nb(t, Ho * Wo, cinP * k * k, cw, B))
+        self.op([OP_CONV, src, dst, res, Hin, Win, CS, Ho, Wo, k, k, c.stride, c.dil, pt, pl, cinP, NP, w_off, b_off,
+                 c.act, out_cs if res >= 0 else 0, out_cs, out_off, cw, int(out_f32), bias_img, bias_img_stride] +
+                extra + [f30, 2 if (rgb and tp) else int(tp)], t, flops, nbytes)
+        return Ho, Wo
+
+    def dw(self, d: Conv, src, dst, H, W, C, in_relu=False, geom=None, tag="dw"):
+        """3x3 depthwise (+ folded BN, activation d.act; in_relu: ReLU on the loaded input) -> (Hout, Wout)."""
+        B, es = self.B, self.es
+        if geom is None:
+            Ho, pt = same_pad(H, 3, d.stride, d.dil)
+            Wo, pl = same_pad(W, 3, d.stride, d.dil)
+        else:
+            Ho, pt, Wo, pl = geom
+        wd, bd = d.folded()
+        w_off = self.blob.add(wd.reshape(C, 9).T, True)   # [9][C] in the compute type
+        b_off = self.blob.add(bd.astype(np.float32), False)
+        self.use(dst, B * Ho * Wo * C * es)
+        self.op([OP_DW, src, dst, H, W, C, Ho, Wo, d.stride, d.dil, pt, pl, w_off, b_off, d.act, int(in_relu)], tag,
+                2.0 * B * Ho * Wo * C * 9, B * (H * W + Ho * Wo) * C * es)
+        return Ho, Wo
+
+    def aspp_pool(self, net, src, h, w, C, part=8, z=9, y=10):
+        """Image pooling folded into the projection as a per-image bias (buffers part, z, y) -> z stride."""
+        B, es = self.B, self.es
+        D = net.aspp0.cout
+        chunk = 64
+        nch = -(-(h * w) // chunk)
+        self.use(part, B * nch * C * 4)
+        zs = _r(D, 64)
+        self.use(z, B * zs * 4)
+        wpool, bpool = net.pool.folded()
+        wproj, bproj = net.project.folded()
+        self.use(y, B * D * 4)
+        wp_off = self.blob.add(_round(wpool.reshape(D, C), self.bf16), False)             # [D][C]
+        bp_off = self.blob.add(bpool.astype(np.float32), False)
+        wq_off = self.blob.add(_round(wproj.reshape(D, -1)[:, :D], self.bf16), False)     # [D (out)][D (pooled ch)]
+        bq_off = self.blob.add(bproj.astype(np.float32), False)
+        self.op([OP_POOL, src, part, z, h, w, C, C, chunk, nch, D, D, wp_off, bp_off, wq_off, bq_off, zs, y], "pool",
+                2.0 * B * (D * C + D * D) + B * h * w * C, B * h * w * C * es)
+        return zs
+
+    def projection_conv(self, net):
+        """The ASPP projection over the concat minus its pooled part (that part arrives as the per-image bias)."""
+        D = net.aspp0.cout
+        return Conv(w=net.project.w[:, D:], gamma=net.project.gamma, beta=net.project.beta, mean=net.project.mean,
+                    var=net.project.var, eps=net.project.eps, act=net.project.act)
+
+    def resize(self, src, dst, h, w, in_cs, C, Ho, Wo, out_cs, out_off):
+        es = self.es
+        self.use(dst, self.B * Ho * Wo * out_cs * es)
+        self.op([OP_RESIZE, src, dst, h, w, in_cs, C, Ho, Wo, out_cs, out_off], "resize", 8.0 * self.B * Ho * Wo * C,
+                self.B * (h * w + Ho * Wo) * C * es)
+
+    def argmax(self, logits, h, w, LCS, ncls, Hc, Wc):
+        self.op([OP_ARGMAX, logits, h, w, LCS, ncls], "argmax", 0, self.B * (h * w * LCS * 4 + Hc * Wc * 8))
+
+    def result(self):
+        self.info["nops"] = len(self.ops)
+        return self.blob.bytes(), np.asarray(self.ops, np.int32), np.asarray(self.need, np.uint64), self.info
+
+
+def lower(net, B: int, bf16: bool, fuse_dw: bool = False, nb=None, fuse_prep: bool = True):
     """-> (weight blob bytes, ops int32 (nops, OP_FIELDS), buffer bytes uint64 (nbufs,), info dict).
     Buffers: 0 input, 1/2 block ping-pong, 3 expanded, 4 depthwise out, 5 ASPP concat, 6 projection,
     7 logits (f32), 8 pooling partials (f32), 9 per-image projection bias (f32), 10 image-pooling
@@ -283,68 +401,22 @@ def lower(net: DeepLab, B: int, bf16: bool, fuse_dw: bool = False, nb=None, fuse
     stem's tap packing, 4 taps x 8 channels per k-step); bit-identical to
     the default plan (separate DW ops through buffer 4) but measured 2.4x slower (5.1 vs 2.2 ms per
     16-frame forward for the pair): the 9 tap loads of every operand chunk serialise ahead of the
-    MFMAs and are recomputed for every 64-channel output tile."""
-    es = 2 if bf16 else 4
-    blob = _Blob(bf16)
-    ops = []
-    need = [256] * 11
-    info = dict(flops=0.0, bytes=0.0, per_op=[])
-
-    def use(buf, nbytes):
-        need[buf] = max(need[buf], int(nbytes))
-
-    def op(rec, tag, flops, nbytes):
-        r = list(rec) + [0] * (OP_FIELDS - len(rec))
-        ops.append(r)
-        info["per_op"].append((tag, float(flops), float(nbytes)))
-        info["flops"] += flops
-        info["bytes"] += nbytes
-
+    MFMAs and are recomputed for every 64-channel output tile.
+    An Xception network (deeplab_xception.DeepLabXception) lowers through lower_xception."""
+    if not isinstance(net, DeepLab):
+        from .deeplab_xception import lower_xception
+        if fuse_dw:
+            raise ValueError("fuse_dw applies to the MobileNetV2 blocks only")
+        return lower_xception(net, B, bf16, nb=nb, fuse_prep=fuse_prep)
+    L = Lowering(B, bf16, 11, nb)
+    es = L.es
     Hc, Wc = crop_hw(net)
-    use(0, B * Hc * Wc * 8 * es)
+    L.use(0, B * Hc * Wc * 8 * es)
     if not fuse_prep:
-        op([OP_PREP, 0], "prep", 0, B * Hc * Wc * (3 + 8 * es))
-
-    def conv(c: Conv, src, H, W, CS, dst, out_cs, out_off=0, res=-1, out_f32=False, bias_img=-1, bias_img_stride=0,
-             zero_bias=False, cout=None, tag="conv", dwf=None, rgb=False):
-        """rgb: the input is the raw u8 RGB frame batch, padded and normalised on load (the stem with
-        fuse_prep; tap field 2)."""
-        k = c.k
-        Ho, pt = same_pad(H, k, c.stride, c.dil)
-        Wo, pl = same_pad(W, k, c.stride, c.dil)
-        extra = [-1, -1, 0]
-        Hin, Win = H, W
-        if dwf is not None:   # (dw conv, its input H, W): this 1x1 runs over the dw output grid
-            d, Hin, Win = dwf
-            Ho, dpt = same_pad(Hin, 3, d.stride, d.dil)
-            Wo, dpl = same_pad(Win, 3, d.stride, d.dil)
-            wd, bd = d.folded()
-            extra = [blob.add(wd.reshape(CS, 9).T, True), blob.add(bd.astype(np.float32), False),
-                     d.stride | d.dil << 8 | dpt << 16 | dpl << 24]
-        tp = CS == 8 and dwf is None and k > 1
-        wp, bias, cinP, NP = pack_conv(c, CS, bf16, tap_packed=tp)
-        if zero_bias:
-            bias = np.zeros_like(bias)
-        w_off = blob.add(wp, True)
-        b_off = blob.add(bias, False)
-        cw = c.cout if cout is None else cout
-        oes = 4 if out_f32 else es
-        use(dst, B * Ho * Wo * out_cs * oes)
-        cin = c.w.shape[1]
-        flops = 2.0 * B * Ho * Wo * c.cout * cin * k * k + (2.0 * B * Ho * Wo * CS * 9 if dwf else 0)
-        nbytes = (B * Hin * Win * 3 if rgb else B * Hin * Win * CS * es) + B * Ho * Wo * cw * oes + \
-            (B * Ho * Wo * cw * es if res >= 0 else 0) + wp.size * es
-        t = tag if dwf is None else "conv dw+project"
-        f30 = nb(t, Ho * Wo, cinP * k * k, cw) if callable(nb) else (nb or _pick_nb(t, Ho * Wo, cinP * k * k, cw, B))
-        op([OP_CONV, src, dst, res, Hin, Win, CS, Ho, Wo, k, k, c.stride, c.dil, pt, pl, cinP, NP, w_off, b_off, c.act,
-            out_cs if res >= 0 else 0, out_cs, out_off, cw, int(out_f32), bias_img, bias_img_stride] + extra +
-           [f30, 2 if (rgb and tp) else int(tp)],
-           tag if dwf is None else "conv dw+project", flops, nbytes)
-        return Ho, Wo
-
+        L.op([OP_PREP, 0], "prep", 0, B * Hc * Wc * (3 + 8 * es))
     # stem
-    H, W = conv(net.stem, 0, Hc, Wc, 8, 1, _r8(net.stem.cout), tag="conv stem", rgb=fuse_prep)
-    if fuse_prep and int(ops[-1][31]) != 2:
+    H, W = L.conv(net.stem, 0, Hc, Wc, 8, 1, _r8(net.stem.cout), tag="conv stem", rgb=fuse_prep)
+    if fuse_prep and int(L.ops[-1][31]) != 2:
         raise ValueError("fuse_prep needs the tap-packed stem (3x3 over the 8-channel input)")
     C = net.stem.cout
     cur = 1
@@ -352,60 +424,38 @@ def lower(net: DeepLab, B: int, bf16: bool, fuse_dw: bool = False, nb=None, fuse
         nxt = 2 if cur == 1 else 1
         x_in, Cin = cur, C
         if blk.expand is not None:
-            conv(blk.expand, x_in, H, W, Cin, 3, blk.expand.cout, tag="conv expand")
+            L.conv(blk.expand, x_in, H, W, Cin, 3, blk.expand.cout, tag="conv expand")
             src, Cm = 3, blk.expand.cout
         else:
             src, Cm = x_in, Cin
         d = blk.dw
-        Ho, pt = same_pad(H, 3, d.stride, d.dil)
-        Wo, pl = same_pad(W, 3, d.stride, d.dil)
         Cout = blk.project.cout
         if fuse_dw:
-            conv(blk.project, src, H, W, Cm, nxt, Cout, res=x_in if blk.residual else -1, dwf=(d, H, W))
+            Ho, _ = same_pad(H, 3, d.stride, d.dil)
+            Wo, _ = same_pad(W, 3, d.stride, d.dil)
+            L.conv(blk.project, src, H, W, Cm, nxt, Cout, res=x_in if blk.residual else -1, dwf=(d, H, W))
             H, W = Ho, Wo
             cur, C = nxt, Cout
             continue
-        wd, bd = d.folded()
-        w_off = blob.add(wd.reshape(Cm, 9).T, True)   # [9][C] in the compute type
-        b_off = blob.add(bd.astype(np.float32), False)
-        use(4, B * Ho * Wo * Cm * es)
-        op([OP_DW, src, 4, H, W, Cm, Ho, Wo, d.stride, d.dil, pt, pl, w_off, b_off], "dw",
-           2.0 * B * Ho * Wo * Cm * 9, B * (H * W + Ho * Wo) * Cm * es)
-        H, W = Ho, Wo
-        conv(blk.project, 4, H, W, Cm, nxt, Cout, res=x_in if blk.residual else -1, tag="conv project")
+        H, W = L.dw(d, src, 4, H, W, Cm)
+        L.conv(blk.project, 4, H, W, Cm, nxt, Cout, res=x_in if blk.residual else -1, tag="conv project")
         cur, C = nxt, Cout
 
     # ASPP
     D = net.aspp0.cout
-    nbr = 1 + len(net.atrous)
-    cat_cs = D * nbr
+    cat_cs = D * (1 + len(net.atrous))
     h, w = H, W
-    chunk = 64
-    nch = -(-(h * w) // chunk)
-    use(8, B * nch * C * 4)
-    zs = _r(D, 64)
-    use(9, B * zs * 4)
-    wpool, bpool = net.pool.folded()
-    wproj, bproj = net.project.folded()
-    use(10, B * D * 4)
-    wp_off = blob.add(_round(wpool.reshape(D, C), bf16), False)             # [D][C]
-    bp_off = blob.add(bpool.astype(np.float32), False)
-    wq_off = blob.add(_round(wproj.reshape(D, -1)[:, :D], bf16), False)     # [D (out)][D (pooled ch)]
-    bq_off = blob.add(bproj.astype(np.float32), False)
-    op([OP_POOL, cur, 8, 9, h, w, C, C, chunk, nch, D, D, wp_off, bp_off, wq_off, bq_off, zs, 10], "pool",
-       2.0 * B * (D * C + D * D) + B * h * w * C, B * h * w * C * es)
-    conv(net.aspp0, cur, h, w, C, 5, cat_cs, out_off=0, tag="conv aspp")
+    zs = L.aspp_pool(net, cur, h, w, C)
+    L.conv(net.aspp0, cur, h, w, C, 5, cat_cs, out_off=0, tag="conv aspp")
     for i, a in enumerate(net.atrous):
-        conv(a, cur, h, w, C, 5, cat_cs, out_off=D * (i + 1), tag="conv atrous")
-    # the projection over the concat minus its pooled part (that part arrives as the per-image bias)
-    pj = Conv(w=net.project.w[:, D:], gamma=net.project.gamma, beta=net.project.beta, mean=net.project.mean,
-              var=net.project.var, eps=net.project.eps, act=net.project.act)
-    conv(pj, 5, h, w, cat_cs, 6, D, bias_img=9, bias_img_stride=zs, zero_bias=True, tag="conv project")
+        L.conv(a, cur, h, w, C, 5, cat_cs, out_off=D * (i + 1), tag="conv atrous")
+    L.conv(L.projection_conv(net), 5, h, w, cat_cs, 6, D, bias_img=9, bias_img_stride=zs, zero_bias=True,
+           tag="conv project")
     LCS = _r(net.num_classes, 8)
-    conv(net.logits, 6, h, w, D, 7, LCS, out_f32=True, cout=LCS, tag="conv logits")
-    op([OP_ARGMAX, 7, h, w, LCS, net.num_classes], "argmax", 0, B * (h * w * LCS * 4 + Hc * Wc * 8))
-    info.update(feature=(h, w), lcs=LCS, nops=len(ops))
-    return blob.bytes(), np.asarray(ops, np.int32), np.asarray(need, np.uint64), info
+    L.conv(net.logits, 6, h, w, D, 7, LCS, out_f32=True, cout=LCS, tag="conv logits")
+    L.argmax(7, h, w, LCS, net.num_classes, Hc, Wc)
+    L.info.update(feature=(h, w), lcs=LCS)
+    return L.result()
 
 
 # ---------------------------------------------------------------- weight file (.npz, no pickle)
@@ -427,16 +477,36 @@ def _convs(net: DeepLab):
     yield "logits", net.logits
 
 
-def save(net: DeepLab, path) -> None:
-    """Weights + topology attributes as a plain .npz (loadable with allow_pickle=False)."""
-    arrs = {}
-    for name, c in _convs(net):
+def conv_arrays(arrs: dict, named_convs) -> None:
+    """Each (name, Conv) as plain arrays: name.{w,b,gamma,beta,mean,var}, name.attrs, name.eps."""
+    for name, c in named_convs:
         for f in _CONV_FIELDS:
             v = getattr(c, f)
             if v is not None:
                 arrs[f"{name}.{f}"] = np.asarray(v, np.float32)
         arrs[f"{name}.attrs"] = np.array([c.act, c.stride, c.dil, int(c.depthwise)], np.int32)
         arrs[f"{name}.eps"] = np.array([c.eps], np.float64)
+
+
+def conv_from(z, name, path="") -> Conv:
+    if f"{name}.w" not in z:
+        raise KeyError(f"{path}: missing {name}.w")
+    act, stride, dil, dw = (int(v) for v in z[f"{name}.attrs"])
+    c = Conv(w=z[f"{name}.w"], act=act, stride=stride, dil=dil, depthwise=bool(dw), eps=float(z[f"{name}.eps"][0]))
+    for f in _CONV_FIELDS[1:]:
+        if f"{name}.{f}" in z:
+            setattr(c, f, z[f"{name}.{f}"])
+    return c
+
+
+def save(net, path) -> None:
+    """Weights + topology attributes as a plain .npz (loadable with allow_pickle=False); either
+    backbone (an Xception network is written by deeplab_xception.save_xception)."""
+    if not isinstance(net, DeepLab):
+        from .deeplab_xception import save_xception
+        return save_xception(net, path)
+    arrs = {}
+    conv_arrays(arrs, _convs(net))
     arrs["net.residual"] = np.array([int(b.residual) for b in net.blocks], np.int32)
     arrs["net.expand"] = np.array([int(b.expand is not None) for b in net.blocks], np.int32)
     arrs["net.attrs"] = np.array([net.num_classes, net.output_stride or 0, net.crop, len(net.atrous)], np.int32)
@@ -444,18 +514,14 @@ def save(net: DeepLab, path) -> None:
     np.savez(path, **arrs)
 
 
-def load(path) -> DeepLab:
+def load(path):
     z = np.load(path, allow_pickle=False)
+    if "net.xattrs" in z:
+        from .deeplab_xception import load_xception
+        return load_xception(z, path)
 
     def conv(name):
-        if f"{name}.w" not in z:
-            raise KeyError(f"{path}: missing {name}.w")
-        act, stride, dil, dw = (int(v) for v in z[f"{name}.attrs"])
-        c = Conv(w=z[f"{name}.w"], act=act, stride=stride, dil=dil, depthwise=bool(dw), eps=float(z[f"{name}.eps"][0]))
-        for f in _CONV_FIELDS[1:]:
-            if f"{name}.{f}" in z:
-                setattr(c, f, z[f"{name}.{f}"])
-        return c
+        return conv_from(z, name, path)
 
     ncls, os_, crop, natr = (int(v) for v in z["net.attrs"])
     blocks = []

@@ -203,6 +203,9 @@ class DeepLabV3(InferenceModel):
     than the crop are refused: the export sizes its image-pooling window and resize from the crop
     (deeplab/model.py, ``crop_size`` given at export), so the graph itself cannot run them.
 
+    Backbones: MobileNetV2 (DeepLabV3, dense or no atrous branches) and Xception-65 (DeepLabV3+:
+    separable ASPP, decoder at output stride 4), the two model-zoo forms (deeplab_xception.py).
+
     Weights: GRAPH_PB_PATH may be a frozen TF DeepLab-MobileNetV2 GraphDef (``deeplab.pb``, read by
     deeplab_graphdef.import_deeplab; the file itself is absent, .MISSING_LARGE_BLOBS:1), a
     ``deeplab_spec.save`` .npz, or None for the seeded synthetic network (``deeplab_spec.build_deeplab``)."""
@@ -213,19 +216,27 @@ class DeepLabV3(InferenceModel):
     CROP_SIZE = 513
 
     def __init__(self, GRAPH_PB_PATH=None, *, net=None, precision: str = "fp32", device: int | None = None,
-                 fuse_dw: bool | None = None, fuse_prep: bool = True):
+                 fuse_dw: bool | None = None, fuse_prep: bool = True, backbone: str = "mobilenet_v2"):
         """precision: "fp32" (default: the parity mode, logits within 1e-3 of the fp32 graph, as a
         drop-in for the reference's TF fp32 sess.run) or "bf16" (the throughput mode the bench uses;
         class ids can differ from fp32 where two logits are close).
         fuse_dw=True computes each depthwise conv inside its projection's operand loads
         (bit-identical, measured slower; deeplab_spec.lower). fuse_prep=False runs the padding +
-        normalisation as its own launch instead of inside the stem's operand loads (bit-identical)."""
+        normalisation as its own launch instead of inside the stem's operand loads (bit-identical).
+        backbone: the seeded synthetic network when neither a file nor ``net`` is given —
+        "mobilenet_v2" (deeplab_spec) or "xception_65" (DeepLabV3+, deeplab_xception)."""
         from . import deeplab_spec
         if precision not in ("fp32", "bf16"):
             raise ValueError("precision must be 'fp32' or 'bf16'")
         if net is None:
             if GRAPH_PB_PATH is None:
-                net = deeplab_spec.build_deeplab()
+                if backbone == "xception_65":
+                    from .deeplab_xception import build_deeplab_xception
+                    net = build_deeplab_xception()
+                elif backbone == "mobilenet_v2":
+                    net = deeplab_spec.build_deeplab()
+                else:
+                    raise ValueError("backbone must be 'mobilenet_v2' or 'xception_65'")
             else:
                 if not os.path.exists(GRAPH_PB_PATH):
                     raise FileNotFoundError(f"{GRAPH_PB_PATH}: no such file")
