@@ -1,4 +1,6 @@
-"""Benchmark of BASELINE config 4: DeepLabV3 (MobileNetV2, output stride 8, ASPP) at 513x513 on MI355X.
+"""Benchmark of BASELINE config 4: DeepLabV3 (MobileNetV2, output stride 8, ASPP) at 513x513 on MI355X;
+``--backbone xception_65`` measures the other model-zoo export, DeepLabV3+ over Xception-65 (output
+stride 16, separable ASPP 6/12/18, decoder at stride 4).
 
 One "step" = the DeepLab plugin's forward (models.DeepLabV3.predict_device: pad + normalise,
 backbone, ASPP, logits, bilinear resize to 513x513, argmax -> int64) over one batch of synthetic
@@ -44,6 +46,7 @@ def parse():
     p.add_argument("--precision", default="bf16", choices=["bf16", "fp32"])
     p.add_argument("--cpu-baseline-seconds", type=float, default=12.0)
     p.add_argument("--no-cpu-baseline", action="store_true")
+    p.add_argument("--backbone", default="mobilenet_v2", choices=["mobilenet_v2", "xception_65"])
     return p.parse_args()
 
 
@@ -83,13 +86,17 @@ def pmc_traffic(tag, batch):
     return None if v is None else round(float(v))
 
 
-def measure(dev, B, steps, warmup, precision, world=1, rank=0):
+WORKLOAD = {"mobilenet_v2": "DeepLabV3 MobileNetV2 OS8 + ASPP (image pooling + 1x1)",
+            "xception_65": "DeepLabV3+ Xception-65 OS16 + separable ASPP 6/12/18 + decoder OS4"}
+
+
+def measure(dev, B, steps, warmup, precision, world=1, rank=0, backbone="mobilenet_v2"):
     """Time `steps` DeepLab forwards of B frames (barrier + sync on both sides, max over ranks), then
     every launch of the plan with HIP events (untimed). Returns (el seconds, model, per-tag table,
     per-op list, forward us)."""
     from bugcar_image_segmentation_amd.models import DeepLabV3
 
-    model = DeepLabV3(precision=precision)
+    model = DeepLabV3(precision=precision, backbone=backbone)
     C = model.net.crop
     frames = torch.from_numpy(np.random.default_rng(rank).integers(0, 256, (B, C, C, 3), dtype=np.uint8)).to(dev)
     out = torch.empty((B, C, C), dtype=torch.int64, device=dev)
@@ -165,12 +172,12 @@ def kernel_summary(per):
             for t, v in sorted(per.items(), key=lambda kv: -kv[1]["us"])}
 
 
-def record(dev, B, steps, warmup, precision, cpu_seconds=0.0):
+def record(dev, B, steps, warmup, precision, cpu_seconds=0.0, backbone="mobilenet_v2"):
     """The config-4 sub-record bench.py adds to its line (one GPU, measured after its timed loop)."""
-    el, model, per, _per_op, fwd_us = measure(dev, B, steps, warmup, precision)
+    el, model, per, _per_op, fwd_us = measure(dev, B, steps, warmup, precision, backbone=backbone)
     res = {"value": round(B * steps / el, 2), "unit": "frames/s", "ms_per_step": round(el / steps * 1e3, 4),
            "steps": steps, "dtype": precision, "per_gpu_batch": B, "crop": model.net.crop,
-           "workload": "config4: DeepLabV3 MobileNetV2 OS8 + ASPP, 513x513 u8 RGB -> SemanticPredictions int64",
+           "workload": f"config4: {WORKLOAD[backbone]}, 513x513 u8 RGB -> SemanticPredictions int64",
            "roofline": roofline(model, per, fwd_us, B, precision)}
     if cpu_seconds > 0:
         res["cpu_baseline"] = cpu_baseline(model.net, cpu_seconds)
@@ -188,19 +195,21 @@ def main():
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
     B = a.batch
-    el, model, per, per_op, fwd_us = measure(dev, B, a.steps, a.warmup, a.precision, world, rank)
+    el, model, per, per_op, fwd_us = measure(dev, B, a.steps, a.warmup, a.precision, world, rank, a.backbone)
     C = model.net.crop
 
     if rank == 0:
         value = B * world * a.steps / el
         res = {
-            "metric": "frames/sec DeepLabV3 513x513 -> SemanticPredictions (synthetic), whole job",
+            "metric": f"frames/sec {'DeepLabV3+' if a.backbone == 'xception_65' else 'DeepLabV3'} 513x513 -> "
+                      "SemanticPredictions (synthetic), whole job",
             "value": round(value, 2), "unit": "frames/s", "n_gpus": world, "steps": a.steps, "warmup": a.warmup,
             "ms_per_step": round(el / a.steps * 1e3, 4), "higher_is_better": True, "scaling": "weak",
             "vs_baseline": None, "dtype": a.precision,
-            "data": "synthetic (uniform u8 RGB frames, seed=rank; random-init DeepLabV3-MobileNetV2 weights seed 4321)",
-            "config": {"workload": f"config4: DeepLabV3 MobileNetV2 OS8 + ASPP (image pooling + 1x1), {C}x{C}, "
-                                   f"batch {B} per GPU, pad/normalise + forward + bilinear resize + argmax int64",
+            "data": f"synthetic (uniform u8 RGB frames, seed=rank; random-init {a.backbone} weights, "
+                    f"seed {model.net.meta.get('seed')})",
+            "config": {"workload": f"config4: {WORKLOAD[a.backbone]}, {C}x{C}, batch {B} per GPU, "
+                                   "pad/normalise + forward + bilinear resize + argmax int64",
                        "global_batch": B * world, "per_gpu_batch": B, "crop": C,
                        "parallelism": f"frame-sharded dp{world}"},
             "roofline": roofline(model, per, fwd_us, B, a.precision),

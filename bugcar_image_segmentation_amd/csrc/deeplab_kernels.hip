@@ -484,7 +484,9 @@ __device__ __forceinline__ float4 relu4(float4 v) {
     return make_float4(fmaxf(v.x, 0.f), fmaxf(v.y, 0.f), fmaxf(v.z, 0.f), fmaxf(v.w, 0.f));
 }
 
-template <typename T, bool S1, int R>
+// ACT: 0 none, 1 ReLU, 2 ReLU6; IRELU: ReLU on the loaded input (compile-time: a runtime switch
+// pushed the R = 8 form from 246 VGPRs into scratch spills)
+template <typename T, bool S1, int R, int ACT, bool IRELU>
 __global__ void __launch_bounds__(256) dl_dw_kernel(const DlDwArgs a) {
     constexpr int NR = S1 ? R + 2 : 2 * R + 1;   // distinct input rows of the R output rows
     constexpr int RB = S1 ? 1 : 2;               // row index offset between consecutive output rows
@@ -542,14 +544,17 @@ __global__ void __launch_bounds__(256) dl_dw_kernel(const DlDwArgs a) {
 #pragma unroll
         for (int j = 0; j < R; ++j) {
             raw4(xr[ky + j * RB][kx], x0, x1);
-            if (a.in_relu) { x0 = relu4(x0); x1 = relu4(x1); }   // padding taps are 0 either way
+            if constexpr (IRELU) { x0 = relu4(x0); x1 = relu4(x1); }   // padding taps are 0 either way
             fma8(acc[j], x0, x1, w0, w1);
         }
     }
     float4 b0, b1;
     ld8f(reinterpret_cast<const float *>(a.bias) + g * 8, b0, b1);
-    const int act = a.act;
-    auto r6 = [act](float v) { return act == 2 ? fminf(fmaxf(v, 0.f), 6.f) : act == 1 ? fmaxf(v, 0.f) : v; };
+    auto r6 = [](float v) {
+        if constexpr (ACT == 2) return fminf(fmaxf(v, 0.f), 6.f);
+        else if constexpr (ACT == 1) return fmaxf(v, 0.f);
+        else return v;
+    };
     T *o = reinterpret_cast<T *>(a.out) + (size_t)b * a.Hout * a.Wout * a.C + g * 8;
 #pragma unroll
     for (int j = 0; j < R; ++j) {
@@ -867,19 +872,30 @@ hipError_t dl_launch_conv(int prec, bool out_f32, const DlConvArgs &a, hipStream
     return hipGetLastError();
 }
 
+template <typename T, int R, int ACT, bool IRELU>
+static void launch_dw_t(const DlDwArgs &a, const dim3 g, hipStream_t s) {
+    if (a.stride == 1) hipLaunchKernelGGL((dl_dw_kernel<T, true, R, ACT, IRELU>), g, dim3(256), 0, s, a);
+    else hipLaunchKernelGGL((dl_dw_kernel<T, false, R, ACT, IRELU>), g, dim3(256), 0, s, a);
+}
+
+// (act, in_relu) forms: MobileNetV2 (ReLU6, -), Xception pre-activation (none, ReLU in), Xception
+// activated-inside / ASPP / decoder (ReLU, -)
+template <typename T, int R>
+static hipError_t launch_dw_a(const DlDwArgs &a, const dim3 g, hipStream_t s) {
+    if (a.act == 2 && !a.in_relu) launch_dw_t<T, R, 2, false>(a, g, s);
+    else if (a.act == 0 && a.in_relu) launch_dw_t<T, R, 0, true>(a, g, s);
+    else if (a.act == 1 && !a.in_relu) launch_dw_t<T, R, 1, false>(a, g, s);
+    else if (a.act == 0 && !a.in_relu) launch_dw_t<T, R, 0, false>(a, g, s);
+    else return hipErrorInvalidValue;
+    return hipGetLastError();
+}
+
 template <int R>
 static hipError_t launch_dw_r(int prec, const DlDwArgs &a, hipStream_t s) {
     const int ph = a.stride == 1 ? a.dil : 1;
     const int n = a.B * ((a.Hout + R * ph - 1) / (R * ph) * ph) * a.Wout * (a.C >> 3);
     const dim3 g((n + 255) / 256);
-    if (prec == PREC_BF16) {
-        if (a.stride == 1) hipLaunchKernelGGL((dl_dw_kernel<__bf16, true, R>), g, dim3(256), 0, s, a);
-        else hipLaunchKernelGGL((dl_dw_kernel<__bf16, false, R>), g, dim3(256), 0, s, a);
-    } else {
-        if (a.stride == 1) hipLaunchKernelGGL((dl_dw_kernel<float, true, R>), g, dim3(256), 0, s, a);
-        else hipLaunchKernelGGL((dl_dw_kernel<float, false, R>), g, dim3(256), 0, s, a);
-    }
-    return hipGetLastError();
+    return prec == PREC_BF16 ? launch_dw_a<__bf16, R>(a, g, s) : launch_dw_a<float, R>(a, g, s);
 }
 
 // Output rows per thread (R). Measured (16 frames, 513x513, per-op HIP events, 17 launches): stride-1

@@ -130,7 +130,7 @@ bool check_op(const bugseg_dl *c, const DlOp &o, std::string &why) {
             !in_range(C, 8, CH) || !in_range(f[8], 1, 255) || !in_range(f[9], 1, 255) || !in_range(f[10], 0, 255) ||
             !in_range(f[11], 0, 255) || (double)B * Hout * Wout >= 2147483648.0) { why = "dw: field out of range"; return false; }
         if (C < 8 || C % 8 || Hin < 1 || Win < 1 || Hout < 1 || Wout < 1 || f[8] < 1 || f[9] < 1) { why = "dw: bad shape"; return false; }
-        if (!in_range(f[14], 0, 2) || !in_range(f[15], 0, 1)) { why = "dw: bad activation flags"; return false; }
+        if (!in_range(f[14], 0, 2) || !in_range(f[15], 0, 1) || (f[15] && f[14])) { why = "dw: bad activation flags"; return false; }
         if (f[8] != 1 && (f[8] != 2 || f[9] != 1)) { why = "dw: stride 2 with dilation (TF has no strided atrous)"; return false; }
         if (!buf_ok(c, src, (double)B * Hin * Win * C * es) || !buf_ok(c, dst, (double)B * Hout * Wout * C * es)) { why = "dw: buffer too small"; return false; }
         if ((double)B * Hin * Win * C * es >= 2147483648.0) { why = "dw: input exceeds 31-bit offsets"; return false; }

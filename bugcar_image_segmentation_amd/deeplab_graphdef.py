@@ -74,8 +74,23 @@ class _Conv:
             raise GraphImportError(f"{n.name}: non-square kernel {self.w.shape[2:]}")
         self.input = n.inputs[0]
         self.out = n.name
+        self.explicit = None     # (pad before, pad after) of an explicit Pad + VALID convolution
+        padding = _s(n.attr.get("padding", b"SAME"))
         # the space-to-batch encoding of an atrous convolution
         src = g.producer_chain(self.input, PASS)
+        if padding == "VALID" and src.op in ("Pad", "PadV2"):
+            # resnet_utils / xception fixed_padding ahead of a strided convolution
+            p = np.asarray(g.const(src.inputs[1]), np.int64).reshape(-1, 2)
+            if len(src.inputs) > 2 and float(np.asarray(g.const(src.inputs[2]))) != 0.0:
+                raise GraphImportError(f"{src.name}: non-zero pad value ahead of {n.name}")
+            if p.shape != (4, 2) or p[0].any() or p[3].any() or not (p[1] == p[2]).all():
+                raise GraphImportError(f"{src.name}: paddings {p.tolist()} ahead of {n.name}")
+            self.explicit = (int(p[1][0]), int(p[1][1]))
+            self.input = src.inputs[0]
+        elif padding == "VALID" and src.op != "SpaceToBatchND":
+            kh = int(g.const(n.inputs[1]).shape[0])
+            if kh != 1:
+                raise GraphImportError(f"{n.name}: VALID {kh}x{kh} convolution without an explicit pad")
         if src.op == "SpaceToBatchND":
             bs = [int(v) for v in g.const(src.inputs[1])]
             if len(bs) != 2 or bs[0] != bs[1]:
@@ -97,9 +112,9 @@ class _Conv:
         return g.producer_chain(self.input, PASS).name
 
 
-def _affine_act(g: Graph, c: _Conv):
+def _affine_act(g: Graph, c: _Conv, act_ends: bool = False):
     """The closure after the convolution as act(a x + b) per channel -> (fields for D.Conv, exit)."""
-    members, exits = elementwise_closure(g, c.out)
+    members, exits = elementwise_closure(g, c.out, act_ends)
     if len(exits) != 1:
         raise GraphImportError(f"the ops after {c.node.name} leave through {len(exits)} tensors ({exits})")
     ex = exits[0]
@@ -166,6 +181,249 @@ def read_crop(g: Graph):
     return h, w
 
 
+def _aspp_concat_perm(g: Graph, concat, by_exit: dict, pool_k, aspp0_k, widths: dict, proj_cin: int):
+    """The ASPP concat's branch order -> (permutation of the projection's input channels into the
+    engine's [pool, 1x1, atrous...] order, the atrous branch keys in concat order). by_exit: branch
+    output tensor -> key; widths: key -> channels."""
+    parts = []
+    for s in concat.inputs[:-1]:
+        n = g.node(s)
+        while n.op in _BROADCAST and n.name not in by_exit:
+            n = g.node(n.inputs[0])
+        _expect(n.name in by_exit, f"{concat.name}: input {s} is not an ASPP branch output")
+        parts.append(by_exit[n.name])
+    _expect(int(g.const(concat.inputs[-1])) % 4 == 3, f"{concat.name}: not a channel concat")
+    _expect(sorted(parts) == sorted(by_exit.values()), f"{concat.name}: branches {parts}")
+    atr_sorted = [a for a in parts if a not in (pool_k, aspp0_k)]
+    order = [pool_k, aspp0_k] + atr_sorted
+    off, start = 0, {}
+    for j in parts:
+        start[j] = off
+        off += widths[j]
+    _expect(off == proj_cin, f"projection takes {proj_cin} channels, concat has {off}")
+    return np.concatenate([np.arange(start[j], start[j] + widths[j]) for j in order]), atr_sorted
+
+
+def _fixed(c: _Conv) -> bool:
+    """A strided convolution padded the xception / resnet_utils way (fixed_padding + VALID)."""
+    ke = c.k + (c.k - 1) * (c.dil - 1)
+    return c.explicit == ((ke - 1) // 2, ke - 1 - (ke - 1) // 2)
+
+
+def _import_xception(g: Graph, convs: list, closures: list, crop_h: int, crop_w: int):
+    """The DeepLabV3+ Xception-65 export (deeplab_xception.py documents the topology) by data flow:
+    root convs, xception modules (three depthwise + pointwise pairs; a ``Relu`` ahead of each pair in
+    the pre-activation modules; an ``Add`` with the module input or with a 1x1 shortcut conv of it),
+    then the ASPP (image pooling, 1x1, separable atrous branches, projection) and the decoder
+    (``ResizeBilinear`` of the projection, concat with a 1x1 over a low-level pointwise output, two
+    separable convs) feeding the logits."""
+    from . import deeplab_xception as X
+    exit_of = {id(c): ex for c, (_, _, ex) in zip(convs, closures)}
+    ex = lambda i: exit_of[id(convs[i])]  # noqa: E731
+    act = lambda i: closures[i][1]  # noqa: E731
+
+    def conv_at(i):
+        f, a, _ = closures[i]
+        return _make(convs[i], f, a)
+
+    def need_act(i, want, role):
+        _expect(act(i) == want, f"{role} ({convs[i].node.name}): expected {_ACT_NAME[want]} after it, "
+                                f"graph has {_ACT_NAME[act(i)]}")
+
+    def strided_ok(i):
+        c = convs[i]
+        if c.stride > 1 and c.k > 1:
+            _expect(_fixed(c), f"{c.node.name}: strided convolution without fixed_padding")
+        else:
+            _expect(c.explicit is None, f"{c.node.name}: explicit padding on a stride-1 convolution")
+
+    n = len(convs)
+    # shortcut convs: 1x1 convs whose output meets a pointwise output at an Add
+    consumers_add = {}
+    for i in range(n):
+        for a in g.consumers[ex(i)]:
+            if a.op in ("Add", "AddV2"):
+                consumers_add.setdefault(a.name, []).append(i)
+    shortcut_of = {}          # add name -> shortcut conv index
+    for add, idx in consumers_add.items():
+        if len(idx) == 2:
+            sc = [i for i in idx if not convs[i].depthwise and convs[i].k == 1 and
+                  not (i > 0 and convs[i - 1].depthwise and convs[i].src(g) == ex(i - 1))]
+            _expect(len(sc) == 1, f"{add}: cannot tell the shortcut from the residual branch")
+            shortcut_of[add] = sc[0]
+    shortcuts = set(shortcut_of.values())
+    seq = [i for i in range(n) if i not in shortcuts]
+
+    r0, r1 = seq[0], seq[1]
+    strided_ok(r0)
+    strided_ok(r1)
+    need_act(r0, D.ACT_RELU, "root conv")
+    need_act(r1, D.ACT_RELU, "root conv")
+    _expect(convs[r1].src(g) == ex(r0) and convs[r1].cin == convs[r0].cout, f"{convs[r1].node.name}: root chain")
+    cur, cur_c = ex(r1), convs[r1].cout
+    modules, pw_pos = [], {}
+    k = 2
+    def starts_module(k):
+        if k + 1 >= len(seq) or not convs[seq[k]].depthwise:
+            return False
+        inp = convs[seq[k]].input
+        return g.producer_chain(inp, PASS).name == cur or _relu_of(g, inp) == cur
+
+    while starts_module(k):
+        mod_in, mod_c = cur, cur_c
+        seps = []
+        src_t = cur
+        for j in range(3):
+            _expect(k + 1 < len(seq), "graph ends inside an xception module")
+            di, pi = seq[k], seq[k + 1]
+            dw, pw = convs[di], convs[pi]
+            _expect(dw.depthwise and dw.k == 3, f"{dw.node.name}: expected a 3x3 depthwise convolution")
+            _expect(not pw.depthwise and pw.k == 1 and pw.src(g) == ex(di),
+                    f"{pw.node.name}: expected the 1x1 pointwise convolution of {dw.node.name}")
+            if g.producer_chain(dw.input, PASS).name == src_t:
+                pre = False
+            else:
+                _expect(_relu_of(g, dw.input) == src_t, f"{dw.node.name}: input is neither {src_t} nor its ReLU")
+                pre = True
+            strided_ok(di)
+            _expect(act(di) in (D.ACT_NONE, D.ACT_RELU) and act(pi) in (D.ACT_NONE, D.ACT_RELU),
+                    f"{dw.node.name}: activation other than ReLU in a separable conv")
+            _expect(dw.cin == cur_c, f"{dw.node.name}: channel count")
+            dwc, pwc = conv_at(di), conv_at(pi)
+            if act(di) == D.ACT_NONE:
+                # pre-activation form: a ReLU between two separable convs that is the pointwise's only
+                # reader joined its closure; it is this conv's input ReLU (same values either way)
+                if j and seps[-1].pw.act == D.ACT_RELU:
+                    seps[-1].pw.act = D.ACT_NONE
+                    pre = True
+                _expect(pre, f"{dw.node.name}: depthwise without ReLU before or after it")
+            else:
+                _expect(not pre and act(pi) == D.ACT_RELU, f"{dw.node.name}: a separable conv is either "
+                                                           "pre-activated or activated inside")
+            seps.append(X.SepConv(dwc, pwc, pre))
+            pw_pos[ex(pi)] = (len(modules), j)
+            src_t, cur_c = ex(pi), pw.cout
+            k += 2
+        _expect(len({sp.pre_relu for sp in seps}) == 1, "module mixes pre-activated and activated separable convs")
+        if seps[0].pre_relu:
+            _expect(seps[2].pw.act == D.ACT_NONE, f"{convs[seq[k - 1]].node.name}: activation before the module sum")
+        adds = [a for a in g.consumers[src_t] if a.op in ("Add", "AddV2")]
+        skip, sc = "none", None
+        if adds:
+            add = adds[0]
+            others = [g.producer_chain(t, PASS).name for t in add.inputs]
+            others.remove(src_t)
+            if add.name in shortcut_of:
+                si = shortcut_of[add.name]
+                _expect(convs[si].src(g) == mod_in and ex(si) == others[0] and convs[si].cin == mod_c,
+                        f"{convs[si].node.name}: shortcut not over the module input")
+                need_act(si, D.ACT_NONE, "shortcut")
+                skip, sc = "conv", conv_at(si)
+            else:
+                _expect(others == [mod_in] and mod_c == cur_c, f"{add.name}: residual over a shape change")
+                skip = "sum"
+            cur = add.name
+        else:
+            cur = src_t
+        modules.append(X.XModule(seps, skip, sc))
+    _expect(len(modules) >= 2, "fewer than two xception modules after the root")
+    backbone, feat_c = cur, cur_c
+    # ASPP + decoder + logits
+    pool = aspp0 = project = logits = low_proj = None
+    pool_k = aspp0_k = proj_i = low_i = None
+    atrous = {}               # pointwise exit -> SepConv
+    dec = []
+    concat = None
+    rest = seq[k:]
+    used = set()
+    for q, j in enumerate(rest):
+        if j in used:
+            continue
+        c = convs[j]
+        src = g.node(c.src(g))
+        if c.depthwise:
+            _expect(q + 1 < len(rest), f"{c.node.name}: depthwise convolution at the end of the graph")
+            pi = rest[q + 1]
+            pw = convs[pi]
+            _expect(not pw.depthwise and pw.k == 1 and pw.src(g) == ex(j), f"{c.node.name}: no pointwise after it")
+            _expect(act(j) == D.ACT_RELU and act(pi) == D.ACT_RELU, f"{c.node.name}: separable conv without ReLUs")
+            used.add(pi)
+            sepc = X.SepConv(conv_at(j), conv_at(pi))
+            if src.name == backbone:
+                atrous[ex(pi)] = sepc
+            else:
+                dec.append((j, pi, sepc))
+        elif src.op in ("Mean", "AvgPool") and g.producer_chain(src.inputs[0], PASS).name == backbone:
+            if src.op == "Mean":
+                ax = sorted(int(v) % 4 for v in np.atleast_1d(g.const(src.inputs[1])))
+                _expect(ax == [1, 2], f"{src.name}: mean over axes {ax}, expected the spatial axes")
+            _expect(pool is None and c.k == 1, f"{c.node.name}: second / non-1x1 image-pooling convolution")
+            need_act(j, D.ACT_RELU, "image pooling")
+            pool, pool_k = conv_at(j), ex(j)
+        elif src.name == backbone:
+            _expect(aspp0 is None and c.k == 1, f"{c.node.name}: second / non-1x1 dense ASPP branch (the Xception "
+                                                "ASPP's atrous branches are separable)")
+            need_act(j, D.ACT_RELU, "ASPP branch")
+            aspp0, aspp0_k = conv_at(j), ex(j)
+        elif src.op == "ConcatV2" and project is None:
+            _expect(c.k == 1, f"{c.node.name}: non-1x1 concat projection")
+            need_act(j, D.ACT_RELU, "concat projection")
+            project, proj_i, concat = conv_at(j), j, src
+        elif src.name in pw_pos and low_proj is None:
+            _expect(c.k == 1, f"{c.node.name}: non-1x1 low-level projection")
+            need_act(j, D.ACT_RELU, "low-level projection")
+            low_proj, low_i, low_at = conv_at(j), j, pw_pos[src.name]
+        elif c.k == 1 and logits is None and act(j) == D.ACT_NONE:
+            logits, logits_src = conv_at(j), src.name
+        else:
+            raise GraphImportError(f"{c.node.name}: convolution fed by {src.name} ({src.op}) has no DeepLab role")
+    _expect(pool is not None and aspp0 is not None and project is not None and logits is not None,
+            "missing ASPP parts: " + ", ".join(nm for nm, v in (("image pooling", pool), ("1x1 branch", aspp0),
+                                                                ("projection", project), ("logits", logits))
+                                                if v is None))
+    by_exit = {pool_k: "pool", aspp0_k: "aspp0", **{e: e for e in atrous}}
+    widths = {"pool": pool.cout, "aspp0": aspp0.cout, **{e: a.pw.cout for e, a in atrous.items()}}
+    perm, atr_sorted = _aspp_concat_perm(g, concat, by_exit, "pool", "aspp0", widths, project.w.shape[1])
+    project.w = np.ascontiguousarray(project.w[:, perm])
+    atrous_seps = [atrous[e] for e in atr_sorted]
+    Dd = aspp0.cout
+    _expect(pool.cout == Dd and all(a.pw.cout == Dd for a in atrous_seps) and project.cout == Dd,
+            "ASPP branches and projection differ in depth")
+    decoder = []
+    if low_proj is not None:
+        _expect(len(dec) == 2, f"decoder has {len(dec)} separable convs, expected 2")
+        d0 = convs[dec[0][0]]
+        cat2 = g.node(d0.src(g))
+        _expect(cat2.op == "ConcatV2" and len(cat2.inputs) == 3, f"{d0.node.name}: decoder input is not a 2-way concat")
+        first = g.node(cat2.inputs[0])
+        while first.op in PASS:
+            first = g.node(first.inputs[0])
+        _expect(first.op in ("ResizeBilinear", "ResizeBilinearV2") and
+                g.producer_chain(first.inputs[0], PASS).name == ex(proj_i) and
+                g.producer_chain(cat2.inputs[1], PASS).name == ex(low_i),
+                f"{cat2.name}: expected [resized ASPP output, low-level projection]")
+        _expect(bool(first.attr.get("align_corners", False)), f"{first.name}: decoder resize without align_corners")
+        _expect(convs[dec[1][0]].src(g) == ex(dec[0][1]), f"{convs[dec[1][0]].node.name}: decoder chain")
+        decoder = [dec[0][2], dec[1][2]]
+        _expect(logits_src == ex(dec[1][1]), "logits not over the decoder output")
+    else:
+        _expect(not dec and logits_src == ex(proj_i), "logits not over the ASPP projection")
+    os_ = convs[r0].stride
+    for m in modules:
+        os_ *= m.seps[2].dw.stride
+    return X.DeepLabXception([conv_at(r0), conv_at(r1)], modules, low_at if low_proj is not None else (1, 1), pool,
+                             aspp0, atrous_seps, project, low_proj, decoder, logits, logits.cout, os_, crop_h,
+                             meta=dict(source="graphdef", backbone="xception_65",
+                                       atrous_rates=tuple(a.dw.dil for a in atrous_seps)),
+                             crop_w=crop_w if crop_w != crop_h else 0)
+
+
+def _relu_of(g: Graph, name: str):
+    """If `name` is (through identity-like ops) a Relu, the tensor it rectifies; else None."""
+    n = g.producer_chain(name, PASS)
+    return g.producer_chain(n.inputs[0], PASS).name if n.op == "Relu" else None
+
+
 def import_deeplab(data: bytes, crop=None, default_crop: int = D.CROP) -> D.DeepLab:
     """Frozen DeepLab-MobileNetV2 GraphDef bytes -> deeplab_spec.DeepLab (weights + topology).
     crop: None reads the export's crop from the graph (read_crop; ``default_crop`` when the graph
@@ -176,6 +434,12 @@ def import_deeplab(data: bytes, crop=None, default_crop: int = D.CROP) -> D.Deep
     crop_h, crop_w = (int(crop), int(crop)) if np.ndim(crop) == 0 else (int(crop[0]), int(crop[1]))
     convs = [_Conv(g, n) for n in g.nodes if n.op in CONV_OPS]
     _expect(len(convs) >= 6, f"graph has {len(convs)} convolutions; not a DeepLab export")
+    st = convs[0]
+    _expect(not st.depthwise and st.cin == 3 and st.k == 3, f"{st.node.name}: the first convolution is not a "
+                                                            "3x3 stem over the RGB input")
+    if not convs[1].depthwise and convs[1].k == 3:
+        # a second full 3x3 convolution: the Xception root (MobileNetV2 goes on with a depthwise one)
+        return _import_xception(g, convs, [_affine_act(g, c, act_ends=True) for c in convs], crop_h, crop_w)
     closures = [_affine_act(g, c) for c in convs]
     exit_of = {id(c): ex for c, (_, _, ex) in zip(convs, closures)}
 
@@ -188,9 +452,8 @@ def import_deeplab(data: bytes, crop=None, default_crop: int = D.CROP) -> D.Deep
                                         f"graph has {_ACT_NAME[closures[i][1]]}")
 
     # stem
-    st = convs[0]
-    _expect(not st.depthwise and st.cin == 3 and st.k == 3, f"{st.node.name}: the first convolution is not a "
-                                                            "3x3 stem over the RGB input")
+    for c in convs:
+        _expect(c.explicit is None, f"{c.node.name}: explicit padding in a MobileNetV2 graph")
     need_act(0, D.ACT_RELU6, "stem")
     stem = conv_at(0)
     cur = exit_of[id(st)]
@@ -275,24 +538,8 @@ def import_deeplab(data: bytes, crop=None, default_crop: int = D.CROP) -> D.Deep
                                                                ("projection", project), ("logits", logits)) if v is None))
     # concat order -> engine order [pool, aspp0, atrous...]
     by_exit = {exit_of[id(convs[j])]: j for j in [pool_i, aspp0_i] + [a for a, _ in atrous]}
-    parts = []
-    for s in concat.inputs[:-1]:
-        n = g.node(s)
-        while n.op in _BROADCAST and n.name not in by_exit:
-            n = g.node(n.inputs[0])
-        _expect(n.name in by_exit, f"{concat.name}: input {s} is not an ASPP branch output")
-        parts.append(by_exit[n.name])
-    _expect(int(g.const(concat.inputs[-1])) % 4 == 3, f"{concat.name}: not a channel concat")
-    _expect(sorted(parts) == sorted(by_exit.values()), f"{concat.name}: branches {parts}")
-    atr_sorted = [a for a in parts if a not in (pool_i, aspp0_i)]
-    order = [pool_i, aspp0_i] + atr_sorted
-    widths = {j: convs[j].cout for j in order}
-    off, start = 0, {}
-    for j in parts:
-        start[j] = off
-        off += widths[j]
-    _expect(off == project.w.shape[1], f"projection takes {project.w.shape[1]} channels, concat has {off}")
-    perm = np.concatenate([np.arange(start[j], start[j] + widths[j]) for j in order])
+    perm, atr_sorted = _aspp_concat_perm(g, concat, by_exit, pool_i, aspp0_i,
+                                         {j: convs[j].cout for j in by_exit.values()}, project.w.shape[1])
     project.w = np.ascontiguousarray(project.w[:, perm])
     atrous_convs = [dict(atrous)[j] for j in atr_sorted]
     Dd = aspp0.cout

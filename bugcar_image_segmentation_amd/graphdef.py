@@ -498,12 +498,15 @@ def _conv_info(g: Graph, n: Node, shapes: dict) -> ConvInfo:
     return ConvInfo(n, kind, np.ascontiguousarray(w, np.float32), sh, dh, pad, nchw, out, out_pad)
 
 
-def elementwise_closure(g: Graph, root: str):
+def elementwise_closure(g: Graph, root: str, act_ends: bool = False):
     """Nodes reachable from tensor `root` through elementwise ops whose other inputs are constant or
     inside the closure, and its single exit (the node whose value leaves the closure).
-    Single-input Concat / identity-like ops are pass-through."""
+    Single-input Concat / identity-like ops are pass-through. act_ends: nothing past an activation
+    (Relu / Relu6) joins, and an activation joins only as the sole consumer of its input — a ReLU
+    that also has an un-rectified reader beside it belongs to the next layer (pre-activation nets)."""
     inside = {_src(root)[0]}
     members: list = []
+    acts = set()
     changed = True
     while changed:
         changed = False
@@ -519,9 +522,16 @@ def elementwise_closure(g: Graph, root: str):
                     data_in = c.inputs[:1]
                     if not all(g.is_const(s) for s in c.inputs[1:5]):
                         continue
+                if act_ends:
+                    if any(_src(s)[0] in acts for s in data_in):
+                        continue
+                    if c.op in ("Relu", "Relu6") and len(g.consumers.get(_src(c.inputs[0])[0], [])) != 1:
+                        continue
                 if all(_src(s)[0] in inside or g.is_const(s) for s in data_in):
                     inside.add(c.name)
                     members.append(c)
+                    if c.op in ("Relu", "Relu6"):
+                        acts.add(c.name)
                     changed = True
     # exits: members (or the root) consumed outside the closure, or not consumed at all
     exits = []

@@ -11,6 +11,12 @@ and to run the graph through the NumPy GraphDef interpreter (oracle/tf_graph.py)
   ``BiasAdd``, dilation in the ``dilations`` attribute, image pooling through ``AvgPool``, concat
   in a different order ([1x1, atrous..., pool]).
 
+An Xception network (deeplab_xception.DeepLabXception) is written the way xception_65 +
+refine_by_decoder build it: strided layers as ``Pad`` (fixed_padding) + VALID convolution, a
+``Relu`` ahead of each separable conv of the pre-activation modules, depthwise + pointwise pairs,
+skips as ``AddV2`` (1x1 shortcut conv or identity), separable ASPP branches, and the decoder's
+``ResizeBilinear`` + ``ConcatV2`` with the 1x1-projected low-level features.
+
 Both take ``ImageTensor`` (B, H, W, 3) u8 and end in ``SemanticPredictions`` (int64, (B, H, W)),
 the reference's tensor names without the ``import/`` scope (models.py:102-103,115-125), with the
 export's preprocessing and bilinear resize (align_corners) + argmax written as graph ops. The pad is
@@ -39,8 +45,9 @@ class DeepLabWriter:
     def i32(self, v):
         return self.g.const(np.asarray(v, np.int32), np.int32)
 
-    def conv(self, x, c: D.Conv, n):
-        """n: input (height, width) -> (output tensor, output (height, width))."""
+    def conv(self, x, c: D.Conv, n, fixed=False):
+        """n: input (height, width) -> (output tensor, output (height, width)). fixed: a strided
+        conv2d_same / separable_conv2d_same — an explicit Pad by fixed_padding, then VALID."""
         g = self.g
         k, s, d = c.k, c.stride, c.dil
         w = np.asarray(c.w, np.float64)
@@ -67,6 +74,13 @@ class DeepLabWriter:
             y = g.node(op, [x, filt], T=F32, strides=[1, 1, 1, 1], padding="VALID", data_format="NHWC")
             y = g.node("BatchToSpaceND", [y, self.i32([d, d]), self.i32([[0, ex[0]], [0, ex[1]]])], T=F32,
                        Tblock_shape=I32, Tcrops=I32)
+        elif fixed and s > 1:
+            ke = k + (k - 1) * (d - 1)
+            p0 = (ke - 1) // 2
+            x = g.node("Pad", [x, self.i32([[0, 0], [p0, ke - 1 - p0], [p0, ke - 1 - p0], [0, 0]])], T=F32,
+                       Tpaddings=I32)
+            y = g.node(op, [x, filt], T=F32, strides=[1, s, s, 1], padding="VALID", data_format="NHWC",
+                       dilations=[1, d, d, 1])
         else:
             y = g.node(op, [x, filt], T=F32, strides=[1, s, s, 1], padding="SAME", data_format="NHWC",
                        dilations=[1, d, d, 1])
@@ -103,6 +117,33 @@ class DeepLabWriter:
         x = g.node("PadV2", [x, pads, g.const(np.float32(127.5))], T=F32, Tpaddings=I32)
         return x, g.node("Pack", [sizes[0][2], sizes[1][2]], T=I32, N=2, axis=0)
 
+    def sep(self, x, sp, n):
+        """A separable conv: [Relu] -> depthwise (+ BN [+ Relu]) -> 1x1 (+ BN [+ Relu])."""
+        if sp.pre_relu:
+            x = self.g.node("Relu", [x], T=F32)
+        x, n = self.conv(x, sp.dw, n, fixed=True)
+        x, _ = self.conv(x, sp.pw, n)
+        return x, n
+
+    def xception(self, x, n):
+        """Root convs and xception modules -> (backbone output, size, low-level tensor, its size)."""
+        g, net = self.g, self.net
+        for c in net.root:
+            x, n = self.conv(x, c, n, fixed=True)
+        low = None
+        for mi, m in enumerate(net.modules):
+            inp, n_in = x, n
+            for si, sp in enumerate(m.seps):
+                x, n = self.sep(x, sp, n)
+                if (mi, si) == tuple(net.low_level):
+                    low = (x, n)
+            if m.skip == "conv":
+                sc, _ = self.conv(inp, m.shortcut, n_in)
+                x = g.node("AddV2", [x, sc], T=F32)
+            elif m.skip == "sum":
+                x = g.node("AddV2", [x, inp], T=F32)
+        return x, n, low
+
     def build(self) -> bytes:
         g, net = self.g, self.net
         B, H, W = self.B, self.H, self.W
@@ -118,15 +159,19 @@ class DeepLabWriter:
             out_size = self.i32(list(C))
         x = g.node("Mul", [x, g.const(np.float32(2.0 / 255.0))], T=F32)
         x = g.node("Sub", [x, g.const(np.float32(1.0))], T=F32)
-        x, n = self.conv(x, net.stem, C)
-        for blk in net.blocks:
-            inp = x
-            if blk.expand is not None:
-                x, _ = self.conv(x, blk.expand, n)
-            x, n = self.conv(x, blk.dw, n)
-            x, _ = self.conv(x, blk.project, n)
-            if blk.residual:
-                x = g.node("AddV2", [x, inp], T=F32)
+        xc = hasattr(net, "modules")
+        if xc:
+            x, n, low = self.xception(x, C)
+        else:
+            x, n = self.conv(x, net.stem, C)
+            for blk in net.blocks:
+                inp = x
+                if blk.expand is not None:
+                    x, _ = self.conv(x, blk.expand, n)
+                x, n = self.conv(x, blk.dw, n)
+                x, _ = self.conv(x, blk.project, n)
+                if blk.residual:
+                    x = g.node("AddV2", [x, inp], T=F32)
         feat = x
         if self.style == "slim":
             p = g.node("Mean", [feat, self.i32([1, 2])], T=F32, Tidx=I32, keep_dims=True)
@@ -136,7 +181,7 @@ class DeepLabWriter:
         p, _ = self.conv(p, net.pool, (1, 1))
         p = g.node("ResizeBilinear", [p, self.i32(list(n))], T=F32, align_corners=True)
         a0, _ = self.conv(feat, net.aspp0, n)
-        atr = [self.conv(feat, a, n)[0] for a in net.atrous]
+        atr = [(self.sep(feat, a, n) if xc else self.conv(feat, a, n))[0] for a in net.atrous]
         parts = [p, a0] + atr if self.style == "slim" else [a0] + atr + [p]
         cat = g.node("ConcatV2", parts + [self.i32(3)], T=F32, N=len(parts), Tidx=I32)
         if self.style == "folded":
@@ -148,6 +193,15 @@ class DeepLabWriter:
         else:
             proj = net.project
         y, _ = self.conv(cat, proj, n)
+        if xc and net.low_proj is not None:
+            # refine_by_decoder: resize to the low-level size, concat [resized, projected low level]
+            lx, ln = low
+            up = g.node("ResizeBilinear", [y, self.i32(list(ln))], T=F32, align_corners=True)
+            lp, _ = self.conv(lx, net.low_proj, ln)
+            y = g.node("ConcatV2", [up, lp, self.i32(3)], T=F32, N=2, Tidx=I32)
+            for sp in net.decoder:
+                y, _ = self.sep(y, sp, ln)
+            n = ln
         lg, _ = self.conv(y, net.logits, n)
         lg = g.node("Identity", [lg], name="logits", T=F32)
         up = g.node("ResizeBilinear", [lg, out_size], T=F32, align_corners=True)

@@ -13,6 +13,7 @@ import pytest
 import torch
 
 from bugcar_image_segmentation_amd import deeplab_spec as S
+from bugcar_image_segmentation_amd import deeplab_xception as X
 from bugcar_image_segmentation_amd.deeplab_graphdef import graphdef_to_npz, import_deeplab
 from bugcar_image_segmentation_amd.graphdef import GraphImportError
 from deeplab_graph_writer import write_deeplab_graph
@@ -111,3 +112,59 @@ def test_rejects_graphs_that_are_not_deeplab():
     net.blocks[2].dw.act = S.ACT_RELU        # wrong activation after a depthwise conv
     with pytest.raises(GraphImportError, match="depthwise"):
         import_deeplab(write_deeplab_graph(net, "slim", 65, 65), crop=CROP)
+
+
+def _same_xception(a, b):
+    na, nb = list(X._named_convs(a)), list(X._named_convs(b))
+    assert [n for n, _ in na] == [n for n, _ in nb]
+    for (name, x), (_, y) in zip(na, nb):
+        assert (x.act, x.stride, x.dil, x.depthwise) == (y.act, y.stride, y.dil, y.depthwise), name
+        wx, bx = x.folded()
+        wy, by = y.folded()
+        np.testing.assert_allclose(wy, wx, rtol=1e-5, atol=1e-6, err_msg=name)
+        np.testing.assert_allclose(by, bx, rtol=1e-5, atol=1e-6, err_msg=name)
+    assert [(m.skip, [sp.pre_relu for sp in m.seps]) for m in a.modules] == \
+        [(m.skip, [sp.pre_relu for sp in m.seps]) for m in b.modules]
+    assert tuple(a.low_level) == tuple(b.low_level) and (a.low_proj is None) == (b.low_proj is None)
+    assert (a.num_classes, a.output_stride, S.crop_hw(a)) == (b.num_classes, b.output_stride, S.crop_hw(b))
+
+
+@pytest.mark.parametrize("style", ["slim", "folded"])
+@pytest.mark.parametrize("kw", [dict(atrous_rates=(2, 4)), dict(atrous_rates=(), decoder=False),
+                                dict(output_stride=8, atrous_rates=(2,), crop=(64, 98))])
+def test_import_xception(style, kw):
+    """Xception-65 / DeepLabV3+ graphs (fixed-padding strided layers, pre-activation ReLUs between
+    separable convs, conv / sum / no skips, separable ASPP, decoder): the importer recovers the
+    network, and the interpreter's logits on the written graph equal the oracle's."""
+    net = X.build_deeplab_xception(width=0.25, middle=2, **{"crop": CROP, "num_classes": 5, **kw})
+    H, W = 60, 64
+    pb = write_deeplab_graph(net, style, H, W)
+    got = import_deeplab(pb)
+    _same_xception(net, got)
+    x = np.random.default_rng(6).integers(0, 256, (1, H, W, 3), dtype=np.uint8)
+    ref = O.forward(net, x).numpy()
+    np.testing.assert_allclose(O.forward(got, x).numpy(), ref, atol=1e-4)
+    lg = tf_graph.run(pb, {"ImageTensor": x}, "logits")
+    np.testing.assert_allclose(np.transpose(lg, (0, 3, 1, 2)), ref, atol=1e-4)
+
+
+def test_xception_npz_round_trip(tmp_path):
+    net = X.build_deeplab_xception(width=0.25, middle=1, crop=(65, 81))
+    p = tmp_path / "x.npz"
+    S.save(net, p)
+    _same_xception(net, S.load(p))
+    got = graphdef_to_npz(write_deeplab_graph(net, "slim", 40, 40), p)
+    _same_xception(got, S.load(p))
+
+
+def test_xception_import_rejects_same_padded_strides():
+    """A strided 3x3 with SAME padding is not the xception export's fixed padding (the two differ
+    on even sizes): refused rather than mis-lowered."""
+    from graph_writer import F32
+    net = X.build_deeplab_xception(width=0.25, middle=1, crop=CROP)
+    from deeplab_graph_writer import DeepLabWriter
+    w = DeepLabWriter(net, "folded", 40, 40)
+    orig = w.conv
+    w.conv = lambda x, c, n, fixed=False: orig(x, c, n, fixed=False)
+    with pytest.raises(GraphImportError, match="fixed_padding"):
+        import_deeplab(w.build())

@@ -235,3 +235,21 @@ def test_xception_fused_prep_bit_identical(gpu, precision):
     b = plain.predict(x)
     assert torch.equal(la, plain.logits_device().cpu())
     assert np.array_equal(a, b)
+
+
+@pytest.mark.parametrize("style", ["slim", "folded"])
+def test_xception_from_frozen_graphdef(gpu, tmp_path, style):
+    """DeepLabV3(<frozen Xception-65 DeepLabV3+ GraphDef>): the imported network on the GPU against
+    the NumPy GraphDef interpreter's logits and the oracle."""
+    from deeplab_graph_writer import write_deeplab_graph
+    from oracle import tf_graph
+    net = X.build_deeplab_xception(width=0.25, middle=2, crop=97, atrous_rates=(2, 4))
+    H, W = 90, 97
+    pb = tmp_path / "deeplab.pb"
+    pb.write_bytes(write_deeplab_graph(net, style, H, W))
+    model = DeepLabV3(str(pb), precision="fp32")
+    assert isinstance(model.net, X.DeepLabXception) and S.crop_hw(model.net) == (97, 97)
+    x = _frames(1, H, W, 13)
+    _check_fp32(model, model.net, x, torch.float64)
+    lg = np.transpose(tf_graph.run(pb.read_bytes(), {"ImageTensor": x}, "logits"), (0, 3, 1, 2))
+    assert np.abs(_gpu_logits(model) - lg).max() < LOGIT_TOL
