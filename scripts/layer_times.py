@@ -18,22 +18,22 @@ BNECK_SHAPES = {(128, 0): "16x16", (128, 1): "20x16", (128, 2): "4x80", (128, 3)
 
 
 def short(name):
-    m = re.search(r"bneck_kernelI(DF16b|f)Li(\d+)ELb(\d)ELi(\d+)ELb\dELi([1-9]\d*)E", name)
+    m = re.search(r"bneck_kernelI(DF16b|DF16_|f)Li(\d+)ELb(\d)ELi(\d+)ELb\dELi([1-9]\d*)E", name)
     if m:   # the downsampling form (non-zero input-channel template argument)
         return f"down C{m.group(2)} {BNECK_SHAPES.get((int(m.group(2)), int(m.group(4))), '?')}"
-    m = re.search(r"bneck_kernelI(DF16b|f)Li(\d+)ELb(\d)ELi(\d+)E", name)
+    m = re.search(r"bneck_kernelI(DF16b|DF16_|f)Li(\d+)ELb(\d)ELi(\d+)E", name)
     if not m:
-        m = re.search(r"bneck_kernel<(__bf16|float), (\d+), (false|true), (\d+)>", name)
+        m = re.search(r"bneck_kernel<(__bf16|_Float16|float), (\d+), (false|true), (\d+)>", name)
     if m:
         asym = m.group(3) in ("1", "true")
         return f"bneck C{m.group(2)}{' asym' if asym else ''} {BNECK_SHAPES.get((int(m.group(2)), int(m.group(4))), '?')}"
-    m = re.search(r"conv_kernelI(DF16b|f)Li(\d+)ELi(\d+)E", name)
+    m = re.search(r"conv_kernelI(DF16b|DF16_|f)Li(\d+)ELi(\d+)E", name)
     if m:
         return f"conv NR{m.group(2)} E{m.group(3)}"
     m = re.search(r"conv_kernel<.*, (\d+)>", name)
     if m:
         return f"conv NR1 E{m.group(1)}"
-    m = re.search(r"up_kernelI(DF16b|f)Li(\d+)ELi(\d+)ELi(\d+)E", name)
+    m = re.search(r"up_kernelI(DF16b|DF16_|f)Li(\d+)ELi(\d+)ELi(\d+)E", name)
     if m:
         return f"up C{m.group(4)}"
     if "cls_kernel" in name:
