@@ -454,6 +454,187 @@ __global__ void __launch_bounds__(256, 2) dl_gemm_kernel(const DlConvArgs a) {
     }
 }
 
+// ------------------------------------------------------------------ 1x1 conv, MFMA-heavy shapes
+// Deep 1x1 convolutions (K >= 256 input channels, >= 128 outputs: Xception's 728/1024/1536-channel
+// pointwise layers, MobileNetV2's 576/960 -> N projections, the ASPP 1x1s) are MFMA-bound, and
+// dl_gemm_kernel's 256 x 64 tile with register-staged k-stages is latency-bound on them (one stage in
+// flight behind 32 MFMAs per wave). Here: a 128-pixel x 128-channel tile, four waves as 2 x 2 (each
+// 64 x 64 = the same acc[4][4] fragment set), k-stages of 64 channels moved global -> LDS by
+// global_load_lds (16 B per lane, no VGPR round trip) into two LDS buffers, so stage s + 1 is in
+// flight while stage s's 32 MFMAs per wave run; one raw barrier after the counted vmcnt wait, one
+// after the reads. LDS rows are 128 B (64 bf16) with the 16-B slots XOR-swizzled by row:
+// slot = kchunk ^ ((row >> 1) & 7), so the 16 rows a ds_read_b128 lane group reads (one k-chunk)
+// land on 16 distinct 16-B bank groups; glds writes lane-linear, so each lane fetches the chunk its
+// slot holds (the swizzle is applied to the global source address). The k-steps go through the same
+// MFMA in the same order as dl_conv_kernel / dl_gemm_kernel with the same epilogue: bit-identical.
+// Tails: rows past M / NP and chunks past CS / K re-read an in-range chunk (finite values; their
+// products meet zero weights or are never stored).
+constexpr int G2_T = 128, G2_KT = 64;
+
+__device__ __forceinline__ void glds16(const void *g, void *lds) {
+    __builtin_amdgcn_global_load_lds((__attribute__((address_space(1))) void *)g,
+                                     (__attribute__((address_space(3))) void *)lds, 16, 0, 0);
+}
+// An LDS read the compiler does not see: its alias tracking of the in-flight glds otherwise puts a
+// vmcnt(0) ahead of the reads and drains the next stage's prefetch. The data is waited for by
+// lds_wait8, which takes the eight destination registers as operands so no MFMA can move above it.
+__device__ __forceinline__ u32x4 lds_read16(const void *p) {
+    u32x4 v;
+    const uint32_t a = (uint32_t)(uintptr_t)(const __attribute__((address_space(3))) void *)p;
+    asm volatile("ds_read_b128 %0, %1" : "=v"(v) : "v"(a));
+    return v;
+}
+__device__ __forceinline__ void lds_wait8(u32x4 &a0, u32x4 &a1, u32x4 &a2, u32x4 &a3, u32x4 &b0, u32x4 &b1,
+                                          u32x4 &b2, u32x4 &b3) {
+    asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(a0), "+v"(a1), "+v"(a2), "+v"(a3), "+v"(b0), "+v"(b1), "+v"(b2),
+                 "+v"(b3));
+}
+
+template <bool OUTF32>
+__global__ void __launch_bounds__(256, 2) dl_gemm128_kernel(const DlConvArgs a) {
+    // two LDS objects, one per buffer, and the k-loop unrolled by two so each buffer's role is static:
+    // the compiler then sees that a stage's ds_reads cannot alias the glds filling the other buffer
+    // and does not drain the prefetch (vmcnt(0)) ahead of them
+    __shared__ __attribute__((aligned(16))) __bf16 sm0[2 * G2_T * G2_KT];   // [A | B][128][64]: 32 KB
+    __shared__ __attribute__((aligned(16))) __bf16 sm1[2 * G2_T * G2_KT];
+    const int tid = threadIdx.x, lane = tid & 63, col = lane & 15, kq = lane >> 4, wave = tid >> 6;
+    const int wm = wave & 1, wn = wave >> 1;
+    const int ntn = (a.NP + G2_T - 1) / G2_T;
+    const int bid = xcd_block(blockIdx.x, gridDim.x);
+    const int n0 = (bid % ntn) * G2_T, p0 = (bid / ntn) * G2_T;
+    const int K = a.cinP;
+    const __bf16 *wg = reinterpret_cast<const __bf16 *>(a.w), *xg = reinterpret_cast<const __bf16 *>(a.in);
+    // this lane's glds sources: instruction i fills LDS rows wave * 32 + i * 8 + (lane >> 3), slot lane & 7
+    const __bf16 *sa[4], *sb[4];
+    int kc[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+        const int r = wave * 32 + i * 8 + (lane >> 3);
+        kc[i] = ((lane & 7) ^ ((r >> 1) & 7)) * 8;
+        sa[i] = wg + (size_t)min(n0 + r, a.NP - 1) * K;
+        sb[i] = xg + (size_t)min(p0 + r, a.M - 1) * a.CS;
+    }
+    auto stage = [&](int st, __bf16 *buf) {
+        const int k0 = st * G2_KT;
+        __bf16 *bA = buf + wave * 32 * G2_KT, *bB = bA + G2_T * G2_KT;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            const int k = k0 + kc[i];
+            glds16(sa[i] + (k < K ? k : 0), bA + i * 8 * G2_KT);
+            glds16(sb[i] + (k < a.CS ? k : 0), bB + i * 8 * G2_KT);
+        }
+    };
+    f32x4 acc[4][4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) acc[j][r] = (f32x4){0.f, 0.f, 0.f, 0.f};
+    auto compute = [&](int st, const __bf16 *bA) {
+        const __bf16 *bB = bA + G2_T * G2_KT;
+#pragma unroll
+        for (int s2 = 0; s2 < G2_KT / 32; ++s2) {
+            if (st * G2_KT + s2 * 32 >= K) break;              // (uniform) 32-channel tail stage
+            const int ch = s2 * 4 + kq;
+            u32x4 ra[4], rb[4];
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                const int row = wn * 64 + r * 16 + col;
+                ra[r] = lds_read16(bA + row * G2_KT + ((ch ^ ((row >> 1) & 7)) << 3));
+            }
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                const int row = wm * 64 + j * 16 + col;
+                rb[j] = lds_read16(bB + row * G2_KT + ((ch ^ ((row >> 1) & 7)) << 3));
+            }
+            lds_wait8(ra[0], ra[1], ra[2], ra[3], rb[0], rb[1], rb[2], rb[3]);
+            RawB wa[4], bx[4];
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                wa[r].v = __builtin_bit_cast(uint4, ra[r]);
+                bx[r].v = __builtin_bit_cast(uint4, rb[r]);
+            }
+#pragma unroll
+            for (int j = 0; j < 4; ++j)
+#pragma unroll
+                for (int r = 0; r < 4; ++r) mma(acc[j][r], wa[r], bx[j]);
+        }
+    };
+    const int nst = (K + G2_KT - 1) / G2_KT;
+    stage(0, sm0);
+    for (int st = 0; st < nst; st += 2) {
+        if (st + 1 < nst) {
+            stage(st + 1, sm1);
+            asm volatile("s_waitcnt vmcnt(8)" ::: "memory");   // this wave's 8 loads of stage st landed
+        } else {
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        }
+        __builtin_amdgcn_s_barrier();                          // ... and every other wave's
+        compute(st, sm0);
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        __builtin_amdgcn_s_barrier();                          // sm0 may be refilled (stage st + 2)
+        if (st + 1 >= nst) break;
+        if (st + 2 < nst) {
+            stage(st + 2, sm0);
+            asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+        } else {
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        }
+        __builtin_amdgcn_s_barrier();
+        compute(st + 1, sm1);
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        __builtin_amdgcn_s_barrier();
+    }
+    // epilogue (dl_gemm_kernel's, per wave: its 64 pixels x 64 channels, 32 pixels at a time)
+    const int nb = n0 + wn * 64;
+    if (nb >= a.NP) return;
+    float *stg = reinterpret_cast<float *>(sm0) + wave * 32 * DL_STG_RS;   // 4 x 8.7 KB of sm0 + sm1
+    const int c8 = (lane & 7) * 8;
+    const bool cok = nb + c8 < a.cout;
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+        if (h) wave_lds_sync();
+#pragma unroll
+        for (int jj = 0; jj < 2; ++jj) {
+            const int j = 2 * h + jj;
+            const int p = p0 + wm * 64 + j * 16 + col;
+            const int pimg = a.bias_img ? (int)fdiv((uint32_t)(p < a.M ? p : 0), a.mHW, a.sHW) : 0;
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                const int nl = r * 16 + kq * 4, n = nb + nl;
+                float4 v = add4(f4(acc[j][r]), ld4f(a.bias + n));
+                if (a.bias_img) v = add4(v, ld4f(a.bias_img + (size_t)pimg * a.bias_img_stride + n));
+                if (a.act >= 1) v = make_float4(fmaxf(v.x, 0.f), fmaxf(v.y, 0.f), fmaxf(v.z, 0.f), fmaxf(v.w, 0.f));
+                if (a.act == 2) v = make_float4(fminf(v.x, 6.f), fminf(v.y, 6.f), fminf(v.z, 6.f), fminf(v.w, 6.f));
+                *reinterpret_cast<float4 *>(stg + (jj * 16 + col) * DL_STG_RS + nl) = v;
+            }
+        }
+        wave_lds_sync();
+#pragma unroll
+        for (int it = 0; it < 4; ++it) {
+            const int pl = it * 8 + (lane >> 3);
+            const int p = p0 + wm * 64 + h * 32 + pl;
+            if (p >= a.M || !cok) continue;
+            float4 v0 = *reinterpret_cast<const float4 *>(stg + pl * DL_STG_RS + c8);
+            float4 v1 = *reinterpret_cast<const float4 *>(stg + pl * DL_STG_RS + c8 + 4);
+            const int n = nb + c8;
+            if (a.res) {
+                const __bf16 *rp = reinterpret_cast<const __bf16 *>(a.res) + (size_t)p * a.res_cs + n;
+                v0 = add4(v0, ld4(rp));
+                v1 = add4(v1, ld4(rp + 4));
+            }
+            if constexpr (OUTF32) {
+                float *o = reinterpret_cast<float *>(a.out) + (size_t)p * a.out_cs + a.out_off + n;
+                st4(o, v0);
+                st4(o + 4, v1);
+            } else {
+                __bf16 *o = reinterpret_cast<__bf16 *>(a.out) + (size_t)p * a.out_cs + a.out_off + n;
+                st4(o, v0);
+                st4(o + 4, v1);
+            }
+        }
+    }
+}
+
 // ------------------------------------------------------------------ depthwise 3x3
 // One thread = one output pixel x 8 channels; threads with consecutive ids take consecutive channel
 // groups of the same pixel (coalesced 16-B loads). Weights [9][C] f32 (already rounded to T's
@@ -858,8 +1039,24 @@ static bool gemm_ok(int prec, const DlConvArgs &a) {
            (size_t)a.NP * a.cinP * 2 < ((size_t)1 << 31);
 }
 
+// the 128 x 128 glds tile for deep, wide 1x1s (K >= 256 and 256+ output rows in whole 128-row tiles;
+// BUGSEG_DL_G128=0 turns it off). Measured (per-op HIP events): Xception's pointwise layers 3.14 ->
+// 2.60 ms per 16-frame forward (462 -> 558 TFLOP/s), the ASPP 1x1s 3% faster; MobileNetV2's
+// 576 / 960 -> 96..320 projections (HBM-bound, NP % 128 = 64) 1-8% slower, so they stay on
+// dl_gemm_kernel
+static bool gemm128_ok(const DlConvArgs &a) {
+    const char *e = std::getenv("BUGSEG_DL_G128");
+    return !(e && *e == '0') && a.cinP >= 256 && a.NP >= 256 && a.NP % 128 == 0 && a.CS % 8 == 0;
+}
+
 hipError_t dl_launch_conv(int prec, bool out_f32, const DlConvArgs &a, hipStream_t s) {
     const bool dwf = a.dw_w != nullptr;
+    if (gemm_ok(prec, a) && gemm128_ok(a)) {
+        const dim3 g(((a.M + G2_T - 1) / G2_T) * ((a.NP + G2_T - 1) / G2_T));
+        if (out_f32) hipLaunchKernelGGL(dl_gemm128_kernel<true>, g, dim3(256), 0, s, a);
+        else hipLaunchKernelGGL(dl_gemm128_kernel<false>, g, dim3(256), 0, s, a);
+        return hipGetLastError();
+    }
     if (gemm_ok(prec, a)) {
         const dim3 g(((a.M + GM_TM - 1) / GM_TM) * (a.NP / GM_TN));
         if (out_f32) hipLaunchKernelGGL(dl_gemm_kernel<true>, g, dim3(256), 0, s, a);

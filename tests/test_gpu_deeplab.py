@@ -253,3 +253,26 @@ def test_xception_from_frozen_graphdef(gpu, tmp_path, style):
     _check_fp32(model, model.net, x, torch.float64)
     lg = np.transpose(tf_graph.run(pb.read_bytes(), {"ImageTensor": x}, "logits"), (0, 3, 1, 2))
     assert np.abs(_gpu_logits(model) - lg).max() < LOGIT_TOL
+
+
+@pytest.mark.parametrize("which", ["mobilenet", "xception"])
+def test_deeplab_gemm128_bit_identical(gpu, monkeypatch, which):
+    """The 128 x 128 glds GEMM of the deep, wide 1x1s (K >= 256, N >= 256: the ASPP 1x1s and
+    projection, Xception's pointwise layers) against the 256 x 64 register-staged one
+    (BUGSEG_DL_G128=0): the same k-steps through the same MFMA in the same order -> identical logits
+    and class maps, over pixel tails, 32-channel k tails (cinP 736 = 11.5 stages), stored-channel
+    tails (CS 728 < cinP), output-channel tails (cout < NP), residual and per-image-bias epilogues."""
+    if which == "mobilenet":
+        net = S.build_deeplab(width=1.0, crop=97, atrous_rates=(6,))
+        x = _frames(3, 97, 90, 43)
+    else:
+        net = X.build_deeplab_xception(width=1.0, middle=1, crop=65)   # 728 channels: cinP 736 = 11.5 stages
+        x = _frames(2, 65, 60, 44)
+    a_model = DeepLabV3(net=net, precision="bf16")
+    a = a_model.predict(x)
+    la = a_model.logits_device().cpu()
+    monkeypatch.setenv("BUGSEG_DL_G128", "0")
+    b_model = DeepLabV3(net=net, precision="bf16")
+    b = b_model.predict(x)
+    assert torch.equal(la, b_model.logits_device().cpu())
+    assert np.array_equal(a, b)
