@@ -422,6 +422,9 @@ def main():
             log("deeplab sub-record")
             res["deeplab"] = bench_deeplab.record(dev, a.deeplab_batch, max(5, a.steps // 2), 3, "bf16",
                                                   cpu_seconds=0 if a.no_cpu_baseline else 6.0)
+            log("deeplab xception sub-record")
+            res["deeplab_xception"] = bench_deeplab.record(dev, 32, max(5, a.steps // 2), 3, "bf16",
+                                                           backbone="xception_65")
         if not a.no_cpu_baseline:
             res["cpu_baseline"] = cpu_baseline(blocks, bev, grid, H, W, a.cpu_baseline_seconds)
         print(json.dumps(res), flush=True)
