@@ -134,6 +134,12 @@ __global__ void __launch_bounds__((BShape<C, V>::NW * 64), (sizeof(T) == 2 ? BSh
 #ifndef BNECK_CH1_K2
 #define BNECK_CH1_K2 4
 #endif
+// k-steps of the symmetric middle conv unrolled together: 3 for C = 128 (9 k-steps; no spills, its
+// launches 1-4% faster), 1 elsewhere (down C64 6% slower at 3; 2 and 9 spill on C = 128).
+// -DBNECK_PH2_UNROLL=N forces one factor everywhere (A/B builds).
+#ifndef BNECK_PH2_UNROLL
+#define BNECK_PH2_UNROLL 0
+#endif
 #ifndef BNECK_REG3_C64
 #define BNECK_REG3_C64 0
 #endif
@@ -506,7 +512,8 @@ __global__ void __launch_bounds__((BShape<C, V>::NW * 64), (sizeof(T) == 2 ? BSh
             for (int j = 0; j < NF2; ++j)
 #pragma unroll
                 for (int r = 0; r < NR1; ++r) acc[j][r] = bias4(cb2 + r * 16 + kq * 4);
-#pragma unroll 1
+            constexpr int PH2U = BNECK_PH2_UNROLL > 0 ? BNECK_PH2_UNROLL : (C == 128 && !DN ? 3 : 1);
+#pragma unroll(PH2U)
             for (int s = 0; s < KS2; ++s) {
                 const int g = s * 4 + kq;
                 const int tap = g / (IS / 8), coff = (g - tap * (IS / 8)) * 8;
