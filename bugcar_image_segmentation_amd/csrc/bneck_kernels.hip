@@ -140,6 +140,9 @@ __global__ void __launch_bounds__((BShape<C, V>::NW * 64), (sizeof(T) == 2 ? BSh
 #ifndef BNECK_PH2_UNROLL
 #define BNECK_PH2_UNROLL 0
 #endif
+#ifndef BNECK_ASYM_UNROLL
+#define BNECK_ASYM_UNROLL 1    // k-steps of the asymmetric 5x1 / 1x5 passes unrolled together (A/B knob)
+#endif
 #ifndef BNECK_REG3_C64
 #define BNECK_REG3_C64 0
 #endif
@@ -547,7 +550,7 @@ __global__ void __launch_bounds__((BShape<C, V>::NW * 64), (sizeof(T) == 2 ? BSh
                 for (int j = 0; j < NF2A; ++j)
 #pragma unroll
                     for (int r = 0; r < NR1; ++r) acc[j][r] = bias4(cb2 + r * 16 + kq * 4);
-#pragma unroll 1
+#pragma unroll(BNECK_ASYM_UNROLL)
                 for (int s = 0; s < KS2; ++s) {
                     const int g = s * 4 + kq;
                     const int tap = g / (IS / 8), coff = (g - tap * (IS / 8)) * 8;
@@ -593,7 +596,7 @@ __global__ void __launch_bounds__((BShape<C, V>::NW * 64), (sizeof(T) == 2 ? BSh
                 for (int j = 0; j < NF2; ++j)
 #pragma unroll
                     for (int r = 0; r < NR1; ++r) acc[j][r] = bias4(cb2b + r * 16 + kq * 4);
-#pragma unroll 1
+#pragma unroll(BNECK_ASYM_UNROLL)
                 for (int s = 0; s < KS2; ++s) {
                     const int g = s * 4 + kq;
                     const int tap = g / (IS / 8), coff = (g - tap * (IS / 8)) * 8;
