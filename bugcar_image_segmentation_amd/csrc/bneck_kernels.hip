@@ -516,7 +516,7 @@ __global__ void __launch_bounds__((BShape<C, V>::NW * 64), (sizeof(T) == 2 ? BSh
 #pragma unroll
                 for (int r = 0; r < NR1; ++r) acc[j][r] = bias4(cb2 + r * 16 + kq * 4);
             constexpr int PH2U = BNECK_PH2_UNROLL > 0 ? BNECK_PH2_UNROLL : (C == 128 && !DN ? 3 : 1);
-#pragma unroll(PH2U)
+#pragma unroll PH2U
             for (int s = 0; s < KS2; ++s) {
                 const int g = s * 4 + kq;
                 const int tap = g / (IS / 8), coff = (g - tap * (IS / 8)) * 8;
@@ -550,7 +550,7 @@ __global__ void __launch_bounds__((BShape<C, V>::NW * 64), (sizeof(T) == 2 ? BSh
                 for (int j = 0; j < NF2A; ++j)
 #pragma unroll
                     for (int r = 0; r < NR1; ++r) acc[j][r] = bias4(cb2 + r * 16 + kq * 4);
-#pragma unroll(BNECK_ASYM_UNROLL)
+#pragma unroll BNECK_ASYM_UNROLL
                 for (int s = 0; s < KS2; ++s) {
                     const int g = s * 4 + kq;
                     const int tap = g / (IS / 8), coff = (g - tap * (IS / 8)) * 8;
@@ -596,7 +596,7 @@ __global__ void __launch_bounds__((BShape<C, V>::NW * 64), (sizeof(T) == 2 ? BSh
                 for (int j = 0; j < NF2; ++j)
 #pragma unroll
                     for (int r = 0; r < NR1; ++r) acc[j][r] = bias4(cb2b + r * 16 + kq * 4);
-#pragma unroll(BNECK_ASYM_UNROLL)
+#pragma unroll BNECK_ASYM_UNROLL
                 for (int s = 0; s < KS2; ++s) {
                     const int g = s * 4 + kq;
                     const int tap = g / (IS / 8), coff = (g - tap * (IS / 8)) * 8;

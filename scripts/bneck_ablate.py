@@ -18,7 +18,7 @@ frames = torch.from_numpy(synthetic.uniform_frames(B, H, W)).cuda()
 seg = torch.empty((B, H, W), dtype=torch.uint8, device="cuda")
 for flags in [int(v) for v in (sys.argv[1:] or ["0", "1", "2", "4", "7"])]:
     os.environ["BUGSEG_BNECK_ABLATE"] = str(flags)
-    m = ENET(weights=blocks, precision="bf16")
+    m = ENET(weights=blocks, precision=os.environ.get("BUGSEG_PREC", "fp16"))
     for _ in range(4):
         m.ctx.forward_bgr(frames, B, H, W, N.OUT_CLASS3_U8, seg)
     torch.cuda.synchronize()
