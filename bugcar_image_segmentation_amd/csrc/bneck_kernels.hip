@@ -30,6 +30,8 @@
 // MFMA operand mapping as conv_kernels.hip: A = weights (row = output channel) from LDS, B = 8
 // channels of one pixel (16-B LDS or global read per lane), accumulator = 4 consecutive channels of
 // one pixel per lane. All three weight matrices stay in LDS for the workgroup's lifetime.
+#include <cstdlib>
+
 #include "bugseg_internal.h"
 #include "mfma_common.h"
 
@@ -41,7 +43,11 @@ namespace bugseg {
 __device__ unsigned long long *bugseg_stamps;
 #define STAMP(k) do { if (tid == 0 && bugseg_stamps) bugseg_stamps[(size_t)tile * 8 + (k)] = __builtin_amdgcn_s_memtime(); } while (0)
 #define STAMP_WG() do { if (tid == 0 && bugseg_stamps) bugseg_stamps[(size_t)tile * 8 + 7] = blockIdx.x; } while (0)
+// per workgroup: kernel entry and exit on the constant 100 MHz clock (s_memrealtime: one time base
+// for every XCD) at [2^19 + 2 blockIdx.x (+1)]
+#define STAMP_ENTRY(k) do { if (threadIdx.x == 0 && bugseg_stamps) bugseg_stamps[(1u << 19) + 2u * blockIdx.x + (k)] = __builtin_amdgcn_s_memrealtime(); } while (0)
 #else
+#define STAMP_ENTRY(k) do {} while (0)
 #define STAMP(k) do {} while (0)
 #define STAMP_WG() do {} while (0)
 #endif
@@ -163,8 +169,34 @@ __global__ void __launch_bounds__((BShape<C, V>::NW * 64), (sizeof(T) == 2 ? BSh
     constexpr int OSTR = C + EPC;                     // staged epilogue: row stride (16-B padded)
     constexpr int RQ3 = !REG3 ? CPL : SWAP ? NR3 / 2 : NR3;   // residual chunks per lane per fragment
     static_assert(TW % 16 == 0, "a fragment is a run of one tile row");
+#ifndef BNECK_NBE
+#define BNECK_NBE -1     // border fragments loaded with the kept ones (-1: per form, see phase 1)
+#endif
+#ifndef BNECK_KEEP
+#define BNECK_KEEP 1
+#endif
+    // KEEP: the residual is the block input phase 1 already loaded. Phase 1 then walks the tile's
+    // interior as phase 3's fragments (a run of one tile row, on the wave that will expand it) and the
+    // halo border separately, and each wave keeps its interior fragments' x in registers through
+    // phase 2 instead of re-reading them (an L2 / Infinity-Cache round trip per fragment; PMC: the
+    // C128 launches fetched 1.67x their compulsory bytes with the re-read). 2-byte storage, symmetric
+    // plain blocks, with the staged (C = 64) or the row-pair-swapped (C = 128) epilogue.
+#ifndef BNECK_GLDS
+#define BNECK_GLDS 1
+#endif
+    constexpr bool GLDS = BNECK_GLDS;                 // weights staged by global_load_lds (see the staging)
+    constexpr bool KEEP = BNECK_KEEP && !DN && sizeof(T) == 2 && !ASYM && (SWAP || !REG3) &&
+                          NF2 * KS1 * 4 <= (C == 128 ? 48 : 32);   // kept VGPRs within the occupancy budget
+    static_assert(!KEEP || !REG3 || KS1 == RQ3, "kept x: one 16-B chunk per k-step and row pair");
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
 
+    STAMP_ENTRY(0);
+    // a workgroup without a tile leaves before staging anything (an LDS-DMA still in flight when
+    // its wave ends would land in LDS the next workgroup on the CU already owns)
+    {
+        const int ch = (a.ntiles + 7) >> 3, sl = (int)(blockIdx.x >> 3);
+        if (sl >= ch || (int)(blockIdx.x & 7) * ch + sl >= a.ntiles) return;   // (the tile walk's first tile)
+    }
     const int tid = threadIdx.x;
     const int lane = tid & 63, col = lane & 15, kq = lane >> 4;
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);   // provably uniform: scalar fragment math
@@ -204,7 +236,36 @@ __global__ void __launch_bounds__((BShape<C, V>::NW * 64), (sizeof(T) == 2 ? BSh
             if (i < N3) { r = i / CPR3; c = i - r * CPR3; src = (const uint4 *)a.w3 + i; dst = (unsigned char *)(w3 + r * K3S) + c * 16; return true; }
             return false;
         };
-        if constexpr (C == 16) {
+        if constexpr (GLDS) {
+            // global_load_lds: the weight region of LDS is a run of 16-B slots (rows of K?S elements:
+            // CPR? data chunks + the pad); each wave instruction fills 64 consecutive slots, a lane
+            // fetching its slot's chunk (pad slots re-read the row's first chunk: never read). No
+            // VGPR round trip and nothing waited for here: the loads fly with the first tile's x
+            // loads and the first tile waits for all of them before its first barrier.
+            (void)buf;
+            constexpr int ES = (int)sizeof(T);
+            constexpr int SR1 = (KS1 * 32 + PADW) * ES / 16, SR2 = (KS2 * 32 + PADW) * ES / 16, SR3 = (32 + PADW) * ES / 16;
+            constexpr int S1 = NR1 * 16 * SR1, S2 = NR1 * 16 * SR2, S3 = C * SR3;
+            constexpr int NSL = S1 + S2 * (ASYM ? 2 : 1) + S3;
+            static_assert((KS1 * 32 + PADW) * ES % 16 == 0 && (KS2 * 32 + PADW) * ES % 16 == 0 && (32 + PADW) * ES % 16 == 0,
+                          "weight rows are whole 16-B slots");
+            for (int base = wave * 64; base < NSL; base += NT) {      // wave-uniform
+                const int q = base + lane;
+                const uint4 *src;
+                auto pick = [&](const void *w, int k, int SR, int CPR) {   // slot k of one matrix
+                    const int r = k / SR, c = k - r * SR;
+                    src = (const uint4 *)w + r * CPR + (c < CPR ? c : 0);
+                };
+                constexpr int O3 = S1 + S2 * (ASYM ? 2 : 1);   // first slot of w3
+                if (q < S1) pick(a.w1, q, SR1, CPR1);
+                else if (q < S1 + S2) pick(a.w2, q - S1, SR2, CPR2);
+                else if (q < O3) pick(a.w2b, q - S1 - S2, SR2, CPR2);
+                else pick(a.w3, q - O3, SR3, CPR3);
+                if (base + lane < NSL)
+                    __builtin_amdgcn_global_load_lds((__attribute__((address_space(1))) void *)src,
+                                                     (__attribute__((address_space(3))) void *)(smem + (size_t)base * 16), 16, 0, 0);
+            }
+        } else if constexpr (C == 16) {
 #pragma unroll
             for (int k = 0; k < PER; ++k) {
                 const uint4 *src;
@@ -390,11 +451,109 @@ __global__ void __launch_bounds__((BShape<C, V>::NW * 64), (sizeof(T) == 2 ? BSh
             }
         };
         STAMP(0); STAMP_WG();
-        __syncthreads();   // weights staged (first tile) / previous tile done with ts
+        // the first tile waits for the glds weight staging (each wave its own loads, then the
+        // barrier makes every wave's visible); KEEP issues its x loads ahead of that wait
+        const bool first = it == slot;
+        if constexpr (!KEEP) {
+            if (GLDS && first) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            __syncthreads();   // weights staged (first tile) / previous tile done with ts
+        }
         STAMP(1);
 
         // ---- phase 1: t0 = act1(W1 x + b1) over tile + halo, 0 outside the image. The loads of CH1
         // fragments are issued together before any of them is consumed (memory-level parallelism).
+        Raw kx[KEEP ? NF2 : 1][KS1];                  // KEEP: this wave's interior fragments of x
+        if constexpr (KEEP) {
+            // every load of the wave's phase-1 work (its interior fragments, kept, and its share of
+            // the border) is issued before the first MFMA: one memory round trip per tile
+            constexpr int NBD = HR - NPX, NFB = (NBD + 15) / 16;   // border pixels / fragments
+            constexpr int NBW = (NFB + NW - 1) / NW;  // border fragments per wave (at most)
+            constexpr int B0 = NFT % NW;              // border fragment k runs on wave (B0 + k) % NW
+            // halo index of pixel pi of interior fragment f (tile pixel (i, j) = halo (i + RY, j + RX))
+            auto int_h = [&](int f) -> int {
+                const int p = f * 16 + col, i = p / TW, j = p - i * TW;
+                return (i + RY) * HWW + j + RX;
+            };
+            // halo index of border pixel b: the RY top and bottom halo rows, then the RX columns
+            // either side of the TH interior rows
+            auto bord_h = [&](int b) -> int {
+                if (b < 2 * RY * HWW) {
+                    const int r = b / HWW, c = b - r * HWW;
+                    return (r < RY ? r : TH + r) * HWW + c;
+                }
+                if constexpr (RX > 0) {
+                    const int bb = b - 2 * RY * HWW, r = bb / (2 * RX), c = bb - r * (2 * RX);
+                    return (RY + r) * HWW + (c < RX ? c : TW + c);
+                }
+                return 0;
+            };
+            auto load_h = [&](int h, bool valid, Raw (&xs)[KS1]) -> bool {
+                const int hy = h / HWW, hx = h - hy * HWW;
+                const int iy = oy0 + dt * ((tr ? hx : hy) - RY), ix = ox0 + dtx * ((tr ? hy : hx) - RX);
+                const bool ok = valid && (unsigned)iy < (unsigned)a.H && (unsigned)ix < (unsigned)a.W;
+#pragma unroll
+                for (int s = 0; s < KS1; ++s) {
+                    const int g = s * 4 + kq;
+                    bld8(xs[s], rxb, ok && g < G1 ? xn + ((__umul24((uint32_t)iy, (uint32_t)a.W) + (uint32_t)ix) * C + g * 8) * (uint32_t)sizeof(T) : OOB);
+                }
+                return ok;
+            };
+            auto proj = [&](int h, bool valid, bool ok, const Raw (&xs)[KS1]) {
+                f32x4 acc[NR1];
+#pragma unroll
+                for (int r = 0; r < NR1; ++r) acc[r] = bias4(cb1 + r * 16 + kq * 4);
+#pragma unroll
+                for (int s = 0; s < KS1; ++s)
+#pragma unroll
+                    for (int r = 0; r < NR1; ++r) {
+                        Raw wf;
+                        ld8(wf, w1 + (r * 16 + col) * K1S + s * 32 + kq * 8);
+                        mma(acc[r], wf, xs[s]);
+                    }
+                if (valid) {
+#pragma unroll
+                    for (int r = 0; r < NR1; ++r) {
+                        const int ch = r * 16 + kq * 4;
+                        if (ch >= IS) continue;
+                        float4 v = act(f4(acc[r]), cs1 + ch);
+                        if (!ok) v = make_float4(0.f, 0.f, 0.f, 0.f);
+                        st4(ts + h * PSTR + ch, v);
+                    }
+                }
+            };
+            bool kok[NF2];
+            Raw bx[NBW][KS1];
+            int bh[NBW];
+            bool bok[NBW];
+            const int wb = wave >= B0 ? wave - B0 : wave - B0 + NW;   // this wave's first border fragment
+#pragma unroll
+            for (int j = 0; j < NF2; ++j)
+                if (wave + NW * j < NFT) kok[j] = load_h(int_h(wave + NW * j), true, kx[j]);   // wave-uniform
+            auto load_b = [&](int k) {
+                const int b = (wb + NW * k) * 16 + col;
+                bh[k] = b < NBD ? bord_h(b) : 0;
+                bok[k] = load_h(bh[k], b < NBD, bx[k]);
+            };
+            // the first NBE border fragments fly with the interior ones; any further ones (a wave
+            // with two) are loaded after, which keeps the x registers within the occupancy budget
+            constexpr int NBE = BNECK_NBE >= 0 ? BNECK_NBE : C == 128 && !RD ? 1 : 0;   // C = 64 / 4x80: spills at 1
+#pragma unroll
+            for (int k = 0; k < NBE && k < NBW; ++k)
+                if (wb + NW * k < NFB) load_b(k);     // wave-uniform
+            // (x loads touch no LDS, so they go ahead of the barrier that frees ts)
+            if (GLDS && first) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            __syncthreads();   // weights staged (first tile) / previous tile done with ts
+#pragma unroll
+            for (int j = 0; j < NF2; ++j)
+                if (wave + NW * j < NFT) proj(int_h(wave + NW * j), true, kok[j], kx[j]);
+#pragma unroll
+            for (int k = 0; k < NBW; ++k) {
+                const int fb = wb + NW * k;
+                if (fb >= NFB) break;
+                if (k >= NBE) load_b(k);
+                proj(bh[k], fb * 16 + col < NBD, bok[k], bx[k]);
+            }
+        } else
         for (int f0 = wave; f0 < NF1; f0 += NW * CH1) {
             Raw xf[CH1][KS1];
             bool okc[CH1];
@@ -491,7 +650,7 @@ __global__ void __launch_bounds__((BShape<C, V>::NW * 64), (sizeof(T) == 2 ? BSh
 #pragma unroll
             for (int j = 0; j < RP; ++j) load_res(j, res[j]);
         };
-        if constexpr (!ASYM) prefetch_res();
+        if constexpr (!ASYM && !KEEP) prefetch_res();
 
         // t1 never goes through LDS: each wave's middle-conv accumulators (quads: lane kq holds channels
         // 4kq..4kq+3 of a pixel) are rounded as the unfused plan stores them and turned into the
@@ -515,7 +674,7 @@ __global__ void __launch_bounds__((BShape<C, V>::NW * 64), (sizeof(T) == 2 ? BSh
             for (int j = 0; j < NF2; ++j)
 #pragma unroll
                 for (int r = 0; r < NR1; ++r) acc[j][r] = bias4(cb2 + r * 16 + kq * 4);
-            constexpr int PH2U = BNECK_PH2_UNROLL > 0 ? BNECK_PH2_UNROLL : (C == 128 && !DN ? 3 : 1);
+            constexpr int PH2U = BNECK_PH2_UNROLL > 0 ? BNECK_PH2_UNROLL : (C == 128 && !DN && !(KEEP && V == 2) ? 3 : 1);
 #pragma unroll PH2U
             for (int s = 0; s < KS2; ++s) {
                 const int g = s * 4 + kq;
@@ -638,12 +797,19 @@ __global__ void __launch_bounds__((BShape<C, V>::NW * 64), (sizeof(T) == 2 ? BSh
 #pragma unroll
             for (int j = 0; j < NF2; ++j) {
                 if (wave + NW * j >= NFT) break;          // wave-uniform
+                if constexpr (KEEP) {
+                    // the kept x: lane (col, kq) holds channels 8 (4 s + kq) .. + 7 of pixel col
 #pragma unroll
-                for (int k = 0; k < CPL; ++k) {
-                    const int q = lane + 64 * k;
-                    if (q < CPF) *reinterpret_cast<uint4 *>(stg + (q / CPP) * OSTR + (q % CPP) * EPC) = res[j % RP][k];
+                    for (int s = 0; s < KS1; ++s)
+                        if (s * 4 + kq < G1) *reinterpret_cast<uint4 *>(stg + col * OSTR + (s * 4 + kq) * EPC) = kx[j][s].v;
+                } else {
+#pragma unroll
+                    for (int k = 0; k < CPL; ++k) {
+                        const int q = lane + 64 * k;
+                        if (q < CPF) *reinterpret_cast<uint4 *>(stg + (q / CPP) * OSTR + (q % CPP) * EPC) = res[j % RP][k];
+                    }
+                    if (j + RP < NF2 && wave + NW * (j + RP) < NFT) load_res(j + RP, res[j % RP]);
                 }
-                if (j + RP < NF2 && wave + NW * (j + RP) < NFT) load_res(j + RP, res[j % RP]);
                 wave_lds_sync();
 #pragma unroll
                 for (int r = 0; r < NR3; ++r) {
@@ -683,7 +849,9 @@ __global__ void __launch_bounds__((BShape<C, V>::NW * 64), (sizeof(T) == 2 ? BSh
 #pragma unroll
             for (int t = 0; t < RQ3; ++t) {
                 const uint32_t off = po == OOB ? OOB : po + (uint32_t)chunk_ch(t) * (uint32_t)sizeof(T);
-                const uint4 rc = res[j % RP][t];
+                uint4 rc;
+                if constexpr (KEEP) rc = kx[j][t].v;
+                else rc = res[j % RP][t];
                 if constexpr (SWAP) {
                     const int r0 = 2 * t, r1 = 2 * t + 1;
                     f32x4 acc0 = bias_in_acc(NR3, 1) ? bias4(cb3 + r0 * 16 + kq * 4) : (f32x4){0.f, 0.f, 0.f, 0.f};
@@ -695,8 +863,19 @@ __global__ void __launch_bounds__((BShape<C, V>::NW * 64), (sizeof(T) == 2 ? BSh
                     mma(acc1, w1, tf[j]);
                     // residual chunk -> quads of rows r0 / r1
                     uint32_t a0 = rc.x, a1 = rc.y, b0 = rc.z, b1 = rc.w;
-                    pl16swap(a0, b0);
-                    pl16swap(a1, b1);
+                    if constexpr (KEEP) {
+                        // kept x (lane kq: channels 32 t + 8 kq .. + 7, dwords d0..d3): row r0's quad
+                        // of lane kq lives in lane kq / 2 (d0, d1 or d2, d3), row r1's in lane 2 + kq / 2;
+                        // a row swap then a half swap of (d0, d2) and of (d1, d3) gathers both
+                        a0 = rc.x; b0 = rc.z; a1 = rc.y; b1 = rc.w;
+                        pl16swap(a0, b0);
+                        pl32swap(a0, b0);
+                        pl16swap(a1, b1);
+                        pl32swap(a1, b1);
+                    } else {
+                        pl16swap(a0, b0);
+                        pl16swap(a1, b1);
+                    }
                     float4 v0 = act(add4(out3(r0, acc0), unpack4<T>((u32x2_t){a0, a1})), cso + r0 * 16 + kq * 4);
                     float4 v1 = act(add4(out3(r1, acc1), unpack4<T>((u32x2_t){b0, b1})), cso + r1 * 16 + kq * 4);
                     u32x2_t p0 = pack4<T>(v0), p1 = pack4<T>(v1);
@@ -719,10 +898,12 @@ __global__ void __launch_bounds__((BShape<C, V>::NW * 64), (sizeof(T) == 2 ? BSh
                     }
                 }
             }
-            if (j + RP < NF2 && wave + NW * (j + RP) < NFT) load_res(j + RP, res[j % RP]);
+            if constexpr (!KEEP)
+                if (j + RP < NF2 && wave + NW * (j + RP) < NFT) load_res(j + RP, res[j % RP]);
         }
         STAMP(6);
     }
+    STAMP_ENTRY(1);
 }
 
 #ifdef BUGSEG_STAMPS
@@ -791,6 +972,12 @@ static hipError_t allow_lds(const void *f) {
 }
 
 int bneck_slots_per_cu(int prec, int C, bool asym, int v, bool tr, int cin) {
+    // cached per form (launch_bneck asks on every launch)
+    static int cache[3][3][2][4][2][3];
+    const int pi = prec == PREC_BF16 ? 0 : prec == PREC_F16 ? 1 : 2, ci = C == 128 ? 0 : C == 64 ? 1 : 2;
+    const int ii = cin == 0 ? 0 : cin == 16 ? 1 : 2;
+    int &slot = cache[pi][ci][asym][v & 3][tr][ii];
+    if (slot > 0) return slot;
     const void *f = bneck_fun(prec, C, asym, v, tr, cin);
     int th, tw, nw;
     bneck_shape(C, v, th, tw, nw, nullptr);
@@ -798,7 +985,7 @@ int bneck_slots_per_cu(int prec, int C, bool asym, int v, bool tr, int cin) {
     int n = 0;
     if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, f, nw * 64, bneck_lds_bytes(prec, C, asym, v, cin)) != hipSuccess)
         return 0;
-    return n;
+    return slot = n;
 }
 
 hipError_t launch_bneck(int prec, int C, bool asym, int v, const BneckArgs &a, hipStream_t s, int cin) {
@@ -811,7 +998,22 @@ hipError_t launch_bneck(int prec, int C, bool asym, int v, const BneckArgs &a, h
         hipError_t e = allow_lds(f);
         if (e != hipSuccess) return e;
     }
-    int g = a.ntiles < 2048 ? a.ntiles : 2048;
+    // grid: one round of resident workgroups (each walks ntiles / grid tiles, staging its weights
+    // once), or the earlier fixed cap of 2048 (BUGSEG_BNECK_GRID=cap: A/B knob, 0 = resident slots)
+    static int grid_cap = -1, n_cu = 0;
+    if (grid_cap < 0) {
+        const char *e = std::getenv("BUGSEG_BNECK_GRID");
+        grid_cap = e ? std::atoi(e) : 0;
+        int dev = 0;
+        if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&n_cu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
+            n_cu = 0;
+    }
+    int cap = grid_cap;
+    if (cap <= 0) {
+        const int spc = bneck_slots_per_cu(prec, C, asym, v, a.tr != 0, cin);
+        cap = spc > 0 && n_cu > 0 ? spc * n_cu : 2048;
+    }
+    int g = a.ntiles < cap ? a.ntiles : cap;
     g = (g + 7) & ~7;
     void *args[] = {const_cast<BneckArgs *>(&a)};
     return hipLaunchKernel(f, dim3(g), dim3(nw * 64), args, lds, s);

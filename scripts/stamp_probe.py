@@ -56,7 +56,11 @@ for i in range(n):
     torch.cuda.synchronize()
     assert lib.bugseg_debug_set_stamps(ctypes.c_void_p(0)) == 0
     us = ev[0].elapsed_time(ev[1]) * 1e3
-    s = stamps.cpu().numpy().reshape(-1, 8)
+    allst = stamps.cpu().numpy()
+    ent = allst[1 << 19:].reshape(-1, 2)
+    nwg = int((ent[:, 0] != 0).sum())
+    ent = ent[:nwg]
+    s = allst[:1 << 19].reshape(-1, 8)
     s = s[s[:, 0] != 0]
     d = np.diff(s[:, :7], axis=1).astype(np.float64)
     names = ["wait0", "ph1", "bar1", "ph2", "mid", "ph3"]
@@ -70,6 +74,16 @@ for i in range(n):
         if len(sx):
             spans.append(sx[:, 6].max() - sx[:, 0].min())
     tile_cyc = (s[:, 6] - s[:, 0]).mean()
+    # entry / exit of every workgroup on the 100 MHz real-time clock, from the first entry (us)
+    e = (ent[:, 0] - ent[:, 0].min()) / 100.0
+    x = (ent[:, 1] - ent[:, 0].min()) / 100.0
+    life = x - e
+    print(f"     realtime: entry p50/p90/max {np.percentile(e, 50):.1f}/{np.percentile(e, 90):.1f}/{e.max():.1f} us  "
+          f"WG life p10/p50/p90 {np.percentile(life, 10):.1f}/{np.percentile(life, 50):.1f}/{np.percentile(life, 90):.1f}  "
+          f"exit p10/p50/p90/max {np.percentile(x, 10):.1f}/{np.percentile(x, 50):.1f}/{np.percentile(x, 90):.1f}/{x.max():.1f} us", flush=True)
+    h, _ = np.histogram(e, bins=10, range=(0, x.max()))
+    hx, _ = np.histogram(x, bins=10, range=(0, x.max()))
+    print(f"     entries per tenth of the span: {h.tolist()}  exits: {hx.tolist()}", flush=True)
     print(f"op {i:2d} {tag:16s} B={B}: {len(s)} tiles on {len(per_wg)} WGs ({per_wg.min()}-{per_wg.max()} tiles/WG); "
           f"{us:.1f} us; span {np.mean(spans):.0f} cyc -> {np.mean(spans) / us / 1e3:.2f} GHz; tile {tile_cyc:.0f} cyc", flush=True)
     print("     " + "  ".join(f"{nm}={d[:, k].mean():7.0f} (p90 {np.percentile(d[:, k], 90):7.0f})" for k, nm in enumerate(names)), flush=True)
