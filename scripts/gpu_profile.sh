@@ -6,7 +6,7 @@ set -o pipefail
 cd $GRAFT_REPO_ROOT
 export TMPDIR=/tmp
 TAG=${1:-prof}; shift
-ARGS="--steps 20 --warmup 5 --no-cpu-baseline $*"
+ARGS="--steps 20 --warmup 5 --no-cpu-baseline --extras 0 $*"
 mkdir -p gpurun_out/$TAG
 timeout -k 10 300 python3 bench.py $ARGS > gpurun_out/$TAG/bench.json 2> gpurun_out/$TAG/bench.err || exit 1
 timeout -k 10 400 rocprofv3 --kernel-trace --stats -d gpurun_out/$TAG/trace -o run --output-format csv -- python3 bench.py $ARGS > gpurun_out/$TAG/trace.log 2>&1 || exit 1
