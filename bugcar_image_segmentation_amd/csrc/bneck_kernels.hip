@@ -52,6 +52,17 @@ __device__ unsigned long long *bugseg_stamps;
 #define STAMP_WG() do {} while (0)
 #endif
 
+// s_waitcnt vmcnt(n) for a wave-uniform n (the immediate has to be a constant): waits until at most n
+// of this wave's vector-memory operations are outstanding. n is clamped to 0..24 in steps of 2.
+__device__ __forceinline__ void vm_wait_upto(int n) {
+#define VMW(k) case k: asm volatile("s_waitcnt vmcnt(" #k ")" ::: "memory"); break;
+    switch (n) {
+        VMW(2) VMW(4) VMW(6) VMW(8) VMW(10) VMW(12) VMW(14) VMW(16) VMW(18) VMW(20) VMW(22) VMW(24)
+        default: asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); break;
+    }
+#undef VMW
+}
+
 // Tile shape variants per channel count: TH x TW tile pixels, NW waves per workgroup, OCC = waves
 // per SIMD the bf16 build is held to (registers), matching what LDS allows. 128 channels: the LDS
 // footprint (weights + halo or output staging, ~75 KB) allows two workgroups per CU, so they are
@@ -184,11 +195,17 @@ __global__ void __launch_bounds__((BShape<C, V>::NW * 64), (sizeof(T) == 2 ? BSh
 #ifndef BNECK_GLDS
 #define BNECK_GLDS 1
 #endif
+#ifndef BNECK_GLDS_PARTIAL
+#define BNECK_GLDS_PARTIAL 1   // KEEP: the first tile waits for the weights only, not for its x loads
+#endif
     constexpr bool GLDS = BNECK_GLDS;                 // weights staged by global_load_lds (see the staging)
+#ifndef BNECK_KEEP_ASYM
+#define BNECK_KEEP_ASYM 0
+#endif
 #ifndef BNECK_KEEP_C64
 #define BNECK_KEEP_C64 0    // C = 64: measured 41.0 vs 38.0 us per launch with the residual kept (wave 0 takes a third load round trip for its second border fragment; batching it spills)
 #endif
-    constexpr bool KEEP = BNECK_KEEP && !DN && sizeof(T) == 2 && !ASYM && (SWAP || !REG3) && (C != 64 || BNECK_KEEP_C64) &&
+    constexpr bool KEEP = BNECK_KEEP && !DN && sizeof(T) == 2 && (!ASYM || BNECK_KEEP_ASYM) && (SWAP || !REG3) && (C != 64 || BNECK_KEEP_C64) &&
                           NF2 * KS1 * 4 <= (C == 128 ? 48 : 32);   // kept VGPRs within the occupancy budget
     static_assert(!KEEP || !REG3 || KS1 == RQ3, "kept x: one 16-B chunk per k-step and row pair");
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
@@ -539,13 +556,25 @@ __global__ void __launch_bounds__((BShape<C, V>::NW * 64), (sizeof(T) == 2 ? BSh
             };
             // the first NBE border fragments fly with the interior ones; any further ones (a wave
             // with two) are loaded after, which keeps the x registers within the occupancy budget
-            constexpr int NBE = BNECK_NBE >= 0 ? BNECK_NBE : C == 128 && !RD ? 1 : 0;   // C = 64 / 4x80: spills at 1
+            constexpr int NBE = BNECK_NBE >= 0 ? BNECK_NBE : C == 128 && !RD && !ASYM ? 1 : 0;   // C = 64 / 4x80: spills at 1
 #pragma unroll
             for (int k = 0; k < NBE && k < NBW; ++k)
                 if (wb + NW * k < NFB) load_b(k);     // wave-uniform
-            // (x loads touch no LDS, so they go ahead of the barrier that frees ts)
-            if (GLDS && first) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-            __syncthreads();   // weights staged (first tile) / previous tile done with ts
+            // (x loads touch no LDS, so they go ahead of the barrier that frees ts). The first tile
+            // waits for the weight LDS-DMA only: it was issued before this wave's x loads, and vmcnt
+            // retires in order, so "at most nld outstanding" leaves the x loads in flight for the
+            // projections to consume one fragment at a time
+            if (GLDS && first) {
+                int nld = 0;
+#pragma unroll
+                for (int j = 0; j < NF2; ++j) nld += wave + NW * j < NFT ? KS1 : 0;
+#pragma unroll
+                for (int k = 0; k < NBE && k < NBW; ++k) nld += wb + NW * k < NFB ? KS1 : 0;
+                vm_wait_upto(BNECK_GLDS_PARTIAL ? nld : 0);
+            }
+            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+            __builtin_amdgcn_s_barrier();   // weights staged (first tile) / previous tile done with ts
+            asm volatile("" ::: "memory");
 #pragma unroll
             for (int j = 0; j < NF2; ++j)
                 if (wave + NW * j < NFT) proj(int_h(wave + NW * j), true, kok[j], kx[j]);
@@ -777,7 +806,7 @@ __global__ void __launch_bounds__((BShape<C, V>::NW * 64), (sizeof(T) == 2 ? BSh
                         for (int r = 0; r < NR1; ++r) mma(acc[j][r], wf[r], xf);
                     }
                 }
-                prefetch_res();
+                if constexpr (!KEEP) prefetch_res();
                 to_tf(acc, cs2b);
             }
         }
