@@ -19,4 +19,4 @@ for n in args:
     d = json.loads([ln for ln in p.read_text().splitlines() if ln.startswith('{"metric"')][-1])
     ks = d["kernels"]
     print(f"{n:12s} {d['value']:9.1f} f/s  {d['ms_per_step']:.4f} ms/step  fwd {d['stages_ms']['enet_forward']:.4f} ms  " +
-          "  ".join(f"{t.split()[1]}{t.split()[2] if len(t.split()) > 2 else ''} {ks[t]['us_per_launch']:.2f}" for t in tags if t in ks))
+          "  ".join(f"[{t}] {ks[t]['us_per_launch']:.2f}" for t in tags if t in ks))

@@ -529,6 +529,24 @@ def test_full_size_batch_properties(bf16_model):
         assert torch.equal(single[0], a[i])
 
 
+@pytest.mark.parametrize("prec", ["fp16", "bf16"])
+def test_multi_tile_workgroups_batch_independent(gpu, blocks, prec):
+    """B = 48 at 480x640: more bottleneck tiles than resident workgroup slots (C128: 720 tiles on
+    512 slots, C64: 3,840 on 1,280), so workgroups walk several tiles — the later tiles of a walk skip
+    the weight-staging wait and the kept-residual forms issue their loads ahead of the ts barrier.
+    Every frame's logits equal its single-frame forward bit for bit."""
+    H, W, B = 480, 640, 48
+    m = ENET(weights=blocks, precision=prec)
+    frames = torch.from_numpy(synthetic.road_frames(B, H, W, seed=11)).cuda()
+    out = torch.empty((B, 15, H, W), dtype=torch.float32, device=gpu)
+    m.ctx.forward_bgr(frames, B, H, W, N.OUT_LOGITS_F32, out)
+    one = torch.empty((1, 15, H, W), dtype=torch.float32, device=gpu)
+    for i in (0, 23, 47):
+        m.ctx.forward_bgr(frames[i:i + 1].contiguous(), 1, H, W, N.OUT_LOGITS_F32, one)
+        torch.cuda.synchronize()
+        assert torch.equal(one[0], out[i]), i
+
+
 def test_errors_are_loud(gpu, blocks):
     m = ENET(weights=blocks, precision="fp32")
     with pytest.raises(ValueError):
