@@ -195,6 +195,9 @@ __global__ void __launch_bounds__((BShape<C, V>::NW * 64), (sizeof(T) == 2 ? BSh
 #ifndef BNECK_GLDS
 #define BNECK_GLDS 1
 #endif
+#ifndef BNECK_CONST_GLDS
+#define BNECK_CONST_GLDS 1   // epilogue constants by LDS-DMA: 0 off, 1 for C != 128 (C64 38.0 -> 36.5 us; C128 23.1 -> 23.5), 2 all
+#endif
 #ifndef BNECK_GLDS_PARTIAL
 #define BNECK_GLDS_PARTIAL 1   // KEEP: the first tile waits for the weights only, not for its x loads
 #endif
@@ -306,11 +309,32 @@ __global__ void __launch_bounds__((BShape<C, V>::NW * 64), (sizeof(T) == 2 ? BSh
                 if (locate(i, src, dst)) *reinterpret_cast<uint4 *>(dst) = *src;
             }
         }
-        for (int i = tid; i < NP1; i += NT) {
-            cb1[i] = a.b1[i]; cs1[i] = a.s1[i]; cb2[i] = a.b2[i]; cs2[i] = a.s2[i];
-            cb2b[i] = ASYM ? a.b2b[i] : 0.f; cs2b[i] = ASYM ? a.s2b[i] : 0.f;
+        if constexpr (GLDS && (BNECK_CONST_GLDS == 2 || (BNECK_CONST_GLDS == 1 && C != 128))) {
+            // the epilogue constants by LDS-DMA as well (one dword per lane, 64 per instruction,
+            // spread over the waves): a plain load -> LDS store here would wait (vmcnt, in order)
+            // for the weight DMA issued above and serialise the staging ahead of the x loads
+            const float *srcs[9] = {a.b1, a.s1, a.b2, a.s2, a.b2b, a.s2b, a.b3, a.s3, a.s_out};
+            float *dsts[9] = {cb1, cs1, cb2, cs2, cb2b, cs2b, cb3, cs3, cso};
+            int item = 0;
+#pragma unroll
+            for (int k = 0; k < 9; ++k) {
+                if (!ASYM && (k == 4 || k == 5)) continue;          // unused without the 1x5 pass
+                const int n = k < 6 ? NP1 : C;
+#pragma unroll
+                for (int c0 = 0; c0 < n; c0 += 64, ++item) {
+                    if (item % NW != wave) continue;                // wave-uniform
+                    if (c0 + lane < n)
+                        __builtin_amdgcn_global_load_lds((__attribute__((address_space(1))) void *)(srcs[k] + c0 + lane),
+                                                         (__attribute__((address_space(3))) void *)(dsts[k] + c0), 4, 0, 0);
+                }
+            }
+        } else {
+            for (int i = tid; i < NP1; i += NT) {
+                cb1[i] = a.b1[i]; cs1[i] = a.s1[i]; cb2[i] = a.b2[i]; cs2[i] = a.s2[i];
+                cb2b[i] = ASYM ? a.b2b[i] : 0.f; cs2b[i] = ASYM ? a.s2b[i] : 0.f;
+            }
+            for (int i = tid; i < C; i += NT) { cb3[i] = a.b3[i]; cs3[i] = a.s3[i]; cso[i] = a.s_out[i]; }
         }
-        for (int i = tid; i < C; i += NT) { cb3[i] = a.b3[i]; cs3[i] = a.s3[i]; cso[i] = a.s_out[i]; }
         if (tid < 16) zpad[tid] = (T)0.f;
     }
     // x / out through buffer descriptors: 32-bit offsets, and an out-of-range offset reads 0 / drops
