@@ -163,7 +163,11 @@ __global__ void __launch_bounds__((BShape<C, V>::NW * 64), (sizeof(T) == 2 ? BSh
 #ifndef BNECK_REG3_C64
 #define BNECK_REG3_C64 0
 #endif
-    constexpr int CH1 = KS1 >= 8 ? 1 : KS1 >= 4 ? (NF1 + NW - 1) / NW : KS1 == 2 ? BNECK_CH1_K2 : 8;   // phase-1 fragments whose loads fly together
+#ifndef BNECK_CH1_C64
+#define BNECK_CH1_C64 4
+#endif
+    constexpr int CH1 = KS1 >= 8 ? 1 : KS1 >= 4 ? (NF1 + NW - 1) / NW
+                      : KS1 == 2 ? (C == 64 && V == 0 && !DN && !ASYM ? BNECK_CH1_C64 : BNECK_CH1_K2) : 8;   // phase-1 fragments whose loads fly together
     // phase-3 chunking (see phase 3): bf16 with an even number of 16-row blocks swaps row pairs
     // into 16-B chunks; bf16 C = 16 stores 8-B quads (HALF); fp32 quads are 16-B chunks
     // REG3: the register epilogue (C = 128 and 16). C = 64 keeps the LDS-staged epilogue: its 128-B
