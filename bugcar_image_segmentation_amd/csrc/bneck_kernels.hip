@@ -164,7 +164,7 @@ __global__ void __launch_bounds__((BShape<C, V>::NW * 64), (sizeof(T) == 2 ? BSh
 #define BNECK_REG3_C64 0
 #endif
 #ifndef BNECK_CH1_C64
-#define BNECK_CH1_C64 4
+#define BNECK_CH1_C64 6   // the symmetric 16x16 C64 form: all of a wave's 5-6 phase-1 fragments in one round trip (37.3 -> 36.0 us)
 #endif
     constexpr int CH1 = KS1 >= 8 ? 1 : KS1 >= 4 ? (NF1 + NW - 1) / NW
                       : KS1 == 2 ? (C == 64 && V == 0 && !DN && !ASYM ? BNECK_CH1_C64 : BNECK_CH1_K2) : 8;   // phase-1 fragments whose loads fly together
