@@ -149,7 +149,7 @@ __global__ void __launch_bounds__((BShape<C, V>::NW * 64), (sizeof(T) == 2 ? BSh
     constexpr int NFA = (NPA + 15) / 16;
     constexpr int NF2A = (NFA + NW - 1) / NW;
 #ifndef BNECK_CH1_K2
-#define BNECK_CH1_K2 4
+#define BNECK_CH1_K2 5   // down C64: 49.9 -> 49.4 us at 5 (one spill); 6 spills 22
 #endif
 // k-steps of the symmetric middle conv unrolled together: 3 for C = 128 (9 k-steps; no spills, its
 // launches 1-4% faster), 1 elsewhere (down C64 6% slower at 3; 2 and 9 spill on C = 128).
@@ -166,7 +166,10 @@ __global__ void __launch_bounds__((BShape<C, V>::NW * 64), (sizeof(T) == 2 ? BSh
 #ifndef BNECK_CH1_C64
 #define BNECK_CH1_C64 6   // the symmetric 16x16 C64 form: all of a wave's 5-6 phase-1 fragments in one round trip (37.3 -> 36.0 us)
 #endif
-    constexpr int CH1 = KS1 >= 8 ? 1 : KS1 >= 4 ? (NF1 + NW - 1) / NW
+#ifndef BNECK_CH1_K8
+#define BNECK_CH1_K8 1
+#endif
+    constexpr int CH1 = KS1 >= 8 ? BNECK_CH1_K8 : KS1 >= 4 ? (NF1 + NW - 1) / NW
                       : KS1 == 2 ? (C == 64 && V == 0 && !DN && !ASYM ? BNECK_CH1_C64 : BNECK_CH1_K2) : 8;   // phase-1 fragments whose loads fly together
     // phase-3 chunking (see phase 3): bf16 with an even number of 16-row blocks swaps row pairs
     // into 16-B chunks; bf16 C = 16 stores 8-B quads (HALF); fp32 quads are 16-B chunks
