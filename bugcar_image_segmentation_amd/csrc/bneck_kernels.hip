@@ -79,7 +79,11 @@ template <> struct BShape<128, 0> { static constexpr int TH = 16, TW = 16, NW = 
 template <> struct BShape<128, 1> { static constexpr int TH = 20, TW = 16, NW = 8, OCC = 4, RP = 2, RD = 0, WIDE = 1; };
 template <> struct BShape<128, 2> { static constexpr int TH = 4, TW = 80, NW = 8, OCC = 4, RP = 2, RD = 1, WIDE = 0; };
 template <> struct BShape<128, 3> { static constexpr int TH = 4, TW = 64, NW = 8, OCC = 4, RP = 2, RD = 1, WIDE = 1; };
+// 8 x 16: the small-batch forms (batch 1: 40 C128 tiles at 60 x 80 instead of 15; 150 C64 tiles at
+// 120 x 160 instead of 80), picked by the runtime's round model only when whole rounds are few
+template <> struct BShape<128, 4> { static constexpr int TH = 8, TW = 16, NW = 8, OCC = 4, RP = 1, RD = 0, WIDE = 1; };
 template <> struct BShape<64, 0> { static constexpr int TH = 16, TW = 16, NW = 4, OCC = 5, RP = 4, RD = 0, WIDE = 1; };
+template <> struct BShape<64, 2> { static constexpr int TH = 8, TW = 16, NW = 4, OCC = 5, RP = 2, RD = 0, WIDE = 1; };
 template <> struct BShape<64, 1> { static constexpr int TH = 20, TW = 16, NW = 4, OCC = 5, RP = 3, RD = 0, WIDE = 1; };
 template <> struct BShape<16, 0> { static constexpr int TH = 16, TW = 16, NW = 4, OCC = 6, RP = 4, RD = 0, WIDE = 1; };
 
@@ -94,16 +98,16 @@ __host__ __device__ constexpr int bneck_pstr(int es, int IS, bool wide) {
 }
 static bool bneck_wide(int C, int v, bool asym) {
 #define BW_CASE(CC, VV) if (C == CC && v == VV) return BShape<CC, VV>::WIDE && !asym;
-    BW_CASE(128, 0) BW_CASE(128, 1) BW_CASE(128, 2) BW_CASE(128, 3) BW_CASE(64, 0) BW_CASE(64, 1) BW_CASE(16, 0)
+    BW_CASE(128, 0) BW_CASE(128, 1) BW_CASE(128, 2) BW_CASE(128, 3) BW_CASE(128, 4) BW_CASE(64, 0) BW_CASE(64, 1) BW_CASE(64, 2) BW_CASE(16, 0)
 #undef BW_CASE
     return false;
 }
 
-int bneck_variants(int C) { return C == 128 ? 4 : C == 64 ? 2 : 1; }
+int bneck_variants(int C) { return C == 128 ? 5 : C == 64 ? 3 : 1; }
 
 void bneck_shape(int C, int v, int &th, int &tw, int &nw, int *rd) {
 #define BS_CASE(CC, VV) if (C == CC && v == VV) { th = BShape<CC, VV>::TH; tw = BShape<CC, VV>::TW; nw = BShape<CC, VV>::NW; if (rd) *rd = BShape<CC, VV>::RD; return; }
-    BS_CASE(128, 0) BS_CASE(128, 1) BS_CASE(128, 2) BS_CASE(128, 3) BS_CASE(64, 0) BS_CASE(64, 1) BS_CASE(16, 0)
+    BS_CASE(128, 0) BS_CASE(128, 1) BS_CASE(128, 2) BS_CASE(128, 3) BS_CASE(128, 4) BS_CASE(64, 0) BS_CASE(64, 1) BS_CASE(64, 2) BS_CASE(16, 0)
 #undef BS_CASE
     th = tw = nw = 0;
     if (rd) *rd = 0;
@@ -997,7 +1001,7 @@ template <typename T>
 static const void *kfun(int C, bool asym, int v, bool tr) {
 #define BK_CASE(CC, VV) \
     if (C == CC && v == VV && !tr) return asym ? (const void *)bneck_kernel<T, CC, true, VV, false> : (const void *)bneck_kernel<T, CC, false, VV, false>;
-    BK_CASE(128, 0) BK_CASE(128, 1) BK_CASE(64, 0) BK_CASE(64, 1) BK_CASE(16, 0)
+    BK_CASE(128, 0) BK_CASE(128, 1) BK_CASE(128, 4) BK_CASE(64, 0) BK_CASE(64, 1) BK_CASE(64, 2) BK_CASE(16, 0)
 #undef BK_CASE
     if (C == 128 && v == 1 && tr && !asym) return (const void *)bneck_kernel<T, 128, false, 1, true>;
     if (C == 128 && v == 2 && !tr && !asym) return (const void *)bneck_kernel<T, 128, false, 2, false>;
@@ -1036,10 +1040,10 @@ static hipError_t allow_lds(const void *f) {
 
 int bneck_slots_per_cu(int prec, int C, bool asym, int v, bool tr, int cin) {
     // cached per form (launch_bneck asks on every launch)
-    static int cache[3][3][2][4][2][3];
+    static int cache[3][3][2][8][2][3];
     const int pi = prec == PREC_BF16 ? 0 : prec == PREC_F16 ? 1 : 2, ci = C == 128 ? 0 : C == 64 ? 1 : 2;
     const int ii = cin == 0 ? 0 : cin == 16 ? 1 : 2;
-    int &slot = cache[pi][ci][asym][v & 3][tr][ii];
+    int &slot = cache[pi][ci][asym][v & 7][tr][ii];
     if (slot > 0) return slot;
     const void *f = bneck_fun(prec, C, asym, v, tr, cin);
     int th, tw, nw;

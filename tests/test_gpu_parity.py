@@ -280,7 +280,7 @@ def test_forward_bgr_equals_preprocess_then_forward(gpu, prec, pool_k):
     assert torch.equal(m.predict_device(x2, N.OUT_LOGITS_F32), c)
 
 
-@pytest.mark.parametrize("variant", [None, "0", "1", "2", "3"])
+@pytest.mark.parametrize("variant", [None, "0", "1", "2", "3", "4"])
 @pytest.mark.parametrize("prec", ["fp32", "bf16", "fp16"])
 @pytest.mark.parametrize("H,W", [(64, 96), (72, 104), (120, 160), (480, 640)])
 def test_fused_bottlenecks_equal_unfused(gpu, blocks, prec, H, W, variant, monkeypatch):
