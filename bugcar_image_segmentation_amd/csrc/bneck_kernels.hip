@@ -33,6 +33,13 @@
 #include <cstdlib>
 
 #include "bugseg_internal.h"
+// output stores: the per-kernel cache-policy choice (OUT_AUX_SEL: sc1 write-through for C >= 64).
+// Round 2, after the kept residual and the LDS-DMA staging: 4-9% faster per launch (C128 20x16
+// 23.3 -> 21.3 us, C64 35.1 -> 34.0 us, forward 0.80 -> 0.77 ms one stream at a time) and equal in
+// the 2-stream bench (round 1 had measured it 2.4% slower there)
+#ifndef BUGSEG_OUT_AUX
+#define BUGSEG_OUT_AUX -1
+#endif
 #include "mfma_common.h"
 
 namespace bugseg {
