@@ -23,6 +23,11 @@
 // divisions, a 16-lane pool loop the whole wave executed). Both input forms go through the same
 // arithmetic, so forward_bgr == preprocess + forward bit for bit.
 #include "bugseg_internal.h"
+// output stores: sc1 write-through (OUT_AUX_SEL, as bneck_kernels.hip): measured 44.9-46.9 -> 43.7-44.2
+// us, the 2-stream bench unchanged
+#ifndef BUGSEG_OUT_AUX
+#define BUGSEG_OUT_AUX -1
+#endif
 #include "mfma_common.h"
 
 namespace bugseg {
