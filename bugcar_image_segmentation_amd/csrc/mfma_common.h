@@ -170,8 +170,8 @@ __device__ __forceinline__ void bst16(__amdgpu_buffer_rsrc_t r, uint32_t off, ui
 // at a time (C128 26.8 -> 25.4 us, PMC reads 66 -> 62 MB per launch) but the 2-stream bench 2.4%
 // slower (37.1k -> 36.2k frames/s; why is not pinned down: with two shards interleaved, write-back
 // lines still in L2 evidently serve more reads than they evict). So the default is 0 (off), except
-// in bneck_kernels.hip, where it was re-measured after the kept residual and the LDS-DMA staging:
-// 4-9% faster per launch and equal in the 2-stream bench, so that file selects per kernel (-1).
+// in bneck_kernels.hip and init_kernels.hip, re-measured after the kept residual and the LDS-DMA staging:
+// 4-9% faster per launch and equal in the 2-stream bench, so those files select per kernel (-1).
 #ifndef BUGSEG_OUT_AUX
 #define BUGSEG_OUT_AUX 0
 #endif
