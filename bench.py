@@ -97,6 +97,8 @@ def parse():
                    help="storage precision of the timed step (fp16: bf16's bytes and MFMA rate, 3 more mantissa bits)")
     p.add_argument("--streams", type=int, default=2, help="frame shards run concurrently on this many HIP streams")
     p.add_argument("--stream-priority", type=int, default=0, help="HIP priority of the side shards' streams")
+    p.add_argument("--chain-forwards", type=int, default=0,
+                   help="1: shard i's forward starts after shard i-1's (its BEV overlaps the next forward)")
     p.add_argument("--graph", type=int, default=0, help="1: replay the step as one captured HIP graph")
     p.add_argument("--cpu-baseline-seconds", type=float, default=12.0)
     p.add_argument("--no-cpu-baseline", action="store_true")
@@ -294,7 +296,7 @@ def main():
     bev = synthetic.synthetic_bev(H, W)
     grid = (synthetic.GRID_W_M, synthetic.GRID_H_M, synthetic.CELL_M)
     pipe = OccupancyPipeline(model, bev, *grid, model_hw=(H, W), streams=a.streams,
-                             stream_priority=a.stream_priority)
+                             stream_priority=a.stream_priority, chain_forwards=bool(a.chain_forwards))
     frames = torch.from_numpy(synthetic.uniform_frames(B, H, W, seed=rank)).to(dev)
 
     run = lambda: pipe.run(frames)  # noqa: E731

@@ -25,11 +25,14 @@ class OccupancyPipeline:
 
     def __init__(self, model: ENET, bev: bev_transform_tools, grid_w_m: float, grid_h_m: float, cell_m: float,
                  model_hw: tuple[int, int] | None = None, ros_layout: bool = False, streams: int = 1,
-                 binary: bool = False, stream_priority: int = 0):
+                 binary: bool = False, stream_priority: int = 0, chain_forwards: bool = False):
         """binary=True is the predict_binary + create_occupancy_grid_binary pairing (models.py:70-82,
         bev.py:97-165): class maps through the binary LUT, the binary rasteriser; in the laserscan-like
         mode its output is the reference's pair, (2, B, ...) (bev.py:164). stream_priority is the HIP
-        priority of the side shards' streams (shard 0 runs on the caller's stream; lower = higher)."""
+        priority of the side shards' streams (shard 0 runs on the caller's stream; lower = higher).
+        chain_forwards=True starts shard i's forward when shard i-1's forward has finished, so each
+        shard's BEV rasteriser runs beside the next shard's forward (only the last one is exposed)
+        instead of all shards' forwards running together and their BEVs together at the end."""
         self.model = model
         self.binary = binary
         self.bev = bev
@@ -43,6 +46,7 @@ class OccupancyPipeline:
             raise ValueError("streams must be >= 1")
         self.streams = streams
         self.stream_priority = stream_priority
+        self.chain_forwards = chain_forwards
         self._ctxs = [model.ctx]
         self._streams = []
         self._x = None
@@ -98,14 +102,18 @@ class OccupancyPipeline:
             if i:
                 st.wait_event(ready)
             with torch.cuda.stream(st):
+                if self.chain_forwards:
+                    self._run_forward(ctxs[i], frames[s:e], x[s:e], seg[s:e], st)
+                    ready = torch.cuda.Event()
+                    ready.record(st)                  # the next shard's forward starts here
                 if pair:
                     # the kernel writes a shard's pair as one contiguous (2, e - s, ...) block; the
                     # batch's pair (2, B, ...) holds it as two slabs, so stage it and copy
                     tmp = self._pair_buf(i, (2, e - s) + tuple(out.shape[2:]), out.device)
-                    self._run_shard(ctxs[i], frames[s:e], x[s:e], seg[s:e], tmp, p, st)
+                    self._run_shard(ctxs[i], frames[s:e], x[s:e], seg[s:e], tmp, p, st, forward=not self.chain_forwards)
                     out[:, s:e].copy_(tmp)
                 else:
-                    self._run_shard(ctxs[i], frames[s:e], x[s:e], seg[s:e], out[s:e], p, st)
+                    self._run_shard(ctxs[i], frames[s:e], x[s:e], seg[s:e], out[s:e], p, st, forward=not self.chain_forwards)
         for st in streams[: self.streams - 1]:
             main.wait_stream(st)
         return out
@@ -131,12 +139,16 @@ class OccupancyPipeline:
             res = self.run(frames_bgr, out)
         return graph.replay, res
 
-    def _run_shard(self, ctx, frames, x, seg, out, p, stream):
+    def _run_forward(self, ctx, frames, x, seg, stream):
         B, H0, W0 = frames.shape[:3]
         if (H0, W0) != (self.H, self.W):
             # resize only (models.py:87); colour swap + normalisation are fused into the initial block
             ctx.preprocess(frames, B, H0, W0, self.H, self.W, N.PRE_BGR_U8, x, stream)
             frames = x
         ctx.forward_bgr(frames, B, self.H, self.W, N.OUT_BINARY_U8 if self.binary else N.OUT_CLASS3_U8, seg, stream)
+
+    def _run_shard(self, ctx, frames, x, seg, out, p, stream, forward=True):
+        if forward:
+            self._run_forward(ctx, frames, x, seg, stream)
         # the shard's own context: its laserscan scratch is never shared with another shard's stream
-        ctx.bev(seg, B, p, out, stream)
+        ctx.bev(seg, frames.shape[0], p, out, stream)

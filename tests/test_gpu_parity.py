@@ -404,9 +404,13 @@ def test_multistream_pipeline_identical(bf16_model):
     bev = synthetic.synthetic_bev(H, W, 300, 300)
     one = OccupancyPipeline(bf16_model, bev, 3.0, 3.0, 0.05, model_hw=(H, W)).run(frames).clone()
     for s in (2, 3):
-        many = OccupancyPipeline(bf16_model, bev, 3.0, 3.0, 0.05, model_hw=(H, W), streams=s).run(frames)
-        torch.cuda.synchronize()
-        assert torch.equal(one, many)
+        for chain in (False, True):       # chain: shard i's forward after shard i-1's (BEV beside it)
+            many = OccupancyPipeline(bf16_model, bev, 3.0, 3.0, 0.05, model_hw=(H, W), streams=s,
+                                     chain_forwards=chain)
+            for _ in range(2):
+                got = many.run(frames)
+            torch.cuda.synchronize()
+            assert torch.equal(one, got)
 
 
 @pytest.mark.parametrize("binary", [False, True])
