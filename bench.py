@@ -44,6 +44,7 @@ SURVEY_BYTES_PER_FRAME = 180.2e6   # bf16 per-layer activation b
 KERNEL_NAMES = {"bneck C128": "bneck_kernel<{t},128,sym>", "bneck C128 asym": "bneck_kernel<{t},128,asym>",
                 "bneck C64": "bneck_kernel<{t},64,sym>", "bneck C16": "bneck_kernel<{t},16,sym>",
                 "init": "init_kernel<{t},bgr>"}
+TEMPLATE_TYPE = {"fp16": "_Float16", "bf16": "__bf16", "fp32": "float"}   # the kernels' template type names
 
 
 def kernel_table(ctx, B, H, W, reps, stream):
@@ -106,6 +107,9 @@ def parse():
                    help="1: add the other precision modes / batch-1 latency / class-agreement / DeepLab sub-records (measured "
                         "outside the timed loop); default: on at N = 1, off for N > 1")
     p.add_argument("--deeplab-batch", type=int, default=64)
+    p.add_argument("--backend", default="nccl", choices=["nccl", "gloo"],
+                   help="N > 1 process group: nccl (= RCCL over xGMI, the product path) or gloo (a functional run "
+                        "of the distributed branch on fewer GPUs than ranks, e.g. 2 ranks on one GPU; not a timing)")
     return p.parse_args()
 
 
@@ -279,8 +283,16 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    # one process per GPU; with more ranks than GPUs (the gloo functional run) ranks share devices
+    ndev = torch.cuda.device_count()
+    if ndev == 0:
+        raise RuntimeError("bench.py needs a HIP GPU")
+    local = local % ndev
     if world > 1:
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        if a.backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        else:
+            dist.init_process_group("gloo")
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
 
@@ -314,6 +326,19 @@ def main():
     for _ in range(a.warmup):
         step()
     torch.cuda.synchronize()
+    gather_check = None
+    if world > 1:
+        # outside the timed region: the all-gathered batch holds every rank's grids in rank order
+        local_g = run().clone()
+        full = gather_grids(local_g, B * world)
+        gather_check = bool(full.shape[0] == B * world and torch.equal(full[rank * B:(rank + 1) * B], local_g))
+        ok = torch.tensor([int(gather_check)], dtype=torch.int32)
+        ok = ok.to(dev) if a.backend == "nccl" else ok
+        dist.all_reduce(ok, op=dist.ReduceOp.MIN)
+        gather_check = bool(ok.item())
+        if not gather_check:
+            raise RuntimeError("all-gathered occupancy grids do not hold the ranks' own grids")
+        torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
@@ -325,7 +350,7 @@ def main():
         dist.barrier()
     el = time.perf_counter() - t0
     if world > 1:
-        t = torch.tensor([el], dtype=torch.float64, device=dev)
+        t = torch.tensor([el], dtype=torch.float64, device=dev if a.backend == "nccl" else "cpu")
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         el = float(t.item())
 
@@ -372,7 +397,7 @@ def main():
         traffic = pmc_traffic(tag)
         res = {
             "metric": "frames/sec ENet 640x480 segmentation -> BEV occupancy grid (synthetic), whole job",
-            "value": round(value, 2), "unit": "frames/s", "n_gpus": world, "steps": a.steps, "warmup": a.warmup,
+            "value": round(value, 2), "unit": "frames/s", "n_gpus": world if a.backend == "nccl" else min(world, ndev), "steps": a.steps, "warmup": a.warmup,
             "ms_per_step": round(el / a.steps * 1e3, 4), "higher_is_better": True, "scaling": "weak",
             "vs_baseline": None, "dtype": a.precision, "data": "synthetic (uniform u8 frames, seed=rank; "
             "random-init canonical ENet weights seed 1234; synthetic BEV calibration)",
@@ -380,12 +405,14 @@ def main():
                                    f"fused BEV warp/occgrid (1000x1000 BEV -> 200x200 cells)",
                        "global_batch": B * world, "per_gpu_batch": B, "height": H, "width": W,
                        "parallelism": f"frame-sharded dp{world}" + (" + RCCL all-gather of grids" if world > 1 else ""),
-                       "streams_per_gpu": a.streams, "hip_graph": bool(a.graph)},
+                       "streams_per_gpu": a.streams, "hip_graph": bool(a.graph),
+                       **({"backend": "rccl" if a.backend == "nccl" else "gloo (functional run, not a timing)",
+                           "gather_check": gather_check} if world > 1 else {})},
             "roofline": {
                 "bound": "hbm", "achieved": round(k_achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                 "frac": round(k_achieved / HBM_PEAK_GBS, 4),
                 "traffic": traffic,
-                "kernel": f"{KERNEL_NAMES.get(tag.rsplit(' ', 1)[0], tag).format(t=a.precision)} [{tag}]: the dominant kernel of the forward "
+                "kernel": f"{KERNEL_NAMES.get(tag.rsplit(' ', 1)[0], tag).format(t=TEMPLATE_TYPE[a.precision])} [{tag}]: the dominant kernel of the forward "
                           f"({k['launches']} launches, {k['total_us']:.0f} us of {t_fwd * 1e3:.0f} us); "
                           f"{k['bytes_per_launch'] / 1e6:.1f} MB per launch = the bytes the launch must move "
                           f"(block input read once + output written once); {k['us_per_launch']:.2f} us per launch "

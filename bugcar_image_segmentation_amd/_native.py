@@ -24,7 +24,7 @@ PRE_ENGINE, PRE_NCHW_F64, PRE_NCHW_F32, PRE_BGR_U8 = 0, 1, 2, 3
 EXPORTED = ("bugseg_version", "bugseg_create", "bugseg_destroy", "bugseg_load_weights", "bugseg_num_classes",
             "bugseg_input_bytes", "bugseg_preprocess", "bugseg_nchw_to_input", "bugseg_enet_forward",
             "bugseg_enet_forward_bgr",
-            "bugseg_bev_occgrid", "bugseg_plan_info", "bugseg_plan_op", "bugseg_plan_launch_op",
+            "bugseg_bev_occgrid", "bugseg_bev_workspace_bytes", "bugseg_bev_occgrid_ws", "bugseg_plan_info", "bugseg_plan_op", "bugseg_plan_launch_op",
             "bugseg_last_error",
             "bugseg_dl_create", "bugseg_dl_destroy", "bugseg_dl_load_weights", "bugseg_dl_set_plan",
             "bugseg_dl_forward", "bugseg_dl_launch_op", "bugseg_dl_read_buffer", "bugseg_dl_last_error",
@@ -74,6 +74,8 @@ def load_library(path: Path | str | None = None) -> ctypes.CDLL:
             "bugseg_enet_forward": (i, [vp, vp, i, i, i, i, vp, vp]),
             "bugseg_enet_forward_bgr": (i, [vp, vp, i, i, i, i, vp, vp]),
             "bugseg_bev_occgrid": (i, [vp, vp, i, ctypes.POINTER(BevParams), vp, vp]),
+            "bugseg_bev_workspace_bytes": (sz, [ctypes.POINTER(BevParams), i]),
+            "bugseg_bev_occgrid_ws": (i, [vp, vp, i, ctypes.POINTER(BevParams), vp, vp, sz, vp]),
             "bugseg_plan_info": (i, [vp, i, i, i, i, i, ctypes.POINTER(i), ctypes.POINTER(ctypes.c_double),
                                      ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_double)]),
             "bugseg_plan_op": (i, [vp, i, i, i, i, cp, i, ctypes.POINTER(ctypes.c_double),
@@ -170,8 +172,17 @@ class Context:
                                                stream_handle(stream)), self.h)
 
     def bev(self, seg, B, params: BevParams, out, stream=None):
-        check(self.lib.bugseg_bev_occgrid(self.h, seg.data_ptr(), B, ctypes.byref(params), out.data_ptr(),
-                                          stream_handle(stream)), self.h)
+        """bugseg_bev_occgrid_ws: the laserscan scratch comes from torch's caching allocator on the
+        stream the work runs on (reuse is stream-ordered; under graph capture it is the graph's pool),
+        so the library never allocates or synchronises for it."""
+        st = stream if stream is not None else torch.cuda.current_stream(seg.device)
+        nws = int(self.lib.bugseg_bev_workspace_bytes(ctypes.byref(params), B))
+        ws = None
+        if nws:
+            with torch.cuda.stream(st):
+                ws = torch.empty(nws, dtype=torch.uint8, device=seg.device)
+        check(self.lib.bugseg_bev_occgrid_ws(self.h, seg.data_ptr(), B, ctypes.byref(params), out.data_ptr(),
+                                             0 if ws is None else ws.data_ptr(), nws, stream_handle(st)), self.h)
 
     def plan_info(self, B, H, W, out_kind, bgr_input=False):
         """-> (launches, per-layer algorithmic bytes, plan compulsory bytes, flops) of one forward."""

@@ -78,6 +78,7 @@ struct Plan {
     std::vector<Op> ops;
     void *arena = nullptr;
     size_t arena_bytes = 0;
+    bool pinned = false;     // a forward on this arena was captured into a graph: never freed before destroy
 };
 
 inline int round_up(int v, int m) { return (v + m - 1) / m * m; }
@@ -108,19 +109,26 @@ struct bugseg_ctx {
     int pre_key[4] = {0, 0, 0, 0};
     void *pre_tab = nullptr;
     size_t pre_tab_bytes = 0;
-    // laserscan mode: polar tables of the last geometry (occ_w, occ_h, variant) and batch scratch
-    int polar_key[3] = {0, 0, -1};
-    int polar_pw = 0, polar_ph = 0;
-    void *polar_tab = nullptr;       // fmap (ph*pw int32) then imap (occ_h*occ_w int32)
-    // per-stream batch scratch: cells (B*occ_h*occ_w u8, 256-B aligned) then rmin (B*ph int32). Keyed
-    // by stream so that calls enqueued on different streams of one context never share intermediate
-    // buffers (the polar tables are read-only once built and are shared).
-    struct LsScratch { void *stream = nullptr; void *p = nullptr; size_t bytes = 0; };
+    // Private non-blocking stream for one-time table builds: a table is built and waited for there
+    // before the caller's work is enqueued, so it never needs a sync of the caller's (or any other)
+    // stream, and a first call made while the caller's stream is being captured into a graph works.
+    hipStream_t setup = nullptr;
+    // laserscan mode: polar tables per grid geometry (occ_w, occ_h, variant), read-only once built
+    struct PolarTab { int key[3] = {0, 0, -1}; int pw = 0, ph = 0; void *tab = nullptr; bool pinned = false; };
+    std::vector<PolarTab> polar_tabs;  // tab: fmap (ph*pw int32) then imap (occ_h*occ_w int32)
+    // laserscan batch scratch of bugseg_bev_occgrid (the caller-workspace entry bugseg_bev_occgrid_ws
+    // needs none): cells (B*occ_h*occ_w u8, 256-B aligned) then rmin (B*ph int32). Keyed by stream
+    // so that calls enqueued on different streams of one context never share intermediate buffers.
+    struct LsScratch { void *stream = nullptr; void *p = nullptr; size_t bytes = 0; uint64_t used = 0; bool pinned = false; };
     std::vector<LsScratch> ls_scratch;
+    uint64_t use_clock = 0;
     // BEV warp-tap tables (bev_kernels.hip bev_table_kernel), one per recent geometry (read-only
-    // once built, shared by every stream); key = the geometry fields of BevArgs
-    struct BevTab { std::vector<unsigned char> key; uint4 *tab = nullptr; };
+    // once built, shared by every stream); key = the geometry fields of BevArgs. pinned: used by a
+    // call that was captured into a graph — never evicted while the context lives.
+    struct BevTab { std::vector<unsigned char> key; uint4 *tab = nullptr; bool pinned = false; };
     std::vector<BevTab> bev_tabs;
+    // memory retired while a stream was capturing (a graph may reference it): freed at destroy
+    std::vector<void *> graveyard;
 };
 
 namespace {
@@ -129,6 +137,38 @@ int fail(bugseg_ctx *c, int code, const std::string &m) {
     if (c) c->err = m;
     else g_thread_err = m;
     return code;
+}
+
+// True when `stream` is being captured into a graph (or its capture state cannot be read, which HIP
+// reports for the legacy stream while another stream captures: treated as capturing, so nothing
+// that synchronises is attempted).
+bool stream_capturing(void *stream) {
+    hipStreamCaptureStatus st = hipStreamCaptureStatusNone;
+    if (hipStreamIsCapturing((hipStream_t)stream, &st) != hipSuccess) return true;
+    return st != hipStreamCaptureStatusNone;
+}
+
+// Lets this thread allocate and wait on the private setup stream while one of its streams is
+// capturing in the global mode (torch.cuda.graph's default): those calls do not touch the capture.
+struct RelaxCapture {
+    hipStreamCaptureMode m = hipStreamCaptureModeRelaxed;
+    RelaxCapture() { (void)hipThreadExchangeStreamCaptureMode(&m); }
+    ~RelaxCapture() { (void)hipThreadExchangeStreamCaptureMode(&m); }
+};
+
+hipStream_t setup_stream(bugseg_ctx *c) {
+    if (!c->setup && hipStreamCreateWithFlags(&c->setup, hipStreamNonBlocking) != hipSuccess) c->setup = nullptr;
+    return c->setup;
+}
+
+// Free device memory that work already enqueued on some stream may still read. Outside a capture
+// that takes a device sync (only the rare evictions come here: a 5th table geometry, a 9th stream
+// on the scratch-owning entry); during a capture the memory is kept until the context is destroyed.
+void retire(bugseg_ctx *c, void *p, bool capturing) {
+    if (!p) return;
+    if (capturing) { c->graveyard.push_back(p); return; }
+    (void)hipDeviceSynchronize();
+    (void)hipFree(p);
 }
 
 struct DeviceGuard {
@@ -994,7 +1034,7 @@ bool finish_conv_args(ConvArgs &a, int epi, size_t es) {
     return true;
 }
 
-bool build_plan(bugseg_ctx *ctx, int B, int H, int W, std::string &why) {
+bool build_plan(bugseg_ctx *ctx, int B, int H, int W, std::string &why, void *stream = nullptr) {
     Plan &pl = ctx->plan;
     if (pl.arena && pl.B == B && pl.H == H && pl.W == W) return true;
     Walker w{ctx, B, H, W};
@@ -1002,10 +1042,13 @@ bool build_plan(bugseg_ctx *ctx, int B, int H, int W, std::string &why) {
     auto al = [](size_t v) { return (v + 4095) / 4096 * 4096; };
     size_t total = 2 * al(w.szX) + 3 * al(w.szT) + al(w.szM);
     for (size_t s : w.szIdx) total += al(s);
+    const bool cap = stream_capturing(stream);
+    RelaxCapture relax;                 // the first forward at a shape may itself be captured
     if (pl.arena) {
-        (void)hipDeviceSynchronize();   // a forward of the old shape may still be running on any stream
-        (void)hipFree(pl.arena);
+        // a forward of the old shape may still be running (or be part of a captured graph)
+        retire(ctx, pl.arena, cap || pl.pinned);
         pl.arena = nullptr;
+        pl.pinned = false;
     }
     if (hipMalloc(&pl.arena, total) != hipSuccess) { why = "hipMalloc of the activation arena failed"; pl.arena = nullptr; return false; }
     unsigned char *p = (unsigned char *)pl.arena;
@@ -1098,9 +1141,11 @@ int bugseg_destroy(bugseg_ctx *ctx) {
     if (ctx->dev_luts) (void)hipFree(ctx->dev_luts);
     if (ctx->plan.arena) (void)hipFree(ctx->plan.arena);
     if (ctx->pre_tab) (void)hipFree(ctx->pre_tab);
-    if (ctx->polar_tab) (void)hipFree(ctx->polar_tab);
+    for (auto &t : ctx->polar_tabs) if (t.tab) (void)hipFree(t.tab);
     for (auto &s : ctx->ls_scratch) if (s.p) (void)hipFree(s.p);
     for (auto &t : ctx->bev_tabs) if (t.tab) (void)hipFree(t.tab);
+    for (void *p : ctx->graveyard) (void)hipFree(p);
+    if (ctx->setup) (void)hipStreamDestroy(ctx->setup);
     delete ctx;
     return BUGSEG_OK;
 }
@@ -1118,7 +1163,11 @@ int bugseg_load_weights(bugseg_ctx *ctx, const void *blob, size_t bytes) {
     if (!pack_all(ctx, why)) return fail(ctx, BUGSEG_EFORMAT, "weight blob: " + why);
     (void)hipDeviceSynchronize();
     if (ctx->dev_w) { (void)hipFree(ctx->dev_w); ctx->dev_w = nullptr; }
-    if (ctx->plan.arena) { (void)hipFree(ctx->plan.arena); ctx->plan = Plan(); }
+    if (ctx->plan.arena) {
+        if (ctx->plan.pinned) ctx->graveyard.push_back(ctx->plan.arena);   // a captured graph may use it
+        else (void)hipFree(ctx->plan.arena);
+        ctx->plan = Plan();
+    }
     if (hipMalloc(&ctx->dev_w, ctx->host_w.size()) != hipSuccess ||
         hipMemcpy(ctx->dev_w, ctx->host_w.data(), ctx->host_w.size(), hipMemcpyHostToDevice) != hipSuccess)
         return fail(ctx, BUGSEG_EHIP, "uploading weights failed");
@@ -1206,8 +1255,9 @@ static int enet_forward(bugseg_ctx *ctx, const void *in, bool bgr, int B, int H,
     if (out_kind < BUGSEG_OUT_LOGITS_F32 || out_kind > BUGSEG_OUT_BINARY_U8) return fail(ctx, BUGSEG_EINVAL, "bad out_kind");
     DeviceGuard g(ctx->device);
     std::string why;
-    if (!build_plan(ctx, B, H, W, why)) return fail(ctx, BUGSEG_EINVAL, why);
+    if (!build_plan(ctx, B, H, W, why, stream)) return fail(ctx, BUGSEG_EINVAL, why);
     Plan &pl = ctx->plan;
+    if (stream_capturing(stream)) pl.pinned = true;
     Op &first = pl.ops.front();
     first.a.in = in;
     first.epi = bgr ? EPI_INIT_BGR : EPI_INIT;
@@ -1305,64 +1355,105 @@ void polar_tables(int pw, int ph, double max_radius, float cx, float cy, int w, 
 }
 #pragma clang fp contract(on)
 
-// Polar tables and scratch for a laserscan call; fills a.fmap / imap / pw / ph / cells / rmin / hit.
-int prepare_laserscan(bugseg_ctx *ctx, const bugseg_bev_params *p, int B, BevArgs &a, void *stream) {
+// warpPolar dsize: (-1, -1) -> (round(L), round(L*pi)) for create_occupancy_grid (bev.py:219); the
+// explicit (w, h) of create_occupancy_grid_binary (bev.py:146). False if the tables cannot hold it.
+bool polar_dims(const bugseg_bev_params *p, int &pw, int &ph) {
     const int w = p->occ_w, h = p->occ_h, L = std::max(w, h);
-    // warpPolar dsize: (-1, -1) -> (round(L), round(L*pi)) for create_occupancy_grid (bev.py:219);
-    // the explicit (w, h) of create_occupancy_grid_binary (bev.py:146)
-    const int pw = p->variant ? w : (int)std::lrint((double)L);
-    const int ph = p->variant ? h : (int)std::lrint((double)L * 3.1415926535897932384626433832795);
-    if (pw <= 0 || ph <= 0 || pw > 32767 || ph > 32767 || w > 32767 || h > 32767)
-        return fail(ctx, BUGSEG_EINVAL, "laserscan grid too large for the polar tables");
-    if (ctx->polar_key[0] != w || ctx->polar_key[1] != h || ctx->polar_key[2] != p->variant || !ctx->polar_tab) {
+    pw = p->variant ? w : (int)std::lrint((double)L);
+    ph = p->variant ? h : (int)std::lrint((double)L * 3.1415926535897932384626433832795);
+    return pw > 0 && ph > 0 && pw <= 32767 && ph <= 32767 && w <= 32767 && h <= 32767;
+}
+
+// Laserscan batch scratch: cells (B*occ_h*occ_w u8, 256-B aligned) then rmin (B*ph int32).
+size_t ls_cells_bytes(int B, const bugseg_bev_params *p) { return ((size_t)B * p->occ_w * p->occ_h + 255) & ~(size_t)255; }
+size_t ls_workspace_bytes(int B, const bugseg_bev_params *p, int ph) {
+    return ls_cells_bytes(B, p) + (size_t)B * ph * sizeof(int32_t);
+}
+
+// The polar tables of a laserscan call (built once per grid geometry on the setup stream, waited
+// for there); fills a.fmap / imap / pw / ph / hit.
+int prepare_polar(bugseg_ctx *ctx, const bugseg_bev_params *p, BevArgs &a, bool cap) {
+    const int w = p->occ_w, h = p->occ_h, L = std::max(w, h);
+    int pw, ph;
+    if (!polar_dims(p, pw, ph)) return fail(ctx, BUGSEG_EINVAL, "laserscan grid too large for the polar tables");
+    bugseg_ctx::PolarTab *hit = nullptr;
+    for (auto &t : ctx->polar_tabs)
+        if (t.key[0] == w && t.key[1] == h && t.key[2] == p->variant) hit = &t;
+    if (!hit) {
         std::vector<int32_t> fmap, imap;
         polar_tables(pw, ph, (double)L, (float)(w / 2.0 - 1), (float)h, w, h, fmap, imap);
-        // the old tables may still be read by work enqueued on ANY stream of this context
-        if (hipDeviceSynchronize() != hipSuccess) return fail(ctx, BUGSEG_EHIP, "device sync failed");
-        if (ctx->polar_tab) (void)hipFree(ctx->polar_tab);
-        ctx->polar_tab = nullptr;
+        if (ctx->polar_tabs.size() >= 4) {            // keep 4 geometries: evict the oldest unpinned one
+            for (size_t i = 0; i < ctx->polar_tabs.size(); ++i)
+                if (!ctx->polar_tabs[i].pinned) {
+                    retire(ctx, ctx->polar_tabs[i].tab, cap);
+                    ctx->polar_tabs.erase(ctx->polar_tabs.begin() + (long)i);
+                    break;
+                }
+        }
+        RelaxCapture relax;
+        hipStream_t s = setup_stream(ctx);
+        if (!s) return fail(ctx, BUGSEG_EHIP, "could not create the table-build stream");
+        bugseg_ctx::PolarTab t;
+        t.key[0] = w; t.key[1] = h; t.key[2] = p->variant;
+        t.pw = pw; t.ph = ph;
         const size_t bytes = (fmap.size() + imap.size()) * sizeof(int32_t);
-        if (hipMalloc(&ctx->polar_tab, bytes) != hipSuccess) return fail(ctx, BUGSEG_ENOMEM, "polar table allocation failed");
-        if (hipMemcpy(ctx->polar_tab, fmap.data(), fmap.size() * 4, hipMemcpyHostToDevice) != hipSuccess ||
-            hipMemcpy((int32_t *)ctx->polar_tab + fmap.size(), imap.data(), imap.size() * 4, hipMemcpyHostToDevice) != hipSuccess)
-            return fail(ctx, BUGSEG_EHIP, "polar table upload failed");
-        ctx->polar_key[0] = w; ctx->polar_key[1] = h; ctx->polar_key[2] = p->variant;
-        ctx->polar_pw = pw; ctx->polar_ph = ph;
+        if (hipMalloc(&t.tab, bytes) != hipSuccess) return fail(ctx, BUGSEG_ENOMEM, "polar table allocation failed");
+        hipError_t e = hipMemcpyAsync(t.tab, fmap.data(), fmap.size() * 4, hipMemcpyHostToDevice, s);
+        if (e == hipSuccess)
+            e = hipMemcpyAsync((int32_t *)t.tab + fmap.size(), imap.data(), imap.size() * 4, hipMemcpyHostToDevice, s);
+        if (e == hipSuccess) e = hipStreamSynchronize(s);
+        if (e != hipSuccess) {
+            (void)hipFree(t.tab);
+            return fail(ctx, BUGSEG_EHIP, std::string("polar table upload: ") + hipGetErrorString(e));
+        }
+        ctx->polar_tabs.push_back(t);
+        hit = &ctx->polar_tabs.back();
     }
-    const size_t cells_bytes = ((size_t)B * w * h + 255) & ~(size_t)255;
-    const size_t need = cells_bytes + (size_t)B * ph * sizeof(int32_t);
-    bugseg_ctx::LsScratch *sc = nullptr;
-    for (auto &x : ctx->ls_scratch) if (x.stream == stream) sc = &x;
-    if (!sc) {
-        ctx->ls_scratch.push_back(bugseg_ctx::LsScratch());
-        sc = &ctx->ls_scratch.back();
-        sc->stream = stream;
-    }
-    if (need > sc->bytes) {
-        // this stream's scratch is only used by this stream's work; a device-wide sync also covers a
-        // caller that reuses a stream handle value after destroying the stream
-        if (hipDeviceSynchronize() != hipSuccess) return fail(ctx, BUGSEG_EHIP, "device sync failed");
-        if (sc->p) (void)hipFree(sc->p);
-        sc->p = nullptr;
-        sc->bytes = 0;
-        if (hipMalloc(&sc->p, need) != hipSuccess) return fail(ctx, BUGSEG_ENOMEM, "laserscan scratch allocation failed");
-        sc->bytes = need;
-    }
+    if (cap) hit->pinned = true;
     a.laserscan = 1;
-    a.fmap = (const int32_t *)ctx->polar_tab;
-    a.imap = (const int32_t *)ctx->polar_tab + (size_t)pw * ph;
+    a.fmap = (const int32_t *)hit->tab;
+    a.imap = (const int32_t *)hit->tab + (size_t)pw * ph;
     a.pw = pw; a.ph = ph;
-    a.cells = (uint8_t *)sc->p;
-    a.rmin = (int32_t *)((unsigned char *)sc->p + cells_bytes);
     a.hit = p->variant ? 100 : 3;
     return BUGSEG_OK;
 }
 
-}  // namespace
+// The scratch-owning entry's per-stream laserscan scratch (bugseg_bev_occgrid without a workspace).
+int internal_scratch(bugseg_ctx *ctx, void *stream, size_t need, bool cap, void *&out) {
+    bugseg_ctx::LsScratch *sc = nullptr;
+    for (auto &x : ctx->ls_scratch) if (x.stream == stream) sc = &x;
+    if (!sc) {
+        if (ctx->ls_scratch.size() >= 8) {            // 8 streams: evict the least recently used unpinned one
+            long victim = -1;
+            for (size_t i = 0; i < ctx->ls_scratch.size(); ++i)
+                if (!ctx->ls_scratch[i].pinned && (victim < 0 || ctx->ls_scratch[i].used < ctx->ls_scratch[(size_t)victim].used))
+                    victim = (long)i;
+            if (victim >= 0) {
+                retire(ctx, ctx->ls_scratch[(size_t)victim].p, cap);
+                ctx->ls_scratch.erase(ctx->ls_scratch.begin() + victim);
+            }
+        }
+        ctx->ls_scratch.push_back(bugseg_ctx::LsScratch());
+        sc = &ctx->ls_scratch.back();
+        sc->stream = stream;
+    }
+    sc->used = ++ctx->use_clock;
+    if (need > sc->bytes) {
+        // work already enqueued on this stream (or captured from it) may still use the old buffer
+        retire(ctx, sc->p, cap || sc->pinned);
+        sc->p = nullptr;
+        sc->bytes = 0;
+        RelaxCapture relax;
+        if (hipMalloc(&sc->p, need) != hipSuccess) return fail(ctx, BUGSEG_ENOMEM, "laserscan scratch allocation failed");
+        sc->bytes = need;
+    }
+    if (cap) sc->pinned = true;
+    out = sc->p;
+    return BUGSEG_OK;
+}
 
-extern "C" {
-
-int bugseg_bev_occgrid(bugseg_ctx *ctx, const uint8_t *seg, int B, const bugseg_bev_params *p, int8_t *out, void *stream) {
+int bev_occgrid(bugseg_ctx *ctx, const uint8_t *seg, int B, const bugseg_bev_params *p, int8_t *out, bool own_ws,
+                void *ws, size_t ws_bytes, void *stream) {
     if (!ctx || !seg || !p || !out) return fail(ctx, BUGSEG_EINVAL, "NULL argument");
     if (B <= 0 || p->in_rows <= 0 || p->in_cols <= 0 || p->warp_w <= 0 || p->warp_h <= 0 || p->occ_w <= 0 ||
         p->occ_h <= 0 || p->occ_w_px <= 0 || p->occ_h_px <= 0)
@@ -1401,8 +1492,17 @@ int bugseg_bev_occgrid(bugseg_ctx *ctx, const uint8_t *seg, int B, const bugseg_
     a.ros_layout = p->ros_layout;
     a.variant = p->variant;
     a.out = out;
+    if (p->laserscan) {
+        // check the workspace before anything is built or enqueued
+        int pw, ph;
+        if (!polar_dims(p, pw, ph)) return fail(ctx, BUGSEG_EINVAL, "laserscan grid too large for the polar tables");
+        if (!own_ws && (!ws || ws_bytes < ls_workspace_bytes(B, p, ph)))
+            return fail(ctx, BUGSEG_EINVAL, "laserscan workspace missing or smaller than bugseg_bev_workspace_bytes()");
+    }
+    const bool cap = stream_capturing(stream);
     {
-        // the geometry's warp-tap table: built once (on this stream), then shared by every call
+        // the geometry's warp-tap table: built once on the setup stream and waited for there, then
+        // shared read-only by every call on any stream
         std::vector<unsigned char> key(sizeof(double) * 11 + sizeof(int) * 12);
         unsigned char *kp = key.data();
         auto put = [&](const void *v, size_t n) { std::memcpy(kp, v, n); kp += n; };
@@ -1415,18 +1515,24 @@ int bugseg_bev_occgrid(bugseg_ctx *ctx, const uint8_t *seg, int B, const bugseg_
         if (!hit) {
             const size_t cells = (size_t)a.occ_h * a.occ_w;
             if (cells * BEV_SLOTS > (size_t)1 << 31) return fail(ctx, BUGSEG_EINVAL, "occupancy grid too large");
-            if (ctx->bev_tabs.size() >= 4) {            // keep the 4 most recent geometries
-                if (hipDeviceSynchronize() != hipSuccess) return fail(ctx, BUGSEG_EHIP, "device sync failed");
-                (void)hipFree(ctx->bev_tabs.front().tab);
-                ctx->bev_tabs.erase(ctx->bev_tabs.begin());
+            if (ctx->bev_tabs.size() >= 4) {            // keep 4 geometries: evict the oldest unpinned one
+                for (size_t i = 0; i < ctx->bev_tabs.size(); ++i)
+                    if (!ctx->bev_tabs[i].pinned) {
+                        retire(ctx, ctx->bev_tabs[i].tab, cap);
+                        ctx->bev_tabs.erase(ctx->bev_tabs.begin() + (long)i);
+                        break;
+                    }
             }
+            RelaxCapture relax;
+            hipStream_t s = setup_stream(ctx);
+            if (!s) return fail(ctx, BUGSEG_EHIP, "could not create the table-build stream");
             bugseg_ctx::BevTab t;
             t.key = key;
             if (hipMalloc(&t.tab, cells * BEV_SLOTS * sizeof(uint4)) != hipSuccess)
                 return fail(ctx, BUGSEG_ENOMEM, "BEV table allocation failed");
             a.wtab = t.tab;
-            hipError_t e = launch_bev_table(a, (hipStream_t)stream);
-            if (e == hipSuccess) e = hipStreamSynchronize((hipStream_t)stream);   // other streams may use it next
+            hipError_t e = launch_bev_table(a, s);
+            if (e == hipSuccess) e = hipStreamSynchronize(s);   // only the build itself is waited for
             if (e != hipSuccess) {
                 (void)hipFree(t.tab);
                 return fail(ctx, BUGSEG_EHIP, std::string("BEV table: ") + hipGetErrorString(e));
@@ -1434,15 +1540,41 @@ int bugseg_bev_occgrid(bugseg_ctx *ctx, const uint8_t *seg, int B, const bugseg_
             ctx->bev_tabs.push_back(std::move(t));
             hit = &ctx->bev_tabs.back();
         }
+        if (cap) hit->pinned = true;
         a.wtab = hit->tab;
     }
     if (p->laserscan) {
-        const int rc = prepare_laserscan(ctx, p, B, a, stream);
+        int rc = prepare_polar(ctx, p, a, cap);
         if (rc != BUGSEG_OK) return rc;
+        if (own_ws) {
+            rc = internal_scratch(ctx, stream, ls_workspace_bytes(B, p, a.ph), cap, ws);
+            if (rc != BUGSEG_OK) return rc;
+        }
+        a.cells = (uint8_t *)ws;
+        a.rmin = (int32_t *)((unsigned char *)ws + ls_cells_bytes(B, p));
     }
     hipError_t e = launch_bev(a, (hipStream_t)stream);
     if (e != hipSuccess) return fail(ctx, BUGSEG_EHIP, std::string("bev launch: ") + hipGetErrorString(e));
     return BUGSEG_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+int bugseg_bev_occgrid(bugseg_ctx *ctx, const uint8_t *seg, int B, const bugseg_bev_params *p, int8_t *out, void *stream) {
+    return bev_occgrid(ctx, seg, B, p, out, true, nullptr, 0, stream);
+}
+
+size_t bugseg_bev_workspace_bytes(const bugseg_bev_params *p, int B) {
+    int pw, ph;
+    if (!p || B <= 0 || p->occ_w <= 0 || p->occ_h <= 0 || !p->laserscan || !polar_dims(p, pw, ph)) return 0;
+    return ls_workspace_bytes(B, p, ph);
+}
+
+int bugseg_bev_occgrid_ws(bugseg_ctx *ctx, const uint8_t *seg, int B, const bugseg_bev_params *p, int8_t *out,
+                          void *workspace, size_t workspace_bytes, void *stream) {
+    return bev_occgrid(ctx, seg, B, p, out, false, workspace, workspace_bytes, stream);
 }
 
 // ---- test hooks (host only: no device, no HIP call) — tests/asan drives them under ASan + UBSan

@@ -467,8 +467,8 @@ __global__ void __launch_bounds__(256, 2) dl_gemm_kernel(const DlConvArgs a) {
 // land on 16 distinct 16-B bank groups; glds writes lane-linear, so each lane fetches the chunk its
 // slot holds (the swizzle is applied to the global source address). The k-steps go through the same
 // MFMA in the same order as dl_conv_kernel / dl_gemm_kernel with the same epilogue: bit-identical.
-// Tails: rows past M / NP and chunks past CS / K re-read an in-range chunk (finite values; their
-// products meet zero weights or are never stored).
+// Tails: rows past M / NP re-read an in-range row (their products are never stored); activation
+// chunks past the stored CS read the weights' zero padding (columns >= cin), so they add exact zeros.
 constexpr int G2_T = 128, G2_KT = 64;
 
 __device__ __forceinline__ void glds16(const void *g, void *lds) {
@@ -521,7 +521,9 @@ __global__ void __launch_bounds__(256, 2) dl_gemm128_kernel(const DlConvArgs a) 
         for (int i = 0; i < 4; ++i) {
             const int k = k0 + kc[i];
             glds16(sa[i] + (k < K ? k : 0), bA + i * 8 * G2_KT);
-            glds16(sb[i] + (k < a.CS ? k : 0), bB + i * 8 * G2_KT);
+            // channels past the stored CS (K padded up to the k-stage) read a zero chunk: the weight
+            // row 0's own padding columns k >= CS >= cin, so a non-finite activation never meets them
+            glds16(k < a.CS ? sb[i] + k : wg + k, bB + i * 8 * G2_KT);
         }
     };
     f32x4 acc[4][4];
@@ -587,7 +589,9 @@ __global__ void __launch_bounds__(256, 2) dl_gemm128_kernel(const DlConvArgs a) 
     // epilogue (dl_gemm_kernel's, per wave: its 64 pixels x 64 channels, 32 pixels at a time)
     const int nb = n0 + wn * 64;
     if (nb >= a.NP) return;
-    float *stg = reinterpret_cast<float *>(sm0) + wave * 32 * DL_STG_RS;   // 4 x 8.7 KB of sm0 + sm1
+    // two waves' 8.7 KB staging areas in each LDS object (each area lies inside one object)
+    static_assert(2 * 32 * DL_STG_RS * sizeof(float) <= sizeof(sm0), "epilogue staging must fit one LDS object");
+    float *stg = reinterpret_cast<float *>(wave < 2 ? sm0 : sm1) + (wave & 1) * 32 * DL_STG_RS;
     const int c8 = (lane & 7) * 8;
     const bool cok = nb + c8 < a.cout;
 #pragma unroll

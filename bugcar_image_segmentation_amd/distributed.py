@@ -39,8 +39,11 @@ def gather_grids(local: torch.Tensor, total: int, group=None) -> torch.Tensor:
         dist.all_gather_into_tensor(buf, pad.contiguous(), group=group)
         parts = list(buf.split(m))
     else:
-        parts = [torch.empty_like(pad) for _ in range(world)]
-        dist.all_gather(parts, pad.contiguous(), group=group)
+        # gloo (CPU tests, and the single-GPU functional run of bench.py's N > 1 branch): host copies
+        host = pad.cpu().contiguous()
+        parts = [torch.empty_like(host) for _ in range(world)]
+        dist.all_gather(parts, host, group=group)
+        return torch.cat([p[:c] for p, c in zip(parts, counts)], 0).to(local.device)
     return torch.cat([p[:c] for p, c in zip(parts, counts)], 0)
 
 

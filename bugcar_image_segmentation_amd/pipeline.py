@@ -126,14 +126,20 @@ class OccupancyPipeline:
             t = self._pairs[i] = torch.empty(shape, dtype=torch.int8, device=dev)
         return t
 
-    def capture(self, frames_bgr: torch.Tensor, out: torch.Tensor | None = None):
+    def capture(self, frames_bgr: torch.Tensor, out: torch.Tensor | None = None, warm: bool = True):
         """Record one ``run`` over these frame / output buffers as a HIP graph (every shard's launches
         and the stream fork / join between them) and return (replay, out): ``replay()`` re-launches the
         whole step with one call, reading whatever the frame buffer holds at that time. The buffers
-        must stay alive and keep their addresses. One eager ``run`` first sizes every arena and table
-        (allocations are not allowed while capturing)."""
-        self.run(frames_bgr, out)
-        torch.cuda.synchronize(frames_bgr.device)
+        must stay alive and keep their addresses. warm=True runs the step once eagerly first;
+        warm=False captures the very first call at this shape and geometry (the library allocates
+        arenas and builds its tables on its own stream during the capture; only the shard contexts
+        and streams are created beforehand)."""
+        dev = frames_bgr.device
+        if warm:
+            self.run(frames_bgr, out)
+        elif self.streams > 1 and frames_bgr.shape[0] >= self.streams:
+            self._shard_ctxs(dev)
+        torch.cuda.synchronize(dev)
         graph = torch.cuda.CUDAGraph()
         with torch.cuda.graph(graph):
             res = self.run(frames_bgr, out)

@@ -16,11 +16,18 @@
  *  - Calls on one context must not overlap in time from several host threads.
  *  - A context's forward activation arena is ONE set of buffers: ENet forwards of one context must
  *    all be enqueued on one stream (run concurrent frame shards on one context each, as
- *    pipeline.py does). bugseg_bev_occgrid keeps its laserscan scratch per stream, so BEV calls of
- *    one context may be enqueued on several streams at once. Any reallocation of a table, scratch
- *    or arena first synchronises the device, so nothing in flight on any stream reads freed memory.
+ *    pipeline.py does). BEV calls of one context may be enqueued on several streams at once: the
+ *    warp-tap and polar tables are read-only once built, and the laserscan batch scratch is either
+ *    the caller's workspace (bugseg_bev_occgrid_ws) or kept per stream (bugseg_bev_occgrid).
+ *  - Stream order, graphs: the BEV entry points never synchronise the caller's stream or the
+ *    device. A table for a new geometry is built on the context's private stream and waited for
+ *    there before the call enqueues its work, so the first call at a new geometry or batch may be
+ *    captured into a HIP graph (so may the first forward at a shape). Memory a captured call used
+ *    (arena, tables, scratch) is kept until bugseg_destroy. The rare eviction of an uncaptured
+ *    table (a 5th geometry) and arena reallocation at a new shape outside a capture synchronise
+ *    the device first, so nothing in flight reads freed memory.
  *  - Tensor shapes: activations are NHWC. The "engine input" tensor is (B, H, W, 8): RGB plus 5
- *    zero channels, in the context precision (f32 or bf16).
+ *    zero channels, in the context precision (f32, bf16 or f16).
  */
 #ifndef BUGSEG_H
 #define BUGSEG_H
@@ -143,6 +150,14 @@ int bugseg_enet_forward_bgr(bugseg_ctx *ctx, const uint8_t *bgr_dev, int B, int 
  * keeps polar tables per geometry in the context and its batch scratch per (context, stream). */
 int bugseg_bev_occgrid(bugseg_ctx *ctx, const uint8_t *seg_dev, int B, const bugseg_bev_params *p,
                        int8_t *out_dev, void *stream);
+
+/* The stream-ordered form of bugseg_bev_occgrid: the laserscan batch scratch is a caller-owned
+ * device workspace of at least bugseg_bev_workspace_bytes(p, B) bytes (0 when p->laserscan is 0:
+ * workspace may then be NULL), used only by the work this call enqueues on `stream` — so the caller's
+ * allocator orders its reuse (e.g. torch's caching allocator, graph pools included). */
+size_t bugseg_bev_workspace_bytes(const bugseg_bev_params *p, int B);
+int bugseg_bev_occgrid_ws(bugseg_ctx *ctx, const uint8_t *seg_dev, int B, const bugseg_bev_params *p,
+                          int8_t *out_dev, void *workspace_dev, size_t workspace_bytes, void *stream);
 
 /* Plan introspection for the bench / roofline, for the engine-input entry (bgr_input = 0) or
  * bugseg_enet_forward_bgr (bgr_input = 1), context precision:

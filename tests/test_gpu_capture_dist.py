@@ -1,0 +1,176 @@
+"""Stream order and graphs: the BEV entry points build their tables on
+the context's private stream and take their laserscan scratch from the caller (torch's allocator),
+so the FIRST call at a new geometry and batch can be captured into a HIP graph — for the rasteriser
+alone and for a whole OccupancyPipeline step, laserscan mode included, on 1 and 2 shard streams.
+
+The N > 1 product path on one GPU: two ranks of a gloo
+process group, both on cuda:0, each runs OccupancyPipeline over its shard_bounds shard and the
+grids go through distributed.gather_grids; and bench.py's distributed branch end to end under
+torch.distributed.run with --backend gloo (a functional run, not a timing).
+"""
+import json
+import os
+import socket
+import subprocess
+import sys
+
+import numpy as np
+import pytest
+import torch
+import torch.multiprocessing as mp
+
+from bugcar_image_segmentation_amd import enet_spec, synthetic
+from bugcar_image_segmentation_amd.models import ENET
+from bugcar_image_segmentation_amd.pipeline import OccupancyPipeline
+from oracle import ocv_c
+
+pytestmark = pytest.mark.gpu
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _fresh_bev(rows, cols, ww, wh, seed):
+    """A calibration no earlier call has used (perturbed matrix): its tables do not exist yet."""
+    rng = np.random.default_rng(1000 + seed)
+    bev = synthetic.synthetic_bev(rows, cols, ww, wh)
+    bev._bev_matrix = bev._bev_matrix @ np.array([[1 + 0.03 * rng.normal(), 0.01 * rng.normal(), 3 * rng.normal()],
+                                                  [0.01 * rng.normal(), 1 + 0.03 * rng.normal(), 3 * rng.normal()],
+                                                  [1e-5 * rng.normal(), 1e-5 * rng.normal(), 1.0]])
+    return bev
+
+
+def _oracle(bev, segs, grid, binary, laserscan):
+    M, ww, wh = bev._bev_matrix, bev.after_warp_width, bev.after_warp_height
+    if binary and laserscan:
+        pairs = [ocv_c.create_occupancy_grid_binary_laserscan(s, M, ww, wh, 1.0, *grid) for s in segs]
+        return np.stack([np.stack([p[0] for p in pairs]), np.stack([p[1] for p in pairs])])
+    f = {(0, 0): ocv_c.create_occupancy_grid, (0, 1): ocv_c.create_occupancy_grid_laserscan,
+         (1, 0): ocv_c.create_occupancy_grid_binary}[(int(binary), int(laserscan))]
+    return np.stack([f(s, M, ww, wh, 1.0, *grid) for s in segs])
+
+
+@pytest.mark.parametrize("binary", [False, True])
+@pytest.mark.parametrize("laserscan", [False, True])
+def test_capture_first_bev_call_at_new_geometry(gpu, laserscan, binary):
+    rows, cols, ww, wh, grid = 120, 160, 300, 260, (3.0, 2.0, 0.05)
+    bev = _fresh_bev(rows, cols, ww, wh, 2 * int(laserscan) + int(binary))
+    bev.laserscan_like_occupancy_grid = laserscan
+    rng = np.random.default_rng(5)
+    a = np.kron(rng.integers(0, 3, size=(5, rows // 8, cols // 8)), np.ones((1, 8, 8), np.int64)).astype(np.uint8)
+    b = rng.integers(0, 3, size=(5, rows, cols)).astype(np.uint8)
+    seg = torch.from_numpy(a).to(gpu)
+    p = bev.occupancy_params(*grid, binary=binary)
+    shape = (5, p.occ_h, p.occ_w)
+    out = torch.empty(((2,) + shape) if binary and laserscan else shape, dtype=torch.int8, device=gpu)
+    torch.cuda.synchronize()
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g):                         # the first call at this geometry and batch
+        bev.create_occupancy_grid_device(seg, *grid, out=out, binary=binary)
+    g.replay()
+    torch.cuda.synchronize()
+    assert np.array_equal(out.cpu().numpy(), _oracle(bev, a, grid, binary, laserscan))
+    seg.copy_(torch.from_numpy(b))                    # the replay re-reads the class maps
+    g.replay()
+    torch.cuda.synchronize()
+    assert np.array_equal(out.cpu().numpy(), _oracle(bev, b, grid, binary, laserscan))
+    # eager calls on the same context after the capture: same tables, same results
+    assert np.array_equal(bev.create_occupancy_grid_device(seg, *grid, binary=binary).cpu().numpy(),
+                          _oracle(bev, b, grid, binary, laserscan))
+
+
+@pytest.mark.parametrize("warm", [False, True])
+@pytest.mark.parametrize("laserscan", [False, True])
+@pytest.mark.parametrize("streams", [1, 2])
+def test_captured_pipeline_laserscan_and_first_call(gpu, blocks, streams, laserscan, warm):
+    """OccupancyPipeline.capture with the laserscan-like mode on and off, on 1 and 2 shard streams;
+    warm=False captures the very first step (arenas, tables and scratch come into being during the
+    capture). The replay equals an eager pipeline on other contexts."""
+    H, W, B = 96, 128, 6
+    bev = _fresh_bev(H, W, 300, 300, 10 + 4 * streams + 2 * int(laserscan) + int(warm))
+    bev.laserscan_like_occupancy_grid = laserscan
+    grid = (3.0, 3.0, 0.05)
+    fa = torch.from_numpy(synthetic.road_frames(B, H, W, seed=31)).to(gpu)
+    fb = torch.from_numpy(synthetic.road_frames(B, H, W, seed=32)).to(gpu)
+    ref_model = ENET(weights=blocks, precision="bf16")
+    eager = OccupancyPipeline(ref_model, bev, *grid, model_hw=(H, W))
+    ref_a, ref_b = eager.run(fa).clone(), eager.run(fb).clone()
+    model = ENET(weights=blocks, precision="bf16")
+    pipe = OccupancyPipeline(model, bev, *grid, model_hw=(H, W), streams=streams)
+    buf = fa.clone()
+    replay, grids = pipe.capture(buf, warm=warm)
+    replay()
+    torch.cuda.synchronize()
+    assert torch.equal(grids, ref_a)
+    buf.copy_(fb)
+    replay()
+    torch.cuda.synchronize()
+    assert torch.equal(grids, ref_b)
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def _gloo_gpu_worker(rank, world, port, total, q):
+    import torch.distributed as dist
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        torch.cuda.set_device(0)
+        from bugcar_image_segmentation_amd.distributed import gather_grids, shard_bounds
+        H, W = 96, 128
+        model = ENET(weights=enet_spec.build_enet(), precision="fp16")
+        bev = synthetic.synthetic_bev(H, W, 300, 300)
+        pipe = OccupancyPipeline(model, bev, 3.0, 3.0, 0.05, model_hw=(H, W), streams=2)
+        frames = synthetic.road_frames(total, H, W, seed=40)     # every rank holds the same batch
+        s, e = shard_bounds(total, world, rank)
+        local = pipe.run(torch.from_numpy(frames[s:e]).cuda())
+        full = gather_grids(local, total)
+        assert full.is_cuda and full.shape[0] == total
+        q.put((rank, full.cpu().numpy()))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.timeout(240)
+def test_sharded_pipeline_two_ranks_one_gpu(gpu, blocks):
+    world, total = 2, 7                              # uneven shards: 4 + 3 frames
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_gloo_gpu_worker, args=(r, world, port, total, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    got = dict(q.get(timeout=200) for _ in range(world))
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    H, W = 96, 128
+    model = ENET(weights=blocks, precision="fp16")
+    bev = synthetic.synthetic_bev(H, W, 300, 300)
+    one = OccupancyPipeline(model, bev, 3.0, 3.0, 0.05, model_hw=(H, W)).run(
+        torch.from_numpy(synthetic.road_frames(total, H, W, seed=40)).to(gpu)).cpu().numpy()
+    for r in range(world):
+        assert np.array_equal(got[r], one), r
+
+
+@pytest.mark.timeout(240)
+def test_bench_distributed_branch_gloo_one_gpu(gpu):
+    """bench.py's N > 1 branch (process group, in-step gather_grids, max-over-ranks timing, the
+    gathered-grid check) run end to end by torch.distributed.run with 2 ranks on this one GPU."""
+    port = _free_port()
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
+           "--master-addr", "127.0.0.1", "--master-port", str(port), "bench.py", "--gpus", "2",
+           "--backend", "gloo", "--steps", "3", "--warmup", "1", "--batch", "4", "--height", "96", "--width", "128",
+           "--extras", "0", "--no-cpu-baseline"]
+    env = dict(os.environ, HSA_ENABLE_IPC_MODE_LEGACY=os.environ.get("HSA_ENABLE_IPC_MODE_LEGACY", "0"))
+    r = subprocess.run(cmd, cwd=ROOT, capture_output=True, text=True, timeout=220, env=env)
+    assert r.returncode == 0, r.stderr[-3000:]
+    line = json.loads([ln for ln in r.stdout.splitlines() if ln.startswith("{")][-1])
+    print(json.dumps({k: line[k] for k in ("value", "n_gpus", "ms_per_step", "config")}))
+    assert line["config"]["global_batch"] == 8 and line["config"]["gather_check"] is True
+    assert line["n_gpus"] == 1 and line["value"] > 0

@@ -2,7 +2,8 @@
 (bugseg_dl_*) against the CPU oracle (oracle/deeplab_oracle.py) on the same synthetic weights.
 
 Tolerances: fp32 mode — logits within 1e-3 absolute of the oracle (fp64 at reduced width, fp32 at
-full size), class maps exact wherever the oracle's top-2 margin of the upsampled logits exceeds 2e-3;
+full size), class maps exact wherever the oracle's top-2 margin of the upsampled logits exceeds 4x the measured max
+logit error (floor 1e-5; the excused near-tie count is printed and bounded);
 the resize + argmax stage is checked bit-exactly against the oracle's TF-formula restatement applied
 to the GPU's own logits. bf16 mode — against the oracle's bf16-storage emulation: mean |dlogit|
 < 2e-2, class agreement > 98%.
@@ -19,7 +20,6 @@ from oracle import deeplab_oracle as O
 pytestmark = pytest.mark.gpu
 
 LOGIT_TOL = 1e-3
-MARGIN = 2e-3
 
 
 def _frames(B, H, W, seed):
@@ -40,13 +40,18 @@ def _check_fp32(model, net, x, ref_dtype):
     # resize + argmax kernel: bit-exact on the GPU's own logits
     assert np.array_equal(got_cls, O.predict(net, x, logits=got))
     # class maps vs the oracle wherever its margin decides them
+    # (the bilinear upsampling is a convex combination: its logits are within the same max error)
+    err = float(np.abs(got - ref).max())
+    thr = max(4.0 * err, 1e-5)
     up = O.resize_bilinear_tf(ref, *S.crop_hw(net))[:, :, :x.shape[1], :x.shape[2]]
     s = np.sort(up, axis=1)
-    decided = (s[:, -1] - s[:, -2]) > MARGIN
+    decided = (s[:, -1] - s[:, -2]) > thr
     ref_cls = O.predict(net, x, logits=ref)
     assert got_cls.dtype == np.int64 and got_cls.shape == x.shape[:3]
     assert np.array_equal(got_cls[decided], ref_cls[decided])
-    assert decided.mean() > 0.98
+    n_exc = int(decided.size - decided.sum())
+    print(f"deeplab fp32 max|dlogit| {err:.2e}; margin threshold {thr:.2e}; excused {n_exc} of {decided.size}")
+    assert n_exc / decided.size <= 1e-3
 
 
 @pytest.mark.parametrize("B,H,W,os_,rates", [(2, 90, 97, 8, ()), (1, 97, 97, 16, (6, 12, 18)), (3, 64, 40, 8, ())])

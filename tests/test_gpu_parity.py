@@ -1,9 +1,11 @@
 """GPU parity: every kernel through the C ABI against the CPU oracle (oracle/), same seeded inputs.
 
 Tolerances (written here, as north_star states them): fp32 mode — logits within 1e-3 absolute of
-the fp32 oracle, class maps exact wherever the oracle's top-2 logit margin exceeds 2e-3 (a pixel
-whose two best classes are closer than the tolerance is undecided by that tolerance); bf16 mode —
-agreement rate reported and bounded. Integer / byte paths (preprocess, BEV rasteriser) bit-exact.
+the fp32 oracle, class maps exact on every pixel whose oracle top-2 logit margin exceeds 4x this
+run's measured max |logit error| (floor 1e-5; with every logit within e of the oracle, a margin
+above 2e is decided identically, so only true near-ties are excused — their count is printed and
+bounded); bf16 / fp16 modes — against the oracle with the same storage numerics, agreement rate
+reported and bounded. Integer / byte paths (preprocess, BEV rasteriser) bit-exact.
 """
 import os
 from pathlib import Path
@@ -23,12 +25,24 @@ from oracle import ocv_c, ocv_np
 pytestmark = pytest.mark.gpu
 
 LOGIT_TOL = 1e-3
-MARGIN = 2e-3
 
 
 def _margin(logits):
     s = np.sort(logits, axis=1)
     return s[:, -1] - s[:, -2]
+
+
+def _decided(ref, got, max_excused=1e-3, what=""):
+    """Mask of the pixels whose oracle top-2 margin exceeds 4 x max|got - ref| (floor 1e-5): the
+    pixels on which class equality is asserted. Prints and bounds the excused (near-tie) share."""
+    err = float(np.abs(got - ref).max())
+    thr = max(4.0 * err, 1e-5)
+    dec = _margin(ref) > thr
+    n_exc = int(dec.size - dec.sum())
+    print(f"{what} max|dlogit| {err:.2e}; margin threshold {thr:.2e}; excused {n_exc} of {dec.size} pixels "
+          f"({n_exc / dec.size:.2e})")
+    assert n_exc / dec.size <= max_excused
+    return dec
 
 
 @pytest.fixture(scope="module")
@@ -48,7 +62,7 @@ def test_enet_fp32_logits_and_classes(fp32_model, blocks, B, H, W):
     got = fp32_model.logits(x)
     assert got.shape == ref.shape and got.dtype == np.float32
     assert np.abs(got - ref).max() < LOGIT_TOL
-    decided = _margin(ref) > MARGIN
+    decided = _decided(ref, got, what=f"fp32 {B}x{H}x{W}")
     cls_ref = eo.argmax_classes(ref)
     raw = fp32_model.predict_device(fp32_model.engine_input(x), N.OUT_CLASS15_U8).cpu().numpy()
     assert (raw[decided] == cls_ref[decided]).all()
@@ -65,8 +79,8 @@ def test_enet_fp32_model_resolution(fp32_model, blocks):
     ref = eo.forward(blocks, x)
     got = fp32_model.logits(x)
     assert np.abs(got - ref).max() < LOGIT_TOL
-    decided = _margin(ref) > MARGIN
-    assert decided.mean() > 0.98
+    decided = _decided(ref, got, max_excused=1e-4, what="fp32 480x640")
+    assert (got.argmax(1)[decided] == eo.argmax_classes(ref)[decided]).all()
     assert (fp32_model.predict(x)[decided] == eo.LUT3[eo.argmax_classes(ref)][decided]).all()
 
 
@@ -131,7 +145,7 @@ def test_class_counts(gpu, ncls):
     got = m.logits(x)
     assert got.shape == ref.shape == (1, ncls, 64, 96)
     assert np.abs(got - ref).max() < LOGIT_TOL
-    decided = _margin(ref) > MARGIN
+    decided = _decided(ref, got, what=f"fp32 {ncls} classes")
     raw = m.predict_device(m.engine_input(x), N.OUT_CLASS15_U8).cpu().numpy()
     assert (raw[decided] == eo.argmax_classes(ref)[decided]).all()
 
@@ -352,7 +366,7 @@ def test_class_layer_kernel_matches_conv_path(gpu, blocks, prec, monkeypatch):
     np.testing.assert_allclose(la, lb, rtol=0, atol=tol * max(1.0, float(np.abs(lb).max())))
     # the kernel's class map is exactly tf.math.argmax of its own logits (lowest index on ties)
     assert np.array_equal(raw.cpu().numpy(), la.argmax(axis=1))
-    decided = _margin(lb) > (MARGIN if prec == "fp32" else 0.1)
+    decided = _decided(lb, la, what=f"class kernel vs conv path ({prec})") if prec == "fp32" else _margin(lb) > 0.1
     assert (la.argmax(axis=1)[decided] == lb.argmax(axis=1)[decided]).all()
 
 
@@ -393,8 +407,10 @@ def test_pipeline_end_to_end_fp32(fp32_model, blocks):
     cls = fp32_model.predict(x)
     own = np.stack([ocv_c.create_occupancy_grid(c, bev._bev_matrix, 1000, 1000, 1.0, *grid) for c in cls])
     assert np.array_equal(out, own)
-    decided = _margin(logits_ref) > MARGIN
+    decided = _decided(logits_ref, fp32_model.logits(x), max_excused=1e-4, what="pipeline fp32 480x640")
     assert (cls[decided] == cls_ref[decided]).all()
+    seg = pipe._seg.cpu().numpy()              # the fused-preprocess class maps of the pipeline itself
+    assert (seg[decided] == cls_ref[decided]).all()
     print(f"end-to-end grid agreement vs oracle {(out == grids_ref).mean():.6f}")
 
 
@@ -476,7 +492,7 @@ def test_config1_reference_resolution_fp32(fp32_model, blocks):
     """BASELINE config 1: a 512x512 BGR frame -> ENET.preprocess (cv2.resize INTER_LINEAR to
     512x256, BGR->RGB, (x/256 - mean)/std; models.py:84-95) -> the fp32 forward at the reference's
     native 256x512 (models.py:19, 42-44) -> logits within 1e-3 of the oracle, class maps (predict and
-    predict_binary, models.py:55-58, 78-80) equal on every pixel whose top-2 margin exceeds 2e-3."""
+    predict_binary, models.py:55-58, 78-80) equal on every pixel whose top-2 margin exceeds 4x the measured max logit error."""
     frame = synthetic.road_frames(1, 512, 512, seed=21)[0]
     x = ENET.preprocess(frame)
     assert x.shape == (1, 3, 256, 512) and x.dtype == np.float64
@@ -485,8 +501,7 @@ def test_config1_reference_resolution_fp32(fp32_model, blocks):
     got = fp32_model.logits(x)
     assert got.shape == ref.shape == (1, 15, 256, 512)
     assert np.abs(got - ref).max() < LOGIT_TOL
-    decided = _margin(ref) > MARGIN
-    assert decided.mean() > 0.98
+    decided = _decided(ref, got, max_excused=1e-4, what="config 1 fp32 256x512")
     cls = eo.argmax_classes(ref)
     p3 = fp32_model.predict(x)
     assert p3.shape == (1, 256, 512) and p3.dtype == np.uint8
@@ -565,7 +580,7 @@ def test_enet_from_graphdef_matches_graph_interpreter(gpu, tmp_path, style):
     (tests/graph_writer.py; the real enet.pb is absent): ENET("x.pb") — the reference's constructor
     (models.py:21-31) through the GraphDef importer — against the NumPy interpreter of the same
     graph (oracle/tf_graph.py, the sess.run stand-in): logits within 1e-3 (fp32), classes equal
-    wherever the interpreter's top-2 margin exceeds 2e-3."""
+    wherever the interpreter's top-2 margin exceeds 4x the measured max logit error."""
     import sys
     sys.path.insert(0, str(Path(__file__).parent))
     from graph_writer import with_biases, write_enet_graphdef
@@ -583,8 +598,7 @@ def test_enet_from_graphdef_matches_graph_interpreter(gpu, tmp_path, style):
     assert got.shape == want.shape
     err = float(np.abs(got - want).max())
     assert err < 1e-3, err
-    s = np.sort(want, axis=1)
-    decided = (s[:, -1] - s[:, -2]) > 2e-3
+    decided = _decided(want, got, what=f"graphdef {style}")
     cls = np.argmax(want, axis=1)
     assert (model.predict(x)[decided] == eo.LUT3[cls][decided]).all()
 
@@ -594,7 +608,7 @@ def test_real_enet_pb_tf_parity(gpu):
     """The one-command TF-parity check for when the reference's pretrained_models/enet.pb is
     supplied: BUGSEG_ENET_PB=.../enet.pb pytest tests/test_gpu_parity.py -m gpu -k real_enet_pb.
     Same bar as the synthetic-graph test: logits within 1e-3 of the graph (interpreted), classes
-    equal wherever the top-2 margin exceeds 2e-3, at the reference's 256 x 512 input."""
+    equal wherever the top-2 margin exceeds 4x the measured max logit error, at the reference's 256 x 512 input."""
     from oracle import tf_graph
     path = os.environ["BUGSEG_ENET_PB"]
     pb = Path(path).read_bytes()
@@ -605,6 +619,5 @@ def test_real_enet_pb_tf_parity(gpu):
     model = ENET(path, precision="fp32")
     got = model.logits(x)
     assert np.abs(got - want).max() < 1e-3
-    s = np.sort(want, axis=1)
-    decided = (s[:, -1] - s[:, -2]) > 2e-3
+    decided = _decided(want, got, max_excused=1e-4, what="enet.pb")
     assert (model.predict(x)[decided] == eo.LUT3[np.argmax(want, axis=1)][decided]).all()
