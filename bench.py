@@ -61,22 +61,25 @@ def kernel_table(ctx, B, H, W, reps, stream):
         evs[r][n].record(stream)
     torch.cuda.synchronize()
     groups = {}
-    for i, (tag, _lb, pb, _fl) in enumerate(info):
+    for i, (tag, _lb, pb, fl) in enumerate(info):
         us = sum(evs[r][i].elapsed_time(evs[r][i + 1]) for r in range(reps)) / reps * 1e3
-        gr = groups.setdefault(tag, {"launches": 0, "total_us": 0.0, "bytes": 0.0})
+        gr = groups.setdefault(tag, {"launches": 0, "total_us": 0.0, "bytes": 0.0, "flops": 0.0})
         gr["launches"] += 1
         gr["total_us"] += us
         gr["bytes"] += pb
+        gr["flops"] += fl
     for gr in groups.values():
         gr["us_per_launch"] = gr["total_us"] / gr["launches"]
         gr["bytes_per_launch"] = gr["bytes"] / gr["launches"]
+        gr["flops_per_launch"] = gr["flops"] / gr["launches"]
     return groups
 
 
-def pmc_traffic(tag):
-    """HBM bytes per launch of `tag` from the committed PMC summary (profiles/pmc_traffic.json, written
-    by scripts/pmc_summary.py from rocprofv3 FETCH_SIZE / WRITE_SIZE passes of this bench), or None."""
-    p = os.path.join(ROOT, "profiles", "pmc_traffic.json")
+def pmc_traffic(tag, precision="fp16"):
+    """HBM bytes per launch of `tag` from the committed PMC summary (profiles/pmc_traffic.json for the
+    2-byte headline mode, profiles/pmc_traffic_fp32.json for the fp32 parity mode; written by
+    scripts/pmc_summary.py from rocprofv3 FETCH_SIZE / WRITE_SIZE passes of this bench), or None."""
+    p = os.path.join(ROOT, "profiles", "pmc_traffic_fp32.json" if precision == "fp32" else "pmc_traffic.json")
     try:
         with open(p) as f:
             t = json.load(f)
@@ -190,9 +193,105 @@ def cpu_baseline(blocks, bev, grid, H, W, budget_s):
                       f"{el:.1f} s at {t} threads (every CPU the process is granted), one frame per call"}
 
 
+def shard_overlap(pipe, frames, seg, g, bev, grid, H, W, reps):
+    """Does running the frame shards on their own streams overlap anything? The same shards' work
+    (forward + BEV per shard) timed (a) as the step runs it, each shard on its own stream, (b) all
+    of it serially on one stream, (c) the forwards alone on their streams, (d) the forwards alone
+    serially. (a) < (b) means the streams overlap; (a) vs (c) shows what the BEV adds to the step."""
+    from bugcar_image_segmentation_amd import _native as N
+    main = torch.cuda.current_stream()
+    ctxs, sts = pipe._shard_ctxs(frames.device)
+    S = pipe.streams
+    B = frames.shape[0]
+    bounds = [B * i // S for i in range(S + 1)]
+    p = pipe._params()
+
+    def run(parallel, with_bev):
+        ready = main.record_event()
+        for i in range(S):
+            s0, e0 = bounds[i], bounds[i + 1]
+            st = main if (i == 0 or not parallel) else sts[i - 1]
+            if st is not main:
+                st.wait_event(ready)
+            ctxs[i].forward_bgr(frames[s0:e0], e0 - s0, H, W, N.OUT_CLASS3_U8, seg[s0:e0], st)
+            if with_bev:
+                ctxs[i].bev(seg[s0:e0], e0 - s0, p, g[s0:e0], st)
+        if parallel:
+            for st in sts[: S - 1]:
+                main.wait_stream(st)
+
+    out = {}
+    for name, par, wb in (("shards_on_own_streams", True, True), ("serial_one_stream", False, True),
+                          ("forwards_only_own_streams", True, False), ("forwards_only_serial", False, False)):
+        run(par, wb)
+        ev = [torch.cuda.Event(enable_timing=True) for _ in range(2)]
+        ev[0].record(main)
+        for _ in range(reps):
+            run(par, wb)
+        ev[1].record(main)
+        ev[1].synchronize()
+        out[name] = round(ev[0].elapsed_time(ev[1]) / reps, 4)
+    out["frames"] = B
+    return out
+
+
+def forward_ms(ctx, fs, Bs, H, W, seg, stream, reps):
+    """Average ms of one forward of the Bs-frame shard (HIP events on the stream it runs on)."""
+    from bugcar_image_segmentation_amd import _native as N
+    ev = [torch.cuda.Event(enable_timing=True) for _ in range(2)]
+    ctx.forward_bgr(fs, Bs, H, W, N.OUT_CLASS3_U8, seg, stream)
+    ev[0].record(stream)
+    for _ in range(reps):
+        ctx.forward_bgr(fs, Bs, H, W, N.OUT_CLASS3_U8, seg, stream)
+    ev[1].record(stream)
+    ev[1].synchronize()
+    return ev[0].elapsed_time(ev[1]) / reps
+
+
+def roofline_record(ctx, Bs, H, W, reps, stream, precision, t_fwd):
+    """`roofline` of the dominant kernel of the forward the context last ran at (Bs, H, W): its
+    bytes per launch / its HIP-event launch time against the HBM peak, the PMC traffic of the same
+    kernel tag from the committed profile, and the whole forward's figures (bytes, and the MFMA
+    fraction against the dense peak of the precision's MFMA: f32 for fp32, bf16/f16 otherwise)."""
+    from bugcar_image_segmentation_amd import _native as N
+    kernels = kernel_table(ctx, Bs, H, W, reps, stream)
+    n_launch, alg_bytes, plan_bytes, flops = ctx.plan_info(Bs, H, W, N.OUT_CLASS3_U8, bgr_input=True)
+    tag, k = max(kernels.items(), key=lambda kv: kv[1]["total_us"])
+    k_achieved = k["bytes_per_launch"] / (k["us_per_launch"] * 1e-6) / 1e9
+    mpeak = MFMA_F32_PEAK_TFLOPS if precision == "fp32" else MFMA_BF16_PEAK_TFLOPS
+    k_flops = k.get("flops_per_launch", 0.0)
+    rec = {
+        "bound": "hbm", "achieved": round(k_achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+        "frac": round(k_achieved / HBM_PEAK_GBS, 4),
+        "traffic": pmc_traffic(tag, precision),
+        "kernel": f"{KERNEL_NAMES.get(tag.rsplit(' ', 1)[0], tag).format(t=TEMPLATE_TYPE[precision])} [{tag}]: the dominant kernel of the forward "
+                  f"({k['launches']} launches, {k['total_us']:.0f} us of {t_fwd * 1e3:.0f} us); "
+                  f"{k['bytes_per_launch'] / 1e6:.1f} MB per launch = the bytes the launch must move "
+                  f"(block input read once + output written once); {k['us_per_launch']:.2f} us per launch "
+                  f"(HIP events around each launch, in forward order)",
+        "kernel_mfma_tflops": round(k_flops / (k["us_per_launch"] * 1e-6) / 1e12, 2),
+        "kernel_mfma_frac": round(k_flops / (k["us_per_launch"] * 1e-6) / 1e12 / mpeak, 4),
+        "mfma_peak_tflops": mpeak,
+        "forward": {
+            "launches": n_launch, "ms": round(t_fwd, 4),
+            "survey_bytes_per_frame": SURVEY_BYTES_PER_FRAME,
+            "frames": Bs,
+            "survey_achieved_gbs": round(SURVEY_BYTES_PER_FRAME * Bs / (t_fwd * 1e-3) / 1e9, 1),
+            "plan_layer_bytes_per_frame": round(alg_bytes / Bs),
+            "plan_bytes_per_frame": round(plan_bytes / Bs),
+            "plan_achieved_gbs": round(plan_bytes / (t_fwd * 1e-3) / 1e9, 1),
+            "mfma_tflops": round(flops / (t_fwd * 1e-3) / 1e12, 2),
+            "mfma_frac": round(flops / (t_fwd * 1e-3) / 1e12 / mpeak, 4)},
+    }
+    table = {t: {"launches": v["launches"], "us_per_launch": round(v["us_per_launch"], 2),
+                 "GBps": round(v["bytes_per_launch"] / (v["us_per_launch"] * 1e-6) / 1e9, 1)}
+             for t, v in sorted(kernels.items(), key=lambda kv: -kv[1]["total_us"])}
+    return rec, table
+
+
 def mode_record(blocks, bev, grid, H, W, frames, streams, steps, precision):
     """Another precision mode (fp32: the parity mode, logits within 1e-3 of the oracle; fp16 / bf16)
-    on the same step, same batch."""
+    on the same step, same batch; with its own roofline (dominant kernel, HBM and MFMA fractions)."""
     from bugcar_image_segmentation_amd.models import ENET
     from bugcar_image_segmentation_amd.pipeline import OccupancyPipeline
     B = frames.shape[0]
@@ -206,9 +305,15 @@ def mode_record(blocks, bev, grid, H, W, frames, streams, steps, precision):
         pipe.run(frames)
     torch.cuda.synchronize()
     el = time.perf_counter() - t0
+    stream = torch.cuda.current_stream()
+    Bs = B // streams if streams > 1 and B >= streams else B
+    _x, seg, _g = pipe._bufs(B, frames.device)
+    t_fwd = forward_ms(model.ctx, frames[:Bs], Bs, H, W, seg[:Bs], stream, 10)
+    roof, table = roofline_record(model.ctx, Bs, H, W, 10, stream, precision, t_fwd)
     del pipe, model
     return {"value": round(B * steps / el, 2), "unit": "frames/s", "ms_per_step": round(el / steps * 1e3, 4),
-            "per_gpu_batch": B, "steps": steps, "streams_per_gpu": streams, "dtype": precision}
+            "per_gpu_batch": B, "steps": steps, "streams_per_gpu": streams, "dtype": precision,
+            "roofline": roof, "kernels": table}
 
 
 def latency_b1(blocks, precision, bev, grid, H, W, frame, iters):
@@ -386,15 +491,12 @@ def main():
     ev[1].synchronize()
     t_ls = ev[0].elapsed_time(ev[1]) / reps
     bev.laserscan_like_occupancy_grid = False
-    n_launch, alg_bytes, plan_bytes, flops = model.ctx.plan_info(Bs, H, W, N.OUT_CLASS3_U8, bgr_input=True)
-    kernels = kernel_table(model.ctx, Bs, H, W, reps, stream)
+    roof, ktable = roofline_record(model.ctx, Bs, H, W, reps, stream, a.precision, t_fwd)
+    overlap = shard_overlap(pipe, frames, seg, g, bev, grid, H, W, reps) if a.streams > 1 and B >= a.streams else None
 
     if rank == 0:
         frames_total = B * world * a.steps
         value = frames_total / el
-        tag, k = max(kernels.items(), key=lambda kv: kv[1]["total_us"])
-        k_achieved = k["bytes_per_launch"] / (k["us_per_launch"] * 1e-6) / 1e9
-        traffic = pmc_traffic(tag)
         res = {
             "metric": "frames/sec ENet 640x480 segmentation -> BEV occupancy grid (synthetic), whole job",
             "value": round(value, 2), "unit": "frames/s", "n_gpus": world if a.backend == "nccl" else min(world, ndev), "steps": a.steps, "warmup": a.warmup,
@@ -408,32 +510,11 @@ def main():
                        "streams_per_gpu": a.streams, "hip_graph": bool(a.graph),
                        **({"backend": "rccl" if a.backend == "nccl" else "gloo (functional run, not a timing)",
                            "gather_check": gather_check} if world > 1 else {})},
-            "roofline": {
-                "bound": "hbm", "achieved": round(k_achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                "frac": round(k_achieved / HBM_PEAK_GBS, 4),
-                "traffic": traffic,
-                "kernel": f"{KERNEL_NAMES.get(tag.rsplit(' ', 1)[0], tag).format(t=TEMPLATE_TYPE[a.precision])} [{tag}]: the dominant kernel of the forward "
-                          f"({k['launches']} launches, {k['total_us']:.0f} us of {t_fwd * 1e3:.0f} us); "
-                          f"{k['bytes_per_launch'] / 1e6:.1f} MB per launch = the bytes the launch must move "
-                          f"(block input read once + output written once); {k['us_per_launch']:.2f} us per launch "
-                          f"(HIP events around each launch, in forward order)",
-                "forward": {
-                    "launches": n_launch, "ms": round(t_fwd, 4),
-                    "survey_bytes_per_frame": SURVEY_BYTES_PER_FRAME,
-                    "frames": Bs,
-                    "survey_achieved_gbs": round(SURVEY_BYTES_PER_FRAME * Bs / (t_fwd * 1e-3) / 1e9, 1),
-                    "plan_layer_bytes_per_frame": round(alg_bytes / Bs),
-                    "plan_bytes_per_frame": round(plan_bytes / Bs),
-                    "plan_achieved_gbs": round(plan_bytes / (t_fwd * 1e-3) / 1e9, 1),
-                    "mfma_tflops": round(flops / (t_fwd * 1e-3) / 1e12, 2),
-                    "mfma_frac": round(flops / (t_fwd * 1e-3) / 1e12 /
-                                       (MFMA_F32_PEAK_TFLOPS if a.precision == "fp32" else MFMA_BF16_PEAK_TFLOPS), 4)},
-            },
-            "kernels": {t: {"launches": v["launches"], "us_per_launch": round(v["us_per_launch"], 2),
-                            "GBps": round(v["bytes_per_launch"] / (v["us_per_launch"] * 1e-6) / 1e9, 1)}
-                        for t, v in sorted(kernels.items(), key=lambda kv: -kv[1]["total_us"])},
+            "roofline": roof,
+            "kernels": ktable,
             "stages_ms": {"frames": Bs, "enet_forward": round(t_fwd, 4), "bev_occgrid": round(t_bev, 4),
                           "bev_occgrid_laserscan": round(t_ls, 4)},
+            "shard_overlap_ms": overlap,
         }
         extras = a.extras if a.extras >= 0 else int(world == 1)
         if extras:
