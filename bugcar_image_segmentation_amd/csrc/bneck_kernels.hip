@@ -30,6 +30,7 @@
 // MFMA operand mapping as conv_kernels.hip: A = weights (row = output channel) from LDS, B = 8
 // channels of one pixel (16-B LDS or global read per lane), accumulator = 4 consecutive channels of
 // one pixel per lane. All three weight matrices stay in LDS for the workgroup's lifetime.
+#include <algorithm>
 #include <cstdlib>
 
 #include "bugseg_internal.h"
@@ -1084,8 +1085,11 @@ hipError_t launch_bneck(int prec, int C, bool asym, int v, const BneckArgs &a, h
     }
     int cap = grid_cap;
     if (cap <= 0) {
+        // (BUGSEG_BNECK_GRID=-k: 1/k of the resident slots, at least one per CU — leaves room for a
+        // concurrent shard's launch on another stream; A/B knob)
         const int spc = bneck_slots_per_cu(prec, C, asym, v, a.tr != 0, cin);
-        cap = spc > 0 && n_cu > 0 ? spc * n_cu : 2048;
+        const int per = grid_cap < 0 ? std::max(1, spc / -grid_cap) : spc;
+        cap = spc > 0 && n_cu > 0 ? per * n_cu : 2048;
     }
     int g = a.ntiles < cap ? a.ntiles : cap;
     g = (g + 7) & ~7;
