@@ -57,11 +57,15 @@ __global__ void __launch_bounds__(256, sizeof(T) == 2 ? 4 : 1) cls_kernel(const 
     using Raw = typename Tr<T>::Raw;
     constexpr int ES = (int)sizeof(T);
     __shared__ float sbias[64];
-    __shared__ int slut[16];
     const int tid = threadIdx.x, lane = tid & 63, col = lane & 31, h = lane >> 5;
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-    if (tid < 64) sbias[tid] = a.bias[tid];
-    if (tid < 16) slut[tid] = a.lut ? (int)a.lut[tid] : tid;
+    // a padding class (row (phase, c) with c >= ncls: zero weights) starts at -inf and stays there, so
+    // the argmax needs no class mask (the logits of those rows are never written)
+    if (tid < 64) sbias[tid] = (tid & 15) < a.ncls ? a.bias[tid] : -INFINITY;
+    // the class LUT as 16 nibbles in a 64-bit scalar: class c -> (lut64 >> 4c) & 15
+    uint64_t lut64 = 0;
+#pragma unroll
+    for (int c = 0; c < 16; ++c) lut64 |= (uint64_t)((a.lut ? (int)a.lut[c] : c) & 15) << (4 * c);
 
     // weights: block b, row r = lane's col -> packed row (phase 2b + ((r >> 2) & 1), class 4 (r >> 3) + (r & 3));
     // this lane's k half = channels 8h .. 8h + 7 of each tap
@@ -84,9 +88,6 @@ __global__ void __launch_bounds__(256, sizeof(T) == 2 ? 4 : 1) cls_kernel(const 
     for (int b = 0; b < 2; ++b) short_blk[b] = __ballot(nonzero(wr[b][2]) || nonzero(wr[b][3])) == 0;
     __syncthreads();
 
-    float cmask[16];                                  // 0 for a class of the model, -inf for padding
-#pragma unroll
-    for (int c = 0; c < 16; ++c) cmask[c] = c < a.ncls ? 0.f : -INFINITY;
     const auto rin = mkbuf(a.in, a.in_bytes);
     const int HWg = a.Hg * a.Wg;
     const size_t plane = (size_t)a.Hout * a.Wout;
@@ -140,15 +141,15 @@ __global__ void __launch_bounds__(256, sizeof(T) == 2 ? 4 : 1) cls_kernel(const 
     };
 
     // one group: MFMAs, argmax, stores; `nxt` first receives the next group's loads (they fly during
-    // this one; the two buffers alternate by unrolling, never by a runtime index)
+    // this one; the two buffers alternate by unrolling, never by a runtime index). Both 32-row blocks'
+    // MFMAs go first, then the two argmax scans run interleaved: two independent compare / select
+    // chains fill each other's VCC hazard slots.
     auto step = [&](int g, const Raw (&cur)[CLS_TAPS], Raw (&nxt)[CLS_TAPS]) {
         if (g + nw < g1) load(g + nw, nxt);
         const Px q = pixel(g);
-        int cls[2];
-        // one 32-row block at a time (16 accumulator VGPRs live)
+        f32x16 acc[2];
 #pragma unroll
         for (int b = 0; b < 2; ++b) {
-            f32x16 acc;
             // (the opaque offset keeps the compiler from hoisting these reads out of the group loop
             // into 32 loop-long VGPRs)
             int boff = (2 * b + h) * 16;
@@ -157,34 +158,46 @@ __global__ void __launch_bounds__(256, sizeof(T) == 2 ? 4 : 1) cls_kernel(const 
 #pragma unroll
             for (int j = 0; j < 4; ++j) {
                 const float4 v = bb[j];
-                acc[4 * j] = v.x; acc[4 * j + 1] = v.y; acc[4 * j + 2] = v.z; acc[4 * j + 3] = v.w;
+                acc[b][4 * j] = v.x; acc[b][4 * j + 1] = v.y; acc[b][4 * j + 2] = v.z; acc[b][4 * j + 3] = v.w;
             }
-            mma32(acc, wr[b][0], cur[0]);
-            mma32(acc, wr[b][1], cur[1]);
+        }
+#pragma unroll
+        for (int b = 0; b < 2; ++b) {
+            mma32(acc[b], wr[b][0], cur[0]);
+            mma32(acc[b], wr[b][1], cur[1]);
             if (!short_blk[b]) {
-                mma32(acc, wr[b][2], cur[2]);
-                mma32(acc, wr[b][3], cur[3]);
+                mma32(acc[b], wr[b][2], cur[2]);
+                mma32(acc[b], wr[b][3], cur[3]);
             }
-            if (LOGITS && q.ok) {
+        }
+        if (LOGITS && q.ok) {
+#pragma unroll
+            for (int b = 0; b < 2; ++b) {
                 float *lo = a.logits_out + (size_t)q.n * a.ncls * plane + (size_t)(2 * q.y + b) * a.Wout + 2 * q.x + h;
 #pragma unroll
                 for (int c = 0; c < 16; ++c)
-                    if (c < a.ncls) lo[(size_t)c * plane] = acc[c];
+                    if (c < a.ncls) lo[(size_t)c * plane] = acc[b][c];
             }
-            // argmax over this lane's classes = the sequential strict > scan from -inf of
-            // tf.math.argmax (models.py:55): the maximum (v_max ignores NaN), then its first index;
-            // nothing above -inf -> 0. Padding classes are masked by adding -inf (in place).
-#pragma unroll
-            for (int c = 0; c < 16; ++c) acc[c] += cmask[c];
-            float best = acc[0];
-#pragma unroll
-            for (int c = 1; c < 16; ++c) best = __builtin_fmaxf(best, acc[c]);
-            int bi = 15;
-#pragma unroll
-            for (int c = 14; c >= 0; --c) bi = acc[c] == best ? c : bi;
-            bi = best > -INFINITY ? bi : 0;
-            cls[b] = slut[bi];
         }
+        // argmax over this lane's classes = the sequential strict > scan from -inf of
+        // tf.math.argmax (models.py:55): the maximum (v_max ignores NaN), then its first index; no
+        // class equal to the maximum (all NaN) -> 0; all -inf -> 0 (class 0 equals the maximum)
+        float best[2];
+        int bi[2];
+#pragma unroll
+        for (int b = 0; b < 2; ++b) {
+            best[b] = acc[b][0];
+#pragma unroll
+            for (int c = 1; c < 16; ++c) best[b] = __builtin_fmaxf(best[b], acc[b][c]);
+            bi[b] = 0;
+        }
+#pragma unroll
+        for (int c = 15; c >= 0; --c)
+#pragma unroll
+            for (int b = 0; b < 2; ++b) bi[b] = acc[b][c] == best[b] ? c : bi[b];
+        int cls[2];
+#pragma unroll
+        for (int b = 0; b < 2; ++b) cls[b] = (int)(lut64 >> (4 * bi[b])) & 15;
         if (a.cls_out) {
             // lanes < 32 take output row 2y (their phase-(0,0) byte + the (0,1) byte of lane + 32), lanes
             // >= 32 row 2y + 1: one 2-byte store of pixels (2x, 2x + 1) each
