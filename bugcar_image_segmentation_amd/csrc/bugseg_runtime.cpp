@@ -1125,9 +1125,20 @@ int bugseg_create(int device, int precision, bugseg_ctx **out) {
             const double x = ((double)v / 256.0 - mean[ch]) / stdv[ch];
             std::memcpy(tab + 32 + (ch * 256 + v) * 8, &x, 8);
         }
-    if (hipMalloc(&c->dev_luts, sizeof(tab)) != hipSuccess || hipMemcpy(c->dev_luts, tab, sizeof(tab), hipMemcpyHostToDevice) != hipSuccess) {
-        delete c;
-        return fail(nullptr, BUGSEG_EHIP, "device allocation failed");
+    {
+        // uploaded on the context's private stream (never the legacy stream, which would join a capture
+        // in progress on another stream), so a context may be created while a stream is capturing
+        RelaxCapture relax;
+        hipStream_t s = setup_stream(c);
+        hipError_t e = s ? hipMalloc(&c->dev_luts, sizeof(tab)) : hipErrorInvalidValue;
+        if (e == hipSuccess) e = hipMemcpyAsync(c->dev_luts, tab, sizeof(tab), hipMemcpyHostToDevice, s);
+        if (e == hipSuccess) e = hipStreamSynchronize(s);
+        if (e != hipSuccess) {
+            if (c->dev_luts) (void)hipFree(c->dev_luts);
+            if (c->setup) (void)hipStreamDestroy(c->setup);
+            delete c;
+            return fail(nullptr, BUGSEG_EHIP, std::string("device allocation failed: ") + hipGetErrorString(e));
+        }
     }
     *out = c;
     return BUGSEG_OK;
