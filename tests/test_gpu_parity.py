@@ -1,10 +1,10 @@
 """GPU parity: every kernel through the C ABI against the CPU oracle (oracle/), same seeded inputs.
 
 Tolerances (written here, as north_star states them): fp32 mode — logits within 1e-3 absolute of
-the fp32 oracle, class maps exact on every pixel whose oracle top-2 logit margin exceeds 4x this
+the fp32 oracle, class maps exact on every pixel whose oracle top-2 logit margin exceeds 2.5x this
 run's measured max |logit error| (floor 1e-5; with every logit within e of the oracle, a margin
-above 2e is decided identically, so only true near-ties are excused — their count is printed and
-bounded); bf16 / fp16 modes — against the oracle with the same storage numerics, agreement rate
+above 2e is provably decided identically — 2.5e leaves room for the margin's own f32 rounding — so
+only true near-ties are excused; their count is printed and bounded); bf16 / fp16 modes — against the oracle with the same storage numerics, agreement rate
 reported and bounded. Integer / byte paths (preprocess, BEV rasteriser) bit-exact.
 """
 import os
@@ -33,10 +33,10 @@ def _margin(logits):
 
 
 def _decided(ref, got, max_excused=1e-3, what=""):
-    """Mask of the pixels whose oracle top-2 margin exceeds 4 x max|got - ref| (floor 1e-5): the
+    """Mask of the pixels whose oracle top-2 margin exceeds 2.5 x max|got - ref| (floor 1e-5): the
     pixels on which class equality is asserted. Prints and bounds the excused (near-tie) share."""
     err = float(np.abs(got - ref).max())
-    thr = max(4.0 * err, 1e-5)
+    thr = max(2.5 * err, 1e-5)
     dec = _margin(ref) > thr
     n_exc = int(dec.size - dec.sum())
     print(f"{what} max|dlogit| {err:.2e}; margin threshold {thr:.2e}; excused {n_exc} of {dec.size} pixels "
@@ -492,7 +492,7 @@ def test_config1_reference_resolution_fp32(fp32_model, blocks):
     """BASELINE config 1: a 512x512 BGR frame -> ENET.preprocess (cv2.resize INTER_LINEAR to
     512x256, BGR->RGB, (x/256 - mean)/std; models.py:84-95) -> the fp32 forward at the reference's
     native 256x512 (models.py:19, 42-44) -> logits within 1e-3 of the oracle, class maps (predict and
-    predict_binary, models.py:55-58, 78-80) equal on every pixel whose top-2 margin exceeds 4x the measured max logit error."""
+    predict_binary, models.py:55-58, 78-80) equal on every pixel whose top-2 margin exceeds 2.5x the measured max logit error."""
     frame = synthetic.road_frames(1, 512, 512, seed=21)[0]
     x = ENET.preprocess(frame)
     assert x.shape == (1, 3, 256, 512) and x.dtype == np.float64
@@ -580,7 +580,7 @@ def test_enet_from_graphdef_matches_graph_interpreter(gpu, tmp_path, style):
     (tests/graph_writer.py; the real enet.pb is absent): ENET("x.pb") — the reference's constructor
     (models.py:21-31) through the GraphDef importer — against the NumPy interpreter of the same
     graph (oracle/tf_graph.py, the sess.run stand-in): logits within 1e-3 (fp32), classes equal
-    wherever the interpreter's top-2 margin exceeds 4x the measured max logit error."""
+    wherever the interpreter's top-2 margin exceeds 2.5x the measured max logit error."""
     import sys
     sys.path.insert(0, str(Path(__file__).parent))
     from graph_writer import with_biases, write_enet_graphdef
@@ -608,7 +608,7 @@ def test_real_enet_pb_tf_parity(gpu):
     """The one-command TF-parity check for when the reference's pretrained_models/enet.pb is
     supplied: BUGSEG_ENET_PB=.../enet.pb pytest tests/test_gpu_parity.py -m gpu -k real_enet_pb.
     Same bar as the synthetic-graph test: logits within 1e-3 of the graph (interpreted), classes
-    equal wherever the top-2 margin exceeds 4x the measured max logit error, at the reference's 256 x 512 input."""
+    equal wherever the top-2 margin exceeds 2.5x the measured max logit error, at the reference's 256 x 512 input."""
     from oracle import tf_graph
     path = os.environ["BUGSEG_ENET_PB"]
     pb = Path(path).read_bytes()
