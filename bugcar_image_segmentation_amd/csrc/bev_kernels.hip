@@ -424,6 +424,150 @@ __global__ void __launch_bounds__(256, 4) bev_occgrid_lds_kernel(const BevArgs a
     }
 }
 
+// ---- band-staged form (the default when in_cols % 16 == 0): a workgroup owns one frame and a band of
+// BEV_BAND grid rows (all columns). A band of grid rows is a band of distances, so every tap its cells
+// read lies in one class-map box that is a few rows deep and at most the image wide; the box is a
+// property of the geometry (bev_bandbox_kernel, once per calibration, stored after the tap table).
+// The box is read with coalesced 16-B loads into LDS as segmap + 1 (bev.py:177, uint8 wrap-around),
+// with zeros where it leaves the image — exactly warpPerspective's BORDER_CONSTANT taps — and then
+// every tap of the band's cells is an unmasked LDS byte read: no gathers from global memory. Bands
+// whose box exceeds BEV_BAND_CAP gather from global memory (same arithmetic). XCD-aware: XCD x takes
+// bands x, x + 8, ... of every frame, so each XCD's L2 holds only its bands' share of the tap table.
+constexpr int BEV_BAND = 8, BEV_BAND_CAP = 40960, BEV_BAND_PF = BEV_BAND_CAP / 16 / 256;
+
+__host__ __device__ inline int bev_bands(int occ_h) { return (occ_h + BEV_BAND - 1) / BEV_BAND; }
+
+// per band: the class-map box (y0, xa, bh, bw) every valid tap of its cells reads, with a one-pixel
+// border, xa and bw whole 16-B chunks; bh = 0: no valid tap (every pixel reads the zero pad);
+// bh = -1: the box (+ its zero pad) exceeds BEV_BAND_CAP
+__global__ void __launch_bounds__(256) bev_bandbox_kernel(const BevArgs a, int4 *bbox) {
+    __shared__ int red[4];
+    const long cells = (long)a.occ_h * a.occ_w;
+    const int band = blockIdx.x, r0 = band * BEV_BAND, r1 = min(a.occ_h, r0 + BEV_BAND);
+    const int n = (r1 - r0) * a.occ_w;
+    int ylo = 1 << 30, yhi = -(1 << 30), xlo = 1 << 30, xhi = -(1 << 30);
+    for (int i = threadIdx.x; i < n * BEV_WIN; i += 256) {
+        const int c = i / BEV_WIN, k = i - c * BEV_WIN;
+        const long rem = (long)r0 * a.occ_w + c;
+        const uint2 e = slot_half(a.wtab[(long)(k >> 1) * cells + rem], k & 1);
+        const uint32_t v = (e.y >> 10) & 15;
+        const int sy = tap_sy(e), sx = tap_sx(e);
+        if (v & 3) { ylo = min(ylo, sy); yhi = max(yhi, sy); }
+        if (v & 12) { ylo = min(ylo, sy + 1); yhi = max(yhi, sy + 1); }
+        if (v & 5) { xlo = min(xlo, sx); xhi = max(xhi, sx); }
+        if (v & 10) { xlo = min(xlo, sx + 1); xhi = max(xhi, sx + 1); }
+    }
+    if (threadIdx.x < 4) red[threadIdx.x] = threadIdx.x & 1 ? -(1 << 30) : (1 << 30);
+    __syncthreads();
+    atomicMin(&red[0], ylo); atomicMax(&red[1], yhi); atomicMin(&red[2], xlo); atomicMax(&red[3], xhi);
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        int4 bx = make_int4(0, 0, 0, 16);
+        if (red[1] >= red[0]) {
+            const int y0 = red[0] - 1, bh = red[1] - red[0] + 3;
+            const int xa = (red[2] - 1) & ~15, bw = ((red[3] + 17) & ~15) - xa;
+            bx = make_int4(y0, xa, (long)bh * bw + 2 * bw + 16 <= BEV_BAND_CAP ? bh : -1, bw);
+        }
+        bbox[band] = bx;
+    }
+}
+
+__global__ void __launch_bounds__(256) bev_band_kernel(const BevArgs a) {
+    __shared__ __attribute__((aligned(16))) uint8_t box[BEV_BAND_CAP];
+    const int tid = threadIdx.x;
+    const long cells = (long)a.occ_h * a.occ_w;
+    const int nbands = bev_bands(a.occ_h), nbs = (nbands + 7) >> 3;
+    const int xcd = blockIdx.x & 7, rest = blockIdx.x >> 3;
+    const int band = (rest % nbs) * 8 + xcd, b = rest / nbs;
+    if (band >= nbands || b >= a.B) return;                    // workgroup-uniform
+    const int4 bb = reinterpret_cast<const int4 *>(a.wtab + (size_t)BEV_SLOTS * cells)[band];
+    const int r0 = band * BEV_BAND, n = (min(a.occ_h, r0 + BEV_BAND) - r0) * a.occ_w;
+    const uint32_t frame_bytes = (uint32_t)a.in_rows * (uint32_t)a.in_cols;
+    const auto seg = __builtin_amdgcn_make_buffer_rsrc(const_cast<uint8_t *>(a.seg) + (size_t)b * frame_bytes, (short)0,
+                                                       (int)frame_bytes, 0x00020000);
+    const bool lds = bb.z >= 0;                                // workgroup-uniform
+    const int y0 = bb.x, xa = bb.y, bh = lds ? bb.z : 0, bw = bb.w, zpad = bh * bw;
+    if (lds) {
+        // the box: all of this thread's 16-B chunks in flight before the first LDS store
+        const int cpr = bw >> 4, nch = bh * cpr;
+        uint4 pf[BEV_BAND_PF];
+        bool in[BEV_BAND_PF];
+#pragma unroll
+        for (int i = 0; i < BEV_BAND_PF; ++i) {
+            const int q = tid + 256 * i;
+            const int r = q / cpr, c = q - r * cpr;
+            const int gy = y0 + r, gx = xa + c * 16;
+            in[i] = q < nch && (unsigned)gy < (unsigned)a.in_rows && (unsigned)gx < (unsigned)a.in_cols;
+            pf[i] = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(
+                seg, in[i] ? (int)(gy * a.in_cols + gx) : (int)0x80000000, 0, 0));
+        }
+#pragma unroll
+        for (int i = 0; i < BEV_BAND_PF; ++i)
+            if (tid + 256 * i < nch)
+                *reinterpret_cast<uint4 *>(box + 16 * (tid + 256 * i)) =
+                    in[i] ? make_uint4(inc4(pf[i].x), inc4(pf[i].y), inc4(pf[i].z), inc4(pf[i].w)) : make_uint4(0u, 0u, 0u, 0u);
+        for (int i = tid; i < 2 * bw + 16; i += 256) box[zpad + i] = 0;
+        __syncthreads();
+    }
+    // value of template pixel e: its 4 taps from the box (or, for an oversized band, from global memory)
+    auto value = [&](uint2 e) -> int {
+        if (!lds) return tab_value(seg, a.in_cols, e);
+        const bool any = ((e.y >> 10) & 15) != 0;
+        const int o = any ? (tap_sy(e) - y0) * bw + (tap_sx(e) - xa) : zpad;
+        const uint8_t *p = box + o;
+        const uint32_t l0 = p[0], l1 = p[1], l2 = p[bw], l3 = p[bw + 1];
+        const uint32_t ax = e.y & 31u, ay = (e.y >> 5) & 31u;
+        const uint32_t wx = 32u + ax * 65535u, wy = 32u + ay * 65535u;   // (32 - a) | a << 16
+        const uint32_t top = dot2(l0 | l1 << 16, wx, 0u), bot = dot2(l2 | l3 << 16, wx, 0u);
+        return (int)(dot2(top | bot << 16, wy, 512u) >> 10);              // (sum + 2^14) >> 15 of OpenCV
+    };
+    const uint32_t inner = 0x739C0u;                  // bits of the 3x3 around p: rows 1..3, cols 1..3
+    for (int c = tid; c < n; c += 256) {
+        const int rem = r0 * a.occ_w + c;
+        const int cy = rem / a.occ_w, cx = rem - cy * a.occ_w;
+        const uint4 *tab = a.wtab + rem;
+        uint4 s3[5];
+#pragma unroll
+        for (int q = 0; q < 5; ++q) s3[q] = tab[(long)q * cells];
+        uint32_t m = 0;
+        int v = 0;
+#pragma unroll
+        for (int i = 0; i < 9; ++i) {
+            const uint2 e = slot_half(s3[i >> 1], i & 1);
+            const int t = value(e);
+            if (i == 0) v = t;
+            // outside the template: 1 (neutral for the erode: OpenCV's default erode border is +inf)
+            m |= (uint32_t)((e.y & TAB_OUT) || occupied(a, t)) << BEV_ORDER[i];
+        }
+        if (occupied(a, v) && (m & inner) != inner) {
+            // the ring completes the 5x5 window (opening at p = OR over q in N3(p) inside the template
+            // of AND over N3(q) of occupancy); if the 3x3 is all occupied, q = p already survives
+            int tx, ty;
+            cell_pixel(a, cx, cy, tx, ty);
+            uint4 sr[8];
+#pragma unroll
+            for (int q = 0; q < 8; ++q) sr[q] = tab[(long)(q + 5) * cells];
+#pragma unroll
+            for (int i = 9; i < BEV_WIN; ++i) {
+                const uint2 e = i == 9 ? slot_half(s3[4], 1) : slot_half(sr[(i >> 1) - 5], i & 1);
+                m |= (uint32_t)((e.y & TAB_OUT) || occupied(a, value(e))) << BEV_ORDER[i];
+            }
+            bool opened = false;
+#pragma unroll
+            for (int qy = -1; qy <= 1; ++qy)
+#pragma unroll
+                for (int qx = -1; qx <= 1; ++qx) {
+                    const bool inside = (unsigned)(tx + qx) < (unsigned)a.occ_w_px && (unsigned)(ty + qy) < (unsigned)a.occ_h_px;
+                    const int sh = qy * 5 + qx;
+                    const uint32_t win = sh >= 0 ? inner << sh : inner >> -sh;
+                    opened |= inside && (m & win) == win;
+                }
+            if (!opened) v = 2;                      // isolated occupied pixel -> free (bev.py:204-205)
+        }
+        bev_emit(a, b, rem, cx, cy, cells, v);
+    }
+}
+
 // ---- laserscan-like occupancy (bev.py:216-240; binary variant bev.py:143-164) ----------------------
 // The reference polar-warps the grid (cv2.warpPolar, nearest), finds per polar row (ray angle) the
 // nearest obstacle (np.where + npi.group_by(...).min — a Python loop over rays follows), stamps a
@@ -493,12 +637,19 @@ __global__ void __launch_bounds__(256) laserscan_kernel(const BevArgs a) {
     }
 }
 
+size_t bev_table_bytes(int occ_w, int occ_h) {
+    return (size_t)occ_w * occ_h * BEV_SLOTS * sizeof(uint4) + (size_t)bev_bands(occ_h) * sizeof(int4);
+}
+
 hipError_t launch_bev_table(const BevArgs &a, hipStream_t s) {
-    const long total = (long)a.occ_h * a.occ_w * BEV_SLOTS;
+    const long cells = (long)a.occ_h * a.occ_w, total = cells * BEV_SLOTS;
     long g = (total + 255) / 256;
     if (g > 8192) g = 8192;
     if (g < 1) g = 1;
     hipLaunchKernelGGL(bev_table_kernel, dim3((unsigned)g), dim3(256), 0, s, a);
+    // the band boxes of the band-staged form, after the tap table (same stream)
+    hipLaunchKernelGGL(bev_bandbox_kernel, dim3((unsigned)bev_bands(a.occ_h)), dim3(256), 0, s, a,
+                       reinterpret_cast<int4 *>(a.wtab + (size_t)BEV_SLOTS * cells));
     return hipGetLastError();
 }
 
@@ -516,7 +667,13 @@ hipError_t launch_bev(const BevArgs &a, hipStream_t s) {
     if (gf < 8) gf = 8;
     const char *fge = std::getenv("BUGSEG_BEV_FG");
     const int FG = fge ? std::atoi(fge) : 0;
-    if (F != 0 && a.in_cols % 16 == 0 && FG > 0) {
+    // BUGSEG_BEV_BAND=0: the gather / block-staged forms (A/B and tests)
+    const char *be = std::getenv("BUGSEG_BEV_BAND");
+    const bool banded = (!be || std::atoi(be) != 0) && !fe && FG == 0 && a.in_cols % 16 == 0;
+    if (banded) {
+        const long grid = 8L * ((bev_bands(a.occ_h) + 7) / 8) * a.B;
+        hipLaunchKernelGGL(bev_band_kernel, dim3((unsigned)grid), dim3(256), 0, s, a);
+    } else if (F != 0 && a.in_cols % 16 == 0 && FG > 0) {
         const long nblk = (long)((a.occ_w + BEV_CB - 1) / BEV_CB) * ((a.occ_h + BEV_CB - 1) / BEV_CB);
         const long grid = nblk * ((a.B + FG - 1) / FG);
         if (grid < (1L << 31)) hipLaunchKernelGGL(bev_occgrid_lds_kernel, dim3((unsigned)grid), dim3(256), 0, s, a, FG);

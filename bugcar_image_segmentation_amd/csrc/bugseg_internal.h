@@ -176,6 +176,7 @@ struct BevArgs {
 };
 hipError_t launch_bev(const BevArgs &a, hipStream_t s);
 hipError_t launch_bev_table(const BevArgs &a, hipStream_t s);
+size_t bev_table_bytes(int occ_w, int occ_h);   // tap table + per-band class-map boxes
 constexpr int BEV_WIN = 25, BEV_SLOTS = 13;
 
 }  // namespace bugseg

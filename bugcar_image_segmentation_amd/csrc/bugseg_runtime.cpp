@@ -1539,7 +1539,7 @@ int bev_occgrid(bugseg_ctx *ctx, const uint8_t *seg, int B, const bugseg_bev_par
             if (!s) return fail(ctx, BUGSEG_EHIP, "could not create the table-build stream");
             bugseg_ctx::BevTab t;
             t.key = key;
-            if (hipMalloc(&t.tab, cells * BEV_SLOTS * sizeof(uint4)) != hipSuccess)
+            if (hipMalloc(&t.tab, bev_table_bytes(a.occ_w, a.occ_h)) != hipSuccess)
                 return fail(ctx, BUGSEG_ENOMEM, "BEV table allocation failed");
             a.wtab = t.tab;
             hipError_t e = launch_bev_table(a, s);

@@ -145,7 +145,11 @@ __global__ void __launch_bounds__(256, sizeof(T) == 2 ? 4 : 1) cls_kernel(const 
     // MFMAs go first, then the two argmax scans run interleaved: two independent compare / select
     // chains fill each other's VCC hazard slots.
     auto step = [&](int g, const Raw (&cur)[CLS_TAPS], Raw (&nxt)[CLS_TAPS]) {
-        if (g + nw < g1) load(g + nw, nxt);
+        // unconditional: past the last group the loads are harmless (an out-of-range group reads
+        // zeros, a neighbour's group is read and dropped), and a static count of loads in flight
+        // lets the waits before the MFMAs name only this group's loads (a conditional prefetch
+        // made the compiler wait vmcnt(3), i.e. for the next group's first load as well)
+        load(g + nw, nxt);
         const Px q = pixel(g);
         f32x16 acc[2];
 #pragma unroll
