@@ -433,7 +433,9 @@ __global__ void __launch_bounds__(256, 4) bev_occgrid_lds_kernel(const BevArgs a
 // every tap of the band's cells is an unmasked LDS byte read: no gathers from global memory. Bands
 // whose box exceeds BEV_BAND_CAP gather from global memory (same arithmetic). XCD-aware: XCD x takes
 // bands x, x + 8, ... of every frame, so each XCD's L2 holds only its bands' share of the tap table.
-constexpr int BEV_BAND = 8, BEV_BAND_CAP = 40960, BEV_BAND_PF = BEV_BAND_CAP / 16 / 256;
+// 4 grid rows: ~1,600 workgroups at 32 frames, all resident at once (16 KB of LDS each); 8 rows (40 KB,
+// 3 per CU) left a second round of workgroups: 58.5 vs 62 us for the gather kernel
+constexpr int BEV_BAND = 4, BEV_BAND_CAP = 16384, BEV_BAND_PF = BEV_BAND_CAP / 16 / 256;
 
 __host__ __device__ inline int bev_bands(int occ_h) { return (occ_h + BEV_BAND - 1) / BEV_BAND; }
 
@@ -522,13 +524,23 @@ __global__ void __launch_bounds__(256) bev_band_kernel(const BevArgs a) {
         return (int)(dot2(top | bot << 16, wy, 512u) >> 10);              // (sum + 2^14) >> 15 of OpenCV
     };
     const uint32_t inner = 0x739C0u;                  // bits of the 3x3 around p: rows 1..3, cols 1..3
+    // the next cell's 3x3 table slots are in flight while this cell is evaluated (always issued, at a
+    // clamped index, so the waits count only the current cell's loads)
+    uint4 s3n[5];
+    auto load3 = [&](int c) {
+        const uint4 *t = a.wtab + r0 * a.occ_w + min(c, n - 1);
+#pragma unroll
+        for (int q = 0; q < 5; ++q) s3n[q] = t[(long)q * cells];
+    };
+    load3(tid);
     for (int c = tid; c < n; c += 256) {
         const int rem = r0 * a.occ_w + c;
         const int cy = rem / a.occ_w, cx = rem - cy * a.occ_w;
         const uint4 *tab = a.wtab + rem;
         uint4 s3[5];
 #pragma unroll
-        for (int q = 0; q < 5; ++q) s3[q] = tab[(long)q * cells];
+        for (int q = 0; q < 5; ++q) s3[q] = s3n[q];
+        load3(c + 256);
         uint32_t m = 0;
         int v = 0;
 #pragma unroll
