@@ -25,6 +25,7 @@
 // + occ_h*occ_w B written, plus the table entries a cell reads (1, 9 or 25 x 8 B, shared by every
 // frame: L2 / Infinity-Cache hits) — gather-bound, far below the HBM roof.
 #include <cstdlib>
+#include <type_traits>
 
 #include "bugseg_internal.h"
 
@@ -511,18 +512,9 @@ __global__ void __launch_bounds__(256) bev_band_kernel(const BevArgs a) {
         for (int i = tid; i < 2 * bw + 16; i += 256) box[zpad + i] = 0;
         __syncthreads();
     }
-    // value of template pixel e: its 4 taps from the box (or, for an oversized band, from global memory)
-    auto value = [&](uint2 e) -> int {
-        if (!lds) return tab_value(seg, a.in_cols, e);
-        const bool any = ((e.y >> 10) & 15) != 0;
-        const int o = any ? (tap_sy(e) - y0) * bw + (tap_sx(e) - xa) : zpad;
-        const uint8_t *p = box + o;
-        const uint32_t l0 = p[0], l1 = p[1], l2 = p[bw], l3 = p[bw + 1];
-        const uint32_t ax = e.y & 31u, ay = (e.y >> 5) & 31u;
-        const uint32_t wx = 32u + ax * 65535u, wy = 32u + ay * 65535u;   // (32 - a) | a << 16
-        const uint32_t top = dot2(l0 | l1 << 16, wx, 0u), bot = dot2(l2 | l3 << 16, wx, 0u);
-        return (int)(dot2(top | bot << 16, wy, 512u) >> 10);              // (sum + 2^14) >> 15 of OpenCV
-    };
+    // value of template pixel e: its 4 taps from the box (L) or, for an oversized band, from global
+    // memory. The two forms are separate loops (a compile-time choice): no branch between the taps,
+    // so each cell's 36 LDS byte reads are in flight together
     const uint32_t inner = 0x739C0u;                  // bits of the 3x3 around p: rows 1..3, cols 1..3
     // the next cell's 3x3 table slots are in flight while this cell is evaluated (always issued, at a
     // clamped index, so the waits count only the current cell's loads)
@@ -532,52 +524,70 @@ __global__ void __launch_bounds__(256) bev_band_kernel(const BevArgs a) {
 #pragma unroll
         for (int q = 0; q < 5; ++q) s3n[q] = t[(long)q * cells];
     };
-    load3(tid);
-    for (int c = tid; c < n; c += 256) {
-        const int rem = r0 * a.occ_w + c;
-        const int cy = rem / a.occ_w, cx = rem - cy * a.occ_w;
-        const uint4 *tab = a.wtab + rem;
-        uint4 s3[5];
-#pragma unroll
-        for (int q = 0; q < 5; ++q) s3[q] = s3n[q];
-        load3(c + 256);
-        uint32_t m = 0;
-        int v = 0;
-#pragma unroll
-        for (int i = 0; i < 9; ++i) {
-            const uint2 e = slot_half(s3[i >> 1], i & 1);
-            const int t = value(e);
-            if (i == 0) v = t;
-            // outside the template: 1 (neutral for the erode: OpenCV's default erode border is +inf)
-            m |= (uint32_t)((e.y & TAB_OUT) || occupied(a, t)) << BEV_ORDER[i];
-        }
-        if (occupied(a, v) && (m & inner) != inner) {
-            // the ring completes the 5x5 window (opening at p = OR over q in N3(p) inside the template
-            // of AND over N3(q) of occupancy); if the 3x3 is all occupied, q = p already survives
-            int tx, ty;
-            cell_pixel(a, cx, cy, tx, ty);
-            uint4 sr[8];
-#pragma unroll
-            for (int q = 0; q < 8; ++q) sr[q] = tab[(long)(q + 5) * cells];
-#pragma unroll
-            for (int i = 9; i < BEV_WIN; ++i) {
-                const uint2 e = i == 9 ? slot_half(s3[4], 1) : slot_half(sr[(i >> 1) - 5], i & 1);
-                m |= (uint32_t)((e.y & TAB_OUT) || occupied(a, value(e))) << BEV_ORDER[i];
+    auto cells_loop = [&](auto from_lds) {
+        constexpr bool L = decltype(from_lds)::value;
+        auto value = [&](uint2 e) -> int {
+            if constexpr (!L) {
+                return tab_value(seg, a.in_cols, e);
+            } else {
+                const bool any = ((e.y >> 10) & 15) != 0;
+                const int o = any ? (tap_sy(e) - y0) * bw + (tap_sx(e) - xa) : zpad;
+                const uint8_t *p = box + o;
+                const uint32_t l0 = p[0], l1 = p[1], l2 = p[bw], l3 = p[bw + 1];
+                const uint32_t ax = e.y & 31u, ay = (e.y >> 5) & 31u;
+                const uint32_t wx = 32u + ax * 65535u, wy = 32u + ay * 65535u;   // (32 - a) | a << 16
+                const uint32_t top = dot2(l0 | l1 << 16, wx, 0u), bot = dot2(l2 | l3 << 16, wx, 0u);
+                return (int)(dot2(top | bot << 16, wy, 512u) >> 10);              // (sum + 2^14) >> 15 of OpenCV
             }
-            bool opened = false;
+        };
+        load3(tid);
+        for (int c = tid; c < n; c += 256) {
+            const int rem = r0 * a.occ_w + c;
+            const int cy = rem / a.occ_w, cx = rem - cy * a.occ_w;
+            const uint4 *tab = a.wtab + rem;
+            uint4 s3[5];
 #pragma unroll
-            for (int qy = -1; qy <= 1; ++qy)
+            for (int q = 0; q < 5; ++q) s3[q] = s3n[q];
+            load3(c + 256);
+            int t9[9];
 #pragma unroll
-                for (int qx = -1; qx <= 1; ++qx) {
-                    const bool inside = (unsigned)(tx + qx) < (unsigned)a.occ_w_px && (unsigned)(ty + qy) < (unsigned)a.occ_h_px;
-                    const int sh = qy * 5 + qx;
-                    const uint32_t win = sh >= 0 ? inner << sh : inner >> -sh;
-                    opened |= inside && (m & win) == win;
+            for (int i = 0; i < 9; ++i) t9[i] = value(slot_half(s3[i >> 1], i & 1));
+            int v = t9[0];
+            uint32_t m = 0;
+#pragma unroll
+            for (int i = 0; i < 9; ++i)
+                // outside the template: 1 (neutral for the erode: OpenCV's default erode border is +inf)
+                m |= (uint32_t)((slot_half(s3[i >> 1], i & 1).y & TAB_OUT) || occupied(a, t9[i])) << BEV_ORDER[i];
+            if (occupied(a, v) && (m & inner) != inner) {
+                // the ring completes the 5x5 window (opening at p = OR over q in N3(p) inside the template
+                // of AND over N3(q) of occupancy); if the 3x3 is all occupied, q = p already survives
+                int tx, ty;
+                cell_pixel(a, cx, cy, tx, ty);
+                uint4 sr[8];
+#pragma unroll
+                for (int q = 0; q < 8; ++q) sr[q] = tab[(long)(q + 5) * cells];
+#pragma unroll
+                for (int i = 9; i < BEV_WIN; ++i) {
+                    const uint2 e = i == 9 ? slot_half(s3[4], 1) : slot_half(sr[(i >> 1) - 5], i & 1);
+                    m |= (uint32_t)((e.y & TAB_OUT) || occupied(a, value(e))) << BEV_ORDER[i];
                 }
-            if (!opened) v = 2;                      // isolated occupied pixel -> free (bev.py:204-205)
+                bool opened = false;
+#pragma unroll
+                for (int qy = -1; qy <= 1; ++qy)
+#pragma unroll
+                    for (int qx = -1; qx <= 1; ++qx) {
+                        const bool inside = (unsigned)(tx + qx) < (unsigned)a.occ_w_px && (unsigned)(ty + qy) < (unsigned)a.occ_h_px;
+                        const int sh = qy * 5 + qx;
+                        const uint32_t win = sh >= 0 ? inner << sh : inner >> -sh;
+                        opened |= inside && (m & win) == win;
+                    }
+                if (!opened) v = 2;                  // isolated occupied pixel -> free (bev.py:204-205)
+            }
+            bev_emit(a, b, rem, cx, cy, cells, v);
         }
-        bev_emit(a, b, rem, cx, cy, cells, v);
-    }
+    };
+    if (lds) cells_loop(std::true_type());
+    else cells_loop(std::false_type());
 }
 
 // ---- laserscan-like occupancy (bev.py:216-240; binary variant bev.py:143-164) ----------------------
