@@ -94,6 +94,10 @@ __device__ __forceinline__ void cell_pixel(const BevArgs &a, int cx, int cy, int
 __device__ constexpr int BEV_ORDER[BEV_WIN] = {12, 6, 7, 8, 11, 13, 16, 17, 18,
                                                0, 1, 2, 3, 4, 5, 9, 10, 14, 15, 19, 20, 21, 22, 23, 24};
 __device__ __forceinline__ uint2 slot_half(const uint4 &s, int h) { return h ? make_uint2(s.z, s.w) : make_uint2(s.x, s.y); }
+// BEV_ORDER as a runtime-indexed table (the band kernel's rolled ring loop); entry 25 (the padding half
+// of the last slot, TAB_OUT) sets bit 25, outside the 5x5 window bits every test reads
+__device__ constexpr int BEV_ORDER_D[2 * BEV_SLOTS] = {12, 6, 7, 8, 11, 13, 16, 17, 18, 0, 1, 2, 3,
+                                                       4, 5, 9, 10, 14, 15, 19, 20, 21, 22, 23, 24, 25};
 
 // One thread per (cell, table slot): the geometry-only half of the rasteriser, run once per
 // calibration. Everything per frame (bev_occgrid_kernel) is then integer gathers and Q15 arithmetic.
@@ -475,7 +479,9 @@ __global__ void __launch_bounds__(256) bev_bandbox_kernel(const BevArgs a, int4 
     }
 }
 
-__global__ void __launch_bounds__(256) bev_band_kernel(const BevArgs a) {
+// held to 72 VGPRs (7 waves per SIMD): the ~1,600 workgroups of a 32-frame call are then one round
+// (at 106 VGPRs, 4 waves per SIMD, they took 1.6 rounds)
+__global__ void __launch_bounds__(256, 7) bev_band_kernel(const BevArgs a) {
     __shared__ __attribute__((aligned(16))) uint8_t box[BEV_BAND_CAP];
     const int tid = threadIdx.x;
     const long cells = (long)a.occ_h * a.occ_w;
@@ -563,13 +569,18 @@ __global__ void __launch_bounds__(256) bev_band_kernel(const BevArgs a) {
                 // of AND over N3(q) of occupancy); if the 3x3 is all occupied, q = p already survives
                 int tx, ty;
                 cell_pixel(a, cx, cy, tx, ty);
-                uint4 sr[8];
-#pragma unroll
-                for (int q = 0; q < 8; ++q) sr[q] = tab[(long)(q + 5) * cells];
-#pragma unroll
-                for (int i = 9; i < BEV_WIN; ++i) {
-                    const uint2 e = i == 9 ? slot_half(s3[4], 1) : slot_half(sr[(i >> 1) - 5], i & 1);
-                    m |= (uint32_t)((e.y & TAB_OUT) || occupied(a, value(e))) << BEV_ORDER[i];
+                {
+                    const uint2 e = slot_half(s3[4], 1);          // ring entry 9 shares the 3x3's last slot
+                    m |= (uint32_t)((e.y & TAB_OUT) || occupied(a, value(e))) << BEV_ORDER[9];
+                }
+                // the other 16 ring entries a slot (two entries) at a time: few cells need the ring,
+                // and holding all 8 slots would cost the occupancy every cell runs at
+#pragma unroll 1
+                for (int q = 5; q < BEV_SLOTS; ++q) {
+                    const uint4 sq = tab[(long)q * cells];
+                    const int i0 = 2 * q;
+                    m |= (uint32_t)((sq.y & TAB_OUT) || occupied(a, value(make_uint2(sq.x, sq.y)))) << BEV_ORDER_D[i0];
+                    m |= (uint32_t)((sq.w & TAB_OUT) || occupied(a, value(make_uint2(sq.z, sq.w)))) << BEV_ORDER_D[i0 + 1];
                 }
                 bool opened = false;
 #pragma unroll
