@@ -63,7 +63,8 @@ __device__ __forceinline__ WarpTap warp_tap(const BevArgs &a, int x, int y) {
 
 // Table entry of a template pixel (bits of .y): 0-4 ax, 5-9 ay, 10-13 which taps (top-left,
 // top-right, bottom-left, bottom-right) are inside the class map, 14 = the pixel lies outside the
-// template (a neutral 1 for the erode: OpenCV's default erode border is +inf). .x = the top-left tap
+// template (a neutral 1 for the erode: OpenCV's default erode border is +inf), 15-31 = the top-left
+// tap's byte offset in the band's LDS box (bev_bandbox_kernel; band-staged form only). .x = the top-left tap
 // (sy << 16 | sx & 0xffff, both 16-bit signed). A pixel inside the template but outside the warped
 // image has no valid tap: value 0 (the crop/pad of bev.py:183-195).
 constexpr uint32_t TAB_OUT = 1u << 14;
@@ -468,14 +469,29 @@ __global__ void __launch_bounds__(256) bev_bandbox_kernel(const BevArgs a, int4 
     __syncthreads();
     atomicMin(&red[0], ylo); atomicMax(&red[1], yhi); atomicMin(&red[2], xlo); atomicMax(&red[3], xhi);
     __syncthreads();
-    if (threadIdx.x == 0) {
-        int4 bx = make_int4(0, 0, 0, 16);
-        if (red[1] >= red[0]) {
-            const int y0 = red[0] - 1, bh = red[1] - red[0] + 3;
-            const int xa = (red[2] - 1) & ~15, bw = ((red[3] + 17) & ~15) - xa;
-            bx = make_int4(y0, xa, (long)bh * bw + 2 * bw + 16 <= BEV_BAND_CAP ? bh : -1, bw);
-        }
-        bbox[band] = bx;
+    int4 bx = make_int4(0, 0, 0, 16);
+    if (red[1] >= red[0]) {
+        const int y0 = red[0] - 1, bh = red[1] - red[0] + 3;
+        const int xa = (red[2] - 1) & ~15, bw = ((red[3] + 17) & ~15) - xa;
+        bx = make_int4(y0, xa, (long)bh * bw + 2 * bw + 16 <= BEV_BAND_CAP ? bh : -1, bw);
+    }
+    if (threadIdx.x == 0) bbox[band] = bx;
+    if (bx.z < 0) return;
+    // each entry's top-left tap as a byte offset in the band's LDS box, in the entry's free bits 15..31
+    // (a template pixel without a valid tap: the zero pad after the box)
+    for (int i = threadIdx.x; i < n * BEV_SLOTS; i += 256) {
+        const int c = i / BEV_SLOTS, q = i - c * BEV_SLOTS;
+        uint4 *sp = a.wtab + (long)q * cells + (long)r0 * a.occ_w + c;
+        uint4 sv = *sp;
+        auto put = [&](uint32_t x, uint32_t &y) {
+            const uint2 e = make_uint2(x, y);
+            const bool any = ((y >> 10) & 15) != 0;
+            const int o = any ? (tap_sy(e) - bx.x) * bx.w + (tap_sx(e) - bx.y) : bx.z * bx.w;
+            y = (y & 0x7fffu) | (uint32_t)o << 15;
+        };
+        put(sv.x, sv.y);
+        put(sv.z, sv.w);
+        *sp = sv;
     }
 }
 
@@ -536,9 +552,7 @@ __global__ void __launch_bounds__(256, 7) bev_band_kernel(const BevArgs a) {
             if constexpr (!L) {
                 return tab_value(seg, a.in_cols, e);
             } else {
-                const bool any = ((e.y >> 10) & 15) != 0;
-                const int o = any ? (tap_sy(e) - y0) * bw + (tap_sx(e) - xa) : zpad;
-                const uint8_t *p = box + o;
+                const uint8_t *p = box + (e.y >> 15);                 // the tap's box offset (bandbox kernel)
                 const uint32_t l0 = p[0], l1 = p[1], l2 = p[bw], l3 = p[bw + 1];
                 const uint32_t ax = e.y & 31u, ay = (e.y >> 5) & 31u;
                 const uint32_t wx = 32u + ax * 65535u, wy = 32u + ay * 65535u;   // (32 - a) | a << 16
