@@ -495,48 +495,58 @@ __global__ void __launch_bounds__(256) bev_bandbox_kernel(const BevArgs a, int4 
     }
 }
 
-// held to 72 VGPRs (7 waves per SIMD): the ~1,600 workgroups of a 32-frame call are then one round
-// (at 106 VGPRs, 4 waves per SIMD, they took 1.6 rounds)
-__global__ void __launch_bounds__(256, 7) bev_band_kernel(const BevArgs a) {
-    __shared__ __attribute__((aligned(16))) uint8_t box[BEV_BAND_CAP];
+// FB frames per workgroup (one box each): a cell's table slots and entry decoding serve all FB frames.
+// Held to 7 waves per SIMD (FB = 1: 72 VGPRs) so the ~1,600 workgroups of a 32-frame call are one
+// round (at 106 VGPRs, 4 waves per SIMD, they took 1.6 rounds).
+template <int FB>
+__global__ void __launch_bounds__(256, FB == 1 ? 7 : 4) bev_band_kernel(const BevArgs a) {
+    __shared__ __attribute__((aligned(16))) uint8_t box[FB][BEV_BAND_CAP];
     const int tid = threadIdx.x;
     const long cells = (long)a.occ_h * a.occ_w;
     const int nbands = bev_bands(a.occ_h), nbs = (nbands + 7) >> 3;
     const int xcd = blockIdx.x & 7, rest = blockIdx.x >> 3;
-    const int band = (rest % nbs) * 8 + xcd, b = rest / nbs;
-    if (band >= nbands || b >= a.B) return;                    // workgroup-uniform
+    const int band = (rest % nbs) * 8 + xcd, b0 = (rest / nbs) * FB;
+    if (band >= nbands || b0 >= a.B) return;                   // workgroup-uniform
+    const int nf = min(FB, a.B - b0);                          // frames of this workgroup
     const int4 bb = reinterpret_cast<const int4 *>(a.wtab + (size_t)BEV_SLOTS * cells)[band];
     const int r0 = band * BEV_BAND, n = (min(a.occ_h, r0 + BEV_BAND) - r0) * a.occ_w;
     const uint32_t frame_bytes = (uint32_t)a.in_rows * (uint32_t)a.in_cols;
-    const auto seg = __builtin_amdgcn_make_buffer_rsrc(const_cast<uint8_t *>(a.seg) + (size_t)b * frame_bytes, (short)0,
-                                                       (int)frame_bytes, 0x00020000);
+    __amdgpu_buffer_rsrc_t seg[FB];
+#pragma unroll
+    for (int f = 0; f < FB; ++f)
+        seg[f] = __builtin_amdgcn_make_buffer_rsrc(const_cast<uint8_t *>(a.seg) + (size_t)(f < nf ? b0 + f : b0) * frame_bytes,
+                                                   (short)0, (int)frame_bytes, 0x00020000);
     const bool lds = bb.z >= 0;                                // workgroup-uniform
     const int y0 = bb.x, xa = bb.y, bh = lds ? bb.z : 0, bw = bb.w, zpad = bh * bw;
     if (lds) {
-        // the box: all of this thread's 16-B chunks in flight before the first LDS store
+        // each frame's box: all of this thread's 16-B chunks in flight before the first LDS store
         const int cpr = bw >> 4, nch = bh * cpr;
-        uint4 pf[BEV_BAND_PF];
-        bool in[BEV_BAND_PF];
 #pragma unroll
-        for (int i = 0; i < BEV_BAND_PF; ++i) {
-            const int q = tid + 256 * i;
-            const int r = q / cpr, c = q - r * cpr;
-            const int gy = y0 + r, gx = xa + c * 16;
-            in[i] = q < nch && (unsigned)gy < (unsigned)a.in_rows && (unsigned)gx < (unsigned)a.in_cols;
-            pf[i] = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(
-                seg, in[i] ? (int)(gy * a.in_cols + gx) : (int)0x80000000, 0, 0));
+        for (int f = 0; f < FB; ++f) {
+            if (f >= nf) break;
+            uint4 pf[BEV_BAND_PF];
+            bool in[BEV_BAND_PF];
+#pragma unroll
+            for (int i = 0; i < BEV_BAND_PF; ++i) {
+                const int q = tid + 256 * i;
+                const int r = q / cpr, c = q - r * cpr;
+                const int gy = y0 + r, gx = xa + c * 16;
+                in[i] = q < nch && (unsigned)gy < (unsigned)a.in_rows && (unsigned)gx < (unsigned)a.in_cols;
+                pf[i] = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(
+                    seg[f], in[i] ? (int)(gy * a.in_cols + gx) : (int)0x80000000, 0, 0));
+            }
+#pragma unroll
+            for (int i = 0; i < BEV_BAND_PF; ++i)
+                if (tid + 256 * i < nch)
+                    *reinterpret_cast<uint4 *>(box[f] + 16 * (tid + 256 * i)) =
+                        in[i] ? make_uint4(inc4(pf[i].x), inc4(pf[i].y), inc4(pf[i].z), inc4(pf[i].w)) : make_uint4(0u, 0u, 0u, 0u);
+            for (int i = tid; i < 2 * bw + 16; i += 256) box[f][zpad + i] = 0;
         }
-#pragma unroll
-        for (int i = 0; i < BEV_BAND_PF; ++i)
-            if (tid + 256 * i < nch)
-                *reinterpret_cast<uint4 *>(box + 16 * (tid + 256 * i)) =
-                    in[i] ? make_uint4(inc4(pf[i].x), inc4(pf[i].y), inc4(pf[i].z), inc4(pf[i].w)) : make_uint4(0u, 0u, 0u, 0u);
-        for (int i = tid; i < 2 * bw + 16; i += 256) box[zpad + i] = 0;
         __syncthreads();
     }
-    // value of template pixel e: its 4 taps from the box (L) or, for an oversized band, from global
-    // memory. The two forms are separate loops (a compile-time choice): no branch between the taps,
-    // so each cell's 36 LDS byte reads are in flight together
+    // value of template pixel e in frame f: its 4 taps from the box (L: the offset the bandbox kernel
+    // stored in the entry) or, for an oversized band, from global memory. The two forms are separate
+    // loops (a compile-time choice): no branch between the taps, so a cell's LDS reads fly together
     const uint32_t inner = 0x739C0u;                  // bits of the 3x3 around p: rows 1..3, cols 1..3
     // the next cell's 3x3 table slots are in flight while this cell is evaluated (always issued, at a
     // clamped index, so the waits count only the current cell's loads)
@@ -548,11 +558,11 @@ __global__ void __launch_bounds__(256, 7) bev_band_kernel(const BevArgs a) {
     };
     auto cells_loop = [&](auto from_lds) {
         constexpr bool L = decltype(from_lds)::value;
-        auto value = [&](uint2 e) -> int {
+        auto value = [&](uint2 e, int f) -> int {
             if constexpr (!L) {
-                return tab_value(seg, a.in_cols, e);
+                return tab_value(seg[f], a.in_cols, e);
             } else {
-                const uint8_t *p = box + (e.y >> 15);                 // the tap's box offset (bandbox kernel)
+                const uint8_t *p = box[f] + (e.y >> 15);
                 const uint32_t l0 = p[0], l1 = p[1], l2 = p[bw], l3 = p[bw + 1];
                 const uint32_t ax = e.y & 31u, ay = (e.y >> 5) & 31u;
                 const uint32_t wx = 32u + ax * 65535u, wy = 32u + ay * 65535u;   // (32 - a) | a << 16
@@ -569,46 +579,65 @@ __global__ void __launch_bounds__(256, 7) bev_band_kernel(const BevArgs a) {
 #pragma unroll
             for (int q = 0; q < 5; ++q) s3[q] = s3n[q];
             load3(c + 256);
-            int t9[9];
+            uint32_t outm = 0;                        // window positions outside the template
 #pragma unroll
-            for (int i = 0; i < 9; ++i) t9[i] = value(slot_half(s3[i >> 1], i & 1));
-            int v = t9[0];
-            uint32_t m = 0;
+            for (int i = 0; i < 9; ++i) outm |= (uint32_t)((slot_half(s3[i >> 1], i & 1).y & TAB_OUT) != 0) << BEV_ORDER[i];
+            int v[FB];
+            uint32_t m[FB];
+            bool need = false;
 #pragma unroll
-            for (int i = 0; i < 9; ++i)
-                // outside the template: 1 (neutral for the erode: OpenCV's default erode border is +inf)
-                m |= (uint32_t)((slot_half(s3[i >> 1], i & 1).y & TAB_OUT) || occupied(a, t9[i])) << BEV_ORDER[i];
-            if (occupied(a, v) && (m & inner) != inner) {
+            for (int f = 0; f < FB; ++f) {
+                int t9[9];
+#pragma unroll
+                for (int i = 0; i < 9; ++i) t9[i] = value(slot_half(s3[i >> 1], i & 1), f);
+                v[f] = t9[0];
+                m[f] = outm;
+#pragma unroll
+                for (int i = 0; i < 9; ++i) m[f] |= (uint32_t)occupied(a, t9[i]) << BEV_ORDER[i];
+                need |= f < nf && occupied(a, v[f]) && (m[f] & inner) != inner;
+            }
+            if (need) {
                 // the ring completes the 5x5 window (opening at p = OR over q in N3(p) inside the template
-                // of AND over N3(q) of occupancy); if the 3x3 is all occupied, q = p already survives
-                int tx, ty;
-                cell_pixel(a, cx, cy, tx, ty);
+                // of AND over N3(q) of occupancy); if the 3x3 is all occupied, q = p already survives.
+                // Ring entry 9 shares the 3x3's last slot; the other 16 a slot (two entries) at a time:
+                // few cells need the ring, and holding all 8 slots would cost every cell's occupancy
                 {
-                    const uint2 e = slot_half(s3[4], 1);          // ring entry 9 shares the 3x3's last slot
-                    m |= (uint32_t)((e.y & TAB_OUT) || occupied(a, value(e))) << BEV_ORDER[9];
+                    const uint2 e = slot_half(s3[4], 1);
+#pragma unroll
+                    for (int f = 0; f < FB; ++f)
+                        m[f] |= (uint32_t)((e.y & TAB_OUT) || occupied(a, value(e, f))) << BEV_ORDER[9];
                 }
-                // the other 16 ring entries a slot (two entries) at a time: few cells need the ring,
-                // and holding all 8 slots would cost the occupancy every cell runs at
 #pragma unroll 1
                 for (int q = 5; q < BEV_SLOTS; ++q) {
                     const uint4 sq = tab[(long)q * cells];
                     const int i0 = 2 * q;
-                    m |= (uint32_t)((sq.y & TAB_OUT) || occupied(a, value(make_uint2(sq.x, sq.y)))) << BEV_ORDER_D[i0];
-                    m |= (uint32_t)((sq.w & TAB_OUT) || occupied(a, value(make_uint2(sq.z, sq.w)))) << BEV_ORDER_D[i0 + 1];
-                }
-                bool opened = false;
 #pragma unroll
-                for (int qy = -1; qy <= 1; ++qy)
-#pragma unroll
-                    for (int qx = -1; qx <= 1; ++qx) {
-                        const bool inside = (unsigned)(tx + qx) < (unsigned)a.occ_w_px && (unsigned)(ty + qy) < (unsigned)a.occ_h_px;
-                        const int sh = qy * 5 + qx;
-                        const uint32_t win = sh >= 0 ? inner << sh : inner >> -sh;
-                        opened |= inside && (m & win) == win;
+                    for (int f = 0; f < FB; ++f) {
+                        m[f] |= (uint32_t)((sq.y & TAB_OUT) || occupied(a, value(make_uint2(sq.x, sq.y), f))) << BEV_ORDER_D[i0];
+                        m[f] |= (uint32_t)((sq.w & TAB_OUT) || occupied(a, value(make_uint2(sq.z, sq.w), f))) << BEV_ORDER_D[i0 + 1];
                     }
-                if (!opened) v = 2;                  // isolated occupied pixel -> free (bev.py:204-205)
+                }
+                int tx, ty;
+                cell_pixel(a, cx, cy, tx, ty);
+#pragma unroll
+                for (int f = 0; f < FB; ++f) {
+                    if (!(occupied(a, v[f]) && (m[f] & inner) != inner)) continue;
+                    bool opened = false;
+#pragma unroll
+                    for (int qy = -1; qy <= 1; ++qy)
+#pragma unroll
+                        for (int qx = -1; qx <= 1; ++qx) {
+                            const bool inside = (unsigned)(tx + qx) < (unsigned)a.occ_w_px && (unsigned)(ty + qy) < (unsigned)a.occ_h_px;
+                            const int sh = qy * 5 + qx;
+                            const uint32_t win = sh >= 0 ? inner << sh : inner >> -sh;
+                            opened |= inside && (m[f] & win) == win;
+                        }
+                    if (!opened) v[f] = 2;           // isolated occupied pixel -> free (bev.py:204-205)
+                }
             }
-            bev_emit(a, b, rem, cx, cy, cells, v);
+#pragma unroll
+            for (int f = 0; f < FB; ++f)
+                if (f < nf) bev_emit(a, b0 + f, rem, cx, cy, cells, v[f]);
         }
     };
     if (lds) cells_loop(std::true_type());
@@ -718,8 +747,12 @@ hipError_t launch_bev(const BevArgs &a, hipStream_t s) {
     const char *be = std::getenv("BUGSEG_BEV_BAND");
     const bool banded = (!be || std::atoi(be) != 0) && !fe && FG == 0 && a.in_cols % 16 == 0;
     if (banded) {
-        const long grid = 8L * ((bev_bands(a.occ_h) + 7) / 8) * a.B;
-        hipLaunchKernelGGL(bev_band_kernel, dim3((unsigned)grid), dim3(256), 0, s, a);
+        // frames per workgroup (BUGSEG_BEV_FB = 1 or 2; read per call)
+        const char *fbe = std::getenv("BUGSEG_BEV_FB");
+        const int FB = fbe && std::atoi(fbe) == 1 ? 1 : 2;
+        const long grid = 8L * ((bev_bands(a.occ_h) + 7) / 8) * ((a.B + FB - 1) / FB);
+        if (FB == 1) hipLaunchKernelGGL(bev_band_kernel<1>, dim3((unsigned)grid), dim3(256), 0, s, a);
+        else hipLaunchKernelGGL(bev_band_kernel<2>, dim3((unsigned)grid), dim3(256), 0, s, a);
     } else if (F != 0 && a.in_cols % 16 == 0 && FG > 0) {
         const long nblk = (long)((a.occ_w + BEV_CB - 1) / BEV_CB) * ((a.occ_h + BEV_CB - 1) / BEV_CB);
         const long grid = nblk * ((a.B + FG - 1) / FG);

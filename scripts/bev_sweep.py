@@ -24,7 +24,11 @@ seg = torch.empty((B, H, W), dtype=torch.uint8, device="cuda")
 model.ctx.forward_bgr(frames, B, H, W, N.OUT_CLASS3_U8, seg)
 print("class histogram", torch.bincount(seg.flatten().long(), minlength=3).tolist())
 ref = None
-for f, fg in [(None, None), ("1", None), ("2", None), ("1", "4"), (None, None), ("1", None)]:
+for f, fg in [(None, None), ("FB1", None), ("1", None), ("2", None), ("1", "4"), (None, None), ("FB1", None), ("1", None)]:
+    os.environ.pop("BUGSEG_BEV_FB", None)
+    if f == "FB1":
+        os.environ["BUGSEG_BEV_FB"] = "1"
+        f = None
     if f is None:
         os.environ.pop("BUGSEG_BEV_F", None)      # the default: the band-staged kernel
     else:
@@ -47,6 +51,6 @@ for f, fg in [(None, None), ("1", None), ("2", None), ("1", "4"), (None, None), 
             if ref is None:
                 ref = g.clone()
             same = bool(torch.equal(ref, g))
-        print(f"F={f} FG={fg} laserscan={ls}: {ev[0].elapsed_time(ev[1]) / reps * 1000:8.1f} us per {B} frames"
+        print(f"F={f} FG={fg} FB={os.environ.get('BUGSEG_BEV_FB', 'default')} laserscan={ls}: {ev[0].elapsed_time(ev[1]) / reps * 1000:8.1f} us per {B} frames"
               + ("" if ls else f"  same grids: {same}"), flush=True)
 bev.laserscan_like_occupancy_grid = False
