@@ -222,7 +222,7 @@ __global__ void __launch_bounds__((BShape<C, V>::NW * 64), (sizeof(T) == 2 ? BSh
 #endif
     constexpr bool GLDS = BNECK_GLDS;                 // weights staged by global_load_lds (see the staging)
 #ifndef BNECK_KEEP_ASYM
-#define BNECK_KEEP_ASYM 0
+#define BNECK_KEEP_ASYM 1   // round 3: with the split 5x1 pass (no spills); round 2 measured the unsplit form 26.3 -> 26.7 us
 #endif
 #ifndef BNECK_KEEP_C64
 #define BNECK_KEEP_C64 0    // C = 64: measured 41.0 vs 38.0 us per launch with the residual kept (wave 0 takes a third load round trip for its second border fragment; batching it spills)
@@ -778,12 +778,20 @@ __global__ void __launch_bounds__((BShape<C, V>::NW * 64), (sizeof(T) == 2 ? BSh
             STAMP(4);
             to_tf(acc, cs2);
         } else {
-            {   // 5x1 over rows (taps dy = -2..2), output width TW+4 (the 1x5's halo)
-                f32x4 acc[NF2A][NR1];
+            // 5x1 over rows (taps dy = -2..2), output width TW+4 (the 1x5's halo). With the residual
+            // kept in registers (KEEP) the pass runs in two fragment halves: the first half's t1a is
+            // rounded and held packed (what the LDS store would write) while the second half
+            // accumulates, so the live accumulators halve — the whole pass at once spilled
+#ifndef BNECK_ASYM_SPLIT
+#define BNECK_ASYM_SPLIT 1
+#endif
+            constexpr bool SPLIT = BNECK_ASYM_SPLIT && KEEP && sizeof(T) == 2 && NF2A >= 2;
+            constexpr int HS = SPLIT ? (NF2A + 1) / 2 : NF2A;   // fragments per pass
+            auto pass5 = [&](int j0, f32x4 (&acc)[HS][NR1]) {
 #pragma unroll
-                for (int j = 0; j < NF2A; ++j)
+                for (int jj = 0; jj < HS; ++jj)
 #pragma unroll
-                    for (int r = 0; r < NR1; ++r) acc[j][r] = bias4(cb2 + r * 16 + kq * 4);
+                    for (int r = 0; r < NR1; ++r) acc[jj][r] = bias4(cb2 + r * 16 + kq * 4);
 #pragma unroll BNECK_ASYM_UNROLL
                 for (int s = 0; s < KS2; ++s) {
                     const int g = s * 4 + kq;
@@ -792,36 +800,66 @@ __global__ void __launch_bounds__((BShape<C, V>::NW * 64), (sizeof(T) == 2 ? BSh
 #pragma unroll
                     for (int r = 0; r < NR1; ++r) ld8(wf[r], w2 + (r * 16 + col) * K2S + s * 32 + kq * 8);
 #pragma unroll
-                    for (int j = 0; j < NF2A; ++j) {
-                        const int f = wave + NW * j;
-                        if (f >= NFA) continue;
+                    for (int jj = 0; jj < HS; ++jj) {
+                        const int j = j0 + jj, f = wave + NW * j;
+                        if (j >= NF2A || f >= NFA) continue;
                         int p = f * 16 + col;
                         if constexpr (NPA % 16 != 0) p = p < NPA ? p : 0;
                         const int oy = p / TWA, ox = p - oy * TWA;
                         Raw xf;
                         ld8(xf, g < G2 ? ts + ((oy + tap) * HWW + ox) * PSTR + coff : zpad);
 #pragma unroll
-                        for (int r = 0; r < NR1; ++r) mma(acc[j][r], wf[r], xf);
+                        for (int r = 0; r < NR1; ++r) mma(acc[jj][r], wf[r], xf);
                     }
                 }
-                __syncthreads();
+            };
+            // t1a of fragment j, row block r: act2, zero outside the image columns (the 1x5 zero-pads
+            // t1a); `where` = its LDS position, or -1 where the fragment / channel does not exist
+            auto t1a_at = [&](int j, int r, const f32x4 &acc, int &where) -> float4 {
+                const int f = wave + NW * j, p = f * 16 + col, ch = r * 16 + kq * 4;
+                where = (j < NF2A && f < NFA && p < NPA && ch < IS) ? p * PSTR + ch : -1;
+                const int ox = p - (p / TWA) * TWA;
+                const bool inside = (unsigned)(ox0 - 2 + ox) < (unsigned)a.W;
+                float4 v = act(f4(acc), cs2 + ch);
+                return inside ? v : make_float4(0.f, 0.f, 0.f, 0.f);
+            };
+            if constexpr (SPLIT) {
+                f32x4 acc[HS][NR1];
+                pass5(0, acc);
+                u32x2_t held[HS][NR1];
+                int hw[HS][NR1];
 #pragma unroll
-                for (int j = 0; j < NF2A; ++j) {
-                    const int f = wave + NW * j;
-                    if (f >= NFA) continue;
-                    const int p = f * 16 + col;
-                    if (p >= NPA) continue;
-                    const int ox = p - (p / TWA) * TWA;
-                    const bool inside = (unsigned)(ox0 - 2 + ox) < (unsigned)a.W;   // the 1x5 zero-pads t1a
+                for (int jj = 0; jj < HS; ++jj)
+#pragma unroll
+                    for (int r = 0; r < NR1; ++r) held[jj][r] = pack4<T>(t1a_at(jj, r, acc[jj][r], hw[jj][r]));
+                pass5(HS, acc);
+                __syncthreads();                          // every wave is done reading t0
+#pragma unroll
+                for (int jj = 0; jj < HS; ++jj)
+#pragma unroll
+                    for (int r = 0; r < NR1; ++r)
+                        if (hw[jj][r] >= 0) *reinterpret_cast<u32x2_t *>(ts + hw[jj][r]) = held[jj][r];
+#pragma unroll
+                for (int jj = 0; jj < HS; ++jj)
 #pragma unroll
                     for (int r = 0; r < NR1; ++r) {
-                        const int ch = r * 16 + kq * 4;
-                        if (ch >= IS) continue;
-                        float4 v = act(f4(acc[j][r]), cs2 + ch);
-                        if (!inside) v = make_float4(0.f, 0.f, 0.f, 0.f);
-                        st4(ts + p * PSTR + ch, v);
+                        int w;
+                        const float4 v = t1a_at(HS + jj, r, acc[jj][r], w);
+                        if (w >= 0) st4(ts + w, v);
                     }
-                }
+                __syncthreads();
+            } else {
+                f32x4 acc[HS][NR1];
+                pass5(0, acc);
+                __syncthreads();
+#pragma unroll
+                for (int j = 0; j < NF2A; ++j)
+#pragma unroll
+                    for (int r = 0; r < NR1; ++r) {
+                        int w;
+                        const float4 v = t1a_at(j, r, acc[j][r], w);
+                        if (w >= 0) st4(ts + w, v);
+                    }
                 __syncthreads();
             }
             {   // 1x5 over columns (taps dx = -2..2)
