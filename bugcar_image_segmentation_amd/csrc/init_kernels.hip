@@ -22,6 +22,8 @@
 // The generic implicit-GEMM path this replaces was VALU-bound (per-lane 3-byte gathers, integer
 // divisions, a 16-lane pool loop the whole wave executed). Both input forms go through the same
 // arithmetic, so forward_bgr == preprocess + forward bit for bit.
+#include <type_traits>
+
 #include "bugseg_internal.h"
 // output stores: sc1 write-through (OUT_AUX_SEL, as bneck_kernels.hip): measured 44.9-46.9 -> 43.7-44.2
 // us, the 2-stream bench unchanged
@@ -84,14 +86,19 @@ __global__ void __launch_bounds__(256) init_kernel(const ConvArgs a) {
 
     const int tiles_x = (a.Wg + IT_W - 1) / IT_W, tiles_y = (a.Hg + IT_H - 1) / IT_H;
     const int per = tiles_x * tiles_y, ntiles = a.B * per;
+    // LDS slot of this thread's patch column: threads past the patch width write the row pad element
+    // (never read), so the stores need no branch
+    const int dslot = qok ? dpatch : IP_RS - 1;
     // XCD-aware tile walk (see conv_kernels.hip)
     const int G = gridDim.x, grp = blockIdx.x & 7, slot = blockIdx.x >> 3, nslots = G >> 3;
     const int CH = (ntiles + 7) >> 3;
     for (int it = slot; it < CH; it += nslots) {
         const int tile = grp * CH + it;
         if (tile >= ntiles) break;
-        const int n = tile / per, tr = tile - n * per;
-        const int ty0 = (tr / tiles_x) * IT_H, tx0 = (tr % tiles_x) * IT_W;
+        // tile -> (frame, tile row, tile column): magic-number divisions (launch_init), no scalar loops
+        const int n = (int)fdiv((uint32_t)tile, a.mHWg, a.sHWg), tr = tile - n * per;
+        const int tyi = (int)fdiv((uint32_t)tr, a.mWg, a.sWg);
+        const int ty0 = tyi * IT_H, tx0 = (tr - tyi * tiles_x) * IT_W;
         const int iy0 = 2 * ty0 - 1, ix0 = 2 * tx0 - 1;
         // ---- patch: all 17 loads issued before any is consumed
         // (the whole offset goes in voffset: the descriptor's range check does not cover soffset)
@@ -99,21 +106,24 @@ __global__ void __launch_bounds__(256) init_kernel(const ConvArgs a) {
         const bool colok = qok && (unsigned)ix < (unsigned)a.Win;
         constexpr uint32_t PB = BGR ? 3u : 8u * (uint32_t)sizeof(T);       // bytes per input pixel (CinS = 8)
         const uint32_t qoff = BGR ? (uint32_t)q : (uint32_t)(px * PB + cb * sizeof(T));
-        const uint32_t rowpix = (uint32_t)((n * a.Hin + iy0) * a.Win + ix0);   // wraps for iy0 = -1: row unused
+        // one vector base per tile plus a scalar row step, no per-row masking: a row or column outside the
+        // frame reads a harmless byte (another row of the batch, or nothing: a negative offset wraps past
+        // the buffer's range and reads 0) and is zeroed when stored below
+        const uint32_t base = (uint32_t)((n * a.Hin + iy0) * a.Win + ix0) * PB + qoff, rowB = (uint32_t)a.Win * PB;
         uint32_t raw[IP_H];
 #pragma unroll
         for (int r = 0; r < IP_H; ++r) {
-            const bool ok = colok && (unsigned)(iy0 + r) < (unsigned)a.Hin;
-            const uint32_t off = ok ? (rowpix + (uint32_t)(r * a.Win)) * PB + qoff : OOB;
-            if constexpr (BGR) raw[r] = __builtin_amdgcn_raw_buffer_load_b8(rin, (int)off, 0, 0);
-            else if constexpr (sizeof(T) == 2) raw[r] = __builtin_amdgcn_raw_buffer_load_b16(rin, (int)off, 0, 0);
-            else raw[r] = __builtin_amdgcn_raw_buffer_load_b32(rin, (int)off, 0, 0);
+            const int off = (int)(base + (uint32_t)r * rowB);
+            if constexpr (BGR) raw[r] = __builtin_amdgcn_raw_buffer_load_b8(rin, off, 0, 0);
+            else if constexpr (sizeof(T) == 2) raw[r] = __builtin_amdgcn_raw_buffer_load_b16(rin, off, 0, 0);
+            else raw[r] = __builtin_amdgcn_raw_buffer_load_b32(rin, off, 0, 0);
         }
         __syncthreads();   // lut staged / previous tile done with the patch
-        if (qok) {
+        // rows outside the frame exist only in the first and last tile rows: a uniform fast path
+        auto store_rows = [&](auto full_rows) {
 #pragma unroll
             for (int r = 0; r < IP_H; ++r) {
-                const bool ok = colok && (unsigned)(iy0 + r) < (unsigned)a.Hin;
+                const bool ok = colok && (decltype(full_rows)::value || (unsigned)(iy0 + r) < (unsigned)a.Hin);
                 T v;
                 if constexpr (BGR) {
                     // f16: through f32, as the separate preprocess stores the engine input (prep_kernels.hip)
@@ -122,9 +132,11 @@ __global__ void __launch_bounds__(256) init_kernel(const ConvArgs a) {
                 }
                 else if constexpr (sizeof(T) == 2) v = __builtin_bit_cast(T, (unsigned short)raw[r]);
                 else v = __builtin_bit_cast(T, raw[r]);
-                patch[r * IP_RS + dpatch] = ok ? v : (T)0.f;
+                patch[r * IP_RS + dslot] = ok ? v : (T)0.f;
             }
-        }
+        };
+        if (iy0 >= 0 && iy0 + IP_H <= a.Hin) store_rows(std::true_type());
+        else store_rows(std::false_type());
         __syncthreads();
 
         // ---- pool maxima: lane (col, kq) -> pixel col of fragment f = kq (row 2*wave + (f>>1))
@@ -203,7 +215,13 @@ int init_tiles(const ConvArgs &a) {
     return a.B * ((a.Hg + IT_H - 1) / IT_H) * ((a.Wg + IT_W - 1) / IT_W);
 }
 
-hipError_t launch_init(int prec, bool bgr, const ConvArgs &a, hipStream_t s) {
+hipError_t launch_init(int prec, bool bgr, const ConvArgs &args, hipStream_t s) {
+    // the kernel's tile divisions: (mHWg, sHWg) by the tiles per frame, (mWg, sWg) by the tiles per row
+    // (the initial block's launch uses neither field otherwise)
+    ConvArgs a = args;
+    const int tiles_x = (a.Wg + IT_W - 1) / IT_W, tiles_y = (a.Hg + IT_H - 1) / IT_H;
+    fastdiv((uint32_t)(tiles_x * tiles_y), a.mHWg, a.sHWg);
+    fastdiv((uint32_t)tiles_x, a.mWg, a.sWg);
     int g = init_tiles(a);
     g = g < 2048 ? g : 2048;
     g = (g + 7) & ~7;

@@ -3,7 +3,7 @@ set -o pipefail
 cd "$GRAFT_REPO_ROOT" || exit 1
 mkdir -p gpurun_out
 export TMPDIR=/tmp
-timeout -k 10 400 python -u -m pytest tests/test_gpu_parity.py tests/test_gpu_capture_dist.py -k "bev or laserscan or pipeline or capture or fused or multi_tile" -m gpu -x -q --timeout 240 --timeout-method thread > gpurun_out/r3_f_tests.log 2>&1 || { echo "tests failed"; tail -40 gpurun_out/r3_f_tests.log; exit 1; }
+timeout -k 10 400 python -u -m pytest tests/test_gpu_parity.py tests/test_gpu_capture_dist.py -k "bev or laserscan or pipeline or capture or fused or multi_tile or forward_bgr or fp32 or fp16 or bf16 or config1" -m gpu -x -q --timeout 240 --timeout-method thread > gpurun_out/r3_f_tests.log 2>&1 || { echo "tests failed"; tail -40 gpurun_out/r3_f_tests.log; exit 1; }
 tail -2 gpurun_out/r3_f_tests.log
 timeout -k 10 120 python scripts/bev_sweep.py 20 > gpurun_out/bev_sweep.txt 2>&1; cat gpurun_out/bev_sweep.txt
 bash scripts/gpu_ab.sh ak0 ak1s0 ak1s1 || exit 1
