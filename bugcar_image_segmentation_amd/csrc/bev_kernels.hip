@@ -749,7 +749,8 @@ hipError_t launch_bev(const BevArgs &a, hipStream_t s) {
     if (banded) {
         // frames per workgroup (BUGSEG_BEV_FB = 1 or 2; read per call)
         const char *fbe = std::getenv("BUGSEG_BEV_FB");
-        const int FB = fbe && std::atoi(fbe) == 1 ? 1 : 2;
+        // (measured at 32 frames of 480x640: FB = 1 38.7-40.1 us, FB = 2 44.6-48.5 us)
+        const int FB = fbe && std::atoi(fbe) == 2 ? 2 : 1;
         const long grid = 8L * ((bev_bands(a.occ_h) + 7) / 8) * ((a.B + FB - 1) / FB);
         if (FB == 1) hipLaunchKernelGGL(bev_band_kernel<1>, dim3((unsigned)grid), dim3(256), 0, s, a);
         else hipLaunchKernelGGL(bev_band_kernel<2>, dim3((unsigned)grid), dim3(256), 0, s, a);

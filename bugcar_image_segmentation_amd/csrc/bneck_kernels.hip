@@ -222,7 +222,10 @@ __global__ void __launch_bounds__((BShape<C, V>::NW * 64), (sizeof(T) == 2 ? BSh
 #endif
     constexpr bool GLDS = BNECK_GLDS;                 // weights staged by global_load_lds (see the staging)
 #ifndef BNECK_KEEP_ASYM
-#define BNECK_KEEP_ASYM 1   // round 3: with the split 5x1 pass (no spills); round 2 measured the unsplit form 26.3 -> 26.7 us
+// the asymmetric form keeps the re-read: kept, its PMC read falls 65.4 -> 45.7 MB per launch (39.3
+// compulsory) but it spills (writes 39.3 -> 44.2 MB) and runs 26.2 -> 27.2 us (round 3 A/B; round 2:
+// 26.3 -> 26.7); with the 5x1 pass split into fragment halves (BNECK_ASYM_SPLIT) 28.2 us
+#define BNECK_KEEP_ASYM 0
 #endif
 #ifndef BNECK_KEEP_C64
 #define BNECK_KEEP_C64 0    // C = 64: measured 41.0 vs 38.0 us per launch with the residual kept (wave 0 takes a third load round trip for its second border fragment; batching it spills)
@@ -783,7 +786,7 @@ __global__ void __launch_bounds__((BShape<C, V>::NW * 64), (sizeof(T) == 2 ? BSh
             // rounded and held packed (what the LDS store would write) while the second half
             // accumulates, so the live accumulators halve — the whole pass at once spilled
 #ifndef BNECK_ASYM_SPLIT
-#define BNECK_ASYM_SPLIT 1
+#define BNECK_ASYM_SPLIT 0
 #endif
             constexpr bool SPLIT = BNECK_ASYM_SPLIT && KEEP && sizeof(T) == 2 && NF2A >= 2;
             constexpr int HS = SPLIT ? (NF2A + 1) / 2 : NF2A;   // fragments per pass

@@ -24,10 +24,10 @@ seg = torch.empty((B, H, W), dtype=torch.uint8, device="cuda")
 model.ctx.forward_bgr(frames, B, H, W, N.OUT_CLASS3_U8, seg)
 print("class histogram", torch.bincount(seg.flatten().long(), minlength=3).tolist())
 ref = None
-for f, fg in [(None, None), ("FB1", None), ("1", None), ("2", None), ("1", "4"), (None, None), ("FB1", None), ("1", None)]:
+for f, fg in [(None, None), ("FB2", None), ("1", None), ("2", None), ("1", "4"), (None, None), ("FB2", None), ("1", None)]:
     os.environ.pop("BUGSEG_BEV_FB", None)
-    if f == "FB1":
-        os.environ["BUGSEG_BEV_FB"] = "1"
+    if f == "FB2":
+        os.environ["BUGSEG_BEV_FB"] = "2"
         f = None
     if f is None:
         os.environ.pop("BUGSEG_BEV_F", None)      # the default: the band-staged kernel

@@ -180,7 +180,7 @@ def _bev_case(rows, cols, ww, wh, seed):
     return bev
 
 
-@pytest.mark.parametrize("form", [None, "FB1", "G", "FG4", "F2"])
+@pytest.mark.parametrize("form", [None, "FB2", "G", "FG4", "F2"])
 @pytest.mark.parametrize("rows,cols,ww,wh,grid,seed", [
     (480, 640, 1000, 1000, (10.0, 10.0, 0.05), 0),
     (120, 160, 300, 260, (3.0, 2.0, 0.05), 1),
@@ -194,8 +194,8 @@ def test_bev_occgrid_bit_exact(gpu, rows, cols, ww, wh, grid, seed, form, monkey
     bev.py:177) included."""
     if form == "G":
         monkeypatch.setenv("BUGSEG_BEV_BAND", "0")
-    elif form == "FB1":
-        monkeypatch.setenv("BUGSEG_BEV_FB", "1")
+    elif form == "FB2":
+        monkeypatch.setenv("BUGSEG_BEV_FB", "2")
     elif form == "FG4":
         monkeypatch.setenv("BUGSEG_BEV_FG", "4")
     elif form == "F2":
