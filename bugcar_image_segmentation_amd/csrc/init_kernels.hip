@@ -82,6 +82,7 @@ __global__ void __launch_bounds__(256) init_kernel(const ConvArgs a) {
     const int q = tid, px = q / 3, cb = q - px * 3;
     const bool qok = q < IP_W * 3;
     const int dpatch = BGR ? px * 3 + (2 - cb) : q;        // BGR byte cb is RGB channel 2 - cb (models.py:87)
+    const int lbase = (2 - cb) * 256;
 
     const int tiles_x = (a.Wg + IT_W - 1) / IT_W, tiles_y = (a.Hg + IT_H - 1) / IT_H;
     const int per = tiles_x * tiles_y, ntiles = a.B * per;
@@ -99,79 +100,43 @@ __global__ void __launch_bounds__(256) init_kernel(const ConvArgs a) {
         const int tyi = (int)fdiv((uint32_t)tr, a.mWg, a.sWg);
         const int ty0 = tyi * IT_H, tx0 = (tr - tyi * tiles_x) * IT_W;
         const int iy0 = 2 * ty0 - 1, ix0 = 2 * tx0 - 1;
-        if constexpr (BGR) {
-            // ---- patch from raw BGR bytes: thread t < 17 x 14 loads ONE 16-B chunk, chunk c of patch row
-            // r = t / 14 (a row's 195 bytes start at any byte: 14 aligned chunks cover them), and scatters
-            // its bytes normalised into LDS. The texture path handles 17 x 14 wide loads per tile instead of
-            // 17 x 195 byte loads (these kernels are address-processing bound: TA busy ~50% of the launch).
-            // Bytes outside the patch, the frame rows or the frame columns are zeroed / dropped at the store;
-            // a negative offset (the frame's first row above the image) wraps past the range and reads 0.
-            constexpr int CPRW = 14;
-            const int r = tid / CPRW, c = tid - r * CPRW;
-            const bool act = r < IP_H;
-            const int rr = act ? r : 0;
-            const int start = ((n * a.Hin + iy0 + rr) * a.Win + ix0) * 3;   // patch row's first byte (may be < 0)
-            const int mis = start & 15, al = start - mis;
-            uint4 ch16 = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(rin, al + 16 * c, 0, 0));
-            if ((uint32_t)(al + 16 * c) < in_bytes && (uint32_t)(al + 16 * c) + 16u > in_bytes) {
-                // the chunk holding the batch's last bytes runs past the buffer (frames whose byte count is
-                // not a multiple of 16): byte by byte, so the range check drops only what lies beyond
-                uint32_t w[4] = {0u, 0u, 0u, 0u};
-                for (int i = 0; i < 16; ++i)
-                    w[i >> 2] |= (uint32_t)__builtin_amdgcn_raw_buffer_load_b8(rin, al + 16 * c + i, 0, 0) << (8 * (i & 3));
-                ch16 = make_uint4(w[0], w[1], w[2], w[3]);
-            }
-            const bool rowok = act && (unsigned)(iy0 + rr) < (unsigned)a.Hin;
-            __syncthreads();   // lut staged / previous tile done with the patch
-            const uint32_t w4[4] = {ch16.x, ch16.y, ch16.z, ch16.w};
-#pragma unroll
-            for (int i = 0; i < 16; ++i) {
-                const int k = 16 * c + i - mis;                 // byte of the patch row, valid 0..194
-                const int kk = k < 0 ? 0 : k;
-                const int pxk = (kk * 171) >> 9, cbk = kk - 3 * pxk;   // k / 3 exact for k < 256
-                const bool ok = rowok && k >= 0 && k < IP_W * 3 && (unsigned)(ix0 + pxk) < (unsigned)a.Win;
-                const uint32_t byte = (w4[i >> 2] >> (8 * (i & 3))) & 0xffu;
-                const float lv = lut[(2 - cbk) * 256 + (int)byte];   // BGR byte cb is RGB channel 2 - cb
-                T v;
-                // f16: through f32, as the separate preprocess stores the engine input (prep_kernels.hip)
-                if constexpr (__is_same(T, _Float16)) v = (T)(float)lv;
-                else v = (T)lv;
-                const bool in_patch = act && k >= 0 && k < IP_W * 3;
-                patch[in_patch ? rr * IP_RS + 3 * pxk + 2 - cbk : IP_RS - 1] = ok ? v : (T)0.f;
-            }
-        } else {
         // ---- patch: all 17 loads issued before any is consumed
         // (the whole offset goes in voffset: the descriptor's range check does not cover soffset)
         const int ix = ix0 + px;
         const bool colok = qok && (unsigned)ix < (unsigned)a.Win;
-        constexpr uint32_t PB = 8u * (uint32_t)sizeof(T);             // bytes per input pixel (CinS = 8)
-        const uint32_t qoff = (uint32_t)(px * PB + cb * sizeof(T));
+        constexpr uint32_t PB = BGR ? 3u : 8u * (uint32_t)sizeof(T);       // bytes per input pixel (CinS = 8)
+        const uint32_t qoff = BGR ? (uint32_t)q : (uint32_t)(px * PB + cb * sizeof(T));
         // one vector base per tile plus a scalar row step, no per-row masking: a row or column outside the
-        // frame reads a harmless element (another row of the batch, or nothing: a negative offset wraps past
+        // frame reads a harmless byte (another row of the batch, or nothing: a negative offset wraps past
         // the buffer's range and reads 0) and is zeroed when stored below
         const uint32_t base = (uint32_t)((n * a.Hin + iy0) * a.Win + ix0) * PB + qoff, rowB = (uint32_t)a.Win * PB;
         uint32_t raw[IP_H];
 #pragma unroll
         for (int r = 0; r < IP_H; ++r) {
             const int off = (int)(base + (uint32_t)r * rowB);
-            if constexpr (sizeof(T) == 2) raw[r] = __builtin_amdgcn_raw_buffer_load_b16(rin, off, 0, 0);
+            if constexpr (BGR) raw[r] = __builtin_amdgcn_raw_buffer_load_b8(rin, off, 0, 0);
+            else if constexpr (sizeof(T) == 2) raw[r] = __builtin_amdgcn_raw_buffer_load_b16(rin, off, 0, 0);
             else raw[r] = __builtin_amdgcn_raw_buffer_load_b32(rin, off, 0, 0);
         }
-        __syncthreads();   // previous tile done with the patch
+        __syncthreads();   // lut staged / previous tile done with the patch
         // rows outside the frame exist only in the first and last tile rows: a uniform fast path
         auto store_rows = [&](auto full_rows) {
 #pragma unroll
             for (int r = 0; r < IP_H; ++r) {
                 const bool ok = colok && (decltype(full_rows)::value || (unsigned)(iy0 + r) < (unsigned)a.Hin);
                 T v;
-                if constexpr (sizeof(T) == 2) v = __builtin_bit_cast(T, (unsigned short)raw[r]);
+                if constexpr (BGR) {
+                    // f16: through f32, as the separate preprocess stores the engine input (prep_kernels.hip)
+                    if constexpr (__is_same(T, _Float16)) v = (T)(float)lut[lbase + (int)(raw[r] & 0xff)];
+                    else v = (T)lut[lbase + (int)(raw[r] & 0xff)];
+                }
+                else if constexpr (sizeof(T) == 2) v = __builtin_bit_cast(T, (unsigned short)raw[r]);
                 else v = __builtin_bit_cast(T, raw[r]);
                 patch[r * IP_RS + dslot] = ok ? v : (T)0.f;
             }
         };
         if (iy0 >= 0 && iy0 + IP_H <= a.Hin) store_rows(std::true_type());
         else store_rows(std::false_type());
-        }
         __syncthreads();
 
         // ---- pool maxima: lane (col, kq) -> pixel col of fragment f = kq (row 2*wave + (f>>1))
