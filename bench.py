@@ -103,6 +103,8 @@ def parse():
     p.add_argument("--stream-priority", type=int, default=0, help="HIP priority of the side shards' streams")
     p.add_argument("--chain-forwards", type=int, default=0,
                    help="1: shard i's forward starts after shard i-1's (its BEV overlaps the next forward)")
+    p.add_argument("--shard-offset", type=int, default=0,
+                   help="k > 0: shard i+1 starts when shard i reaches its k-th launch (different layers side by side)")
     p.add_argument("--graph", type=int, default=0, help="1: replay the step as one captured HIP graph")
     p.add_argument("--cpu-baseline-seconds", type=float, default=12.0)
     p.add_argument("--no-cpu-baseline", action="store_true")
@@ -413,7 +415,8 @@ def main():
     bev = synthetic.synthetic_bev(H, W)
     grid = (synthetic.GRID_W_M, synthetic.GRID_H_M, synthetic.CELL_M)
     pipe = OccupancyPipeline(model, bev, *grid, model_hw=(H, W), streams=a.streams,
-                             stream_priority=a.stream_priority, chain_forwards=bool(a.chain_forwards))
+                             stream_priority=a.stream_priority, chain_forwards=bool(a.chain_forwards),
+                             shard_offset=a.shard_offset)
     frames = torch.from_numpy(synthetic.uniform_frames(B, H, W, seed=rank)).to(dev)
 
     run = lambda: pipe.run(frames)  # noqa: E731
@@ -507,7 +510,7 @@ def main():
                                    f"fused BEV warp/occgrid (1000x1000 BEV -> 200x200 cells)",
                        "global_batch": B * world, "per_gpu_batch": B, "height": H, "width": W,
                        "parallelism": f"frame-sharded dp{world}" + (" + RCCL all-gather of grids" if world > 1 else ""),
-                       "streams_per_gpu": a.streams, "hip_graph": bool(a.graph),
+                       "streams_per_gpu": a.streams, "hip_graph": bool(a.graph), "shard_offset": a.shard_offset,
                        **({"backend": "rccl" if a.backend == "nccl" else "gloo (functional run, not a timing)",
                            "gather_check": gather_check} if world > 1 else {})},
             "roofline": roof,

@@ -23,7 +23,7 @@ PRE_ENGINE, PRE_NCHW_F64, PRE_NCHW_F32, PRE_BGR_U8 = 0, 1, 2, 3
 
 EXPORTED = ("bugseg_version", "bugseg_create", "bugseg_destroy", "bugseg_load_weights", "bugseg_num_classes",
             "bugseg_input_bytes", "bugseg_preprocess", "bugseg_nchw_to_input", "bugseg_enet_forward",
-            "bugseg_enet_forward_bgr",
+            "bugseg_enet_forward_bgr", "bugseg_enet_forward_bgr_ops",
             "bugseg_bev_occgrid", "bugseg_bev_workspace_bytes", "bugseg_bev_occgrid_ws", "bugseg_plan_info", "bugseg_plan_op", "bugseg_plan_launch_op",
             "bugseg_last_error",
             "bugseg_dl_create", "bugseg_dl_destroy", "bugseg_dl_load_weights", "bugseg_dl_set_plan",
@@ -73,6 +73,7 @@ def load_library(path: Path | str | None = None) -> ctypes.CDLL:
             "bugseg_nchw_to_input": (i, [vp, vp, i, i, i, i, vp, vp]),
             "bugseg_enet_forward": (i, [vp, vp, i, i, i, i, vp, vp]),
             "bugseg_enet_forward_bgr": (i, [vp, vp, i, i, i, i, vp, vp]),
+            "bugseg_enet_forward_bgr_ops": (i, [vp, vp, i, i, i, i, vp, i, i, vp]),
             "bugseg_bev_occgrid": (i, [vp, vp, i, ctypes.POINTER(BevParams), vp, vp]),
             "bugseg_bev_workspace_bytes": (sz, [ctypes.POINTER(BevParams), i]),
             "bugseg_bev_occgrid_ws": (i, [vp, vp, i, ctypes.POINTER(BevParams), vp, vp, sz, vp]),
@@ -170,6 +171,11 @@ class Context:
     def forward_bgr(self, bgr, B, H, W, out_kind, out, stream=None):
         check(self.lib.bugseg_enet_forward_bgr(self.h, bgr.data_ptr(), B, H, W, out_kind, out.data_ptr(),
                                                stream_handle(stream)), self.h)
+
+    def forward_bgr_ops(self, bgr, B, H, W, out_kind, out, first_op, last_op, stream=None):
+        """Launches [first_op, last_op) of forward_bgr's plan only (last_op = -1: to the end)."""
+        check(self.lib.bugseg_enet_forward_bgr_ops(self.h, bgr.data_ptr(), B, H, W, out_kind, out.data_ptr(),
+                                                   first_op, last_op, stream_handle(stream)), self.h)
 
     def bev(self, seg, B, params: BevParams, out, stream=None):
         """bugseg_bev_occgrid_ws: the laserscan scratch comes from torch's caching allocator on the

@@ -1260,7 +1260,7 @@ int bugseg_nchw_to_input(bugseg_ctx *ctx, const void *x, int is_f64, int B, int 
 }
 
 static int enet_forward(bugseg_ctx *ctx, const void *in, bool bgr, int B, int H, int W, int out_kind, void *out,
-                        void *stream) {
+                        void *stream, int first_op = 0, int last_op = -1) {
     if (!ctx || !in || !out) return fail(ctx, BUGSEG_EINVAL, "NULL argument");
     if (!ctx->loaded) return fail(ctx, BUGSEG_ESTATE, "no weights loaded");
     if (out_kind < BUGSEG_OUT_LOGITS_F32 || out_kind > BUGSEG_OUT_BINARY_U8) return fail(ctx, BUGSEG_EINVAL, "bad out_kind");
@@ -1282,8 +1282,11 @@ static int enet_forward(bugseg_ctx *ctx, const void *in, bool bgr, int B, int H,
     case BUGSEG_OUT_CLASS3_U8: last.cls_out = (uint8_t *)out; last.lut = luts; break;
     case BUGSEG_OUT_BINARY_U8: last.cls_out = (uint8_t *)out; last.lut = luts + 16; break;
     }
-    for (size_t i = 0; i < pl.ops.size(); ++i) {
-        const Op &op = pl.ops[i];
+    const int nops = (int)pl.ops.size();
+    if (last_op < 0 || last_op > nops) last_op = nops;
+    if (first_op < 0 || first_op > last_op) return fail(ctx, BUGSEG_EINVAL, "bad op range");
+    for (int i = first_op; i < last_op; ++i) {
+        const Op &op = pl.ops[(size_t)i];
         hipError_t e = op.kind == 1 ? launch_bneck(ctx->prec, op.bn_c, op.bn_asym, op.bn_var, op.bn, (hipStream_t)stream, op.bn_cin)
                      : op.kind == 2 ? launch_up(ctx->prec, op.up_cin, op.up_it, op.up_cout, op.up, (hipStream_t)stream)
                                     : launch_conv(ctx->prec, op.nr, op.epi, op.a, (hipStream_t)stream);
@@ -1299,6 +1302,11 @@ int bugseg_enet_forward(bugseg_ctx *ctx, const void *in, int B, int H, int W, in
 int bugseg_enet_forward_bgr(bugseg_ctx *ctx, const uint8_t *bgr, int B, int H, int W, int out_kind, void *out,
                             void *stream) {
     return enet_forward(ctx, bgr, true, B, H, W, out_kind, out, stream);
+}
+
+int bugseg_enet_forward_bgr_ops(bugseg_ctx *ctx, const uint8_t *bgr, int B, int H, int W, int out_kind, void *out,
+                                int first_op, int last_op, void *stream) {
+    return enet_forward(ctx, bgr, true, B, H, W, out_kind, out, stream, first_op, last_op);
 }
 
 }  // extern "C"

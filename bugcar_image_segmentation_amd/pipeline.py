@@ -25,14 +25,17 @@ class OccupancyPipeline:
 
     def __init__(self, model: ENET, bev: bev_transform_tools, grid_w_m: float, grid_h_m: float, cell_m: float,
                  model_hw: tuple[int, int] | None = None, ros_layout: bool = False, streams: int = 1,
-                 binary: bool = False, stream_priority: int = 0, chain_forwards: bool = False):
+                 binary: bool = False, stream_priority: int = 0, chain_forwards: bool = False, shard_offset: int = 0):
         """binary=True is the predict_binary + create_occupancy_grid_binary pairing (models.py:70-82,
         bev.py:97-165): class maps through the binary LUT, the binary rasteriser; in the laserscan-like
         mode its output is the reference's pair, (2, B, ...) (bev.py:164). stream_priority is the HIP
         priority of the side shards' streams (shard 0 runs on the caller's stream; lower = higher).
         chain_forwards=True starts shard i's forward when shard i-1's forward has finished, so each
         shard's BEV rasteriser runs beside the next shard's forward (only the last one is exposed)
-        instead of all shards' forwards running together and their BEVs together at the end."""
+        instead of all shards' forwards running together and their BEVs together at the end.
+        shard_offset=k > 0 starts shard i+1 when shard i has reached its k-th launch (an
+        event between launches k-1 and k of its forward), so the shards run different layers side by
+        side instead of the same layer at the same time."""
         self.model = model
         self.binary = binary
         self.bev = bev
@@ -47,6 +50,7 @@ class OccupancyPipeline:
         self.streams = streams
         self.stream_priority = stream_priority
         self.chain_forwards = chain_forwards
+        self.shard_offset = int(shard_offset)
         self._ctxs = [model.ctx]
         self._streams = []
         self._x = None
@@ -101,8 +105,12 @@ class OccupancyPipeline:
             st = main if i == 0 else streams[i - 1]
             if i:
                 st.wait_event(ready)
+            split_done = self.chain_forwards or (self.shard_offset > 0 and i + 1 < self.streams)
             with torch.cuda.stream(st):
-                if self.chain_forwards:
+                if self.shard_offset > 0 and i + 1 < self.streams:
+                    self._run_forward(ctxs[i], frames[s:e], x[s:e], seg[s:e], st, split=self.shard_offset)
+                    ready = self._split_event
+                elif self.chain_forwards:
                     self._run_forward(ctxs[i], frames[s:e], x[s:e], seg[s:e], st)
                     ready = torch.cuda.Event()
                     ready.record(st)                  # the next shard's forward starts here
@@ -110,10 +118,10 @@ class OccupancyPipeline:
                     # the kernel writes a shard's pair as one contiguous (2, e - s, ...) block; the
                     # batch's pair (2, B, ...) holds it as two slabs, so stage it and copy
                     tmp = self._pair_buf(i, (2, e - s) + tuple(out.shape[2:]), out.device)
-                    self._run_shard(ctxs[i], frames[s:e], x[s:e], seg[s:e], tmp, p, st, forward=not self.chain_forwards)
+                    self._run_shard(ctxs[i], frames[s:e], x[s:e], seg[s:e], tmp, p, st, forward=not split_done)
                     out[:, s:e].copy_(tmp)
                 else:
-                    self._run_shard(ctxs[i], frames[s:e], x[s:e], seg[s:e], out[s:e], p, st, forward=not self.chain_forwards)
+                    self._run_shard(ctxs[i], frames[s:e], x[s:e], seg[s:e], out[s:e], p, st, forward=not split_done)
         for st in streams[: self.streams - 1]:
             main.wait_stream(st)
         return out
@@ -145,13 +153,21 @@ class OccupancyPipeline:
             res = self.run(frames_bgr, out)
         return graph.replay, res
 
-    def _run_forward(self, ctx, frames, x, seg, stream):
+    def _run_forward(self, ctx, frames, x, seg, stream, split=0):
         B, H0, W0 = frames.shape[:3]
         if (H0, W0) != (self.H, self.W):
             # resize only (models.py:87); colour swap + normalisation are fused into the initial block
             ctx.preprocess(frames, B, H0, W0, self.H, self.W, N.PRE_BGR_U8, x, stream)
             frames = x
-        ctx.forward_bgr(frames, B, self.H, self.W, N.OUT_BINARY_U8 if self.binary else N.OUT_CLASS3_U8, seg, stream)
+        kind = N.OUT_BINARY_U8 if self.binary else N.OUT_CLASS3_U8
+        if split <= 0:
+            ctx.forward_bgr(frames, B, self.H, self.W, kind, seg, stream)
+            return
+        # launches [0, split), an event (the next shard starts there), then the rest
+        ctx.forward_bgr_ops(frames, B, self.H, self.W, kind, seg, 0, split, stream)
+        self._split_event = torch.cuda.Event()
+        self._split_event.record(stream)
+        ctx.forward_bgr_ops(frames, B, self.H, self.W, kind, seg, split, -1, stream)
 
     def _run_shard(self, ctx, frames, x, seg, out, p, stream, forward=True):
         if forward:

@@ -143,6 +143,13 @@ int bugseg_enet_forward(bugseg_ctx *ctx, const void *in_dev, int B, int H, int W
 int bugseg_enet_forward_bgr(bugseg_ctx *ctx, const uint8_t *bgr_dev, int B, int H, int W, int out_kind,
                             void *out_dev, void *stream);
 
+/* bugseg_enet_forward_bgr enqueuing only launches [first_op, last_op) of the forward's plan
+ * (last_op = -1: to the end; bugseg_plan_info gives the count). Calling it for [0, k) and then for
+ * [k, -1) enqueues exactly the full forward; in between the caller may record an event, so another
+ * stream's work can start at a chosen point of this forward (pipeline.py: the shard offset). */
+int bugseg_enet_forward_bgr_ops(bugseg_ctx *ctx, const uint8_t *bgr_dev, int B, int H, int W, int out_kind,
+                                void *out_dev, int first_op, int last_op, void *stream);
+
 /* Fused BEV rasteriser over a batch of class maps: seg_dev (B, in_rows, in_cols) u8
  * -> out_dev (B, occ_h, occ_w) int8 (or the ROS layout, see ros_layout).
  * Replaces bev_transform_tools.create_occupancy_grid (bev.py:166-246) or, with variant = 1,

@@ -425,9 +425,10 @@ def test_multistream_pipeline_identical(bf16_model):
     bev = synthetic.synthetic_bev(H, W, 300, 300)
     one = OccupancyPipeline(bf16_model, bev, 3.0, 3.0, 0.05, model_hw=(H, W)).run(frames).clone()
     for s in (2, 3):
-        for chain in (False, True):       # chain: shard i's forward after shard i-1's (BEV beside it)
+        for chain, off in ((False, 0), (True, 0), (False, 7)):   # chain: shard i's forward after shard
+            # i-1's (BEV beside it); off: shard i+1 starts at shard i's 7th launch
             many = OccupancyPipeline(bf16_model, bev, 3.0, 3.0, 0.05, model_hw=(H, W), streams=s,
-                                     chain_forwards=chain)
+                                     chain_forwards=chain, shard_offset=off)
             for _ in range(2):
                 got = many.run(frames)
             torch.cuda.synchronize()
