@@ -13,7 +13,7 @@ from collections import defaultdict
 
 
 # tile shape of each fused-bottleneck variant (bneck_kernels.hip BShape)
-BNECK_SHAPES = {(128, 0): "16x16", (128, 1): "20x16", (128, 2): "4x80", (128, 3): "4x64", (64, 0): "16x16", (64, 1): "20x16",
+BNECK_SHAPES = {(128, 0): "16x16", (128, 1): "20x16", (128, 2): "4x80", (128, 3): "4x64", (128, 4): "8x16", (64, 0): "16x16", (64, 1): "20x16", (64, 2): "8x16",
                 (16, 0): "16x16"}
 
 
@@ -21,9 +21,13 @@ def short(name):
     m = re.search(r"bneck_kernelI(DF16b|DF16_|f)Li(\d+)ELb(\d)ELi(\d+)ELb\dELi([1-9]\d*)E", name)
     if m:   # the downsampling form (non-zero input-channel template argument)
         return f"down C{m.group(2)} {BNECK_SHAPES.get((int(m.group(2)), int(m.group(4))), '?')}"
+    # (the f32 kernels appear demangled: "void bugseg::bneck_kernel<float, 64, false, 2, false, 0>(...)")
+    m = re.search(r"bneck_kernel<(?:__bf16|_Float16|float), (\d+), (?:false|true), (\d+), (?:false|true), ([1-9]\d*)>", name)
+    if m:
+        return f"down C{m.group(1)} {BNECK_SHAPES.get((int(m.group(1)), int(m.group(2))), '?')}"
     m = re.search(r"bneck_kernelI(DF16b|DF16_|f)Li(\d+)ELb(\d)ELi(\d+)E", name)
     if not m:
-        m = re.search(r"bneck_kernel<(__bf16|_Float16|float), (\d+), (false|true), (\d+)>", name)
+        m = re.search(r"bneck_kernel<(__bf16|_Float16|float), (\d+), (false|true), (\d+)", name)
     if m:
         asym = m.group(3) in ("1", "true")
         return f"bneck C{m.group(2)}{' asym' if asym else ''} {BNECK_SHAPES.get((int(m.group(2)), int(m.group(4))), '?')}"
@@ -36,6 +40,9 @@ def short(name):
     m = re.search(r"up_kernelI(DF16b|DF16_|f)Li(\d+)ELi(\d+)ELi(\d+)E", name)
     if m:
         return f"up C{m.group(4)}"
+    m = re.search(r"up_kernel<(?:__bf16|_Float16|float), (\d+), (\d+), (\d+)>", name)
+    if m:
+        return f"up C{m.group(3)}"
     if "cls_kernel" in name:
         return "classes"
     if "init_kernel" in name:
