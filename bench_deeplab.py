@@ -70,11 +70,11 @@ def cpu_baseline(net, budget_s):
                       f"semantics), {el:.1f} s at {threads} threads, one frame per call"}
 
 
-def pmc_traffic(tag, batch):
+def pmc_traffic(tag, batch, backbone="mobilenet_v2"):
     """HBM bytes per launch of op tag `tag` from the committed PMC summary
     (profiles/dl_pmc_traffic.json, written by scripts/dl_pmc_summary.py from rocprofv3 FETCH_SIZE /
     WRITE_SIZE passes of this script at the same batch), or None."""
-    p = os.path.join(ROOT, "profiles", "dl_pmc_traffic.json")
+    p = os.path.join(ROOT, "profiles", "dl_pmc_traffic_xception.json" if backbone == "xception_65" else "dl_pmc_traffic.json")
     try:
         with open(p) as f:
             d = json.load(f)
@@ -145,14 +145,23 @@ def measure(dev, B, steps, warmup, precision, world=1, rank=0, backbone="mobilen
     return el, model, per, per_op, fwd_us
 
 
-def roofline(model, per, fwd_us, B, precision):
+def roofline(model, per, fwd_us, B, precision, backbone="mobilenet_v2"):
+    """Dominant op tag's roofline. MobileNetV2 is HBM-bound (its dominant tag moves ~1 B per 2 flops);
+    Xception-65's dominant tag is the pointwise 1x1 GEMMs (108 GFLOP per frame), priced against the
+    dense MFMA peak of the dtype."""
     info = model.plan_info
     tag, k = max(per.items(), key=lambda kv: kv[1]["us"])
     achieved = k["bytes"] / (k["us"] * 1e-6) / 1e9
     peak_tf = MFMA_PEAK_TFLOPS[precision]
+    tflops = k["flops"] / (k["us"] * 1e-6) / 1e12
+    mfma = backbone == "xception_65"
+    bound = ({"bound": "mfma", "achieved": round(tflops, 1), "peak": peak_tf, "unit": "TFLOP/s",
+              "frac": round(tflops / peak_tf, 4), "hbm_achieved_gbs": round(achieved, 1),
+              "hbm_frac": round(achieved / HBM_PEAK_GBS, 4)} if mfma else
+             {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+              "frac": round(achieved / HBM_PEAK_GBS, 4)})
     return {
-        "bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-        "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": pmc_traffic(tag, B),
+        **bound, "traffic": pmc_traffic(tag, B, backbone),
         "kernel": f"{tag}: dominant kernel tag ({k['launches']} launches, {k['us']:.0f} us of {fwd_us:.0f} us "
                   f"per forward); {k['bytes'] / k['launches'] / 1e6:.1f} MB per launch (input once + output "
                   f"once + residual + weights); {k['flops'] / (k['us'] * 1e-6) / 1e12:.1f} TFLOP/s "
@@ -178,7 +187,7 @@ def record(dev, B, steps, warmup, precision, cpu_seconds=0.0, backbone="mobilene
     res = {"value": round(B * steps / el, 2), "unit": "frames/s", "ms_per_step": round(el / steps * 1e3, 4),
            "steps": steps, "dtype": precision, "per_gpu_batch": B, "crop": model.net.crop,
            "workload": f"config4: {WORKLOAD[backbone]}, 513x513 u8 RGB -> SemanticPredictions int64",
-           "roofline": roofline(model, per, fwd_us, B, precision)}
+           "roofline": roofline(model, per, fwd_us, B, precision, backbone)}
     if cpu_seconds > 0:
         res["cpu_baseline"] = cpu_baseline(model.net, cpu_seconds)
     del model
@@ -212,7 +221,7 @@ def main():
                                    "pad/normalise + forward + bilinear resize + argmax int64",
                        "global_batch": B * world, "per_gpu_batch": B, "crop": C,
                        "parallelism": f"frame-sharded dp{world}"},
-            "roofline": roofline(model, per, fwd_us, B, a.precision),
+            "roofline": roofline(model, per, fwd_us, B, a.precision, a.backbone),
             "kernels": kernel_summary(per),
             "per_op": per_op,
         }

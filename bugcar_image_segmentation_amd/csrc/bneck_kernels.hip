@@ -233,6 +233,15 @@ __global__ void __launch_bounds__((BShape<C, V>::NW * 64), (sizeof(T) == 2 ? BSh
     constexpr bool KEEP = BNECK_KEEP && !DN && sizeof(T) == 2 && (!ASYM || BNECK_KEEP_ASYM) && (SWAP || !REG3) && (C != 64 || BNECK_KEEP_C64) &&
                           NF2 * KS1 * 4 <= (C == 128 ? 48 : 32);   // kept VGPRs within the occupancy budget
     static_assert(!KEEP || !REG3 || KS1 == RQ3, "kept x: one 16-B chunk per k-step and row pair");
+#ifndef BNECK_DKEEP
+#define BNECK_DKEEP 1
+#endif
+    // DKEEP (down forms, 2-byte storage): phase 1 walks the tile as KEEP does and the main-branch pool
+    // of each interior fragment stays in registers, already in the kept-x chunk layout (lane kq:
+    // channels 32 t + 8 kq .. + 7), as phase 3's residual — instead of a global scratch round trip
+    // (PMC: down C64 read + wrote 1.33x, down C128 1.36x their compulsory bytes with the scratch)
+    constexpr bool DKEEP = BNECK_DKEEP && DN && sizeof(T) == 2 && SWAP;
+    constexpr int NPK = DN ? (CI + 31) / 32 : 1;      // DKEEP: pooled 16-B chunks per lane and fragment
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
 
     STAMP_ENTRY(0);
@@ -376,18 +385,34 @@ __global__ void __launch_bounds__((BShape<C, V>::NW * 64), (sizeof(T) == 2 ? BSh
     // halo re-reads of neighbouring tiles hit the same L2
     const int G = gridDim.x, grp = blockIdx.x & 7, slot = blockIdx.x >> 3, nslots = G >> 3;
     const int CH = (a.ntiles + 7) >> 3;
-    for (int it = slot; it < CH; it += nslots) {
-        const int tile = grp * CH + it;
-        if (tile >= a.ntiles) break;
-        // tile -> frame n, phase (py, px), tile row / column of that phase's sub-image (scalar math)
+    // tile -> frame n and image pixel (oy0, ox0) of tile pixel (0, 0): phase (py, px), tile row /
+    // column of that phase's sub-image (scalar math). Tile pixel (i, j) is image (oy0 + dt i, ox0 +
+    // dt j), or (oy0 + dt j, ox0 + dt i) transposed
+    auto tile_geom = [&](int tile, int &n, int &oy0, int &ox0) {
         int t = tile;
         const int txi = t % a.tiles_x; t /= a.tiles_x;
         const int tyi = t % a.tiles_y; t /= a.tiles_y;
-        const int ph = t % a.phases, n = t / a.phases;
+        const int ph = t % a.phases;
+        n = t / a.phases;
         const int py = RD ? ph : ph / dt, px = RD ? 0 : ph - py * dt;   // RD: phases = row phases
-        // image pixel of tile pixel (0, 0); tile pixel (i, j) is image (oy0 + dt i, ox0 + dt j), or
-        // (oy0 + dt j, ox0 + dt i) transposed
-        const int oy0 = py + dt * tyi * (tr ? TW : TH), ox0 = RD ? 0 : px + dt * txi * (tr ? TH : TW);
+        oy0 = py + dt * tyi * (tr ? TW : TH);
+        ox0 = RD ? 0 : px + dt * txi * (tr ? TH : TW);
+    };
+    // PIPE (KEEP forms, a workgroup walking several tiles): as phase 3 retires fragment j's kept x
+    // (its residual), the same registers take the NEXT tile's fragment j, so the next tile's interior
+    // loads fly under this tile's expansion and stores instead of after them
+#ifndef BNECK_PIPE
+#define BNECK_PIPE 1
+#endif
+    constexpr bool PIPE = BNECK_PIPE && KEEP && REG3;
+    Raw kx[KEEP ? NF2 : 1][KS1];                      // KEEP: this wave's interior fragments of x
+    bool kok[KEEP ? NF2 : 1];
+    bool pf = false;                                  // kx / kok already hold this tile's interior (PIPE)
+    for (int it = slot; it < CH; it += nslots) {
+        const int tile = grp * CH + it;
+        if (tile >= a.ntiles) break;
+        int n, oy0, ox0;
+        tile_geom(tile, n, oy0, ox0);
         const int dtx = RD ? 1 : dt;                  // column step of the tile
         const uint32_t xn = (uint32_t)(n * a.H * a.W) * (uint32_t)(C * sizeof(T));   // frame byte offset
         const uint32_t xin_n = (uint32_t)(n * 4 * a.H * a.W) * (uint32_t)(CI * sizeof(T));   // down: input frame
@@ -425,7 +450,7 @@ __global__ void __launch_bounds__((BShape<C, V>::NW * 64), (sizeof(T) == 2 ? BSh
         // down: main-branch maxpool of output pixel (y, x) from the projection's B fragments (see the
         // kernel comment); the first maximum in window order wins (strict >, NaN / -inf never chosen:
         // as a key, larger value first, then lower window position; position 4 = no candidate -> 0)
-        auto pool_store = [&](const Raw (&xs)[KS1], bool interior, int y, int x) {
+        auto pool_store = [&](const Raw (&xs)[KS1], bool interior, int y, int x, uint4 (&pk)[NPK]) {
             if constexpr (DN) {
                 if (__ballot(interior) == 0) return;          // halo-only fragment (wave-uniform)
                 auto elems = [&](const Raw &r, float (&e)[8]) {
@@ -438,7 +463,7 @@ __global__ void __launch_bounds__((BShape<C, V>::NW * 64), (sizeof(T) == 2 ? BSh
                     }
                 };
                 const uint32_t pix = (uint32_t)((n * a.H + y) * a.W + x);
-                auto emit = [&](int cc, const float (&bv)[8], const int (&bp)[8], bool wr) {
+                auto emit = [&](int cc, const float (&bv)[8], const int (&bp)[8], bool wr, int kslot, bool kval) {
                     // 8 pooled channels (exact input values) + their window positions (4 = none -> 0)
                     uint32_t pw[8 * sizeof(T) / 4];
                     if constexpr (sizeof(T) == 2) {
@@ -456,10 +481,15 @@ __global__ void __launch_bounds__((BShape<C, V>::NW * 64), (sizeof(T) == 2 ? BSh
                         lo |= (uint32_t)(bp[i] & 3) << (8 * i);
                         hi |= (uint32_t)(bp[4 + i] & 3) << (8 * i);
                     }
-                    const uint32_t po = wr ? (pix * CI + cc * 8) * (uint32_t)sizeof(T) : OOB;
+                    if constexpr (DKEEP) {
+                        pk[kslot] = kval ? make_uint4(pw[0], pw[1], pw[2], pw[3]) : make_uint4(0u, 0u, 0u, 0u);
+                    } else {
+                        (void)kslot; (void)kval;
+                        const uint32_t po = wr ? (pix * CI + cc * 8) * (uint32_t)sizeof(T) : OOB;
 #pragma unroll
-                    for (int i = 0; i < (int)(8 * sizeof(T) / 16); ++i)
-                        bst16(rpb, po == OOB ? OOB : po + 16 * i, make_uint4(pw[4 * i], pw[4 * i + 1], pw[4 * i + 2], pw[4 * i + 3]));
+                        for (int i = 0; i < (int)(8 * sizeof(T) / 16); ++i)
+                            bst16(rpb, po == OOB ? OOB : po + 16 * i, make_uint4(pw[4 * i], pw[4 * i + 1], pw[4 * i + 2], pw[4 * i + 3]));
+                    }
                     __builtin_amdgcn_raw_buffer_store_b64((u32x2_t){lo, hi}, rib, wr ? (int)(pix * a.idxCS + cc * 8) : (int)OOB, 0, 0);
                 };
                 // in window order: strict > from -inf (NaN and -inf never taken), position 4 = none
@@ -482,7 +512,7 @@ __global__ void __launch_bounds__((BShape<C, V>::NW * 64), (sizeof(T) == 2 ? BSh
 #pragma unroll
                             for (int i = 0; i < 8; ++i) seq(bv[i], bp[i], e[i], tap);
                         }
-                        emit(hgrp * 4 + kq, bv, bp, interior);
+                        emit(hgrp * 4 + kq, bv, bp, interior, hgrp, true);
                     }
                 } else {
                     // CI = 16: step s holds dy = s, dx = kq >> 1, group kq & 1; the dx = 1 half of the
@@ -512,7 +542,7 @@ __global__ void __launch_bounds__((BShape<C, V>::NW * 64), (sizeof(T) == 2 ? BSh
                         bp[i] = t ? pp : bp[i];
                     }
                     // both halves now agree; lanes 0-31 (groups kq = 0, 1) write
-                    emit(kq & 1, bv, bp, interior && lo_half);
+                    emit(kq & 1, bv, bp, interior && lo_half, 0, lo_half);   // (DKEEP: channels 16-31 are 0)
                 }
             }
         };
@@ -528,73 +558,78 @@ __global__ void __launch_bounds__((BShape<C, V>::NW * 64), (sizeof(T) == 2 ? BSh
 
         // ---- phase 1: t0 = act1(W1 x + b1) over tile + halo, 0 outside the image. The loads of CH1
         // fragments are issued together before any of them is consumed (memory-level parallelism).
-        Raw kx[KEEP ? NF2 : 1][KS1];                  // KEEP: this wave's interior fragments of x
+        // halo index of pixel pi of interior fragment f (tile pixel (i, j) = halo (i + RY, j + RX))
+        auto int_h = [&](int f) -> int {
+            const int p = f * 16 + col, i = p / TW, j = p - i * TW;
+            return (i + RY) * HWW + j + RX;
+        };
+        // loads of halo pixel h of the tile at (ty0, tx0) in frame byte offset txn (KS1 16-B chunks)
+        auto load_hg = [&](int ty0, int tx0, uint32_t txn, int h, bool valid, Raw (&xs)[KS1]) -> bool {
+            const int hy = h / HWW, hx = h - hy * HWW;
+            const int iy = ty0 + dt * ((tr ? hx : hy) - RY), ix = tx0 + dtx * ((tr ? hy : hx) - RX);
+            const bool ok = valid && (unsigned)iy < (unsigned)a.H && (unsigned)ix < (unsigned)a.W;
+#pragma unroll
+            for (int s = 0; s < KS1; ++s) {
+                const int g = s * 4 + kq;
+                bld8(xs[s], rxb, ok && g < G1 ? txn + ((__umul24((uint32_t)iy, (uint32_t)a.W) + (uint32_t)ix) * C + g * 8) * (uint32_t)sizeof(T) : OOB);
+            }
+            return ok;
+        };
+        // KEEP / DKEEP walk: the tile's interior as phase 3's fragments (a run of one tile row, on the
+        // wave that will expand it), then the halo border
+        constexpr int NBD = HR - NPX, NFB = (NBD + 15) / 16;   // border pixels / fragments
+        constexpr int NBW = (NFB + NW - 1) / NW;      // border fragments per wave (at most)
+        constexpr int B0 = NFT % NW;                  // border fragment k runs on wave (B0 + k) % NW
+        const int wb = wave >= B0 ? wave - B0 : wave - B0 + NW;   // this wave's first border fragment
+        // halo index of border pixel b: the RY top and bottom halo rows, then the RX columns either
+        // side of the TH interior rows
+        auto bord_h = [&](int b) -> int {
+            if (b < 2 * RY * HWW) {
+                const int r = b / HWW, c = b - r * HWW;
+                return (r < RY ? r : TH + r) * HWW + c;
+            }
+            if constexpr (RX > 0) {
+                const int bb = b - 2 * RY * HWW, r = bb / (2 * RX), c = bb - r * (2 * RX);
+                return (RY + r) * HWW + (c < RX ? c : TW + c);
+            }
+            return 0;
+        };
+        auto proj = [&](int h, bool valid, bool ok, const Raw (&xs)[KS1]) {
+            f32x4 acc[NR1];
+#pragma unroll
+            for (int r = 0; r < NR1; ++r) acc[r] = bias4(cb1 + r * 16 + kq * 4);
+#pragma unroll
+            for (int s = 0; s < KS1; ++s)
+#pragma unroll
+                for (int r = 0; r < NR1; ++r) {
+                    Raw wf;
+                    ld8(wf, w1 + (r * 16 + col) * K1S + s * 32 + kq * 8);
+                    mma(acc[r], wf, xs[s]);
+                }
+            if (valid) {
+#pragma unroll
+                for (int r = 0; r < NR1; ++r) {
+                    const int ch = r * 16 + kq * 4;
+                    if (ch >= IS) continue;
+                    float4 v = act(f4(acc[r]), cs1 + ch);
+                    if (!ok) v = make_float4(0.f, 0.f, 0.f, 0.f);
+                    st4(ts + h * PSTR + ch, v);
+                }
+            }
+        };
+        uint4 pres[DKEEP ? NF2 : 1][NPK];             // DKEEP: pooled residual of the interior fragments
         if constexpr (KEEP) {
             // every load of the wave's phase-1 work (its interior fragments, kept, and its share of
             // the border) is issued before the first MFMA: one memory round trip per tile
-            constexpr int NBD = HR - NPX, NFB = (NBD + 15) / 16;   // border pixels / fragments
-            constexpr int NBW = (NFB + NW - 1) / NW;  // border fragments per wave (at most)
-            constexpr int B0 = NFT % NW;              // border fragment k runs on wave (B0 + k) % NW
-            // halo index of pixel pi of interior fragment f (tile pixel (i, j) = halo (i + RY, j + RX))
-            auto int_h = [&](int f) -> int {
-                const int p = f * 16 + col, i = p / TW, j = p - i * TW;
-                return (i + RY) * HWW + j + RX;
-            };
-            // halo index of border pixel b: the RY top and bottom halo rows, then the RX columns
-            // either side of the TH interior rows
-            auto bord_h = [&](int b) -> int {
-                if (b < 2 * RY * HWW) {
-                    const int r = b / HWW, c = b - r * HWW;
-                    return (r < RY ? r : TH + r) * HWW + c;
-                }
-                if constexpr (RX > 0) {
-                    const int bb = b - 2 * RY * HWW, r = bb / (2 * RX), c = bb - r * (2 * RX);
-                    return (RY + r) * HWW + (c < RX ? c : TW + c);
-                }
-                return 0;
-            };
-            auto load_h = [&](int h, bool valid, Raw (&xs)[KS1]) -> bool {
-                const int hy = h / HWW, hx = h - hy * HWW;
-                const int iy = oy0 + dt * ((tr ? hx : hy) - RY), ix = ox0 + dtx * ((tr ? hy : hx) - RX);
-                const bool ok = valid && (unsigned)iy < (unsigned)a.H && (unsigned)ix < (unsigned)a.W;
-#pragma unroll
-                for (int s = 0; s < KS1; ++s) {
-                    const int g = s * 4 + kq;
-                    bld8(xs[s], rxb, ok && g < G1 ? xn + ((__umul24((uint32_t)iy, (uint32_t)a.W) + (uint32_t)ix) * C + g * 8) * (uint32_t)sizeof(T) : OOB);
-                }
-                return ok;
-            };
-            auto proj = [&](int h, bool valid, bool ok, const Raw (&xs)[KS1]) {
-                f32x4 acc[NR1];
-#pragma unroll
-                for (int r = 0; r < NR1; ++r) acc[r] = bias4(cb1 + r * 16 + kq * 4);
-#pragma unroll
-                for (int s = 0; s < KS1; ++s)
-#pragma unroll
-                    for (int r = 0; r < NR1; ++r) {
-                        Raw wf;
-                        ld8(wf, w1 + (r * 16 + col) * K1S + s * 32 + kq * 8);
-                        mma(acc[r], wf, xs[s]);
-                    }
-                if (valid) {
-#pragma unroll
-                    for (int r = 0; r < NR1; ++r) {
-                        const int ch = r * 16 + kq * 4;
-                        if (ch >= IS) continue;
-                        float4 v = act(f4(acc[r]), cs1 + ch);
-                        if (!ok) v = make_float4(0.f, 0.f, 0.f, 0.f);
-                        st4(ts + h * PSTR + ch, v);
-                    }
-                }
-            };
-            bool kok[NF2];
+            auto load_h = [&](int h, bool valid, Raw (&xs)[KS1]) -> bool { return load_hg(oy0, ox0, xn, h, valid, xs); };
             Raw bx[NBW][KS1];
             int bh[NBW];
             bool bok[NBW];
-            const int wb = wave >= B0 ? wave - B0 : wave - B0 + NW;   // this wave's first border fragment
+            if (!pf) {                                                 // (PIPE: prefetched in the previous tile's phase 3)
 #pragma unroll
-            for (int j = 0; j < NF2; ++j)
-                if (wave + NW * j < NFT) kok[j] = load_h(int_h(wave + NW * j), true, kx[j]);   // wave-uniform
+                for (int j = 0; j < NF2; ++j)
+                    if (wave + NW * j < NFT) kok[j] = load_h(int_h(wave + NW * j), true, kx[j]);   // wave-uniform
+            }
             auto load_b = [&](int k) {
                 const int b = (wb + NW * k) * 16 + col;
                 bh[k] = b < NBD ? bord_h(b) : 0;
@@ -630,6 +665,65 @@ __global__ void __launch_bounds__((BShape<C, V>::NW * 64), (sizeof(T) == 2 ? BSh
                 if (fb >= NFB) break;
                 if (k >= NBE) load_b(k);
                 proj(bh[k], fb * 16 + col < NBD, bok[k], bx[k]);
+            }
+        } else if constexpr (DKEEP) {
+            // down forms: the wave's interior fragments, then its border share, CH1 fragments' loads in
+            // flight at a time (the 2x2 stride-2 taps of the block input)
+            constexpr int NQ = NF2 + NBW;
+            auto load_dn = [&](int h, bool valid, Raw (&xs)[KS1]) -> bool {
+                const int hy = h / HWW, hx = h - hy * HWW;
+                const int iy = oy0 + hy - 1, ix = ox0 + hx - 1;
+                const bool ok = valid && (unsigned)iy < (unsigned)a.H && (unsigned)ix < (unsigned)a.W;
+#pragma unroll
+                for (int s = 0; s < KS1; ++s) {
+                    const int g = s * 4 + kq;
+                    const int tap = g / CG1, cc = g - tap * CG1;   // pack_conv's K order: dy = tap >> 1, dx = tap & 1
+                    const uint32_t sy = (uint32_t)(2 * iy + (tap >> 1)), sx = (uint32_t)(2 * ix + (tap & 1));
+                    uint32_t v = xin_n + ((__umul24(sy, (uint32_t)(2 * a.W)) + sx) * CI + cc * 8) * (uint32_t)sizeof(T);
+                    asm volatile("" : "+v"(v));
+                    bld8(xs[s], rxb, ok && g < G1 ? v : OOB);
+                }
+                return ok;
+            };
+#pragma unroll
+            for (int j = 0; j < NF2; ++j)
+#pragma unroll
+                for (int k = 0; k < NPK; ++k) pres[j][k] = make_uint4(0u, 0u, 0u, 0u);
+#pragma unroll
+            for (int q0 = 0; q0 < NQ; q0 += CH1) {
+                Raw xf[CH1][KS1];
+                bool okc[CH1], vq[CH1];
+                int hq[CH1];
+#pragma unroll
+                for (int c = 0; c < CH1; ++c) {
+                    const int q = q0 + c;
+                    if (q >= NQ) break;
+                    if (q < NF2) {
+                        const int f = wave + NW * q;
+                        vq[c] = f < NFT;
+                        hq[c] = vq[c] ? int_h(f) : 0;
+                    } else {
+                        const int b = (wb + NW * (q - NF2)) * 16 + col;
+                        vq[c] = b < NBD;
+                        hq[c] = vq[c] ? bord_h(b) : 0;
+                    }
+                    okc[c] = load_dn(hq[c], vq[c], xf[c]);
+                }
+#pragma unroll
+                for (int c = 0; c < CH1; ++c) {
+                    const int q = q0 + c;
+                    if (q >= NQ) break;
+                    if (q < NF2) {
+                        const int f = wave + NW * q;
+                        if (f >= NFT) continue;               // wave-uniform
+                        proj(hq[c], true, okc[c], xf[c]);
+                        const int p = f * 16 + col, ti = p / TW, tj = p - ti * TW;
+                        pool_store(xf[c], okc[c], oy0 + ti, ox0 + tj, pres[q]);
+                    } else {
+                        if (wb + NW * (q - NF2) >= NFB) continue;   // wave-uniform
+                        proj(hq[c], vq[c], okc[c], xf[c]);
+                    }
+                }
             }
         } else
         for (int f0 = wave; f0 < NF1; f0 += NW * CH1) {
@@ -684,7 +778,8 @@ __global__ void __launch_bounds__((BShape<C, V>::NW * 64), (sizeof(T) == 2 ? BSh
                 if constexpr (DN) {
                     const int hy = h / HWW, hx = h - hy * HWW;
                     const bool interior = okc[c] && hy >= 1 && hy <= TH && hx >= 1 && hx <= TW;
-                    pool_store(xf[c], interior, oy0 + (hy - 1), ox0 + (hx - 1));
+                    uint4 pkd[NPK];
+                    pool_store(xf[c], interior, oy0 + (hy - 1), ox0 + (hx - 1), pkd);
                 }
             }
         }
@@ -728,7 +823,7 @@ __global__ void __launch_bounds__((BShape<C, V>::NW * 64), (sizeof(T) == 2 ? BSh
 #pragma unroll
             for (int j = 0; j < RP; ++j) load_res(j, res[j]);
         };
-        if constexpr (!ASYM && !KEEP) prefetch_res();
+        if constexpr (!ASYM && !KEEP && !DKEEP) prefetch_res();
 
         // t1 never goes through LDS: each wave's middle-conv accumulators (quads: lane kq holds channels
         // 4kq..4kq+3 of a pixel) are rounded as the unfused plan stores them and turned into the
@@ -954,6 +1049,12 @@ __global__ void __launch_bounds__((BShape<C, V>::NW * 64), (sizeof(T) == 2 ? BSh
             continue;
         }
         STAMP(5);
+        // PIPE: the next tile of this workgroup's walk (wave-uniform), prefetched fragment by fragment
+        const int itn = it + nslots, tilen = grp * CH + itn;
+        const bool nxt = PIPE && itn < CH && tilen < a.ntiles;
+        int nn = 0, noy0 = 0, nox0 = 0;
+        if (nxt) tile_geom(tilen, nn, noy0, nox0);
+        const uint32_t nxn = (uint32_t)(nn * a.H * a.W) * (uint32_t)(C * sizeof(T));
 #pragma unroll
         for (int j = 0; j < NF2; ++j) {
             if (wave + NW * j >= NFT) break;              // wave-uniform
@@ -967,6 +1068,7 @@ __global__ void __launch_bounds__((BShape<C, V>::NW * 64), (sizeof(T) == 2 ? BSh
                 const uint32_t off = po == OOB ? OOB : po + (uint32_t)chunk_ch(t) * (uint32_t)sizeof(T);
                 uint4 rc;
                 if constexpr (KEEP) rc = kx[j][t].v;
+                else if constexpr (DKEEP) rc = t < NPK ? pres[j][t < NPK ? t : 0] : make_uint4(0u, 0u, 0u, 0u);
                 else rc = res[j % RP][t];
                 if constexpr (SWAP) {
                     const int r0 = 2 * t, r1 = 2 * t + 1;
@@ -979,7 +1081,7 @@ __global__ void __launch_bounds__((BShape<C, V>::NW * 64), (sizeof(T) == 2 ? BSh
                     mma(acc1, w1, tf[j]);
                     // residual chunk -> quads of rows r0 / r1
                     uint32_t a0 = rc.x, a1 = rc.y, b0 = rc.z, b1 = rc.w;
-                    if constexpr (KEEP) {
+                    if constexpr (KEEP || DKEEP) {
                         // kept x (lane kq: channels 32 t + 8 kq .. + 7, dwords d0..d3): row r0's quad
                         // of lane kq lives in lane kq / 2 (d0, d1 or d2, d3), row r1's in lane 2 + kq / 2;
                         // a row swap then a half swap of (d0, d2) and of (d1, d3) gathers both
@@ -1014,9 +1116,12 @@ __global__ void __launch_bounds__((BShape<C, V>::NW * 64), (sizeof(T) == 2 ? BSh
                     }
                 }
             }
-            if constexpr (!KEEP)
+            if constexpr (!KEEP && !DKEEP)
                 if (j + RP < NF2 && wave + NW * (j + RP) < NFT) load_res(j + RP, res[j % RP]);
+            if constexpr (PIPE)
+                if (nxt) kok[j] = load_hg(noy0, nox0, nxn, int_h(wave + NW * j), true, kx[j]);
         }
+        if constexpr (PIPE) pf = nxt;
         STAMP(6);
     }
     STAMP_ENTRY(1);
@@ -1116,14 +1221,15 @@ hipError_t launch_bneck(int prec, int C, bool asym, int v, const BneckArgs &a, h
     }
     // grid: one round of resident workgroups (each walks ntiles / grid tiles, staging its weights
     // once), or the earlier fixed cap of 2048 (BUGSEG_BNECK_GRID=cap: A/B knob, 0 = resident slots)
-    static int grid_cap = -1, n_cu = 0;
-    if (grid_cap < 0) {
-        const char *e = std::getenv("BUGSEG_BNECK_GRID");
-        grid_cap = e ? std::atoi(e) : 0;
+    // (read per launch, so a test can force multi-tile walks at any shape)
+    static int n_cu = -1;
+    if (n_cu < 0) {
         int dev = 0;
         if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&n_cu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
             n_cu = 0;
     }
+    const char *ge = std::getenv("BUGSEG_BNECK_GRID");
+    const int grid_cap = ge ? std::atoi(ge) : 0;
     int cap = grid_cap;
     if (cap <= 0) {
         // (BUGSEG_BNECK_GRID=-k: 1/k of the resident slots, at least one per CU — leaves room for a

@@ -12,7 +12,8 @@ FETCH_SIZE is doubled on gfx950. Writes a markdown table (per op tag: launches, 
 launch) and profiles/dl_pmc_traffic.json ({"per_launch_bytes": {tag: bytes}}), which
 bench_deeplab.py reports as roofline.traffic for its dominant op tag.
 
-usage: python scripts/dl_pmc_summary.py gpurun_out/<tag> [out.md] [out.json] [--batch 16]
+usage: python scripts/dl_pmc_summary.py gpurun_out/<tag> [out.md] [out.json] [--batch 16] [--backbone xception_65]
+(Xception-65: profiles/dl_pmc_traffic_xception.json, which bench_deeplab.py reads for that backbone)
 """
 import csv
 import json
@@ -39,10 +40,13 @@ def dispatches(path, counter):
     return [tuple(rows[d]) for d in sorted(rows)]
 
 
-def op_kinds(B):
+def op_kinds(B, backbone="mobilenet_v2"):
     from bugcar_image_segmentation_amd import deeplab_spec as D
-    net = D.build_deeplab()
-    _, ops, _, info = D.lower(net, B, True)
+    if backbone == "xception_65":
+        from bugcar_image_segmentation_amd import deeplab_xception as X
+        _, ops, _, info = X.lower_xception(X.build_deeplab_xception(), B, True)
+    else:
+        _, ops, _, info = D.lower(D.build_deeplab(), B, True)
     return [int(o[0]) for o in ops], [t for t, _, _ in info["per_op"]]
 
 
@@ -58,7 +62,9 @@ def per_op(disp, kinds):
                 ok = False
                 break
             name = disp[j][1]
-            want = {D.OP_PREP: "dl_prep", D.OP_CONV: "dl_conv", D.OP_DW: "dl_dw", D.OP_ARGMAX: "argmax"}.get(kind)
+            # (the 1x1 convs run on dl_conv_kernel or one of the two GEMM kernels)
+            want = {D.OP_PREP: ("dl_prep",), D.OP_CONV: ("dl_conv", "dl_gemm"), D.OP_DW: ("dl_dw",),
+                    D.OP_ARGMAX: ("argmax",), D.OP_RESIZE: ("dl_resize_kernel",)}.get(kind, ())
             if kind == D.OP_POOL:
                 v, j0 = 0.0, j
                 while j < len(disp) and ("gap" in disp[j][1] or "pool" in disp[j][1]):
@@ -69,7 +75,7 @@ def per_op(disp, kinds):
                     break
                 vals.append(v)
                 continue
-            if want not in name:
+            if not any(w in name for w in want):
                 ok = False
                 break
             vals.append(disp[j][2])
@@ -98,15 +104,19 @@ def main(argv):
     if argv and argv[0] == "--sq":
         print(sq_table(argv[1]))
         return None
-    B = 16
+    B, backbone = 16, "mobilenet_v2"
     if "--batch" in argv:
         i = argv.index("--batch")
         B = int(argv[i + 1])
         argv = argv[:i] + argv[i + 2:]
+    if "--backbone" in argv:
+        i = argv.index("--backbone")
+        backbone = argv[i + 1]
+        argv = argv[:i] + argv[i + 2:]
     d = Path(argv[0])
     out_md = argv[1] if len(argv) > 1 else None
     out_json = argv[2] if len(argv) > 2 else None
-    kinds, tags = op_kinds(B)
+    kinds, tags = op_kinds(B, backbone)
     rd = per_op(dispatches(next((d / "fetch").glob("*counter_collection.csv")), "FETCH_SIZE"), kinds)
     wr = per_op(dispatches(next((d / "write").glob("*counter_collection.csv")), "WRITE_SIZE"), kinds)
     if not rd or not wr:
@@ -133,7 +143,7 @@ def main(argv):
     if out_md:
         Path(out_md).write_text(text + "\n")
     if out_json:
-        Path(out_json).write_text(json.dumps({"source": str(d), "correction": "FETCH_SIZE x2 (gfx950)", "batch": B,
+        Path(out_json).write_text(json.dumps({"source": str(d), "correction": "FETCH_SIZE x2 (gfx950)", "batch": B, "backbone": backbone,
                                               "per_launch_bytes": per,
                                               "per_op_bytes": [r + w for r, w in zip(r_op, w_op)]}, indent=1) + "\n")
     return per

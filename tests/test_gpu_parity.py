@@ -326,6 +326,33 @@ def test_fused_bottlenecks_equal_unfused(gpu, blocks, prec, H, W, variant, monke
     assert torch.equal(a, b)
 
 
+@pytest.mark.parametrize("grid", ["8", "-2"])
+@pytest.mark.parametrize("variant", [None, "0", "2", "4"])
+@pytest.mark.parametrize("prec", ["bf16", "fp16"])
+@pytest.mark.parametrize("H,W", [(72, 104), (480, 640)])
+def test_fused_bottlenecks_multi_tile_walks(gpu, blocks, prec, H, W, variant, grid, monkeypatch):
+    """Every fused bottleneck launch on a small grid (BUGSEG_BNECK_GRID: 8 workgroups, or half the
+    resident slots), so each workgroup walks several tiles and the kept-residual forms prefetch the
+    next tile's interior x under the current tile's expansion (BNECK_PIPE): bit-identical to the
+    unfused chain."""
+    B = 2
+    bgr = torch.from_numpy(synthetic.road_frames(B, H, W, seed=H + 1)).cuda()
+    if variant is not None:
+        monkeypatch.setenv("BUGSEG_BNECK_VARIANT", variant)
+    monkeypatch.setenv("BUGSEG_BNECK_GRID", grid)
+    fused = ENET(weights=blocks, precision=prec)
+    a = torch.empty((B, 15, H, W), dtype=torch.float32, device=gpu)
+    fused.ctx.forward_bgr(bgr, B, H, W, N.OUT_LOGITS_F32, a)
+    torch.cuda.synchronize()
+    monkeypatch.delenv("BUGSEG_BNECK_VARIANT", raising=False)
+    monkeypatch.delenv("BUGSEG_BNECK_GRID", raising=False)
+    monkeypatch.setenv("BUGSEG_NO_FUSE", "1")
+    plain = ENET(weights=blocks, precision=prec)
+    b = torch.empty_like(a)
+    plain.ctx.forward_bgr(bgr, B, H, W, N.OUT_LOGITS_F32, b)
+    assert torch.equal(a, b)
+
+
 @pytest.mark.parametrize("prec", ["fp32", "bf16", "fp16"])
 def test_up_block_pair_equals_separate(gpu, blocks, prec, monkeypatch):
     """The upsampling blocks' main and extension 1x1 convolutions merged into one launch (one read
