@@ -68,6 +68,7 @@ def kernel_table(ctx, B, H, W, reps, stream):
         gr["total_us"] += us
         gr["bytes"] += pb
         gr["flops"] += fl
+    groups.pop("fused", None)     # op 1 when the initial block ran fused into it ("init+down C64": op 0)
     for gr in groups.values():
         gr["us_per_launch"] = gr["total_us"] / gr["launches"]
         gr["bytes_per_launch"] = gr["bytes"] / gr["launches"]

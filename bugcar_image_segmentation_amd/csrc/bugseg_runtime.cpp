@@ -79,6 +79,10 @@ struct Plan {
     void *arena = nullptr;
     size_t arena_bytes = 0;
     bool pinned = false;     // a forward on this arena was captured into a graph: never freed before destroy
+    // the last forward ran ops 0 + 1 (initial block on BGR frames + the first downsampling block) as
+    // one launch (launch_bneck_init); plan_op / plan_launch_op then report and launch op 0 as that
+    // pair and op 1 as empty ("fused")
+    bool init_fused = false;
 };
 
 inline int round_up(int v, int m) { return (v + m - 1) / m * m; }
@@ -1259,6 +1263,34 @@ int bugseg_nchw_to_input(bugseg_ctx *ctx, const void *x, int is_f64, int B, int 
     return BUGSEG_OK;
 }
 
+// The initial block on raw BGR frames and the 16 -> 64 downsampling block after it, as one launch
+// (bneck_kernels.hip INI form): 2-byte storage, ENet's canonical shapes, both ops planned as the
+// initial-block kernel and the fused down form. BUGSEG_NO_INIT_FUSE=1 keeps the two launches (A/B;
+// results are bit-identical).
+static bool init_fusable(const bugseg_ctx *ctx, const Plan &pl) {
+    const char *nf = std::getenv("BUGSEG_NO_INIT_FUSE");
+    if (nf && *nf && *nf != '0') return false;
+    if (ctx->prec == PREC_F32 || pl.ops.size() < 3) return false;
+    const Op &o0 = pl.ops[0], &o1 = pl.ops[1];
+    if (o0.kind != 0 || o1.kind != 1 || o1.bn_cin != 16 || o1.bn_c != 64 || o1.bn_asym) return false;
+    if (o0.a.cconv + o0.a.cpool != 16 || o0.a.cpool > 3 || (o0.a.pool_k != 2 && o0.a.pool_k != 3)) return false;
+    if (o0.a.Hg != 2 * o1.bn.H || o0.a.Wg != 2 * o1.bn.W || o0.a.Hin != 2 * o0.a.Hg || o0.a.Win != 2 * o0.a.Wg) return false;
+    if ((double)o0.a.B * o0.a.Hin * o0.a.Win * 3.0 >= 2147483648.0) return false;
+    return bneck_init_supported(ctx->prec, o1.bn_c, o1.bn_var, o1.bn_cin);
+}
+
+static hipError_t launch_init_down(const bugseg_ctx *ctx, const Plan &pl, hipStream_t stream) {
+    const Op &o0 = pl.ops[0], &o1 = pl.ops[1];
+    BneckArgs q = o1.bn;
+    q.bgr = (const uint8_t *)o0.a.in;
+    q.bgr_bytes = (uint32_t)((size_t)o0.a.B * o0.a.Hin * o0.a.Win * 3);
+    q.nlut = o0.a.nlut;
+    q.w0 = o0.a.w; q.kpad0 = o0.a.Kpad;
+    q.b0 = o0.a.bias; q.s0 = o0.a.slope1; q.p0 = o0.a.pscale;
+    q.cconv = o0.a.cconv; q.cpool = o0.a.cpool; q.pool_k = o0.a.pool_k;
+    return launch_bneck_init(ctx->prec, o1.bn_c, o1.bn_var, q, stream, o1.bn_cin);
+}
+
 static int enet_forward(bugseg_ctx *ctx, const void *in, bool bgr, int B, int H, int W, int out_kind, void *out,
                         void *stream, int first_op = 0, int last_op = -1) {
     if (!ctx || !in || !out) return fail(ctx, BUGSEG_EINVAL, "NULL argument");
@@ -1285,7 +1317,18 @@ static int enet_forward(bugseg_ctx *ctx, const void *in, bool bgr, int B, int H,
     const int nops = (int)pl.ops.size();
     if (last_op < 0 || last_op > nops) last_op = nops;
     if (first_op < 0 || first_op > last_op) return fail(ctx, BUGSEG_EINVAL, "bad op range");
-    for (int i = first_op; i < last_op; ++i) {
+    int i0 = first_op;
+    if (first_op == 0 && last_op >= 2) {
+        pl.init_fused = bgr && init_fusable(ctx, pl);
+        if (pl.init_fused) {
+            hipError_t e = launch_init_down(ctx, pl, (hipStream_t)stream);
+            if (e != hipSuccess) return fail(ctx, BUGSEG_EHIP, std::string("initial + down launch: ") + hipGetErrorString(e));
+            i0 = 2;
+        }
+    } else if (first_op == 0) {
+        pl.init_fused = false;
+    }
+    for (int i = i0; i < last_op; ++i) {
         const Op &op = pl.ops[(size_t)i];
         hipError_t e = op.kind == 1 ? launch_bneck(ctx->prec, op.bn_c, op.bn_asym, op.bn_var, op.bn, (hipStream_t)stream, op.bn_cin)
                      : op.kind == 2 ? launch_up(ctx->prec, op.up_cin, op.up_it, op.up_cout, op.up, (hipStream_t)stream)
@@ -1640,10 +1683,14 @@ int bugseg_plan_info(bugseg_ctx *ctx, int B, int H, int W, int out_kind, int bgr
     // final epilogue output
     const double fin = out_kind == BUGSEG_OUT_LOGITS_F32 ? (double)B * H * W * ctx->ncls * 4 : (double)B * H * W;
     // raw BGR input (bugseg_enet_forward_bgr): 3 bytes per pixel instead of the 8-channel engine input
-    const double adj = bgr_input ? (double)B * H * W * (8.0 * prec_es(ctx->prec) - 3.0) : 0.0;
+    double adj = bgr_input ? (double)B * H * W * (8.0 * prec_es(ctx->prec) - 3.0) : 0.0;
+    // ... and the initial block fused into the first downsampling block: its output is neither
+    // written nor read back (plan bytes only; the per-layer figure keeps the unfused definition)
+    const double fused = bgr_input && init_fusable(ctx, ctx->plan)
+                             ? 2.0 * (double)B * (H / 2) * (W / 2) * 16 * prec_es(ctx->prec) : 0.0;
     if (n_launches) *n_launches = (int)ctx->plan.ops.size();
     if (alg_bytes) *alg_bytes = lb + fin - adj;
-    if (plan_bytes) *plan_bytes = pb + fin - adj;
+    if (plan_bytes) *plan_bytes = pb + fin - adj - fused;
     if (flops) *flops = fl;
     return BUGSEG_OK;
 }
@@ -1657,6 +1704,25 @@ int bugseg_plan_op(bugseg_ctx *ctx, int B, int H, int W, int op, char *kernel, i
     if (op < 0 || op >= (int)pl.ops.size()) return fail(ctx, BUGSEG_EINVAL, "op index out of range");
     const Op &o = pl.ops[op];
     std::string tag;
+    if (pl.init_fused && op <= 1) {
+        // op 0: the initial block + the first downsampling block as one launch (BGR in, the down
+        // block's output and indices out); op 1: nothing left to launch
+        const Op &o1 = pl.ops[1];
+        const int es = prec_es(ctx->prec);
+        const double ib = (double)o1.bn.B * 4 * o1.bn.H * 4 * o1.bn.W * 3;      // BGR frames
+        const double x0 = (double)o1.bn.B * 2 * o1.bn.H * 2 * o1.bn.W * 16 * es;   // the initial block's output
+        const double pb = op == 0 ? ib + (o1.bytes - x0) + (double)o.a.Npad * o.a.Kpad * es : 0.0;
+        const double lb = op == 0 ? ib + x0 + (o1.layer_bytes >= 0 ? o1.layer_bytes : o1.bytes) : 0.0;
+        tag = op == 0 ? "init+down C64" : "fused";
+        if (kernel && kernel_len > 0) {
+            std::strncpy(kernel, tag.c_str(), (size_t)kernel_len - 1);
+            kernel[kernel_len - 1] = 0;
+        }
+        if (alg_bytes) *alg_bytes = lb;
+        if (plan_bytes) *plan_bytes = pb;
+        if (flops) *flops = op == 0 ? o.flops + o1.flops : 0.0;
+        return BUGSEG_OK;
+    }
     if (o.kind == 2) {
         tag = "up C" + std::to_string(o.up_cout);
     } else if (o.kind == 1) {
@@ -1698,7 +1764,9 @@ int bugseg_plan_launch_op(bugseg_ctx *ctx, int B, int H, int W, int op, void *st
     if (op < 0 || op >= (int)pl.ops.size()) return fail(ctx, BUGSEG_EINVAL, "op index out of range");
     DeviceGuard g(ctx->device);
     const Op &o = pl.ops[op];
-    hipError_t e = o.kind == 1 ? launch_bneck(ctx->prec, o.bn_c, o.bn_asym, o.bn_var, o.bn, (hipStream_t)stream, o.bn_cin)
+    if (pl.init_fused && op == 1) return BUGSEG_OK;       // (launched with op 0)
+    hipError_t e = pl.init_fused && op == 0 ? launch_init_down(ctx, pl, (hipStream_t)stream)
+                 : o.kind == 1 ? launch_bneck(ctx->prec, o.bn_c, o.bn_asym, o.bn_var, o.bn, (hipStream_t)stream, o.bn_cin)
                  : o.kind == 2 ? launch_up(ctx->prec, o.up_cin, o.up_it, o.up_cout, o.up, (hipStream_t)stream)
                                : launch_conv(ctx->prec, o.nr, o.epi, o.a, (hipStream_t)stream);
     if (e != hipSuccess) return fail(ctx, BUGSEG_EHIP, "launch of op " + std::to_string(op) + ": " + hipGetErrorString(e));

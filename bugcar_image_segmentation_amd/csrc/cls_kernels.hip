@@ -51,6 +51,11 @@ __device__ __forceinline__ bool nonzero(const RawF &r) {
 
 // Taps: the 2x2 input neighbourhood (dy, dx) = (s >> 1, s & 1) of the k = 3 layer in pack_tconv's
 // order (D = {0, 1}, tap = ty * 2 + tx). LOGITS: the fp32 logits are written too (parity runs).
+// groups whose loads are in flight ahead of the one computing (1: the next; 2: the next two).
+// Measured (round 3, fp16, B = 32): 2 is no faster (37.3 vs 36.9 us per launch; 127 vs 109 VGPRs)
+#ifndef CLS_DEPTH
+#define CLS_DEPTH 1
+#endif
 template <typename T, bool LOGITS>
 __global__ void __launch_bounds__(256, sizeof(T) == 2 ? 4 : 1) cls_kernel(const ConvArgs a) {
     constexpr int CLS_TAPS = 4;
@@ -149,7 +154,7 @@ __global__ void __launch_bounds__(256, sizeof(T) == 2 ? 4 : 1) cls_kernel(const 
         // zeros, a neighbour's group is read and dropped), and a static count of loads in flight
         // lets the waits before the MFMAs name only this group's loads (a conditional prefetch
         // made the compiler wait vmcnt(3), i.e. for the next group's first load as well)
-        load(g + nw, nxt);
+        load(g + CLS_DEPTH * nw, nxt);
         const Px q = pixel(g);
         f32x16 acc[2];
 #pragma unroll
@@ -215,13 +220,32 @@ __global__ void __launch_bounds__(256, sizeof(T) == 2 ? 4 : 1) cls_kernel(const 
     };
     Raw xa[CLS_TAPS], xb[CLS_TAPS];
     int g = g0 + wi;
-    if (g < g1) load(g, xa);
-    while (g < g1) {
-        step(g, xa, xb);
-        g += nw;
-        if (g >= g1) break;
-        step(g, xb, xa);
-        g += nw;
+    if constexpr (CLS_DEPTH == 1) {
+        if (g < g1) load(g, xa);
+        while (g < g1) {
+            step(g, xa, xb);
+            g += nw;
+            if (g >= g1) break;
+            step(g, xb, xa);
+            g += nw;
+        }
+    } else {
+        // two groups ahead: three rotating buffers (the group after next is in flight as well)
+        Raw xc[CLS_TAPS];
+        if (g < g1) {
+            load(g, xa);
+            load(g + nw, xb);
+        }
+        while (g < g1) {
+            step(g, xa, xc);
+            g += nw;
+            if (g >= g1) break;
+            step(g, xb, xa);
+            g += nw;
+            if (g >= g1) break;
+            step(g, xc, xb);
+            g += nw;
+        }
     }
 }
 

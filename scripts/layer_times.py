@@ -18,6 +18,10 @@ BNECK_SHAPES = {(128, 0): "16x16", (128, 1): "20x16", (128, 2): "4x80", (128, 3)
 
 
 def short(name):
+    # the initial block fused into the first downsampling block (INI template argument true)
+    m = re.search(r"bneck_kernelI(DF16b|DF16_|f)Li(\d+)ELb\dELi\d+ELb\dELi[1-9]\d*ELb1E", name)
+    if m:
+        return f"init+down C{m.group(2)}"
     m = re.search(r"bneck_kernelI(DF16b|DF16_|f)Li(\d+)ELb(\d)ELi(\d+)ELb\dELi([1-9]\d*)E", name)
     if m:   # the downsampling form (non-zero input-channel template argument)
         return f"down C{m.group(2)} {BNECK_SHAPES.get((int(m.group(2)), int(m.group(4))), '?')}"

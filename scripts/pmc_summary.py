@@ -38,7 +38,7 @@ def main(tag_dir, out_md=None, out_json=None):
              "|---|---|---|---|---|"]
     per = {}
     for k in sorted(fetch, key=lambda k: -sum(fetch[k])):
-        if not any(t in k for t in ("conv", "bneck", "down", "init", "bev", "up C", "classes")):
+        if not any(t in k for t in ("conv", "bneck", "down", "init", "bev", "up C", "classes")):   # ("init+down" too)
             continue
         n = len(fetch[k])
         r = 2 * sum(fetch[k]) / n
