@@ -444,6 +444,14 @@ __global__ void __launch_bounds__(256, 4) bev_occgrid_lds_kernel(const BevArgs a
 constexpr int BEV_BAND = 4, BEV_BAND_CAP = 16384, BEV_BAND_PF = BEV_BAND_CAP / 16 / 256;
 
 __host__ __device__ inline int bev_bands(int occ_h) { return (occ_h + BEV_BAND - 1) / BEV_BAND; }
+// The band kernel's compact table, after the band boxes: [BEV_WIN][cells] u32, entry i of every cell
+// (BEV_ORDER_D order: the sample, its 3x3, then the ring) as the .y word alone — the tap's byte offset
+// in the band's LDS box, the fractions, the valid-tap and outside-template bits: what the LDS form
+// reads (4 B per entry instead of 8; no slot halves to pick). Filled by bev_bandbox_kernel for the
+// bands that stage their box.
+__host__ __device__ inline size_t bev_ctab_offset(int occ_w, int occ_h) {   // bytes from the table start
+    return ((size_t)occ_w * occ_h * BEV_SLOTS * 16 + (size_t)bev_bands(occ_h) * 16 + 255) & ~(size_t)255;
+}
 
 // per band: the class-map box (y0, xa, bh, bw) every valid tap of its cells reads, with a one-pixel
 // border, xa and bw whole 16-B chunks; bh = 0: no valid tap (every pixel reads the zero pad);
@@ -478,10 +486,13 @@ __global__ void __launch_bounds__(256) bev_bandbox_kernel(const BevArgs a, int4 
     if (threadIdx.x == 0) bbox[band] = bx;
     if (bx.z < 0) return;
     // each entry's top-left tap as a byte offset in the band's LDS box, in the entry's free bits 15..31
-    // (a template pixel without a valid tap: the zero pad after the box)
+    // (a template pixel without a valid tap: the zero pad after the box); the .y words also go to the
+    // compact table (bev_ctab_offset)
+    uint32_t *ctab = reinterpret_cast<uint32_t *>(reinterpret_cast<unsigned char *>(a.wtab) + bev_ctab_offset(a.occ_w, a.occ_h));
     for (int i = threadIdx.x; i < n * BEV_SLOTS; i += 256) {
         const int c = i / BEV_SLOTS, q = i - c * BEV_SLOTS;
-        uint4 *sp = a.wtab + (long)q * cells + (long)r0 * a.occ_w + c;
+        const long rem = (long)r0 * a.occ_w + c;
+        uint4 *sp = a.wtab + (long)q * cells + rem;
         uint4 sv = *sp;
         auto put = [&](uint32_t x, uint32_t &y) {
             const uint2 e = make_uint2(x, y);
@@ -492,6 +503,8 @@ __global__ void __launch_bounds__(256) bev_bandbox_kernel(const BevArgs a, int4 
         put(sv.x, sv.y);
         put(sv.z, sv.w);
         *sp = sv;
+        ctab[(long)(2 * q) * cells + rem] = sv.y;
+        if (2 * q + 1 < BEV_WIN) ctab[(long)(2 * q + 1) * cells + rem] = sv.w;
     }
 }
 
@@ -640,8 +653,92 @@ __global__ void __launch_bounds__(256, FB == 1 ? 7 : 4) bev_band_kernel(const Be
                 if (f < nf) bev_emit(a, b0 + f, rem, cx, cy, cells, v[f]);
         }
     };
-    if (lds) cells_loop(std::true_type());
-    else cells_loop(std::false_type());
+// (measured, round 3, 32 frames of 480x640, scripts/bev_sweep.py: 42.2-49.0 -> 35.6-39.2 us per launch,
+// laserscan 52.6-55.8 -> 49.8-52.1; BEV_CTAB=0: the uint4-slot form)
+#ifndef BEV_CTAB
+#define BEV_CTAB 1
+#endif
+    if (lds && BEV_CTAB) {
+        // the LDS form on the compact table: 4-B entries, the 3x3's 9 of the next cell in flight while
+        // this one is evaluated, and the 16 ring entries of a cell that needs them issued together (one
+        // L2 round trip instead of one per slot)
+        const uint32_t *ct = reinterpret_cast<const uint32_t *>(reinterpret_cast<const unsigned char *>(a.wtab) +
+                                                                bev_ctab_offset(a.occ_w, a.occ_h)) + (size_t)r0 * a.occ_w;
+        auto value = [&](uint32_t ey, int f) -> int {
+            const uint8_t *p = box[f] + (ey >> 15);
+            const uint32_t l0 = p[0], l1 = p[1], l2 = p[bw], l3 = p[bw + 1];
+            const uint32_t ax = ey & 31u, ay = (ey >> 5) & 31u;
+            const uint32_t wx = 32u + ax * 65535u, wy = 32u + ay * 65535u;   // (32 - a) | a << 16
+            const uint32_t top = dot2(l0 | l1 << 16, wx, 0u), bot = dot2(l2 | l3 << 16, wx, 0u);
+            return (int)(dot2(top | bot << 16, wy, 512u) >> 10);              // (sum + 2^14) >> 15 of OpenCV
+        };
+        uint32_t c9n[9];
+        auto load9 = [&](int c) {
+            const uint32_t *t = ct + min(c, n - 1);
+#pragma unroll
+            for (int i = 0; i < 9; ++i) c9n[i] = t[(long)i * cells];
+        };
+        load9(tid);
+        for (int c = tid; c < n; c += 256) {
+            const int rem = r0 * a.occ_w + c;
+            const int cy = rem / a.occ_w, cx = rem - cy * a.occ_w;
+            uint32_t e9[9];
+#pragma unroll
+            for (int i = 0; i < 9; ++i) e9[i] = c9n[i];
+            load9(c + 256);
+            uint32_t outm = 0;
+#pragma unroll
+            for (int i = 0; i < 9; ++i) outm |= (uint32_t)((e9[i] & TAB_OUT) != 0) << BEV_ORDER[i];
+            int v[FB];
+            uint32_t m[FB];
+            bool need = false;
+#pragma unroll
+            for (int f = 0; f < FB; ++f) {
+                int t9[9];
+#pragma unroll
+                for (int i = 0; i < 9; ++i) t9[i] = value(e9[i], f);
+                v[f] = t9[0];
+                m[f] = outm;
+#pragma unroll
+                for (int i = 0; i < 9; ++i) m[f] |= (uint32_t)occupied(a, t9[i]) << BEV_ORDER[i];
+                need |= f < nf && occupied(a, v[f]) && (m[f] & inner) != inner;
+            }
+            if (need) {
+                uint32_t er[BEV_WIN - 9];
+#pragma unroll
+                for (int k = 0; k < BEV_WIN - 9; ++k) er[k] = ct[(long)(9 + k) * cells + c];
+#pragma unroll
+                for (int f = 0; f < FB; ++f)
+#pragma unroll
+                    for (int k = 0; k < BEV_WIN - 9; ++k)
+                        m[f] |= (uint32_t)((er[k] & TAB_OUT) || occupied(a, value(er[k], f))) << BEV_ORDER[9 + k];
+                int tx, ty;
+                cell_pixel(a, cx, cy, tx, ty);
+#pragma unroll
+                for (int f = 0; f < FB; ++f) {
+                    if (!(occupied(a, v[f]) && (m[f] & inner) != inner)) continue;
+                    bool opened = false;
+#pragma unroll
+                    for (int qy = -1; qy <= 1; ++qy)
+#pragma unroll
+                        for (int qx = -1; qx <= 1; ++qx) {
+                            const bool inside = (unsigned)(tx + qx) < (unsigned)a.occ_w_px && (unsigned)(ty + qy) < (unsigned)a.occ_h_px;
+                            const int sh = qy * 5 + qx;
+                            const uint32_t win = sh >= 0 ? inner << sh : inner >> -sh;
+                            opened |= inside && (m[f] & win) == win;
+                        }
+                    if (!opened) v[f] = 2;           // isolated occupied pixel -> free (bev.py:204-205)
+                }
+            }
+#pragma unroll
+            for (int f = 0; f < FB; ++f)
+                if (f < nf) bev_emit(a, b0 + f, rem, cx, cy, cells, v[f]);
+        }
+    } else if (lds) {
+        cells_loop(std::true_type());
+    } else {
+        cells_loop(std::false_type());
+    }
 }
 
 // ---- laserscan-like occupancy (bev.py:216-240; binary variant bev.py:143-164) ----------------------
@@ -714,7 +811,7 @@ __global__ void __launch_bounds__(256) laserscan_kernel(const BevArgs a) {
 }
 
 size_t bev_table_bytes(int occ_w, int occ_h) {
-    return (size_t)occ_w * occ_h * BEV_SLOTS * sizeof(uint4) + (size_t)bev_bands(occ_h) * sizeof(int4);
+    return bev_ctab_offset(occ_w, occ_h) + (size_t)occ_w * occ_h * BEV_WIN * sizeof(uint32_t);
 }
 
 hipError_t launch_bev_table(const BevArgs &a, hipStream_t s) {

@@ -131,7 +131,11 @@ void bneck_shape(int C, int v, int &th, int &tw, int &nw, int *rd) {
 // INI: the ENet initial block (preprocessing fused: models.py:84-95) computed
 // inside this kernel from the raw BGR frames, feeding the 16 -> 64 downsampling block's projection
 // directly (see the INI notes at the patch staging and at init_dn): the initial block's output never
-// goes through HBM.
+// goes through HBM. Bit-identical to the two launches, but measured slower than them (round 3, fp16,
+// B = 32: 113-121 us vs 43.5 + 49 us): the 52 KB patch holds the form to 3 workgroups (12 waves) per
+// CU, where the initial block's LDS-latency-bound arithmetic needs the 6-8 waves per SIMD its own
+// kernel runs at; a BGR-order patch (8-B LDS stores instead of 2-B ones) changes the initial conv's
+// MFMA k order, so it is no longer bit-identical. Opt-in (BUGSEG_INIT_FUSE=1, bugseg_runtime.cpp).
 template <typename T, int C, bool ASYM, int V, bool TR, int CI = 0, bool INI = false>
 __global__ void __launch_bounds__((BShape<C, V>::NW * 64), (sizeof(T) == 2 ? (INI ? 3 : BShape<C, V>::OCC) : 1)) bneck_kernel(const BneckArgs a) {
     using Raw = typename Tr<T>::Raw;

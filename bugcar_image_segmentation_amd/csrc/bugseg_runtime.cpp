@@ -1265,11 +1265,13 @@ int bugseg_nchw_to_input(bugseg_ctx *ctx, const void *x, int is_f64, int B, int 
 
 // The initial block on raw BGR frames and the 16 -> 64 downsampling block after it, as one launch
 // (bneck_kernels.hip INI form): 2-byte storage, ENet's canonical shapes, both ops planned as the
-// initial-block kernel and the fused down form. BUGSEG_NO_INIT_FUSE=1 keeps the two launches (A/B;
-// results are bit-identical).
+// initial-block kernel and the fused down form. Opt-in (BUGSEG_INIT_FUSE=1; results bit-identical):
+// measured slower than the two launches (round 3, fp16, B = 32: 113-121 us vs 43.5 + 49 us) — the
+// fused form holds the BGR patch in LDS (52 KB: 3 workgroups, 12 waves per CU) and its initial-block
+// arithmetic is latency-bound at that occupancy, where the separate kernels run 6-8 waves per SIMD.
 static bool init_fusable(const bugseg_ctx *ctx, const Plan &pl) {
-    const char *nf = std::getenv("BUGSEG_NO_INIT_FUSE");
-    if (nf && *nf && *nf != '0') return false;
+    const char *on = std::getenv("BUGSEG_INIT_FUSE");
+    if (!on || !*on || *on == '0') return false;
     if (ctx->prec == PREC_F32 || pl.ops.size() < 3) return false;
     const Op &o0 = pl.ops[0], &o1 = pl.ops[1];
     if (o0.kind != 0 || o1.kind != 1 || o1.bn_cin != 16 || o1.bn_c != 64 || o1.bn_asym) return false;

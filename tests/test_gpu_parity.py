@@ -304,23 +304,24 @@ def test_forward_bgr_equals_preprocess_then_forward(gpu, prec, pool_k):
 @pytest.mark.parametrize("pool_k", [3, 2])
 @pytest.mark.parametrize("B,H,W", [(2, 72, 104), (1, 480, 640), (3, 96, 128)])
 def test_initial_block_fused_into_down1_bit_identical(gpu, prec, pool_k, B, H, W, grid, monkeypatch):
-    """forward_bgr in 2-byte storage runs the initial block (preprocess fused) inside the first
-    downsampling block's launch (bneck_kernels.hip INI form: the initial block's output never leaves
-    the chip). Logits and the class map are bit-identical to the two launches
-    (BUGSEG_NO_INIT_FUSE=1), at partial tiles, several frames, both pool windows, and with every
+    """With BUGSEG_INIT_FUSE=1, forward_bgr in 2-byte storage runs the initial block (preprocess
+    fused) inside the first downsampling block's launch (bneck_kernels.hip INI form: the initial
+    block's output never leaves the chip). Logits and the class map are bit-identical to the two
+    launches (the default), at partial tiles, several frames, both pool windows, and with every
     workgroup walking many tiles (BUGSEG_BNECK_GRID=8)."""
     bl = enet_spec.build_enet(seed=19, initial_pool_k=pool_k)
     m = ENET(weights=bl, precision=prec)
     bgr = torch.from_numpy(synthetic.road_frames(B, H, W, seed=H + pool_k)).cuda()
     if grid is not None:
         monkeypatch.setenv("BUGSEG_BNECK_GRID", grid)
+    monkeypatch.setenv("BUGSEG_INIT_FUSE", "1")
     a = torch.empty((B, 15, H, W), dtype=torch.float32, device=gpu)
     m.ctx.forward_bgr(bgr, B, H, W, N.OUT_LOGITS_F32, a)
     ca = torch.empty((B, H, W), dtype=torch.uint8, device=gpu)
     m.ctx.forward_bgr(bgr, B, H, W, N.OUT_CLASS3_U8, ca)
     torch.cuda.synchronize()
     assert m.ctx.plan_op(B, H, W, 0)[0] == "init+down C64"
-    monkeypatch.setenv("BUGSEG_NO_INIT_FUSE", "1")
+    monkeypatch.delenv("BUGSEG_INIT_FUSE")
     b = torch.empty_like(a)
     m.ctx.forward_bgr(bgr, B, H, W, N.OUT_LOGITS_F32, b)
     cb = torch.empty_like(ca)
@@ -434,11 +435,11 @@ def test_class_layer_kernel_matches_conv_path(gpu, blocks, prec, monkeypatch):
     assert (la.argmax(axis=1)[decided] == lb.argmax(axis=1)[decided]).all()
 
 
-def test_canonical_plan_is_one_launch_per_block(gpu, blocks):
+def test_canonical_plan_is_one_launch_per_block(gpu, blocks, monkeypatch):
     """At the bench shape every ENet block of the canonical graph runs as ONE fused launch: initial
     block, 2 downsampling, 23 regular / dilated / asymmetric bottlenecks, 2 upsampling blocks and
-    the class layer (29 planned launches); the unfused reference plan has one launch per
-    convolution. On raw BGR frames in 2-byte storage the initial block runs inside the first
+    the class layer (29 launches); the unfused reference plan has one launch per convolution. With
+    BUGSEG_INIT_FUSE=1, on raw BGR frames in 2-byte storage, the initial block runs inside the first
     downsampling block's launch (28 launches); from the engine input (or in fp32) it is its own."""
     B, H, W = 2, 480, 640
     m = ENET(weights=blocks, precision="bf16")
@@ -448,10 +449,14 @@ def test_canonical_plan_is_one_launch_per_block(gpu, blocks):
     n = m.ctx.plan_info(B, H, W, N.OUT_CLASS3_U8, bgr_input=True)[0]
     tags = [m.ctx.plan_op(B, H, W, i)[0] for i in range(n)]
     assert n == 29
-    assert tags[0] == "init+down C64" and tags[1] == "fused" and tags[-1] == "classes"
+    assert tags[0] == "init" and tags[-1] == "classes"
     assert [t.split(" ")[0] + " " + t.split(" ")[1] for t in tags if t.startswith(("down", "up"))] == \
-        ["down C128", "up C64", "up C16"]
+        ["down C64", "down C128", "up C64", "up C16"]
     assert sum(t.startswith("bneck") for t in tags) == 23
+    monkeypatch.setenv("BUGSEG_INIT_FUSE", "1")
+    m.ctx.forward_bgr(bgr, B, H, W, N.OUT_CLASS3_U8, seg)
+    tags = [m.ctx.plan_op(B, H, W, i)[0] for i in range(n)]
+    assert tags[0] == "init+down C64" and tags[1] == "fused" and tags[2].startswith("bneck C64")
     x = ENET.preprocess_device(bgr, N.PRE_ENGINE, ctx=m.ctx, width=W, height=H)
     m.predict_device(x, N.OUT_CLASS3_U8)
     tags = [m.ctx.plan_op(B, H, W, i)[0] for i in range(n)]
