@@ -94,6 +94,11 @@ template <> struct BShape<64, 0> { static constexpr int TH = 16, TW = 16, NW = 4
 template <> struct BShape<64, 2> { static constexpr int TH = 8, TW = 16, NW = 4, OCC = 5, RP = 2, RD = 0, WIDE = 1; };
 template <> struct BShape<64, 1> { static constexpr int TH = 20, TW = 16, NW = 4, OCC = 5, RP = 3, RD = 0, WIDE = 1; };
 template <> struct BShape<16, 0> { static constexpr int TH = 16, TW = 16, NW = 4, OCC = 6, RP = 4, RD = 0, WIDE = 1; };
+// larger C = 16 tiles for the 240 x 320 stage-5 block (9,600 short 16 x 16 tiles at 32 frames): 32 x 16
+// and 16 x 32. Measured slower (round 3, fp16, B = 32: 56.9 / 56.6 vs 49.4-50.4 us per launch); the
+// runtime's cost model keeps 16 x 16, BUGSEG_BNECK_VARIANT_C16 forces one (A/B)
+template <> struct BShape<16, 1> { static constexpr int TH = 32, TW = 16, NW = 4, OCC = 6, RP = 4, RD = 0, WIDE = 1; };
+template <> struct BShape<16, 2> { static constexpr int TH = 16, TW = 32, NW = 4, OCC = 6, RP = 4, RD = 0, WIDE = 1; };
 
 // LDS strides (elements). bf16: a 16-lane group of ds_read_b128 (one 16-B k group of 16 pixels or
 // weight rows) is conflict-free when the row stride is 8, 24, 40 or 56 dwords mod 64 (the SQ counters
@@ -107,15 +112,17 @@ __host__ __device__ constexpr int bneck_pstr(int es, int IS, bool wide) {
 static bool bneck_wide(int C, int v, bool asym) {
 #define BW_CASE(CC, VV) if (C == CC && v == VV) return BShape<CC, VV>::WIDE && !asym;
     BW_CASE(128, 0) BW_CASE(128, 1) BW_CASE(128, 2) BW_CASE(128, 3) BW_CASE(128, 4) BW_CASE(64, 0) BW_CASE(64, 1) BW_CASE(64, 2) BW_CASE(16, 0)
+    BW_CASE(16, 1) BW_CASE(16, 2)
 #undef BW_CASE
     return false;
 }
 
-int bneck_variants(int C) { return C == 128 ? 5 : C == 64 ? 3 : 1; }
+int bneck_variants(int C) { return C == 128 ? 5 : 3; }
 
 void bneck_shape(int C, int v, int &th, int &tw, int &nw, int *rd) {
 #define BS_CASE(CC, VV) if (C == CC && v == VV) { th = BShape<CC, VV>::TH; tw = BShape<CC, VV>::TW; nw = BShape<CC, VV>::NW; if (rd) *rd = BShape<CC, VV>::RD; return; }
     BS_CASE(128, 0) BS_CASE(128, 1) BS_CASE(128, 2) BS_CASE(128, 3) BS_CASE(128, 4) BS_CASE(64, 0) BS_CASE(64, 1) BS_CASE(64, 2) BS_CASE(16, 0)
+    BS_CASE(16, 1) BS_CASE(16, 2)
 #undef BS_CASE
     th = tw = nw = 0;
     if (rd) *rd = 0;
@@ -1312,7 +1319,8 @@ template <typename T>
 static const void *kfun(int C, bool asym, int v, bool tr) {
 #define BK_CASE(CC, VV) \
     if (C == CC && v == VV && !tr) return asym ? (const void *)bneck_kernel<T, CC, true, VV, false> : (const void *)bneck_kernel<T, CC, false, VV, false>;
-    BK_CASE(128, 0) BK_CASE(128, 1) BK_CASE(128, 4) BK_CASE(64, 0) BK_CASE(64, 1) BK_CASE(64, 2) BK_CASE(16, 0)
+    BK_CASE(128, 0) BK_CASE(128, 1) BK_CASE(128, 4) BK_CASE(64, 0) BK_CASE(64, 1) BK_CASE(64, 2) BK_CASE(16, 0) BK_CASE(16, 1)
+    BK_CASE(16, 2)
 #undef BK_CASE
     if (C == 128 && v == 1 && tr && !asym) return (const void *)bneck_kernel<T, 128, false, 1, true>;
     if (C == 128 && v == 2 && !tr && !asym) return (const void *)bneck_kernel<T, 128, false, 2, false>;

@@ -639,6 +639,171 @@ __global__ void __launch_bounds__(256, 2) dl_gemm128_kernel(const DlConvArgs a) 
     }
 }
 
+// ------------------------------------------------------------------ 1x1 conv, 256 x 256 tiles
+// dl_gemm128_kernel's scheme on a 256-pixel x 256-channel tile: eight waves as 4 (pixels) x 2
+// (channels), each 64 pixels x 128 channels (acc[4][8]), k-stages of 64 channels by global_load_lds into
+// two LDS buffers of 64 KB each (one workgroup per CU, 2 waves per SIMD). Per stage and wave: 8 LDS-DMA
+// pieces and 24 ds_read_b128 for 64 MFMAs, where the 128 x 128 tile issues 8 pieces and 16 reads for
+// 32 — the DMA issue and the barriers, not the matrix pipe, bounded that kernel (0.24 of the dense
+// bf16 peak on Xception's pointwise layers). Same swizzle, same k order per output, same epilogue
+// (two 64-channel halves per wave): bit-identical to dl_gemm128_kernel / dl_gemm_kernel. Needs
+// NP % 256 == 0. Measured SLOWER (round 3, Xception-65 B = 32: pointwise 4.87 -> 5.27 ms per forward,
+// 597 -> 550 TFLOP/s; MobileNetV2 unchanged): with one workgroup per CU nothing overlaps a tile's
+// barriers, epilogue and first-stage latency, which the 128 x 128 tile's two co-resident workgroups
+// hide from each other, and 411 tiles on 256 CUs quantise to 2 rounds. Opt-in: BUGSEG_DL_G256=1.
+constexpr int G3_T = 256, G3_KT = 64;
+
+__device__ __forceinline__ void lds_wait12(u32x4 (&a)[8], u32x4 (&b)[4]) {
+    asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(a[0]), "+v"(a[1]), "+v"(a[2]), "+v"(a[3]), "+v"(a[4]), "+v"(a[5]),
+                 "+v"(a[6]), "+v"(a[7]), "+v"(b[0]), "+v"(b[1]), "+v"(b[2]), "+v"(b[3]));
+}
+
+template <bool OUTF32>
+__global__ void __launch_bounds__(512, 1) dl_gemm256_kernel(const DlConvArgs a) {
+    __shared__ __attribute__((aligned(16))) __bf16 sm0[2 * G3_T * G3_KT];   // [A | B][256][64]: 64 KB
+    __shared__ __attribute__((aligned(16))) __bf16 sm1[2 * G3_T * G3_KT];
+    const int tid = threadIdx.x, lane = tid & 63, col = lane & 15, kq = lane >> 4, wave = tid >> 6;
+    const int wm = wave & 3, wn = wave >> 2;
+    const int ntn = a.NP / G3_T;
+    const int bid = xcd_block(blockIdx.x, gridDim.x);
+    const int n0 = (bid % ntn) * G3_T, p0 = (bid / ntn) * G3_T;
+    const int K = a.cinP;
+    const __bf16 *wg = reinterpret_cast<const __bf16 *>(a.w), *xg = reinterpret_cast<const __bf16 *>(a.in);
+    // this lane's glds sources: instruction i fills LDS rows wave * 32 + i * 8 + (lane >> 3), slot lane & 7
+    const __bf16 *sa[4], *sb[4];
+    int kc[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+        const int r = wave * 32 + i * 8 + (lane >> 3);
+        kc[i] = ((lane & 7) ^ ((r >> 1) & 7)) * 8;
+        sa[i] = wg + (size_t)(n0 + r) * K;
+        sb[i] = xg + (size_t)min(p0 + r, a.M - 1) * a.CS;
+    }
+    auto stage = [&](int st, __bf16 *buf) {
+        const int k0 = st * G3_KT;
+        __bf16 *bA = buf + wave * 32 * G3_KT, *bB = bA + G3_T * G3_KT;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            const int k = k0 + kc[i];
+            glds16(sa[i] + (k < K ? k : 0), bA + i * 8 * G3_KT);
+            // channels past the stored CS read a zero chunk (weight row 0's padding columns k >= CS >= cin)
+            glds16(k < a.CS ? sb[i] + k : wg + k, bB + i * 8 * G3_KT);
+        }
+    };
+    f32x4 acc[4][8];
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+#pragma unroll
+        for (int r = 0; r < 8; ++r) acc[j][r] = (f32x4){0.f, 0.f, 0.f, 0.f};
+    auto compute = [&](int st, const __bf16 *bA) {
+        const __bf16 *bB = bA + G3_T * G3_KT;
+#pragma unroll
+        for (int s2 = 0; s2 < G3_KT / 32; ++s2) {
+            if (st * G3_KT + s2 * 32 >= K) break;              // (uniform) 32-channel tail stage
+            const int ch = s2 * 4 + kq;
+            u32x4 ra[8], rb[4];
+#pragma unroll
+            for (int r = 0; r < 8; ++r) {
+                const int row = wn * 128 + r * 16 + col;
+                ra[r] = lds_read16(bA + row * G3_KT + ((ch ^ ((row >> 1) & 7)) << 3));
+            }
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                const int row = wm * 64 + j * 16 + col;
+                rb[j] = lds_read16(bB + row * G3_KT + ((ch ^ ((row >> 1) & 7)) << 3));
+            }
+            lds_wait12(ra, rb);
+            RawB wa[8], bx[4];
+#pragma unroll
+            for (int r = 0; r < 8; ++r) wa[r].v = __builtin_bit_cast(uint4, ra[r]);
+#pragma unroll
+            for (int j = 0; j < 4; ++j) bx[j].v = __builtin_bit_cast(uint4, rb[j]);
+#pragma unroll
+            for (int j = 0; j < 4; ++j)
+#pragma unroll
+                for (int r = 0; r < 8; ++r) mma(acc[j][r], wa[r], bx[j]);
+        }
+    };
+    const int nst = (K + G3_KT - 1) / G3_KT;
+    stage(0, sm0);
+    for (int st = 0; st < nst; st += 2) {
+        if (st + 1 < nst) {
+            stage(st + 1, sm1);
+            asm volatile("s_waitcnt vmcnt(8)" ::: "memory");   // this wave's 8 loads of stage st landed
+        } else {
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        }
+        __builtin_amdgcn_s_barrier();                          // ... and every other wave's
+        compute(st, sm0);
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        __builtin_amdgcn_s_barrier();                          // sm0 may be refilled (stage st + 2)
+        if (st + 1 >= nst) break;
+        if (st + 2 < nst) {
+            stage(st + 2, sm0);
+            asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+        } else {
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        }
+        __builtin_amdgcn_s_barrier();
+        compute(st + 1, sm1);
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        __builtin_amdgcn_s_barrier();
+    }
+    // epilogue (dl_gemm128_kernel's per 64 channels), per wave: its 64 pixels x 128 channels as two
+    // 64-channel halves, 32 pixels at a time; four waves' 8.7 KB staging areas in each LDS object
+    static_assert(4 * 32 * DL_STG_RS * sizeof(float) <= sizeof(sm0), "epilogue staging must fit one LDS object");
+    float *stg = reinterpret_cast<float *>(wave < 4 ? sm0 : sm1) + (wave & 3) * 32 * DL_STG_RS;
+    const int c8 = (lane & 7) * 8;
+#pragma unroll
+    for (int hn = 0; hn < 2; ++hn) {
+        const int nb = n0 + wn * 128 + hn * 64;
+        const bool cok = nb + c8 < a.cout;
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+            if (h || hn) wave_lds_sync();
+#pragma unroll
+            for (int jj = 0; jj < 2; ++jj) {
+                const int j = 2 * h + jj;
+                const int p = p0 + wm * 64 + j * 16 + col;
+                const int pimg = a.bias_img ? (int)fdiv((uint32_t)(p < a.M ? p : 0), a.mHW, a.sHW) : 0;
+#pragma unroll
+                for (int r = 0; r < 4; ++r) {
+                    const int nl = r * 16 + kq * 4, n = nb + nl;
+                    float4 v = add4(f4(acc[j][hn * 4 + r]), ld4f(a.bias + n));
+                    if (a.bias_img) v = add4(v, ld4f(a.bias_img + (size_t)pimg * a.bias_img_stride + n));
+                    if (a.act >= 1) v = make_float4(fmaxf(v.x, 0.f), fmaxf(v.y, 0.f), fmaxf(v.z, 0.f), fmaxf(v.w, 0.f));
+                    if (a.act == 2) v = make_float4(fminf(v.x, 6.f), fminf(v.y, 6.f), fminf(v.z, 6.f), fminf(v.w, 6.f));
+                    *reinterpret_cast<float4 *>(stg + (jj * 16 + col) * DL_STG_RS + nl) = v;
+                }
+            }
+            wave_lds_sync();
+#pragma unroll
+            for (int it = 0; it < 4; ++it) {
+                const int pl = it * 8 + (lane >> 3);
+                const int p = p0 + wm * 64 + h * 32 + pl;
+                if (p >= a.M || !cok) continue;
+                float4 v0 = *reinterpret_cast<const float4 *>(stg + pl * DL_STG_RS + c8);
+                float4 v1 = *reinterpret_cast<const float4 *>(stg + pl * DL_STG_RS + c8 + 4);
+                const int n = nb + c8;
+                if (a.res) {
+                    const __bf16 *rp = reinterpret_cast<const __bf16 *>(a.res) + (size_t)p * a.res_cs + n;
+                    v0 = add4(v0, ld4(rp));
+                    v1 = add4(v1, ld4(rp + 4));
+                }
+                if constexpr (OUTF32) {
+                    float *o = reinterpret_cast<float *>(a.out) + (size_t)p * a.out_cs + a.out_off + n;
+                    st4(o, v0);
+                    st4(o + 4, v1);
+                } else {
+                    __bf16 *o = reinterpret_cast<__bf16 *>(a.out) + (size_t)p * a.out_cs + a.out_off + n;
+                    st4(o, v0);
+                    st4(o + 4, v1);
+                }
+            }
+        }
+    }
+}
+
 // ------------------------------------------------------------------ depthwise 3x3
 // One thread = one output pixel x 8 channels; threads with consecutive ids take consecutive channel
 // groups of the same pixel (coalesced 16-B loads). Weights [9][C] f32 (already rounded to T's
@@ -1053,8 +1218,21 @@ static bool gemm128_ok(const DlConvArgs &a) {
     return !(e && *e == '0') && a.cinP >= 256 && a.NP >= 256 && a.NP % 128 == 0 && a.CS % 8 == 0;
 }
 
+// the 256 x 256 tile (opt-in, BUGSEG_DL_G256=1: measured slower, see the kernel): the gemm128 shapes
+// whose output rows come in whole 256-row tiles
+static bool gemm256_ok(const DlConvArgs &a) {
+    const char *e = std::getenv("BUGSEG_DL_G256");
+    return e && *e == '1' && gemm128_ok(a) && a.NP % 256 == 0;
+}
+
 hipError_t dl_launch_conv(int prec, bool out_f32, const DlConvArgs &a, hipStream_t s) {
     const bool dwf = a.dw_w != nullptr;
+    if (gemm_ok(prec, a) && gemm256_ok(a)) {
+        const dim3 g(((a.M + G3_T - 1) / G3_T) * (a.NP / G3_T));
+        if (out_f32) hipLaunchKernelGGL(dl_gemm256_kernel<true>, g, dim3(512), 0, s, a);
+        else hipLaunchKernelGGL(dl_gemm256_kernel<false>, g, dim3(512), 0, s, a);
+        return hipGetLastError();
+    }
     if (gemm_ok(prec, a) && gemm128_ok(a)) {
         const dim3 g(((a.M + G2_T - 1) / G2_T) * ((a.NP + G2_T - 1) / G2_T));
         if (out_f32) hipLaunchKernelGGL(dl_gemm128_kernel<true>, g, dim3(256), 0, s, a);

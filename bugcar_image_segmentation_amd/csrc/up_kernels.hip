@@ -49,10 +49,10 @@ __global__ void __launch_bounds__(256, (sizeof(T) == 2 ? (CIN >= 128 ? 2 : 3) : 
     constexpr int UPAD = ES == 2 ? 16 : 16 / ES;
     constexpr int K1S = CIN + UPAD, K2S = 32 + UPAD, K3S = 32 + UPAD;
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-    T *w1 = reinterpret_cast<T *>(smem);
-    T *w2 = w1 + NR1 * 16 * K1S;
-    T *w3 = w2 + NR2 * 16 * K2S;
-    float *cb1 = reinterpret_cast<float *>(w3 + NR3 * 16 * K3S), *cs1 = cb1 + NR1 * 16;
+    T *w1s = reinterpret_cast<T *>(smem);
+    T *w2s = w1s + NR1 * 16 * K1S;
+    T *w3s = w2s + NR2 * 16 * K2S;
+    float *cb1 = reinterpret_cast<float *>(w3s + NR3 * 16 * K3S), *cs1 = cb1 + NR1 * 16;
     float *cb2 = cs1 + NR1 * 16, *cs2 = cb2 + NR2 * 16;
     float *cb3 = cs2 + NR2 * 16, *cs3 = cb3 + NR3 * 16, *cso = cs3 + NR3 * 16;
     const int tid = threadIdx.x;
@@ -65,9 +65,9 @@ __global__ void __launch_bounds__(256, (sizeof(T) == 2 ? (CIN >= 128 ? 2 : 3) : 
                 *reinterpret_cast<uint4 *>(reinterpret_cast<unsigned char *>(dst + (size_t)r * kstride) + c * 16) = s[i];
             }
         };
-        stage(w1, a.w1, NR1 * 16, CIN, K1S);           // pair pack: K = CIN exactly (1x1, CinS = CIN)
-        stage(w2, a.w2, NR2 * 16, 32, K2S);
-        stage(w3, a.w3, NR3 * 16, 32, K3S);
+        stage(w1s, a.w1, NR1 * 16, CIN, K1S);          // pair pack: K = CIN exactly (1x1, CinS = CIN)
+        stage(w2s, a.w2, NR2 * 16, 32, K2S);
+        stage(w3s, a.w3, NR3 * 16, 32, K3S);
         for (int i = tid; i < NR1 * 16; i += 256) { cb1[i] = a.b1[i]; cs1[i] = a.s1[i]; }
         for (int i = tid; i < NR2 * 16; i += 256) { cb2[i] = a.b2[i]; cs2[i] = a.s2[i]; }
         for (int i = tid; i < NR3 * 16; i += 256) { cb3[i] = a.b3[i]; cs3[i] = a.s3[i]; cso[i] = a.s_out[i]; }
@@ -99,6 +99,13 @@ __global__ void __launch_bounds__(256, (sizeof(T) == 2 ? (CIN >= 128 ? 2 : 3) : 
     };
     if (gw < nfrag) load(gw);
     for (int f = gw; f < nfrag; f += nw) {
+        // an opaque per-fragment offset keeps the weight fragments' LDS reads inside the loop for the
+        // CIN = 128 form (hoisted, all 24 of GEMM 1's A fragments sat in registers: 226 VGPRs, 2 waves
+        // per SIMD; in the loop 96 VGPRs, 3 per SIMD by LDS): up C64 37.8 -> 36.5 us per 32-frame
+        // launch (round 3, fp16); the CIN = 64 form measured 35.1 -> 36.1 with it, so it keeps them hoisted
+        int wofs = 0;
+        if constexpr (CIN >= 128) asm volatile("" : "+v"(wofs));
+        const T *w1 = w1s + wofs, *w2 = w2s + wofs, *w3 = w3s + wofs;
         const int p = f * 16 + col;
         const bool pv = p < a.M;
         const uint32_t pp = pv ? (uint32_t)p : 0u;
