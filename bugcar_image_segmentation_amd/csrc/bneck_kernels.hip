@@ -143,8 +143,13 @@ void bneck_shape(int C, int v, int &th, int &tw, int &nw, int *rd) {
 // CU, where the initial block's LDS-latency-bound arithmetic needs the 6-8 waves per SIMD its own
 // kernel runs at; a BGR-order patch (8-B LDS stores instead of 2-B ones) changes the initial conv's
 // MFMA k order, so it is no longer bit-identical. Opt-in (BUGSEG_INIT_FUSE=1, bugseg_runtime.cpp).
+// fp32 (parity mode): registers unconstrained (LDS bounds the C = 64 / 128 forms first), except C = 16,
+// held to 5 waves per SIMD (unconstrained it took 16 AGPRs on top of 91 VGPRs: 4; LDS allows 5)
+#ifndef BNECK_F32_OCC16
+#define BNECK_F32_OCC16 5
+#endif
 template <typename T, int C, bool ASYM, int V, bool TR, int CI = 0, bool INI = false>
-__global__ void __launch_bounds__((BShape<C, V>::NW * 64), (sizeof(T) == 2 ? (INI ? 3 : BShape<C, V>::OCC) : 1)) bneck_kernel(const BneckArgs a) {
+__global__ void __launch_bounds__((BShape<C, V>::NW * 64), (sizeof(T) == 2 ? (INI ? 3 : BShape<C, V>::OCC) : C == 16 ? BNECK_F32_OCC16 : 1)) bneck_kernel(const BneckArgs a) {
     using Raw = typename Tr<T>::Raw;
     constexpr int TH = BShape<C, V>::TH, TW = BShape<C, V>::TW, NW = BShape<C, V>::NW, NT = NW * 64;
     constexpr int I = CI > 0 ? CI / 4 : C / 4;      // internal channels (ENet: input / 4)

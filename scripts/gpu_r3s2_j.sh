@@ -1,0 +1,9 @@
+#!/bin/bash
+# round 3 session 2: parity of the touched forms, then the round profiles (fp16 headline + fp32)
+set -o pipefail
+cd "$GRAFT_REPO_ROOT" || exit 1
+mkdir -p gpurun_out/r3s2j
+export TMPDIR=/tmp
+timeout -k 10 400 python -u -m pytest tests/test_gpu_parity.py -k "fp32 or fused_bottlenecks_equal" -m gpu -x -q --timeout 240 --timeout-method thread > gpurun_out/r3s2j/tests.log 2>&1 || { echo "tests failed"; tail -40 gpurun_out/r3s2j/tests.log; exit 1; }
+tail -1 gpurun_out/r3s2j/tests.log
+TAG=r03_b bash scripts/gpu_r3_prof.sh || exit 1
