@@ -396,7 +396,10 @@ def main():
     if ndev == 0:
         raise RuntimeError("bench.py needs a HIP GPU")
     local = local % ndev
-    if world > 1:
+    # the process-group branch runs whenever the job has a process group: N > 1, or a 1-rank job
+    # started by torch.distributed.run (the RCCL path exercised on a one-GPU box)
+    dist_on = world > 1 or "TORCHELASTIC_RUN_ID" in os.environ
+    if dist_on:
         if a.backend == "nccl":
             dist.init_process_group("nccl", device_id=torch.device("cuda", local))
         else:
@@ -427,7 +430,7 @@ def main():
 
     def step():
         g = run()
-        if world > 1:
+        if dist_on:
             gather_grids(g, B * world)
         return g
 
@@ -436,7 +439,7 @@ def main():
         step()
     torch.cuda.synchronize()
     gather_check = None
-    if world > 1:
+    if dist_on:
         # outside the timed region: the all-gathered batch holds every rank's grids in rank order
         local_g = run().clone()
         full = gather_grids(local_g, B * world)
@@ -448,17 +451,17 @@ def main():
         if not gather_check:
             raise RuntimeError("all-gathered occupancy grids do not hold the ranks' own grids")
         torch.cuda.synchronize()
-    if world > 1:
+    if dist_on:
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     for _ in range(a.steps):
         step()
     torch.cuda.synchronize()
-    if world > 1:
+    if dist_on:
         dist.barrier()
     el = time.perf_counter() - t0
-    if world > 1:
+    if dist_on:
         t = torch.tensor([el], dtype=torch.float64, device=dev if a.backend == "nccl" else "cpu")
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         el = float(t.item())
@@ -514,10 +517,10 @@ def main():
             "config": {"workload": f"config3/5: ENet {W}x{H} batch {B} per GPU, preprocess + forward + argmax/LUT + "
                                    f"fused BEV warp/occgrid (1000x1000 BEV -> 200x200 cells)",
                        "global_batch": B * world, "per_gpu_batch": B, "height": H, "width": W,
-                       "parallelism": f"frame-sharded dp{world}" + (" + RCCL all-gather of grids" if world > 1 else ""),
+                       "parallelism": f"frame-sharded dp{world}" + (" + RCCL all-gather of grids" if dist_on and a.backend == "nccl" else ""),
                        "streams_per_gpu": a.streams, "hip_graph": bool(a.graph), "shard_offset": a.shard_offset,
                        **({"backend": "rccl" if a.backend == "nccl" else "gloo (functional run, not a timing)",
-                           "gather_check": gather_check} if world > 1 else {})},
+                           "gather_check": gather_check} if dist_on else {})},
             "roofline": roof,
             "kernels": ktable,
             "stages_ms": {"frames": Bs, "enet_forward": round(t_fwd, 4), "bev_occgrid": round(t_bev, 4),
@@ -546,7 +549,7 @@ def main():
         if not a.no_cpu_baseline and world == 1:   # the CPU baseline is an N = 1 record (rank 0)
             res["cpu_baseline"] = cpu_baseline(blocks, bev, grid, H, W, a.cpu_baseline_seconds)
         print(json.dumps(res), flush=True)
-    if world > 1:
+    if dist_on:
         dist.barrier()
         dist.destroy_process_group()
 

@@ -195,6 +195,11 @@ __global__ void __launch_bounds__((BShape<C, V>::NW * 64), (sizeof(T) == 2 ? (IN
 #ifndef BNECK_REG3_C64
 #define BNECK_REG3_C64 0
 #endif
+// fp32 (parity mode) C = 64 with the register epilogue: no staging region, so the LDS footprint is the
+// halo's (8 x 16 tile: 42.7 -> 39.7 KB, 3 -> 4 workgroups per CU); its quads are 16-B chunks already
+#ifndef BNECK_REG3_C64_F32
+#define BNECK_REG3_C64_F32 0
+#endif
 #ifndef BNECK_CH1_C64
 #define BNECK_CH1_C64 6   // the symmetric 16x16 C64 form: all of a wave's 5-6 phase-1 fragments in one round trip (37.3 -> 36.0 us)
 #endif
@@ -209,7 +214,7 @@ __global__ void __launch_bounds__((BShape<C, V>::NW * 64), (sizeof(T) == 2 ? (IN
     // pixels would be written as half lines by the register layout, which measured slower there
     // (44.7 vs 43.0 us per launch with t1 in registers).
     // (the down form's C = 64 launch measured faster with the register epilogue: 53 vs 55 us)
-    constexpr bool REG3 = C != 64 || DN || BNECK_REG3_C64;
+    constexpr bool REG3 = C != 64 || DN || BNECK_REG3_C64 || (sizeof(T) == 4 && BNECK_REG3_C64_F32);
     constexpr bool SWAP = REG3 && sizeof(T) == 2 && NR3 % 2 == 0;
     constexpr bool HALF = REG3 && sizeof(T) == 2 && NR3 % 2 != 0;
     constexpr int EPC = 16 / (int)sizeof(T);          // elements per 16-B chunk
@@ -1313,7 +1318,8 @@ size_t bneck_lds_bytes(int prec, int C, bool asym, int v, int cin, bool ini) {
     const size_t wts = (size_t)NR1 * 16 * (KS1 * 32 + padw) + (size_t)NR1 * 16 * (KS2 * 32 + padw) * (asym ? 2 : 1) +
                        (size_t)C * (32 + padw);
     const size_t halo = (size_t)(TH + 2 * R) * (TW + 2 * RX) * bneck_pstr(es, IS, wide);
-    const size_t stage = C == 64 && !BNECK_REG3_C64 ? (size_t)NW * 16 * (C + pad) : 0;    // staged epilogue (REG3 off)
+    const bool staged = C == 64 && !BNECK_REG3_C64 && !(es == 4 && BNECK_REG3_C64_F32);
+    const size_t stage = staged ? (size_t)NW * 16 * (C + pad) : 0;    // staged epilogue (REG3 off)
     const size_t consts = ((size_t)6 * NR1 * 16 + 3 * (size_t)C) * sizeof(float);
     if (ini) return (wts + 16 + halo + ipatch) * es + consts;          // (INI: REG3, no staging)
     return (wts + 16 + (halo > stage ? halo : stage)) * es + consts;   // + the zero pad

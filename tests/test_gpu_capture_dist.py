@@ -177,3 +177,25 @@ def test_bench_distributed_branch_gloo_one_gpu(gpu):
     print(json.dumps({k: line[k] for k in ("value", "n_gpus", "ms_per_step", "config")}))
     assert line["config"]["global_batch"] == 8 and line["config"]["gather_check"] is True
     assert line["n_gpus"] == 1 and line["value"] > 0
+
+
+@pytest.mark.timeout(240)
+def test_bench_rccl_branch_one_rank(gpu):
+    """bench.py's process-group branch on RCCL (backend nccl: init_process_group with the device id,
+    the in-step all_gather_into_tensor of the grids, the all-reduced gathered-grid check and the
+    MAX all-reduce of the elapsed time, all on GPU tensors) run by torch.distributed.run as a 1-rank
+    job on this one GPU. Two ranks cannot share a GPU under RCCL; this is the N = 8 product path's
+    code, executed end to end with a world of one."""
+    port = _free_port()
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "1",
+           "--master-addr", "127.0.0.1", "--master-port", str(port), "bench.py", "--gpus", "1",
+           "--backend", "nccl", "--steps", "3", "--warmup", "1", "--batch", "4", "--height", "96", "--width", "128",
+           "--extras", "0", "--no-cpu-baseline"]
+    env = dict(os.environ, HSA_ENABLE_IPC_MODE_LEGACY=os.environ.get("HSA_ENABLE_IPC_MODE_LEGACY", "0"))
+    r = subprocess.run(cmd, cwd=ROOT, capture_output=True, text=True, timeout=220, env=env)
+    assert r.returncode == 0, r.stderr[-3000:]
+    line = json.loads([ln for ln in r.stdout.splitlines() if ln.startswith("{")][-1])
+    print(json.dumps({k: line[k] for k in ("value", "n_gpus", "ms_per_step", "config")}))
+    assert line["config"]["backend"] == "rccl" and line["config"]["gather_check"] is True
+    assert "RCCL all-gather" in line["config"]["parallelism"]
+    assert line["n_gpus"] == 1 and line["value"] > 0
