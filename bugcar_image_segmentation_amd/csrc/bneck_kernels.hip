@@ -196,9 +196,16 @@ __global__ void __launch_bounds__((BShape<C, V>::NW * 64), (sizeof(T) == 2 ? (IN
 #define BNECK_REG3_C64 0
 #endif
 // fp32 (parity mode) C = 64 with the register epilogue: no staging region, so the LDS footprint is the
-// halo's (8 x 16 tile: 42.7 -> 39.7 KB, 3 -> 4 workgroups per CU); its quads are 16-B chunks already
+// halo's (8 x 16 tile: 42.7 -> 39.7 KB, 3 -> 4 workgroups per CU); its quads are 16-B chunks already.
+// Measured slower (round 3: 94.1 -> 104.7 us per launch: a pixel's 256 B leave as four 64-B pieces)
 #ifndef BNECK_REG3_C64_F32
 #define BNECK_REG3_C64_F32 0
+#endif
+// fp32 C = 64: the staged epilogue one 32-channel half at a time (HSTG below). Measured (round 3, fp32,
+// B = 32): the 8 x 16 form 94.2 -> 89.4 us per launch (3 -> 4 workgroups per CU), fp32 bench
+// 13,890 -> 14,065-14,095 frames/s; bit-identical (GPU-tested)
+#ifndef BNECK_F32_HSTG
+#define BNECK_F32_HSTG 1
 #endif
 #ifndef BNECK_CH1_C64
 #define BNECK_CH1_C64 6   // the symmetric 16x16 C64 form: all of a wave's 5-6 phase-1 fragments in one round trip (37.3 -> 36.0 us)
@@ -221,7 +228,11 @@ __global__ void __launch_bounds__((BShape<C, V>::NW * 64), (sizeof(T) == 2 ? (IN
     constexpr int CPP = C / EPC;                      // 16-B chunks per pixel
     constexpr int CPF = 16 * CPP;                     // (staged) 16-B chunks of one 16-pixel fragment
     constexpr int CPL = (CPF + 63) / 64;              // ... per lane
-    constexpr int OSTR = C + EPC;                     // staged epilogue: row stride (16-B padded)
+    // HSTG (fp32 C = 64, staged epilogue): the fragment is staged one 32-channel half at a time — a
+    // pixel's half is 128 B, one whole line, so the stores stay full-line while the staging region
+    // halves (the 8 x 16 tile: 42.7 -> 39.7 KB of LDS, 3 -> 4 workgroups per CU)
+    constexpr bool HSTG = !REG3 && sizeof(T) == 4 && C == 64 && BNECK_F32_HSTG;
+    constexpr int OSTR = (HSTG ? C / 2 : C) + EPC;    // staged epilogue: row stride (16-B padded)
     constexpr int RQ3 = !REG3 ? CPL : SWAP ? NR3 / 2 : NR3;   // residual chunks per lane per fragment
     static_assert(TW % 16 == 0, "a fragment is a run of one tile row");
 #ifndef BNECK_NBE
@@ -964,16 +975,20 @@ __global__ void __launch_bounds__((BShape<C, V>::NW * 64), (sizeof(T) == 2 ? (IN
         // passes' live ranges apart); phase 3 refills the ring as it consumes it.
         constexpr int RP = BShape<C, V>::RP < NF2 ? BShape<C, V>::RP : NF2;
         uint4 res[RP][RQ3];
+        // staged epilogue: lane chunk k of a fragment is channel chunk sc_ch(k) of its pixel sc_px(k)
+        // (coalesced 16-B loads and stores); HSTG: chunks 0 .. CPL/2 - 1 are the first 32-channel half
+        auto sc_q = [&](int k) -> int { return HSTG ? lane + 64 * (k % (CPL / 2)) : lane + 64 * k; };
+        auto sc_px = [&](int k) -> int { return HSTG ? sc_q(k) / (CPP / 2) : sc_q(k) / CPP; };
+        auto sc_ch = [&](int k) -> int {
+            return HSTG ? (k / (CPL / 2)) * (CPP / 2) + sc_q(k) % (CPP / 2) : sc_q(k) % CPP;
+        };
         auto load_res = [&](int j, uint4 (&r)[RQ3]) {
             if constexpr (!REG3) {
-                // staged epilogue: lane chunk q of fragment f is channel chunk q % CPP of its pixel
-                // q / CPP (coalesced 16-B loads)
                 const int f = wave + NW * j;
 #pragma unroll
                 for (int k = 0; k < CPL; ++k) {
-                    const int q = lane + 64 * k;
-                    const uint32_t off = res_off(f, q / CPP, (q % CPP) * EPC);
-                    r[k] = bld16(rrb, q < CPF ? off : OOB);
+                    const uint32_t off = res_off(f, sc_px(k), sc_ch(k) * EPC);
+                    r[k] = bld16(rrb, HSTG || sc_q(k) < CPF ? off : OOB);
                 }
                 return;
             }
@@ -1176,6 +1191,46 @@ __global__ void __launch_bounds__((BShape<C, V>::NW * 64), (sizeof(T) == 2 ? (IN
             __syncthreads();
             STAMP(5);
             T *stg = ts + wave * 16 * OSTR;
+            if constexpr (HSTG) {
+                static_assert(!KEEP && CPL % 2 == 0 && NR3 % 2 == 0, "half staging: fp32 C = 64");
+#pragma unroll
+                for (int j = 0; j < NF2; ++j) {
+                    if (wave + NW * j >= NFT) break;      // wave-uniform
+#pragma unroll
+                    for (int h = 0; h < 2; ++h) {
+#pragma unroll
+                        for (int kk = 0; kk < CPL / 2; ++kk) {
+                            const int k = h * (CPL / 2) + kk;
+                            *reinterpret_cast<uint4 *>(stg + sc_px(k) * OSTR + (sc_ch(k) - h * (CPP / 2)) * EPC) = res[j % RP][k];
+                        }
+                        if (h == 1 && j + RP < NF2 && wave + NW * (j + RP) < NFT) load_res(j + RP, res[j % RP]);
+                        wave_lds_sync();
+#pragma unroll
+                        for (int rr = 0; rr < NR3 / 2; ++rr) {
+                            const int r = h * (NR3 / 2) + rr;
+                            const int ch = r * 16 + kq * 4;
+                            f32x4 acc = bias_in_acc(NR3, 1) ? bias4(cb3 + ch) : (f32x4){0.f, 0.f, 0.f, 0.f};
+                            Raw wf;
+                            ld8(wf, w3 + (r * 16 + col) * K3S + kq * 8);
+                            mma(acc, wf, tf[j]);
+                            T *sp = stg + col * OSTR + (ch - h * (C / 2));
+                            float4 v = act(bias_in_acc(NR3, 1) ? f4(acc) : add4(f4(acc), ld4f(cb3 + ch)), cs3 + ch);
+                            v = act(add4(v, ld4(sp)), cso + ch);
+                            st4(sp, v);
+                        }
+                        wave_lds_sync();
+#pragma unroll
+                        for (int kk = 0; kk < CPL / 2; ++kk) {
+                            const int k = h * (CPL / 2) + kk;
+                            const uint32_t off = pix_off(wave + NW * j, sc_px(k), sc_ch(k) * EPC);
+                            bst16o<OAUX>(rob, off, *reinterpret_cast<const uint4 *>(stg + sc_px(k) * OSTR + (sc_ch(k) - h * (CPP / 2)) * EPC));
+                        }
+                        wave_lds_sync();
+                    }
+                }
+                STAMP(6);
+                continue;
+            }
 #pragma unroll
             for (int j = 0; j < NF2; ++j) {
                 if (wave + NW * j >= NFT) break;          // wave-uniform
@@ -1319,7 +1374,8 @@ size_t bneck_lds_bytes(int prec, int C, bool asym, int v, int cin, bool ini) {
                        (size_t)C * (32 + padw);
     const size_t halo = (size_t)(TH + 2 * R) * (TW + 2 * RX) * bneck_pstr(es, IS, wide);
     const bool staged = C == 64 && !BNECK_REG3_C64 && !(es == 4 && BNECK_REG3_C64_F32);
-    const size_t stage = staged ? (size_t)NW * 16 * (C + pad) : 0;    // staged epilogue (REG3 off)
+    const bool hstg = staged && es == 4 && BNECK_F32_HSTG;            // fp32 C = 64: one 32-channel half at a time
+    const size_t stage = staged ? (size_t)NW * 16 * ((hstg ? C / 2 : C) + pad) : 0;    // staged epilogue (REG3 off)
     const size_t consts = ((size_t)6 * NR1 * 16 + 3 * (size_t)C) * sizeof(float);
     if (ini) return (wts + 16 + halo + ipatch) * es + consts;          // (INI: REG3, no staging)
     return (wts + 16 + (halo > stage ? halo : stage)) * es + consts;   // + the zero pad
