@@ -261,6 +261,10 @@ __global__ void __launch_bounds__(256, sizeof(T) == 2 ? 4 : 1) cls_kernel(const 
 // lane-swap rounds (v_permlane16_swap / v_permlane32_swap). A wave step is 16 input pixels (lane col);
 // lane kq holds channels 4 kq .. 4 kq + 3 of each tap (one 16-B load per tap); sub-MFMA j contracts
 // channels {4 kq + j}. Same argmax semantics as cls_kernel (NaN-ignoring maximum, its lowest index).
+// Measured SLOWER (round 3, fp32, B = 32 at 480 x 640): 159.6 vs 141.5-142.0 us per launch — 9 of 12
+// products, but 16-pixel steps (twice the per-pixel load / address / store work of the 32 x 32 form)
+// and the two swap rounds per phase; the fp32 bench 14,040-14,073 vs 14,107-14,117 frames/s. Opt-in
+// (BUGSEG_CLS16=1), GPU-tested against the 32 x 32 form.
 template <bool LOGITS>
 __global__ void __launch_bounds__(256, 2) cls16_kernel(const ConvArgs a) {
     constexpr int TAPS = 4, PH = 4;
@@ -324,7 +328,9 @@ __global__ void __launch_bounds__(256, 2) cls16_kernel(const ConvArgs a) {
     };
     // the 4-lane reductions: the value of lane l ^ 16 / l ^ 32
     auto x16 = [&](uint32_t v) -> uint32_t { uint32_t p = v, q = v; pl16swap(p, q); return (kq & 1) ? p : q; };
-    auto x32 = [&](uint32_t v) -> uint32_t { uint32_t p = v, q = v; pl32swap(p, q); return kq < 2 ? p : q; };
+    // (v_permlane16_swap: odd rows of the first operand <-> even rows of the second; v_permlane32_swap:
+    // upper half of the first <-> lower half of the second)
+    auto x32 = [&](uint32_t v) -> uint32_t { uint32_t p = v, q = v; pl32swap(p, q); return kq < 2 ? q : p; };
     auto step = [&](int g, const float4 (&cur)[TAPS], float4 (&nxt)[TAPS]) {
         load(g + nw, nxt);
         const Px q = pixel(g);
@@ -384,10 +390,10 @@ bool cls_supported(const ConvArgs &a) {
            a.Hout == 2 * a.Hg && a.Wout == 2 * a.Wg && a.Hg == a.Hin && a.Wg == a.Win;
 }
 
-// the fp32 16 x 16 form (cls16_kernel): BUGSEG_CLS16=0 keeps the 32 x 32 one (read per launch: A/B, tests)
+// the fp32 16 x 16 form (cls16_kernel, measured slower): BUGSEG_CLS16=1 (read per launch: A/B, tests)
 static bool cls16_on() {
     const char *e = std::getenv("BUGSEG_CLS16");
-    return !(e && *e == '0');
+    return e && *e == '1';
 }
 
 hipError_t launch_cls(int prec, const ConvArgs &a, hipStream_t s) {
