@@ -99,6 +99,10 @@ template <> struct BShape<16, 0> { static constexpr int TH = 16, TW = 16, NW = 4
 // runtime's cost model keeps 16 x 16, BUGSEG_BNECK_VARIANT_C16 forces one (A/B)
 template <> struct BShape<16, 1> { static constexpr int TH = 32, TW = 16, NW = 4, OCC = 6, RP = 4, RD = 0, WIDE = 1; };
 template <> struct BShape<16, 2> { static constexpr int TH = 16, TW = 32, NW = 4, OCC = 6, RP = 4, RD = 0, WIDE = 1; };
+// 20 x 16: 7,680 tiles at 32 frames, 5 whole rounds of the 1,536 resident slots (16 x 16: 9,600 tiles,
+// 6.25 rounds -> 7); the cost model picks it. Measured (round 3, fp16, B = 32): 48.0-48.4 vs 48.6-48.8 us
+// per launch — equal within noise: the stage-5 block is not round-quantisation bound
+template <> struct BShape<16, 3> { static constexpr int TH = 20, TW = 16, NW = 4, OCC = 6, RP = 4, RD = 0, WIDE = 1; };
 
 // LDS strides (elements). bf16: a 16-lane group of ds_read_b128 (one 16-B k group of 16 pixels or
 // weight rows) is conflict-free when the row stride is 8, 24, 40 or 56 dwords mod 64 (the SQ counters
@@ -112,17 +116,17 @@ __host__ __device__ constexpr int bneck_pstr(int es, int IS, bool wide) {
 static bool bneck_wide(int C, int v, bool asym) {
 #define BW_CASE(CC, VV) if (C == CC && v == VV) return BShape<CC, VV>::WIDE && !asym;
     BW_CASE(128, 0) BW_CASE(128, 1) BW_CASE(128, 2) BW_CASE(128, 3) BW_CASE(128, 4) BW_CASE(64, 0) BW_CASE(64, 1) BW_CASE(64, 2) BW_CASE(16, 0)
-    BW_CASE(16, 1) BW_CASE(16, 2)
+    BW_CASE(16, 1) BW_CASE(16, 2) BW_CASE(16, 3)
 #undef BW_CASE
     return false;
 }
 
-int bneck_variants(int C) { return C == 128 ? 5 : 3; }
+int bneck_variants(int C) { return C == 128 ? 5 : C == 16 ? 4 : 3; }
 
 void bneck_shape(int C, int v, int &th, int &tw, int &nw, int *rd) {
 #define BS_CASE(CC, VV) if (C == CC && v == VV) { th = BShape<CC, VV>::TH; tw = BShape<CC, VV>::TW; nw = BShape<CC, VV>::NW; if (rd) *rd = BShape<CC, VV>::RD; return; }
     BS_CASE(128, 0) BS_CASE(128, 1) BS_CASE(128, 2) BS_CASE(128, 3) BS_CASE(128, 4) BS_CASE(64, 0) BS_CASE(64, 1) BS_CASE(64, 2) BS_CASE(16, 0)
-    BS_CASE(16, 1) BS_CASE(16, 2)
+    BS_CASE(16, 1) BS_CASE(16, 2) BS_CASE(16, 3)
 #undef BS_CASE
     th = tw = nw = 0;
     if (rd) *rd = 0;
@@ -1389,6 +1393,9 @@ static const void *kfun(int C, bool asym, int v, bool tr) {
     BK_CASE(128, 0) BK_CASE(128, 1) BK_CASE(128, 4) BK_CASE(64, 0) BK_CASE(64, 1) BK_CASE(64, 2) BK_CASE(16, 0) BK_CASE(16, 1)
     BK_CASE(16, 2)
 #undef BK_CASE
+    // (2-byte storage only: the fp32 instance spills 9 VGPRs)
+    if constexpr (sizeof(T) == 2)
+        if (C == 16 && v == 3 && !tr) return asym ? nullptr : (const void *)bneck_kernel<T, 16, false, 3, false>;
     if (C == 128 && v == 1 && tr && !asym) return (const void *)bneck_kernel<T, 128, false, 1, true>;
     if (C == 128 && v == 2 && !tr && !asym) return (const void *)bneck_kernel<T, 128, false, 2, false>;
     if (C == 128 && v == 3 && !tr && !asym) return (const void *)bneck_kernel<T, 128, false, 3, false>;

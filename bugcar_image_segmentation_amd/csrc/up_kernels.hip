@@ -25,6 +25,10 @@
 namespace bugseg {
 
 
+#ifndef UP_SWZ
+#define UP_SWZ 0
+#endif
+
 template <typename T, int CIN, int I, int COUT>
 __global__ void __launch_bounds__(256, (sizeof(T) == 2 ? (CIN >= 128 ? 2 : 3) : 1)) up_kernel(const UpArgs a) {
     using Raw = typename Tr<T>::Raw;
@@ -46,8 +50,20 @@ __global__ void __launch_bounds__(256, (sizeof(T) == 2 ? (CIN >= 128 ? 2 : 3) : 
     // LDS: weights of the three GEMMs (+16 B row pad) and their per-row constants
     // row pads: bf16 16 elements (row strides 8 / 24 / 40 dwords mod 64: conflict-free ds_read_b128
     // groups, bneck_kernels.hip bneck_padw), fp32 16 B
-    constexpr int UPAD = ES == 2 ? 16 : 16 / ES;
+    // SWZ (2-byte storage, CIN = 128): unpadded weight rows with the 16-B chunks XOR-swizzled per row
+    // instead of the row pads: 47 -> 39 KB of LDS, 3 -> 4 workgroups per CU. Measured (round 3, fp16,
+    // B = 32): up C64 36.0-36.4 -> 34.9-35.2 us per launch, the 2-stream bench within noise (41.7-41.8k
+    // vs 41.9-42.0k frames/s): opt-in (-DUP_SWZ=1), bit-identical (GPU-tested)
+    constexpr bool SWZ = UP_SWZ && ES == 2 && CIN == 128;
+    constexpr int UPAD = SWZ ? 0 : ES == 2 ? 16 : 16 / ES;
     constexpr int K1S = CIN + UPAD, K2S = 32 + UPAD, K3S = 32 + UPAD;
+    // element offset of the 8-element chunk c of weight row r (a lane's fragment read): a ds_read_b128 lane group reads 16 rows
+    // (lane col) at one chunk; 256-B rows (K = 128): chunk ^ (row & 15); 64-B rows (K = 32):
+    // chunk ^ g((row >> 2) & 3), g = (0, 2, 3, 1) — 16 distinct bank slots per group either way
+    auto wch = [](int r, int c, int k) -> int {
+        if constexpr (!SWZ) return c * 8;
+        else return (k == 128 ? c ^ (r & 15) : c ^ ((0x78 >> (2 * ((r >> 2) & 3))) & 3)) * 8;
+    };
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     T *w1s = reinterpret_cast<T *>(smem);
     T *w2s = w1s + NR1 * 16 * K1S;
@@ -62,7 +78,8 @@ __global__ void __launch_bounds__(256, (sizeof(T) == 2 ? (CIN >= 128 ? 2 : 3) : 
             const uint4 *s = reinterpret_cast<const uint4 *>(src);
             for (int i = tid; i < rows * cpr; i += 256) {
                 const int r = i / cpr, c = i - r * cpr;
-                *reinterpret_cast<uint4 *>(reinterpret_cast<unsigned char *>(dst + (size_t)r * kstride) + c * 16) = s[i];
+                // (c counts 16-B chunks: 8 elements in 2-byte storage, 4 in fp32, where nothing is swizzled)
+                *reinterpret_cast<uint4 *>(dst + (size_t)r * kstride + (SWZ ? wch(r, c, kpad) : c * (16 / ES))) = s[i];
             }
         };
         stage(w1s, a.w1, NR1 * 16, CIN, K1S);          // pair pack: K = CIN exactly (1x1, CinS = CIN)
@@ -128,7 +145,7 @@ __global__ void __launch_bounds__(256, (sizeof(T) == 2 ? (CIN >= 128 ? 2 : 3) : 
 #pragma unroll
             for (int r = 0; r < NR1; ++r) {
                 Raw wf;
-                ld8(wf, w1 + (r * 16 + col) * K1S + s * 32 + kq * 8);
+                ld8(wf, w1 + (r * 16 + col) * K1S + wch(col, s * 4 + kq, CIN));
                 mma(acc1[r], wf, xf[s]);
             }
         auto ep1 = [&](int r) {
@@ -152,7 +169,7 @@ __global__ void __launch_bounds__(256, (sizeof(T) == 2 ? (CIN >= 128 ? 2 : 3) : 
                 const int r2 = ph * NE + e;
                 acc2[e] = B2ACC ? bias4(cb2 + r2 * 16 + kq * 4) : (f32x4){0.f, 0.f, 0.f, 0.f};
                 Raw wf;
-                ld8(wf, w2 + (r2 * 16 + col) * K2S + kq * 8);
+                ld8(wf, w2 + (r2 * 16 + col) * K2S + wch(col, kq, 32));
                 mma(acc2[e], wf, bop2);
             }
             auto ep2 = [&](int e) {
@@ -166,7 +183,7 @@ __global__ void __launch_bounds__(256, (sizeof(T) == 2 ? (CIN >= 128 ? 2 : 3) : 
                 const int c = r * 16 + kq * 4;
                 f32x4 acc = B3ACC ? bias4(cb3 + c) : (f32x4){0.f, 0.f, 0.f, 0.f};
                 Raw wf;
-                ld8(wf, w3 + (r * 16 + col) * K3S + kq * 8);
+                ld8(wf, w3 + (r * 16 + col) * K3S + wch(col, kq, 32));
                 mma(acc, wf, bop3);
                 float4 v = act(B3ACC ? f4(acc) : add4(f4(acc), ld4f(cb3 + c)), cs3 + c);
                 // MaxUnpool2d(2): the main value lands where its pooling index points
@@ -205,7 +222,7 @@ template <typename T, int CIN, int I, int COUT>
 static size_t up_lds() {
     constexpr int ES = (int)sizeof(T);
     constexpr int NR1 = (COUT + I) / 16, NR2 = 4 * I / 16, NR3 = COUT / 16;
-    constexpr int UPAD = ES == 2 ? 16 : 16 / ES;      // = up_kernel's
+    constexpr int UPAD = UP_SWZ && ES == 2 && CIN == 128 ? 0 : ES == 2 ? 16 : 16 / ES;      // = up_kernel's
     return (size_t)(NR1 * 16 * (CIN + UPAD) + NR2 * 16 * (32 + UPAD) + NR3 * 16 * (32 + UPAD)) * ES +
            (size_t)(2 * NR1 * 16 + 2 * NR2 * 16 + 3 * NR3 * 16) * sizeof(float);
 }
