@@ -106,7 +106,9 @@ def parse():
                    help="1: shard i's forward starts after shard i-1's (its BEV overlaps the next forward)")
     p.add_argument("--shard-offset", type=int, default=0,
                    help="k > 0: shard i+1 starts when shard i reaches its k-th launch (different layers side by side)")
-    p.add_argument("--graph", type=int, default=0, help="1: replay the step as one captured HIP graph")
+    p.add_argument("--graph", type=int, default=1,
+                   help="1: replay the step (both shards' forwards + BEV on their streams) as one captured HIP "
+                        "graph — measured 41.8-41.9k vs 41.7k frames/s eager (round 3); 0: eager launches")
     p.add_argument("--cpu-baseline-seconds", type=float, default=12.0)
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--extras", type=int, default=-1,

@@ -816,6 +816,142 @@ __global__ void __launch_bounds__(256, 2) dl_gemm128p_kernel(const DlConvArgs a)
     }
 }
 
+// ------------------------------------------------------------------ 1x1 conv, 256 x 128 tiles, 2 per CU
+// The 128 x 128 tile is bound by operand delivery (DL_G2_ABL: 92 % of its time with the MFMAs removed):
+// 64 B of operands per CU-clock at the MFMA rate. A 256-pixel x 128-channel tile needs 25 % fewer bytes
+// per FLOP, and with 32-channel k-stages in three 24 KB buffers ([A 128 rows | B 256 rows] x 64 B) two
+// such workgroups still fit a CU (144 KB), so the co-resident workgroup that hides one's barriers and
+// epilogue is kept (the 256 x 256 tile lost it). Eight waves as 4 (pixels) x 2 (channels), each the
+// usual 64 x 64 acc[4][4]; LDS rows and swizzle as dl_gemm128p_kernel (g4_slot); two stages in flight.
+// Same k-steps, same MFMA, same order, same epilogue: bit-identical to dl_gemm128_kernel (GPU-tested).
+// Measured (round 3, Xception-65 B = 32): pointwise 4,797-4,798 -> 4,866-4,870 us per forward (605 ->
+// 596 TFLOP/s): fewer operand bytes per FLOP do not pay here, the 64-B half-line stages cost what they
+// save. Opt-in: BUGSEG_DL_P2=1.
+constexpr int G5_TM = 256, G5_TN = 128, G5_KT = 32, G5_NBUF = 3;
+
+template <bool OUTF32>
+__global__ void __launch_bounds__(512, 4) dl_gemm_p2_kernel(const DlConvArgs a) {
+    constexpr int SBUF = (G5_TN + G5_TM) * G5_KT;                 // elements per stage buffer (24 KB)
+    __shared__ __attribute__((aligned(16))) __bf16 sm[G5_NBUF * SBUF];
+    const int tid = threadIdx.x, lane = tid & 63, col = lane & 15, kq = lane >> 4, wave = tid >> 6;
+    const int wm = wave & 3, wn = wave >> 2;
+    const int ntn = (a.NP + G5_TN - 1) / G5_TN;
+    const int bid = xcd_block(blockIdx.x, gridDim.x);
+    const int n0 = (bid % ntn) * G5_TN, p0 = (bid / ntn) * G5_TM;
+    const int K = a.cinP;
+    const __bf16 *wg = reinterpret_cast<const __bf16 *>(a.w), *xg = reinterpret_cast<const __bf16 *>(a.in);
+    // glds sources: A rows wave * 16 + (lane >> 2) (one instruction), B rows (2 wave + i) * 16 + (lane >> 2)
+    const int ra = wave * 16 + (lane >> 2);
+    const int kca = g4_slot(lane & 3, ra) * 8;
+    const __bf16 *sa = wg + (size_t)min(n0 + ra, a.NP - 1) * K;
+    const __bf16 *sb[2];
+    int kcb[2];
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+        const int r = (2 * wave + i) * 16 + (lane >> 2);
+        kcb[i] = g4_slot(lane & 3, r) * 8;
+        sb[i] = xg + (size_t)min(p0 + r, a.M - 1) * a.CS;
+    }
+    const int nst = K / G5_KT;
+    auto stage = [&](int st) {
+        const int k0 = st * G5_KT;
+        __bf16 *bA = sm + (st % G5_NBUF) * SBUF, *bB = bA + G5_TN * G5_KT;
+        glds16(sa + k0 + kca, bA + wave * 16 * G5_KT);
+#pragma unroll
+        for (int i = 0; i < 2; ++i) {
+            const int k = k0 + kcb[i];
+            // channels past the stored CS read the weight row 0's zero padding (columns >= cin)
+            glds16(k < a.CS ? sb[i] + k : wg + k, bB + (2 * wave + i) * 16 * G5_KT);
+        }
+    };
+    f32x4 acc[4][4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) acc[j][r] = (f32x4){0.f, 0.f, 0.f, 0.f};
+    const int rslot = g4_slot(kq, col) * 8;
+    auto compute = [&](int st) {
+        const __bf16 *bA = sm + (st % G5_NBUF) * SBUF, *bB = bA + G5_TN * G5_KT;
+        u32x4 ra4[4], rb4[4];
+#pragma unroll
+        for (int r = 0; r < 4; ++r) ra4[r] = lds_read16(bA + (wn * 64 + r * 16 + col) * G5_KT + rslot);
+#pragma unroll
+        for (int j = 0; j < 4; ++j) rb4[j] = lds_read16(bB + (wm * 64 + j * 16 + col) * G5_KT + rslot);
+        lds_wait8(ra4[0], ra4[1], ra4[2], ra4[3], rb4[0], rb4[1], rb4[2], rb4[3]);
+        RawB wa[4], bx[4];
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+            wa[r].v = __builtin_bit_cast(uint4, ra4[r]);
+            bx[r].v = __builtin_bit_cast(uint4, rb4[r]);
+        }
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+#pragma unroll
+            for (int r = 0; r < 4; ++r) mma(acc[j][r], wa[r], bx[j]);
+    };
+#pragma unroll
+    for (int q = 0; q < G5_NBUF - 1; ++q)
+        if (q < nst) stage(q);
+    for (int st = 0; st < nst; ++st) {
+        // stages issued after st: min(1, nst - 1 - st), 3 glds each (wave-uniform)
+        if (st + 1 < nst) asm volatile("s_waitcnt vmcnt(3)" ::: "memory");
+        else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __builtin_amdgcn_s_barrier();
+        if (st + G5_NBUF - 1 < nst) stage(st + G5_NBUF - 1);   // into stage st - 1's buffer
+        compute(st);
+    }
+    __syncthreads();
+    const int nb = n0 + wn * 64;
+    if (nb >= a.NP) return;
+    static_assert(8 * 32 * DL_STG_RS * sizeof(float) <= sizeof(sm), "epilogue staging must fit the stage buffers");
+    float *stg = reinterpret_cast<float *>(sm) + wave * 32 * DL_STG_RS;
+    const int c8 = (lane & 7) * 8;
+    const bool cok = nb + c8 < a.cout;
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+        if (h) wave_lds_sync();
+#pragma unroll
+        for (int jj = 0; jj < 2; ++jj) {
+            const int j = 2 * h + jj;
+            const int p = p0 + wm * 64 + j * 16 + col;
+            const int pimg = a.bias_img ? (int)fdiv((uint32_t)(p < a.M ? p : 0), a.mHW, a.sHW) : 0;
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                const int nl = r * 16 + kq * 4, n = nb + nl;
+                float4 v = add4(f4(acc[j][r]), ld4f(a.bias + n));
+                if (a.bias_img) v = add4(v, ld4f(a.bias_img + (size_t)pimg * a.bias_img_stride + n));
+                if (a.act >= 1) v = make_float4(fmaxf(v.x, 0.f), fmaxf(v.y, 0.f), fmaxf(v.z, 0.f), fmaxf(v.w, 0.f));
+                if (a.act == 2) v = make_float4(fminf(v.x, 6.f), fminf(v.y, 6.f), fminf(v.z, 6.f), fminf(v.w, 6.f));
+                *reinterpret_cast<float4 *>(stg + (jj * 16 + col) * DL_STG_RS + nl) = v;
+            }
+        }
+        wave_lds_sync();
+#pragma unroll
+        for (int it = 0; it < 4; ++it) {
+            const int pl = it * 8 + (lane >> 3);
+            const int p = p0 + wm * 64 + h * 32 + pl;
+            if (p >= a.M || !cok) continue;
+            float4 v0 = *reinterpret_cast<const float4 *>(stg + pl * DL_STG_RS + c8);
+            float4 v1 = *reinterpret_cast<const float4 *>(stg + pl * DL_STG_RS + c8 + 4);
+            const int n = nb + c8;
+            if (a.res) {
+                const __bf16 *rp = reinterpret_cast<const __bf16 *>(a.res) + (size_t)p * a.res_cs + n;
+                v0 = add4(v0, ld4(rp));
+                v1 = add4(v1, ld4(rp + 4));
+            }
+            if constexpr (OUTF32) {
+                float *o = reinterpret_cast<float *>(a.out) + (size_t)p * a.out_cs + a.out_off + n;
+                st4(o, v0);
+                st4(o + 4, v1);
+            } else {
+                __bf16 *o = reinterpret_cast<__bf16 *>(a.out) + (size_t)p * a.out_cs + a.out_off + n;
+                st4(o, v0);
+                st4(o + 4, v1);
+            }
+        }
+    }
+}
+
 // ------------------------------------------------------------------ 1x1 conv, 256 x 256 tiles
 // dl_gemm128_kernel's scheme on a 256-pixel x 256-channel tile: eight waves as 4 (pixels) x 2
 // (channels), each 64 pixels x 128 channels (acc[4][8]), k-stages of 64 channels by global_load_lds into
@@ -1410,12 +1546,24 @@ static int gemm_pipe_bufs() {
     return n >= 3 && n <= 5 ? n : 0;
 }
 
+// the 256 x 128 two-per-CU tile (dl_gemm_p2_kernel) for the gemm128 shapes: BUGSEG_DL_P2=1 (A/B)
+static bool gemm_p2_on() {
+    const char *e = std::getenv("BUGSEG_DL_P2");
+    return e && *e == '1';
+}
+
 hipError_t dl_launch_conv(int prec, bool out_f32, const DlConvArgs &a, hipStream_t s) {
     const bool dwf = a.dw_w != nullptr;
     if (gemm_ok(prec, a) && gemm256_ok(a)) {
         const dim3 g(((a.M + G3_T - 1) / G3_T) * (a.NP / G3_T));
         if (out_f32) hipLaunchKernelGGL(dl_gemm256_kernel<true>, g, dim3(512), 0, s, a);
         else hipLaunchKernelGGL(dl_gemm256_kernel<false>, g, dim3(512), 0, s, a);
+        return hipGetLastError();
+    }
+    if (gemm_p2_on() && gemm_ok(prec, a) && gemm128_ok(a)) {
+        const dim3 g(((a.M + G5_TM - 1) / G5_TM) * ((a.NP + G5_TN - 1) / G5_TN));
+        if (out_f32) hipLaunchKernelGGL(dl_gemm_p2_kernel<true>, g, dim3(512), 0, s, a);
+        else hipLaunchKernelGGL(dl_gemm_p2_kernel<false>, g, dim3(512), 0, s, a);
         return hipGetLastError();
     }
     const int gp = gemm_pipe_bufs();
