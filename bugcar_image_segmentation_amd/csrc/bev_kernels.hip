@@ -658,11 +658,6 @@ __global__ void __launch_bounds__(256, FB == 1 ? 7 : 4) bev_band_kernel(const Be
 #ifndef BEV_CTAB
 #define BEV_CTAB 1
 #endif
-#ifndef BEV_DEAD
-// the compact-table form's early exit for waves of cells outside the footprint: bit-exact (GPU-tested)
-// but measured no faster (round 3, 32 frames: 38.6-39.0 vs 38.4-38.6 us per launch), so off
-#define BEV_DEAD 0
-#endif
     if (lds && BEV_CTAB) {
         // the LDS form on the compact table: 4-B entries, the 3x3's 9 of the next cell in flight while
         // this one is evaluated, and the 16 ring entries of a cell that needs them issued together (one
@@ -691,21 +686,6 @@ __global__ void __launch_bounds__(256, FB == 1 ? 7 : 4) bev_band_kernel(const Be
 #pragma unroll
             for (int i = 0; i < 9; ++i) e9[i] = c9n[i];
             load9(c + 256);
-            if constexpr (BEV_DEAD) {
-                // a cell none of whose 3x3 template pixels has a tap inside the class map (outside the
-                // camera's footprint): every value is the zero pad's 0, nothing is occupied, the ring is
-                // never read, so the cell is 0 in every frame. A wave of such cells (the two lower
-                // corners of a forward-looking grid) skips the 36 LDS reads and Q15 blends per frame
-                uint32_t anyv = 0;
-#pragma unroll
-                for (int i = 0; i < 9; ++i) anyv |= e9[i];
-                if (__ballot(((anyv >> 10) & 15u) != 0u) == 0) {   // wave-uniform
-#pragma unroll
-                    for (int f = 0; f < FB; ++f)
-                        if (f < nf) bev_emit(a, b0 + f, rem, cx, cy, cells, 0);
-                    continue;
-                }
-            }
             uint32_t outm = 0;
 #pragma unroll
             for (int i = 0; i < 9; ++i) outm |= (uint32_t)((e9[i] & TAB_OUT) != 0) << BEV_ORDER[i];

@@ -94,15 +94,11 @@ template <> struct BShape<64, 0> { static constexpr int TH = 16, TW = 16, NW = 4
 template <> struct BShape<64, 2> { static constexpr int TH = 8, TW = 16, NW = 4, OCC = 5, RP = 2, RD = 0, WIDE = 1; };
 template <> struct BShape<64, 1> { static constexpr int TH = 20, TW = 16, NW = 4, OCC = 5, RP = 3, RD = 0, WIDE = 1; };
 template <> struct BShape<16, 0> { static constexpr int TH = 16, TW = 16, NW = 4, OCC = 6, RP = 4, RD = 0, WIDE = 1; };
-// larger C = 16 tiles for the 240 x 320 stage-5 block (9,600 short 16 x 16 tiles at 32 frames): 32 x 16
-// and 16 x 32. Measured slower (round 3, fp16, B = 32: 56.9 / 56.6 vs 49.4-50.4 us per launch); the
-// runtime's cost model keeps 16 x 16, BUGSEG_BNECK_VARIANT_C16 forces one (A/B)
-template <> struct BShape<16, 1> { static constexpr int TH = 32, TW = 16, NW = 4, OCC = 6, RP = 4, RD = 0, WIDE = 1; };
-template <> struct BShape<16, 2> { static constexpr int TH = 16, TW = 32, NW = 4, OCC = 6, RP = 4, RD = 0, WIDE = 1; };
 // 20 x 16: 7,680 tiles at 32 frames, 5 whole rounds of the 1,536 resident slots (16 x 16: 9,600 tiles,
-// 6.25 rounds -> 7); the cost model picks it. Measured (round 3, fp16, B = 32): 48.0-48.4 vs 48.6-48.8 us
+// 6.25 rounds -> 7); the cost model picks it (32 x 16 and 16 x 32 tiles measured slower in round 3:
+// 56.9 / 56.6 vs 49.4-50.4 us per launch, and were removed). Measured (round 3, fp16, B = 32): 48.0-48.4 vs 48.6-48.8 us
 // per launch — equal within noise: the stage-5 block is not round-quantisation bound
-template <> struct BShape<16, 3> { static constexpr int TH = 20, TW = 16, NW = 4, OCC = 6, RP = 4, RD = 0, WIDE = 1; };
+template <> struct BShape<16, 1> { static constexpr int TH = 20, TW = 16, NW = 4, OCC = 6, RP = 4, RD = 0, WIDE = 1; };
 
 // LDS strides (elements). bf16: a 16-lane group of ds_read_b128 (one 16-B k group of 16 pixels or
 // weight rows) is conflict-free when the row stride is 8, 24, 40 or 56 dwords mod 64 (the SQ counters
@@ -115,18 +111,16 @@ __host__ __device__ constexpr int bneck_pstr(int es, int IS, bool wide) {
 }
 static bool bneck_wide(int C, int v, bool asym) {
 #define BW_CASE(CC, VV) if (C == CC && v == VV) return BShape<CC, VV>::WIDE && !asym;
-    BW_CASE(128, 0) BW_CASE(128, 1) BW_CASE(128, 2) BW_CASE(128, 3) BW_CASE(128, 4) BW_CASE(64, 0) BW_CASE(64, 1) BW_CASE(64, 2) BW_CASE(16, 0)
-    BW_CASE(16, 1) BW_CASE(16, 2) BW_CASE(16, 3)
+    BW_CASE(128, 0) BW_CASE(128, 1) BW_CASE(128, 2) BW_CASE(128, 3) BW_CASE(128, 4) BW_CASE(64, 0) BW_CASE(64, 1) BW_CASE(64, 2) BW_CASE(16, 0) BW_CASE(16, 1)
 #undef BW_CASE
     return false;
 }
 
-int bneck_variants(int C) { return C == 128 ? 5 : C == 16 ? 4 : 3; }
+int bneck_variants(int C) { return C == 128 ? 5 : C == 16 ? 2 : 3; }
 
 void bneck_shape(int C, int v, int &th, int &tw, int &nw, int *rd) {
 #define BS_CASE(CC, VV) if (C == CC && v == VV) { th = BShape<CC, VV>::TH; tw = BShape<CC, VV>::TW; nw = BShape<CC, VV>::NW; if (rd) *rd = BShape<CC, VV>::RD; return; }
-    BS_CASE(128, 0) BS_CASE(128, 1) BS_CASE(128, 2) BS_CASE(128, 3) BS_CASE(128, 4) BS_CASE(64, 0) BS_CASE(64, 1) BS_CASE(64, 2) BS_CASE(16, 0)
-    BS_CASE(16, 1) BS_CASE(16, 2) BS_CASE(16, 3)
+    BS_CASE(128, 0) BS_CASE(128, 1) BS_CASE(128, 2) BS_CASE(128, 3) BS_CASE(128, 4) BS_CASE(64, 0) BS_CASE(64, 1) BS_CASE(64, 2) BS_CASE(16, 0) BS_CASE(16, 1)
 #undef BS_CASE
     th = tw = nw = 0;
     if (rd) *rd = 0;
@@ -139,21 +133,13 @@ void bneck_shape(int C, int v, int &th, int &tw, int &nw, int *rd) {
 // projection's own B fragments (lane kq holds taps of one 8-channel group: the 4 taps in-lane for
 // CI >= 32, two taps in-lane + one v_permlane32_swap for CI = 16) and leaves the pooled values in a
 // small global scratch (a.pool) that phase 3 reads back as its residual (L2 hits).
-// INI: the ENet initial block (preprocessing fused: models.py:84-95) computed
-// inside this kernel from the raw BGR frames, feeding the 16 -> 64 downsampling block's projection
-// directly (see the INI notes at the patch staging and at init_dn): the initial block's output never
-// goes through HBM. Bit-identical to the two launches, but measured slower than them (round 3, fp16,
-// B = 32: 113-121 us vs 43.5 + 49 us): the 52 KB patch holds the form to 3 workgroups (12 waves) per
-// CU, where the initial block's LDS-latency-bound arithmetic needs the 6-8 waves per SIMD its own
-// kernel runs at; a BGR-order patch (8-B LDS stores instead of 2-B ones) changes the initial conv's
-// MFMA k order, so it is no longer bit-identical. Opt-in (BUGSEG_INIT_FUSE=1, bugseg_runtime.cpp).
 // fp32 (parity mode): registers unconstrained (LDS bounds the C = 64 / 128 forms first), except C = 16,
 // held to 5 waves per SIMD (unconstrained it took 16 AGPRs on top of 91 VGPRs: 4; LDS allows 5)
 #ifndef BNECK_F32_OCC16
 #define BNECK_F32_OCC16 5
 #endif
-template <typename T, int C, bool ASYM, int V, bool TR, int CI = 0, bool INI = false>
-__global__ void __launch_bounds__((BShape<C, V>::NW * 64), (sizeof(T) == 2 ? (INI ? 3 : BShape<C, V>::OCC) : C == 16 ? BNECK_F32_OCC16 : 1)) bneck_kernel(const BneckArgs a) {
+template <typename T, int C, bool ASYM, int V, bool TR, int CI = 0>
+__global__ void __launch_bounds__((BShape<C, V>::NW * 64), (sizeof(T) == 2 ? BShape<C, V>::OCC : C == 16 ? BNECK_F32_OCC16 : 1)) bneck_kernel(const BneckArgs a) {
     using Raw = typename Tr<T>::Raw;
     constexpr int TH = BShape<C, V>::TH, TW = BShape<C, V>::TW, NW = BShape<C, V>::NW, NT = NW * 64;
     constexpr int I = CI > 0 ? CI / 4 : C / 4;      // internal channels (ENet: input / 4)
@@ -217,8 +203,8 @@ __global__ void __launch_bounds__((BShape<C, V>::NW * 64), (sizeof(T) == 2 ? (IN
 #ifndef BNECK_CH1_K8
 #define BNECK_CH1_K8 1
 #endif
-    constexpr int CH1 = INI ? 1 : KS1 >= 8 ? BNECK_CH1_K8 : KS1 >= 4 ? (NF1 + NW - 1) / NW
-                      : KS1 == 2 ? (C == 64 && V == 0 && !DN && !ASYM ? BNECK_CH1_C64 : BNECK_CH1_K2) : 8;   // phase-1 fragments whose loads fly together
+    constexpr int CH1 = KS1 >= 8 ? BNECK_CH1_K8 : KS1 >= 4 ? (NF1 + NW - 1) / NW
+                    : KS1 == 2 ? (C == 64 && V == 0 && !DN && !ASYM ? BNECK_CH1_C64 : BNECK_CH1_K2) : 8;   // phase-1 fragments whose loads fly together
     // phase-3 chunking (see phase 3): bf16 with an even number of 16-row blocks swaps row pairs
     // into 16-B chunks; bf16 C = 16 stores 8-B quads (HALF); fp32 quads are 16-B chunks
     // REG3: the register epilogue (C = 128 and 16). C = 64 keeps the LDS-staged epilogue: its 128-B
@@ -283,15 +269,6 @@ __global__ void __launch_bounds__((BShape<C, V>::NW * 64), (sizeof(T) == 2 ? (IN
     // Measured (round 3, fp16, B = 32): down C64 52.9 -> 48.1 us, down C128 33.7 -> 28.7 us
     constexpr bool DKEEP = BNECK_DKEEP && DN && sizeof(T) == 2 && SWAP;
     constexpr int NPK = DN ? (CI + 31) / 32 : 1;      // DKEEP: pooled 16-B chunks per lane and fragment
-    static_assert(!INI || (DKEEP && CI == 16 && KS1 == 2 && !TR), "fused initial block: the 2-byte 16 -> C down form");
-    // INI patch: the BGR input under the tile's halo. Down pixel (i, j) of the halo (0..TH+1, 0..TW+1)
-    // projects initial-block pixels (2i + dy, 2j + dx), whose 3x3 stride-2 windows cover input rows
-    // 4i + 2dy + 0..2: IPH x IPW input pixels, stored as normalised RGB elements (init_kernels.hip's
-    // patch layout: element 3 px + c, rows of IPRS elements, even)
-    constexpr int IPH = INI ? 4 * (TH + 2) + 1 : 0, IPW = INI ? 4 * (TW + 2) + 1 : 0;
-    constexpr int IPRS = INI ? IPW * 3 + 1 : 0;
-    constexpr int IPD = INI ? (IPW * 3 + 1 + 3) / 4 : 0;   // dwords per patch row (one lead byte: see the load)
-    constexpr int IPL = INI ? (IPH * IPD + NW * 64 - 1) / (NW * 64) : 0;   // dword loads per thread
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
 
     STAMP_ENTRY(0);
@@ -319,8 +296,6 @@ __global__ void __launch_bounds__((BShape<C, V>::NW * 64), (sizeof(T) == 2 ? (IN
     // 16 zero elements: masked-off B fragments read them (an address select, not a divergent branch)
     T *zpad = reinterpret_cast<T *>(cso + C);
     T *ts = zpad + 16;                                // t0 / t1a / t1 region
-    T *ipatch = ts + HR * PSTR;                       // INI: the tile's input patch, then the 3 x 256 LUT
-    T *ilut = ipatch + IPH * IPRS;
     {
         // C = 16 (small weights, many short tiles): every load of the staging is issued before the
         // first LDS store (one L2 round trip at kernel start instead of one per 16-B chunk a thread
@@ -420,23 +395,6 @@ __global__ void __launch_bounds__((BShape<C, V>::NW * 64), (sizeof(T) == 2 ? (IN
         }
         if (tid < 16) zpad[tid] = (T)0.f;
     }
-    // INI: the normalisation LUT (rounded to T exactly as init_kernel stores its patch: f64 -> f32 -> T),
-    // the initial conv's A fragment (init_kernel's K order) and its per-lane epilogue constants
-    typename Tr<T>::Raw wf0;
-    float4 ib4 = make_float4(0.f, 0.f, 0.f, 0.f), is4 = ib4, ip4 = ib4;
-    if constexpr (INI) {
-        for (int i = threadIdx.x; i < 3 * 256; i += NT) ilut[i] = (T)(float)a.nlut[i];
-        const T *wp = reinterpret_cast<const T *>(a.w0);
-        const int cl = threadIdx.x & 15, kqq = (threadIdx.x & 63) >> 4;
-        T wv[8];
-#pragma unroll
-        for (int j = 0; j < 8; ++j) {
-            const int dy = kqq < 3 ? kqq : j, e = kqq < 3 ? j : (j < 3 ? 8 : -1);
-            wv[j] = e >= 0 ? wp[cl * a.kpad0 + (dy * 3 + e / 3) * 8 + e % 3] : (T)0.f;
-        }
-        set8(wf0, wv);
-        ib4 = ld4f(a.b0 + kqq * 4); is4 = ld4f(a.s0 + kqq * 4); ip4 = ld4f(a.p0 + kqq * 4);
-    }
     // x / out through buffer descriptors: 32-bit offsets, and an out-of-range offset reads 0 / drops
     // the store (mfma_common.h), so image-border masking costs one select per access
     // down mode: x is the (2H, 2W, CI) block input; the residual comes from the pooled scratch
@@ -467,20 +425,8 @@ __global__ void __launch_bounds__((BShape<C, V>::NW * 64), (sizeof(T) == 2 ? (IN
         oy0 = py + dt * tyi * (tr ? TW : TH);
         ox0 = RD ? 0 : px + dt * txi * (tr ? TH : TW);
     };
-    // PIPE (KEEP forms, a workgroup walking several tiles): as phase 3 retires fragment j's kept x
-    // (its residual), the same registers take the NEXT tile's fragment j, so the next tile's interior
-    // loads fly under this tile's expansion and stores instead of after them. Measured (round 3, fp16,
-    // B = 32): no gain — at the default grid (one round of tiles) nothing walks a second tile and the
-    // extra live registers cost 2-3 spills (C128 20x16 22.5 -> 23.7 us); with half the slots (two tiles
-    // per workgroup) 26.8 -> 27.3 us, the same as without it: the overlap the chip needs comes from
-    // other resident workgroups, not from inside one. Off; A/B knob
-#ifndef BNECK_PIPE
-#define BNECK_PIPE 0
-#endif
-    constexpr bool PIPE = BNECK_PIPE && KEEP && REG3;
     Raw kx[KEEP ? NF2 : 1][KS1];                      // KEEP: this wave's interior fragments of x
     bool kok[KEEP ? NF2 : 1];
-    bool pf = false;                                  // kx / kok already hold this tile's interior (PIPE)
     for (int it = slot; it < CH; it += nslots) {
         const int tile = grp * CH + it;
         if (tile >= a.ntiles) break;
@@ -623,52 +569,9 @@ __global__ void __launch_bounds__((BShape<C, V>::NW * 64), (sizeof(T) == 2 ? (IN
         // the first tile waits for the glds weight staging (each wave its own loads, then the
         // barrier makes every wave's visible); KEEP issues its x loads ahead of that wait
         const bool first = it == slot;
-        // INI: the tile's BGR patch, dword loads all in flight before the barrier. Input pixel column
-        // 4 ox0 - 5 starts at byte 12 ox0 - 15 of its row, one byte past a dword boundary (rows are
-        // 3 * 4W bytes: whole dwords), so row r is IPD dwords from that boundary with one lead byte.
-        // Rows outside the frame read 0 (negative / past-the-end offsets are out of range) and are
-        // zeroed anyway; columns outside it are zeroed per byte (the conv's zero padding)
-        uint32_t pdw[INI ? IPL : 1];
-        const int piy0 = 4 * oy0 - 5, pix0 = 4 * ox0 - 5, Hin = 4 * a.H, Win = 4 * a.W;
-        if constexpr (INI) {
-            const auto rbg = mkbuf(a.bgr, a.bgr_bytes);
-#pragma unroll
-            for (int i = 0; i < IPL; ++i) {
-                // (opaque: the per-thread chunk coordinates are tile-invariant, and hoisted out of the
-                // tile loop they held ~48 VGPRs for the kernel's lifetime)
-                int k = tid + NT * i;
-                asm volatile("" : "+v"(k));
-                const int r = k / IPD, d = k - r * IPD;
-                const int iy = piy0 + r;
-                const bool ok = k < IPH * IPD && (unsigned)iy < (unsigned)Hin;
-                const uint32_t off = ((uint32_t)(n * Hin + iy) * (uint32_t)Win) * 3u + (uint32_t)(12 * ox0 - 16 + 4 * d);
-                pdw[i] = __builtin_amdgcn_raw_buffer_load_b32(rbg, ok ? (int)off : (int)OOB, 0, 0);
-            }
-        }
         if constexpr (!KEEP) {
             if (GLDS && first) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
             __syncthreads();   // weights staged (first tile) / previous tile done with ts (and the patch)
-        }
-        if constexpr (INI) {
-            // bytes -> normalised RGB elements (BGR byte cb is RGB channel 2 - cb, models.py:87)
-#pragma unroll
-            for (int i = 0; i < IPL; ++i) {
-                int k = tid + NT * i;
-                asm volatile("" : "+v"(k));
-                const int r = k / IPD, d = k - r * IPD;
-                const bool rok = k < IPH * IPD && (unsigned)(piy0 + r) < (unsigned)Hin;
-#pragma unroll
-                for (int b = 0; b < 4; ++b) {
-                    const int e = 4 * d + b - 1;                  // element (byte) of the patch row
-                    const int px = (e * 171) >> 9, cb = e - 3 * px;  // e / 3 for 0 <= e < 512
-                    const bool in = (unsigned)e < (unsigned)(3 * IPW) && k < IPH * IPD;
-                    const bool ok = rok && (unsigned)(pix0 + px) < (unsigned)Win;
-                    const T v = ilut[(2 - cb) * 256 + (int)((pdw[i] >> (8 * b)) & 255u)];
-                    if (in) ipatch[r * IPRS + px * 3 + (2 - cb)] = ok ? v : (T)0.f;
-                }
-                asm volatile("" ::: "memory");   // one dword's LUT reads at a time (registers)
-            }
-            __syncthreads();
         }
         STAMP(1);
 
@@ -741,11 +644,9 @@ __global__ void __launch_bounds__((BShape<C, V>::NW * 64), (sizeof(T) == 2 ? (IN
             Raw bx[NBW][KS1];
             int bh[NBW];
             bool bok[NBW];
-            if (!pf) {                                                 // (PIPE: prefetched in the previous tile's phase 3)
 #pragma unroll
-                for (int j = 0; j < NF2; ++j)
-                    if (wave + NW * j < NFT) kok[j] = load_h(int_h(wave + NW * j), true, kx[j]);   // wave-uniform
-            }
+            for (int j = 0; j < NF2; ++j)
+                if (wave + NW * j < NFT) kok[j] = load_h(int_h(wave + NW * j), true, kx[j]);   // wave-uniform
             auto load_b = [&](int k) {
                 const int b = (wb + NW * k) * 16 + col;
                 bh[k] = b < NBD ? bord_h(b) : 0;
@@ -801,75 +702,6 @@ __global__ void __launch_bounds__((BShape<C, V>::NW * 64), (sizeof(T) == 2 ? (IN
                 }
                 return ok;
             };
-            // INI: the projection's B fragments of halo pixel h computed from the patch instead of
-            // loaded: k-step s holds taps 2s, 2s + 1 (lane kq: tap 2s + kq / 2, channels 8 (kq & 1) ..
-            // + 7), i.e. the initial-block outputs of the 4 taps — two 16-channel quads per k-step
-            // through to_bop. Each tap is init_kernel's arithmetic exactly (one MFMA over K = 27 from the
-            // bias, the pool channels' maxima added with their scale, PReLU, rounded to T), so the fused
-            // pair is bit-identical to the two launches. Lane (col, kq) computes the pool maxima of tap
-            // kq of pixel col; ds_bpermute hands them to the lanes holding the pool channels.
-            auto init_dn = [&](int h, bool valid, Raw (&xs)[KS1]) -> bool {
-                const int hy = h / HWW, hx = h - hy * HWW;
-                const int iy = oy0 + hy - 1, ix = ox0 + hx - 1;
-                const bool ok = valid && (unsigned)iy < (unsigned)a.H && (unsigned)ix < (unsigned)a.W;
-                // tap t's initial-block pixel: patch row 2 (2 hy + (t >> 1)), element 6 (2 hx + (t & 1))
-                const int po = a.pool_k == 3 ? 0 : 1;      // pool window: patch offsets po .. 2
-                float pm[3];
-                {
-                    const int R = 2 * hy + (kq >> 1), Cc = 2 * hx + (kq & 1);
-                    const T *pp = ipatch + 2 * R * IPRS + 6 * Cc;
-                    const bool top = piy0 + 2 * R < 0, left = pix0 + 2 * Cc < 0;   // window row / col 0 outside
-#pragma unroll
-                    for (int ch = 0; ch < 3; ++ch) {
-                        float mx = -INFINITY;
-#pragma unroll
-                        for (int dy = 0; dy < 3; ++dy) {
-                            if (dy < po || (dy == 0 && top)) continue;
-#pragma unroll
-                            for (int dx = 0; dx < 3; ++dx) {
-                                if (dx < po || (dx == 0 && left)) continue;
-                                mx = fmaxf(mx, (float)pp[dy * IPRS + dx * 3 + ch]);
-                            }
-                        }
-                        pm[ch] = mx;
-                    }
-                }
-                float4 q[4];
-                const int c0 = kq * 4;
-#pragma unroll
-                for (int t = 0; t < 4; ++t) {
-                    const int R = 2 * hy + (t >> 1), Cc = 2 * hx + (t & 1);
-                    const T *pp = ipatch + 2 * R * IPRS + 6 * Cc;
-                    Raw xf;
-                    if (kq < 3) {
-                        const uint32_t *s32 = reinterpret_cast<const uint32_t *>(pp + kq * IPRS);
-                        xf.v = make_uint4(s32[0], s32[1], s32[2], s32[3]);
-                    } else {
-                        T xv[8];
-#pragma unroll
-                        for (int j = 0; j < 8; ++j) xv[j] = j < 3 ? pp[j * IPRS + 8] : (T)0.f;
-                        set8(xf, xv);
-                    }
-                    f32x4 acc = (f32x4){ib4.x, ib4.y, ib4.z, ib4.w};   // the MFMA adds the bias
-                    mma(acc, wf0, xf);
-                    float4 v = f4(acc);
-                    const int src = (col + 16 * t) << 2;
-                    float pf[3];
-#pragma unroll
-                    for (int ch = 0; ch < 3; ++ch)
-                        pf[ch] = __int_as_float(__builtin_amdgcn_ds_bpermute(src, __float_as_int(pm[ch])));
-                    float pv[4] = {0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-                    for (int r = 0; r < 4; ++r) {
-                        const int ch = c0 + r - a.cconv;
-                        if (ch >= 0 && ch < a.cpool) pv[r] = (ch == 0 ? pf[0] : ch == 1 ? pf[1] : pf[2]) * get(ip4, r);
-                    }
-                    q[t] = prelu4(add4(v, make_float4(pv[0], pv[1], pv[2], pv[3])), is4);
-                }
-                to_bop(xs[0], q[0], q[1]);
-                to_bop(xs[1], q[2], q[3]);
-                return ok;
-            };
 #pragma unroll
             for (int j = 0; j < NF2; ++j)
 #pragma unroll
@@ -892,8 +724,7 @@ __global__ void __launch_bounds__((BShape<C, V>::NW * 64), (sizeof(T) == 2 ? (IN
                         vq[c] = b < NBD;
                         hq[c] = vq[c] ? bord_h(b) : 0;
                     }
-                    if constexpr (INI) okc[c] = init_dn(hq[c], vq[c], xf[c]);
-                    else okc[c] = load_dn(hq[c], vq[c], xf[c]);
+                    okc[c] = load_dn(hq[c], vq[c], xf[c]);
                 }
 #pragma unroll
                 for (int c = 0; c < CH1; ++c) {
@@ -1066,90 +897,48 @@ __global__ void __launch_bounds__((BShape<C, V>::NW * 64), (sizeof(T) == 2 ? (IN
             STAMP(4);
             to_tf(acc, cs2);
         } else {
-            // 5x1 over rows (taps dy = -2..2), output width TW+4 (the 1x5's halo). With the residual
-            // kept in registers (KEEP) the pass runs in two fragment halves: the first half's t1a is
-            // rounded and held packed (what the LDS store would write) while the second half
-            // accumulates, so the live accumulators halve — the whole pass at once spilled
-#ifndef BNECK_ASYM_SPLIT
-#define BNECK_ASYM_SPLIT 0
-#endif
-            constexpr bool SPLIT = BNECK_ASYM_SPLIT && KEEP && sizeof(T) == 2 && NF2A >= 2;
-            constexpr int HS = SPLIT ? (NF2A + 1) / 2 : NF2A;   // fragments per pass
-            auto pass5 = [&](int j0, f32x4 (&acc)[HS][NR1]) {
+            // 5x1 over rows (taps dy = -2..2), output width TW+4 (the 1x5's halo). (Run in two fragment
+            // halves with the residual kept in registers it measured slower, round 3: 28.2 vs 26.2 us)
+            f32x4 acc5[NF2A][NR1];
 #pragma unroll
-                for (int jj = 0; jj < HS; ++jj)
+            for (int j = 0; j < NF2A; ++j)
 #pragma unroll
-                    for (int r = 0; r < NR1; ++r) acc[jj][r] = bias4(cb2 + r * 16 + kq * 4);
+                for (int r = 0; r < NR1; ++r) acc5[j][r] = bias4(cb2 + r * 16 + kq * 4);
 #pragma unroll BNECK_ASYM_UNROLL
-                for (int s = 0; s < KS2; ++s) {
-                    const int g = s * 4 + kq;
-                    const int tap = g / (IS / 8), coff = (g - tap * (IS / 8)) * 8;
-                    Raw wf[NR1];
+            for (int s = 0; s < KS2; ++s) {
+                const int g = s * 4 + kq;
+                const int tap = g / (IS / 8), coff = (g - tap * (IS / 8)) * 8;
+                Raw wf[NR1];
 #pragma unroll
-                    for (int r = 0; r < NR1; ++r) ld8(wf[r], w2 + (r * 16 + col) * K2S + s * 32 + kq * 8);
+                for (int r = 0; r < NR1; ++r) ld8(wf[r], w2 + (r * 16 + col) * K2S + s * 32 + kq * 8);
 #pragma unroll
-                    for (int jj = 0; jj < HS; ++jj) {
-                        const int j = j0 + jj, f = wave + NW * j;
-                        if (j >= NF2A || f >= NFA) continue;
-                        int p = f * 16 + col;
-                        if constexpr (NPA % 16 != 0) p = p < NPA ? p : 0;
-                        const int oy = p / TWA, ox = p - oy * TWA;
-                        Raw xf;
-                        ld8(xf, g < G2 ? ts + ((oy + tap) * HWW + ox) * PSTR + coff : zpad);
+                for (int j = 0; j < NF2A; ++j) {
+                    const int f = wave + NW * j;
+                    if (f >= NFA) continue;
+                    int p = f * 16 + col;
+                    if constexpr (NPA % 16 != 0) p = p < NPA ? p : 0;
+                    const int oy = p / TWA, ox = p - oy * TWA;
+                    Raw xf;
+                    ld8(xf, g < G2 ? ts + ((oy + tap) * HWW + ox) * PSTR + coff : zpad);
 #pragma unroll
-                        for (int r = 0; r < NR1; ++r) mma(acc[jj][r], wf[r], xf);
+                    for (int r = 0; r < NR1; ++r) mma(acc5[j][r], wf[r], xf);
+                }
+            }
+            __syncthreads();
+            // t1a of fragment j, row block r: act2, zero outside the image columns (the 1x5 zero-pads t1a)
+#pragma unroll
+            for (int j = 0; j < NF2A; ++j)
+#pragma unroll
+                for (int r = 0; r < NR1; ++r) {
+                    const int f = wave + NW * j, p = f * 16 + col, ch = r * 16 + kq * 4;
+                    if (f < NFA && p < NPA && ch < IS) {
+                        const int ox = p - (p / TWA) * TWA;
+                        const bool inside = (unsigned)(ox0 - 2 + ox) < (unsigned)a.W;
+                        const float4 v = act(f4(acc5[j][r]), cs2 + ch);
+                        st4(ts + p * PSTR + ch, inside ? v : make_float4(0.f, 0.f, 0.f, 0.f));
                     }
                 }
-            };
-            // t1a of fragment j, row block r: act2, zero outside the image columns (the 1x5 zero-pads
-            // t1a); `where` = its LDS position, or -1 where the fragment / channel does not exist
-            auto t1a_at = [&](int j, int r, const f32x4 &acc, int &where) -> float4 {
-                const int f = wave + NW * j, p = f * 16 + col, ch = r * 16 + kq * 4;
-                where = (j < NF2A && f < NFA && p < NPA && ch < IS) ? p * PSTR + ch : -1;
-                const int ox = p - (p / TWA) * TWA;
-                const bool inside = (unsigned)(ox0 - 2 + ox) < (unsigned)a.W;
-                float4 v = act(f4(acc), cs2 + ch);
-                return inside ? v : make_float4(0.f, 0.f, 0.f, 0.f);
-            };
-            if constexpr (SPLIT) {
-                f32x4 acc[HS][NR1];
-                pass5(0, acc);
-                u32x2_t held[HS][NR1];
-                int hw[HS][NR1];
-#pragma unroll
-                for (int jj = 0; jj < HS; ++jj)
-#pragma unroll
-                    for (int r = 0; r < NR1; ++r) held[jj][r] = pack4<T>(t1a_at(jj, r, acc[jj][r], hw[jj][r]));
-                pass5(HS, acc);
-                __syncthreads();                          // every wave is done reading t0
-#pragma unroll
-                for (int jj = 0; jj < HS; ++jj)
-#pragma unroll
-                    for (int r = 0; r < NR1; ++r)
-                        if (hw[jj][r] >= 0) *reinterpret_cast<u32x2_t *>(ts + hw[jj][r]) = held[jj][r];
-#pragma unroll
-                for (int jj = 0; jj < HS; ++jj)
-#pragma unroll
-                    for (int r = 0; r < NR1; ++r) {
-                        int w;
-                        const float4 v = t1a_at(HS + jj, r, acc[jj][r], w);
-                        if (w >= 0) st4(ts + w, v);
-                    }
-                __syncthreads();
-            } else {
-                f32x4 acc[HS][NR1];
-                pass5(0, acc);
-                __syncthreads();
-#pragma unroll
-                for (int j = 0; j < NF2A; ++j)
-#pragma unroll
-                    for (int r = 0; r < NR1; ++r) {
-                        int w;
-                        const float4 v = t1a_at(j, r, acc[j][r], w);
-                        if (w >= 0) st4(ts + w, v);
-                    }
-                __syncthreads();
-            }
+            __syncthreads();
             {   // 1x5 over columns (taps dx = -2..2)
                 f32x4 acc[NF2][NR1];
 #pragma unroll
@@ -1279,12 +1068,6 @@ __global__ void __launch_bounds__((BShape<C, V>::NW * 64), (sizeof(T) == 2 ? (IN
             continue;
         }
         STAMP(5);
-        // PIPE: the next tile of this workgroup's walk (wave-uniform), prefetched fragment by fragment
-        const int itn = it + nslots, tilen = grp * CH + itn;
-        const bool nxt = PIPE && itn < CH && tilen < a.ntiles;
-        int nn = 0, noy0 = 0, nox0 = 0;
-        if (nxt) tile_geom(tilen, nn, noy0, nox0);
-        const uint32_t nxn = (uint32_t)(nn * a.H * a.W) * (uint32_t)(C * sizeof(T));
 #pragma unroll
         for (int j = 0; j < NF2; ++j) {
             if (wave + NW * j >= NFT) break;              // wave-uniform
@@ -1348,10 +1131,7 @@ __global__ void __launch_bounds__((BShape<C, V>::NW * 64), (sizeof(T) == 2 ? (IN
             }
             if constexpr (!KEEP && !DKEEP)
                 if (j + RP < NF2 && wave + NW * (j + RP) < NFT) load_res(j + RP, res[j % RP]);
-            if constexpr (PIPE)
-                if (nxt) kok[j] = load_hg(noy0, nox0, nxn, int_h(wave + NW * j), true, kx[j]);
         }
-        if constexpr (PIPE) pf = nxt;
         STAMP(6);
     }
     STAMP_ENTRY(1);
@@ -1363,11 +1143,9 @@ extern "C" int bugseg_debug_set_stamps(void *p) {
 }
 #endif
 
-size_t bneck_lds_bytes(int prec, int C, bool asym, int v, int cin, bool ini) {
+size_t bneck_lds_bytes(int prec, int C, bool asym, int v, int cin) {
     int TH, TW, NW, RD;
     bneck_shape(C, v, TH, TW, NW, &RD);
-    // INI (fused initial block): the BGR patch and the 3 x 256 LUT after the t0 region
-    const size_t ipatch = ini ? (size_t)(4 * (TH + 2) + 1) * ((4 * (TW + 2) + 1) * 3 + 1) + 3 * 256 : 0;
     const int es = prec_es(prec), pad = 16 / es;
     const int I = cin > 0 ? cin / 4 : C / 4, IS = I < 8 ? 8 : I, NR1 = (I + 15) / 16;
     const int KS1 = ((cin > 0 ? cin / 2 : C / 8) + 3) / 4, KS2 = ((asym ? 5 : 9) * IS / 8 + 3) / 4;
@@ -1381,7 +1159,6 @@ size_t bneck_lds_bytes(int prec, int C, bool asym, int v, int cin, bool ini) {
     const bool hstg = staged && es == 4 && BNECK_F32_HSTG;            // fp32 C = 64: one 32-channel half at a time
     const size_t stage = staged ? (size_t)NW * 16 * ((hstg ? C / 2 : C) + pad) : 0;    // staged epilogue (REG3 off)
     const size_t consts = ((size_t)6 * NR1 * 16 + 3 * (size_t)C) * sizeof(float);
-    if (ini) return (wts + 16 + halo + ipatch) * es + consts;          // (INI: REG3, no staging)
     return (wts + 16 + (halo > stage ? halo : stage)) * es + consts;   // + the zero pad
 }
 
@@ -1390,12 +1167,11 @@ template <typename T>
 static const void *kfun(int C, bool asym, int v, bool tr) {
 #define BK_CASE(CC, VV) \
     if (C == CC && v == VV && !tr) return asym ? (const void *)bneck_kernel<T, CC, true, VV, false> : (const void *)bneck_kernel<T, CC, false, VV, false>;
-    BK_CASE(128, 0) BK_CASE(128, 1) BK_CASE(128, 4) BK_CASE(64, 0) BK_CASE(64, 1) BK_CASE(64, 2) BK_CASE(16, 0) BK_CASE(16, 1)
-    BK_CASE(16, 2)
+    BK_CASE(128, 0) BK_CASE(128, 1) BK_CASE(128, 4) BK_CASE(64, 0) BK_CASE(64, 1) BK_CASE(64, 2) BK_CASE(16, 0)
 #undef BK_CASE
     // (2-byte storage only: the fp32 instance spills 9 VGPRs)
     if constexpr (sizeof(T) == 2)
-        if (C == 16 && v == 3 && !tr) return asym ? nullptr : (const void *)bneck_kernel<T, 16, false, 3, false>;
+        if (C == 16 && v == 1 && !tr) return asym ? nullptr : (const void *)bneck_kernel<T, 16, false, 1, false>;
     if (C == 128 && v == 1 && tr && !asym) return (const void *)bneck_kernel<T, 128, false, 1, true>;
     if (C == 128 && v == 2 && !tr && !asym) return (const void *)bneck_kernel<T, 128, false, 2, false>;
     if (C == 128 && v == 3 && !tr && !asym) return (const void *)bneck_kernel<T, 128, false, 3, false>;
@@ -1446,47 +1222,6 @@ int bneck_slots_per_cu(int prec, int C, bool asym, int v, bool tr, int cin) {
     if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, f, nw * 64, bneck_lds_bytes(prec, C, asym, v, cin)) != hipSuccess)
         return 0;
     return slot = n;
-}
-
-// the fused initial block + down form (2-byte storage; ENet's down1: 16 -> 64 on 16 x 16 tiles)
-static const void *bneck_init_fun(int prec, int C, int v, int cin) {
-    if (C != 64 || v != 0 || cin != 16) return nullptr;
-    return prec == PREC_BF16 ? (const void *)bneck_kernel<__bf16, 64, false, 0, false, 16, true>
-         : prec == PREC_F16  ? (const void *)bneck_kernel<_Float16, 64, false, 0, false, 16, true> : nullptr;
-}
-
-bool bneck_init_supported(int prec, int C, int v, int cin) {
-    const void *f = bneck_init_fun(prec, C, v, cin);
-    if (!f || allow_lds(f) != hipSuccess) return false;
-    int n = 0;
-    int th, tw, nw;
-    bneck_shape(C, v, th, tw, nw, nullptr);
-    return hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, f, nw * 64, bneck_lds_bytes(prec, C, false, v, cin, true)) == hipSuccess && n > 0;
-}
-
-hipError_t launch_bneck_init(int prec, int C, int v, const BneckArgs &a, hipStream_t s, int cin) {
-    const void *f = bneck_init_fun(prec, C, v, cin);
-    if (!f) return hipErrorInvalidValue;
-    int th, tw, nw;
-    bneck_shape(C, v, th, tw, nw, nullptr);
-    const size_t lds = bneck_lds_bytes(prec, C, false, v, cin, true);
-    hipError_t e = allow_lds(f);
-    if (e != hipSuccess) return e;
-    static int n_cu = -1;
-    if (n_cu < 0) {
-        int dev = 0;
-        if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&n_cu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
-            n_cu = 0;
-    }
-    int spc = 0;
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&spc, f, nw * 64, lds) != hipSuccess) spc = 0;
-    const char *ge = std::getenv("BUGSEG_BNECK_GRID");
-    const int grid_cap = ge ? std::atoi(ge) : 0;
-    const int cap = grid_cap > 0 ? grid_cap : spc > 0 && n_cu > 0 ? spc * n_cu : 2048;
-    int g = a.ntiles < cap ? a.ntiles : cap;
-    g = (g + 7) & ~7;
-    void *args[] = {const_cast<BneckArgs *>(&a)};
-    return hipLaunchKernel(f, dim3(g), dim3(nw * 64), args, lds, s);
 }
 
 hipError_t launch_bneck(int prec, int C, bool asym, int v, const BneckArgs &a, hipStream_t s, int cin) {

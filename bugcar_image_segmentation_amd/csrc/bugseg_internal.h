@@ -97,14 +97,6 @@ struct BneckArgs {
     uint8_t *idx_out;
     int idxCS;
     uint32_t xin_bytes, pool_bytes, idx_bytes;
-    // the initial block fused into the first downsampling block (launch_bneck_init): xin unused; the
-    // raw BGR frames (B, 4H, 4W, 3) u8 and the initial block's packed weights / constants
-    const uint8_t *bgr;
-    uint32_t bgr_bytes;
-    const double *nlut;                               // (v / 256 - mean) / std per RGB channel, 3 x 256
-    const void *w0;                                   // initial conv, packed [16][Kpad0] (k = tap * 8 + c)
-    const float *b0, *s0, *p0;                        // its bias, PReLU slope, pool-channel scale (16 each)
-    int kpad0, cconv, cpool, pool_k;
 };
 // tile-shape variants of the fused kernel for C channels: 0 .. bneck_variants(C) - 1
 int bneck_variants(int C);
@@ -112,14 +104,10 @@ int bneck_variants(int C);
 void bneck_shape(int C, int v, int &th, int &tw, int &nw, int *rd = nullptr);
 // cin > 0: the downsampling form (bneck_kernels.hip) with a cin-channel input; built for (64, v0,
 // cin 16) and (128, v1, cin 64)
-size_t bneck_lds_bytes(int prec, int C, bool asym, int v, int cin = 0, bool ini = false);
+size_t bneck_lds_bytes(int prec, int C, bool asym, int v, int cin = 0);
 // resident workgroups per CU (occupancy API); 0 if (C, asym, v, tr, cin) is not built
 int bneck_slots_per_cu(int prec, int C, bool asym, int v, bool tr, int cin = 0);
 hipError_t launch_bneck(int prec, int C, bool asym, int v, const BneckArgs &a, hipStream_t s, int cin = 0);
-// the initial block (BGR input, preprocessing fused) + the 16 -> 64 downsampling block in one launch
-// (bneck_kernels.hip, 2-byte storage): false when that form is not built for (prec, C, v, cin)
-bool bneck_init_supported(int prec, int C, int v, int cin);
-hipError_t launch_bneck_init(int prec, int C, int v, const BneckArgs &a, hipStream_t s, int cin);
 
 // ---- fused upsampling bottleneck (up_kernels.hip) ----------------------------------------------
 struct UpArgs {

@@ -79,10 +79,6 @@ struct Plan {
     void *arena = nullptr;
     size_t arena_bytes = 0;
     bool pinned = false;     // a forward on this arena was captured into a graph: never freed before destroy
-    // the last forward ran ops 0 + 1 (initial block on BGR frames + the first downsampling block) as
-    // one launch (launch_bneck_init); plan_op / plan_launch_op then report and launch op 0 as that
-    // pair and op 1 as empty ("fused")
-    bool init_fused = false;
 };
 
 inline int round_up(int v, int m) { return (v + m - 1) / m * m; }
@@ -109,10 +105,11 @@ struct bugseg_ctx {
     void *dev_w = nullptr;
     void *dev_luts = nullptr;                      // [0..15] lut3, [16..31] binary, then 3x256 f64 norm lut
     Plan plan;
-    // preprocess resize tables
-    int pre_key[4] = {0, 0, 0, 0};
-    void *pre_tab = nullptr;
-    size_t pre_tab_bytes = 0;
+    // preprocess resize tables (mode 2), one per recent (H0, W0, H, W): read-only once built, shared by
+    // every stream; pinned: used by a call that was captured into a graph — never evicted while the
+    // context lives (as the BEV and polar tables)
+    struct PreTab { int key[4] = {0, 0, 0, 0}; void *tab = nullptr; bool pinned = false; };
+    std::vector<PreTab> pre_tabs;
     // Private non-blocking stream for one-time table builds: a table is built and waited for there
     // before the caller's work is enqueued, so it never needs a sync of the caller's (or any other)
     // stream, and a first call made while the caller's stream is being captured into a graph works.
@@ -1155,7 +1152,7 @@ int bugseg_destroy(bugseg_ctx *ctx) {
     if (ctx->dev_w) (void)hipFree(ctx->dev_w);
     if (ctx->dev_luts) (void)hipFree(ctx->dev_luts);
     if (ctx->plan.arena) (void)hipFree(ctx->plan.arena);
-    if (ctx->pre_tab) (void)hipFree(ctx->pre_tab);
+    for (auto &t : ctx->pre_tabs) if (t.tab) (void)hipFree(t.tab);
     for (auto &t : ctx->polar_tabs) if (t.tab) (void)hipFree(t.tab);
     for (auto &s : ctx->ls_scratch) if (s.p) (void)hipFree(s.p);
     for (auto &t : ctx->bev_tabs) if (t.tab) (void)hipFree(t.tab);
@@ -1177,7 +1174,12 @@ int bugseg_load_weights(bugseg_ctx *ctx, const void *blob, size_t bytes) {
     ctx->loaded = false;
     if (!pack_all(ctx, why)) return fail(ctx, BUGSEG_EFORMAT, "weight blob: " + why);
     (void)hipDeviceSynchronize();
-    if (ctx->dev_w) { (void)hipFree(ctx->dev_w); ctx->dev_w = nullptr; }
+    if (ctx->dev_w) {
+        // a captured graph's kernels hold pointers into the old weights (and arena): kept until destroy
+        if (ctx->plan.pinned) ctx->graveyard.push_back(ctx->dev_w);
+        else (void)hipFree(ctx->dev_w);
+        ctx->dev_w = nullptr;
+    }
     if (ctx->plan.arena) {
         if (ctx->plan.pinned) ctx->graveyard.push_back(ctx->plan.arena);   // a captured graph may use it
         else (void)hipFree(ctx->plan.arena);
@@ -1221,7 +1223,11 @@ int bugseg_preprocess(bugseg_ctx *ctx, const uint8_t *bgr, int B, int H0, int W0
             a.mode = 2;
             const int key[4] = {H0, W0, H, W};
             const size_t need = (size_t)W * 4 + (size_t)W * 4 + (size_t)H * 4 + (size_t)H * 4;
-            if (!ctx->pre_tab || std::memcmp(key, ctx->pre_key, sizeof(key)) != 0) {
+            const bool cap = stream_capturing(stream);
+            bugseg_ctx::PreTab *hit = nullptr;
+            for (auto &t : ctx->pre_tabs)
+                if (std::memcmp(t.key, key, sizeof(key)) == 0) hit = &t;
+            if (!hit) {
                 std::vector<unsigned char> h(need);
                 int *xo = (int *)h.data();
                 short *xa = (short *)(h.data() + (size_t)W * 4);
@@ -1229,19 +1235,33 @@ int bugseg_preprocess(bugseg_ctx *ctx, const uint8_t *bgr, int B, int H0, int W0
                 short *yb = (short *)(h.data() + (size_t)W * 8 + (size_t)H * 4);
                 linear_coeffs(W, W0, sx, xo, xa);
                 linear_coeffs(H, H0, sy, yo, yb);
-                // the old table may still be read by work enqueued on any stream of this context
-                if (hipDeviceSynchronize() != hipSuccess) return fail(ctx, BUGSEG_EHIP, "device sync failed");
-                if (ctx->pre_tab) (void)hipFree(ctx->pre_tab);
-                ctx->pre_tab = nullptr;
-                if (hipMalloc(&ctx->pre_tab, need) != hipSuccess ||
-                    hipMemcpy(ctx->pre_tab, h.data(), need, hipMemcpyHostToDevice) != hipSuccess) {
-                    ctx->pre_tab = nullptr;
-                    return fail(ctx, BUGSEG_EHIP, "resize table upload failed");
+                if (ctx->pre_tabs.size() >= 4) {            // keep 4 geometries: evict the oldest unpinned one
+                    for (size_t i = 0; i < ctx->pre_tabs.size(); ++i)
+                        if (!ctx->pre_tabs[i].pinned) {
+                            // work enqueued on any stream may still read it: retire syncs (or defers)
+                            retire(ctx, ctx->pre_tabs[i].tab, cap);
+                            ctx->pre_tabs.erase(ctx->pre_tabs.begin() + (long)i);
+                            break;
+                        }
                 }
-                std::memcpy(ctx->pre_key, key, sizeof(key));
-                ctx->pre_tab_bytes = need;
+                // built on the private stream and waited for there, so the caller's stream is never
+                // synchronised and a capture in progress on it stays valid
+                bugseg_ctx::PreTab t;
+                std::memcpy(t.key, key, sizeof(key));
+                RelaxCapture relax;
+                hipStream_t st = setup_stream(ctx);
+                hipError_t e = st ? hipMalloc(&t.tab, need) : hipErrorInvalidValue;
+                if (e == hipSuccess) e = hipMemcpyAsync(t.tab, h.data(), need, hipMemcpyHostToDevice, st);
+                if (e == hipSuccess) e = hipStreamSynchronize(st);
+                if (e != hipSuccess) {
+                    if (t.tab) (void)hipFree(t.tab);
+                    return fail(ctx, BUGSEG_EHIP, std::string("resize table upload failed: ") + hipGetErrorString(e));
+                }
+                ctx->pre_tabs.push_back(t);
+                hit = &ctx->pre_tabs.back();
             }
-            unsigned char *t = (unsigned char *)ctx->pre_tab;
+            if (cap) hit->pinned = true;
+            unsigned char *t = (unsigned char *)hit->tab;
             a.xofs = (const int *)t;
             a.xa = (const short *)(t + (size_t)W * 4);
             a.yofs = (const int *)(t + (size_t)W * 8);
@@ -1261,36 +1281,6 @@ int bugseg_nchw_to_input(bugseg_ctx *ctx, const void *x, int is_f64, int B, int 
     hipError_t e = launch_nchw_to_input(a, (hipStream_t)stream);
     if (e != hipSuccess) return fail(ctx, BUGSEG_EHIP, std::string("layout launch: ") + hipGetErrorString(e));
     return BUGSEG_OK;
-}
-
-// The initial block on raw BGR frames and the 16 -> 64 downsampling block after it, as one launch
-// (bneck_kernels.hip INI form): 2-byte storage, ENet's canonical shapes, both ops planned as the
-// initial-block kernel and the fused down form. Opt-in (BUGSEG_INIT_FUSE=1; results bit-identical):
-// measured slower than the two launches (round 3, fp16, B = 32: 113-121 us vs 43.5 + 49 us) — the
-// fused form holds the BGR patch in LDS (52 KB: 3 workgroups, 12 waves per CU) and its initial-block
-// arithmetic is latency-bound at that occupancy, where the separate kernels run 6-8 waves per SIMD.
-static bool init_fusable(const bugseg_ctx *ctx, const Plan &pl) {
-    const char *on = std::getenv("BUGSEG_INIT_FUSE");
-    if (!on || !*on || *on == '0') return false;
-    if (ctx->prec == PREC_F32 || pl.ops.size() < 3) return false;
-    const Op &o0 = pl.ops[0], &o1 = pl.ops[1];
-    if (o0.kind != 0 || o1.kind != 1 || o1.bn_cin != 16 || o1.bn_c != 64 || o1.bn_asym) return false;
-    if (o0.a.cconv + o0.a.cpool != 16 || o0.a.cpool > 3 || (o0.a.pool_k != 2 && o0.a.pool_k != 3)) return false;
-    if (o0.a.Hg != 2 * o1.bn.H || o0.a.Wg != 2 * o1.bn.W || o0.a.Hin != 2 * o0.a.Hg || o0.a.Win != 2 * o0.a.Wg) return false;
-    if ((double)o0.a.B * o0.a.Hin * o0.a.Win * 3.0 >= 2147483648.0) return false;
-    return bneck_init_supported(ctx->prec, o1.bn_c, o1.bn_var, o1.bn_cin);
-}
-
-static hipError_t launch_init_down(const bugseg_ctx *ctx, const Plan &pl, hipStream_t stream) {
-    const Op &o0 = pl.ops[0], &o1 = pl.ops[1];
-    BneckArgs q = o1.bn;
-    q.bgr = (const uint8_t *)o0.a.in;
-    q.bgr_bytes = (uint32_t)((size_t)o0.a.B * o0.a.Hin * o0.a.Win * 3);
-    q.nlut = o0.a.nlut;
-    q.w0 = o0.a.w; q.kpad0 = o0.a.Kpad;
-    q.b0 = o0.a.bias; q.s0 = o0.a.slope1; q.p0 = o0.a.pscale;
-    q.cconv = o0.a.cconv; q.cpool = o0.a.cpool; q.pool_k = o0.a.pool_k;
-    return launch_bneck_init(ctx->prec, o1.bn_c, o1.bn_var, q, stream, o1.bn_cin);
 }
 
 static int enet_forward(bugseg_ctx *ctx, const void *in, bool bgr, int B, int H, int W, int out_kind, void *out,
@@ -1319,18 +1309,7 @@ static int enet_forward(bugseg_ctx *ctx, const void *in, bool bgr, int B, int H,
     const int nops = (int)pl.ops.size();
     if (last_op < 0 || last_op > nops) last_op = nops;
     if (first_op < 0 || first_op > last_op) return fail(ctx, BUGSEG_EINVAL, "bad op range");
-    int i0 = first_op;
-    if (first_op == 0 && last_op >= 2) {
-        pl.init_fused = bgr && init_fusable(ctx, pl);
-        if (pl.init_fused) {
-            hipError_t e = launch_init_down(ctx, pl, (hipStream_t)stream);
-            if (e != hipSuccess) return fail(ctx, BUGSEG_EHIP, std::string("initial + down launch: ") + hipGetErrorString(e));
-            i0 = 2;
-        }
-    } else if (first_op == 0) {
-        pl.init_fused = false;
-    }
-    for (int i = i0; i < last_op; ++i) {
+    for (int i = first_op; i < last_op; ++i) {
         const Op &op = pl.ops[(size_t)i];
         hipError_t e = op.kind == 1 ? launch_bneck(ctx->prec, op.bn_c, op.bn_asym, op.bn_var, op.bn, (hipStream_t)stream, op.bn_cin)
                      : op.kind == 2 ? launch_up(ctx->prec, op.up_cin, op.up_it, op.up_cout, op.up, (hipStream_t)stream)
@@ -1686,13 +1665,9 @@ int bugseg_plan_info(bugseg_ctx *ctx, int B, int H, int W, int out_kind, int bgr
     const double fin = out_kind == BUGSEG_OUT_LOGITS_F32 ? (double)B * H * W * ctx->ncls * 4 : (double)B * H * W;
     // raw BGR input (bugseg_enet_forward_bgr): 3 bytes per pixel instead of the 8-channel engine input
     double adj = bgr_input ? (double)B * H * W * (8.0 * prec_es(ctx->prec) - 3.0) : 0.0;
-    // ... and the initial block fused into the first downsampling block: its output is neither
-    // written nor read back (plan bytes only; the per-layer figure keeps the unfused definition)
-    const double fused = bgr_input && init_fusable(ctx, ctx->plan)
-                             ? 2.0 * (double)B * (H / 2) * (W / 2) * 16 * prec_es(ctx->prec) : 0.0;
     if (n_launches) *n_launches = (int)ctx->plan.ops.size();
     if (alg_bytes) *alg_bytes = lb + fin - adj;
-    if (plan_bytes) *plan_bytes = pb + fin - adj - fused;
+    if (plan_bytes) *plan_bytes = pb + fin - adj;
     if (flops) *flops = fl;
     return BUGSEG_OK;
 }
@@ -1706,25 +1681,6 @@ int bugseg_plan_op(bugseg_ctx *ctx, int B, int H, int W, int op, char *kernel, i
     if (op < 0 || op >= (int)pl.ops.size()) return fail(ctx, BUGSEG_EINVAL, "op index out of range");
     const Op &o = pl.ops[op];
     std::string tag;
-    if (pl.init_fused && op <= 1) {
-        // op 0: the initial block + the first downsampling block as one launch (BGR in, the down
-        // block's output and indices out); op 1: nothing left to launch
-        const Op &o1 = pl.ops[1];
-        const int es = prec_es(ctx->prec);
-        const double ib = (double)o1.bn.B * 4 * o1.bn.H * 4 * o1.bn.W * 3;      // BGR frames
-        const double x0 = (double)o1.bn.B * 2 * o1.bn.H * 2 * o1.bn.W * 16 * es;   // the initial block's output
-        const double pb = op == 0 ? ib + (o1.bytes - x0) + (double)o.a.Npad * o.a.Kpad * es : 0.0;
-        const double lb = op == 0 ? ib + x0 + (o1.layer_bytes >= 0 ? o1.layer_bytes : o1.bytes) : 0.0;
-        tag = op == 0 ? "init+down C64" : "fused";
-        if (kernel && kernel_len > 0) {
-            std::strncpy(kernel, tag.c_str(), (size_t)kernel_len - 1);
-            kernel[kernel_len - 1] = 0;
-        }
-        if (alg_bytes) *alg_bytes = lb;
-        if (plan_bytes) *plan_bytes = pb;
-        if (flops) *flops = op == 0 ? o.flops + o1.flops : 0.0;
-        return BUGSEG_OK;
-    }
     if (o.kind == 2) {
         tag = "up C" + std::to_string(o.up_cout);
     } else if (o.kind == 1) {
@@ -1766,9 +1722,7 @@ int bugseg_plan_launch_op(bugseg_ctx *ctx, int B, int H, int W, int op, void *st
     if (op < 0 || op >= (int)pl.ops.size()) return fail(ctx, BUGSEG_EINVAL, "op index out of range");
     DeviceGuard g(ctx->device);
     const Op &o = pl.ops[op];
-    if (pl.init_fused && op == 1) return BUGSEG_OK;       // (launched with op 0)
-    hipError_t e = pl.init_fused && op == 0 ? launch_init_down(ctx, pl, (hipStream_t)stream)
-                 : o.kind == 1 ? launch_bneck(ctx->prec, o.bn_c, o.bn_asym, o.bn_var, o.bn, (hipStream_t)stream, o.bn_cin)
+    hipError_t e = o.kind == 1 ? launch_bneck(ctx->prec, o.bn_c, o.bn_asym, o.bn_var, o.bn, (hipStream_t)stream, o.bn_cin)
                  : o.kind == 2 ? launch_up(ctx->prec, o.up_cin, o.up_it, o.up_cout, o.up, (hipStream_t)stream)
                                : launch_conv(ctx->prec, o.nr, o.epi, o.a, (hipStream_t)stream);
     if (e != hipSuccess) return fail(ctx, BUGSEG_EHIP, "launch of op " + std::to_string(op) + ": " + hipGetErrorString(e));

@@ -15,8 +15,6 @@
 // The whole layer's weights (64 rows x 4 taps x 16 channels) live in 32 VGPRs per lane for the
 // kernel's lifetime; the only per-pixel traffic is the B fragments (one 16-B load per lane and tap,
 // the next group's loads in flight while the current group computes) and the class bytes.
-#include <cstdlib>
-
 #include "bugseg_internal.h"
 #include "mfma_common.h"
 
@@ -53,11 +51,8 @@ __device__ __forceinline__ bool nonzero(const RawF &r) {
 
 // Taps: the 2x2 input neighbourhood (dy, dx) = (s >> 1, s & 1) of the k = 3 layer in pack_tconv's
 // order (D = {0, 1}, tap = ty * 2 + tx). LOGITS: the fp32 logits are written too (parity runs).
-// groups whose loads are in flight ahead of the one computing (1: the next; 2: the next two).
-// Measured (round 3, fp16, B = 32): 2 is no faster (37.3 vs 36.9 us per launch; 127 vs 109 VGPRs)
-#ifndef CLS_DEPTH
-#define CLS_DEPTH 1
-#endif
+// The next group's loads are in flight while one computes (two groups ahead measured no faster,
+// round 3: 37.3 vs 36.9 us per launch, 127 vs 109 VGPRs).
 template <typename T, bool LOGITS>
 __global__ void __launch_bounds__(256, sizeof(T) == 2 ? 4 : 1) cls_kernel(const ConvArgs a) {
     constexpr int CLS_TAPS = 4;
@@ -156,7 +151,7 @@ __global__ void __launch_bounds__(256, sizeof(T) == 2 ? 4 : 1) cls_kernel(const 
         // zeros, a neighbour's group is read and dropped), and a static count of loads in flight
         // lets the waits before the MFMAs name only this group's loads (a conditional prefetch
         // made the compiler wait vmcnt(3), i.e. for the next group's first load as well)
-        load(g + CLS_DEPTH * nw, nxt);
+        load(g + nw, nxt);
         const Px q = pixel(g);
         f32x16 acc[2];
 #pragma unroll
@@ -222,156 +217,6 @@ __global__ void __launch_bounds__(256, sizeof(T) == 2 ? 4 : 1) cls_kernel(const 
     };
     Raw xa[CLS_TAPS], xb[CLS_TAPS];
     int g = g0 + wi;
-    if constexpr (CLS_DEPTH == 1) {
-        if (g < g1) load(g, xa);
-        while (g < g1) {
-            step(g, xa, xb);
-            g += nw;
-            if (g >= g1) break;
-            step(g, xb, xa);
-            g += nw;
-        }
-    } else {
-        // two groups ahead: three rotating buffers (the group after next is in flight as well)
-        Raw xc[CLS_TAPS];
-        if (g < g1) {
-            load(g, xa);
-            load(g + nw, xb);
-        }
-        while (g < g1) {
-            step(g, xa, xc);
-            g += nw;
-            if (g >= g1) break;
-            step(g, xb, xa);
-            g += nw;
-            if (g >= g1) break;
-            step(g, xc, xb);
-            g += nw;
-        }
-    }
-}
-
-// fp32 (parity mode): the same layer on v_mfma_f32_16x16x4_f32, one 16 x 16 block per (output phase,
-// tap). The 32 x 32 form above contracts every tap a row block's two phases need for both of them: 12
-// (phase, tap) products per input pixel where the 3 x 3 stride-2 kernel has 9 (phase (0, 0) sees one
-// tap, (0, 1) and (1, 0) two, (1, 1) four) — in fp32, where the f32 MFMA is 16x slower per k than
-// bf16, those zero products made the layer MFMA-bound. Here a (phase, tap) block whose weights are all
-// zero is skipped (a wave-uniform test made once), so the matrix pipe does 9 of 12. The price: a
-// pixel's 16 classes of one phase sit in 4 lanes (rows 4 kq .. 4 kq + 3), so the argmax ends with two
-// lane-swap rounds (v_permlane16_swap / v_permlane32_swap). A wave step is 16 input pixels (lane col);
-// lane kq holds channels 4 kq .. 4 kq + 3 of each tap (one 16-B load per tap); sub-MFMA j contracts
-// channels {4 kq + j}. Same argmax semantics as cls_kernel (NaN-ignoring maximum, its lowest index).
-// Measured SLOWER (round 3, fp32, B = 32 at 480 x 640): 159.6 vs 141.5-142.0 us per launch — 9 of 12
-// products, but 16-pixel steps (twice the per-pixel load / address / store work of the 32 x 32 form)
-// and the two swap rounds per phase; the fp32 bench 14,040-14,073 vs 14,107-14,117 frames/s. Opt-in
-// (BUGSEG_CLS16=1), GPU-tested against the 32 x 32 form.
-template <bool LOGITS>
-__global__ void __launch_bounds__(256, 2) cls16_kernel(const ConvArgs a) {
-    constexpr int TAPS = 4, PH = 4;
-    __shared__ float sbias[64];
-    const int tid = threadIdx.x, lane = tid & 63, col = lane & 15, kq = lane >> 4;
-    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-    if (tid < 64) sbias[tid] = (tid & 15) < a.ncls ? a.bias[tid] : -INFINITY;
-    uint64_t lut64 = 0;
-#pragma unroll
-    for (int c = 0; c < 16; ++c) lut64 |= (uint64_t)((a.lut ? (int)a.lut[c] : c) & 15) << (4 * c);
-    // weights of (phase P, tap s): lane (class col, kq) holds W[16 P + col][16 s + 4 kq .. + 3]
-    float4 wr[PH][TAPS];
-    uint32_t use = 0;                                 // bit 4 P + s: block (P, s) has a nonzero weight
-    {
-        const float *w = reinterpret_cast<const float *>(a.w);
-#pragma unroll
-        for (int P = 0; P < PH; ++P)
-#pragma unroll
-            for (int s = 0; s < TAPS; ++s) {
-                wr[P][s] = *reinterpret_cast<const float4 *>(w + (size_t)(16 * P + col) * a.Kpad + s * 16 + 4 * kq);
-                const float4 v = wr[P][s];
-                use |= (uint32_t)(__ballot(v.x != 0.f || v.y != 0.f || v.z != 0.f || v.w != 0.f) != 0) << (4 * P + s);
-            }
-    }
-    __syncthreads();
-    const auto rin = mkbuf(a.in, a.in_bytes);
-    const int HWg = a.Hg * a.Wg;
-    const size_t plane = (size_t)a.Hout * a.Wout;
-    const int groups = (a.M + 15) >> 4;
-    const int xcd = blockIdx.x & 7, nw = (gridDim.x >> 3) * 4, wi = (blockIdx.x >> 3) * 4 + wave;
-    const int C = (groups + 7) >> 3, g0 = xcd * C, g1 = g0 + C < groups ? g0 + C : groups;
-    const uint32_t pixB = (uint32_t)(a.CinS * 4), rowB = (uint32_t)a.Win * pixB;
-    struct Px { int n, y, x; bool ok; };
-    auto pixel = [&](int g) -> Px {
-        const uint32_t p0 = (uint32_t)g * 16u;
-        const int n0 = (int)(__umulhi(p0, a.mHWg) >> a.sHWg);
-        const uint32_t r = p0 - (uint32_t)(n0 * HWg);
-        const int y0 = (int)(__umulhi(r, a.mWg) >> a.sWg), x0 = (int)r - y0 * a.Wg;
-        Px q;
-        q.ok = (int)p0 + col < a.M;
-        q.x = x0 + col;
-        const bool wrap = q.x >= a.Wg;
-        q.x = wrap ? q.x - a.Wg : q.x;
-        q.y = y0 + (wrap ? 1 : 0);
-        const bool wrapn = q.y >= a.Hg;
-        q.y = wrapn ? 0 : q.y;
-        q.n = n0 + (wrapn ? 1 : 0);
-        return q;
-    };
-    auto load = [&](int g, float4 (&xf)[TAPS]) {
-        const Px q = pixel(g);
-        const uint32_t base = (uint32_t)((q.n * a.Hin + q.y) * a.Win + q.x) * pixB + (uint32_t)(16 * kq);
-        const bool okx = q.x + 1 < a.Win, oky = q.y + 1 < a.Hin;
-        const int vo[TAPS] = {(int)(q.ok ? base : OOB), (int)(q.ok && okx ? base : OOB), (int)(q.ok && oky ? base : OOB),
-                              (int)(q.ok && okx && oky ? base : OOB)};
-#pragma unroll
-        for (int s = 0; s < TAPS; ++s) {
-            const int d = (int)((uint32_t)(s >> 1) * rowB + (uint32_t)(s & 1) * pixB);
-            xf[s] = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(rin, vo[s], d, 0));
-        }
-    };
-    // the 4-lane reductions: the value of lane l ^ 16 / l ^ 32
-    auto x16 = [&](uint32_t v) -> uint32_t { uint32_t p = v, q = v; pl16swap(p, q); return (kq & 1) ? p : q; };
-    // (v_permlane16_swap: odd rows of the first operand <-> even rows of the second; v_permlane32_swap:
-    // upper half of the first <-> lower half of the second)
-    auto x32 = [&](uint32_t v) -> uint32_t { uint32_t p = v, q = v; pl32swap(p, q); return kq < 2 ? q : p; };
-    auto step = [&](int g, const float4 (&cur)[TAPS], float4 (&nxt)[TAPS]) {
-        load(g + nw, nxt);
-        const Px q = pixel(g);
-        int cls[PH];
-#pragma unroll
-        for (int P = 0; P < PH; ++P) {
-            const float4 b4 = *reinterpret_cast<const float4 *>(sbias + 16 * P + 4 * kq);
-            f32x4 acc = {b4.x, b4.y, b4.z, b4.w};
-#pragma unroll
-            for (int s = 0; s < TAPS; ++s) {
-                if (!((use >> (4 * P + s)) & 1u)) continue;   // wave-uniform
-                acc = __builtin_amdgcn_mfma_f32_16x16x4f32(wr[P][s].x, cur[s].x, acc, 0, 0, 0);
-                acc = __builtin_amdgcn_mfma_f32_16x16x4f32(wr[P][s].y, cur[s].y, acc, 0, 0, 0);
-                acc = __builtin_amdgcn_mfma_f32_16x16x4f32(wr[P][s].z, cur[s].z, acc, 0, 0, 0);
-                acc = __builtin_amdgcn_mfma_f32_16x16x4f32(wr[P][s].w, cur[s].w, acc, 0, 0, 0);
-            }
-            if (LOGITS && q.ok) {
-                float *lo = a.logits_out + (size_t)q.n * a.ncls * plane + (size_t)(2 * q.y + (P >> 1)) * a.Wout + 2 * q.x + (P & 1);
-#pragma unroll
-                for (int i = 0; i < 4; ++i)
-                    if (4 * kq + i < a.ncls) lo[(size_t)(4 * kq + i) * plane] = acc[i];
-            }
-            float m = __builtin_fmaxf(__builtin_fmaxf(acc[0], acc[1]), __builtin_fmaxf(acc[2], acc[3]));
-            m = __builtin_fmaxf(m, __builtin_bit_cast(float, x16(__builtin_bit_cast(uint32_t, m))));
-            m = __builtin_fmaxf(m, __builtin_bit_cast(float, x32(__builtin_bit_cast(uint32_t, m))));
-            int bi = 16;
-#pragma unroll
-            for (int i = 3; i >= 0; --i) bi = acc[i] == m ? 4 * kq + i : bi;
-            bi = min(bi, (int)x16((uint32_t)bi));
-            bi = min(bi, (int)x32((uint32_t)bi));
-            cls[P] = (int)(lut64 >> (4 * (bi & 15))) & 15;   // (no class equal to the maximum: 16 -> 0)
-        }
-        // lane kq = 0 / 1 writes output row 2y / 2y + 1: the class bytes of pixels (2x, 2x + 1)
-        if (a.cls_out && q.ok && kq < 2) {
-            const uint32_t c0 = (uint32_t)(kq ? cls[2] : cls[0]), c1 = (uint32_t)(kq ? cls[3] : cls[1]);
-            const size_t o = ((size_t)q.n * a.Hout + 2 * q.y + kq) * a.Wout + 2 * q.x;
-            *reinterpret_cast<uint16_t *>(a.cls_out + o) = (uint16_t)(c0 | (c1 << 8));
-        }
-    };
-    float4 xa[TAPS], xb[TAPS];
-    int g = g0 + wi;
     if (g < g1) load(g, xa);
     while (g < g1) {
         step(g, xa, xb);
@@ -390,12 +235,6 @@ bool cls_supported(const ConvArgs &a) {
            a.Hout == 2 * a.Hg && a.Wout == 2 * a.Wg && a.Hg == a.Hin && a.Wg == a.Win;
 }
 
-// the fp32 16 x 16 form (cls16_kernel, measured slower): BUGSEG_CLS16=1 (read per launch: A/B, tests)
-static bool cls16_on() {
-    const char *e = std::getenv("BUGSEG_CLS16");
-    return e && *e == '1';
-}
-
 hipError_t launch_cls(int prec, const ConvArgs &a, hipStream_t s) {
     // waves stream over 32-pixel groups: enough workgroups to fill every CU at 4 waves per SIMD,
     // a multiple of 8 for the XCD split
@@ -410,14 +249,6 @@ hipError_t launch_cls(int prec, const ConvArgs &a, hipStream_t s) {
     } else if (prec == PREC_F16) {
         if (lg) hipLaunchKernelGGL((cls_kernel<_Float16, true>), dim3(g), dim3(256), 0, s, a);
         else hipLaunchKernelGGL((cls_kernel<_Float16, false>), dim3(g), dim3(256), 0, s, a);
-    } else if (cls16_on()) {
-        // 16-pixel wave steps: twice the groups of the 32 x 32 form
-        int g16 = (a.M + 15) / 16;
-        g16 = (g16 + 3) / 4;
-        g16 = g16 < 2048 ? g16 : 2048;
-        g16 = (g16 + 7) & ~7;
-        if (lg) hipLaunchKernelGGL((cls16_kernel<true>), dim3(g16), dim3(256), 0, s, a);
-        else hipLaunchKernelGGL((cls16_kernel<false>), dim3(g16), dim3(256), 0, s, a);
     } else {
         if (lg) hipLaunchKernelGGL((cls_kernel<float, true>), dim3(g), dim3(256), 0, s, a);
         else hipLaunchKernelGGL((cls_kernel<float, false>), dim3(g), dim3(256), 0, s, a);

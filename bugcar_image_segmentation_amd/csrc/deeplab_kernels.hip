@@ -490,15 +490,11 @@ __device__ __forceinline__ void lds_wait8(u32x4 &a0, u32x4 &a1, u32x4 &a2, u32x4
                  "+v"(b3));
 }
 
-// DL_G2_ABL (debug ablation, wrong results; scripts/gpu_r3s3_c.sh): 1 = no MFMAs, 2 = no operand
-// loads. Measured (round 3, Xception-65 B = 32, the 63 pointwise launches per forward): 4,826 us as
+// Ablation builds (round 3, Xception-65 B = 32, the 63 pointwise launches per forward): 4,826 us as
 // built, 4,454 us without the MFMAs, 3,479 us without the operand loads — the tile is bound by the
 // operand delivery (global -> LDS, 64 B per CU-clock at the MFMA rate for a 128 x 128 tile), not by the
 // matrix pipe. Reading both k-steps' fragments ahead of the first step's MFMAs (opaque asm reads with
 // a counted lgkmcnt) gave wrong results: the register allocator copied a pending read's destination
-#ifndef DL_G2_ABL
-#define DL_G2_ABL 0
-#endif
 
 template <bool OUTF32>
 __global__ void __launch_bounds__(256, 2) dl_gemm128_kernel(const DlConvArgs a) {
@@ -525,7 +521,6 @@ __global__ void __launch_bounds__(256, 2) dl_gemm128_kernel(const DlConvArgs a) 
         sb[i] = xg + (size_t)min(p0 + r, a.M - 1) * a.CS;
     }
     auto stage = [&](int st, __bf16 *buf) {
-        if constexpr (DL_G2_ABL == 2) return;                  // (ablation: no operand traffic)
         const int k0 = st * G2_KT;
         __bf16 *bA = buf + wave * 32 * G2_KT, *bB = bA + G2_T * G2_KT;
 #pragma unroll
@@ -564,12 +559,10 @@ __global__ void __launch_bounds__(256, 2) dl_gemm128_kernel(const DlConvArgs a) 
             wa[r].v = __builtin_bit_cast(uint4, ra[r]);
             bx[r].v = __builtin_bit_cast(uint4, rb[r]);
         }
-        if constexpr (DL_G2_ABL != 1) {
 #pragma unroll
-            for (int j = 0; j < 4; ++j)
+        for (int j = 0; j < 4; ++j)
 #pragma unroll
-                for (int r = 0; r < 4; ++r) mma(acc[j][r], wa[r], bx[j]);
-        }
+            for (int r = 0; r < 4; ++r) mma(acc[j][r], wa[r], bx[j]);
     };
     auto compute = [&](int st, const __bf16 *bA) {
         const bool two = st * G2_KT + 32 < K;                  // (uniform) 32-channel tail stage
@@ -660,462 +653,12 @@ __global__ void __launch_bounds__(256, 2) dl_gemm128_kernel(const DlConvArgs a) 
     }
 }
 
-// ------------------------------------------------------------------ 1x1 conv, deep glds pipeline
-// dl_gemm128_kernel's 128 x 128 tile and 2 x 2 wave layout with k-stages of 32 channels in NBUF LDS
-// buffers of 16 KB ([A | B][128][32]), NBUF - 1 stages in flight. The 128 x 128 kernel keeps one
-// 64-channel stage (32 KB) in flight behind 32 MFMAs per wave: on Xception's middle-flow pointwise
-// layers (728 x 728 over 34,848 pixels at B = 32) a stage then waits about as long as an L2 /
-// Infinity-Cache round trip, not as long as its MFMAs (0.27 of the dense bf16 peak at 55 us per launch).
-// Here 48 KB (NBUF = 4) or 64 KB (NBUF = 5) per workgroup are in flight, one raw barrier per stage:
-//   wait (counted vmcnt) for stage s -> barrier (everyone's share of s landed, everyone done reading
-//   stage s - 1) -> issue stage s + NBUF - 1 into stage s - 1's buffer -> 16 MFMAs per wave on s.
-// LDS rows are 64 B (32 bf16); a ds_read_b128 lane group (lanes {0-3,12-15,20-27}, ... : two k-chunks
-// kq, 16 rows) reads 16 rows at one chunk, so the chunk's physical slot is kq ^ g((row >> 2) & 3) with
-// g = (0, 2, 3, 1): the 16 lanes of every group then cover the 16 bank slots of a 256-B LDS line (the
-// bank slot of (row, slot) is 4 (row & 3) + slot). glds writes lane-linear (lane l: row l >> 2, slot
-// l & 3), so each lane fetches the logical chunk its physical slot holds. Same k-steps, same MFMA, same
-// order, same epilogue: bit-identical to dl_gemm128_kernel (GPU-tested). K = cinP is a multiple of 32
-// (gemm_ok). Measured SLOWER (round 3, Xception-65 B = 32, the 63 pointwise launches per forward):
-// 4,863 us with dl_gemm128_kernel -> 5,211 / 5,482 / 5,644 us at NBUF = 3 / 4 / 5 (597 -> 557 / 529 /
-// 514 TFLOP/s): more stages in flight do not help a tile whose operand delivery, not its load
-// latency, is the bound (DL_G2_ABL above), and a 32-channel stage fetches every 128-B line of a pixel
-// or weight row as two 64-B halves. Opt-in: BUGSEG_DL_GP=3|4|5.
-constexpr int G4_T = 128, G4_KT = 32;
-
-__device__ __forceinline__ int g4_slot(int kc, int row) {
-    // g = (0, 2, 3, 1) as a 2-bit lookup in one constant
-    return kc ^ ((0x78 >> (2 * ((row >> 2) & 3))) & 3);
-}
-
-template <bool OUTF32, int NBUF>
-__global__ void __launch_bounds__(256, 2) dl_gemm128p_kernel(const DlConvArgs a) {
-    static_assert(NBUF >= 3 && NBUF <= 5, "3..5 stage buffers");
-    constexpr int SBUF = 2 * G4_T * G4_KT;                        // elements per stage buffer (16 KB)
-    __shared__ __attribute__((aligned(16))) __bf16 sm[NBUF * SBUF];
-    const int tid = threadIdx.x, lane = tid & 63, col = lane & 15, kq = lane >> 4, wave = tid >> 6;
-    const int wm = wave & 1, wn = wave >> 1;
-    const int ntn = (a.NP + G4_T - 1) / G4_T;
-    const int bid = xcd_block(blockIdx.x, gridDim.x);
-    const int n0 = (bid % ntn) * G4_T, p0 = (bid / ntn) * G4_T;
-    const int K = a.cinP;
-    const __bf16 *wg = reinterpret_cast<const __bf16 *>(a.w), *xg = reinterpret_cast<const __bf16 *>(a.in);
-    // this lane's glds sources: instruction i (0, 1) fills rows (2 wave + i) * 16 + (lane >> 2), physical
-    // slot lane & 3, i.e. logical chunk g4_slot(lane & 3, row) (the map is an involution per row)
-    const __bf16 *sa[2], *sb[2];
-    int kc[2];
-#pragma unroll
-    for (int i = 0; i < 2; ++i) {
-        const int r = (2 * wave + i) * 16 + (lane >> 2);
-        kc[i] = g4_slot(lane & 3, r) * 8;
-        sa[i] = wg + (size_t)min(n0 + r, a.NP - 1) * K;
-        sb[i] = xg + (size_t)min(p0 + r, a.M - 1) * a.CS;
-    }
-    const int nst = K / G4_KT;
-    auto stage = [&](int st) {
-        const int k0 = st * G4_KT;
-        __bf16 *bA = sm + (st % NBUF) * SBUF + wave * 32 * G4_KT, *bB = bA + G4_T * G4_KT;
-#pragma unroll
-        for (int i = 0; i < 2; ++i) {
-            const int k = k0 + kc[i];
-            glds16(sa[i] + k, bA + i * 16 * G4_KT);
-            // channels past the stored CS read the weight row 0's zero padding (columns >= cin)
-            glds16(k < a.CS ? sb[i] + k : wg + k, bB + i * 16 * G4_KT);
-        }
-    };
-    f32x4 acc[4][4];
-#pragma unroll
-    for (int j = 0; j < 4; ++j)
-#pragma unroll
-        for (int r = 0; r < 4; ++r) acc[j][r] = (f32x4){0.f, 0.f, 0.f, 0.f};
-    // this lane's read offsets inside a stage buffer (elements): row = base + col, so the slot only
-    // depends on col
-    const int rslot = g4_slot(kq, col) * 8;
-    auto compute = [&](int st) {
-        const __bf16 *bA = sm + (st % NBUF) * SBUF, *bB = bA + G4_T * G4_KT;
-        u32x4 ra[4], rb[4];
-#pragma unroll
-        for (int r = 0; r < 4; ++r) ra[r] = lds_read16(bA + (wn * 64 + r * 16 + col) * G4_KT + rslot);
-#pragma unroll
-        for (int j = 0; j < 4; ++j) rb[j] = lds_read16(bB + (wm * 64 + j * 16 + col) * G4_KT + rslot);
-        lds_wait8(ra[0], ra[1], ra[2], ra[3], rb[0], rb[1], rb[2], rb[3]);
-        RawB wa[4], bx[4];
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-            wa[r].v = __builtin_bit_cast(uint4, ra[r]);
-            bx[r].v = __builtin_bit_cast(uint4, rb[r]);
-        }
-#pragma unroll
-        for (int j = 0; j < 4; ++j)
-#pragma unroll
-            for (int r = 0; r < 4; ++r) mma(acc[j][r], wa[r], bx[j]);
-    };
-#pragma unroll
-    for (int s = 0; s < NBUF - 1; ++s)
-        if (s < nst) stage(s);
-    for (int st = 0; st < nst; ++st) {
-        // stages issued after st: min(NBUF - 2, nst - 1 - st), 4 glds each (wave-uniform)
-        const int after = min(NBUF - 2, nst - 1 - st);
-        if (after >= 3) asm volatile("s_waitcnt vmcnt(12)" ::: "memory");
-        else if (after == 2) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
-        else if (after == 1) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
-        else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        __builtin_amdgcn_s_barrier();
-        if (st + NBUF - 1 < nst) stage(st + NBUF - 1);   // into stage st - 1's buffer (everyone is past it)
-        compute(st);
-    }
-    // epilogue (dl_gemm128_kernel's): the staging areas overlay the stage buffers
-    __syncthreads();
-    const int nb = n0 + wn * 64;
-    if (nb >= a.NP) return;
-    static_assert(4 * 32 * DL_STG_RS * sizeof(float) <= sizeof(sm), "epilogue staging must fit the stage buffers");
-    float *stg = reinterpret_cast<float *>(sm) + wave * 32 * DL_STG_RS;
-    const int c8 = (lane & 7) * 8;
-    const bool cok = nb + c8 < a.cout;
-#pragma unroll
-    for (int h = 0; h < 2; ++h) {
-        if (h) wave_lds_sync();
-#pragma unroll
-        for (int jj = 0; jj < 2; ++jj) {
-            const int j = 2 * h + jj;
-            const int p = p0 + wm * 64 + j * 16 + col;
-            const int pimg = a.bias_img ? (int)fdiv((uint32_t)(p < a.M ? p : 0), a.mHW, a.sHW) : 0;
-#pragma unroll
-            for (int r = 0; r < 4; ++r) {
-                const int nl = r * 16 + kq * 4, n = nb + nl;
-                float4 v = add4(f4(acc[j][r]), ld4f(a.bias + n));
-                if (a.bias_img) v = add4(v, ld4f(a.bias_img + (size_t)pimg * a.bias_img_stride + n));
-                if (a.act >= 1) v = make_float4(fmaxf(v.x, 0.f), fmaxf(v.y, 0.f), fmaxf(v.z, 0.f), fmaxf(v.w, 0.f));
-                if (a.act == 2) v = make_float4(fminf(v.x, 6.f), fminf(v.y, 6.f), fminf(v.z, 6.f), fminf(v.w, 6.f));
-                *reinterpret_cast<float4 *>(stg + (jj * 16 + col) * DL_STG_RS + nl) = v;
-            }
-        }
-        wave_lds_sync();
-#pragma unroll
-        for (int it = 0; it < 4; ++it) {
-            const int pl = it * 8 + (lane >> 3);
-            const int p = p0 + wm * 64 + h * 32 + pl;
-            if (p >= a.M || !cok) continue;
-            float4 v0 = *reinterpret_cast<const float4 *>(stg + pl * DL_STG_RS + c8);
-            float4 v1 = *reinterpret_cast<const float4 *>(stg + pl * DL_STG_RS + c8 + 4);
-            const int n = nb + c8;
-            if (a.res) {
-                const __bf16 *rp = reinterpret_cast<const __bf16 *>(a.res) + (size_t)p * a.res_cs + n;
-                v0 = add4(v0, ld4(rp));
-                v1 = add4(v1, ld4(rp + 4));
-            }
-            if constexpr (OUTF32) {
-                float *o = reinterpret_cast<float *>(a.out) + (size_t)p * a.out_cs + a.out_off + n;
-                st4(o, v0);
-                st4(o + 4, v1);
-            } else {
-                __bf16 *o = reinterpret_cast<__bf16 *>(a.out) + (size_t)p * a.out_cs + a.out_off + n;
-                st4(o, v0);
-                st4(o + 4, v1);
-            }
-        }
-    }
-}
-
-// ------------------------------------------------------------------ 1x1 conv, 256 x 128 tiles, 2 per CU
-// The 128 x 128 tile is bound by operand delivery (DL_G2_ABL: 92 % of its time with the MFMAs removed):
-// 64 B of operands per CU-clock at the MFMA rate. A 256-pixel x 128-channel tile needs 25 % fewer bytes
-// per FLOP, and with 32-channel k-stages in three 24 KB buffers ([A 128 rows | B 256 rows] x 64 B) two
-// such workgroups still fit a CU (144 KB), so the co-resident workgroup that hides one's barriers and
-// epilogue is kept (the 256 x 256 tile lost it). Eight waves as 4 (pixels) x 2 (channels), each the
-// usual 64 x 64 acc[4][4]; LDS rows and swizzle as dl_gemm128p_kernel (g4_slot); two stages in flight.
-// Same k-steps, same MFMA, same order, same epilogue: bit-identical to dl_gemm128_kernel (GPU-tested).
-// Measured (round 3, Xception-65 B = 32): pointwise 4,797-4,798 -> 4,866-4,870 us per forward (605 ->
-// 596 TFLOP/s): fewer operand bytes per FLOP do not pay here, the 64-B half-line stages cost what they
-// save. Opt-in: BUGSEG_DL_P2=1.
-constexpr int G5_TM = 256, G5_TN = 128, G5_KT = 32, G5_NBUF = 3;
-
-template <bool OUTF32>
-__global__ void __launch_bounds__(512, 4) dl_gemm_p2_kernel(const DlConvArgs a) {
-    constexpr int SBUF = (G5_TN + G5_TM) * G5_KT;                 // elements per stage buffer (24 KB)
-    __shared__ __attribute__((aligned(16))) __bf16 sm[G5_NBUF * SBUF];
-    const int tid = threadIdx.x, lane = tid & 63, col = lane & 15, kq = lane >> 4, wave = tid >> 6;
-    const int wm = wave & 3, wn = wave >> 2;
-    const int ntn = (a.NP + G5_TN - 1) / G5_TN;
-    const int bid = xcd_block(blockIdx.x, gridDim.x);
-    const int n0 = (bid % ntn) * G5_TN, p0 = (bid / ntn) * G5_TM;
-    const int K = a.cinP;
-    const __bf16 *wg = reinterpret_cast<const __bf16 *>(a.w), *xg = reinterpret_cast<const __bf16 *>(a.in);
-    // glds sources: A rows wave * 16 + (lane >> 2) (one instruction), B rows (2 wave + i) * 16 + (lane >> 2)
-    const int ra = wave * 16 + (lane >> 2);
-    const int kca = g4_slot(lane & 3, ra) * 8;
-    const __bf16 *sa = wg + (size_t)min(n0 + ra, a.NP - 1) * K;
-    const __bf16 *sb[2];
-    int kcb[2];
-#pragma unroll
-    for (int i = 0; i < 2; ++i) {
-        const int r = (2 * wave + i) * 16 + (lane >> 2);
-        kcb[i] = g4_slot(lane & 3, r) * 8;
-        sb[i] = xg + (size_t)min(p0 + r, a.M - 1) * a.CS;
-    }
-    const int nst = K / G5_KT;
-    auto stage = [&](int st) {
-        const int k0 = st * G5_KT;
-        __bf16 *bA = sm + (st % G5_NBUF) * SBUF, *bB = bA + G5_TN * G5_KT;
-        glds16(sa + k0 + kca, bA + wave * 16 * G5_KT);
-#pragma unroll
-        for (int i = 0; i < 2; ++i) {
-            const int k = k0 + kcb[i];
-            // channels past the stored CS read the weight row 0's zero padding (columns >= cin)
-            glds16(k < a.CS ? sb[i] + k : wg + k, bB + (2 * wave + i) * 16 * G5_KT);
-        }
-    };
-    f32x4 acc[4][4];
-#pragma unroll
-    for (int j = 0; j < 4; ++j)
-#pragma unroll
-        for (int r = 0; r < 4; ++r) acc[j][r] = (f32x4){0.f, 0.f, 0.f, 0.f};
-    const int rslot = g4_slot(kq, col) * 8;
-    auto compute = [&](int st) {
-        const __bf16 *bA = sm + (st % G5_NBUF) * SBUF, *bB = bA + G5_TN * G5_KT;
-        u32x4 ra4[4], rb4[4];
-#pragma unroll
-        for (int r = 0; r < 4; ++r) ra4[r] = lds_read16(bA + (wn * 64 + r * 16 + col) * G5_KT + rslot);
-#pragma unroll
-        for (int j = 0; j < 4; ++j) rb4[j] = lds_read16(bB + (wm * 64 + j * 16 + col) * G5_KT + rslot);
-        lds_wait8(ra4[0], ra4[1], ra4[2], ra4[3], rb4[0], rb4[1], rb4[2], rb4[3]);
-        RawB wa[4], bx[4];
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-            wa[r].v = __builtin_bit_cast(uint4, ra4[r]);
-            bx[r].v = __builtin_bit_cast(uint4, rb4[r]);
-        }
-#pragma unroll
-        for (int j = 0; j < 4; ++j)
-#pragma unroll
-            for (int r = 0; r < 4; ++r) mma(acc[j][r], wa[r], bx[j]);
-    };
-#pragma unroll
-    for (int q = 0; q < G5_NBUF - 1; ++q)
-        if (q < nst) stage(q);
-    for (int st = 0; st < nst; ++st) {
-        // stages issued after st: min(1, nst - 1 - st), 3 glds each (wave-uniform)
-        if (st + 1 < nst) asm volatile("s_waitcnt vmcnt(3)" ::: "memory");
-        else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        __builtin_amdgcn_s_barrier();
-        if (st + G5_NBUF - 1 < nst) stage(st + G5_NBUF - 1);   // into stage st - 1's buffer
-        compute(st);
-    }
-    __syncthreads();
-    const int nb = n0 + wn * 64;
-    if (nb >= a.NP) return;
-    static_assert(8 * 32 * DL_STG_RS * sizeof(float) <= sizeof(sm), "epilogue staging must fit the stage buffers");
-    float *stg = reinterpret_cast<float *>(sm) + wave * 32 * DL_STG_RS;
-    const int c8 = (lane & 7) * 8;
-    const bool cok = nb + c8 < a.cout;
-#pragma unroll
-    for (int h = 0; h < 2; ++h) {
-        if (h) wave_lds_sync();
-#pragma unroll
-        for (int jj = 0; jj < 2; ++jj) {
-            const int j = 2 * h + jj;
-            const int p = p0 + wm * 64 + j * 16 + col;
-            const int pimg = a.bias_img ? (int)fdiv((uint32_t)(p < a.M ? p : 0), a.mHW, a.sHW) : 0;
-#pragma unroll
-            for (int r = 0; r < 4; ++r) {
-                const int nl = r * 16 + kq * 4, n = nb + nl;
-                float4 v = add4(f4(acc[j][r]), ld4f(a.bias + n));
-                if (a.bias_img) v = add4(v, ld4f(a.bias_img + (size_t)pimg * a.bias_img_stride + n));
-                if (a.act >= 1) v = make_float4(fmaxf(v.x, 0.f), fmaxf(v.y, 0.f), fmaxf(v.z, 0.f), fmaxf(v.w, 0.f));
-                if (a.act == 2) v = make_float4(fminf(v.x, 6.f), fminf(v.y, 6.f), fminf(v.z, 6.f), fminf(v.w, 6.f));
-                *reinterpret_cast<float4 *>(stg + (jj * 16 + col) * DL_STG_RS + nl) = v;
-            }
-        }
-        wave_lds_sync();
-#pragma unroll
-        for (int it = 0; it < 4; ++it) {
-            const int pl = it * 8 + (lane >> 3);
-            const int p = p0 + wm * 64 + h * 32 + pl;
-            if (p >= a.M || !cok) continue;
-            float4 v0 = *reinterpret_cast<const float4 *>(stg + pl * DL_STG_RS + c8);
-            float4 v1 = *reinterpret_cast<const float4 *>(stg + pl * DL_STG_RS + c8 + 4);
-            const int n = nb + c8;
-            if (a.res) {
-                const __bf16 *rp = reinterpret_cast<const __bf16 *>(a.res) + (size_t)p * a.res_cs + n;
-                v0 = add4(v0, ld4(rp));
-                v1 = add4(v1, ld4(rp + 4));
-            }
-            if constexpr (OUTF32) {
-                float *o = reinterpret_cast<float *>(a.out) + (size_t)p * a.out_cs + a.out_off + n;
-                st4(o, v0);
-                st4(o + 4, v1);
-            } else {
-                __bf16 *o = reinterpret_cast<__bf16 *>(a.out) + (size_t)p * a.out_cs + a.out_off + n;
-                st4(o, v0);
-                st4(o + 4, v1);
-            }
-        }
-    }
-}
-
-// ------------------------------------------------------------------ 1x1 conv, 256 x 256 tiles
-// dl_gemm128_kernel's scheme on a 256-pixel x 256-channel tile: eight waves as 4 (pixels) x 2
-// (channels), each 64 pixels x 128 channels (acc[4][8]), k-stages of 64 channels by global_load_lds into
-// two LDS buffers of 64 KB each (one workgroup per CU, 2 waves per SIMD). Per stage and wave: 8 LDS-DMA
-// pieces and 24 ds_read_b128 for 64 MFMAs, where the 128 x 128 tile issues 8 pieces and 16 reads for
-// 32 — the DMA issue and the barriers, not the matrix pipe, bounded that kernel (0.24 of the dense
-// bf16 peak on Xception's pointwise layers). Same swizzle, same k order per output, same epilogue
-// (two 64-channel halves per wave): bit-identical to dl_gemm128_kernel / dl_gemm_kernel. Needs
-// NP % 256 == 0. Measured SLOWER (round 3, Xception-65 B = 32: pointwise 4.87 -> 5.27 ms per forward,
-// 597 -> 550 TFLOP/s; MobileNetV2 unchanged): with one workgroup per CU nothing overlaps a tile's
-// barriers, epilogue and first-stage latency, which the 128 x 128 tile's two co-resident workgroups
-// hide from each other, and 411 tiles on 256 CUs quantise to 2 rounds. Opt-in: BUGSEG_DL_G256=1.
-constexpr int G3_T = 256, G3_KT = 64;
-
-__device__ __forceinline__ void lds_wait12(u32x4 (&a)[8], u32x4 (&b)[4]) {
-    asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(a[0]), "+v"(a[1]), "+v"(a[2]), "+v"(a[3]), "+v"(a[4]), "+v"(a[5]),
-                 "+v"(a[6]), "+v"(a[7]), "+v"(b[0]), "+v"(b[1]), "+v"(b[2]), "+v"(b[3]));
-}
-
-template <bool OUTF32>
-__global__ void __launch_bounds__(512, 1) dl_gemm256_kernel(const DlConvArgs a) {
-    __shared__ __attribute__((aligned(16))) __bf16 sm0[2 * G3_T * G3_KT];   // [A | B][256][64]: 64 KB
-    __shared__ __attribute__((aligned(16))) __bf16 sm1[2 * G3_T * G3_KT];
-    const int tid = threadIdx.x, lane = tid & 63, col = lane & 15, kq = lane >> 4, wave = tid >> 6;
-    const int wm = wave & 3, wn = wave >> 2;
-    const int ntn = a.NP / G3_T;
-    const int bid = xcd_block(blockIdx.x, gridDim.x);
-    const int n0 = (bid % ntn) * G3_T, p0 = (bid / ntn) * G3_T;
-    const int K = a.cinP;
-    const __bf16 *wg = reinterpret_cast<const __bf16 *>(a.w), *xg = reinterpret_cast<const __bf16 *>(a.in);
-    // this lane's glds sources: instruction i fills LDS rows wave * 32 + i * 8 + (lane >> 3), slot lane & 7
-    const __bf16 *sa[4], *sb[4];
-    int kc[4];
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-        const int r = wave * 32 + i * 8 + (lane >> 3);
-        kc[i] = ((lane & 7) ^ ((r >> 1) & 7)) * 8;
-        sa[i] = wg + (size_t)(n0 + r) * K;
-        sb[i] = xg + (size_t)min(p0 + r, a.M - 1) * a.CS;
-    }
-    auto stage = [&](int st, __bf16 *buf) {
-        const int k0 = st * G3_KT;
-        __bf16 *bA = buf + wave * 32 * G3_KT, *bB = bA + G3_T * G3_KT;
-#pragma unroll
-        for (int i = 0; i < 4; ++i) {
-            const int k = k0 + kc[i];
-            glds16(sa[i] + (k < K ? k : 0), bA + i * 8 * G3_KT);
-            // channels past the stored CS read a zero chunk (weight row 0's padding columns k >= CS >= cin)
-            glds16(k < a.CS ? sb[i] + k : wg + k, bB + i * 8 * G3_KT);
-        }
-    };
-    f32x4 acc[4][8];
-#pragma unroll
-    for (int j = 0; j < 4; ++j)
-#pragma unroll
-        for (int r = 0; r < 8; ++r) acc[j][r] = (f32x4){0.f, 0.f, 0.f, 0.f};
-    auto compute = [&](int st, const __bf16 *bA) {
-        const __bf16 *bB = bA + G3_T * G3_KT;
-#pragma unroll
-        for (int s2 = 0; s2 < G3_KT / 32; ++s2) {
-            if (st * G3_KT + s2 * 32 >= K) break;              // (uniform) 32-channel tail stage
-            const int ch = s2 * 4 + kq;
-            u32x4 ra[8], rb[4];
-#pragma unroll
-            for (int r = 0; r < 8; ++r) {
-                const int row = wn * 128 + r * 16 + col;
-                ra[r] = lds_read16(bA + row * G3_KT + ((ch ^ ((row >> 1) & 7)) << 3));
-            }
-#pragma unroll
-            for (int j = 0; j < 4; ++j) {
-                const int row = wm * 64 + j * 16 + col;
-                rb[j] = lds_read16(bB + row * G3_KT + ((ch ^ ((row >> 1) & 7)) << 3));
-            }
-            lds_wait12(ra, rb);
-            RawB wa[8], bx[4];
-#pragma unroll
-            for (int r = 0; r < 8; ++r) wa[r].v = __builtin_bit_cast(uint4, ra[r]);
-#pragma unroll
-            for (int j = 0; j < 4; ++j) bx[j].v = __builtin_bit_cast(uint4, rb[j]);
-#pragma unroll
-            for (int j = 0; j < 4; ++j)
-#pragma unroll
-                for (int r = 0; r < 8; ++r) mma(acc[j][r], wa[r], bx[j]);
-        }
-    };
-    const int nst = (K + G3_KT - 1) / G3_KT;
-    stage(0, sm0);
-    for (int st = 0; st < nst; st += 2) {
-        if (st + 1 < nst) {
-            stage(st + 1, sm1);
-            asm volatile("s_waitcnt vmcnt(8)" ::: "memory");   // this wave's 8 loads of stage st landed
-        } else {
-            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        }
-        __builtin_amdgcn_s_barrier();                          // ... and every other wave's
-        compute(st, sm0);
-        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-        __builtin_amdgcn_s_barrier();                          // sm0 may be refilled (stage st + 2)
-        if (st + 1 >= nst) break;
-        if (st + 2 < nst) {
-            stage(st + 2, sm0);
-            asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
-        } else {
-            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        }
-        __builtin_amdgcn_s_barrier();
-        compute(st + 1, sm1);
-        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-        __builtin_amdgcn_s_barrier();
-    }
-    // epilogue (dl_gemm128_kernel's per 64 channels), per wave: its 64 pixels x 128 channels as two
-    // 64-channel halves, 32 pixels at a time; four waves' 8.7 KB staging areas in each LDS object
-    static_assert(4 * 32 * DL_STG_RS * sizeof(float) <= sizeof(sm0), "epilogue staging must fit one LDS object");
-    float *stg = reinterpret_cast<float *>(wave < 4 ? sm0 : sm1) + (wave & 3) * 32 * DL_STG_RS;
-    const int c8 = (lane & 7) * 8;
-#pragma unroll
-    for (int hn = 0; hn < 2; ++hn) {
-        const int nb = n0 + wn * 128 + hn * 64;
-        const bool cok = nb + c8 < a.cout;
-#pragma unroll
-        for (int h = 0; h < 2; ++h) {
-            if (h || hn) wave_lds_sync();
-#pragma unroll
-            for (int jj = 0; jj < 2; ++jj) {
-                const int j = 2 * h + jj;
-                const int p = p0 + wm * 64 + j * 16 + col;
-                const int pimg = a.bias_img ? (int)fdiv((uint32_t)(p < a.M ? p : 0), a.mHW, a.sHW) : 0;
-#pragma unroll
-                for (int r = 0; r < 4; ++r) {
-                    const int nl = r * 16 + kq * 4, n = nb + nl;
-                    float4 v = add4(f4(acc[j][hn * 4 + r]), ld4f(a.bias + n));
-                    if (a.bias_img) v = add4(v, ld4f(a.bias_img + (size_t)pimg * a.bias_img_stride + n));
-                    if (a.act >= 1) v = make_float4(fmaxf(v.x, 0.f), fmaxf(v.y, 0.f), fmaxf(v.z, 0.f), fmaxf(v.w, 0.f));
-                    if (a.act == 2) v = make_float4(fminf(v.x, 6.f), fminf(v.y, 6.f), fminf(v.z, 6.f), fminf(v.w, 6.f));
-                    *reinterpret_cast<float4 *>(stg + (jj * 16 + col) * DL_STG_RS + nl) = v;
-                }
-            }
-            wave_lds_sync();
-#pragma unroll
-            for (int it = 0; it < 4; ++it) {
-                const int pl = it * 8 + (lane >> 3);
-                const int p = p0 + wm * 64 + h * 32 + pl;
-                if (p >= a.M || !cok) continue;
-                float4 v0 = *reinterpret_cast<const float4 *>(stg + pl * DL_STG_RS + c8);
-                float4 v1 = *reinterpret_cast<const float4 *>(stg + pl * DL_STG_RS + c8 + 4);
-                const int n = nb + c8;
-                if (a.res) {
-                    const __bf16 *rp = reinterpret_cast<const __bf16 *>(a.res) + (size_t)p * a.res_cs + n;
-                    v0 = add4(v0, ld4(rp));
-                    v1 = add4(v1, ld4(rp + 4));
-                }
-                if constexpr (OUTF32) {
-                    float *o = reinterpret_cast<float *>(a.out) + (size_t)p * a.out_cs + a.out_off + n;
-                    st4(o, v0);
-                    st4(o + 4, v1);
-                } else {
-                    __bf16 *o = reinterpret_cast<__bf16 *>(a.out) + (size_t)p * a.out_cs + a.out_off + n;
-                    st4(o, v0);
-                    st4(o + 4, v1);
-                }
-            }
-        }
-    }
-}
+// (Round 3 measured three other tilings of these shapes, all bit-identical and all slower, and removed
+// them: 3-5 stage buffers of 32 channels on the 128 x 128 tile, 4,863 -> 5,211-5,644 us per Xception-65
+// forward at B = 32 (a 32-channel stage fetches every 128-B line as two 64-B halves, and more stages do
+// not help a delivery-bound tile); a 256 x 128 tile two per CU, 4,797 -> 4,866 us; a 256 x 256 tile one
+// per CU, 4.87 -> 5.27 ms (its barriers, epilogue and first-stage latency are no longer hidden by a
+// co-resident workgroup, and 411 tiles on 256 CUs quantise to 2 rounds).)
 
 // ------------------------------------------------------------------ depthwise 3x3
 // One thread = one output pixel x 8 channels; threads with consecutive ids take consecutive channel
@@ -1531,53 +1074,8 @@ static bool gemm128_ok(const DlConvArgs &a) {
     return !(e && *e == '0') && a.cinP >= 256 && a.NP >= 256 && a.NP % 128 == 0 && a.CS % 8 == 0;
 }
 
-// the 256 x 256 tile (opt-in, BUGSEG_DL_G256=1: measured slower, see the kernel): the gemm128 shapes
-// whose output rows come in whole 256-row tiles
-static bool gemm256_ok(const DlConvArgs &a) {
-    const char *e = std::getenv("BUGSEG_DL_G256");
-    return e && *e == '1' && gemm128_ok(a) && a.NP % 256 == 0;
-}
-
-// the deep-pipeline form of the 128 x 128 tile (dl_gemm128p_kernel): BUGSEG_DL_GP = its stage buffers
-// (3, 4 or 5; 0 = the two-buffer dl_gemm128_kernel). Read per launch (tests switch it).
-static int gemm_pipe_bufs() {
-    const char *e = std::getenv("BUGSEG_DL_GP");
-    const int n = e ? std::atoi(e) : 0;
-    return n >= 3 && n <= 5 ? n : 0;
-}
-
-// the 256 x 128 two-per-CU tile (dl_gemm_p2_kernel) for the gemm128 shapes: BUGSEG_DL_P2=1 (A/B)
-static bool gemm_p2_on() {
-    const char *e = std::getenv("BUGSEG_DL_P2");
-    return e && *e == '1';
-}
-
 hipError_t dl_launch_conv(int prec, bool out_f32, const DlConvArgs &a, hipStream_t s) {
     const bool dwf = a.dw_w != nullptr;
-    if (gemm_ok(prec, a) && gemm256_ok(a)) {
-        const dim3 g(((a.M + G3_T - 1) / G3_T) * (a.NP / G3_T));
-        if (out_f32) hipLaunchKernelGGL(dl_gemm256_kernel<true>, g, dim3(512), 0, s, a);
-        else hipLaunchKernelGGL(dl_gemm256_kernel<false>, g, dim3(512), 0, s, a);
-        return hipGetLastError();
-    }
-    if (gemm_p2_on() && gemm_ok(prec, a) && gemm128_ok(a)) {
-        const dim3 g(((a.M + G5_TM - 1) / G5_TM) * ((a.NP + G5_TN - 1) / G5_TN));
-        if (out_f32) hipLaunchKernelGGL(dl_gemm_p2_kernel<true>, g, dim3(512), 0, s, a);
-        else hipLaunchKernelGGL(dl_gemm_p2_kernel<false>, g, dim3(512), 0, s, a);
-        return hipGetLastError();
-    }
-    const int gp = gemm_pipe_bufs();
-    if (gp && gemm_ok(prec, a) && gemm128_ok(a)) {
-        const dim3 g(((a.M + G4_T - 1) / G4_T) * ((a.NP + G4_T - 1) / G4_T));
-#define GP_CASE(NB)                                                                   \
-        if (gp == NB) {                                                               \
-            if (out_f32) hipLaunchKernelGGL((dl_gemm128p_kernel<true, NB>), g, dim3(256), 0, s, a);   \
-            else hipLaunchKernelGGL((dl_gemm128p_kernel<false, NB>), g, dim3(256), 0, s, a);          \
-        }
-        GP_CASE(3) GP_CASE(4) GP_CASE(5)
-#undef GP_CASE
-        return hipGetLastError();
-    }
     if (gemm_ok(prec, a) && gemm128_ok(a)) {
         const dim3 g(((a.M + G2_T - 1) / G2_T) * ((a.NP + G2_T - 1) / G2_T));
         if (out_f32) hipLaunchKernelGGL(dl_gemm128_kernel<true>, g, dim3(256), 0, s, a);

@@ -25,10 +25,6 @@
 namespace bugseg {
 
 
-#ifndef UP_SWZ
-#define UP_SWZ 0
-#endif
-
 template <typename T, int CIN, int I, int COUT>
 __global__ void __launch_bounds__(256, (sizeof(T) == 2 ? (CIN >= 128 ? 2 : 3) : 1)) up_kernel(const UpArgs a) {
     using Raw = typename Tr<T>::Raw;
@@ -50,20 +46,12 @@ __global__ void __launch_bounds__(256, (sizeof(T) == 2 ? (CIN >= 128 ? 2 : 3) : 
     // LDS: weights of the three GEMMs (+16 B row pad) and their per-row constants
     // row pads: bf16 16 elements (row strides 8 / 24 / 40 dwords mod 64: conflict-free ds_read_b128
     // groups, bneck_kernels.hip bneck_padw), fp32 16 B
-    // SWZ (2-byte storage, CIN = 128): unpadded weight rows with the 16-B chunks XOR-swizzled per row
-    // instead of the row pads: 47 -> 39 KB of LDS, 3 -> 4 workgroups per CU. Measured (round 3, fp16,
-    // B = 32): up C64 36.0-36.4 -> 34.9-35.2 us per launch, the 2-stream bench within noise (41.7-41.8k
-    // vs 41.9-42.0k frames/s): opt-in (-DUP_SWZ=1), bit-identical (GPU-tested)
-    constexpr bool SWZ = UP_SWZ && ES == 2 && CIN == 128;
-    constexpr int UPAD = SWZ ? 0 : ES == 2 ? 16 : 16 / ES;
+    // (unpadded rows with XOR-swizzled chunks for CIN = 128 measured no faster in the 2-stream bench,
+    // round 3, and were removed)
+    constexpr int UPAD = ES == 2 ? 16 : 16 / ES;
     constexpr int K1S = CIN + UPAD, K2S = 32 + UPAD, K3S = 32 + UPAD;
-    // element offset of the 8-element chunk c of weight row r (a lane's fragment read): a ds_read_b128 lane group reads 16 rows
-    // (lane col) at one chunk; 256-B rows (K = 128): chunk ^ (row & 15); 64-B rows (K = 32):
-    // chunk ^ g((row >> 2) & 3), g = (0, 2, 3, 1) — 16 distinct bank slots per group either way
-    auto wch = [](int r, int c, int k) -> int {
-        if constexpr (!SWZ) return c * 8;
-        else return (k == 128 ? c ^ (r & 15) : c ^ ((0x78 >> (2 * ((r >> 2) & 3))) & 3)) * 8;
-    };
+    // element offset of the 8-element chunk c of a weight row (a lane's fragment read)
+    auto wch = [](int, int c, int) -> int { return c * 8; };
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     T *w1s = reinterpret_cast<T *>(smem);
     T *w2s = w1s + NR1 * 16 * K1S;
@@ -79,7 +67,7 @@ __global__ void __launch_bounds__(256, (sizeof(T) == 2 ? (CIN >= 128 ? 2 : 3) : 
             for (int i = tid; i < rows * cpr; i += 256) {
                 const int r = i / cpr, c = i - r * cpr;
                 // (c counts 16-B chunks: 8 elements in 2-byte storage, 4 in fp32, where nothing is swizzled)
-                *reinterpret_cast<uint4 *>(dst + (size_t)r * kstride + (SWZ ? wch(r, c, kpad) : c * (16 / ES))) = s[i];
+                *reinterpret_cast<uint4 *>(dst + (size_t)r * kstride + c * (16 / ES)) = s[i];
             }
         };
         stage(w1s, a.w1, NR1 * 16, CIN, K1S);          // pair pack: K = CIN exactly (1x1, CinS = CIN)
@@ -222,7 +210,7 @@ template <typename T, int CIN, int I, int COUT>
 static size_t up_lds() {
     constexpr int ES = (int)sizeof(T);
     constexpr int NR1 = (COUT + I) / 16, NR2 = 4 * I / 16, NR3 = COUT / 16;
-    constexpr int UPAD = UP_SWZ && ES == 2 && CIN == 128 ? 0 : ES == 2 ? 16 : 16 / ES;      // = up_kernel's
+    constexpr int UPAD = ES == 2 ? 16 : 16 / ES;      // = up_kernel's
     return (size_t)(NR1 * 16 * (CIN + UPAD) + NR2 * 16 * (32 + UPAD) + NR3 * 16 * (32 + UPAD)) * ES +
            (size_t)(2 * NR1 * 16 + 2 * NR2 * 16 + 3 * NR3 * 16) * sizeof(float);
 }

@@ -109,6 +109,67 @@ def test_captured_pipeline_laserscan_and_first_call(gpu, blocks, streams, lasers
     assert torch.equal(grids, ref_b)
 
 
+@pytest.mark.parametrize("warm", [False, True])
+def test_captured_pipeline_with_resize_then_other_geometry(gpu, blocks, warm):
+    """frames NOT at the model resolution (the resize table of bugseg_preprocess mode 2).
+    The capture (warm or the very first call) builds that table on the private stream; an eager
+    step at a third source resolution afterwards builds another one and must not free the table
+    the graph reads: the replay still equals an eager pipeline."""
+    H, W, B = 96, 128, 4
+    H0, W0 = 131, 170                                   # not 2x: the fixed-point linear resize
+    bev = _fresh_bev(H, W, 300, 300, 40 + int(warm))
+    grid = (3.0, 3.0, 0.05)
+    fa = torch.from_numpy(synthetic.road_frames(B, H0, W0, seed=51)).to(gpu)
+    fb = torch.from_numpy(synthetic.road_frames(B, H0, W0, seed=52)).to(gpu)
+    fc = torch.from_numpy(synthetic.road_frames(B, 110, 150, seed=53)).to(gpu)
+    eager = OccupancyPipeline(ENET(weights=blocks, precision="fp16"), bev, *grid, model_hw=(H, W))
+    ref_a, ref_b, ref_c = eager.run(fa).clone(), eager.run(fb).clone(), eager.run(fc).clone()
+    pipe = OccupancyPipeline(ENET(weights=blocks, precision="fp16"), bev, *grid, model_hw=(H, W))
+    buf = fa.clone()
+    replay, grids = pipe.capture(buf, warm=warm)
+    replay()
+    torch.cuda.synchronize()
+    assert torch.equal(grids, ref_a)
+    # an eager step at a third source resolution (another resize table) on the same context
+    out_c = torch.empty_like(grids)
+    pipe.run(fc, out=out_c)
+    torch.cuda.synchronize()
+    assert torch.equal(out_c, ref_c)
+    buf.copy_(fb)
+    replay()
+    torch.cuda.synchronize()
+    assert torch.equal(grids, ref_b)
+
+
+def test_weight_reload_keeps_captured_graph_memory(gpu, blocks):
+    """load_weights after a capture keeps the old weights (and arena) the graph's kernels
+    point at until the context is destroyed, so replaying the old graph still computes with the old
+    weights, and eager forwards use the new ones."""
+    H, W, B = 64, 96, 2
+    frames = torch.from_numpy(synthetic.road_frames(B, H, W, seed=61)).to(gpu)
+    other = enet_spec.build_enet(seed=77)
+    m = ENET(weights=blocks, precision="fp16")
+    seg = torch.empty((B, H, W), dtype=torch.uint8, device=gpu)
+    m.ctx.forward_bgr(frames, B, H, W, N.OUT_CLASS15_U8, seg)
+    want_old = seg.clone()
+    torch.cuda.synchronize()
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g):
+        m.ctx.forward_bgr(frames, B, H, W, N.OUT_CLASS15_U8, seg)
+    ref_new = ENET(weights=other, precision="fp16")
+    want_new = torch.empty_like(seg)
+    ref_new.ctx.forward_bgr(frames, B, H, W, N.OUT_CLASS15_U8, want_new)
+    m.ctx.load_weights(ref_new.blob)                    # the old weights go to the graveyard
+    seg.zero_()
+    g.replay()
+    torch.cuda.synchronize()
+    assert torch.equal(seg, want_old)
+    fresh = torch.empty_like(seg)
+    m.ctx.forward_bgr(frames, B, H, W, N.OUT_CLASS15_U8, fresh)
+    torch.cuda.synchronize()
+    assert torch.equal(fresh, want_new)
+
+
 def _free_port():
     s = socket.socket()
     s.bind(("127.0.0.1", 0))

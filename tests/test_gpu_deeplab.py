@@ -260,41 +260,24 @@ def test_xception_from_frozen_graphdef(gpu, tmp_path, style):
     assert np.abs(_gpu_logits(model) - lg).max() < LOGIT_TOL
 
 
-@pytest.mark.parametrize("mode", ["g128_vs_g64", "g256_vs_g128", "gp3_vs_g128", "gp4_vs_g128", "gp5_vs_g128", "p2_vs_g128"])
 @pytest.mark.parametrize("which", ["mobilenet", "xception"])
-def test_deeplab_gemm128_bit_identical(gpu, monkeypatch, which, mode):
+def test_deeplab_gemm128_bit_identical(gpu, monkeypatch, which):
     """The 128 x 128 glds GEMM of the deep, wide 1x1s (K >= 256, N >= 256: the ASPP 1x1s and
     projection, Xception's pointwise layers) against the 256 x 64 register-staged one
-    (BUGSEG_DL_G128=0), and the opt-in 256 x 256 tile (BUGSEG_DL_G256=1, whole 256-row N tiles)
-    against the 128 x 128 one: the same k-steps through the same MFMA in the same order -> identical
+    (BUGSEG_DL_G128=0): the same k-steps through the same MFMA in the same order -> identical
     logits and class maps, over pixel tails, 32-channel k tails (cinP 736 = 11.5 stages),
     stored-channel tails (CS 728 < cinP), output-channel tails (cout < NP), residual and per-image-bias
-    epilogues. gpN: the deep-pipeline form (BUGSEG_DL_GP=N stage buffers of 32 channels, swizzled
-    64-B LDS rows) against the two-buffer 128 x 128 tile; p2: the 256 x 128 two-per-CU tile
-    (BUGSEG_DL_P2=1) against it."""
+    epilogues."""
     if which == "mobilenet":
         net = S.build_deeplab(width=1.0, crop=97, atrous_rates=(6,))
         x = _frames(3, 97, 90, 43)
     else:
         net = X.build_deeplab_xception(width=1.0, middle=1, crop=65)   # 728 channels: cinP 736 = 11.5 stages
         x = _frames(2, 65, 60, 44)
-    if mode == "g256_vs_g128":
-        monkeypatch.setenv("BUGSEG_DL_G256", "1")
-    elif mode.startswith("gp"):
-        monkeypatch.setenv("BUGSEG_DL_GP", mode[2])
-    elif mode == "p2_vs_g128":
-        monkeypatch.setenv("BUGSEG_DL_P2", "1")
     a_model = DeepLabV3(net=net, precision="bf16")
     a = a_model.predict(x)
     la = a_model.logits_device().cpu()
-    if mode == "g256_vs_g128":
-        monkeypatch.delenv("BUGSEG_DL_G256")
-    elif mode.startswith("gp"):
-        monkeypatch.setenv("BUGSEG_DL_GP", "0")
-    elif mode == "p2_vs_g128":
-        monkeypatch.setenv("BUGSEG_DL_P2", "0")
-    else:
-        monkeypatch.setenv("BUGSEG_DL_G128", "0")
+    monkeypatch.setenv("BUGSEG_DL_G128", "0")
     b_model = DeepLabV3(net=net, precision="bf16")
     b = b_model.predict(x)
     assert torch.equal(la, b_model.logits_device().cpu())

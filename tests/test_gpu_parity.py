@@ -299,39 +299,6 @@ def test_forward_bgr_equals_preprocess_then_forward(gpu, prec, pool_k):
     assert torch.equal(m.predict_device(x2, N.OUT_LOGITS_F32), c)
 
 
-@pytest.mark.parametrize("grid", [None, "8"])
-@pytest.mark.parametrize("prec", ["bf16", "fp16"])
-@pytest.mark.parametrize("pool_k", [3, 2])
-@pytest.mark.parametrize("B,H,W", [(2, 72, 104), (1, 480, 640), (3, 96, 128)])
-def test_initial_block_fused_into_down1_bit_identical(gpu, prec, pool_k, B, H, W, grid, monkeypatch):
-    """With BUGSEG_INIT_FUSE=1, forward_bgr in 2-byte storage runs the initial block (preprocess
-    fused) inside the first downsampling block's launch (bneck_kernels.hip INI form: the initial
-    block's output never leaves the chip). Logits and the class map are bit-identical to the two
-    launches (the default), at partial tiles, several frames, both pool windows, and with every
-    workgroup walking many tiles (BUGSEG_BNECK_GRID=8)."""
-    bl = enet_spec.build_enet(seed=19, initial_pool_k=pool_k)
-    m = ENET(weights=bl, precision=prec)
-    bgr = torch.from_numpy(synthetic.road_frames(B, H, W, seed=H + pool_k)).cuda()
-    if grid is not None:
-        monkeypatch.setenv("BUGSEG_BNECK_GRID", grid)
-    monkeypatch.setenv("BUGSEG_INIT_FUSE", "1")
-    a = torch.empty((B, 15, H, W), dtype=torch.float32, device=gpu)
-    m.ctx.forward_bgr(bgr, B, H, W, N.OUT_LOGITS_F32, a)
-    ca = torch.empty((B, H, W), dtype=torch.uint8, device=gpu)
-    m.ctx.forward_bgr(bgr, B, H, W, N.OUT_CLASS3_U8, ca)
-    torch.cuda.synchronize()
-    assert m.ctx.plan_op(B, H, W, 0)[0] == "init+down C64"
-    monkeypatch.delenv("BUGSEG_INIT_FUSE")
-    b = torch.empty_like(a)
-    m.ctx.forward_bgr(bgr, B, H, W, N.OUT_LOGITS_F32, b)
-    cb = torch.empty_like(ca)
-    m.ctx.forward_bgr(bgr, B, H, W, N.OUT_CLASS3_U8, cb)
-    torch.cuda.synchronize()
-    assert m.ctx.plan_op(B, H, W, 0)[0] == "init"
-    assert torch.equal(a, b)
-    assert torch.equal(ca, cb)
-
-
 @pytest.mark.parametrize("variant", [None, "0", "1", "2", "3", "4"])
 @pytest.mark.parametrize("prec", ["fp32", "bf16", "fp16"])
 @pytest.mark.parametrize("H,W", [(64, 96), (72, 104), (120, 160), (480, 640)])
@@ -365,9 +332,7 @@ def test_fused_bottlenecks_equal_unfused(gpu, blocks, prec, H, W, variant, monke
 @pytest.mark.parametrize("H,W", [(72, 104), (480, 640)])
 def test_fused_bottlenecks_multi_tile_walks(gpu, blocks, prec, H, W, variant, grid, monkeypatch):
     """Every fused bottleneck launch on a small grid (BUGSEG_BNECK_GRID: 8 workgroups, or half the
-    resident slots), so each workgroup walks several tiles and the kept-residual forms prefetch the
-    next tile's interior x under the current tile's expansion (BNECK_PIPE): bit-identical to the
-    unfused chain."""
+    resident slots), so each workgroup walks several tiles: bit-identical to the unfused chain."""
     B = 2
     bgr = torch.from_numpy(synthetic.road_frames(B, H, W, seed=H + 1)).cuda()
     if variant is not None:
@@ -435,39 +400,10 @@ def test_class_layer_kernel_matches_conv_path(gpu, blocks, prec, monkeypatch):
     assert (la.argmax(axis=1)[decided] == lb.argmax(axis=1)[decided]).all()
 
 
-@pytest.mark.parametrize("ncls", [3, 15, 16])
-def test_fp32_class_layer_16x16_form(gpu, ncls, monkeypatch):
-    """The fp32 class layer on 16 x 16 x 4 MFMAs (cls16_kernel: one block per (output phase, tap), the
-    all-zero (phase, tap) blocks of the 3 x 3 stride-2 kernel skipped, argmax across the 4 lanes of a
-    pixel's classes; opt-in BUGSEG_CLS16=1, measured slower) against the 32 x 32 form: logits to rounding (the two sum the
-    same products in different orders), and its class map exactly the argmax of its own logits, at
-    3 / 15 / 16 classes over ragged pixel groups (W = 200: 16-pixel groups wrap rows)."""
-    bl = enet_spec.build_enet(seed=40 + ncls, num_classes=ncls)
-    H, W = 96, 200
-    bgr = torch.from_numpy(synthetic.road_frames(3, H, W, seed=ncls)).cuda()
-    out = {}
-    for form in ("1", "0"):
-        monkeypatch.setenv("BUGSEG_CLS16", form)
-        m = ENET(weights=bl, precision="fp32")
-        lg = torch.empty((3, ncls, H, W), dtype=torch.float32, device=gpu)
-        m.ctx.forward_bgr(bgr, 3, H, W, N.OUT_LOGITS_F32, lg)
-        raw = torch.empty((3, H, W), dtype=torch.uint8, device=gpu)
-        m.ctx.forward_bgr(bgr, 3, H, W, N.OUT_CLASS15_U8, raw)
-        out[form] = (lg.cpu().numpy(), raw.cpu().numpy())
-    (la, ra), (lb, rb) = out["1"], out["0"]
-    np.testing.assert_allclose(la, lb, rtol=0, atol=1e-5 * max(1.0, float(np.abs(lb).max())))
-    assert np.array_equal(ra, la.argmax(axis=1))
-    assert np.array_equal(rb, lb.argmax(axis=1))
-    decided = _decided(lb, la, what=f"fp32 class layer 16x16 vs 32x32 ({ncls} classes)")
-    assert (ra[decided] == rb[decided]).all()
-
-
 def test_canonical_plan_is_one_launch_per_block(gpu, blocks, monkeypatch):
     """At the bench shape every ENet block of the canonical graph runs as ONE fused launch: initial
     block, 2 downsampling, 23 regular / dilated / asymmetric bottlenecks, 2 upsampling blocks and
-    the class layer (29 launches); the unfused reference plan has one launch per convolution. With
-    BUGSEG_INIT_FUSE=1, on raw BGR frames in 2-byte storage, the initial block runs inside the first
-    downsampling block's launch (28 launches); from the engine input (or in fp32) it is its own."""
+    the class layer (29 launches); the unfused reference plan has one launch per convolution."""
     B, H, W = 2, 480, 640
     m = ENET(weights=blocks, precision="bf16")
     bgr = torch.from_numpy(synthetic.uniform_frames(B, H, W)).cuda()
@@ -480,10 +416,6 @@ def test_canonical_plan_is_one_launch_per_block(gpu, blocks, monkeypatch):
     assert [t.split(" ")[0] + " " + t.split(" ")[1] for t in tags if t.startswith(("down", "up"))] == \
         ["down C64", "down C128", "up C64", "up C16"]
     assert sum(t.startswith("bneck") for t in tags) == 23
-    monkeypatch.setenv("BUGSEG_INIT_FUSE", "1")
-    m.ctx.forward_bgr(bgr, B, H, W, N.OUT_CLASS3_U8, seg)
-    tags = [m.ctx.plan_op(B, H, W, i)[0] for i in range(n)]
-    assert tags[0] == "init+down C64" and tags[1] == "fused" and tags[2].startswith("bneck C64")
     x = ENET.preprocess_device(bgr, N.PRE_ENGINE, ctx=m.ctx, width=W, height=H)
     m.predict_device(x, N.OUT_CLASS3_U8)
     tags = [m.ctx.plan_op(B, H, W, i)[0] for i in range(n)]
