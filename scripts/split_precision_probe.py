@@ -1,0 +1,88 @@
+"""CPU experiment: how close to the fp32 oracle would the fp32 parity mode stay if its MFMA products
+were split-bf16 (hi/lo halves of both operands, 3 or 6 bf16 products per f32 product, f32 sums)
+instead of exact f32 products? Emulates the engine's fp32 numerics (BN folded, f32 storage) with the
+conv products replaced, at 480x640, and reports max |dlogit| against the fp32 oracle and the share of
+pixels a 2.5x-error margin would excuse (tests/test_gpu_parity.py _decided)."""
+import sys, os
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+import numpy as np
+import torch
+import torch.nn.functional as F
+from bugcar_image_segmentation_amd import enet_spec
+from oracle import enet_oracle as eo
+
+torch.set_num_threads(8)
+conv2d, convt = F.conv2d, F.conv_transpose2d
+
+
+def bf(t):
+    return t.to(torch.bfloat16).to(torch.float32)
+
+
+def trunc(t):
+    return (t.view(torch.int32) & ~0xffff).view(torch.float32)
+
+
+def hf(t):
+    return t.to(torch.float16).to(torch.float32)
+
+
+def split(t, n, mode):
+    parts = []
+    r = t
+    for _ in range(n):
+        h = bf(r) if mode == "rne" else hf(r) if mode == "f16" else trunc(r)
+        parts.append(h)
+        r = r - h
+    return parts
+
+
+def make(n_x, n_w, terms, mode, wscale=0):
+    def wrap(fn):
+        def f(x, w, b=None, *args, **kw):
+            xs, ws = split(x, n_x, mode), split(w * 2.0 ** wscale, n_w, mode)
+            ws = [q * 2.0 ** -wscale for q in ws]
+            y = None
+            for (i, j) in sorted(terms, key=lambda ij: -(ij[0] + ij[1])):   # small terms first
+                if i < len(xs) and j < len(ws):
+                    t = fn(xs[i], ws[j], None, *args, **kw).double()
+                    y = t if y is None else y + t
+            y = y.float()
+            if b is not None:
+                y = y + b.view(1, -1, 1, 1)
+            return y
+        return f
+    return wrap
+
+
+def run(blocks, x, cfg):
+    if cfg is None:
+        F.conv2d, F.conv_transpose2d = conv2d, convt
+    else:
+        F.conv2d, F.conv_transpose2d = make(*cfg)(conv2d), make(*cfg)(convt)
+    try:
+        return eo.forward_storage(blocks, x, torch.float32)
+    finally:
+        F.conv2d, F.conv_transpose2d = conv2d, convt
+
+
+blocks = enet_spec.build_enet()
+H, W = (int(sys.argv[1]), int(sys.argv[2])) if len(sys.argv) > 2 else (480, 640)
+x = np.random.default_rng(7).normal(size=(1, 3, H, W)).astype(np.float32)
+ref = eo.forward(blocks, x)
+s = np.sort(ref, axis=1)
+margin = s[:, -1] - s[:, -2]
+cfgs = {"f32 products (folded, f32 storage)": None,
+        "bf16x3 rne (hh, hl, lh)": (2, 2, [(0, 0), (0, 1), (1, 0)], "rne"),
+        "f16x3 (hh, hl, lh)": (2, 2, [(0, 0), (0, 1), (1, 0)], "f16"),
+        "f16x3, weights x2^8": (2, 2, [(0, 0), (0, 1), (1, 0)], "f16", 8),
+        "f16x4 (+ll), weights x2^8": (2, 2, [(0, 0), (0, 1), (1, 0), (1, 1)], "f16", 8),
+        "x3-split x, w 2-split rne (5 terms)": (3, 2, [(0, 0), (0, 1), (1, 0), (1, 1), (2, 0)], "rne"),
+        "bf16x6 rne": (3, 3, [(0, 0), (0, 1), (1, 0), (1, 1), (0, 2), (2, 0)], "rne")}
+for name, cfg in cfgs.items():
+    got = run(blocks, x, cfg)
+    err = float(np.abs(got - ref).max())
+    thr = max(2.5 * err, 1e-5)
+    exc = float((margin <= thr).mean())
+    agree = float((got.argmax(1) == ref.argmax(1)).mean())
+    print(f"{name:40s} max|d| {err:.2e} mean|d| {np.abs(got - ref).mean():.2e} excused {exc:.2e} agreement {agree:.6f}", flush=True)
