@@ -141,6 +141,7 @@ void bneck_shape(int C, int v, int &th, int &tw, int &nw, int *rd) {
 template <typename T, int C, bool ASYM, int V, bool TR, int CI = 0>
 __global__ void __launch_bounds__((BShape<C, V>::NW * 64), (sizeof(T) == 2 ? BShape<C, V>::OCC : C == 16 ? BNECK_F32_OCC16 : 1)) bneck_kernel(const BneckArgs a) {
     using Raw = typename Tr<T>::Raw;
+    using WRaw = typename WTr<T>::Raw;   // weight operand (fp32 mode: split-f16 parts)
     constexpr int TH = BShape<C, V>::TH, TW = BShape<C, V>::TW, NW = BShape<C, V>::NW, NT = NW * 64;
     constexpr int I = CI > 0 ? CI / 4 : C / 4;      // internal channels (ENet: input / 4)
     constexpr int IS = I < 8 ? 8 : I;                 // stored internal channels (8-channel groups)
@@ -621,7 +622,7 @@ __global__ void __launch_bounds__((BShape<C, V>::NW * 64), (sizeof(T) == 2 ? BSh
             for (int s = 0; s < KS1; ++s)
 #pragma unroll
                 for (int r = 0; r < NR1; ++r) {
-                    Raw wf;
+                    WRaw wf;
                     ld8(wf, w1 + (r * 16 + col) * K1S + s * 32 + kq * 8);
                     mma(acc[r], wf, xs[s]);
                 }
@@ -778,7 +779,7 @@ __global__ void __launch_bounds__((BShape<C, V>::NW * 64), (sizeof(T) == 2 ? BSh
                 for (int s = 0; s < KS1; ++s)
 #pragma unroll
                     for (int r = 0; r < NR1; ++r) {
-                        Raw wf;
+                        WRaw wf;
                         ld8(wf, w1 + (r * 16 + col) * K1S + s * 32 + kq * 8);
                         mma(acc[r], wf, xf[c][s]);
                     }
@@ -876,7 +877,7 @@ __global__ void __launch_bounds__((BShape<C, V>::NW * 64), (sizeof(T) == 2 ? BSh
                 const int ky = tap / 3, kx = tap - ky * 3;
                 // tap offset in tile axes (RD: the column offset is (kx - 1) d inside the tile)
                 const int ti = tr ? kx : ky, tj = RD ? (kx - 1) * dt : tr ? ky : kx;
-                Raw wf[NR1];
+                WRaw wf[NR1];
 #pragma unroll
                 for (int r = 0; r < NR1; ++r) ld8(wf[r], w2 + (r * 16 + col) * K2S + s * 32 + kq * 8);
 #pragma unroll
@@ -908,7 +909,7 @@ __global__ void __launch_bounds__((BShape<C, V>::NW * 64), (sizeof(T) == 2 ? BSh
             for (int s = 0; s < KS2; ++s) {
                 const int g = s * 4 + kq;
                 const int tap = g / (IS / 8), coff = (g - tap * (IS / 8)) * 8;
-                Raw wf[NR1];
+                WRaw wf[NR1];
 #pragma unroll
                 for (int r = 0; r < NR1; ++r) ld8(wf[r], w2 + (r * 16 + col) * K2S + s * 32 + kq * 8);
 #pragma unroll
@@ -949,7 +950,7 @@ __global__ void __launch_bounds__((BShape<C, V>::NW * 64), (sizeof(T) == 2 ? BSh
                 for (int s = 0; s < KS2; ++s) {
                     const int g = s * 4 + kq;
                     const int tap = g / (IS / 8), coff = (g - tap * (IS / 8)) * 8;
-                    Raw wf[NR1];
+                    WRaw wf[NR1];
 #pragma unroll
                     for (int r = 0; r < NR1; ++r) ld8(wf[r], w2b + (r * 16 + col) * K2S + s * 32 + kq * 8);
 #pragma unroll
@@ -1003,7 +1004,7 @@ __global__ void __launch_bounds__((BShape<C, V>::NW * 64), (sizeof(T) == 2 ? BSh
                             const int r = h * (NR3 / 2) + rr;
                             const int ch = r * 16 + kq * 4;
                             f32x4 acc = bias_in_acc(NR3, 1) ? bias4(cb3 + ch) : (f32x4){0.f, 0.f, 0.f, 0.f};
-                            Raw wf;
+                            WRaw wf;
                             ld8(wf, w3 + (r * 16 + col) * K3S + kq * 8);
                             mma(acc, wf, tf[j]);
                             T *sp = stg + col * OSTR + (ch - h * (C / 2));
@@ -1045,7 +1046,7 @@ __global__ void __launch_bounds__((BShape<C, V>::NW * 64), (sizeof(T) == 2 ? BSh
                 for (int r = 0; r < NR3; ++r) {
                     const int ch = r * 16 + kq * 4;
                     f32x4 acc = bias_in_acc(NR3, 1) ? bias4(cb3 + ch) : (f32x4){0.f, 0.f, 0.f, 0.f};
-                    Raw wf;
+                    WRaw wf;
                     ld8(wf, w3 + (r * 16 + col) * K3S + kq * 8);
                     mma(acc, wf, tf[j]);
                     T *sp = stg + col * OSTR + ch;
@@ -1087,7 +1088,7 @@ __global__ void __launch_bounds__((BShape<C, V>::NW * 64), (sizeof(T) == 2 ? BSh
                     const int r0 = 2 * t, r1 = 2 * t + 1;
                     f32x4 acc0 = bias_in_acc(NR3, 1) ? bias4(cb3 + r0 * 16 + kq * 4) : (f32x4){0.f, 0.f, 0.f, 0.f};
                     f32x4 acc1 = bias_in_acc(NR3, 1) ? bias4(cb3 + r1 * 16 + kq * 4) : (f32x4){0.f, 0.f, 0.f, 0.f};
-                    Raw w0, w1;
+                    WRaw w0, w1;
                     ld8(w0, w3 + (r0 * 16 + col) * K3S + kq * 8);
                     ld8(w1, w3 + (r1 * 16 + col) * K3S + kq * 8);
                     mma(acc0, w0, tf[j]);
@@ -1117,7 +1118,7 @@ __global__ void __launch_bounds__((BShape<C, V>::NW * 64), (sizeof(T) == 2 ? BSh
                 } else {
                     const int r = t;
                     f32x4 acc = bias_in_acc(NR3, 1) ? bias4(cb3 + r * 16 + kq * 4) : (f32x4){0.f, 0.f, 0.f, 0.f};
-                    Raw wf;
+                    WRaw wf;
                     ld8(wf, w3 + (r * 16 + col) * K3S + kq * 8);
                     mma(acc, wf, tf[j]);
                     if constexpr (HALF) {

@@ -276,6 +276,14 @@ uint16_t f32_to_f16(float f) {
     if (rem > 0x1000u || (rem == 0x1000u && (h & 1u))) ++h;   // may carry into the exponent (-> inf): correct
     return (uint16_t)(sign | h);
 }
+// the float value of IEEE binary16 bits (exact)
+float f16_to_f32(uint16_t h) {
+    const float s = (h & 0x8000u) ? -1.f : 1.f;
+    const int e = (h >> 10) & 31, m = h & 1023;
+    if (e == 31) return m ? std::nanf("") : s * INFINITY;
+    if (e == 0) return s * std::ldexp((float)m, -24);
+    return s * std::ldexp((float)(m | 1024), e - 25);
+}
 
 struct Packer {
     int prec;
@@ -303,8 +311,18 @@ struct Packer {
             }
             return push(h.data(), h.size() * 2);
         }
-        std::vector<float> h(w.begin(), w.end());
-        return push(h.data(), h.size() * 4);
+        // fp32 parity mode: the split-f16 operand of mfma_common.h (RawS): per 8 consecutive k of a
+        // row (rows are whole 32-k steps), the 8 hi parts f16(w) then the 8 lo parts f16(w - hi),
+        // w rounded to f32 first (the f32 weight the exact-product path used)
+        std::vector<uint16_t> h(w.size() * 2);
+        for (size_t g = 0; g < w.size(); g += 8)
+            for (size_t i = 0; i < 8 && g + i < w.size(); ++i) {
+                const float f = (float)w[g + i];
+                const uint16_t hi = f32_to_f16(f);
+                h[2 * g + i] = hi;
+                h[2 * g + 8 + i] = f32_to_f16(f - f16_to_f32(hi));   // exact difference in f32
+            }
+        return push(h.data(), h.size() * 2);
     }
     size_t push_f(const std::vector<float> &v) { return push(v.data(), v.size() * 4); }
 };

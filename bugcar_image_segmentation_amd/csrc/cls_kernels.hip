@@ -4,7 +4,7 @@
 //
 // GEMM view as conv_kernels.hip: a column is one input pixel, K = (tap of the 2x2 input
 // neighbourhood, channel), rows = (output phase, class). The MFMA is v_mfma_f32_32x32x16_bf16
-// (fp32 parity mode: 8 x v_mfma_f32_32x32x2_f32 per tap, one per channel pair): its accumulator gives
+// (fp32 parity mode: split-f16 products, 3 x v_mfma_f32_32x32x16_f16 per tap): its accumulator gives
 // lane (col, h) the 16 rows {8j + 4h + i}. Rows are permuted (the weights are gathered with the
 // permutation, nothing is repacked) so that those 16 rows are the 16 classes of ONE output phase:
 //   block b (two per column), lane half h  ->  phase 2b + h = output pixel (2y + b, 2x + h),
@@ -30,23 +30,21 @@ __device__ __forceinline__ void mma32(f32x16 &acc, const RawH &w, const RawH &x)
     acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(__builtin_bit_cast(f16x8, w.v), __builtin_bit_cast(f16x8, x.v),
                                                  acc, 0, 0, 0);
 }
-// fp32: sub-MFMA j contracts element j of both lane halves (channels j and 8 + j of the tap)
-__device__ __forceinline__ void mma32(f32x16 &acc, const RawF &w, const RawF &x) {
-    acc = __builtin_amdgcn_mfma_f32_32x32x2f32(w.a.x, x.a.x, acc, 0, 0, 0);
-    acc = __builtin_amdgcn_mfma_f32_32x32x2f32(w.a.y, x.a.y, acc, 0, 0, 0);
-    acc = __builtin_amdgcn_mfma_f32_32x32x2f32(w.a.z, x.a.z, acc, 0, 0, 0);
-    acc = __builtin_amdgcn_mfma_f32_32x32x2f32(w.a.w, x.a.w, acc, 0, 0, 0);
-    acc = __builtin_amdgcn_mfma_f32_32x32x2f32(w.b.x, x.b.x, acc, 0, 0, 0);
-    acc = __builtin_amdgcn_mfma_f32_32x32x2f32(w.b.y, x.b.y, acc, 0, 0, 0);
-    acc = __builtin_amdgcn_mfma_f32_32x32x2f32(w.b.z, x.b.z, acc, 0, 0, 0);
-    acc = __builtin_amdgcn_mfma_f32_32x32x2f32(w.b.w, x.b.w, acc, 0, 0, 0);
+// fp32 parity mode: split-f16 products (mfma_common.h mma(RawS, RawF)) on the 32 x 32 shape: the
+// lane's 8 channels (8h .. 8h + 7 of the tap) as hi / lo f16 parts, three MFMAs
+__device__ __forceinline__ void mma32(f32x16 &acc, const RawS &w, const RawF &x) {
+    f16x8 xh, xl;
+    split_f16(x, xh, xl);
+    const f16x8 wh = __builtin_bit_cast(f16x8, w.h), wl = __builtin_bit_cast(f16x8, w.l);
+    acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(wl, xh, acc, 0, 0, 0);
+    acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(wh, xl, acc, 0, 0, 0);
+    acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(wh, xh, acc, 0, 0, 0);
 }
 
 __device__ __forceinline__ bool nonzero(const RawB &r) { return (r.v.x | r.v.y | r.v.z | r.v.w) != 0u; }
 __device__ __forceinline__ bool nonzero(const RawH &r) { return (r.v.x | r.v.y | r.v.z | r.v.w) != 0u; }
-__device__ __forceinline__ bool nonzero(const RawF &r) {
-    const uint4 u = __builtin_bit_cast(uint4, r.a), v = __builtin_bit_cast(uint4, r.b);
-    return (u.x | u.y | u.z | u.w | v.x | v.y | v.z | v.w) != 0u;
+__device__ __forceinline__ bool nonzero(const RawS &r) {
+    return (r.h.x | r.h.y | r.h.z | r.h.w | r.l.x | r.l.y | r.l.z | r.l.w) != 0u;
 }
 
 // Taps: the 2x2 input neighbourhood (dy, dx) = (s >> 1, s & 1) of the k = 3 layer in pack_tconv's
@@ -57,6 +55,7 @@ template <typename T, bool LOGITS>
 __global__ void __launch_bounds__(256, sizeof(T) == 2 ? 4 : 1) cls_kernel(const ConvArgs a) {
     constexpr int CLS_TAPS = 4;
     using Raw = typename Tr<T>::Raw;
+    using WRaw = typename WTr<T>::Raw;   // weight operand (fp32 mode: split-f16 parts)
     constexpr int ES = (int)sizeof(T);
     __shared__ float sbias[64];
     const int tid = threadIdx.x, lane = tid & 63, col = lane & 31, h = lane >> 5;
@@ -71,7 +70,7 @@ __global__ void __launch_bounds__(256, sizeof(T) == 2 ? 4 : 1) cls_kernel(const 
 
     // weights: block b, row r = lane's col -> packed row (phase 2b + ((r >> 2) & 1), class 4 (r >> 3) + (r & 3));
     // this lane's k half = channels 8h .. 8h + 7 of each tap
-    Raw wr[2][CLS_TAPS];
+    WRaw wr[2][CLS_TAPS];
     {
         const T *w = reinterpret_cast<const T *>(a.w);
 #pragma unroll

@@ -59,6 +59,7 @@ __global__ void __launch_bounds__(256, sizeof(T) == 2 ? (NR == 8 ? 3 : 4) : 1) c
     // VGPRs); fp32 (parity mode) keeps half
     constexpr int KC = ES == 2 ? (MR >= 4 || NR >= 8 ? 2 : 4) : (MR >= 4 || NR >= 8 ? 1 : 2);
     using Raw = typename Tr<T>::Raw;
+    using WRaw = typename WTr<T>::Raw;   // weight operand (fp32 mode: split-f16 parts)
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
 
     const int tid = threadIdx.x;
@@ -193,7 +194,7 @@ __global__ void __launch_bounds__(256, sizeof(T) == 2 ? (NR == 8 ? 3 : 4) : 1) c
                 if (s0 + kc >= a.Ksteps) break;
 #pragma unroll
                 for (int n = 0; n < NR; ++n) {
-                    Raw wf;
+                    WRaw wf;
                     ld8(wf, wl + (n * 16 + col) * KS + (s0 + kc) * 32 + kq * 8);
 #pragma unroll
                     for (int m = 0; m < MR; ++m) mma(acc[m][n], wf, xf[kc][m]);

@@ -49,6 +49,7 @@ __global__ void __launch_bounds__(256) init_kernel(const ConvArgs a) {
     __shared__ __attribute__((aligned(16))) T patch[IP_H * IP_RS];
     __shared__ float lut[BGR ? 3 * 256 : 1];
     using Raw = typename Tr<T>::Raw;
+    using WRaw = typename WTr<T>::Raw;   // weight operand (fp32 mode: split-f16 parts)
     const int tid = threadIdx.x;
     const int lane = tid & 63, col = lane & 15, kq = lane >> 4;
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -58,8 +59,20 @@ __global__ void __launch_bounds__(256) init_kernel(const ConvArgs a) {
     }
     // A operand (weights), loop-invariant: row = output channel `col`, k = 8*kq + j in the order of
     // init_k, from the generic packing [Npad][Kpad] with k' = tap * 8 + c.
-    Raw wf;
-    {
+    WRaw wf;
+    if constexpr (sizeof(T) == 4) {
+        // fp32 mode: the split-f16 parts of each weight (mfma_common.h RawS)
+        const float *wp = reinterpret_cast<const float *>(a.w) + (size_t)col * a.Kpad;
+        _Float16 hi[8], lo[8];
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+            int dy, e;
+            init_k(kq, j, dy, e);
+            hi[j] = lo[j] = (_Float16)0.f;
+            if (e >= 0) wsplit_elem(wp, (dy * 3 + e / 3) * 8 + e % 3, hi[j], lo[j]);
+        }
+        set8(wf, hi, lo);
+    } else {
         const T *wp = reinterpret_cast<const T *>(a.w);
         T wv[8];
 #pragma unroll

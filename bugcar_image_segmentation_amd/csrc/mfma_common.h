@@ -71,8 +71,56 @@ __device__ __forceinline__ void mma(f32x4 &acc, const RawB &w, const RawB &x) {
     acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, w.v), __builtin_bit_cast(bf16x8, x.v),
                                                   acc, 0, 0, 0);
 }
-// fp32 parity mode: sub-MFMA j contracts element j of every lane's 8-group (lane>>4 = group),
-// so the 8 sub-MFMAs together cover the same 32 k as one bf16 MFMA (exact f32 products).
+// fp32 parity mode, round 4: split-f16 products. The weights are packed on the host as two f16
+// parts per element (bugseg_runtime.cpp Packer::push_w: hi = f16(w), lo = f16(w - hi); every 8
+// consecutive k of a row are 32 B, the 8 hi parts then the 8 lo parts — the bytes of 8 floats), the
+// f32 activation operand is split the same way in registers, and one f32 product becomes three
+// v_mfma_f32_16x16x32_f16 (lo*hi + hi*lo + hi*hi, products exact in f32, f32 accumulation; the
+// dropped lo*lo term and the parts' rounding leave ~2^-21 relative per product). 48 MFMA cycles per
+// 32-k step instead of 256 for the 8 exact v_mfma_f32_16x16x4_f32. Emulated end to end at 480 x 640
+// (scripts/split_precision_probe.py): max |dlogit| vs the fp32 oracle 2.1e-5 (exact f32 products:
+// 1.5e-5), near-tie share 4.9e-5 (4.2e-5); bf16 splits need 6 products for the same (3 give 3.6).
+// Operands must lie within the f16 range (|v| < 65504; f16 subnormals are kept: MODE.denorm).
+struct RawS { uint4 h, l; };       // 8 weights as f16 hi parts + 8 f16 lo parts (fp32 mode)
+template <typename T> struct WTr { using Raw = typename Tr<T>::Raw; };
+template <> struct WTr<float> { using Raw = RawS; };
+__device__ __forceinline__ void ld8(RawS &r, const float *p) {
+    r.h = reinterpret_cast<const uint4 *>(p)[0];
+    r.l = reinterpret_cast<const uint4 *>(p)[1];
+}
+__device__ __forceinline__ void zero(RawS &r) { r.h = make_uint4(0, 0, 0, 0); r.l = r.h; }
+// the hi / lo f16 parts of element k of a packed fp32-mode weight row
+__device__ __forceinline__ void wsplit_elem(const float *row, int k, _Float16 &hi, _Float16 &lo) {
+    const _Float16 *p = reinterpret_cast<const _Float16 *>(row) + (k >> 3) * 16 + (k & 7);
+    hi = p[0];
+    lo = p[8];
+}
+__device__ __forceinline__ void set8(RawS &r, const _Float16 (&hi)[8], const _Float16 (&lo)[8]) {
+    const f16x8 h = {hi[0], hi[1], hi[2], hi[3], hi[4], hi[5], hi[6], hi[7]};
+    const f16x8 l = {lo[0], lo[1], lo[2], lo[3], lo[4], lo[5], lo[6], lo[7]};
+    r.h = __builtin_bit_cast(uint4, h);
+    r.l = __builtin_bit_cast(uint4, l);
+}
+// x = hi + lo: hi = f16(x) (round to nearest even), lo = f16(x - hi) (x - hi is exact in f32)
+__device__ __forceinline__ void split_f16(const RawF &x, f16x8 &hi, f16x8 &lo) {
+    const float v[8] = {x.a.x, x.a.y, x.a.z, x.a.w, x.b.x, x.b.y, x.b.z, x.b.w};
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+        const _Float16 h = (_Float16)v[i];
+        hi[i] = h;
+        lo[i] = (_Float16)(v[i] - (float)h);
+    }
+}
+__device__ __forceinline__ void mma(f32x4 &acc, const RawS &w, const RawF &x) {
+    f16x8 xh, xl;
+    split_f16(x, xh, xl);
+    const f16x8 wh = __builtin_bit_cast(f16x8, w.h), wl = __builtin_bit_cast(f16x8, w.l);
+    acc = __builtin_amdgcn_mfma_f32_16x16x32_f16(wl, xh, acc, 0, 0, 0);
+    acc = __builtin_amdgcn_mfma_f32_16x16x32_f16(wh, xl, acc, 0, 0, 0);
+    acc = __builtin_amdgcn_mfma_f32_16x16x32_f16(wh, xh, acc, 0, 0, 0);
+}
+// exact f32 products (DeepLab's fp32 mode): sub-MFMA j contracts element j of every lane's 8-group
+// (lane>>4 = group), so the 8 sub-MFMAs together cover the same 32 k as one bf16 MFMA.
 __device__ __forceinline__ void mma(f32x4 &acc, const RawF &w, const RawF &x) {
     acc = __builtin_amdgcn_mfma_f32_16x16x4f32(w.a.x, x.a.x, acc, 0, 0, 0);
     acc = __builtin_amdgcn_mfma_f32_16x16x4f32(w.a.y, x.a.y, acc, 0, 0, 0);

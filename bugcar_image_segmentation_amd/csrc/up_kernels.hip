@@ -28,6 +28,7 @@ namespace bugseg {
 template <typename T, int CIN, int I, int COUT>
 __global__ void __launch_bounds__(256, (sizeof(T) == 2 ? (CIN >= 128 ? 2 : 3) : 1)) up_kernel(const UpArgs a) {
     using Raw = typename Tr<T>::Raw;
+    using WRaw = typename WTr<T>::Raw;   // weight operand (fp32 mode: split-f16 parts)
     constexpr int ES = (int)sizeof(T);
     constexpr int OAUX = OUT_AUX_SEL(CIN >= 128 ? 16 : 0);   // sc1 output stores (mfma_common.h)
     constexpr int NR1 = (COUT + I) / 16;              // GEMM 1 rows: main then e1
@@ -132,7 +133,7 @@ __global__ void __launch_bounds__(256, (sizeof(T) == 2 ? (CIN >= 128 ? 2 : 3) : 
         for (int s = 0; s < KS1; ++s)
 #pragma unroll
             for (int r = 0; r < NR1; ++r) {
-                Raw wf;
+                WRaw wf;
                 ld8(wf, w1 + (r * 16 + col) * K1S + wch(col, s * 4 + kq, CIN));
                 mma(acc1[r], wf, xf[s]);
             }
@@ -156,7 +157,7 @@ __global__ void __launch_bounds__(256, (sizeof(T) == 2 ? (CIN >= 128 ? 2 : 3) : 
             for (int e = 0; e < NE; ++e) {
                 const int r2 = ph * NE + e;
                 acc2[e] = B2ACC ? bias4(cb2 + r2 * 16 + kq * 4) : (f32x4){0.f, 0.f, 0.f, 0.f};
-                Raw wf;
+                WRaw wf;
                 ld8(wf, w2 + (r2 * 16 + col) * K2S + wch(col, kq, 32));
                 mma(acc2[e], wf, bop2);
             }
@@ -170,7 +171,7 @@ __global__ void __launch_bounds__(256, (sizeof(T) == 2 ? (CIN >= 128 ? 2 : 3) : 
             auto ep3 = [&](int r) {
                 const int c = r * 16 + kq * 4;
                 f32x4 acc = B3ACC ? bias4(cb3 + c) : (f32x4){0.f, 0.f, 0.f, 0.f};
-                Raw wf;
+                WRaw wf;
                 ld8(wf, w3 + (r * 16 + col) * K3S + wch(col, kq, 32));
                 mma(acc, wf, bop3);
                 float4 v = act(B3ACC ? f4(acc) : add4(f4(acc), ld4f(cb3 + c)), cs3 + c);
