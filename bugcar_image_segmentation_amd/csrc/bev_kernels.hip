@@ -441,9 +441,7 @@ __global__ void __launch_bounds__(256, 4) bev_occgrid_lds_kernel(const BevArgs a
 // bands x, x + 8, ... of every frame, so each XCD's L2 holds only its bands' share of the tap table.
 // 4 grid rows: ~1,600 workgroups at 32 frames, all resident at once (16 KB of LDS each); 8 rows (40 KB,
 // 3 per CU) left a second round of workgroups: 58.5 vs 62 us for the gather kernel
-constexpr int BEV_BAND = 4, BEV_BAND_CAP = 16384, BEV_BAND_PF = BEV_BAND_CAP / 16 / 256;
-
-__host__ __device__ inline int bev_bands(int occ_h) { return (occ_h + BEV_BAND - 1) / BEV_BAND; }
+constexpr int BEV_BAND_CAP = 16384, BEV_BAND_PF = BEV_BAND_CAP / 16 / 256;   // (BEV_BAND, bev_bands: bugseg_internal.h)
 // The band kernel's compact table, after the band boxes: [BEV_WIN][cells] u32, entry i of every cell
 // (BEV_ORDER_D order: the sample, its 3x3, then the ring) as the .y word alone — the tap's byte offset
 // in the band's LDS box, the fractions, the valid-tap and outside-template bits: what the LDS form
@@ -506,11 +504,81 @@ __global__ void __launch_bounds__(256) bev_bandbox_kernel(const BevArgs a, int4 
         ctab[(long)(2 * q) * cells + rem] = sv.y;
         if (2 * q + 1 < BEV_WIN) ctab[(long)(2 * q + 1) * cells + rem] = sv.w;
     }
+    // per cell: which of the 25 window positions lie outside the template (bit B5(dx, dy)), a geometry
+    // fact the band kernel would otherwise re-derive from 9-25 entries (and the cell's pixel) per frame
+    __syncthreads();
+    uint32_t *omask = ctab + (size_t)BEV_WIN * cells;
+    for (int c = threadIdx.x; c < n; c += 256) {
+        const long rem = (long)r0 * a.occ_w + c;
+        uint32_t m = 0;
+        for (int k = 0; k < BEV_WIN; ++k)
+            m |= (uint32_t)((ctab[(long)k * cells + rem] & TAB_OUT) != 0) << BEV_ORDER[k];
+        omask[rem] = m;
+    }
 }
 
 // FB frames per workgroup (one box each): a cell's table slots and entry decoding serve all FB frames.
 // Held to 7 waves per SIMD (FB = 1: 72 VGPRs) so the ~1,600 workgroups of a 32-frame call are one
 // round (at 106 VGPRs, 4 waves per SIMD, they took 1.6 rounds).
+// One cell of one frame from a band's LDS box (bev_band_kernel's compact-table form and
+// bev_pipe_kernel): e9 = the cell's sample + 3x3 entries (offset in the box, Q5 fractions; BEV_ORDER),
+// outm = its 25-bit outside-template mask, ring = its 16 ring entries (stride `cells`), read only when
+// the opening needs them. Returns the template value after the speckle opening (bev.py:196-205).
+__device__ __forceinline__ int bev_cell_lds(const BevArgs &a, const uint8_t *box, int bw, const uint32_t (&e9)[9],
+                                            uint32_t outm, const uint32_t *ring, long cells) {
+    const uint32_t inner = 0x739C0u;                  // bits of the 3x3 around p: rows 1..3, cols 1..3
+    auto value = [&](uint32_t ey) -> int {
+        const uint8_t *p = box + (ey >> 15);
+        const uint32_t l0 = p[0], l1 = p[1], l2 = p[bw], l3 = p[bw + 1];
+        const uint32_t ax = ey & 31u, ay = (ey >> 5) & 31u;
+        const uint32_t wx = 32u + ax * 65535u, wy = 32u + ay * 65535u;   // (32 - a) | a << 16
+        const uint32_t top = dot2(l0 | l1 << 16, wx, 0u), bot = dot2(l2 | l3 << 16, wx, 0u);
+        return (int)(dot2(top | bot << 16, wy, 512u) >> 10);              // (sum + 2^14) >> 15 of OpenCV
+    };
+    int t9[9];
+#pragma unroll
+    for (int i = 0; i < 9; ++i) t9[i] = value(e9[i]);
+    int v = t9[0];
+    uint32_t m = outm;                                // occupied or outside, per window bit
+#pragma unroll
+    for (int i = 0; i < 9; ++i) m |= (uint32_t)occupied(a, t9[i]) << BEV_ORDER[i];
+    if (!(occupied(a, v) && (m & inner) != inner)) return v;
+    // opening at p = OR over the q in N3(p) inside the template of AND over N3(q). The centre already
+    // failed (its 3x3 is not all occupied), so the candidates are the 8 neighbours whose part of N3(q)
+    // inside the 3x3 is all occupied; only their ring pixels are evaluated (outside-template ones count
+    // as occupied and are set already). The 16 ring entries fly in one round trip
+    uint32_t cand = 0, rneed = 0;
+#pragma unroll
+    for (int qi = 0; qi < 9; ++qi) {
+        if (qi == 4) continue;
+        const int qx = qi % 3 - 1, qy = qi / 3 - 1, sh = qy * 5 + qx;
+        const uint32_t win = sh >= 0 ? inner << sh : inner >> -sh, wi = win & inner;
+        const bool ok = !((outm >> B5(qx, qy)) & 1u) && (m & wi) == wi;
+        cand |= ok ? 1u << qi : 0u;
+        rneed |= ok ? win & ~inner & ~outm : 0u;
+    }
+    uint32_t er[BEV_WIN - 9];
+#pragma unroll
+    for (int k = 0; k < BEV_WIN - 9; ++k) er[k] = ring[(long)k * cells];
+#pragma unroll
+    for (int k = 0; k < BEV_WIN - 9; ++k) {
+        const int bit = BEV_ORDER[9 + k];
+        if ((rneed >> bit) & 1u) m |= (uint32_t)occupied(a, value(er[k])) << bit;
+    }
+    bool opened = false;
+#pragma unroll
+    for (int qi = 0; qi < 9; ++qi) {
+        if (qi == 4) continue;
+        const int qx = qi % 3 - 1, qy = qi / 3 - 1, sh = qy * 5 + qx;
+        const uint32_t win = sh >= 0 ? inner << sh : inner >> -sh;
+        opened |= ((cand >> qi) & 1u) && (m & win) == win;
+    }
+    return opened ? v : 2;                            // isolated occupied pixel -> free (bev.py:204-205)
+}
+
+#ifndef BEV_CTAB
+#define BEV_CTAB 1
+#endif
 template <int FB>
 __global__ void __launch_bounds__(256, FB == 1 ? 7 : 4) bev_band_kernel(const BevArgs a) {
     __shared__ __attribute__((aligned(16))) uint8_t box[FB][BEV_BAND_CAP];
@@ -531,6 +599,19 @@ __global__ void __launch_bounds__(256, FB == 1 ? 7 : 4) bev_band_kernel(const Be
                                                    (short)0, (int)frame_bytes, 0x00020000);
     const bool lds = bb.z >= 0;                                // workgroup-uniform
     const int y0 = bb.x, xa = bb.y, bh = lds ? bb.z : 0, bw = bb.w, zpad = bh * bw;
+    // the LDS form's compact table (BEV_WIN planes of 4-B entries) and per-cell outside-template mask;
+    // the first cell's entries are requested before the box staging, so their latency overlaps it
+    const uint32_t *ct = reinterpret_cast<const uint32_t *>(reinterpret_cast<const unsigned char *>(a.wtab) +
+                                                            bev_ctab_offset(a.occ_w, a.occ_h)) + (size_t)r0 * a.occ_w;
+    const uint32_t *om = ct + (size_t)BEV_WIN * cells;
+    uint32_t c9n[9], omn = 0;
+    auto load9 = [&](int c) {
+        const uint32_t *t = ct + min(c, n - 1);
+#pragma unroll
+        for (int i = 0; i < 9; ++i) c9n[i] = t[(long)i * cells];
+        omn = om[min(c, n - 1)];
+    };
+    if (lds && BEV_CTAB) load9(tid);
     if (lds) {
         // each frame's box: all of this thread's 16-B chunks in flight before the first LDS store
         const int cpr = bw >> 4, nch = bh * cpr;
@@ -655,89 +736,114 @@ __global__ void __launch_bounds__(256, FB == 1 ? 7 : 4) bev_band_kernel(const Be
     };
 // (measured, round 3, 32 frames of 480x640, scripts/bev_sweep.py: 42.2-49.0 -> 35.6-39.2 us per launch,
 // laserscan 52.6-55.8 -> 49.8-52.1; BEV_CTAB=0: the uint4-slot form)
-#ifndef BEV_CTAB
-#define BEV_CTAB 1
-#endif
     if (lds && BEV_CTAB) {
-        // the LDS form on the compact table: 4-B entries, the 3x3's 9 of the next cell in flight while
-        // this one is evaluated, and the 16 ring entries of a cell that needs them issued together (one
-        // L2 round trip instead of one per slot)
-        const uint32_t *ct = reinterpret_cast<const uint32_t *>(reinterpret_cast<const unsigned char *>(a.wtab) +
-                                                                bev_ctab_offset(a.occ_w, a.occ_h)) + (size_t)r0 * a.occ_w;
-        auto value = [&](uint32_t ey, int f) -> int {
-            const uint8_t *p = box[f] + (ey >> 15);
-            const uint32_t l0 = p[0], l1 = p[1], l2 = p[bw], l3 = p[bw + 1];
-            const uint32_t ax = ey & 31u, ay = (ey >> 5) & 31u;
-            const uint32_t wx = 32u + ax * 65535u, wy = 32u + ay * 65535u;   // (32 - a) | a << 16
-            const uint32_t top = dot2(l0 | l1 << 16, wx, 0u), bot = dot2(l2 | l3 << 16, wx, 0u);
-            return (int)(dot2(top | bot << 16, wy, 512u) >> 10);              // (sum + 2^14) >> 15 of OpenCV
-        };
-        uint32_t c9n[9];
-        auto load9 = [&](int c) {
-            const uint32_t *t = ct + min(c, n - 1);
-#pragma unroll
-            for (int i = 0; i < 9; ++i) c9n[i] = t[(long)i * cells];
-        };
-        load9(tid);
+        // the LDS form on the compact table: 4-B entries, the 3x3's 9 (and the outside-template mask) of
+        // the next cell in flight while this one is evaluated (bev_cell_lds)
         for (int c = tid; c < n; c += 256) {
             const int rem = r0 * a.occ_w + c;
             const int cy = rem / a.occ_w, cx = rem - cy * a.occ_w;
             uint32_t e9[9];
 #pragma unroll
             for (int i = 0; i < 9; ++i) e9[i] = c9n[i];
+            const uint32_t outm = omn;
             load9(c + 256);
-            uint32_t outm = 0;
-#pragma unroll
-            for (int i = 0; i < 9; ++i) outm |= (uint32_t)((e9[i] & TAB_OUT) != 0) << BEV_ORDER[i];
-            int v[FB];
-            uint32_t m[FB];
-            bool need = false;
-#pragma unroll
-            for (int f = 0; f < FB; ++f) {
-                int t9[9];
-#pragma unroll
-                for (int i = 0; i < 9; ++i) t9[i] = value(e9[i], f);
-                v[f] = t9[0];
-                m[f] = outm;
-#pragma unroll
-                for (int i = 0; i < 9; ++i) m[f] |= (uint32_t)occupied(a, t9[i]) << BEV_ORDER[i];
-                need |= f < nf && occupied(a, v[f]) && (m[f] & inner) != inner;
-            }
-            if (need) {
-                uint32_t er[BEV_WIN - 9];
-#pragma unroll
-                for (int k = 0; k < BEV_WIN - 9; ++k) er[k] = ct[(long)(9 + k) * cells + c];
-#pragma unroll
-                for (int f = 0; f < FB; ++f)
-#pragma unroll
-                    for (int k = 0; k < BEV_WIN - 9; ++k)
-                        m[f] |= (uint32_t)((er[k] & TAB_OUT) || occupied(a, value(er[k], f))) << BEV_ORDER[9 + k];
-                int tx, ty;
-                cell_pixel(a, cx, cy, tx, ty);
-#pragma unroll
-                for (int f = 0; f < FB; ++f) {
-                    if (!(occupied(a, v[f]) && (m[f] & inner) != inner)) continue;
-                    bool opened = false;
-#pragma unroll
-                    for (int qy = -1; qy <= 1; ++qy)
-#pragma unroll
-                        for (int qx = -1; qx <= 1; ++qx) {
-                            const bool inside = (unsigned)(tx + qx) < (unsigned)a.occ_w_px && (unsigned)(ty + qy) < (unsigned)a.occ_h_px;
-                            const int sh = qy * 5 + qx;
-                            const uint32_t win = sh >= 0 ? inner << sh : inner >> -sh;
-                            opened |= inside && (m[f] & win) == win;
-                        }
-                    if (!opened) v[f] = 2;           // isolated occupied pixel -> free (bev.py:204-205)
-                }
-            }
 #pragma unroll
             for (int f = 0; f < FB; ++f)
-                if (f < nf) bev_emit(a, b0 + f, rem, cx, cy, cells, v[f]);
+                if (f < nf) bev_emit(a, b0 + f, rem, cx, cy, cells, bev_cell_lds(a, box[f], bw, e9, outm, ct + (size_t)9 * cells + c, cells));
         }
     } else if (lds) {
         cells_loop(std::true_type());
     } else {
         cells_loop(std::false_type());
+    }
+}
+
+// The band kernel with its latencies hidden (round 4, the default when a band has at most 1,024
+// cells and its box fits LDS). bev_band_kernel runs one (band, frame) per workgroup, all ~1,600 of them
+// resident at once, so every workgroup waits out its box staging and table loads together (SQ counters:
+// 51-59 % of wave cycles waiting). Here a workgroup takes one band and BEV_PIPE_FPW consecutive frames:
+//   * waves 0-3 (256 threads) evaluate frame b from LDS box[b & 1], the next cell's table entries in
+//     flight while one is evaluated (L2 hits);
+//   * wave 4 is a loader: while frame b is evaluated it stages frame b + 1's box into box[(b + 1) & 1]
+//     (all of its 16-B loads in flight, then the +1 label transform and the LDS stores). The compute
+//     waves never issue those loads, so their waits (ring entries) do not wait for them;
+//   * one barrier per frame hands the boxes over.
+// Same arithmetic as the band kernel (bev_cell_lds): bit-identical.
+constexpr int BEV_PIPE_FPW = 2, BEV_PIPE_KC = 4;       // frames per workgroup, max cells per compute thread
+constexpr int BEV_PIPE_LD = BEV_BAND_CAP / 1024;         // LDS-DMA instructions per box (1 KB each)
+__global__ void __launch_bounds__(320) bev_pipe_kernel(const BevArgs a) {
+    __shared__ __attribute__((aligned(16))) uint8_t box[2][BEV_BAND_CAP];
+    const int tid = threadIdx.x;
+    const bool loader = tid >= 256;                                        // wave 4 (wave-uniform)
+    const long cells = (long)a.occ_h * a.occ_w;
+    const int nbands = bev_bands(a.occ_h), nbs = (nbands + 7) >> 3;
+    const int xcd = blockIdx.x & 7, rest = blockIdx.x >> 3;
+    const int band = (rest % nbs) * 8 + xcd, f0 = (rest / nbs) * BEV_PIPE_FPW;
+    if (band >= nbands || f0 >= a.B) return;                               // workgroup-uniform
+    const int f1 = min(a.B, f0 + BEV_PIPE_FPW);
+    const int4 bb = reinterpret_cast<const int4 *>(a.wtab + (size_t)BEV_SLOTS * cells)[band];
+    const int r0 = band * BEV_BAND, n = (min(a.occ_h, r0 + BEV_BAND) - r0) * a.occ_w;
+    const uint32_t frame_bytes = (uint32_t)a.in_rows * (uint32_t)a.in_cols;
+    const int y0 = bb.x, xa = bb.y, bh = bb.z, bw = bb.w, zpad = bh * bw;   // (the host launches this form only
+    const int cpr = bw >> 4, nch = bh * cpr;                                //  when every box fits: bh >= 0)
+    // loader: frame b's box -> box[b & 1] by LDS-DMA (buffer_load ... lds: 1 KB per wave instruction, no
+    // VGPR round trip; out-of-image chunks read 0 — the image width is a multiple of 16 and xa is
+    // 16-aligned, so a chunk is all inside or all outside), then in place the labels + 1 (u8 wrap, as
+    // np.add) of the inside chunks, and the zero pad the outside-template and tap-less entries point at
+    auto stage = [&](int b) {
+        const auto seg = __builtin_amdgcn_make_buffer_rsrc(const_cast<uint8_t *>(a.seg) + (size_t)b * frame_bytes,
+                                                           (short)0, (int)frame_bytes, 0x00020000);
+        const int l = tid - 256;
+        uint8_t *bx = box[b & 1];
+        auto chunk_off = [&](int q) -> int {
+            const int r = q / cpr, c = q - r * cpr;
+            const int gy = y0 + r, gx = xa + c * 16;
+            const bool in = q < nch && (unsigned)gy < (unsigned)a.in_rows && (unsigned)gx < (unsigned)a.in_cols;
+            return in ? gy * a.in_cols + gx : -1;
+        };
+        for (int i = 0; i < BEV_PIPE_LD && 64 * i < nch; ++i) {              // (wave-uniform)
+            const int o = chunk_off(l + 64 * i);
+            __builtin_amdgcn_raw_ptr_buffer_load_lds(seg, (__attribute__((address_space(3))) void *)(bx + 1024 * i), 16,
+                                                     o >= 0 ? o : (int)0x80000000, 0, 0, 0);
+        }
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        for (int q = l; q < nch; q += 64) {
+            uint4 *pv = reinterpret_cast<uint4 *>(bx + 16 * q);
+            const uint4 v = *pv;
+            *pv = chunk_off(q) >= 0 ? make_uint4(inc4(v.x), inc4(v.y), inc4(v.z), inc4(v.w)) : make_uint4(0u, 0u, 0u, 0u);
+        }
+        for (int i = l; i < 2 * bw + 16; i += 64) bx[zpad + i] = 0;
+    };
+    // compute threads: the next cell's 3x3 entries and outside mask in flight while one is evaluated
+    // (L2 hits: the table is shared by every frame; their waits never include the loader's box loads)
+    const uint32_t *ct = reinterpret_cast<const uint32_t *>(reinterpret_cast<const unsigned char *>(a.wtab) +
+                                                            bev_ctab_offset(a.occ_w, a.occ_h)) + (size_t)r0 * a.occ_w;
+    uint32_t c9n[9], omn = 0;
+    auto load9 = [&](int c) {
+        const uint32_t *t = ct + min(c, n - 1);
+#pragma unroll
+        for (int i = 0; i < 9; ++i) c9n[i] = t[(long)i * cells];
+        omn = t[(long)BEV_WIN * cells];
+    };
+    if (loader) stage(f0);
+    else load9(tid);
+    for (int b = f0; b < f1; ++b) {
+        __syncthreads();                              // box[b & 1] staged; box[(b + 1) & 1] free again
+        if (loader) {
+            if (b + 1 < f1) stage(b + 1);
+            continue;
+        }
+        const uint8_t *bx = box[b & 1];
+        for (int c = tid; c < n; c += 256) {
+            const int rem = r0 * a.occ_w + c;
+            const int cy = rem / a.occ_w, cx = rem - cy * a.occ_w;
+            uint32_t e9[9];
+#pragma unroll
+            for (int i = 0; i < 9; ++i) e9[i] = c9n[i];
+            const uint32_t outm = omn;
+            load9(c + 256 < n ? c + 256 : tid);       // (the next frame's first cell after the last one)
+            bev_emit(a, b, rem, cx, cy, cells, bev_cell_lds(a, bx, bw, e9, outm, ct + (size_t)9 * cells + c, cells));
+        }
     }
 }
 
@@ -811,7 +917,8 @@ __global__ void __launch_bounds__(256) laserscan_kernel(const BevArgs a) {
 }
 
 size_t bev_table_bytes(int occ_w, int occ_h) {
-    return bev_ctab_offset(occ_w, occ_h) + (size_t)occ_w * occ_h * BEV_WIN * sizeof(uint32_t);
+    // tap table, band boxes, compact table (BEV_WIN planes) and the per-cell outside-template mask plane
+    return bev_ctab_offset(occ_w, occ_h) + (size_t)occ_w * occ_h * (BEV_WIN + 1) * sizeof(uint32_t);
 }
 
 hipError_t launch_bev_table(const BevArgs &a, hipStream_t s) {
@@ -843,7 +950,14 @@ hipError_t launch_bev(const BevArgs &a, hipStream_t s) {
     // BUGSEG_BEV_BAND=0: the gather / block-staged forms (A/B and tests)
     const char *be = std::getenv("BUGSEG_BEV_BAND");
     const bool banded = (!be || std::atoi(be) != 0) && !fe && FG == 0 && a.in_cols % 16 == 0;
-    if (banded) {
+    // BUGSEG_BEV_PIPE=0: the one-frame-per-workgroup band kernel (A/B and tests)
+    const char *pe = std::getenv("BUGSEG_BEV_PIPE");
+    const bool pipe = banded && (!pe || std::atoi(pe) != 0) && !std::getenv("BUGSEG_BEV_FB") && a.pipe_ok &&
+                      (long)BEV_BAND * a.occ_w <= 256L * BEV_PIPE_KC;
+    if (pipe) {
+        const long grid = 8L * ((bev_bands(a.occ_h) + 7) / 8) * ((a.B + BEV_PIPE_FPW - 1) / BEV_PIPE_FPW);
+        hipLaunchKernelGGL(bev_pipe_kernel, dim3((unsigned)grid), dim3(320), 0, s, a);
+    } else if (banded) {
         // frames per workgroup (BUGSEG_BEV_FB = 1 or 2; read per call)
         const char *fbe = std::getenv("BUGSEG_BEV_FB");
         // (measured at 32 frames of 480x640: FB = 1 38.7-40.1 us, FB = 2 44.6-48.5 us)

@@ -173,10 +173,14 @@ struct BevArgs {
     // [BEV_SLOTS][occ_h*occ_w] (the 3x3 around the sample first); a property of the geometry only,
     // built once per calibration by launch_bev_table and shared by every frame
     uint4 *wtab;
+    int pipe_ok;         // every band's class-map box fits LDS (the pipelined band kernel applies)
 };
 hipError_t launch_bev(const BevArgs &a, hipStream_t s);
 hipError_t launch_bev_table(const BevArgs &a, hipStream_t s);
 size_t bev_table_bytes(int occ_w, int occ_h);   // tap table + per-band class-map boxes
+// the band-staged forms cut the grid into bands of BEV_BAND rows (one class-map box each)
+constexpr int BEV_BAND = 4;
+__host__ __device__ inline int bev_bands(int occ_h) { return (occ_h + BEV_BAND - 1) / BEV_BAND; }
 constexpr int BEV_WIN = 25, BEV_SLOTS = 13;
 
 }  // namespace bugseg

@@ -51,13 +51,22 @@ __device__ __forceinline__ bool nonzero(const RawS &r) {
 // order (D = {0, 1}, tap = ty * 2 + tx). LOGITS: the fp32 logits are written too (parity runs).
 // The next group's loads are in flight while one computes (two groups ahead measured no faster,
 // round 3: 37.3 vs 36.9 us per launch, 127 vs 109 VGPRs).
+// CLS_LOWREG (round 4): the weights stay in LDS (each lane's fragments at its own 16-B slots: conflict-free
+// ds_read_b128, re-read per group) instead of 32 kernel-long VGPRs, and the two 32-row blocks run one
+// after the other (one 16-register accumulator live, not two), so the kernel fits 8 waves per SIMD
+// (2-byte storage) instead of 4: twice the groups' loads in flight per CU
+#ifndef CLS_LOWREG
+#define CLS_LOWREG 1
+#endif
 template <typename T, bool LOGITS>
-__global__ void __launch_bounds__(256, sizeof(T) == 2 ? 4 : 1) cls_kernel(const ConvArgs a) {
+__global__ void __launch_bounds__(256, sizeof(T) == 2 ? (CLS_LOWREG ? 7 : 4) : (CLS_LOWREG ? 4 : 1)) cls_kernel(const ConvArgs a) {
     constexpr int CLS_TAPS = 4;
     using Raw = typename Tr<T>::Raw;
     using WRaw = typename WTr<T>::Raw;   // weight operand (fp32 mode: split-f16 parts)
     constexpr int ES = (int)sizeof(T);
     __shared__ float sbias[64];
+    // CLS_LOWREG: the weight fragments, [block][tap][lane] (WRaw: 16 B, fp32 split parts 32 B)
+    __shared__ __attribute__((aligned(16))) WRaw sw[CLS_LOWREG ? 2 * CLS_TAPS * 64 : 1];
     const int tid = threadIdx.x, lane = tid & 63, col = lane & 31, h = lane >> 5;
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
     // a padding class (row (phase, c) with c >= ncls: zero weights) starts at -inf and stays there, so
@@ -87,7 +96,26 @@ __global__ void __launch_bounds__(256, sizeof(T) == 2 ? 4 : 1) cls_kernel(const 
     bool short_blk[2];
 #pragma unroll
     for (int b = 0; b < 2; ++b) short_blk[b] = __ballot(nonzero(wr[b][2]) || nonzero(wr[b][3])) == 0;
+    if constexpr (CLS_LOWREG) {
+        if (wave == 0) {
+#pragma unroll
+            for (int b = 0; b < 2; ++b)
+#pragma unroll
+                for (int s = 0; s < CLS_TAPS; ++s) sw[(b * CLS_TAPS + s) * 64 + lane] = wr[b][s];
+        }
+    }
     __syncthreads();
+    // the weight fragment of (block b, tap s) for this lane: registers, or (CLS_LOWREG) read from LDS
+    // where it is used (an opaque index keeps the reads inside the group loop)
+    auto wfrag = [&](int b, int s) -> WRaw {
+        if constexpr (CLS_LOWREG) {
+            int i = (b * CLS_TAPS + s) * 64 + lane;
+            asm volatile("" : "+v"(i));
+            return sw[i];
+        } else {
+            return wr[b][s];
+        }
+    };
 
     const auto rin = mkbuf(a.in, a.in_bytes);
     const int HWg = a.Hg * a.Wg;
@@ -142,19 +170,21 @@ __global__ void __launch_bounds__(256, sizeof(T) == 2 ? 4 : 1) cls_kernel(const 
     };
 
     // one group: MFMAs, argmax, stores; `nxt` first receives the next group's loads (they fly during
-    // this one; the two buffers alternate by unrolling, never by a runtime index). Both 32-row blocks'
-    // MFMAs go first, then the two argmax scans run interleaved: two independent compare / select
-    // chains fill each other's VCC hazard slots.
-    auto step = [&](int g, const Raw (&cur)[CLS_TAPS], Raw (&nxt)[CLS_TAPS]) {
+    // this one; the two buffers alternate by unrolling, never by a runtime index).
+    auto step = [&](int g, Raw (&cur)[CLS_TAPS], Raw (&nxt)[CLS_TAPS]) {
         // unconditional: past the last group the loads are harmless (an out-of-range group reads
         // zeros, a neighbour's group is read and dropped), and a static count of loads in flight
         // lets the waits before the MFMAs name only this group's loads (a conditional prefetch
-        // made the compiler wait vmcnt(3), i.e. for the next group's first load as well)
-        load(g + nw, nxt);
+        // made the compiler wait vmcnt(3), i.e. for the next group's first load as well).
+        // CLS_LOWREG: one buffer — the next group's loads go into `cur` once its last MFMA has read it
+        if constexpr (!CLS_LOWREG) load(g + nw, nxt);
         const Px q = pixel(g);
-        f32x16 acc[2];
-#pragma unroll
-        for (int b = 0; b < 2; ++b) {
+        // per block: accumulators from the bias, the taps' MFMAs, (parity runs) the logits, and the
+        // argmax over this lane's classes = the sequential strict > scan from -inf of tf.math.argmax
+        // (models.py:55): the maximum (v_max ignores NaN), then its first index; no class equal to the
+        // maximum (all NaN) -> 0; all -inf -> 0 (class 0 equals the maximum). The two blocks one after
+        // the other (CLS_LOWREG) or interleaved
+        auto block = [&](int b, f32x16 &acc) {
             // (the opaque offset keeps the compiler from hoisting these reads out of the group loop
             // into 32 loop-long VGPRs)
             int boff = (2 * b + h) * 16;
@@ -163,46 +193,59 @@ __global__ void __launch_bounds__(256, sizeof(T) == 2 ? 4 : 1) cls_kernel(const 
 #pragma unroll
             for (int j = 0; j < 4; ++j) {
                 const float4 v = bb[j];
-                acc[b][4 * j] = v.x; acc[b][4 * j + 1] = v.y; acc[b][4 * j + 2] = v.z; acc[b][4 * j + 3] = v.w;
+                acc[4 * j] = v.x; acc[4 * j + 1] = v.y; acc[4 * j + 2] = v.z; acc[4 * j + 3] = v.w;
             }
-        }
-#pragma unroll
-        for (int b = 0; b < 2; ++b) {
-            mma32(acc[b], wr[b][0], cur[0]);
-            mma32(acc[b], wr[b][1], cur[1]);
+            mma32(acc, wfrag(b, 0), cur[0]);
+            mma32(acc, wfrag(b, 1), cur[1]);
             if (!short_blk[b]) {
-                mma32(acc[b], wr[b][2], cur[2]);
-                mma32(acc[b], wr[b][3], cur[3]);
+                mma32(acc, wfrag(b, 2), cur[2]);
+                mma32(acc, wfrag(b, 3), cur[3]);
             }
-        }
-        if (LOGITS && q.ok) {
-#pragma unroll
-            for (int b = 0; b < 2; ++b) {
+            if (LOGITS && q.ok) {
                 float *lo = a.logits_out + (size_t)q.n * a.ncls * plane + (size_t)(2 * q.y + b) * a.Wout + 2 * q.x + h;
 #pragma unroll
                 for (int c = 0; c < 16; ++c)
-                    if (c < a.ncls) lo[(size_t)c * plane] = acc[b][c];
+                    if (c < a.ncls) lo[(size_t)c * plane] = acc[c];
             }
-        }
-        // argmax over this lane's classes = the sequential strict > scan from -inf of
-        // tf.math.argmax (models.py:55): the maximum (v_max ignores NaN), then its first index; no
-        // class equal to the maximum (all NaN) -> 0; all -inf -> 0 (class 0 equals the maximum)
-        float best[2];
-        int bi[2];
+        };
+        auto argmax = [&](const f32x16 &acc) -> int {
+            float best = acc[0];
 #pragma unroll
-        for (int b = 0; b < 2; ++b) {
-            best[b] = acc[b][0];
+            for (int c = 1; c < 16; ++c) best = __builtin_fmaxf(best, acc[c]);
+            int bi = 0;
 #pragma unroll
-            for (int c = 1; c < 16; ++c) best[b] = __builtin_fmaxf(best[b], acc[b][c]);
-            bi[b] = 0;
-        }
-#pragma unroll
-        for (int c = 15; c >= 0; --c)
-#pragma unroll
-            for (int b = 0; b < 2; ++b) bi[b] = acc[b][c] == best[b] ? c : bi[b];
+            for (int c = 15; c >= 0; --c) bi = acc[c] == best ? c : bi;
+            return (int)(lut64 >> (4 * bi)) & 15;
+        };
         int cls[2];
+        if constexpr (CLS_LOWREG) {
 #pragma unroll
-        for (int b = 0; b < 2; ++b) cls[b] = (int)(lut64 >> (4 * bi[b])) & 15;
+            for (int b = 0; b < 2; ++b) {
+                f32x16 acc;
+                block(b, acc);
+                if (b == 1) load(g + nw, cur);
+                cls[b] = argmax(acc);
+            }
+        } else {
+            f32x16 acc[2];
+            block(0, acc[0]);
+            block(1, acc[1]);
+            float best[2];
+            int bi[2];
+#pragma unroll
+            for (int b = 0; b < 2; ++b) {
+                best[b] = acc[b][0];
+#pragma unroll
+                for (int c = 1; c < 16; ++c) best[b] = __builtin_fmaxf(best[b], acc[b][c]);
+                bi[b] = 0;
+            }
+#pragma unroll
+            for (int c = 15; c >= 0; --c)
+#pragma unroll
+                for (int b = 0; b < 2; ++b) bi[b] = acc[b][c] == best[b] ? c : bi[b];
+#pragma unroll
+            for (int b = 0; b < 2; ++b) cls[b] = (int)(lut64 >> (4 * bi[b])) & 15;
+        }
         if (a.cls_out) {
             // lanes < 32 take output row 2y (their phase-(0,0) byte + the (0,1) byte of lane + 32), lanes
             // >= 32 row 2y + 1: one 2-byte store of pixels (2x, 2x + 1) each
@@ -217,6 +260,10 @@ __global__ void __launch_bounds__(256, sizeof(T) == 2 ? 4 : 1) cls_kernel(const 
     Raw xa[CLS_TAPS], xb[CLS_TAPS];
     int g = g0 + wi;
     if (g < g1) load(g, xa);
+    if constexpr (CLS_LOWREG) {
+        for (; g < g1; g += nw) step(g, xa, xa);
+        return;
+    }
     while (g < g1) {
         step(g, xa, xb);
         g += nw;
@@ -238,10 +285,28 @@ hipError_t launch_cls(int prec, const ConvArgs &a, hipStream_t s) {
     // waves stream over 32-pixel groups: enough workgroups to fill every CU at 4 waves per SIMD,
     // a multiple of 8 for the XCD split
     const int groups = (a.M + 31) / 32;
-    int g = (groups + 3) / 4;
-    g = g < 1024 ? g : 1024;
-    g = (g + 7) & ~7;
     const bool lg = a.logits_out != nullptr;
+    const void *f = prec == PREC_BF16 ? (lg ? (const void *)cls_kernel<__bf16, true> : (const void *)cls_kernel<__bf16, false>)
+                  : prec == PREC_F16  ? (lg ? (const void *)cls_kernel<_Float16, true> : (const void *)cls_kernel<_Float16, false>)
+                                      : (lg ? (const void *)cls_kernel<float, true> : (const void *)cls_kernel<float, false>);
+    // one round of resident workgroups (occupancy API per kernel instance, cached)
+    static const void *fs[6] = {};
+    static int caps[6] = {};
+    int cap = 0;
+    for (int i = 0; i < 6; ++i)
+        if (fs[i] == f) cap = caps[i];
+    if (!cap) {
+        int dev = 0, cus = 0, per = 0;
+        if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
+            cus = 256;
+        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, f, 256, 0) != hipSuccess || per <= 0) per = 4;
+        cap = cus * per;
+        for (int i = 0; i < 6; ++i)
+            if (!fs[i]) { fs[i] = f; caps[i] = cap; break; }
+    }
+    int g = (groups + 3) / 4;
+    g = g < cap ? g : cap;
+    g = (g + 7) & ~7;
     if (prec == PREC_BF16) {
         if (lg) hipLaunchKernelGGL((cls_kernel<__bf16, true>), dim3(g), dim3(256), 0, s, a);
         else hipLaunchKernelGGL((cls_kernel<__bf16, false>), dim3(g), dim3(256), 0, s, a);

@@ -24,8 +24,13 @@ seg = torch.empty((B, H, W), dtype=torch.uint8, device="cuda")
 model.ctx.forward_bgr(frames, B, H, W, N.OUT_CLASS3_U8, seg)
 print("class histogram", torch.bincount(seg.flatten().long(), minlength=3).tolist())
 ref = None
-for f, fg in [(None, None), ("FB2", None), ("1", None), ("2", None), ("1", "4"), (None, None), ("FB2", None), ("1", None)]:
+for f, fg in [(None, None), ("BAND", None), ("FB2", None), ("1", None), ("2", None), ("1", "4"), (None, None), ("BAND", None),
+              ("FB2", None), ("1", None)]:
     os.environ.pop("BUGSEG_BEV_FB", None)
+    os.environ.pop("BUGSEG_BEV_PIPE", None)
+    if f == "BAND":
+        os.environ["BUGSEG_BEV_PIPE"] = "0"
+        f = None
     if f == "FB2":
         os.environ["BUGSEG_BEV_FB"] = "2"
         f = None
@@ -51,6 +56,6 @@ for f, fg in [(None, None), ("FB2", None), ("1", None), ("2", None), ("1", "4"),
             if ref is None:
                 ref = g.clone()
             same = bool(torch.equal(ref, g))
-        print(f"F={f} FG={fg} FB={os.environ.get('BUGSEG_BEV_FB', 'default')} laserscan={ls}: {ev[0].elapsed_time(ev[1]) / reps * 1000:8.1f} us per {B} frames"
+        print(f"F={f} FG={fg} FB={os.environ.get('BUGSEG_BEV_FB', 'default')} PIPE={os.environ.get('BUGSEG_BEV_PIPE', 'default')} laserscan={ls}: {ev[0].elapsed_time(ev[1]) / reps * 1000:8.1f} us per {B} frames"
               + ("" if ls else f"  same grids: {same}"), flush=True)
 bev.laserscan_like_occupancy_grid = False

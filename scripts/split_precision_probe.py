@@ -27,11 +27,16 @@ def hf(t):
     return t.to(torch.float16).to(torch.float32)
 
 
+def hf_ftz(t):
+    h = hf(t)
+    return torch.where(h.abs() < 2.0 ** -14, torch.zeros_like(h), h)
+
+
 def split(t, n, mode):
     parts = []
     r = t
     for _ in range(n):
-        h = bf(r) if mode == "rne" else hf(r) if mode == "f16" else trunc(r)
+        h = bf(r) if mode == "rne" else hf(r) if mode == "f16" else hf_ftz(r) if mode == "f16ftz" else trunc(r)
         parts.append(h)
         r = r - h
     return parts
@@ -76,6 +81,7 @@ cfgs = {"f32 products (folded, f32 storage)": None,
         "bf16x3 rne (hh, hl, lh)": (2, 2, [(0, 0), (0, 1), (1, 0)], "rne"),
         "f16x3 (hh, hl, lh)": (2, 2, [(0, 0), (0, 1), (1, 0)], "f16"),
         "f16x3, weights x2^8": (2, 2, [(0, 0), (0, 1), (1, 0)], "f16", 8),
+        "f16x3 flushing f16 subnormals": (2, 2, [(0, 0), (0, 1), (1, 0)], "f16ftz"),
         "f16x4 (+ll), weights x2^8": (2, 2, [(0, 0), (0, 1), (1, 0), (1, 1)], "f16", 8),
         "x3-split x, w 2-split rne (5 terms)": (3, 2, [(0, 0), (0, 1), (1, 0), (1, 1), (2, 0)], "rne"),
         "bf16x6 rne": (3, 3, [(0, 0), (0, 1), (1, 0), (1, 1), (0, 2), (2, 0)], "rne")}

@@ -180,7 +180,7 @@ def _bev_case(rows, cols, ww, wh, seed):
     return bev
 
 
-@pytest.mark.parametrize("form", [None, "FB2", "G", "FG4", "F2"])
+@pytest.mark.parametrize("form", [None, "BAND", "FB2", "G", "FG4", "F2"])
 @pytest.mark.parametrize("rows,cols,ww,wh,grid,seed", [
     (480, 640, 1000, 1000, (10.0, 10.0, 0.05), 0),
     (120, 160, 300, 260, (3.0, 2.0, 0.05), 1),
@@ -188,11 +188,14 @@ def _bev_case(rows, cols, ww, wh, seed):
     (64, 80, 200, 150, (1.0, 1.0, 0.1), 3),
 ])
 def test_bev_occgrid_bit_exact(gpu, rows, cols, ww, wh, grid, seed, form, monkeypatch):
-    """Every form of the rasteriser (bev_kernels.hip: the default band-staged kernel, the gather
-    kernel, the block-staged one, 2 frames per thread) is bit-exact against the C restatement; class
-    maps with labels past the 3-class range (up to 255: segmap + 1 wraps in uint8 as np.add does,
-    bev.py:177) included."""
-    if form == "G":
+    """Every form of the rasteriser (bev_kernels.hip: the default pipelined band kernel, the
+    one-frame-per-workgroup band kernel, the gather kernel, the block-staged one, 2 frames per thread)
+    is bit-exact against the C restatement; class maps with labels past the 3-class range (up to 255:
+    segmap + 1 wraps in uint8 as np.add does, bev.py:177) included. Batches of 3 frames: the pipelined
+    kernel's 2-frame workgroups run one full and one partial frame pair."""
+    if form == "BAND":
+        monkeypatch.setenv("BUGSEG_BEV_PIPE", "0")
+    elif form == "G":
         monkeypatch.setenv("BUGSEG_BEV_BAND", "0")
     elif form == "FB2":
         monkeypatch.setenv("BUGSEG_BEV_FB", "2")
