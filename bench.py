@@ -12,10 +12,10 @@ Run:  python bench.py [--gpus N --steps K --warmup W]
       python -m torch.distributed.run --nproc-per-node N --master-addr 127.0.0.1 ... bench.py --gpus N
 Rank 0 prints ONE JSON line. `roofline` describes the dominant kernel of the forward (largest total
 time): the bytes one launch must move (block input read once, output written once) / its average
-launch duration, measured here with HIP events around every launch of shard 0's forward on the
-stream the kernels run on while the step's other shard runs on its own stream ("in-step", as the
-timed region and rocprofv3's averages see the launches; the same kernel alone on the GPU is reported
-beside it as `frac_isolated`), against the 8 TB/s HBM peak; `traffic` is the PMC-measured HBM bytes per launch of
+launch duration, measured here with HIP events around every launch of one shard's forward on the
+stream the kernels run on, that shard alone on the GPU ("isolated": `roofline.timing`; the
+graph-replayed 2-stream step runs the same launches ~7% longer per rocprofv3), against the 8 TB/s
+HBM peak; `traffic` is the PMC-measured HBM bytes per launch of
 that kernel from the committed profile (profiles/pmc_traffic.json). `roofline.forward` adds the
 whole-forward figures (SURVEY.md 8(d)'s 180.2 MB/frame per-layer definition and the plan's own byte
 counts). The CPU oracle (PyTorch-CPU ENet + C BEV restatement) is timed on a bounded sample on rank 0
@@ -49,29 +49,22 @@ KERNEL_NAMES = {"bneck C128": "bneck_kernel<{t},128,sym>", "bneck C128 asym": "b
 TEMPLATE_TYPE = {"fp16": "_Float16", "bf16": "__bf16", "fp32": "float"}   # the kernels' template type names
 
 
-def kernel_table(ctx, B, H, W, reps, stream, side=None):
+def kernel_table(ctx, B, H, W, reps, stream):
     """Per-launch durations of the forward the context last ran, measured with HIP events recorded
     around every launch on the stream the kernels run on, in forward order (so each kernel sees the
-    cache state it has in the pipeline). Grouped by kernel tag.
-    side = (stream, fn): "in-step" timing — before each timed forward, fn() enqueues the other frame
-    shards' work of the step on their own streams (started together with this shard, as the timed
-    step runs them), so each launch is timed while those shards' kernels share the GPU with it: the
-    condition the timed region (and rocprofv3's per-kernel averages of the bench command) sees.
-    side = None: "isolated" timing, this shard alone on the GPU."""
+    cache state it has in the pipeline), this shard alone on the GPU ("isolated"). Grouped by kernel
+    tag. (Timing shard 0's launches one by one while the other shard's step runs on its stream was
+    tried in round 4: the two shards' kernels then share the GPU for most of each launch, so the
+    per-launch durations double and say nothing about the kernel; rocprofv3's per-kernel averages of
+    the graph-replayed bench command run ~7% above these isolated figures.)"""
     n = ctx.plan_info(B, H, W, 2)[0]
     info = [ctx.plan_op(B, H, W, i) for i in range(n)]
     evs = [[torch.cuda.Event(enable_timing=True) for _ in range(n + 1)] for _ in range(reps)]
     for r in range(reps):
-        if side is not None:
-            ready = stream.record_event()
-            side[0].wait_event(ready)
-            side[1]()
         for i in range(n):
             evs[r][i].record(stream)
             ctx.launch_op(B, H, W, i, stream)
         evs[r][n].record(stream)
-        if side is not None:
-            stream.wait_stream(side[0])
     torch.cuda.synchronize()
     groups = {}
     for i, (tag, _lb, pb, fl) in enumerate(info):
@@ -253,31 +246,6 @@ def shard_overlap(pipe, frames, seg, g, bev, grid, H, W, reps):
     return out
 
 
-def step_side(pipe, frames, seg, g, H, W):
-    """(stream, fn) for kernel_table's in-step timing: fn enqueues shards 1.. of the step (forward +
-    BEV, each on its own stream, all on stream 1's queue order as the step does) — shard 0 is the one
-    timed op by op on the caller's stream."""
-    from bugcar_image_segmentation_amd import _native as N
-    if pipe.streams < 2 or frames.shape[0] < pipe.streams:
-        return None
-    ctxs, sts = pipe._shard_ctxs(frames.device)
-    S, B = pipe.streams, frames.shape[0]
-    bounds = [B * i // S for i in range(S + 1)]
-    p = pipe._params()
-
-    def fn():
-        for i in range(1, S):
-            s0, e0 = bounds[i], bounds[i + 1]
-            st = sts[i - 1]
-            if i > 1:
-                st.wait_stream(sts[0])
-            ctxs[i].forward_bgr(frames[s0:e0], e0 - s0, H, W, N.OUT_CLASS3_U8, seg[s0:e0], st)
-            ctxs[i].bev(seg[s0:e0], e0 - s0, p, g[s0:e0], st)
-        for st in sts[1: S - 1]:
-            sts[0].wait_stream(st)
-    return sts[0], fn
-
-
 def forward_ms(ctx, fs, Bs, H, W, seg, stream, reps):
     """Average ms of one forward of the Bs-frame shard (HIP events on the stream it runs on)."""
     from bugcar_image_segmentation_amd import _native as N
@@ -291,24 +259,17 @@ def forward_ms(ctx, fs, Bs, H, W, seg, stream, reps):
     return ev[0].elapsed_time(ev[1]) / reps
 
 
-def roofline_record(ctx, Bs, H, W, reps, stream, precision, t_fwd, side=None):
+def roofline_record(ctx, Bs, H, W, reps, stream, precision, t_fwd):
     """`roofline` of the dominant kernel of the forward the context last ran at (Bs, H, W): its
     bytes per launch / its HIP-event launch time against the HBM peak, the PMC traffic of the same
     kernel tag from the committed profile, and the whole forward's figures (bytes, and the MFMA
-    fraction against the dense peak of the precision's MFMA: f32 for fp32, bf16/f16 otherwise).
-    With `side` (the other shards of the step, kernel_table) the launch times are in-step: `achieved`
-    and `frac` are then what the launches reach inside the timed step; the same kernel timed alone
-    on the GPU is reported beside them as `achieved_isolated` / `frac_isolated`."""
+    fraction against the dense peak of the precision's MFMA: f32 for fp32, bf16/f16 otherwise). The
+    launch times are isolated (kernel_table); `timing` says so."""
     from bugcar_image_segmentation_amd import _native as N
-    kernels = kernel_table(ctx, Bs, H, W, reps, stream, side)
-    iso = kernel_table(ctx, Bs, H, W, reps, stream) if side is not None else kernels
+    kernels = kernel_table(ctx, Bs, H, W, reps, stream)
     n_launch, alg_bytes, plan_bytes, flops = ctx.plan_info(Bs, H, W, N.OUT_CLASS3_U8, bgr_input=True)
     tag, k = max(kernels.items(), key=lambda kv: kv[1]["total_us"])
     k_achieved = k["bytes_per_launch"] / (k["us_per_launch"] * 1e-6) / 1e9
-    ki = iso[tag]
-    k_iso = ki["bytes_per_launch"] / (ki["us_per_launch"] * 1e-6) / 1e9
-    timing = "in-step (HIP events around each launch of shard 0, the other shards running on their streams)" \
-        if side is not None else "isolated (HIP events around each launch, this shard alone on the GPU)"
     mpeak = MFMA_F32_PEAK_TFLOPS if precision == "fp32" else MFMA_BF16_PEAK_TFLOPS
     k_flops = k.get("flops_per_launch", 0.0)
     rec = {
@@ -318,11 +279,12 @@ def roofline_record(ctx, Bs, H, W, reps, stream, precision, t_fwd, side=None):
         "kernel": f"{KERNEL_NAMES.get(tag.rsplit(' ', 1)[0], tag).format(t=TEMPLATE_TYPE[precision])} [{tag}]: the dominant kernel of the forward "
                   f"({k['launches']} launches, {k['total_us']:.0f} us of {t_fwd * 1e3:.0f} us); "
                   f"{k['bytes_per_launch'] / 1e6:.1f} MB per launch = the bytes the launch must move "
-                  f"(block input read once + output written once); {k['us_per_launch']:.2f} us per launch, "
-                  f"{timing}, in forward order",
-        "timing": "in-step" if side is not None else "isolated",
-        "achieved_isolated": round(k_iso, 1), "frac_isolated": round(k_iso / HBM_PEAK_GBS, 4),
-        "us_per_launch": round(k["us_per_launch"], 3), "us_per_launch_isolated": round(ki["us_per_launch"], 3),
+                  f"(block input read once + output written once); {k['us_per_launch']:.2f} us per launch "
+                  f"(HIP events around each launch, this shard alone on the GPU, in forward order)",
+        "timing": "isolated: HIP events around each launch of one shard's forward with nothing else on the GPU; "
+                  "rocprofv3's per-kernel average of the graph-replayed 2-stream bench command runs ~7% longer "
+                  "(profiles/r04_*_fp16_b64s2.md), so the in-step fraction is ~0.93x this one",
+        "us_per_launch": round(k["us_per_launch"], 3),
         "kernel_mfma_tflops": round(k_flops / (k["us_per_launch"] * 1e-6) / 1e12, 2),
         "kernel_mfma_frac": round(k_flops / (k["us_per_launch"] * 1e-6) / 1e12 / mpeak, 4),
         "mfma_peak_tflops": mpeak,
@@ -338,8 +300,7 @@ def roofline_record(ctx, Bs, H, W, reps, stream, precision, t_fwd, side=None):
             "mfma_frac": round(flops / (t_fwd * 1e-3) / 1e12 / mpeak, 4)},
     }
     table = {t: {"launches": v["launches"], "us_per_launch": round(v["us_per_launch"], 2),
-                 "GBps": round(v["bytes_per_launch"] / (v["us_per_launch"] * 1e-6) / 1e9, 1),
-                 **({"us_per_launch_isolated": round(iso[t]["us_per_launch"], 2)} if side is not None and t in iso else {})}
+                 "GBps": round(v["bytes_per_launch"] / (v["us_per_launch"] * 1e-6) / 1e9, 1)}
              for t, v in sorted(kernels.items(), key=lambda kv: -kv[1]["total_us"])}
     return rec, table
 
@@ -364,8 +325,7 @@ def mode_record(blocks, bev, grid, H, W, frames, streams, steps, precision):
     Bs = B // streams if streams > 1 and B >= streams else B
     _x, seg, _g = pipe._bufs(B, frames.device)
     t_fwd = forward_ms(model.ctx, frames[:Bs], Bs, H, W, seg[:Bs], stream, 10)
-    roof, table = roofline_record(model.ctx, Bs, H, W, 10, stream, precision, t_fwd,
-                                  step_side(pipe, frames, seg, _g, H, W))
+    roof, table = roofline_record(model.ctx, Bs, H, W, 10, stream, precision, t_fwd)
     del pipe, model
     return {"value": round(B * steps / el, 2), "unit": "frames/s", "ms_per_step": round(el / steps * 1e3, 4),
             "per_gpu_batch": B, "steps": steps, "streams_per_gpu": streams, "dtype": precision,
@@ -555,8 +515,7 @@ def main():
     ev[1].synchronize()
     t_ls = ev[0].elapsed_time(ev[1]) / reps
     bev.laserscan_like_occupancy_grid = False
-    roof, ktable = roofline_record(model.ctx, Bs, H, W, reps, stream, a.precision, t_fwd,
-                                   step_side(pipe, frames, seg, g, H, W))
+    roof, ktable = roofline_record(model.ctx, Bs, H, W, reps, stream, a.precision, t_fwd)
     overlap = shard_overlap(pipe, frames, seg, g, bev, grid, H, W, reps) if a.streams > 1 and B >= a.streams else None
 
     if rank == 0:

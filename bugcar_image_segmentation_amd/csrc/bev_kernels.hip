@@ -162,6 +162,9 @@ __device__ __forceinline__ bool occupied(const BevArgs &a, int v) {
 // encode template value v of cell (cx, cy) of frame b and store it (or, in the laserscan mode, the
 // polar warp's source)
 __device__ __forceinline__ void bev_emit(const BevArgs &a, int b, int rem, int cx, int cy, long cells, int v) {
+#ifdef BEV_ABL
+    if constexpr (BEV_ABL & 2) { if (v == 12345) a.out[0] = 0; return; }
+#endif
     const long o_i = (long)b * cells + rem;
     int8_t o;
     if (!a.variant) {
@@ -441,7 +444,8 @@ __global__ void __launch_bounds__(256, 4) bev_occgrid_lds_kernel(const BevArgs a
 // bands x, x + 8, ... of every frame, so each XCD's L2 holds only its bands' share of the tap table.
 // 4 grid rows: ~1,600 workgroups at 32 frames, all resident at once (16 KB of LDS each); 8 rows (40 KB,
 // 3 per CU) left a second round of workgroups: 58.5 vs 62 us for the gather kernel
-constexpr int BEV_BAND_CAP = 16384, BEV_BAND_PF = BEV_BAND_CAP / 16 / 256;   // (BEV_BAND, bev_bands: bugseg_internal.h)
+constexpr int BEV_BAND_CAP = 16384, BEV_BAND_PF = BEV_BAND_CAP / 16 / 256;
+constexpr int BEV_WL = 512;                          // band kernel: ring work-list records per workgroup   // (BEV_BAND, bev_bands: bugseg_internal.h)
 // The band kernel's compact table, after the band boxes: [BEV_WIN][cells] u32, entry i of every cell
 // (BEV_ORDER_D order: the sample, its 3x3, then the ring) as the .y word alone — the tap's byte offset
 // in the band's LDS box, the fractions, the valid-tap and outside-template bits: what the LDS form
@@ -524,38 +528,58 @@ __global__ void __launch_bounds__(256) bev_bandbox_kernel(const BevArgs a, int4 
 // bev_pipe_kernel): e9 = the cell's sample + 3x3 entries (offset in the box, Q5 fractions; BEV_ORDER),
 // outm = its 25-bit outside-template mask, ring = its 16 ring entries (stride `cells`), read only when
 // the opening needs them. Returns the template value after the speckle opening (bev.py:196-205).
-__device__ __forceinline__ int bev_cell_lds(const BevArgs &a, const uint8_t *box, int bw, const uint32_t (&e9)[9],
-                                            uint32_t outm, const uint32_t *ring, long cells) {
-    const uint32_t inner = 0x739C0u;                  // bits of the 3x3 around p: rows 1..3, cols 1..3
-    auto value = [&](uint32_t ey) -> int {
-        const uint8_t *p = box + (ey >> 15);
-        const uint32_t l0 = p[0], l1 = p[1], l2 = p[bw], l3 = p[bw + 1];
-        const uint32_t ax = ey & 31u, ay = (ey >> 5) & 31u;
-        const uint32_t wx = 32u + ax * 65535u, wy = 32u + ay * 65535u;   // (32 - a) | a << 16
-        const uint32_t top = dot2(l0 | l1 << 16, wx, 0u), bot = dot2(l2 | l3 << 16, wx, 0u);
-        return (int)(dot2(top | bot << 16, wy, 512u) >> 10);              // (sum + 2^14) >> 15 of OpenCV
-    };
+// BEV_ABL (debug ablation builds, wrong grids; scripts/gpu_r4_abl.sh): 1 = no ring pass, 4 = no template
+// values (the sample's entry bits stand in), 2 = no output stores (bev_emit), 8 = no box staging
+#ifndef BEV_ABL
+#define BEV_ABL 0
+#endif
+__device__ __forceinline__ int bev_value_lds(const uint8_t *box, int bw, uint32_t ey) {
+    const uint8_t *p = box + (ey >> 15);
+    const uint32_t l0 = p[0], l1 = p[1], l2 = p[bw], l3 = p[bw + 1];
+    const uint32_t ax = ey & 31u, ay = (ey >> 5) & 31u;
+    const uint32_t wx = 32u + ax * 65535u, wy = 32u + ay * 65535u;   // (32 - a) | a << 16
+    const uint32_t top = dot2(l0 | l1 << 16, wx, 0u), bot = dot2(l2 | l3 << 16, wx, 0u);
+    return (int)(dot2(top | bot << 16, wy, 512u) >> 10);              // (sum + 2^14) >> 15 of OpenCV
+}
+constexpr uint32_t BEV_INNER = 0x739C0u;          // bits of the 3x3 around p: rows 1..3, cols 1..3
+// First pass of a cell: v = the sample's template value, m = occupancy of the 3x3 (outside-template
+// positions of the whole 5x5 counted occupied), and — when the opening is undecided by the 3x3 —
+// cand = the neighbours q of p whose part of N3(q) inside the 3x3 is all occupied. Returns true when v
+// is final (not occupied, the 3x3 all occupied, or no candidate: then v is already the speckle's 2).
+// Opening at p (bev.py:196-205) = OR over the q in N3(p) inside the template of AND over N3(q); the
+// centre fails whenever the 3x3 is not all occupied, so only the 8 neighbours can open p.
+__device__ __forceinline__ bool bev_cell_pass1(const BevArgs &a, const uint8_t *box, int bw, const uint32_t (&e9)[9],
+                                               uint32_t outm, int &v, uint32_t &m, uint32_t &cand) {
     int t9[9];
 #pragma unroll
-    for (int i = 0; i < 9; ++i) t9[i] = value(e9[i]);
-    int v = t9[0];
-    uint32_t m = outm;                                // occupied or outside, per window bit
+    for (int i = 0; i < 9; ++i) t9[i] = bev_value_lds(box, bw, e9[i]);
+    v = t9[0];
+    m = outm;
 #pragma unroll
     for (int i = 0; i < 9; ++i) m |= (uint32_t)occupied(a, t9[i]) << BEV_ORDER[i];
-    if (!(occupied(a, v) && (m & inner) != inner)) return v;
-    // opening at p = OR over the q in N3(p) inside the template of AND over N3(q). The centre already
-    // failed (its 3x3 is not all occupied), so the candidates are the 8 neighbours whose part of N3(q)
-    // inside the 3x3 is all occupied; only their ring pixels are evaluated (outside-template ones count
-    // as occupied and are set already). The 16 ring entries fly in one round trip
-    uint32_t cand = 0, rneed = 0;
+    cand = 0;
+    if (!(occupied(a, v) && (m & BEV_INNER) != BEV_INNER)) return true;
 #pragma unroll
     for (int qi = 0; qi < 9; ++qi) {
         if (qi == 4) continue;
         const int qx = qi % 3 - 1, qy = qi / 3 - 1, sh = qy * 5 + qx;
-        const uint32_t win = sh >= 0 ? inner << sh : inner >> -sh, wi = win & inner;
-        const bool ok = !((outm >> B5(qx, qy)) & 1u) && (m & wi) == wi;
-        cand |= ok ? 1u << qi : 0u;
-        rneed |= ok ? win & ~inner & ~outm : 0u;
+        const uint32_t win = sh >= 0 ? BEV_INNER << sh : BEV_INNER >> -sh, wi = win & BEV_INNER;
+        cand |= (!((outm >> B5(qx, qy)) & 1u) && (m & wi) == wi) ? 1u << qi : 0u;
+    }
+    if (cand == 0) { v = 2; return true; }           // isolated occupied pixel -> free (bev.py:204-205)
+    return false;
+}
+// Second pass: the candidates' ring pixels (the 16 ring entries in one round trip, only the needed
+// ones evaluated), then the opening. ring = the cell's ring entries, stride `cells`.
+__device__ __forceinline__ int bev_cell_pass2(const BevArgs &a, const uint8_t *box, int bw, int v, uint32_t m,
+                                              uint32_t cand, uint32_t outm, const uint32_t *ring, long cells) {
+    if constexpr (BEV_ABL & 1) return v;
+    uint32_t rneed = 0;
+#pragma unroll
+    for (int qi = 0; qi < 9; ++qi) {
+        const int qx = qi % 3 - 1, qy = qi / 3 - 1, sh = qy * 5 + qx;
+        const uint32_t win = sh >= 0 ? BEV_INNER << sh : BEV_INNER >> -sh;
+        rneed |= ((cand >> qi) & 1u) ? win & ~BEV_INNER & ~outm : 0u;
     }
     uint32_t er[BEV_WIN - 9];
 #pragma unroll
@@ -563,17 +587,27 @@ __device__ __forceinline__ int bev_cell_lds(const BevArgs &a, const uint8_t *box
 #pragma unroll
     for (int k = 0; k < BEV_WIN - 9; ++k) {
         const int bit = BEV_ORDER[9 + k];
-        if ((rneed >> bit) & 1u) m |= (uint32_t)occupied(a, value(er[k])) << bit;
+        if ((rneed >> bit) & 1u) m |= (uint32_t)occupied(a, bev_value_lds(box, bw, er[k])) << bit;
     }
     bool opened = false;
 #pragma unroll
     for (int qi = 0; qi < 9; ++qi) {
         if (qi == 4) continue;
         const int qx = qi % 3 - 1, qy = qi / 3 - 1, sh = qy * 5 + qx;
-        const uint32_t win = sh >= 0 ? inner << sh : inner >> -sh;
+        const uint32_t win = sh >= 0 ? BEV_INNER << sh : BEV_INNER >> -sh;
         opened |= ((cand >> qi) & 1u) && (m & win) == win;
     }
-    return opened ? v : 2;                            // isolated occupied pixel -> free (bev.py:204-205)
+    return opened ? v : 2;
+}
+// One cell of one frame from a band's LDS box, both passes (the FB = 2 form): e9 = the cell's sample +
+// 3x3 entries (offset in the box, Q5 fractions; BEV_ORDER), outm = its 25-bit outside-template mask.
+__device__ __forceinline__ int bev_cell_lds(const BevArgs &a, const uint8_t *box, int bw, const uint32_t (&e9)[9],
+                                            uint32_t outm, const uint32_t *ring, long cells) {
+    if constexpr (BEV_ABL & 4) return (int)(e9[0] & 3u) | (int)(outm & 1u);
+    int v;
+    uint32_t m, cand;
+    if (bev_cell_pass1(a, box, bw, e9, outm, v, m, cand)) return v;
+    return bev_cell_pass2(a, box, bw, v, m, cand, outm, ring, cells);
 }
 
 #ifndef BEV_CTAB
@@ -612,7 +646,7 @@ __global__ void __launch_bounds__(256, FB == 1 ? 7 : 4) bev_band_kernel(const Be
         omn = om[min(c, n - 1)];
     };
     if (lds && BEV_CTAB) load9(tid);
-    if (lds) {
+    if (lds && !(BEV_ABL & 8)) {
         // each frame's box: all of this thread's 16-B chunks in flight before the first LDS store
         const int cpr = bw >> 4, nch = bh * cpr;
 #pragma unroll
@@ -736,9 +770,52 @@ __global__ void __launch_bounds__(256, FB == 1 ? 7 : 4) bev_band_kernel(const Be
     };
 // (measured, round 3, 32 frames of 480x640, scripts/bev_sweep.py: 42.2-49.0 -> 35.6-39.2 us per launch,
 // laserscan 52.6-55.8 -> 49.8-52.1; BEV_CTAB=0: the uint4-slot form)
-    if (lds && BEV_CTAB) {
+    if (lds && BEV_CTAB && FB == 1) {
         // the LDS form on the compact table: 4-B entries, the 3x3's 9 (and the outside-template mask) of
-        // the next cell in flight while this one is evaluated (bev_cell_lds)
+        // the next cell in flight while one is evaluated. Two passes: every cell's 3x3 first (most are
+        // decided there), the cells whose opening needs ring pixels appended to a work list in LDS; then
+        // the list, so the ring work runs on full waves instead of as divergent branches of waves whose
+        // other lanes are idle (with noisy class maps the ring pass took ~40 % of the kernel)
+        __shared__ uint32_t wl_n;
+        __shared__ uint2 wl[BEV_WL];                 // (cell | cand << 16 | v << 25, m)
+        if (tid == 0) wl_n = 0;
+        __syncthreads();
+        for (int c = tid; c < n; c += 256) {
+            const int rem = r0 * a.occ_w + c;
+            uint32_t e9[9];
+#pragma unroll
+            for (int i = 0; i < 9; ++i) e9[i] = c9n[i];
+            const uint32_t outm = omn;
+            load9(c + 256);
+            int v;
+            uint32_t m, cand;
+            bool done = true;
+            if constexpr (BEV_ABL & 4) v = (int)(e9[0] & 3u) | (int)(outm & 1u);
+            else done = bev_cell_pass1(a, box[0], bw, e9, outm, v, m, cand);
+            if (!done) {
+                const uint32_t slot = c < 65536 ? atomicAdd(&wl_n, 1u) : (uint32_t)BEV_WL;
+                if (slot < (uint32_t)BEV_WL) {
+                    wl[slot] = make_uint2((uint32_t)c | cand << 16 | (uint32_t)v << 25, m);
+                    continue;
+                }
+                v = bev_cell_pass2(a, box[0], bw, v, m, cand, outm, ct + (size_t)9 * cells + c, cells);   // (list full)
+            }
+            const int cy = rem / a.occ_w, cx = rem - cy * a.occ_w;
+            bev_emit(a, b0, rem, cx, cy, cells, v);
+        }
+        __syncthreads();
+        const int nw = (int)min(wl_n, (uint32_t)BEV_WL);
+        for (int i = tid; i < nw; i += 256) {
+            const uint2 r = wl[i];
+            const int c = (int)(r.x & 0xffffu), rem = r0 * a.occ_w + c;
+            const uint32_t outm = ct[(long)BEV_WIN * cells + c];        // (L2: read again rather than kept)
+            const int v = bev_cell_pass2(a, box[0], bw, (int)(r.x >> 25), r.y, (r.x >> 16) & 0x1ffu, outm,
+                                         ct + (size_t)9 * cells + c, cells);
+            const int cy = rem / a.occ_w, cx = rem - cy * a.occ_w;
+            bev_emit(a, b0, rem, cx, cy, cells, v);
+        }
+    } else if (lds && BEV_CTAB) {
+        // (FB = 2: each cell's both passes in place)
         for (int c = tid; c < n; c += 256) {
             const int rem = r0 * a.occ_w + c;
             const int cy = rem / a.occ_w, cx = rem - cy * a.occ_w;
@@ -758,94 +835,10 @@ __global__ void __launch_bounds__(256, FB == 1 ? 7 : 4) bev_band_kernel(const Be
     }
 }
 
-// The band kernel with its latencies hidden (round 4, the default when a band has at most 1,024
-// cells and its box fits LDS). bev_band_kernel runs one (band, frame) per workgroup, all ~1,600 of them
-// resident at once, so every workgroup waits out its box staging and table loads together (SQ counters:
-// 51-59 % of wave cycles waiting). Here a workgroup takes one band and BEV_PIPE_FPW consecutive frames:
-//   * waves 0-3 (256 threads) evaluate frame b from LDS box[b & 1], the next cell's table entries in
-//     flight while one is evaluated (L2 hits);
-//   * wave 4 is a loader: while frame b is evaluated it stages frame b + 1's box into box[(b + 1) & 1]
-//     (all of its 16-B loads in flight, then the +1 label transform and the LDS stores). The compute
-//     waves never issue those loads, so their waits (ring entries) do not wait for them;
-//   * one barrier per frame hands the boxes over.
-// Same arithmetic as the band kernel (bev_cell_lds): bit-identical.
-constexpr int BEV_PIPE_FPW = 2, BEV_PIPE_KC = 4;       // frames per workgroup, max cells per compute thread
-constexpr int BEV_PIPE_LD = BEV_BAND_CAP / 1024;         // LDS-DMA instructions per box (1 KB each)
-__global__ void __launch_bounds__(320) bev_pipe_kernel(const BevArgs a) {
-    __shared__ __attribute__((aligned(16))) uint8_t box[2][BEV_BAND_CAP];
-    const int tid = threadIdx.x;
-    const bool loader = tid >= 256;                                        // wave 4 (wave-uniform)
-    const long cells = (long)a.occ_h * a.occ_w;
-    const int nbands = bev_bands(a.occ_h), nbs = (nbands + 7) >> 3;
-    const int xcd = blockIdx.x & 7, rest = blockIdx.x >> 3;
-    const int band = (rest % nbs) * 8 + xcd, f0 = (rest / nbs) * BEV_PIPE_FPW;
-    if (band >= nbands || f0 >= a.B) return;                               // workgroup-uniform
-    const int f1 = min(a.B, f0 + BEV_PIPE_FPW);
-    const int4 bb = reinterpret_cast<const int4 *>(a.wtab + (size_t)BEV_SLOTS * cells)[band];
-    const int r0 = band * BEV_BAND, n = (min(a.occ_h, r0 + BEV_BAND) - r0) * a.occ_w;
-    const uint32_t frame_bytes = (uint32_t)a.in_rows * (uint32_t)a.in_cols;
-    const int y0 = bb.x, xa = bb.y, bh = bb.z, bw = bb.w, zpad = bh * bw;   // (the host launches this form only
-    const int cpr = bw >> 4, nch = bh * cpr;                                //  when every box fits: bh >= 0)
-    // loader: frame b's box -> box[b & 1] by LDS-DMA (buffer_load ... lds: 1 KB per wave instruction, no
-    // VGPR round trip; out-of-image chunks read 0 — the image width is a multiple of 16 and xa is
-    // 16-aligned, so a chunk is all inside or all outside), then in place the labels + 1 (u8 wrap, as
-    // np.add) of the inside chunks, and the zero pad the outside-template and tap-less entries point at
-    auto stage = [&](int b) {
-        const auto seg = __builtin_amdgcn_make_buffer_rsrc(const_cast<uint8_t *>(a.seg) + (size_t)b * frame_bytes,
-                                                           (short)0, (int)frame_bytes, 0x00020000);
-        const int l = tid - 256;
-        uint8_t *bx = box[b & 1];
-        auto chunk_off = [&](int q) -> int {
-            const int r = q / cpr, c = q - r * cpr;
-            const int gy = y0 + r, gx = xa + c * 16;
-            const bool in = q < nch && (unsigned)gy < (unsigned)a.in_rows && (unsigned)gx < (unsigned)a.in_cols;
-            return in ? gy * a.in_cols + gx : -1;
-        };
-        for (int i = 0; i < BEV_PIPE_LD && 64 * i < nch; ++i) {              // (wave-uniform)
-            const int o = chunk_off(l + 64 * i);
-            __builtin_amdgcn_raw_ptr_buffer_load_lds(seg, (__attribute__((address_space(3))) void *)(bx + 1024 * i), 16,
-                                                     o >= 0 ? o : (int)0x80000000, 0, 0, 0);
-        }
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        for (int q = l; q < nch; q += 64) {
-            uint4 *pv = reinterpret_cast<uint4 *>(bx + 16 * q);
-            const uint4 v = *pv;
-            *pv = chunk_off(q) >= 0 ? make_uint4(inc4(v.x), inc4(v.y), inc4(v.z), inc4(v.w)) : make_uint4(0u, 0u, 0u, 0u);
-        }
-        for (int i = l; i < 2 * bw + 16; i += 64) bx[zpad + i] = 0;
-    };
-    // compute threads: the next cell's 3x3 entries and outside mask in flight while one is evaluated
-    // (L2 hits: the table is shared by every frame; their waits never include the loader's box loads)
-    const uint32_t *ct = reinterpret_cast<const uint32_t *>(reinterpret_cast<const unsigned char *>(a.wtab) +
-                                                            bev_ctab_offset(a.occ_w, a.occ_h)) + (size_t)r0 * a.occ_w;
-    uint32_t c9n[9], omn = 0;
-    auto load9 = [&](int c) {
-        const uint32_t *t = ct + min(c, n - 1);
-#pragma unroll
-        for (int i = 0; i < 9; ++i) c9n[i] = t[(long)i * cells];
-        omn = t[(long)BEV_WIN * cells];
-    };
-    if (loader) stage(f0);
-    else load9(tid);
-    for (int b = f0; b < f1; ++b) {
-        __syncthreads();                              // box[b & 1] staged; box[(b + 1) & 1] free again
-        if (loader) {
-            if (b + 1 < f1) stage(b + 1);
-            continue;
-        }
-        const uint8_t *bx = box[b & 1];
-        for (int c = tid; c < n; c += 256) {
-            const int rem = r0 * a.occ_w + c;
-            const int cy = rem / a.occ_w, cx = rem - cy * a.occ_w;
-            uint32_t e9[9];
-#pragma unroll
-            for (int i = 0; i < 9; ++i) e9[i] = c9n[i];
-            const uint32_t outm = omn;
-            load9(c + 256 < n ? c + 256 : tid);       // (the next frame's first cell after the last one)
-            bev_emit(a, b, rem, cx, cy, cells, bev_cell_lds(a, bx, bw, e9, outm, ct + (size_t)9 * cells + c, cells));
-        }
-    }
-}
+// (Round 4 measured a pipelined form — one band and 2 frames per workgroup, a loader wave staging the
+// next frame's box by LDS-DMA while four waves evaluate the current one — at 35.3-39.5 us per 32
+// frames against 35.3-36.4 for this kernel: the band kernel is not bound by its box staging latency.
+// Removed.)
 
 // ---- laserscan-like occupancy (bev.py:216-240; binary variant bev.py:143-164) ----------------------
 // The reference polar-warps the grid (cv2.warpPolar, nearest), finds per polar row (ray angle) the
@@ -950,14 +943,7 @@ hipError_t launch_bev(const BevArgs &a, hipStream_t s) {
     // BUGSEG_BEV_BAND=0: the gather / block-staged forms (A/B and tests)
     const char *be = std::getenv("BUGSEG_BEV_BAND");
     const bool banded = (!be || std::atoi(be) != 0) && !fe && FG == 0 && a.in_cols % 16 == 0;
-    // BUGSEG_BEV_PIPE=0: the one-frame-per-workgroup band kernel (A/B and tests)
-    const char *pe = std::getenv("BUGSEG_BEV_PIPE");
-    const bool pipe = banded && (!pe || std::atoi(pe) != 0) && !std::getenv("BUGSEG_BEV_FB") && a.pipe_ok &&
-                      (long)BEV_BAND * a.occ_w <= 256L * BEV_PIPE_KC;
-    if (pipe) {
-        const long grid = 8L * ((bev_bands(a.occ_h) + 7) / 8) * ((a.B + BEV_PIPE_FPW - 1) / BEV_PIPE_FPW);
-        hipLaunchKernelGGL(bev_pipe_kernel, dim3((unsigned)grid), dim3(320), 0, s, a);
-    } else if (banded) {
+    if (banded) {
         // frames per workgroup (BUGSEG_BEV_FB = 1 or 2; read per call)
         const char *fbe = std::getenv("BUGSEG_BEV_FB");
         // (measured at 32 frames of 480x640: FB = 1 38.7-40.1 us, FB = 2 44.6-48.5 us)

@@ -138,8 +138,16 @@ void bneck_shape(int C, int v, int &th, int &tw, int &nw, int *rd) {
 #ifndef BNECK_F32_OCC16
 #define BNECK_F32_OCC16 5
 #endif
+// fp32 C = 64 / 128: waves per SIMD the build is held to (1 = registers unconstrained; A/B knob, round 4:
+// with split-f16 products the fp32 forms are issue / latency bound at 2-3 waves per SIMD)
+#ifndef BNECK_F32_OCC64
+#define BNECK_F32_OCC64 1
+#endif
+#ifndef BNECK_F32_OCC128
+#define BNECK_F32_OCC128 1
+#endif
 template <typename T, int C, bool ASYM, int V, bool TR, int CI = 0>
-__global__ void __launch_bounds__((BShape<C, V>::NW * 64), (sizeof(T) == 2 ? BShape<C, V>::OCC : C == 16 ? BNECK_F32_OCC16 : 1)) bneck_kernel(const BneckArgs a) {
+__global__ void __launch_bounds__((BShape<C, V>::NW * 64), (sizeof(T) == 2 ? BShape<C, V>::OCC : C == 16 ? BNECK_F32_OCC16 : C == 64 ? BNECK_F32_OCC64 : BNECK_F32_OCC128)) bneck_kernel(const BneckArgs a) {
     using Raw = typename Tr<T>::Raw;
     using WRaw = typename WTr<T>::Raw;   // weight operand (fp32 mode: split-f16 parts)
     constexpr int TH = BShape<C, V>::TH, TW = BShape<C, V>::TW, NW = BShape<C, V>::NW, NT = NW * 64;

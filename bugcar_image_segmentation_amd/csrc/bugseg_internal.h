@@ -47,6 +47,8 @@ struct ConvArgs {
     int coutP;           // per-phase padded channel count (EPI_SHUFFLE / EPI_CLASSES)
     int ncls;            // EPI_CLASSES
     const uint8_t *lut;  // EPI_CLASSES: 16-entry class remap (nullptr: raw class id)
+    int lut_kind;        // EPI_CLASSES: which remap `lut` is — 0 any / none, 1 the 3-class map (models.py:56-58),
+                         // 2 the binary map (models.py:79-80): the class kernel's group-max argmax
     uint8_t *cls_out;    // EPI_CLASSES: (B, Hout, Wout) u8, may be nullptr
     float *logits_out;   // EPI_CLASSES: (B, ncls, Hout, Wout) f32 NCHW, may be nullptr
     const double *nlut;  // EPI_INIT_BGR: [3][256] normalisation table, RGB order (models.py:91)
@@ -173,7 +175,6 @@ struct BevArgs {
     // [BEV_SLOTS][occ_h*occ_w] (the 3x3 around the sample first); a property of the geometry only,
     // built once per calibration by launch_bev_table and shared by every frame
     uint4 *wtab;
-    int pipe_ok;         // every band's class-map box fits LDS (the pipelined band kernel applies)
 };
 hipError_t launch_bev(const BevArgs &a, hipStream_t s);
 hipError_t launch_bev_table(const BevArgs &a, hipStream_t s);

@@ -126,7 +126,7 @@ struct bugseg_ctx {
     // BEV warp-tap tables (bev_kernels.hip bev_table_kernel), one per recent geometry (read-only
     // once built, shared by every stream); key = the geometry fields of BevArgs. pinned: used by a
     // call that was captured into a graph — never evicted while the context lives.
-    struct BevTab { std::vector<unsigned char> key; uint4 *tab = nullptr; bool pinned = false; bool pipe_ok = false; };
+    struct BevTab { std::vector<unsigned char> key; uint4 *tab = nullptr; bool pinned = false; };
     std::vector<BevTab> bev_tabs;
     // memory retired while a stream was capturing (a graph may reference it): freed at destroy
     std::vector<void *> graveyard;
@@ -1316,13 +1316,13 @@ static int enet_forward(bugseg_ctx *ctx, const void *in, bool bgr, int B, int H,
     first.epi = bgr ? EPI_INIT_BGR : EPI_INIT;
     first.a.nlut = bgr ? (const double *)((const unsigned char *)ctx->dev_luts + 32) : nullptr;
     ConvArgs &last = pl.ops.back().a;
-    last.cls_out = nullptr; last.logits_out = nullptr; last.lut = nullptr;
+    last.cls_out = nullptr; last.logits_out = nullptr; last.lut = nullptr; last.lut_kind = 0;
     const uint8_t *luts = (const uint8_t *)ctx->dev_luts;
     switch (out_kind) {
     case BUGSEG_OUT_LOGITS_F32: last.logits_out = (float *)out; break;
     case BUGSEG_OUT_CLASS15_U8: last.cls_out = (uint8_t *)out; break;
-    case BUGSEG_OUT_CLASS3_U8: last.cls_out = (uint8_t *)out; last.lut = luts; break;
-    case BUGSEG_OUT_BINARY_U8: last.cls_out = (uint8_t *)out; last.lut = luts + 16; break;
+    case BUGSEG_OUT_CLASS3_U8: last.cls_out = (uint8_t *)out; last.lut = luts; last.lut_kind = 1; break;
+    case BUGSEG_OUT_BINARY_U8: last.cls_out = (uint8_t *)out; last.lut = luts + 16; last.lut_kind = 2; break;
     }
     const int nops = (int)pl.ops.size();
     if (last_op < 0 || last_op > nops) last_op = nops;
@@ -1593,24 +1593,17 @@ int bev_occgrid(bugseg_ctx *ctx, const uint8_t *seg, int B, const bugseg_bev_par
                 return fail(ctx, BUGSEG_ENOMEM, "BEV table allocation failed");
             a.wtab = t.tab;
             hipError_t e = launch_bev_table(a, s);
-            // the band boxes come back to the host (one int4 per band): the pipelined band kernel needs
-            // every band's box in LDS (bev_kernels.hip bev_pipe_kernel)
-            std::vector<int4> boxes((size_t)bev_bands(a.occ_h));
-            if (e == hipSuccess)
-                e = hipMemcpyAsync(boxes.data(), t.tab + (size_t)BEV_SLOTS * cells, boxes.size() * sizeof(int4),
-                                   hipMemcpyDeviceToHost, s);
             if (e == hipSuccess) e = hipStreamSynchronize(s);   // only the build itself is waited for
             if (e != hipSuccess) {
                 (void)hipFree(t.tab);
                 return fail(ctx, BUGSEG_EHIP, std::string("BEV table: ") + hipGetErrorString(e));
             }
-            t.pipe_ok = std::all_of(boxes.begin(), boxes.end(), [](const int4 &b) { return b.z >= 0; });
+
             ctx->bev_tabs.push_back(std::move(t));
             hit = &ctx->bev_tabs.back();
         }
         if (cap) hit->pinned = true;
         a.wtab = hit->tab;
-        a.pipe_ok = hit->pipe_ok ? 1 : 0;
     }
     if (p->laserscan) {
         int rc = prepare_polar(ctx, p, a, cap);

@@ -51,22 +51,33 @@ __device__ __forceinline__ bool nonzero(const RawS &r) {
 // order (D = {0, 1}, tap = ty * 2 + tx). LOGITS: the fp32 logits are written too (parity runs).
 // The next group's loads are in flight while one computes (two groups ahead measured no faster,
 // round 3: 37.3 vs 36.9 us per launch, 127 vs 109 VGPRs).
-// CLS_LOWREG (round 4): the weights stay in LDS (each lane's fragments at its own 16-B slots: conflict-free
-// ds_read_b128, re-read per group) instead of 32 kernel-long VGPRs, and the two 32-row blocks run one
-// after the other (one 16-register accumulator live, not two), so the kernel fits 8 waves per SIMD
-// (2-byte storage) instead of 4: twice the groups' loads in flight per CU
-#ifndef CLS_LOWREG
-#define CLS_LOWREG 1
+// CLS_ABL (debug ablation builds, wrong classes; scripts/gpu_r4_abl.sh): 1 = no MFMAs, 2 = no argmax,
+// 4 = no class stores, 8 = no input loads
+#ifndef CLS_ABL
+#define CLS_ABL 0
 #endif
-template <typename T, bool LOGITS>
-__global__ void __launch_bounds__(256, sizeof(T) == 2 ? (CLS_LOWREG ? 7 : 4) : (CLS_LOWREG ? 4 : 1)) cls_kernel(const ConvArgs a) {
+// (Round 4 measured a low-register form — weights from LDS, the two blocks one after the other, 7 waves
+// per SIMD instead of 4 — at 37.5 vs 34.7 us per 32-frame launch (fp16) and 75.3 vs 74.7 (fp32): the
+// class layer is not occupancy-bound. Removed.)
+// LK (round 4): the remapped class maps need only the GROUP of the first maximal class, not its index.
+// LK = 1: the 3-class map (models.py:56-58: {0, 1} -> 1, {2, 9} -> 0, the rest -> 2), LK = 2: the binary
+// map (models.py:79-80: {0, 1} -> 1, the rest -> 0). Per pixel the groups' maxima (v_max3 over the
+// members) and the overall maximum; when exactly one group attains it, that group holds the first
+// maximal class and its value is the answer. Otherwise (a tie across groups, or no class equal to the
+// maximum: all NaN) the full first-index scan decides, on a wave-uniform branch that noisy real-valued
+// logits essentially never take. LK = 0: the full scan always (raw class ids, parity runs).
+template <int LK> struct ClsGroups;
+template <> struct ClsGroups<1> { static constexpr int N = 3; static constexpr uint32_t mask[3] = {0x0204u, 0x0003u, 0xfdf8u};
+                                  static constexpr int val[3] = {0, 1, 2}; };
+template <> struct ClsGroups<2> { static constexpr int N = 2; static constexpr uint32_t mask[3] = {0x0003u, 0xfffcu, 0u};
+                                  static constexpr int val[3] = {1, 0, 0}; };
+template <typename T, bool LOGITS, int LK = 0>
+__global__ void __launch_bounds__(256, sizeof(T) == 2 ? 4 : 1) cls_kernel(const ConvArgs a) {
     constexpr int CLS_TAPS = 4;
     using Raw = typename Tr<T>::Raw;
     using WRaw = typename WTr<T>::Raw;   // weight operand (fp32 mode: split-f16 parts)
     constexpr int ES = (int)sizeof(T);
     __shared__ float sbias[64];
-    // CLS_LOWREG: the weight fragments, [block][tap][lane] (WRaw: 16 B, fp32 split parts 32 B)
-    __shared__ __attribute__((aligned(16))) WRaw sw[CLS_LOWREG ? 2 * CLS_TAPS * 64 : 1];
     const int tid = threadIdx.x, lane = tid & 63, col = lane & 31, h = lane >> 5;
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
     // a padding class (row (phase, c) with c >= ncls: zero weights) starts at -inf and stays there, so
@@ -96,26 +107,7 @@ __global__ void __launch_bounds__(256, sizeof(T) == 2 ? (CLS_LOWREG ? 7 : 4) : (
     bool short_blk[2];
 #pragma unroll
     for (int b = 0; b < 2; ++b) short_blk[b] = __ballot(nonzero(wr[b][2]) || nonzero(wr[b][3])) == 0;
-    if constexpr (CLS_LOWREG) {
-        if (wave == 0) {
-#pragma unroll
-            for (int b = 0; b < 2; ++b)
-#pragma unroll
-                for (int s = 0; s < CLS_TAPS; ++s) sw[(b * CLS_TAPS + s) * 64 + lane] = wr[b][s];
-        }
-    }
     __syncthreads();
-    // the weight fragment of (block b, tap s) for this lane: registers, or (CLS_LOWREG) read from LDS
-    // where it is used (an opaque index keeps the reads inside the group loop)
-    auto wfrag = [&](int b, int s) -> WRaw {
-        if constexpr (CLS_LOWREG) {
-            int i = (b * CLS_TAPS + s) * 64 + lane;
-            asm volatile("" : "+v"(i));
-            return sw[i];
-        } else {
-            return wr[b][s];
-        }
-    };
 
     const auto rin = mkbuf(a.in, a.in_bytes);
     const int HWg = a.Hg * a.Wg;
@@ -149,6 +141,12 @@ __global__ void __launch_bounds__(256, sizeof(T) == 2 ? (CLS_LOWREG ? 7 : 4) : (
         return q;
     };
     auto load = [&](int g, Raw (&xf)[CLS_TAPS]) {
+        if constexpr ((CLS_ABL & 8) != 0) {
+#pragma unroll
+            for (int s = 0; s < CLS_TAPS; ++s) zero(xf[s]);
+            if constexpr (sizeof(T) == 2) xf[0].v.x = (uint32_t)g;   // (something that varies, so nothing is hoisted)
+            return;
+        }
         const Px q = pixel(g);
         const uint32_t base = (uint32_t)((q.n * a.Hin + q.y) * a.Win + q.x) * pixB + (uint32_t)(8 * h * ES);
         const bool okx = q.x + 1 < a.Win, oky = q.y + 1 < a.Hin;
@@ -171,19 +169,18 @@ __global__ void __launch_bounds__(256, sizeof(T) == 2 ? (CLS_LOWREG ? 7 : 4) : (
 
     // one group: MFMAs, argmax, stores; `nxt` first receives the next group's loads (they fly during
     // this one; the two buffers alternate by unrolling, never by a runtime index).
-    auto step = [&](int g, Raw (&cur)[CLS_TAPS], Raw (&nxt)[CLS_TAPS]) {
+    auto step = [&](int g, const Raw (&cur)[CLS_TAPS], Raw (&nxt)[CLS_TAPS]) {
         // unconditional: past the last group the loads are harmless (an out-of-range group reads
         // zeros, a neighbour's group is read and dropped), and a static count of loads in flight
         // lets the waits before the MFMAs name only this group's loads (a conditional prefetch
         // made the compiler wait vmcnt(3), i.e. for the next group's first load as well).
-        // CLS_LOWREG: one buffer — the next group's loads go into `cur` once its last MFMA has read it
-        if constexpr (!CLS_LOWREG) load(g + nw, nxt);
+        load(g + nw, nxt);
         const Px q = pixel(g);
         // per block: accumulators from the bias, the taps' MFMAs, (parity runs) the logits, and the
         // argmax over this lane's classes = the sequential strict > scan from -inf of tf.math.argmax
         // (models.py:55): the maximum (v_max ignores NaN), then its first index; no class equal to the
-        // maximum (all NaN) -> 0; all -inf -> 0 (class 0 equals the maximum). The two blocks one after
-        // the other (CLS_LOWREG) or interleaved
+        // maximum (all NaN) -> 0; all -inf -> 0 (class 0 equals the maximum). Both blocks' MFMAs go
+        // first, then the two argmax scans interleaved
         auto block = [&](int b, f32x16 &acc) {
             // (the opaque offset keeps the compiler from hoisting these reads out of the group loop
             // into 32 loop-long VGPRs)
@@ -195,11 +192,12 @@ __global__ void __launch_bounds__(256, sizeof(T) == 2 ? (CLS_LOWREG ? 7 : 4) : (
                 const float4 v = bb[j];
                 acc[4 * j] = v.x; acc[4 * j + 1] = v.y; acc[4 * j + 2] = v.z; acc[4 * j + 3] = v.w;
             }
-            mma32(acc, wfrag(b, 0), cur[0]);
-            mma32(acc, wfrag(b, 1), cur[1]);
+            if constexpr ((CLS_ABL & 1) != 0 && sizeof(T) == 2) { acc[0] += __builtin_bit_cast(float, cur[0].v.x & 1u); return; }
+            mma32(acc, wr[b][0], cur[0]);
+            mma32(acc, wr[b][1], cur[1]);
             if (!short_blk[b]) {
-                mma32(acc, wfrag(b, 2), cur[2]);
-                mma32(acc, wfrag(b, 3), cur[3]);
+                mma32(acc, wr[b][2], cur[2]);
+                mma32(acc, wr[b][3], cur[3]);
             }
             if (LOGITS && q.ok) {
                 float *lo = a.logits_out + (size_t)q.n * a.ncls * plane + (size_t)(2 * q.y + b) * a.Wout + 2 * q.x + h;
@@ -208,28 +206,42 @@ __global__ void __launch_bounds__(256, sizeof(T) == 2 ? (CLS_LOWREG ? 7 : 4) : (
                     if (c < a.ncls) lo[(size_t)c * plane] = acc[c];
             }
         };
-        auto argmax = [&](const f32x16 &acc) -> int {
-            float best = acc[0];
-#pragma unroll
-            for (int c = 1; c < 16; ++c) best = __builtin_fmaxf(best, acc[c]);
-            int bi = 0;
-#pragma unroll
-            for (int c = 15; c >= 0; --c) bi = acc[c] == best ? c : bi;
-            return (int)(lut64 >> (4 * bi)) & 15;
-        };
         int cls[2];
-        if constexpr (CLS_LOWREG) {
+        f32x16 acc[2];
+        block(0, acc[0]);
+        block(1, acc[1]);
+        bool full = LK == 0;
+        if constexpr (LK != 0) {
+            // the groups' maxima, the maximum, which groups attain it
+            using G = ClsGroups<LK>;
+            bool tie = false;
 #pragma unroll
             for (int b = 0; b < 2; ++b) {
-                f32x16 acc;
-                block(b, acc);
-                if (b == 1) load(g + nw, cur);
-                cls[b] = argmax(acc);
+                float gm[G::N];
+#pragma unroll
+                for (int k = 0; k < G::N; ++k) {
+                    float m = -INFINITY;
+#pragma unroll
+                    for (int c = 0; c < 16; ++c)
+                        if ((G::mask[k] >> c) & 1u) m = __builtin_fmaxf(m, acc[b][c]);
+                    gm[k] = m;
+                }
+                float mx = gm[0];
+#pragma unroll
+                for (int k = 1; k < G::N; ++k) mx = __builtin_fmaxf(mx, gm[k]);
+                int hits = 0, v = 0;
+#pragma unroll
+                for (int k = 0; k < G::N; ++k) {
+                    const bool e = gm[k] == mx;
+                    hits += e ? 1 : 0;
+                    v = e ? G::val[k] : v;
+                }
+                cls[b] = v;
+                tie |= hits != 1;
             }
-        } else {
-            f32x16 acc[2];
-            block(0, acc[0]);
-            block(1, acc[1]);
+            full = __ballot(tie) != 0;                // wave-uniform: rare
+        }
+        if (full) {
             float best[2];
             int bi[2];
 #pragma unroll
@@ -246,12 +258,14 @@ __global__ void __launch_bounds__(256, sizeof(T) == 2 ? (CLS_LOWREG ? 7 : 4) : (
 #pragma unroll
             for (int b = 0; b < 2; ++b) cls[b] = (int)(lut64 >> (4 * bi[b])) & 15;
         }
+        if constexpr ((CLS_ABL & 2) != 0)
+            for (int b = 0; b < 2; ++b) cls[b] = acc[b][b] > acc[b][5] ? 1 : 0;
         if (a.cls_out) {
             // lanes < 32 take output row 2y (their phase-(0,0) byte + the (0,1) byte of lane + 32), lanes
             // >= 32 row 2y + 1: one 2-byte store of pixels (2x, 2x + 1) each
             uint32_t c0 = (uint32_t)cls[0], c1 = (uint32_t)cls[1];
             pl32swap(c0, c1);
-            if (q.ok) {
+            if (q.ok && (!(CLS_ABL & 4) || c0 == 77)) {
                 const size_t o = ((size_t)q.n * a.Hout + 2 * q.y + h) * a.Wout + 2 * q.x;
                 *reinterpret_cast<uint16_t *>(a.cls_out + o) = (uint16_t)(c0 | (c1 << 8));
             }
@@ -260,10 +274,6 @@ __global__ void __launch_bounds__(256, sizeof(T) == 2 ? (CLS_LOWREG ? 7 : 4) : (
     Raw xa[CLS_TAPS], xb[CLS_TAPS];
     int g = g0 + wi;
     if (g < g1) load(g, xa);
-    if constexpr (CLS_LOWREG) {
-        for (; g < g1; g += nw) step(g, xa, xa);
-        return;
-    }
     while (g < g1) {
         step(g, xa, xb);
         g += nw;
@@ -281,19 +291,26 @@ bool cls_supported(const ConvArgs &a) {
            a.Hout == 2 * a.Hg && a.Wout == 2 * a.Wg && a.Hg == a.Hin && a.Wg == a.Win;
 }
 
+template <typename T>
+static const void *cls_fun(bool lg, int lk) {
+    if (lg) return (const void *)cls_kernel<T, true, 0>;         // (parity runs: the full scan)
+    return lk == 1 ? (const void *)cls_kernel<T, false, 1> : lk == 2 ? (const void *)cls_kernel<T, false, 2>
+                   : (const void *)cls_kernel<T, false, 0>;
+}
+
 hipError_t launch_cls(int prec, const ConvArgs &a, hipStream_t s) {
     // waves stream over 32-pixel groups: enough workgroups to fill every CU at 4 waves per SIMD,
     // a multiple of 8 for the XCD split
     const int groups = (a.M + 31) / 32;
     const bool lg = a.logits_out != nullptr;
-    const void *f = prec == PREC_BF16 ? (lg ? (const void *)cls_kernel<__bf16, true> : (const void *)cls_kernel<__bf16, false>)
-                  : prec == PREC_F16  ? (lg ? (const void *)cls_kernel<_Float16, true> : (const void *)cls_kernel<_Float16, false>)
-                                      : (lg ? (const void *)cls_kernel<float, true> : (const void *)cls_kernel<float, false>);
+    // the group-max argmax applies when the class map is the remap (a.lut) the kind names
+    const int lk = a.lut && (a.lut_kind == 1 || a.lut_kind == 2) ? a.lut_kind : 0;
+    const void *f = prec == PREC_BF16 ? cls_fun<__bf16>(lg, lk) : prec == PREC_F16 ? cls_fun<_Float16>(lg, lk) : cls_fun<float>(lg, lk);
     // one round of resident workgroups (occupancy API per kernel instance, cached)
-    static const void *fs[6] = {};
-    static int caps[6] = {};
+    static const void *fs[12] = {};
+    static int caps[12] = {};
     int cap = 0;
-    for (int i = 0; i < 6; ++i)
+    for (int i = 0; i < 12; ++i)
         if (fs[i] == f) cap = caps[i];
     if (!cap) {
         int dev = 0, cus = 0, per = 0;
@@ -301,23 +318,14 @@ hipError_t launch_cls(int prec, const ConvArgs &a, hipStream_t s) {
             cus = 256;
         if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, f, 256, 0) != hipSuccess || per <= 0) per = 4;
         cap = cus * per;
-        for (int i = 0; i < 6; ++i)
+        for (int i = 0; i < 12; ++i)
             if (!fs[i]) { fs[i] = f; caps[i] = cap; break; }
     }
     int g = (groups + 3) / 4;
     g = g < cap ? g : cap;
     g = (g + 7) & ~7;
-    if (prec == PREC_BF16) {
-        if (lg) hipLaunchKernelGGL((cls_kernel<__bf16, true>), dim3(g), dim3(256), 0, s, a);
-        else hipLaunchKernelGGL((cls_kernel<__bf16, false>), dim3(g), dim3(256), 0, s, a);
-    } else if (prec == PREC_F16) {
-        if (lg) hipLaunchKernelGGL((cls_kernel<_Float16, true>), dim3(g), dim3(256), 0, s, a);
-        else hipLaunchKernelGGL((cls_kernel<_Float16, false>), dim3(g), dim3(256), 0, s, a);
-    } else {
-        if (lg) hipLaunchKernelGGL((cls_kernel<float, true>), dim3(g), dim3(256), 0, s, a);
-        else hipLaunchKernelGGL((cls_kernel<float, false>), dim3(g), dim3(256), 0, s, a);
-    }
-    return hipGetLastError();
+    void *args[] = {const_cast<ConvArgs *>(&a)};
+    return hipLaunchKernel(f, dim3(g), dim3(256), args, 0, s);
 }
 
 }  // namespace bugseg

@@ -180,7 +180,7 @@ def _bev_case(rows, cols, ww, wh, seed):
     return bev
 
 
-@pytest.mark.parametrize("form", [None, "BAND", "FB2", "G", "FG4", "F2"])
+@pytest.mark.parametrize("form", [None, "FB2", "G", "FG4", "F2"])
 @pytest.mark.parametrize("rows,cols,ww,wh,grid,seed", [
     (480, 640, 1000, 1000, (10.0, 10.0, 0.05), 0),
     (120, 160, 300, 260, (3.0, 2.0, 0.05), 1),
@@ -188,14 +188,11 @@ def _bev_case(rows, cols, ww, wh, seed):
     (64, 80, 200, 150, (1.0, 1.0, 0.1), 3),
 ])
 def test_bev_occgrid_bit_exact(gpu, rows, cols, ww, wh, grid, seed, form, monkeypatch):
-    """Every form of the rasteriser (bev_kernels.hip: the default pipelined band kernel, the
-    one-frame-per-workgroup band kernel, the gather kernel, the block-staged one, 2 frames per thread)
-    is bit-exact against the C restatement; class maps with labels past the 3-class range (up to 255:
-    segmap + 1 wraps in uint8 as np.add does, bev.py:177) included. Batches of 3 frames: the pipelined
-    kernel's 2-frame workgroups run one full and one partial frame pair."""
-    if form == "BAND":
-        monkeypatch.setenv("BUGSEG_BEV_PIPE", "0")
-    elif form == "G":
+    """Every form of the rasteriser (bev_kernels.hip: the default band-staged kernel, 2 frames per
+    band workgroup, the gather kernel, the block-staged one, 2 frames per thread) is bit-exact against
+    the C restatement; class maps with labels past the 3-class range (up to 255: segmap + 1 wraps in
+    uint8 as np.add does, bev.py:177) included."""
+    if form == "G":
         monkeypatch.setenv("BUGSEG_BEV_BAND", "0")
     elif form == "FB2":
         monkeypatch.setenv("BUGSEG_BEV_FB", "2")
@@ -401,6 +398,37 @@ def test_class_layer_kernel_matches_conv_path(gpu, blocks, prec, monkeypatch):
     assert np.array_equal(raw.cpu().numpy(), la.argmax(axis=1))
     decided = _decided(lb, la, what=f"class kernel vs conv path ({prec})") if prec == "fp32" else _margin(lb) > 0.1
     assert (la.argmax(axis=1)[decided] == lb.argmax(axis=1)[decided]).all()
+
+
+@pytest.mark.parametrize("prec", ["fp32", "fp16"])
+@pytest.mark.parametrize("tied", [False, True])
+def test_class_layer_group_argmax_is_lut_of_first_maximum(gpu, blocks, prec, tied):
+    """The remapped maps (CLASS3, BINARY) take the class kernel's group-maxima argmax (LK = 1 / 2 in
+    cls_kernels.hip); it must equal LUT[first-index argmax] of the same kernel's logits exactly. With
+    ``tied`` class 3 is given class 0's weights and bias, so every pixel whose maximum is class 0 ties
+    across groups ({0, 1} vs the rest) and takes the full-scan fallback: the first maximum, class 0."""
+    import copy
+    bl = blocks
+    if tied:
+        bl = copy.deepcopy(blocks)
+        u = bl[-1].units[0]
+        ax = [i for i, s in enumerate(u.w.shape) if s == 15][0]
+        w = np.moveaxis(u.w, ax, 0)
+        w[3] = w[0]
+        u.b[0] += 3.0                            # make class 0 win often enough
+        u.b[3] = u.b[0]
+    H, W = 120, 160
+    bgr = torch.from_numpy(synthetic.road_frames(2, H, W, seed=7)).cuda()
+    model = ENET(weights=bl, precision=prec)
+    lg = torch.empty((2, 15, H, W), dtype=torch.float32, device=gpu)
+    model.ctx.forward_bgr(bgr, 2, H, W, N.OUT_LOGITS_F32, lg)
+    first = lg.cpu().numpy().argmax(axis=1)
+    if tied:
+        assert (first == 0).mean() > 0.01        # the tie path is taken on a fair share of pixels
+    for kind, lut in ((N.OUT_CLASS3_U8, eo.LUT3), (N.OUT_BINARY_U8, eo.LUT_BINARY)):
+        seg = torch.empty((2, H, W), dtype=torch.uint8, device=gpu)
+        model.ctx.forward_bgr(bgr, 2, H, W, kind, seg)
+        assert np.array_equal(seg.cpu().numpy(), lut[first]), kind
 
 
 def test_canonical_plan_is_one_launch_per_block(gpu, blocks, monkeypatch):
