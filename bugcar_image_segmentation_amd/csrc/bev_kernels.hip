@@ -445,54 +445,100 @@ __global__ void __launch_bounds__(256, 4) bev_occgrid_lds_kernel(const BevArgs a
 // 4 grid rows: ~1,600 workgroups at 32 frames, all resident at once (16 KB of LDS each); 8 rows (40 KB,
 // 3 per CU) left a second round of workgroups: 58.5 vs 62 us for the gather kernel
 constexpr int BEV_BAND_CAP = 16384, BEV_BAND_PF = BEV_BAND_CAP / 16 / 256;
-constexpr int BEV_WL = 512;                          // band kernel: ring work-list records per workgroup   // (BEV_BAND, bev_bands: bugseg_internal.h)
+// per band BEV_BOXREC int4 records: (P, rows per part, 0, 0), then the box of each of its P row parts.
+// A band whose box would exceed BEV_BAND_CAP is split into 2 or 4 row parts (the nearest bands of a
+// forward camera span many image rows), each staged and evaluated in turn by the same workgroup;
+// only a part whose single-row box still exceeds the cap gathers from global memory.
+static_assert(BEV_BOXREC == 1 + BEV_BAND, "band record: header + one box per row part");
+constexpr int BEV_WL = 512;                          // band kernel: ring work-list records per workgroup
+static_assert(BEV_WL <= 2 * 256, "a thread takes at most two work-list records");
 // The band kernel's compact table, after the band boxes: [BEV_WIN][cells] u32, entry i of every cell
 // (BEV_ORDER_D order: the sample, its 3x3, then the ring) as the .y word alone — the tap's byte offset
 // in the band's LDS box, the fractions, the valid-tap and outside-template bits: what the LDS form
 // reads (4 B per entry instead of 8; no slot halves to pick). Filled by bev_bandbox_kernel for the
 // bands that stage their box.
-__host__ __device__ inline size_t bev_ctab_offset(int occ_w, int occ_h) {   // bytes from the table start
-    return ((size_t)occ_w * occ_h * BEV_SLOTS * 16 + (size_t)bev_bands(occ_h) * 16 + 255) & ~(size_t)255;
-}
+// (bev_ctab_offset: bugseg_internal.h)
 
 // per band: the class-map box (y0, xa, bh, bw) every valid tap of its cells reads, with a one-pixel
 // border, xa and bw whole 16-B chunks; bh = 0: no valid tap (every pixel reads the zero pad);
 // bh = -1: the box (+ its zero pad) exceeds BEV_BAND_CAP
 __global__ void __launch_bounds__(256) bev_bandbox_kernel(const BevArgs a, int4 *bbox) {
-    __shared__ int red[4];
+    __shared__ int red[BEV_BAND][4];
+    __shared__ int4 pbox[BEV_BAND];
+    __shared__ int np_rpp[2];
     const long cells = (long)a.occ_h * a.occ_w;
     const int band = blockIdx.x, r0 = band * BEV_BAND, r1 = min(a.occ_h, r0 + BEV_BAND);
-    const int n = (r1 - r0) * a.occ_w;
-    int ylo = 1 << 30, yhi = -(1 << 30), xlo = 1 << 30, xhi = -(1 << 30);
+    const int nr = r1 - r0, n = nr * a.occ_w;
+    // per band row: the extent of every valid tap of its cells
+    int ylo[BEV_BAND], yhi[BEV_BAND], xlo[BEV_BAND], xhi[BEV_BAND];
+#pragma unroll
+    for (int k = 0; k < BEV_BAND; ++k) { ylo[k] = xlo[k] = 1 << 30; yhi[k] = xhi[k] = -(1 << 30); }
     for (int i = threadIdx.x; i < n * BEV_WIN; i += 256) {
-        const int c = i / BEV_WIN, k = i - c * BEV_WIN;
+        const int c = i / BEV_WIN, k = i - c * BEV_WIN, ri = c / a.occ_w;
         const long rem = (long)r0 * a.occ_w + c;
         const uint2 e = slot_half(a.wtab[(long)(k >> 1) * cells + rem], k & 1);
         const uint32_t v = (e.y >> 10) & 15;
         const int sy = tap_sy(e), sx = tap_sx(e);
-        if (v & 3) { ylo = min(ylo, sy); yhi = max(yhi, sy); }
-        if (v & 12) { ylo = min(ylo, sy + 1); yhi = max(yhi, sy + 1); }
-        if (v & 5) { xlo = min(xlo, sx); xhi = max(xhi, sx); }
-        if (v & 10) { xlo = min(xlo, sx + 1); xhi = max(xhi, sx + 1); }
+        int y_lo = 1 << 30, y_hi = -(1 << 30), x_lo = 1 << 30, x_hi = -(1 << 30);
+        if (v & 3) { y_lo = min(y_lo, sy); y_hi = max(y_hi, sy); }
+        if (v & 12) { y_lo = min(y_lo, sy + 1); y_hi = max(y_hi, sy + 1); }
+        if (v & 5) { x_lo = min(x_lo, sx); x_hi = max(x_hi, sx); }
+        if (v & 10) { x_lo = min(x_lo, sx + 1); x_hi = max(x_hi, sx + 1); }
+#pragma unroll
+        for (int q = 0; q < BEV_BAND; ++q)
+            if (q == ri) { ylo[q] = min(ylo[q], y_lo); yhi[q] = max(yhi[q], y_hi); xlo[q] = min(xlo[q], x_lo); xhi[q] = max(xhi[q], x_hi); }
     }
-    if (threadIdx.x < 4) red[threadIdx.x] = threadIdx.x & 1 ? -(1 << 30) : (1 << 30);
+    if (threadIdx.x < 4 * BEV_BAND) red[threadIdx.x >> 2][threadIdx.x & 3] = threadIdx.x & 1 ? -(1 << 30) : (1 << 30);
     __syncthreads();
-    atomicMin(&red[0], ylo); atomicMax(&red[1], yhi); atomicMin(&red[2], xlo); atomicMax(&red[3], xhi);
-    __syncthreads();
-    int4 bx = make_int4(0, 0, 0, 16);
-    if (red[1] >= red[0]) {
-        const int y0 = red[0] - 1, bh = red[1] - red[0] + 3;
-        const int xa = (red[2] - 1) & ~15, bw = ((red[3] + 17) & ~15) - xa;
-        bx = make_int4(y0, xa, (long)bh * bw + 2 * bw + 16 <= BEV_BAND_CAP ? bh : -1, bw);
+#pragma unroll
+    for (int q = 0; q < BEV_BAND; ++q) {
+        atomicMin(&red[q][0], ylo[q]); atomicMax(&red[q][1], yhi[q]); atomicMin(&red[q][2], xlo[q]); atomicMax(&red[q][3], xhi[q]);
     }
-    if (threadIdx.x == 0) bbox[band] = bx;
-    if (bx.z < 0) return;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        // the box of rows [q0, q1) of the band: (y0, xa, bh, bw), bh = 0: no valid tap, -1: over the cap
+        auto boxof = [&](int q0, int q1) {
+            int yl = 1 << 30, yh = -(1 << 30), xl = 1 << 30, xh = -(1 << 30);
+            for (int q = q0; q < q1 && q < nr; ++q) {
+                yl = min(yl, red[q][0]); yh = max(yh, red[q][1]); xl = min(xl, red[q][2]); xh = max(xh, red[q][3]);
+            }
+            int4 bx = make_int4(0, 0, 0, 16);
+            if (yh >= yl) {
+                const int y0 = yl - 1, bh = yh - yl + 3;
+                const int xa = (xl - 1) & ~15, bw = ((xh + 17) & ~15) - xa;
+                bx = make_int4(y0, xa, (long)bh * bw + 2 * bw + 16 <= BEV_BAND_CAP ? bh : -1, bw);
+            }
+            return bx;
+        };
+        int P = 1;
+        for (; P < BEV_BAND; P *= 2) {                 // fewest row parts whose boxes all fit
+            bool fit = true;
+            for (int k = 0; k < P; ++k) fit = fit && boxof(k * (BEV_BAND / P), (k + 1) * (BEV_BAND / P)).z >= 0;
+            if (fit) break;
+        }
+        int rpp = BEV_BAND / P;
+        for (int k = 0; k < BEV_BAND; ++k) pbox[k] = k < P ? boxof(k * rpp, (k + 1) * rpp) : make_int4(0, 0, 0, 16);
+        bool fit = true;
+        for (int k = 0; k < P; ++k) fit = fit && pbox[k].z >= 0;
+        if (!fit) {                                    // even one row is over the cap: the whole band gathers
+            P = 1; rpp = BEV_BAND;
+            pbox[0] = boxof(0, BEV_BAND);
+            pbox[0].z = -1;
+        }
+        np_rpp[0] = P; np_rpp[1] = rpp;
+        bbox[(size_t)band * BEV_BOXREC] = make_int4(P, rpp, 0, 0);
+        for (int k = 0; k < BEV_BAND; ++k) bbox[(size_t)band * BEV_BOXREC + 1 + k] = pbox[k];
+    }
+    __syncthreads();
+    const int rpp = np_rpp[1];
     // each entry's top-left tap as a byte offset in the band's LDS box, in the entry's free bits 15..31
     // (a template pixel without a valid tap: the zero pad after the box); the .y words also go to the
     // compact table (bev_ctab_offset)
     uint32_t *ctab = reinterpret_cast<uint32_t *>(reinterpret_cast<unsigned char *>(a.wtab) + bev_ctab_offset(a.occ_w, a.occ_h));
     for (int i = threadIdx.x; i < n * BEV_SLOTS; i += 256) {
         const int c = i / BEV_SLOTS, q = i - c * BEV_SLOTS;
+        const int4 bx = pbox[(c / a.occ_w) / rpp];     // this cell's row part
+        if (bx.z < 0) continue;                        // (an oversized part gathers from global memory)
         const long rem = (long)r0 * a.occ_w + c;
         uint4 *sp = a.wtab + (long)q * cells + rem;
         uint4 sv = *sp;
@@ -513,6 +559,7 @@ __global__ void __launch_bounds__(256) bev_bandbox_kernel(const BevArgs a, int4 
     __syncthreads();
     uint32_t *omask = ctab + (size_t)BEV_WIN * cells;
     for (int c = threadIdx.x; c < n; c += 256) {
+        if (pbox[(c / a.occ_w) / rpp].z < 0) continue;
         const long rem = (long)r0 * a.occ_w + c;
         uint32_t m = 0;
         for (int k = 0; k < BEV_WIN; ++k)
@@ -529,7 +576,8 @@ __global__ void __launch_bounds__(256) bev_bandbox_kernel(const BevArgs a, int4 
 // outm = its 25-bit outside-template mask, ring = its 16 ring entries (stride `cells`), read only when
 // the opening needs them. Returns the template value after the speckle opening (bev.py:196-205).
 // BEV_ABL (debug ablation builds, wrong grids; scripts/gpu_r4_abl.sh): 1 = no ring pass, 4 = no template
-// values (the sample's entry bits stand in), 2 = no output stores (bev_emit), 8 = no box staging
+// values (the sample's entry bits stand in), 2 = no output stores (bev_emit), 8 = no box staging,
+// 16 = no compact-table loads (the cell index stands in), 32 = every workgroup leaves at once
 #ifndef BEV_ABL
 #define BEV_ABL 0
 #endif
@@ -618,20 +666,28 @@ __global__ void __launch_bounds__(256, FB == 1 ? 7 : 4) bev_band_kernel(const Be
     __shared__ __attribute__((aligned(16))) uint8_t box[FB][BEV_BAND_CAP];
     const int tid = threadIdx.x;
     const long cells = (long)a.occ_h * a.occ_w;
-    const int nbands = bev_bands(a.occ_h), nbs = (nbands + 7) >> 3;
+    // one work item (a band's row part) per workgroup, item i on XCD i % 8
+    const int nis = (a.nitems + 7) >> 3;
     const int xcd = blockIdx.x & 7, rest = blockIdx.x >> 3;
-    const int band = (rest % nbs) * 8 + xcd, b0 = (rest / nbs) * FB;
-    if (band >= nbands || b0 >= a.B) return;                   // workgroup-uniform
+    const int item = (rest % nis) * 8 + xcd, b0 = (rest / nis) * FB;
+    if (item >= a.nitems || b0 >= a.B || (BEV_ABL & 32)) return;  // workgroup-uniform
+    const int2 wi = reinterpret_cast<const int2 *>(reinterpret_cast<const unsigned char *>(a.wtab) +
+                                                   bev_items_offset(a.occ_w, a.occ_h))[item];
+    const int band = wi.x, part = wi.y;
     const int nf = min(FB, a.B - b0);                          // frames of this workgroup
-    const int4 bb = reinterpret_cast<const int4 *>(a.wtab + (size_t)BEV_SLOTS * cells)[band];
-    const int r0 = band * BEV_BAND, n = (min(a.occ_h, r0 + BEV_BAND) - r0) * a.occ_w;
     const uint32_t frame_bytes = (uint32_t)a.in_rows * (uint32_t)a.in_cols;
     __amdgpu_buffer_rsrc_t seg[FB];
 #pragma unroll
     for (int f = 0; f < FB; ++f)
         seg[f] = __builtin_amdgcn_make_buffer_rsrc(const_cast<uint8_t *>(a.seg) + (size_t)(f < nf ? b0 + f : b0) * frame_bytes,
                                                    (short)0, (int)frame_bytes, 0x00020000);
-    const bool lds = bb.z >= 0;                                // workgroup-uniform
+    // the band's row parts (BEV_BOXREC), evaluated in turn: part k = rows r0 .. r0 + rpp - 1 of the band
+    const int4 *rec = reinterpret_cast<const int4 *>(a.wtab + (size_t)BEV_SLOTS * cells) + (size_t)band * BEV_BOXREC;
+    const int4 hdr = rec[0];
+    (void)hdr;
+    // rows r0 .. of the band (n cells) with box bb: from LDS, or (Lc false) gathered from global memory
+    auto body = [&](const int4 bb, const int r0, const int n, auto Lc) {
+    constexpr bool lds = decltype(Lc)::value;
     const int y0 = bb.x, xa = bb.y, bh = lds ? bb.z : 0, bw = bb.w, zpad = bh * bw;
     // the LDS form's compact table (BEV_WIN planes of 4-B entries) and per-cell outside-template mask;
     // the first cell's entries are requested before the box staging, so their latency overlaps it
@@ -642,8 +698,8 @@ __global__ void __launch_bounds__(256, FB == 1 ? 7 : 4) bev_band_kernel(const Be
     auto load9 = [&](int c) {
         const uint32_t *t = ct + min(c, n - 1);
 #pragma unroll
-        for (int i = 0; i < 9; ++i) c9n[i] = t[(long)i * cells];
-        omn = om[min(c, n - 1)];
+        for (int i = 0; i < 9; ++i) c9n[i] = (BEV_ABL & 16) ? (uint32_t)(c + i) : t[(long)i * cells];
+        omn = (BEV_ABL & 16) ? (uint32_t)c : om[min(c, n - 1)];
     };
     if (lds && BEV_CTAB) load9(tid);
     if (lds && !(BEV_ABL & 8)) {
@@ -780,7 +836,11 @@ __global__ void __launch_bounds__(256, FB == 1 ? 7 : 4) bev_band_kernel(const Be
         __shared__ uint2 wl[BEV_WL];                 // (cell | cand << 16 | v << 25, m)
         if (tid == 0) wl_n = 0;
         __syncthreads();
-        for (int c = tid; c < n; c += 256) {
+        // the grid stores wait until the end: a store ahead of the next cell's table loads would hold
+        // them (vmcnt retires in order), so the first 4 cells' values stay in registers (bytes of pv)
+        uint32_t pv = 0, pdone = 0;
+        int it = 0;
+        for (int c = tid; c < n; c += 256, ++it) {
             const int rem = r0 * a.occ_w + c;
             uint32_t e9[9];
 #pragma unroll
@@ -800,20 +860,40 @@ __global__ void __launch_bounds__(256, FB == 1 ? 7 : 4) bev_band_kernel(const Be
                 }
                 v = bev_cell_pass2(a, box[0], bw, v, m, cand, outm, ct + (size_t)9 * cells + c, cells);   // (list full)
             }
-            const int cy = rem / a.occ_w, cx = rem - cy * a.occ_w;
-            bev_emit(a, b0, rem, cx, cy, cells, v);
+            if (it < 4) {
+                pv |= (uint32_t)v << (8 * it);
+                pdone |= 1u << it;
+            } else {
+                const int cy = rem / a.occ_w, cx = rem - cy * a.occ_w;
+                bev_emit(a, b0, rem, cx, cy, cells, v);
+            }
         }
         __syncthreads();
         const int nw = (int)min(wl_n, (uint32_t)BEV_WL);
-        for (int i = tid; i < nw; i += 256) {
+        int qv[2] = {0, 0}, qc[2] = {-1, -1};        // this thread's (at most two) list results
+#pragma unroll
+        for (int k = 0; k < 2; ++k) {
+            const int i = tid + 256 * k;
+            if (i >= nw) break;
             const uint2 r = wl[i];
-            const int c = (int)(r.x & 0xffffu), rem = r0 * a.occ_w + c;
+            const int c = (int)(r.x & 0xffffu);
             const uint32_t outm = ct[(long)BEV_WIN * cells + c];        // (L2: read again rather than kept)
-            const int v = bev_cell_pass2(a, box[0], bw, (int)(r.x >> 25), r.y, (r.x >> 16) & 0x1ffu, outm,
-                                         ct + (size_t)9 * cells + c, cells);
-            const int cy = rem / a.occ_w, cx = rem - cy * a.occ_w;
-            bev_emit(a, b0, rem, cx, cy, cells, v);
+            qv[k] = bev_cell_pass2(a, box[0], bw, (int)(r.x >> 25), r.y, (r.x >> 16) & 0x1ffu, outm,
+                                   ct + (size_t)9 * cells + c, cells);
+            qc[k] = c;
         }
+#pragma unroll
+        for (int k = 0; k < 4; ++k)
+            if ((pdone >> k) & 1u) {
+                const int rem = r0 * a.occ_w + tid + 256 * k, cy = rem / a.occ_w, cx = rem - cy * a.occ_w;
+                bev_emit(a, b0, rem, cx, cy, cells, (int)((pv >> (8 * k)) & 0xffu));
+            }
+#pragma unroll
+        for (int k = 0; k < 2; ++k)
+            if (qc[k] >= 0) {
+                const int rem = r0 * a.occ_w + qc[k], cy = rem / a.occ_w, cx = rem - cy * a.occ_w;
+                bev_emit(a, b0, rem, cx, cy, cells, qv[k]);
+            }
     } else if (lds && BEV_CTAB) {
         // (FB = 2: each cell's both passes in place)
         for (int c = tid; c < n; c += 256) {
@@ -833,6 +913,12 @@ __global__ void __launch_bounds__(256, FB == 1 ? 7 : 4) bev_band_kernel(const Be
     } else {
         cells_loop(std::false_type());
     }
+    };
+    const int r0 = band * BEV_BAND + part * hdr.y, n = (min(a.occ_h, r0 + hdr.y) - r0) * a.occ_w;
+    if (n <= 0) return;                                        // (a partial last band)
+    // (rec[1].z < 0: a band some single-row part of which exceeds BEV_BAND_CAP gathers as one part)
+    if (rec[1 + part].z < 0) body(rec[1 + part], r0, n, std::false_type());
+    else body(rec[1 + part], r0, n, std::true_type());
 }
 
 // (Round 4 measured a pipelined form — one band and 2 frames per workgroup, a loader wave staging the
@@ -910,8 +996,7 @@ __global__ void __launch_bounds__(256) laserscan_kernel(const BevArgs a) {
 }
 
 size_t bev_table_bytes(int occ_w, int occ_h) {
-    // tap table, band boxes, compact table (BEV_WIN planes) and the per-cell outside-template mask plane
-    return bev_ctab_offset(occ_w, occ_h) + (size_t)occ_w * occ_h * (BEV_WIN + 1) * sizeof(uint32_t);
+    return bev_items_offset(occ_w, occ_h) + (size_t)bev_bands(occ_h) * BEV_BAND * sizeof(int2);
 }
 
 hipError_t launch_bev_table(const BevArgs &a, hipStream_t s) {
@@ -948,7 +1033,7 @@ hipError_t launch_bev(const BevArgs &a, hipStream_t s) {
         const char *fbe = std::getenv("BUGSEG_BEV_FB");
         // (measured at 32 frames of 480x640: FB = 1 38.7-40.1 us, FB = 2 44.6-48.5 us)
         const int FB = fbe && std::atoi(fbe) == 2 ? 2 : 1;
-        const long grid = 8L * ((bev_bands(a.occ_h) + 7) / 8) * ((a.B + FB - 1) / FB);
+        const long grid = 8L * ((a.nitems + 7) / 8) * ((a.B + FB - 1) / FB);
         if (FB == 1) hipLaunchKernelGGL(bev_band_kernel<1>, dim3((unsigned)grid), dim3(256), 0, s, a);
         else hipLaunchKernelGGL(bev_band_kernel<2>, dim3((unsigned)grid), dim3(256), 0, s, a);
     } else if (F != 0 && a.in_cols % 16 == 0 && FG > 0) {

@@ -33,6 +33,8 @@
 #include <algorithm>
 #include <cstdlib>
 
+#include <type_traits>
+
 #include "bugseg_internal.h"
 // output stores: the per-kernel cache-policy choice (OUT_AUX_SEL: sc1 write-through for C >= 64).
 // Round 2, after the kept residual and the LDS-DMA staging: 4-9% faster per launch (C128 20x16
@@ -105,6 +107,8 @@ template <> struct BShape<16, 1> { static constexpr int TH = 20, TW = 16, NW = 4
 // had 35% of LDS cycles in bank conflicts with the 16-B pads): weight rows pad 16 elements; t0
 // pixels unpadded for 8 / 16 internal channels and 48 elements for 32 where the workgroup still fits
 // twice per CU (WIDE; asymmetric and 4x80 tiles keep 40); fp32 (parity mode) keeps 16-B pads.
+// (fp32 keeps 16-B pads: 32-B pads by the bf16 rule measured neutral on C = 128 with the split t0 below
+// — 45.8 vs 45.8 us per launch — and slower on C = 64 / 16, 77.0 -> 81.5 / 96.7 -> 108.4 us; round 4)
 __host__ __device__ constexpr int bneck_padw(int es, int C, bool wide) { return es == 2 && (C != 128 || wide) ? 16 : 16 / es; }
 __host__ __device__ constexpr int bneck_pstr(int es, int IS, bool wide) {
     return es != 2 ? IS + 16 / es : IS == 32 ? (wide ? 48 : 40) : IS;
@@ -134,9 +138,12 @@ void bneck_shape(int C, int v, int &th, int &tw, int &nw, int *rd) {
 // CI >= 32, two taps in-lane + one v_permlane32_swap for CI = 16) and leaves the pooled values in a
 // small global scratch (a.pool) that phase 3 reads back as its residual (L2 hits).
 // fp32 (parity mode): registers unconstrained (LDS bounds the C = 64 / 128 forms first), except C = 16,
-// held to 5 waves per SIMD (unconstrained it took 16 AGPRs on top of 91 VGPRs: 4; LDS allows 5)
+// held to 4 waves per SIMD (5 spilled with the split t0 storage below; unconstrained: 16 AGPRs on top of 91 VGPRs)
+#ifndef BNECK_F32_SPLIT_T0
+#define BNECK_F32_SPLIT_T0 1
+#endif
 #ifndef BNECK_F32_OCC16
-#define BNECK_F32_OCC16 5
+#define BNECK_F32_OCC16 4   // (5 spilled 32 B with the split t0: 102.0 vs 90.8 us per launch at 4)
 #endif
 // fp32 C = 64 / 128: waves per SIMD the build is held to (1 = registers unconstrained; A/B knob, round 4:
 // with split-f16 products the fp32 forms are issue / latency bound at 2-3 waves per SIMD)
@@ -279,6 +286,14 @@ __global__ void __launch_bounds__((BShape<C, V>::NW * 64), (sizeof(T) == 2 ? BSh
     constexpr bool DKEEP = BNECK_DKEEP && DN && sizeof(T) == 2 && SWAP;
     constexpr int NPK = DN ? (CI + 31) / 32 : 1;      // DKEEP: pooled 16-B chunks per lane and fragment
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+    // fp32 (parity mode): t0 / t1a live in LDS as split-f16 parts (mfma_common.h st4s: the weights'
+    // layout, 32 B per 8 channels as the f32 values take), split once when written rather than at every
+    // one of the middle conv's 9 (asymmetric: 5 + 5) operand reads. Bit-identical (the same parts).
+    using SRaw = typename std::conditional<sizeof(T) == 4 && BNECK_F32_SPLIT_T0, RawS, Raw>::type;
+    auto st4t = [](T *p, int ch, float4 v) {
+        if constexpr (sizeof(T) == 4 && BNECK_F32_SPLIT_T0) st4s(reinterpret_cast<float *>(p) - (ch & 7), ch & 7, v);
+        else st4(p, v);
+    };
 
     STAMP_ENTRY(0);
     // a workgroup without a tile leaves before staging anything (an LDS-DMA still in flight when
@@ -641,7 +656,7 @@ __global__ void __launch_bounds__((BShape<C, V>::NW * 64), (sizeof(T) == 2 ? BSh
                     if (ch >= IS) continue;
                     float4 v = act(f4(acc[r]), cs1 + ch);
                     if (!ok) v = make_float4(0.f, 0.f, 0.f, 0.f);
-                    st4(ts + h * PSTR + ch, v);
+                    st4t(ts + h * PSTR + ch, ch, v);
                 }
             }
         };
@@ -798,7 +813,7 @@ __global__ void __launch_bounds__((BShape<C, V>::NW * 64), (sizeof(T) == 2 ? BSh
                         if (ch >= IS) continue;
                         float4 v = act(f4(acc[r]), cs1 + ch);
                         if (!okc[c]) v = make_float4(0.f, 0.f, 0.f, 0.f);
-                        st4(ts + h * PSTR + ch, v);
+                        st4t(ts + h * PSTR + ch, ch, v);
                     }
                 }
                 if constexpr (DN) {
@@ -894,7 +909,7 @@ __global__ void __launch_bounds__((BShape<C, V>::NW * 64), (sizeof(T) == 2 ? BSh
                     int p = (wave + NW * j) * 16 + col;
                     if constexpr (NPX % 16 != 0) p = p < NPX ? p : 0;   // partial fragment: read anything, discarded
                     const int oy = p / TW, ox = p - oy * TW;
-                    Raw xf;
+                    SRaw xf;
                     const bool in = g < G2 && (!RD || (unsigned)(ox + tj) < (unsigned)TW);
                     int off = ((oy + ti) * HWW + (ox + tj)) * PSTR + coff;
                     asm volatile("" : "+v"(off));
@@ -927,7 +942,7 @@ __global__ void __launch_bounds__((BShape<C, V>::NW * 64), (sizeof(T) == 2 ? BSh
                     int p = f * 16 + col;
                     if constexpr (NPA % 16 != 0) p = p < NPA ? p : 0;
                     const int oy = p / TWA, ox = p - oy * TWA;
-                    Raw xf;
+                    SRaw xf;
                     ld8(xf, g < G2 ? ts + ((oy + tap) * HWW + ox) * PSTR + coff : zpad);
 #pragma unroll
                     for (int r = 0; r < NR1; ++r) mma(acc5[j][r], wf[r], xf);
@@ -944,7 +959,7 @@ __global__ void __launch_bounds__((BShape<C, V>::NW * 64), (sizeof(T) == 2 ? BSh
                         const int ox = p - (p / TWA) * TWA;
                         const bool inside = (unsigned)(ox0 - 2 + ox) < (unsigned)a.W;
                         const float4 v = act(f4(acc5[j][r]), cs2 + ch);
-                        st4(ts + p * PSTR + ch, inside ? v : make_float4(0.f, 0.f, 0.f, 0.f));
+                        st4t(ts + p * PSTR + ch, ch, inside ? v : make_float4(0.f, 0.f, 0.f, 0.f));
                     }
                 }
             __syncthreads();
@@ -967,7 +982,7 @@ __global__ void __launch_bounds__((BShape<C, V>::NW * 64), (sizeof(T) == 2 ? BSh
                         int p = (wave + NW * j) * 16 + col;
                         if constexpr (NPX % 16 != 0) p = p < NPX ? p : 0;
                         const int oy = p / TW, ox = p - oy * TW;
-                        Raw xf;
+                        SRaw xf;
                         ld8(xf, g < G2 ? ts + (oy * TWA + ox + tap) * PSTR + coff : zpad);
 #pragma unroll
                         for (int r = 0; r < NR1; ++r) mma(acc[j][r], wf[r], xf);

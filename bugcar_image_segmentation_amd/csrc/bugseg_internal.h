@@ -52,6 +52,8 @@ struct ConvArgs {
     uint8_t *cls_out;    // EPI_CLASSES: (B, Hout, Wout) u8, may be nullptr
     float *logits_out;   // EPI_CLASSES: (B, ncls, Hout, Wout) f32 NCHW, may be nullptr
     const double *nlut;  // EPI_INIT_BGR: [3][256] normalisation table, RGB order (models.py:91)
+    float naff[6];       // EPI_INIT_BGR, naff_on: the table as fmaf(v, naff[c], naff[3 + c]) (exact, see bugseg_runtime.cpp)
+    int naff_on;
     int ntiles;
     int stg_elems;       // per-wave output staging (elements)
     int stage_ok;        // EPI_SHUFFLE: fragments never straddle an input row (Wg % 16 == 0, M % 16 == 0)
@@ -78,6 +80,9 @@ hipError_t launch_cls(int prec, const ConvArgs &a, hipStream_t s);
 // ---- initial block (init_kernels.hip): EPI_INIT / EPI_INIT_BGR launches of launch_conv land here.
 // Requires the initial block's shape (3x3 s2 p1 conv of 3 channels packed as tap*8 + c, pool_k 2|3).
 hipError_t launch_init(int prec, bool bgr, const ConvArgs &a, hipStream_t s);
+// the normalisation table's exact affine form: candidates within NAFF_R ulps of base (init_kernels.hip)
+constexpr int NAFF_R = 64;
+hipError_t launch_naff_search(int prec, const double *nlut, const float *base, uint8_t *ok, hipStream_t s);
 
 // ---- fused regular / dilated / asymmetric bottleneck (bneck_kernels.hip) ---------------------
 struct BneckArgs {
@@ -175,13 +180,29 @@ struct BevArgs {
     // [BEV_SLOTS][occ_h*occ_w] (the 3x3 around the sample first); a property of the geometry only,
     // built once per calibration by launch_bev_table and shared by every frame
     uint4 *wtab;
+    // band-staged form: the (band, row part) work items (bev_items_offset in the table), heaviest first;
+    // set by the host from the band records after the table build (bugseg_runtime.cpp bev_occgrid)
+    int nitems;
 };
 hipError_t launch_bev(const BevArgs &a, hipStream_t s);
 hipError_t launch_bev_table(const BevArgs &a, hipStream_t s);
 size_t bev_table_bytes(int occ_w, int occ_h);   // tap table + per-band class-map boxes
+
 // the band-staged forms cut the grid into bands of BEV_BAND rows (one class-map box each)
 constexpr int BEV_BAND = 4;
 __host__ __device__ inline int bev_bands(int occ_h) { return (occ_h + BEV_BAND - 1) / BEV_BAND; }
 constexpr int BEV_WIN = 25, BEV_SLOTS = 13;
+// table layout (bytes from its start): tap table [BEV_SLOTS][cells] uint4; the band records (per band
+// BEV_BOXREC int4: (P, rows per part, 0, 0), then its BEV_BAND row-part boxes); the compact table
+// [BEV_WIN][cells] u32 + the outside-template mask plane [cells] u32; the work items (int2 (band,
+// part), at most BEV_BAND per band)
+constexpr int BEV_BOXREC = 5;
+__host__ __device__ inline size_t bev_records_offset(int occ_w, int occ_h) { return (size_t)occ_w * occ_h * BEV_SLOTS * 16; }
+__host__ __device__ inline size_t bev_ctab_offset(int occ_w, int occ_h) {
+    return (bev_records_offset(occ_w, occ_h) + (size_t)bev_bands(occ_h) * BEV_BOXREC * 16 + 255) & ~(size_t)255;
+}
+__host__ __device__ inline size_t bev_items_offset(int occ_w, int occ_h) {
+    return (bev_ctab_offset(occ_w, occ_h) + (size_t)occ_w * occ_h * (BEV_WIN + 1) * 4 + 255) & ~(size_t)255;
+}
 
 }  // namespace bugseg

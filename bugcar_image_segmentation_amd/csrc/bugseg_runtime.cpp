@@ -94,6 +94,8 @@ inline int pow2_nr(int npad) {   // 16-row fragments, rounded up to 1, 2, 4 or 8
 struct bugseg_ctx {
     int device = 0;
     int prec = PREC_F32;
+    float naff[6] = {};                            // exact affine form of the normalisation table (find_affine)
+    bool naff_on = false;
     std::string err;
     bool loaded = false;
     int ncls = 0;
@@ -126,7 +128,7 @@ struct bugseg_ctx {
     // BEV warp-tap tables (bev_kernels.hip bev_table_kernel), one per recent geometry (read-only
     // once built, shared by every stream); key = the geometry fields of BevArgs. pinned: used by a
     // call that was captured into a graph — never evicted while the context lives.
-    struct BevTab { std::vector<unsigned char> key; uint4 *tab = nullptr; bool pinned = false; };
+    struct BevTab { std::vector<unsigned char> key; uint4 *tab = nullptr; bool pinned = false; int nitems = 0; };
     std::vector<BevTab> bev_tabs;
     // memory retired while a stream was capturing (a graph may reference it): freed at destroy
     std::vector<void *> graveyard;
@@ -1144,6 +1146,7 @@ int bugseg_create(int device, int precision, bugseg_ctx **out) {
             const double x = ((double)v / 256.0 - mean[ch]) / stdv[ch];
             std::memcpy(tab + 32 + (ch * 256 + v) * 8, &x, 8);
         }
+
     {
         // uploaded on the context's private stream (never the legacy stream, which would join a capture
         // in progress on another stream), so a context may be created while a stream is capturing
@@ -1152,6 +1155,43 @@ int bugseg_create(int device, int precision, bugseg_ctx **out) {
         hipError_t e = s ? hipMalloc(&c->dev_luts, sizeof(tab)) : hipErrorInvalidValue;
         if (e == hipSuccess) e = hipMemcpyAsync(c->dev_luts, tab, sizeof(tab), hipMemcpyHostToDevice, s);
         if (e == hipSuccess) e = hipStreamSynchronize(s);
+        // bf16 / fp16: the fused initial block evaluates the table as one fmaf per byte when an f32
+        // pair (a, b) near (1 / (256 std), -mean / std) reproduces all 256 stored values of a channel
+        // bit for bit (searched on the device, with its own conversions: init_kernels.hip
+        // naff_search_kernel) — no LDS lookups, whose data-dependent addresses conflict; fp32 keeps
+        // the table. BUGSEG_INIT_TABLE=1 forces the table (A/B)
+        if (e == hipSuccess && c->prec != PREC_F32) {
+            float base[6];
+            for (int ch = 0; ch < 3; ++ch) {
+                base[ch] = (float)(1.0 / (256.0 * stdv[ch]));
+                base[3 + ch] = (float)(-mean[ch] / stdv[ch]);
+            }
+            constexpr int N = 2 * NAFF_R + 1;
+            std::vector<uint8_t> okh((size_t)3 * N * N);
+            uint8_t *okd = nullptr;
+            hipError_t e2 = hipMalloc(&okd, okh.size());
+            if (e2 == hipSuccess) e2 = launch_naff_search(c->prec, (const double *)((const unsigned char *)c->dev_luts + 32), base, okd, s);
+            if (e2 == hipSuccess) e2 = hipMemcpyAsync(okh.data(), okd, okh.size(), hipMemcpyDeviceToHost, s);
+            if (e2 == hipSuccess) e2 = hipStreamSynchronize(s);
+            if (okd) (void)hipFree(okd);
+            bool all = e2 == hipSuccess;
+            for (int ch = 0; ch < 3 && all; ++ch) {
+                int best = -1, bestd = 1 << 30;
+                for (int k = 0; k < N * N; ++k) {
+                    const int da = k / N - NAFF_R, db = k % N - NAFF_R, d = std::max(std::abs(da), std::abs(db));
+                    if (okh[(size_t)ch * N * N + k] && d < bestd) { best = k; bestd = d; }
+                }
+                if (best < 0) { all = false; break; }
+                int32_t ia, ib;
+                std::memcpy(&ia, &base[ch], 4);
+                std::memcpy(&ib, &base[3 + ch], 4);
+                ia += best / N - NAFF_R;
+                ib += best % N - NAFF_R;
+                std::memcpy(&c->naff[ch], &ia, 4);
+                std::memcpy(&c->naff[3 + ch], &ib, 4);
+            }
+            c->naff_on = all;
+        }
         if (e != hipSuccess) {
             if (c->dev_luts) (void)hipFree(c->dev_luts);
             if (c->setup) (void)hipStreamDestroy(c->setup);
@@ -1315,6 +1355,8 @@ static int enet_forward(bugseg_ctx *ctx, const void *in, bool bgr, int B, int H,
     first.a.in = in;
     first.epi = bgr ? EPI_INIT_BGR : EPI_INIT;
     first.a.nlut = bgr ? (const double *)((const unsigned char *)ctx->dev_luts + 32) : nullptr;
+    first.a.naff_on = bgr && ctx->naff_on && !std::getenv("BUGSEG_INIT_TABLE");
+    std::memcpy(first.a.naff, ctx->naff, sizeof(ctx->naff));
     ConvArgs &last = pl.ops.back().a;
     last.cls_out = nullptr; last.logits_out = nullptr; last.lut = nullptr; last.lut_kind = 0;
     const uint8_t *luts = (const uint8_t *)ctx->dev_luts;
@@ -1594,6 +1636,23 @@ int bev_occgrid(bugseg_ctx *ctx, const uint8_t *seg, int B, const bugseg_bev_par
             a.wtab = t.tab;
             hipError_t e = launch_bev_table(a, s);
             if (e == hipSuccess) e = hipStreamSynchronize(s);   // only the build itself is waited for
+            // the band-staged form's work items from the band records: one per (band, row part), the
+            // nearest bands (largest boxes, most opening work) first so they start in the first round
+            const int nb = bev_bands(a.occ_h);
+            std::vector<int4> rec((size_t)nb * BEV_BOXREC);
+            std::vector<int2> items;
+            if (e == hipSuccess)
+                e = hipMemcpyAsync(rec.data(), (unsigned char *)t.tab + bev_records_offset(a.occ_w, a.occ_h),
+                                   rec.size() * sizeof(int4), hipMemcpyDeviceToHost, s);
+            if (e == hipSuccess) e = hipStreamSynchronize(s);
+            if (e == hipSuccess) {
+                for (int b = nb - 1; b >= 0; --b)
+                    for (int k = 0; k < std::max(1, std::min(BEV_BAND, rec[(size_t)b * BEV_BOXREC].x)); ++k) items.push_back(make_int2(b, k));
+                e = hipMemcpyAsync((unsigned char *)t.tab + bev_items_offset(a.occ_w, a.occ_h), items.data(),
+                                   items.size() * sizeof(int2), hipMemcpyHostToDevice, s);
+            }
+            if (e == hipSuccess) e = hipStreamSynchronize(s);
+            t.nitems = (int)items.size();
             if (e != hipSuccess) {
                 (void)hipFree(t.tab);
                 return fail(ctx, BUGSEG_EHIP, std::string("BEV table: ") + hipGetErrorString(e));
@@ -1604,6 +1663,7 @@ int bev_occgrid(bugseg_ctx *ctx, const uint8_t *seg, int B, const bugseg_bev_par
         }
         if (cap) hit->pinned = true;
         a.wtab = hit->tab;
+        a.nitems = hit->nitems;
     }
     if (p->laserscan) {
         int rc = prepare_polar(ctx, p, a, cap);

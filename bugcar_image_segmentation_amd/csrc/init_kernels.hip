@@ -34,6 +34,12 @@
 
 namespace bugseg {
 
+// INIT_ABL (debug ablation builds, wrong results; scripts/gpu_r4_abl.sh): 1 = no normalisation table
+// (the byte itself), 2 = no output stores, 4 = no pool channels, 8 = no patch loads
+#ifndef INIT_ABL
+#define INIT_ABL 0
+#endif
+
 constexpr int IT_H = 8, IT_W = 32;                        // output tile
 constexpr int IP_H = 2 * IT_H + 1, IP_W = 2 * IT_W + 1;   // input patch (pixels)
 constexpr int IP_RS = IP_W * 3 + 1;                       // LDS patch row stride (elements, even)
@@ -55,7 +61,8 @@ __global__ void __launch_bounds__(256) init_kernel(const ConvArgs a) {
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
     if constexpr (BGR) {
         // rounded exactly as the engine-input path rounds it (f64 -> f32 -> T)
-        for (int i = tid; i < 3 * 256; i += 256) lut[i] = (float)(T)(float)a.nlut[i];
+        if (!(sizeof(T) == 2 && a.naff_on))
+            for (int i = tid; i < 3 * 256; i += 256) lut[i] = (float)(T)(float)a.nlut[i];
     }
     // A operand (weights), loop-invariant: row = output channel `col`, k = 8*kq + j in the order of
     // init_k, from the generic packing [Npad][Kpad] with k' = tap * 8 + c.
@@ -96,6 +103,9 @@ __global__ void __launch_bounds__(256) init_kernel(const ConvArgs a) {
     const bool qok = q < IP_W * 3;
     const int dpatch = BGR ? px * 3 + (2 - cb) : q;        // BGR byte cb is RGB channel 2 - cb (models.py:87)
     const int lbase = (2 - cb) * 256;
+    // the table's exact affine form (bf16 / fp16, when the host found one: bugseg_runtime.cpp
+    // find_affine): this thread's channel constants, no LDS lookups
+    const float na = a.naff[2 - cb], nb = a.naff[5 - cb];
 
     const int tiles_x = (a.Wg + IT_W - 1) / IT_W, tiles_y = (a.Hg + IT_H - 1) / IT_H;
     const int per = tiles_x * tiles_y, ntiles = a.B * per;
@@ -130,7 +140,8 @@ __global__ void __launch_bounds__(256) init_kernel(const ConvArgs a) {
 #pragma unroll
         for (int r = 0; r < IP_H; ++r) {
             const int off = (int)(base + (uint32_t)r * rowB);
-            if constexpr (BGR) raw[r] = __builtin_amdgcn_raw_buffer_load_b8(rin, off, 0, 0);
+            if constexpr ((INIT_ABL & 8) != 0) raw[r] = (uint32_t)(off + r);
+            else if constexpr (BGR) raw[r] = __builtin_amdgcn_raw_buffer_load_b8(rin, off, 0, 0);
             else if constexpr (sizeof(T) == 2) raw[r] = __builtin_amdgcn_raw_buffer_load_b16(rin, off, 0, 0);
             else raw[r] = __builtin_amdgcn_raw_buffer_load_b32(rin, off, 0, 0);
         }
@@ -160,7 +171,9 @@ __global__ void __launch_bounds__(256) init_kernel(const ConvArgs a) {
                 T v;
                 if constexpr (BGR) {
                     // f16: through f32, as the separate preprocess stores the engine input (prep_kernels.hip)
-                    if constexpr (__is_same(T, _Float16)) v = (T)(float)lut[lbase + (int)(raw[r] & 0xff)];
+                    if constexpr ((INIT_ABL & 1) != 0) v = (T)(float)(raw[r] & 0xff);
+                    else if (sizeof(T) == 2 && a.naff_on) v = (T)__builtin_fmaf((float)(raw[r] & 0xff), na, nb);
+                    else if constexpr (__is_same(T, _Float16)) v = (T)(float)lut[lbase + (int)(raw[r] & 0xff)];
                     else v = (T)lut[lbase + (int)(raw[r] & 0xff)];
                 }
                 else if constexpr (sizeof(T) == 2) v = __builtin_bit_cast(T, (unsigned short)raw[r]);
@@ -194,7 +207,7 @@ __global__ void __launch_bounds__(256) init_kernel(const ConvArgs a) {
                         mx = fmaxf(mx, (float)pp[dy * IP_RS + dx * 3 + ch]);
                     }
                 }
-                pm[ch] = mx;
+                pm[ch] = (INIT_ABL & 4) ? 0.f : mx;
             }
         }
 
@@ -237,7 +250,7 @@ __global__ void __launch_bounds__(256) init_kernel(const ConvArgs a) {
             }
             v = prelu4(add4(v, make_float4(pv[0], pv[1], pv[2], pv[3])), s4);
             const int oy = ty0 + lr, ox = tx0 + lc;
-            const bool ok = oy < a.Hg && ox < a.Wg && c0 < a.outC;
+            const bool ok = oy < a.Hg && ox < a.Wg && c0 < a.outC && (!(INIT_ABL & 2) || v.x == 12345.f);
             const uint32_t off = ok ? (uint32_t)(((n * a.Hg + oy) * a.Wg + ox) * a.outC + c0) * (uint32_t)sizeof(T) : OOB;
             if constexpr (sizeof(T) == 2) {
                 bst8o<OUT_AUX_SEL(16)>(rout, off, pack4<T>(v));
@@ -246,6 +259,35 @@ __global__ void __launch_bounds__(256) init_kernel(const ConvArgs a) {
             }
         }
     }
+}
+
+// The exact affine form of the normalisation table (bf16 / fp16 storage): candidate k of channel c is the
+// f32 pair (a, b) = (base[c], base[3 + c]) moved by (da, db) ulps, |da|, |db| <= NAFF_R; it is exact when
+// T(fmaf(v, a, b)) == T((float)nlut[c][v]) — the stored table value, bits compared — for all 256
+// bytes v. Evaluated here with the device's own conversions, so the init kernel's fmaf form is the
+// table's value by construction. ok[c * NAFF_N^2 + (da + R) * NAFF_N + db + R] = 1 when exact.
+struct NaffBase { float v[6]; };
+template <typename T>
+__global__ void __launch_bounds__(256) naff_search_kernel(const double *nlut, NaffBase base, uint8_t *ok) {
+    constexpr int N = 2 * NAFF_R + 1, NC = N * N;
+    const int i = blockIdx.x * 256 + threadIdx.x;
+    if (i >= 3 * NC) return;
+    const int c = i / NC, k = i - c * NC, da = k / N - NAFF_R, db = k % N - NAFF_R;
+    const float a = __int_as_float(__float_as_int(base.v[c]) + da), b = __int_as_float(__float_as_int(base.v[3 + c]) + db);
+    bool good = true;
+    for (int v = 0; v < 256 && good; ++v) {
+        const T want = (T)(float)nlut[c * 256 + v], got = (T)__builtin_fmaf((float)v, a, b);
+        good = __builtin_bit_cast(unsigned short, want) == __builtin_bit_cast(unsigned short, got);
+    }
+    ok[i] = good ? 1 : 0;
+}
+hipError_t launch_naff_search(int prec, const double *nlut, const float *base, uint8_t *ok, hipStream_t s) {
+    NaffBase b;
+    for (int i = 0; i < 6; ++i) b.v[i] = base[i];
+    const int n = 3 * (2 * NAFF_R + 1) * (2 * NAFF_R + 1), g = (n + 255) / 256;
+    if (prec == PREC_BF16) hipLaunchKernelGGL(naff_search_kernel<__bf16>, dim3(g), dim3(256), 0, s, nlut, b, ok);
+    else hipLaunchKernelGGL(naff_search_kernel<_Float16>, dim3(g), dim3(256), 0, s, nlut, b, ok);
+    return hipGetLastError();
 }
 
 int init_tiles(const ConvArgs &a) {

@@ -122,6 +122,30 @@ __device__ __forceinline__ void mma(f32x4 &acc, const RawS &w, const RawF &x) {
     acc = __builtin_amdgcn_mfma_f32_16x16x32_f16(wh, xl, acc, 0, 0, 0);
     acc = __builtin_amdgcn_mfma_f32_16x16x32_f16(wh, xh, acc, 0, 0, 0);
 }
+// both operands already split (fp32-mode activations stored as split parts, bneck_kernels.hip): the
+// same three products in the same order as above, so the same result bit for bit
+__device__ __forceinline__ void mma(f32x4 &acc, const RawS &w, const RawS &x) {
+    const f16x8 wh = __builtin_bit_cast(f16x8, w.h), wl = __builtin_bit_cast(f16x8, w.l);
+    const f16x8 xh = __builtin_bit_cast(f16x8, x.h), xl = __builtin_bit_cast(f16x8, x.l);
+    acc = __builtin_amdgcn_mfma_f32_16x16x32_f16(wl, xh, acc, 0, 0, 0);
+    acc = __builtin_amdgcn_mfma_f32_16x16x32_f16(wh, xl, acc, 0, 0, 0);
+    acc = __builtin_amdgcn_mfma_f32_16x16x32_f16(wh, xh, acc, 0, 0, 0);
+}
+// 4 consecutive channels (first channel % 8 = sub: 0 or 4) of an 8-channel group stored as split-f16
+// parts in the weight layout (32 B: the 8 hi parts, then the 8 lo parts), split as split_f16 does
+__device__ __forceinline__ void st4s(float *grp, int sub, float4 v) {
+    const float e[4] = {v.x, v.y, v.z, v.w};
+    _Float16 h[4], l[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+        h[i] = (_Float16)e[i];
+        l[i] = (_Float16)(e[i] - (float)h[i]);
+    }
+    const f16x4 hv = {h[0], h[1], h[2], h[3]}, lv = {l[0], l[1], l[2], l[3]};
+    unsigned char *g = reinterpret_cast<unsigned char *>(grp);
+    *reinterpret_cast<f16x4 *>(g + 2 * sub) = hv;
+    *reinterpret_cast<f16x4 *>(g + 16 + 2 * sub) = lv;
+}
 // exact f32 products (DeepLab's fp32 mode): sub-MFMA j contracts element j of every lane's 8-group
 // (lane>>4 = group), so the 8 sub-MFMAs together cover the same 32 k as one bf16 MFMA.
 __device__ __forceinline__ void mma(f32x4 &acc, const RawF &w, const RawF &x) {

@@ -299,6 +299,22 @@ def test_forward_bgr_equals_preprocess_then_forward(gpu, prec, pool_k):
     assert torch.equal(m.predict_device(x2, N.OUT_LOGITS_F32), c)
 
 
+@pytest.mark.parametrize("prec", ["bf16", "fp16"])
+def test_init_affine_normalisation_equals_table(gpu, blocks, prec, monkeypatch):
+    """bf16 / fp16: the fused initial block normalises each byte as one fmaf with per-channel constants
+    the context found exact on the device (bugseg_runtime.cpp, init_kernels.hip naff_search_kernel);
+    the table form (BUGSEG_INIT_TABLE=1) gives the same logits bit for bit, at the bench shape."""
+    B, H, W = 2, 480, 640
+    bgr = torch.from_numpy(synthetic.uniform_frames(B, H, W)).cuda()
+    m = ENET(weights=blocks, precision=prec)
+    a = torch.empty((B, 15, H, W), dtype=torch.float32, device=gpu)
+    m.ctx.forward_bgr(bgr, B, H, W, N.OUT_LOGITS_F32, a)
+    monkeypatch.setenv("BUGSEG_INIT_TABLE", "1")
+    b = torch.empty_like(a)
+    m.ctx.forward_bgr(bgr, B, H, W, N.OUT_LOGITS_F32, b)
+    assert torch.equal(a, b)
+
+
 @pytest.mark.parametrize("variant", [None, "0", "1", "2", "3", "4"])
 @pytest.mark.parametrize("prec", ["fp32", "bf16", "fp16"])
 @pytest.mark.parametrize("H,W", [(64, 96), (72, 104), (120, 160), (480, 640)])
