@@ -272,9 +272,17 @@ __global__ void __launch_bounds__((BShape<C, V>::NW * 64), (sizeof(T) == 2 ? BSh
 #ifndef BNECK_KEEP_C64
 #define BNECK_KEEP_C64 0    // C = 64: measured 41.0 vs 38.0 us per launch with the residual kept (wave 0 takes a third load round trip for its second border fragment; batching it spills)
 #endif
-    constexpr bool KEEP = BNECK_KEEP && !DN && sizeof(T) == 2 && (!ASYM || BNECK_KEEP_ASYM) && (SWAP || !REG3) && (C != 64 || BNECK_KEEP_C64) &&
-                          NF2 * KS1 * 4 <= (C == 128 ? 48 : 32);   // kept VGPRs within the occupancy budget
-    static_assert(!KEEP || !REG3 || KS1 == RQ3, "kept x: one 16-B chunk per k-step and row pair");
+#ifndef BNECK_KEEP_F32
+#define BNECK_KEEP_F32 1
+#endif
+    // KEEPF (round 4): the fp32 C = 128 forms keep their residual too. One workgroup per CU (LDS), so
+    // 256 VGPRs per lane: the 96 of the kept x replace the 64 of the residual ring. A lane's k-step s
+    // chunk holds channels 32 s + 8 kq .. + 7 as two quads; phase 3 wants quad 16 r + 4 kq .. + 3 of
+    // row block r: a row swap then a half swap per dword gather rows 2 s and 2 s + 1 (as in bf16)
+    constexpr bool KEEPF = BNECK_KEEP_F32 && !DN && sizeof(T) == 4 && !ASYM && C == 128 && REG3 && !SWAP;
+    constexpr bool KEEP = (BNECK_KEEP && !DN && sizeof(T) == 2 && (!ASYM || BNECK_KEEP_ASYM) && (SWAP || !REG3) && (C != 64 || BNECK_KEEP_C64) &&
+                           NF2 * KS1 * 4 <= (C == 128 ? 48 : 32)) || KEEPF;   // kept VGPRs within the occupancy budget
+    static_assert(!KEEP || !REG3 || (KEEPF ? 2 * KS1 == RQ3 : KS1 == RQ3), "kept x: one 16-B chunk per k-step and row pair");
 #ifndef BNECK_DKEEP
 #define BNECK_DKEEP 1
 #endif
@@ -688,11 +696,12 @@ __global__ void __launch_bounds__((BShape<C, V>::NW * 64), (sizeof(T) == 2 ? BSh
             // projections to consume one fragment at a time
             if (GLDS && first) {
                 int nld = 0;
+                constexpr int LPS = sizeof(T) == 4 ? 2 : 1;   // 16-B loads per k-step chunk (fp32: two)
 #pragma unroll
-                for (int j = 0; j < NF2; ++j) nld += wave + NW * j < NFT ? KS1 : 0;
+                for (int j = 0; j < NF2; ++j) nld += wave + NW * j < NFT ? KS1 * LPS : 0;
 #pragma unroll
-                for (int k = 0; k < NBE && k < NBW; ++k) nld += wb + NW * k < NFB ? KS1 : 0;
-                vm_wait_upto(BNECK_GLDS_PARTIAL ? nld : 0);
+                for (int k = 0; k < NBE && k < NBW; ++k) nld += wb + NW * k < NFB ? KS1 * LPS : 0;
+                vm_wait_upto(BNECK_GLDS_PARTIAL ? (nld < 24 ? nld & ~1 : 24) : 0);   // (fewer outstanding: still after the weights)
             }
             asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
             __builtin_amdgcn_s_barrier();   // weights staged (first tile) / previous tile done with ts
@@ -1096,6 +1105,22 @@ __global__ void __launch_bounds__((BShape<C, V>::NW * 64), (sizeof(T) == 2 ? BSh
         for (int j = 0; j < NF2; ++j) {
             if (wave + NW * j >= NFT) break;              // wave-uniform
             const uint32_t po = pix_base(wave + NW * j, col);
+            if constexpr (KEEPF) {
+                // kept fp32 x -> residual quads in place: .a = row 2 s, .b = row 2 s + 1
+#pragma unroll
+                for (int s = 0; s < KS1; ++s) {
+                    RawF &k = reinterpret_cast<RawF &>(kx[j][s]);
+                    uint32_t a[4] = {__float_as_uint(k.a.x), __float_as_uint(k.a.y), __float_as_uint(k.a.z), __float_as_uint(k.a.w)};
+                    uint32_t b[4] = {__float_as_uint(k.b.x), __float_as_uint(k.b.y), __float_as_uint(k.b.z), __float_as_uint(k.b.w)};
+#pragma unroll
+                    for (int d = 0; d < 4; ++d) {
+                        pl16swap(a[d], b[d]);
+                        pl32swap(a[d], b[d]);
+                    }
+                    k.a = make_float4(__uint_as_float(a[0]), __uint_as_float(a[1]), __uint_as_float(a[2]), __uint_as_float(a[3]));
+                    k.b = make_float4(__uint_as_float(b[0]), __uint_as_float(b[1]), __uint_as_float(b[2]), __uint_as_float(b[3]));
+                }
+            }
             auto out3 = [&](int r, const f32x4 &acc) {
                 const int ch = r * 16 + kq * 4;
                 return act(bias_in_acc(NR3, 1) ? f4(acc) : add4(f4(acc), ld4f(cb3 + ch)), cs3 + ch);
@@ -1104,7 +1129,10 @@ __global__ void __launch_bounds__((BShape<C, V>::NW * 64), (sizeof(T) == 2 ? BSh
             for (int t = 0; t < RQ3; ++t) {
                 const uint32_t off = po == OOB ? OOB : po + (uint32_t)chunk_ch(t) * (uint32_t)sizeof(T);
                 uint4 rc;
-                if constexpr (KEEP) rc = kx[j][t].v;
+                if constexpr (KEEPF) {
+                    const RawF &k = reinterpret_cast<const RawF &>(kx[j][t >> 1]);
+                    rc = __builtin_bit_cast(uint4, (t & 1) ? k.b : k.a);
+                } else if constexpr (KEEP) rc = reinterpret_cast<const RawH &>(kx[j][t]).v;
                 else if constexpr (DKEEP) rc = t < NPK ? pres[j][t < NPK ? t : 0] : make_uint4(0u, 0u, 0u, 0u);
                 else rc = res[j % RP][t];
                 if constexpr (SWAP) {
