@@ -305,20 +305,25 @@ def roofline_record(ctx, Bs, H, W, reps, stream, precision, t_fwd):
     return rec, table
 
 
-def mode_record(blocks, bev, grid, H, W, frames, streams, steps, precision):
+def mode_record(blocks, bev, grid, H, W, frames, streams, steps, precision, graph=True):
     """Another precision mode (fp32: the parity mode, logits within 1e-3 of the oracle; fp16 / bf16)
-    on the same step, same batch; with its own roofline (dominant kernel, HBM and MFMA fractions)."""
+    on the same step, same batch, timed as the headline is (the step replayed as one captured HIP graph
+    unless --graph 0); with its own roofline (dominant kernel, HBM and MFMA fractions)."""
     from bugcar_image_segmentation_amd.models import ENET
     from bugcar_image_segmentation_amd.pipeline import OccupancyPipeline
     B = frames.shape[0]
     model = ENET(weights=blocks, precision=precision)
     pipe = OccupancyPipeline(model, bev, *grid, model_hw=(H, W), streams=streams)
-    for _ in range(3):
-        pipe.run(frames)
+    run = lambda: pipe.run(frames)  # noqa: E731
+    if graph:
+        replay, _grids = pipe.capture(frames)
+        run = replay
+    for _ in range(5):
+        run()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     for _ in range(steps):
-        pipe.run(frames)
+        run()
     torch.cuda.synchronize()
     el = time.perf_counter() - t0
     stream = torch.cuda.current_stream()
@@ -328,7 +333,7 @@ def mode_record(blocks, bev, grid, H, W, frames, streams, steps, precision):
     roof, table = roofline_record(model.ctx, Bs, H, W, 10, stream, precision, t_fwd)
     del pipe, model
     return {"value": round(B * steps / el, 2), "unit": "frames/s", "ms_per_step": round(el / steps * 1e3, 4),
-            "per_gpu_batch": B, "steps": steps, "streams_per_gpu": streams, "dtype": precision,
+            "per_gpu_batch": B, "steps": steps, "streams_per_gpu": streams, "hip_graph": bool(graph), "dtype": precision,
             "roofline": roof, "kernels": table}
 
 
@@ -545,7 +550,7 @@ def main():
             for prec in ("fp32", "fp16", "bf16"):
                 if prec != a.precision:
                     log(f"{prec} sub-record")
-                    res[prec] = mode_record(blocks, bev, grid, H, W, frames, a.streams, max(5, a.steps // 2), prec)
+                    res[prec] = mode_record(blocks, bev, grid, H, W, frames, a.streams, max(10, a.steps), prec, bool(a.graph))
             log("batch-1 latency sub-records")
             res["latency_b1_ms"] = latency_b1(blocks, a.precision, bev, grid, H, W, frames[:1], 100)
             # BASELINE config 2 names bf16 at batch 1

@@ -275,11 +275,14 @@ __global__ void __launch_bounds__((BShape<C, V>::NW * 64), (sizeof(T) == 2 ? BSh
 #ifndef BNECK_KEEP_F32
 #define BNECK_KEEP_F32 1
 #endif
+#ifndef BNECK_KEEP_F32_ASYM
+#define BNECK_KEEP_F32_ASYM 1
+#endif
     // KEEPF (round 4): the fp32 C = 128 forms keep their residual too. One workgroup per CU (LDS), so
     // 256 VGPRs per lane: the 96 of the kept x replace the 64 of the residual ring. A lane's k-step s
     // chunk holds channels 32 s + 8 kq .. + 7 as two quads; phase 3 wants quad 16 r + 4 kq .. + 3 of
     // row block r: a row swap then a half swap per dword gather rows 2 s and 2 s + 1 (as in bf16)
-    constexpr bool KEEPF = BNECK_KEEP_F32 && !DN && sizeof(T) == 4 && !ASYM && C == 128 && REG3 && !SWAP;
+    constexpr bool KEEPF = BNECK_KEEP_F32 && !DN && sizeof(T) == 4 && (!ASYM || BNECK_KEEP_F32_ASYM) && C == 128 && REG3 && !SWAP;
     constexpr bool KEEP = (BNECK_KEEP && !DN && sizeof(T) == 2 && (!ASYM || BNECK_KEEP_ASYM) && (SWAP || !REG3) && (C != 64 || BNECK_KEEP_C64) &&
                            NF2 * KS1 * 4 <= (C == 128 ? 48 : 32)) || KEEPF;   // kept VGPRs within the occupancy budget
     static_assert(!KEEP || !REG3 || (KEEPF ? 2 * KS1 == RQ3 : KS1 == RQ3), "kept x: one 16-B chunk per k-step and row pair");

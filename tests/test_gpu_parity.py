@@ -206,7 +206,12 @@ def test_bev_occgrid_bit_exact(gpu, rows, cols, ww, wh, grid, seed, form, monkey
     blocky = np.kron(rng.integers(0, 3, size=(rows // 8, cols // 8)), np.ones((8, 8), np.int64)).astype(np.uint8)
     noise = rng.integers(0, 3, size=(rows, cols)).astype(np.uint8)
     wide = rng.integers(0, 256, size=(rows, cols)).astype(np.uint8)
-    segs = np.stack([blocky, noise, wide])
+    # 3-class noise with sparse outliers (7, 255): some band boxes take the 2-bit quad form, some not
+    sparse = noise.copy()
+    pick = rng.random((rows, cols))
+    sparse[pick < 0.002] = 7
+    sparse[(pick >= 0.002) & (pick < 0.004)] = 255
+    segs = np.stack([blocky, noise, wide, sparse])
     ref = np.stack([ocv_c.create_occupancy_grid(s, bev._bev_matrix, ww, wh, 1.0, *grid) for s in segs])
     got = bev.create_occupancy_grid_device(torch.from_numpy(segs).cuda(), *grid).cpu().numpy()
     assert got.dtype == np.int8 and got.shape == ref.shape
