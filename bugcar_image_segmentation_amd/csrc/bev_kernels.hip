@@ -450,7 +450,7 @@ constexpr int BEV_BAND_CAP = 16384, BEV_BAND_PF = BEV_BAND_CAP / 16 / 256;
 // forward camera span many image rows), each staged and evaluated in turn by the same workgroup;
 // only a part whose single-row box still exceeds the cap gathers from global memory.
 static_assert(BEV_BOXREC == 1 + BEV_BAND, "band record: header + one box per row part");
-constexpr int BEV_WL = 512;                          // band kernel: ring work-list records per workgroup
+constexpr int BEV_WL = 448;                          // band kernel: ring work-list records per workgroup (LDS: 8 per CU)
 static_assert(BEV_WL <= 2 * 256, "a thread takes at most two work-list records");
 // The band kernel's compact table, after the band boxes: [BEV_WIN][cells] u32, entry i of every cell
 // (BEV_ORDER_D order: the sample, its 3x3, then the ring) as the .y word alone — the tap's byte offset
@@ -569,8 +569,9 @@ __global__ void __launch_bounds__(256) bev_bandbox_kernel(const BevArgs a, int4 
 }
 
 // FB frames per workgroup (one box each): a cell's table slots and entry decoding serve all FB frames.
-// Held to 7 waves per SIMD (FB = 1: 72 VGPRs) so the ~1,600 workgroups of a 32-frame call are one
-// round (at 106 VGPRs, 4 waves per SIMD, they took 1.6 rounds).
+// Held to 8 waves per SIMD (FB = 1: 64 VGPRs, no spills; LDS 19.97 KB with a 448-record work list)
+// so the 58 work items x 32 frames of a bench call (1,856 workgroups; the near bands' row parts add
+// 8 items to the 50 bands) are one round of 2,048 slots — at 7 per CU, 64 of them took a second round.
 // One cell of one frame from a band's LDS box (bev_band_kernel's compact-table form and
 // bev_pipe_kernel): e9 = the cell's sample + 3x3 entries (offset in the box, Q5 fractions; BEV_ORDER),
 // outm = its 25-bit outside-template mask, ring = its 16 ring entries (stride `cells`), read only when
@@ -662,7 +663,7 @@ __device__ __forceinline__ int bev_cell_lds(const BevArgs &a, const uint8_t *box
 #define BEV_CTAB 1
 #endif
 template <int FB>
-__global__ void __launch_bounds__(256, FB == 1 ? 7 : 4) bev_band_kernel(const BevArgs a) {
+__global__ void __launch_bounds__(256, FB == 1 ? 8 : 4) bev_band_kernel(const BevArgs a) {
     __shared__ __attribute__((aligned(16))) uint8_t box[FB][BEV_BAND_CAP];
     const int tid = threadIdx.x;
     const long cells = (long)a.occ_h * a.occ_w;

@@ -264,10 +264,10 @@ __global__ void __launch_bounds__((BShape<C, V>::NW * 64), (sizeof(T) == 2 ? BSh
 #endif
     constexpr bool GLDS = BNECK_GLDS;                 // weights staged by global_load_lds (see the staging)
 #ifndef BNECK_KEEP_ASYM
-// the asymmetric form keeps the re-read: kept, its PMC read falls 65.4 -> 45.7 MB per launch (39.3
-// compulsory) but it spills (writes 39.3 -> 44.2 MB) and runs 26.2 -> 27.2 us (round 3 A/B; round 2:
-// 26.3 -> 26.7); with the 5x1 pass split into fragment halves (BNECK_ASYM_SPLIT) 28.2 us
-#define BNECK_KEEP_ASYM 0
+// the asymmetric form keeps its residual too (round 4: with the single-pass 5x1 it spills 3 VGPRs and
+// runs 26.7 vs 26.5 us per launch re-reading, i.e. equal, for ~25 MB less HBM traffic per launch;
+// round 3, before that rewrite, it had spilled more and run 26.2 -> 27.2 us)
+#define BNECK_KEEP_ASYM 1
 #endif
 #ifndef BNECK_KEEP_C64
 #define BNECK_KEEP_C64 0    // C = 64: measured 41.0 vs 38.0 us per launch with the residual kept (wave 0 takes a third load round trip for its second border fragment; batching it spills)
