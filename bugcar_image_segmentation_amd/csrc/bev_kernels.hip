@@ -662,6 +662,14 @@ __device__ __forceinline__ int bev_cell_lds(const BevArgs &a, const uint8_t *box
 #ifndef BEV_CTAB
 #define BEV_CTAB 1
 #endif
+// Debug build only (-DBUGSEG_STAMPS, scripts/bev_stamp_probe.py): thread 0 of each band workgroup
+// records the constant 100 MHz clock at its phase boundaries, bugseg_bev_stamps[blockIdx.x * 8 + k]
+#ifdef BUGSEG_STAMPS
+__device__ unsigned long long *bugseg_bev_stamps;
+#define BSTAMP(k) do { if (threadIdx.x == 0 && bugseg_bev_stamps) bugseg_bev_stamps[(size_t)blockIdx.x * 8 + (k)] = __builtin_amdgcn_s_memrealtime(); } while (0)
+#else
+#define BSTAMP(k) do {} while (0)
+#endif
 template <int FB>
 __global__ void __launch_bounds__(256, FB == 1 ? 8 : 4) bev_band_kernel(const BevArgs a) {
     __shared__ __attribute__((aligned(16))) uint8_t box[FB][BEV_BAND_CAP];
@@ -672,6 +680,7 @@ __global__ void __launch_bounds__(256, FB == 1 ? 8 : 4) bev_band_kernel(const Be
     const int xcd = blockIdx.x & 7, rest = blockIdx.x >> 3;
     const int item = (rest % nis) * 8 + xcd, b0 = (rest / nis) * FB;
     if (item >= a.nitems || b0 >= a.B || (BEV_ABL & 32)) return;  // workgroup-uniform
+    BSTAMP(0);
     const int2 wi = reinterpret_cast<const int2 *>(reinterpret_cast<const unsigned char *>(a.wtab) +
                                                    bev_items_offset(a.occ_w, a.occ_h))[item];
     const int band = wi.x, part = wi.y;
@@ -729,6 +738,7 @@ __global__ void __launch_bounds__(256, FB == 1 ? 8 : 4) bev_band_kernel(const Be
         }
         __syncthreads();
     }
+    BSTAMP(1);
     // value of template pixel e in frame f: its 4 taps from the box (L: the offset the bandbox kernel
     // stored in the entry) or, for an oversized band, from global memory. The two forms are separate
     // loops (a compile-time choice): no branch between the taps, so a cell's LDS reads fly together
@@ -870,6 +880,7 @@ __global__ void __launch_bounds__(256, FB == 1 ? 8 : 4) bev_band_kernel(const Be
             }
         }
         __syncthreads();
+        BSTAMP(2);
         const int nw = (int)min(wl_n, (uint32_t)BEV_WL);
         int qv[2] = {0, 0}, qc[2] = {-1, -1};        // this thread's (at most two) list results
 #pragma unroll
@@ -883,6 +894,7 @@ __global__ void __launch_bounds__(256, FB == 1 ? 8 : 4) bev_band_kernel(const Be
                                    ct + (size_t)9 * cells + c, cells);
             qc[k] = c;
         }
+        BSTAMP(3);
 #pragma unroll
         for (int k = 0; k < 4; ++k)
             if ((pdone >> k) & 1u) {
@@ -895,6 +907,10 @@ __global__ void __launch_bounds__(256, FB == 1 ? 8 : 4) bev_band_kernel(const Be
                 const int rem = r0 * a.occ_w + qc[k], cy = rem / a.occ_w, cx = rem - cy * a.occ_w;
                 bev_emit(a, b0, rem, cx, cy, cells, qv[k]);
             }
+        BSTAMP(4);
+#ifdef BUGSEG_STAMPS
+        if (tid == 0 && bugseg_bev_stamps) bugseg_bev_stamps[(size_t)blockIdx.x * 8 + 6] = (unsigned long long)nw | (unsigned long long)band << 16 | (unsigned long long)n << 32;
+#endif
     } else if (lds && BEV_CTAB) {
         // (FB = 2: each cell's both passes in place)
         for (int c = tid; c < n; c += 256) {
@@ -1012,6 +1028,11 @@ hipError_t launch_bev_table(const BevArgs &a, hipStream_t s) {
     return hipGetLastError();
 }
 
+#ifdef BUGSEG_STAMPS
+extern "C" int bugseg_debug_set_bev_stamps(void *p) {
+    return hipMemcpyToSymbol(HIP_SYMBOL(bugseg_bev_stamps), &p, sizeof(p)) == hipSuccess ? 0 : -3;
+}
+#endif
 hipError_t launch_bev(const BevArgs &a, hipStream_t s) {
     // form (measured, scripts/bev_probe.py): the gather kernel, 1 frame per thread (BUGSEG_BEV_F = 2 / 4:
     // frames per thread; BUGSEG_BEV_FG = n > 0: the LDS-staged kernel with n frames per workgroup);
