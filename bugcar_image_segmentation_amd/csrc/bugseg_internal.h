@@ -54,6 +54,7 @@ struct ConvArgs {
     const double *nlut;  // EPI_INIT_BGR: [3][256] normalisation table, RGB order (models.py:91)
     float naff[6];       // EPI_INIT_BGR, naff_on: the table as fmaf(v, naff[c], naff[3 + c]) (exact, see bugseg_runtime.cpp)
     int naff_on;
+    int pool_scan;       // init (A/B and tests): 1 = the per-tap pool scan instead of the packed f16 form
     int ntiles;
     int stg_elems;       // per-wave output staging (elements)
     int stage_ok;        // EPI_SHUFFLE: fragments never straddle an input row (Wg % 16 == 0, M % 16 == 0)

@@ -22,6 +22,7 @@
 // The generic implicit-GEMM path this replaces was VALU-bound (per-lane 3-byte gathers, integer
 // divisions, a 16-lane pool loop the whole wave executed). Both input forms go through the same
 // arithmetic, so forward_bgr == preprocess + forward bit for bit.
+#include <cstdlib>
 #include <type_traits>
 
 #include "bugseg_internal.h"
@@ -40,6 +41,9 @@ namespace bugseg {
 #define INIT_ABL 0
 #endif
 
+#ifndef INIT_POOL_PK
+#define INIT_POOL_PK 1
+#endif
 constexpr int IT_H = 8, IT_W = 32;                        // output tile
 constexpr int IP_H = 2 * IT_H + 1, IP_W = 2 * IT_W + 1;   // input patch (pixels)
 constexpr int IP_RS = IP_W * 3 + 1;                       // LDS patch row stride (elements, even)
@@ -51,7 +55,7 @@ __device__ __forceinline__ void init_k(int kq, int j, int &dy, int &e) {
 }
 
 template <typename T, bool BGR>
-__global__ void __launch_bounds__(256) init_kernel(const ConvArgs a) {
+__global__ void __launch_bounds__(256, sizeof(T) == 2 ? 6 : 1) init_kernel(const ConvArgs a) {   // (fp16 with the packed pool took 82 registers: 5 waves per SIMD)
     __shared__ __attribute__((aligned(16))) T patch[IP_H * IP_RS];
     __shared__ float lut[BGR ? 3 * 256 : 1];
     using Raw = typename Tr<T>::Raw;
@@ -191,7 +195,39 @@ __global__ void __launch_bounds__(256) init_kernel(const ConvArgs a) {
 
         // ---- pool maxima: lane (col, kq) -> pixel col of fragment f = kq (row 2*wave + (f>>1))
         float pm[3];
-        {
+        if (__is_same(T, _Float16) && INIT_POOL_PK && !a.pool_scan) {
+            // fp16 (round 4): a window row's 9 elements (3 pixels x 3 channels) as 5 aligned dwords
+            // (ds_read_b32; the row starts 4-B aligned) and the maxima as packed f16 pairs — (ch0, ch1)
+            // from dwords 0, 1:2 (shifted by one element) and 3, ch2 from halves of dwords 1, 2 and 4.
+            // Excluded taps (outside the frame; pool_k 2's row / column 0) are -inf. The same maxima as
+            // the per-tap scan: max is exact in f16 as in f32
+            const int lr = 2 * wave + (kq >> 1), lc = (kq & 1) * 16 + col;
+            const uint32_t *pw = reinterpret_cast<const uint32_t *>(patch + 2 * lr * IP_RS + 6 * lc);
+            const bool row0 = po > 0 || iy0 + 2 * lr < 0, col0 = po > 0 || ix0 + 2 * lc < 0;
+            typedef _Float16 h2 __attribute__((ext_vector_type(2)));
+            const uint32_t NINF2 = 0xFC00FC00u, NINF = 0xFC00u;
+            auto pmax = [](uint32_t x, uint32_t y) {
+                return __builtin_bit_cast(uint32_t, __builtin_elementwise_max(__builtin_bit_cast(h2, x), __builtin_bit_cast(h2, y)));
+            };
+            uint32_t m01 = NINF2, m2 = NINF2;
+#pragma unroll
+            for (int dy = 0; dy < 3; ++dy) {
+                const uint32_t *r = pw + dy * (IP_RS / 2);
+                const uint32_t d0 = r[0], d1 = r[1], d2 = r[2], d3 = r[3], d4 = r[4];
+                const uint32_t p01 = col0 ? NINF2 : d0;                              // (ch0, ch1) of dx 0
+                const uint32_t q01 = __builtin_amdgcn_alignbyte(d2, d1, 2);          // (ch0, ch1) of dx 1
+                const uint32_t a01 = pmax(pmax(p01, q01), d3);                        // d3: dx 2
+                const uint32_t c2a = (col0 ? NINF : (d1 & 0xffffu)) | (d2 & 0xffff0000u);   // (ch2 dx 0, ch2 dx 1)
+                const uint32_t a2 = pmax(c2a, (d4 & 0xffffu) | (d4 << 16));          // ch2 dx 2 in both halves
+                const bool skip = dy == 0 && row0;
+                m01 = skip ? m01 : pmax(m01, a01);
+                m2 = skip ? m2 : pmax(m2, a2);
+            }
+            const h2 v01 = __builtin_bit_cast(h2, m01), v2 = __builtin_bit_cast(h2, m2);
+            pm[0] = (INIT_ABL & 4) ? 0.f : (float)v01.x;
+            pm[1] = (INIT_ABL & 4) ? 0.f : (float)v01.y;
+            pm[2] = (INIT_ABL & 4) ? 0.f : (float)__builtin_elementwise_max(v2.x, v2.y);
+        } else {
             const int lr = 2 * wave + (kq >> 1), lc = (kq & 1) * 16 + col;
             const T *pp = patch + 2 * lr * IP_RS + 6 * lc;
             const bool top = iy0 + 2 * lr < 0, left = ix0 + 2 * lc < 0;   // window row/col 0 outside the frame
@@ -323,6 +359,7 @@ hipError_t launch_init(int prec, bool bgr, const ConvArgs &args, hipStream_t s) 
     int g = init_tiles(a);
     g = g < cap ? g : cap;
     g = g & ~7 ? g & ~7 : 8;
+    a.pool_scan = getenv("BUGSEG_INIT_POOL_SCAN") != nullptr;
     if (prec == PREC_BF16) {
         if (bgr) hipLaunchKernelGGL((init_kernel<__bf16, true>), dim3(g), dim3(256), 0, s, a);
         else hipLaunchKernelGGL((init_kernel<__bf16, false>), dim3(g), dim3(256), 0, s, a);

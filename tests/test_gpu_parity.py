@@ -320,6 +320,27 @@ def test_init_affine_normalisation_equals_table(gpu, blocks, prec, monkeypatch):
     assert torch.equal(a, b)
 
 
+@pytest.mark.parametrize("pool_k", [3, 2])
+def test_init_packed_pool_equals_scan(gpu, pool_k, monkeypatch):
+    """fp16: the initial block's pool maxima as packed f16 pairs from 5-dword window rows
+    (init_kernels.hip) equal the per-tap scan (BUGSEG_INIT_POOL_SCAN=1) bit for bit — frame edges (the
+    excluded -inf taps) and pool_k 2's window included, raw-BGR and engine-input entries alike."""
+    bl = enet_spec.build_enet(seed=19, initial_pool_k=pool_k)
+    m = ENET(weights=bl, precision="fp16")
+    B, H, W = 2, 72, 104
+    bgr = torch.from_numpy(synthetic.road_frames(B, H, W, seed=9)).cuda()
+    x = ENET.preprocess_device(bgr, N.PRE_ENGINE, ctx=m.ctx, width=W, height=H)
+    outs = []
+    for scan in (False, True):
+        if scan:
+            monkeypatch.setenv("BUGSEG_INIT_POOL_SCAN", "1")
+        a = torch.empty((B, 15, H, W), dtype=torch.float32, device=gpu)
+        m.ctx.forward_bgr(bgr, B, H, W, N.OUT_LOGITS_F32, a)
+        outs.append((a, m.predict_device(x, N.OUT_LOGITS_F32)))
+    assert torch.equal(outs[0][0], outs[1][0])
+    assert torch.equal(outs[0][1], outs[1][1])
+
+
 @pytest.mark.parametrize("variant", [None, "0", "1", "2", "3", "4"])
 @pytest.mark.parametrize("prec", ["fp32", "bf16", "fp16"])
 @pytest.mark.parametrize("H,W", [(64, 96), (72, 104), (120, 160), (480, 640)])
