@@ -123,32 +123,36 @@ __global__ void __launch_bounds__(256, sizeof(T) == 2 ? 4 : 1) cls_kernel(const 
 
     // lane pixel of group g: the group's first pixel is divided out on the scalar unit (g is
     // wave-uniform; Hg * Wg, Wg >= 32 > 1), each lane then steps at most one row on
-    struct Px { int n, y, x; bool ok; };
+    // (the input grid is the class layer's own grid, cls_supported: a pixel's flat index p addresses
+    // its input, and its output pixels (2y + h, 2x) sit at byte 4p - 2x + 2hWg of the class map)
+    struct Px { uint32_t p; int n, y, x; bool ok; };
     auto pixel = [&](int g) -> Px {
         const uint32_t p0 = (uint32_t)g * 32u;
         const int n0 = (int)(__umulhi(p0, a.mHWg) >> a.sHWg);
         const uint32_t r = p0 - (uint32_t)(n0 * HWg);
         const int y0 = (int)(__umulhi(r, a.mWg) >> a.sWg), x0 = (int)r - y0 * a.Wg;
         Px q;
-        q.ok = (int)p0 + col < a.M;
+        q.p = p0 + (uint32_t)col;
+        q.ok = (int)q.p < a.M;
         q.x = x0 + col;
         const bool wrap = q.x >= a.Wg;
         q.x = wrap ? q.x - a.Wg : q.x;
         q.y = y0 + (wrap ? 1 : 0);
         const bool wrapn = q.y >= a.Hg;
         q.y = wrapn ? 0 : q.y;
-        q.n = n0 + (wrapn ? 1 : 0);
+        q.n = n0 + (wrapn ? 1 : 0);          // (the logits path only)
         return q;
     };
-    auto load = [&](int g, Raw (&xf)[CLS_TAPS]) {
+    // (the group's pixel is computed once, with its loads, and handed to the step that consumes them)
+    auto load = [&](int g, Raw (&xf)[CLS_TAPS], Px &q) {
+        q = pixel(g);
         if constexpr ((CLS_ABL & 8) != 0) {
 #pragma unroll
             for (int s = 0; s < CLS_TAPS; ++s) zero(xf[s]);
             if constexpr (sizeof(T) == 2) xf[0].v.x = (uint32_t)g;   // (something that varies, so nothing is hoisted)
             return;
         }
-        const Px q = pixel(g);
-        const uint32_t base = (uint32_t)((q.n * a.Hin + q.y) * a.Win + q.x) * pixB + (uint32_t)(8 * h * ES);
+        const uint32_t base = q.p * pixB + (uint32_t)(8 * h * ES);
         const bool okx = q.x + 1 < a.Win, oky = q.y + 1 < a.Hin;
         const int v00 = (int)(q.ok ? base : OOB), v01 = (int)(q.ok && okx ? base : OOB);
         const int v10 = (int)(q.ok && oky ? base : OOB), v11 = (int)(q.ok && okx && oky ? base : OOB);
@@ -169,13 +173,13 @@ __global__ void __launch_bounds__(256, sizeof(T) == 2 ? 4 : 1) cls_kernel(const 
 
     // one group: MFMAs, argmax, stores; `nxt` first receives the next group's loads (they fly during
     // this one; the two buffers alternate by unrolling, never by a runtime index).
-    auto step = [&](int g, const Raw (&cur)[CLS_TAPS], Raw (&nxt)[CLS_TAPS]) {
+    const auto rcls = mkbuf(a.cls_out, (uint32_t)((size_t)a.B * plane));
+    auto step = [&](int g, const Raw (&cur)[CLS_TAPS], Raw (&nxt)[CLS_TAPS], const Px &q, Px &qn) {
         // unconditional: past the last group the loads are harmless (an out-of-range group reads
         // zeros, a neighbour's group is read and dropped), and a static count of loads in flight
         // lets the waits before the MFMAs name only this group's loads (a conditional prefetch
         // made the compiler wait vmcnt(3), i.e. for the next group's first load as well).
-        load(g + nw, nxt);
-        const Px q = pixel(g);
+        load(g + nw, nxt, qn);
         // per block: accumulators from the bias, the taps' MFMAs, (parity runs) the logits, and the
         // argmax over this lane's classes = the sequential strict > scan from -inf of tf.math.argmax
         // (models.py:55): the maximum (v_max ignores NaN), then its first index; no class equal to the
@@ -265,20 +269,21 @@ __global__ void __launch_bounds__(256, sizeof(T) == 2 ? 4 : 1) cls_kernel(const 
             // >= 32 row 2y + 1: one 2-byte store of pixels (2x, 2x + 1) each
             uint32_t c0 = (uint32_t)cls[0], c1 = (uint32_t)cls[1];
             pl32swap(c0, c1);
-            if (q.ok && (!(CLS_ABL & 4) || c0 == 77)) {
-                const size_t o = ((size_t)q.n * a.Hout + 2 * q.y + h) * a.Wout + 2 * q.x;
-                *reinterpret_cast<uint16_t *>(a.cls_out + o) = (uint16_t)(c0 | (c1 << 8));
-            }
+            // (32-bit offsets through a buffer descriptor: a masked lane's store is dropped)
+            const uint32_t o = 4u * q.p - 2u * (uint32_t)q.x + (uint32_t)(2 * h * a.Wg);
+            if (!(CLS_ABL & 4) || c0 == 77)
+                __builtin_amdgcn_raw_buffer_store_b16((unsigned short)(c0 | (c1 << 8)), rcls, q.ok ? (int)o : (int)OOB, 0, 0);
         }
     };
     Raw xa[CLS_TAPS], xb[CLS_TAPS];
+    Px qa, qb;
     int g = g0 + wi;
-    if (g < g1) load(g, xa);
+    if (g < g1) load(g, xa, qa);
     while (g < g1) {
-        step(g, xa, xb);
+        step(g, xa, xb, qa, qb);
         g += nw;
         if (g >= g1) break;
-        step(g, xb, xa);
+        step(g, xb, xa, qb, qa);
         g += nw;
     }
 }
