@@ -56,6 +56,9 @@ __device__ __forceinline__ bool nonzero(const RawS &r) {
 #ifndef CLS_ABL
 #define CLS_ABL 0
 #endif
+#ifndef CLS_BIAS_REG
+#define CLS_BIAS_REG 1
+#endif
 // (Round 4 measured a low-register form — weights from LDS, the two blocks one after the other, 7 waves
 // per SIMD instead of 4 — at 37.5 vs 34.7 us per 32-frame launch (fp16) and 75.3 vs 74.7 (fp32): the
 // class layer is not occupancy-bound. Removed.)
@@ -109,6 +112,26 @@ __global__ void __launch_bounds__(256, sizeof(T) == 2 ? 4 : 1) cls_kernel(const 
     for (int b = 0; b < 2; ++b) short_blk[b] = __ballot(nonzero(wr[b][2]) || nonzero(wr[b][3])) == 0;
     __syncthreads();
 
+    // The accumulators start at the bias. pack_tconv (bugseg_runtime.cpp) writes the same per-class bias
+    // into all four phases' rows, so sbias[(2b + h) * 16 + k] is one 16-vector for every block and lane
+    // half: CLS_BIAS_REG holds it in 16 loop-long registers instead of reading it from LDS per group.
+    auto ldbias = [&](int b) {
+        // (the opaque offset keeps the compiler from hoisting these reads out of the group loop)
+        int boff = (2 * b + h) * 16;
+        asm volatile("" : "+v"(boff));
+        const float4 *bb = reinterpret_cast<const float4 *>(sbias + boff);
+        f32x16 v;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            const float4 q = bb[j];
+            v[4 * j] = q.x; v[4 * j + 1] = q.y; v[4 * j + 2] = q.z; v[4 * j + 3] = q.w;
+        }
+        return v;
+    };
+    // (2-byte class maps only: the logits form and fp32 have no registers to spare)
+    constexpr bool BREG = CLS_BIAS_REG && !LOGITS && sizeof(T) == 2;
+    f32x16 bvec;
+    if constexpr (BREG) bvec = ldbias(0);
     const auto rin = mkbuf(a.in, a.in_bytes);
     const int HWg = a.Hg * a.Wg;
     const size_t plane = (size_t)a.Hout * a.Wout;
@@ -186,16 +209,7 @@ __global__ void __launch_bounds__(256, sizeof(T) == 2 ? 4 : 1) cls_kernel(const 
         // maximum (all NaN) -> 0; all -inf -> 0 (class 0 equals the maximum). Both blocks' MFMAs go
         // first, then the two argmax scans interleaved
         auto block = [&](int b, f32x16 &acc) {
-            // (the opaque offset keeps the compiler from hoisting these reads out of the group loop
-            // into 32 loop-long VGPRs)
-            int boff = (2 * b + h) * 16;
-            asm volatile("" : "+v"(boff));
-            const float4 *bb = reinterpret_cast<const float4 *>(sbias + boff);
-#pragma unroll
-            for (int j = 0; j < 4; ++j) {
-                const float4 v = bb[j];
-                acc[4 * j] = v.x; acc[4 * j + 1] = v.y; acc[4 * j + 2] = v.z; acc[4 * j + 3] = v.w;
-            }
+            acc = BREG ? bvec : ldbias(b);
             if constexpr ((CLS_ABL & 1) != 0 && sizeof(T) == 2) { acc[0] += __builtin_bit_cast(float, cur[0].v.x & 1u); return; }
             mma32(acc, wr[b][0], cur[0]);
             mma32(acc, wr[b][1], cur[1]);
