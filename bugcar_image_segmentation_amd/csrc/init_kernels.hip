@@ -47,6 +47,13 @@ namespace bugseg {
 constexpr int IT_H = 8, IT_W = 32;                        // output tile
 constexpr int IP_H = 2 * IT_H + 1, IP_W = 2 * IT_W + 1;   // input patch (pixels)
 constexpr int IP_RS = IP_W * 3 + 1;                       // LDS patch row stride (elements, even)
+constexpr int IP_PATCH = (IP_H * IP_RS + 7) & ~7;           // one patch buffer (elements, 16-B multiple)
+#ifndef INIT_DB
+#define INIT_DB 1
+#endif
+#ifndef INIT_OCC2
+#define INIT_OCC2 6                                          // 2-byte storage: waves per SIMD the registers allow
+#endif
 
 // k -> (window row, element of the row's 9-run), the B/A fragment K order described above
 __device__ __forceinline__ void init_k(int kq, int j, int &dy, int &e) {
@@ -55,8 +62,10 @@ __device__ __forceinline__ void init_k(int kq, int j, int &dy, int &e) {
 }
 
 template <typename T, bool BGR>
-__global__ void __launch_bounds__(256, sizeof(T) == 2 ? 6 : 1) init_kernel(const ConvArgs a) {   // (fp16 with the packed pool took 82 registers: 5 waves per SIMD)
-    __shared__ __attribute__((aligned(16))) T patch[IP_H * IP_RS];
+__global__ void __launch_bounds__(256, sizeof(T) == 2 ? INIT_OCC2 : 1) init_kernel(const ConvArgs a) {   // (fp16 with the packed pool took 82 registers: 5 waves per SIMD)
+    // INIT_DB: two patch buffers — the next tile's patch is stored while this one is computed, one
+    // barrier per tile instead of two
+    __shared__ __attribute__((aligned(16))) T patch_buf[(INIT_DB ? 2 : 1) * IP_PATCH];
     __shared__ float lut[BGR ? 3 * 256 : 1];
     using Raw = typename Tr<T>::Raw;
     using WRaw = typename WTr<T>::Raw;   // weight operand (fp32 mode: split-f16 parts)
@@ -157,21 +166,14 @@ __global__ void __launch_bounds__(256, sizeof(T) == 2 ? 6 : 1) init_kernel(const
 #ifndef INIT_PF
 #define INIT_PF 1
 #endif
-    if (slot < CH && grp * CH + slot < ntiles) load_raw(geom(grp * CH + slot));
-    for (int it = slot; it < CH; it += nslots) {
-        const int tile = grp * CH + it;
-        if (tile >= ntiles) break;
-        const Tile tg = geom(tile);
-        const int n = tg.n, ty0 = tg.ty0, tx0 = tg.tx0, iy0 = tg.iy0, ix0 = tg.ix0;
-        const int ix = ix0 + px;
-        const bool colok = qok && (unsigned)ix < (unsigned)a.Win;
-        if (!INIT_PF && it != slot) load_raw(tg);
-        __syncthreads();   // lut staged / previous tile done with the patch
-        // rows outside the frame exist only in the first and last tile rows: a uniform fast path
+    // this thread's patch column of tile t, from the raw bytes, into patch buffer dst
+    // (rows outside the frame exist only in the first and last tile rows: a uniform fast path)
+    auto store_patch = [&](const Tile &t, T *dst) {
+        const bool colok = qok && (unsigned)(t.ix0 + px) < (unsigned)a.Win;
         auto store_rows = [&](auto full_rows) {
 #pragma unroll
             for (int r = 0; r < IP_H; ++r) {
-                const bool ok = colok && (decltype(full_rows)::value || (unsigned)(iy0 + r) < (unsigned)a.Hin);
+                const bool ok = colok && (decltype(full_rows)::value || (unsigned)(t.iy0 + r) < (unsigned)a.Hin);
                 T v;
                 if constexpr (BGR) {
                     // f16: through f32, as the separate preprocess stores the engine input (prep_kernels.hip)
@@ -182,16 +184,46 @@ __global__ void __launch_bounds__(256, sizeof(T) == 2 ? 6 : 1) init_kernel(const
                 }
                 else if constexpr (sizeof(T) == 2) v = __builtin_bit_cast(T, (unsigned short)raw[r]);
                 else v = __builtin_bit_cast(T, raw[r]);
-                patch[r * IP_RS + dslot] = ok ? v : (T)0.f;
+                dst[r * IP_RS + dslot] = ok ? v : (T)0.f;
             }
         };
-        if (iy0 >= 0 && iy0 + IP_H <= a.Hin) store_rows(std::true_type());
+        if (t.iy0 >= 0 && t.iy0 + IP_H <= a.Hin) store_rows(std::true_type());
         else store_rows(std::false_type());
-        if (INIT_PF) {
-            const int tn = tile + nslots;   // (the walk's next tile: same XCD group, next slot round)
-            if (it + nslots < CH && tn < ntiles) load_raw(geom(tn));
+    };
+    if (slot < CH && grp * CH + slot < ntiles) load_raw(geom(grp * CH + slot));
+    if constexpr (INIT_DB) {
+        // prologue: the first tile's patch into buffer 0, the second tile's loads in flight
+        __syncthreads();   // lut staged
+        if (slot < CH && grp * CH + slot < ntiles) {
+            store_patch(geom(grp * CH + slot), patch_buf);
+            if (slot + nslots < CH && grp * CH + slot + nslots < ntiles) load_raw(geom(grp * CH + slot + nslots));
         }
-        __syncthreads();
+    }
+    int pbuf = 0;
+    for (int it = slot; it < CH; it += nslots) {
+        const int tile = grp * CH + it;
+        if (tile >= ntiles) break;
+        const Tile tg = geom(tile);
+        const int n = tg.n, ty0 = tg.ty0, tx0 = tg.tx0, iy0 = tg.iy0, ix0 = tg.ix0;
+        const T *patch = patch_buf + pbuf * IP_PATCH;
+        if constexpr (INIT_DB) {
+            __syncthreads();   // this tile's patch complete; the other buffer's last reader (the previous tile) done
+            const int tn = tile + nslots;   // (the walk's next tile: same XCD group, next slot round)
+            if (it + nslots < CH && tn < ntiles) {
+                store_patch(geom(tn), patch_buf + (pbuf ^ 1) * IP_PATCH);
+                if (it + 2 * nslots < CH && tn + nslots < ntiles) load_raw(geom(tn + nslots));
+            }
+            pbuf ^= 1;
+        } else {
+            if (!INIT_PF && it != slot) load_raw(tg);
+            __syncthreads();   // lut staged / previous tile done with the patch
+            store_patch(tg, patch_buf);
+            if (INIT_PF) {
+                const int tn = tile + nslots;   // (the walk's next tile: same XCD group, next slot round)
+                if (it + nslots < CH && tn < ntiles) load_raw(geom(tn));
+            }
+            __syncthreads();
+        }
 
         // ---- pool maxima: lane (col, kq) -> pixel col of fragment f = kq (row 2*wave + (f>>1))
         float pm[3];
