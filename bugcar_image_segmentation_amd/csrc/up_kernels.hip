@@ -25,8 +25,16 @@
 namespace bugseg {
 
 
+// threads per workgroup: the 2-byte CIN = 128 form (46 KB of weights in LDS: 3 workgroups per CU) runs
+// 8 waves per workgroup (UP_NT128), so the weights staged once per CU serve twice the waves
+#ifndef UP_NT128
+#define UP_NT128 512
+#endif
+template <typename T, int CIN>
+__host__ __device__ constexpr int up_threads() { return sizeof(T) == 2 && CIN >= 128 ? UP_NT128 : 256; }
+
 template <typename T, int CIN, int I, int COUT>
-__global__ void __launch_bounds__(256, (sizeof(T) == 2 ? (CIN >= 128 ? 2 : 3) : 1)) up_kernel(const UpArgs a) {
+__global__ void __launch_bounds__((up_threads<T, CIN>()), (sizeof(T) == 2 ? (CIN >= 128 ? (UP_NT128 == 512 ? 4 : 2) : 3) : 1)) up_kernel(const UpArgs a) {
     using Raw = typename Tr<T>::Raw;
     using WRaw = typename WTr<T>::Raw;   // weight operand (fp32 mode: split-f16 parts)
     constexpr int ES = (int)sizeof(T);
@@ -60,12 +68,13 @@ __global__ void __launch_bounds__(256, (sizeof(T) == 2 ? (CIN >= 128 ? 2 : 3) : 
     float *cb1 = reinterpret_cast<float *>(w3s + NR3 * 16 * K3S), *cs1 = cb1 + NR1 * 16;
     float *cb2 = cs1 + NR1 * 16, *cs2 = cb2 + NR2 * 16;
     float *cb3 = cs2 + NR2 * 16, *cs3 = cb3 + NR3 * 16, *cso = cs3 + NR3 * 16;
+    constexpr int NT = up_threads<T, CIN>();
     const int tid = threadIdx.x;
     {
         auto stage = [&](T *dst, const void *src, int rows, int kpad, int kstride) {
             const int cpr = kpad * ES / 16;
             const uint4 *s = reinterpret_cast<const uint4 *>(src);
-            for (int i = tid; i < rows * cpr; i += 256) {
+            for (int i = tid; i < rows * cpr; i += NT) {
                 const int r = i / cpr, c = i - r * cpr;
                 // (c counts 16-B chunks: 8 elements in 2-byte storage, 4 in fp32, where nothing is swizzled)
                 *reinterpret_cast<uint4 *>(dst + (size_t)r * kstride + c * (16 / ES)) = s[i];
@@ -74,9 +83,9 @@ __global__ void __launch_bounds__(256, (sizeof(T) == 2 ? (CIN >= 128 ? 2 : 3) : 
         stage(w1s, a.w1, NR1 * 16, CIN, K1S);          // pair pack: K = CIN exactly (1x1, CinS = CIN)
         stage(w2s, a.w2, NR2 * 16, 32, K2S);
         stage(w3s, a.w3, NR3 * 16, 32, K3S);
-        for (int i = tid; i < NR1 * 16; i += 256) { cb1[i] = a.b1[i]; cs1[i] = a.s1[i]; }
-        for (int i = tid; i < NR2 * 16; i += 256) { cb2[i] = a.b2[i]; cs2[i] = a.s2[i]; }
-        for (int i = tid; i < NR3 * 16; i += 256) { cb3[i] = a.b3[i]; cs3[i] = a.s3[i]; cso[i] = a.s_out[i]; }
+        for (int i = tid; i < NR1 * 16; i += NT) { cb1[i] = a.b1[i]; cs1[i] = a.s1[i]; }
+        for (int i = tid; i < NR2 * 16; i += NT) { cb2[i] = a.b2[i]; cs2[i] = a.s2[i]; }
+        for (int i = tid; i < NR3 * 16; i += NT) { cb3[i] = a.b3[i]; cs3[i] = a.s3[i]; cso[i] = a.s_out[i]; }
     }
     __syncthreads();
     const int lane = tid & 63, col = lane & 15, kq = lane >> 4;
@@ -87,7 +96,7 @@ __global__ void __launch_bounds__(256, (sizeof(T) == 2 ? (CIN >= 128 ? 2 : 3) : 
     const auto ro = mkbuf(a.out, a.out_bytes);
     const int hw = a.h * a.w;
     const int nfrag = (a.M + 15) >> 4;
-    const int gw = blockIdx.x * 4 + __builtin_amdgcn_readfirstlane(tid >> 6), nw = gridDim.x * 4;
+    const int gw = blockIdx.x * (NT / 64) + __builtin_amdgcn_readfirstlane(tid >> 6), nw = gridDim.x * (NT / 64);
 
     // The grid is sized to the resident waves (launch_up) and each wave streams over fragments: the
     // next fragment's block input and pooling indices are in flight while this one computes.
@@ -224,10 +233,10 @@ template <int CI, int II, int CO>
 static hipError_t launch_shape(int prec, const UpArgs &a, dim3 g, hipStream_t s) {
     if (prec == PREC_BF16) {
         const size_t lds = up_lds<__bf16, CI, II, CO>();
-        hipLaunchKernelGGL((up_kernel<__bf16, CI, II, CO>), g, dim3(256), lds, s, a);
+        hipLaunchKernelGGL((up_kernel<__bf16, CI, II, CO>), g, dim3(up_threads<__bf16, CI>()), lds, s, a);
     } else if (prec == PREC_F16) {
         const size_t lds = up_lds<_Float16, CI, II, CO>();
-        hipLaunchKernelGGL((up_kernel<_Float16, CI, II, CO>), g, dim3(256), lds, s, a);
+        hipLaunchKernelGGL((up_kernel<_Float16, CI, II, CO>), g, dim3(up_threads<_Float16, CI>()), lds, s, a);
     } else {
         const size_t lds = up_lds<float, CI, II, CO>();
         if (lds > 64 * 1024) {
@@ -235,7 +244,7 @@ static hipError_t launch_shape(int prec, const UpArgs &a, dim3 g, hipStream_t s)
                                                hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
             if (e != hipSuccess) return e;
         }
-        hipLaunchKernelGGL((up_kernel<float, CI, II, CO>), g, dim3(256), lds, s, a);
+        hipLaunchKernelGGL((up_kernel<float, CI, II, CO>), g, dim3(up_threads<float, CI>()), lds, s, a);
     }
     return hipGetLastError();
 }
@@ -248,7 +257,7 @@ static int up_resident() {
         int dev = 0, cus = 0, per = 0;
         if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
             cus = 256;
-        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, (const void *)up_kernel<T, CI, II, CO>, 256, up_lds<T, CI, II, CO>()) !=
+        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, (const void *)up_kernel<T, CI, II, CO>, up_threads<T, CI>(), up_lds<T, CI, II, CO>()) !=
                 hipSuccess || per <= 0)
             per = 2;
         n = cus * per;
@@ -258,7 +267,8 @@ static int up_resident() {
 
 hipError_t launch_up(int prec, int cin, int it, int cout, const UpArgs &a, hipStream_t s) {
     const int nfrag = (a.M + 15) / 16;
-    int g = (nfrag + 3) / 4;
+    const int wpg = (cin == 128 && prec != PREC_F32 ? UP_NT128 : 256) / 64;   // waves per workgroup (up_threads)
+    int g = (nfrag + wpg - 1) / wpg;
     // one resident round of workgroups, each streaming over its fragments (prefetch in the kernel)
     const int res = cin == 128 ? (prec == PREC_BF16  ? up_resident<__bf16, 128, 32, 64>()
                                   : prec == PREC_F16 ? up_resident<_Float16, 128, 32, 64>()
