@@ -181,7 +181,7 @@ struct BevArgs {
     // [BEV_SLOTS][occ_h*occ_w] (the 3x3 around the sample first); a property of the geometry only,
     // built once per calibration by launch_bev_table and shared by every frame
     uint4 *wtab;
-    // band-staged form: the (band, row part) work items (bev_items_offset in the table), heaviest first;
+    // band-staged form: the (band, row part) work items (bev_items_offset in the table), far bands first;
     // set by the host from the band records after the table build (bugseg_runtime.cpp bev_occgrid)
     int nitems;
 };
