@@ -180,7 +180,7 @@ def _bev_case(rows, cols, ww, wh, seed):
     return bev
 
 
-@pytest.mark.parametrize("form", [None, "FB2", "G", "FG4", "F2"])
+@pytest.mark.parametrize("form", [None, "NEAR", "FB2", "G", "FG4", "F2"])
 @pytest.mark.parametrize("rows,cols,ww,wh,grid,seed", [
     (480, 640, 1000, 1000, (10.0, 10.0, 0.05), 0),
     (120, 160, 300, 260, (3.0, 2.0, 0.05), 1),
@@ -189,7 +189,8 @@ def _bev_case(rows, cols, ww, wh, seed):
 ])
 def test_bev_occgrid_bit_exact(gpu, rows, cols, ww, wh, grid, seed, form, monkeypatch):
     """Every form of the rasteriser (bev_kernels.hip: the default band-staged kernel, 2 frames per
-    band workgroup, the gather kernel, the block-staged one, 2 frames per thread) is bit-exact against
+    band workgroup, the gather kernel, the block-staged one, 2 frames per thread; NEAR: the band
+    kernel's work items nearest band first, the earlier order, if this context builds the table) is bit-exact against
     the C restatement; class maps with labels past the 3-class range (up to 255: segmap + 1 wraps in
     uint8 as np.add does, bev.py:177) included."""
     if form == "G":
@@ -200,6 +201,8 @@ def test_bev_occgrid_bit_exact(gpu, rows, cols, ww, wh, grid, seed, form, monkey
         monkeypatch.setenv("BUGSEG_BEV_FG", "4")
     elif form == "F2":
         monkeypatch.setenv("BUGSEG_BEV_F", "2")
+    elif form == "NEAR":
+        monkeypatch.setenv("BUGSEG_BEV_NEAR_FIRST", "1")
     bev = _bev_case(rows, cols, ww, wh, seed)
     rng = np.random.default_rng(seed)
     # blocky class maps (realistic regions + speckles) and pure noise
