@@ -187,7 +187,7 @@ __global__ void __launch_bounds__((BShape<C, V>::NW * 64), (sizeof(T) == 2 ? BSh
     constexpr int NFA = (NPA + 15) / 16;
     constexpr int NF2A = (NFA + NW - 1) / NW;
 #ifndef BNECK_CH1_K2
-#define BNECK_CH1_K2 5   // down C64: 49.9 -> 49.4 us at 5 (one spill); 6 spills 22
+#define BNECK_CH1_K2 4   // down C64: 49.9 -> 49.4 us at 5 (one spill; round 2); round 4, with DKEEP: 4 spills none, 48.6-49.5 -> 47.4-47.9 us (its 6 fragments per wave take two round trips either way); 6 spills 22
 #endif
 // k-steps of the symmetric middle conv unrolled together: 3 for C = 128 (9 k-steps; no spills, its
 // launches 1-4% faster), 1 elsewhere (down C64 6% slower at 3; 2 and 9 spill on C = 128).
