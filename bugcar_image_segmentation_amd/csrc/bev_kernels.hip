@@ -453,9 +453,6 @@ static_assert(BEV_BOXREC == 1 + BEV_BAND, "band record: header + one box per row
 #ifndef BEV_MINP
 #define BEV_MINP 1                                   // fewest row parts per band (A/B knob: 1, 2, 4)
 #endif
-#ifndef BEV_ITEM_MAJOR
-#define BEV_ITEM_MAJOR 1                             // workgroup order: all frames of an item together (0: all items of a frame)
-#endif
 constexpr int BEV_WL = 448;                          // band kernel: ring work-list records per workgroup (LDS: 8 per CU)
 static_assert(BEV_WL <= 2 * 256, "a thread takes at most two work-list records");
 // The band kernel's compact table, after the band boxes: [BEV_WIN][cells] u32, entry i of every cell
@@ -672,7 +669,7 @@ __device__ __forceinline__ int bev_cell_lds(const BevArgs &a, const uint8_t *box
 // records the constant 100 MHz clock at its phase boundaries, bugseg_bev_stamps[blockIdx.x * 8 + k]
 #ifdef BUGSEG_STAMPS
 __device__ unsigned long long *bugseg_bev_stamps;
-#define BSTAMP(k) do { if (threadIdx.x == 0 && bugseg_bev_stamps) bugseg_bev_stamps[(size_t)blockIdx.x * 8 + (k)] = __builtin_amdgcn_s_memrealtime(); } while (0)
+#define BSTAMP(k) do { if (threadIdx.x == 0 && bugseg_bev_stamps) bugseg_bev_stamps[((size_t)blockIdx.y * gridDim.x + blockIdx.x) * 8 + (k)] = __builtin_amdgcn_s_memrealtime(); } while (0)
 #else
 #define BSTAMP(k) do {} while (0)
 #endif
@@ -681,14 +678,14 @@ __global__ void __launch_bounds__(256, FB == 1 ? 8 : 4) bev_band_kernel(const Be
     __shared__ __attribute__((aligned(16))) uint8_t box[FB][BEV_BAND_CAP];
     const int tid = threadIdx.x;
     const long cells = (long)a.occ_h * a.occ_w;
-    // one work item (a band's row part) per workgroup, item i on XCD i % 8; consecutive workgroups of an
-    // XCD take the same item for successive frames (BEV_ITEM_MAJOR), so the item's compact-table words
-    // are L2 hits for all but the first frames: 30.9 -> 26.3 us per 32 frames against the frame-major
-    // order (all items of frame 0, then frame 1, ...), bit-identical (scripts/gpu_r4_im.sh)
-    const int nis = (a.nitems + 7) >> 3;
-    const int xcd = blockIdx.x & 7, rest = blockIdx.x >> 3;
-    const int nfg = (a.B + FB - 1) / FB;
-    const int item = (BEV_ITEM_MAJOR ? rest / nfg : rest % nis) * 8 + xcd, b0 = (BEV_ITEM_MAJOR ? rest % nfg : rest / nis) * FB;
+    // one work item (a band's row part) per workgroup: workgroup (x, y) = (frame group f * 8 + XCD x % 8,
+    // item slot y) runs item 8 y + x % 8 of frames f FB .. Dispatch order is x fastest, so consecutive
+    // workgroups of an XCD take the same item for successive frames and the item's compact-table words
+    // are L2 hits for all but the first frames (item-major): 30.9 -> 26.3 us per 32 frames against the
+    // frame-major order (all items of frame 0, then frame 1, ...), bit-identical (scripts/gpu_r4_im.sh).
+    // (A 2-D grid, not a division of the linear index: the division cost the kernel 3 spilled VGPRs.)
+    const int xcd = blockIdx.x & 7;
+    const int item = (int)blockIdx.y * 8 + xcd, b0 = (int)(blockIdx.x >> 3) * FB;
     if (item >= a.nitems || b0 >= a.B || (BEV_ABL & 32)) return;  // workgroup-uniform
     BSTAMP(0);
     const int2 wi = reinterpret_cast<const int2 *>(reinterpret_cast<const unsigned char *>(a.wtab) +
@@ -920,7 +917,7 @@ __global__ void __launch_bounds__(256, FB == 1 ? 8 : 4) bev_band_kernel(const Be
             }
         BSTAMP(4);
 #ifdef BUGSEG_STAMPS
-        if (tid == 0 && bugseg_bev_stamps) bugseg_bev_stamps[(size_t)blockIdx.x * 8 + 6] = (unsigned long long)nw | (unsigned long long)band << 16 | (unsigned long long)n << 32;
+        if (tid == 0 && bugseg_bev_stamps) bugseg_bev_stamps[((size_t)blockIdx.y * gridDim.x + blockIdx.x) * 8 + 6] = (unsigned long long)nw | (unsigned long long)band << 16 | (unsigned long long)n << 32;
 #endif
     } else if (lds && BEV_CTAB) {
         // (FB = 2: each cell's both passes in place)
@@ -1066,9 +1063,9 @@ hipError_t launch_bev(const BevArgs &a, hipStream_t s) {
         const char *fbe = std::getenv("BUGSEG_BEV_FB");
         // (measured at 32 frames of 480x640: FB = 1 38.7-40.1 us, FB = 2 44.6-48.5 us)
         const int FB = fbe && std::atoi(fbe) == 2 ? 2 : 1;
-        const long grid = 8L * ((a.nitems + 7) / 8) * ((a.B + FB - 1) / FB);
-        if (FB == 1) hipLaunchKernelGGL(bev_band_kernel<1>, dim3((unsigned)grid), dim3(256), 0, s, a);
-        else hipLaunchKernelGGL(bev_band_kernel<2>, dim3((unsigned)grid), dim3(256), 0, s, a);
+        const dim3 grid(8u * (unsigned)((a.B + FB - 1) / FB), (unsigned)((a.nitems + 7) / 8));   // (frame group x XCD, item slot)
+        if (FB == 1) hipLaunchKernelGGL(bev_band_kernel<1>, grid, dim3(256), 0, s, a);
+        else hipLaunchKernelGGL(bev_band_kernel<2>, grid, dim3(256), 0, s, a);
     } else if (F != 0 && a.in_cols % 16 == 0 && FG > 0) {
         const long nblk = (long)((a.occ_w + BEV_CB - 1) / BEV_CB) * ((a.occ_h + BEV_CB - 1) / BEV_CB);
         const long grid = nblk * ((a.B + FG - 1) / FG);
