@@ -10,16 +10,22 @@ config 5's share at N=8).
 
 Run:  python bench.py [--gpus N --steps K --warmup W]
       python -m torch.distributed.run --nproc-per-node N --master-addr 127.0.0.1 ... bench.py --gpus N
+The headline is the fp32 mode (`--precision fp32`, the default since round 5): the reference's own
+arithmetic (TF fp32 sess.run, models.py:43-44), logits within 1e-3 of the fp32 oracle over the whole
+f32 range (tests/test_gpu_range.py). fp16 and bf16 (2-byte storage) are sub-records.
+
 Rank 0 prints ONE JSON line. `roofline` describes the dominant kernel of the forward (largest total
-time): the bytes one launch must move (block input read once, output written once) / its average
-launch duration, measured here with HIP events around every launch of one shard's forward on the
-stream the kernels run on, that shard alone on the GPU ("isolated": `roofline.timing`; the
-graph-replayed 2-stream step runs the same launches ~7% longer per rocprofv3), against the 8 TB/s
-HBM peak; `traffic` is the PMC-measured HBM bytes per launch of
-that kernel from the committed profile (profiles/pmc_traffic.json). `roofline.forward` adds the
+in-step time): the bytes one launch must move (block input read once, output written once) / its
+average launch duration IN THE STEP — HIP events recorded around every launch of shard 0 inside a
+captured copy of the timed 2-stream graph step (graph event-record nodes), the other shard running
+beside it as in the timed loop ("timing": "in-step") — against the 8 TB/s HBM peak; the isolated
+figures (one shard alone on the GPU) sit beside it; `traffic` is the PMC-measured HBM bytes per launch
+of that kernel from the committed profile (profiles/pmc_traffic*.json). `roofline.forward` adds the
 whole-forward figures (SURVEY.md 8(d)'s 180.2 MB/frame per-layer definition and the plan's own byte
-counts). The CPU oracle (PyTorch-CPU ENet + C BEV restatement) is timed on a bounded sample on rank 0
-as the reported CPU baseline.
+counts) and the MFMA fraction — for fp32 against the instructions the hardware issues (three f16
+MFMAs per f32 product, at the dense f16 peak) and, beside it, the f32-equivalent figure. The CPU
+oracle (PyTorch-CPU ENet + C BEV restatement) is timed on a bounded sample on rank 0 as the reported
+CPU baseline.
 """
 from __future__ import annotations
 
@@ -37,8 +43,9 @@ import torch  # noqa: E402
 import torch.distributed as dist  # noqa: E402
 
 HBM_PEAK_GBS = 8000.0          # MI355X_MICROARCH.md chip table (spec)
-MFMA_BF16_PEAK_TFLOPS = 2500.0  # dense bf16 (spec)
+MFMA_BF16_PEAK_TFLOPS = 2500.0  # dense bf16 / f16 (spec)
 MFMA_F32_PEAK_TFLOPS = 157.3
+F32_SPLIT_PRODUCTS = 3          # fp32 mode: one f32 product = three f16 MFMA products (mfma_common.h)
 
 
 SURVEY_BYTES_PER_FRAME = 180.2e6   # bf16 per-layer activation bytes per 480x640 frame
@@ -104,8 +111,9 @@ def parse():
     p.add_argument("--batch", type=int, default=64, help="frames per GPU")
     p.add_argument("--height", type=int, default=480)
     p.add_argument("--width", type=int, default=640)
-    p.add_argument("--precision", default="fp16", choices=["bf16", "fp16", "fp32"],
-                   help="storage precision of the timed step (fp16: bf16's bytes and MFMA rate, 3 more mantissa bits)")
+    p.add_argument("--precision", default="fp32", choices=["bf16", "fp16", "fp32"],
+                   help="precision of the timed step: fp32 (default; the reference's arithmetic, logits within 1e-3 "
+                        "over the whole f32 range), fp16 / bf16 (2-byte storage throughput modes)")
     p.add_argument("--streams", type=int, default=2, help="frame shards run concurrently on this many HIP streams")
     p.add_argument("--stream-priority", type=int, default=0, help="HIP priority of the side shards' streams")
     p.add_argument("--chain-forwards", type=int, default=0,
@@ -259,48 +267,181 @@ def forward_ms(ctx, fs, Bs, H, W, seg, stream, reps):
     return ev[0].elapsed_time(ev[1]) / reps
 
 
-def roofline_record(ctx, Bs, H, W, reps, stream, precision, t_fwd):
-    """`roofline` of the dominant kernel of the forward the context last ran at (Bs, H, W): its
-    bytes per launch / its HIP-event launch time against the HBM peak, the PMC traffic of the same
-    kernel tag from the committed profile, and the whole forward's figures (bytes, and the MFMA
-    fraction against the dense peak of the precision's MFMA: f32 for fp32, bf16/f16 otherwise). The
-    launch times are isolated (kernel_table); `timing` says so."""
+class HipEvents:
+    """Raw HIP events recorded with hipEventRecordWithFlags(..., hipEventRecordExternal), so that inside
+    a stream capture each record becomes an event-record node of the graph (torch's Event.record only
+    records a capture dependency there); timed with hipEventElapsedTime after a replay. Bound to the HIP
+    runtime torch loaded (libamdhip64.so.7, the soname libbugseg.so links)."""
+
+    def __init__(self, n):
+        import ctypes
+        self.ct = ctypes
+        self.hip = ctypes.CDLL("libamdhip64.so.7")
+        vp = ctypes.c_void_p
+        self.hip.hipEventCreate.argtypes = [ctypes.POINTER(vp)]
+        self.hip.hipEventRecordWithFlags.argtypes = [vp, vp, ctypes.c_uint]
+        self.hip.hipEventElapsedTime.argtypes = [ctypes.POINTER(ctypes.c_float), vp, vp]
+        self.hip.hipEventDestroy.argtypes = [vp]
+        self.ev = []
+        for _ in range(n):
+            e = vp()
+            if self.hip.hipEventCreate(ctypes.byref(e)) != 0:
+                raise RuntimeError("hipEventCreate failed")
+            self.ev.append(e)
+
+    def record(self, i, stream):
+        if self.hip.hipEventRecordWithFlags(self.ev[i], self.ct.c_void_p(int(stream.cuda_stream)), 1) != 0:
+            raise RuntimeError("hipEventRecordWithFlags failed")
+
+    def ms(self, i, j):
+        t = self.ct.c_float()
+        if self.hip.hipEventElapsedTime(self.ct.byref(t), self.ev[i], self.ev[j]) != 0:
+            raise RuntimeError("hipEventElapsedTime failed")
+        return float(t.value)
+
+    def close(self):
+        for e in self.ev:
+            self.hip.hipEventDestroy(e)
+        self.ev = []
+
+
+def instep_kernel_table(pipe, frames, H, W, reps):
+    """Per-launch durations IN THE STEP: a captured copy of the timed step (every shard's forward + BEV
+    on its own stream, as pipe.run launches them) in which shard 0's forward is issued launch by launch
+    with a HIP event-record node before each and after the last; replayed `reps` times, host-synced
+    after each replay to read the events. Grouped by kernel tag like kernel_table. Also returns the
+    instrumented step's ms (the event nodes' own cost shows as its excess over the plain step)."""
     from bugcar_image_segmentation_amd import _native as N
-    kernels = kernel_table(ctx, Bs, H, W, reps, stream)
+    dev = frames.device
+    B, S = frames.shape[0], pipe.streams
+    ctxs, sts = pipe._shard_ctxs(dev)
+    _x, seg, g = pipe._bufs(B, dev)
+    prm = pipe._params()
+    bounds = [B * i // S for i in range(S + 1)]
+    Bs = bounds[1]
+    kind = N.OUT_CLASS3_U8
+    n = ctxs[0].plan_info(Bs, H, W, kind, bgr_input=True)[0]
+    hev = HipEvents(n + 1)
+
+    def step():
+        main = torch.cuda.current_stream(dev)
+        ready = main.record_event()
+        for i in range(S):
+            s0, e0 = bounds[i], bounds[i + 1]
+            st = main if i == 0 else sts[i - 1]
+            if i:
+                st.wait_event(ready)
+            with torch.cuda.stream(st):
+                if i == 0:
+                    for op in range(n):
+                        hev.record(op, st)
+                        ctxs[0].forward_bgr_ops(frames[s0:e0], e0 - s0, H, W, kind, seg[s0:e0], op, op + 1, st)
+                    hev.record(n, st)
+                else:
+                    ctxs[i].forward_bgr(frames[s0:e0], e0 - s0, H, W, kind, seg[s0:e0], st)
+                ctxs[i].bev(seg[s0:e0], e0 - s0, prm, g[s0:e0], st)
+        for st in sts[: S - 1]:
+            main.wait_stream(st)
+
+    step()
+    torch.cuda.synchronize()
+    graph = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(graph):
+        step()
+    for _ in range(3):
+        graph.replay()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(reps):
+        graph.replay()
+    torch.cuda.synchronize()
+    step_ms = (time.perf_counter() - t0) / reps * 1e3
+    tot = [0.0] * (n + 1)
+    for _ in range(reps):
+        graph.replay()
+        torch.cuda.synchronize()
+        for i in range(n):
+            tot[i] += hev.ms(i, i + 1)
+        tot[n] += hev.ms(0, n)
+    hev.close()
+    del graph
+    groups = {}
+    for i in range(n):
+        tag, _lb, pb, fl = ctxs[0].plan_op(Bs, H, W, i)
+        gr = groups.setdefault(tag, {"launches": 0, "total_us": 0.0, "bytes": 0.0, "flops": 0.0})
+        gr["launches"] += 1
+        gr["total_us"] += tot[i] / reps * 1e3
+        gr["bytes"] += pb
+        gr["flops"] += fl
+    groups.pop("fused", None)
+    for gr in groups.values():
+        gr["us_per_launch"] = gr["total_us"] / gr["launches"]
+        gr["bytes_per_launch"] = gr["bytes"] / gr["launches"]
+        gr["flops_per_launch"] = gr["flops"] / gr["launches"]
+    return groups, {"instrumented_step_ms": round(step_ms, 4), "shard0_forward_ms": round(tot[n] / reps, 4)}
+
+
+def roofline_record(ctx, Bs, H, W, reps, stream, precision, t_fwd, instep=None):
+    """`roofline` of the dominant kernel of the forward (largest total time; in-step timing when the
+    in-step table is given, isolated otherwise): its bytes per launch / its average launch time against
+    the HBM peak, the PMC traffic of the same kernel tag from the committed profile, the isolated
+    figures beside the in-step ones, and the whole forward's figures (bytes; the MFMA fraction — fp32:
+    against the three f16 MFMAs per product the hardware issues at the dense f16 peak, and the
+    f32-equivalent against the f32 peak)."""
+    from bugcar_image_segmentation_amd import _native as N
+    iso = kernel_table(ctx, Bs, H, W, reps, stream)
+    kernels, meta = instep if instep is not None else (iso, None)
     n_launch, alg_bytes, plan_bytes, flops = ctx.plan_info(Bs, H, W, N.OUT_CLASS3_U8, bgr_input=True)
     tag, k = max(kernels.items(), key=lambda kv: kv[1]["total_us"])
     k_achieved = k["bytes_per_launch"] / (k["us_per_launch"] * 1e-6) / 1e9
-    mpeak = MFMA_F32_PEAK_TFLOPS if precision == "fp32" else MFMA_BF16_PEAK_TFLOPS
+    ki = iso.get(tag, k)
+    iso_achieved = ki["bytes_per_launch"] / (ki["us_per_launch"] * 1e-6) / 1e9
+    f32 = precision == "fp32"
+    issue = F32_SPLIT_PRODUCTS if f32 else 1          # MFMA products issued per algorithmic product
+    mpeak = MFMA_BF16_PEAK_TFLOPS                       # the f16 / bf16 MFMAs every mode issues
     k_flops = k.get("flops_per_launch", 0.0)
+    k_tf = k_flops / (k["us_per_launch"] * 1e-6) / 1e12
+    t_fwd_instep = meta["shard0_forward_ms"] if meta else t_fwd
+    fwd_tf = flops / (t_fwd_instep * 1e-3) / 1e12
+    timing = ("in-step: HIP event-record nodes around each launch of shard 0 inside a captured copy of the "
+              "timed 2-stream graph step (the other shard beside it, as timed); `isolated` = the same launch "
+              "with that shard alone on the GPU") if meta else "isolated: one shard alone on the GPU"
     rec = {
         "bound": "hbm", "achieved": round(k_achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
         "frac": round(k_achieved / HBM_PEAK_GBS, 4),
         "traffic": pmc_traffic(tag, precision),
         "kernel": f"{KERNEL_NAMES.get(tag.rsplit(' ', 1)[0], tag).format(t=TEMPLATE_TYPE[precision])} [{tag}]: the dominant kernel of the forward "
-                  f"({k['launches']} launches, {k['total_us']:.0f} us of {t_fwd * 1e3:.0f} us); "
+                  f"({k['launches']} launches, {k['total_us']:.0f} us of {t_fwd_instep * 1e3:.0f} us in step); "
                   f"{k['bytes_per_launch'] / 1e6:.1f} MB per launch = the bytes the launch must move "
-                  f"(block input read once + output written once); {k['us_per_launch']:.2f} us per launch "
-                  f"(HIP events around each launch, this shard alone on the GPU, in forward order)",
-        "timing": "isolated: HIP events around each launch of one shard's forward with nothing else on the GPU; "
-                  "rocprofv3's per-kernel average of the graph-replayed 2-stream bench command runs ~7% longer "
-                  "(profiles/r04_*_fp16_b64s2.md), so the in-step fraction is ~0.93x this one",
+                  f"(block input read once + output written once); {k['us_per_launch']:.2f} us per launch",
+        "timing": timing,
         "us_per_launch": round(k["us_per_launch"], 3),
-        "kernel_mfma_tflops": round(k_flops / (k["us_per_launch"] * 1e-6) / 1e12, 2),
-        "kernel_mfma_frac": round(k_flops / (k["us_per_launch"] * 1e-6) / 1e12 / mpeak, 4),
+        "isolated": {"us_per_launch": round(ki["us_per_launch"], 3), "achieved": round(iso_achieved, 1),
+                     "frac": round(iso_achieved / HBM_PEAK_GBS, 4)},
+        "kernel_mfma_tflops": round(k_tf, 2),
+        "kernel_mfma_frac": round(k_tf * issue / mpeak, 4),
         "mfma_peak_tflops": mpeak,
+        "mfma_pricing": (f"fp32: {F32_SPLIT_PRODUCTS} v_mfma_f32_*_f16 per f32 product (split-f16, mfma_common.h), "
+                         f"priced at the dense f16 peak; f32-equivalent beside it") if f32 else "dense bf16/f16 peak",
         "forward": {
-            "launches": n_launch, "ms": round(t_fwd, 4),
+            "launches": n_launch, "ms": round(t_fwd_instep, 4), "ms_isolated": round(t_fwd, 4),
             "survey_bytes_per_frame": SURVEY_BYTES_PER_FRAME,
             "frames": Bs,
-            "survey_achieved_gbs": round(SURVEY_BYTES_PER_FRAME * Bs / (t_fwd * 1e-3) / 1e9, 1),
+            "survey_achieved_gbs": round(SURVEY_BYTES_PER_FRAME * Bs / (t_fwd_instep * 1e-3) / 1e9, 1),
             "plan_layer_bytes_per_frame": round(alg_bytes / Bs),
             "plan_bytes_per_frame": round(plan_bytes / Bs),
-            "plan_achieved_gbs": round(plan_bytes / (t_fwd * 1e-3) / 1e9, 1),
-            "mfma_tflops": round(flops / (t_fwd * 1e-3) / 1e12, 2),
-            "mfma_frac": round(flops / (t_fwd * 1e-3) / 1e12 / mpeak, 4)},
+            "plan_achieved_gbs": round(plan_bytes / (t_fwd_instep * 1e-3) / 1e9, 1),
+            "mfma_tflops": round(fwd_tf, 2),
+            "mfma_frac": round(fwd_tf * issue / mpeak, 4)},
     }
+    if f32:
+        rec["kernel_mfma_frac_f32_equiv"] = round(k_tf / MFMA_F32_PEAK_TFLOPS, 4)
+        rec["forward"]["mfma_frac_f32_equiv"] = round(fwd_tf / MFMA_F32_PEAK_TFLOPS, 4)
+    if meta:
+        rec["instep"] = meta
     table = {t: {"launches": v["launches"], "us_per_launch": round(v["us_per_launch"], 2),
-                 "GBps": round(v["bytes_per_launch"] / (v["us_per_launch"] * 1e-6) / 1e9, 1)}
+                 "GBps": round(v["bytes_per_launch"] / (v["us_per_launch"] * 1e-6) / 1e9, 1),
+                 "us_per_launch_isolated": round(iso[t]["us_per_launch"], 2) if t in iso else None}
              for t, v in sorted(kernels.items(), key=lambda kv: -kv[1]["total_us"])}
     return rec, table
 
@@ -329,8 +470,9 @@ def mode_record(blocks, bev, grid, H, W, frames, streams, steps, precision, grap
     stream = torch.cuda.current_stream()
     Bs = B // streams if streams > 1 and B >= streams else B
     _x, seg, _g = pipe._bufs(B, frames.device)
+    instep = instep_kernel_table(pipe, frames, H, W, 10) if streams > 1 and B >= streams else None
     t_fwd = forward_ms(model.ctx, frames[:Bs], Bs, H, W, seg[:Bs], stream, 10)
-    roof, table = roofline_record(model.ctx, Bs, H, W, 10, stream, precision, t_fwd)
+    roof, table = roofline_record(model.ctx, Bs, H, W, 10, stream, precision, t_fwd, instep)
     del pipe, model
     return {"value": round(B * steps / el, 2), "unit": "frames/s", "ms_per_step": round(el / steps * 1e3, 4),
             "per_gpu_batch": B, "steps": steps, "streams_per_gpu": streams, "hip_graph": bool(graph), "dtype": precision,
@@ -367,6 +509,35 @@ def latency_b1(blocks, precision, bev, grid, H, W, frame, iters):
             "eager_ms": e_mean, "eager_median_ms": e_med, "eager_p99_ms": e_p99,
             "graph_ms": g_mean, "graph_median_ms": g_med, "graph_p99_ms": g_p99,
             "graph_fps": round(1e3 / g_mean, 1)}
+
+
+def grid_agreement(blocks, bev, grid, H, W, frame_sets, streams, precs=("fp16", "bf16")):
+    """What the ROS loop consumes: the occupancy grids (and 3-class maps) of the 2-byte modes against
+    the fp32 mode's, at the bench configuration (the timed pipeline, same shards and streams), on the
+    bench's own frames and on structured road scenes. Torch ops here only compare engine outputs."""
+    from bugcar_image_segmentation_amd.models import ENET
+    from bugcar_image_segmentation_amd.pipeline import OccupancyPipeline
+    outs = {}
+    for prec in ("fp32",) + tuple(precs):
+        m = ENET(weights=blocks, precision=prec)
+        pipe = OccupancyPipeline(m, bev, *grid, model_hw=(H, W), streams=streams)
+        for name, fr in frame_sets.items():
+            g = pipe.run(fr).clone()
+            _x, seg, _g = pipe._bufs(fr.shape[0], fr.device)
+            outs[(prec, name)] = (g, seg.clone())
+        torch.cuda.synchronize()
+        del pipe, m
+    res = {}
+    for prec in precs:
+        res[prec] = {}
+        for name, fr in frame_sets.items():
+            g32, s32 = outs[("fp32", name)]
+            g, sg = outs[(prec, name)]
+            nd = int((g32 != g).sum())
+            res[prec][name] = {"frames": int(fr.shape[0]), "cells": int(g32.numel()), "cells_differing": nd,
+                               "cell_agreement": round(1.0 - nd / g32.numel(), 7),
+                               "class3_pixel_agreement": round(float((s32 == sg).float().mean()), 7)}
+    return res
 
 
 def class_agreement(blocks, H, W, nframes, dev, precs=("bf16", "fp16")):
@@ -520,8 +691,10 @@ def main():
     ev[1].synchronize()
     t_ls = ev[0].elapsed_time(ev[1]) / reps
     bev.laserscan_like_occupancy_grid = False
-    roof, ktable = roofline_record(model.ctx, Bs, H, W, reps, stream, a.precision, t_fwd)
     overlap = shard_overlap(pipe, frames, seg, g, bev, grid, H, W, reps) if a.streams > 1 and B >= a.streams else None
+    log("in-step kernel table")
+    instep = instep_kernel_table(pipe, frames, H, W, reps) if a.streams > 1 and B >= a.streams else None
+    roof, ktable = roofline_record(model.ctx, Bs, H, W, reps, stream, a.precision, t_fwd, instep)
 
     if rank == 0:
         frames_total = B * world * a.steps
@@ -553,12 +726,20 @@ def main():
                     res[prec] = mode_record(blocks, bev, grid, H, W, frames, a.streams, max(10, a.steps), prec, bool(a.graph))
             log("batch-1 latency sub-records")
             res["latency_b1_ms"] = latency_b1(blocks, a.precision, bev, grid, H, W, frames[:1], 100)
-            # BASELINE config 2 names bf16 at batch 1
-            res["latency_b1_ms_bf16"] = latency_b1(blocks, "bf16", bev, grid, H, W, frames[:1], 100)
+            # BASELINE config 2 names bf16 at batch 1 (logits within 1e-3 only in fp32: latency_b1_ms)
+            for prec in ("fp32", "fp16", "bf16"):
+                if prec != a.precision:
+                    res[f"latency_b1_ms_{prec}"] = latency_b1(blocks, prec, bev, grid, H, W, frames[:1], 100)
             log("class agreement sub-records")
             agree = class_agreement(blocks, H, W, 4, dev)
             res["bf16_class_agreement_vs_fp32"] = agree["bf16"]
             res["fp16_class_agreement_vs_fp32"] = agree["fp16"]
+            log("grid agreement sub-records")
+            road = torch.from_numpy(synthetic.road_frames(B, H, W, seed=77)).to(dev)
+            gagree = grid_agreement(blocks, bev, grid, H, W, {"bench_frames": frames, "road_frames": road}, a.streams)
+            res["fp16_grid_agreement_vs_fp32"] = gagree["fp16"]
+            res["bf16_grid_agreement_vs_fp32"] = gagree["bf16"]
+            del road
             import bench_deeplab
             log("deeplab sub-record")
             res["deeplab"] = bench_deeplab.record(dev, a.deeplab_batch, max(5, a.steps // 2), 3, "bf16",

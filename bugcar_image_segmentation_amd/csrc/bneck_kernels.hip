@@ -294,8 +294,15 @@ __global__ void __launch_bounds__((BShape<C, V>::NW * 64), (sizeof(T) == 2 ? BSh
     // channels 32 t + 8 kq .. + 7), as phase 3's residual — instead of a global scratch round trip
     // (PMC: down C64 read + wrote 1.33x, down C128 1.36x their compulsory bytes with the scratch).
     // Measured (round 3, fp16, B = 32): down C64 52.9 -> 48.1 us, down C128 33.7 -> 28.7 us
-    constexpr bool DKEEP = BNECK_DKEEP && DN && sizeof(T) == 2 && SWAP;
-    constexpr int NPK = DN ? (CI + 31) / 32 : 1;      // DKEEP: pooled 16-B chunks per lane and fragment
+    // fp32 (round 5): the same walk; a pooled chunk is 8 floats (two 16-B words) in the
+    // kept-x layout of KEEPF, turned into phase 3's row quads by the same two lane swaps (PMC before: down
+    // C64 1.27x, down C128 1.37x their compulsory bytes with the scratch round trip)
+#ifndef BNECK_DKEEP_F32
+#define BNECK_DKEEP_F32 1
+#endif
+    constexpr bool DKEEP = BNECK_DKEEP && DN && ((sizeof(T) == 2 && SWAP) || (sizeof(T) == 4 && BNECK_DKEEP_F32 && REG3));
+    constexpr int NPK = DN ? (CI + 31) / 32 : 1;      // DKEEP: pooled chunks (32 channels of the row pair) per lane and fragment
+    constexpr int PKW = sizeof(T) == 4 ? 2 : 1;       // 16-B words per pooled chunk
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     // fp32 (parity mode): t0 / t1a live in LDS as split-f16 parts (mfma_common.h st4s: the weights'
     // layout, 32 B per 8 channels as the f32 values take), split once when written rather than at every
@@ -443,6 +450,67 @@ __global__ void __launch_bounds__((BShape<C, V>::NW * 64), (sizeof(T) == 2 ? BSh
     const int dt = a.dt;                              // tiling dilation (1 for asymmetric blocks)
     constexpr bool tr = TR && !ASYM;                  // transposed tile
 
+    // fp32 mode range scaling (bugseg_internal.h RangeArgs, mfma_common.h): the exponents of x (measured
+    // by the launch that wrote it), t0, t1 (asymmetric: t1a, t1; rigorous bounds from x's range) and
+    // the multipliers of the accumulators; scl is false — no multiply anywhere — when every exponent is 0
+    constexpr bool F32 = sizeof(T) == 4;
+
+    bool scl = false;
+    float xm = 1.f, b1m = 1.f, o1m = 1.f, b2m = 1.f, o2m = 1.f, b2bm = 1.f, o2bm = 1.f, b3m = 1.f, o3m = 1.f;
+    float amo = 0.f;                                  // max |out| of this lane's stores
+    if constexpr (F32) {
+      const RangeArgs &g = a.rg;
+      if (!g.off) {
+        const float amx = rng_read(g);
+        const int sx = rng_exp_meas(amx), e1 = sx + g.sw[0];
+        const float B0 = g.n[0] * amx + g.c[0];
+        const int s0 = rng_exp_bound(B0, e1), e2 = s0 + g.sw[1];
+        const float B1 = g.n[1] * B0 + g.c[1];
+        const int s1 = rng_exp_bound(B1, e2);
+        int e2b = 0, s1b = 0;
+        if constexpr (ASYM) {
+            e2b = s1 + g.sw[2];
+            s1b = rng_exp_bound(g.n[2] * B1 + g.c[2], e2b);
+        }
+        const int e3 = (ASYM ? s1b : s1) + g.sw[3];
+        scl = e3 != 0;                                // (only phase 3 branches; the rest always multiplies)
+        xm = rng_pow2(sx); b1m = rng_pow2(e1); o1m = rng_pow2(s0 - e1); b2m = rng_pow2(e2); o2m = rng_pow2(s1 - e2);
+        b2bm = rng_pow2(e2b); o2bm = rng_pow2(s1b - e2b); b3m = rng_pow2(e3); o3m = rng_pow2(-e3);
+      }
+    }
+    // the projection of one fragment. fp32: always scaled (the multipliers are 1 when nothing needs it):
+    // a branch to a scaled copy of this code cost the fp32 kernels 15-40 VGPRs (register allocation
+    // covers both paths), the multiplies cost ~0.5 VALU per element (v_pk_mul_f32)
+    auto proj_mfma = [&](f32x4 (&acc)[NR1], const Raw (&xs)[KS1]) {
+#pragma unroll
+        for (int r = 0; r < NR1; ++r) acc[r] = bias4(cb1 + r * 16 + kq * 4);
+        if constexpr (F32) {
+#pragma unroll
+            for (int r = 0; r < NR1; ++r) acc[r] = mul4(acc[r], b1m);
+#pragma unroll
+            for (int s = 0; s < KS1; ++s) {
+                const RawF xq = scale8(reinterpret_cast<const RawF &>(xs[s]), xm);
+#pragma unroll
+                for (int r = 0; r < NR1; ++r) {
+                    WRaw wf;
+                    ld8(wf, w1 + (r * 16 + col) * K1S + s * 32 + kq * 8);
+                    mma(acc[r], wf, xq);
+                }
+            }
+#pragma unroll
+            for (int r = 0; r < NR1; ++r) acc[r] = mul4(acc[r], o1m);
+        } else {
+#pragma unroll
+            for (int s = 0; s < KS1; ++s)
+#pragma unroll
+                for (int r = 0; r < NR1; ++r) {
+                    WRaw wf;
+                    ld8(wf, w1 + (r * 16 + col) * K1S + s * 32 + kq * 8);
+                    mma(acc[r], wf, xs[s]);
+                }
+        }
+    };
+
     // XCD-aware tile walk (see conv_kernels.hip): each XCD takes a contiguous run of tiles, so the
     // halo re-reads of neighbouring tiles hit the same L2
     const int G = gridDim.x, grp = blockIdx.x & 7, slot = blockIdx.x >> 3, nslots = G >> 3;
@@ -504,7 +572,7 @@ __global__ void __launch_bounds__((BShape<C, V>::NW * 64), (sizeof(T) == 2 ? BSh
         // down: main-branch maxpool of output pixel (y, x) from the projection's B fragments (see the
         // kernel comment); the first maximum in window order wins (strict >, NaN / -inf never chosen:
         // as a key, larger value first, then lower window position; position 4 = no candidate -> 0)
-        auto pool_store = [&](const Raw (&xs)[KS1], bool interior, int y, int x, uint4 (&pk)[NPK]) {
+        auto pool_store = [&](const Raw (&xs)[KS1], bool interior, int y, int x, uint4 (&pk)[NPK * PKW]) {
             if constexpr (DN) {
                 if (__ballot(interior) == 0) return;          // halo-only fragment (wave-uniform)
                 auto elems = [&](const Raw &r, float (&e)[8]) {
@@ -536,7 +604,9 @@ __global__ void __launch_bounds__((BShape<C, V>::NW * 64), (sizeof(T) == 2 ? BSh
                         hi |= (uint32_t)(bp[4 + i] & 3) << (8 * i);
                     }
                     if constexpr (DKEEP) {
-                        pk[kslot] = kval ? make_uint4(pw[0], pw[1], pw[2], pw[3]) : make_uint4(0u, 0u, 0u, 0u);
+                        pk[kslot * PKW] = kval ? make_uint4(pw[0], pw[1], pw[2], pw[3]) : make_uint4(0u, 0u, 0u, 0u);
+                        if constexpr (PKW == 2)
+                            pk[kslot * PKW + 1] = kval ? make_uint4(pw[4], pw[5], pw[6], pw[7]) : make_uint4(0u, 0u, 0u, 0u);
                     } else {
                         (void)kslot; (void)kval;
                         const uint32_t po = wr ? (pix * CI + cc * 8) * (uint32_t)sizeof(T) : OOB;
@@ -650,16 +720,7 @@ __global__ void __launch_bounds__((BShape<C, V>::NW * 64), (sizeof(T) == 2 ? BSh
         };
         auto proj = [&](int h, bool valid, bool ok, const Raw (&xs)[KS1]) {
             f32x4 acc[NR1];
-#pragma unroll
-            for (int r = 0; r < NR1; ++r) acc[r] = bias4(cb1 + r * 16 + kq * 4);
-#pragma unroll
-            for (int s = 0; s < KS1; ++s)
-#pragma unroll
-                for (int r = 0; r < NR1; ++r) {
-                    WRaw wf;
-                    ld8(wf, w1 + (r * 16 + col) * K1S + s * 32 + kq * 8);
-                    mma(acc[r], wf, xs[s]);
-                }
+            proj_mfma(acc, xs);
             if (valid) {
 #pragma unroll
                 for (int r = 0; r < NR1; ++r) {
@@ -671,7 +732,7 @@ __global__ void __launch_bounds__((BShape<C, V>::NW * 64), (sizeof(T) == 2 ? BSh
                 }
             }
         };
-        uint4 pres[DKEEP ? NF2 : 1][NPK];             // DKEEP: pooled residual of the interior fragments
+        uint4 pres[DKEEP ? NF2 : 1][NPK * PKW];       // DKEEP: pooled residual of the interior fragments
         if constexpr (KEEP) {
             // every load of the wave's phase-1 work (its interior fragments, kept, and its share of
             // the border) is issued before the first MFMA: one memory round trip per tile
@@ -741,7 +802,7 @@ __global__ void __launch_bounds__((BShape<C, V>::NW * 64), (sizeof(T) == 2 ? BSh
 #pragma unroll
             for (int j = 0; j < NF2; ++j)
 #pragma unroll
-                for (int k = 0; k < NPK; ++k) pres[j][k] = make_uint4(0u, 0u, 0u, 0u);
+                for (int k = 0; k < NPK * PKW; ++k) pres[j][k] = make_uint4(0u, 0u, 0u, 0u);
 #pragma unroll
             for (int q0 = 0; q0 < NQ; q0 += CH1) {
                 Raw xf[CH1][KS1];
@@ -808,16 +869,7 @@ __global__ void __launch_bounds__((BShape<C, V>::NW * 64), (sizeof(T) == 2 ? BSh
             for (int c = 0; c < CH1; ++c) {
                 const int h = (f0 + c * NW) * 16 + col;
                 f32x4 acc[NR1];
-#pragma unroll
-                for (int r = 0; r < NR1; ++r) acc[r] = bias4(cb1 + r * 16 + kq * 4);
-#pragma unroll
-                for (int s = 0; s < KS1; ++s)
-#pragma unroll
-                    for (int r = 0; r < NR1; ++r) {
-                        WRaw wf;
-                        ld8(wf, w1 + (r * 16 + col) * K1S + s * 32 + kq * 8);
-                        mma(acc[r], wf, xf[c][s]);
-                    }
+                proj_mfma(acc, xf[c]);
                 if (h < HR) {
 #pragma unroll
                     for (int r = 0; r < NR1; ++r) {
@@ -831,7 +883,7 @@ __global__ void __launch_bounds__((BShape<C, V>::NW * 64), (sizeof(T) == 2 ? BSh
                 if constexpr (DN) {
                     const int hy = h / HWW, hx = h - hy * HWW;
                     const bool interior = okc[c] && hy >= 1 && hy <= TH && hx >= 1 && hx <= TW;
-                    uint4 pkd[NPK];
+                    uint4 pkd[NPK * PKW];
                     pool_store(xf[c], interior, oy0 + (hy - 1), ox0 + (hx - 1), pkd);
                 }
             }
@@ -887,13 +939,25 @@ __global__ void __launch_bounds__((BShape<C, V>::NW * 64), (sizeof(T) == 2 ? BSh
         // expansion's B operand (lane kq: channels 8kq..8kq+7) with two lane swaps (to_bop) — the
         // expansion of a fragment runs on the wave that computed it, so no barrier is needed either
         Raw tf[NF2];
-        auto to_tf = [&](const f32x4 (&acc)[NF2][NR1], const float *cs) {
+        auto to_tf = [&](f32x4 (&acc)[NF2][NR1], const float *cs, float om) {
+            if constexpr (F32) {
+#pragma unroll
+                for (int j = 0; j < NF2; ++j)
+#pragma unroll
+                    for (int r = 0; r < NR1; ++r) acc[j][r] = mul4(acc[j][r], om);
+            }
 #pragma unroll
             for (int j = 0; j < NF2; ++j) {
                 const float4 q0 = act(f4(acc[j][0]), cs + kq * 4);
                 const float4 q1 = NR1 > 1 ? act(f4(acc[j][NR1 > 1 ? 1 : 0]), cs + 16 + kq * 4) : make_float4(0.f, 0.f, 0.f, 0.f);
                 to_bop(tf[j], q0, q1);
             }
+        };
+        // accumulators starting at the bias (fp32: times m, the accumulator's scale)
+        auto bias_m = [&](const float *p, float m) -> f32x4 {
+            f32x4 b = bias4(p);
+            if constexpr (F32) b = mul4(b, m);
+            return b;
         };
         static_assert(NR1 <= 2, "t1 in registers: at most 32 internal channels");
 
@@ -903,7 +967,7 @@ __global__ void __launch_bounds__((BShape<C, V>::NW * 64), (sizeof(T) == 2 ? BSh
 #pragma unroll
             for (int j = 0; j < NF2; ++j)
 #pragma unroll
-                for (int r = 0; r < NR1; ++r) acc[j][r] = bias4(cb2 + r * 16 + kq * 4);
+                for (int r = 0; r < NR1; ++r) acc[j][r] = bias_m(cb2 + r * 16 + kq * 4, b2m);
             constexpr int PH2U = BNECK_PH2_UNROLL > 0 ? BNECK_PH2_UNROLL : (C == 128 && !DN && !(KEEP && V == 2) ? 3 : 1);
 #pragma unroll PH2U
             for (int s = 0; s < KS2; ++s) {
@@ -931,7 +995,7 @@ __global__ void __launch_bounds__((BShape<C, V>::NW * 64), (sizeof(T) == 2 ? BSh
                 }
             }
             STAMP(4);
-            to_tf(acc, cs2);
+            to_tf(acc, cs2, o2m);
         } else {
             // 5x1 over rows (taps dy = -2..2), output width TW+4 (the 1x5's halo). (Run in two fragment
             // halves with the residual kept in registers it measured slower, round 3: 28.2 vs 26.2 us)
@@ -939,7 +1003,7 @@ __global__ void __launch_bounds__((BShape<C, V>::NW * 64), (sizeof(T) == 2 ? BSh
 #pragma unroll
             for (int j = 0; j < NF2A; ++j)
 #pragma unroll
-                for (int r = 0; r < NR1; ++r) acc5[j][r] = bias4(cb2 + r * 16 + kq * 4);
+                for (int r = 0; r < NR1; ++r) acc5[j][r] = bias_m(cb2 + r * 16 + kq * 4, b2m);
 #pragma unroll BNECK_ASYM_UNROLL
             for (int s = 0; s < KS2; ++s) {
                 const int g = s * 4 + kq;
@@ -970,7 +1034,9 @@ __global__ void __launch_bounds__((BShape<C, V>::NW * 64), (sizeof(T) == 2 ? BSh
                     if (f < NFA && p < NPA && ch < IS) {
                         const int ox = p - (p / TWA) * TWA;
                         const bool inside = (unsigned)(ox0 - 2 + ox) < (unsigned)a.W;
-                        const float4 v = act(f4(acc5[j][r]), cs2 + ch);
+                        float4 v = f4(acc5[j][r]);
+                        if constexpr (F32) v = mul4(v, o2m);
+                        v = act(v, cs2 + ch);
                         st4t(ts + p * PSTR + ch, ch, inside ? v : make_float4(0.f, 0.f, 0.f, 0.f));
                     }
                 }
@@ -980,7 +1046,7 @@ __global__ void __launch_bounds__((BShape<C, V>::NW * 64), (sizeof(T) == 2 ? BSh
 #pragma unroll
                 for (int j = 0; j < NF2; ++j)
 #pragma unroll
-                    for (int r = 0; r < NR1; ++r) acc[j][r] = bias4(cb2b + r * 16 + kq * 4);
+                    for (int r = 0; r < NR1; ++r) acc[j][r] = bias_m(cb2b + r * 16 + kq * 4, b2bm);
 #pragma unroll BNECK_ASYM_UNROLL
                 for (int s = 0; s < KS2; ++s) {
                     const int g = s * 4 + kq;
@@ -1001,7 +1067,7 @@ __global__ void __launch_bounds__((BShape<C, V>::NW * 64), (sizeof(T) == 2 ? BSh
                     }
                 }
                 if constexpr (!KEEP) prefetch_res();
-                to_tf(acc, cs2b);
+                to_tf(acc, cs2b, o2bm);
             }
         }
 
@@ -1038,13 +1104,19 @@ __global__ void __launch_bounds__((BShape<C, V>::NW * 64), (sizeof(T) == 2 ? BSh
                         for (int rr = 0; rr < NR3 / 2; ++rr) {
                             const int r = h * (NR3 / 2) + rr;
                             const int ch = r * 16 + kq * 4;
-                            f32x4 acc = bias_in_acc(NR3, 1) ? bias4(cb3 + ch) : (f32x4){0.f, 0.f, 0.f, 0.f};
+                            static_assert(bias_in_acc(NR3, 1), "expansion: one k step, bias in the accumulator");
+                            f32x4 acc = bias_m(cb3 + ch, b3m);
                             WRaw wf;
                             ld8(wf, w3 + (r * 16 + col) * K3S + kq * 8);
                             mma(acc, wf, tf[j]);
                             T *sp = stg + col * OSTR + (ch - h * (C / 2));
-                            float4 v = act(bias_in_acc(NR3, 1) ? f4(acc) : add4(f4(acc), ld4f(cb3 + ch)), cs3 + ch);
+                            float4 v = f4(acc);
+                            if constexpr (F32) {
+                                if (scl) v = mul4(v, o3m);
+                            }
+                            v = act(v, cs3 + ch);
                             v = act(add4(v, ld4(sp)), cso + ch);
+                            if constexpr (F32) rng_acc4(amo, v);
                             st4(sp, v);
                         }
                         wave_lds_sync();
@@ -1080,13 +1152,18 @@ __global__ void __launch_bounds__((BShape<C, V>::NW * 64), (sizeof(T) == 2 ? BSh
 #pragma unroll
                 for (int r = 0; r < NR3; ++r) {
                     const int ch = r * 16 + kq * 4;
-                    f32x4 acc = bias_in_acc(NR3, 1) ? bias4(cb3 + ch) : (f32x4){0.f, 0.f, 0.f, 0.f};
+                    f32x4 acc = bias_m(cb3 + ch, b3m);
                     WRaw wf;
                     ld8(wf, w3 + (r * 16 + col) * K3S + kq * 8);
                     mma(acc, wf, tf[j]);
                     T *sp = stg + col * OSTR + ch;
-                    float4 v = act(bias_in_acc(NR3, 1) ? f4(acc) : add4(f4(acc), ld4f(cb3 + ch)), cs3 + ch);
+                    float4 v = f4(acc);
+                    if constexpr (F32) {
+                        if (scl) v = mul4(v, o3m);
+                    }
+                    v = act(v, cs3 + ch);
                     v = act(add4(v, ld4(sp)), cso + ch);
+                    if constexpr (F32) rng_acc4(amo, v);
                     st4(sp, v);
                 }
                 wave_lds_sync();
@@ -1108,25 +1185,34 @@ __global__ void __launch_bounds__((BShape<C, V>::NW * 64), (sizeof(T) == 2 ? BSh
         for (int j = 0; j < NF2; ++j) {
             if (wave + NW * j >= NFT) break;              // wave-uniform
             const uint32_t po = pix_base(wave + NW * j, col);
-            if constexpr (KEEPF) {
-                // kept fp32 x -> residual quads in place: .a = row 2 s, .b = row 2 s + 1
+            // kept fp32 x (KEEPF) / pooled fp32 main branch (DKEEP) -> residual quads in place: chunk s
+            // (lane kq: channels 32 s + 8 kq .. + 7) becomes .a = row 2 s, .b = row 2 s + 1
+            auto to_quads = [&](RawF &k) {
+                uint32_t a[4] = {__float_as_uint(k.a.x), __float_as_uint(k.a.y), __float_as_uint(k.a.z), __float_as_uint(k.a.w)};
+                uint32_t b[4] = {__float_as_uint(k.b.x), __float_as_uint(k.b.y), __float_as_uint(k.b.z), __float_as_uint(k.b.w)};
 #pragma unroll
-                for (int s = 0; s < KS1; ++s) {
-                    RawF &k = reinterpret_cast<RawF &>(kx[j][s]);
-                    uint32_t a[4] = {__float_as_uint(k.a.x), __float_as_uint(k.a.y), __float_as_uint(k.a.z), __float_as_uint(k.a.w)};
-                    uint32_t b[4] = {__float_as_uint(k.b.x), __float_as_uint(k.b.y), __float_as_uint(k.b.z), __float_as_uint(k.b.w)};
-#pragma unroll
-                    for (int d = 0; d < 4; ++d) {
-                        pl16swap(a[d], b[d]);
-                        pl32swap(a[d], b[d]);
-                    }
-                    k.a = make_float4(__uint_as_float(a[0]), __uint_as_float(a[1]), __uint_as_float(a[2]), __uint_as_float(a[3]));
-                    k.b = make_float4(__uint_as_float(b[0]), __uint_as_float(b[1]), __uint_as_float(b[2]), __uint_as_float(b[3]));
+                for (int d = 0; d < 4; ++d) {
+                    pl16swap(a[d], b[d]);
+                    pl32swap(a[d], b[d]);
                 }
+                k.a = make_float4(__uint_as_float(a[0]), __uint_as_float(a[1]), __uint_as_float(a[2]), __uint_as_float(a[3]));
+                k.b = make_float4(__uint_as_float(b[0]), __uint_as_float(b[1]), __uint_as_float(b[2]), __uint_as_float(b[3]));
+            };
+            if constexpr (DKEEP && PKW == 2) {
+#pragma unroll
+                for (int s = 0; s < NPK; ++s) to_quads(reinterpret_cast<RawF &>(pres[j][2 * s]));
+            }
+            if constexpr (KEEPF) {
+#pragma unroll
+                for (int s = 0; s < KS1; ++s) to_quads(reinterpret_cast<RawF &>(kx[j][s]));
             }
             auto out3 = [&](int r, const f32x4 &acc) {
                 const int ch = r * 16 + kq * 4;
-                return act(bias_in_acc(NR3, 1) ? f4(acc) : add4(f4(acc), ld4f(cb3 + ch)), cs3 + ch);
+                float4 v = f4(acc);
+                if constexpr (F32) {
+                    if (scl) v = mul4(v, o3m);
+                }
+                return act(v, cs3 + ch);
             };
 #pragma unroll
             for (int t = 0; t < RQ3; ++t) {
@@ -1136,12 +1222,13 @@ __global__ void __launch_bounds__((BShape<C, V>::NW * 64), (sizeof(T) == 2 ? BSh
                     const RawF &k = reinterpret_cast<const RawF &>(kx[j][t >> 1]);
                     rc = __builtin_bit_cast(uint4, (t & 1) ? k.b : k.a);
                 } else if constexpr (KEEP) rc = reinterpret_cast<const RawH &>(kx[j][t]).v;
+                else if constexpr (DKEEP && PKW == 2) rc = t < 2 * NPK ? pres[j][t < 2 * NPK ? t : 0] : make_uint4(0u, 0u, 0u, 0u);
                 else if constexpr (DKEEP) rc = t < NPK ? pres[j][t < NPK ? t : 0] : make_uint4(0u, 0u, 0u, 0u);
                 else rc = res[j % RP][t];
                 if constexpr (SWAP) {
                     const int r0 = 2 * t, r1 = 2 * t + 1;
-                    f32x4 acc0 = bias_in_acc(NR3, 1) ? bias4(cb3 + r0 * 16 + kq * 4) : (f32x4){0.f, 0.f, 0.f, 0.f};
-                    f32x4 acc1 = bias_in_acc(NR3, 1) ? bias4(cb3 + r1 * 16 + kq * 4) : (f32x4){0.f, 0.f, 0.f, 0.f};
+                    f32x4 acc0 = bias4(cb3 + r0 * 16 + kq * 4);   // (2-byte storage: no range scaling)
+                    f32x4 acc1 = bias4(cb3 + r1 * 16 + kq * 4);
                     WRaw w0, w1;
                     ld8(w0, w3 + (r0 * 16 + col) * K3S + kq * 8);
                     ld8(w1, w3 + (r1 * 16 + col) * K3S + kq * 8);
@@ -1171,7 +1258,7 @@ __global__ void __launch_bounds__((BShape<C, V>::NW * 64), (sizeof(T) == 2 ? BSh
                     bst16o<OAUX>(rob, off, make_uint4(x0, x1, y0, y1));
                 } else {
                     const int r = t;
-                    f32x4 acc = bias_in_acc(NR3, 1) ? bias4(cb3 + r * 16 + kq * 4) : (f32x4){0.f, 0.f, 0.f, 0.f};
+                    f32x4 acc = bias_m(cb3 + r * 16 + kq * 4, b3m);
                     WRaw wf;
                     ld8(wf, w3 + (r * 16 + col) * K3S + kq * 8);
                     mma(acc, wf, tf[j]);
@@ -1180,6 +1267,7 @@ __global__ void __launch_bounds__((BShape<C, V>::NW * 64), (sizeof(T) == 2 ? BSh
                         bst8o<OAUX>(rob, off, pack4<T>(v));
                     } else {
                         float4 v = act(add4(out3(r, acc), __builtin_bit_cast(float4, rc)), cso + r * 16 + kq * 4);
+                        if constexpr (F32) rng_acc4(amo, v);
                         bst16o<OAUX>(rob, off, __builtin_bit_cast(uint4, v));
                     }
                 }
@@ -1189,6 +1277,7 @@ __global__ void __launch_bounds__((BShape<C, V>::NW * 64), (sizeof(T) == 2 ? BSh
         }
         STAMP(6);
     }
+    if constexpr (F32) rng_commit(amo, a.rg.amax_out);
     STAMP_ENTRY(1);
 }
 
@@ -1250,33 +1339,13 @@ static const void *bneck_fun(int prec, int C, bool asym, int v, bool tr, int cin
                                                             : kfun<float>(C, asym, v, tr);
 }
 
-// dynamic LDS above 64 KB must be allowed per kernel (once)
-static hipError_t allow_lds(const void *f) {
-    static const void *done[64] = {};
-    for (const void *d : done)
-        if (d == f) return hipSuccess;
-    hipError_t e = hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
-    if (e != hipSuccess) return e;
-    for (const void *&d : done)
-        if (!d) { d = f; break; }
-    return hipSuccess;
-}
-
 int bneck_slots_per_cu(int prec, int C, bool asym, int v, bool tr, int cin) {
-    // cached per form (launch_bneck asks on every launch)
-    static int cache[3][3][2][8][2][3];
-    const int pi = prec == PREC_BF16 ? 0 : prec == PREC_F16 ? 1 : 2, ci = C == 128 ? 0 : C == 64 ? 1 : 2;
-    const int ii = cin == 0 ? 0 : cin == 16 ? 1 : 2;
-    int &slot = cache[pi][ci][asym][v & 7][tr][ii];
-    if (slot > 0) return slot;
+    // (cached per device and form: launch_bneck asks on every launch; bugseg_runtime.cpp occupancy_per_cu)
     const void *f = bneck_fun(prec, C, asym, v, tr, cin);
     int th, tw, nw;
     bneck_shape(C, v, th, tw, nw, nullptr);
-    if (!f || allow_lds(f) != hipSuccess) return 0;
-    int n = 0;
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, f, nw * 64, bneck_lds_bytes(prec, C, asym, v, cin)) != hipSuccess)
-        return 0;
-    return slot = n;
+    if (!f || allow_dynamic_lds(f) != hipSuccess) return 0;
+    return occupancy_per_cu(f, nw * 64, bneck_lds_bytes(prec, C, asym, v, cin));
 }
 
 hipError_t launch_bneck(int prec, int C, bool asym, int v, const BneckArgs &a, hipStream_t s, int cin) {
@@ -1286,18 +1355,13 @@ hipError_t launch_bneck(int prec, int C, bool asym, int v, const BneckArgs &a, h
     bneck_shape(C, v, th, tw, nw, nullptr);
     const size_t lds = bneck_lds_bytes(prec, C, asym, v, cin);
     if (lds > 64 * 1024) {
-        hipError_t e = allow_lds(f);
+        hipError_t e = allow_dynamic_lds(f);
         if (e != hipSuccess) return e;
     }
     // grid: one round of resident workgroups (each walks ntiles / grid tiles, staging its weights
     // once), or the earlier fixed cap of 2048 (BUGSEG_BNECK_GRID=cap: A/B knob, 0 = resident slots)
     // (read per launch, so a test can force multi-tile walks at any shape)
-    static int n_cu = -1;
-    if (n_cu < 0) {
-        int dev = 0;
-        if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&n_cu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
-            n_cu = 0;
-    }
+    const int n_cu = device_cus();
     const char *ge = std::getenv("BUGSEG_BNECK_GRID");
     const int grid_cap = ge ? std::atoi(ge) : 0;
     int cap = grid_cap;

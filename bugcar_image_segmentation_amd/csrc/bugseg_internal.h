@@ -26,6 +26,28 @@ enum Prec { PREC_F32 = 0, PREC_BF16 = 1, PREC_F16 = 2 };
 // bytes per stored element: fp32 parity mode 4; bf16 / f16 storage modes 2
 inline constexpr int prec_es(int prec) { return prec == PREC_F32 ? 4 : 2; }
 
+// ---- fp32 mode: range scaling of the split-f16 operands (round 5; mfma_common.h "range scaling").
+// The fp32 mode's products take f16 hi / lo parts (|v| < 65504, full precision for |v| >= 2^-3), so
+// every operand is brought into that window by an exact power of two: each stored tensor's max |v| is
+// measured by the launch that writes it (atomic max into RNG_SLOTS words, spread over the slots by
+// workgroup), the launch that reads it derives its exponent from it, the tensors that never leave a
+// fused launch take theirs from a rigorous bound (|t_i| <= n_i |t_(i-1)| + c_i from the weights' row
+// sums), and the weights carry a static exponent (packed w = w * 2^sw). The epilogues multiply the
+// accumulators back. Exact in f32 (powers of two); when every exponent is 0 — activations and
+// weights inside the window, the common case — no multiply runs at all (a wave-uniform branch).
+constexpr int RNG_SLOTS = 64;
+struct RangeArgs {
+    const float *amax_in;   // RNG_SLOTS words holding max |x| of the launch's input (nullptr: amax_static)
+    float *amax_out;        // RNG_SLOTS words the launch max-accumulates max |out| into (nullptr: not measured)
+    float amax_static;      // max |x| when amax_in is nullptr (the BGR input: the normalisation table's max)
+    int sw[4];              // weight exponents of the launch's matrices, in launch order
+    float n[3], c[3];       // internal tensors: |t_i| <= n[i] * |t_(i-1)| + c[i], t_(-1) = the input
+    int off;                // BUGSEG_F32_RANGE=0 (A/B, negative control of tests/test_gpu_range.py): no scaling
+};
+// weight exponent of a matrix whose largest |w| is m (the measured-tensor window of the kernels)
+int range_weight_exp(double m);
+hipError_t launch_amax(const float *x, size_t n, float *slots, hipStream_t s);
+
 struct ConvArgs {
     const void *in;      // NHWC input (B, Hin, Win, CinS)
     int B, Hin, Win, CinS;
@@ -63,10 +85,19 @@ struct ConvArgs {
     uint32_t in_bytes, out_bytes, res_bytes, idx_bytes;
     int cpr_sh;          // log2(outC / (16 B / elem)): 16-B chunks per output pixel (power of two)
     int slopes_le1;      // every slope1 / slope2 <= 1: PReLU as max(v, s*v)
+    RangeArgs rg;        // fp32 mode: the input's measured range, sw[0] = the weights' exponent
 };
 
 // magic number for fdiv (mfma_common.h): divisor d >= 1
 void fastdiv(uint32_t d, uint32_t &m, int &s);
+
+// Launch-path caches (bugseg_runtime.cpp), keyed by the current device and guarded by a mutex (several
+// host threads, several devices per process): CUs of the device; resident workgroups per CU of kernel f
+// at (threads, dynamic LDS) from the occupancy API (0 on failure); the >64 KB dynamic-LDS opt-in, once
+// per (device, kernel).
+int device_cus();
+int occupancy_per_cu(const void *f, int threads, size_t lds);
+hipError_t allow_dynamic_lds(const void *f);
 
 // Launch one convolution. nr = Npad / 16 in {1, 2, 4, 8}. Returns hipSuccess or the launch error.
 hipError_t launch_conv(int prec, int nr, int epi, const ConvArgs &a, hipStream_t s);
@@ -105,6 +136,7 @@ struct BneckArgs {
     uint8_t *idx_out;
     int idxCS;
     uint32_t xin_bytes, pool_bytes, idx_bytes;
+    RangeArgs rg;        // fp32 mode: sw = {w1, w2, w2b, w3}; n / c: t0, t1 (asym: t1a), t1 (asym)
 };
 // tile-shape variants of the fused kernel for C channels: 0 .. bneck_variants(C) - 1
 int bneck_variants(int C);
@@ -128,6 +160,7 @@ struct UpArgs {
     const float *b1, *s1, *b2, *s2, *b3, *s3, *s_out;
     uint32_t x_bytes, idx_bytes, out_bytes;
     int slopes_le1;
+    RangeArgs rg;             // fp32 mode: sw = {pair, tconv, expansion}; n / c: e1 output, tconv output
 };
 bool up_supported(int cin, int it, int cout);
 hipError_t launch_up(int prec, int cin, int it, int cout, const UpArgs &a, hipStream_t s);

@@ -18,11 +18,64 @@
 #include <vector>
 #include <algorithm>
 #include <cstdlib>
+#include <mutex>
 
 #include "bugseg_internal.h"
 #include "../../include/bugseg.h"
 
 using namespace bugseg;
+
+// ---- launch-path caches (bugseg_internal.h)
+namespace {
+std::mutex g_occ_mu;
+struct OccKey { int dev; const void *f; int threads; size_t lds; int val; };
+std::vector<OccKey> g_occ;          // val: resident workgroups per CU; f == nullptr: the CU count
+int current_device() {
+    int d = 0;
+    return hipGetDevice(&d) == hipSuccess ? d : 0;
+}
+}  // namespace
+int bugseg::device_cus() {
+    const int dev = current_device();
+    std::lock_guard<std::mutex> lk(g_occ_mu);
+    for (const OccKey &k : g_occ)
+        if (k.dev == dev && !k.f) return k.val;
+    int n = 0;
+    if (hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || n <= 0) n = 256;
+    g_occ.push_back({dev, nullptr, 0, 0, n});
+    return n;
+}
+int bugseg::occupancy_per_cu(const void *f, int threads, size_t lds) {
+    const int dev = current_device();
+    std::lock_guard<std::mutex> lk(g_occ_mu);
+    for (const OccKey &k : g_occ)
+        if (k.dev == dev && k.f == f && k.threads == threads && k.lds == lds) return k.val;
+    int n = 0;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, f, threads, lds) != hipSuccess || n < 0) n = 0;
+    g_occ.push_back({dev, f, threads, lds, n});
+    return n;
+}
+hipError_t bugseg::allow_dynamic_lds(const void *f) {
+    const int dev = current_device();
+    std::lock_guard<std::mutex> lk(g_occ_mu);
+    for (const OccKey &k : g_occ)
+        if (k.dev == dev && k.f == f && k.threads == -1) return hipSuccess;
+    hipError_t e = hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+    if (e == hipSuccess) g_occ.push_back({dev, f, -1, 0, 1});
+    return e;
+}
+
+// the weights' exponent for the fp32 mode's split-f16 products: 0 while the largest |w| lies in the
+// kernels' measured window [2^-2, 2^15) (mfma_common.h rng_exp_meas), else the exponent that brings it
+// to [2^14, 2^15), clamped as the kernels clamp
+int bugseg::range_weight_exp(double m) {
+    if (!(m > 0) || !std::isfinite(m)) return 0;
+    int e = 0;
+    (void)std::frexp(m, &e);
+    const int l = e - 1;
+    if (l >= -2 && l < 15) return 0;
+    return std::max(-40, std::min(40, 14 - l));   // (mfma_common.h RNG_EMAX)
+}
 
 namespace {
 
@@ -53,6 +106,10 @@ struct Packed {
     int phases = 1;
     double macs_per_px = 0;   // MACs per GEMM pixel (flop accounting)
     size_t o_w = 0, o_gtab = 0, o_bias = 0, o_s1 = 0, o_s2 = 0, o_ps = 0;
+    // fp32 mode range scaling (bugseg_internal.h RangeArgs): the weights' exponent (packed w = w * 2^sw)
+    // and per packed row the bound terms of its activated output: sum |w|, |bias|, max(1, |slope|)
+    int sw = 0;
+    std::vector<float> rabs, rbias, rslope;
 };
 
 struct Op {
@@ -76,6 +133,8 @@ struct Op {
 struct Plan {
     int B = 0, H = 0, W = 0;
     std::vector<Op> ops;
+    float *words = nullptr;  // fp32 mode: RNG_SLOTS range words per measured tensor (block 0: the engine input)
+    size_t words_bytes = 0;
     void *arena = nullptr;
     size_t arena_bytes = 0;
     bool pinned = false;     // a forward on this arena was captured into a graph: never freed before destroy
@@ -96,6 +155,8 @@ struct bugseg_ctx {
     int prec = PREC_F32;
     float naff[6] = {};                            // exact affine form of the normalisation table (find_affine)
     bool naff_on = false;
+    float norm_amax = 0.f;                         // max |table| (the BGR input's range, fp32 range scaling)
+    bool range_off = false;                        // BUGSEG_F32_RANGE=0 at load_weights: no fp32 range scaling (A/B)
     std::string err;
     bool loaded = false;
     int ncls = 0;
@@ -296,7 +357,7 @@ struct Packer {
         std::memcpy(buf.data() + off, d, n);
         return off;
     }
-    size_t push_w(const std::vector<double> &w) {
+    size_t push_w(const std::vector<double> &w, int sw = 0) {
         if (prec == PREC_F16) {
             std::vector<uint16_t> h(w.size());
             for (size_t i = 0; i < w.size(); ++i) h[i] = f32_to_f16((float)w[i]);
@@ -315,11 +376,15 @@ struct Packer {
         }
         // fp32 parity mode: the split-f16 operand of mfma_common.h (RawS): per 8 consecutive k of a
         // row (rows are whole 32-k steps), the 8 hi parts f16(w) then the 8 lo parts f16(w - hi),
-        // w rounded to f32 first (the f32 weight the exact-product path used)
-        std::vector<uint16_t> h(w.size() * 2);
+        // w * 2^sw rounded to f32 first (the f32 weight the exact-product path used, times the power of
+        // two that brings the matrix into the split's window: range_weight_exp)
+        // (rows are whole 32-k steps, so w.size() is a multiple of 8; a partial last group would be
+        // zero-padded to 8, never written past the buffer)
+        const double scale = std::ldexp(1.0, sw);
+        std::vector<uint16_t> h((w.size() + 7) / 8 * 16, 0);
         for (size_t g = 0; g < w.size(); g += 8)
             for (size_t i = 0; i < 8 && g + i < w.size(); ++i) {
-                const float f = (float)w[g + i];
+                const float f = (float)(w[g + i] * scale);
                 const uint16_t hi = f32_to_f16(f);
                 h[2 * g + i] = hi;
                 h[2 * g + 8 + i] = f32_to_f16(f - f16_to_f32(hi));   // exact difference in f32
@@ -340,6 +405,41 @@ void bn_fold(const UnitDesc &u, std::vector<double> &scale, std::vector<double> 
 }
 
 int gentry(int dy, int dx, int coff) { return (dy & 0xff) | ((dx & 0xff) << 8) | (coff << 16); }
+
+// fp32 mode range scaling: the weight exponent of the packed matrix and its rows' bound terms
+// (bugseg_internal.h RangeArgs). w: the folded [Npad][Kpad] matrix; bias / slope per row.
+void range_stats(Packed &p, int prec, const std::vector<double> &w, const std::vector<float> &bias,
+                 const std::vector<float> &slope) {
+    const char *off = std::getenv("BUGSEG_F32_RANGE");          // (read at pack time: load_weights)
+    p.sw = 0;
+    p.rabs.assign(p.Npad, 0.f);
+    p.rbias.assign(p.Npad, 0.f);
+    p.rslope.assign(p.Npad, 1.f);
+    double mx = 0;
+    for (int r = 0; r < p.Npad; ++r) {
+        double sa = 0;
+        for (int k = 0; k < p.Kpad; ++k) {
+            const double v = std::fabs(w[(size_t)r * p.Kpad + k]);
+            sa += v;
+            mx = std::max(mx, v);
+        }
+        p.rabs[r] = (float)sa;
+        p.rbias[r] = std::fabs(bias[r]);
+        p.rslope[r] = std::max(1.f, std::fabs(slope[r]));
+    }
+    if (prec == PREC_F32 && !(off && *off == '0')) p.sw = range_weight_exp(mx);
+}
+// |act(W x + b)| <= n |x| + c over the rows [r0, r1) of a packed matrix (a 1e-4 margin for the f32
+// arithmetic the kernels evaluate the bound in)
+void row_bound(const Packed &p, int r0, int r1, float &n, float &c) {
+    n = c = 0.f;
+    for (int r = r0; r < r1 && r < (int)p.rabs.size(); ++r) {
+        n = std::max(n, p.rabs[r] * p.rslope[r]);
+        c = std::max(c, p.rbias[r] * p.rslope[r]);
+    }
+    n *= 1.0001f;
+    c *= 1.0001f;
+}
 
 // Ordinary convolution (OIHW weights) on an NHWC input with CinS storage channels.
 Packed pack_conv(Packer &pk, const UnitDesc &u, int CinS, const std::vector<float> *slope2) {
@@ -377,7 +477,8 @@ Packed pack_conv(Packer &pk, const UnitDesc &u, int CinS, const std::vector<floa
         s1[c] = u.slope[c];
         if (slope2) s2[c] = (*slope2)[c];
     }
-    p.o_w = pk.push_w(w);
+    range_stats(p, pk.prec, w, bias, s1);
+    p.o_w = pk.push_w(w, p.sw);
     p.o_gtab = pk.push(gt.data(), gt.size() * 4);
     p.o_bias = pk.push_f(bias);
     p.o_s1 = pk.push_f(s1);
@@ -459,7 +560,8 @@ Packed pack_tconv(Packer &pk, const UnitDesc &u, int CinS, std::string &why, int
             bias[ph * p.coutP + c] = (float)shift[c];
             s1[ph * p.coutP + c] = u.slope[c];
         }
-    p.o_w = pk.push_w(w);
+    range_stats(p, pk.prec, w, bias, s1);
+    p.o_w = pk.push_w(w, p.sw);
     p.o_gtab = pk.push(gt.data(), gt.size() * 4);
     p.o_bias = pk.push_f(bias);
     p.o_s1 = pk.push_f(s1);
@@ -738,6 +840,29 @@ struct Walker {
     unsigned char *X[2] = {nullptr, nullptr}, *T[3] = {nullptr, nullptr, nullptr}, *Mb = nullptr;
     std::vector<unsigned char *> idx;
     std::vector<Op> ops;
+    // fp32 mode range scaling (bugseg_internal.h RangeArgs): RNG_SLOTS words per measured tensor, block 0
+    // for the engine input; which block holds the range of each buffer's current contents
+    float *words = nullptr;
+    int nwords = 1;
+    std::vector<std::pair<const void *, float *>> wmap;
+    static int max_words(size_t nblocks) { return (int)(4 * nblocks + 4); }
+    float *take_words() {
+        float *w = words && es == 4 ? words + (size_t)nwords * RNG_SLOTS : nullptr;
+        ++nwords;
+        return w;
+    }
+    void wrote(const void *buf, float *w) {
+        for (auto &e : wmap)
+            if (e.first == buf) { e.second = w; return; }
+        wmap.push_back({buf, w});
+    }
+    float *words_of(const void *buf) const {
+        if (es != 4) return nullptr;
+        if (!buf) return words;                          // the engine input
+        for (const auto &e : wmap)
+            if (e.first == buf) return e.second;
+        return nullptr;
+    }
 
     size_t tbytes(const Shape &s) const { return (size_t)B * s.H * s.W * s.C * es; }
 
@@ -755,6 +880,14 @@ struct Walker {
         a.slopes_le1 = 1;
         for (int c = 0; c < p.Npad; ++c)
             if (!(s1[c] <= 1.f) || !(s2[c] <= 1.f)) a.slopes_le1 = 0;
+        // fp32 range scaling: the input's measured range, the weights' exponent, this output measured
+        a.rg.amax_in = words_of(in);
+        a.rg.sw[0] = p.sw;
+        a.rg.off = ctx->range_off;
+        if (out && epi != EPI_CLASSES) {
+            a.rg.amax_out = take_words();
+            wrote(out, a.rg.amax_out);
+        }
         op.a = a; op.nr = p.nr; op.epi = epi;
         op.flops = 2.0 * p.macs_per_px * a.M;
         op.bytes = (double)B * si.H * si.W * si.C * es + (double)p.Npad * p.Kpad * es +
@@ -770,6 +903,8 @@ struct Walker {
         const unsigned char *curp = nullptr;    // engine input, patched per call
         int xi = 0;
         ops.clear();
+        nwords = 1;
+        wmap.clear();
         for (size_t bi = 0; bi < nb; ++bi) {
             const BlockDesc &b = ctx->blocks[bi];
             const std::vector<int> &ids = ctx->block_convs[bi];
@@ -831,6 +966,13 @@ struct Walker {
                         q.pool_bytes = (uint32_t)std::min<size_t>(tbytes(sp), 0x7fffffff);
                         q.idx_out = idx[bi]; q.idxCS = idxCS;
                         q.idx_bytes = (uint32_t)std::min<size_t>((size_t)B * so.H * so.W * idxCS, 0x7fffffff);
+                        q.rg.amax_in = words_of(curp);
+                        q.rg.off = ctx->range_off;
+                        q.rg.sw[0] = p1.sw; q.rg.sw[1] = p2.sw; q.rg.sw[2] = p2.sw; q.rg.sw[3] = p3.sw;
+                        row_bound(p1, 0, p1.cout, q.rg.n[0], q.rg.c[0]);
+                        row_bound(p2, 0, p2.cout, q.rg.n[1], q.rg.c[1]);
+                        q.rg.amax_out = take_words();
+                        wrote(dst, q.rg.amax_out);
                         const double px = (double)B * so.H * so.W;
                         double wb = 0, fl = 0;
                         for (int i = 0; i < 3; ++i) { wb += (double)P(i).Npad * P(i).Kpad * es; fl += 2.0 * P(i).macs_per_px * px; }
@@ -886,6 +1028,14 @@ struct Walker {
                         q.w2b = dw + p2b.o_w; q.b2b = (const float *)(dw + p2b.o_bias); q.s2b = (const float *)(dw + p2b.o_s1);
                         q.w3 = dw + p3.o_w; q.b3 = (const float *)(dw + p3.o_bias); q.s3 = (const float *)(dw + p3.o_s1);
                         q.s_out = (const float *)(dw + p3.o_s2);
+                        q.rg.amax_in = words_of(curp);
+                        q.rg.off = ctx->range_off;
+                        q.rg.sw[0] = p1.sw; q.rg.sw[1] = p2.sw; q.rg.sw[2] = p2b.sw; q.rg.sw[3] = p3.sw;
+                        row_bound(p1, 0, p1.cout, q.rg.n[0], q.rg.c[0]);
+                        row_bound(p2, 0, p2.cout, q.rg.n[1], q.rg.c[1]);
+                        row_bound(p2b, 0, p2b.cout, q.rg.n[2], q.rg.c[2]);
+                        q.rg.amax_out = take_words();
+                        wrote(dst, q.rg.amax_out);
                         q.slopes_le1 = 1;
                         const std::pair<size_t, int> slopes[] = {{p1.o_s1, p1.Npad}, {p2.o_s1, p2.Npad}, {p2b.o_s1, p2b.Npad},
                                                                  {p3.o_s1, p3.Npad}, {p3.o_s2, p3.Npad}};
@@ -959,6 +1109,13 @@ struct Walker {
                         q.w2 = dw + p2.o_w; q.b2 = (const float *)(dw + p2.o_bias); q.s2 = (const float *)(dw + p2.o_s1);
                         q.w3 = dw + p3.o_w; q.b3 = (const float *)(dw + p3.o_bias); q.s3 = (const float *)(dw + p3.o_s1);
                         q.s_out = (const float *)(dw + p3.o_s2);
+                        q.rg.amax_in = words_of(curp);
+                        q.rg.off = ctx->range_off;
+                        q.rg.sw[0] = p1.sw; q.rg.sw[1] = p2.sw; q.rg.sw[2] = p3.sw;
+                        row_bound(p1, cout_b, cout_b + it_b, q.rg.n[0], q.rg.c[0]);   // the pair's e1 rows
+                        row_bound(p2, 0, p2.Npad, q.rg.n[1], q.rg.c[1]);
+                        q.rg.amax_out = take_words();
+                        wrote(dst, q.rg.amax_out);
                         q.x_bytes = (uint32_t)std::min<size_t>((size_t)B * cur.H * cur.W * cur.C * es, 0x7fffffff);
                         q.idx_bytes = (uint32_t)std::min<size_t>((size_t)B * cur.H * cur.W * q.idxCS, 0x7fffffff);
                         q.out_bytes = (uint32_t)std::min<size_t>((size_t)B * so.H * so.W * so.C * es, 0x7fffffff);
@@ -1063,6 +1220,8 @@ bool build_plan(bugseg_ctx *ctx, int B, int H, int W, std::string &why, void *st
     auto al = [](size_t v) { return (v + 4095) / 4096 * 4096; };
     size_t total = 2 * al(w.szX) + 3 * al(w.szT) + al(w.szM);
     for (size_t s : w.szIdx) total += al(s);
+    const size_t words_bytes = ctx->prec == PREC_F32 ? (size_t)Walker::max_words(ctx->blocks.size()) * RNG_SLOTS * 4 : 0;
+    total += al(words_bytes);
     const bool cap = stream_capturing(stream);
     RelaxCapture relax;                 // the first forward at a shape may itself be captured
     if (pl.arena) {
@@ -1079,7 +1238,10 @@ bool build_plan(bugseg_ctx *ctx, int B, int H, int W, std::string &why, void *st
     w.Mb = p; p += al(w.szM);
     w.idx.assign(w.szIdx.size(), nullptr);
     for (size_t i = 0; i < w.szIdx.size(); ++i) if (w.szIdx[i]) { w.idx[i] = p; p += al(w.szIdx[i]); }
+    w.words = words_bytes ? (float *)p : nullptr;
+    p += al(words_bytes);
     if (!w.run(true, why)) return false;
+    if (words_bytes && w.nwords > Walker::max_words(ctx->blocks.size())) { why = "range words: plan too long"; return false; }
     for (Op &op : w.ops) {
         if (op.kind == 1) {
             const double bytes = (double)op.bn.B * op.bn.H * op.bn.W * op.bn_c * w.es;
@@ -1091,6 +1253,8 @@ bool build_plan(bugseg_ctx *ctx, int B, int H, int W, std::string &why, void *st
         if (!finish_conv_args(op.a, op.epi, w.es)) { why = "batch too large for 32-bit tensor offsets"; return false; }
     }
     pl.ops = std::move(w.ops);
+    pl.words = w.words;
+    pl.words_bytes = words_bytes;
     pl.B = B; pl.H = H; pl.W = W;
     pl.arena_bytes = total;
     return true;
@@ -1145,6 +1309,7 @@ int bugseg_create(int device, int precision, bugseg_ctx **out) {
         for (int v = 0; v < 256; ++v) {
             const double x = ((double)v / 256.0 - mean[ch]) / stdv[ch];
             std::memcpy(tab + 32 + (ch * 256 + v) * 8, &x, 8);
+            c->norm_amax = std::max(c->norm_amax, (float)std::fabs(x) * 1.0001f);
         }
 
     {
@@ -1230,6 +1395,10 @@ int bugseg_load_weights(bugseg_ctx *ctx, const void *blob, size_t bytes) {
     ctx->blocks = std::move(blocks);
     ctx->ncls = ncls;
     ctx->loaded = false;
+    {
+        const char *off = std::getenv("BUGSEG_F32_RANGE");
+        ctx->range_off = off && *off == '0';
+    }
     if (!pack_all(ctx, why)) return fail(ctx, BUGSEG_EFORMAT, "weight blob: " + why);
     (void)hipDeviceSynchronize();
     if (ctx->dev_w) {
@@ -1357,6 +1526,10 @@ static int enet_forward(bugseg_ctx *ctx, const void *in, bool bgr, int B, int H,
     first.a.nlut = bgr ? (const double *)((const unsigned char *)ctx->dev_luts + 32) : nullptr;
     first.a.naff_on = bgr && ctx->naff_on && !std::getenv("BUGSEG_INIT_TABLE");
     std::memcpy(first.a.naff, ctx->naff, sizeof(ctx->naff));
+    // fp32 range scaling: the BGR input's range is the normalisation table's (static); an engine input
+    // the caller supplied is measured (block 0 of the range words)
+    first.a.rg.amax_in = bgr ? nullptr : pl.words;
+    first.a.rg.amax_static = bgr ? ctx->norm_amax : 0.f;
     ConvArgs &last = pl.ops.back().a;
     last.cls_out = nullptr; last.logits_out = nullptr; last.lut = nullptr; last.lut_kind = 0;
     const uint8_t *luts = (const uint8_t *)ctx->dev_luts;
@@ -1369,6 +1542,12 @@ static int enet_forward(bugseg_ctx *ctx, const void *in, bool bgr, int B, int H,
     const int nops = (int)pl.ops.size();
     if (last_op < 0 || last_op > nops) last_op = nops;
     if (first_op < 0 || first_op > last_op) return fail(ctx, BUGSEG_EINVAL, "bad op range");
+    if (pl.words && first_op == 0) {
+        // every launch max-accumulates its output's range: cleared once per forward (a memset node when captured)
+        hipError_t e = hipMemsetAsync(pl.words, 0, pl.words_bytes, (hipStream_t)stream);
+        if (e == hipSuccess && !bgr) e = launch_amax((const float *)in, (size_t)B * H * W * 8, pl.words, (hipStream_t)stream);
+        if (e != hipSuccess) return fail(ctx, BUGSEG_EHIP, std::string("range words: ") + hipGetErrorString(e));
+    }
     for (int i = first_op; i < last_op; ++i) {
         const Op &op = pl.ops[(size_t)i];
         hipError_t e = op.kind == 1 ? launch_bneck(ctx->prec, op.bn_c, op.bn_asym, op.bn_var, op.bn, (hipStream_t)stream, op.bn_cin)
@@ -1716,6 +1895,16 @@ int bugseg_debug_parse_pack(const void *blob, size_t bytes, int precision, int *
     if (!pack_all(&c, why)) return fail(nullptr, BUGSEG_EFORMAT, "weight blob: " + why);
     if (ncls) *ncls = c.ncls;
     return BUGSEG_OK;
+}
+
+int bugseg_debug_ctx_info(const bugseg_ctx *ctx, int what, int arg) {
+    if (!ctx) return -1;
+    switch (what) {
+    case 0: return ctx->naff_on ? 1 : 0;
+    case 1: return ctx->range_off ? 1 : 0;
+    case 2: return arg >= 0 && arg < (int)ctx->packed.size() ? ctx->packed[(size_t)arg].sw : -1000;
+    default: return -1;
+    }
 }
 
 int bugseg_debug_polar_tables(int w, int h, int variant, int32_t *fmap, size_t fmap_n, int32_t *imap, size_t imap_n,

@@ -132,6 +132,18 @@ __global__ void __launch_bounds__(256, sizeof(T) == 2 ? 4 : 1) cls_kernel(const 
     constexpr bool BREG = CLS_BIAS_REG && !LOGITS && sizeof(T) == 2;
     f32x16 bvec;
     if constexpr (BREG) bvec = ldbias(0);
+    // fp32 mode range scaling (bugseg_internal.h RangeArgs): the input measured by its producer, the
+    // weights' exponent; the accumulators are multiplied back (scl false: nothing to do)
+    constexpr bool F32 = ES == 4;
+    bool scl = false;
+    float xm = 1.f, bm = 1.f, om = 1.f;
+    if constexpr (F32) {
+        if (!a.rg.off) {
+            const int sx = rng_exp_meas(rng_read(a.rg)), e = sx + a.rg.sw[0];
+            scl = (sx | e) != 0;
+            xm = rng_pow2(sx); bm = rng_pow2(e); om = rng_pow2(-e);
+        }
+    }
     const auto rin = mkbuf(a.in, a.in_bytes);
     const int HWg = a.Hg * a.Wg;
     const size_t plane = (size_t)a.Hout * a.Wout;
@@ -208,15 +220,34 @@ __global__ void __launch_bounds__(256, sizeof(T) == 2 ? 4 : 1) cls_kernel(const 
         // (models.py:55): the maximum (v_max ignores NaN), then its first index; no class equal to the
         // maximum (all NaN) -> 0; all -inf -> 0 (class 0 equals the maximum). Both blocks' MFMAs go
         // first, then the two argmax scans interleaved
+        auto taps = [&](int b, f32x16 &acc, auto sc) {
+            auto tap = [&](int s) {
+                Raw xq = cur[s];
+                if constexpr (decltype(sc)::value) mul8(reinterpret_cast<RawF &>(xq), xm);
+                mma32(acc, wr[b][s], xq);
+            };
+            tap(0);
+            tap(1);
+            if (!short_blk[b]) {
+                tap(2);
+                tap(3);
+            }
+        };
         auto block = [&](int b, f32x16 &acc) {
             acc = BREG ? bvec : ldbias(b);
             if constexpr ((CLS_ABL & 1) != 0 && sizeof(T) == 2) { acc[0] += __builtin_bit_cast(float, cur[0].v.x & 1u); return; }
-            mma32(acc, wr[b][0], cur[0]);
-            mma32(acc, wr[b][1], cur[1]);
-            if (!short_blk[b]) {
-                mma32(acc, wr[b][2], cur[2]);
-                mma32(acc, wr[b][3], cur[3]);
+            bool done = false;
+            if constexpr (F32) {
+                if (scl) {
+#pragma unroll
+                    for (int c = 0; c < 16; ++c) acc[c] *= bm;
+                    taps(b, acc, std::true_type());
+#pragma unroll
+                    for (int c = 0; c < 16; ++c) acc[c] *= om;
+                    done = true;
+                }
             }
+            if (!done) taps(b, acc, std::false_type());
             if (LOGITS && q.ok) {
                 float *lo = a.logits_out + (size_t)q.n * a.ncls * plane + (size_t)(2 * q.y + b) * a.Wout + 2 * q.x + h;
 #pragma unroll
@@ -325,21 +356,10 @@ hipError_t launch_cls(int prec, const ConvArgs &a, hipStream_t s) {
     // the group-max argmax applies when the class map is the remap (a.lut) the kind names
     const int lk = a.lut && (a.lut_kind == 1 || a.lut_kind == 2) ? a.lut_kind : 0;
     const void *f = prec == PREC_BF16 ? cls_fun<__bf16>(lg, lk) : prec == PREC_F16 ? cls_fun<_Float16>(lg, lk) : cls_fun<float>(lg, lk);
-    // one round of resident workgroups (occupancy API per kernel instance, cached)
-    static const void *fs[12] = {};
-    static int caps[12] = {};
-    int cap = 0;
-    for (int i = 0; i < 12; ++i)
-        if (fs[i] == f) cap = caps[i];
-    if (!cap) {
-        int dev = 0, cus = 0, per = 0;
-        if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
-            cus = 256;
-        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, f, 256, 0) != hipSuccess || per <= 0) per = 4;
-        cap = cus * per;
-        for (int i = 0; i < 12; ++i)
-            if (!fs[i]) { fs[i] = f; caps[i] = cap; break; }
-    }
+    // one round of resident workgroups (occupancy API per kernel instance, cached per device:
+    // bugseg_runtime.cpp occupancy_per_cu)
+    const int per = occupancy_per_cu(f, 256, 0);
+    const int cap = device_cus() * (per > 0 ? per : 4);
     int g = (groups + 3) / 4;
     g = g < cap ? g : cap;
     g = (g + 7) & ~7;

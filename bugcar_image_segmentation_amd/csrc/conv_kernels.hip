@@ -106,6 +106,19 @@ __global__ void __launch_bounds__(256, sizeof(T) == 2 ? (NR == 8 ? 3 : 4) : 1) c
     auto act2 = [&](float4 v, int c) { return fast ? prelu4m(v, ld4f(cs2 + c)) : prelu4(v, ld4f(cs2 + c)); };
 
     const int HWg = a.Hg * a.Wg;
+    // fp32 mode range scaling (bugseg_internal.h RangeArgs): the input measured by its producer, the
+    // weights' exponent sw[0]; the accumulators are multiplied back (scl false: nothing to do); the
+    // output's max |v| is measured for its consumer
+    constexpr bool F32 = ES == 4;
+    bool scl = false;
+    float xm = 1.f, bm = 1.f, om = 1.f, amo = 0.f;
+    if constexpr (F32) {
+        if (!a.rg.off) {
+            const int sx = rng_exp_meas(rng_read(a.rg)), e = sx + a.rg.sw[0];
+            scl = (sx | e) != 0;
+            xm = rng_pow2(sx); bm = rng_pow2(e); om = rng_pow2(-e);
+        }
+    }
     // XCD-aware tile walk: gridDim.x is a multiple of 8; group x = blockIdx%8 owns the contiguous
     // chunk [x*C, (x+1)*C) of tiles (speed only; any placement is correct).
     const int G = gridDim.x, grp = blockIdx.x & 7, slot = blockIdx.x >> 3, nslots = G >> 3;
@@ -174,6 +187,14 @@ __global__ void __launch_bounds__(256, sizeof(T) == 2 ? (NR == 8 ? 3 : 4) : 1) c
 #pragma unroll
             for (int n = 0; n < NR; ++n)
                 acc[m][n] = bia ? bias4(cbias + n * 16 + kq * 4) : (f32x4){0.f, 0.f, 0.f, 0.f};
+        if constexpr (F32) {
+            if (scl && bia) {
+#pragma unroll
+                for (int m = 0; m < MR; ++m)
+#pragma unroll
+                    for (int n = 0; n < NR; ++n) acc[m][n] = mul4(acc[m][n], bm);
+            }
+        }
 
         // KC k-steps per chunk: all their B-fragment loads are issued before the first MFMA, so a
         // tile waits on memory ceil(Ksteps / KC) times instead of Ksteps times (the tap table is padded
@@ -187,6 +208,14 @@ __global__ void __launch_bounds__(256, sizeof(T) == 2 ? (NR == 8 ? 3 : 4) : 1) c
                 for (int m = 0; m < MR; ++m) {
                     const bool ok = (unsigned)(y0[m] + g.x) < (unsigned)a.Hin && (unsigned)(x0[m] + g.y) < (unsigned)a.Win;
                     bld8(xf[kc][m], rin, ok ? boff[m] + (uint32_t)g.z : OOB);
+                }
+            }
+            if constexpr (F32) {
+                if (scl) {
+#pragma unroll
+                    for (int kc = 0; kc < KC; ++kc)
+#pragma unroll
+                        for (int m = 0; m < MR; ++m) mul8(xf[kc][m], xm);
                 }
             }
 #pragma unroll
@@ -203,6 +232,14 @@ __global__ void __launch_bounds__(256, sizeof(T) == 2 ? (NR == 8 ? 3 : 4) : 1) c
         }
 
         // ------------------------------- epilogues -------------------------------------------
+        if constexpr (F32) {
+            if (scl) {
+#pragma unroll
+                for (int m = 0; m < MR; ++m)
+#pragma unroll
+                    for (int n = 0; n < NR; ++n) acc[m][n] = mul4(acc[m][n], om);
+            }
+        }
         if constexpr (EPI == EPI_CLASSES) {
             // n fragment = output phase (a,b) (NR == 4); rows = 16 (padded) classes, 4 per lane. The
             // fragment's 64 output pixels x 16 logits go to the wave's LDS region (pixel q = n*16 +
@@ -288,6 +325,9 @@ __global__ void __launch_bounds__(256, sizeof(T) == 2 ? (NR == 8 ? 3 : 4) : 1) c
                         const int ph = phn[n], cl = cln[n] + kq * 4;
                         if (cl >= a.outC) continue;
                         v = act1(v, c);
+                        if constexpr (F32) {
+                            if (pv[m]) rng_acc4(amo, v);
+                        }
                         if (staged) {
                             st4(stg + ((ph >> 1) * 32 + 2 * col + (ph & 1)) * OSTR + cl, v);
                         } else if (pv[m]) {
@@ -338,6 +378,7 @@ __global__ void __launch_bounds__(256, sizeof(T) == 2 ? (NR == 8 ? 3 : 4) : 1) c
                         }
                         v = act2(v, c);
                     }
+                    if constexpr (F32) rng_acc4(amo, v);
                     if (staged) st4(stg + col * OSTR + c, v);
                     else st4(reinterpret_cast<T *>(a.out) + (size_t)p * a.outC + c, v);
                 }
@@ -365,6 +406,7 @@ __global__ void __launch_bounds__(256, sizeof(T) == 2 ? (NR == 8 ? 3 : 4) : 1) c
             }
         }
     }
+    if constexpr (F32) rng_commit(amo, a.rg.amax_out);
 }
 
 int conv_tile_pixels(int nr) { return 4 * (nr >= 4 ? 2 : 4) * 16; }

@@ -105,6 +105,18 @@ __global__ void __launch_bounds__(256, sizeof(T) == 2 ? INIT_OCC2 : 1) init_kern
     }
     const int c0 = kq * 4;
     const float4 b4 = ld4f(a.bias + c0), s4 = ld4f(a.slope1 + c0), p4 = ld4f(a.pscale + c0);
+    // fp32 mode range scaling (bugseg_internal.h RangeArgs): the input's range (the BGR path: the
+    // normalisation table's max, static), the weights' exponent; scl false: nothing to do
+    constexpr bool F32 = sizeof(T) == 4;
+    bool scl = false;
+    float xm = 1.f, bm = 1.f, om = 1.f, amo = 0.f;
+    if constexpr (F32) {
+        if (!a.rg.off) {
+            const int sx = rng_exp_meas(rng_read(a.rg)), e = sx + a.rg.sw[0];
+            scl = (sx | e) != 0;
+            xm = rng_pow2(sx); bm = rng_pow2(e); om = rng_pow2(-e);
+        }
+    }
     const int po = a.pool_k == 3 ? 0 : 1;                  // pool window: patch offsets po .. 2
     const uint32_t in_bytes = BGR ? (uint32_t)((size_t)a.B * a.Hin * a.Win * 3)
                                   : (uint32_t)((size_t)a.B * a.Hin * a.Win * a.CinS * sizeof(T));
@@ -302,7 +314,17 @@ __global__ void __launch_bounds__(256, sizeof(T) == 2 ? INIT_OCC2 : 1) init_kern
                 set8(xf, xv);
             }
             f32x4 acc = (f32x4){b4.x, b4.y, b4.z, b4.w};   // the MFMA adds the bias
-            mma(acc, wf, xf);
+            bool done = false;
+            if constexpr (F32) {
+                if (scl) {
+                    mul8(reinterpret_cast<RawF &>(xf), xm);
+                    acc = mul4(acc, bm);
+                    mma(acc, wf, xf);
+                    acc = mul4(acc, om);
+                    done = true;
+                }
+            }
+            if (!done) mma(acc, wf, xf);
             float4 v = f4(acc);
             // this fragment's pool maxima for pixel col live in lane col + 16 f
             float pv[4] = {0.f, 0.f, 0.f, 0.f};
@@ -319,6 +341,9 @@ __global__ void __launch_bounds__(256, sizeof(T) == 2 ? INIT_OCC2 : 1) init_kern
             v = prelu4(add4(v, make_float4(pv[0], pv[1], pv[2], pv[3])), s4);
             const int oy = ty0 + lr, ox = tx0 + lc;
             const bool ok = oy < a.Hg && ox < a.Wg && c0 < a.outC && (!(INIT_ABL & 2) || v.x == 12345.f);
+            if constexpr (F32) {
+                if (ok) rng_acc4(amo, v);
+            }
             const uint32_t off = ok ? (uint32_t)(((n * a.Hg + oy) * a.Wg + ox) * a.outC + c0) * (uint32_t)sizeof(T) : OOB;
             if constexpr (sizeof(T) == 2) {
                 bst8o<OUT_AUX_SEL(16)>(rout, off, pack4<T>(v));
@@ -327,6 +352,7 @@ __global__ void __launch_bounds__(256, sizeof(T) == 2 ? INIT_OCC2 : 1) init_kern
             }
         }
     }
+    if constexpr (F32) rng_commit(amo, a.rg.amax_out);
 }
 
 // The exact affine form of the normalisation table (bf16 / fp16 storage): candidate k of channel c is the
@@ -372,17 +398,8 @@ hipError_t launch_init(int prec, bool bgr, const ConvArgs &args, hipStream_t s) 
     // one round of resident workgroups (occupancy API per kernel instance, cached), each walking its
     // tiles with the next patch in flight
     auto resident = [](const void *f) {
-        static const void *fs[6] = {};
-        static int ns[6] = {};
-        for (int i = 0; i < 6; ++i)
-            if (fs[i] == f) return ns[i];
-        int dev = 0, cus = 0, per = 0;
-        if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
-            cus = 256;
-        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, f, 256, 0) != hipSuccess || per <= 0) per = 8;
-        for (int i = 0; i < 6; ++i)
-            if (!fs[i]) { fs[i] = f; ns[i] = cus * per; break; }
-        return cus * per;
+        const int per = occupancy_per_cu(f, 256, 0);   // (cached per device: bugseg_runtime.cpp)
+        return device_cus() * (per > 0 ? per : 8);
     };
     const void *f = prec == PREC_BF16 ? (bgr ? (const void *)init_kernel<__bf16, true> : (const void *)init_kernel<__bf16, false>)
                   : prec == PREC_F16  ? (bgr ? (const void *)init_kernel<_Float16, true> : (const void *)init_kernel<_Float16, false>)

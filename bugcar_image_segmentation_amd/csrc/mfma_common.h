@@ -2,6 +2,8 @@
 #pragma once
 #include <hip/hip_runtime.h>
 
+#include "bugseg_internal.h"
+
 namespace bugseg {
 
 // LDS hand-off between lanes of ONE wave: wait for the wave's LDS operations, keep the compiler
@@ -113,6 +115,23 @@ __device__ __forceinline__ void split_f16(const RawF &x, f16x8 &hi, f16x8 &lo) {
         hi[i] = h;
         lo[i] = (_Float16)(v[i] - (float)h);
     }
+}
+typedef float f32x2 __attribute__((ext_vector_type(2)));
+// 2 floats times a (wave-uniform) scale, one v_pk_mul_f32; opaque to the compiler, which would fuse a
+// scalar multiply feeding an f16 conversion into v_fma_mix* (those flush f16 subnormals: split_f16)
+__device__ __forceinline__ f32x2 pkmul(f32x2 v, f32x2 s) {
+    f32x2 r;
+    asm("v_pk_mul_f32 %0, %1, %2" : "=v"(r) : "v"(v), "s"(s));
+    return r;
+}
+__device__ __forceinline__ RawF scale8(const RawF &x, float m) {
+    const f32x2 s = {m, m};
+    const f32x2 a0 = pkmul((f32x2){x.a.x, x.a.y}, s), a1 = pkmul((f32x2){x.a.z, x.a.w}, s);
+    const f32x2 b0 = pkmul((f32x2){x.b.x, x.b.y}, s), b1 = pkmul((f32x2){x.b.z, x.b.w}, s);
+    RawF r;
+    r.a = make_float4(a0.x, a0.y, a1.x, a1.y);
+    r.b = make_float4(b0.x, b0.y, b1.x, b1.y);
+    return r;
 }
 __device__ __forceinline__ void mma(f32x4 &acc, const RawS &w, const RawF &x) {
     f16x8 xh, xl;
@@ -357,6 +376,69 @@ __device__ __forceinline__ void to_bop(RawF &r, float4 qa, float4 qb) {
     }
     r.a = make_float4(__uint_as_float(a[0]), __uint_as_float(a[1]), __uint_as_float(a[2]), __uint_as_float(a[3]));
     r.b = make_float4(__uint_as_float(b[0]), __uint_as_float(b[1]), __uint_as_float(b[2]), __uint_as_float(b[3]));
+}
+
+// ---- fp32 mode range scaling (round 5; bugseg_internal.h RangeArgs). Exponents are clamped to
+// [-RNG_EMAX, RNG_EMAX] (tensors of max |v| in [2^-26, 2^54] are scaled exactly into the window; beyond
+// that the split degrades gracefully) so every multiplier, a difference of two exponents plus a weight
+// exponent, stays a normal float. Everything here is wave-uniform: exponents are scalars
+// (readfirstlane) and multipliers are built from their bits on the scalar unit.
+constexpr int RNG_EMAX = 40;
+__device__ __forceinline__ int rng_clamp(int e) { return e < -RNG_EMAX ? -RNG_EMAX : e > RNG_EMAX ? RNG_EMAX : e; }
+// floor(log2 m) of a finite m > 0
+__device__ __forceinline__ int rng_log2(float m) { return __builtin_amdgcn_readfirstlane(__builtin_amdgcn_frexp_expf(m)) - 1; }
+// a measured max |v| = m: 0 while m lies in [2^-2, 2^15) (or is 0 / not finite), else the exponent
+// that brings it to [2^14, 2^15)
+__device__ __forceinline__ int rng_exp_meas(float m) {
+    if (!(m > 0.f) || !(m < INFINITY)) return 0;
+    const int l = rng_log2(m);
+    return l >= -2 && l < 15 ? 0 : rng_clamp(14 - l);
+}
+// a rigorous bound B of |t|: the preferred exponent p (the accumulator's, so no multiply) while the
+// scaled bound lies in [2^3, 2^15), else the exponent that brings B to [2^14, 2^15)
+__device__ __forceinline__ int rng_exp_bound(float B, int p) {
+    if (!(B > 0.f) || !(B < INFINITY)) return p;
+    const int l = rng_log2(B);
+    return l + p >= 3 && l + p < 15 ? p : rng_clamp(14 - l);
+}
+// 2^e for |e| <= 126, from the exponent bits (a scalar when e is)
+__device__ __forceinline__ float rng_pow2(int e) { return __int_as_float((e + 127) << 23); }
+// max |v| of a launch's input: the RNG_SLOTS words (one per lane, then a wave reduction)
+__device__ __forceinline__ float rng_read(const RangeArgs &r) {
+    if (!r.amax_in) return r.amax_static;
+    const int lane = threadIdx.x & 63;
+    float m = lane < RNG_SLOTS ? r.amax_in[lane] : 0.f;
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) m = __builtin_fmaxf(m, __shfl_xor(m, o));
+    return __int_as_float(__builtin_amdgcn_readfirstlane(__float_as_int(m)));
+}
+// m = max(m, |v|) (v_max3 with abs modifiers: NaN operands are ignored, as v_max does)
+__device__ __forceinline__ void rng_acc(float &m, float a, float b) {
+    asm("v_max3_f32 %0, %1, |%2|, |%3|" : "=v"(m) : "v"(m), "v"(a), "v"(b));
+}
+__device__ __forceinline__ void rng_acc4(float &m, float4 v) { rng_acc(m, v.x, v.y); rng_acc(m, v.z, v.w); }
+// the wave's max into the launch's output words (a global atomic max on the float bits: |v| >= 0
+// orders as unsigned; one slot per workgroup modulo RNG_SLOTS, so the atomics do not pile on one word)
+__device__ __forceinline__ void rng_commit(float m, float *slots) {
+    if (!slots) return;
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) m = __builtin_fmaxf(m, __shfl_xor(m, o));
+    if ((threadIdx.x & 63) == 0 && m > 0.f)
+        atomicMax(reinterpret_cast<unsigned int *>(slots) + (blockIdx.x & (RNG_SLOTS - 1)), __float_as_uint(m));
+}
+__device__ __forceinline__ f32x4 mul4(f32x4 v, float s) { return (f32x4){v[0] * s, v[1] * s, v[2] * s, v[3] * s}; }
+__device__ __forceinline__ float4 mul4(float4 v, float s) { return make_float4(v.x * s, v.y * s, v.z * s, v.w * s); }
+// x *= s before a split, as an opaque v_mul_f32: a plain multiply feeding an f16 conversion is fused by
+// the compiler into v_fma_mix*, which flushes f16 subnormals (see split_f16)
+__device__ __forceinline__ float mulp2(float v, float s) {
+    float r;
+    asm("v_mul_f32 %0, %1, %2" : "=v"(r) : "v"(v), "v"(s));
+    return r;
+}
+__device__ __forceinline__ float4 mulp2(float4 v, float s) { return make_float4(mulp2(v.x, s), mulp2(v.y, s), mulp2(v.z, s), mulp2(v.w, s)); }
+__device__ __forceinline__ void mul8(RawF &x, float s) {
+    x.a = mulp2(x.a, s);
+    x.b = mulp2(x.b, s);
 }
 
 __device__ __forceinline__ float4 prelu4m(float4 v, float4 s) {

@@ -7,6 +7,8 @@
 // a per-channel 256-entry float64 table computed on the host with the reference's expression,
 // so the f64 output equals NumPy's bit for bit and the f32 / bf16 outputs are its roundings.
 // HBM-bound: 3 B read (x up to 4 taps, L1/L2-served) + 16 B (bf16 engine layout) written per pixel.
+#include <algorithm>
+
 #include "bugseg_internal.h"
 #include "mfma_common.h"
 #include "../../include/bugseg.h"
@@ -127,6 +129,22 @@ hipError_t launch_nchw_to_input(const NchwArgs &a, hipStream_t s) {
     if (g > 4096) g = 4096;
     if (g < 1) g = 1;
     hipLaunchKernelGGL(nchw_to_input_kernel, dim3((unsigned)g), dim3(256), 0, s, a);
+    return hipGetLastError();
+}
+
+// max |x| over n floats into RNG_SLOTS words (the fp32 mode's range of an engine input the caller
+// supplied, bugseg_enet_forward; the BGR path's range is the normalisation table's, known statically)
+__global__ void __launch_bounds__(256) amax_kernel(const float *x, size_t n, float *slots) {
+    float m = 0.f;
+    const size_t n4 = n / 4;
+    for (size_t i = (size_t)blockIdx.x * 256 + threadIdx.x; i < n4; i += (size_t)gridDim.x * 256)
+        rng_acc4(m, reinterpret_cast<const float4 *>(x)[i]);
+    if (blockIdx.x == 0 && threadIdx.x < n - n4 * 4) rng_acc(m, x[n4 * 4 + threadIdx.x], 0.f);
+    rng_commit(m, slots);
+}
+hipError_t launch_amax(const float *x, size_t n, float *slots, hipStream_t s) {
+    const size_t blocks = std::min<size_t>((n / 4 + 255) / 256 + 1, 2048);
+    hipLaunchKernelGGL(amax_kernel, dim3((unsigned)blocks), dim3(256), 0, s, x, n, slots);
     return hipGetLastError();
 }
 

@@ -97,6 +97,32 @@ __global__ void __launch_bounds__((up_threads<T, CIN>()), (sizeof(T) == 2 ? (CIN
     const int hw = a.h * a.w;
     const int nfrag = (a.M + 15) >> 4;
     const int gw = blockIdx.x * (NT / 64) + __builtin_amdgcn_readfirstlane(tid >> 6), nw = gridDim.x * (NT / 64);
+    // fp32 mode range scaling (bugseg_internal.h RangeArgs): x measured by its producer, e1's output and
+    // the tconv's from rigorous bounds; scl false (no multiply anywhere) when every exponent is 0
+    constexpr bool F32 = ES == 4;
+    bool scl = false;
+    float xm = 1.f, b1m = 1.f, m1m = 1.f, o1m = 1.f, b2m = 1.f, o2m = 1.f, b3m = 1.f, o3m = 1.f;
+    float amo = 0.f;
+    if constexpr (F32) {
+      const RangeArgs &g = a.rg;
+      if (!g.off) {
+        const float amx = rng_read(g);
+        const int sx = rng_exp_meas(amx), e1 = sx + g.sw[0];
+        const float Br = g.n[0] * amx + g.c[0];
+        const int sr = rng_exp_bound(Br, e1), e2 = sr + g.sw[1];
+        const int st = rng_exp_bound(g.n[1] * Br + g.c[1], e2), e3 = st + g.sw[2];
+        scl = e3 != 0;                                // (only the expansion branches; the rest always multiplies)
+        xm = rng_pow2(sx); b1m = rng_pow2(e1); m1m = rng_pow2(-e1); o1m = rng_pow2(sr - e1);
+        b2m = rng_pow2(e2); o2m = rng_pow2(st - e2); b3m = rng_pow2(e3); o3m = rng_pow2(-e3);
+      }
+    }
+    // (fp32: the accumulators start at the bias times their scale; always multiplied — a branch to scaled
+    // copies of the GEMMs cost 46 VGPRs here — the multipliers are 1 when nothing needs scaling)
+    auto bias_m = [&](const float *p, float m) -> f32x4 {
+        f32x4 b = bias4(p);
+        if constexpr (F32) b = mul4(b, m);
+        return b;
+    };
 
     // The grid is sized to the resident waves (launch_up) and each wave streams over fragments: the
     // next fragment's block input and pooling indices are in flight while this one computes.
@@ -136,19 +162,28 @@ __global__ void __launch_bounds__((up_threads<T, CIN>()), (sizeof(T) == 2 ? (CIN
         for (int r = 0; r < NM; ++r) id[r] = idn[r];
         if (f + nw < nfrag) load(f + nw);
         f32x4 acc1[NR1];
+        static_assert(B1ACC, "GEMM 1 starts from the bias");
 #pragma unroll
-        for (int r = 0; r < NR1; ++r) acc1[r] = B1ACC ? bias4(cb1 + r * 16 + kq * 4) : (f32x4){0.f, 0.f, 0.f, 0.f};
+        for (int r = 0; r < NR1; ++r) acc1[r] = bias_m(cb1 + r * 16 + kq * 4, b1m);
 #pragma unroll
-        for (int s = 0; s < KS1; ++s)
+        for (int s = 0; s < KS1; ++s) {
+            Raw xq = xf[s];
+            if constexpr (F32) xq = scale8(xf[s], xm);
 #pragma unroll
             for (int r = 0; r < NR1; ++r) {
                 WRaw wf;
                 ld8(wf, w1 + (r * 16 + col) * K1S + wch(col, s * 4 + kq, CIN));
-                mma(acc1[r], wf, xf[s]);
+                mma(acc1[r], wf, xq);
             }
+        }
+        if constexpr (F32) {
+            // main rows back to true units, e1 rows to their tconv operand's scale
+#pragma unroll
+            for (int r = 0; r < NR1; ++r) acc1[r] = mul4(acc1[r], r < NM ? m1m : o1m);
+        }
         auto ep1 = [&](int r) {
             const int c = r * 16 + kq * 4;
-            return round_t(act(B1ACC ? f4(acc1[r]) : add4(f4(acc1[r]), ld4f(cb1 + c)), cs1 + c), (const T *)nullptr);
+            return round_t(act(f4(acc1[r]), cs1 + c), (const T *)nullptr);
         };
         float4 mv[NM];
 #pragma unroll
@@ -165,25 +200,32 @@ __global__ void __launch_bounds__((up_threads<T, CIN>()), (sizeof(T) == 2 ? (CIN
 #pragma unroll
             for (int e = 0; e < NE; ++e) {
                 const int r2 = ph * NE + e;
-                acc2[e] = B2ACC ? bias4(cb2 + r2 * 16 + kq * 4) : (f32x4){0.f, 0.f, 0.f, 0.f};
+                static_assert(B2ACC, "the tconv starts from the bias");
+                acc2[e] = bias_m(cb2 + r2 * 16 + kq * 4, b2m);
                 WRaw wf;
                 ld8(wf, w2 + (r2 * 16 + col) * K2S + wch(col, kq, 32));
                 mma(acc2[e], wf, bop2);
+                if constexpr (F32) acc2[e] = mul4(acc2[e], o2m);
             }
             auto ep2 = [&](int e) {
                 const int c = (ph * NE + e) * 16 + kq * 4;
-                return round_t(act(B2ACC ? f4(acc2[e]) : add4(f4(acc2[e]), ld4f(cb2 + c)), cs2 + c), (const T *)nullptr);
+                return round_t(act(f4(acc2[e]), cs2 + c), (const T *)nullptr);
             };
             Raw bop3;
             to_bop(bop3, ep2(0), NE > 1 ? ep2(1) : make_float4(0.f, 0.f, 0.f, 0.f));
             const uint32_t opix = obase + (uint32_t)((ph >> 1) * 2 * a.w + (ph & 1));
             auto ep3 = [&](int r) {
                 const int c = r * 16 + kq * 4;
-                f32x4 acc = B3ACC ? bias4(cb3 + c) : (f32x4){0.f, 0.f, 0.f, 0.f};
+                static_assert(B3ACC, "the expansion starts from the bias");
+                f32x4 acc = bias_m(cb3 + c, b3m);
                 WRaw wf;
                 ld8(wf, w3 + (r * 16 + col) * K3S + wch(col, kq, 32));
                 mma(acc, wf, bop3);
-                float4 v = act(B3ACC ? f4(acc) : add4(f4(acc), ld4f(cb3 + c)), cs3 + c);
+                float4 v = f4(acc);
+                if constexpr (F32) {
+                    if (scl) v = mul4(v, o3m);
+                }
+                v = act(v, cs3 + c);
                 // MaxUnpool2d(2): the main value lands where its pooling index points
                 const uint32_t w = id[r];
                 const uint32_t pos = (uint32_t)ph;
@@ -207,6 +249,7 @@ __global__ void __launch_bounds__((up_threads<T, CIN>()), (sizeof(T) == 2 ? (CIN
 #pragma unroll
                 for (int r = 0; r < NR3; ++r) {
                     const float4 v = ep3(r);
+                    if constexpr (F32) rng_acc4(amo, v);
                     const uint32_t off = pv ? (opix * COUT + r * 16 + kq * 4) * ES : OOB;
                     if constexpr (ES == 2) bst8o<OAUX>(ro, off, pack4<T>(v));
                     else bst16o<OAUX>(ro, off, __builtin_bit_cast(uint4, v));
@@ -214,6 +257,7 @@ __global__ void __launch_bounds__((up_threads<T, CIN>()), (sizeof(T) == 2 ? (CIN
             }
         }
     }
+    if constexpr (F32) rng_commit(amo, a.rg.amax_out);
 }
 
 template <typename T, int CIN, int I, int COUT>
@@ -240,8 +284,7 @@ static hipError_t launch_shape(int prec, const UpArgs &a, dim3 g, hipStream_t s)
     } else {
         const size_t lds = up_lds<float, CI, II, CO>();
         if (lds > 64 * 1024) {
-            hipError_t e = hipFuncSetAttribute((const void *)up_kernel<float, CI, II, CO>,
-                                               hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+            hipError_t e = allow_dynamic_lds((const void *)up_kernel<float, CI, II, CO>);
             if (e != hipSuccess) return e;
         }
         hipLaunchKernelGGL((up_kernel<float, CI, II, CO>), g, dim3(up_threads<float, CI>()), lds, s, a);
@@ -252,17 +295,11 @@ static hipError_t launch_shape(int prec, const UpArgs &a, dim3 g, hipStream_t s)
 // workgroups resident at once (occupancy API, per kernel instance), cached
 template <typename T, int CI, int II, int CO>
 static int up_resident() {
-    static int n = 0;
-    if (n == 0) {
-        int dev = 0, cus = 0, per = 0;
-        if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
-            cus = 256;
-        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, (const void *)up_kernel<T, CI, II, CO>, up_threads<T, CI>(), up_lds<T, CI, II, CO>()) !=
-                hipSuccess || per <= 0)
-            per = 2;
-        n = cus * per;
-    }
-    return n;
+    // (cached per device: bugseg_runtime.cpp occupancy_per_cu; the >64 KB LDS opt-in first, or the
+    // occupancy API sees a kernel that cannot launch)
+    if (up_lds<T, CI, II, CO>() > 64 * 1024) (void)allow_dynamic_lds((const void *)up_kernel<T, CI, II, CO>);
+    const int per = occupancy_per_cu((const void *)up_kernel<T, CI, II, CO>, up_threads<T, CI>(), up_lds<T, CI, II, CO>());
+    return device_cus() * (per > 0 ? per : 2);
 }
 
 hipError_t launch_up(int prec, int cin, int it, int cout, const UpArgs &a, hipStream_t s) {

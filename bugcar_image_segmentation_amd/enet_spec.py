@@ -139,8 +139,9 @@ def slope_for(act: str, c: int) -> np.ndarray:
 
 
 def build_enet(seed: int = 1234, num_classes: int = NUM_CLASSES, fullconv_k: int = 3,
-               initial_pool_k: int = 3, bn_gamma_scale: float = 1.0):
-    """Canonical ENet with deterministic synthetic weights -> list[Block]."""
+               initial_pool_k: int = 3, bn_gamma_scale: float = 1.0, res_gamma=RES_GAMMA):
+    """Canonical ENet with deterministic synthetic weights -> list[Block]. res_gamma=(0.5, 1.5) is
+    SURVEY.md §8(d)'s undamped draw (logits grow to ~1e6; the fp32 range tests use it)."""
     ini = _Init(seed, bn_gamma_scale)
     blocks = []
     for typ, name, a in canonical_enet_layout(num_classes, fullconv_k, initial_pool_k):
@@ -160,7 +161,7 @@ def build_enet(seed: int = 1234, num_classes: int = NUM_CLASSES, fullconv_k: int
             it = cin // 4
             us = [ini.unit(UNIT_CONV, it, cin, 2, 2, a["act"], stride=2),
                   ini.unit(UNIT_CONV, it, it, 3, 3, a["act"], pad=(1, 1)),
-                  ini.unit(UNIT_CONV, cout, it, 1, 1, a["act"], gamma_range=RES_GAMMA)]
+                  ini.unit(UNIT_CONV, cout, it, 1, 1, a["act"], gamma_range=res_gamma)]
             blocks.append(Block(typ, name, dict(cin=cin, cout=cout), us, dict(out_slope=slope_for(a["act"], cout))))
         elif typ == "regular":
             ch, k, d = a["ch"], a["k"], a["dil"]
@@ -172,7 +173,7 @@ def build_enet(seed: int = 1234, num_classes: int = NUM_CLASSES, fullconv_k: int
                 us.append(ini.unit(UNIT_CONV, it, it, 1, k, a["act"], pad=(0, p)))
             else:
                 us.append(ini.unit(UNIT_CONV, it, it, k, k, a["act"], pad=(d, d), dil=(d, d)))
-            us.append(ini.unit(UNIT_CONV, ch, it, 1, 1, a["act"], gamma_range=RES_GAMMA))
+            us.append(ini.unit(UNIT_CONV, ch, it, 1, 1, a["act"], gamma_range=res_gamma))
             blocks.append(Block(typ, name, dict(ch=ch), us, dict(out_slope=slope_for(a["act"], ch))))
         elif typ == "up":
             cin, cout = a["cin"], a["cout"]
@@ -181,7 +182,7 @@ def build_enet(seed: int = 1234, num_classes: int = NUM_CLASSES, fullconv_k: int
             us = [ini.unit(UNIT_CONV, cout, cin, 1, 1, "none"),
                   ini.unit(UNIT_CONV, it, cin, 1, 1, a["act"]),
                   ini.unit(UNIT_TCONV, it, it, 2, 2, a["act"], stride=2),
-                  ini.unit(UNIT_CONV, cout, it, 1, 1, a["act"], gamma_range=RES_GAMMA)]
+                  ini.unit(UNIT_CONV, cout, it, 1, 1, a["act"], gamma_range=res_gamma)]
             blocks.append(Block(typ, name, dict(cin=cin, cout=cout, pool_ref=ref), us,
                                 dict(out_slope=slope_for(a["act"], cout))))
         elif typ == "fullconv":

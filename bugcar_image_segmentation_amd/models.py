@@ -77,9 +77,15 @@ class ENET(InferenceModel):
     def __init__(self, GRAPH_PB_PATH=None, *, weights=None, precision: str = "fp32", device: int | None = None):
         """GRAPH_PB_PATH: weight file (default "./pretrained_models/enet.pb", models.py:23-24).
         weights: a BSG1 blob (bytes) or an enet_spec block list, instead of a file.
-        precision: "fp32" (parity mode), "bf16" or "fp16" (throughput modes: 2-byte activations and
-        weights, f32 accumulation; fp16 keeps 3 more mantissa bits than bf16, so its class maps agree
-        more closely with fp32, within fp16's +-65504 range)."""
+        precision: "fp32" (parity mode: f32 storage and accumulation; each f32 product is computed as
+        three f16 MFMA products of split operands, hi = f16(v), lo = f16(v - hi), ~2^-21 relative per
+        product, within f32's accuracy over the whole f32 range: every operand is first brought into
+        the f16 window by an exact power of two — measured per tensor, bounded for a fused block's
+        internals, static for the weights — so no value overflows or underflows the split; see
+        tests/test_gpu_range.py), "bf16" or "fp16" (throughput modes: 2-byte activations and weights,
+        f32 accumulation; fp16 keeps 3 more mantissa bits than bf16, so its class maps agree more
+        closely with fp32, but values beyond fp16's +-65504 become inf — a graph whose activations
+        leave that range needs fp32 or bf16)."""
         if precision not in ("fp32", "bf16", "fp16"):
             raise ValueError("precision must be 'fp32', 'bf16' or 'fp16'")
         if weights is None:

@@ -196,6 +196,11 @@ const char *bugseg_last_error(const bugseg_ctx *ctx);
 int bugseg_debug_parse_pack(const void *blob, size_t bytes, int precision, int *ncls);
 int bugseg_debug_polar_tables(int w, int h, int variant, int32_t *fmap, size_t fmap_n, int32_t *imap, size_t imap_n,
                               int *pw, int *ph);
+/* Test hook: a context fact. what = 0: the fused initial block normalises bytes with the exact affine
+ * form (bf16 / fp16; 0 = the table), 1: fp32 range scaling switched off (BUGSEG_F32_RANGE=0 at load),
+ * 2: the weights' exponent of packed convolution `arg` (fp32 range scaling; -1000 if no such conv).
+ * Returns -1 for an unknown `what` or a NULL ctx. */
+int bugseg_debug_ctx_info(const bugseg_ctx *ctx, int what, int arg);
 
 /* ---- DeepLabV3 (BASELINE config 4) -------------------------------------
  * Replaces DeepLabV3 (models.py:98-136): tf.compat.v1.Session + GraphDef import (models.py:105-113)

@@ -1,0 +1,279 @@
+"""Golden fixtures from the REFERENCE'S OWN Python glue. Run in the build container
+only (it reads /root/reference, which the GPU box does not have); the output is data only:
+
+    python tests/golden/make_ref_glue.py        ->  tests/golden/ref_glue.npz
+
+The reference imports cv2, tensorflow, numpy_indexed, rospy and the ROS message packages, none of
+which exist here. They are replaced by small module stand-ins whose functions are this repo's own
+restatements (oracle/ocv_np.py for OpenCV, NumPy for the three TF ops models.py calls, a dict-backed
+message object for ROS); scipy is the real one. The reference's own code then runs unmodified:
+
+* bev.py:166-246  bev_transform_tools.create_occupancy_grid, both branches (laserscan on / off);
+* bev.py:97-165   create_occupancy_grid_binary, both branches;
+* bev.py:24-41    fromJSON;
+* occgrid_to_ros.py:13-61  convert_to_occupancy_grid_msg (real scipy Rotation);
+* models.py:42-69, 70-82   ENET.predict / predict_binary post-processing on given logits (the
+                           session is a stand-in returning them), models.py:84-95 ENET.preprocess.
+
+What this pins: the reference's glue — the geometry's int() truncations, the crop / pad slicing, the
+label lift and its uint8 wrap, the speckle mask arithmetic, the binary variant's uint8 encoding, the
+laserscan flow (polar warp orientation, group-by, circle stamping, merge), the ROS layout / origin /
+quaternion, the argmax + LUT logic, the preprocess normalisation. What it does NOT pin: OpenCV's or
+TensorFlow's arithmetic (the stand-ins are the oracle's restatements of it), which stays unpinned
+(DESIGN.md §2). Checked by tests/test_ref_glue.py (CPU: oracle + drop-in host code) and
+tests/test_gpu_parity.py::test_bev_equals_reference_glue_fixtures (the HIP rasteriser).
+"""
+from __future__ import annotations
+
+import io
+import json
+import os
+import sys
+import tempfile
+import types
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+sys.path.insert(0, ROOT)
+REF_PARENT = "/root"                       # /root/reference is the package `reference`
+
+from oracle import ocv_np  # noqa: E402
+
+
+# ------------------------------------------------------------------ module stand-ins
+def _cv2():
+    m = types.ModuleType("cv2")
+    m.INTER_NEAREST, m.INTER_LINEAR, m.MORPH_OPEN = 0, 1, 2
+    m.WARP_POLAR_LINEAR, m.WARP_INVERSE_MAP = 0, 16
+    m.COLOR_BGR2RGB, m.ROTATE_90_COUNTERCLOCKWISE = 4, 2
+
+    def warpPerspective(src, M, dsize):
+        assert src.dtype == np.uint8 and src.ndim == 2
+        return ocv_np.warp_perspective(src, M, tuple(dsize))
+
+    def morphologyEx(src, op, kernel=None):
+        assert op == m.MORPH_OPEN and np.array_equal(np.asarray(kernel), np.ones((3, 3)))
+        return ocv_np.morph_open3x3(src)
+
+    def subtract(a, b):                      # saturating, dtype of a (u8)
+        return np.clip(a.astype(np.int16) - b.astype(np.int16), 0, 255).astype(a.dtype)
+
+    def resize(src, dsize, interpolation=1):
+        if interpolation == m.INTER_NEAREST:
+            return ocv_np.resize_nearest(src, tuple(dsize))
+        return ocv_np.resize_linear(src, tuple(dsize))
+
+    def warpPolar(src, dsize, center, maxRadius, flags):
+        return ocv_np.warp_polar(src, tuple(dsize), center, maxRadius, inverse=bool(flags & m.WARP_INVERSE_MAP))
+
+    def circle(img, center, radius, color, thickness):
+        assert radius == 1 and thickness == -1
+        return ocv_np.circle_filled_r1(img, center, color)
+
+    def flip(img, code):
+        assert code == 0
+        return np.ascontiguousarray(img[::-1, :])
+
+    def rotate(img, code):
+        assert code == m.ROTATE_90_COUNTERCLOCKWISE
+        return np.ascontiguousarray(np.rot90(img, 1))
+
+    def cvtColor(img, code):
+        assert code == m.COLOR_BGR2RGB
+        return np.ascontiguousarray(img[..., ::-1])
+
+    m.warpPerspective, m.morphologyEx, m.subtract, m.resize = warpPerspective, morphologyEx, subtract, resize
+    m.warpPolar, m.circle, m.flip, m.rotate, m.cvtColor = warpPolar, circle, flip, rotate, cvtColor
+    m.imshow = lambda *a, **k: None
+    return m
+
+
+class _T(np.ndarray):
+    """A tensor stand-in: a NumPy array with .numpy()."""
+    def numpy(self):
+        return np.asarray(self)
+
+
+def _t(a):
+    return np.asarray(a).view(_T)
+
+
+def _tf():
+    m = types.ModuleType("tensorflow")
+    m.math = types.SimpleNamespace(argmax=lambda x, axis: _t(np.argmax(np.asarray(x), axis=axis)))  # first max: TF's
+    m.ones = lambda shape: _t(np.ones(shape, np.float32))
+    m.where = lambda c, x, y: _t(np.where(np.asarray(c), x, y))
+    m.logical_or = lambda a, b: _t(np.logical_or(np.asarray(a), np.asarray(b)))
+    m.bitwise = types.SimpleNamespace(bitwise_or=lambda a, b: _t(np.bitwise_or(np.asarray(a), np.asarray(b))))
+    m.cast = lambda x, dt: _t(np.asarray(x).astype(dt))
+    m.uint8 = np.uint8
+    return m
+
+
+def _npi():
+    m = types.ModuleType("numpy_indexed")
+
+    class _G:
+        def __init__(self, keys):
+            self.keys = np.asarray(keys)
+
+        def min(self, values):
+            return ocv_np._group_min(self.keys, np.asarray(values))
+
+    m.group_by = _G
+    return m
+
+
+class _Msg:
+    """A ROS message stand-in: attributes set freely; OccupancyGrid's `data` is a list."""
+    def __init__(self):
+        self.data = []
+
+
+def _ros():
+    mods = {}
+    rospy = types.ModuleType("rospy")
+    rospy.Time = types.SimpleNamespace(now=lambda: 0)
+    mods["rospy"] = rospy
+    for pkg, names in (("std_msgs", ["Header"]), ("nav_msgs", ["OccupancyGrid", "MapMetaData"]),
+                       ("geometry_msgs", ["Pose", "Point", "Quaternion"])):
+        p = types.ModuleType(pkg)
+        msg = types.ModuleType(pkg + ".msg")
+        for n in names:
+            setattr(msg, n, type(n, (_Msg,), {}))
+        p.msg = msg
+        mods[pkg] = p
+        mods[pkg + ".msg"] = msg
+    return mods
+
+
+def import_reference():
+    # the reference was written for NumPy 1.x (TF 2.2, requirements.txt:2): bev.py:186 uses the np.Inf
+    # alias NumPy 2 removed. Its uint8 arithmetic (np.add, * 100, 200 - g, np.where with -1) ends in the
+    # same int8 / uint8 values under NumPy 2's promotion rules as under 1.x's value-based casting (the
+    # oracle emulates 1.x explicitly, ocv_np.create_occupancy_grid_binary; tests/test_ref_glue.py
+    # compares the two)
+    if "Inf" not in np.__dict__:
+        np.Inf = np.inf
+    stand = {"cv2": _cv2(), "tensorflow": _tf(), "numpy_indexed": _npi(), **_ros()}
+    saved = {k: sys.modules.get(k) for k in stand}
+    sys.modules.update(stand)
+    sys.path.insert(0, REF_PARENT)
+    try:
+        import importlib
+        bev = importlib.import_module("reference.bev")
+        occ = importlib.import_module("reference.occgrid_to_ros")
+        models = importlib.import_module("reference.models")
+    finally:
+        sys.path.remove(REF_PARENT)
+    return bev, occ, models, saved
+
+
+# ------------------------------------------------------------------ cases
+def _geometries():
+    """(name, JSON dict, grid (w_m, h_m, cell_m)): the bench calibration and smaller ones with negative
+    crop offsets (the template wider / taller than the warped image) and a non-integer cell."""
+    from bugcar_image_segmentation_amd import synthetic
+    b = synthetic.synthetic_bev(480, 640)
+    g = []
+    for name, bev, grid in (("bench", b, (synthetic.GRID_W_M, synthetic.GRID_H_M, synthetic.CELL_M)),
+                            ("small_neg", synthetic.synthetic_bev(60, 80, out_w=90, out_h=70), (1.6, 1.2, 0.05)),
+                            ("small_odd", synthetic.synthetic_bev(48, 64, out_w=120, out_h=100), (0.93, 0.71, 0.03))):
+        d = {"input image size": [bev.input_width, bev.input_height],
+             "output image size": [bev.after_warp_width, bev.after_warp_height],
+             "bev matrix": np.asarray(bev._bev_matrix, np.float64).ravel().tolist(),
+             "distance to target": [0.0, 50.0], "tile_length": 40.0, "cm_per_px": float(bev.cm_per_px),
+             "yaw": 0.0, "is_laserscan": False}
+        g.append((name, d, grid))
+    return g
+
+
+def main(out_path=None):
+    out_path = out_path or os.path.join(os.path.dirname(os.path.abspath(__file__)), "ref_glue.npz")
+    bev_mod, occ_mod, models_mod, _saved = import_reference()
+    rng = np.random.default_rng(20251018)
+    out = {}
+    tmp = tempfile.mkdtemp()
+    for gname, d, (gw, gh, cell) in _geometries():
+        rows, cols = d["input image size"]
+        path = os.path.join(tmp, gname + ".json")
+        with open(path, "w") as f:
+            json.dump(d, f)
+        saved_stdout, sys.stdout = sys.stdout, io.StringIO()      # fromJSON prints is_laserscan
+        try:
+            b = bev_mod.bev_transform_tools.fromJSON(path)
+        finally:
+            sys.stdout = saved_stdout
+        out[f"{gname}/json"] = np.frombuffer(json.dumps(d).encode(), np.uint8)
+        out[f"{gname}/grid"] = np.array([gw, gh, cell])
+        out[f"{gname}/fromjson_M"] = np.asarray(b._bev_matrix, np.float64)
+        out[f"{gname}/fromjson_sizes"] = np.array([b.input_width, b.input_height, b.after_warp_width,
+                                                   b.after_warp_height], np.int64)
+        # segmaps: 3-class maps (the product's), 15-class maps, labels over the whole u8 range (wrap),
+        # and a structured map (blobs + speckles) so the opening and the laserscan flow have work
+        segs = [rng.integers(0, 3, (rows, cols), dtype=np.uint8),
+                rng.integers(0, 15, (rows, cols), dtype=np.uint8),
+                rng.integers(0, 256, (rows, cols), dtype=np.uint8)]
+        s = np.ones((rows, cols), np.uint8)
+        s[rows // 3: rows // 2, cols // 4: cols // 2] = 2
+        s[rows // 2:, cols // 2:] = 0
+        sp = rng.random((rows, cols)) < 0.02
+        s[sp] = 2
+        segs.append(s)
+        out[f"{gname}/segmaps"] = np.stack(segs)
+        for ls in (False, True):
+            b.laserscan_like_occupancy_grid = ls
+            g0, g1, g1b = [], [], []
+            for seg in segs:
+                g0.append(np.asarray(b.create_occupancy_grid(seg, gw, gh, cell)))
+                r = b.create_occupancy_grid_binary(seg, gw, gh, cell)
+                if ls:
+                    g1.append(np.asarray(r[0]))
+                    g1b.append(np.asarray(r[1]))
+                else:
+                    g1.append(np.asarray(r))
+            tag = "ls" if ls else "plain"
+            out[f"{gname}/{tag}/occgrid"] = np.stack(g0)
+            out[f"{gname}/{tag}/occgrid_binary"] = np.stack(g1)
+            if ls:
+                out[f"{gname}/{tag}/occgrid_binary_new"] = np.stack(g1b)
+        b.laserscan_like_occupancy_grid = False
+        # the ROS message of the first grid
+        grid = out[f"{gname}/plain/occgrid"][0]
+        pose = np.array([0.3, -0.2, 0.1, 0.05, -0.1, 0.7])
+        msg = occ_mod.convert_to_occupancy_grid_msg(grid, cell, gw, gh, 12345, "base_link", pose)
+        out[f"{gname}/ros/data"] = np.asarray(msg.data, np.int64)
+        out[f"{gname}/ros/pose"] = pose
+        out[f"{gname}/ros/info"] = np.array([msg.info.height, msg.info.width, msg.info.resolution,
+                                             msg.info.origin.position.x, msg.info.origin.position.y,
+                                             msg.info.origin.position.z, msg.info.origin.orientation.x,
+                                             msg.info.origin.orientation.y, msg.info.origin.orientation.z,
+                                             msg.info.origin.orientation.w], np.float64)
+        out[f"{gname}/ros/header"] = np.frombuffer(json.dumps({"frame_id": msg.header.frame_id,
+                                                               "stamp": msg.header.stamp}).encode(), np.uint8)
+    # ENET.predict / predict_binary on given logits: random, with exact ties between classes of different
+    # LUT groups (first index wins), and all-equal pixels
+    E = models_mod.ENET
+    enet = E.__new__(E)
+    logits = rng.normal(size=(2, 15, 24, 40)).astype(np.float32)
+    logits[0, 3, :4] = logits[0, 0, :4] = 9.0          # classes 0 and 3 tied at the max: class 0
+    logits[0, 9, 4:8] = logits[0, 1, 4:8] = 9.0        # 1 and 9 tied: class 1
+    logits[1, :, :2] = 0.5                              # all equal: class 0
+    enet.sess = types.SimpleNamespace(run=lambda name, feed_dict: logits)
+    saved_stdout, sys.stdout = sys.stdout, io.StringIO()      # predict prints the shape
+    try:
+        out["enet/logits"] = logits
+        out["enet/predict"] = np.asarray(enet.predict(None))
+        out["enet/predict_binary"] = np.asarray(enet.predict_binary(None))
+    finally:
+        sys.stdout = saved_stdout
+    bgr = rng.integers(0, 256, (300, 420, 3), dtype=np.uint8)
+    out["enet/preprocess_in"] = bgr
+    out["enet/preprocess"] = np.asarray(E.preprocess(bgr))
+    np.savez_compressed(out_path, **out)
+    print(f"wrote {out_path}: {len(out)} arrays")
+
+
+if __name__ == "__main__":
+    main()
