@@ -10,9 +10,10 @@ and weights far outside the f16 range and compare the logits with the fp64 oracl
 The criterion, per pixel e = max over classes |dlogit| / max |logit| (scripts/range_diag.py measured it):
 
 * every logit finite;
-* 99% of the pixels within REL99 = 2e-6 and 99.9% within REL = 5e-6 of the max (f32 itself: the fp32
-  oracle is 2.0e-6 of the max away from fp64 on the undamped 480x640 case, its p99 6e-7);
-* at most MAX_OFF = 0.5% of the pixels beyond REL: where a max-pool window's top two inputs lie
+* 99% of the pixels within REL99 = 2e-6 of the max (f32 itself: the fp32 oracle is 2.0e-6 of the max
+  away from fp64 on the undamped 480x640 case, its p99 6e-7);
+* at most MAX_OFF = 0.5% of the pixels of a frame (and at least 2 x 32 x 32 of them allowed: one flip's
+  footprint at the network's 1/8 stage) beyond REL: where a max-pool window's top two inputs lie
   within rounding of each other, a different argmax index moves a value to another position through
   max-unpool — a discontinuity every f32 evaluation order can hit (the fp32 oracle itself does on
   some of these frames: 2.9e-2 of the max on 0.25% of the pixels of one). An f16 range failure shows
@@ -62,7 +63,9 @@ def _verdict(got, ref, what):
     msg = (f"{what}: max|logit| {amax:.3e}; per-pixel error / max: p50 {np.percentile(e, 50):.1e} "
            f"p99 {p99:.1e} p99.9 {p999:.1e} max {e.max():.1e}; {int(off.sum())} of {off.size} pixels "
            f"beyond {REL:g}; classes {'exact' if cls_ok else 'DIFFER'} on {int(dec.sum())} decided pixels")
-    return (p99 <= REL99 and p999 <= REL and off.mean() <= MAX_OFF and cls_ok), msg
+    n_off = off.reshape(off.shape[0], -1).sum(1)
+    allowed = max(MAX_OFF * off[0].size, 2 * 32 * 32)
+    return (p99 <= REL99 and bool((n_off <= allowed).all()) and cls_ok), msg
 
 
 def _check(blocks, x, what):
