@@ -268,10 +268,9 @@ def forward_ms(ctx, fs, Bs, H, W, seg, stream, reps):
 
 
 class HipEvents:
-    """Raw HIP events recorded with hipEventRecordWithFlags(..., hipEventRecordExternal), so that inside
-    a stream capture each record becomes an event-record node of the graph (torch's Event.record only
-    records a capture dependency there); timed with hipEventElapsedTime after a replay. Bound to the HIP
-    runtime torch loaded (libamdhip64.so.7, the soname libbugseg.so links)."""
+    """Raw HIP events that, recorded inside a stream capture, become event-record nodes of the graph
+    (torch's Event.record only records a capture dependency there); timed with hipEventElapsedTime after
+    a replay. Bound to the HIP runtime torch loaded (libamdhip64.so.7, the soname libbugseg.so links)."""
 
     def __init__(self, n):
         import ctypes
@@ -279,7 +278,7 @@ class HipEvents:
         self.hip = ctypes.CDLL("libamdhip64.so.7")
         vp = ctypes.c_void_p
         self.hip.hipEventCreate.argtypes = [ctypes.POINTER(vp)]
-        self.hip.hipEventRecordWithFlags.argtypes = [vp, vp, ctypes.c_uint]
+        self.hip.hipEventRecord.argtypes = [vp, vp]
         self.hip.hipEventElapsedTime.argtypes = [ctypes.POINTER(ctypes.c_float), vp, vp]
         self.hip.hipEventDestroy.argtypes = [vp]
         self.ev = []
@@ -290,8 +289,26 @@ class HipEvents:
             self.ev.append(e)
 
     def record(self, i, stream):
-        if self.hip.hipEventRecordWithFlags(self.ev[i], self.ct.c_void_p(int(stream.cuda_stream)), 1) != 0:
-            raise RuntimeError("hipEventRecordWithFlags failed")
+        """Outside a capture: hipEventRecord. Inside one: an event-record node spliced after the
+        capture's current dependencies (hipGraphAddEventRecordNode + hipStreamUpdateCaptureDependencies;
+        the HIP runtime torch ships rejects hipEventRecordWithFlags(External) while capturing)."""
+        ct, vp = self.ct, self.ct.c_void_p
+        s = vp(int(stream.cuda_stream))
+        status, cid, graph = ct.c_int(), ct.c_ulonglong(), vp()
+        deps, nd = ct.POINTER(vp)(), ct.c_size_t()
+        if self.hip.hipStreamGetCaptureInfo_v2(s, ct.byref(status), ct.byref(cid), ct.byref(graph),
+                                               ct.byref(deps), ct.byref(nd)) != 0:
+            raise RuntimeError("hipStreamGetCaptureInfo_v2 failed")
+        if status.value != 1:                                   # not capturing
+            if self.hip.hipEventRecord(self.ev[i], s) != 0:
+                raise RuntimeError("hipEventRecord failed")
+            return
+        node = vp()
+        darr = (vp * max(1, nd.value))(*[deps[k] for k in range(nd.value)])
+        if self.hip.hipGraphAddEventRecordNode(ct.byref(node), graph, darr, nd, self.ev[i]) != 0:
+            raise RuntimeError("hipGraphAddEventRecordNode failed")
+        if self.hip.hipStreamUpdateCaptureDependencies(s, (vp * 1)(node), ct.c_size_t(1), ct.c_uint(1)) != 0:
+            raise RuntimeError("hipStreamUpdateCaptureDependencies failed")
 
     def ms(self, i, j):
         t = self.ct.c_float()
