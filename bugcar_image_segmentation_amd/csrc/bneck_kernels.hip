@@ -338,6 +338,7 @@ __global__ void __launch_bounds__((BShape<C, V>::NW * 64), (sizeof(T) == 2 ? BSh
     // 16 zero elements: masked-off B fragments read them (an address select, not a divergent branch)
     T *zpad = reinterpret_cast<T *>(cso + C);
     T *ts = zpad + 16;                                // t0 / t1a / t1 region
+    float *wmx = reinterpret_cast<float *>(ts + HR * PSTR);   // fp32 asymmetric: NW per-wave max |t1a| slots
     {
         // C = 16 (small weights, many short tiles): every load of the staging is issued before the
         // first LDS store (one L2 round trip at kernel start instead of one per 16-B chunk a thread
@@ -458,6 +459,7 @@ __global__ void __launch_bounds__((BShape<C, V>::NW * 64), (sizeof(T) == 2 ? BSh
     bool scl = false;
     float xm = 1.f, b1m = 1.f, o1m = 1.f, b2m = 1.f, o2m = 1.f, b2bm = 1.f, o2bm = 1.f, b3m = 1.f, o3m = 1.f;
     float amo = 0.f;                                  // max |out| of this lane's stores
+    int rs1 = 0, re2b = 0;                            // asymmetric: t1a's exponent, the 1x5's accumulator exponent
     if constexpr (F32) {
       const RangeArgs &g = a.rg;
       if (!g.off) {
@@ -473,6 +475,7 @@ __global__ void __launch_bounds__((BShape<C, V>::NW * 64), (sizeof(T) == 2 ? BSh
             s1b = rng_exp_bound(g.n[2] * B1 + g.c[2], e2b);
         }
         const int e3 = (ASYM ? s1b : s1) + g.sw[3];
+        rs1 = s1; re2b = e2b;
         scl = e3 != 0;                                // (only phase 3 branches; the rest always multiplies)
         xm = rng_pow2(sx); b1m = rng_pow2(e1); o1m = rng_pow2(s0 - e1); b2m = rng_pow2(e2); o2m = rng_pow2(s1 - e2);
         b2bm = rng_pow2(e2b); o2bm = rng_pow2(s1b - e2b); b3m = rng_pow2(e3); o3m = rng_pow2(-e3);
@@ -1026,6 +1029,7 @@ __global__ void __launch_bounds__((BShape<C, V>::NW * 64), (sizeof(T) == 2 ? BSh
             }
             __syncthreads();
             // t1a of fragment j, row block r: act2, zero outside the image columns (the 1x5 zero-pads t1a)
+            float m1a = 0.f;                          // fp32: max |t1a| of the tile (the 1x5's output bound)
 #pragma unroll
             for (int j = 0; j < NF2A; ++j)
 #pragma unroll
@@ -1037,10 +1041,31 @@ __global__ void __launch_bounds__((BShape<C, V>::NW * 64), (sizeof(T) == 2 ? BSh
                         float4 v = f4(acc5[j][r]);
                         if constexpr (F32) v = mul4(v, o2m);
                         v = act(v, cs2 + ch);
-                        st4t(ts + p * PSTR + ch, ch, inside ? v : make_float4(0.f, 0.f, 0.f, 0.f));
+                        v = inside ? v : make_float4(0.f, 0.f, 0.f, 0.f);
+                        if constexpr (F32) rng_acc4(m1a, v);
+                        st4t(ts + p * PSTR + ch, ch, v);
                     }
                 }
+            if constexpr (F32) {
+                // the bound of t1 = act(1x5 (t1a)) from the tile's measured t1a (n2b max|t1a| + c2b)
+                // rather than from x's (n2b (n2 B0 + c2) + c2b: 1e5-3e5 for the default weights, past
+                // the window, where the tile's is ~3e3): one slot per wave, read after the barrier
+#pragma unroll
+                for (int o = 32; o > 0; o >>= 1) m1a = __builtin_fmaxf(m1a, __shfl_xor(m1a, o));
+                if (lane == 0) wmx[wave] = m1a;
+            }
             __syncthreads();
+            if constexpr (F32) {
+                if (!a.rg.off) {
+                    float mt = 0.f;
+#pragma unroll
+                    for (int w = 0; w < NW; ++w) mt = __builtin_fmaxf(mt, wmx[w]);
+                    mt = __int_as_float(__builtin_amdgcn_readfirstlane(__float_as_int(mt))) * rng_pow2(-rs1);
+                    const int s1b = rng_exp_bound(a.rg.n[2] * mt + a.rg.c[2], re2b), e3 = s1b + a.rg.sw[3];
+                    o2bm = rng_pow2(s1b - re2b); b3m = rng_pow2(e3); o3m = rng_pow2(-e3);
+                    scl = e3 != 0;
+                }
+            }
             {   // 1x5 over columns (taps dx = -2..2)
                 f32x4 acc[NF2][NR1];
 #pragma unroll
@@ -1303,7 +1328,8 @@ size_t bneck_lds_bytes(int prec, int C, bool asym, int v, int cin) {
     const bool hstg = staged && es == 4 && BNECK_F32_HSTG;            // fp32 C = 64: one 32-channel half at a time
     const size_t stage = staged ? (size_t)NW * 16 * ((hstg ? C / 2 : C) + pad) : 0;    // staged epilogue (REG3 off)
     const size_t consts = ((size_t)6 * NR1 * 16 + 3 * (size_t)C) * sizeof(float);
-    return (wts + 16 + (halo > stage ? halo : stage)) * es + consts;   // + the zero pad
+    return (wts + 16 + (halo > stage ? halo : stage)) * es + consts +   // + the zero pad
+           (asym && es == 4 ? (size_t)NW * sizeof(float) : 0);             // + fp32 asymmetric max slots
 }
 
 // kernel symbol of (precision, C, asym, variant, transposed); nullptr if not built
