@@ -3,9 +3,12 @@
 One "step" = one pass of the hot path over one batch of synthetic 640x480x3 BGR frames already
 resident in HBM: ENet forward (29 launches, one per block: the initial block normalises the raw
 bytes as it loads them, argmax + 3-class remap in the class layer's epilogue) -> fused BEV
-rasteriser -> (N > 1) RCCL all-gather of the int8 grids. The batch is split into `--streams` frame
-shards run concurrently on their own HIP streams. Per-GPU batch is fixed (weak scaling): rank r of N
-owns `--batch` frames of the N*batch global batch (BASELINE configs 3 and 5: 64 frames per GPU =
+rasteriser -> (N > 1) RCCL all-gather of the int8 grids. The whole per-GPU batch runs as one launch
+chain on one HIP stream (`--streams 1`, the default since round 5; `--streams S` splits it into S frame
+shards on their own streams — ~7% more frames/s from overlapping the kernels' tails, recorded as the
+`two_streams` sub-record, but concurrent launches stretch each other and a profiler serialises them,
+so no per-launch duration of that form is reproducible). Per-GPU batch is fixed (weak scaling): rank r
+of N owns `--batch` frames of the N*batch global batch (BASELINE configs 3 and 5: 64 frames per GPU =
 config 5's share at N=8).
 
 Run:  python bench.py [--gpus N --steps K --warmup W]
@@ -16,9 +19,10 @@ f32 range (tests/test_gpu_range.py). fp16 and bf16 (2-byte storage) are sub-reco
 
 Rank 0 prints ONE JSON line. `roofline` describes the dominant kernel of the forward (largest total
 in-step time): the bytes one launch must move (block input read once, output written once) / its
-average launch duration IN THE STEP — HIP events recorded around every launch of shard 0 inside a
-captured copy of the timed 2-stream graph step (graph event-record nodes), the other shard running
-beside it as in the timed loop ("timing": "in-step") — against the 8 TB/s HBM peak; the isolated
+average launch duration IN THE STEP — each launch's first-workgroup entry to last-workgroup exit on
+the GPU's 100 MHz clock, recorded by the kernels themselves (bugseg_debug_set_spans) in a captured copy
+of the timed graph step ("timing": "in-step"; what rocprofv3's kernel trace reports per launch) —
+against the 8 TB/s HBM peak; the isolated
 figures (one shard alone on the GPU) sit beside it; `traffic` is the PMC-measured HBM bytes per launch
 of that kernel from the committed profile (profiles/pmc_traffic*.json). `roofline.forward` adds the
 whole-forward figures (SURVEY.md 8(d)'s 180.2 MB/frame per-layer definition and the plan's own byte
@@ -89,7 +93,7 @@ def kernel_table(ctx, B, H, W, reps, stream):
     return groups
 
 
-def pmc_traffic(tag, precision="fp16"):
+def pmc_traffic(tag, precision="fp16", frames=None):
     """HBM bytes per launch of `tag` from the committed PMC summary (profiles/pmc_traffic.json for the
     2-byte headline mode, profiles/pmc_traffic_fp32.json for the fp32 parity mode; written by
     scripts/pmc_summary.py from rocprofv3 FETCH_SIZE / WRITE_SIZE passes of this bench), or None."""
@@ -97,6 +101,8 @@ def pmc_traffic(tag, precision="fp16"):
     try:
         with open(p) as f:
             t = json.load(f)
+        if frames is not None and t.get("frames_per_launch", 32) != frames:
+            return None                  # a profile of another launch shape
         v = t.get("per_launch_bytes", {}).get(tag)
         return None if v is None else round(float(v))
     except (OSError, ValueError):
@@ -114,7 +120,8 @@ def parse():
     p.add_argument("--precision", default="fp32", choices=["bf16", "fp16", "fp32"],
                    help="precision of the timed step: fp32 (default; the reference's arithmetic, logits within 1e-3 "
                         "over the whole f32 range), fp16 / bf16 (2-byte storage throughput modes)")
-    p.add_argument("--streams", type=int, default=2, help="frame shards run concurrently on this many HIP streams")
+    p.add_argument("--streams", type=int, default=1,
+                   help="frame shards run concurrently on this many HIP streams (1: the whole batch per launch)")
     p.add_argument("--stream-priority", type=int, default=0, help="HIP priority of the side shards' streams")
     p.add_argument("--chain-forwards", type=int, default=0,
                    help="1: shard i's forward starts after shard i-1's (its BEV overlaps the next forward)")
@@ -267,78 +274,38 @@ def forward_ms(ctx, fs, Bs, H, W, seg, stream, reps):
     return ev[0].elapsed_time(ev[1]) / reps
 
 
-class HipEvents:
-    """Raw HIP events that, recorded inside a stream capture, become event-record nodes of the graph
-    (torch's Event.record only records a capture dependency there); timed with hipEventElapsedTime after
-    a replay. Bound to the HIP runtime torch loaded (libamdhip64.so.7, the soname libbugseg.so links)."""
-
-    def __init__(self, n):
-        import ctypes
-        self.ct = ctypes
-        self.hip = ctypes.CDLL("libamdhip64.so.7")
-        vp = ctypes.c_void_p
-        self.hip.hipEventCreate.argtypes = [ctypes.POINTER(vp)]
-        self.hip.hipEventRecord.argtypes = [vp, vp]
-        self.hip.hipEventElapsedTime.argtypes = [ctypes.POINTER(ctypes.c_float), vp, vp]
-        self.hip.hipEventDestroy.argtypes = [vp]
-        self.ev = []
-        for _ in range(n):
-            e = vp()
-            if self.hip.hipEventCreate(ctypes.byref(e)) != 0:
-                raise RuntimeError("hipEventCreate failed")
-            self.ev.append(e)
-
-    def record(self, i, stream):
-        """Outside a capture: hipEventRecord. Inside one: an event-record node spliced after the
-        capture's current dependencies (hipGraphAddEventRecordNode + hipStreamUpdateCaptureDependencies;
-        the HIP runtime torch ships rejects hipEventRecordWithFlags(External) while capturing)."""
-        ct, vp = self.ct, self.ct.c_void_p
-        s = vp(int(stream.cuda_stream))
-        status, cid, graph = ct.c_int(), ct.c_ulonglong(), vp()
-        deps, nd = ct.POINTER(vp)(), ct.c_size_t()
-        if self.hip.hipStreamGetCaptureInfo_v2(s, ct.byref(status), ct.byref(cid), ct.byref(graph),
-                                               ct.byref(deps), ct.byref(nd)) != 0:
-            raise RuntimeError("hipStreamGetCaptureInfo_v2 failed")
-        if status.value != 1:                                   # not capturing
-            if self.hip.hipEventRecord(self.ev[i], s) != 0:
-                raise RuntimeError("hipEventRecord failed")
-            return
-        node = vp()
-        darr = (vp * max(1, nd.value))(*[deps[k] for k in range(nd.value)])
-        if self.hip.hipGraphAddEventRecordNode(ct.byref(node), graph, darr, nd, self.ev[i]) != 0:
-            raise RuntimeError("hipGraphAddEventRecordNode failed")
-        if self.hip.hipStreamUpdateCaptureDependencies(s, (vp * 1)(node), ct.c_size_t(1), ct.c_uint(1)) != 0:
-            raise RuntimeError("hipStreamUpdateCaptureDependencies failed")
-
-    def ms(self, i, j):
-        t = self.ct.c_float()
-        if self.hip.hipEventElapsedTime(self.ct.byref(t), self.ev[i], self.ev[j]) != 0:
-            raise RuntimeError("hipEventElapsedTime failed")
-        return float(t.value)
-
-    def close(self):
-        for e in self.ev:
-            self.hip.hipEventDestroy(e)
-        self.ev = []
+SPAN_TICK_NS = 10.0      # s_memrealtime: the constant 100 MHz clock (mfma_common.h span_enter / span_exit)
 
 
 def instep_kernel_table(pipe, frames, H, W, reps):
-    """Per-launch durations IN THE STEP: a captured copy of the timed step (every shard's forward + BEV
-    on its own stream, as pipe.run launches them) in which shard 0's forward is issued launch by launch
-    with a HIP event-record node before each and after the last; replayed `reps` times, host-synced
-    after each replay to read the events. Grouped by kernel tag like kernel_table. Also returns the
-    instrumented step's ms (the event nodes' own cost shows as its excess over the plain step)."""
+    """Per-launch durations IN THE STEP, as the profiler defines a launch's duration (first workgroup
+    start to last workgroup end): a captured copy of the timed step (every shard's forward + BEV on its
+    own stream, as pipe.run launches them) in which shard 0's launches carry armed span slots
+    (bugseg_debug_set_spans: each workgroup folds the 100 MHz clock into [min entry, max exit]); replayed
+    `reps` times, slots reset before and read after each replay. Grouped by kernel tag like kernel_table.
+    Also returns the instrumented step's ms and shard 0's forward span."""
     from bugcar_image_segmentation_amd import _native as N
     dev = frames.device
     B, S = frames.shape[0], pipe.streams
-    ctxs, sts = pipe._shard_ctxs(dev)
+    if S > 1 and B >= S:
+        ctxs, sts = pipe._shard_ctxs(dev)
+    else:                                # one stream: the model's own context runs the whole batch
+        S, ctxs, sts = 1, [pipe.model.ctx], []
     _x, seg, g = pipe._bufs(B, dev)
     prm = pipe._params()
     bounds = [B * i // S for i in range(S + 1)]
     Bs = bounds[1]
     kind = N.OUT_CLASS3_U8
     n = ctxs[0].plan_info(Bs, H, W, kind, bgr_input=True)[0]
-    hev = HipEvents(n + 1)
+    spans = torch.zeros((n, 64, 8), dtype=torch.int64, device=dev)   # 64 slots of [entry, exit] per op, 64 B apart
+
+    def reset():
+        spans[:, :, 0].fill_(-1)         # UINT64_MAX: the entry slots take a min
+        spans[:, :, 1].zero_()
+
+    def read():
+        sp = spans.cpu().numpy().view(np.uint64)
+        return sp[:, :, 0].min(1), sp[:, :, 1].max(1)
 
     def step():
         main = torch.cuda.current_stream(dev)
@@ -348,23 +315,20 @@ def instep_kernel_table(pipe, frames, H, W, reps):
             st = main if i == 0 else sts[i - 1]
             if i:
                 st.wait_event(ready)
-            with torch.cuda.stream(st):
-                if i == 0:
-                    for op in range(n):
-                        hev.record(op, st)
-                        ctxs[0].forward_bgr_ops(frames[s0:e0], e0 - s0, H, W, kind, seg[s0:e0], op, op + 1, st)
-                    hev.record(n, st)
-                else:
-                    ctxs[i].forward_bgr(frames[s0:e0], e0 - s0, H, W, kind, seg[s0:e0], st)
-                ctxs[i].bev(seg[s0:e0], e0 - s0, prm, g[s0:e0], st)
+            ctxs[i].forward_bgr(frames[s0:e0], e0 - s0, H, W, kind, seg[s0:e0], st)
+            ctxs[i].bev(seg[s0:e0], e0 - s0, prm, g[s0:e0], st)
         for st in sts[: S - 1]:
             main.wait_stream(st)
 
-    step()
-    torch.cuda.synchronize()
-    graph = torch.cuda.CUDAGraph()
-    with torch.cuda.graph(graph):
+    ctxs[0].set_spans(spans)
+    try:
         step()
+        torch.cuda.synchronize()
+        graph = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(graph):
+            step()
+    finally:
+        ctxs[0].set_spans(None)          # (launches outside this graph stay unarmed)
     for _ in range(3):
         graph.replay()
     torch.cuda.synchronize()
@@ -373,21 +337,36 @@ def instep_kernel_table(pipe, frames, H, W, reps):
         graph.replay()
     torch.cuda.synchronize()
     step_ms = (time.perf_counter() - t0) / reps * 1e3
-    tot = [0.0] * (n + 1)
+    tot = np.zeros(n)
+    fwd = 0.0
     for _ in range(reps):
+        reset()
         graph.replay()
         torch.cuda.synchronize()
-        for i in range(n):
-            tot[i] += hev.ms(i, i + 1)
-        tot[n] += hev.ms(0, n)
-    hev.close()
+        st, en = read()
+        tot += (en - st).astype(np.float64) * SPAN_TICK_NS * 1e-3
+        fwd += float(en[n - 1] - st[0]) * SPAN_TICK_NS * 1e-6
     del graph
+    # the clock check: shard 0's forward alone, its launch spans against HIP events around it
+    ev = [torch.cuda.Event(enable_timing=True) for _ in range(2)]
+    main = torch.cuda.current_stream(dev)
+    ctxs[0].set_spans(spans)
+    try:
+        reset()
+        ev[0].record(main)
+        ctxs[0].forward_bgr(frames[:Bs], Bs, H, W, kind, seg[:Bs], main)
+        ev[1].record(main)
+        ev[1].synchronize()
+    finally:
+        ctxs[0].set_spans(None)
+    st, en = read()
+    clock_check = float(en[n - 1] - st[0]) * SPAN_TICK_NS * 1e-6 / ev[0].elapsed_time(ev[1])
     groups = {}
     for i in range(n):
         tag, _lb, pb, fl = ctxs[0].plan_op(Bs, H, W, i)
         gr = groups.setdefault(tag, {"launches": 0, "total_us": 0.0, "bytes": 0.0, "flops": 0.0})
         gr["launches"] += 1
-        gr["total_us"] += tot[i] / reps * 1e3
+        gr["total_us"] += tot[i] / reps
         gr["bytes"] += pb
         gr["flops"] += fl
     groups.pop("fused", None)
@@ -395,7 +374,9 @@ def instep_kernel_table(pipe, frames, H, W, reps):
         gr["us_per_launch"] = gr["total_us"] / gr["launches"]
         gr["bytes_per_launch"] = gr["bytes"] / gr["launches"]
         gr["flops_per_launch"] = gr["flops"] / gr["launches"]
-    return groups, {"instrumented_step_ms": round(step_ms, 4), "shard0_forward_ms": round(tot[n] / reps, 4)}
+    return groups, {"instrumented_step_ms": round(step_ms, 4), "shard0_forward_ms": round(fwd / reps, 4),
+                    "shard0_sum_of_launch_spans_ms": round(float(tot.sum()) / reps * 1e-3, 4),
+                    "span_clock_check": round(clock_check, 4)}
 
 
 def roofline_record(ctx, Bs, H, W, reps, stream, precision, t_fwd, instep=None):
@@ -420,13 +401,16 @@ def roofline_record(ctx, Bs, H, W, reps, stream, precision, t_fwd, instep=None):
     k_tf = k_flops / (k["us_per_launch"] * 1e-6) / 1e12
     t_fwd_instep = meta["shard0_forward_ms"] if meta else t_fwd
     fwd_tf = flops / (t_fwd_instep * 1e-3) / 1e12
-    timing = ("in-step: HIP event-record nodes around each launch of shard 0 inside a captured copy of the "
-              "timed 2-stream graph step (the other shard beside it, as timed); `isolated` = the same launch "
-              "with that shard alone on the GPU") if meta else "isolated: one shard alone on the GPU"
+    timing = ("in-step: each launch of the timed step's first shard (with --streams 1, the default, the whole "
+              "batch) from its first workgroup's entry to its last workgroup's exit (the 100 MHz GPU clock, "
+              "bugseg_debug_set_spans) in a captured copy of the timed graph step, any other shards running beside "
+              "it as timed — the duration rocprofv3's kernel trace reports for a launch; `isolated` = HIP events "
+              "around the same launch alone; instep.span_clock_check = that shard's forward alone, spans / events"
+              ) if meta else "isolated: one shard alone on the GPU"
     rec = {
         "bound": "hbm", "achieved": round(k_achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
         "frac": round(k_achieved / HBM_PEAK_GBS, 4),
-        "traffic": pmc_traffic(tag, precision),
+        "traffic": pmc_traffic(tag, precision, Bs),
         "kernel": f"{KERNEL_NAMES.get(tag.rsplit(' ', 1)[0], tag).format(t=TEMPLATE_TYPE[precision])} [{tag}]: the dominant kernel of the forward "
                   f"({k['launches']} launches, {k['total_us']:.0f} us of {t_fwd_instep * 1e3:.0f} us in step); "
                   f"{k['bytes_per_launch'] / 1e6:.1f} MB per launch = the bytes the launch must move "
@@ -487,7 +471,7 @@ def mode_record(blocks, bev, grid, H, W, frames, streams, steps, precision, grap
     stream = torch.cuda.current_stream()
     Bs = B // streams if streams > 1 and B >= streams else B
     _x, seg, _g = pipe._bufs(B, frames.device)
-    instep = instep_kernel_table(pipe, frames, H, W, 10) if streams > 1 and B >= streams else None
+    instep = instep_kernel_table(pipe, frames, H, W, 10)
     t_fwd = forward_ms(model.ctx, frames[:Bs], Bs, H, W, seg[:Bs], stream, 10)
     roof, table = roofline_record(model.ctx, Bs, H, W, 10, stream, precision, t_fwd, instep)
     del pipe, model
@@ -657,6 +641,10 @@ def main():
         if not gather_check:
             raise RuntimeError("all-gathered occupancy grids do not hold the ranks' own grids")
         torch.cuda.synchronize()
+    # a one-element int16 fill on either side of the timed region (outside its synchronisation): the
+    # markers scripts/prof_summary.py finds in a kernel trace to pick out the timed loop's launches
+    marker = torch.empty(1, dtype=torch.int16, device=dev)
+    marker.fill_(1)
     if dist_on:
         dist.barrier()
     torch.cuda.synchronize()
@@ -667,6 +655,7 @@ def main():
     if dist_on:
         dist.barrier()
     el = time.perf_counter() - t0
+    marker.fill_(2)
     if dist_on:
         t = torch.tensor([el], dtype=torch.float64, device=dev if a.backend == "nccl" else "cpu")
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
@@ -710,7 +699,7 @@ def main():
     bev.laserscan_like_occupancy_grid = False
     overlap = shard_overlap(pipe, frames, seg, g, bev, grid, H, W, reps) if a.streams > 1 and B >= a.streams else None
     log("in-step kernel table")
-    instep = instep_kernel_table(pipe, frames, H, W, reps) if a.streams > 1 and B >= a.streams else None
+    instep = instep_kernel_table(pipe, frames, H, W, reps)
     roof, ktable = roofline_record(model.ctx, Bs, H, W, reps, stream, a.precision, t_fwd, instep)
 
     if rank == 0:
@@ -737,6 +726,11 @@ def main():
         }
         extras = a.extras if a.extras >= 0 else int(world == 1)
         if extras:
+            if a.streams == 1:
+                # the same step as two frame shards on two streams (more throughput from the kernels' tails
+                # overlapping, but no per-launch duration a profiler reproduces: it serialises the streams)
+                log("two-stream sub-record")
+                res["two_streams"] = mode_record(blocks, bev, grid, H, W, frames, 2, max(10, a.steps), a.precision, bool(a.graph))
             for prec in ("fp32", "fp16", "bf16"):
                 if prec != a.precision:
                     log(f"{prec} sub-record")

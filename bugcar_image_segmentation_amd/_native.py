@@ -28,7 +28,7 @@ EXPORTED = ("bugseg_version", "bugseg_create", "bugseg_destroy", "bugseg_load_we
             "bugseg_last_error",
             "bugseg_dl_create", "bugseg_dl_destroy", "bugseg_dl_load_weights", "bugseg_dl_set_plan",
             "bugseg_dl_forward", "bugseg_dl_launch_op", "bugseg_dl_read_buffer", "bugseg_dl_last_error",
-            "bugseg_debug_parse_pack", "bugseg_debug_polar_tables", "bugseg_debug_ctx_info", "bugseg_dl_debug_check_plan")
+            "bugseg_debug_parse_pack", "bugseg_debug_polar_tables", "bugseg_debug_ctx_info", "bugseg_debug_set_spans", "bugseg_dl_debug_check_plan")
 DL_OP_FIELDS = 32
 
 
@@ -94,6 +94,7 @@ def load_library(path: Path | str | None = None) -> ctypes.CDLL:
             "bugseg_debug_parse_pack": (i, [vp, sz, i, ctypes.POINTER(i)]),
             "bugseg_debug_polar_tables": (i, [i, i, i, vp, sz, vp, sz, ctypes.POINTER(i), ctypes.POINTER(i)]),
             "bugseg_debug_ctx_info": (i, [vp, i, i]),
+            "bugseg_debug_set_spans": (i, [vp, vp]),
             "bugseg_dl_debug_check_plan": (i, [vp, i, vp, i, i, i, i, i, sz]),
         }
         for name, (res, args) in proto.items():
@@ -218,6 +219,11 @@ class Context:
         """Test hook (bugseg_debug_ctx_info): 0 = exact affine byte normalisation in use, 1 = fp32 range
         scaling off, 2 = weight exponent of packed convolution `arg`."""
         return int(self.lib.bugseg_debug_ctx_info(self.h, what, arg))
+
+    def set_spans(self, spans=None):
+        """Measurement hook (bugseg_debug_set_spans): a CUDA int64 tensor of 512 words per plan op (64
+        [entry, exit] slots, 64 B apart) that later launches fold their clock into (None disarms)."""
+        check(self.lib.bugseg_debug_set_spans(self.h, ctypes.c_void_p(spans.data_ptr() if spans is not None else 0)), self.h)
 
 
 _shared: dict[int, Context] = {}

@@ -313,6 +313,7 @@ __global__ void __launch_bounds__((BShape<C, V>::NW * 64), (sizeof(T) == 2 ? BSh
         else st4(p, v);
     };
 
+    span_enter(a.span);
     STAMP_ENTRY(0);
     // a workgroup without a tile leaves before staging anything (an LDS-DMA still in flight when
     // its wave ends would land in LDS the next workgroup on the CU already owns)
@@ -1303,6 +1304,7 @@ __global__ void __launch_bounds__((BShape<C, V>::NW * 64), (sizeof(T) == 2 ? BSh
         STAMP(6);
     }
     if constexpr (F32) rng_commit(amo, a.rg.amax_out);
+    span_exit(a.span);
     STAMP_ENTRY(1);
 }
 

@@ -86,6 +86,7 @@ struct ConvArgs {
     int cpr_sh;          // log2(outC / (16 B / elem)): 16-B chunks per output pixel (power of two)
     int slopes_le1;      // every slope1 / slope2 <= 1: PReLU as max(v, s*v)
     RangeArgs rg;        // fp32 mode: the input's measured range, sw[0] = the weights' exponent
+    unsigned long long *span;   // launch span (bugseg_debug_set_spans): [min entry, max exit] clock, or null
 };
 
 // magic number for fdiv (mfma_common.h): divisor d >= 1
@@ -137,6 +138,7 @@ struct BneckArgs {
     int idxCS;
     uint32_t xin_bytes, pool_bytes, idx_bytes;
     RangeArgs rg;        // fp32 mode: sw = {w1, w2, w2b, w3}; n / c: t0, t1 (asym: t1a), t1 (asym)
+    unsigned long long *span;   // launch span (bugseg_debug_set_spans), or null
 };
 // tile-shape variants of the fused kernel for C channels: 0 .. bneck_variants(C) - 1
 int bneck_variants(int C);
@@ -161,6 +163,7 @@ struct UpArgs {
     uint32_t x_bytes, idx_bytes, out_bytes;
     int slopes_le1;
     RangeArgs rg;             // fp32 mode: sw = {pair, tconv, expansion}; n / c: e1 output, tconv output
+    unsigned long long *span; // launch span (bugseg_debug_set_spans), or null
 };
 bool up_supported(int cin, int it, int cout);
 hipError_t launch_up(int prec, int cin, int it, int cout, const UpArgs &a, hipStream_t s);

@@ -157,6 +157,7 @@ struct bugseg_ctx {
     bool naff_on = false;
     float norm_amax = 0.f;                         // max |table| (the BGR input's range, fp32 range scaling)
     bool range_off = false;                        // BUGSEG_F32_RANGE=0 at load_weights: no fp32 range scaling (A/B)
+    unsigned long long *spans = nullptr;           // bugseg_debug_set_spans: 512 u64 of launch-span slots per op, or null
     std::string err;
     bool loaded = false;
     int ncls = 0;
@@ -1510,6 +1511,16 @@ int bugseg_nchw_to_input(bugseg_ctx *ctx, const void *x, int is_f64, int B, int 
     return BUGSEG_OK;
 }
 
+// one plan op, with its launch-span slots when bugseg_debug_set_spans armed them
+static hipError_t launch_op(const bugseg_ctx *ctx, const Op &o, int i, hipStream_t s) {
+    unsigned long long *sp = ctx->spans ? ctx->spans + 512 * (size_t)i : nullptr;   // (mfma_common.h: 64 slots x 64 B)
+    if (o.kind == 1) { BneckArgs q = o.bn; q.span = sp; return launch_bneck(ctx->prec, o.bn_c, o.bn_asym, o.bn_var, q, s, o.bn_cin); }
+    if (o.kind == 2) { UpArgs q = o.up; q.span = sp; return launch_up(ctx->prec, o.up_cin, o.up_it, o.up_cout, q, s); }
+    ConvArgs q = o.a;
+    q.span = sp;
+    return launch_conv(ctx->prec, o.nr, o.epi, q, s);
+}
+
 static int enet_forward(bugseg_ctx *ctx, const void *in, bool bgr, int B, int H, int W, int out_kind, void *out,
                         void *stream, int first_op = 0, int last_op = -1) {
     if (!ctx || !in || !out) return fail(ctx, BUGSEG_EINVAL, "NULL argument");
@@ -1549,10 +1560,7 @@ static int enet_forward(bugseg_ctx *ctx, const void *in, bool bgr, int B, int H,
         if (e != hipSuccess) return fail(ctx, BUGSEG_EHIP, std::string("range words: ") + hipGetErrorString(e));
     }
     for (int i = first_op; i < last_op; ++i) {
-        const Op &op = pl.ops[(size_t)i];
-        hipError_t e = op.kind == 1 ? launch_bneck(ctx->prec, op.bn_c, op.bn_asym, op.bn_var, op.bn, (hipStream_t)stream, op.bn_cin)
-                     : op.kind == 2 ? launch_up(ctx->prec, op.up_cin, op.up_it, op.up_cout, op.up, (hipStream_t)stream)
-                                    : launch_conv(ctx->prec, op.nr, op.epi, op.a, (hipStream_t)stream);
+        hipError_t e = launch_op(ctx, pl.ops[(size_t)i], i, (hipStream_t)stream);
         if (e != hipSuccess) return fail(ctx, BUGSEG_EHIP, "conv launch " + std::to_string(i) + ": " + hipGetErrorString(e));
     }
     return BUGSEG_OK;
@@ -1897,6 +1905,12 @@ int bugseg_debug_parse_pack(const void *blob, size_t bytes, int precision, int *
     return BUGSEG_OK;
 }
 
+int bugseg_debug_set_spans(bugseg_ctx *ctx, void *spans) {
+    if (!ctx) return fail(ctx, BUGSEG_EINVAL, "NULL ctx");
+    ctx->spans = (unsigned long long *)spans;
+    return BUGSEG_OK;
+}
+
 int bugseg_debug_ctx_info(const bugseg_ctx *ctx, int what, int arg) {
     if (!ctx) return -1;
     switch (what) {
@@ -1996,10 +2010,7 @@ int bugseg_plan_launch_op(bugseg_ctx *ctx, int B, int H, int W, int op, void *st
         return fail(ctx, BUGSEG_ESTATE, "no forward has run at these dimensions");
     if (op < 0 || op >= (int)pl.ops.size()) return fail(ctx, BUGSEG_EINVAL, "op index out of range");
     DeviceGuard g(ctx->device);
-    const Op &o = pl.ops[op];
-    hipError_t e = o.kind == 1 ? launch_bneck(ctx->prec, o.bn_c, o.bn_asym, o.bn_var, o.bn, (hipStream_t)stream, o.bn_cin)
-                 : o.kind == 2 ? launch_up(ctx->prec, o.up_cin, o.up_it, o.up_cout, o.up, (hipStream_t)stream)
-                               : launch_conv(ctx->prec, o.nr, o.epi, o.a, (hipStream_t)stream);
+    hipError_t e = launch_op(ctx, pl.ops[op], op, (hipStream_t)stream);
     if (e != hipSuccess) return fail(ctx, BUGSEG_EHIP, "launch of op " + std::to_string(op) + ": " + hipGetErrorString(e));
     return BUGSEG_OK;
 }

@@ -76,6 +76,7 @@ template <> struct ClsGroups<2> { static constexpr int N = 2; static constexpr u
                                   static constexpr int val[3] = {1, 0, 0}; };
 template <typename T, bool LOGITS, int LK = 0>
 __global__ void __launch_bounds__(256, sizeof(T) == 2 ? 4 : 1) cls_kernel(const ConvArgs a) {
+    span_enter(a.span);
     constexpr int CLS_TAPS = 4;
     using Raw = typename Tr<T>::Raw;
     using WRaw = typename WTr<T>::Raw;   // weight operand (fp32 mode: split-f16 parts)
@@ -331,6 +332,7 @@ __global__ void __launch_bounds__(256, sizeof(T) == 2 ? 4 : 1) cls_kernel(const 
         step(g, xb, xa, qb, qa);
         g += nw;
     }
+    span_exit(a.span);
 }
 
 // 16 input channels in two 8-channel groups per tap, the 4 taps of the k = 3 layer (Kpad = 4 x 16: a

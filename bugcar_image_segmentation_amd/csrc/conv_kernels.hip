@@ -52,6 +52,7 @@ constexpr int TAP_PAD = -(1 << 24);    // row offset of a padding k group / an i
 // occupancy is worth a few registers; fp32 (parity mode) is left to the compiler.
 template <typename T, int NR, int EPI>
 __global__ void __launch_bounds__(256, sizeof(T) == 2 ? (NR == 8 ? 3 : 4) : 1) conv_kernel(const ConvArgs a) {
+    span_enter(a.span);
     constexpr int MR = Cfg<NR>::MR;
     constexpr int TILE = 4 * MR * 16;
     constexpr int ES = (int)sizeof(T), EPC = 16 / ES;
@@ -407,6 +408,7 @@ __global__ void __launch_bounds__(256, sizeof(T) == 2 ? (NR == 8 ? 3 : 4) : 1) c
         }
     }
     if constexpr (F32) rng_commit(amo, a.rg.amax_out);
+    span_exit(a.span);
 }
 
 int conv_tile_pixels(int nr) { return 4 * (nr >= 4 ? 2 : 4) * 16; }

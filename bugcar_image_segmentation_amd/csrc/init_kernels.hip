@@ -63,6 +63,7 @@ __device__ __forceinline__ void init_k(int kq, int j, int &dy, int &e) {
 
 template <typename T, bool BGR>
 __global__ void __launch_bounds__(256, sizeof(T) == 2 ? INIT_OCC2 : 1) init_kernel(const ConvArgs a) {   // (fp16 with the packed pool took 82 registers: 5 waves per SIMD)
+    span_enter(a.span);
     // INIT_DB: two patch buffers — the next tile's patch is stored while this one is computed, one
     // barrier per tile instead of two
     __shared__ __attribute__((aligned(16))) T patch_buf[(INIT_DB ? 2 : 1) * IP_PATCH];
@@ -353,6 +354,7 @@ __global__ void __launch_bounds__(256, sizeof(T) == 2 ? INIT_OCC2 : 1) init_kern
         }
     }
     if constexpr (F32) rng_commit(amo, a.rg.amax_out);
+    span_exit(a.span);
 }
 
 // The exact affine form of the normalisation table (bf16 / fp16 storage): candidate k of channel c is the

@@ -378,6 +378,21 @@ __device__ __forceinline__ void to_bop(RawF &r, float4 qa, float4 qb) {
     r.b = make_float4(__uint_as_float(b[0]), __uint_as_float(b[1]), __uint_as_float(b[2]), __uint_as_float(b[3]));
 }
 
+// Launch spans (bugseg_debug_set_spans; null in normal runs — one scalar test per workgroup): thread 0
+// of every workgroup folds the constant 100 MHz clock (s_memrealtime, one time base across XCDs) into
+// its slot's [0] at entry (min) and [1] at exit (max) — 64 slots, 64 B apart, by workgroup index, so
+// the atomics do not queue on one address — and the host's min / max over the slots is the launch's
+// duration as the profiler defines it (first workgroup start to last workgroup end).
+constexpr int SPAN_SLOTS = 64, SPAN_STRIDE = 8;     // u64 per slot stride (64 B)
+__device__ __forceinline__ void span_enter(unsigned long long *s) {
+    if (s && threadIdx.x == 0)
+        atomicMin(s + (blockIdx.x & (SPAN_SLOTS - 1)) * SPAN_STRIDE, (unsigned long long)__builtin_amdgcn_s_memrealtime());
+}
+__device__ __forceinline__ void span_exit(unsigned long long *s) {
+    if (s && threadIdx.x == 0)
+        atomicMax(s + (blockIdx.x & (SPAN_SLOTS - 1)) * SPAN_STRIDE + 1, (unsigned long long)__builtin_amdgcn_s_memrealtime());
+}
+
 // ---- fp32 mode range scaling (round 5; bugseg_internal.h RangeArgs). Exponents are clamped to
 // [-RNG_EMAX, RNG_EMAX] (tensors of max |v| in [2^-26, 2^54] are scaled exactly into the window; beyond
 // that the split degrades gracefully) so every multiplier, a difference of two exponents plus a weight

@@ -35,6 +35,7 @@ __host__ __device__ constexpr int up_threads() { return sizeof(T) == 2 && CIN >=
 
 template <typename T, int CIN, int I, int COUT>
 __global__ void __launch_bounds__((up_threads<T, CIN>()), (sizeof(T) == 2 ? (CIN >= 128 ? (UP_NT128 == 512 ? 4 : 2) : 3) : 1)) up_kernel(const UpArgs a) {
+    span_enter(a.span);
     using Raw = typename Tr<T>::Raw;
     using WRaw = typename WTr<T>::Raw;   // weight operand (fp32 mode: split-f16 parts)
     constexpr int ES = (int)sizeof(T);
@@ -258,6 +259,7 @@ __global__ void __launch_bounds__((up_threads<T, CIN>()), (sizeof(T) == 2 ? (CIN
         }
     }
     if constexpr (F32) rng_commit(amo, a.rg.amax_out);
+    span_exit(a.span);
 }
 
 template <typename T, int CIN, int I, int COUT>

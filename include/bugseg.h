@@ -201,6 +201,13 @@ int bugseg_debug_polar_tables(int w, int h, int variant, int32_t *fmap, size_t f
  * 2: the weights' exponent of packed convolution `arg` (fp32 range scaling; -1000 if no such conv).
  * Returns -1 for an unknown `what` or a NULL ctx. */
 int bugseg_debug_ctx_info(const bugseg_ctx *ctx, int what, int arg);
+/* Measurement hook (bench.py's in-step kernel table): arm launch spans. spans = device memory of
+ * 512 x uint64 per plan op (NULL disarms): 64 slots 64 B apart, slot k = [k*8] entry, [k*8+1] exit;
+ * every later launch of op i folds the constant 100 MHz GPU clock into the slots of op i (workgroup w
+ * into slot w % 64: min at entry, max at exit) — the caller sets entries to UINT64_MAX and exits to 0
+ * before the run it reads and takes the min / max over the slots. Launches already captured keep
+ * their slots. */
+int bugseg_debug_set_spans(bugseg_ctx *ctx, void *spans);
 
 /* ---- DeepLabV3 (BASELINE config 4) -------------------------------------
  * Replaces DeepLabV3 (models.py:98-136): tf.compat.v1.Session + GraphDef import (models.py:105-113)

@@ -10,7 +10,7 @@ well defined.
 Writes a markdown table and profiles/pmc_traffic.json ({"per_launch_bytes": {tag: bytes}}), which
 bench.py reports as roofline.traffic for its dominant kernel.
 
-usage: python scripts/pmc_summary.py gpurun_out/<tag> [out.md] [out.json]
+usage: python scripts/pmc_summary.py gpurun_out/<tag> [out.md] [out.json] [frames per launch]
 """
 import csv
 import json
@@ -30,7 +30,7 @@ def per_kernel(path, counter):
     return vals
 
 
-def main(tag_dir, out_md=None, out_json=None):
+def main(tag_dir, out_md=None, out_json=None, frames=None):
     d = Path(tag_dir)
     fetch = per_kernel(next((d / "fetch").glob("*counter_collection.csv")), "FETCH_SIZE")
     write = per_kernel(next((d / "write").glob("*counter_collection.csv")), "WRITE_SIZE")
@@ -51,9 +51,10 @@ def main(tag_dir, out_md=None, out_json=None):
         Path(out_md).write_text(text + "\n")
     if out_json:
         Path(out_json).write_text(json.dumps({"source": str(d), "correction": "FETCH_SIZE x2 (gfx950)",
+                                              "frames_per_launch": int(frames) if frames else None,
                                               "per_launch_bytes": per}, indent=1) + "\n")
     return per
 
 
 if __name__ == "__main__":
-    main(*sys.argv[1:4])
+    main(*sys.argv[1:5])

@@ -39,6 +39,26 @@ def main(prof_dir, bench_json, out_md):
               "| tag | launches | avg us | total ms |", "|---|---|---|---|"]
     for tag, v in sorted(by.items(), key=lambda kv: -sum(kv[1])):
         lines.append(f"| {tag} | {len(v)} | {sum(v) / len(v):.2f} | {sum(v) / 1e3:.3f} |")
+    # the timed loop alone: bench.py fills a one-element int16 tensor right before and right after it
+    marks = sorted(int(r["Start_Timestamp"]) for r in trace if "FillFunctor<short>" in r["Kernel_Name"])
+    if len(marks) >= 2:
+        t0, t1 = marks[0], marks[1]
+        win = defaultdict(list)
+        for r in trace:
+            st = int(r["Start_Timestamp"])
+            if t0 < st < t1:
+                win[short(r["Kernel_Name"])].append((int(r["End_Timestamp"]) - st) / 1e3)
+        lines += ["", f"## the timed loop only (launches between bench.py's two marker fills, {(t1 - t0) / 1e6:.3f} ms)", "",
+                  "| tag | launches | avg us | min us | max us | total ms |", "|---|---|---|---|---|---|"]
+        for tag, v in sorted(win.items(), key=lambda kv: -sum(kv[1])):
+            lines.append(f"| {tag} | {len(v)} | {sum(v) / len(v):.2f} | {min(v):.2f} | {max(v):.2f} | {sum(v) / 1e3:.3f} |")
+        if bench:
+            rl = bench.get("roofline", {})
+            tag = rl.get("kernel", "").split("[")[-1].split("]")[0]
+            if tag in win and rl.get("us_per_launch"):
+                avg = sum(win[tag]) / len(win[tag])
+                lines += ["", f"bench `roofline.us_per_launch` {rl['us_per_launch']:.2f} us vs the timed loop's "
+                              f"{tag} average {avg:.2f} us: ratio {rl['us_per_launch'] / avg:.3f}"]
     if bench:
         rl = bench.get("roofline", {})
         lines += ["", "## bench line of the same command", "",
