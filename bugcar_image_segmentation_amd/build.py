@@ -37,15 +37,20 @@ def _stale(target: Path, deps) -> bool:
     return any(Path(d).stat().st_mtime > t for d in deps)
 
 
-def build_native(force: bool = False, verbose: bool = False, stamps: bool = False) -> Path:
+def build_native(force: bool = False, verbose: bool = False, stamps: bool = False, variant: str = "",
+                 defines=()) -> Path:
     """stamps=True: the debug variant libbugseg_stamps.so (-DBUGSEG_STAMPS: in-kernel phase clocks,
-    scripts/stamp_probe.py); never loaded by the product path."""
-    obj_dir = OBJ / "stamps" if stamps else OBJ
-    lib = PKG / "libbugseg_stamps.so" if stamps else LIB
+    scripts/stamp_probe.py); variant="name" with defines=("-DX=1", ...): an A/B build
+    libbugseg_<name>.so (loaded through BUGSEG_LIB by measurement scripts). Neither is loaded by the
+    product path."""
+    if stamps:
+        variant, defines = "stamps", ("-DBUGSEG_STAMPS", *defines)
+    obj_dir = OBJ / variant if variant else OBJ
+    lib = PKG / f"libbugseg_{variant}.so" if variant else LIB
     obj_dir.mkdir(parents=True, exist_ok=True)
     hipcc = _hipcc()
     flags = [f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-Wall", "-Wno-unused-function",
-             f"-I{ROOT / 'include'}", f"-I{CSRC}"] + (["-DBUGSEG_STAMPS"] if stamps else [])
+             f"-I{ROOT / 'include'}", f"-I{CSRC}", *defines]
     jobs = []
     for s in SOURCES:
         src = CSRC / s
@@ -77,4 +82,6 @@ def build_native(force: bool = False, verbose: bool = False, stamps: bool = Fals
 
 
 if __name__ == "__main__":
-    print(build_native(force="--force" in sys.argv, verbose=True, stamps="--stamps" in sys.argv))
+    var = next((a.split("=", 1)[1] for a in sys.argv if a.startswith("--variant=")), "")
+    print(build_native(force="--force" in sys.argv, verbose=True, stamps="--stamps" in sys.argv, variant=var,
+                       defines=tuple(a for a in sys.argv if a.startswith("-D"))))

@@ -153,8 +153,45 @@ void bneck_shape(int C, int v, int &th, int &tw, int &nw, int *rd) {
 #ifndef BNECK_F32_OCC128
 #define BNECK_F32_OCC128 1
 #endif
-template <typename T, int C, bool ASYM, int V, bool TR, int CI = 0>
-__global__ void __launch_bounds__((BShape<C, V>::NW * 64), (sizeof(T) == 2 ? BShape<C, V>::OCC : C == 16 ? BNECK_F32_OCC16 : C == 64 ? BNECK_F32_OCC64 : BNECK_F32_OCC128)) bneck_kernel(const BneckArgs a) {
+// fp32 mode range scaling (bugseg_internal.h RangeArgs, mfma_common.h): the exponents of x (measured by
+// the launch that wrote it), t0, t1 (asymmetric: t1a, t1; rigorous bounds from x's range), as the
+// multipliers of the accumulators. `any`: some multiply is needed — the asymmetric 1x5's output aside,
+// whose exponent each tile decides from its own t1a. The kernel runs the body instantiated with no
+// multiply at all first (SCL = false: the unscaled instruction stream; the scaled one measured 8% slower
+// on the forward with every multiplier 1, round 5); that body reads the range only once its first
+// tile's loads are in flight (a wait for the range words alone at kernel start cost the C128 launches
+// ~4 us) and, if some exponent is non-zero, drains its loads and returns before computing anything —
+// the kernel then runs the scaled body from the start.
+struct BneckRange {
+    float xm = 1.f, b1m = 1.f, o1m = 1.f, b2m = 1.f, o2m = 1.f, b2bm = 1.f, o2bm = 1.f, b3m = 1.f, o3m = 1.f;
+    int rs1 = 0, re2b = 0;                            // asymmetric: t1a's exponent, the 1x5's accumulator exponent
+    bool scl = false, any = false;                    // scl: phase 3 multiplies (e3 != 0)
+};
+template <bool ASYM>
+__device__ __forceinline__ BneckRange bneck_range(const RangeArgs &g, float amx) {
+    BneckRange r;
+    if (g.off) return r;
+    const int sx = rng_exp_meas(amx), e1 = sx + g.sw[0];
+    const float B0 = g.n[0] * amx + g.c[0];
+    const int s0 = rng_exp_bound(B0, e1), e2 = s0 + g.sw[1];
+    const float B1 = g.n[1] * B0 + g.c[1];
+    const int s1 = rng_exp_bound(B1, e2);
+    int e2b = 0, s1b = 0;
+    if constexpr (ASYM) {
+        e2b = s1 + g.sw[2];
+        s1b = rng_exp_bound(g.n[2] * B1 + g.c[2], e2b);
+    }
+    const int e3 = (ASYM ? s1b : s1) + g.sw[3];
+    r.rs1 = s1; r.re2b = e2b;
+    r.scl = e3 != 0;
+    r.xm = rng_pow2(sx); r.b1m = rng_pow2(e1); r.o1m = rng_pow2(s0 - e1); r.b2m = rng_pow2(e2); r.o2m = rng_pow2(s1 - e2);
+    r.b2bm = rng_pow2(e2b); r.o2bm = rng_pow2(s1b - e2b); r.b3m = rng_pow2(e3); r.o3m = rng_pow2(-e3);
+    r.any = (sx | e1 | s0 | e2 | s1) != 0 || (ASYM ? (e2b != 0 || g.sw[3] != 0) : e3 != 0);
+    return r;
+}
+
+template <typename T, int C, bool ASYM, int V, bool TR, int CI, bool SCL>
+__device__ __forceinline__ bool bneck_body(const BneckArgs &a, float rlane) {
     using Raw = typename Tr<T>::Raw;
     using WRaw = typename WTr<T>::Raw;   // weight operand (fp32 mode: split-f16 parts)
     constexpr int TH = BShape<C, V>::TH, TW = BShape<C, V>::TW, NW = BShape<C, V>::NW, NT = NW * 64;
@@ -319,7 +356,7 @@ __global__ void __launch_bounds__((BShape<C, V>::NW * 64), (sizeof(T) == 2 ? BSh
     // its wave ends would land in LDS the next workgroup on the CU already owns)
     {
         const int ch = (a.ntiles + 7) >> 3, sl = (int)(blockIdx.x >> 3);
-        if (sl >= ch || (int)(blockIdx.x & 7) * ch + sl >= a.ntiles) return;   // (the tile walk's first tile)
+        if (sl >= ch || (int)(blockIdx.x & 7) * ch + sl >= a.ntiles) return true;   // (the tile walk's first tile)
     }
     const int tid = threadIdx.x;
     const int lane = tid & 63, col = lane & 15, kq = lane >> 4;
@@ -452,43 +489,19 @@ __global__ void __launch_bounds__((BShape<C, V>::NW * 64), (sizeof(T) == 2 ? BSh
     const int dt = a.dt;                              // tiling dilation (1 for asymmetric blocks)
     constexpr bool tr = TR && !ASYM;                  // transposed tile
 
-    // fp32 mode range scaling (bugseg_internal.h RangeArgs, mfma_common.h): the exponents of x (measured
-    // by the launch that wrote it), t0, t1 (asymmetric: t1a, t1; rigorous bounds from x's range) and
-    // the multipliers of the accumulators; scl is false — no multiply anywhere — when every exponent is 0
     constexpr bool F32 = sizeof(T) == 4;
-
-    bool scl = false;
-    float xm = 1.f, b1m = 1.f, o1m = 1.f, b2m = 1.f, o2m = 1.f, b2bm = 1.f, o2bm = 1.f, b3m = 1.f, o3m = 1.f;
+    BneckRange rg0;                                   // SCL = false: every exponent 0 (checked at the first tile)
+    if constexpr (F32 && SCL) rg0 = bneck_range<ASYM>(a.rg, rng_reduce(rlane));
+    bool scl = rg0.scl;
+    float xm = rg0.xm, b1m = rg0.b1m, o1m = rg0.o1m, b2m = rg0.b2m, o2m = rg0.o2m, b2bm = rg0.b2bm, o2bm = rg0.o2bm;
+    float b3m = rg0.b3m, o3m = rg0.o3m;
+    const int rs1 = rg0.rs1, re2b = rg0.re2b;
     float amo = 0.f;                                  // max |out| of this lane's stores
-    int rs1 = 0, re2b = 0;                            // asymmetric: t1a's exponent, the 1x5's accumulator exponent
-    if constexpr (F32) {
-      const RangeArgs &g = a.rg;
-      if (!g.off) {
-        const float amx = rng_read(g);
-        const int sx = rng_exp_meas(amx), e1 = sx + g.sw[0];
-        const float B0 = g.n[0] * amx + g.c[0];
-        const int s0 = rng_exp_bound(B0, e1), e2 = s0 + g.sw[1];
-        const float B1 = g.n[1] * B0 + g.c[1];
-        const int s1 = rng_exp_bound(B1, e2);
-        int e2b = 0, s1b = 0;
-        if constexpr (ASYM) {
-            e2b = s1 + g.sw[2];
-            s1b = rng_exp_bound(g.n[2] * B1 + g.c[2], e2b);
-        }
-        const int e3 = (ASYM ? s1b : s1) + g.sw[3];
-        rs1 = s1; re2b = e2b;
-        scl = e3 != 0;                                // (only phase 3 branches; the rest always multiplies)
-        xm = rng_pow2(sx); b1m = rng_pow2(e1); o1m = rng_pow2(s0 - e1); b2m = rng_pow2(e2); o2m = rng_pow2(s1 - e2);
-        b2bm = rng_pow2(e2b); o2bm = rng_pow2(s1b - e2b); b3m = rng_pow2(e3); o3m = rng_pow2(-e3);
-      }
-    }
-    // the projection of one fragment. fp32: always scaled (the multipliers are 1 when nothing needs it):
-    // a branch to a scaled copy of this code cost the fp32 kernels 15-40 VGPRs (register allocation
-    // covers both paths), the multiplies cost ~0.5 VALU per element (v_pk_mul_f32)
+    // the projection of one fragment (SCL: operands and accumulators scaled)
     auto proj_mfma = [&](f32x4 (&acc)[NR1], const Raw (&xs)[KS1]) {
 #pragma unroll
         for (int r = 0; r < NR1; ++r) acc[r] = bias4(cb1 + r * 16 + kq * 4);
-        if constexpr (F32) {
+        if constexpr (F32 && SCL) {
 #pragma unroll
             for (int r = 0; r < NR1; ++r) acc[r] = mul4(acc[r], b1m);
 #pragma unroll
@@ -681,6 +694,14 @@ __global__ void __launch_bounds__((BShape<C, V>::NW * 64), (sizeof(T) == 2 ? BSh
         if constexpr (!KEEP) {
             if (GLDS && first) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
             __syncthreads();   // weights staged (first tile) / previous tile done with ts (and the patch)
+            if constexpr (F32 && !SCL) {
+                // the range words arrived with the loads issued before them: bail out to the scaled body
+                if (first && bneck_range<ASYM>(a.rg, rng_reduce(rlane)).any) {
+                    asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+                    __syncthreads();
+                    return false;
+                }
+            }
         }
         STAMP(1);
 
@@ -774,6 +795,14 @@ __global__ void __launch_bounds__((BShape<C, V>::NW * 64), (sizeof(T) == 2 ? BSh
             asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
             __builtin_amdgcn_s_barrier();   // weights staged (first tile) / previous tile done with ts
             asm volatile("" ::: "memory");
+            if constexpr (F32 && !SCL) {
+                // the range words arrived with the loads issued before them: bail out to the scaled body
+                if (first && bneck_range<ASYM>(a.rg, rng_reduce(rlane)).any) {
+                    asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+                    __syncthreads();
+                    return false;
+                }
+            }
 #pragma unroll
             for (int j = 0; j < NF2; ++j)
                 if (wave + NW * j < NFT) proj(int_h(wave + NW * j), true, kok[j], kx[j]);
@@ -943,12 +972,14 @@ __global__ void __launch_bounds__((BShape<C, V>::NW * 64), (sizeof(T) == 2 ? BSh
         // expansion's B operand (lane kq: channels 8kq..8kq+7) with two lane swaps (to_bop) — the
         // expansion of a fragment runs on the wave that computed it, so no barrier is needed either
         Raw tf[NF2];
-        auto to_tf = [&](f32x4 (&acc)[NF2][NR1], const float *cs, float om) {
+        auto to_tf = [&](f32x4 (&acc)[NF2][NR1], const float *cs, float om, bool mul) {
             if constexpr (F32) {
+                if (mul) {
 #pragma unroll
-                for (int j = 0; j < NF2; ++j)
+                    for (int j = 0; j < NF2; ++j)
 #pragma unroll
-                    for (int r = 0; r < NR1; ++r) acc[j][r] = mul4(acc[j][r], om);
+                        for (int r = 0; r < NR1; ++r) acc[j][r] = mul4(acc[j][r], om);
+                }
             }
 #pragma unroll
             for (int j = 0; j < NF2; ++j) {
@@ -957,10 +988,11 @@ __global__ void __launch_bounds__((BShape<C, V>::NW * 64), (sizeof(T) == 2 ? BSh
                 to_bop(tf[j], q0, q1);
             }
         };
-        // accumulators starting at the bias (fp32: times m, the accumulator's scale)
-        auto bias_m = [&](const float *p, float m) -> f32x4 {
+        // accumulators starting at the bias (fp32, mul: times m, the accumulator's scale)
+        auto bias_m = [&](const float *p, float m, bool mul) -> f32x4 {
             f32x4 b = bias4(p);
-            if constexpr (F32) b = mul4(b, m);
+            if constexpr (F32)
+                if (mul) b = mul4(b, m);
             return b;
         };
         static_assert(NR1 <= 2, "t1 in registers: at most 32 internal channels");
@@ -971,7 +1003,7 @@ __global__ void __launch_bounds__((BShape<C, V>::NW * 64), (sizeof(T) == 2 ? BSh
 #pragma unroll
             for (int j = 0; j < NF2; ++j)
 #pragma unroll
-                for (int r = 0; r < NR1; ++r) acc[j][r] = bias_m(cb2 + r * 16 + kq * 4, b2m);
+                for (int r = 0; r < NR1; ++r) acc[j][r] = bias_m(cb2 + r * 16 + kq * 4, b2m, SCL);
             constexpr int PH2U = BNECK_PH2_UNROLL > 0 ? BNECK_PH2_UNROLL : (C == 128 && !DN && !(KEEP && V == 2) ? 3 : 1);
 #pragma unroll PH2U
             for (int s = 0; s < KS2; ++s) {
@@ -999,7 +1031,7 @@ __global__ void __launch_bounds__((BShape<C, V>::NW * 64), (sizeof(T) == 2 ? BSh
                 }
             }
             STAMP(4);
-            to_tf(acc, cs2, o2m);
+            to_tf(acc, cs2, o2m, SCL);
         } else {
             // 5x1 over rows (taps dy = -2..2), output width TW+4 (the 1x5's halo). (Run in two fragment
             // halves with the residual kept in registers it measured slower, round 3: 28.2 vs 26.2 us)
@@ -1007,7 +1039,7 @@ __global__ void __launch_bounds__((BShape<C, V>::NW * 64), (sizeof(T) == 2 ? BSh
 #pragma unroll
             for (int j = 0; j < NF2A; ++j)
 #pragma unroll
-                for (int r = 0; r < NR1; ++r) acc5[j][r] = bias_m(cb2 + r * 16 + kq * 4, b2m);
+                for (int r = 0; r < NR1; ++r) acc5[j][r] = bias_m(cb2 + r * 16 + kq * 4, b2m, SCL);
 #pragma unroll BNECK_ASYM_UNROLL
             for (int s = 0; s < KS2; ++s) {
                 const int g = s * 4 + kq;
@@ -1040,7 +1072,7 @@ __global__ void __launch_bounds__((BShape<C, V>::NW * 64), (sizeof(T) == 2 ? BSh
                         const int ox = p - (p / TWA) * TWA;
                         const bool inside = (unsigned)(ox0 - 2 + ox) < (unsigned)a.W;
                         float4 v = f4(acc5[j][r]);
-                        if constexpr (F32) v = mul4(v, o2m);
+                        if constexpr (F32 && SCL) v = mul4(v, o2m);
                         v = act(v, cs2 + ch);
                         v = inside ? v : make_float4(0.f, 0.f, 0.f, 0.f);
                         if constexpr (F32) rng_acc4(m1a, v);
@@ -1072,7 +1104,7 @@ __global__ void __launch_bounds__((BShape<C, V>::NW * 64), (sizeof(T) == 2 ? BSh
 #pragma unroll
                 for (int j = 0; j < NF2; ++j)
 #pragma unroll
-                    for (int r = 0; r < NR1; ++r) acc[j][r] = bias_m(cb2b + r * 16 + kq * 4, b2bm);
+                    for (int r = 0; r < NR1; ++r) acc[j][r] = bias_m(cb2b + r * 16 + kq * 4, b2bm, SCL);
 #pragma unroll BNECK_ASYM_UNROLL
                 for (int s = 0; s < KS2; ++s) {
                     const int g = s * 4 + kq;
@@ -1093,7 +1125,7 @@ __global__ void __launch_bounds__((BShape<C, V>::NW * 64), (sizeof(T) == 2 ? BSh
                     }
                 }
                 if constexpr (!KEEP) prefetch_res();
-                to_tf(acc, cs2b, o2bm);
+                to_tf(acc, cs2b, o2bm, SCL || o2bm != 1.f);
             }
         }
 
@@ -1131,7 +1163,7 @@ __global__ void __launch_bounds__((BShape<C, V>::NW * 64), (sizeof(T) == 2 ? BSh
                             const int r = h * (NR3 / 2) + rr;
                             const int ch = r * 16 + kq * 4;
                             static_assert(bias_in_acc(NR3, 1), "expansion: one k step, bias in the accumulator");
-                            f32x4 acc = bias_m(cb3 + ch, b3m);
+                            f32x4 acc = bias_m(cb3 + ch, b3m, SCL || scl);
                             WRaw wf;
                             ld8(wf, w3 + (r * 16 + col) * K3S + kq * 8);
                             mma(acc, wf, tf[j]);
@@ -1178,7 +1210,7 @@ __global__ void __launch_bounds__((BShape<C, V>::NW * 64), (sizeof(T) == 2 ? BSh
 #pragma unroll
                 for (int r = 0; r < NR3; ++r) {
                     const int ch = r * 16 + kq * 4;
-                    f32x4 acc = bias_m(cb3 + ch, b3m);
+                    f32x4 acc = bias_m(cb3 + ch, b3m, SCL || scl);
                     WRaw wf;
                     ld8(wf, w3 + (r * 16 + col) * K3S + kq * 8);
                     mma(acc, wf, tf[j]);
@@ -1284,7 +1316,7 @@ __global__ void __launch_bounds__((BShape<C, V>::NW * 64), (sizeof(T) == 2 ? BSh
                     bst16o<OAUX>(rob, off, make_uint4(x0, x1, y0, y1));
                 } else {
                     const int r = t;
-                    f32x4 acc = bias_m(cb3 + r * 16 + kq * 4, b3m);
+                    f32x4 acc = bias_m(cb3 + r * 16 + kq * 4, b3m, SCL || scl);
                     WRaw wf;
                     ld8(wf, w3 + (r * 16 + col) * K3S + kq * 8);
                     mma(acc, wf, tf[j]);
@@ -1303,9 +1335,20 @@ __global__ void __launch_bounds__((BShape<C, V>::NW * 64), (sizeof(T) == 2 ? BSh
         }
         STAMP(6);
     }
-    if constexpr (F32) rng_commit(amo, a.rg.amax_out);
+    if constexpr (F32) rng_commit_wg(amo, a.rg.amax_out, reinterpret_cast<float *>(ts), NW);
     span_exit(a.span);
     STAMP_ENTRY(1);
+    return true;
+}
+
+template <typename T, int C, bool ASYM, int V, bool TR, int CI = 0>
+__global__ void __launch_bounds__((BShape<C, V>::NW * 64), (sizeof(T) == 2 ? BShape<C, V>::OCC : C == 16 ? BNECK_F32_OCC16 : C == 64 ? BNECK_F32_OCC64 : BNECK_F32_OCC128)) bneck_kernel(const BneckArgs a) {
+    if constexpr (sizeof(T) == 4) {
+        const float rl = rng_lane(a.rg);              // issued first, consumed after the first tile's loads
+        if (!bneck_body<T, C, ASYM, V, TR, CI, false>(a, rl)) bneck_body<T, C, ASYM, V, TR, CI, true>(a, rl);
+    } else {
+        bneck_body<T, C, ASYM, V, TR, CI, false>(a, 0.f);
+    }
 }
 
 #ifdef BUGSEG_STAMPS

@@ -35,7 +35,7 @@ inline constexpr int prec_es(int prec) { return prec == PREC_F32 ? 4 : 2; }
 // sums), and the weights carry a static exponent (packed w = w * 2^sw). The epilogues multiply the
 // accumulators back. Exact in f32 (powers of two); when every exponent is 0 — activations and
 // weights inside the window, the common case — no multiply runs at all (a wave-uniform branch).
-constexpr int RNG_SLOTS = 64;
+constexpr int RNG_SLOTS = 256;   // (4 per lane of the reading wave; the writing waves spread over them)
 struct RangeArgs {
     const float *amax_in;   // RNG_SLOTS words holding max |x| of the launch's input (nullptr: amax_static)
     float *amax_out;        // RNG_SLOTS words the launch max-accumulates max |out| into (nullptr: not measured)

@@ -124,7 +124,11 @@ __device__ __forceinline__ f32x2 pkmul(f32x2 v, f32x2 s) {
     asm("v_pk_mul_f32 %0, %1, %2" : "=v"(r) : "v"(v), "s"(s));
     return r;
 }
+#ifndef BUGSEG_RANGE
+#define BUGSEG_RANGE 31    // fp32 range scaling; A/B builds clear bits to compile parts out: 1 operand scale8,
+#endif                     // 2 accumulator mul4, 4 output max tracking (rng_acc / rng_commit), 8 mulp2, 16 rng_read
 __device__ __forceinline__ RawF scale8(const RawF &x, float m) {
+    if constexpr (!(BUGSEG_RANGE & 1)) return x;
     const f32x2 s = {m, m};
     const f32x2 a0 = pkmul((f32x2){x.a.x, x.a.y}, s), a1 = pkmul((f32x2){x.a.z, x.a.w}, s);
     const f32x2 b0 = pkmul((f32x2){x.b.x, x.b.y}, s), b1 = pkmul((f32x2){x.b.z, x.b.w}, s);
@@ -418,34 +422,77 @@ __device__ __forceinline__ int rng_exp_bound(float B, int p) {
 }
 // 2^e for |e| <= 126, from the exponent bits (a scalar when e is)
 __device__ __forceinline__ float rng_pow2(int e) { return __int_as_float((e + 127) << 23); }
-// max |v| of a launch's input: the RNG_SLOTS words (one per lane, then a wave reduction)
-__device__ __forceinline__ float rng_read(const RangeArgs &r) {
+// max |v| of a launch's input: the RNG_SLOTS words (four per lane, then a wave reduction)
+// rng_read in two halves: the lane's slot load (issue it early) and the wave reduction (consume it
+// after the launch's first operand loads are in flight, so no wave waits a memory latency for it alone)
+__device__ __forceinline__ float rng_lane(const RangeArgs &r) {
+    if constexpr (!(BUGSEG_RANGE & 16)) return 0.f;
     if (!r.amax_in) return r.amax_static;
-    const int lane = threadIdx.x & 63;
-    float m = lane < RNG_SLOTS ? r.amax_in[lane] : 0.f;
+    static_assert(RNG_SLOTS == 256, "one float4 of slots per lane");
+    const float4 q = reinterpret_cast<const float4 *>(r.amax_in)[threadIdx.x & 63];
+    return __builtin_fmaxf(__builtin_fmaxf(q.x, q.y), __builtin_fmaxf(q.z, q.w));
+}
+__device__ __forceinline__ float rng_reduce(float m) {
 #pragma unroll
     for (int o = 32; o > 0; o >>= 1) m = __builtin_fmaxf(m, __shfl_xor(m, o));
     return __int_as_float(__builtin_amdgcn_readfirstlane(__float_as_int(m)));
 }
+__device__ __forceinline__ float rng_read(const RangeArgs &r) { return rng_reduce(rng_lane(r)); }
 // m = max(m, |v|) (v_max3 with abs modifiers: NaN operands are ignored, as v_max does)
+// (compiler-visible maxNum of |.|: v_max_f32 with abs modifiers then one v_max3 into m — a chain of one
+// dependent op per quad, schedulable; NaN operands are ignored, as v_max does)
 __device__ __forceinline__ void rng_acc(float &m, float a, float b) {
-    asm("v_max3_f32 %0, %1, |%2|, |%3|" : "=v"(m) : "v"(m), "v"(a), "v"(b));
+    if constexpr (!(BUGSEG_RANGE & 4)) return;
+    m = __builtin_fmaxf(m, __builtin_fmaxf(__builtin_fabsf(a), __builtin_fabsf(b)));
 }
-__device__ __forceinline__ void rng_acc4(float &m, float4 v) { rng_acc(m, v.x, v.y); rng_acc(m, v.z, v.w); }
+__device__ __forceinline__ void rng_acc4(float &m, float4 v) {
+    if constexpr (!(BUGSEG_RANGE & 4)) return;
+    m = __builtin_fmaxf(m, __builtin_fmaxf(__builtin_fmaxf(__builtin_fabsf(v.x), __builtin_fabsf(v.y)),
+                                           __builtin_fmaxf(__builtin_fabsf(v.z), __builtin_fabsf(v.w))));
+}
 // the wave's max into the launch's output words (a global atomic max on the float bits: |v| >= 0
-// orders as unsigned; one slot per workgroup modulo RNG_SLOTS, so the atomics do not pile on one word)
+// orders as unsigned; one slot per wave modulo RNG_SLOTS, so the atomics do not pile on one word)
 __device__ __forceinline__ void rng_commit(float m, float *slots) {
-    if (!slots) return;
+    if (!(BUGSEG_RANGE & 4) || !slots) return;
 #pragma unroll
     for (int o = 32; o > 0; o >>= 1) m = __builtin_fmaxf(m, __shfl_xor(m, o));
+    // (slot: this wave's index in the grid: the waves' atomics spread over every slot — 64 slots by
+    // workgroup measured 4 us per C128 launch of same-address atomics queueing at the memory side)
+    const unsigned wg = blockIdx.x * ((blockDim.x + 63) >> 6) + (threadIdx.x >> 6);
     if ((threadIdx.x & 63) == 0 && m > 0.f)
-        atomicMax(reinterpret_cast<unsigned int *>(slots) + (blockIdx.x & (RNG_SLOTS - 1)), __float_as_uint(m));
+        atomicMax(reinterpret_cast<unsigned int *>(slots) + (wg & (RNG_SLOTS - 1)), __float_as_uint(m));
 }
-__device__ __forceinline__ f32x4 mul4(f32x4 v, float s) { return (f32x4){v[0] * s, v[1] * s, v[2] * s, v[3] * s}; }
-__device__ __forceinline__ float4 mul4(float4 v, float s) { return make_float4(v.x * s, v.y * s, v.z * s, v.w * s); }
+// the workgroup's max into the output words with ONE atomic (rng_commit's per-wave atomics measured
+// ~2-4 us per fp32 C128 launch: 8 waves x 256 workgroups on 256 words). Every wave of the workgroup
+// calls it at the kernel's end; wm: NW floats of LDS nothing else uses any more (two barriers)
+__device__ __forceinline__ void rng_commit_wg(float m, float *slots, float *wm, int nw) {
+    if (!(BUGSEG_RANGE & 4) || !slots) return;
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) m = __builtin_fmaxf(m, __shfl_xor(m, o));
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    __syncthreads();
+    if (lane == 0) wm[wave] = m;
+    __syncthreads();
+    if (wave == 0) {
+        float t = lane < nw ? wm[lane] : 0.f;
+#pragma unroll
+        for (int o = 32; o > 0; o >>= 1) t = __builtin_fmaxf(t, __shfl_xor(t, o));
+        if (lane == 0 && t > 0.f)
+            atomicMax(reinterpret_cast<unsigned int *>(slots) + (blockIdx.x & (RNG_SLOTS - 1)), __float_as_uint(t));
+    }
+}
+__device__ __forceinline__ f32x4 mul4(f32x4 v, float s) {
+    if constexpr (!(BUGSEG_RANGE & 2)) return v;
+    return (f32x4){v[0] * s, v[1] * s, v[2] * s, v[3] * s};
+}
+__device__ __forceinline__ float4 mul4(float4 v, float s) {
+    if constexpr (!(BUGSEG_RANGE & 2)) return v;
+    return make_float4(v.x * s, v.y * s, v.z * s, v.w * s);
+}
 // x *= s before a split, as an opaque v_mul_f32: a plain multiply feeding an f16 conversion is fused by
 // the compiler into v_fma_mix*, which flushes f16 subnormals (see split_f16)
 __device__ __forceinline__ float mulp2(float v, float s) {
+    if constexpr (!(BUGSEG_RANGE & 8)) return v;
     float r;
     asm("v_mul_f32 %0, %1, %2" : "=v"(r) : "v"(v), "v"(s));
     return r;

@@ -1,18 +1,19 @@
-# A/B of whole-library variants (scripts/build_variant_all.sh): per variant, per-kernel-tag launch times
-# (batch_probe.py at the bench shard size), the bench line (no CPU baseline, no sub-records) and the
-# HBM traffic counters of batch_probe in two separate rocprofv3 passes (FETCH_SIZE, WRITE_SIZE).
-# usage: [NOPMC=1] bash scripts/gpu_ab.sh NAME ...   (summaries: python scripts/pmc_summary.py gpurun_out/ab/NAME)
+#!/bin/bash
+# A/B of library builds on the bench command: one bench line per library (BUGSEG_LIB), twice each, alternating
+#   bash scripts/gpu_ab.sh TAG "libA.so libB.so" "bench args"
 set -o pipefail
-cd $GRAFT_REPO_ROOT
+cd "$GRAFT_REPO_ROOT" || exit 1
+T=${1:-ab}; LIBS=${2:-libbugseg.so}; ARGS=${3:-}
+mkdir -p gpurun_out/$T
 export TMPDIR=/tmp
-for n in "$@"; do
-  lib=$PWD/bugcar_image_segmentation_amd/_variants/libbugseg_$n.so
-  o=gpurun_out/ab/$n
-  mkdir -p $o
-  BUGSEG_LIB=$lib timeout -k 10 120 python scripts/batch_probe.py 32 > $o/probe.txt 2>&1 || exit 1
-  BUGSEG_LIB=$lib timeout -k 10 120 python bench.py --no-cpu-baseline --extras 0 > $o/bench.json 2> $o/bench.err || exit 1
-  if [ -n "$NOPMC" ]; then echo "$n done"; continue; fi
-  BUGSEG_LIB=$lib timeout -k 10 120 rocprofv3 --pmc FETCH_SIZE --kernel-trace -d $o/fetch -o run --output-format csv -- python3 scripts/batch_probe.py 32 > $o/fetch.log 2>&1 || exit 1
-  BUGSEG_LIB=$lib timeout -k 10 120 rocprofv3 --pmc WRITE_SIZE --kernel-trace -d $o/write -o run --output-format csv -- python3 scripts/batch_probe.py 32 > $o/write.log 2>&1 || exit 1
-  echo "$n done"
+for rep in 1 2; do
+  for l in $LIBS; do
+    n=$(basename $l .so)
+    BUGSEG_LIB=$GRAFT_REPO_ROOT/bugcar_image_segmentation_amd/$l timeout -k 10 240 python -u bench.py --extras 0 --no-cpu-baseline $ARGS > gpurun_out/$T/$n.$rep.json 2> gpurun_out/$T/$n.$rep.err || { echo "$n failed"; tail -5 gpurun_out/$T/$n.$rep.err; exit 1; }
+    python - "$n" gpurun_out/$T/$n.$rep.json <<'PY'
+import json, sys
+r = json.loads(open(sys.argv[2]).read().strip().splitlines()[-1])
+print(f"{sys.argv[1]:24s} {r['value']:9.1f} fps {r['ms_per_step']:.3f} ms  " + "  ".join(f"{k}:{v['us_per_launch']}" for k, v in r["kernels"].items()), flush=True)
+PY
+  done
 done

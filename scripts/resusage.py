@@ -1,6 +1,6 @@
 """Per-kernel register / spill / occupancy table for one HIP source (compile-only, no GPU).
 
-    python scripts/resusage.py bugcar_image_segmentation_amd/csrc/bneck_kernels.hip
+    python scripts/resusage.py bugcar_image_segmentation_amd/csrc/bneck_kernels.hip [-DNAME=VALUE ...]
 """
 import re
 import subprocess
@@ -11,9 +11,9 @@ import os
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
-def main(src):
+def main(src, *defines):
     with tempfile.TemporaryDirectory() as d:
-        cmd = ["/opt/rocm/bin/hipcc", "--offload-arch=gfx950", "-O3", "-std=c++17",
+        cmd = ["/opt/rocm/bin/hipcc", *defines, "--offload-arch=gfx950", "-O3", "-std=c++17",
                f"-I{ROOT}/include", f"-I{ROOT}/bugcar_image_segmentation_amd/csrc", "-x", "hip", "-c", src,
                "-o", os.path.join(d, "o.o"), "-Rpass-analysis=kernel-resource-usage"]
         r = subprocess.run(cmd, capture_output=True, text=True)
@@ -39,4 +39,4 @@ def main(src):
 
 
 if __name__ == "__main__":
-    main(sys.argv[1])
+    main(sys.argv[1], *sys.argv[2:])

@@ -21,7 +21,7 @@ laserscan flow (polar warp orientation, group-by, circle stamping, merge), the R
 quaternion, the argmax + LUT logic, the preprocess normalisation. What it does NOT pin: OpenCV's or
 TensorFlow's arithmetic (the stand-ins are the oracle's restatements of it), which stays unpinned
 (DESIGN.md §2). Checked by tests/test_ref_glue.py (CPU: oracle + drop-in host code) and
-tests/test_gpu_parity.py::test_bev_equals_reference_glue_fixtures (the HIP rasteriser).
+tests/test_gpu_ref_glue.py (the HIP rasteriser and ENET.preprocess).
 """
 from __future__ import annotations
 
