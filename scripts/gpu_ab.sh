@@ -1,15 +1,16 @@
 #!/bin/bash
 # A/B of library builds on the bench command: one bench line per library (BUGSEG_LIB), twice each, alternating
-#   bash scripts/gpu_ab.sh TAG "libA.so libB.so" "bench args"
+#   bash scripts/gpu_ab.sh TAG "libA.so libB.so libA.so@VAR=value" "bench args"   (@: an environment setting)
 set -o pipefail
 cd "$GRAFT_REPO_ROOT" || exit 1
 T=${1:-ab}; LIBS=${2:-libbugseg.so}; ARGS=${3:-}
 mkdir -p gpurun_out/$T
 export TMPDIR=/tmp
 for rep in 1 2; do
-  for l in $LIBS; do
-    n=$(basename $l .so)
-    BUGSEG_LIB=$GRAFT_REPO_ROOT/bugcar_image_segmentation_amd/$l timeout -k 10 240 python -u bench.py --extras 0 --no-cpu-baseline $ARGS > gpurun_out/$T/$n.$rep.json 2> gpurun_out/$T/$n.$rep.err || { echo "$n failed"; tail -5 gpurun_out/$T/$n.$rep.err; exit 1; }
+  for spec in $LIBS; do
+    l=${spec%%@*}; ev=""; [ "$spec" != "$l" ] && ev=${spec#*@}
+    n=$(basename $l .so)${ev:+_$ev}
+    env $ev BUGSEG_LIB=$GRAFT_REPO_ROOT/bugcar_image_segmentation_amd/$l timeout -k 10 240 python -u bench.py --extras 0 --no-cpu-baseline $ARGS > gpurun_out/$T/$n.$rep.json 2> gpurun_out/$T/$n.$rep.err || { echo "$n failed"; tail -5 gpurun_out/$T/$n.$rep.err; exit 1; }
     python - "$n" gpurun_out/$T/$n.$rep.json <<'PY'
 import json, sys
 r = json.loads(open(sys.argv[2]).read().strip().splitlines()[-1])

@@ -18,23 +18,24 @@ BNECK_SHAPES = {(128, 0): "16x16", (128, 1): "20x16", (128, 2): "4x80", (128, 3)
 
 
 def short(name):
-    # the initial block fused into the first downsampling block (INI template argument true)
-    m = re.search(r"bneck_kernelI(DF16b|DF16_|f)Li(\d+)ELb\dELi\d+ELb\dELi[1-9]\d*ELb1E", name)
-    if m:
-        return f"init+down C{m.group(2)}"
+    # fp32 bneck forms come as two kernels (bneck_kernels.hip SCL): the range-scaled one is tagged apart
+    # (launched beside every unscaled one, it returns at once unless an exponent is non-zero)
+    scl = bool(re.search(r"bneck_kernelI(DF16b|DF16_|f)Li\d+ELb\dELi\d+ELb\dELi\d+ELb1E", name) or
+               re.search(r"bneck_kernel<[^>]*, true>", name))
+    sfx = " (scaled)" if scl else ""
     m = re.search(r"bneck_kernelI(DF16b|DF16_|f)Li(\d+)ELb(\d)ELi(\d+)ELb\dELi([1-9]\d*)E", name)
     if m:   # the downsampling form (non-zero input-channel template argument)
-        return f"down C{m.group(2)} {BNECK_SHAPES.get((int(m.group(2)), int(m.group(4))), '?')}"
-    # (the f32 kernels appear demangled: "void bugseg::bneck_kernel<float, 64, false, 2, false, 0>(...)")
-    m = re.search(r"bneck_kernel<(?:__bf16|_Float16|float), (\d+), (?:false|true), (\d+), (?:false|true), ([1-9]\d*)>", name)
+        return f"down C{m.group(2)} {BNECK_SHAPES.get((int(m.group(2)), int(m.group(4))), '?')}{sfx}"
+    # (the f32 kernels appear demangled: "void bugseg::bneck_kernel<float, 64, false, 2, false, 0, false>(...)")
+    m = re.search(r"bneck_kernel<(?:__bf16|_Float16|float), (\d+), (?:false|true), (\d+), (?:false|true), ([1-9]\d*)[,>]", name)
     if m:
-        return f"down C{m.group(1)} {BNECK_SHAPES.get((int(m.group(1)), int(m.group(2))), '?')}"
+        return f"down C{m.group(1)} {BNECK_SHAPES.get((int(m.group(1)), int(m.group(2))), '?')}{sfx}"
     m = re.search(r"bneck_kernelI(DF16b|DF16_|f)Li(\d+)ELb(\d)ELi(\d+)E", name)
     if not m:
         m = re.search(r"bneck_kernel<(__bf16|_Float16|float), (\d+), (false|true), (\d+)", name)
     if m:
         asym = m.group(3) in ("1", "true")
-        return f"bneck C{m.group(2)}{' asym' if asym else ''} {BNECK_SHAPES.get((int(m.group(2)), int(m.group(4))), '?')}"
+        return f"bneck C{m.group(2)}{' asym' if asym else ''} {BNECK_SHAPES.get((int(m.group(2)), int(m.group(4))), '?')}{sfx}"
     m = re.search(r"conv_kernelI(DF16b|DF16_|f)Li(\d+)ELi(\d+)E", name)
     if m:
         return f"conv NR{m.group(2)} E{m.group(3)}"
