@@ -547,11 +547,25 @@ __device__ __forceinline__ bool bneck_body(const BneckArgs &a, float rlane) {
     };
     Raw kx[KEEP ? NF2 : 1][KS1];                      // KEEP: this wave's interior fragments of x
     bool kok[KEEP ? NF2 : 1];
+    // PREF (KEEP, register epilogue; A/B knob, off): as phase 3 finishes with a fragment's kept x, the
+    // same registers receive that fragment's x of the workgroup's NEXT tile, so its loads fly during the
+    // rest of this tile's phase 3. Measured slower (round 5, B = 64: fp32 C128 20x16 90.9 -> 100.6 us,
+    // fp16 33.4 -> 34.4 us; the loads contend with phase 3's stores and cost the fp16 form 5 spilled VGPRs)
+#ifndef BNECK_PREF
+#define BNECK_PREF 0
+#endif
+    constexpr bool PREF = BNECK_PREF && KEEP && REG3 && !DN;
+    bool pref = false;                                // this tile's kx already loaded (prefetched)
     for (int it = slot; it < CH; it += nslots) {
         const int tile = grp * CH + it;
         if (tile >= a.ntiles) break;
         int n, oy0, ox0;
         tile_geom(tile, n, oy0, ox0);
+        // the next tile of this workgroup's walk (PREF)
+        const int ntile = grp * CH + it + nslots;
+        const bool has_next = PREF && it + nslots < CH && ntile < a.ntiles;
+        int nn = 0, noy0 = 0, nox0 = 0;
+        if (has_next) tile_geom(ntile, nn, noy0, nox0);
         const int dtx = RD ? 1 : dt;                  // column step of the tile
         const uint32_t xn = (uint32_t)(n * a.H * a.W) * (uint32_t)(C * sizeof(T));   // frame byte offset
         const uint32_t xin_n = (uint32_t)(n * 4 * a.H * a.W) * (uint32_t)(CI * sizeof(T));   // down: input frame
@@ -765,9 +779,11 @@ __device__ __forceinline__ bool bneck_body(const BneckArgs &a, float rlane) {
             Raw bx[NBW][KS1];
             int bh[NBW];
             bool bok[NBW];
+            if (!pref) {
 #pragma unroll
-            for (int j = 0; j < NF2; ++j)
-                if (wave + NW * j < NFT) kok[j] = load_h(int_h(wave + NW * j), true, kx[j]);   // wave-uniform
+                for (int j = 0; j < NF2; ++j)
+                    if (wave + NW * j < NFT) kok[j] = load_h(int_h(wave + NW * j), true, kx[j]);   // wave-uniform
+            }
             auto load_b = [&](int k) {
                 const int b = (wb + NW * k) * 16 + col;
                 bh[k] = b < NBD ? bord_h(b) : 0;
@@ -1332,7 +1348,14 @@ __device__ __forceinline__ bool bneck_body(const BneckArgs &a, float rlane) {
             }
             if constexpr (!KEEP && !DKEEP)
                 if (j + RP < NF2 && wave + NW * (j + RP) < NFT) load_res(j + RP, res[j % RP]);
+            if constexpr (PREF) {
+                if (has_next) {
+                    const uint32_t nxn = (uint32_t)(nn * a.H * a.W) * (uint32_t)(C * sizeof(T));
+                    kok[j] = load_hg(noy0, nox0, nxn, int_h(wave + NW * j), true, kx[j]);
+                }
+            }
         }
+        pref = has_next;
         STAMP(6);
     }
     if constexpr (F32) rng_commit_wg(amo, a.rg.amax_out, reinterpret_cast<float *>(ts), NW);
