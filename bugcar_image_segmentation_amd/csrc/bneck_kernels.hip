@@ -1020,7 +1020,10 @@ __device__ __forceinline__ bool bneck_body(const BneckArgs &a, float rlane) {
             for (int j = 0; j < NF2; ++j)
 #pragma unroll
                 for (int r = 0; r < NR1; ++r) acc[j][r] = bias_m(cb2 + r * 16 + kq * 4, b2m, SCL);
-            constexpr int PH2U = BNECK_PH2_UNROLL > 0 ? BNECK_PH2_UNROLL : (C == 128 && !DN && !(KEEP && V == 2) ? 3 : 1);
+            // (fp32 C = 16 / 64 non-down forms: 3 as well — round 5, B = 64: C16 166.8 -> 163.4 us, C64 8x16
+            // 145.0 -> 143.9 us; the fp32 down C64 form lost 12 us at 3, so it keeps 1)
+            constexpr int PH2U = BNECK_PH2_UNROLL > 0 ? BNECK_PH2_UNROLL
+                               : ((C == 128 && !DN && !(KEEP && V == 2)) || (sizeof(T) == 4 && C != 128 && !DN)) ? 3 : 1;
 #pragma unroll PH2U
             for (int s = 0; s < KS2; ++s) {
                 const int g = s * 4 + kq;
