@@ -260,3 +260,41 @@ def test_bench_rccl_branch_one_rank(gpu):
     assert line["config"]["backend"] == "rccl" and line["config"]["gather_check"] is True
     assert "RCCL all-gather" in line["config"]["parallelism"]
     assert line["n_gpus"] == 1 and line["value"] > 0
+
+
+@pytest.mark.parametrize("prec", ["fp32", "fp16"])
+def test_launch_spans_inside_a_captured_step(gpu, blocks, prec):
+    """bench.py's in-step timing hook (bugseg_debug_set_spans): every launch of a replayed graph folds
+    its workgroups' entry / exit clock into its own slots — each launch's span is positive, launches
+    of one stream follow each other, and the armed launches' results equal unarmed ones bit for bit."""
+    B, H, W = 4, 96, 128
+    m = ENET(weights=blocks, precision=prec)
+    dev = torch.device("cuda", 0)
+    frames = torch.from_numpy(synthetic.uniform_frames(B, H, W, seed=5)).to(dev)
+    seg0 = torch.empty((B, H, W), dtype=torch.uint8, device=dev)
+    m.ctx.forward_bgr(frames, B, H, W, N.OUT_CLASS3_U8, seg0)
+    n = m.ctx.plan_info(B, H, W, N.OUT_CLASS3_U8, bgr_input=True)[0]
+    spans = torch.zeros((n, 64, 8), dtype=torch.int64, device=dev)
+    seg = torch.empty_like(seg0)
+    torch.cuda.synchronize()
+    m.ctx.set_spans(spans)
+    try:
+        g = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g):
+            m.ctx.forward_bgr(frames, B, H, W, N.OUT_CLASS3_U8, seg, torch.cuda.current_stream())
+    finally:
+        m.ctx.set_spans(None)
+    spans[:, :, 0].fill_(-1)
+    spans[:, :, 1].zero_()
+    g.replay()
+    torch.cuda.synchronize()
+    sp = spans.cpu().numpy().view(np.uint64)
+    st, en = sp[:, :, 0].min(1), sp[:, :, 1].max(1)
+    assert (st < np.uint64(2 ** 63)).all() and (en > st).all()          # every launch stamped
+    assert (st[1:] >= en[:-1]).all()                                      # stream order
+    assert torch.equal(seg, seg0)
+    # disarmed: a later eager forward leaves the slots alone
+    before = spans.clone()
+    m.ctx.forward_bgr(frames, B, H, W, N.OUT_CLASS3_U8, seg)
+    torch.cuda.synchronize()
+    assert torch.equal(spans, before)
