@@ -731,6 +731,13 @@ def main():
                 # overlapping, but no per-launch duration a profiler reproduces: it serialises the streams)
                 log("two-stream sub-record")
                 res["two_streams"] = mode_record(blocks, bev, grid, H, W, frames, 2, max(10, a.steps), a.precision, bool(a.graph))
+            if a.precision == "fp32":
+                # SURVEY 8(d)'s undamped draw (logits ~1e6, activations past f16's range from the 16th block
+                # on): the range-scaled kernels' cost where scaling is needed (tests/test_gpu_range.py)
+                log("fp32 undamped sub-record")
+                und = enet_spec.build_enet(res_gamma=(0.5, 1.5))
+                rec = mode_record(und, bev, grid, H, W, frames, a.streams, max(10, a.steps), "fp32", bool(a.graph))
+                res["fp32_undamped_weights"] = {k: rec[k] for k in ("value", "unit", "ms_per_step", "kernels")}
             for prec in ("fp32", "fp16", "bf16"):
                 if prec != a.precision:
                     log(f"{prec} sub-record")
