@@ -791,7 +791,8 @@ __device__ __forceinline__ bool bneck_body(const BneckArgs &a, float rlane) {
             };
             // the first NBE border fragments fly with the interior ones; any further ones (a wave
             // with two) are loaded after, which keeps the x registers within the occupancy budget
-            constexpr int NBE = BNECK_NBE >= 0 ? BNECK_NBE : C == 128 && !RD && !ASYM ? 1 : 0;   // C = 64 / 4x80: spills at 1
+            // (C = 64 / 4x80: spills at 1; fp32 C128: 0 measured 1-4 us per 64-frame launch faster, round 5)
+            constexpr int NBE = BNECK_NBE >= 0 ? BNECK_NBE : C == 128 && !RD && !ASYM && sizeof(T) == 2 ? 1 : 0;
 #pragma unroll
             for (int k = 0; k < NBE && k < NBW; ++k)
                 if (wb + NW * k < NFB) load_b(k);     // wave-uniform
