@@ -37,6 +37,8 @@ def gather_grids(local: torch.Tensor, total: int, group=None) -> torch.Tensor:
     if dist.get_backend(group) == "nccl":
         buf = torch.empty((world * m,) + tuple(local.shape[1:]), dtype=local.dtype, device=local.device)
         dist.all_gather_into_tensor(buf, pad.contiguous(), group=group)
+        if all(c == m for c in counts):
+            return buf                        # equal shards: rank order already, no copy
         parts = list(buf.split(m))
     else:
         # gloo (CPU tests, and the single-GPU functional run of bench.py's N > 1 branch): host copies
