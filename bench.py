@@ -137,7 +137,7 @@ def parse():
                         "outside the timed loop); default: on at N = 1, off for N > 1")
     p.add_argument("--deeplab-batch", type=int, default=64)
     p.add_argument("--overlap-gather", type=int, default=1,
-                   help="N > 1 over RCCL: overlap step k's grid all-gather with step k+1's forward")
+                   help="N > 1 over RCCL: overlap step k's grid all-gather with step k+1's forward (2: on gloo too)")
     p.add_argument("--backend", default="nccl", choices=["nccl", "gloo"],
                    help="N > 1 process group: nccl (= RCCL over xGMI, the product path) or gloo (a functional run "
                         "of the distributed branch on fewer GPUs than ranks, e.g. 2 ranks on one GPU; not a timing)")
@@ -630,9 +630,10 @@ def main():
     # (two captured steps write two grid buffers in turn; a forward waits only for the gather that last
     # read its buffer). Every step still ends in its gathered batch; the timed region's closing sync
     # covers the last gather.
-    # (world > 1 only: a one-rank gather is a local copy, and overlapping it measured 0.9% slower)
-    overlap = dist_on and world > 1 and a.backend == "nccl" and a.graph and bool(a.overlap_gather)
-    if overlap:
+    # (world > 1 only: a one-rank gather is a local copy, and overlapping it measured 0.9% slower;
+    # --overlap-gather 2 forces the form onto a gloo group too: the multi-rank test one GPU can host)
+    gather_overlap = dist_on and world > 1 and a.graph and (a.overlap_gather == 2 or (a.backend == "nccl" and a.overlap_gather == 1))
+    if gather_overlap:
         replay2, grids2 = pipe.capture(frames, out=torch.empty_like(grids))
         comm = torch.cuda.Stream(device=dev)
         slots = [(replay, grids), (replay2, grids2)]
@@ -743,7 +744,7 @@ def main():
                                    f"fused BEV warp/occgrid (1000x1000 BEV -> 200x200 cells)",
                        "global_batch": B * world, "per_gpu_batch": B, "height": H, "width": W,
                        "parallelism": f"frame-sharded dp{world}" + (" + RCCL all-gather of grids" if dist_on and a.backend == "nccl" else "")
-                                      + (" (overlapped with the next step's forward)" if overlap else ""),
+                                      + (" (overlapped with the next step's forward)" if gather_overlap else ""),
                        "streams_per_gpu": a.streams, "hip_graph": bool(a.graph), "shard_offset": a.shard_offset,
                        **({"backend": "rccl" if a.backend == "nccl" else "gloo (functional run, not a timing)",
                            "gather_check": gather_check} if dist_on else {})},

@@ -223,14 +223,17 @@ def test_sharded_pipeline_two_ranks_one_gpu(gpu, blocks):
 
 
 @pytest.mark.timeout(240)
-def test_bench_distributed_branch_gloo_one_gpu(gpu):
+@pytest.mark.parametrize("overlap", [0, 2])
+def test_bench_distributed_branch_gloo_one_gpu(gpu, overlap):
     """bench.py's N > 1 branch (process group, in-step gather_grids, max-over-ranks timing, the
-    gathered-grid check) run end to end by torch.distributed.run with 2 ranks on this one GPU."""
+    gathered-grid check) run end to end by torch.distributed.run with 2 ranks on this one GPU;
+    --overlap-gather 2 forces the RCCL run's overlapped form (two captured steps, the gather on a
+    communication stream) onto the gloo group, the only multi-rank group one GPU can host."""
     port = _free_port()
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
            "--master-addr", "127.0.0.1", "--master-port", str(port), "bench.py", "--gpus", "2",
-           "--backend", "gloo", "--steps", "3", "--warmup", "1", "--batch", "4", "--height", "96", "--width", "128",
-           "--extras", "0", "--no-cpu-baseline"]
+           "--backend", "gloo", "--steps", "5", "--warmup", "3", "--batch", "4", "--height", "96", "--width", "128",
+           "--extras", "0", "--no-cpu-baseline", "--overlap-gather", str(overlap)]
     env = dict(os.environ, HSA_ENABLE_IPC_MODE_LEGACY=os.environ.get("HSA_ENABLE_IPC_MODE_LEGACY", "0"))
     r = subprocess.run(cmd, cwd=ROOT, capture_output=True, text=True, timeout=220, env=env)
     assert r.returncode == 0, r.stderr[-3000:]
@@ -238,6 +241,7 @@ def test_bench_distributed_branch_gloo_one_gpu(gpu):
     print(json.dumps({k: line[k] for k in ("value", "n_gpus", "ms_per_step", "config")}))
     assert line["config"]["global_batch"] == 8 and line["config"]["gather_check"] is True
     assert line["n_gpus"] == 1 and line["value"] > 0
+    assert ("overlapped" in line["config"]["parallelism"]) == (overlap == 2)
 
 
 @pytest.mark.timeout(240)
