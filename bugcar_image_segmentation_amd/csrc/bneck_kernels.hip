@@ -200,7 +200,22 @@ __device__ __forceinline__ bool bneck_body(const BneckArgs &a, float rlane) {
     constexpr int NR1 = (I + 15) / 16;                // 16-row fragments of t0 / t1
     constexpr int NR3 = C / 16;                       // 16-row fragments of out
     constexpr bool DN = CI > 0;                       // (I above already depends on it)
-    constexpr int OAUX = OUT_AUX_SEL((C >= 64 && CI != 16) ? 16 : 0);   // sc1 output stores (mfma_common.h)
+    // output store policy (mfma_common.h): sc1 for C >= 64; the fp32 C = 64 (non-down) form streams its
+    // output non-temporally (nt) — round 5, B = 64, one stream: the blocks reading it (down C128, up C16)
+    // 14-18 us faster per launch. nt measured worse for the fp32 C16 form (itself +4 us), the down forms
+    // (down C64 +32 us) and the C128 forms (+10%) — A/B knobs BNECK_NT_F32_C64 / _C16 / _DN
+#ifndef BNECK_NT_F32_C64
+#define BNECK_NT_F32_C64 1
+#endif
+#ifndef BNECK_NT_F32_C16
+#define BNECK_NT_F32_C16 0
+#endif
+#ifndef BNECK_NT_F32_DN
+#define BNECK_NT_F32_DN 0
+#endif
+    constexpr bool NTO = sizeof(T) == 4 && ((CI == 0 && ((C == 64 && BNECK_NT_F32_C64) || (C == 16 && BNECK_NT_F32_C16))) ||
+                                            (CI != 0 && BNECK_NT_F32_DN));
+    constexpr int OAUX = OUT_AUX_SEL(NTO ? 2 : (C >= 64 && CI != 16) ? 16 : 0);
     static_assert(!DN || (!ASYM && !TR && !BShape<C, V>::RD && (CI == 16 || CI % 32 == 0)), "down mode: plain tiles");
     constexpr int G1 = DN ? CI / 2 : C / 8, KS1 = (G1 + 3) / 4;   // proj k groups / steps (down: 4 taps x CI)
     constexpr int CG1 = CI / 8;                       // down: 8-channel groups per tap

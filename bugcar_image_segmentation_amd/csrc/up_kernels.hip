@@ -39,7 +39,14 @@ __global__ void __launch_bounds__((up_threads<T, CIN>()), (sizeof(T) == 2 ? (CIN
     using Raw = typename Tr<T>::Raw;
     using WRaw = typename WTr<T>::Raw;   // weight operand (fp32 mode: split-f16 parts)
     constexpr int ES = (int)sizeof(T);
-    constexpr int OAUX = OUT_AUX_SEL(CIN >= 128 ? 16 : 0);   // sc1 output stores (mfma_common.h)
+// fp32, the 128 -> 64 block: non-temporal output stores (round 5, B = 64, one stream: the bottleneck that
+// reads them 13 us faster, this launch 7 us slower; the 64 -> 16 block lost 26 us for 7, so it keeps
+// the default) — A/B knob UP_NT_F32 (0 off, 1 that block, 2 both)
+#ifndef UP_NT_F32
+#define UP_NT_F32 1
+#endif
+    constexpr int OAUX = sizeof(T) == 4 && (UP_NT_F32 == 2 || (UP_NT_F32 == 1 && CIN >= 128)) ? 2
+                       : OUT_AUX_SEL(CIN >= 128 ? 16 : 0);   // sc1 output stores (mfma_common.h)
     constexpr int NR1 = (COUT + I) / 16;              // GEMM 1 rows: main then e1
     constexpr int NM = COUT / 16, NE = I / 16;        // row fragments of main / e1 (per tconv phase)
     constexpr int KS1 = CIN / 32;                     // GEMM 1 k-steps
