@@ -218,7 +218,11 @@ __device__ __forceinline__ bool bneck_body(const BneckArgs &a, float rlane) {
 #ifndef BNECK_AUX_F32_C128
 #define BNECK_AUX_F32_C128 16
 #endif
-    constexpr int OAUX = OUT_AUX_SEL(NTO ? 2 : (sizeof(T) == 4 && C == 128) ? BNECK_AUX_F32_C128 : (C >= 64 && CI != 16) ? 16 : 0);
+#ifndef BNECK_AUX_F32_LOW
+#define BNECK_AUX_F32_LOW 0    // fp32 forms that take the default policy (C16, down C64): A/B knob
+#endif
+    constexpr int OAUX = OUT_AUX_SEL(NTO ? 2 : (sizeof(T) == 4 && C == 128) ? BNECK_AUX_F32_C128
+                                     : (C >= 64 && CI != 16) ? 16 : sizeof(T) == 4 ? BNECK_AUX_F32_LOW : 0);
     static_assert(!DN || (!ASYM && !TR && !BShape<C, V>::RD && (CI == 16 || CI % 32 == 0)), "down mode: plain tiles");
     constexpr int G1 = DN ? CI / 2 : C / 8, KS1 = (G1 + 3) / 4;   // proj k groups / steps (down: 4 taps x CI)
     constexpr int CG1 = CI / 8;                       // down: 8-channel groups per tap
