@@ -56,6 +56,9 @@ __device__ __forceinline__ bool nonzero(const RawS &r) {
 #ifndef CLS_ABL
 #define CLS_ABL 0
 #endif
+#ifndef CLS_AUX
+#define CLS_AUX 0          // class-map store policy (A/B knob; the BEV rasteriser reads them next)
+#endif
 #ifndef CLS_BIAS_REG
 #define CLS_BIAS_REG 1
 #endif
@@ -318,7 +321,7 @@ __global__ void __launch_bounds__(256, sizeof(T) == 2 ? 4 : 1) cls_kernel(const 
             // (32-bit offsets through a buffer descriptor: a masked lane's store is dropped)
             const uint32_t o = 4u * q.p - 2u * (uint32_t)q.x + (uint32_t)(2 * h * a.Wg);
             if (!(CLS_ABL & 4) || c0 == 77)
-                __builtin_amdgcn_raw_buffer_store_b16((unsigned short)(c0 | (c1 << 8)), rcls, q.ok ? (int)o : (int)OOB, 0, 0);
+                __builtin_amdgcn_raw_buffer_store_b16((unsigned short)(c0 | (c1 << 8)), rcls, q.ok ? (int)o : (int)OOB, 0, CLS_AUX);
         }
     };
     Raw xa[CLS_TAPS], xb[CLS_TAPS];
