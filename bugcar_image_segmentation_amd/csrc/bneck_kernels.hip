@@ -213,8 +213,12 @@ __device__ __forceinline__ bool bneck_body(const BneckArgs &a, float rlane) {
 #ifndef BNECK_NT_F32_DN
 #define BNECK_NT_F32_DN 0
 #endif
-    constexpr bool NTO = sizeof(T) == 4 && ((CI == 0 && ((C == 64 && BNECK_NT_F32_C64) || (C == 16 && BNECK_NT_F32_C16))) ||
-                                            (CI != 0 && BNECK_NT_F32_DN));
+#ifndef BNECK_NT_2B_C64
+#define BNECK_NT_2B_C64 0
+#endif
+    constexpr bool NTO = (sizeof(T) == 4 && ((CI == 0 && ((C == 64 && BNECK_NT_F32_C64) || (C == 16 && BNECK_NT_F32_C16))) ||
+                                             (CI != 0 && BNECK_NT_F32_DN))) ||
+                         (sizeof(T) == 2 && CI == 0 && C == 64 && BNECK_NT_2B_C64);
 #ifndef BNECK_AUX_F32_C128
 #define BNECK_AUX_F32_C128 16
 #endif

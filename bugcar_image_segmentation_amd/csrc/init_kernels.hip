@@ -48,6 +48,9 @@ constexpr int IT_H = 8, IT_W = 32;                        // output tile
 constexpr int IP_H = 2 * IT_H + 1, IP_W = 2 * IT_W + 1;   // input patch (pixels)
 constexpr int IP_RS = IP_W * 3 + 1;                       // LDS patch row stride (elements, even)
 constexpr int IP_PATCH = (IP_H * IP_RS + 7) & ~7;           // one patch buffer (elements, 16-B multiple)
+#ifndef INIT_NT_2B
+#define INIT_NT_2B 0      // 2-byte output stores non-temporal (A/B knob)
+#endif
 #ifndef INIT_NT_F32
 #define INIT_NT_F32 1     // fp32 output stores non-temporal: the down block that reads them 11 us faster, this 2 us slower (round 5)
 #endif
@@ -350,7 +353,7 @@ __global__ void __launch_bounds__(256, sizeof(T) == 2 ? INIT_OCC2 : 1) init_kern
             }
             const uint32_t off = ok ? (uint32_t)(((n * a.Hg + oy) * a.Wg + ox) * a.outC + c0) * (uint32_t)sizeof(T) : OOB;
             if constexpr (sizeof(T) == 2) {
-                bst8o<OUT_AUX_SEL(16)>(rout, off, pack4<T>(v));
+                bst8o<INIT_NT_2B ? 2 : OUT_AUX_SEL(16)>(rout, off, pack4<T>(v));
             } else {
                 bst16o<INIT_NT_F32 ? 2 : OUT_AUX_SEL(16)>(rout, off, __builtin_bit_cast(uint4, v));
             }

@@ -48,7 +48,10 @@ __global__ void __launch_bounds__((up_threads<T, CIN>()), (sizeof(T) == 2 ? (CIN
 #ifndef UP_AUX_F32_LOW
 #define UP_AUX_F32_LOW 0       // fp32 64 -> 16 block's policy (A/B knob)
 #endif
-    constexpr int OAUX = sizeof(T) == 4 && (UP_NT_F32 == 2 || (UP_NT_F32 == 1 && CIN >= 128)) ? 2
+#ifndef UP_NT_2B
+#define UP_NT_2B 0
+#endif
+    constexpr int OAUX = (sizeof(T) == 4 && (UP_NT_F32 == 2 || (UP_NT_F32 == 1 && CIN >= 128))) || (sizeof(T) == 2 && UP_NT_2B && CIN >= 128) ? 2
                        : sizeof(T) == 4 && CIN < 128 ? UP_AUX_F32_LOW
                        : OUT_AUX_SEL(CIN >= 128 ? 16 : 0);   // sc1 output stores (mfma_common.h)
     constexpr int NR1 = (COUT + I) / 16;              // GEMM 1 rows: main then e1
