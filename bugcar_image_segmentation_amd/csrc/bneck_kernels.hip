@@ -214,7 +214,7 @@ __device__ __forceinline__ bool bneck_body(const BneckArgs &a, float rlane) {
 #define BNECK_NT_F32_DN 0
 #endif
 #ifndef BNECK_NT_2B_C64
-#define BNECK_NT_2B_C64 0
+#define BNECK_NT_2B_C64 1
 #endif
     constexpr bool NTO = (sizeof(T) == 4 && ((CI == 0 && ((C == 64 && BNECK_NT_F32_C64) || (C == 16 && BNECK_NT_F32_C16))) ||
                                              (CI != 0 && BNECK_NT_F32_DN))) ||
