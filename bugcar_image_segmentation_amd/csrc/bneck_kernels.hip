@@ -150,6 +150,9 @@ void bneck_shape(int C, int v, int &th, int &tw, int &nw, int *rd) {
 #ifndef BNECK_F32_OCC64
 #define BNECK_F32_OCC64 1
 #endif
+#ifndef BNECK_F32_OCC64_V2
+#define BNECK_F32_OCC64_V2 4   // the 8 x 16 C = 64 form: 127 VGPRs, no spills at 4 (round 5: 139.8 -> 137.9 us per launch; 1 = unconstrained, 154 VGPRs, 3 waves per SIMD)
+#endif
 #ifndef BNECK_F32_OCC128
 #define BNECK_F32_OCC128 1
 #endif
@@ -1395,7 +1398,7 @@ __device__ __forceinline__ bool bneck_body(const BneckArgs &a, float rlane) {
 }
 
 template <typename T, int C, bool ASYM, int V, bool TR, int CI = 0>
-__global__ void __launch_bounds__((BShape<C, V>::NW * 64), (sizeof(T) == 2 ? BShape<C, V>::OCC : C == 16 ? BNECK_F32_OCC16 : C == 64 ? BNECK_F32_OCC64 : BNECK_F32_OCC128)) bneck_kernel(const BneckArgs a) {
+__global__ void __launch_bounds__((BShape<C, V>::NW * 64), (sizeof(T) == 2 ? BShape<C, V>::OCC : C == 16 ? BNECK_F32_OCC16 : C == 64 ? (V == 2 ? BNECK_F32_OCC64_V2 : BNECK_F32_OCC64) : BNECK_F32_OCC128)) bneck_kernel(const BneckArgs a) {
     if constexpr (sizeof(T) == 4) {
         const float rl = rng_lane(a.rg);              // issued first, consumed after the first tile's loads
         if (!bneck_body<T, C, ASYM, V, TR, CI, false>(a, rl)) bneck_body<T, C, ASYM, V, TR, CI, true>(a, rl);

@@ -799,6 +799,8 @@ int pick_bneck_variant(const bugseg_ctx *ctx, int C, bool asym, int d, int B, in
     if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, ctx->device) != hipSuccess || cus <= 0) cus = 256;
     const char *force = std::getenv("BUGSEG_BNECK_VARIANT");
     if (const char *fc = std::getenv(("BUGSEG_BNECK_VARIANT_C" + std::to_string(C)).c_str())) force = fc;   // debug
+    if (asym)
+        if (const char *fa = std::getenv("BUGSEG_BNECK_VARIANT_ASYM")) force = fa;   // debug
     const int R = asym ? 2 : 1;
     const int hs = (H + d - 1) / d, ws = (W + d - 1) / d;    // phase sub-image (largest phase)
     int best = -1;
