@@ -1,6 +1,6 @@
 """Debug: in-kernel phase clocks of the fused bottleneck (libbugseg_stamps.so, -DBUGSEG_STAMPS).
 
-Runs one bf16 forward at batch B, then launches each fused-bottleneck op of the plan alone with the
+Runs one forward (bf16 unless given) at batch B, then launches each fused-bottleneck op of the plan alone with the
 stamp buffer armed and prints, per op, the mean shader-clock cycles of each tile phase:
   wait0  top-of-tile barrier (previous tile's phase 3 of the slowest wave)
   ph1    projection over tile + halo (global loads -> MFMA -> t0 in LDS)
@@ -10,7 +10,7 @@ stamp buffer armed and prints, per op, the mean shader-clock cycles of each tile
   ph3    expansion + residual + stores issued
 and the span of the launch in clocks next to its HIP-event duration (-> effective clock).
 
-usage: python scripts/stamp_probe.py [B]   (build: python -m bugcar_image_segmentation_amd.build --stamps)"""
+usage: python scripts/stamp_probe.py [B] [precision: bf16 | fp16 | fp32]   (build: python -m bugcar_image_segmentation_amd.build --stamps)"""
 import ctypes
 import os
 import sys
@@ -29,7 +29,7 @@ B = int(sys.argv[1]) if len(sys.argv) > 1 else 32
 H, W = 480, 640
 lib = N.load_library()
 lib.bugseg_debug_set_stamps.argtypes = [ctypes.c_void_p]
-m = ENET(weights=enet_spec.build_enet(), precision="bf16")
+m = ENET(weights=enet_spec.build_enet(), precision=sys.argv[2] if len(sys.argv) > 2 else "bf16")
 frames = torch.from_numpy(synthetic.uniform_frames(B, H, W)).cuda()
 seg = torch.empty((B, H, W), dtype=torch.uint8, device="cuda")
 for _ in range(3):
