@@ -285,7 +285,10 @@ __device__ __forceinline__ bool bneck_body(const BneckArgs &a, float rlane) {
 #ifndef BNECK_CH1_K8
 #define BNECK_CH1_K8 1
 #endif
-    constexpr int CH1 = KS1 >= 8 ? BNECK_CH1_K8 : KS1 >= 4 ? (NF1 + NW - 1) / NW
+#ifndef BNECK_CH1_K8_F32
+#define BNECK_CH1_K8_F32 1   // fp32 down C128 (the only KS1 >= 8 form): phase-1 fragments in flight (A/B knob; 2: 241 VGPRs, no spills, 115.5-117.0 -> 120.2-121.6 us, round 5)
+#endif
+    constexpr int CH1 = KS1 >= 8 ? (sizeof(T) == 4 ? BNECK_CH1_K8_F32 : BNECK_CH1_K8) : KS1 >= 4 ? (NF1 + NW - 1) / NW
                     : KS1 == 2 ? (C == 64 && V == 0 && !DN && !ASYM ? BNECK_CH1_C64 : BNECK_CH1_K2) : 8;   // phase-1 fragments whose loads fly together
     // phase-3 chunking (see phase 3): bf16 with an even number of 16-row blocks swaps row pairs
     // into 16-B chunks; bf16 C = 16 stores 8-B quads (HALF); fp32 quads are 16-B chunks
