@@ -355,6 +355,17 @@ __device__ __forceinline__ bool bneck_body(const BneckArgs &a, float rlane) {
     constexpr bool KEEP = (BNECK_KEEP && !DN && sizeof(T) == 2 && (!ASYM || BNECK_KEEP_ASYM) && (SWAP || !REG3) && (C != 64 || BNECK_KEEP_C64) &&
                            NF2 * KS1 * 4 <= (C == 128 ? 48 : 32)) || KEEPF;   // kept VGPRs within the occupancy budget
     static_assert(!KEEP || !REG3 || (KEEPF ? 2 * KS1 == RQ3 : KS1 == RQ3), "kept x: one 16-B chunk per k-step and row pair");
+#ifndef BNECK_EARLY_FREE
+#define BNECK_EARLY_FREE 0   // A/B knob, off: bit-identical (GPU parity green) but measured neutral to slower (round 5:
+                             // fp32 C128 16x16 85.8-86.2 -> 86.7-87.0 us, fp16 frames/s -0.3%): a tile's critical
+                             // path is its waves with the most fragments, whichever barrier the others wait at
+#endif
+    // EARLY_FREE (kept x, register epilogue): phase 3 touches no LDS but the read-only weights and
+    // constants (t1 goes from the accumulators to B operands in registers), so the t0 region is free
+    // once every wave has finished phase 2. The barrier that protects it moves from the top of the next
+    // tile to the end of phase 2 (the first tile keeps its top barrier: the weight staging), and a wave
+    // done with its stores starts the next tile's projection while the others are still storing
+    constexpr bool EARLY_FREE = BNECK_EARLY_FREE && KEEP && REG3;
 #ifndef BNECK_DKEEP
 #define BNECK_DKEEP 1
 #endif
@@ -842,7 +853,7 @@ __device__ __forceinline__ bool bneck_body(const BneckArgs &a, float rlane) {
                 vm_wait_upto(BNECK_GLDS_PARTIAL ? (nld < 24 ? nld & ~1 : 24) : 0);   // (fewer outstanding: still after the weights)
             }
             asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-            __builtin_amdgcn_s_barrier();   // weights staged (first tile) / previous tile done with ts
+            if (!EARLY_FREE || first) __builtin_amdgcn_s_barrier();   // weights staged (first tile) / previous tile done with ts
             asm volatile("" ::: "memory");
             if constexpr (F32 && !SCL) {
                 // the range words arrived with the loads issued before them: bail out to the scaled body
@@ -1290,6 +1301,7 @@ __device__ __forceinline__ bool bneck_body(const BneckArgs &a, float rlane) {
             STAMP(6);
             continue;
         }
+        if constexpr (EARLY_FREE) __syncthreads();        // every wave done reading t0 / t1a: the next tile may write them
         STAMP(5);
 #pragma unroll
         for (int j = 0; j < NF2; ++j) {
