@@ -109,9 +109,17 @@ template <> struct BShape<16, 1> { static constexpr int TH = 20, TW = 16, NW = 4
 // twice per CU (WIDE; asymmetric and 4x80 tiles keep 40); fp32 (parity mode) keeps 16-B pads.
 // (fp32 keeps 16-B pads: 32-B pads by the bf16 rule measured neutral on C = 128 with the split t0 below
 // — 45.8 vs 45.8 us per launch — and slower on C = 64 / 16, 77.0 -> 81.5 / 96.7 -> 108.4 us; round 4)
-__host__ __device__ constexpr int bneck_padw(int es, int C, bool wide) { return es == 2 && (C != 128 || wide) ? 16 : 16 / es; }
+// fp32 C = 128 (not the down form): HL, the grouped split layout (see the body) — weight rows and t0 pixels
+// padded to 8 / 40 dwords mod 64, the conflict-free strides for its 16-B-per-lane reads
+#ifndef BNECK_F32_HL
+#define BNECK_F32_HL 1
+#endif
+__host__ __device__ constexpr bool bneck_hl(int es, int C, bool dn) { return BNECK_F32_HL && es == 4 && C == 128 && !dn; }
+__host__ __device__ constexpr int bneck_padw(int es, int C, bool wide, bool dn) {
+    return bneck_hl(es, C, dn) ? 8 : es == 2 && (C != 128 || wide) ? 16 : 16 / es;
+}
 __host__ __device__ constexpr int bneck_pstr(int es, int IS, bool wide) {
-    return es != 2 ? IS + 16 / es : IS == 32 ? (wide ? 48 : 40) : IS;
+    return es != 2 ? (BNECK_F32_HL && es == 4 && IS == 32 ? 40 : IS + 16 / es) : IS == 32 ? (wide ? 48 : 40) : IS;
 }
 static bool bneck_wide(int C, int v, bool asym) {
 #define BW_CASE(CC, VV) if (C == CC && v == VV) return BShape<CC, VV>::WIDE && !asym;
@@ -243,7 +251,7 @@ __device__ __forceinline__ bool bneck_body(const BneckArgs &a, float rlane) {
     constexpr int HWW = TW + 2 * RX, HR = (TH + 2 * RY) * HWW;
     constexpr int NF1 = (HR + 15) / 16;               // 16-pixel fragments of tile + halo
     constexpr bool WIDE = BShape<C, V>::WIDE && !ASYM;
-    constexpr int PADW = bneck_padw((int)sizeof(T), C, WIDE);   // weight-row pad (elements)
+    constexpr int PADW = bneck_padw((int)sizeof(T), C, WIDE, CI > 0);   // weight-row pad (elements)
     constexpr int PSTR = bneck_pstr((int)sizeof(T), IS, WIDE);  // LDS pixel stride (elements)
     constexpr int NPX = TH * TW;
     constexpr int NFT = (NPX + 15) / 16;              // 16-pixel fragments of the tile
@@ -388,8 +396,18 @@ __device__ __forceinline__ bool bneck_body(const BneckArgs &a, float rlane) {
     // layout, 32 B per 8 channels as the f32 values take), split once when written rather than at every
     // one of the middle conv's 9 (asymmetric: 5 + 5) operand reads. Bit-identical (the same parts).
     using SRaw = typename std::conditional<sizeof(T) == 4 && BNECK_F32_SPLIT_T0, RawS, Raw>::type;
+    // HL (fp32 C = 128, round 5): in LDS a 32-element k-step of a split weight row, and a t0 / t1a pixel's
+    // 32 channels, hold the four 8-channel groups' hi parts (16 B each) and then their lo parts, instead of
+    // hi + lo per group — so each of a lane's two 16-B reads is 4 dwords at 4 kq dwords apart, as in bf16,
+    // and rows of 8 / 40 dwords mod 64 make every ds_read_b128 lane group conflict-free (SQ: 41% of the
+    // LDS cycles of these forms were bank conflicts with 32-B groups). The weight staging permutes the
+    // 16-B chunks (the packed matrices in HBM keep the shared layout); the same parts feed the same products
+    constexpr bool HL = bneck_hl((int)sizeof(T), C, CI > 0);
+    static_assert(!HL || (BNECK_F32_SPLIT_T0 && IS == 32 && BNECK_GLDS), "HL: split t0 of 32 channels, LDS-DMA staging");
+    constexpr int ZP = HL ? 32 : 16;                  // zero-pad elements below ts
     auto st4t = [](T *p, int ch, float4 v) {
-        if constexpr (sizeof(T) == 4 && BNECK_F32_SPLIT_T0) st4s(reinterpret_cast<float *>(p) - (ch & 7), ch & 7, v);
+        if constexpr (HL) st4hl(reinterpret_cast<float *>(p) - ch, ch, v);
+        else if constexpr (sizeof(T) == 4 && BNECK_F32_SPLIT_T0) st4s(reinterpret_cast<float *>(p) - (ch & 7), ch & 7, v);
         else st4(p, v);
     };
 
@@ -407,6 +425,15 @@ __device__ __forceinline__ bool bneck_body(const BneckArgs &a, float rlane) {
     // first channel of this lane's phase-3 chunk t
     auto chunk_ch = [&](int t) -> int { return SWAP ? (2 * t + (kq & 1)) * 16 + 8 * (kq >> 1) : t * 16 + kq * 4; };
     const int K1S = KS1 * 32 + PADW, K2S = KS2 * 32 + PADW, K3S = 32 + PADW;
+    // A operand: group kq of the k-step at p (a weight row + 32 s)
+    auto ldw = [&](WRaw &r, const T *p) {
+        if constexpr (HL) {
+            r.h = *reinterpret_cast<const uint4 *>(p + kq * 4);
+            r.l = *reinterpret_cast<const uint4 *>(p + 16 + kq * 4);
+        } else {
+            ld8(r, p + kq * 8);
+        }
+    };
     T *w1 = reinterpret_cast<T *>(smem);
     T *w2 = w1 + NR1 * 16 * K1S;
     T *w2b = w2 + NR1 * 16 * K2S;                     // asymmetric second conv (1x5)
@@ -418,7 +445,7 @@ __device__ __forceinline__ bool bneck_body(const BneckArgs &a, float rlane) {
     float *cb2b = cs2 + NP1, *cs2b = cb2b + NP1, *cb3 = cs2b + NP1, *cs3 = cb3 + C, *cso = cs3 + C;
     // 16 zero elements: masked-off B fragments read them (an address select, not a divergent branch)
     T *zpad = reinterpret_cast<T *>(cso + C);
-    T *ts = zpad + 16;                                // t0 / t1a / t1 region
+    T *ts = zpad + ZP;                                // t0 / t1a / t1 region
     float *wmx = reinterpret_cast<float *>(ts + HR * PSTR);   // fp32 asymmetric: NW per-wave max |t1a| slots
     {
         // C = 16 (small weights, many short tiles): every load of the staging is issued before the
@@ -459,7 +486,10 @@ __device__ __forceinline__ bool bneck_body(const BneckArgs &a, float rlane) {
                 const uint4 *src;
                 auto pick = [&](const void *w, int k, int SR, int CPR) {   // slot k of one matrix
                     const int r = k / SR, c = k - r * SR;
-                    src = (const uint4 *)w + r * CPR + (c < CPR ? c : 0);
+                    // HL: LDS chunk d of each 8-chunk k-step is hi (d < 4) / lo part of group d % 4, packed
+                    // chunk 2 (d % 4) + (d >= 4)
+                    const int cs = HL ? (c & ~7) | ((c & 7) < 4 ? 2 * (c & 7) : 2 * (c & 3) + 1) : c;
+                    src = (const uint4 *)w + r * CPR + (c < CPR ? cs : 0);
                 };
                 constexpr int O3 = S1 + S2 * (ASYM ? 2 : 1);   // first slot of w3
                 if (q < S1) pick(a.w1, q, SR1, CPR1);
@@ -517,7 +547,7 @@ __device__ __forceinline__ bool bneck_body(const BneckArgs &a, float rlane) {
             }
             for (int i = tid; i < C; i += NT) { cb3[i] = a.b3[i]; cs3[i] = a.s3[i]; cso[i] = a.s_out[i]; }
         }
-        if (tid < 16) zpad[tid] = (T)0.f;
+        if (tid < ZP) zpad[tid] = (T)0.f;
     }
     // x / out through buffer descriptors: 32-bit offsets, and an out-of-range offset reads 0 / drops
     // the store (mfma_common.h), so image-border masking costs one select per access
@@ -553,7 +583,7 @@ __device__ __forceinline__ bool bneck_body(const BneckArgs &a, float rlane) {
 #pragma unroll
                 for (int r = 0; r < NR1; ++r) {
                     WRaw wf;
-                    ld8(wf, w1 + (r * 16 + col) * K1S + s * 32 + kq * 8);
+                    ldw(wf, w1 + (r * 16 + col) * K1S + s * 32);
                     mma(acc[r], wf, xq);
                 }
             }
@@ -565,7 +595,7 @@ __device__ __forceinline__ bool bneck_body(const BneckArgs &a, float rlane) {
 #pragma unroll
                 for (int r = 0; r < NR1; ++r) {
                     WRaw wf;
-                    ld8(wf, w1 + (r * 16 + col) * K1S + s * 32 + kq * 8);
+                    ldw(wf, w1 + (r * 16 + col) * K1S + s * 32);
                     mma(acc[r], wf, xs[s]);
                 }
         }
@@ -1077,7 +1107,7 @@ __device__ __forceinline__ bool bneck_body(const BneckArgs &a, float rlane) {
                 const int ti = tr ? kx : ky, tj = RD ? (kx - 1) * dt : tr ? ky : kx;
                 WRaw wf[NR1];
 #pragma unroll
-                for (int r = 0; r < NR1; ++r) ld8(wf[r], w2 + (r * 16 + col) * K2S + s * 32 + kq * 8);
+                for (int r = 0; r < NR1; ++r) ldw(wf[r], w2 + (r * 16 + col) * K2S + s * 32);
 #pragma unroll
                 for (int j = 0; j < NF2; ++j) {
                     if (wave + NW * j >= NFT) continue;       // wave-uniform
@@ -1086,9 +1116,15 @@ __device__ __forceinline__ bool bneck_body(const BneckArgs &a, float rlane) {
                     const int oy = p / TW, ox = p - oy * TW;
                     SRaw xf;
                     const bool in = g < G2 && (!RD || (unsigned)(ox + tj) < (unsigned)TW);
-                    int off = ((oy + ti) * HWW + (ox + tj)) * PSTR + coff;
+                    int off = ((oy + ti) * HWW + (ox + tj)) * PSTR + (HL ? coff >> 1 : coff);
                     asm volatile("" : "+v"(off));
-                    ld8(xf, ts + (in ? off : -16));           // masked: the zero pad just below ts
+                    if constexpr (HL) {
+                        const int o = in ? off : -ZP;         // masked: the zero pad just below ts
+                        xf.h = *reinterpret_cast<const uint4 *>(ts + o);
+                        xf.l = *reinterpret_cast<const uint4 *>(ts + o + 16);
+                    } else {
+                        ld8(xf, ts + (in ? off : -16));       // masked: the zero pad just below ts
+                    }
 #pragma unroll
                     for (int r = 0; r < NR1; ++r) mma(acc[j][r], wf[r], xf);
                 }
@@ -1109,7 +1145,7 @@ __device__ __forceinline__ bool bneck_body(const BneckArgs &a, float rlane) {
                 const int tap = g / (IS / 8), coff = (g - tap * (IS / 8)) * 8;
                 WRaw wf[NR1];
 #pragma unroll
-                for (int r = 0; r < NR1; ++r) ld8(wf[r], w2 + (r * 16 + col) * K2S + s * 32 + kq * 8);
+                for (int r = 0; r < NR1; ++r) ldw(wf[r], w2 + (r * 16 + col) * K2S + s * 32);
 #pragma unroll
                 for (int j = 0; j < NF2A; ++j) {
                     const int f = wave + NW * j;
@@ -1118,7 +1154,13 @@ __device__ __forceinline__ bool bneck_body(const BneckArgs &a, float rlane) {
                     if constexpr (NPA % 16 != 0) p = p < NPA ? p : 0;
                     const int oy = p / TWA, ox = p - oy * TWA;
                     SRaw xf;
-                    ld8(xf, g < G2 ? ts + ((oy + tap) * HWW + ox) * PSTR + coff : zpad);
+                    if constexpr (HL) {
+                        const T *q = g < G2 ? ts + ((oy + tap) * HWW + ox) * PSTR + (coff >> 1) : zpad;
+                        xf.h = *reinterpret_cast<const uint4 *>(q);
+                        xf.l = *reinterpret_cast<const uint4 *>(q + 16);
+                    } else {
+                        ld8(xf, g < G2 ? ts + ((oy + tap) * HWW + ox) * PSTR + coff : zpad);
+                    }
 #pragma unroll
                     for (int r = 0; r < NR1; ++r) mma(acc5[j][r], wf[r], xf);
                 }
@@ -1174,7 +1216,7 @@ __device__ __forceinline__ bool bneck_body(const BneckArgs &a, float rlane) {
                     const int tap = g / (IS / 8), coff = (g - tap * (IS / 8)) * 8;
                     WRaw wf[NR1];
 #pragma unroll
-                    for (int r = 0; r < NR1; ++r) ld8(wf[r], w2b + (r * 16 + col) * K2S + s * 32 + kq * 8);
+                    for (int r = 0; r < NR1; ++r) ldw(wf[r], w2b + (r * 16 + col) * K2S + s * 32);
 #pragma unroll
                     for (int j = 0; j < NF2; ++j) {
                         if (wave + NW * j >= NFT) continue;
@@ -1182,7 +1224,13 @@ __device__ __forceinline__ bool bneck_body(const BneckArgs &a, float rlane) {
                         if constexpr (NPX % 16 != 0) p = p < NPX ? p : 0;
                         const int oy = p / TW, ox = p - oy * TW;
                         SRaw xf;
-                        ld8(xf, g < G2 ? ts + (oy * TWA + ox + tap) * PSTR + coff : zpad);
+                        if constexpr (HL) {
+                            const T *q = g < G2 ? ts + (oy * TWA + ox + tap) * PSTR + (coff >> 1) : zpad;
+                            xf.h = *reinterpret_cast<const uint4 *>(q);
+                            xf.l = *reinterpret_cast<const uint4 *>(q + 16);
+                        } else {
+                            ld8(xf, g < G2 ? ts + (oy * TWA + ox + tap) * PSTR + coff : zpad);
+                        }
 #pragma unroll
                         for (int r = 0; r < NR1; ++r) mma(acc[j][r], wf[r], xf);
                     }
@@ -1228,7 +1276,7 @@ __device__ __forceinline__ bool bneck_body(const BneckArgs &a, float rlane) {
                             static_assert(bias_in_acc(NR3, 1), "expansion: one k step, bias in the accumulator");
                             f32x4 acc = bias_m(cb3 + ch, b3m, SCL || scl);
                             WRaw wf;
-                            ld8(wf, w3 + (r * 16 + col) * K3S + kq * 8);
+                            ldw(wf, w3 + (r * 16 + col) * K3S);
                             mma(acc, wf, tf[j]);
                             T *sp = stg + col * OSTR + (ch - h * (C / 2));
                             float4 v = f4(acc);
@@ -1275,7 +1323,7 @@ __device__ __forceinline__ bool bneck_body(const BneckArgs &a, float rlane) {
                     const int ch = r * 16 + kq * 4;
                     f32x4 acc = bias_m(cb3 + ch, b3m, SCL || scl);
                     WRaw wf;
-                    ld8(wf, w3 + (r * 16 + col) * K3S + kq * 8);
+                    ldw(wf, w3 + (r * 16 + col) * K3S);
                     mma(acc, wf, tf[j]);
                     T *sp = stg + col * OSTR + ch;
                     float4 v = f4(acc);
@@ -1352,8 +1400,8 @@ __device__ __forceinline__ bool bneck_body(const BneckArgs &a, float rlane) {
                     f32x4 acc0 = bias4(cb3 + r0 * 16 + kq * 4);   // (2-byte storage: no range scaling)
                     f32x4 acc1 = bias4(cb3 + r1 * 16 + kq * 4);
                     WRaw w0, w1;
-                    ld8(w0, w3 + (r0 * 16 + col) * K3S + kq * 8);
-                    ld8(w1, w3 + (r1 * 16 + col) * K3S + kq * 8);
+                    ldw(w0, w3 + (r0 * 16 + col) * K3S);
+                    ldw(w1, w3 + (r1 * 16 + col) * K3S);
                     mma(acc0, w0, tf[j]);
                     mma(acc1, w1, tf[j]);
                     // residual chunk -> quads of rows r0 / r1
@@ -1382,7 +1430,7 @@ __device__ __forceinline__ bool bneck_body(const BneckArgs &a, float rlane) {
                     const int r = t;
                     f32x4 acc = bias_m(cb3 + r * 16 + kq * 4, b3m, SCL || scl);
                     WRaw wf;
-                    ld8(wf, w3 + (r * 16 + col) * K3S + kq * 8);
+                    ldw(wf, w3 + (r * 16 + col) * K3S);
                     mma(acc, wf, tf[j]);
                     if constexpr (HALF) {
                         float4 v = act(add4(out3(r, acc), unpack4<T>((u32x2_t){rc.x, rc.y})), cso + r * 16 + kq * 4);
@@ -1436,7 +1484,8 @@ size_t bneck_lds_bytes(int prec, int C, bool asym, int v, int cin) {
     const int KS1 = ((cin > 0 ? cin / 2 : C / 8) + 3) / 4, KS2 = ((asym ? 5 : 9) * IS / 8 + 3) / 4;
     const int R = asym ? 2 : 1, RX = RD ? 0 : R;
     const bool wide = bneck_wide(C, v, asym);
-    const int padw = bneck_padw(es, C, wide);
+    const int padw = bneck_padw(es, C, wide, cin > 0);
+    const int zp = bneck_hl(es, C, cin > 0) ? 32 : 16;
     const size_t wts = (size_t)NR1 * 16 * (KS1 * 32 + padw) + (size_t)NR1 * 16 * (KS2 * 32 + padw) * (asym ? 2 : 1) +
                        (size_t)C * (32 + padw);
     const size_t halo = (size_t)(TH + 2 * R) * (TW + 2 * RX) * bneck_pstr(es, IS, wide);
@@ -1444,7 +1493,7 @@ size_t bneck_lds_bytes(int prec, int C, bool asym, int v, int cin) {
     const bool hstg = staged && es == 4 && BNECK_F32_HSTG;            // fp32 C = 64: one 32-channel half at a time
     const size_t stage = staged ? (size_t)NW * 16 * ((hstg ? C / 2 : C) + pad) : 0;    // staged epilogue (REG3 off)
     const size_t consts = ((size_t)6 * NR1 * 16 + 3 * (size_t)C) * sizeof(float);
-    return (wts + 16 + (halo > stage ? halo : stage)) * es + consts +   // + the zero pad
+    return (wts + zp + (halo > stage ? halo : stage)) * es + consts +   // + the zero pad
            (asym && es == 4 ? (size_t)NW * sizeof(float) : 0);             // + fp32 asymmetric max slots
 }
 

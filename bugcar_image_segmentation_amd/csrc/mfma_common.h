@@ -169,6 +169,21 @@ __device__ __forceinline__ void st4s(float *grp, int sub, float4 v) {
     *reinterpret_cast<f16x4 *>(g + 2 * sub) = hv;
     *reinterpret_cast<f16x4 *>(g + 16 + 2 * sub) = lv;
 }
+// the same split, in the grouped layout of a 32-channel run (bneck_kernels.hip HL: the four 8-channel
+// groups' hi parts, 16 B each, then their lo parts): 4 consecutive channels from ch (ch % 4 == 0)
+__device__ __forceinline__ void st4hl(float *run, int ch, float4 v) {
+    const float e[4] = {v.x, v.y, v.z, v.w};
+    _Float16 h[4], l[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+        h[i] = (_Float16)e[i];
+        l[i] = (_Float16)(e[i] - (float)h[i]);
+    }
+    const f16x4 hv = {h[0], h[1], h[2], h[3]}, lv = {l[0], l[1], l[2], l[3]};
+    unsigned char *g = reinterpret_cast<unsigned char *>(run) + (ch >> 3) * 16 + (ch & 7) * 2;
+    *reinterpret_cast<f16x4 *>(g) = hv;
+    *reinterpret_cast<f16x4 *>(g + 64) = lv;
+}
 // exact f32 products (DeepLab's fp32 mode): sub-MFMA j contracts element j of every lane's 8-group
 // (lane>>4 = group), so the 8 sub-MFMAs together cover the same 32 k as one bf16 MFMA.
 __device__ __forceinline__ void mma(f32x4 &acc, const RawF &w, const RawF &x) {

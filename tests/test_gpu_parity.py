@@ -376,7 +376,7 @@ def test_fused_bottlenecks_equal_unfused(gpu, blocks, prec, H, W, variant, monke
 
 @pytest.mark.parametrize("grid", ["8", "-2"])
 @pytest.mark.parametrize("variant", [None, "0", "2", "4"])
-@pytest.mark.parametrize("prec", ["bf16", "fp16"])
+@pytest.mark.parametrize("prec", ["fp32", "bf16", "fp16"])
 @pytest.mark.parametrize("H,W", [(72, 104), (480, 640)])
 def test_fused_bottlenecks_multi_tile_walks(gpu, blocks, prec, H, W, variant, grid, monkeypatch):
     """Every fused bottleneck launch on a small grid (BUGSEG_BNECK_GRID: 8 workgroups, or half the
