@@ -13,9 +13,18 @@ config 5's share at N=8).
 
 Run:  python bench.py [--gpus N --steps K --warmup W]
       python -m torch.distributed.run --nproc-per-node N --master-addr 127.0.0.1 ... bench.py --gpus N
+Without a launcher (WORLD_SIZE unset), `--gpus N` with N > 1 starts N ranks itself: this process runs
+`torch.distributed.run --nproc-per-node N` as a CHILD before touching the GPU and exits with its code
+(it never re-execs). Under a launcher, WORLD_SIZE must equal --gpus (else exit 2).
 The headline is the fp32 mode (`--precision fp32`, the default since round 5): the reference's own
-arithmetic (TF fp32 sess.run, models.py:43-44), logits within 1e-3 of the fp32 oracle over the whole
-f32 range (tests/test_gpu_range.py). fp16 and bf16 (2-byte storage) are sub-records.
+arithmetic (TF fp32 sess.run, models.py:43-44). What the tests enforce: on the default (damped) weights
+the logits lie within 1e-3 absolute of the fp32 oracle, the timed B = 64 configuration included
+(tests/test_gpu_timed_config.py); over the f32 range (SURVEY's undamped draw, logits ~1e6, and layers
+scaled by 1e-6 .. 1e6) a RELATIVE bar against fp64: p99 of the per-pixel error <= 2e-6 of the frame's
+max |logit|, and every pixel beyond 5e-6 of it attributed to a max-pool index the engine flipped at an
+fp64 near-tie (tests/test_gpu_range.py; operands are range-scaled by powers of two clamped to 2^+-40,
+so tensors with max |v| outside [2^-26, 2^54] lose precision gracefully). fp16 and bf16 (2-byte
+storage) are sub-records.
 
 Rank 0 prints ONE JSON line. `roofline` describes the dominant kernel of the forward (largest total
 in-step time): the bytes one launch must move (block input read once, output written once) / its
@@ -118,8 +127,9 @@ def parse():
     p.add_argument("--height", type=int, default=480)
     p.add_argument("--width", type=int, default=640)
     p.add_argument("--precision", default="fp32", choices=["bf16", "fp16", "fp32"],
-                   help="precision of the timed step: fp32 (default; the reference's arithmetic, logits within 1e-3 "
-                        "over the whole f32 range), fp16 / bf16 (2-byte storage throughput modes)")
+                   help="precision of the timed step: fp32 (default; the reference's arithmetic: logits within 1e-3 "
+                        "absolute of the fp32 oracle on the default weights, a relative bar vs fp64 over the f32 range "
+                        "— tests/test_gpu_range.py), fp16 / bf16 (2-byte storage throughput modes)")
     p.add_argument("--streams", type=int, default=1,
                    help="frame shards run concurrently on this many HIP streams (1: the whole batch per launch)")
     p.add_argument("--stream-priority", type=int, default=0, help="HIP priority of the side shards' streams")
@@ -141,7 +151,65 @@ def parse():
     p.add_argument("--backend", default="nccl", choices=["nccl", "gloo"],
                    help="N > 1 process group: nccl (= RCCL over xGMI, the product path) or gloo (a functional run "
                         "of the distributed branch on fewer GPUs than ranks, e.g. 2 ranks on one GPU; not a timing)")
+    p.add_argument("--launcher-check", action="store_true",
+                   help="CPU-only functional check of the N-rank launch and the grid all-gather (gloo; synthetic int8 "
+                        "grids, no GPU, no engine): what tests/test_distributed_gloo.py runs without a GPU")
     return p.parse_args()
+
+
+def _free_port():
+    import socket
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def launch_ranks(a) -> int:
+    """`python bench.py --gpus N` (N > 1) with no launcher: run this script under torch.distributed.run
+    with N ranks, one per GPU (LOCAL_RANK = device), as a child process started before anything here
+    touched the GPU; returns its exit code. (torch.cuda.device_count() does not initialise the GPU.)"""
+    import subprocess
+    if a.backend == "nccl" and not a.launcher_check:
+        ndev = torch.cuda.device_count()
+        if ndev < a.gpus:
+            log(f"--gpus {a.gpus} over RCCL needs {a.gpus} GPUs, {ndev} visible (use --backend gloo for a functional run)")
+            return 2
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={a.gpus}",
+           "--master-addr", "127.0.0.1", "--master-port", str(_free_port()), os.path.abspath(__file__), *sys.argv[1:]]
+    env = dict(os.environ, HSA_ENABLE_IPC_MODE_LEGACY=os.environ.get("HSA_ENABLE_IPC_MODE_LEGACY", "0"))
+    log(f"starting {a.gpus} ranks: {' '.join(cmd)}")
+    return subprocess.run(cmd, env=env).returncode
+
+
+def launcher_check(a, world, rank):
+    """--launcher-check: the process group, the in-step gather, the gathered-batch check and the
+    MAX-over-ranks timing of the N > 1 branch, on gloo with synthetic per-rank grids (CPU only)."""
+    from bugcar_image_segmentation_amd.distributed import gather_grids
+    dist.init_process_group("gloo")
+    B = a.batch
+    local = torch.from_numpy(np.random.default_rng(rank).integers(-1, 101, (B, 200, 200)).astype(np.int8))
+    for _ in range(a.warmup):
+        gather_grids(local, B * world)
+    dist.barrier()
+    t0 = time.perf_counter()
+    for _ in range(a.steps):
+        full = gather_grids(local, B * world)
+    dist.barrier()
+    el = time.perf_counter() - t0
+    ok = all(torch.equal(full[r * B:(r + 1) * B],
+                         torch.from_numpy(np.random.default_rng(r).integers(-1, 101, (B, 200, 200)).astype(np.int8)))
+             for r in range(world))
+    t = torch.tensor([el, float(ok)], dtype=torch.float64)
+    dist.all_reduce(t[:1], op=dist.ReduceOp.MAX)
+    dist.all_reduce(t[1:], op=dist.ReduceOp.MIN)
+    if rank == 0:
+        print(json.dumps({"check": "launcher", "ranks": world, "n_gpus": world, "backend": "gloo",
+                          "global_batch": B * world, "gather_check": bool(t[1].item() == 1.0),
+                          "gather_ms": round(float(t[0]) / max(1, a.steps) * 1e3, 4)}), flush=True)
+    dist.barrier()
+    dist.destroy_process_group()
 
 
 _T0 = time.perf_counter()
@@ -580,9 +648,17 @@ def class_agreement(blocks, H, W, nframes, dev, precs=("bf16", "fp16")):
 
 def main():
     a = parse()
-    world = int(os.environ.get("WORLD_SIZE", "1"))
+    env_world = os.environ.get("WORLD_SIZE")
+    if env_world is None and a.gpus > 1:
+        sys.exit(launch_ranks(a))             # N ranks as a child launcher; nothing here touched the GPU
+    world = int(env_world or "1")
+    if env_world is not None and world != a.gpus:
+        log(f"WORLD_SIZE {world} != --gpus {a.gpus}: refusing to report {a.gpus} GPUs for a {world}-rank job")
+        sys.exit(2)
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    if a.launcher_check:
+        return launcher_check(a, world, rank)
     # one process per GPU; with more ranks than GPUs (the gloo functional run) ranks share devices
     ndev = torch.cuda.device_count()
     if ndev == 0:
@@ -736,7 +812,7 @@ def main():
         value = frames_total / el
         res = {
             "metric": "frames/sec ENet 640x480 segmentation -> BEV occupancy grid (synthetic), whole job",
-            "value": round(value, 2), "unit": "frames/s", "n_gpus": world if a.backend == "nccl" else min(world, ndev), "steps": a.steps, "warmup": a.warmup,
+            "value": round(value, 2), "unit": "frames/s", "n_gpus": world, "steps": a.steps, "warmup": a.warmup,
             "ms_per_step": round(el / a.steps * 1e3, 4), "higher_is_better": True, "scaling": "weak",
             "vs_baseline": None, "dtype": a.precision, "data": "synthetic (uniform u8 frames, seed=rank; "
             "random-init canonical ENet weights seed 1234; synthetic BEV calibration)",
@@ -746,8 +822,10 @@ def main():
                        "parallelism": f"frame-sharded dp{world}" + (" + RCCL all-gather of grids" if dist_on and a.backend == "nccl" else "")
                                       + (" (overlapped with the next step's forward)" if gather_overlap else ""),
                        "streams_per_gpu": a.streams, "hip_graph": bool(a.graph), "shard_offset": a.shard_offset,
-                       **({"backend": "rccl" if a.backend == "nccl" else "gloo (functional run, not a timing)",
-                           "gather_check": gather_check} if dist_on else {})},
+                       "ranks": world, "devices": min(world, ndev),
+                       "backend": ("rccl" if a.backend == "nccl" else "gloo (functional run, not a timing)") if dist_on
+                                  else "none (one process)",
+                       **({"gather_check": gather_check} if dist_on else {})},
             "roofline": roof,
             "kernels": ktable,
             "stages_ms": {"frames": Bs, "enet_forward": round(t_fwd, 4), "bev_occgrid": round(t_bev, 4),

@@ -28,7 +28,8 @@ EXPORTED = ("bugseg_version", "bugseg_create", "bugseg_destroy", "bugseg_load_we
             "bugseg_last_error",
             "bugseg_dl_create", "bugseg_dl_destroy", "bugseg_dl_load_weights", "bugseg_dl_set_plan",
             "bugseg_dl_forward", "bugseg_dl_launch_op", "bugseg_dl_read_buffer", "bugseg_dl_last_error",
-            "bugseg_debug_parse_pack", "bugseg_debug_polar_tables", "bugseg_debug_ctx_info", "bugseg_debug_set_spans", "bugseg_dl_debug_check_plan")
+            "bugseg_debug_parse_pack", "bugseg_debug_polar_tables", "bugseg_debug_ctx_info", "bugseg_debug_set_spans", "bugseg_debug_pool_indices",
+            "bugseg_dl_debug_check_plan")
 DL_OP_FIELDS = 32
 
 
@@ -94,7 +95,8 @@ def load_library(path: Path | str | None = None) -> ctypes.CDLL:
             "bugseg_debug_parse_pack": (i, [vp, sz, i, ctypes.POINTER(i)]),
             "bugseg_debug_polar_tables": (i, [i, i, i, vp, sz, vp, sz, ctypes.POINTER(i), ctypes.POINTER(i)]),
             "bugseg_debug_ctx_info": (i, [vp, i, i]),
-            "bugseg_debug_set_spans": (i, [vp, vp]),
+            "bugseg_debug_set_spans": (i, [vp, vp, i]),
+            "bugseg_debug_pool_indices": (i, [vp, i, i, i, i, vp, sz, ctypes.POINTER(ctypes.c_int), vp]),
             "bugseg_dl_debug_check_plan": (i, [vp, i, vp, i, i, i, i, i, sz]),
         }
         for name, (res, args) in proto.items():
@@ -222,8 +224,25 @@ class Context:
 
     def set_spans(self, spans=None):
         """Measurement hook (bugseg_debug_set_spans): a CUDA int64 tensor of 512 words per plan op (64
-        [entry, exit] slots, 64 B apart) that later launches fold their clock into (None disarms)."""
-        check(self.lib.bugseg_debug_set_spans(self.h, ctypes.c_void_p(spans.data_ptr() if spans is not None else 0)), self.h)
+        [entry, exit] slots, 64 B apart) that later launches fold their clock into (None disarms); ops
+        beyond the tensor's size are never armed."""
+        if spans is None:
+            check(self.lib.bugseg_debug_set_spans(self.h, ctypes.c_void_p(0), 0), self.h)
+            return
+        if not spans.is_cuda or spans.dtype != torch.int64 or not spans.is_contiguous() or spans.numel() % 512:
+            raise ValueError("spans must be a contiguous CUDA int64 tensor of 512 words per op")
+        check(self.lib.bugseg_debug_set_spans(self.h, ctypes.c_void_p(spans.data_ptr()), spans.numel() // 512), self.h)
+
+    def pool_indices(self, B: int, H: int, W: int, block: int, shape: tuple, stream=None) -> torch.Tensor:
+        """Test hook (bugseg_debug_pool_indices): the pooling indices the last forward at (B, H, W) wrote
+        for downsampling block `block`, as a uint8 (B, h, w, idx_cs) device tensor; shape = (h, w, idx_cs)."""
+        out = torch.empty((B,) + tuple(shape), dtype=torch.uint8, device=torch.device("cuda", self.device))
+        cs = ctypes.c_int(0)
+        check(self.lib.bugseg_debug_pool_indices(self.h, B, H, W, block, ctypes.c_void_p(out.data_ptr()), out.numel(),
+                                                 ctypes.byref(cs), ctypes.c_void_p(stream_handle(stream))), self.h)
+        if cs.value != shape[-1]:
+            raise ValueError(f"index tensor has channel stride {cs.value}, not {shape[-1]}")
+        return out
 
 
 _shared: dict[int, Context] = {}

@@ -138,6 +138,8 @@ struct Plan {
     void *arena = nullptr;
     size_t arena_bytes = 0;
     bool pinned = false;     // a forward on this arena was captured into a graph: never freed before destroy
+    std::vector<unsigned char *> idx;   // per block: its pooling-index tensor in the arena (down blocks), else null
+    std::vector<size_t> idx_bytes;
 };
 
 inline int round_up(int v, int m) { return (v + m - 1) / m * m; }
@@ -158,6 +160,7 @@ struct bugseg_ctx {
     float norm_amax = 0.f;                         // max |table| (the BGR input's range, fp32 range scaling)
     bool range_off = false;                        // BUGSEG_F32_RANGE=0 at load_weights: no fp32 range scaling (A/B)
     unsigned long long *spans = nullptr;           // bugseg_debug_set_spans: 512 u64 of launch-span slots per op, or null
+    int spans_ops = 0;                             // ... for ops [0, spans_ops) only (the caller's buffer size)
     std::string err;
     bool loaded = false;
     int ncls = 0;
@@ -1256,6 +1259,8 @@ bool build_plan(bugseg_ctx *ctx, int B, int H, int W, std::string &why, void *st
         if (!finish_conv_args(op.a, op.epi, w.es)) { why = "batch too large for 32-bit tensor offsets"; return false; }
     }
     pl.ops = std::move(w.ops);
+    pl.idx = w.idx;
+    pl.idx_bytes = w.szIdx;
     pl.words = w.words;
     pl.words_bytes = words_bytes;
     pl.B = B; pl.H = H; pl.W = W;
@@ -1515,7 +1520,7 @@ int bugseg_nchw_to_input(bugseg_ctx *ctx, const void *x, int is_f64, int B, int 
 
 // one plan op, with its launch-span slots when bugseg_debug_set_spans armed them
 static hipError_t launch_op(const bugseg_ctx *ctx, const Op &o, int i, hipStream_t s) {
-    unsigned long long *sp = ctx->spans ? ctx->spans + 512 * (size_t)i : nullptr;   // (mfma_common.h: 64 slots x 64 B)
+    unsigned long long *sp = ctx->spans && i < ctx->spans_ops ? ctx->spans + 512 * (size_t)i : nullptr;   // (mfma_common.h: 64 slots x 64 B)
     if (o.kind == 1) { BneckArgs q = o.bn; q.span = sp; return launch_bneck(ctx->prec, o.bn_c, o.bn_asym, o.bn_var, q, s, o.bn_cin); }
     if (o.kind == 2) { UpArgs q = o.up; q.span = sp; return launch_up(ctx->prec, o.up_cin, o.up_it, o.up_cout, q, s); }
     ConvArgs q = o.a;
@@ -1907,9 +1912,28 @@ int bugseg_debug_parse_pack(const void *blob, size_t bytes, int precision, int *
     return BUGSEG_OK;
 }
 
-int bugseg_debug_set_spans(bugseg_ctx *ctx, void *spans) {
+int bugseg_debug_set_spans(bugseg_ctx *ctx, void *spans, int n_ops) {
     if (!ctx) return fail(ctx, BUGSEG_EINVAL, "NULL ctx");
+    if (spans && n_ops <= 0) return fail(ctx, BUGSEG_EINVAL, "spans: n_ops must be positive");
     ctx->spans = (unsigned long long *)spans;
+    ctx->spans_ops = spans ? n_ops : 0;
+    return BUGSEG_OK;
+}
+
+int bugseg_debug_pool_indices(bugseg_ctx *ctx, int B, int H, int W, int block, void *dst, size_t bytes, int *idx_cs,
+                              void *stream) {
+    if (!ctx || !dst) return fail(ctx, BUGSEG_EINVAL, "NULL argument");
+    if (!ctx->loaded) return fail(ctx, BUGSEG_ESTATE, "no weights loaded");
+    Plan &pl = ctx->plan;
+    if (!pl.arena || pl.B != B || pl.H != H || pl.W != W) return fail(ctx, BUGSEG_ESTATE, "no forward has run at these dimensions");
+    if (block < 0 || block >= (int)pl.idx.size() || !pl.idx[(size_t)block])
+        return fail(ctx, BUGSEG_EINVAL, "block " + std::to_string(block) + " is not a downsampling block");
+    if (bytes != pl.idx_bytes[(size_t)block])
+        return fail(ctx, BUGSEG_EINVAL, "index tensor is " + std::to_string(pl.idx_bytes[(size_t)block]) + " bytes");
+    if (idx_cs) *idx_cs = cstore(ctx->blocks[(size_t)block].attrs[0]);
+    DeviceGuard g(ctx->device);
+    hipError_t e = hipMemcpyAsync(dst, pl.idx[(size_t)block], bytes, hipMemcpyDeviceToDevice, (hipStream_t)stream);
+    if (e != hipSuccess) return fail(ctx, BUGSEG_EHIP, std::string("pool indices copy: ") + hipGetErrorString(e));
     return BUGSEG_OK;
 }
 

@@ -429,14 +429,23 @@ __device__ __forceinline__ int rng_exp_meas(float m) {
     return l >= -2 && l < 15 ? 0 : rng_clamp(14 - l);
 }
 // a rigorous bound B of |t|: the preferred exponent p (the accumulator's, so no multiply) while the
-// scaled bound lies in [2^3, 2^15), else the exponent that brings B to [2^14, 2^15)
+// scaled bound lies in [2^3, 2^15), else the exponent that brings B to [2^14, 2^15). A bound that is
+// not finite (|t| may exceed f32 itself) takes the largest down-scale, never the unscaled p; p itself
+// (an accumulator exponent: a tensor exponent plus a weight exponent) is clamped to +-2 RNG_EMAX, so a
+// chained accumulator exponent (this plus the next weight's) stays within +-3 RNG_EMAX = +-120
 __device__ __forceinline__ int rng_exp_bound(float B, int p) {
-    if (!(B > 0.f) || !(B < INFINITY)) return p;
+    p = p < -2 * RNG_EMAX ? -2 * RNG_EMAX : p > 2 * RNG_EMAX ? 2 * RNG_EMAX : p;
+    if (!(B < INFINITY)) return -RNG_EMAX;
+    if (!(B > 0.f)) return p;
     const int l = rng_log2(B);
     return l + p >= 3 && l + p < 15 ? p : rng_clamp(14 - l);
 }
-// 2^e for |e| <= 126, from the exponent bits (a scalar when e is)
-__device__ __forceinline__ float rng_pow2(int e) { return __int_as_float((e + 127) << 23); }
+// 2^e from the exponent bits (a scalar when e is); e clamped to [-126, 126] so no exponent can wrap
+// into the sign or exponent field (a multiplier needing more than that is beyond f32 anyway)
+__device__ __forceinline__ float rng_pow2(int e) {
+    e = e < -126 ? -126 : e > 126 ? 126 : e;
+    return __int_as_float((e + 127) << 23);
+}
 // max |v| of a launch's input: the RNG_SLOTS words (four per lane, then a wave reduction)
 // rng_read in two halves: the lane's slot load (issue it early) and the wave reduction (consume it
 // after the launch's first operand loads are in flight, so no wave waits a memory latency for it alone)

@@ -146,7 +146,13 @@ int bugseg_enet_forward_bgr(bugseg_ctx *ctx, const uint8_t *bgr_dev, int B, int 
 /* bugseg_enet_forward_bgr enqueuing only launches [first_op, last_op) of the forward's plan
  * (last_op = -1: to the end; bugseg_plan_info gives the count). Calling it for [0, k) and then for
  * [k, -1) enqueues exactly the full forward; in between the caller may record an event, so another
- * stream's work can start at a chosen point of this forward (pipeline.py: the shard offset). */
+ * stream's work can start at a chosen point of this forward (pipeline.py: the shard offset).
+ * fp32 range precondition: the range words (the measured max |.| of every stored activation, which
+ * pick the launches' power-of-two exponents) are cleared, and the input measured, only by a range that
+ * starts at op 0; launches of a range starting at first_op > 0 read the words the earlier launches of
+ * the SAME forward wrote — so call [0, k) before [k, -1) on the same input, as pipeline.py does.
+ * Started at k > 0 without it, a range uses whatever the last forward left (stale exponents: still
+ * overflow-safe, as the words only grow, but not necessarily those of a full forward on this input). */
 int bugseg_enet_forward_bgr_ops(bugseg_ctx *ctx, const uint8_t *bgr_dev, int B, int H, int W, int out_kind,
                                 void *out_dev, int first_op, int last_op, void *stream);
 
@@ -181,7 +187,9 @@ int bugseg_plan_info(bugseg_ctx *ctx, int B, int H, int W, int out_kind, int bgr
  * last forward call at those dimensions left it (its input / output buffers must still be alive).
  * bugseg_plan_op: kernel tag ("init", "conv NR<n> E<epilogue>", "bneck C<c>[ asym]") and the
  * launch's per-layer algorithmic bytes, the bytes it must move, and its flops.
- * bugseg_plan_launch_op: enqueue that one launch on `stream` (bench.py times kernels with it). */
+ * bugseg_plan_launch_op: enqueue that one launch on `stream` (bench.py times kernels with it). In
+ * the fp32 mode it reads the range words as the last forward left them (see
+ * bugseg_enet_forward_bgr_ops) and max-accumulates its own output's into them. */
 int bugseg_plan_op(bugseg_ctx *ctx, int B, int H, int W, int op, char *kernel, int kernel_len, double *alg_bytes,
                    double *plan_bytes, double *flops);
 int bugseg_plan_launch_op(bugseg_ctx *ctx, int B, int H, int W, int op, void *stream);
@@ -202,12 +210,18 @@ int bugseg_debug_polar_tables(int w, int h, int variant, int32_t *fmap, size_t f
  * Returns -1 for an unknown `what` or a NULL ctx. */
 int bugseg_debug_ctx_info(const bugseg_ctx *ctx, int what, int arg);
 /* Measurement hook (bench.py's in-step kernel table): arm launch spans. spans = device memory of
- * 512 x uint64 per plan op (NULL disarms): 64 slots 64 B apart, slot k = [k*8] entry, [k*8+1] exit;
- * every later launch of op i folds the constant 100 MHz GPU clock into the slots of op i (workgroup w
- * into slot w % 64: min at entry, max at exit) — the caller sets entries to UINT64_MAX and exits to 0
- * before the run it reads and takes the min / max over the slots. Launches already captured keep
- * their slots. */
-int bugseg_debug_set_spans(bugseg_ctx *ctx, void *spans);
+ * 512 x uint64 per plan op for n_ops ops (NULL disarms): 64 slots 64 B apart, slot k = [k*8] entry,
+ * [k*8+1] exit; every later launch of op i < n_ops folds the constant 100 MHz GPU clock into the slots
+ * of op i (workgroup w into slot w % 64: min at entry, max at exit) — the caller sets entries to
+ * UINT64_MAX and exits to 0 before the run it reads and takes the min / max over the slots. Ops at or
+ * beyond n_ops (a plan of another shape) are never armed. Launches already captured keep their slots. */
+int bugseg_debug_set_spans(bugseg_ctx *ctx, void *spans, int n_ops);
+/* Test hook (tests/test_gpu_range.py): copy the pooling indices the last forward at (B, H, W) wrote for
+ * downsampling block `block` (index into the block list) to device memory dst, on `stream`: u8 NHWC
+ * (B, h, w, idx_cs), one byte per channel = the window position 2*dy + dx of the first maximum
+ * (MaxPoolWithArgmax, models.py:43-44 inside enet.pb). bytes must equal the tensor's size. */
+int bugseg_debug_pool_indices(bugseg_ctx *ctx, int B, int H, int W, int block, void *dst, size_t bytes, int *idx_cs,
+                              void *stream);
 
 /* ---- DeepLabV3 (BASELINE config 4) -------------------------------------
  * Replaces DeepLabV3 (models.py:98-136): tf.compat.v1.Session + GraphDef import (models.py:105-113)

@@ -1,7 +1,10 @@
 """Golden fixtures from the REFERENCE'S OWN Python glue. Run in the build container
 only (it reads /root/reference, which the GPU box does not have); the output is data only:
 
-    python tests/golden/make_ref_glue.py        ->  tests/golden/ref_glue.npz
+    python tests/golden/make_ref_glue.py        ->  tests/golden/ref_glue.npz (+ ref_glue.sha256)
+
+It executes the reference's (untrusted) code in this process, so no test or CI path runs it: it is
+run by hand, and tests/test_ref_glue.py checks the committed .npz by its committed SHA-256.
 
 The reference imports cv2, tensorflow, numpy_indexed, rospy and the ROS message packages, none of
 which exist here. They are replaced by small module stand-ins whose functions are this repo's own
@@ -272,7 +275,12 @@ def main(out_path=None):
     out["enet/preprocess_in"] = bgr
     out["enet/preprocess"] = np.asarray(E.preprocess(bgr))
     np.savez_compressed(out_path, **out)
-    print(f"wrote {out_path}: {len(out)} arrays")
+    import hashlib
+    with open(out_path, "rb") as f:
+        digest = hashlib.sha256(f.read()).hexdigest()
+    with open(str(out_path).replace(".npz", ".sha256"), "w") as f:
+        f.write(digest + "\n")
+    print(f"wrote {out_path}: {len(out)} arrays, sha256 {digest}")
 
 
 if __name__ == "__main__":

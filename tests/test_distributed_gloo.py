@@ -60,3 +60,36 @@ def test_sharded_equals_single_process(world, total):
     segs = np.random.default_rng(0).integers(0, 3, size=(total, 48, 64)).astype(np.uint8)
     ref = np.stack([ocv_c.create_occupancy_grid(s, bev._bev_matrix, 120, 100, 1.0, 1.0, 1.0, 0.05) for s in segs])
     assert np.array_equal(got, ref)
+
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+@pytest.mark.timeout(300)
+def test_bench_gpus_n_starts_n_ranks_without_a_launcher():
+    """`python bench.py --gpus 2 --backend gloo` with no launcher: bench.py starts
+    torch.distributed.run with 2 ranks as a child, the ranks form a gloo group, all-gather their grids
+    and check the gathered batch (--launcher-check: synthetic grids, no GPU)."""
+    import json
+    import subprocess
+    import sys
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
+    r = subprocess.run([sys.executable, "bench.py", "--gpus", "2", "--backend", "gloo", "--launcher-check",
+                        "--steps", "3", "--warmup", "1", "--batch", "3"], cwd=ROOT, env=env,
+                       capture_output=True, text=True, timeout=280)
+    assert r.returncode == 0, r.stderr[-3000:]
+    lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1                           # rank 0 prints the one line
+    line = json.loads(lines[0])
+    assert line["ranks"] == 2 and line["n_gpus"] == 2 and line["backend"] == "gloo"
+    assert line["global_batch"] == 6 and line["gather_check"] is True
+
+
+def test_bench_refuses_world_size_other_than_gpus():
+    """Under a launcher, WORLD_SIZE != --gpus exits 2 before any work (no mislabelled n_gpus)."""
+    import subprocess
+    import sys
+    env = dict(os.environ, WORLD_SIZE="2", RANK="0", LOCAL_RANK="0")
+    r = subprocess.run([sys.executable, "bench.py", "--gpus", "4", "--launcher-check"], cwd=ROOT, env=env,
+                       capture_output=True, text=True, timeout=120)
+    assert r.returncode == 2 and "WORLD_SIZE 2 != --gpus 4" in r.stderr

@@ -226,21 +226,24 @@ def test_sharded_pipeline_two_ranks_one_gpu(gpu, blocks):
 @pytest.mark.parametrize("overlap", [0, 2])
 def test_bench_distributed_branch_gloo_one_gpu(gpu, overlap):
     """bench.py's N > 1 branch (process group, in-step gather_grids, max-over-ranks timing, the
-    gathered-grid check) run end to end by torch.distributed.run with 2 ranks on this one GPU;
-    --overlap-gather 2 forces the RCCL run's overlapped form (two captured steps, the gather on a
-    communication stream) onto the gloo group, the only multi-rank group one GPU can host."""
-    port = _free_port()
-    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
-           "--master-addr", "127.0.0.1", "--master-port", str(port), "bench.py", "--gpus", "2",
+    gathered-grid check) run end to end as `python bench.py --gpus 2 --backend gloo` with NO launcher:
+    bench.py starts the 2 ranks itself (a torch.distributed.run child, started before it touches the
+    GPU); both ranks share this one GPU. --overlap-gather 2 forces the RCCL run's overlapped form (two
+    captured steps, the gather on a communication stream) onto the gloo group, the only multi-rank
+    group one GPU can host."""
+    cmd = [sys.executable, "bench.py", "--gpus", "2",
            "--backend", "gloo", "--steps", "5", "--warmup", "3", "--batch", "4", "--height", "96", "--width", "128",
            "--extras", "0", "--no-cpu-baseline", "--overlap-gather", str(overlap)]
     env = dict(os.environ, HSA_ENABLE_IPC_MODE_LEGACY=os.environ.get("HSA_ENABLE_IPC_MODE_LEGACY", "0"))
+    for k in ("WORLD_SIZE", "RANK", "LOCAL_RANK"):
+        env.pop(k, None)
     r = subprocess.run(cmd, cwd=ROOT, capture_output=True, text=True, timeout=220, env=env)
     assert r.returncode == 0, r.stderr[-3000:]
     line = json.loads([ln for ln in r.stdout.splitlines() if ln.startswith("{")][-1])
     print(json.dumps({k: line[k] for k in ("value", "n_gpus", "ms_per_step", "config")}))
     assert line["config"]["global_batch"] == 8 and line["config"]["gather_check"] is True
-    assert line["n_gpus"] == 1 and line["value"] > 0
+    assert line["n_gpus"] == 2 and line["config"]["ranks"] == 2 and line["config"]["devices"] == 1
+    assert line["config"]["backend"].startswith("gloo") and line["value"] > 0
     assert ("overlapped" in line["config"]["parallelism"]) == (overlap == 2)
 
 
@@ -262,7 +265,7 @@ def test_bench_rccl_branch_one_rank(gpu):
     line = json.loads([ln for ln in r.stdout.splitlines() if ln.startswith("{")][-1])
     print(json.dumps({k: line[k] for k in ("value", "n_gpus", "ms_per_step", "config")}))
     assert line["config"]["backend"] == "rccl" and line["config"]["gather_check"] is True
-    assert "RCCL all-gather" in line["config"]["parallelism"]
+    assert "RCCL all-gather" in line["config"]["parallelism"] and line["config"]["ranks"] == 1
     assert line["n_gpus"] == 1 and line["value"] > 0
 
 

@@ -19,7 +19,7 @@ import pytest
 import torch
 
 from bugcar_image_segmentation_amd import _native as N
-from bugcar_image_segmentation_amd import synthetic
+from bugcar_image_segmentation_amd import enet_spec, synthetic
 from bugcar_image_segmentation_amd.models import ENET
 from bugcar_image_segmentation_amd.pipeline import OccupancyPipeline
 from oracle import enet_oracle as eo
@@ -74,3 +74,97 @@ def test_timed_configuration_vs_storage_oracle(gpu, blocks, prec):
                                            bev.cm_per_px, *grid)
         assert np.array_equal(g_np[i], want), i
     print(f"{prec}: worst per-frame agreement {min(worst):.5f}")
+
+
+# ---------------------------------------------------------------- the credited configuration (fp32)
+def _engine_x(frame_bgr, H, W):
+    """The engine's own normalisation of a BGR frame (the fused table rounds (v/256 - mean)/std to f32)."""
+    return ENET.preprocess_device(frame_bgr, width=W, height=H).cpu().numpy().astype(np.float32)
+
+
+def test_fp32_timed_configuration_b64_one_stream(gpu, blocks):
+    """What bench.py times and credits: 64 frames of 480x640 through
+    OccupancyPipeline(streams=1) in fp32 — ONE context at B = 64, so the B = 64 tile choices (C64 8x16,
+    C128 16x16 / 20x16 / 4x80 / asym) and that launch's range exponents. Frames 0, 31 and 63 (first /
+    middle / last of the batch): the logits of the B = 64 context within 1e-3 of the fp32 oracle, the
+    class maps exact on decided pixels, the step's class maps the LUT of those logits, its grids the C
+    rasteriser's on them. Then batch independence: every frame's logits equal the same frame's
+    single-frame forward bit for bit (damped default weights: every range exponent 0)."""
+    H, W, B = 480, 640, 64
+    model = ENET(weights=blocks, precision="fp32")
+    bev = synthetic.synthetic_bev(H, W)
+    grid = (synthetic.GRID_W_M, synthetic.GRID_H_M, synthetic.CELL_M)
+    pipe = OccupancyPipeline(model, bev, *grid, model_hw=(H, W), streams=1)
+    frames = torch.from_numpy(synthetic.uniform_frames(B, H, W, seed=0)).to(gpu)   # bench.py's rank-0 frames
+    grids = pipe.run(frames).clone()
+    seg = pipe._seg.clone()
+    logits = torch.empty((B, model.num_classes, H, W), dtype=torch.float32, device=gpu)
+    model.ctx.forward_bgr(frames, B, H, W, N.OUT_LOGITS_F32, logits)          # the same B = 64 context
+    torch.cuda.synchronize()
+    lut3 = torch.tensor(eo.LUT3, device=gpu)
+    assert torch.equal(seg, lut3[logits.argmax(1)].to(torch.uint8))
+    seg_np, g_np = seg.cpu().numpy(), grids.cpu().numpy()
+    for i in (0, 31, 63):
+        x = _engine_x(frames[i].cpu().numpy(), H, W)
+        ref = eo.forward(blocks, x)[0]
+        got = logits[i].cpu().numpy()
+        err = float(np.abs(got - ref).max())
+        s = np.sort(ref, axis=0)
+        decided = (s[-1] - s[-2]) > max(2.5 * err, 1e-5)
+        n_exc = int(decided.size - decided.sum())
+        print(f"fp32 B=64 frame {i}: max|dlogit| {err:.2e}, excused near-ties {n_exc} of {decided.size}")
+        assert err < 1e-3
+        assert n_exc <= 1e-4 * decided.size
+        assert (got.argmax(0)[decided] == ref.argmax(0)[decided]).all()
+        assert (seg_np[i][decided] == eo.LUT3[ref.argmax(0)][decided]).all()
+        want = ocv_c.create_occupancy_grid(seg_np[i], bev._bev_matrix, bev.after_warp_width, bev.after_warp_height,
+                                           bev.cm_per_px, *grid)
+        assert np.array_equal(g_np[i], want), i
+    # batch independence: a B = 1 context, frame by frame, bit for bit
+    assert model.ctx.debug_info(1) == 0
+    one = ENET(weights=blocks, precision="fp32")
+    lg1 = torch.empty((1, model.num_classes, H, W), dtype=torch.float32, device=gpu)
+    differ = []
+    for i in range(B):
+        one.ctx.forward_bgr(frames[i:i + 1], 1, H, W, N.OUT_LOGITS_F32, lg1)
+        if not torch.equal(lg1[0], logits[i]):
+            differ.append((i, float((lg1[0] - logits[i]).abs().max())))
+    torch.cuda.synchronize()
+    print(f"fp32 batch independence: {B - len(differ)} of {B} frames bit-identical at B = 1 and B = 64; {differ[:4]}")
+    assert not differ
+
+
+def test_fp32_mixed_range_batch_undamped(gpu):
+    """The range exponents are per LAUNCH (a max over the whole batch, mfma_common.h), so with scaling
+    active a frame's logits can depend on the other frames in its batch. SURVEY's undamped draw
+    (activations past f16's range) at B = 8, 240x320, with frame 1's input x1e3 and frame 2's x1e-3
+    among normal frames: every frame passes the attributed range bar against fp64 relative to its own
+    max |logit| (oracle range_verdict), and its difference from its own single-frame forward is
+    printed and bounded by the same bar (p99 <= 2e-6 of its max, <= 0.5% of its pixels beyond 5e-6)."""
+    bl = enet_spec.build_enet(res_gamma=(0.5, 1.5))
+    B, H, W = 8, 240, 320
+    bgr = synthetic.road_frames(B, H, W, seed=21)
+    x = np.ascontiguousarray(np.moveaxis(((bgr[..., ::-1] / 256.0 - eo.IMAGE_MEAN) / eo.IMAGE_STD), -1, 1))
+    x = x.astype(np.float32)
+    x[1] *= np.float32(1e3)
+    x[2] *= np.float32(1e-3)
+    m = ENET(weights=bl, precision="fp32")
+    got = m.logits(x)
+    ties = eo.PoolTies()
+    ref = eo.forward(bl, x.astype(np.float64), torch.float64, ties=ties)
+    idx = eo.engine_pool_indices(m.ctx, bl, ties, B, H, W)
+    ok, msg, _st = eo.range_verdict(got, ref, ties, idx, "undamped mixed-range batch B=8")
+    print(msg)
+    assert ok, msg
+    one = ENET(weights=bl, precision="fp32")
+    worst = []
+    for i in range(B):
+        g1 = one.logits(x[i:i + 1])[0]
+        amax = float(np.abs(ref[i]).max())
+        e = np.abs(g1 - got[i]).max(0) / amax
+        p99, off = float(np.percentile(e, 99)), int((e > eo.RANGE_REL).sum())
+        worst.append((i, float(e.max()), p99, off))
+        print(f"frame {i}: max|logit| {amax:.2e}; |batch - single| / max: max {e.max():.1e} p99 {p99:.1e}, "
+              f"{off} pixels beyond {eo.RANGE_REL:g}")
+        assert np.isfinite(g1).all()
+        assert p99 <= eo.RANGE_REL99 and off <= max(eo.RANGE_MAX_OFF * e.size, 2 * 32 * 32)

@@ -271,3 +271,70 @@ def test_golden_enet(blocks):
     logits = eo.forward(blocks, g["x"], torch.float64)
     assert np.abs(logits - g["logits"]).max() < 1e-9
     assert np.array_equal(eo.LUT3[eo.argmax_classes(logits)], g["cls3"])
+
+
+# ---------------------------------------------------------------- the fp32 range bar's attribution
+def _undamped_case(H=480, W=640, seed=5, n=2):
+    bl = enet_spec.build_enet(res_gamma=(0.5, 1.5))
+    bgr = synthetic.road_frames(n, H, W, seed=seed)
+    x = np.ascontiguousarray(np.moveaxis(((bgr[..., ::-1] / 256.0 - eo.IMAGE_MEAN) / eo.IMAGE_STD), -1, 1))
+    return bl, x.astype(np.float32)
+
+
+def _as_engine_idx(ties):
+    """A PoolTies' own first-maximum positions in the engine's NHWC index layout."""
+    return {i: np.ascontiguousarray(p.permute(0, 2, 3, 1).numpy()) for i, p in ties.pos.items()}
+
+
+def test_range_bar_attributes_the_fp32_oracles_own_pool_flips():
+    """The fp32 oracle on SURVEY's undamped draw (480x640, the frame where it leaves the bar on ~625
+    pixels vs fp64): its own pool indices, taken as the 'engine' indices, flip only at fp64 near-ties,
+    and every pixel beyond the bar lies in their footprint — the range verdict passes. Then two faults
+    the verdict must catch: an index flipped at a window that is no near-tie, and an error injected
+    outside the footprint."""
+    bl, x = _undamped_case()
+    t64, t32 = eo.PoolTies(), eo.PoolTies()
+    r64 = eo.forward(bl, x.astype(np.float64), torch.float64, ties=t64)
+    r32 = eo.forward(bl, x, torch.float32, ties=t32)
+    idx = _as_engine_idx(t32)
+    ok, msg, st = eo.range_verdict(r32, r64, t64, idx, "fp32 oracle vs fp64")
+    print(msg)
+    assert ok, msg
+    assert st["beyond"] > 0 and st["flipped_windows"] > 0     # the case exercises the attribution
+    # fault 1: flip one decided (gap > kappa) window of the deeper pool
+    d = eo.down_blocks(bl)[-1]
+    g = t64.gap[d]
+    n, c, yy, xx = [int(v[0]) for v in torch.nonzero(g > 1e-2, as_tuple=True)]
+    bad = {k: v.copy() for k, v in idx.items()}
+    bad[d][n, yy, xx, c] = (bad[d][n, yy, xx, c] + 1) % 4
+    ok, msg, st = eo.range_verdict(r32, r64, t64, bad, "one decided window flipped")
+    assert not ok and st["flips_not_near_tie"] == 1, msg
+    # fault 2: an error of 1e-5 of the max at a pixel outside the footprint
+    fp = t64.footprint(t64.flips(idx))
+    n, yy, xx = [int(v[0]) for v in np.nonzero(~fp)]
+    got = r32.copy()
+    got[n, 3, yy, xx] += 1e-5 * np.abs(r64).max()
+    ok, msg, st = eo.range_verdict(got, r64, t64, idx, "error outside the footprint")
+    assert not ok and st["beyond_outside_footprint"] == 1, msg
+
+
+def test_pool_tie_footprint_geometry():
+    """The footprint of one flipped window of each pool at 96x128: a flip at the 1/8 stage reaches
+    further than one at the 1/4 stage, both are local (far below the frame), and no flips -> empty."""
+    bl, x = _undamped_case(96, 128, seed=3, n=1)
+    t = eo.PoolTies()
+    eo.forward(bl, x.astype(np.float64), torch.float64, ties=t)
+    d1, d2 = eo.down_blocks(bl)
+    none = {i: torch.zeros_like(p, dtype=torch.bool) for i, p in t.pos.items()}
+    assert not t.footprint(none).any()
+    sizes = {}
+    for d in (d1, d2):
+        w = {i: v.clone() for i, v in none.items()}
+        w[d][0, 0, w[d].shape[2] // 2, w[d].shape[3] // 2] = True
+        fp = t.footprint(w)
+        sizes[d] = int(fp.sum())
+        ys, xs = np.nonzero(fp[0])
+        s = 8 if d == d2 else 4                 # the pool output's stride in logits pixels
+        cy, cx = w[d].shape[2] // 2 * s, w[d].shape[3] // 2 * s
+        assert ys.min() <= cy + s // 2 <= ys.max() and xs.min() <= cx + s // 2 <= xs.max()
+    assert 0 < sizes[d1] < sizes[d2] < 96 * 128 // 4

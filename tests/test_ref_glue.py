@@ -20,6 +20,17 @@ FIX = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", "ref_gl
 GEOMS = ("bench", "small_neg", "small_odd")
 
 
+def test_fixture_is_the_committed_one():
+    """The fixture file is the one the generator wrote when it was run (its SHA-256 is committed beside
+    it): the generator executes the reference's own code, so it is never run by a test or CI job —
+    only by hand in the build container — and its output is checked by content here."""
+    import hashlib
+    with open(FIX, "rb") as f:
+        got = hashlib.sha256(f.read()).hexdigest()
+    with open(FIX.replace(".npz", ".sha256")) as f:
+        assert got == f.read().strip()
+
+
 @pytest.fixture(scope="module")
 def fx():
     with np.load(FIX, allow_pickle=False) as z:
