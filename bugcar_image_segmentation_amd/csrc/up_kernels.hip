@@ -61,6 +61,17 @@ __global__ void __launch_bounds__((up_threads<T, CIN>()), (sizeof(T) == 2 ? (CIN
     constexpr int NR3 = COUT / 16;                    // expansion rows
     static_assert(COUT % 16 == 0 && I % 16 == 0 && CIN % 32 == 0 && I <= 32, "up_kernel shape");
     constexpr bool SWAP = ES == 2 && NR3 % 2 == 0;    // 16-B output chunks by lane-pair swaps (bneck phase 3)
+// fp32, COUT = 64 (a pixel = two 128-B lines): LINES stores whole lines. An accumulator quad is 16 B
+// (channels 16 r + 4 kq .. + 3 of pixel col), so a store per row block r writes 16 pixels x 64 B —
+// half lines, and under the non-temporal policy each half went to HBM on its own (PMC, round 5: 422 MB
+// written per 64-frame launch against 315 MB of output). With LINES the quads of row blocks 2 t and
+// 2 t + 1 of pixels col and col ^ 8 are traded across lanes 8 apart (one DPP row rotation per dword),
+// so each of the two stores per t writes the whole line t of 8 pixels (lanes col and col ^ 8: the
+// line's two 64-B halves). Same values, other lanes: bit-identical output
+#ifndef UP_F32_LINES
+#define UP_F32_LINES 1
+#endif
+    constexpr bool LINES = ES == 4 && NR3 % 2 == 0 && UP_F32_LINES;
     // bias placement of the unfused launches (bias_in_acc of their row counts): the main and e1
     // 1x1s both accumulate from the bias (the host plans this kernel only then), the tconv and the
     // expansion as their own row counts say
@@ -208,6 +219,18 @@ __global__ void __launch_bounds__((up_threads<T, CIN>()), (sizeof(T) == 2 ? (CIN
 
         // ---- per output phase (a, b): t = act(tconv) -> expansion -> + unpooled main -> act -> store
         const uint32_t obase = pv ? (uint32_t)((n * 2 * a.h + 2 * y) * (2 * a.w) + 2 * x) : 0u;   // output pixel (2y, 2x)
+        // LINES: lanes col < 8 store pixels col (first store) and col + 8 (second), lanes col >= 8 pixels
+        // col - 8 and col: the output base of the fragment's other pixel f * 16 + (col ^ 8)
+        uint32_t obase_o = 0u;
+        bool pv_o = false;
+        if constexpr (LINES) {
+            const int po = f * 16 + (col ^ 8);
+            pv_o = po < a.M;
+            const uint32_t ppo = pv_o ? (uint32_t)po : 0u;
+            const int no = (int)fdiv(ppo, a.mHW, a.sHW), rro = (int)ppo - no * hw;
+            const int yo = (int)fdiv((uint32_t)rro, a.mW, a.sW), xo = rro - yo * a.w;
+            obase_o = pv_o ? (uint32_t)((no * 2 * a.h + 2 * yo) * (2 * a.w) + 2 * xo) : 0u;
+        }
         // (not unrolled: one phase's weight fragments live at a time)
 #pragma unroll 1
         for (int ph = 0; ph < 4; ++ph) {
@@ -228,7 +251,8 @@ __global__ void __launch_bounds__((up_threads<T, CIN>()), (sizeof(T) == 2 ? (CIN
             };
             Raw bop3;
             to_bop(bop3, ep2(0), NE > 1 ? ep2(1) : make_float4(0.f, 0.f, 0.f, 0.f));
-            const uint32_t opix = obase + (uint32_t)((ph >> 1) * 2 * a.w + (ph & 1));
+            const uint32_t pho = (uint32_t)((ph >> 1) * 2 * a.w + (ph & 1));
+            const uint32_t opix = obase + pho;
             auto ep3 = [&](int r) {
                 const int c = r * 16 + kq * 4;
                 static_assert(B3ACC, "the expansion starts from the bias");
@@ -259,6 +283,31 @@ __global__ void __launch_bounds__((up_threads<T, CIN>()), (sizeof(T) == 2 ? (CIN
                     pl16swap(x1, y1);
                     const int ch = (2 * t + (kq & 1)) * 16 + 8 * (kq >> 1);
                     bst16o<OAUX>(ro, pv ? (opix * COUT + ch) * ES : OOB, make_uint4(x0, x1, y0, y1));
+                }
+            } else if constexpr (LINES) {
+                const bool lo8 = col < 8;
+                // first store: pixel col & 7 (lanes col < 8 their own, col >= 8 the other's); second: + 8
+                const uint32_t pa = lo8 ? obase + pho : obase_o + pho, pb = lo8 ? obase_o + pho : obase + pho;
+                const bool va = lo8 ? pv : pv_o, vb = lo8 ? pv_o : pv;
+                const int hc = lo8 ? 0 : 16;                  // channel half of the line this lane writes
+#pragma unroll
+                for (int t = 0; t < NR3 / 2; ++t) {
+                    const float4 v0 = ep3(2 * t), v1 = ep3(2 * t + 1);
+                    rng_acc4(amo, v0);
+                    rng_acc4(amo, v1);
+                    const uint4 u0 = __builtin_bit_cast(uint4, v0), u1 = __builtin_bit_cast(uint4, v1);
+                    // lanes col < 8 send their block 2t + 1 quad, lanes col >= 8 their block 2t quad, to the
+                    // lane 8 apart in the 16-lane row (row_ror:8 is its own inverse)
+                    const uint4 xs = lo8 ? u1 : u0;
+                    uint4 ys;
+                    ys.x = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)xs.x, 0x128, 0xf, 0xf, false);
+                    ys.y = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)xs.y, 0x128, 0xf, 0xf, false);
+                    ys.z = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)xs.z, 0x128, 0xf, 0xf, false);
+                    ys.w = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)xs.w, 0x128, 0xf, 0xf, false);
+                    const uint4 qa = lo8 ? u0 : ys, qb = lo8 ? ys : u1;
+                    const int ch = t * 32 + hc + kq * 4;
+                    bst16o<OAUX>(ro, va ? (pa * COUT + ch) * ES : OOB, qa);
+                    bst16o<OAUX>(ro, vb ? (pb * COUT + ch) * ES : OOB, qb);
                 }
             } else {
 #pragma unroll

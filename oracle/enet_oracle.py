@@ -142,7 +142,8 @@ class PoolTies:
                 t = self._up2(win[ref], size)
                 m = t if m is None else (t | self._grow(self._up2(m, size), *self._radius(units[1:])))
             elif e[0] == "fullconv":
-                size, B, k = e[1], e[2], e[3]
+                size, k = e[1], e[3]
+                B = next(iter(self.pos.values())).shape[0] if self.pos else e[2]
                 m = (torch.zeros((B,) + tuple(size), dtype=torch.bool) if m is None
                      else self._grow(self._up2(m, size), (k - 1) // 2, (k - 1) // 2))
         return m.numpy()
@@ -280,7 +281,9 @@ def range_verdict(got, ref, ties: PoolTies, engine_idx: dict, what: str):
     cls_ok = bool((got.argmax(1)[dec] == ref.argmax(1)[dec]).all())
     n_off = off.reshape(off.shape[0], -1).sum(1)
     allowed = max(RANGE_MAX_OFF * off[0].size, 2 * 32 * 32)
+    e_out = e[~fp]
     stats = {"p99": p99, "max": float(e.max()), "beyond": int(off.sum()), "flipped_windows": n_flip,
+             "p99_outside_footprint": float(np.percentile(e_out, 99)) if e_out.size else 0.0,
              "flips_not_near_tie": bad_flip, "max_flip_gap": max_gap, "footprint": int(fp.sum()),
              "beyond_outside_footprint": int(outside.sum()),
              "max_outside_footprint": float(np.where(fp, 0.0, e).max())}

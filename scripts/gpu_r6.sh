@@ -8,7 +8,7 @@ T=${1:-r6}
 STEPS=${2:-"range suite smoke bench"}
 mkdir -p gpurun_out/$T
 export TMPDIR=/tmp
-PYT="python -u -m pytest -x -v --timeout 300 --timeout-method thread"
+PYT="python -u -m pytest -x -v -s --timeout 300 --timeout-method thread"
 for s in $STEPS; do
   case $s in
     range) timeout -k 10 600 $PYT tests/test_gpu_range.py > gpurun_out/$T/range.log 2>&1; rc=$? ;;
