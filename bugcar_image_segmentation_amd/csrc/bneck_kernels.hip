@@ -391,6 +391,17 @@ __device__ __forceinline__ bool bneck_body(const BneckArgs &a, float rlane) {
     constexpr bool DKEEP = BNECK_DKEEP && DN && ((sizeof(T) == 2 && SWAP) || (sizeof(T) == 4 && BNECK_DKEEP_F32 && REG3));
     constexpr int NPK = DN ? (CI + 31) / 32 : 1;      // DKEEP: pooled chunks (32 channels of the row pair) per lane and fragment
     constexpr int PKW = sizeof(T) == 4 ? 2 : 1;       // 16-B words per pooled chunk
+    // LINES (fp32 register epilogue, C = 128, round 6; on the fp32 down C64 form it cost 4 VGPRs and the third
+    // wave per SIMD): an accumulator quad is 16 B (channels 16 r + 4 kq ..
+    // + 3 of pixel col), so one store per row r writes 16 pixels x 64 B — half lines. With LINES the quads
+    // of rows 2u and 2u + 1 of pixels col and col ^ 8 are traded across lanes 8 apart (one DPP row
+    // rotation per dword) and each of the two stores per u writes the whole 128-B line u of 8 pixels.
+    // Same values, other lanes: bit-identical (the fp32 up C64 block's form of this cut its HBM writes
+    // 422 -> 315 MB and its time 129 -> 111 us per 64-frame launch)
+#ifndef BNECK_F32_LINES
+#define BNECK_F32_LINES 1
+#endif
+    constexpr bool LINES = BNECK_F32_LINES && sizeof(T) == 4 && REG3 && C == 128 && (KEEPF || (DKEEP && PKW == 2)) && RQ3 % 2 == 0;
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     // fp32 (parity mode): t0 / t1a live in LDS as split-f16 parts (mfma_common.h st4s: the weights'
     // layout, 32 B per 8 channels as the f32 values take), split once when written rather than at every
@@ -1384,6 +1395,45 @@ __device__ __forceinline__ bool bneck_body(const BneckArgs &a, float rlane) {
                 }
                 return act(v, cs3 + ch);
             };
+            if constexpr (LINES) {
+                // whole-line stores (see LINES): rows 2u / 2u + 1 of pixels col and col ^ 8 traded across
+                // lanes 8 apart, then line u of pixel col & 7 and of pixel (col & 7) + 8
+                const uint32_t po_o = pix_base(wave + NW * j, col ^ 8);
+                const bool lo8 = col < 8;
+                const uint32_t pa = lo8 ? po : po_o, pb = lo8 ? po_o : po;
+#pragma unroll
+                for (int u = 0; u < RQ3 / 2; ++u) {
+                    float4 v2[2];
+#pragma unroll
+                    for (int h = 0; h < 2; ++h) {
+                        const int t = 2 * u + h;
+                        uint4 rc;
+                        if constexpr (KEEPF) {
+                            const RawF &k = reinterpret_cast<const RawF &>(kx[j][t >> 1]);
+                            rc = __builtin_bit_cast(uint4, (t & 1) ? k.b : k.a);
+                        } else {
+                            rc = t < 2 * NPK ? pres[j][t < 2 * NPK ? t : 0] : make_uint4(0u, 0u, 0u, 0u);
+                        }
+                        f32x4 acc = bias_m(cb3 + t * 16 + kq * 4, b3m, SCL || scl);
+                        WRaw wf;
+                        ldw(wf, w3 + (t * 16 + col) * K3S);
+                        mma(acc, wf, tf[j]);
+                        v2[h] = act(add4(out3(t, acc), __builtin_bit_cast(float4, rc)), cso + t * 16 + kq * 4);
+                        rng_acc4(amo, v2[h]);
+                    }
+                    const uint4 u0 = __builtin_bit_cast(uint4, v2[0]), u1 = __builtin_bit_cast(uint4, v2[1]);
+                    const uint4 xs = lo8 ? u1 : u0;
+                    uint4 ys;
+                    ys.x = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)xs.x, 0x128, 0xf, 0xf, false);
+                    ys.y = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)xs.y, 0x128, 0xf, 0xf, false);
+                    ys.z = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)xs.z, 0x128, 0xf, 0xf, false);
+                    ys.w = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)xs.w, 0x128, 0xf, 0xf, false);
+                    const uint32_t cb = (uint32_t)(u * 32 + (lo8 ? 0 : 16) + kq * 4) * (uint32_t)sizeof(T);
+                    bst16o<OAUX>(rob, pa == OOB ? OOB : pa + cb, lo8 ? u0 : ys);
+                    bst16o<OAUX>(rob, pb == OOB ? OOB : pb + cb, lo8 ? ys : u1);
+                }
+                continue;
+            }
 #pragma unroll
             for (int t = 0; t < RQ3; ++t) {
                 const uint32_t off = po == OOB ? OOB : po + (uint32_t)chunk_ch(t) * (uint32_t)sizeof(T);

@@ -440,11 +440,12 @@ __device__ __forceinline__ int rng_exp_bound(float B, int p) {
     const int l = rng_log2(B);
     return l + p >= 3 && l + p < 15 ? p : rng_clamp(14 - l);
 }
-// 2^e from the exponent bits (a scalar when e is); e clamped to [-126, 126] so no exponent can wrap
-// into the sign or exponent field (a multiplier needing more than that is beyond f32 anyway)
+// 2^e as a scalar: v_ldexp_f32 saturates (0 / inf beyond f32) where building the exponent bits would
+// wrap into the sign or exponent field for |e| > 126 (a difference of two chained exponents can reach
+// that only for pathological ranges); readfirstlane keeps it an SGPR. (Clamping e on the scalar unit
+// instead cost the fp32 down C64 form 14 VGPRs and its third wave per SIMD: 141 -> 157 us per launch)
 __device__ __forceinline__ float rng_pow2(int e) {
-    e = e < -126 ? -126 : e > 126 ? 126 : e;
-    return __int_as_float((e + 127) << 23);
+    return __int_as_float(__builtin_amdgcn_readfirstlane(__float_as_int(__builtin_ldexpf(1.f, e))));
 }
 // max |v| of a launch's input: the RNG_SLOTS words (four per lane, then a wave reduction)
 // rng_read in two halves: the lane's slot load (issue it early) and the wave reduction (consume it
