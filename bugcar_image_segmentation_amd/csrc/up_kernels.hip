@@ -72,6 +72,9 @@ __global__ void __launch_bounds__((up_threads<T, CIN>()), (sizeof(T) == 2 ? (CIN
 #define UP_F32_LINES 1
 #endif
     constexpr bool LINES = ES == 4 && NR3 % 2 == 0 && UP_F32_LINES;
+    // COUT = 16 (a pixel = 64 B): the two column phases of an output row are adjacent pixels, one line —
+    // the even phase's quad waits in registers and is traded and stored with the odd one's
+    constexpr bool LINES16 = ES == 4 && NR3 == 1 && UP_F32_LINES;
     // bias placement of the unfused launches (bias_in_acc of their row counts): the main and e1
     // 1x1s both accumulate from the bias (the host plans this kernel only then), the tconv and the
     // expansion as their own row counts say
@@ -223,7 +226,7 @@ __global__ void __launch_bounds__((up_threads<T, CIN>()), (sizeof(T) == 2 ? (CIN
         // col - 8 and col: the output base of the fragment's other pixel f * 16 + (col ^ 8)
         uint32_t obase_o = 0u;
         bool pv_o = false;
-        if constexpr (LINES) {
+        if constexpr (LINES || LINES16) {
             const int po = f * 16 + (col ^ 8);
             pv_o = po < a.M;
             const uint32_t ppo = pv_o ? (uint32_t)po : 0u;
@@ -231,6 +234,7 @@ __global__ void __launch_bounds__((up_threads<T, CIN>()), (sizeof(T) == 2 ? (CIN
             const int yo = (int)fdiv((uint32_t)rro, a.mW, a.sW), xo = rro - yo * a.w;
             obase_o = pv_o ? (uint32_t)((no * 2 * a.h + 2 * yo) * (2 * a.w) + 2 * xo) : 0u;
         }
+        float4 ev_prev = make_float4(0.f, 0.f, 0.f, 0.f);   // LINES16: the even phase's quad
         // (not unrolled: one phase's weight fragments live at a time)
 #pragma unroll 1
         for (int ph = 0; ph < 4; ++ph) {
@@ -283,6 +287,28 @@ __global__ void __launch_bounds__((up_threads<T, CIN>()), (sizeof(T) == 2 ? (CIN
                     pl16swap(x1, y1);
                     const int ch = (2 * t + (kq & 1)) * 16 + 8 * (kq >> 1);
                     bst16o<OAUX>(ro, pv ? (opix * COUT + ch) * ES : OOB, make_uint4(x0, x1, y0, y1));
+                }
+            } else if constexpr (LINES16) {
+                const float4 v = ep3(0);
+                rng_acc4(amo, v);
+                if ((ph & 1) == 0) {
+                    ev_prev = v;
+                } else {
+                    // line of input pixel p: output pixels (2y + ph / 2, 2x) and (.., 2x + 1), 32 channels
+                    const bool lo8 = col < 8;
+                    const uint32_t phe = pho - 1u;             // the even pixel of this row
+                    const uint32_t pa = (lo8 ? obase : obase_o) + phe, pb = (lo8 ? obase_o : obase) + phe;
+                    const bool va = lo8 ? pv : pv_o, vb = lo8 ? pv_o : pv;
+                    const uint4 u0 = __builtin_bit_cast(uint4, ev_prev), u1 = __builtin_bit_cast(uint4, v);
+                    const uint4 xs = lo8 ? u1 : u0;
+                    uint4 ys;
+                    ys.x = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)xs.x, 0x128, 0xf, 0xf, false);
+                    ys.y = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)xs.y, 0x128, 0xf, 0xf, false);
+                    ys.z = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)xs.z, 0x128, 0xf, 0xf, false);
+                    ys.w = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)xs.w, 0x128, 0xf, 0xf, false);
+                    const int ch = (lo8 ? 0 : 16) + kq * 4;   // channel 16 + c of the even pixel = c of the odd one
+                    bst16o<OAUX>(ro, va ? (pa * COUT + ch) * ES : OOB, lo8 ? u0 : ys);
+                    bst16o<OAUX>(ro, vb ? (pb * COUT + ch) * ES : OOB, lo8 ? ys : u1);
                 }
             } else if constexpr (LINES) {
                 const bool lo8 = col < 8;
