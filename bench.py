@@ -64,6 +64,7 @@ F32_SPLIT_PRODUCTS = 3          # fp32 mode: one f32 product = three f16 MFMA pr
 SURVEY_BYTES_PER_FRAME = 180.2e6   # bf16 per-layer activation bytes per 480x640 frame
 # rocprofv3 kernel names of the plan's kernel tags (scripts/layer_times.py maps them back)
 KERNEL_NAMES = {"bneck C128": "bneck_kernel<{t},128,sym>", "bneck C128 asym": "bneck_kernel<{t},128,asym>",
+                "bneck2 C128": "bneck2_f32_kernel",
                 "bneck C64": "bneck_kernel<{t},64,sym>", "bneck C16": "bneck_kernel<{t},16,sym>",
                 "init": "init_kernel<{t},bgr>"}
 TEMPLATE_TYPE = {"fp16": "_Float16", "bf16": "__bf16", "fp32": "float"}   # the kernels' template type names

@@ -128,9 +128,10 @@ static bool bneck_wide(int C, int v, bool asym) {
     return false;
 }
 
-int bneck_variants(int C) { return C == 128 ? 5 : C == 16 ? 2 : 3; }
+int bneck_variants(int C) { return C == 128 ? 6 : C == 16 ? 2 : 3; }   // C128 variant 5: bneck2_kernels.hip (fp32)
 
 void bneck_shape(int C, int v, int &th, int &tw, int &nw, int *rd) {
+    if (C == 128 && v == BNECK2_V) { th = 16; tw = 16; nw = 16; if (rd) *rd = 0; return; }
 #define BS_CASE(CC, VV) if (C == CC && v == VV) { th = BShape<CC, VV>::TH; tw = BShape<CC, VV>::TW; nw = BShape<CC, VV>::NW; if (rd) *rd = BShape<CC, VV>::RD; return; }
     BS_CASE(128, 0) BS_CASE(128, 1) BS_CASE(128, 2) BS_CASE(128, 3) BS_CASE(128, 4) BS_CASE(64, 0) BS_CASE(64, 1) BS_CASE(64, 2) BS_CASE(16, 0) BS_CASE(16, 1)
 #undef BS_CASE
@@ -173,34 +174,6 @@ void bneck_shape(int C, int v, int &th, int &tw, int &nw, int *rd) {
 // tile's loads are in flight (a wait for the range words alone at kernel start cost the C128 launches
 // ~4 us) and, if some exponent is non-zero, drains its loads and returns before computing anything —
 // the kernel then runs the scaled body from the start.
-struct BneckRange {
-    float xm = 1.f, b1m = 1.f, o1m = 1.f, b2m = 1.f, o2m = 1.f, b2bm = 1.f, o2bm = 1.f, b3m = 1.f, o3m = 1.f;
-    int rs1 = 0, re2b = 0;                            // asymmetric: t1a's exponent, the 1x5's accumulator exponent
-    bool scl = false, any = false;                    // scl: phase 3 multiplies (e3 != 0)
-};
-template <bool ASYM>
-__device__ __forceinline__ BneckRange bneck_range(const RangeArgs &g, float amx) {
-    BneckRange r;
-    if (g.off) return r;
-    const int sx = rng_exp_meas(amx), e1 = sx + g.sw[0];
-    const float B0 = g.n[0] * amx + g.c[0];
-    const int s0 = rng_exp_bound(B0, e1), e2 = s0 + g.sw[1];
-    const float B1 = g.n[1] * B0 + g.c[1];
-    const int s1 = rng_exp_bound(B1, e2);
-    int e2b = 0, s1b = 0;
-    if constexpr (ASYM) {
-        e2b = s1 + g.sw[2];
-        s1b = rng_exp_bound(g.n[2] * B1 + g.c[2], e2b);
-    }
-    const int e3 = (ASYM ? s1b : s1) + g.sw[3];
-    r.rs1 = s1; r.re2b = e2b;
-    r.scl = e3 != 0;
-    r.xm = rng_pow2(sx); r.b1m = rng_pow2(e1); r.o1m = rng_pow2(s0 - e1); r.b2m = rng_pow2(e2); r.o2m = rng_pow2(s1 - e2);
-    r.b2bm = rng_pow2(e2b); r.o2bm = rng_pow2(s1b - e2b); r.b3m = rng_pow2(e3); r.o3m = rng_pow2(-e3);
-    r.any = (sx | e1 | s0 | e2 | s1) != 0 || (ASYM ? (e2b != 0 || g.sw[3] != 0) : e3 != 0);
-    return r;
-}
-
 template <typename T, int C, bool ASYM, int V, bool TR, int CI, bool SCL>
 __device__ __forceinline__ bool bneck_body(const BneckArgs &a, float rlane) {
     using Raw = typename Tr<T>::Raw;
@@ -1527,6 +1500,7 @@ extern "C" int bugseg_debug_set_stamps(void *p) {
 #endif
 
 size_t bneck_lds_bytes(int prec, int C, bool asym, int v, int cin) {
+    if (C == 128 && v == BNECK2_V) return prec == PREC_F32 && !asym && cin == 0 ? bneck2_lds_bytes() : (size_t)1 << 30;
     int TH, TW, NW, RD;
     bneck_shape(C, v, TH, TW, NW, &RD);
     const int es = prec_es(prec), pad = 16 / es;
@@ -1581,6 +1555,10 @@ static const void *bneck_fun(int prec, int C, bool asym, int v, bool tr, int cin
 }
 
 int bneck_slots_per_cu(int prec, int C, bool asym, int v, bool tr, int cin) {
+    if (C == 128 && v == BNECK2_V) {
+        const char *off = std::getenv("BUGSEG_BNECK2");                 // 0: never plan it (A/B knob)
+        return prec == PREC_F32 && !asym && !tr && cin == 0 && !(off && *off == '0') ? bneck2_slots_per_cu() : 0;
+    }
     // (cached per device and form: launch_bneck asks on every launch; bugseg_runtime.cpp occupancy_per_cu)
     const void *f = bneck_fun(prec, C, asym, v, tr, cin);
     int th, tw, nw;
@@ -1590,6 +1568,8 @@ int bneck_slots_per_cu(int prec, int C, bool asym, int v, bool tr, int cin) {
 }
 
 hipError_t launch_bneck(int prec, int C, bool asym, int v, const BneckArgs &a, hipStream_t s, int cin) {
+    if (C == 128 && v == BNECK2_V)
+        return prec == PREC_F32 && !asym && !a.tr && cin == 0 ? launch_bneck2(a, s) : hipErrorInvalidValue;
     const void *f = bneck_fun(prec, C, asym, v, a.tr != 0, cin);
     if (!f) return hipErrorInvalidValue;
     int th, tw, nw;

@@ -150,6 +150,12 @@ size_t bneck_lds_bytes(int prec, int C, bool asym, int v, int cin = 0);
 // resident workgroups per CU (occupancy API); 0 if (C, asym, v, tr, cin) is not built
 int bneck_slots_per_cu(int prec, int C, bool asym, int v, bool tr, int cin = 0);
 hipError_t launch_bneck(int prec, int C, bool asym, int v, const BneckArgs &a, hipStream_t s, int cin = 0);
+// variant BNECK2_V of C = 128 (fp32, symmetric, untransposed 16 x 16 tiles): bneck2_kernels.hip, one
+// 16-wave workgroup per CU running two phase-shifted tiles on one weight copy
+constexpr int BNECK2_V = 5;
+size_t bneck2_lds_bytes();
+int bneck2_slots_per_cu();
+hipError_t launch_bneck2(const BneckArgs &a, hipStream_t s);
 
 // ---- fused upsampling bottleneck (up_kernels.hip) ----------------------------------------------
 struct UpArgs {

@@ -2001,8 +2001,8 @@ int bugseg_plan_op(bugseg_ctx *ctx, int B, int H, int W, int op, char *kernel, i
     } else if (o.kind == 1) {
         int th, tw, nw;
         bneck_shape(o.bn_c, o.bn_var, th, tw, nw, nullptr);
-        tag = std::string(o.bn_cin ? "down C" : "bneck C") + std::to_string(o.bn_c) + (o.bn_asym ? " asym" : "") + " " +
-              std::to_string(th) + "x" + std::to_string(tw);
+        tag = std::string(o.bn_cin ? "down C" : o.bn_var == BNECK2_V && o.bn_c == 128 ? "bneck2 C" : "bneck C") +
+              std::to_string(o.bn_c) + (o.bn_asym ? " asym" : "") + " " + std::to_string(th) + "x" + std::to_string(tw);
         (void)nw;
     }
     else if (o.epi == EPI_INIT || o.epi == EPI_INIT_BGR) tag = "init";

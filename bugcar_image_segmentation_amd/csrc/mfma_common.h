@@ -528,6 +528,36 @@ __device__ __forceinline__ void mul8(RawF &x, float s) {
     x.b = mulp2(x.b, s);
 }
 
+// the fused bottleneck's exponents (bneck_kernels.hip, bneck2_kernels.hip): the multipliers of x, of
+// the accumulators and of the internal tensors, from the launch's input range and the weights' bounds
+struct BneckRange {
+    float xm = 1.f, b1m = 1.f, o1m = 1.f, b2m = 1.f, o2m = 1.f, b2bm = 1.f, o2bm = 1.f, b3m = 1.f, o3m = 1.f;
+    int rs1 = 0, re2b = 0;                            // asymmetric: t1a's exponent, the 1x5's accumulator exponent
+    bool scl = false, any = false;                    // scl: phase 3 multiplies (e3 != 0)
+};
+template <bool ASYM>
+__device__ __forceinline__ BneckRange bneck_range(const RangeArgs &g, float amx) {
+    BneckRange r;
+    if (g.off) return r;
+    const int sx = rng_exp_meas(amx), e1 = sx + g.sw[0];
+    const float B0 = g.n[0] * amx + g.c[0];
+    const int s0 = rng_exp_bound(B0, e1), e2 = s0 + g.sw[1];
+    const float B1 = g.n[1] * B0 + g.c[1];
+    const int s1 = rng_exp_bound(B1, e2);
+    int e2b = 0, s1b = 0;
+    if constexpr (ASYM) {
+        e2b = s1 + g.sw[2];
+        s1b = rng_exp_bound(g.n[2] * B1 + g.c[2], e2b);
+    }
+    const int e3 = (ASYM ? s1b : s1) + g.sw[3];
+    r.rs1 = s1; r.re2b = e2b;
+    r.scl = e3 != 0;
+    r.xm = rng_pow2(sx); r.b1m = rng_pow2(e1); r.o1m = rng_pow2(s0 - e1); r.b2m = rng_pow2(e2); r.o2m = rng_pow2(s1 - e2);
+    r.b2bm = rng_pow2(e2b); r.o2bm = rng_pow2(s1b - e2b); r.b3m = rng_pow2(e3); r.o3m = rng_pow2(-e3);
+    r.any = (sx | e1 | s0 | e2 | s1) != 0 || (ASYM ? (e2b != 0 || g.sw[3] != 0) : e3 != 0);
+    return r;
+}
+
 __device__ __forceinline__ float4 prelu4m(float4 v, float4 s) {
     return make_float4(vmax(v.x, v.x * s.x), vmax(v.y, v.y * s.y), vmax(v.z, v.z * s.z), vmax(v.w, v.w * s.w));
 }

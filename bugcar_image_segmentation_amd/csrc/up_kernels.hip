@@ -71,10 +71,13 @@ __global__ void __launch_bounds__((up_threads<T, CIN>()), (sizeof(T) == 2 ? (CIN
 #ifndef UP_F32_LINES
 #define UP_F32_LINES 1
 #endif
+#ifndef UP_F32_LINES16
+#define UP_F32_LINES16 0    // the C16 block's phase-pair form: measured slower (round 6, A/B: up C16 122 -> 134 us per 64-frame launch)
+#endif
     constexpr bool LINES = ES == 4 && NR3 % 2 == 0 && UP_F32_LINES;
     // COUT = 16 (a pixel = 64 B): the two column phases of an output row are adjacent pixels, one line —
     // the even phase's quad waits in registers and is traded and stored with the odd one's
-    constexpr bool LINES16 = ES == 4 && NR3 == 1 && UP_F32_LINES;
+    constexpr bool LINES16 = ES == 4 && NR3 == 1 && UP_F32_LINES16;
     // bias placement of the unfused launches (bias_in_acc of their row counts): the main and e1
     // 1x1s both accumulate from the bias (the host plans this kernel only then), the tconv and the
     // expansion as their own row counts say

@@ -17,7 +17,7 @@ done
 /opt/rocm/bin/hipcc $FLAGS $SAN -c tests/asan/asan_driver.cpp -o $OUT/asan_driver.o &
 wait
 KOBJ=""
-for s in conv_kernels cls_kernels init_kernels bneck_kernels up_kernels prep_kernels bev_kernels deeplab_kernels; do
+for s in conv_kernels cls_kernels init_kernels bneck_kernels bneck2_kernels up_kernels prep_kernels bev_kernels deeplab_kernels; do
   KOBJ="$KOBJ $P/_build/$s.hip.o"
 done
 /opt/rocm/bin/hipcc --offload-arch=gfx950 $SAN -o $OUT/asan_driver $OUT/asan_driver.o $OUT/bugseg_runtime.o $OUT/deeplab_runtime.o $KOBJ
