@@ -51,14 +51,8 @@ static_assert(P2_LDS <= 160 * 1024, "two t0 buffers and one weight copy in 160 K
 #ifndef BNECK2_CH1
 #define BNECK2_CH1 2      // phase-1 fragments whose x loads fly together (VGPRs: 32 each)
 #endif
-#ifndef BNECK2_RESPF
-#define BNECK2_RESPF 0    // 1: both fragments' residuals loaded before the middle conv (64 VGPRs live through it)
-#endif
 #ifndef BNECK2_U2
 #define BNECK2_U2 1       // middle-conv k-steps unrolled together
-#endif
-#ifndef BNECK2_RESPAIR
-#define BNECK2_RESPAIR 1  // phase 3 loads each row pair's residual chunks right before it (else a fragment's 8 at once)
 #endif
 #ifndef BNECK2_FENCE1
 #define BNECK2_FENCE1 1   // phase 1: no weight read hoisted across k-steps (hoisted, they need 64 VGPRs)
@@ -215,78 +209,53 @@ __device__ __forceinline__ void bneck2_body(const BneckArgs &a, float rlane, flo
         int col, kq;
         lane_xy(col, kq);
         const float *w2 = w2s, *w3 = w3s;
-        // residual (x at the tile pixels, the quads of phase 3) of both fragments, in flight during the
-        // middle conv: fragment j = tile row f = hw + 8 j, pixel column col
-        uint32_t po[P2_NF2];
-        uint4 res[BNECK2_RESPF ? P2_NF2 : 1][P2_NR3];
-        auto load_res = [&](int j, uint4 (&r)[P2_NR3]) {
-#pragma unroll
-            for (int t = 0; t < P2_NR3; ++t) r[t] = bld16(rxb, po[j] == OOB ? OOB : po[j] + (uint32_t)(t * 16 + kq * 4) * 4u);
-        };
-#pragma unroll
+        const bool lo8 = col < 8;
+        // fragment by fragment (j: tile row f = hw + 8 j, pixel column col): its residual loads (x at the
+        // tile pixels, phase 3's quads) are issued first and land during its middle conv; then the
+        // expansion. (Both fragments' middle convs together, sharing each k-step's weight reads, need
+        // their accumulators and phase-3 operands live at once: past the 128-VGPR budget with the
+        // residual in flight.) The products and their order per output are the same either way.
+#pragma unroll 1
         for (int j = 0; j < P2_NF2; ++j) {
             const int f = hw + P2_NWH * j;
-            po[j] = pix_base(n, oy0 + dt * f, ox0 + dt * col);
-            if constexpr (BNECK2_RESPF) load_res(j, res[j]);
-        }
-        // phase 2: t1 = act2(W2 * t0 + b2): k-step s = tap s (4 groups of 8 channels), taps (ky, kx) = (s / 3, s % 3)
-        f32x4 acc[P2_NF2][P2_NR1];
+            const uint32_t po = pix_base(n, oy0 + dt * f, ox0 + dt * col);
+            uint4 res[P2_NR3];
 #pragma unroll
-        for (int j = 0; j < P2_NF2; ++j)
+            for (int t = 0; t < P2_NR3; ++t) res[t] = bld16(rxb, po == OOB ? OOB : po + (uint32_t)(t * 16 + kq * 4) * 4u);
+            // phase 2: t1 = act2(W2 * t0 + b2): k-step s = tap s (4 groups of 8 channels), (ky, kx) = (s / 3, s % 3)
+            f32x4 acc[P2_NR1];
 #pragma unroll
             for (int r = 0; r < P2_NR1; ++r) {
-                acc[j][r] = bias4(cb2 + r * 16 + kq * 4);
-                if constexpr (SCL) acc[j][r] = mul4(acc[j][r], b2m);
+                acc[r] = bias4(cb2 + r * 16 + kq * 4);
+                if constexpr (SCL) acc[r] = mul4(acc[r], b2m);
             }
 #pragma unroll BNECK2_U2
-        for (int s = 0; s < P2_KS2; ++s) {
-            const int ky = s / 3, kx = s - ky * 3;
-            RawS wf[P2_NR1];
+            for (int s = 0; s < P2_KS2; ++s) {
+                const int ky = s / 3, kx = s - ky * 3;
+                RawS wf[P2_NR1];
 #pragma unroll
-            for (int r = 0; r < P2_NR1; ++r) ldw(wf[r], w2 + (r * 16 + col) * P2_K2S + s * 32, kq);
-#pragma unroll
-            for (int j = 0; j < P2_NF2; ++j) {
-                const int f = hw + P2_NWH * j;
+                for (int r = 0; r < P2_NR1; ++r) ldw(wf[r], w2 + (r * 16 + col) * P2_K2S + s * 32, kq);
                 int h = (f + ky) * P2_HWW + (col + kx);
                 asm volatile("" : "+v"(h));
                 RawS xf;
                 xf.h = *reinterpret_cast<const uint4 *>(ts + tso(h, kq));
                 xf.l = *reinterpret_cast<const uint4 *>(ts + tso(h, 4 + kq));
 #pragma unroll
-                for (int r = 0; r < P2_NR1; ++r) mma(acc[j][r], wf[r], xf);
+                for (int r = 0; r < P2_NR1; ++r) mma(acc[r], wf[r], xf);
+                if (BNECK2_FENCE1) asm volatile("" ::: "memory");
             }
-            if (BNECK2_FENCE1) asm volatile("" ::: "memory");
-        }
-        RawF tf[P2_NF2];
-#pragma unroll
-        for (int j = 0; j < P2_NF2; ++j) {
             if constexpr (SCL) {
 #pragma unroll
-                for (int r = 0; r < P2_NR1; ++r) acc[j][r] = mul4(acc[j][r], o2m);
+                for (int r = 0; r < P2_NR1; ++r) acc[r] = mul4(acc[r], o2m);
             }
-            const float4 q0 = act(f4(acc[j][0]), cs2 + kq * 4);
-            const float4 q1 = act(f4(acc[j][1]), cs2 + 16 + kq * 4);
-            to_bop(tf[j], q0, q1);
-        }
-        // phase 3: out = act_out(act3(W3 t1 + b3) + x), whole-line stores (bneck_kernels.hip LINES)
-        const bool lo8 = col < 8;
-#pragma unroll
-        for (int j = 0; j < P2_NF2; ++j) {
-            const int f = hw + P2_NWH * j;
-            if constexpr (!BNECK2_RESPF && BNECK2_RESPAIR == 0) load_res(j, res[0]);
-            const int jr = BNECK2_RESPF ? j : 0;
+            RawF tf;
+            to_bop(tf, act(f4(acc[0]), cs2 + kq * 4), act(f4(acc[1]), cs2 + 16 + kq * 4));
+            // phase 3: out = act_out(act3(W3 t1 + b3) + x), whole-line stores (bneck_kernels.hip LINES)
             const uint32_t po_o = pix_base(n, oy0 + dt * f, ox0 + dt * (col ^ 8));
-            const uint32_t pa = lo8 ? po[j] : po_o, pb = lo8 ? po_o : po[j];
+            const uint32_t pa = lo8 ? po : po_o, pb = lo8 ? po_o : po;
 #pragma unroll
             for (int u = 0; u < P2_NR3 / 2; ++u) {
                 float4 v2[2];
-                if constexpr (BNECK2_RESPAIR) {        // this row pair's residual chunks only (8 VGPRs)
-#pragma unroll
-                    for (int hh = 0; hh < 2; ++hh) {
-                        const int t = 2 * u + hh;
-                        res[0][t] = bld16(rxb, po[j] == OOB ? OOB : po[j] + (uint32_t)(t * 16 + kq * 4) * 4u);
-                    }
-                }
 #pragma unroll
                 for (int hh = 0; hh < 2; ++hh) {
                     const int t = 2 * u + hh, ch = t * 16 + kq * 4;
@@ -294,11 +263,11 @@ __device__ __forceinline__ void bneck2_body(const BneckArgs &a, float rlane, flo
                     if (SCL || scl) ac = mul4(ac, b3m);
                     RawS wf;
                     ldw(wf, w3 + (t * 16 + col) * P2_K3S, kq);
-                    mma(ac, wf, tf[j]);
+                    mma(ac, wf, tf);
                     float4 v = f4(ac);
                     if (scl) v = mul4(v, o3m);
                     v = act(v, cs3 + ch);
-                    v2[hh] = act(add4(v, __builtin_bit_cast(float4, res[jr][t])), cso + ch);
+                    v2[hh] = act(add4(v, __builtin_bit_cast(float4, res[t])), cso + ch);
                     rng_acc4(amo, v2[hh]);
                 }
                 const uint4 u0 = __builtin_bit_cast(uint4, v2[0]), u1 = __builtin_bit_cast(uint4, v2[1]);
