@@ -1556,8 +1556,10 @@ static const void *bneck_fun(int prec, int C, bool asym, int v, bool tr, int cin
 
 int bneck_slots_per_cu(int prec, int C, bool asym, int v, bool tr, int cin) {
     if (C == 128 && v == BNECK2_V) {
-        const char *off = std::getenv("BUGSEG_BNECK2");                 // 0: never plan it (A/B knob)
-        return prec == PREC_F32 && !asym && !tr && cin == 0 && !(off && *off == '0') ? bneck2_slots_per_cu() : 0;
+        // planned only with BUGSEG_BNECK2=1: measured slower (round 6, B = 64, A/B on one box: 103 vs 87 us
+        // per launch; bneck2_kernels.hip says why)
+        const char *on = std::getenv("BUGSEG_BNECK2");
+        return prec == PREC_F32 && !asym && !tr && cin == 0 && on && *on == '1' ? bneck2_slots_per_cu() : 0;
     }
     // (cached per device and form: launch_bneck asks on every launch; bugseg_runtime.cpp occupancy_per_cu)
     const void *f = bneck_fun(prec, C, asym, v, tr, cin);

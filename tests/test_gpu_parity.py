@@ -374,6 +374,27 @@ def test_fused_bottlenecks_equal_unfused(gpu, blocks, prec, H, W, variant, monke
     assert torch.equal(a, b)
 
 
+@pytest.mark.parametrize("H,W", [(72, 104), (120, 160), (480, 640)])
+def test_bneck2_two_tile_form_equals_unfused(gpu, blocks, H, W, monkeypatch):
+    """The fp32 C128 two-phase-shifted-tiles kernel (bneck2_kernels.hip, BUGSEG_BNECK2=1; measured slower
+    and off by default) is bit-identical to the unfused chain: same products, same order."""
+    B = 2
+    bgr = torch.from_numpy(synthetic.road_frames(B, H, W, seed=H + 1)).cuda()
+    monkeypatch.setenv("BUGSEG_BNECK2", "1")
+    fused = ENET(weights=blocks, precision="fp32")
+    a = torch.empty((B, 15, H, W), dtype=torch.float32, device=gpu)
+    fused.ctx.forward_bgr(bgr, B, H, W, N.OUT_LOGITS_F32, a)
+    n = fused.ctx.plan_info(B, H, W, N.OUT_LOGITS_F32)[0]
+    tags = [fused.ctx.plan_op(B, H, W, i)[0] for i in range(n)]
+    assert any(t.startswith("bneck2") for t in tags), tags
+    monkeypatch.delenv("BUGSEG_BNECK2")
+    monkeypatch.setenv("BUGSEG_NO_FUSE", "1")
+    plain = ENET(weights=blocks, precision="fp32")
+    b = torch.empty_like(a)
+    plain.ctx.forward_bgr(bgr, B, H, W, N.OUT_LOGITS_F32, b)
+    assert torch.equal(a, b)
+
+
 @pytest.mark.parametrize("grid", ["8", "-2"])
 @pytest.mark.parametrize("variant", [None, "0", "2", "4"])
 @pytest.mark.parametrize("prec", ["fp32", "bf16", "fp16"])
