@@ -381,6 +381,7 @@ def test_bneck2_two_tile_form_equals_unfused(gpu, blocks, H, W, monkeypatch):
     B = 2
     bgr = torch.from_numpy(synthetic.road_frames(B, H, W, seed=H + 1)).cuda()
     monkeypatch.setenv("BUGSEG_BNECK2", "1")
+    monkeypatch.setenv("BUGSEG_BNECK_VARIANT_C128", "5")     # every symmetric C128 layer, any efficiency
     fused = ENET(weights=blocks, precision="fp32")
     a = torch.empty((B, 15, H, W), dtype=torch.float32, device=gpu)
     fused.ctx.forward_bgr(bgr, B, H, W, N.OUT_LOGITS_F32, a)
@@ -388,6 +389,7 @@ def test_bneck2_two_tile_form_equals_unfused(gpu, blocks, H, W, monkeypatch):
     tags = [fused.ctx.plan_op(B, H, W, i)[0] for i in range(n)]
     assert any(t.startswith("bneck2") for t in tags), tags
     monkeypatch.delenv("BUGSEG_BNECK2")
+    monkeypatch.delenv("BUGSEG_BNECK_VARIANT_C128")
     monkeypatch.setenv("BUGSEG_NO_FUSE", "1")
     plain = ENET(weights=blocks, precision="fp32")
     b = torch.empty_like(a)
