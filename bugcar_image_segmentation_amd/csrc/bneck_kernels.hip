@@ -114,7 +114,20 @@ template <> struct BShape<16, 1> { static constexpr int TH = 20, TW = 16, NW = 4
 #ifndef BNECK_F32_HL
 #define BNECK_F32_HL 1
 #endif
-__host__ __device__ constexpr bool bneck_hl(int es, int C, bool dn) { return BNECK_F32_HL && es == 4 && C == 128 && !dn; }
+// fp32 C = 64 (round 6): the weights in the same HL layout (rows 8 / 40 dwords mod 64) and
+// t0 as two PLANES — every pixel's 16 channels' hi parts (32 B) in one, their lo parts in the other, 8
+// dwords per pixel each, unpadded: the middle conv's 16-lane read groups then hit distinct banks (lanes
+// col and col + 8 of a group read the same bank row but the other 8-channel group) — where the interleaved
+// split layout (hi + lo per group, 20-dword pixels) was 2-way conflicted on every read (SQ: 35% of the
+// C64 forms' LDS cycles), in less LDS (two planes of 8 dwords vs 20 dwords per pixel; the weights' wider
+// pads fit in the difference, so the 8 x 16 form keeps its 4 workgroups per CU)
+#ifndef BNECK_F32_HL64
+#define BNECK_F32_HL64 1
+#endif
+__host__ __device__ constexpr bool bneck_hl(int es, int C, bool dn) {
+    return BNECK_F32_HL && es == 4 && (C == 128 || (C == 64 && BNECK_F32_HL64)) && !dn;
+}
+__host__ __device__ constexpr bool bneck_pl(int es, int C, bool dn) { return bneck_hl(es, C, dn) && C == 64; }
 __host__ __device__ constexpr int bneck_padw(int es, int C, bool wide, bool dn) {
     return bneck_hl(es, C, dn) ? 8 : es == 2 && (C != 128 || wide) ? 16 : 16 / es;
 }
@@ -225,7 +238,8 @@ __device__ __forceinline__ bool bneck_body(const BneckArgs &a, float rlane) {
     constexpr int NF1 = (HR + 15) / 16;               // 16-pixel fragments of tile + halo
     constexpr bool WIDE = BShape<C, V>::WIDE && !ASYM;
     constexpr int PADW = bneck_padw((int)sizeof(T), C, WIDE, CI > 0);   // weight-row pad (elements)
-    constexpr int PSTR = bneck_pstr((int)sizeof(T), IS, WIDE);  // LDS pixel stride (elements)
+    constexpr bool PL = bneck_pl((int)sizeof(T), C, CI > 0) && !ASYM;  // fp32 C = 64: t0 as hi / lo planes
+    constexpr int PSTR = PL ? 8 : bneck_pstr((int)sizeof(T), IS, WIDE);  // LDS pixel stride (elements; PL: per plane)
     constexpr int NPX = TH * TW;
     constexpr int NFT = (NPX + 15) / 16;              // 16-pixel fragments of the tile
     constexpr int NF2 = (NFT + NW - 1) / NW;          // ... per wave (the last may be partial / absent)
@@ -386,11 +400,24 @@ __device__ __forceinline__ bool bneck_body(const BneckArgs &a, float rlane) {
     // and rows of 8 / 40 dwords mod 64 make every ds_read_b128 lane group conflict-free (SQ: 41% of the
     // LDS cycles of these forms were bank conflicts with 32-B groups). The weight staging permutes the
     // 16-B chunks (the packed matrices in HBM keep the shared layout); the same parts feed the same products
-    constexpr bool HL = bneck_hl((int)sizeof(T), C, CI > 0);
-    static_assert(!HL || (BNECK_F32_SPLIT_T0 && IS == 32 && BNECK_GLDS), "HL: split t0 of 32 channels, LDS-DMA staging");
+    constexpr bool HL = bneck_hl((int)sizeof(T), C, CI > 0) && !(C == 64 && ASYM);   // (no C64 asymmetric block in ENet)
+    static_assert(!HL || (BNECK_F32_SPLIT_T0 && (IS == 32 || (PL && IS == 16)) && BNECK_GLDS), "HL: split t0 of 32 channels (PL: 16), LDS-DMA staging");
+    constexpr int PLO = PL ? HR * PSTR : 0;           // PL: the lo plane's offset from the hi plane (elements)
     constexpr int ZP = HL ? 32 : 16;                  // zero-pad elements below ts
     auto st4t = [](T *p, int ch, float4 v) {
-        if constexpr (HL) st4hl(reinterpret_cast<float *>(p) - ch, ch, v);
+        if constexpr (PL) {
+            // p = plane pixel base + ch: hi parts of channels ch .. ch + 3 into the hi plane, lo into the lo plane
+            const float e[4] = {v.x, v.y, v.z, v.w};
+            _Float16 hh[4], ll[4];
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+                hh[i] = (_Float16)e[i];
+                ll[i] = (_Float16)(e[i] - (float)hh[i]);
+            }
+            unsigned char *b = reinterpret_cast<unsigned char *>(reinterpret_cast<float *>(p) - ch) + (ch >> 3) * 16 + (ch & 7) * 2;
+            *reinterpret_cast<f16x4 *>(b) = (f16x4){hh[0], hh[1], hh[2], hh[3]};
+            *reinterpret_cast<f16x4 *>(b + PLO * 4) = (f16x4){ll[0], ll[1], ll[2], ll[3]};
+        } else if constexpr (HL) st4hl(reinterpret_cast<float *>(p) - ch, ch, v);
         else if constexpr (sizeof(T) == 4 && BNECK_F32_SPLIT_T0) st4s(reinterpret_cast<float *>(p) - (ch & 7), ch & 7, v);
         else st4(p, v);
     };
@@ -1102,7 +1129,10 @@ __device__ __forceinline__ bool bneck_body(const BneckArgs &a, float rlane) {
                     const bool in = g < G2 && (!RD || (unsigned)(ox + tj) < (unsigned)TW);
                     int off = ((oy + ti) * HWW + (ox + tj)) * PSTR + (HL ? coff >> 1 : coff);
                     asm volatile("" : "+v"(off));
-                    if constexpr (HL) {
+                    if constexpr (PL) {
+                        xf.h = *reinterpret_cast<const uint4 *>(in ? ts + off : zpad);
+                        xf.l = *reinterpret_cast<const uint4 *>(in ? ts + PLO + off : zpad);
+                    } else if constexpr (HL) {
                         const int o = in ? off : -ZP;         // masked: the zero pad just below ts
                         xf.h = *reinterpret_cast<const uint4 *>(ts + o);
                         xf.l = *reinterpret_cast<const uint4 *>(ts + o + 16);
@@ -1512,7 +1542,7 @@ size_t bneck_lds_bytes(int prec, int C, bool asym, int v, int cin) {
     const int zp = bneck_hl(es, C, cin > 0) ? 32 : 16;
     const size_t wts = (size_t)NR1 * 16 * (KS1 * 32 + padw) + (size_t)NR1 * 16 * (KS2 * 32 + padw) * (asym ? 2 : 1) +
                        (size_t)C * (32 + padw);
-    const size_t halo = (size_t)(TH + 2 * R) * (TW + 2 * RX) * bneck_pstr(es, IS, wide);
+    const size_t halo = (size_t)(TH + 2 * R) * (TW + 2 * RX) * (bneck_pl(es, C, cin > 0) && !asym ? 16 : bneck_pstr(es, IS, wide));
     const bool staged = C == 64 && !BNECK_REG3_C64 && !(es == 4 && BNECK_REG3_C64_F32);
     const bool hstg = staged && es == 4 && BNECK_F32_HSTG;            // fp32 C = 64: one 32-channel half at a time
     const size_t stage = staged ? (size_t)NW * 16 * ((hstg ? C / 2 : C) + pad) : 0;    // staged epilogue (REG3 off)
