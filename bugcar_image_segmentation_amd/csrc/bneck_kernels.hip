@@ -334,7 +334,12 @@ __device__ __forceinline__ bool bneck_body(const BneckArgs &a, float rlane) {
 #define BNECK_KEEP_ASYM 1
 #endif
 #ifndef BNECK_KEEP_C64
-#define BNECK_KEEP_C64 0    // C = 64: measured 41.0 vs 38.0 us per launch with the residual kept (wave 0 takes a third load round trip for its second border fragment; batching it spills)
+// C = 64, 2-byte: the residual kept (16 x 16 and 8 x 16 tiles; the 20 x 16 tile's five fragments per wave
+// exceed the kept-register budget). Round 2 (B = 32, two streams) measured it slower: 41.0 vs 38.0 us per
+// launch. Round 6 (B = 64, one stream): the 20 x 16 form re-reads its residual from HBM (PMC 228 MB read
+// per launch, 1.45x the 157 MB compulsory) while 16 x 16 kept reads 160 MB (1.02x) in 70.9 vs 71.8 us —
+// so it is on, and the tile picker charges the 20 x 16 form for its re-read (bugseg_runtime.cpp)
+#define BNECK_KEEP_C64 1
 #endif
 #ifndef BNECK_KEEP_F32
 #define BNECK_KEEP_F32 1
@@ -1528,6 +1533,9 @@ extern "C" int bugseg_debug_set_stamps(void *p) {
     return hipMemcpyToSymbol(HIP_SYMBOL(bugseg_stamps), &p, sizeof(p)) == hipSuccess ? 0 : -3;
 }
 #endif
+
+// the C = 64 2-byte forms that keep their residual in registers (BNECK_KEEP_C64): all but 20 x 16
+bool bneck_keeps_c64(int prec, int v) { return BNECK_KEEP_C64 && prec != PREC_F32 && v != 1; }
 
 size_t bneck_lds_bytes(int prec, int C, bool asym, int v, int cin) {
     if (C == 128 && v == BNECK2_V) return prec == PREC_F32 && !asym && cin == 0 ? bneck2_lds_bytes() : (size_t)1 << 30;

@@ -142,6 +142,7 @@ struct BneckArgs {
 };
 // tile-shape variants of the fused kernel for C channels: 0 .. bneck_variants(C) - 1
 int bneck_variants(int C);
+bool bneck_keeps_c64(int prec, int v);
 // rd (optional): 1 for a row-dilated full-width variant (tiles_x = 1, phases = d, needs W <= tw)
 void bneck_shape(int C, int v, int &th, int &tw, int &nw, int *rd = nullptr);
 // cin > 0: the downsampling form (bneck_kernels.hip) with a cin-channel input; built for (64, v0,
