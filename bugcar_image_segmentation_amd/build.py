@@ -19,7 +19,7 @@ OBJ = PKG / "_build"
 LIB = PKG / "libbugseg.so"
 SOURCES = ["conv_kernels.hip", "cls_kernels.hip", "init_kernels.hip", "bneck_kernels.hip", "bneck2_kernels.hip", "up_kernels.hip", "prep_kernels.hip",
            "bev_kernels.hip", "deeplab_kernels.hip", "bugseg_runtime.cpp", "deeplab_runtime.cpp"]
-HEADERS = [CSRC / "bugseg_internal.h", CSRC / "deeplab_internal.h", CSRC / "mfma_common.h", ROOT / "include" / "bugseg.h"]
+HEADERS = [CSRC / "bugseg_internal.h", CSRC / "deeplab_internal.h", CSRC / "mfma_common.h", CSRC / "cls_common.h", ROOT / "include" / "bugseg.h"]
 ARCH = os.environ.get("BUGSEG_OFFLOAD_ARCH", "gfx950")
 
 

@@ -43,7 +43,7 @@
 #ifndef BUGSEG_OUT_AUX
 #define BUGSEG_OUT_AUX -1
 #endif
-#include "mfma_common.h"
+#include "cls_common.h"
 
 namespace bugseg {
 
@@ -187,7 +187,7 @@ void bneck_shape(int C, int v, int &th, int &tw, int &nw, int *rd) {
 // tile's loads are in flight (a wait for the range words alone at kernel start cost the C128 launches
 // ~4 us) and, if some exponent is non-zero, drains its loads and returns before computing anything —
 // the kernel then runs the scaled body from the start.
-template <typename T, int C, bool ASYM, int V, bool TR, int CI, bool SCL>
+template <typename T, int C, bool ASYM, int V, bool TR, int CI, bool SCL, int FC = -1>
 __device__ __forceinline__ bool bneck_body(const BneckArgs &a, float rlane) {
     using Raw = typename Tr<T>::Raw;
     using WRaw = typename WTr<T>::Raw;   // weight operand (fp32 mode: split-f16 parts)
@@ -394,6 +394,23 @@ __device__ __forceinline__ bool bneck_body(const BneckArgs &a, float rlane) {
 #define BNECK_F32_LINES 1
 #endif
     constexpr bool LINES = BNECK_F32_LINES && sizeof(T) == 4 && REG3 && C == 128 && (KEEPF || (DKEEP && PKW == 2)) && RQ3 % 2 == 0;
+    // FC >= 0 (round 6): ENet's class layer fused into its last bottleneck (C = 16, 16 x 16 tiles), FC =
+    // the class map's LUT kind (cls_common.h cls_argmax). Tiles overlap by one row and one column (a
+    // 15 x 15 stride): phase 3 leaves the block output of all 16 x 16 tile pixels in LDS (otile) instead
+    // of HBM, and the class phase computes the transposed conv + argmax of the 15 x 15 pixels whose 2 x 2
+    // input neighbourhood lies in the tile (the 16th row / column is the next tile's first). The block
+    // output never reaches HBM: 2 x 315 MB (fp32, B = 64) less traffic, one launch less. Bit-identical class
+    // maps (GPU-tested) but MEASURED SLOWER (round 6, B = 64, 480 x 640, one stream): fp32 424 us vs 162 + 116
+    // us for the two launches, fp16 156 vs 97 + 45 — the class layer is not HBM-bound (0.37 of HBM alone), so
+    // the bytes saved buy little, while the out tile and class weights in LDS (fp32 63.5 KB per workgroup:
+    // 2 instead of 4 per CU) and the class phase's serial 32x32 MFMA chains behind a per-tile barrier cost
+    // the bottleneck its latency hiding. Opt-in (BUGSEG_CLS_FUSE=1, bugseg_runtime.cpp Plan::cls_ok).
+    constexpr bool CLS = FC >= 0;
+    static_assert(!CLS || (C == 16 && !ASYM && !DN && !TR && REG3 && !KEEP && !SWAP && TH == 16 && TW == 16 && NW == 4),
+                  "class fusion: the 16 x 16 C16 form");
+    // otile pixel stride (elements): 80 B (fp32) / 48 B — 5 / 3 16-B units, so the 16-B reads of any 16
+    // consecutive pixels fall in distinct bank groups
+    constexpr int OPS = sizeof(T) == 4 ? 20 : 24;
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     // fp32 (parity mode): t0 / t1a live in LDS as split-f16 parts (mfma_common.h st4s: the weights'
     // layout, 32 B per 8 channels as the f32 values take), split once when written rather than at every
@@ -463,6 +480,12 @@ __device__ __forceinline__ bool bneck_body(const BneckArgs &a, float rlane) {
     T *zpad = reinterpret_cast<T *>(cso + C);
     T *ts = zpad + ZP;                                // t0 / t1a / t1 region
     float *wmx = reinterpret_cast<float *>(ts + HR * PSTR);   // fp32 asymmetric: NW per-wave max |t1a| slots
+    // CLS: the tile's block output, the class weights as [8 (block, tap)][64 lanes] 16-B slots (fp32: the
+    // hi parts, then a plane of the lo parts), the class bias (64 rows), per-wave tile maxima (fp32)
+    T *otile = ts + HR * PSTR;
+    uint4 *cwl = reinterpret_cast<uint4 *>(otile + (CLS ? NPX * OPS : 0));
+    float *cbl = reinterpret_cast<float *>(cwl + (CLS ? (sizeof(T) == 4 ? 1024 : 512) : 0));
+    float *cmx = cbl + 64;
     {
         // C = 16 (small weights, many short tiles): every load of the staging is issued before the
         // first LDS store (one L2 round trip at kernel start instead of one per 16-B chunk a thread
@@ -565,6 +588,36 @@ __device__ __forceinline__ bool bneck_body(const BneckArgs &a, float rlane) {
         }
         if (tid < ZP) zpad[tid] = (T)0.f;
     }
+    // CLS: the class layer's weights (packed [64][64]: row = phase * 16 + class, k = tap * 16 + channel) into
+    // the lane slots its MFMAs read, its bias (padding classes at -inf: never the maximum), the LUT, and
+    // which blocks skip the dy = 1 taps (all-zero weights: output row 2y never sees input row y + 1) —
+    // the class kernel's rules (cls_kernels.hip), decided the same way
+    using CRaw = typename WTr<T>::Raw;
+    uint64_t lut64 = 0;
+    bool cshort[2] = {false, false};
+    if constexpr (CLS) {
+        const T *cw = reinterpret_cast<const T *>(a.cw);
+        for (int q = tid; q < 512; q += NT) {
+            const int bs = q >> 6, ln = q & 63;
+            const T *src = cw + (size_t)cls_prow(bs >> 2, ln & 31) * 64 + (bs & 3) * 16 + 8 * (ln >> 5);
+            if constexpr (sizeof(T) == 4) {
+                cwl[q] = reinterpret_cast<const uint4 *>(src)[0];
+                cwl[512 + q] = reinterpret_cast<const uint4 *>(src)[1];
+            } else {
+                cwl[q] = *reinterpret_cast<const uint4 *>(src);
+            }
+        }
+        if (tid < 64) cbl[tid] = (tid & 15) < a.ncls ? a.cbias[tid] : -INFINITY;
+        lut64 = cls_lut64(a.lut);
+#pragma unroll
+        for (int b = 0; b < 2; ++b) {
+            CRaw w2_, w3_;
+            const T *r = cw + (size_t)cls_prow(b, lane & 31) * 64 + 8 * (lane >> 5);
+            ld8(w2_, r + 32);
+            ld8(w3_, r + 48);
+            cshort[b] = __ballot(nonzero(w2_) || nonzero(w3_)) == 0;
+        }
+    }
     // x / out through buffer descriptors: 32-bit offsets, and an out-of-range offset reads 0 / drops
     // the store (mfma_common.h), so image-border masking costs one select per access
     // down mode: x is the (2H, 2W, CI) block input; the residual comes from the pooled scratch
@@ -631,8 +684,8 @@ __device__ __forceinline__ bool bneck_body(const BneckArgs &a, float rlane) {
         const int ph = t % a.phases;
         n = t / a.phases;
         const int py = RD ? ph : ph / dt, px = RD ? 0 : ph - py * dt;   // RD: phases = row phases
-        oy0 = py + dt * tyi * (tr ? TW : TH);
-        ox0 = RD ? 0 : px + dt * txi * (tr ? TH : TW);
+        oy0 = py + dt * tyi * (tr ? TW : TH) - (CLS ? tyi : 0);    // (CLS: tiles 15 apart)
+        ox0 = RD ? 0 : px + dt * txi * (tr ? TH : TW) - (CLS ? txi : 0);
     };
     Raw kx[KEEP ? NF2 : 1][KS1];                      // KEEP: this wave's interior fragments of x
     bool kok[KEEP ? NF2 : 1];
@@ -650,6 +703,7 @@ __device__ __forceinline__ bool bneck_body(const BneckArgs &a, float rlane) {
         if (tile >= a.ntiles) break;
         int n, oy0, ox0;
         tile_geom(tile, n, oy0, ox0);
+        float tmo = 0.f;                              // CLS, fp32: this lane's max |out| over the tile
         // the next tile of this workgroup's walk (PREF)
         const int ntile = grp * CH + it + nslots;
         const bool has_next = PREF && it + nslots < CH && ntile < a.ntiles;
@@ -1490,13 +1544,21 @@ __device__ __forceinline__ bool bneck_body(const BneckArgs &a, float rlane) {
                     WRaw wf;
                     ldw(wf, w3 + (r * 16 + col) * K3S);
                     mma(acc, wf, tf[j]);
+                    // (CLS: into the out tile, as the unfused plan would store it)
+                    T *ot = otile + ((wave + NW * j) * 16 + col) * OPS + chunk_ch(t);
                     if constexpr (HALF) {
                         float4 v = act(add4(out3(r, acc), unpack4<T>((u32x2_t){rc.x, rc.y})), cso + r * 16 + kq * 4);
-                        bst8o<OAUX>(rob, off, pack4<T>(v));
+                        if constexpr (CLS) *reinterpret_cast<u32x2_t *>(ot) = pack4<T>(v);
+                        else bst8o<OAUX>(rob, off, pack4<T>(v));
                     } else {
                         float4 v = act(add4(out3(r, acc), __builtin_bit_cast(float4, rc)), cso + r * 16 + kq * 4);
-                        if constexpr (F32) rng_acc4(amo, v);
-                        bst16o<OAUX>(rob, off, __builtin_bit_cast(uint4, v));
+                        if constexpr (CLS) {
+                            rng_acc4(tmo, v);
+                            *reinterpret_cast<float4 *>(ot) = v;
+                        } else {
+                            if constexpr (F32) rng_acc4(amo, v);
+                            bst16o<OAUX>(rob, off, __builtin_bit_cast(uint4, v));
+                        }
                     }
                 }
             }
@@ -1507,6 +1569,102 @@ __device__ __forceinline__ bool bneck_body(const BneckArgs &a, float rlane) {
                     const uint32_t nxn = (uint32_t)(nn * a.H * a.W) * (uint32_t)(C * sizeof(T));
                     kok[j] = load_hg(noy0, nox0, nxn, int_h(wave + NW * j), true, kx[j]);
                 }
+            }
+        }
+        if constexpr (CLS) {
+            // ---- class phase: ENet's final transposed conv (16 -> ncls, 3x3 stride 2) + argmax + LUT of the
+            // tile's 15 x 15 inner pixels from the out tile, the class kernel's arithmetic (cls_common.h):
+            // 8 groups of 32 pixels (tile rows 2g, 2g + 1; column 15 and row 15 are the next tiles'), two per
+            // wave; lane (c, h) holds channels 8h .. 8h + 7 of its pixel's four taps (the 2 x 2 neighbourhood;
+            // 0 outside the image, as the class kernel's masked loads) and gets output pixels (2y + b, 2x + h).
+            // fp32 range scaling: the input exponent from the TILE's measured max |out| (the class kernel's
+            // is the batch's: equal whenever both lie in the measured window), the weights' exponent csw
+            float xm = 1.f, bm = 1.f, om = 1.f;
+            bool csc = false;
+            if constexpr (F32) {
+#pragma unroll
+                for (int o = 32; o > 0; o >>= 1) tmo = __builtin_fmaxf(tmo, __shfl_xor(tmo, o));
+                if (lane == 0) cmx[wave] = tmo;
+            }
+            __syncthreads();                          // every wave's rows of the out tile written
+            if constexpr (F32) {
+                if (!a.rg.off) {
+                    float mt = 0.f;
+#pragma unroll
+                    for (int w = 0; w < NW; ++w) mt = __builtin_fmaxf(mt, cmx[w]);
+                    mt = __int_as_float(__builtin_amdgcn_readfirstlane(__float_as_int(mt)));
+                    const int sx = rng_exp_meas(mt), e = sx + a.csw;
+                    csc = (sx | e) != 0;
+                    xm = rng_pow2(sx); bm = rng_pow2(e); om = rng_pow2(-e);
+                }
+            }
+            // (an opaque lane id: lane-derived addresses recomputed here rather than hoisted out of the
+            // tile loop, where they would stay live through phases 1-3 and spill)
+            int ln = lane;
+            asm volatile("" : "+v"(ln));
+            const int c32 = ln & 31, hh = ln >> 5;
+            const auto rcls = mkbuf(a.cls_out, a.cls_bytes);
+            const uint32_t W2 = (uint32_t)(2 * a.W), plane = (uint32_t)(2 * a.H) * W2;
+#pragma unroll 1
+            for (int gq = 0; gq < 2; ++gq) {
+                const int i = 2 * (wave * 2 + gq) + (c32 >> 4), jj = c32 & 15;
+                const int y = oy0 + i, x = ox0 + jj;
+                // tap s of this lane's pixel, read when its MFMAs issue (LDS; nothing held across blocks)
+                auto tap_x = [&](int s, Raw &xq) {
+                    const int dy = s >> 1, dx = s & 1;
+                    const bool ok = i + dy < TH && jj + dx < TW && y + dy < a.H && x + dx < a.W;
+                    int off = ((i + dy) * TW + jj + dx) * OPS + 8 * hh;
+                    asm volatile("" : "+v"(off));
+                    ld8(xq, ok ? otile + off : zpad);
+                };
+                int cls[2];
+#pragma unroll
+                for (int b = 0; b < 2; ++b) {
+                    f32x16 acc;
+                    const float4 *bb = reinterpret_cast<const float4 *>(cbl + (2 * b + hh) * 16);
+#pragma unroll
+                    for (int q = 0; q < 4; ++q) {
+                        const float4 v = bb[q];
+                        acc[4 * q] = v.x; acc[4 * q + 1] = v.y; acc[4 * q + 2] = v.z; acc[4 * q + 3] = v.w;
+                    }
+                    auto taps = [&](auto sc) {
+#pragma unroll
+                        for (int s = 0; s < 4; ++s) {
+                            if (s >= 2 && cshort[b]) break;       // wave-uniform
+                            CRaw w;
+                            if constexpr (sizeof(T) == 4) {
+                                w.h = cwl[(b * 4 + s) * 64 + ln];
+                                w.l = cwl[512 + (b * 4 + s) * 64 + ln];
+                            } else {
+                                w.v = cwl[(b * 4 + s) * 64 + ln];
+                            }
+                            Raw xq;
+                            tap_x(s, xq);
+                            if constexpr (decltype(sc)::value) mul8(reinterpret_cast<RawF &>(xq), xm);
+                            mma32(acc, w, xq);
+                        }
+                    };
+                    bool done = false;
+                    if constexpr (F32) {
+                        if (csc) {
+#pragma unroll
+                            for (int c = 0; c < 16; ++c) acc[c] *= bm;
+                            taps(std::true_type());
+#pragma unroll
+                            for (int c = 0; c < 16; ++c) acc[c] *= om;
+                            done = true;
+                        }
+                    }
+                    if (!done) taps(std::false_type());
+                    cls[b] = cls_argmax1<(FC < 0 ? 0 : FC)>(acc, lut64);
+                }
+                // lanes < 32 store output row 2y (pixels 2x, 2x + 1: theirs and lane + 32's block 0), lanes
+                // >= 32 row 2y + 1
+                uint32_t c0 = (uint32_t)cls[0], c1 = (uint32_t)cls[1];
+                pl32swap(c0, c1);
+                const bool valid = i < TH - 1 && jj < TW - 1 && y < a.H && x < a.W;
+                const uint32_t o = (uint32_t)n * plane + (uint32_t)(2 * y + hh) * W2 + 2u * (uint32_t)x;
+                __builtin_amdgcn_raw_buffer_store_b16((unsigned short)(c0 | (c1 << 8)), rcls, valid ? (int)o : (int)OOB, 0, 0);
             }
         }
         pref = has_next;
@@ -1528,6 +1686,17 @@ __global__ void __launch_bounds__((BShape<C, V>::NW * 64), (sizeof(T) == 2 ? BSh
     }
 }
 
+// C = 16 with the class layer fused (FC = the class map's LUT kind); launch bounds as the C = 16 form
+template <typename T, int FC>
+__global__ void __launch_bounds__(256, (sizeof(T) == 2 ? BShape<16, 0>::OCC : BNECK_F32_OCC16)) bneck_cls_kernel(const BneckArgs a) {
+    if constexpr (sizeof(T) == 4) {
+        const float rl = rng_lane(a.rg);
+        if (!bneck_body<T, 16, false, 0, false, 0, false, FC>(a, rl)) bneck_body<T, 16, false, 0, false, 0, true, FC>(a, rl);
+    } else {
+        bneck_body<T, 16, false, 0, false, 0, false, FC>(a, 0.f);
+    }
+}
+
 #ifdef BUGSEG_STAMPS
 extern "C" int bugseg_debug_set_stamps(void *p) {
     return hipMemcpyToSymbol(HIP_SYMBOL(bugseg_stamps), &p, sizeof(p)) == hipSuccess ? 0 : -3;
@@ -1537,7 +1706,7 @@ extern "C" int bugseg_debug_set_stamps(void *p) {
 // the C = 64 2-byte forms that keep their residual in registers (BNECK_KEEP_C64): all but 20 x 16
 bool bneck_keeps_c64(int prec, int v) { return BNECK_KEEP_C64 && prec != PREC_F32 && v != 1; }
 
-size_t bneck_lds_bytes(int prec, int C, bool asym, int v, int cin) {
+size_t bneck_lds_bytes(int prec, int C, bool asym, int v, int cin, bool cls) {
     if (C == 128 && v == BNECK2_V) return prec == PREC_F32 && !asym && cin == 0 ? bneck2_lds_bytes() : (size_t)1 << 30;
     int TH, TW, NW, RD;
     bneck_shape(C, v, TH, TW, NW, &RD);
@@ -1555,8 +1724,10 @@ size_t bneck_lds_bytes(int prec, int C, bool asym, int v, int cin) {
     const bool hstg = staged && es == 4 && BNECK_F32_HSTG;            // fp32 C = 64: one 32-channel half at a time
     const size_t stage = staged ? (size_t)NW * 16 * ((hstg ? C / 2 : C) + pad) : 0;    // staged epilogue (REG3 off)
     const size_t consts = ((size_t)6 * NR1 * 16 + 3 * (size_t)C) * sizeof(float);
+    // class fusion (C = 16): the out tile, the class weights, bias and the per-wave tile maxima
+    const size_t clsb = cls ? (size_t)TH * TW * (es == 4 ? 20 : 24) * es + (es == 4 ? 16384 : 8192) + 64 * 4 + (size_t)NW * 4 : 0;
     return (wts + zp + (halo > stage ? halo : stage)) * es + consts +   // + the zero pad
-           (asym && es == 4 ? (size_t)NW * sizeof(float) : 0);             // + fp32 asymmetric max slots
+           (asym && es == 4 ? (size_t)NW * sizeof(float) : 0) + clsb;      // + fp32 asymmetric max slots
 }
 
 // kernel symbol of (precision, C, asym, variant, transposed); nullptr if not built
@@ -1637,6 +1808,31 @@ hipError_t launch_bneck(int prec, int C, bool asym, int v, const BneckArgs &a, h
     g = (g + 7) & ~7;
     void *args[] = {const_cast<BneckArgs *>(&a)};
     return hipLaunchKernel(f, dim3(g), dim3(nw * 64), args, lds, s);
+}
+
+template <typename T>
+static const void *kfun_cls(int lk) {
+    return lk == 1 ? (const void *)bneck_cls_kernel<T, 1> : lk == 2 ? (const void *)bneck_cls_kernel<T, 2>
+                   : (const void *)bneck_cls_kernel<T, 0>;
+}
+
+hipError_t launch_bneck_cls(int prec, const BneckArgs &a, hipStream_t s) {
+    const int lk = a.lut && (a.lut_kind == 1 || a.lut_kind == 2) ? a.lut_kind : 0;
+    const void *f = prec == PREC_BF16 ? kfun_cls<__bf16>(lk) : prec == PREC_F16 ? kfun_cls<_Float16>(lk) : kfun_cls<float>(lk);
+    const size_t lds = bneck_lds_bytes(prec, 16, false, 0, 0, true);
+    if (lds > 64 * 1024) {
+        hipError_t e = allow_dynamic_lds(f);
+        if (e != hipSuccess) return e;
+    }
+    // one round of resident workgroups, as launch_bneck
+    const int spc = occupancy_per_cu(f, 256, lds), n_cu = device_cus();
+    const char *ge = std::getenv("BUGSEG_BNECK_GRID");
+    const int grid_cap = ge ? std::atoi(ge) : 0;
+    const int cap = grid_cap > 0 ? grid_cap : spc > 0 && n_cu > 0 ? spc * n_cu : 2048;
+    int g = a.ntiles < cap ? a.ntiles : cap;
+    g = (g + 7) & ~7;
+    void *args[] = {const_cast<BneckArgs *>(&a)};
+    return hipLaunchKernel(f, dim3(g), dim3(256), args, lds, s);
 }
 
 }  // namespace bugseg

@@ -139,6 +139,15 @@ struct BneckArgs {
     uint32_t xin_bytes, pool_bytes, idx_bytes;
     RangeArgs rg;        // fp32 mode: sw = {w1, w2, w2b, w3}; n / c: t0, t1 (asym: t1a), t1 (asym)
     unsigned long long *span;   // launch span (bugseg_debug_set_spans), or null
+    // the class layer fused into the C = 16 block (launch_bneck_cls; out is not written): its packed weights
+    // [64][64] and bias [64] (the EPI_CLASSES op's), the class map (B, 2H, 2W) u8 and its size, the LUT
+    // (16 bytes, nullptr = raw ids) and its kind (ConvArgs::lut_kind), the class count, the weights' exponent
+    const void *cw;
+    const float *cbias;
+    uint8_t *cls_out;
+    uint32_t cls_bytes;
+    const uint8_t *lut;
+    int lut_kind, ncls, csw;
 };
 // tile-shape variants of the fused kernel for C channels: 0 .. bneck_variants(C) - 1
 int bneck_variants(int C);
@@ -147,10 +156,13 @@ bool bneck_keeps_c64(int prec, int v);
 void bneck_shape(int C, int v, int &th, int &tw, int &nw, int *rd = nullptr);
 // cin > 0: the downsampling form (bneck_kernels.hip) with a cin-channel input; built for (64, v0,
 // cin 16) and (128, v1, cin 64)
-size_t bneck_lds_bytes(int prec, int C, bool asym, int v, int cin = 0);
+size_t bneck_lds_bytes(int prec, int C, bool asym, int v, int cin = 0, bool cls = false);
 // resident workgroups per CU (occupancy API); 0 if (C, asym, v, tr, cin) is not built
 int bneck_slots_per_cu(int prec, int C, bool asym, int v, bool tr, int cin = 0);
 hipError_t launch_bneck(int prec, int C, bool asym, int v, const BneckArgs &a, hipStream_t s, int cin = 0);
+// the C = 16 block with the class layer fused (variant 0, untransposed; tiles 15 apart: tiles_x =
+// ceil(W / 15), tiles_y = ceil(H / 15)); bneck_lds_bytes(..., cls = true) its LDS
+hipError_t launch_bneck_cls(int prec, const BneckArgs &a, hipStream_t s);
 // variant BNECK2_V of C = 128 (fp32, symmetric, untransposed 16 x 16 tiles): bneck2_kernels.hip, one
 // 16-wave workgroup per CU running two phase-shifted tiles on one weight copy
 constexpr int BNECK2_V = 5;

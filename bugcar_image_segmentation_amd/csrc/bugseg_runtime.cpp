@@ -140,6 +140,11 @@ struct Plan {
     bool pinned = false;     // a forward on this arena was captured into a graph: never freed before destroy
     std::vector<unsigned char *> idx;   // per block: its pooling-index tensor in the arena (down blocks), else null
     std::vector<size_t> idx_bytes;
+    // ENet's last bottleneck (C = 16) and the class layer as ONE launch (bneck_kernels.hip, class fusion;
+    // opt-in, BUGSEG_CLS_FUSE=1: measured slower, see there): possible for this plan (cls_ok: the plan ends
+    // with that bottleneck feeding the class kernel), and taken by the last forward (cls_on: a class-map
+    // output, both ops in its range). The last op then launches nothing; its plan_op tag is "fused".
+    bool cls_ok = false, cls_on = false;
 };
 
 inline int round_up(int v, int m) { return (v + m - 1) / m * m; }
@@ -1263,6 +1268,16 @@ bool build_plan(bugseg_ctx *ctx, int B, int H, int W, std::string &why, void *st
         if (!finish_conv_args(op.a, op.epi, w.es)) { why = "batch too large for 32-bit tensor offsets"; return false; }
     }
     pl.ops = std::move(w.ops);
+    pl.cls_ok = false;
+    pl.cls_on = false;
+    if (pl.ops.size() >= 2) {
+        const Op &l = pl.ops.back(), &q = pl.ops[pl.ops.size() - 2];
+        const char *fe = std::getenv("BUGSEG_CLS_FUSE");
+        pl.cls_ok = fe && *fe == '1' && l.kind == 0 && l.epi == EPI_CLASSES && cls_supported(l.a) &&
+                    !std::getenv("BUGSEG_CLS_CONV") && q.kind == 1 && q.bn_c == 16 && !q.bn_asym && q.bn_cin == 0 &&
+                    q.bn.dt == 1 && q.bn.phases == 1 && q.bn.out == l.a.in && l.a.B == q.bn.B && l.a.Hin == q.bn.H &&
+                    l.a.Win == q.bn.W && (double)B * l.a.Hout * l.a.Wout < 2147483648.0;
+    }
     pl.idx = w.idx;
     pl.idx_bytes = w.szIdx;
     pl.words = w.words;
@@ -1522,9 +1537,34 @@ int bugseg_nchw_to_input(bugseg_ctx *ctx, const void *x, int is_f64, int B, int 
     return BUGSEG_OK;
 }
 
+// the class-fused launch's arguments (Plan::cls_ok): the last bottleneck's, 15 x 15-strided 16 x 16
+// tiles, no block output or range words written, the class op's weights / bias / output / LUT
+static BneckArgs cls_fused_args(const Plan &pl) {
+    const Op &q = pl.ops[pl.ops.size() - 2], &l = pl.ops.back();
+    BneckArgs a = q.bn;
+    a.rg.amax_out = nullptr;
+    a.tr = 0;
+    a.tiles_y = (a.H + 14) / 15;
+    a.tiles_x = (a.W + 14) / 15;
+    a.ntiles = a.B * a.tiles_y * a.tiles_x;
+    a.cw = l.a.w;
+    a.cbias = l.a.bias;
+    a.cls_out = l.a.cls_out;
+    a.cls_bytes = (uint32_t)((size_t)l.a.B * l.a.Hout * l.a.Wout);
+    a.lut = l.a.lut;
+    a.lut_kind = l.a.lut_kind;
+    a.ncls = l.a.ncls;
+    a.csw = l.a.rg.sw[0];
+    return a;
+}
+
 // one plan op, with its launch-span slots when bugseg_debug_set_spans armed them
-static hipError_t launch_op(const bugseg_ctx *ctx, const Op &o, int i, hipStream_t s) {
+static hipError_t launch_op(const bugseg_ctx *ctx, int i, hipStream_t s) {
+    const Plan &pl = ctx->plan;
+    const Op &o = pl.ops[(size_t)i];
     unsigned long long *sp = ctx->spans && i < ctx->spans_ops ? ctx->spans + 512 * (size_t)i : nullptr;   // (mfma_common.h: 64 slots x 64 B)
+    if (pl.cls_on && i + 2 == (int)pl.ops.size()) { BneckArgs q = cls_fused_args(pl); q.span = sp; return launch_bneck_cls(ctx->prec, q, s); }
+    if (pl.cls_on && i + 1 == (int)pl.ops.size()) return hipSuccess;   // (ran within op i - 1)
     if (o.kind == 1) { BneckArgs q = o.bn; q.span = sp; return launch_bneck(ctx->prec, o.bn_c, o.bn_asym, o.bn_var, q, s, o.bn_cin); }
     if (o.kind == 2) { UpArgs q = o.up; q.span = sp; return launch_up(ctx->prec, o.up_cin, o.up_it, o.up_cout, q, s); }
     ConvArgs q = o.a;
@@ -1570,8 +1610,9 @@ static int enet_forward(bugseg_ctx *ctx, const void *in, bool bgr, int B, int H,
         if (e == hipSuccess && !bgr) e = launch_amax((const float *)in, (size_t)B * H * W * 8, pl.words, (hipStream_t)stream);
         if (e != hipSuccess) return fail(ctx, BUGSEG_EHIP, std::string("range words: ") + hipGetErrorString(e));
     }
+    pl.cls_on = pl.cls_ok && out_kind != BUGSEG_OUT_LOGITS_F32 && first_op <= nops - 2 && last_op == nops;
     for (int i = first_op; i < last_op; ++i) {
-        hipError_t e = launch_op(ctx, pl.ops[(size_t)i], i, (hipStream_t)stream);
+        hipError_t e = launch_op(ctx, i, (hipStream_t)stream);
         if (e != hipSuccess) return fail(ctx, BUGSEG_EHIP, "conv launch " + std::to_string(i) + ": " + hipGetErrorString(e));
     }
     return BUGSEG_OK;
@@ -1982,6 +2023,11 @@ int bugseg_plan_info(bugseg_ctx *ctx, int B, int H, int W, int out_kind, int bgr
     }
     // final epilogue output
     const double fin = out_kind == BUGSEG_OUT_LOGITS_F32 ? (double)B * H * W * ctx->ncls * 4 : (double)B * H * W;
+    // class fusion: the last bottleneck's output is neither written nor read back
+    if (ctx->plan.cls_ok && out_kind != BUGSEG_OUT_LOGITS_F32) {
+        const Op &q = ctx->plan.ops[ctx->plan.ops.size() - 2];
+        pb -= 2.0 * q.bn.B * q.bn.H * q.bn.W * q.bn_c * prec_es(ctx->prec);
+    }
     // raw BGR input (bugseg_enet_forward_bgr): 3 bytes per pixel instead of the 8-channel engine input
     double adj = bgr_input ? (double)B * H * W * (8.0 * prec_es(ctx->prec) - 3.0) : 0.0;
     if (n_launches) *n_launches = (int)ctx->plan.ops.size();
@@ -1999,7 +2045,28 @@ int bugseg_plan_op(bugseg_ctx *ctx, int B, int H, int W, int op, char *kernel, i
     if (!pl.arena || pl.B != B || pl.H != H || pl.W != W) return fail(ctx, BUGSEG_ESTATE, "no forward has run at these dimensions");
     if (op < 0 || op >= (int)pl.ops.size()) return fail(ctx, BUGSEG_EINVAL, "op index out of range");
     const Op &o = pl.ops[op];
+    const int nops = (int)pl.ops.size();
     std::string tag;
+    if (pl.cls_on && op + 1 == nops) {
+        // ran within the previous op (class fusion)
+        if (kernel && kernel_len > 0) std::snprintf(kernel, (size_t)kernel_len, "fused");
+        if (alg_bytes) *alg_bytes = 0;
+        if (plan_bytes) *plan_bytes = 0;
+        if (flops) *flops = 0;
+        return BUGSEG_OK;
+    }
+    if (pl.cls_on && op + 2 == nops) {
+        // the last bottleneck and the class layer in one launch: block input in, class map out
+        const Op &l = pl.ops.back();
+        const double outb = (double)o.bn.B * o.bn.H * o.bn.W * o.bn_c * prec_es(ctx->prec);
+        const double fin = (double)B * H * W;
+        if (kernel && kernel_len > 0) std::snprintf(kernel, (size_t)kernel_len, "bneck C16+classes 16x16");
+        const double lb_b = o.layer_bytes >= 0 ? o.layer_bytes : o.bytes, lb_l = l.layer_bytes >= 0 ? l.layer_bytes : l.bytes;
+        if (alg_bytes) *alg_bytes = lb_b + lb_l + fin;
+        if (plan_bytes) *plan_bytes = o.bytes - outb + (l.bytes - outb) + fin;
+        if (flops) *flops = o.flops + l.flops;
+        return BUGSEG_OK;
+    }
     if (o.kind == 2) {
         tag = "up C" + std::to_string(o.up_cout);
     } else if (o.kind == 1) {
@@ -2040,7 +2107,7 @@ int bugseg_plan_launch_op(bugseg_ctx *ctx, int B, int H, int W, int op, void *st
         return fail(ctx, BUGSEG_ESTATE, "no forward has run at these dimensions");
     if (op < 0 || op >= (int)pl.ops.size()) return fail(ctx, BUGSEG_EINVAL, "op index out of range");
     DeviceGuard g(ctx->device);
-    hipError_t e = launch_op(ctx, pl.ops[op], op, (hipStream_t)stream);
+    hipError_t e = launch_op(ctx, op, (hipStream_t)stream);
     if (e != hipSuccess) return fail(ctx, BUGSEG_EHIP, "launch of op " + std::to_string(op) + ": " + hipGetErrorString(e));
     return BUGSEG_OK;
 }

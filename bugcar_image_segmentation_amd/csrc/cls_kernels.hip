@@ -16,36 +16,9 @@
 // kernel's lifetime; the only per-pixel traffic is the B fragments (one 16-B load per lane and tap,
 // the next group's loads in flight while the current group computes) and the class bytes.
 #include "bugseg_internal.h"
-#include "mfma_common.h"
+#include "cls_common.h"
 
 namespace bugseg {
-
-typedef float f32x16 __attribute__((ext_vector_type(16)));
-
-__device__ __forceinline__ void mma32(f32x16 &acc, const RawB &w, const RawB &x) {
-    acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(bf16x8, w.v), __builtin_bit_cast(bf16x8, x.v),
-                                                  acc, 0, 0, 0);
-}
-__device__ __forceinline__ void mma32(f32x16 &acc, const RawH &w, const RawH &x) {
-    acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(__builtin_bit_cast(f16x8, w.v), __builtin_bit_cast(f16x8, x.v),
-                                                 acc, 0, 0, 0);
-}
-// fp32 parity mode: split-f16 products (mfma_common.h mma(RawS, RawF)) on the 32 x 32 shape: the
-// lane's 8 channels (8h .. 8h + 7 of the tap) as hi / lo f16 parts, three MFMAs
-__device__ __forceinline__ void mma32(f32x16 &acc, const RawS &w, const RawF &x) {
-    f16x8 xh, xl;
-    split_f16(x, xh, xl);
-    const f16x8 wh = __builtin_bit_cast(f16x8, w.h), wl = __builtin_bit_cast(f16x8, w.l);
-    acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(wl, xh, acc, 0, 0, 0);
-    acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(wh, xl, acc, 0, 0, 0);
-    acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(wh, xh, acc, 0, 0, 0);
-}
-
-__device__ __forceinline__ bool nonzero(const RawB &r) { return (r.v.x | r.v.y | r.v.z | r.v.w) != 0u; }
-__device__ __forceinline__ bool nonzero(const RawH &r) { return (r.v.x | r.v.y | r.v.z | r.v.w) != 0u; }
-__device__ __forceinline__ bool nonzero(const RawS &r) {
-    return (r.h.x | r.h.y | r.h.z | r.h.w | r.l.x | r.l.y | r.l.z | r.l.w) != 0u;
-}
 
 // Taps: the 2x2 input neighbourhood (dy, dx) = (s >> 1, s & 1) of the k = 3 layer in pack_tconv's
 // order (D = {0, 1}, tap = ty * 2 + tx). LOGITS: the fp32 logits are written too (parity runs).
@@ -65,18 +38,7 @@ __device__ __forceinline__ bool nonzero(const RawS &r) {
 // (Round 4 measured a low-register form — weights from LDS, the two blocks one after the other, 7 waves
 // per SIMD instead of 4 — at 37.5 vs 34.7 us per 32-frame launch (fp16) and 75.3 vs 74.7 (fp32): the
 // class layer is not occupancy-bound. Removed.)
-// LK (round 4): the remapped class maps need only the GROUP of the first maximal class, not its index.
-// LK = 1: the 3-class map (models.py:56-58: {0, 1} -> 1, {2, 9} -> 0, the rest -> 2), LK = 2: the binary
-// map (models.py:79-80: {0, 1} -> 1, the rest -> 0). Per pixel the groups' maxima (v_max3 over the
-// members) and the overall maximum; when exactly one group attains it, that group holds the first
-// maximal class and its value is the answer. Otherwise (a tie across groups, or no class equal to the
-// maximum: all NaN) the full first-index scan decides, on a wave-uniform branch that noisy real-valued
-// logits essentially never take. LK = 0: the full scan always (raw class ids, parity runs).
-template <int LK> struct ClsGroups;
-template <> struct ClsGroups<1> { static constexpr int N = 3; static constexpr uint32_t mask[3] = {0x0204u, 0x0003u, 0xfdf8u};
-                                  static constexpr int val[3] = {0, 1, 2}; };
-template <> struct ClsGroups<2> { static constexpr int N = 2; static constexpr uint32_t mask[3] = {0x0003u, 0xfffcu, 0u};
-                                  static constexpr int val[3] = {1, 0, 0}; };
+// LK: the class map's group-max argmax (cls_common.h cls_argmax)
 template <typename T, bool LOGITS, int LK = 0>
 __global__ void __launch_bounds__(256, sizeof(T) == 2 ? 4 : 1) cls_kernel(const ConvArgs a) {
     span_enter(a.span);
@@ -91,9 +53,7 @@ __global__ void __launch_bounds__(256, sizeof(T) == 2 ? 4 : 1) cls_kernel(const 
     // the argmax needs no class mask (the logits of those rows are never written)
     if (tid < 64) sbias[tid] = (tid & 15) < a.ncls ? a.bias[tid] : -INFINITY;
     // the class LUT as 16 nibbles in a 64-bit scalar: class c -> (lut64 >> 4c) & 15
-    uint64_t lut64 = 0;
-#pragma unroll
-    for (int c = 0; c < 16; ++c) lut64 |= (uint64_t)((a.lut ? (int)a.lut[c] : c) & 15) << (4 * c);
+    const uint64_t lut64 = cls_lut64(a.lut);
 
     // weights: block b, row r = lane's col -> packed row (phase 2b + ((r >> 2) & 1), class 4 (r >> 3) + (r & 3));
     // this lane's k half = channels 8h .. 8h + 7 of each tap
@@ -102,7 +62,7 @@ __global__ void __launch_bounds__(256, sizeof(T) == 2 ? 4 : 1) cls_kernel(const 
         const T *w = reinterpret_cast<const T *>(a.w);
 #pragma unroll
         for (int b = 0; b < 2; ++b) {
-            const int prow = (2 * b + ((col >> 2) & 1)) * 16 + 4 * (col >> 3) + (col & 3);
+            const int prow = cls_prow(b, col);
 #pragma unroll
             for (int s = 0; s < CLS_TAPS; ++s) {
                 ld8(wr[b][s], w + (size_t)prow * a.Kpad + s * 16 + 8 * h);
@@ -263,54 +223,7 @@ __global__ void __launch_bounds__(256, sizeof(T) == 2 ? 4 : 1) cls_kernel(const 
         f32x16 acc[2];
         block(0, acc[0]);
         block(1, acc[1]);
-        bool full = LK == 0;
-        if constexpr (LK != 0) {
-            // the groups' maxima, the maximum, which groups attain it
-            using G = ClsGroups<LK>;
-            bool tie = false;
-#pragma unroll
-            for (int b = 0; b < 2; ++b) {
-                float gm[G::N];
-#pragma unroll
-                for (int k = 0; k < G::N; ++k) {
-                    float m = -INFINITY;
-#pragma unroll
-                    for (int c = 0; c < 16; ++c)
-                        if ((G::mask[k] >> c) & 1u) m = __builtin_fmaxf(m, acc[b][c]);
-                    gm[k] = m;
-                }
-                float mx = gm[0];
-#pragma unroll
-                for (int k = 1; k < G::N; ++k) mx = __builtin_fmaxf(mx, gm[k]);
-                int hits = 0, v = 0;
-#pragma unroll
-                for (int k = 0; k < G::N; ++k) {
-                    const bool e = gm[k] == mx;
-                    hits += e ? 1 : 0;
-                    v = e ? G::val[k] : v;
-                }
-                cls[b] = v;
-                tie |= hits != 1;
-            }
-            full = __ballot(tie) != 0;                // wave-uniform: rare
-        }
-        if (full) {
-            float best[2];
-            int bi[2];
-#pragma unroll
-            for (int b = 0; b < 2; ++b) {
-                best[b] = acc[b][0];
-#pragma unroll
-                for (int c = 1; c < 16; ++c) best[b] = __builtin_fmaxf(best[b], acc[b][c]);
-                bi[b] = 0;
-            }
-#pragma unroll
-            for (int c = 15; c >= 0; --c)
-#pragma unroll
-                for (int b = 0; b < 2; ++b) bi[b] = acc[b][c] == best[b] ? c : bi[b];
-#pragma unroll
-            for (int b = 0; b < 2; ++b) cls[b] = (int)(lut64 >> (4 * bi[b])) & 15;
-        }
+        cls_argmax<LK>(acc, lut64, cls);
         if constexpr ((CLS_ABL & 2) != 0)
             for (int b = 0; b < 2; ++b) cls[b] = acc[b][b] > acc[b][5] ? 1 : 0;
         if (a.cls_out) {

@@ -36,6 +36,8 @@ def short(name):
     if m:
         asym = m.group(3) in ("1", "true")
         return f"bneck C{m.group(2)}{' asym' if asym else ''} {BNECK_SHAPES.get((int(m.group(2)), int(m.group(4))), '?')}{sfx}"
+    if "bneck_cls_kernel" in name:
+        return "bneck C16+classes 16x16"
     if "bneck2_f32_kernel" in name:
         return "bneck2 C128 16x16"
     m = re.search(r"conv_kernelI(DF16b|DF16_|f)Li(\d+)ELi(\d+)E", name)

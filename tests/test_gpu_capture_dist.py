@@ -297,6 +297,9 @@ def test_launch_spans_inside_a_captured_step(gpu, blocks, prec):
     torch.cuda.synchronize()
     sp = spans.cpu().numpy().view(np.uint64)
     st, en = sp[:, :, 0].min(1), sp[:, :, 1].max(1)
+    # (with class fusion, BUGSEG_CLS_FUSE=1, op "fused" ran within the previous launch)
+    launched = np.array([m.ctx.plan_op(B, H, W, i)[0] != "fused" for i in range(n)])
+    st, en = st[launched], en[launched]
     assert (st < np.uint64(2 ** 63)).all() and (en > st).all()          # every launch stamped
     assert (st[1:] >= en[:-1]).all()                                      # stream order
     assert torch.equal(seg, seg0)

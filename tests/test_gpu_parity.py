@@ -422,6 +422,73 @@ def test_fused_bottlenecks_multi_tile_walks(gpu, blocks, prec, H, W, variant, gr
     assert torch.equal(a, b)
 
 
+_CLASS_KINDS = (N.OUT_CLASS15_U8, N.OUT_CLASS3_U8, N.OUT_BINARY_U8)
+
+
+@pytest.mark.parametrize("grid", [None, "8"])
+@pytest.mark.parametrize("prec", ["fp32", "bf16", "fp16"])
+@pytest.mark.parametrize("B,H,W", [(3, 72, 104), (2, 64, 96), (2, 120, 160), (1, 480, 640)])
+def test_class_fusion_equals_separate_launches(gpu, blocks, prec, B, H, W, grid, monkeypatch):
+    """ENet's last bottleneck and the class layer as ONE launch (class fusion, bneck_kernels.hip FC:
+    tiles 15 apart, the block output in LDS) against the two launches (BUGSEG_CLS_FUSE=0): every class
+    map (raw ids, the 3-class and the binary map) equal byte for byte — edge tiles included (the C16
+    maps 36 x 52 / 32 x 48 are not multiples of 15), and with grid "8" every workgroup walks many tiles.
+    The fused form (opt-in: BUGSEG_CLS_FUSE=1, measured slower) runs for class maps only."""
+    bgr = torch.from_numpy(synthetic.road_frames(B, H, W, seed=H + 3)).cuda()
+    monkeypatch.setenv("BUGSEG_CLS_FUSE", "1")
+    if grid is not None:
+        monkeypatch.setenv("BUGSEG_BNECK_GRID", grid)
+    fused = ENET(weights=blocks, precision=prec)
+    got = {}
+    for kind in _CLASS_KINDS:
+        seg = torch.empty((B, H, W), dtype=torch.uint8, device=gpu)
+        fused.ctx.forward_bgr(bgr, B, H, W, kind, seg)
+        got[kind] = seg
+    n = fused.ctx.plan_info(B, H, W, N.OUT_CLASS3_U8, bgr_input=True)[0]
+    tags = [fused.ctx.plan_op(B, H, W, i)[0] for i in range(n)]
+    assert tags[-2] == "bneck C16+classes 16x16" and tags[-1] == "fused", tags[-3:]
+    torch.cuda.synchronize()
+    monkeypatch.delenv("BUGSEG_BNECK_GRID", raising=False)
+    monkeypatch.setenv("BUGSEG_CLS_FUSE", "0")
+    plain = ENET(weights=blocks, precision=prec)
+    for kind in _CLASS_KINDS:
+        ref = torch.empty((B, H, W), dtype=torch.uint8, device=gpu)
+        plain.ctx.forward_bgr(bgr, B, H, W, kind, ref)
+        assert plain.ctx.plan_op(B, H, W, n - 1)[0] == "classes"
+        diff = int((got[kind] != ref).sum())
+        assert diff == 0, f"kind {kind}: {diff} of {ref.numel()} pixels differ"
+
+
+def test_class_fusion_under_range_scaling(gpu):
+    """fp32 with the survey's undamped weights (activations past f16's range): the fused class phase
+    scales its input by the TILE's measured max (the class kernel: the batch's), so its logits differ
+    from the separate launches' in the last bits where either exponent is non-zero — the class maps
+    then agree wherever the top-2 logit margin exceeds 1e-5 of the frame's max |logit|, and the fused
+    map equals LUT[first argmax] of the separate launch's logits there."""
+    bl = enet_spec.build_enet(res_gamma=(0.5, 1.5))
+    B, H, W = 2, 240, 320
+    os.environ["BUGSEG_CLS_FUSE"] = "1"
+    bgr = torch.from_numpy(synthetic.road_frames(B, H, W, seed=12)).cuda()
+    try:
+        m = ENET(weights=bl, precision="fp32")
+        lg = torch.empty((B, m.num_classes, H, W), dtype=torch.float32, device=gpu)
+        m.ctx.forward_bgr(bgr, B, H, W, N.OUT_LOGITS_F32, lg)       # (the plan, and its fusion choice, is built here)
+    finally:
+        del os.environ["BUGSEG_CLS_FUSE"]
+    seg = torch.empty((B, H, W), dtype=torch.uint8, device=gpu)
+    m.ctx.forward_bgr(bgr, B, H, W, N.OUT_CLASS15_U8, seg)
+    assert m.ctx.plan_op(B, H, W, m.ctx.plan_info(B, H, W, N.OUT_CLASS15_U8)[0] - 1)[0] == "fused"
+    la = lg.cpu().numpy()
+    assert np.abs(la).max() > 1e4          # the case really scales
+    mx = np.abs(la).reshape(B, -1).max(1)[:, None, None]
+    dec = _margin(la) > 1e-5 * mx
+    s = seg.cpu().numpy()
+    print(f"undamped fp32 class fusion: {int((~dec).sum())} near-tie pixels of {dec.size}; "
+          f"{int(((s != la.argmax(1)) & dec).sum())} decided pixels differ")
+    assert (~dec).mean() < 1e-3
+    assert np.array_equal(s[dec], la.argmax(1)[dec])
+
+
 @pytest.mark.parametrize("prec", ["fp32", "bf16", "fp16"])
 def test_up_block_pair_equals_separate(gpu, blocks, prec, monkeypatch):
     """The upsampling blocks' main and extension 1x1 convolutions merged into one launch (one read
