@@ -32,6 +32,10 @@ namespace bugseg {
 #ifndef CLS_AUX
 #define CLS_AUX 0          // class-map store policy (A/B knob; the BEV rasteriser reads them next)
 #endif
+#ifndef CLS_SPLIT1
+#define CLS_SPLIT1 0       // fp32: each tap's operand split once per group for both blocks (A/B knob; round 6, with
+                           // VGPR-form MFMAs: 109 -> 113 us per 64-frame launch — the up-front splits delay the MFMAs)
+#endif
 #ifndef CLS_BIAS_REG
 #define CLS_BIAS_REG 1
 #endif
@@ -40,7 +44,10 @@ namespace bugseg {
 // class layer is not occupancy-bound. Removed.)
 // LK: the class map's group-max argmax (cls_common.h cls_argmax)
 template <typename T, bool LOGITS, int LK = 0>
-__global__ void __launch_bounds__(256, sizeof(T) == 2 ? 4 : 1) cls_kernel(const ConvArgs a) {
+#ifndef CLS_OCC_F32
+#define CLS_OCC_F32 1      // fp32: waves per SIMD the build is held to (A/B knob; 3: 28 VGPRs spilled, 109 -> 257 us)
+#endif
+__global__ void __launch_bounds__(256, sizeof(T) == 2 ? 4 : CLS_OCC_F32) cls_kernel(const ConvArgs a) {
     span_enter(a.span);
     constexpr int CLS_TAPS = 4;
     using Raw = typename Tr<T>::Raw;
@@ -179,6 +186,18 @@ __global__ void __launch_bounds__(256, sizeof(T) == 2 ? 4 : 1) cls_kernel(const 
         // lets the waits before the MFMAs name only this group's loads (a conditional prefetch
         // made the compiler wait vmcnt(3), i.e. for the next group's first load as well).
         load(g + nw, nxt, qn);
+        // CLS_SPLIT1 (fp32): the four taps' hi / lo parts, scaled first when the launch scales (the same
+        // parts the per-block split would make: bit-identical)
+        constexpr bool S1 = F32 && CLS_SPLIT1;
+        f16x8 sxh[S1 ? CLS_TAPS : 1], sxl[S1 ? CLS_TAPS : 1];
+        if constexpr (S1) {
+#pragma unroll
+            for (int s = 0; s < CLS_TAPS; ++s) {
+                RawF xq = reinterpret_cast<const RawF &>(cur[s]);
+                if (scl) mul8(xq, xm);
+                split_f16(xq, sxh[s], sxl[s]);
+            }
+        }
         // per block: accumulators from the bias, the taps' MFMAs, (parity runs) the logits, and the
         // argmax over this lane's classes = the sequential strict > scan from -inf of tf.math.argmax
         // (models.py:55): the maximum (v_max ignores NaN), then its first index; no class equal to the
@@ -186,6 +205,10 @@ __global__ void __launch_bounds__(256, sizeof(T) == 2 ? 4 : 1) cls_kernel(const 
         // first, then the two argmax scans interleaved
         auto taps = [&](int b, f32x16 &acc, auto sc) {
             auto tap = [&](int s) {
+                if constexpr (S1) {
+                    if constexpr (F32) mma32s(acc, reinterpret_cast<const RawS &>(wr[b][s]), sxh[s], sxl[s]);
+                    return;
+                }
                 Raw xq = cur[s];
                 if constexpr (decltype(sc)::value) mul8(reinterpret_cast<RawF &>(xq), xm);
                 mma32(acc, wr[b][s], xq);
