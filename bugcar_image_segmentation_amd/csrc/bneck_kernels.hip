@@ -265,6 +265,13 @@ __device__ __forceinline__ bool bneck_body(const BneckArgs &a, float rlane) {
 // fp32 (parity mode) C = 64 with the register epilogue: no staging region, so the LDS footprint is the
 // halo's (8 x 16 tile: 42.7 -> 39.7 KB, 3 -> 4 workgroups per CU); its quads are 16-B chunks already.
 // Measured slower (round 3: 94.1 -> 104.7 us per launch: a pixel's 256 B leave as four 64-B pieces)
+// fp32 C = 64 (non-down) with the register epilogue AND whole-line stores (LINES below; round 6, A/B knob):
+// the residual is loaded in the same line layout and traded back with the same DPP row rotation.
+// Bit-identical (44 fp32 parity cases) but measured slower: 8 x 16 138.8 -> 147.5 us per 64-frame launch
+// (124 VGPRs, no spills; the half-staged LDS epilogue, HSTG, stays)
+#ifndef BNECK_F32_LINES64
+#define BNECK_F32_LINES64 0
+#endif
 #ifndef BNECK_REG3_C64_F32
 #define BNECK_REG3_C64_F32 0
 #endif
@@ -291,7 +298,7 @@ __device__ __forceinline__ bool bneck_body(const BneckArgs &a, float rlane) {
     // pixels would be written as half lines by the register layout, which measured slower there
     // (44.7 vs 43.0 us per launch with t1 in registers).
     // (the down form's C = 64 launch measured faster with the register epilogue: 53 vs 55 us)
-    constexpr bool REG3 = C != 64 || DN || BNECK_REG3_C64 || (sizeof(T) == 4 && BNECK_REG3_C64_F32);
+    constexpr bool REG3 = C != 64 || DN || BNECK_REG3_C64 || (sizeof(T) == 4 && (BNECK_REG3_C64_F32 || BNECK_F32_LINES64));
     constexpr bool SWAP = REG3 && sizeof(T) == 2 && NR3 % 2 == 0;
     constexpr bool HALF = REG3 && sizeof(T) == 2 && NR3 % 2 != 0;
     constexpr int EPC = 16 / (int)sizeof(T);          // elements per 16-B chunk
@@ -393,7 +400,9 @@ __device__ __forceinline__ bool bneck_body(const BneckArgs &a, float rlane) {
 #ifndef BNECK_F32_LINES
 #define BNECK_F32_LINES 1
 #endif
-    constexpr bool LINES = BNECK_F32_LINES && sizeof(T) == 4 && REG3 && C == 128 && (KEEPF || (DKEEP && PKW == 2)) && RQ3 % 2 == 0;
+    constexpr bool LINES64 = BNECK_F32_LINES64 && sizeof(T) == 4 && REG3 && C == 64 && !DN && !KEEP;   // residual from the ring
+    constexpr bool LINES = (BNECK_F32_LINES && sizeof(T) == 4 && REG3 && C == 128 && (KEEPF || (DKEEP && PKW == 2)) && RQ3 % 2 == 0) ||
+                           LINES64;
     // FC >= 0 (round 6): ENet's class layer fused into its last bottleneck (C = 16, 16 x 16 tiles), FC =
     // the class map's LUT kind (cls_common.h cls_argmax). Tiles overlap by one row and one column (a
     // 15 x 15 stride): phase 3 leaves the block output of all 16 x 16 tile pixels in LDS (otile) instead
@@ -1108,6 +1117,20 @@ __device__ __forceinline__ bool bneck_body(const BneckArgs &a, float rlane) {
                 }
                 return;
             }
+            if constexpr (LINES64) {
+                // whole lines, as LINES stores them: per u, line u of pixels col and col ^ 8 (the lane's 16 B
+                // of each); phase 3 trades them back into its row 2u / 2u + 1 quads (see there)
+                const uint32_t pc = pix_base(wave + NW * j, col), po8 = pix_base(wave + NW * j, col ^ 8);
+                const bool lo8 = col < 8;
+                const uint32_t pa = lo8 ? pc : po8, pb = lo8 ? po8 : pc;
+#pragma unroll
+                for (int u = 0; u < RQ3 / 2; ++u) {
+                    const uint32_t cb = (uint32_t)(u * 32 + (lo8 ? 0 : 16) + kq * 4) * (uint32_t)sizeof(T);
+                    r[2 * u] = bld16(rrb, pa == OOB ? OOB : pa + cb);
+                    r[2 * u + 1] = bld16(rrb, pb == OOB ? OOB : pb + cb);
+                }
+                return;
+            }
             const uint32_t po = DN ? 0u : pix_base(wave + NW * j, col);
 #pragma unroll
             for (int t = 0; t < RQ3; ++t) {
@@ -1466,11 +1489,27 @@ __device__ __forceinline__ bool bneck_body(const BneckArgs &a, float rlane) {
 #pragma unroll
                 for (int u = 0; u < RQ3 / 2; ++u) {
                     float4 v2[2];
+                    // LINES64: the ring holds line u of pixels pa / pb (load_res); lane col's row 2u quad is its
+                    // own first word (lo8) or lane col - 8's second, row 2u + 1 the mirror image
+                    uint4 rl[2];
+                    if constexpr (LINES64) {
+                        const uint4 l1 = res[j % RP][2 * u], l2 = res[j % RP][2 * u + 1];
+                        const uint4 xs = lo8 ? l2 : l1;
+                        uint4 ys;
+                        ys.x = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)xs.x, 0x128, 0xf, 0xf, false);
+                        ys.y = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)xs.y, 0x128, 0xf, 0xf, false);
+                        ys.z = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)xs.z, 0x128, 0xf, 0xf, false);
+                        ys.w = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)xs.w, 0x128, 0xf, 0xf, false);
+                        rl[0] = lo8 ? l1 : ys;
+                        rl[1] = lo8 ? ys : l2;
+                    }
 #pragma unroll
                     for (int h = 0; h < 2; ++h) {
                         const int t = 2 * u + h;
                         uint4 rc;
-                        if constexpr (KEEPF) {
+                        if constexpr (LINES64) {
+                            rc = rl[h];
+                        } else if constexpr (KEEPF) {
                             const RawF &k = reinterpret_cast<const RawF &>(kx[j][t >> 1]);
                             rc = __builtin_bit_cast(uint4, (t & 1) ? k.b : k.a);
                         } else {
@@ -1494,6 +1533,8 @@ __device__ __forceinline__ bool bneck_body(const BneckArgs &a, float rlane) {
                     bst16o<OAUX>(rob, pa == OOB ? OOB : pa + cb, lo8 ? u0 : ys);
                     bst16o<OAUX>(rob, pb == OOB ? OOB : pb + cb, lo8 ? ys : u1);
                 }
+                if constexpr (LINES64)   // (the ring's refill, as below)
+                    if (j + RP < NF2 && wave + NW * (j + RP) < NFT) load_res(j + RP, res[j % RP]);
                 continue;
             }
 #pragma unroll
@@ -1720,7 +1761,7 @@ size_t bneck_lds_bytes(int prec, int C, bool asym, int v, int cin, bool cls) {
     const size_t wts = (size_t)NR1 * 16 * (KS1 * 32 + padw) + (size_t)NR1 * 16 * (KS2 * 32 + padw) * (asym ? 2 : 1) +
                        (size_t)C * (32 + padw);
     const size_t halo = (size_t)(TH + 2 * R) * (TW + 2 * RX) * (bneck_pl(es, C, cin > 0) && !asym ? 16 : bneck_pstr(es, IS, wide));
-    const bool staged = C == 64 && !BNECK_REG3_C64 && !(es == 4 && BNECK_REG3_C64_F32);
+    const bool staged = C == 64 && !BNECK_REG3_C64 && !(es == 4 && (BNECK_REG3_C64_F32 || (BNECK_F32_LINES64 && cin == 0)));
     const bool hstg = staged && es == 4 && BNECK_F32_HSTG;            // fp32 C = 64: one 32-channel half at a time
     const size_t stage = staged ? (size_t)NW * 16 * ((hstg ? C / 2 : C) + pad) : 0;    // staged epilogue (REG3 off)
     const size_t consts = ((size_t)6 * NR1 * 16 + 3 * (size_t)C) * sizeof(float);
