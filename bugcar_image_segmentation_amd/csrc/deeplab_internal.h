@@ -24,7 +24,8 @@ struct DlConvArgs {
     const float *bias;   // [NP]
     const float *bias_img;  // optional per-image bias (B, bias_img_stride) f32
     int bias_img_stride;
-    int act;             // 0 none, 1 ReLU, 2 ReLU6
+    int act;             // 0 none, 1 ReLU, 2 ReLU6 (before the residual add), 3 ReLU after the residual add
+                         // (ResNet: relu(shortcut + residual))
     const void *res;     // optional residual NHWC T, (B, Hout, Wout, res_cs)
     int res_cs;
     void *out;           // NHWC (B, Hout, Wout, out_cs), channels [out_off, out_off + cout)
@@ -92,7 +93,17 @@ struct DlArgmaxArgs {
     int64_t *out;        // (B, Hout, Wout)
 };
 
+// Max pooling, TF 'SAME' / 'VALID' geometry given as pads (taps outside the input are skipped, i.e. -inf
+// padding): ResNet's 3x3 s2 root pool, and with k = 1 its strided-identity shortcut (resnet_utils.subsample)
+struct DlMaxPoolArgs {
+    const void *in;      // (B, Hin, Win, C) T
+    int B, Hin, Win, C;
+    int Hout, Wout, k, stride, pad_t, pad_l;
+    void *out;           // (B, Hout, Wout, C) T
+};
+
 hipError_t dl_launch_prep(int prec, const DlPrepArgs &a, hipStream_t s);
+hipError_t dl_launch_maxpool(int prec, const DlMaxPoolArgs &a, hipStream_t s);
 hipError_t dl_launch_conv(int prec, bool out_f32, const DlConvArgs &a, hipStream_t s);
 hipError_t dl_launch_dw(int prec, const DlDwArgs &a, hipStream_t s);
 hipError_t dl_launch_pool(int prec, const DlPoolArgs &a, hipStream_t s);

@@ -292,7 +292,7 @@ __global__ void __launch_bounds__(256) dl_conv_kernel(const DlConvArgs a) {
                 const int nl = r * 16 + kq * 4, n = n0 + nl;
                 float4 v = add4(f4(acc[j][r]), ld4f(a.bias + n));
                 if (a.bias_img) v = add4(v, ld4f(a.bias_img + (size_t)pb[j] * a.bias_img_stride + n));
-                if (a.act >= 1) v = make_float4(fmaxf(v.x, 0.f), fmaxf(v.y, 0.f), fmaxf(v.z, 0.f), fmaxf(v.w, 0.f));
+                if (a.act == 1 || a.act == 2) v = make_float4(fmaxf(v.x, 0.f), fmaxf(v.y, 0.f), fmaxf(v.z, 0.f), fmaxf(v.w, 0.f));
                 if (a.act == 2) v = make_float4(fminf(v.x, 6.f), fminf(v.y, 6.f), fminf(v.z, 6.f), fminf(v.w, 6.f));
                 *reinterpret_cast<float4 *>(st + (jj * 16 + col) * DL_STG_RS + nl) = v;
             }
@@ -310,6 +310,10 @@ __global__ void __launch_bounds__(256) dl_conv_kernel(const DlConvArgs a) {
                 const T *rp = reinterpret_cast<const T *>(a.res) + (size_t)p * a.res_cs + n;
                 v0 = add4(v0, ld4(rp));
                 v1 = add4(v1, ld4(rp + 4));
+            }
+            if (a.act == 3) {              // ReLU after the residual add (ResNet units)
+                v0 = make_float4(fmaxf(v0.x, 0.f), fmaxf(v0.y, 0.f), fmaxf(v0.z, 0.f), fmaxf(v0.w, 0.f));
+                v1 = make_float4(fmaxf(v1.x, 0.f), fmaxf(v1.y, 0.f), fmaxf(v1.z, 0.f), fmaxf(v1.w, 0.f));
             }
             if constexpr (OUTF32) {
                 float *o = reinterpret_cast<float *>(a.out) + (size_t)p * a.out_cs + a.out_off + n;
@@ -422,7 +426,7 @@ __global__ void __launch_bounds__(256, 2) dl_gemm_kernel(const DlConvArgs a) {
                 const int nl = r * 16 + kq * 4, n = n0 + nl;
                 float4 v = add4(f4(acc[j][r]), ld4f(a.bias + n));
                 if (a.bias_img) v = add4(v, ld4f(a.bias_img + (size_t)pimg * a.bias_img_stride + n));
-                if (a.act >= 1) v = make_float4(fmaxf(v.x, 0.f), fmaxf(v.y, 0.f), fmaxf(v.z, 0.f), fmaxf(v.w, 0.f));
+                if (a.act == 1 || a.act == 2) v = make_float4(fmaxf(v.x, 0.f), fmaxf(v.y, 0.f), fmaxf(v.z, 0.f), fmaxf(v.w, 0.f));
                 if (a.act == 2) v = make_float4(fminf(v.x, 6.f), fminf(v.y, 6.f), fminf(v.z, 6.f), fminf(v.w, 6.f));
                 *reinterpret_cast<float4 *>(st + (jj * 16 + col) * DL_STG_RS + nl) = v;
             }
@@ -440,6 +444,10 @@ __global__ void __launch_bounds__(256, 2) dl_gemm_kernel(const DlConvArgs a) {
                 const __bf16 *rp = reinterpret_cast<const __bf16 *>(a.res) + (size_t)p * a.res_cs + n;
                 v0 = add4(v0, ld4(rp));
                 v1 = add4(v1, ld4(rp + 4));
+            }
+            if (a.act == 3) {              // ReLU after the residual add (ResNet units)
+                v0 = make_float4(fmaxf(v0.x, 0.f), fmaxf(v0.y, 0.f), fmaxf(v0.z, 0.f), fmaxf(v0.w, 0.f));
+                v1 = make_float4(fmaxf(v1.x, 0.f), fmaxf(v1.y, 0.f), fmaxf(v1.z, 0.f), fmaxf(v1.w, 0.f));
             }
             if constexpr (OUTF32) {
                 float *o = reinterpret_cast<float *>(a.out) + (size_t)p * a.out_cs + a.out_off + n;
@@ -621,7 +629,7 @@ __global__ void __launch_bounds__(256, 2) dl_gemm128_kernel(const DlConvArgs a) 
                 const int nl = r * 16 + kq * 4, n = nb + nl;
                 float4 v = add4(f4(acc[j][r]), ld4f(a.bias + n));
                 if (a.bias_img) v = add4(v, ld4f(a.bias_img + (size_t)pimg * a.bias_img_stride + n));
-                if (a.act >= 1) v = make_float4(fmaxf(v.x, 0.f), fmaxf(v.y, 0.f), fmaxf(v.z, 0.f), fmaxf(v.w, 0.f));
+                if (a.act == 1 || a.act == 2) v = make_float4(fmaxf(v.x, 0.f), fmaxf(v.y, 0.f), fmaxf(v.z, 0.f), fmaxf(v.w, 0.f));
                 if (a.act == 2) v = make_float4(fminf(v.x, 6.f), fminf(v.y, 6.f), fminf(v.z, 6.f), fminf(v.w, 6.f));
                 *reinterpret_cast<float4 *>(stg + (jj * 16 + col) * DL_STG_RS + nl) = v;
             }
@@ -639,6 +647,10 @@ __global__ void __launch_bounds__(256, 2) dl_gemm128_kernel(const DlConvArgs a) 
                 const __bf16 *rp = reinterpret_cast<const __bf16 *>(a.res) + (size_t)p * a.res_cs + n;
                 v0 = add4(v0, ld4(rp));
                 v1 = add4(v1, ld4(rp + 4));
+            }
+            if (a.act == 3) {              // ReLU after the residual add (ResNet units)
+                v0 = make_float4(fmaxf(v0.x, 0.f), fmaxf(v0.y, 0.f), fmaxf(v0.z, 0.f), fmaxf(v0.w, 0.f));
+                v1 = make_float4(fmaxf(v1.x, 0.f), fmaxf(v1.y, 0.f), fmaxf(v1.z, 0.f), fmaxf(v1.w, 0.f));
             }
             if constexpr (OUTF32) {
                 float *o = reinterpret_cast<float *>(a.out) + (size_t)p * a.out_cs + a.out_off + n;
@@ -1011,6 +1023,39 @@ __global__ void __launch_bounds__(256) dl_resize_kernel(const DlResizeArgs a) {
     st4(op + 4, make_float4(o[4], o[5], o[6], o[7]));
 }
 
+// Max pooling (DlMaxPoolArgs): one thread = 8 channels of one output pixel; the taps inside the input
+// only (TF pads max pooling with -inf); the result is one of the inputs, so it is exact in T
+template <typename T>
+__global__ void __launch_bounds__(256) dl_maxpool_kernel(const DlMaxPoolArgs a) {
+    const int groups = a.C >> 3;
+    const int i = blockIdx.x * 256 + threadIdx.x;
+    if (i >= a.B * a.Hout * a.Wout * groups) return;
+    const int g = i % groups, q = i / groups;
+    const int x = q % a.Wout, t = q / a.Wout, y = t % a.Hout, b = t / a.Hout;
+    const T *base = reinterpret_cast<const T *>(a.in) + (size_t)b * a.Hin * a.Win * a.C + g * 8;
+    using Raw = typename Tr<T>::Raw;
+    float m[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) m[j] = -INFINITY;
+    for (int dy = 0; dy < a.k; ++dy) {
+        const int iy = y * a.stride - a.pad_t + dy;
+        if ((unsigned)iy >= (unsigned)a.Hin) continue;
+        for (int dx = 0; dx < a.k; ++dx) {
+            const int ix = x * a.stride - a.pad_l + dx;
+            if ((unsigned)ix >= (unsigned)a.Win) continue;
+            Raw r;
+            ld8(r, base + ((size_t)iy * a.Win + ix) * a.C);
+            float4 v[2];
+            raw4(r, v[0], v[1]);
+#pragma unroll
+            for (int j = 0; j < 8; ++j) m[j] = fmaxf(m[j], get(v[j >> 2], j & 3));
+        }
+    }
+    T *op = reinterpret_cast<T *>(a.out) + (((size_t)b * a.Hout + y) * a.Wout + x) * a.C + g * 8;
+    st4(op, make_float4(m[0], m[1], m[2], m[3]));
+    st4(op + 4, make_float4(m[4], m[5], m[6], m[7]));
+}
+
 // ------------------------------------------------------------------ launchers
 hipError_t dl_launch_prep(int prec, const DlPrepArgs &a, hipStream_t s) {
     const int n = a.B * a.Hc * a.Wc;
@@ -1146,6 +1191,14 @@ hipError_t dl_launch_pool(int prec, const DlPoolArgs &a, hipStream_t s) {
         hipLaunchKernelGGL((dl_pool_gemv_kernel<float, 0>), dim3((a.B * a.cmid + 3) / 4), dim3(256), 0, s, a);
         hipLaunchKernelGGL((dl_pool_gemv_kernel<float, 1>), dim3((a.B * a.cout + 3) / 4), dim3(256), 0, s, a);
     }
+    return hipGetLastError();
+}
+
+hipError_t dl_launch_maxpool(int prec, const DlMaxPoolArgs &a, hipStream_t s) {
+    if ((a.C & 7) || a.k < 1 || a.stride < 1) return hipErrorInvalidValue;
+    const int n = a.B * a.Hout * a.Wout * (a.C >> 3);
+    if (prec == PREC_BF16) hipLaunchKernelGGL(dl_maxpool_kernel<__bf16>, dim3((n + 255) / 256), dim3(256), 0, s, a);
+    else hipLaunchKernelGGL(dl_maxpool_kernel<float>, dim3((n + 255) / 256), dim3(256), 0, s, a);
     return hipGetLastError();
 }
 

@@ -21,7 +21,7 @@ namespace {
 
 thread_local std::string g_dl_err;
 
-enum { OP_PREP = 1, OP_CONV = 2, OP_DW = 3, OP_POOL = 4, OP_ARGMAX = 5, OP_RESIZE = 6 };
+enum { OP_PREP = 1, OP_CONV = 2, OP_DW = 3, OP_POOL = 4, OP_ARGMAX = 5, OP_RESIZE = 6, OP_MAXPOOL = 7 };
 
 struct DlOp {
     int f[BUGSEG_DL_OP_FIELDS];
@@ -98,7 +98,7 @@ bool check_op(const bugseg_dl *c, const DlOp &o, std::string &why) {
             !in_range(cout, 8, CH) || !in_range(bimg_stride, 0, 1 << 20) || (f[31] != 0 && f[31] != 1 && f[31] != 2) ||
             (double)B * Hout * Wout >= 2147483648.0) { why = "conv: field out of range"; return false; }
         if (Hin < 1 || Win < 1 || Hout < 1 || Wout < 1 || kh < 1 || kw < 1 || stride < 1 || dil < 1 || CS < 8 ||
-            CS % 8 || cinP % 32 || cinP < 32 || NP % 64 || NP < 64 || act < 0 || act > 2 || cout < 8 || cout % 8 ||
+            CS % 8 || cinP % 32 || cinP < 32 || NP % 64 || NP < 64 || act < 0 || act > 3 || cout < 8 || cout % 8 ||
             cout > NP || out_off % 8 || out_off + cout > out_cs) { why = "conv: bad shape"; return false; }
         if (!buf_ok(c, src, (double)B * Hin * Win * CS * es)) { why = "conv: source buffer too small"; return false; }
         if (!buf_ok(c, dst, (double)B * Hout * Wout * out_cs * (out_f32 ? 4.0 : es))) { why = "conv: destination too small"; return false; }
@@ -165,6 +165,17 @@ bool check_op(const bugseg_dl *c, const DlOp &o, std::string &why) {
         if (C % 8 || in_cs % 8 || out_cs % 8 || out_off % 8 || C > in_cs || out_off + C > out_cs) { why = "resize: bad shape"; return false; }
         if (!buf_ok(c, src, (double)B * h * w * in_cs * es) || !buf_ok(c, dst, (double)B * Ho * Wo * out_cs * es)) {
             why = "resize: buffer too small"; return false;
+        }
+        return true;
+    }
+    case OP_MAXPOOL: {
+        const int src = f[1], dst = f[2], Hin = f[3], Win = f[4], C = f[5], Hout = f[6], Wout = f[7];
+        if (!in_range(Hin, 1, SP) || !in_range(Win, 1, SP) || !in_range(Hout, 1, SP) || !in_range(Wout, 1, SP) ||
+            !in_range(C, 8, CH) || !in_range(f[8], 1, 15) || !in_range(f[9], 1, 255) || !in_range(f[10], 0, 15) ||
+            !in_range(f[11], 0, 15) || (double)B * Hout * Wout * C >= 2147483648.0) { why = "maxpool: field out of range"; return false; }
+        if (C % 8 || (Hout - 1) * f[9] - f[10] > Hin - 1 || (Wout - 1) * f[9] - f[11] > Win - 1) { why = "maxpool: bad shape"; return false; }
+        if (!buf_ok(c, src, (double)B * Hin * Win * C * es) || !buf_ok(c, dst, (double)B * Hout * Wout * C * es)) {
+            why = "maxpool: buffer too small"; return false;
         }
         return true;
     }
@@ -244,6 +255,13 @@ hipError_t run_op(bugseg_dl *c, const DlOp &o, const uint8_t *rgb, int H, int W,
         a.z_stride = f[16];
         a.y = static_cast<float *>(bufp(c, f[17]));
         return dl_launch_pool(c->prec, a, s);
+    }
+    case OP_MAXPOOL: {
+        DlMaxPoolArgs a{};
+        a.in = bufp(c, f[1]); a.out = bufp(c, f[2]);
+        a.B = B; a.Hin = f[3]; a.Win = f[4]; a.C = f[5]; a.Hout = f[6]; a.Wout = f[7];
+        a.k = f[8]; a.stride = f[9]; a.pad_t = f[10]; a.pad_l = f[11];
+        return dl_launch_maxpool(c->prec, a, s);
     }
     case OP_ARGMAX: {
         DlArgmaxArgs a{};

@@ -31,6 +31,8 @@ Op list (``lower``): int32 records of ``OP_FIELDS`` fields, interpreted by deepl
   POOL   [4, src, part, z, H, W, C, CS, chunk_px, nchunks, cmid, cout, wp_off, bp_off, wq_off, bq_off, z_stride, y]
   ARGMAX [5, logits, h, w, LCS, ncls]
   RESIZE [6, src, dst, h, w, in_cs, C, Hout, Wout, out_cs, out_off]   (bilinear, align_corners; DeepLabV3+ decoder)
+  MAXPOOL [7, src, dst, Hin, Win, C, Hout, Wout, k, stride, pad_t, pad_l]   (ResNet root pool / subsample)
+CONV act: 0 none, 1 ReLU, 2 ReLU6 (before the residual add), 3 ReLU after the residual add (ResNet).
 """
 from __future__ import annotations
 
@@ -41,7 +43,7 @@ import numpy as np
 import torch
 
 OP_FIELDS = 32
-OP_PREP, OP_CONV, OP_DW, OP_POOL, OP_ARGMAX, OP_RESIZE = 1, 2, 3, 4, 5, 6
+OP_PREP, OP_CONV, OP_DW, OP_POOL, OP_ARGMAX, OP_RESIZE, OP_MAXPOOL = 1, 2, 3, 4, 5, 6, 7
 ACT_NONE, ACT_RELU, ACT_RELU6 = 0, 1, 2
 BN_EPS = 1e-3
 CROP = 513
@@ -349,6 +351,20 @@ class Lowering:
                 2.0 * B * Ho * Wo * C * 9, B * (H * W + Ho * Wo) * C * es)
         return Ho, Wo
 
+    def maxpool(self, src, dst, H, W, C, k, s, tag="maxpool"):
+        """k x k max pool, stride s: TF SAME for k > 1 (slim max_pool2d in resnet_arg_scope), VALID for the
+        1x1 subsample (resnet_utils.subsample) -> (Hout, Wout)."""
+        B, es = self.B, self.es
+        if k == 1:
+            Ho, pt, Wo, pl = (H - 1) // s + 1, 0, (W - 1) // s + 1, 0
+        else:
+            Ho, pt = same_pad(H, k, s, 1)
+            Wo, pl = same_pad(W, k, s, 1)
+        self.use(dst, B * Ho * Wo * C * es)
+        self.op([OP_MAXPOOL, src, dst, H, W, C, Ho, Wo, k, s, pt, pl], tag, float(B * Ho * Wo * C * k * k),
+                B * (H * W + Ho * Wo) * C * es)
+        return Ho, Wo
+
     def aspp_pool(self, net, src, h, w, C, part=8, z=9, y=10):
         """Image pooling folded into the projection as a per-image bias (buffers part, z, y) -> z stride."""
         B, es = self.B, self.es
@@ -402,8 +418,14 @@ def lower(net, B: int, bf16: bool, fuse_dw: bool = False, nb=None, fuse_prep: bo
     the default plan (separate DW ops through buffer 4) but measured 2.4x slower (5.1 vs 2.2 ms per
     16-frame forward for the pair): the 9 tap loads of every operand chunk serialise ahead of the
     MFMAs and are recomputed for every 64-channel output tile.
-    An Xception network (deeplab_xception.DeepLabXception) lowers through lower_xception."""
+    An Xception network (deeplab_xception.DeepLabXception) lowers through lower_xception, a ResNet one
+    (deeplab_resnet.DeepLabResNet) through lower_resnet."""
     if not isinstance(net, DeepLab):
+        from .deeplab_resnet import DeepLabResNet, lower_resnet
+        if isinstance(net, DeepLabResNet):
+            if fuse_dw:
+                raise ValueError("fuse_dw applies to the MobileNetV2 blocks only")
+            return lower_resnet(net, B, bf16, nb=nb, fuse_prep=fuse_prep)
         from .deeplab_xception import lower_xception
         if fuse_dw:
             raise ValueError("fuse_dw applies to the MobileNetV2 blocks only")
@@ -503,6 +525,9 @@ def save(net, path) -> None:
     """Weights + topology attributes as a plain .npz (loadable with allow_pickle=False); either
     backbone (an Xception network is written by deeplab_xception.save_xception)."""
     if not isinstance(net, DeepLab):
+        from .deeplab_resnet import DeepLabResNet, save_resnet
+        if isinstance(net, DeepLabResNet):
+            return save_resnet(net, path)
         from .deeplab_xception import save_xception
         return save_xception(net, path)
     arrs = {}
@@ -519,6 +544,9 @@ def load(path):
     if "net.xattrs" in z:
         from .deeplab_xception import load_xception
         return load_xception(z, path)
+    if "net.rattrs" in z:
+        from .deeplab_resnet import load_resnet
+        return load_resnet(z, path)
 
     def conv(name):
         return conv_from(z, name, path)

@@ -213,7 +213,8 @@ class DeepLabV3(InferenceModel):
     (deeplab/model.py, ``crop_size`` given at export), so the graph itself cannot run them.
 
     Backbones: MobileNetV2 (DeepLabV3, dense or no atrous branches) and Xception-65 (DeepLabV3+:
-    separable ASPP, decoder at output stride 4), the two model-zoo forms (deeplab_xception.py).
+    separable ASPP, decoder at output stride 4), the two model-zoo forms (deeplab_xception.py), and
+    ResNet-v1-50 / 101 "beta" (DeepLabV3, dense atrous ASPP; deeplab_resnet.py).
 
     Weights: GRAPH_PB_PATH may be a frozen TF DeepLab-MobileNetV2 GraphDef (``deeplab.pb``, read by
     deeplab_graphdef.import_deeplab; the file itself is absent, .MISSING_LARGE_BLOBS:1), a
@@ -233,7 +234,8 @@ class DeepLabV3(InferenceModel):
         (bit-identical, measured slower; deeplab_spec.lower). fuse_prep=False runs the padding +
         normalisation as its own launch instead of inside the stem's operand loads (bit-identical).
         backbone: the seeded synthetic network when neither a file nor ``net`` is given —
-        "mobilenet_v2" (deeplab_spec) or "xception_65" (DeepLabV3+, deeplab_xception)."""
+        "mobilenet_v2" (deeplab_spec), "xception_65" (DeepLabV3+, deeplab_xception) or
+        "resnet_v1_50_beta" / "resnet_v1_101_beta" (DeepLabV3, deeplab_resnet)."""
         from . import deeplab_spec
         if precision not in ("fp32", "bf16"):
             raise ValueError("precision must be 'fp32' or 'bf16'")
@@ -244,8 +246,12 @@ class DeepLabV3(InferenceModel):
                     net = build_deeplab_xception()
                 elif backbone == "mobilenet_v2":
                     net = deeplab_spec.build_deeplab()
+                elif backbone in ("resnet_v1_50_beta", "resnet_v1_101_beta"):
+                    from .deeplab_resnet import build_deeplab_resnet
+                    net = build_deeplab_resnet(depth=50 if "50" in backbone else 101)
                 else:
-                    raise ValueError("backbone must be 'mobilenet_v2' or 'xception_65'")
+                    raise ValueError("backbone must be 'mobilenet_v2', 'xception_65', 'resnet_v1_50_beta' or "
+                                     "'resnet_v1_101_beta'")
             else:
                 if not os.path.exists(GRAPH_PB_PATH):
                     raise FileNotFoundError(f"{GRAPH_PB_PATH}: no such file")

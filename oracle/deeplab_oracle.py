@@ -2,9 +2,9 @@
 
 CPU restatement of the DeepLab inference the reference runs through TF ``sess.run``
 (models.py:115-125: ``ImageTensor`` u8 -> ``SemanticPredictions`` int64) for the standard TF
-DeepLab exports over MobileNetV2 (deeplab_spec.py documents the topology) and over Xception-65 with
-the DeepLabV3+ decoder (deeplab_xception.py; ``forward_xception``), on PyTorch-CPU ops with TF's
-semantics written out:
+DeepLab exports over MobileNetV2 (deeplab_spec.py documents the topology), over Xception-65 with
+the DeepLabV3+ decoder (deeplab_xception.py; ``forward_xception``) and over ResNet-v1-beta
+(deeplab_resnet.py; ``forward_resnet``), on PyTorch-CPU ops with TF's semantics written out:
 
 * ``preprocess``  deeplab input_preprocess + mobilenet ``_preprocess_zero_mean_unit_range``: pad to
                   the crop with 127.5 (pad_to_bounding_box), ``f32(2/255) * x - 1`` in f32;
@@ -121,6 +121,8 @@ def forward(net, rgb: np.ndarray, dtype=torch.float64, bf16_storage: bool = Fals
     MobileNetV2, the decoder's for Xception), f32."""
     if hasattr(net, "modules"):
         return forward_xception(net, rgb, dtype, bf16_storage)
+    if hasattr(net, "units"):
+        return forward_resnet(net, rgb, dtype, bf16_storage)
     n = _Num(torch.float32 if bf16_storage else dtype, bf16_storage)
     x = torch.from_numpy(preprocess(rgb, crop_hw(net))).permute(0, 3, 1, 2).to(n.dtype)
     x = n.store(x)
@@ -197,6 +199,44 @@ def forward_xception(net, rgb: np.ndarray, dtype=torch.float64, bf16_storage: bo
         for sp in net.decoder:
             cat = n.store(_conv(n, n.store(_conv(n, cat, sp.dw, groups=cat.shape[1])), sp.pw))
         p = cat
+    logits = _conv(n, p, net.logits)
+    return logits.to(torch.float32)
+
+
+def _maxpool_same(x, k, s):
+    """TF max_pool2d 'SAME' (k > 1): pads with -inf (pad_before = total // 2); 'VALID' for k = 1
+    (resnet_utils.subsample)."""
+    if k == 1:
+        return x[:, :, ::s, ::s]
+    pads = []
+    for n in (x.shape[3], x.shape[2]):
+        out = -(-n // s)
+        tot = max((out - 1) * s + k - n, 0)
+        pads += [tot // 2, tot - tot // 2]
+    return F.max_pool2d(F.pad(x, pads, value=float("-inf")), k, s)
+
+
+def forward_resnet(net, rgb: np.ndarray, dtype=torch.float64, bf16_storage: bool = False) -> torch.Tensor:
+    """DeepLabV3 ResNet-v1-beta (bugcar_image_segmentation_amd/deeplab_resnet.py documents the
+    topology; deeplab/core/resnet_v1_beta.py, slim resnet_utils): root convs (conv2d_same: fixed padding
+    when strided), 3x3 s2 SAME max pool, v1 bottleneck units — out = ReLU(shortcut + conv3(conv2(conv1(x))))
+    with the shortcut a 1x1 conv + BN or the input subsampled by the unit stride — then the dense ASPP
+    and logits at the backbone resolution."""
+    n = _Num(torch.float32 if bf16_storage else dtype, bf16_storage)
+    x = torch.from_numpy(preprocess(rgb, crop_hw(net))).permute(0, 3, 1, 2).to(n.dtype)
+    x = n.store(x)
+    for c in net.root:
+        x = n.store(_conv(n, x, c, fixed=True))
+    x = _maxpool_same(x, 3, 2)
+    for u in net.units:
+        if u.shortcut is not None:
+            sc = n.store(_conv(n, x, u.shortcut, fixed=True))
+        else:
+            sc = _maxpool_same(x, 1, u.stride)
+        r = n.store(_conv(n, x, u.conv1))
+        r = n.store(_conv(n, r, u.conv2, fixed=True))
+        x = n.store(F.relu(_conv(n, r, u.conv3) + sc))
+    p = _aspp(n, x, net)
     logits = _conv(n, p, net.logits)
     return logits.to(torch.float32)
 
