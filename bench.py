@@ -875,6 +875,9 @@ def main():
             log("deeplab xception sub-record")
             res["deeplab_xception"] = bench_deeplab.record(dev, 32, max(5, a.steps // 2), 3, "bf16",
                                                            backbone="xception_65")
+            log("deeplab resnet sub-record")
+            res["deeplab_resnet"] = bench_deeplab.record(dev, 16, max(5, a.steps // 2), 3, "bf16",
+                                                         backbone="resnet_v1_101_beta")
         if not a.no_cpu_baseline and world == 1:   # the CPU baseline is an N = 1 record (rank 0)
             res["cpu_baseline"] = cpu_baseline(blocks, bev, grid, H, W, a.cpu_baseline_seconds)
         print(json.dumps(res), flush=True)

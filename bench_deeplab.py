@@ -46,7 +46,7 @@ def parse():
     p.add_argument("--precision", default="bf16", choices=["bf16", "fp32"])
     p.add_argument("--cpu-baseline-seconds", type=float, default=12.0)
     p.add_argument("--no-cpu-baseline", action="store_true")
-    p.add_argument("--backbone", default="mobilenet_v2", choices=["mobilenet_v2", "xception_65"])
+    p.add_argument("--backbone", default="mobilenet_v2", choices=["mobilenet_v2", "xception_65", "resnet_v1_101_beta"])
     return p.parse_args()
 
 
@@ -74,6 +74,8 @@ def pmc_traffic(tag, batch, backbone="mobilenet_v2"):
     """HBM bytes per launch of op tag `tag` from the committed PMC summary
     (profiles/dl_pmc_traffic.json, written by scripts/dl_pmc_summary.py from rocprofv3 FETCH_SIZE /
     WRITE_SIZE passes of this script at the same batch), or None."""
+    if backbone not in ("mobilenet_v2", "xception_65"):
+        return None
     p = os.path.join(ROOT, "profiles", "dl_pmc_traffic_xception.json" if backbone == "xception_65" else "dl_pmc_traffic.json")
     try:
         with open(p) as f:
@@ -87,7 +89,8 @@ def pmc_traffic(tag, batch, backbone="mobilenet_v2"):
 
 
 WORKLOAD = {"mobilenet_v2": "DeepLabV3 MobileNetV2 OS8 + ASPP (image pooling + 1x1)",
-            "xception_65": "DeepLabV3+ Xception-65 OS16 + separable ASPP 6/12/18 + decoder OS4"}
+            "xception_65": "DeepLabV3+ Xception-65 OS16 + separable ASPP 6/12/18 + decoder OS4",
+            "resnet_v1_101_beta": "DeepLabV3 ResNet-v1-101-beta OS16 + dense ASPP 6/12/18"}
 
 
 def measure(dev, B, steps, warmup, precision, world=1, rank=0, backbone="mobilenet_v2"):
@@ -154,7 +157,7 @@ def roofline(model, per, fwd_us, B, precision, backbone="mobilenet_v2"):
     achieved = k["bytes"] / (k["us"] * 1e-6) / 1e9
     peak_tf = MFMA_PEAK_TFLOPS[precision]
     tflops = k["flops"] / (k["us"] * 1e-6) / 1e12
-    mfma = backbone == "xception_65"
+    mfma = backbone != "mobilenet_v2"
     bound = ({"bound": "mfma", "achieved": round(tflops, 1), "peak": peak_tf, "unit": "TFLOP/s",
               "frac": round(tflops / peak_tf, 4), "hbm_achieved_gbs": round(achieved, 1),
               "hbm_frac": round(achieved / HBM_PEAK_GBS, 4)} if mfma else

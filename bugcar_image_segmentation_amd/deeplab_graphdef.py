@@ -24,6 +24,12 @@ folding of graphdef.py, and returns the network the engine runs:
 * the projection's input channels are permuted from the graph's concat order to the engine's
   [image pooling, 1x1, atrous...] order.
 
+The other two backbone families are told apart by the root: a second full 3x3 convolution is the
+Xception-65 root (``_import_xception``: modules of separable convs, separable ASPP, decoder), a third one
+the ResNet-v1-beta root (``_import_resnet``: a 3x3 s2 ``MaxPool``, then bottleneck units found by data
+flow — 1x1 + ReLU, 3x3 + ReLU, linear 1x1 meeting the shortcut at an ``Add`` + ``Relu`` — and the dense
+ASPP head shared with MobileNetV2, ``_dense_aspp``).
+
 The crop size IS read from the graph: deeplab/input_preprocess.py pads every image to
 ``image_size + max(crop - image_size, 0)`` per axis, which a frozen export holds as
 ``Maximum(Sub(Const crop, StridedSlice(Shape(image), [axis])), 0)`` — the two ``Const`` operands give
@@ -418,6 +424,160 @@ def _import_xception(g: Graph, convs: list, closures: list, crop_h: int, crop_w:
                              crop_w=crop_w if crop_w != crop_h else 0)
 
 
+def _dense_aspp(g: Graph, convs: list, rest: list, backbone: str, exit_of: dict, conv_at, need_act):
+    """The DeepLabV3 head over `backbone` with dense ASPP branches (MobileNetV2, ResNet): convolutions
+    `rest` classified by what feeds them — a spatial Mean / AvgPool of the backbone: image pooling; the
+    backbone itself: the 1x1 branch or a 3x3 atrous branch; the branches' ConcatV2: the projection; the
+    projection's output: the logits — and the projection's input channels permuted from the graph's
+    concat order to the engine's [pool, 1x1, atrous...] -> (pool, aspp0, atrous convs, project, logits)."""
+    pool = aspp0 = project = logits = None
+    pool_i = aspp0_i = proj_i = None
+    atrous = []            # (index, conv)
+    concat = None
+    for j in rest:
+        c = convs[j]
+        _expect(not c.depthwise, f"{c.node.name}: depthwise convolution in the ASPP head (separable ASPP is "
+                                 "the Xception variant; not supported)")
+        src = g.node(c.src(g))
+        if src.op in ("Mean", "AvgPool") and g.producer_chain(src.inputs[0], PASS).name == backbone:
+            if src.op == "Mean":
+                ax = sorted(int(v) % 4 for v in np.atleast_1d(g.const(src.inputs[1])))
+                _expect(ax == [1, 2], f"{src.name}: mean over axes {ax}, expected the spatial axes")
+            _expect(pool is None and c.k == 1, f"{c.node.name}: second / non-1x1 image-pooling convolution")
+            need_act(j, D.ACT_RELU, "image pooling")
+            pool, pool_i = conv_at(j), j
+        elif src.name == backbone:
+            need_act(j, D.ACT_RELU, "ASPP branch")
+            if c.k == 1:
+                _expect(aspp0 is None, f"{c.node.name}: second 1x1 ASPP branch")
+                aspp0, aspp0_i = conv_at(j), j
+            else:
+                _expect(c.k == 3, f"{c.node.name}: ASPP branch kernel {c.k}")
+                atrous.append((j, conv_at(j)))
+        elif src.op == "ConcatV2":
+            _expect(project is None and c.k == 1, f"{c.node.name}: second / non-1x1 concat projection")
+            need_act(j, D.ACT_RELU, "concat projection")
+            project, proj_i = conv_at(j), j
+            concat = src
+        elif proj_i is not None and c.src(g) == exit_of[id(convs[proj_i])]:
+            _expect(logits is None and c.k == 1, f"{c.node.name}: second / non-1x1 logits convolution")
+            need_act(j, D.ACT_NONE, "logits")
+            logits = conv_at(j)
+        else:
+            raise GraphImportError(f"{c.node.name}: convolution fed by {src.name} ({src.op}) has no DeepLab role")
+    _expect(pool is not None and aspp0 is not None and project is not None and logits is not None,
+            "missing ASPP parts: " + ", ".join(n for n, v in (("image pooling", pool), ("1x1 branch", aspp0),
+                                                               ("projection", project), ("logits", logits)) if v is None))
+    # concat order -> engine order [pool, aspp0, atrous...]
+    by_exit = {exit_of[id(convs[j])]: j for j in [pool_i, aspp0_i] + [a for a, _ in atrous]}
+    perm, atr_sorted = _aspp_concat_perm(g, concat, by_exit, pool_i, aspp0_i,
+                                         {j: convs[j].cout for j in by_exit.values()}, project.w.shape[1])
+    project.w = np.ascontiguousarray(project.w[:, perm])
+    atrous_convs = [dict(atrous)[j] for j in atr_sorted]
+    Dd = aspp0.cout
+    _expect(pool.cout == Dd and all(a.cout == Dd for a in atrous_convs) and project.cout == Dd,
+            "ASPP branches and projection differ in depth")
+    return pool, aspp0, atrous_convs, project, logits
+
+
+def _import_resnet(g: Graph, convs: list, closures: list, crop_h: int, crop_w: int):
+    """The DeepLabV3 ResNet-v1-beta export (deeplab_resnet.py documents the topology) by data flow:
+    three root convs (the first strided with fixed_padding), a 3x3 s2 ``MaxPool``, then bottleneck units
+    — a 1x1 + ReLU reading the unit input, a 3x3 + ReLU after it, a linear 1x1 whose output meets the
+    shortcut (the unit input, its 1x1 ``MaxPool`` subsample, or a linear 1x1 conv of it) at an ``Add``
+    followed by ``Relu`` — until no unit starts at the current tensor; then the dense ASPP head."""
+    from . import deeplab_resnet as R
+    exit_of = {id(c): ex for c, (_, _, ex) in zip(convs, closures)}
+    ex = lambda i: exit_of[id(convs[i])]  # noqa: E731
+    act = lambda i: closures[i][1]  # noqa: E731
+
+    def conv_at(i):
+        f, a, _ = closures[i]
+        return _make(convs[i], f, a)
+
+    def need_act(i, want, role):
+        _expect(act(i) == want, f"{role} ({convs[i].node.name}): expected {_ACT_NAME[want]} after it, "
+                                f"graph has {_ACT_NAME[act(i)]}")
+
+    def strided_ok(i):
+        c = convs[i]
+        if c.stride > 1 and c.k > 1:
+            _expect(_fixed(c), f"{c.node.name}: strided convolution without fixed_padding")
+        else:
+            _expect(c.explicit is None, f"{c.node.name}: explicit padding on a stride-1 convolution")
+
+    n = len(convs)
+    for i in range(3):
+        strided_ok(i)
+        need_act(i, D.ACT_RELU, "root conv")
+        _expect(not convs[i].depthwise and convs[i].k == 3, f"{convs[i].node.name}: root conv")
+        if i:
+            _expect(convs[i].src(g) == ex(i - 1) and convs[i].cin == convs[i - 1].cout, f"{convs[i].node.name}: root chain")
+    pools = [m for m in g.consumers[ex(2)] if m.op == "MaxPool"]
+    _expect(len(pools) == 1, f"{convs[2].node.name}: no max pool after the root")
+    mp = pools[0]
+    _expect([int(v) for v in mp.attr.get("ksize")] == [1, 3, 3, 1] and [int(v) for v in mp.attr.get("strides")] == [1, 2, 2, 1]
+            and _s(mp.attr.get("padding", b"")) == "SAME", f"{mp.name}: expected a 3x3 stride-2 SAME max pool")
+    by_src: dict = {}
+    for j in range(3, n):
+        by_src.setdefault(convs[j].src(g), []).append(j)
+    cur, cur_c = mp.name, convs[2].cout
+    units, used = [], set(range(3))
+    os_ = convs[0].stride * 2
+    while True:
+        found = None
+        for j1 in by_src.get(cur, []):
+            c1 = convs[j1]
+            if c1.depthwise or c1.k != 1 or act(j1) != D.ACT_RELU:
+                continue
+            n2 = by_src.get(ex(j1), [])
+            if len(n2) != 1 or convs[n2[0]].depthwise or convs[n2[0]].k != 3 or act(n2[0]) != D.ACT_RELU:
+                continue
+            n3 = by_src.get(ex(n2[0]), [])
+            if len(n3) != 1 or convs[n3[0]].depthwise or convs[n3[0]].k != 1 or act(n3[0]) != D.ACT_NONE:
+                continue
+            adds = [a for a in g.consumers[ex(n3[0])] if a.op in ("Add", "AddV2")]
+            if len(adds) == 1:
+                found = (j1, n2[0], n3[0], adds[0])
+                break
+        if found is None:
+            break
+        j1, j2, j3, add = found
+        others = [g.producer_chain(t, PASS) for t in add.inputs if g.producer_chain(t, PASS).name != ex(j3)]
+        _expect(len(others) == 1, f"{add.name}: not a two-way residual add")
+        o, stride = others[0], convs[j2].stride
+        strided_ok(j2)
+        _expect(convs[j1].cin == cur_c and convs[j2].cin == convs[j1].cout and convs[j3].cin == convs[j2].cout,
+                f"{convs[j1].node.name}: bottleneck channel counts")
+        sc = None
+        if o.name == cur:
+            _expect(stride == 1 and convs[j3].cout == cur_c, f"{add.name}: identity shortcut over a shape change")
+        elif o.op == "MaxPool" and g.producer_chain(o.inputs[0], PASS).name == cur:
+            _expect([int(v) for v in o.attr.get("ksize")] == [1, 1, 1, 1] and
+                    [int(v) for v in o.attr.get("strides")] == [1, stride, stride, 1] and convs[j3].cout == cur_c,
+                    f"{o.name}: shortcut subsample does not match the unit stride")
+        else:
+            js = [j for j in by_src.get(cur, []) if ex(j) == o.name]
+            _expect(len(js) == 1 and convs[js[0]].k == 1 and not convs[js[0]].depthwise and convs[js[0]].stride == stride
+                    and convs[js[0]].cout == convs[j3].cout, f"{add.name}: shortcut is not a 1x1 conv of the unit input")
+            need_act(js[0], D.ACT_NONE, "shortcut")
+            sc = conv_at(js[0])
+            used.add(js[0])
+        relus = [r for r in g.consumers[add.name] if r.op == "Relu"]
+        _expect(len(relus) == 1, f"{add.name}: no ReLU after the residual add")
+        units.append(R.Unit(conv_at(j1), conv_at(j2), conv_at(j3), sc, stride))
+        used.update((j1, j2, j3))
+        cur, cur_c = relus[0].name, convs[j3].cout
+        os_ *= stride
+    _expect(units, "no bottleneck units after the root")
+    rest = [j for j in range(n) if j not in used]
+    pool, aspp0, atrous_convs, project, logits = _dense_aspp(g, convs, rest, cur, exit_of, conv_at, need_act)
+    return R.DeepLabResNet([conv_at(0), conv_at(1), conv_at(2)], units, pool, aspp0, atrous_convs, project, logits,
+                           logits.cout, os_, crop_h,
+                           meta=dict(source="graphdef", backbone="resnet_v1_beta", atrous_rates=tuple(a.dil for a in atrous_convs)),
+                           crop_w=crop_w if crop_w != crop_h else 0)
+
+
 def _relu_of(g: Graph, name: str):
     """If `name` is (through identity-like ops) a Relu, the tensor it rectifies; else None."""
     n = g.producer_chain(name, PASS)
@@ -425,7 +585,9 @@ def _relu_of(g: Graph, name: str):
 
 
 def import_deeplab(data: bytes, crop=None, default_crop: int = D.CROP) -> D.DeepLab:
-    """Frozen DeepLab-MobileNetV2 GraphDef bytes -> deeplab_spec.DeepLab (weights + topology).
+    """Frozen DeepLab GraphDef bytes -> the engine's network (weights + topology): deeplab_spec.DeepLab
+    (MobileNetV2), deeplab_xception.DeepLabXception or deeplab_resnet.DeepLabResNet, told apart by the
+    root's convolutions.
     crop: None reads the export's crop from the graph (read_crop; ``default_crop`` when the graph
     holds none), an int or (height, width) overrides it."""
     g = Graph(parse_graphdef(data))
@@ -438,8 +600,12 @@ def import_deeplab(data: bytes, crop=None, default_crop: int = D.CROP) -> D.Deep
     _expect(not st.depthwise and st.cin == 3 and st.k == 3, f"{st.node.name}: the first convolution is not a "
                                                             "3x3 stem over the RGB input")
     if not convs[1].depthwise and convs[1].k == 3:
-        # a second full 3x3 convolution: the Xception root (MobileNetV2 goes on with a depthwise one)
-        return _import_xception(g, convs, [_affine_act(g, c, act_ends=True) for c in convs], crop_h, crop_w)
+        # a second full 3x3 convolution: the Xception root (MobileNetV2 goes on with a depthwise one); a third
+        # one: the ResNet-v1-beta root (Xception goes on with a depthwise one)
+        closures = [_affine_act(g, c, act_ends=True) for c in convs]
+        if len(convs) > 2 and not convs[2].depthwise and convs[2].k == 3:
+            return _import_resnet(g, convs, closures, crop_h, crop_w)
+        return _import_xception(g, convs, closures, crop_h, crop_w)
     closures = [_affine_act(g, c) for c in convs]
     exit_of = {id(c): ex for c, (_, _, ex) in zip(convs, closures)}
 
@@ -497,54 +663,8 @@ def import_deeplab(data: bytes, crop=None, default_crop: int = D.CROP) -> D.Deep
         i = pj_i + 1
     _expect(blocks, "no inverted residual blocks after the stem")
     backbone = cur
-    # ASPP
-    pool = aspp0 = project = logits = None
-    pool_i = aspp0_i = proj_i = None
-    atrous = []            # (index, conv)
-    rest = list(range(i, len(convs)))
-    for j in rest:
-        c = convs[j]
-        _expect(not c.depthwise, f"{c.node.name}: depthwise convolution in the ASPP head (separable ASPP is "
-                                 "the Xception variant; not supported)")
-        src = g.node(c.src(g))
-        if src.op in ("Mean", "AvgPool") and g.producer_chain(src.inputs[0], PASS).name == backbone:
-            if src.op == "Mean":
-                ax = sorted(int(v) % 4 for v in np.atleast_1d(g.const(src.inputs[1])))
-                _expect(ax == [1, 2], f"{src.name}: mean over axes {ax}, expected the spatial axes")
-            _expect(pool is None and c.k == 1, f"{c.node.name}: second / non-1x1 image-pooling convolution")
-            need_act(j, D.ACT_RELU, "image pooling")
-            pool, pool_i = conv_at(j), j
-        elif src.name == backbone:
-            need_act(j, D.ACT_RELU, "ASPP branch")
-            if c.k == 1:
-                _expect(aspp0 is None, f"{c.node.name}: second 1x1 ASPP branch")
-                aspp0, aspp0_i = conv_at(j), j
-            else:
-                _expect(c.k == 3, f"{c.node.name}: ASPP branch kernel {c.k}")
-                atrous.append((j, conv_at(j)))
-        elif src.op == "ConcatV2":
-            _expect(project is None and c.k == 1, f"{c.node.name}: second / non-1x1 concat projection")
-            need_act(j, D.ACT_RELU, "concat projection")
-            project, proj_i = conv_at(j), j
-            concat = src
-        elif proj_i is not None and c.src(g) == exit_of[id(convs[proj_i])]:
-            _expect(logits is None and c.k == 1, f"{c.node.name}: second / non-1x1 logits convolution")
-            need_act(j, D.ACT_NONE, "logits")
-            logits = conv_at(j)
-        else:
-            raise GraphImportError(f"{c.node.name}: convolution fed by {src.name} ({src.op}) has no DeepLab role")
-    _expect(pool is not None and aspp0 is not None and project is not None and logits is not None,
-            "missing ASPP parts: " + ", ".join(n for n, v in (("image pooling", pool), ("1x1 branch", aspp0),
-                                                               ("projection", project), ("logits", logits)) if v is None))
-    # concat order -> engine order [pool, aspp0, atrous...]
-    by_exit = {exit_of[id(convs[j])]: j for j in [pool_i, aspp0_i] + [a for a, _ in atrous]}
-    perm, atr_sorted = _aspp_concat_perm(g, concat, by_exit, pool_i, aspp0_i,
-                                         {j: convs[j].cout for j in by_exit.values()}, project.w.shape[1])
-    project.w = np.ascontiguousarray(project.w[:, perm])
-    atrous_convs = [dict(atrous)[j] for j in atr_sorted]
-    Dd = aspp0.cout
-    _expect(pool.cout == Dd and all(a.cout == Dd for a in atrous_convs) and project.cout == Dd,
-            "ASPP branches and projection differ in depth")
+    pool, aspp0, atrous_convs, project, logits = _dense_aspp(g, convs, list(range(i, len(convs))), backbone, exit_of,
+                                                             conv_at, need_act)
     # output stride: product of the strides on the way to the backbone output
     os_ = stem.stride
     for b in blocks:
@@ -568,5 +688,6 @@ if __name__ == "__main__":
         sys.exit(2)
     with open(sys.argv[1], "rb") as f:
         net = graphdef_to_npz(f.read(), sys.argv[2])
-    print(f"{sys.argv[2]}: {len(net.blocks)} blocks, {net.num_classes} classes, output stride {net.output_stride}, "
-          f"crop {D.crop_hw(net)}")
+    body = net.blocks if hasattr(net, "blocks") else net.modules if hasattr(net, "modules") else net.units
+    print(f"{sys.argv[2]}: {type(net).__name__}, {len(body)} blocks, {net.num_classes} classes, output stride "
+          f"{net.output_stride}, crop {D.crop_hw(net)}")

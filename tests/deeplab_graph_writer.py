@@ -17,7 +17,12 @@ refine_by_decoder build it: strided layers as ``Pad`` (fixed_padding) + VALID co
 skips as ``AddV2`` (1x1 shortcut conv or identity), separable ASPP branches, and the decoder's
 ``ResizeBilinear`` + ``ConcatV2`` with the 1x1-projected low-level features.
 
-Both take ``ImageTensor`` (B, H, W, 3) u8 and end in ``SemanticPredictions`` (int64, (B, H, W)),
+A ResNet network (deeplab_resnet.DeepLabResNet) is written the way resnet_v1_beta + slim's
+bottleneck build it: the three root convs (the strided one as ``Pad`` + VALID), a 3x3 s2 SAME
+``MaxPool``, per unit the shortcut first (a 1x1 conv + BN, a 1x1 ``MaxPool`` subsample, or the input
+itself), then 1x1 / 3x3 / 1x1 and ``Relu(AddV2(shortcut, residual))``, and the dense ASPP.
+
+All take ``ImageTensor`` (B, H, W, 3) u8 and end in ``SemanticPredictions`` (int64, (B, H, W)),
 the reference's tensor names without the ``import/`` scope (models.py:102-103,115-125), with the
 export's preprocessing and bilinear resize (align_corners) + argmax written as graph ops. The pad is
 the export's dynamic form (deeplab/input_preprocess.py): per axis ``size + Maximum(Sub(crop, size), 0)``
@@ -144,6 +149,28 @@ class DeepLabWriter:
                 x = g.node("AddV2", [x, inp], T=F32)
         return x, n, low
 
+    def resnet(self, x, n):
+        """Root convs, max pool and bottleneck units -> (backbone output, size)."""
+        g, net = self.g, self.net
+        for c in net.root:
+            x, n = self.conv(x, c, n, fixed=True)
+        x = g.node("MaxPool", [x], T=F32, ksize=[1, 3, 3, 1], strides=[1, 2, 2, 1], padding="SAME", data_format="NHWC")
+        n = tuple(-(-v // 2) for v in n)
+        for u in net.units:
+            inp, n_in = x, n
+            if u.shortcut is not None:
+                sc, _ = self.conv(inp, u.shortcut, n_in)
+            elif u.stride > 1:
+                sc = g.node("MaxPool", [inp], T=F32, ksize=[1, 1, 1, 1], strides=[1, u.stride, u.stride, 1],
+                            padding="SAME", data_format="NHWC")
+            else:
+                sc = inp
+            r, _ = self.conv(inp, u.conv1, n_in)
+            r, n = self.conv(r, u.conv2, n_in, fixed=True)
+            r, _ = self.conv(r, u.conv3, n)
+            x = g.node("Relu", [g.node("AddV2", [sc, r], T=F32)], T=F32)
+        return x, n
+
     def build(self) -> bytes:
         g, net = self.g, self.net
         B, H, W = self.B, self.H, self.W
@@ -162,6 +189,8 @@ class DeepLabWriter:
         xc = hasattr(net, "modules")
         if xc:
             x, n, low = self.xception(x, C)
+        elif hasattr(net, "units"):
+            x, n = self.resnet(x, C)
         else:
             x, n = self.conv(x, net.stem, C)
             for blk in net.blocks:

@@ -347,3 +347,20 @@ def test_resnet_weight_file_round_trip(gpu, tmp_path):
     m = DeepLabV3(str(p), precision="fp32")
     assert isinstance(m.net, R.DeepLabResNet)
     assert np.array_equal(a, m.predict(x))
+
+
+def test_resnet_from_frozen_graphdef(gpu, tmp_path):
+    """DeepLabV3(<frozen ResNet-v1-beta DeepLabV3 GraphDef>): the imported network on the GPU against
+    the NumPy GraphDef interpreter's logits and the oracle."""
+    from deeplab_graph_writer import write_deeplab_graph
+    from oracle import tf_graph
+    net = R.build_deeplab_resnet(depth=50, width=0.25, units=(1, 2, 2, 2), crop=97, atrous_rates=(2, 4))
+    H, W = 90, 97
+    pb = tmp_path / "deeplab.pb"
+    pb.write_bytes(write_deeplab_graph(net, "slim", H, W))
+    model = DeepLabV3(str(pb), precision="fp32")
+    assert isinstance(model.net, R.DeepLabResNet) and S.crop_hw(model.net) == (97, 97)
+    x = _frames(1, H, W, 27)
+    _check_fp32(model, model.net, x, torch.float64)
+    lg = np.transpose(tf_graph.run(pb.read_bytes(), {"ImageTensor": x}, "logits"), (0, 3, 1, 2))
+    assert np.abs(_gpu_logits(model) - lg).max() < LOGIT_TOL
