@@ -43,6 +43,7 @@ struct DlConvArgs {
     // the (B, Hin, Win, 8) operand is formed on load (dl_prep_kernel's padding and normalisation)
     const uint8_t *rgb;
     int img_h, img_w;
+    const void *zero;    // >= 16 zero bytes (after the weight blob): the implicit-GEMM conv's padding taps
 };
 
 struct DlDwArgs {

@@ -340,7 +340,7 @@ __global__ void __launch_bounds__(256) dl_conv_kernel(const DlConvArgs a) {
 // same order and with the same epilogue as dl_conv_kernel, so the results are bit-identical.
 constexpr int GM_TM = 256, GM_TN = 64, GM_KT = 64, GM_RS = GM_KT + 16;   // LDS row: 80 elements (40 dwords)
 
-template <bool OUTF32>
+template <bool OUTF32, bool RPF>
 __global__ void __launch_bounds__(256, 2) dl_gemm_kernel(const DlConvArgs a) {
     __shared__ __attribute__((aligned(16))) __bf16 sm[(GM_TN + GM_TM) * GM_RS];
     __bf16 *sA = sm, *sB = sm + GM_TN * GM_RS;
@@ -379,6 +379,20 @@ __global__ void __launch_bounds__(256, 2) dl_gemm_kernel(const DlConvArgs a) {
 #pragma unroll
         for (int r = 0; r < 4; ++r) acc[j][r] = (f32x4){0.f, 0.f, 0.f, 0.f};
     const int nst = (K + GM_KT - 1) / GM_KT;
+    const int c8 = (lane & 7) * 8;
+    const bool cok = n0 + c8 < a.cout;
+    uint4 rres[2][4];   // the epilogue's residual, loaded ahead of the k-loop (as dl_gemm128_kernel)
+    if constexpr (RPF) {
+#pragma unroll
+        for (int h = 0; h < 2; ++h)
+#pragma unroll
+            for (int it = 0; it < 4; ++it) {
+                const int p = p0 + wave * 64 + h * 32 + it * 8 + (lane >> 3);
+                rres[h][it] = cok && p < a.M ? *reinterpret_cast<const uint4 *>(reinterpret_cast<const __bf16 *>(a.res) +
+                                                                                (size_t)p * a.res_cs + n0 + c8)
+                                             : make_uint4(0, 0, 0, 0);
+            }
+    }
     fetch(0);
     for (int st = 0; st < nst; ++st) {
         __syncthreads();                          // every wave is done reading the previous stage
@@ -411,8 +425,6 @@ __global__ void __launch_bounds__(256, 2) dl_gemm_kernel(const DlConvArgs a) {
     // epilogue (dl_conv_kernel's, 32 pixels at a time through the wave's share of the staging LDS)
     __syncthreads();
     float *st = reinterpret_cast<float *>(sm) + wave * 32 * DL_STG_RS;
-    const int c8 = (lane & 7) * 8;
-    const bool cok = n0 + c8 < a.cout;
 #pragma unroll
     for (int h = 0; h < 2; ++h) {
         if (h) wave_lds_sync();
@@ -440,10 +452,12 @@ __global__ void __launch_bounds__(256, 2) dl_gemm_kernel(const DlConvArgs a) {
             float4 v0 = *reinterpret_cast<const float4 *>(st + pl * DL_STG_RS + c8);
             float4 v1 = *reinterpret_cast<const float4 *>(st + pl * DL_STG_RS + c8 + 4);
             const int n = n0 + c8;
-            if (a.res) {
-                const __bf16 *rp = reinterpret_cast<const __bf16 *>(a.res) + (size_t)p * a.res_cs + n;
-                v0 = add4(v0, ld4(rp));
-                v1 = add4(v1, ld4(rp + 4));
+            if (RPF) {
+                const uint4 u = rres[h][it];
+                v0 = add4(v0, make_float4(__uint_as_float(u.x << 16), __uint_as_float(u.x & 0xffff0000u),
+                                          __uint_as_float(u.y << 16), __uint_as_float(u.y & 0xffff0000u)));
+                v1 = add4(v1, make_float4(__uint_as_float(u.z << 16), __uint_as_float(u.z & 0xffff0000u),
+                                          __uint_as_float(u.w << 16), __uint_as_float(u.w & 0xffff0000u)));
             }
             if (a.act == 3) {              // ReLU after the residual add (ResNet units)
                 v0 = make_float4(fmaxf(v0.x, 0.f), fmaxf(v0.y, 0.f), fmaxf(v0.z, 0.f), fmaxf(v0.w, 0.f));
@@ -504,40 +518,86 @@ __device__ __forceinline__ void lds_wait8(u32x4 &a0, u32x4 &a1, u32x4 &a2, u32x4
 // matrix pipe. Reading both k-steps' fragments ahead of the first step's MFMAs (opaque asm reads with
 // a counted lgkmcnt) gave wrong results: the register allocator copied a pending read's destination
 
-template <bool OUTF32>
+//
+// CONV = true: the same tile as an implicit-GEMM k x k convolution (ResNet's dense 3x3s, strided or
+// atrous, and the ASPP atrous branches): K = taps * cinP with cinP = CS a multiple of 64, so each
+// 64-channel k-stage lies inside one tap (ky, kx) and its pixel rows read the input pixel
+// (y * stride - pad_t + ky * dil, x * stride - pad_l + kx * dil) — no im2col buffer. Taps outside the
+// image read a 16-B zero chunk placed after the weight blob (a.zero). The k order is the packing's
+// (tap-major, 32-channel steps), the order dl_conv_kernel walks, through the same MFMA: bit-identical.
+// s_waitcnt vmcnt(N): all but the N most recent vector-memory loads of this wave have landed
+template <int N> __device__ __forceinline__ void vm_wait_stage();
+template <> __device__ __forceinline__ void vm_wait_stage<8>() { asm volatile("s_waitcnt vmcnt(8)" ::: "memory"); }
+template <> __device__ __forceinline__ void vm_wait_stage<10>() { asm volatile("s_waitcnt vmcnt(10)" ::: "memory"); }
+
+template <bool OUTF32, bool CONV, bool RPF, int TPX = G2_T>
 __global__ void __launch_bounds__(256, 2) dl_gemm128_kernel(const DlConvArgs a) {
+    // TPX = pixels per tile: 128 (the 128 x 128 tile, waves 2 x 2) or 256 (256 pixels x 64 channels,
+    // waves 4 x 1: 64-channel outputs, ResNet's root and block-1 3x3s); each wave's 64 x 64 is the same
+    constexpr int TN = G2_T * G2_T / TPX, WM = TPX / 64, NA = TN / 32, NBL = TPX / 32;   // glds per wave: NA + NBL
     // two LDS objects, one per buffer, and the k-loop unrolled by two so each buffer's role is static:
     // the compiler then sees that a stage's ds_reads cannot alias the glds filling the other buffer
     // and does not drain the prefetch (vmcnt(0)) ahead of them
-    __shared__ __attribute__((aligned(16))) __bf16 sm0[2 * G2_T * G2_KT];   // [A | B][128][64]: 32 KB
-    __shared__ __attribute__((aligned(16))) __bf16 sm1[2 * G2_T * G2_KT];
+    __shared__ __attribute__((aligned(16))) __bf16 sm0[(TN + TPX) * G2_KT];   // [A | B][rows][64]: 32 / 40 KB
+    __shared__ __attribute__((aligned(16))) __bf16 sm1[(TN + TPX) * G2_KT];
     const int tid = threadIdx.x, lane = tid & 63, col = lane & 15, kq = lane >> 4, wave = tid >> 6;
-    const int wm = wave & 1, wn = wave >> 1;
-    const int ntn = (a.NP + G2_T - 1) / G2_T;
+    const int wm = wave % WM, wn = wave / WM;
+    const int ntn = (a.NP + TN - 1) / TN;
     const int bid = xcd_block(blockIdx.x, gridDim.x);
-    const int n0 = (bid % ntn) * G2_T, p0 = (bid / ntn) * G2_T;
-    const int K = a.cinP;
+    const int n0 = (bid % ntn) * TN, p0 = (bid / ntn) * TPX;
     const __bf16 *wg = reinterpret_cast<const __bf16 *>(a.w), *xg = reinterpret_cast<const __bf16 *>(a.in);
-    // this lane's glds sources: instruction i fills LDS rows wave * 32 + i * 8 + (lane >> 3), slot lane & 7
-    const __bf16 *sa[4], *sb[4];
-    int kc[4];
+    // this lane's glds sources: A instruction i fills LDS rows wave * TN / 4 + i * 8 + (lane >> 3), B
+    // instruction i rows wave * TPX / 4 + i * 8 + (lane >> 3); slot lane & 7
+    const int K = CONV ? a.taps * a.cinP : a.cinP;
+    const __bf16 *sa[NA], *sb[NBL];
+    int ka[NA], kb[NBL], y0[NBL], x0[NBL];
 #pragma unroll
-    for (int i = 0; i < 4; ++i) {
-        const int r = wave * 32 + i * 8 + (lane >> 3);
-        kc[i] = ((lane & 7) ^ ((r >> 1) & 7)) * 8;
+    for (int i = 0; i < NA; ++i) {
+        const int r = wave * (TN / 4) + i * 8 + (lane >> 3);
+        ka[i] = ((lane & 7) ^ ((r >> 1) & 7)) * 8;
         sa[i] = wg + (size_t)min(n0 + r, a.NP - 1) * K;
-        sb[i] = xg + (size_t)min(p0 + r, a.M - 1) * a.CS;
+    }
+#pragma unroll
+    for (int i = 0; i < NBL; ++i) {
+        const int r = wave * (TPX / 4) + i * 8 + (lane >> 3);
+        kb[i] = ((lane & 7) ^ ((r >> 1) & 7)) * 8;
+        const int p = min(p0 + r, a.M - 1);
+        if constexpr (CONV) {   // this row's output pixel -> its top-left tap in the input image
+            const int b = (int)fdiv((uint32_t)p, a.mHW, a.sHW), q = p - b * a.Hout * a.Wout;
+            const int y = (int)fdiv((uint32_t)q, a.mW, a.sW), x = q - y * a.Wout;
+            y0[i] = y * a.stride - a.pad_t;
+            x0[i] = x * a.stride - a.pad_l;
+            sb[i] = xg + (size_t)b * a.Hin * a.Win * a.CS + kb[i];
+        } else {
+            sb[i] = xg + (size_t)p * a.CS;
+        }
     }
     auto stage = [&](int st, __bf16 *buf) {
         const int k0 = st * G2_KT;
-        __bf16 *bA = buf + wave * 32 * G2_KT, *bB = bA + G2_T * G2_KT;
+        __bf16 *bA = buf + wave * (TN / 4) * G2_KT, *bB = buf + TN * G2_KT + wave * (TPX / 4) * G2_KT;
 #pragma unroll
-        for (int i = 0; i < 4; ++i) {
-            const int k = k0 + kc[i];
+        for (int i = 0; i < NA; ++i) {
+            const int k = k0 + ka[i];
             glds16(sa[i] + (k < K ? k : 0), bA + i * 8 * G2_KT);
-            // channels past the stored CS (K padded up to the k-stage) read a zero chunk: the weight
-            // row 0's own padding columns k >= CS >= cin, so a non-finite activation never meets them
-            glds16(k < a.CS ? sb[i] + k : wg + k, bB + i * 8 * G2_KT);
+        }
+        if constexpr (CONV) {
+            const int tap = k0 / a.cinP, c0 = k0 - tap * a.cinP;   // uniform
+            const int ky = tap / a.kw, dy = ky * a.dil, dx = (tap - ky * a.kw) * a.dil;
+#pragma unroll
+            for (int i = 0; i < NBL; ++i) {
+                const int iy = y0[i] + dy, ix = x0[i] + dx;
+                const bool in = (unsigned)iy < (unsigned)a.Hin && (unsigned)ix < (unsigned)a.Win;
+                glds16(in ? sb[i] + ((size_t)iy * a.Win + ix) * a.CS + c0 : reinterpret_cast<const __bf16 *>(a.zero),
+                       bB + i * 8 * G2_KT);
+            }
+        } else {
+#pragma unroll
+            for (int i = 0; i < NBL; ++i) {
+                const int k = k0 + kb[i];
+                // channels past the stored CS (K padded up to the k-stage) read a zero chunk: the weight
+                // row 0's own padding columns k >= CS >= cin, so a non-finite activation never meets them
+                glds16(k < a.CS ? sb[i] + k : wg + k, bB + i * 8 * G2_KT);
+            }
         }
     };
     f32x4 acc[4][4];
@@ -547,7 +607,7 @@ __global__ void __launch_bounds__(256, 2) dl_gemm128_kernel(const DlConvArgs a) 
         for (int r = 0; r < 4; ++r) acc[j][r] = (f32x4){0.f, 0.f, 0.f, 0.f};
     // one 32-channel k-step's fragments: 4 weight rows, 4 pixel rows (ds_read_b128, swizzled slots)
     auto rd = [&](const __bf16 *bA, int s2, u32x4 (&ra)[4], u32x4 (&rb)[4]) {
-        const __bf16 *bB = bA + G2_T * G2_KT;
+        const __bf16 *bB = bA + TN * G2_KT;
         const int ch = s2 * 4 + kq;
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
@@ -584,11 +644,30 @@ __global__ void __launch_bounds__(256, 2) dl_gemm128_kernel(const DlConvArgs a) 
         }
     };
     const int nst = (K + G2_KT - 1) / G2_KT;
+    // RPF (launches with a residual: the ResNet units' expansions): the epilogue's residual (64 pixels x
+    // 64 channels per wave, 8 x 16 B per lane) is loaded ahead of the k-loop, so its latency hides behind
+    // the MFMAs. Measured (ResNet-101, B = 16): expansions 1,200 -> 1,120 us per forward; an
+    // instantiation of its own because the 32 extra VGPRs slow the launches without one by ~5%
+    const int nb = n0 + wn * 64;
+    const int c8 = (lane & 7) * 8;
+    const bool cok = nb < a.NP && nb + c8 < a.cout;
+    uint4 rres[2][4];
+    if constexpr (RPF) {
+#pragma unroll
+        for (int h = 0; h < 2; ++h)
+#pragma unroll
+            for (int it = 0; it < 4; ++it) {
+                const int p = p0 + wm * 64 + h * 32 + it * 8 + (lane >> 3);
+                rres[h][it] = cok && p < a.M ? *reinterpret_cast<const uint4 *>(reinterpret_cast<const __bf16 *>(a.res) +
+                                                                                (size_t)p * a.res_cs + nb + c8)
+                                             : make_uint4(0, 0, 0, 0);
+            }
+    }
     stage(0, sm0);
     for (int st = 0; st < nst; st += 2) {
         if (st + 1 < nst) {
             stage(st + 1, sm1);
-            asm volatile("s_waitcnt vmcnt(8)" ::: "memory");   // this wave's 8 loads of stage st landed
+            vm_wait_stage<NA + NBL>();                         // this wave's loads of stage st landed
         } else {
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         }
@@ -599,7 +678,7 @@ __global__ void __launch_bounds__(256, 2) dl_gemm128_kernel(const DlConvArgs a) 
         if (st + 1 >= nst) break;
         if (st + 2 < nst) {
             stage(st + 2, sm0);
-            asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+            vm_wait_stage<NA + NBL>();
         } else {
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         }
@@ -609,13 +688,10 @@ __global__ void __launch_bounds__(256, 2) dl_gemm128_kernel(const DlConvArgs a) 
         __builtin_amdgcn_s_barrier();
     }
     // epilogue (dl_gemm_kernel's, per wave: its 64 pixels x 64 channels, 32 pixels at a time)
-    const int nb = n0 + wn * 64;
     if (nb >= a.NP) return;
     // two waves' 8.7 KB staging areas in each LDS object (each area lies inside one object)
     static_assert(2 * 32 * DL_STG_RS * sizeof(float) <= sizeof(sm0), "epilogue staging must fit one LDS object");
     float *stg = reinterpret_cast<float *>(wave < 2 ? sm0 : sm1) + (wave & 1) * 32 * DL_STG_RS;
-    const int c8 = (lane & 7) * 8;
-    const bool cok = nb + c8 < a.cout;
 #pragma unroll
     for (int h = 0; h < 2; ++h) {
         if (h) wave_lds_sync();
@@ -643,10 +719,12 @@ __global__ void __launch_bounds__(256, 2) dl_gemm128_kernel(const DlConvArgs a) 
             float4 v0 = *reinterpret_cast<const float4 *>(stg + pl * DL_STG_RS + c8);
             float4 v1 = *reinterpret_cast<const float4 *>(stg + pl * DL_STG_RS + c8 + 4);
             const int n = nb + c8;
-            if (a.res) {
-                const __bf16 *rp = reinterpret_cast<const __bf16 *>(a.res) + (size_t)p * a.res_cs + n;
-                v0 = add4(v0, ld4(rp));
-                v1 = add4(v1, ld4(rp + 4));
+            if (RPF) {
+                const uint4 u = rres[h][it];
+                v0 = add4(v0, make_float4(__uint_as_float(u.x << 16), __uint_as_float(u.x & 0xffff0000u),
+                                          __uint_as_float(u.y << 16), __uint_as_float(u.y & 0xffff0000u)));
+                v1 = add4(v1, make_float4(__uint_as_float(u.z << 16), __uint_as_float(u.z & 0xffff0000u),
+                                          __uint_as_float(u.w << 16), __uint_as_float(u.w & 0xffff0000u)));
             }
             if (a.act == 3) {              // ReLU after the residual add (ResNet units)
                 v0 = make_float4(fmaxf(v0.x, 0.f), fmaxf(v0.y, 0.f), fmaxf(v0.z, 0.f), fmaxf(v0.w, 0.f));
@@ -1119,18 +1197,50 @@ static bool gemm128_ok(const DlConvArgs &a) {
     return !(e && *e == '0') && a.cinP >= 256 && a.NP >= 256 && a.NP % 128 == 0 && a.CS % 8 == 0;
 }
 
+// implicit-GEMM k x k conv on the glds tile: bf16, dense (not tap-packed, no fused depthwise), every
+// 64-channel k-stage inside one tap (cinP = CS, a multiple of 64); 128 x 128 tiles when the outputs
+// come in whole 128-channel tiles, else (BUGSEG_DL_IG64=1) 256 pixels x 64 channels. BUGSEG_DL_IG=0
+// sends these to dl_conv_kernel for A/B runs.
+static bool igemm_ok(int prec, const DlConvArgs &a) {
+    const char *e = std::getenv("BUGSEG_DL_IG"), *e64 = std::getenv("BUGSEG_DL_IG64");
+    const bool ig64 = e64 && *e64 == '1';
+    return !(e && *e == '0') && (ig64 || a.NP % 128 == 0) && prec == PREC_BF16 && !a.dw_w && !a.tap_packed &&
+           a.taps > 1 && a.zero && a.cinP == a.CS && a.cinP % 64 == 0 && a.NP % 64 == 0 &&
+           (size_t)a.NP * a.taps * a.cinP * 2 < ((size_t)1 << 31);
+}
+
+template <bool CONV, int TPX>
+static void launch_g2(bool out_f32, const DlConvArgs &a, hipStream_t s) {
+    const dim3 g(((a.M + TPX - 1) / TPX) * ((a.NP + G2_T * G2_T / TPX - 1) / (G2_T * G2_T / TPX)));
+    if (a.res) {
+        if (out_f32) hipLaunchKernelGGL((dl_gemm128_kernel<true, CONV, true, TPX>), g, dim3(256), 0, s, a);
+        else hipLaunchKernelGGL((dl_gemm128_kernel<false, CONV, true, TPX>), g, dim3(256), 0, s, a);
+    } else {
+        if (out_f32) hipLaunchKernelGGL((dl_gemm128_kernel<true, CONV, false, TPX>), g, dim3(256), 0, s, a);
+        else hipLaunchKernelGGL((dl_gemm128_kernel<false, CONV, false, TPX>), g, dim3(256), 0, s, a);
+    }
+}
+
 hipError_t dl_launch_conv(int prec, bool out_f32, const DlConvArgs &a, hipStream_t s) {
     const bool dwf = a.dw_w != nullptr;
+    if (igemm_ok(prec, a)) {
+        if (a.NP % 128 == 0) launch_g2<true, 128>(out_f32, a, s);
+        else launch_g2<true, 256>(out_f32, a, s);
+        return hipGetLastError();
+    }
     if (gemm_ok(prec, a) && gemm128_ok(a)) {
-        const dim3 g(((a.M + G2_T - 1) / G2_T) * ((a.NP + G2_T - 1) / G2_T));
-        if (out_f32) hipLaunchKernelGGL(dl_gemm128_kernel<true>, g, dim3(256), 0, s, a);
-        else hipLaunchKernelGGL(dl_gemm128_kernel<false>, g, dim3(256), 0, s, a);
+        launch_g2<false, 128>(out_f32, a, s);
         return hipGetLastError();
     }
     if (gemm_ok(prec, a)) {
         const dim3 g(((a.M + GM_TM - 1) / GM_TM) * (a.NP / GM_TN));
-        if (out_f32) hipLaunchKernelGGL(dl_gemm_kernel<true>, g, dim3(256), 0, s, a);
-        else hipLaunchKernelGGL(dl_gemm_kernel<false>, g, dim3(256), 0, s, a);
+        if (a.res) {
+            if (out_f32) hipLaunchKernelGGL((dl_gemm_kernel<true, true>), g, dim3(256), 0, s, a);
+            else hipLaunchKernelGGL((dl_gemm_kernel<false, true>), g, dim3(256), 0, s, a);
+        } else {
+            if (out_f32) hipLaunchKernelGGL((dl_gemm_kernel<true, false>), g, dim3(256), 0, s, a);
+            else hipLaunchKernelGGL((dl_gemm_kernel<false, false>), g, dim3(256), 0, s, a);
+        }
         return hipGetLastError();
     }
     if (a.nb == 8 && prec == PREC_BF16 && !dwf) conv_nb<8>(prec, out_f32, false, a, s);

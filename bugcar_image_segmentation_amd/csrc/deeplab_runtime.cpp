@@ -33,7 +33,7 @@ struct bugseg_dl {
     int device = 0, prec = 0;
     std::string err;
     void *dev_w = nullptr;
-    size_t w_bytes = 0;
+    size_t w_bytes = 0, zero_off = 0;
     std::vector<DlOp> ops;
     std::vector<size_t> buf_bytes, buf_off;
     void *arena = nullptr;
@@ -211,6 +211,7 @@ hipError_t run_op(bugseg_dl *c, const DlOp &o, const uint8_t *rgb, int H, int W,
         a.bias_img_stride = f[26];
         a.in_bytes = (uint32_t)((size_t)B * a.Hin * a.Win * a.CS * (c->prec == PREC_BF16 ? 2 : 4));
         a.nb = f[30] == 8 ? 8 : f[30] == 4 ? 4 : 2;
+        a.zero = wb + c->zero_off;
         a.tap_packed = f[31] != 0;
         if (f[31] == 2) { a.rgb = rgb; a.img_h = H; a.img_w = W; }   // stem with the preprocessing fused
         if (f[27] >= 0) {
@@ -305,8 +306,12 @@ int bugseg_dl_load_weights(bugseg_dl *c, const void *blob, size_t bytes) {
     if (!c || !blob || bytes == 0 || bytes >= (size_t)1 << 31) return dl_fail(c, BUGSEG_EINVAL, "bad weight blob");
     DevGuard g(c->device);
     if (c->dev_w) { (void)hipDeviceSynchronize(); (void)hipFree(c->dev_w); c->dev_w = nullptr; }
-    if (hipMalloc(&c->dev_w, bytes) != hipSuccess) return dl_fail(c, BUGSEG_ENOMEM, "weight allocation failed");
-    if (hipMemcpy(c->dev_w, blob, bytes, hipMemcpyHostToDevice) != hipSuccess) return dl_fail(c, BUGSEG_EHIP, "weight upload failed");
+    // the blob, then 256 zero bytes at a 256-B boundary (the implicit-GEMM conv's padding taps read them)
+    const size_t zoff = (bytes + 255) / 256 * 256;
+    if (hipMalloc(&c->dev_w, zoff + 256) != hipSuccess) return dl_fail(c, BUGSEG_ENOMEM, "weight allocation failed");
+    if (hipMemcpy(c->dev_w, blob, bytes, hipMemcpyHostToDevice) != hipSuccess ||
+        hipMemset(static_cast<char *>(c->dev_w) + zoff, 0, 256) != hipSuccess) return dl_fail(c, BUGSEG_EHIP, "weight upload failed");
+    c->zero_off = zoff;
     c->w_bytes = bytes;
     c->ops.clear();
     return BUGSEG_OK;

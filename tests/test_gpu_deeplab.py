@@ -364,3 +364,27 @@ def test_resnet_from_frozen_graphdef(gpu, tmp_path):
     _check_fp32(model, model.net, x, torch.float64)
     lg = np.transpose(tf_graph.run(pb.read_bytes(), {"ImageTensor": x}, "logits"), (0, 3, 1, 2))
     assert np.abs(_gpu_logits(model) - lg).max() < LOGIT_TOL
+
+
+@pytest.mark.parametrize("ig64", ["0", "1"])
+@pytest.mark.parametrize("os_,crop,rates,B", [(16, 97, (6, 12, 18), 2), (8, 65, (2,), 3)])
+def test_resnet_implicit_gemm_bit_identical(gpu, monkeypatch, os_, crop, rates, B, ig64):
+    """The implicit-GEMM k x k conv on the 128 x 128 glds tile (bf16 default for dense convs with
+    64-channel-aligned inputs and 128-channel-aligned outputs: the root's 64 -> 128 3x3, block 2-4's
+    3x3s strided / atrous / multi-grid, the ASPP atrous branches) against dl_conv_kernel
+    (BUGSEG_DL_IG=0): the same (tap, 32-channel) k-steps in the same order through the same MFMA and
+    epilogue -> identical logits — over pixel tails, the fixed padding of the strided 3x3, and ASPP
+    rates past the feature map (taps wholly in the zero padding)."""
+    net = R.build_deeplab_resnet(depth=50, units=(1, 1, 2, 1), crop=crop, output_stride=os_, atrous_rates=rates)
+    x = _frames(B, crop, crop - 4, 45)
+    monkeypatch.setenv("BUGSEG_DL_IG64", ig64)   # "1": the 64-channel-output convs on the 256 x 64 tile too
+    ig = DeepLabV3(net=net, precision="bf16")
+    a = ig.predict(x)
+    la = ig.logits_device().cpu()
+    monkeypatch.setenv("BUGSEG_DL_IG", "0")
+    direct = DeepLabV3(net=net, precision="bf16")
+    b = direct.predict(x)
+    lb = direct.logits_device().cpu()
+    print(f"implicit GEMM vs direct: max|d| {(la - lb).abs().max().item():.3e}")
+    assert torch.equal(la, lb)
+    assert np.array_equal(a, b)
