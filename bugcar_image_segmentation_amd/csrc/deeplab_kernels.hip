@@ -1199,11 +1199,14 @@ static bool gemm128_ok(const DlConvArgs &a) {
 
 // implicit-GEMM k x k conv on the glds tile: bf16, dense (not tap-packed, no fused depthwise), every
 // 64-channel k-stage inside one tap (cinP = CS, a multiple of 64); 128 x 128 tiles when the outputs
-// come in whole 128-channel tiles, else (BUGSEG_DL_IG64=1) 256 pixels x 64 channels. BUGSEG_DL_IG=0
-// sends these to dl_conv_kernel for A/B runs.
+// come in whole 128-channel tiles, else 256 pixels x 64 channels. BUGSEG_DL_IG=0 sends these to
+// dl_conv_kernel for A/B runs, BUGSEG_DL_IG64=0 only the 64-channel ones. Measured (ResNet-101, B = 16,
+// per-op HIP events): the implicit GEMM 1,723 -> 2,827 frames/s (3x3s 3,826 -> 1,715 us, ASPP atrous
+// 1,859 -> 847, root 825 -> 518); the 256 x 64 tile for the 64-channel root / block-1 convs then
+// 2,827 -> 2,939 (root 518 -> 390 us, 3x3s 1,715 -> 1,633)
 static bool igemm_ok(int prec, const DlConvArgs &a) {
     const char *e = std::getenv("BUGSEG_DL_IG"), *e64 = std::getenv("BUGSEG_DL_IG64");
-    const bool ig64 = e64 && *e64 == '1';
+    const bool ig64 = !(e64 && *e64 == '0');
     return !(e && *e == '0') && (ig64 || a.NP % 128 == 0) && prec == PREC_BF16 && !a.dw_w && !a.tap_packed &&
            a.taps > 1 && a.zero && a.cinP == a.CS && a.cinP % 64 == 0 && a.NP % 64 == 0 &&
            (size_t)a.NP * a.taps * a.cinP * 2 < ((size_t)1 << 31);

@@ -377,7 +377,7 @@ def test_resnet_implicit_gemm_bit_identical(gpu, monkeypatch, os_, crop, rates, 
     rates past the feature map (taps wholly in the zero padding)."""
     net = R.build_deeplab_resnet(depth=50, units=(1, 1, 2, 1), crop=crop, output_stride=os_, atrous_rates=rates)
     x = _frames(B, crop, crop - 4, 45)
-    monkeypatch.setenv("BUGSEG_DL_IG64", ig64)   # "1": the 64-channel-output convs on the 256 x 64 tile too
+    monkeypatch.setenv("BUGSEG_DL_IG64", ig64)   # "0": the 64-channel-output convs stay on dl_conv_kernel
     ig = DeepLabV3(net=net, precision="bf16")
     a = ig.predict(x)
     la = ig.logits_device().cpu()
