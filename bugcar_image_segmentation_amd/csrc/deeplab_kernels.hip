@@ -340,22 +340,26 @@ __global__ void __launch_bounds__(256) dl_conv_kernel(const DlConvArgs a) {
 // same order and with the same epilogue as dl_conv_kernel, so the results are bit-identical.
 constexpr int GM_TM = 256, GM_TN = 64, GM_KT = 64, GM_RS = GM_KT + 16;   // LDS row: 80 elements (40 dwords)
 
-template <bool OUTF32, bool RPF>
+// TM = pixels per workgroup tile: 256 (4 fragments per wave) or 128 (2 fragments per wave: a smaller
+// LDS and register footprint, so more workgroups per CU keep more loads and stores in flight)
+template <bool OUTF32, bool RPF, bool PD2 = false, int TM = GM_TM>
 __global__ void __launch_bounds__(256, 2) dl_gemm_kernel(const DlConvArgs a) {
-    __shared__ __attribute__((aligned(16))) __bf16 sm[(GM_TN + GM_TM) * GM_RS];
+    constexpr int FJ = TM / 64, WPX = TM / 4, NBC = TM / 32;   // fragments / pixels per wave, B chunks per thread
+    constexpr int SMB = (GM_TN + TM) * GM_RS * 2, STB = 4 * 32 * DL_STG_RS * 4;   // operand / staging bytes
+    __shared__ __attribute__((aligned(16))) __bf16 sm[(SMB > STB ? SMB : STB) / 2];
     __bf16 *sA = sm, *sB = sm + GM_TN * GM_RS;
     const int tid = threadIdx.x, lane = tid & 63, col = lane & 15, kq = lane >> 4, wave = tid >> 6;
     const int ntn = a.NP >> 6;
     const int bid = xcd_block(blockIdx.x, gridDim.x);
-    const int n0 = (bid % ntn) * GM_TN, p0 = (bid / ntn) * GM_TM;
+    const int n0 = (bid % ntn) * GM_TN, p0 = (bid / ntn) * TM;
     const int K = a.cinP;
     const __amdgpu_buffer_rsrc_t rin = mkbuf(a.in, a.in_bytes);
     const __amdgpu_buffer_rsrc_t rw = mkbuf(a.w, (uint32_t)((size_t)a.NP * K * 2));
     // this thread's 16-B chunks of a stage: pixel rows q >> 3 (8 per thread), weight rows (2 per thread)
-    uint32_t boff[8], woff[2];
-    int bk[8], wk[2];
+    uint32_t boff[NBC], woff[2];
+    int bk[NBC], wk[2];
 #pragma unroll
-    for (int i = 0; i < 8; ++i) {
+    for (int i = 0; i < NBC; ++i) {
         const int q = tid + 256 * i, px = q >> 3;
         bk[i] = (q & 7) * 8;
         boff[i] = p0 + px < a.M ? (uint32_t)((p0 + px) * a.CS + bk[i]) * 2u : OOB;
@@ -366,72 +370,94 @@ __global__ void __launch_bounds__(256, 2) dl_gemm_kernel(const DlConvArgs a) {
         wk[i] = (q & 7) * 8;
         woff[i] = (uint32_t)((n0 + row) * K + wk[i]) * 2u;
     }
-    uint4 pb[8], pw[2];
-    auto fetch = [&](int k0) {
+    uint4 pb[NBC], pw[2], qb[NBC], qw[2];   // qb / qw: PD2's second stage in flight
+    auto fetch_to = [&](int k0, uint4 (&xb)[NBC], uint4 (&xw)[2]) {
 #pragma unroll
-        for (int i = 0; i < 8; ++i) pb[i] = bld16(rin, boff[i] != OOB && k0 + bk[i] < a.CS ? boff[i] + k0 * 2 : OOB);
+        for (int i = 0; i < NBC; ++i) xb[i] = bld16(rin, boff[i] != OOB && k0 + bk[i] < a.CS ? boff[i] + k0 * 2 : OOB);
 #pragma unroll
-        for (int i = 0; i < 2; ++i) pw[i] = bld16(rw, k0 + wk[i] < K ? woff[i] + k0 * 2 : OOB);
+        for (int i = 0; i < 2; ++i) xw[i] = bld16(rw, k0 + wk[i] < K ? woff[i] + k0 * 2 : OOB);
     };
-    f32x4 acc[4][4];
+    auto fetch = [&](int k0) { fetch_to(k0, pb, pw); };
+    f32x4 acc[FJ][4];
 #pragma unroll
-    for (int j = 0; j < 4; ++j)
+    for (int j = 0; j < FJ; ++j)
 #pragma unroll
         for (int r = 0; r < 4; ++r) acc[j][r] = (f32x4){0.f, 0.f, 0.f, 0.f};
     const int nst = (K + GM_KT - 1) / GM_KT;
     const int c8 = (lane & 7) * 8;
     const bool cok = n0 + c8 < a.cout;
-    uint4 rres[2][4];   // the epilogue's residual, loaded ahead of the k-loop (as dl_gemm128_kernel)
+    uint4 rres[FJ / 2][4];   // the epilogue's residual, loaded ahead of the k-loop (as dl_gemm128_kernel)
     if constexpr (RPF) {
 #pragma unroll
-        for (int h = 0; h < 2; ++h)
+        for (int h = 0; h < FJ / 2; ++h)
 #pragma unroll
             for (int it = 0; it < 4; ++it) {
-                const int p = p0 + wave * 64 + h * 32 + it * 8 + (lane >> 3);
+                const int p = p0 + wave * WPX + h * 32 + it * 8 + (lane >> 3);
                 rres[h][it] = cok && p < a.M ? *reinterpret_cast<const uint4 *>(reinterpret_cast<const __bf16 *>(a.res) +
                                                                                 (size_t)p * a.res_cs + n0 + c8)
                                              : make_uint4(0, 0, 0, 0);
             }
     }
-    fetch(0);
-    for (int st = 0; st < nst; ++st) {
+    auto put = [&](const uint4 (&xb)[NBC], const uint4 (&xw)[2]) {
         __syncthreads();                          // every wave is done reading the previous stage
 #pragma unroll
-        for (int i = 0; i < 8; ++i) {
+        for (int i = 0; i < NBC; ++i) {
             const int q = tid + 256 * i;
-            *reinterpret_cast<uint4 *>(sB + (q >> 3) * GM_RS + (q & 7) * 8) = pb[i];
+            *reinterpret_cast<uint4 *>(sB + (q >> 3) * GM_RS + (q & 7) * 8) = xb[i];
         }
 #pragma unroll
         for (int i = 0; i < 2; ++i) {
             const int q = tid + 256 * i;
-            *reinterpret_cast<uint4 *>(sA + (q >> 3) * GM_RS + (q & 7) * 8) = pw[i];
+            *reinterpret_cast<uint4 *>(sA + (q >> 3) * GM_RS + (q & 7) * 8) = xw[i];
         }
         __syncthreads();
-        if (st + 1 < nst) fetch((st + 1) * GM_KT);
+    };
+    auto compute = [&](int st) {
 #pragma unroll
         for (int s2 = 0; s2 < GM_KT / 32; ++s2) {
             if (st * GM_KT + s2 * 32 >= K) break;  // (uniform) a 32-channel tail stage: no empty k-step
-            RawB wa[4], bx[4];
+            RawB wa[4], bx[FJ];
 #pragma unroll
             for (int r = 0; r < 4; ++r) ld8(wa[r], sA + (r * 16 + col) * GM_RS + s2 * 32 + kq * 8);
 #pragma unroll
-            for (int j = 0; j < 4; ++j) ld8(bx[j], sB + (wave * 64 + j * 16 + col) * GM_RS + s2 * 32 + kq * 8);
+            for (int j = 0; j < FJ; ++j) ld8(bx[j], sB + (wave * WPX + j * 16 + col) * GM_RS + s2 * 32 + kq * 8);
 #pragma unroll
-            for (int j = 0; j < 4; ++j)
+            for (int j = 0; j < FJ; ++j)
 #pragma unroll
                 for (int r = 0; r < 4; ++r) mma(acc[j][r], wa[r], bx[j]);
+        }
+    };
+    fetch(0);
+    if constexpr (PD2) {
+        // two stages in flight in registers (K > 64: a stage's 32 MFMAs per wave are too short to
+        // cover one fetch's latency); the loop unrolled by two so each register set's role is static
+        if (nst > 1) fetch_to(GM_KT, qb, qw);
+        for (int st = 0; st < nst; st += 2) {
+            put(pb, pw);
+            if (st + 2 < nst) fetch_to((st + 2) * GM_KT, pb, pw);
+            compute(st);
+            if (st + 1 >= nst) break;
+            put(qb, qw);
+            if (st + 3 < nst) fetch_to((st + 3) * GM_KT, qb, qw);
+            compute(st + 1);
+        }
+    } else {
+        for (int st = 0; st < nst; ++st) {
+            put(pb, pw);
+            if (st + 1 < nst) fetch((st + 1) * GM_KT);
+            compute(st);
         }
     }
     // epilogue (dl_conv_kernel's, 32 pixels at a time through the wave's share of the staging LDS)
     __syncthreads();
     float *st = reinterpret_cast<float *>(sm) + wave * 32 * DL_STG_RS;
 #pragma unroll
-    for (int h = 0; h < 2; ++h) {
+    for (int h = 0; h < FJ / 2; ++h) {
         if (h) wave_lds_sync();
 #pragma unroll
         for (int jj = 0; jj < 2; ++jj) {
             const int j = 2 * h + jj;
-            const int p = p0 + wave * 64 + j * 16 + col;
+            const int p = p0 + wave * WPX + j * 16 + col;
             const int pimg = a.bias_img ? (int)fdiv((uint32_t)(p < a.M ? p : 0), a.mHW, a.sHW) : 0;
 #pragma unroll
             for (int r = 0; r < 4; ++r) {
@@ -447,7 +473,7 @@ __global__ void __launch_bounds__(256, 2) dl_gemm_kernel(const DlConvArgs a) {
 #pragma unroll
         for (int it = 0; it < 4; ++it) {
             const int pl = it * 8 + (lane >> 3);
-            const int p = p0 + wave * 64 + h * 32 + pl;
+            const int p = p0 + wave * WPX + h * 32 + pl;
             if (p >= a.M || !cok) continue;
             float4 v0 = *reinterpret_cast<const float4 *>(st + pl * DL_STG_RS + c8);
             float4 v1 = *reinterpret_cast<const float4 *>(st + pl * DL_STG_RS + c8 + 4);
@@ -1235,9 +1261,41 @@ hipError_t dl_launch_conv(int prec, bool out_f32, const DlConvArgs &a, hipStream
         launch_g2<false, 128>(out_f32, a, s);
         return hipGetLastError();
     }
+    if (const char *e = std::getenv("BUGSEG_DL_G2ALL"); e && *e != '0' && gemm_ok(prec, a) && a.CS % 8 == 0) {
+        // (A/B knob) every other 1x1 on the glds tile: 1 = 128 x 128 where the outputs come in 128s,
+        // else 256 x 64; 2 = 256 x 64 always
+        if ((*e == '1' && a.NP % 128 == 0) || *e == '3') launch_g2<false, 128>(out_f32, a, s);
+        else launch_g2<false, 256>(out_f32, a, s);
+        return hipGetLastError();
+    }
     if (gemm_ok(prec, a)) {
         const dim3 g(((a.M + GM_TM - 1) / GM_TM) * (a.NP / GM_TN));
-        if (a.res) {
+        const char *pe = std::getenv("BUGSEG_DL_GPD2"), *te = std::getenv("BUGSEG_DL_GTM");
+        const bool pd2 = pe && *pe == '1' && a.cinP > GM_KT;
+        // 128-pixel tiles below 2^19 output pixels (BUGSEG_DL_GTM=0 / 1 forces 256 / 128). Measured
+        // (per-op HIP events): MobileNetV2 B = 64 9,240 -> 9,430 frames/s (the 65x65 projections
+        // 110 -> 97 us, 212 -> 184 us; the 257^2 / 129^2 layers are slower with 128, hence the bound);
+        // ResNet-101 B = 16 and Xception-65 B = 32 within +-0.3%. PD2 (BUGSEG_DL_GPD2=1: a second stage
+        // in flight in registers) measured slower: 9,220 -> 8,935 (196-234 VGPRs: 2 workgroups per CU)
+        const bool tm128 = te ? *te == '1' : a.M <= (1 << 19);
+        if (tm128 && !pd2) {
+            const dim3 g1(((a.M + 127) / 128) * (a.NP / GM_TN));
+            if (a.res) {
+                if (out_f32) hipLaunchKernelGGL((dl_gemm_kernel<true, true, false, 128>), g1, dim3(256), 0, s, a);
+                else hipLaunchKernelGGL((dl_gemm_kernel<false, true, false, 128>), g1, dim3(256), 0, s, a);
+            } else {
+                if (out_f32) hipLaunchKernelGGL((dl_gemm_kernel<true, false, false, 128>), g1, dim3(256), 0, s, a);
+                else hipLaunchKernelGGL((dl_gemm_kernel<false, false, false, 128>), g1, dim3(256), 0, s, a);
+            }
+        } else if (pd2) {
+            if (a.res) {
+                if (out_f32) hipLaunchKernelGGL((dl_gemm_kernel<true, true, true>), g, dim3(256), 0, s, a);
+                else hipLaunchKernelGGL((dl_gemm_kernel<false, true, true>), g, dim3(256), 0, s, a);
+            } else {
+                if (out_f32) hipLaunchKernelGGL((dl_gemm_kernel<true, false, true>), g, dim3(256), 0, s, a);
+                else hipLaunchKernelGGL((dl_gemm_kernel<false, false, true>), g, dim3(256), 0, s, a);
+            }
+        } else if (a.res) {
             if (out_f32) hipLaunchKernelGGL((dl_gemm_kernel<true, true>), g, dim3(256), 0, s, a);
             else hipLaunchKernelGGL((dl_gemm_kernel<false, true>), g, dim3(256), 0, s, a);
         } else {

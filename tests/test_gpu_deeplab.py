@@ -171,14 +171,16 @@ def test_deeplab_from_frozen_graphdef(gpu, tmp_path, style, crop):
     assert np.abs(_gpu_logits(model) - lg).max() < LOGIT_TOL
 
 
+@pytest.mark.parametrize("gtm", ["0", "1"])
 @pytest.mark.parametrize("width,crop,B", [(0.5, 129, 2), (1.0, 97, 3)])
-def test_deeplab_gemm_1x1_bit_identical(gpu, monkeypatch, width, crop, B):
+def test_deeplab_gemm_1x1_bit_identical(gpu, monkeypatch, width, crop, B, gtm):
     """The LDS-staged GEMM kernel of the 1x1 convolutions (default in bf16) against dl_conv_kernel
     (BUGSEG_DL_GEMM=0): the same k-steps through the same MFMA in the same order and the same
     epilogue, so identical logits and class maps — over tile tails (pixel counts not a multiple of
     256), 32-channel k tails, the residual projections and the per-image-bias projection."""
     net = S.build_deeplab(width=width, crop=crop, atrous_rates=(6,))
     x = _frames(B, crop, crop - 5, 41)
+    monkeypatch.setenv("BUGSEG_DL_GTM", gtm)   # 256- / 128-pixel tiles
     gemm = DeepLabV3(net=net, precision="bf16")
     a = gemm.predict(x)
     la = gemm.logits_device().cpu()
