@@ -99,7 +99,8 @@ def measure(dev, B, steps, warmup, precision, world=1, rank=0, backbone="mobilen
     per-op list, forward us)."""
     from bugcar_image_segmentation_amd.models import DeepLabV3
 
-    model = DeepLabV3(precision=precision, backbone=backbone)
+    # BUGSEG_DL_FUSE_PREP=0 (A/B knob): the separate padding / normalisation launch instead of the stem's fused loads
+    model = DeepLabV3(precision=precision, backbone=backbone, fuse_prep=os.environ.get("BUGSEG_DL_FUSE_PREP", "1") != "0")
     C = model.net.crop
     frames = torch.from_numpy(np.random.default_rng(rank).integers(0, 256, (B, C, C, 3), dtype=np.uint8)).to(dev)
     out = torch.empty((B, C, C), dtype=torch.int64, device=dev)

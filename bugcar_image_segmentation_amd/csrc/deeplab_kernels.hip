@@ -975,6 +975,16 @@ __global__ void __launch_bounds__(256) dl_pool_gemv_kernel(const DlPoolArgs a) {
 // value = top_row + (bottom_row - top_row) * y_lerp with row = left + (right - left) * x_lerp.
 // Then argmax over classes (first maximum).
 constexpr int AM_PX = 8, AM_PY = 1, AM_C = 24;   // classes held in registers (LCS <= AM_C uses this kernel)
+// Round 6 (MobileNetV2 B = 64, per-op HIP events): the class loops fully unrolled (no s_set_gpr_idx),
+// the corner differences once per cell and packed f32 lerps: 140 -> 102-108 us; the same without the
+// class loop (AM_ABL = 1) 42 us. Tried and dropped: the logit rows staged in LDS per 8-row workgroup
+// (252 us) and wave-staged whole-line stores (142 us, with the rolled loop).
+#ifndef AM_OPT
+#define AM_OPT 1   // corner differences once per cell + packed f32 lerps (0: the per-pixel scalar chain)
+#endif
+#ifndef AM_ABL
+#define AM_ABL 0   // debug ablation (wrong classes): 1 = no class loop
+#endif
 // One thread = AM_PX consecutive output pixels in each of AM_PY consecutive rows; the 4 corner logit
 // vectors are reloaded only when the corner cell (x0, y0) changes (at the 65 -> 513 scale of 1/8, once
 // per 8 pixels of a row). Class ids of a run go out as 16-B stores (two int64) where the address
@@ -1006,19 +1016,46 @@ __global__ void __launch_bounds__(256) dl_resize_argmax_kernel(const DlArgmaxArg
             if (x0 != curx || y0 != cury) {
                 curx = x0;
                 cury = y0;
+                // every loop over classes is fully unrolled with predicates, not a runtime break: a
+                // partly rolled loop indexes tl[] .. br[] with s_set_gpr_idx (serialising), the form
+                // the kernel had until round 6
 #pragma unroll
                 for (int c0 = 0; c0 < AM_C; c0 += 4) {
-                    if (c0 >= a.LCS) break;
-                    const float4 q0 = ld4f(row0 + x0 * a.LCS + c0), q1 = ld4f(row0 + x1 * a.LCS + c0);
-                    const float4 q2 = ld4f(row1 + x0 * a.LCS + c0), q3 = ld4f(row1 + x1 * a.LCS + c0);
+                    const bool in = c0 < a.LCS;
+                    const float4 z = make_float4(0.f, 0.f, 0.f, 0.f);
+                    const float4 q0 = in ? ld4f(row0 + x0 * a.LCS + c0) : z, q1 = in ? ld4f(row0 + x1 * a.LCS + c0) : z;
+                    const float4 q2 = in ? ld4f(row1 + x0 * a.LCS + c0) : z, q3 = in ? ld4f(row1 + x1 * a.LCS + c0) : z;
                     tl[c0] = q0.x; tl[c0 + 1] = q0.y; tl[c0 + 2] = q0.z; tl[c0 + 3] = q0.w;
                     tr[c0] = q1.x; tr[c0 + 1] = q1.y; tr[c0 + 2] = q1.z; tr[c0 + 3] = q1.w;
                     bl[c0] = q2.x; bl[c0 + 1] = q2.y; bl[c0 + 2] = q2.z; bl[c0 + 3] = q2.w;
                     br[c0] = q3.x; br[c0 + 1] = q3.y; br[c0 + 2] = q3.z; br[c0 + 3] = q3.w;
                 }
+#if AM_OPT
+                // the corner differences once per cell (the same f32 subtractions TF's lerp does per pixel)
+#pragma unroll
+                for (int c = 0; c < AM_C; ++c) {
+                    tr[c] = tr[c] - tl[c];
+                    br[c] = br[c] - bl[c];
+                }
+#endif
             }
             float best = 0.f;
             int bi = 0;
+#if AM_ABL
+            best = lx + ly;
+#elif AM_OPT
+            // two classes per packed f32 op (v_pk_mul_f32 / v_pk_add_f32: per-lane IEEE, as the scalar chain)
+            typedef float f2 __attribute__((ext_vector_type(2)));
+            const f2 lx2 = {lx, lx}, ly2 = {ly, ly};
+#pragma unroll
+            for (int c = 0; c < AM_C; c += 2) {
+                const f2 t2 = (f2){tl[c], tl[c + 1]} + (f2){tr[c], tr[c + 1]} * lx2;
+                const f2 b2 = (f2){bl[c], bl[c + 1]} + (f2){br[c], br[c + 1]} * lx2;
+                const f2 v2 = t2 + (b2 - t2) * ly2;
+                if (c == 0 || (c < a.ncls && v2.x > best)) { best = v2.x; bi = c; }
+                if (c + 1 < a.ncls && v2.y > best) { best = v2.y; bi = c + 1; }
+            }
+#else
 #pragma unroll
             for (int c = 0; c < AM_C; ++c) {
                 if (c >= a.ncls) break;
@@ -1027,6 +1064,7 @@ __global__ void __launch_bounds__(256) dl_resize_argmax_kernel(const DlArgmaxArg
                 const float v = top + (bot - top) * ly;
                 if (c == 0 || v > best) { best = v; bi = c; }
             }
+#endif
             if (j < 4) packed[0] |= (uint32_t)bi << (8 * j);
             else packed[1] |= (uint32_t)bi << (8 * (j - 4));
         }
