@@ -46,6 +46,13 @@ struct DlConvArgs {
     const void *zero;    // >= 16 zero bytes (after the weight blob): the implicit-GEMM conv's padding taps
 };
 
+// n same-shape implicit-GEMM convs (bf16 out, no residual) as one launch (dl_launch_conv_group)
+constexpr int DL_GROUP_MAX = 4;
+struct DlConvGroup {
+    DlConvArgs a[DL_GROUP_MAX];
+    int n, tiles;   // tiles: set by the launcher
+};
+
 struct DlDwArgs {
     const void *in;      // (B, Hin, Win, C) T
     int B, Hin, Win, C;
@@ -105,6 +112,7 @@ struct DlMaxPoolArgs {
 
 hipError_t dl_launch_prep(int prec, const DlPrepArgs &a, hipStream_t s);
 hipError_t dl_launch_maxpool(int prec, const DlMaxPoolArgs &a, hipStream_t s);
+hipError_t dl_launch_conv_group(int prec, const DlConvGroup &g, hipStream_t s);   // hipErrorNotSupported: launch singly
 hipError_t dl_launch_conv(int prec, bool out_f32, const DlConvArgs &a, hipStream_t s);
 hipError_t dl_launch_dw(int prec, const DlDwArgs &a, hipStream_t s);
 hipError_t dl_launch_pool(int prec, const DlPoolArgs &a, hipStream_t s);

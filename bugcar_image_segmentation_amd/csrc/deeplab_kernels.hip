@@ -557,7 +557,7 @@ template <> __device__ __forceinline__ void vm_wait_stage<8>() { asm volatile("s
 template <> __device__ __forceinline__ void vm_wait_stage<10>() { asm volatile("s_waitcnt vmcnt(10)" ::: "memory"); }
 
 template <bool OUTF32, bool CONV, bool RPF, int TPX = G2_T>
-__global__ void __launch_bounds__(256, 2) dl_gemm128_kernel(const DlConvArgs a) {
+__device__ __forceinline__ void g2_body(const DlConvArgs &a, const int bid) {
     // TPX = pixels per tile: 128 (the 128 x 128 tile, waves 2 x 2) or 256 (256 pixels x 64 channels,
     // waves 4 x 1: 64-channel outputs, ResNet's root and block-1 3x3s); each wave's 64 x 64 is the same
     constexpr int TN = G2_T * G2_T / TPX, WM = TPX / 64, NA = TN / 32, NBL = TPX / 32;   // glds per wave: NA + NBL
@@ -569,7 +569,6 @@ __global__ void __launch_bounds__(256, 2) dl_gemm128_kernel(const DlConvArgs a) 
     const int tid = threadIdx.x, lane = tid & 63, col = lane & 15, kq = lane >> 4, wave = tid >> 6;
     const int wm = wave % WM, wn = wave / WM;
     const int ntn = (a.NP + TN - 1) / TN;
-    const int bid = xcd_block(blockIdx.x, gridDim.x);
     const int n0 = (bid % ntn) * TN, p0 = (bid / ntn) * TPX;
     const __bf16 *wg = reinterpret_cast<const __bf16 *>(a.w), *xg = reinterpret_cast<const __bf16 *>(a.in);
     // this lane's glds sources: A instruction i fills LDS rows wave * TN / 4 + i * 8 + (lane >> 3), B
@@ -767,6 +766,20 @@ __global__ void __launch_bounds__(256, 2) dl_gemm128_kernel(const DlConvArgs a) 
             }
         }
     }
+}
+
+template <bool OUTF32, bool CONV, bool RPF, int TPX = G2_T>
+__global__ void __launch_bounds__(256, 2) dl_gemm128_kernel(const DlConvArgs a) {
+    g2_body<OUTF32, CONV, RPF, TPX>(a, xcd_block(blockIdx.x, gridDim.x));
+}
+
+// Grouped launch: n convolutions of one shape (the ASPP's atrous branches: same input, same output
+// buffer at their own channel offsets, their own rates and weights) as one grid, branch = logical
+// block / tiles — 3 x 274 tiles at B = 16 fill the chip where each alone left half the slots idle.
+template <bool CONV, int TPX>
+__global__ void __launch_bounds__(256, 2) dl_gemm128_group_kernel(const DlConvGroup g) {
+    const int L = xcd_block(blockIdx.x, gridDim.x), gi = L / g.tiles;
+    g2_body<false, CONV, false, TPX>(g.a[gi], L - gi * g.tiles);
 }
 
 // (Round 3 measured three other tilings of these shapes, all bit-identical and all slower, and removed
@@ -1286,6 +1299,18 @@ static void launch_g2(bool out_f32, const DlConvArgs &a, hipStream_t s) {
         if (out_f32) hipLaunchKernelGGL((dl_gemm128_kernel<true, CONV, false, TPX>), g, dim3(256), 0, s, a);
         else hipLaunchKernelGGL((dl_gemm128_kernel<false, CONV, false, TPX>), g, dim3(256), 0, s, a);
     }
+}
+
+hipError_t dl_launch_conv_group(int prec, const DlConvGroup &g, hipStream_t s) {
+    if (g.n < 2 || g.n > DL_GROUP_MAX) return hipErrorNotSupported;
+    for (int i = 0; i < g.n; ++i) {
+        const DlConvArgs &a = g.a[i];
+        if (!igemm_ok(prec, a) || a.res || a.NP % 128 || a.M != g.a[0].M || a.NP != g.a[0].NP) return hipErrorNotSupported;
+    }
+    DlConvGroup h = g;
+    h.tiles = ((g.a[0].M + G2_T - 1) / G2_T) * (g.a[0].NP / G2_T);
+    hipLaunchKernelGGL((dl_gemm128_group_kernel<true, 128>), dim3(h.tiles * g.n), dim3(256), 0, s, h);
+    return hipGetLastError();
 }
 
 hipError_t dl_launch_conv(int prec, bool out_f32, const DlConvArgs &a, hipStream_t s) {

@@ -35,6 +35,7 @@ struct bugseg_dl {
     void *dev_w = nullptr;
     size_t w_bytes = 0, zero_off = 0;
     std::vector<DlOp> ops;
+    std::vector<int> group_len;   // per op: > 1 at the first of that many same-shape convs run as one launch
     std::vector<size_t> buf_bytes, buf_off;
     void *arena = nullptr;
     int B = 0, Hc = 0, Wc = 0;
@@ -185,6 +186,65 @@ bool check_op(const bugseg_dl *c, const DlOp &o, std::string &why) {
     }
 }
 
+// Runs of consecutive k x k CONV ops of one shape that read the same buffer and write the same one
+// (the ASPP's atrous branches, each at its channel offset of the concat): same input / output
+// geometry, packing, no residual, depthwise or per-image bias, 2-byte output. -> per op, the length
+// of the run starting there (1 = launched alone); the launcher still checks each member's form.
+std::vector<int> conv_groups(const std::vector<DlOp> &ops) {
+    std::vector<int> len(ops.size(), 1);
+    auto alone_ok = [](const int *f) {
+        return f[0] == OP_CONV && f[3] < 0 && f[9] > 1 && f[10] > 1 && f[24] == 0 && f[25] < 0 && f[27] < 0 && f[31] == 0;
+    };
+    auto same = [](const int *x, const int *y) {
+        for (int k : {1, 2, 4, 5, 6, 7, 8, 9, 10, 15, 16, 21})
+            if (x[k] != y[k]) return false;
+        return true;
+    };
+    for (size_t i = 0; i < ops.size();) {
+        size_t n = 1;
+        if (alone_ok(ops[i].f))
+            while (i + n < ops.size() && (int)n < DL_GROUP_MAX && alone_ok(ops[i + n].f) && same(ops[i].f, ops[i + n].f)) ++n;
+        if (n > 1) len[i] = (int)n;
+        i += n;
+    }
+    return len;
+}
+
+// The DlConvArgs of CONV op o (run_op and the grouped launch in bugseg_dl_forward).
+DlConvArgs conv_args(bugseg_dl *c, const DlOp &o, const uint8_t *rgb, int H, int W) {
+    const int *f = o.f;
+    const char *wb = static_cast<const char *>(c->dev_w);
+    const int B = c->B;
+    DlConvArgs a{};
+    a.in = bufp(c, f[1]);
+    a.B = B; a.Hin = f[4]; a.Win = f[5]; a.CS = f[6];
+    a.Hout = f[7]; a.Wout = f[8]; a.M = B * a.Hout * a.Wout;
+    a.kh = f[9]; a.kw = f[10]; a.taps = a.kh * a.kw; a.stride = f[11]; a.dil = f[12]; a.pad_t = f[13]; a.pad_l = f[14];
+    a.cinP = f[15]; a.NP = f[16];
+    a.w = wb + f[17];
+    a.bias = reinterpret_cast<const float *>(wb + f[18]);
+    a.act = f[19];
+    a.res = f[3] >= 0 ? bufp(c, f[3]) : nullptr;
+    a.res_cs = f[20];
+    a.out = bufp(c, f[2]); a.out_cs = f[21]; a.out_off = f[22]; a.cout = f[23];
+    a.bias_img = f[25] >= 0 ? static_cast<const float *>(bufp(c, f[25])) : nullptr;
+    a.bias_img_stride = f[26];
+    a.in_bytes = (uint32_t)((size_t)B * a.Hin * a.Win * a.CS * (c->prec == PREC_BF16 ? 2 : 4));
+    a.nb = f[30] == 8 ? 8 : f[30] == 4 ? 4 : 2;
+    a.zero = wb + c->zero_off;
+    a.tap_packed = f[31] != 0;
+    if (f[31] == 2) { a.rgb = rgb; a.img_h = H; a.img_w = W; }   // stem with the preprocessing fused
+    if (f[27] >= 0) {
+        a.dw_w = wb + f[27];
+        a.dw_b = reinterpret_cast<const float *>(wb + f[28]);
+        a.dw_stride = f[29] & 0xff; a.dw_dil = (f[29] >> 8) & 0xff;
+        a.dw_pt = (f[29] >> 16) & 0xff; a.dw_pl = (f[29] >> 24) & 0xff;
+    }
+    fastdiv((uint32_t)(a.Hout * a.Wout), a.mHW, a.sHW);
+    fastdiv((uint32_t)a.Wout, a.mW, a.sW);
+    return a;
+}
+
 hipError_t run_op(bugseg_dl *c, const DlOp &o, const uint8_t *rgb, int H, int W, int64_t *out, hipStream_t s) {
     const int *f = o.f;
     const char *wb = static_cast<const char *>(c->dev_w);
@@ -195,33 +255,7 @@ hipError_t run_op(bugseg_dl *c, const DlOp &o, const uint8_t *rgb, int H, int W,
         return dl_launch_prep(c->prec, a, s);
     }
     case OP_CONV: {
-        DlConvArgs a{};
-        a.in = bufp(c, f[1]);
-        a.B = B; a.Hin = f[4]; a.Win = f[5]; a.CS = f[6];
-        a.Hout = f[7]; a.Wout = f[8]; a.M = B * a.Hout * a.Wout;
-        a.kh = f[9]; a.kw = f[10]; a.taps = a.kh * a.kw; a.stride = f[11]; a.dil = f[12]; a.pad_t = f[13]; a.pad_l = f[14];
-        a.cinP = f[15]; a.NP = f[16];
-        a.w = wb + f[17];
-        a.bias = reinterpret_cast<const float *>(wb + f[18]);
-        a.act = f[19];
-        a.res = f[3] >= 0 ? bufp(c, f[3]) : nullptr;
-        a.res_cs = f[20];
-        a.out = bufp(c, f[2]); a.out_cs = f[21]; a.out_off = f[22]; a.cout = f[23];
-        a.bias_img = f[25] >= 0 ? static_cast<const float *>(bufp(c, f[25])) : nullptr;
-        a.bias_img_stride = f[26];
-        a.in_bytes = (uint32_t)((size_t)B * a.Hin * a.Win * a.CS * (c->prec == PREC_BF16 ? 2 : 4));
-        a.nb = f[30] == 8 ? 8 : f[30] == 4 ? 4 : 2;
-        a.zero = wb + c->zero_off;
-        a.tap_packed = f[31] != 0;
-        if (f[31] == 2) { a.rgb = rgb; a.img_h = H; a.img_w = W; }   // stem with the preprocessing fused
-        if (f[27] >= 0) {
-            a.dw_w = wb + f[27];
-            a.dw_b = reinterpret_cast<const float *>(wb + f[28]);
-            a.dw_stride = f[29] & 0xff; a.dw_dil = (f[29] >> 8) & 0xff;
-            a.dw_pt = (f[29] >> 16) & 0xff; a.dw_pl = (f[29] >> 24) & 0xff;
-        }
-        fastdiv((uint32_t)(a.Hout * a.Wout), a.mHW, a.sHW);
-        fastdiv((uint32_t)a.Wout, a.mW, a.sW);
+        const DlConvArgs a = conv_args(c, o, rgb, H, W);
         return dl_launch_conv(c->prec, f[24] != 0, a, s);
     }
     case OP_DW: {
@@ -377,6 +411,7 @@ int bugseg_dl_set_plan(bugseg_dl *c, const int32_t *ops, int nops, const uint64_
     }
     if (hipMalloc(&c->arena, total) != hipSuccess) return dl_fail(c, BUGSEG_ENOMEM, "activation arena allocation failed");
     c->ops = std::move(v);
+    c->group_len = conv_groups(c->ops);
     c->buf_bytes = std::move(bb);
     c->buf_off = std::move(off);
     c->B = B; c->Hc = Hc; c->Wc = Wc;
@@ -392,7 +427,19 @@ int bugseg_dl_forward(bugseg_dl *c, const uint8_t *rgb_dev, int B, int H, int W,
                                              std::to_string(c->Hc) + "x" + std::to_string(c->Wc) + ")");
     DevGuard g(c->device);
     hipStream_t s = static_cast<hipStream_t>(stream);
+    const char *ge = std::getenv("BUGSEG_DL_GROUP");
+    const bool group = !(ge && *ge == '0');
     for (size_t i = 0; i < c->ops.size(); ++i) {
+        const int n = group ? c->group_len[i] : 1;
+        if (n > 1) {   // same-shape convs as one launch (the ASPP's atrous branches)
+            DlConvGroup g{};
+            g.n = n;
+            for (int k = 0; k < n; ++k) g.a[k] = conv_args(c, c->ops[i + k], rgb_dev, H, W);
+            const hipError_t e = dl_launch_conv_group(c->prec, g, s);
+            if (e == hipSuccess) { i += n - 1; continue; }
+            if (e != hipErrorNotSupported) return dl_fail(c, BUGSEG_EHIP, "grouped launch at op " + std::to_string(i) + ": " + hipGetErrorString(e));
+            (void)hipGetLastError();
+        }
         const hipError_t e = run_op(c, c->ops[i], rgb_dev, H, W, out_dev, s);
         if (e != hipSuccess) return dl_fail(c, BUGSEG_EHIP, "launch of op " + std::to_string(i) + ": " + hipGetErrorString(e));
     }

@@ -390,3 +390,19 @@ def test_resnet_implicit_gemm_bit_identical(gpu, monkeypatch, os_, crop, rates, 
     print(f"implicit GEMM vs direct: max|d| {(la - lb).abs().max().item():.3e}")
     assert torch.equal(la, lb)
     assert np.array_equal(a, b)
+
+
+def test_resnet_grouped_aspp_bit_identical(gpu, monkeypatch):
+    """The ASPP's atrous branches as one grouped launch (bugseg_dl_forward's same-shape conv runs,
+    dl_gemm128_group_kernel) against one launch each (BUGSEG_DL_GROUP=0): every tile runs the same
+    code on its own branch's arguments -> identical logits."""
+    net = R.build_deeplab_resnet(depth=50, units=(1, 1, 1, 1), crop=97, atrous_rates=(6, 12, 18))
+    x = _frames(2, 97, 90, 46)
+    grouped = DeepLabV3(net=net, precision="bf16")
+    a = grouped.predict(x)
+    la = grouped.logits_device().cpu()
+    monkeypatch.setenv("BUGSEG_DL_GROUP", "0")
+    single = DeepLabV3(net=net, precision="bf16")
+    b = single.predict(x)
+    assert torch.equal(la, single.logits_device().cpu())
+    assert np.array_equal(a, b)
