@@ -348,6 +348,7 @@ int bugseg_dl_load_weights(bugseg_dl *c, const void *blob, size_t bytes) {
     c->zero_off = zoff;
     c->w_bytes = bytes;
     c->ops.clear();
+    c->group_len.clear();
     return BUGSEG_OK;
 }
 
@@ -432,10 +433,10 @@ int bugseg_dl_forward(bugseg_dl *c, const uint8_t *rgb_dev, int B, int H, int W,
     for (size_t i = 0; i < c->ops.size(); ++i) {
         const int n = group ? c->group_len[i] : 1;
         if (n > 1) {   // same-shape convs as one launch (the ASPP's atrous branches)
-            DlConvGroup g{};
-            g.n = n;
-            for (int k = 0; k < n; ++k) g.a[k] = conv_args(c, c->ops[i + k], rgb_dev, H, W);
-            const hipError_t e = dl_launch_conv_group(c->prec, g, s);
+            DlConvGroup grp{};
+            grp.n = n;
+            for (int k = 0; k < n; ++k) grp.a[k] = conv_args(c, c->ops[i + k], rgb_dev, H, W);
+            const hipError_t e = dl_launch_conv_group(c->prec, grp, s);
             if (e == hipSuccess) { i += n - 1; continue; }
             if (e != hipErrorNotSupported) return dl_fail(c, BUGSEG_EHIP, "grouped launch at op " + std::to_string(i) + ": " + hipGetErrorString(e));
             (void)hipGetLastError();
